@@ -1,0 +1,150 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Graph500-style BFS GTEPS on RMAT-26 over N MI355X GPUs.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` -- for N > 1
+launched with ``torch.distributed.run`` (one process per GPU; RANK, LOCAL_RANK,
+WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment).  One *step* = one
+complete BFS traversal from a fresh random root (degree >= 1) on the fixed
+RMAT-26 graph (strong scaling: the graph is 1D-partitioned over the N GPUs).
+W untimed warm-up traversals, then EXACTLY K traversals timed between a
+barrier + device synchronisation on both sides, max over ranks; rank 0 prints
+one JSON line.  value = total traversed edges of the K traversals / timed wall
+time (whole job, all GPUs).  The graph is generated on the GPUs with the
+Graph500 Kronecker parameters (a=.57 b=.19 c=.19, edge factor 16, scrambled
+vertex labels); weights/data are synthetic by construction (no dataset).
+
+The reference (xxcclong/Distributed-CUDA-BFS) publishes no number
+(BASELINE.md), so vs_baseline is null unless --baseline-gteps is given.
+This process never imports torch: it uses the native core's own HIP runtime
+and RCCL communicator.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "GTEPS (traversed edges/sec) on RMAT-26 + soc-LiveJournal1 at 1/2/4/8 MI355X"
+
+
+def log(msg: str) -> None:
+    print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple"])
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--root-seed", type=int, default=12345)
+    ap.add_argument("--alpha", type=float, default=14.0)
+    ap.add_argument("--beta", type=float, default=24.0)
+    ap.add_argument("--bu-lane-limit", type=int, default=8)
+    ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--baseline-gteps", type=float, default=None)
+    ap.add_argument("--per-level", action="store_true", help="print per-level records of the first timed run")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            log(f"--gpus {args.gpus} requested but WORLD_SIZE=1: launch with torch.distributed.run "
+                f"--nproc-per-node {args.gpus}")
+            return 2
+    import distributed_cuda_bfs_amd as dbfs
+    from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
+    from distributed_cuda_bfs_amd.utils.metrics import harmonic_mean
+
+    N = dbfs.native
+    rt = init_runtime(args.device)
+    rank, nranks = rt.rank, rt.world
+    log(f"backend {rt.backend.name}, comm {rt.comm.name}, ranks {nranks}")
+
+    params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
+    t0 = time.time()
+    bfs = dbfs.BFS(params, rt, mode=args.mode, alpha=args.alpha, beta=args.beta,
+                   bu_lane_limit=args.bu_lane_limit)
+    rt.backend.synchronize()
+    rt.barrier()
+    gen_s = time.time() - t0
+    log(f"generated RMAT-{args.scale} shard: rows {bfs.graph.rows} nnz {bfs.graph.nnz} in {gen_s:.2f}s")
+
+    roots = bfs.sample_roots(args.warmup + args.steps, seed=args.root_seed)
+    if len(roots) < args.warmup + args.steps:
+        log("could not sample enough roots")
+        return 3
+    warm, timed = roots[:args.warmup], roots[args.warmup:]
+
+    validated = None
+    for i, r in enumerate(warm):
+        res = bfs.run(r)
+        if i == 0 and not args.no_validate:
+            validated = bfs.validate(r)
+            log(f"validation of root {r}: {'OK' if validated else 'FAILED'}")
+            if not validated:
+                return 4
+        log(f"warmup root {r}: {res.ms:.3f} ms, {res.gteps:.2f} GTEPS, depth {res.depth}")
+
+    rt.barrier()
+    rt.backend.synchronize()
+    t_start = time.perf_counter()
+    results = [bfs.run(r) for r in timed]
+    rt.backend.synchronize()
+    rt.barrier()
+    wall_ms = (time.perf_counter() - t_start) * 1e3
+    wall_ms = rt.comm.max_host(wall_ms)
+
+    edges = sum(r.edges for r in results)
+    bfs_ms = sum(r.ms for r in results)
+    value = edges / (wall_ms * 1e6)
+    if rank == 0:
+        if args.per_level:
+            for lv in results[0].levels:
+                log(f"  level {lv['level']} {lv['dir']} frontier {lv['frontier']} edges {lv['frontier_edges']}"
+                    f" new {lv['discovered']}")
+        out = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "GTEPS",
+            "n_gpus": nranks,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_ms / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": (round(value / args.baseline_gteps, 4) if args.baseline_gteps else None),
+            "dtype": "int32",
+            "data": "synthetic (Graph500 RMAT generated on device, random roots)",
+            "config": {
+                "model": f"RMAT-{args.scale} (Graph500 Kronecker a=.57 b=.19 c=.19, edge factor {args.edge_factor})",
+                "global_batch": 1,
+                "seq_len": None,
+                "parallelism": f"1d-vertex-partition x{nranks}",
+                "mode": args.mode,
+                "vertices": params.n,
+                "input_edges": params.m,
+                "directed_edges": bfs.engine.global_directed_edges,
+            },
+            "bfs_ms_mean": round(bfs_ms / len(results), 4),
+            "harmonic_mean_gteps": round(harmonic_mean([r.gteps for r in results]), 4),
+            "traversed_edges_mean": edges // len(results),
+            "depth_mean": sum(r.depth for r in results) / len(results),
+            "validated": validated,
+            "generate_s": round(gen_s, 3),
+        }
+        print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,180 @@
+// HIP backend: one gfx950 device, one non-blocking HIP stream; every primitive
+// is a hand-written kernel launch (csrc/kernels/*.hip) enqueued on that stream.
+//
+// Replaces the reference's device runtime layer (initCuda2
+// bfs.cu:308-360, __managed__ registry bfs.cu:252-269): explicit device
+// allocations instead of managed memory, checked errors instead of the
+// comma-expression idiom that discards them (bfs.cu:336-351, D3).
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "dbfs/backend.hpp"
+#include "../kernels/launch.hpp"
+
+namespace dbfs {
+
+#define HIP_CHECK(expr)                                                                              \
+  do {                                                                                               \
+    hipError_t e_ = (expr);                                                                          \
+    if (e_ != hipSuccess)                                                                            \
+      ::dbfs::raise_error(__FILE__, __LINE__, std::string("HIP error ") + hipGetErrorString(e_) +    \
+                                                  " in " #expr);                                     \
+  } while (0)
+
+namespace {
+
+class HipBackend final : public Backend {
+ public:
+  explicit HipBackend(int dev) : dev_(dev) {
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    DBFS_CHECK(dev >= 0 && dev < n, "HIP device " + std::to_string(dev) + " not present (" + std::to_string(n) + " visible)");
+    HIP_CHECK(hipSetDevice(dev_));
+    HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    hipDeviceProp_t prop{};
+    HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
+    arch_ = prop.gcnArchName;
+    cus_ = prop.multiProcessorCount;
+  }
+  ~HipBackend() override {
+    hipSetDevice(dev_);
+    hipStreamSynchronize(st_);
+    for (hipEvent_t e : events_) hipEventDestroy(e);
+    if (scan_tmp_) hipFree(scan_tmp_);
+    hipStreamDestroy(st_);
+  }
+
+  DeviceKind kind() const override { return DeviceKind::HIP; }
+  std::string name() const override {
+    return "hip:" + std::to_string(dev_) + " (" + arch_ + ", " + std::to_string(cus_) + " CUs)";
+  }
+  int device_id() const override { return dev_; }
+  void* stream_handle() override { return st_; }
+
+  void* alloc(size_t bytes) override {
+    on();
+    void* p = nullptr;
+    if (bytes == 0) bytes = 64;
+    HIP_CHECK(hipMalloc(&p, bytes));
+    return p;
+  }
+  void dealloc(void* p) override {
+    on();
+    hipStreamSynchronize(st_);
+    hipFree(p);
+  }
+  void memset_async(void* p, int v, size_t bytes) override {
+    if (!bytes) return;
+    on();
+    HIP_CHECK(hipMemsetAsync(p, v, bytes, st_));
+  }
+  void copy_async(void* d, const void* s, size_t bytes) override {
+    if (!bytes) return;
+    on();
+    HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDefault, st_));
+  }
+  void to_host(void* d, const void* s, size_t bytes) override {
+    on();
+    if (bytes) HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+  }
+  void to_device(void* d, const void* s, size_t bytes) override {
+    on();
+    if (bytes) HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+  }
+  void synchronize() override {
+    on();
+    HIP_CHECK(hipStreamSynchronize(st_));
+  }
+
+  int record_event() override {
+    on();
+    if (ev_used_ == events_.size()) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreate(&e));
+      events_.push_back(e);
+    }
+    HIP_CHECK(hipEventRecord(events_[ev_used_], st_));
+    return static_cast<int>(ev_used_++);
+  }
+  double elapsed_ms(int a, int b) override {
+    on();
+    HIP_CHECK(hipEventSynchronize(events_.at(b)));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, events_.at(a), events_.at(b)));
+    return ms;
+  }
+  void reset_events() override { ev_used_ = 0; }
+
+  void fill_level(lvl_t* level, int64_t n, lvl_t value) override { on(); kern::fill_level(level, n, value, st_); chk(); }
+  void set_bit(word_t* bm, int64_t bit) override { on(); kern::set_bit(bm, bit, st_); chk(); }
+  void update_frontier(const UpdateArgs& a) override { on(); kern::update_frontier(a, st_); chk(); }
+  void scan_segments(const ScanArgs& a) override { on(); kern::scan_segments(a, st_); chk(); }
+  void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
+  void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
+  void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
+  void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
+  void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
+  void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
+  void ref_accept(const RefAcceptArgs& a) override { on(); kern::ref_accept(a, st_); chk(); }
+  void validate_levels(const ValidateArgs& a) override { on(); kern::validate_levels(a, st_); chk(); }
+
+  void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
+    on();
+    kern::gen_count_degrees(p, lo, rows, deg, st_);
+    chk();
+  }
+  void exclusive_scan(eid_t* data, int64_t n) override {
+    on();
+    const size_t need = static_cast<size_t>(kern::scan_tmp_elems(n));
+    if (need > scan_tmp_n_) {
+      HIP_CHECK(hipStreamSynchronize(st_));
+      if (scan_tmp_) HIP_CHECK(hipFree(scan_tmp_));
+      HIP_CHECK(hipMalloc(&scan_tmp_, need * sizeof(eid_t)));
+      scan_tmp_n_ = need;
+    }
+    kern::exclusive_scan(data, n, scan_tmp_, st_);
+    chk();
+  }
+  void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) override {
+    on();
+    kern::gen_fill(p, lo, rows, cursor, col, st_);
+    chk();
+  }
+  void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) override {
+    on();
+    HIP_CHECK(hipMemsetAsync(out2, 0, 2 * sizeof(int64_t), st_));
+    kern::reached_degree_sum(g, level, out2, st_);
+    chk();
+  }
+
+ private:
+  // Other libraries (RCCL init, user code) may change the calling thread's
+  // current device, so it is re-asserted on every call (a TLS write).
+  void on() { HIP_CHECK(hipSetDevice(dev_)); }
+  static void chk() { HIP_CHECK(hipGetLastError()); }
+
+  int dev_;
+  hipStream_t st_ = nullptr;
+  std::string arch_;
+  int cus_ = 0;
+  std::vector<hipEvent_t> events_;
+  size_t ev_used_ = 0;
+  eid_t* scan_tmp_ = nullptr;
+  size_t scan_tmp_n_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_hip_backend(int device) { return std::make_unique<HipBackend>(device); }
+
+int hip_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // namespace dbfs

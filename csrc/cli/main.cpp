@@ -1,0 +1,383 @@
+// `bfs` -- command-line driver, compatible with the reference's
+// `./a.out <src> <file>` (README.md:4-14, bfs.cu:783-823) and its stdout lines
+// (SURVEY Appendix A), plus the flags of SURVEY §5.6.
+//
+//   bfs <src> <edge-list|.mtx|.csr> [flags]
+//   bfs --rmat SCALE[:EF] [src] [flags]
+//
+// Execution models:
+//   default            1 GPU (HIP backend, device --device)
+//   --gpus P           P GPUs in one process, one host thread + one RCCL
+//                      communicator per GPU (ncclCommInitAll) -- replaces
+//                      the reference's intra-node bfs.cu
+//   --virtual-ranks P  P partitions on ONE device (threads + VirtualComm):
+//                      exercises the distributed code path on one GPU
+//   --cpu              CPU backend (no GPU needed)
+//   WORLD_SIZE > 1     one process per GPU (torchrun / any launcher): TCP
+//                      bootstrap on MASTER_ADDR:MASTER_PORT+1, RCCL -- replaces
+//                      the reference's MPI build bfs_mpi.cu
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "dbfs/engine.hpp"
+
+using namespace dbfs;
+
+namespace {
+
+struct Args {
+  int64_t src = 0;
+  bool src_given = false;
+  std::string path;
+  int gpus = 1;
+  int virtual_ranks = 0;
+  int device = 0;
+  bool cpu = false;
+  std::string mode = "do";
+  double alpha = 14.0, beta = 24.0;
+  int bu_lane_limit = 8;
+  int rmat_scale = 0, rmat_ef = 16;
+  int64_t uni_n = 0, uni_m = 0;
+  uint64_t seed = 1;
+  int roots = 0;
+  bool oracle = true;
+  bool validate = false;
+  std::string levels_out;
+  std::string cache_out;
+  bool json = false;
+  bool quiet = false;
+  bool phase_timing = false;
+};
+
+[[noreturn]] void usage(const char* msg = nullptr) {
+  if (msg) std::fprintf(stderr, "error: %s\n\n", msg);
+  std::fprintf(stderr,
+               "usage: bfs <src> <edge-list|.mtx|.csr> [flags]\n"
+               "       bfs --rmat SCALE[:EF] [<src>] [flags]\n"
+               "flags: --gpus P | --virtual-ranks P | --cpu | --device D\n"
+               "       --mode ref|td|bu|do|simple  --alpha A --beta B --bu-lane-limit K\n"
+               "       --rmat SCALE[:EF] | --uniform N:M   --seed S\n"
+               "       --roots K (random sources, GTEPS summary)  --no-oracle  --validate\n"
+               "       --levels-out FILE  --cache FILE (write binary CSR)  --json  --quiet  --phase-timing\n");
+  std::exit(2);
+}
+
+Args parse(int argc, char** argv) {
+  Args a;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + s).c_str());
+      return argv[++i];
+    };
+    if (s == "--gpus") a.gpus = std::stoi(next());
+    else if (s == "--virtual-ranks") a.virtual_ranks = std::stoi(next());
+    else if (s == "--device") a.device = std::stoi(next());
+    else if (s == "--cpu") a.cpu = true;
+    else if (s == "--mode") a.mode = next();
+    else if (s == "--alpha") a.alpha = std::stod(next());
+    else if (s == "--beta") a.beta = std::stod(next());
+    else if (s == "--bu-lane-limit") a.bu_lane_limit = std::stoi(next());
+    else if (s == "--rmat") {
+      std::string v = next();
+      auto c = v.find(':');
+      a.rmat_scale = std::stoi(v.substr(0, c));
+      if (c != std::string::npos) a.rmat_ef = std::stoi(v.substr(c + 1));
+    } else if (s == "--uniform") {
+      std::string v = next();
+      auto c = v.find(':');
+      if (c == std::string::npos) usage("--uniform expects N:M");
+      a.uni_n = std::stoll(v.substr(0, c));
+      a.uni_m = std::stoll(v.substr(c + 1));
+    } else if (s == "--seed") a.seed = std::stoull(next());
+    else if (s == "--roots") a.roots = std::stoi(next());
+    else if (s == "--no-oracle") a.oracle = false;
+    else if (s == "--validate") a.validate = true;
+    else if (s == "--levels-out") a.levels_out = next();
+    else if (s == "--cache") a.cache_out = next();
+    else if (s == "--json") a.json = true;
+    else if (s == "--quiet") a.quiet = true;
+    else if (s == "--phase-timing") a.phase_timing = true;
+    else if (s == "-h" || s == "--help") usage();
+    else if (!s.empty() && s[0] == '-' && s.size() > 1 && !std::isdigit(static_cast<unsigned char>(s[1])))
+      usage(("unknown flag " + s).c_str());
+    else pos.push_back(s);
+  }
+  const bool synth = a.rmat_scale > 0 || a.uni_n > 0;
+  if (!synth) {
+    if (pos.size() != 2) usage("expected <src> <edge-list> (reference argument order)");
+    a.path = pos[1];
+  } else if (pos.size() > 1) {
+    usage("synthetic graphs take at most one positional argument (<src>)");
+  }
+  if (!pos.empty()) {
+    char* end = nullptr;
+    a.src = std::strtoll(pos[0].c_str(), &end, 10);
+    if (!end || *end) usage("source vertex must be an integer");
+    a.src_given = true;
+  }
+  if (a.gpus < 1) usage("--gpus must be >= 1");
+  return a;
+}
+
+int env_int(const char* k, int dflt) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+// One rank's state.
+struct RankCtx {
+  std::unique_ptr<Backend> be;
+  std::unique_ptr<Comm> comm;
+  std::unique_ptr<DeviceGraph> graph;
+  std::unique_ptr<Engine> engine;
+};
+
+void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCtx&)>& fn) {
+  if (ranks.size() == 1) {
+    fn(0, ranks[0]);
+    return;
+  }
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> errs(ranks.size());
+  for (size_t r = 0; r < ranks.size(); ++r)
+    th.emplace_back([&, r] {
+      try {
+        fn(static_cast<int>(r), ranks[r]);
+      } catch (...) {
+        errs[r] = std::current_exception();
+      }
+    });
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
+std::string json_run(const RunResult& r, const std::string& graph, int64_t n, int64_t m, int P, const char* mode,
+                     const std::string& backend) {
+  std::string s = "{\"graph\":\"" + graph + "\",\"n\":" + std::to_string(n) + ",\"m\":" + std::to_string(m) +
+                  ",\"ranks\":" + std::to_string(P) + ",\"mode\":\"" + mode + "\",\"backend\":\"" + backend +
+                  "\",\"source\":" + std::to_string(r.source) + ",\"ms\":" + std::to_string(r.ms) +
+                  ",\"reached\":" + std::to_string(r.reached) + ",\"edges\":" + std::to_string(r.edges) +
+                  ",\"gteps\":" + std::to_string(r.gteps) + ",\"depth\":" + std::to_string(r.depth) + ",\"levels\":[";
+  for (size_t i = 0; i < r.levels.size(); ++i) {
+    const auto& l = r.levels[i];
+    if (i) s += ",";
+    s += "{\"l\":" + std::to_string(l.level) + ",\"dir\":\"" + std::string(1, l.direction) +
+         "\",\"frontier\":" + std::to_string(l.frontier) + ",\"edges\":" + std::to_string(l.frontier_edges) +
+         ",\"new\":" + std::to_string(l.discovered) + ",\"ms\":" + std::to_string(l.ms) + "}";
+  }
+  return s + "]}";
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a = parse(argc, argv);
+  const int world = env_int("WORLD_SIZE", 1);
+  const int wrank = env_int("RANK", 0);
+  const bool multiproc = world > 1;
+  const bool leader = !multiproc || wrank == 0;
+  const bool ref_lines = !a.quiet && leader;
+  try {
+    // ---- graph ingestion ----
+    HostCSR full;
+    bool have_host = false;
+    std::string gname;
+    GenParams gp;
+    bool synth = false;
+    if (!a.path.empty()) {
+      gname = a.path;
+      if (ref_lines) std::printf("%s\n", a.path.c_str());
+      if (is_binary_csr(a.path)) {
+        full = read_binary_csr(a.path);
+      } else {
+        ReadOptions ro;
+        ro.verbose_reference_lines = ref_lines;
+        EdgeList el = read_edge_list(a.path, ro);
+        full = build_csr(el);
+      }
+      have_host = true;
+      if (ref_lines) std::printf("finish load graph\n");
+    } else {
+      synth = true;
+      if (a.rmat_scale > 0) {
+        gp = rmat_params(a.rmat_scale, a.rmat_ef, a.seed);
+        gname = "rmat" + std::to_string(a.rmat_scale) + "_ef" + std::to_string(a.rmat_ef);
+      } else {
+        gp = uniform_params(a.uni_n, a.uni_m, a.seed);
+        gname = "uniform_n" + std::to_string(a.uni_n) + "_m" + std::to_string(a.uni_m);
+      }
+      // Host copy only when the CPU oracle / cache / CPU backend needs it.
+      if (a.oracle || !a.cache_out.empty()) {
+        EdgeList el;
+        el.n = gp.n;
+        el.u.resize(static_cast<size_t>(gp.m));
+        el.v.resize(static_cast<size_t>(gp.m));
+        for (int64_t i = 0; i < gp.m; ++i) {
+          uint64_t u, v;
+          gen_edge(gp, static_cast<uint64_t>(i), u, v);
+          el.u[i] = static_cast<vid_t>(u);
+          el.v[i] = static_cast<vid_t>(v);
+        }
+        full = build_csr(el);
+        have_host = true;
+      }
+    }
+    const int64_t n = have_host ? full.n : gp.n;
+    const int64_t m_in = have_host ? full.input_edges : gp.m;
+    if (ref_lines) {
+      std::printf("Number of vertices %lld\n", static_cast<long long>(n));
+      std::printf("Number of edges %lld\n\n", static_cast<long long>(have_host ? full.directed_edges() : 2 * gp.m));
+    }
+    if (!a.cache_out.empty() && leader) write_binary_csr(a.cache_out, full);
+    if (a.src < 0 || a.src >= n) throw Error("source vertex " + std::to_string(a.src) + " out of range [0, " + std::to_string(n) + ")");
+
+    // ---- CPU oracle (bfs.cu:798-802) ----
+    std::vector<lvl_t> expected;
+    if (a.oracle && have_host && leader) {
+      if (ref_lines) std::printf("Starting sequential bfs.\n");
+      auto c0 = std::chrono::steady_clock::now();
+      expected = cpu_bfs(full, a.src).level;
+      auto c1 = std::chrono::steady_clock::now();
+      if (ref_lines)
+        std::printf("Elapsed time in milliseconds : %li ms.\n\n",
+                    static_cast<long>(std::chrono::duration_cast<std::chrono::milliseconds>(c1 - c0).count()));
+    }
+
+    // ---- ranks / devices ----
+    int P = 1;
+    if (multiproc) P = world;
+    else if (a.virtual_ranks > 0) P = a.virtual_ranks;
+    else if (!a.cpu) P = a.gpus;
+    const Partition part = Partition::block(n, P);
+    const int nlocal = multiproc ? 1 : P;
+    std::vector<RankCtx> ranks(static_cast<size_t>(nlocal));
+    if (!a.cpu && ref_lines) std::printf("Enabling peer access between GPU0 and GPU1...\n");
+    std::shared_ptr<VirtualGroup> vgroup;
+    if (a.virtual_ranks > 0 && !multiproc) vgroup = std::make_shared<VirtualGroup>(P);
+    for (int i = 0; i < nlocal; ++i) {
+      if (a.cpu) ranks[i].be = make_cpu_backend();
+      else if (multiproc) ranks[i].be = make_hip_backend(env_int("LOCAL_RANK", 0));
+      else if (a.virtual_ranks > 0) ranks[i].be = make_hip_backend(a.device);
+      else ranks[i].be = make_hip_backend(P > 1 ? i : a.device);
+    }
+    if (multiproc) {
+      const char* addr = std::getenv("MASTER_ADDR");
+      const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
+      TcpBootstrap boot(addr ? addr : "127.0.0.1", port, wrank, world);
+      std::string uid = boot.broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+      ranks[0].comm = std::make_unique<NcclComm>(uid, wrank, world, *ranks[0].be);
+    } else if (vgroup) {
+      for (int i = 0; i < P; ++i) ranks[i].comm = std::make_unique<VirtualComm>(vgroup, i, *ranks[i].be);
+    } else if (P > 1) {
+      std::vector<Backend*> bes;
+      for (auto& r : ranks) bes.push_back(r.be.get());
+      auto comms = NcclComm::init_all(bes);
+      for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
+    } else {
+      ranks[0].comm = std::make_unique<LocalComm>(*ranks[0].be);
+    }
+
+    EngineOptions eo;
+    eo.mode = parse_mode(a.mode);
+    eo.alpha = a.alpha;
+    eo.beta = a.beta;
+    eo.bu_lane_limit = a.bu_lane_limit;
+    eo.phase_timing = a.phase_timing;
+    run_ranks(ranks, [&](int i, RankCtx& rc) {
+      const int rk = multiproc ? wrank : i;
+      if (synth) rc.graph = DeviceGraph::generate(*rc.be, gp, part, rk);
+      else rc.graph = DeviceGraph::from_host(*rc.be, full, part, rk);
+      rc.engine = std::make_unique<Engine>(*rc.graph, *rc.comm, eo);
+    });
+
+    // ---- the reference's single run from <src> ----
+    std::vector<RunResult> res(static_cast<size_t>(nlocal));
+    std::vector<lvl_t> got;
+    std::vector<std::vector<int64_t>> viol(static_cast<size_t>(nlocal));
+    if (ref_lines) std::printf("Starting queue parallel bfs.\n");
+    run_ranks(ranks, [&](int i, RankCtx& rc) {
+      res[i] = rc.engine->run(a.src);
+      std::vector<lvl_t> lv = rc.engine->gather_levels();
+      if (i == 0) got = std::move(lv);
+      if (a.validate) viol[i] = rc.engine->validate(a.src);
+    });
+    if (ref_lines) std::printf("Elapsed time in milliseconds : %li ms.\n", static_cast<long>(res[0].ms));
+    int rc_exit = 0;
+    if (leader && !expected.empty()) {
+      for (int64_t i = 0; i < n; ++i) {
+        if (got[i] != expected[i]) {
+          std::printf("%lld %d %d\n", static_cast<long long>(i), got[i], expected[i]);
+          std::printf("Wrong output!\n");
+          return 1;
+        }
+      }
+      if (!a.quiet) std::printf("Output OK!\n\n");
+    }
+    if (a.validate && leader) {
+      const auto& v = viol[0];
+      if (v[0] || v[1] || v[2]) {
+        std::printf("Validation FAILED: depth-gap %lld, reached-unreached %lld, orphan %lld\n",
+                    static_cast<long long>(v[0]), static_cast<long long>(v[1]), static_cast<long long>(v[2]));
+        rc_exit = 1;
+      } else if (!a.quiet) {
+        std::printf("Validation OK (Graph500 level checks)\n");
+      }
+    }
+    if (!a.levels_out.empty() && leader) write_levels(a.levels_out, got);
+    const std::string bname = ranks[0].be->name();
+    if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
+
+    // ---- optional K random roots (Graph500-style GTEPS) ----
+    if (a.roots > 0) {
+      std::mt19937_64 rng(a.seed * 7919 + 17);
+      std::vector<int64_t> roots;
+      // roots are chosen on the leader among vertices with degree >= 1
+      int tries = 0;
+      while (static_cast<int>(roots.size()) < a.roots && tries < 100 * a.roots) {
+        ++tries;
+        const int64_t v = static_cast<int64_t>(rng() % static_cast<uint64_t>(n));
+        // degree check through the owning rank's shard (single-process: any rank ctx)
+        int64_t deg = 0;
+        if (!multiproc) {
+          const int own = part.owner(v);
+          deg = ranks[own].graph->degrees_of({v - part.lo(own)})[0];
+        } else {
+          const int own = part.owner(v);
+          int64_t d = (own == wrank) ? ranks[0].graph->degrees_of({v - part.lo(own)})[0] : 0;
+          deg = ranks[0].comm->sum_host(d);
+        }
+        if (deg > 0) roots.push_back(v);
+      }
+      double inv_sum = 0, ms_sum = 0;
+      int64_t e_sum = 0;
+      for (int64_t root : roots) {
+        run_ranks(ranks, [&](int i, RankCtx& rc) { res[i] = rc.engine->run(root); });
+        inv_sum += res[0].gteps > 0 ? 1.0 / res[0].gteps : 0;
+        ms_sum += res[0].ms;
+        e_sum += res[0].edges;
+        if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
+      }
+      if (leader && !roots.empty()) {
+        const double hm = inv_sum > 0 ? roots.size() / inv_sum : 0.0;
+        std::printf("roots %zu  mean ms %.3f  harmonic-mean GTEPS %.3f  aggregate GTEPS %.3f\n", roots.size(),
+                    ms_sum / roots.size(), hm, ms_sum > 0 ? e_sum / (ms_sum * 1e6) : 0.0);
+      }
+    }
+    return rc_exit;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "bfs: %s\n", e.what());
+    return 1;
+  }
+}

@@ -1,0 +1,134 @@
+// LocalComm, VirtualComm and the host-value helpers shared by every Comm.
+//
+// VirtualComm runs P ranks as threads of one process on any backend: the
+// partitioned engine (shards, owner routing, bitmap exchange) is then testable
+// on a single GPU or on the CPU, which the reference cannot do (its multi-GPU
+// path needs >= 2 real GPUs with peer access).
+#include <algorithm>
+#include <vector>
+
+#include "dbfs/comm.hpp"
+
+namespace dbfs {
+
+int64_t Comm::sum_host(int64_t x) {
+  DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
+  DBuf<int64_t> b(*be_, 1);
+  be_->to_device(b.data(), &x, sizeof(x));
+  allreduce_sum_i64(b.data(), 1);
+  be_->to_host(&x, b.data(), sizeof(x));
+  return x;
+}
+
+double Comm::max_host(double x) {
+  DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
+  const int n = size();
+  DBuf<double> s(*be_, 1), r(*be_, static_cast<size_t>(n));
+  be_->to_device(s.data(), &x, sizeof(x));
+  allgather(s.data(), r.data(), sizeof(double));
+  std::vector<double> h(static_cast<size_t>(n));
+  be_->to_host(h.data(), r.data(), h.size() * sizeof(double));
+  return *std::max_element(h.begin(), h.end());
+}
+
+// ---- LocalComm ----------------------------------------------------------------
+
+void LocalComm::alltoall(const void* send, void* recv, size_t bytes) {
+  if (send != recv) be_->copy_async(recv, send, bytes);
+}
+void LocalComm::allgather(const void* send, void* recv, size_t bytes) {
+  if (send != recv) be_->copy_async(recv, send, bytes);
+}
+void LocalComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                          const int64_t* rd, size_t eb) {
+  DBFS_CHECK(sc[0] == rc[0], "LocalComm alltoallv count mismatch");
+  be_->copy_async(static_cast<char*>(recv) + rd[0] * eb, static_cast<const char*>(send) + sd[0] * eb,
+                  static_cast<size_t>(sc[0]) * eb);
+}
+void LocalComm::barrier() { be_->synchronize(); }
+
+// ---- VirtualGroup / VirtualComm -----------------------------------------------
+
+VirtualGroup::VirtualGroup(int nranks) : n_(nranks), slots_(static_cast<size_t>(nranks)) {
+  DBFS_CHECK(nranks >= 1, "virtual group needs >= 1 rank");
+}
+
+void VirtualGroup::barrier() {
+  std::unique_lock<std::mutex> lk(mu_);
+  const uint64_t gen = generation_;
+  if (++arrived_ == n_) {
+    arrived_ = 0;
+    ++generation_;
+    cv_.notify_all();
+  } else {
+    cv_.wait(lk, [&] { return generation_ != gen; });
+  }
+}
+
+VirtualComm::VirtualComm(std::shared_ptr<VirtualGroup> g, int rank, Backend& be) : g_(std::move(g)), rank_(rank) {
+  DBFS_CHECK(rank >= 0 && rank < g_->size(), "virtual rank out of range");
+  bind_backend(&be);
+}
+
+void VirtualComm::alltoall(const void* send, void* recv, size_t bytes) {
+  be_->synchronize();
+  auto& sl = g_->slots();
+  sl[rank_].send = send;
+  sl[rank_].be = be_;
+  g_->barrier();
+  for (int r = 0; r < size(); ++r)
+    be_->copy_async(static_cast<char*>(recv) + r * bytes, static_cast<const char*>(sl[r].send) + rank_ * bytes, bytes);
+  be_->synchronize();
+  g_->barrier();
+}
+
+void VirtualComm::allgather(const void* send, void* recv, size_t bytes) {
+  be_->synchronize();
+  auto& sl = g_->slots();
+  sl[rank_].send = send;
+  g_->barrier();
+  for (int r = 0; r < size(); ++r)
+    be_->copy_async(static_cast<char*>(recv) + r * bytes, sl[r].send, bytes);
+  be_->synchronize();
+  g_->barrier();
+}
+
+void VirtualComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  be_->synchronize();
+  auto& sl = g_->slots();
+  sl[rank_].send = buf;
+  g_->barrier();
+  std::vector<int64_t> acc(count, 0), tmp(count);
+  for (int r = 0; r < size(); ++r) {
+    be_->to_host(tmp.data(), sl[r].send, count * sizeof(int64_t));
+    for (size_t i = 0; i < count; ++i) acc[i] += tmp[i];
+  }
+  g_->barrier();
+  be_->to_device(buf, acc.data(), count * sizeof(int64_t));
+  g_->barrier();
+}
+
+void VirtualComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                            const int64_t* rd, size_t eb) {
+  be_->synchronize();
+  auto& sl = g_->slots();
+  sl[rank_].send = send;
+  sl[rank_].counts = sc;
+  sl[rank_].displs = sd;
+  g_->barrier();
+  for (int r = 0; r < size(); ++r) {
+    const int64_t n = sl[r].counts[rank_];
+    DBFS_CHECK(n == rc[r], "VirtualComm alltoallv count mismatch");
+    be_->copy_async(static_cast<char*>(recv) + rd[r] * eb,
+                    static_cast<const char*>(sl[r].send) + sl[r].displs[rank_] * eb, static_cast<size_t>(n) * eb);
+  }
+  be_->synchronize();
+  g_->barrier();
+}
+
+void VirtualComm::barrier() {
+  be_->synchronize();
+  g_->barrier();
+}
+
+}  // namespace dbfs

@@ -1,0 +1,122 @@
+// RCCL communicator: the per-level exchange over xGMI.
+//
+// Reference call sites replaced: per-pair synchronous
+// cudaMemcpyPeer (bfs.cu:595-609) and CUDA-aware MPI_Sendrecv / MPI_Allreduce
+// (bfs_mpi.cu:614-621).  Every collective here is enqueued on the owning
+// backend's HIP stream, so it is ordered after the expansion kernels without a
+// host synchronisation.  On MI355X each GPU has 7 direct xGMI links, one per
+// peer: all-to-all and all-gather drive all of them at once, which is why the
+// engine exchanges equal-sized bitmap slices (ncclAllToAll / ncclAllGather)
+// instead of ring all-reduces.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dbfs/comm.hpp"
+
+namespace dbfs {
+
+#define NCCL_CHECK(expr)                                                                         \
+  do {                                                                                           \
+    ncclResult_t r_ = (expr);                                                                    \
+    if (r_ != ncclSuccess)                                                                       \
+      ::dbfs::raise_error(__FILE__, __LINE__,                                                    \
+                          std::string("RCCL error ") + ncclGetErrorString(r_) + " in " #expr);   \
+  } while (0)
+
+#define HIP_CHECK(expr)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      ::dbfs::raise_error(__FILE__, __LINE__, std::string("HIP error ") + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+inline ncclComm_t C(void* p) { return static_cast<ncclComm_t>(p); }
+inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->stream_handle()); }
+}  // namespace
+
+std::string NcclComm::unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+NcclComm::NcclComm(const std::string& uid, int rank, int nranks, Backend& be) : rank_(rank), size_(nranks) {
+  DBFS_CHECK(be.kind() == DeviceKind::HIP, "NcclComm requires a HIP backend");
+  DBFS_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "bad RCCL unique id size");
+  bind_backend(&be);
+  HIP_CHECK(hipSetDevice(be.device_id()));
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t c = nullptr;
+  NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  comm_ = c;
+}
+
+std::vector<std::unique_ptr<NcclComm>> NcclComm::init_all(const std::vector<Backend*>& bes) {
+  const int n = static_cast<int>(bes.size());
+  std::vector<int> devs(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) {
+    DBFS_CHECK(bes[i]->kind() == DeviceKind::HIP, "NcclComm requires HIP backends");
+    devs[i] = bes[i]->device_id();
+  }
+  std::vector<ncclComm_t> comms(static_cast<size_t>(n));
+  NCCL_CHECK(ncclCommInitAll(comms.data(), n, devs.data()));
+  std::vector<std::unique_ptr<NcclComm>> out;
+  for (int i = 0; i < n; ++i) {
+    std::unique_ptr<NcclComm> c(new NcclComm());
+    c->comm_ = comms[i];
+    c->rank_ = i;
+    c->size_ = n;
+    c->bind_backend(bes[i]);
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
+NcclComm::~NcclComm() {
+  if (comm_) ncclCommDestroy(C(comm_));
+}
+
+void NcclComm::alltoall(const void* send, void* recv, size_t bytes) {
+  HIP_CHECK(hipSetDevice(be_->device_id()));
+  NCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclChar, C(comm_), S(be_)));
+}
+
+void NcclComm::allgather(const void* send, void* recv, size_t bytes) {
+  HIP_CHECK(hipSetDevice(be_->device_id()));
+  NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, C(comm_), S(be_)));
+}
+
+void NcclComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  HIP_CHECK(hipSetDevice(be_->device_id()));
+  NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, C(comm_), S(be_)));
+}
+
+void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                         const int64_t* rd, size_t eb) {
+  HIP_CHECK(hipSetDevice(be_->device_id()));
+  NCCL_CHECK(ncclGroupStart());
+  for (int r = 0; r < size_; ++r) {
+    if (sc[r] > 0)
+      NCCL_CHECK(ncclSend(static_cast<const char*>(send) + sd[r] * eb, static_cast<size_t>(sc[r]) * eb, ncclChar, r,
+                          C(comm_), S(be_)));
+    if (rc[r] > 0)
+      NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + rd[r] * eb, static_cast<size_t>(rc[r]) * eb, ncclChar, r,
+                          C(comm_), S(be_)));
+  }
+  NCCL_CHECK(ncclGroupEnd());
+}
+
+void NcclComm::barrier() {
+  DBuf<int64_t> b(*be_, 1);
+  be_->memset_async(b.data(), 0, sizeof(int64_t));
+  allreduce_sum_i64(b.data(), 1);
+  be_->synchronize();
+}
+
+}  // namespace dbfs

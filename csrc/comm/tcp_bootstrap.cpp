@@ -1,0 +1,160 @@
+// Minimal TCP bootstrap (star topology, rank 0 hosts).
+//
+// Replaces MPI_Init/Comm_rank (bfs_mpi.cu:800-808): there is no MPI on this
+// platform, and the launcher (torch.distributed.run or any other) only needs to
+// provide RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT.  Used to ship the
+// 128-byte RCCL unique id and for host-side barriers.
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "dbfs/comm.hpp"
+
+namespace dbfs {
+namespace {
+
+void write_all(int fd, const void* p, size_t n) {
+  const char* c = static_cast<const char*>(p);
+  while (n) {
+    ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) throw Error(std::string("bootstrap send failed: ") + std::strerror(errno));
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+}
+
+void read_all(int fd, void* p, size_t n) {
+  char* c = static_cast<char*>(p);
+  while (n) {
+    ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) throw Error("bootstrap peer closed the connection");
+    c += k;
+    n -= static_cast<size_t>(k);
+  }
+}
+
+void send_msg(int fd, const std::string& s) {
+  const uint64_t n = s.size();
+  write_all(fd, &n, sizeof(n));
+  if (n) write_all(fd, s.data(), n);
+}
+
+std::string recv_msg(int fd) {
+  uint64_t n = 0;
+  read_all(fd, &n, sizeof(n));
+  std::string s(n, '\0');
+  if (n) read_all(fd, &s[0], n);
+  return s;
+}
+
+sockaddr_in resolve(const std::string& host, int port) {
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res)
+      throw Error("bootstrap cannot resolve host " + host);
+    a.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+    freeaddrinfo(res);
+  }
+  return a;
+}
+
+}  // namespace
+
+TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nranks, double timeout_s)
+    : rank_(rank), size_(nranks) {
+  DBFS_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad bootstrap rank/size");
+  if (nranks == 1) return;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  if (rank == 0) {
+    listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (listen_fd_ < 0) throw Error("bootstrap socket() failed");
+    int one = 1;
+    setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port));
+    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
+      throw Error("bootstrap bind to port " + std::to_string(port) + " failed: " + std::strerror(errno));
+    if (::listen(listen_fd_, nranks) != 0) throw Error("bootstrap listen failed");
+    peers_.assign(static_cast<size_t>(nranks), -1);
+    for (int k = 1; k < nranks; ++k) {
+      int fd = ::accept(listen_fd_, nullptr, nullptr);
+      if (fd < 0) throw Error("bootstrap accept failed");
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      int32_t r = -1;
+      read_all(fd, &r, sizeof(r));
+      if (r <= 0 || r >= nranks || peers_[r] != -1) throw Error("bootstrap got bad rank " + std::to_string(r));
+      peers_[r] = fd;
+    }
+  } else {
+    const sockaddr_in a = resolve(host, port);
+    int fd = -1;
+    for (;;) {
+      fd = ::socket(AF_INET, SOCK_STREAM, 0);
+      if (fd < 0) throw Error("bootstrap socket() failed");
+      if (::connect(fd, reinterpret_cast<const sockaddr*>(&a), sizeof(a)) == 0) break;
+      ::close(fd);
+      if (std::chrono::steady_clock::now() > deadline)
+        throw Error("bootstrap connect to " + host + ":" + std::to_string(port) + " timed out");
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    const int32_t r = rank;
+    write_all(fd, &r, sizeof(r));
+    peers_.assign(1, fd);
+  }
+}
+
+TcpBootstrap::~TcpBootstrap() {
+  for (int fd : peers_)
+    if (fd >= 0) ::close(fd);
+  if (listen_fd_ >= 0) ::close(listen_fd_);
+}
+
+std::string TcpBootstrap::broadcast(const std::string& data, int root) {
+  DBFS_CHECK(root == 0, "TcpBootstrap broadcast supports root 0 only");
+  if (size_ == 1) return data;
+  if (rank_ == 0) {
+    for (int r = 1; r < size_; ++r) send_msg(peers_[r], data);
+    return data;
+  }
+  return recv_msg(peers_[0]);
+}
+
+std::vector<std::string> TcpBootstrap::allgather(const std::string& data) {
+  std::vector<std::string> out(static_cast<size_t>(size_));
+  if (size_ == 1) {
+    out[0] = data;
+    return out;
+  }
+  if (rank_ == 0) {
+    out[0] = data;
+    for (int r = 1; r < size_; ++r) out[r] = recv_msg(peers_[r]);
+    for (int r = 1; r < size_; ++r)
+      for (int k = 0; k < size_; ++k) send_msg(peers_[r], out[k]);
+  } else {
+    send_msg(peers_[0], data);
+    for (int k = 0; k < size_; ++k) out[k] = recv_msg(peers_[0]);
+  }
+  return out;
+}
+
+void TcpBootstrap::barrier() { allgather(std::string()); }
+
+}  // namespace dbfs

@@ -1,0 +1,498 @@
+// Distributed BFS engine (see dbfs/engine.hpp for the design summary).
+//
+// Per level of the bitmap engine (rank r of P, W = slice words):
+//   TD: compact(frontier[r]) -> work list; memset(next); td_expand -> next (N bits);
+//       P > 1: alltoall(next slices) -> recv (P x W words, OR-reduced in update)
+//   BU: bu_step(visited[r], frontier[*]) -> cand (W words)
+//   update(cand) -> visited[r] |= new, frontier[r] = new, level[new] = L+1,
+//                   per-segment counts/degree sums
+//   scan -> work-list offsets + local totals
+//   P > 1: allgather(frontier[r]) -> frontier[*]; visited |= frontier
+//   allreduce(totals) -> host: termination + Beamer direction heuristic
+// Reference per level (bfs.cu:569-620): kernel per device, full device sync,
+// serialized peer copies per (i, j), host reads of managed counters, memset.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "dbfs/engine.hpp"
+
+namespace dbfs {
+
+Mode parse_mode(const std::string& s) {
+  if (s == "ref" || s == "reference") return Mode::Ref;
+  if (s == "td" || s == "topdown" || s == "top-down") return Mode::TopDown;
+  if (s == "bu" || s == "bottomup" || s == "bottom-up") return Mode::BottomUp;
+  if (s == "do" || s == "diropt" || s == "direction-optimizing" || s == "hybrid") return Mode::DirOpt;
+  if (s == "simple" || s == "status") return Mode::Simple;
+  throw Error("unknown mode '" + s + "' (expected ref|td|bu|do|simple)");
+}
+
+const char* mode_name(Mode m) {
+  switch (m) {
+    case Mode::Ref: return "ref";
+    case Mode::TopDown: return "td";
+    case Mode::BottomUp: return "bu";
+    case Mode::DirOpt: return "do";
+    case Mode::Simple: return "simple";
+  }
+  return "?";
+}
+
+// ---- DeviceGraph ----------------------------------------------------------------
+
+std::unique_ptr<DeviceGraph> DeviceGraph::from_host(Backend& be, const HostCSR& csr, const Partition& part,
+                                                    int rank) {
+  DBFS_CHECK(csr.n == part.n, "partition vertex count does not match the graph");
+  auto g = std::unique_ptr<DeviceGraph>(new DeviceGraph());
+  g->be_ = &be;
+  g->part_ = part;
+  g->rank_ = rank;
+  g->lo_ = part.lo(rank);
+  g->rows_ = part.count(rank);
+  g->input_edges_ = csr.input_edges;
+  const eid_t* ro = nullptr;
+  const vid_t* col = nullptr;
+  std::vector<eid_t> rel;
+  if (csr.row_lo == 0 && csr.rows == csr.n) {
+    const eid_t base = csr.row_off[g->lo_];
+    rel.resize(static_cast<size_t>(g->rows_ + 1));
+    for (int64_t r = 0; r <= g->rows_; ++r) rel[r] = csr.row_off[g->lo_ + r] - base;
+    ro = rel.data();
+    col = csr.col.data() + base;
+  } else {
+    DBFS_CHECK(csr.row_lo == g->lo_ && csr.rows == g->rows_, "host shard does not match this rank's partition");
+    ro = csr.row_off.data();
+    col = csr.col.data();
+  }
+  g->nnz_ = ro[g->rows_];
+  g->row_off_ = DBuf<eid_t>(be, static_cast<size_t>(g->rows_ + 1));
+  g->col_ = DBuf<vid_t>(be, static_cast<size_t>(std::max<int64_t>(g->nnz_, 1)));
+  be.to_device(g->row_off_.data(), ro, static_cast<size_t>(g->rows_ + 1) * sizeof(eid_t));
+  if (g->nnz_) be.to_device(g->col_.data(), col, static_cast<size_t>(g->nnz_) * sizeof(vid_t));
+  return g;
+}
+
+std::unique_ptr<DeviceGraph> DeviceGraph::generate(Backend& be, const GenParams& p, const Partition& part, int rank) {
+  DBFS_CHECK(p.n == part.n, "partition vertex count does not match the generator");
+  DBFS_CHECK(p.n <= int64_t(UINT32_MAX), "generator vertex count exceeds 2^32");
+  auto g = std::unique_ptr<DeviceGraph>(new DeviceGraph());
+  g->be_ = &be;
+  g->part_ = part;
+  g->rank_ = rank;
+  g->lo_ = part.lo(rank);
+  g->rows_ = part.count(rank);
+  g->input_edges_ = p.m;
+  g->row_off_ = DBuf<eid_t>(be, static_cast<size_t>(g->rows_ + 1));
+  be.memset_async(g->row_off_.data(), 0, g->row_off_.bytes());
+  be.gen_count_degrees(p, g->lo_, g->rows_, g->row_off_.data());
+  be.exclusive_scan(g->row_off_.data(), g->rows_);
+  eid_t nnz = 0;
+  be.to_host(&nnz, g->row_off_.data() + g->rows_, sizeof(eid_t));
+  g->nnz_ = nnz;
+  g->col_ = DBuf<vid_t>(be, static_cast<size_t>(std::max<int64_t>(nnz, 1)));
+  {
+    DBuf<eid_t> cursor(be, static_cast<size_t>(std::max<int64_t>(g->rows_, 1)));
+    be.copy_async(cursor.data(), g->row_off_.data(), static_cast<size_t>(g->rows_) * sizeof(eid_t));
+    be.gen_fill(p, g->lo_, g->rows_, cursor.data(), g->col_.data());
+    be.synchronize();
+  }
+  return g;
+}
+
+ShardView DeviceGraph::view() const {
+  ShardView v;
+  v.row_off = row_off_.data();
+  v.col = col_.data();
+  v.n = part_.n;
+  v.lo = lo_;
+  v.rows = rows_;
+  v.nnz = nnz_;
+  return v;
+}
+
+HostCSR DeviceGraph::to_host() const {
+  HostCSR h;
+  h.n = part_.n;
+  h.row_lo = lo_;
+  h.rows = rows_;
+  h.input_edges = input_edges_;
+  h.row_off.resize(static_cast<size_t>(rows_ + 1));
+  h.col.resize(static_cast<size_t>(nnz_));
+  be_->to_host(h.row_off.data(), row_off_.data(), h.row_off.size() * sizeof(eid_t));
+  if (nnz_) be_->to_host(h.col.data(), col_.data(), h.col.size() * sizeof(vid_t));
+  return h;
+}
+
+std::vector<eid_t> DeviceGraph::degrees_of(const std::vector<int64_t>& local_rows) const {
+  std::vector<eid_t> out;
+  out.reserve(local_rows.size());
+  for (int64_t r : local_rows) {
+    DBFS_CHECK(r >= 0 && r < rows_, "row out of range");
+    eid_t a[2];
+    be_->to_host(a, row_off_.data() + r, sizeof(a));
+    out.push_back(a[1] - a[0]);
+  }
+  return out;
+}
+
+// ---- Engine ----------------------------------------------------------------------
+
+Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
+    : g_(g), comm_(comm), be_(g.backend()), opt_(opt), part_(g.partition()) {
+  DBFS_CHECK(comm.size() == part_.nranks, "communicator size does not match the partition");
+  DBFS_CHECK(comm.rank() == g.rank(), "communicator rank does not match the shard");
+  comm_.bind_backend(&be_);
+  total_directed_ = comm_.sum_host(g.nnz());
+  level_ = DBuf<lvl_t>(be_, static_cast<size_t>(std::max<int64_t>(g.rows(), 1)));
+  be_.fill_level(level_.data(), g.rows(), kUnreached);
+}
+
+Engine::~Engine() = default;
+
+void Engine::alloc_bitmap_state() {
+  if (bitmap_ready_) return;
+  const int64_t W = part_.slice_words(), GW = part_.global_words();
+  const int P = part_.nranks;
+  visited_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  frontier_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  next_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  if (P > 1) recv_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  cand_ = DBuf<word_t>(be_, static_cast<size_t>(W));
+  nseg_ = div_up(W, kSegWords);
+  seg_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(nseg_ + 1));
+  seg_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(nseg_ + 1));
+  qscan_ = DBuf<int64_t>(be_, static_cast<size_t>(g_.rows() + 1));
+  qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
+  blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
+  stats_ = DBuf<int64_t>(be_, 8);
+  bitmap_ready_ = true;
+}
+
+void Engine::alloc_ref_state() {
+  if (ref_ready_) return;
+  const int P = part_.nranks;
+  const int64_t cap = part_.part;
+  dist_ = DBuf<lvl_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.n, 1)));
+  queue_ = DBuf<vid_t>(be_, static_cast<size_t>(std::max<int64_t>(cap, 1)));
+  buckets_ = DBuf<vid_t>(be_, static_cast<size_t>(P * cap));
+  recvq_ = DBuf<vid_t>(be_, static_cast<size_t>(P * cap));
+  bucket_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * P));
+  qcount_ = DBuf<int64_t>(be_, 1);
+  ref_ready_ = true;
+}
+
+RunResult Engine::run(int64_t source) {
+  DBFS_CHECK(source >= 0 && source < part_.n, "source vertex out of range");
+  RunResult r;
+  if (opt_.mode == Mode::Ref) {
+    r = run_ref(source);
+    // Traversed-edge accounting (Graph500), outside the timed region.
+    DBuf<int64_t> acc(be_, 2);
+    be_.reached_degree_sum(g_.view(), level_.data(), acc.data());
+    comm_.allreduce_sum_i64(acc.data(), 2);
+    int64_t h[2];
+    be_.to_host(h, acc.data(), sizeof(h));
+    r.reached = h[0];
+    r.edges = h[1] / 2;
+  } else {
+    // The bitmap engine already knows sum(deg) of every level's new vertices.
+    r = run_bitmap(source);
+  }
+  r.gteps = r.ms > 0 ? static_cast<double>(r.edges) / (r.ms * 1e6) : 0.0;
+  return r;
+}
+
+RunResult Engine::run_bitmap(int64_t source) {
+  alloc_bitmap_state();
+  const int P = part_.nranks;
+  const int me = comm_.rank();
+  const int64_t W = part_.slice_words(), GW = part_.global_words();
+  const int64_t lo = g_.lo();
+  const ShardView gv = g_.view();
+  word_t* vis_own = visited_.data() + me * W;
+  word_t* fr_own = frontier_.data() + me * W;
+
+  RunResult res;
+  res.source = source;
+  be_.reset_events();
+  comm_.barrier();
+  const auto t0 = std::chrono::steady_clock::now();
+
+  // ---- init (inside the timed window) ----
+  be_.fill_level(level_.data(), g_.rows(), kUnreached);
+  be_.memset_async(visited_.data(), 0, visited_.bytes());
+  be_.memset_async(cand_.data(), 0, cand_.bytes());
+  if (part_.owner(source) == me) be_.set_bit(cand_.data(), source - lo);
+
+  auto update_and_exchange = [&](const word_t* cand, int nchunks, int64_t stride, lvl_t new_level,
+                                 int64_t* host_stats) {
+    UpdateArgs ua;
+    ua.g = gv;
+    ua.cand = cand;
+    ua.nchunks = nchunks;
+    ua.cand_stride = stride;
+    ua.visited = vis_own;
+    ua.frontier = fr_own;
+    ua.level = level_.data();
+    ua.new_level = new_level;
+    ua.words = W;
+    ua.seg_cnt = seg_cnt_.data();
+    ua.seg_deg = seg_deg_.data();
+    be_.update_frontier(ua);
+    ScanArgs sa;
+    sa.seg_cnt = seg_cnt_.data();
+    sa.seg_deg = seg_deg_.data();
+    sa.nseg = nseg_;
+    sa.stats = stats_.data();
+    sa.qscan = qscan_.data();
+    be_.scan_segments(sa);
+    if (P > 1) {
+      comm_.allgather(fr_own, frontier_.data(), static_cast<size_t>(W) * sizeof(word_t));
+      be_.bitmap_or(visited_.data(), frontier_.data(), GW);
+    }
+    comm_.allreduce_sum_i64(stats_.data() + 2, 2);
+    be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
+  };
+
+  int64_t hs[4];
+  update_and_exchange(cand_.data(), 1, W, 0, hs);
+  int64_t q_local = hs[0], m_local = hs[1], n_f = hs[2], m_f = hs[3];
+  int64_t vis_deg = m_f;
+  int64_t prev_nf = 0;
+
+  char dir;
+  switch (opt_.mode) {
+    case Mode::BottomUp: dir = 'B'; break;
+    case Mode::Simple: dir = 'S'; break;
+    default: dir = 'T'; break;
+  }
+  lvl_t L = 0;
+  const double n_d = static_cast<double>(part_.n);
+  while (n_f > 0) {
+    if (opt_.mode == Mode::DirOpt) {
+      const double m_u = static_cast<double>(total_directed_ - vis_deg);
+      if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha) {
+        dir = 'B';
+      } else if (dir == 'B' && static_cast<double>(n_f) < n_d / opt_.beta && n_f < prev_nf) {
+        dir = 'T';
+      }
+    }
+    const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    const word_t* cand = nullptr;
+    int nchunks = 1;
+    if (dir == 'T' || dir == 'S') {
+      be_.memset_async(next_.data(), 0, next_.bytes());
+      if (dir == 'T') {
+        if (q_local > 0) {
+          CompactArgs ca;
+          ca.g = gv;
+          ca.frontier = fr_own;
+          ca.words = W;
+          ca.seg_cnt_off = seg_cnt_.data();
+          ca.seg_deg_off = seg_deg_.data();
+          ca.qscan = qscan_.data();
+          ca.qbase = qbase_.data();
+          ca.blk_vstart = blk_vstart_.data();
+          be_.compact_frontier(ca);
+          TdArgs ta;
+          ta.g = gv;
+          ta.qscan = qscan_.data();
+          ta.qbase = qbase_.data();
+          ta.blk_vstart = blk_vstart_.data();
+          ta.q = q_local;
+          ta.m = m_local;
+          ta.visited = visited_.data();
+          ta.next = next_.data();
+          be_.td_expand(ta);
+        }
+      } else {
+        StatusArgs sa;
+        sa.g = gv;
+        sa.level = level_.data();
+        sa.cur = L;
+        sa.visited = visited_.data();
+        sa.next = next_.data();
+        be_.status_expand(sa);
+      }
+      if (P > 1) {
+        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
+        cand = recv_.data();
+        nchunks = P;
+      } else {
+        cand = next_.data();
+      }
+    } else {
+      BuArgs ba;
+      ba.g = gv;
+      ba.visited = vis_own;
+      ba.frontier = frontier_.data();
+      ba.cand = cand_.data();
+      ba.words = W;
+      ba.lane_limit = opt_.bu_lane_limit;
+      be_.bu_step(ba);
+      cand = cand_.data();
+    }
+    update_and_exchange(cand, nchunks, W, L + 1, hs);
+    LevelRecord rec;
+    rec.level = L;
+    rec.direction = dir;
+    rec.frontier = n_f;
+    rec.frontier_edges = m_f;
+    rec.discovered = hs[2];
+    if (opt_.phase_timing) {
+      const int ev1 = be_.record_event();
+      rec.ms = be_.elapsed_ms(ev0, ev1);
+    }
+    res.levels.push_back(rec);
+    prev_nf = n_f;
+    q_local = hs[0];
+    m_local = hs[1];
+    n_f = hs[2];
+    m_f = hs[3];
+    vis_deg += m_f;
+    ++L;
+  }
+  be_.synchronize();
+  const auto t1 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  res.ms = comm_.max_host(ms);
+  res.depth = res.levels.empty() ? 1 : static_cast<int>(res.levels.size());
+  res.edges = vis_deg / 2;
+  res.reached = 1;
+  for (const auto& l : res.levels) res.reached += l.discovered;
+  return res;
+}
+
+RunResult Engine::run_ref(int64_t source) {
+  alloc_ref_state();
+  const int P = part_.nranks;
+  const int me = comm_.rank();
+  const int64_t cap = part_.part;
+  const ShardView gv = g_.view();
+  RunResult res;
+  res.source = source;
+  be_.reset_events();
+  comm_.barrier();
+  const auto t0 = std::chrono::steady_clock::now();
+
+  // initializeCudaBfs2 (bfs.cu:402-422): distance = INT_MAX everywhere, 0 at the
+  // source on every rank; the source is queued on its owner only.
+  be_.fill_level(dist_.data(), part_.n, kUnreached);
+  be_.fill_level(dist_.data() + source, 1, 0);
+  int64_t q = 0;
+  if (part_.owner(source) == me) {
+    const vid_t s = static_cast<vid_t>(source);
+    be_.to_device(queue_.data(), &s, sizeof(s));
+    q = 1;
+  }
+  int64_t total_q = 1;
+  lvl_t L = 0;
+  std::vector<int64_t> hcnt(static_cast<size_t>(P)), hrc(static_cast<size_t>(P)), sd(static_cast<size_t>(P)),
+      rd(static_cast<size_t>(P));
+  while (total_q > 0) {
+    const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    be_.memset_async(bucket_cnt_.data(), 0, static_cast<size_t>(P) * sizeof(int64_t));
+    RefExpandArgs ea;
+    ea.g = gv;
+    ea.queue = queue_.data();
+    ea.q = q;
+    ea.next_level = L + 1;
+    ea.dist = dist_.data();
+    ea.part = part_.part;
+    ea.bucket_cnt = bucket_cnt_.data();
+    ea.buckets = buckets_.data();
+    ea.bucket_cap = cap;
+    be_.ref_expand(ea);
+    be_.to_host(hcnt.data(), bucket_cnt_.data(), static_cast<size_t>(P) * sizeof(int64_t));
+    if (P == 1) {
+      be_.copy_async(queue_.data(), buckets_.data(), static_cast<size_t>(hcnt[0]) * sizeof(vid_t));
+      q = hcnt[0];
+    } else {
+      // count exchange (the reference reads the peers' managed counters)
+      comm_.alltoall(bucket_cnt_.data(), bucket_cnt_.data() + P, sizeof(int64_t));
+      be_.to_host(hrc.data(), bucket_cnt_.data() + P, static_cast<size_t>(P) * sizeof(int64_t));
+      int64_t tot = 0;
+      for (int r = 0; r < P; ++r) {
+        sd[r] = r * cap;
+        rd[r] = tot;
+        tot += hrc[r];
+      }
+      comm_.alltoallv(buckets_.data(), hcnt.data(), sd.data(), recvq_.data(), hrc.data(), rd.data(), sizeof(vid_t));
+      be_.memset_async(qcount_.data(), 0, sizeof(int64_t));
+      RefAcceptArgs aa;
+      aa.recv = recvq_.data();
+      aa.total = tot;
+      aa.self_begin = rd[me];
+      aa.self_end = rd[me] + hrc[me];
+      aa.next_level = L + 1;
+      aa.dist = dist_.data();
+      aa.queue = queue_.data();
+      aa.qcount = qcount_.data();
+      be_.ref_accept(aa);
+      be_.to_host(&q, qcount_.data(), sizeof(int64_t));
+    }
+    LevelRecord rec;
+    rec.level = L;
+    rec.direction = 'R';
+    rec.frontier = total_q;
+    total_q = (P == 1) ? q : comm_.sum_host(q);
+    rec.discovered = total_q;
+    if (opt_.phase_timing) {
+      const int ev1 = be_.record_event();
+      rec.ms = be_.elapsed_ms(ev0, ev1);
+    }
+    res.levels.push_back(rec);
+    ++L;
+  }
+  // Owned slice of the replicated distances is authoritative.
+  be_.copy_async(level_.data(), dist_.data() + g_.lo(), static_cast<size_t>(g_.rows()) * sizeof(lvl_t));
+  be_.synchronize();
+  const auto t1 = std::chrono::steady_clock::now();
+  res.ms = comm_.max_host(std::chrono::duration<double, std::milli>(t1 - t0).count());
+  res.depth = static_cast<int>(res.levels.size());
+  return res;
+}
+
+std::vector<lvl_t> Engine::levels_local() const {
+  std::vector<lvl_t> h(static_cast<size_t>(g_.rows()));
+  if (!h.empty()) be_.to_host(h.data(), level_.data(), h.size() * sizeof(lvl_t));
+  return h;
+}
+
+std::vector<lvl_t> Engine::gather_levels() {
+  const int P = part_.nranks;
+  const int64_t part = part_.part;
+  DBuf<lvl_t> send(be_, static_cast<size_t>(part)), recv(be_, static_cast<size_t>(P * part));
+  be_.fill_level(send.data(), part, kUnreached);
+  be_.copy_async(send.data(), level_.data(), static_cast<size_t>(g_.rows()) * sizeof(lvl_t));
+  comm_.allgather(send.data(), recv.data(), static_cast<size_t>(part) * sizeof(lvl_t));
+  std::vector<lvl_t> h(static_cast<size_t>(P * part));
+  be_.to_host(h.data(), recv.data(), h.size() * sizeof(lvl_t));
+  h.resize(static_cast<size_t>(part_.n));
+  return h;
+}
+
+std::vector<int64_t> Engine::validate(int64_t source) {
+  const int P = part_.nranks;
+  const int64_t part = part_.part;
+  DBuf<lvl_t> send(be_, static_cast<size_t>(part)), full(be_, static_cast<size_t>(P * part));
+  be_.fill_level(send.data(), part, kUnreached);
+  be_.copy_async(send.data(), level_.data(), static_cast<size_t>(g_.rows()) * sizeof(lvl_t));
+  comm_.allgather(send.data(), full.data(), static_cast<size_t>(part) * sizeof(lvl_t));
+  DBuf<int64_t> out(be_, 3);
+  be_.memset_async(out.data(), 0, out.bytes());
+  ValidateArgs va;
+  va.g = g_.view();
+  va.level_global = full.data();
+  va.src = source;
+  va.out = out.data();
+  be_.validate_levels(va);
+  comm_.allreduce_sum_i64(out.data(), 3);
+  std::vector<int64_t> h(3);
+  be_.to_host(h.data(), out.data(), 3 * sizeof(int64_t));
+  return h;
+}
+
+}  // namespace dbfs

@@ -1,0 +1,248 @@
+// Device abstraction the BFS engine is written against.
+//
+// Two implementations:
+//   HipBackend  -- hand-written gfx950 HIP kernels on one HIP stream (the
+//                  production path; csrc/backend/hip_backend.hip,
+//                  csrc/kernels/*.hip).
+//   CpuBackend  -- straightforward host loops with the identical semantics,
+//                  used by the CPU test-suite (gloo multi-process tests) and
+//                  the `--cpu` CLI path (csrc/backend/cpu_backend.cpp).
+//
+// Every primitive is asynchronous with respect to the host on the backend's
+// stream (CpuBackend executes eagerly).  The reference has no such layer: its
+// kernels take raw pointers pulled out of __managed__ tables (bfs.cu:252-269,
+// 580-585).
+#pragma once
+
+#include <cstddef>
+#include <memory>
+#include <string>
+#include <utility>
+
+#include "dbfs/common.hpp"
+#include "dbfs/rmat.hpp"
+
+namespace dbfs {
+
+enum class DeviceKind { CPU, HIP };
+
+// ---- kernel argument blocks -------------------------------------------------
+
+// Local CSR shard: rows [lo, lo + rows) of an n-vertex graph, global column ids.
+struct ShardView {
+  const eid_t* row_off = nullptr;  // rows + 1 (local)
+  const vid_t* col = nullptr;      // row_off[rows]
+  int64_t n = 0, lo = 0, rows = 0, nnz = 0;
+};
+
+// Frontier bookkeeping is organised in "segments" of 64 bitmap words
+// (4096 vertices) -- one wave64 per segment in the HIP kernels.
+constexpr int kSegWords = 64;
+constexpr int kSegVertices = kSegWords * kWordBits;
+// Top-down expansion handles kTdEdgesPerBlock frontier edges per workgroup.
+constexpr int kTdThreads = 256;
+constexpr int kTdItems = 8;
+constexpr int kTdEdgesPerBlock = kTdThreads * kTdItems;
+
+// new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice:
+// visited |= new; frontier = new; level[v] = new_level for v in new;
+// seg_cnt[s] / seg_deg[s] = count / degree-sum of new vertices with degree > 0.
+struct UpdateArgs {
+  ShardView g;
+  const word_t* cand = nullptr;
+  int nchunks = 1;
+  int64_t cand_stride = 0;       // words between chunks
+  word_t* visited = nullptr;     // owned slice of the global visited bitmap
+  word_t* frontier = nullptr;    // owned slice of the global frontier bitmap
+  lvl_t* level = nullptr;        // rows
+  lvl_t new_level = 0;
+  int64_t words = 0;             // words of the owned slice
+  int64_t* seg_cnt = nullptr;    // nseg
+  int64_t* seg_deg = nullptr;    // nseg
+};
+
+// In-place exclusive scan of seg_cnt / seg_deg (nseg entries); writes totals to
+// stats[0..1] and stats[2..3] (the latter is all-reduced by the engine), and the
+// end sentinel qscan[total_cnt] = total_deg.
+struct ScanArgs {
+  int64_t* seg_cnt = nullptr;
+  int64_t* seg_deg = nullptr;
+  int64_t nseg = 0;
+  int64_t* stats = nullptr;
+  int64_t* qscan = nullptr;
+};
+
+// Owned frontier bitmap -> load-balanced top-down work list:
+// qscan[i] = exclusive prefix of degrees, qbase[i] = row_off[v_i] - qscan[i],
+// blk_vstart[b] = index of the entry covering edge b * kTdEdgesPerBlock.
+struct CompactArgs {
+  ShardView g;
+  const word_t* frontier = nullptr;
+  int64_t words = 0;
+  const int64_t* seg_cnt_off = nullptr;
+  const int64_t* seg_deg_off = nullptr;
+  int64_t* qscan = nullptr;
+  int64_t* qbase = nullptr;
+  int32_t* blk_vstart = nullptr;
+};
+
+// For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
+struct TdArgs {
+  ShardView g;
+  const int64_t* qscan = nullptr;
+  const int64_t* qbase = nullptr;
+  const int32_t* blk_vstart = nullptr;
+  int64_t q = 0;        // work-list entries
+  int64_t m = 0;        // work-list edges (qscan[q])
+  const word_t* visited = nullptr;  // global
+  word_t* next = nullptr;           // global
+};
+
+// For every owned unvisited v: if some neighbour u has frontier[u]: cand[v] = 1.
+struct BuArgs {
+  ShardView g;
+  const word_t* visited = nullptr;   // owned slice
+  const word_t* frontier = nullptr;  // global
+  word_t* cand = nullptr;            // owned slice (fully overwritten)
+  int64_t words = 0;
+  int lane_limit = 8;                // neighbours scanned per lane before wave cooperation
+};
+
+// Vertex-centric ("status array") top-down: every owned v with level[v] == cur
+// marks its unvisited neighbours in next.  (The reference's simple/multiBfs
+// variant, bfs.cu:101-130, made race-free.)
+struct StatusArgs {
+  ShardView g;
+  const lvl_t* level = nullptr;
+  lvl_t cur = 0;
+  const word_t* visited = nullptr;  // global
+  word_t* next = nullptr;           // global
+};
+
+// Reference-algorithm mode (bfs.cu:134-165): thread per frontier vertex,
+// atomicMin claim on a replicated distance array, one atomic counter per owner
+// bucket.
+struct RefExpandArgs {
+  ShardView g;
+  const vid_t* queue = nullptr;  // global ids of owned frontier vertices
+  int64_t q = 0;
+  lvl_t next_level = 0;
+  lvl_t* dist = nullptr;         // replicated, n entries
+  int64_t part = 0;              // owner(v) = v / part
+  int64_t* bucket_cnt = nullptr; // nranks
+  vid_t* buckets = nullptr;      // nranks * bucket_cap
+  int64_t bucket_cap = 0;
+};
+
+// Received ids: entries in [self_begin, self_end) were claimed locally and are
+// kept; the others are kept iff this rank's atomicMin claim succeeds.  Kept ids
+// are appended to queue (counter *qcount).
+struct RefAcceptArgs {
+  const vid_t* recv = nullptr;
+  int64_t total = 0;
+  int64_t self_begin = 0, self_end = 0;
+  lvl_t next_level = 0;
+  lvl_t* dist = nullptr;
+  vid_t* queue = nullptr;
+  int64_t* qcount = nullptr;
+};
+
+// Graph500-style validation of a full level array against a shard: counts
+// violations of (a) |level[u] - level[v]| <= 1 over every edge with both ends
+// reached, (b) reached-unreached edges, (c) reached v != src without a
+// neighbour at level[v] - 1.  out[0..2] += counts.
+struct ValidateArgs {
+  ShardView g;
+  const lvl_t* level_global = nullptr;  // n entries
+  int64_t src = 0;
+  int64_t* out = nullptr;               // 3 counters (device)
+};
+
+// ---- backend ----------------------------------------------------------------
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual DeviceKind kind() const = 0;
+  virtual std::string name() const = 0;
+  virtual int device_id() const { return -1; }
+  virtual void* stream_handle() { return nullptr; }
+
+  // memory (alloc/free are synchronous; copies/memsets are stream-ordered)
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void dealloc(void* p) = 0;
+  virtual void memset_async(void* p, int value, size_t bytes) = 0;
+  virtual void copy_async(void* dst, const void* src, size_t bytes) = 0;
+  virtual void to_host(void* host_dst, const void* dev_src, size_t bytes) = 0;   // blocking
+  virtual void to_device(void* dev_dst, const void* host_src, size_t bytes) = 0; // blocking
+  virtual void synchronize() = 0;
+
+  // timing: ms between two recorded points (events on HIP)
+  virtual int record_event() = 0;
+  virtual double elapsed_ms(int ev_begin, int ev_end) = 0;
+  virtual void reset_events() = 0;
+
+  // BFS primitives
+  virtual void fill_level(lvl_t* level, int64_t n, lvl_t value) = 0;
+  virtual void set_bit(word_t* bitmap, int64_t bit) = 0;
+  virtual void update_frontier(const UpdateArgs& a) = 0;
+  virtual void scan_segments(const ScanArgs& a) = 0;
+  virtual void compact_frontier(const CompactArgs& a) = 0;
+  virtual void td_expand(const TdArgs& a) = 0;
+  virtual void bu_step(const BuArgs& a) = 0;
+  virtual void status_expand(const StatusArgs& a) = 0;
+  virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;
+  virtual void ref_expand(const RefExpandArgs& a) = 0;
+  virtual void ref_accept(const RefAcceptArgs& a) = 0;
+  virtual void validate_levels(const ValidateArgs& a) = 0;
+
+  // graph construction on the device
+  // deg[r] += number of edge endpoints owned in rows [lo, lo + rows) (deg zeroed by caller)
+  virtual void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) = 0;
+  // in-place exclusive scan of n+1 entries (data[n] receives the total)
+  virtual void exclusive_scan(eid_t* data, int64_t n) = 0;
+  // col[cursor[u - lo]++] = v for every generated endpoint u owned
+  virtual void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) = 0;
+  // sum of degrees of vertices with level != kUnreached (device scalar out)
+  virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
+};
+
+std::unique_ptr<Backend> make_cpu_backend();
+std::unique_ptr<Backend> make_hip_backend(int device);
+int hip_device_count();  // 0 when no GPU / runtime unavailable
+
+// RAII device buffer.
+template <class T>
+class DBuf {
+ public:
+  DBuf() = default;
+  DBuf(Backend& be, size_t n) : be_(&be), n_(n) {
+    if (n_) p_ = static_cast<T*>(be_->alloc(n_ * sizeof(T)));
+  }
+  ~DBuf() { reset(); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept { *this = std::move(o); }
+  DBuf& operator=(DBuf&& o) noexcept {
+    if (this != &o) {
+      reset();
+      be_ = o.be_; p_ = o.p_; n_ = o.n_;
+      o.be_ = nullptr; o.p_ = nullptr; o.n_ = 0;
+    }
+    return *this;
+  }
+  void reset() {
+    if (p_ && be_) be_->dealloc(p_);
+    p_ = nullptr; n_ = 0;
+  }
+  T* data() const { return p_; }
+  size_t size() const { return n_; }
+  size_t bytes() const { return n_ * sizeof(T); }
+
+ private:
+  Backend* be_ = nullptr;
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+}  // namespace dbfs

@@ -1,0 +1,131 @@
+// Distributed level-synchronous BFS engine.
+//
+// Reference: runCudaQueueBfs (bfs.cu:542-629, bfs_mpi.cu:549-643) -- a host
+// loop that per level launches queueBfs on every device, synchronises, copies
+// owner buckets peer-to-peer and reads managed counters.  This engine keeps the
+// level-synchronous, owner-computes structure but:
+//   * shards the CSR (owned rows only) instead of replicating it per device;
+//   * represents frontier / visited as bitmaps (64 vertices per wave ballot);
+//   * exchanges discoveries as equal-size bitmap slices (ncclAllToAll) and the
+//     new frontier with one ncclAllGather, so no count exchange is needed;
+//   * switches direction (Beamer alpha/beta) between top-down load-balanced
+//     expansion and bottom-up parent search;
+//   * keeps the reference algorithm as Mode::Ref (the measured baseline) and
+//     the status-array variant as Mode::Simple.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dbfs/backend.hpp"
+#include "dbfs/comm.hpp"
+#include "dbfs/graph.hpp"
+#include "dbfs/partition.hpp"
+
+namespace dbfs {
+
+enum class Mode { Ref, TopDown, BottomUp, DirOpt, Simple };
+Mode parse_mode(const std::string& s);
+const char* mode_name(Mode m);
+
+// A CSR shard resident in backend memory.
+class DeviceGraph {
+ public:
+  // `csr` is either the full graph (rows == n) or exactly this rank's shard.
+  static std::unique_ptr<DeviceGraph> from_host(Backend& be, const HostCSR& csr, const Partition& part, int rank);
+  // Generate this rank's shard of a synthetic graph directly on the device.
+  static std::unique_ptr<DeviceGraph> generate(Backend& be, const GenParams& p, const Partition& part, int rank);
+
+  ShardView view() const;
+  HostCSR to_host() const;  // the shard, copied back
+  Backend& backend() const { return *be_; }
+  const Partition& partition() const { return part_; }
+  int rank() const { return rank_; }
+  int64_t n() const { return part_.n; }
+  int64_t lo() const { return lo_; }
+  int64_t rows() const { return rows_; }
+  int64_t nnz() const { return nnz_; }
+  int64_t input_edges() const { return input_edges_; }
+  std::vector<eid_t> degrees_of(const std::vector<int64_t>& local_rows) const;
+
+ private:
+  Backend* be_ = nullptr;
+  Partition part_;
+  int rank_ = 0;
+  int64_t lo_ = 0, rows_ = 0, nnz_ = 0, input_edges_ = 0;
+  DBuf<eid_t> row_off_;
+  DBuf<vid_t> col_;
+};
+
+struct EngineOptions {
+  Mode mode = Mode::DirOpt;
+  double alpha = 14.0;  // TD -> BU when m_f > m_u / alpha
+  double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
+  int bu_lane_limit = 8;
+  bool phase_timing = false;  // per-level device timing (adds events)
+};
+
+struct LevelRecord {
+  int level = 0;
+  char direction = 'T';       // 'T' top-down, 'B' bottom-up, 'R' reference, 'S' simple
+  int64_t frontier = 0;       // global frontier vertices expanded at this level
+  int64_t frontier_edges = 0; // global sum of their degrees
+  int64_t discovered = 0;     // global new vertices
+  double ms = 0.0;            // device time of the level (phase_timing only)
+};
+
+struct RunResult {
+  int64_t source = 0;
+  double ms = 0.0;             // wall time of the traversal (max over ranks)
+  int64_t reached = 0;         // vertices reached (global)
+  int64_t edges = 0;           // traversed undirected edges (Graph500)
+  int depth = 0;               // number of levels (max level + 1)
+  double gteps = 0.0;
+  std::vector<LevelRecord> levels;
+};
+
+class Engine {
+ public:
+  Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt = {});
+  ~Engine();
+  RunResult run(int64_t source);
+  // Owned slice of the last run's levels.
+  std::vector<lvl_t> levels_local() const;
+  // Full level array (all ranks participate).
+  std::vector<lvl_t> gather_levels();
+  // Graph500-style device validation of the last run; returns violation counts
+  // {depth-gap, reached-unreached, orphan} summed over ranks (all must be 0).
+  std::vector<int64_t> validate(int64_t source);
+  int64_t global_directed_edges() const { return total_directed_; }
+  const EngineOptions& options() const { return opt_; }
+  void set_options(const EngineOptions& o) { opt_ = o; }
+
+ private:
+  RunResult run_bitmap(int64_t source);
+  RunResult run_ref(int64_t source);
+  void alloc_bitmap_state();
+  void alloc_ref_state();
+
+  DeviceGraph& g_;
+  Comm& comm_;
+  Backend& be_;
+  EngineOptions opt_;
+  Partition part_;
+  int64_t total_directed_ = 0;
+
+  DBuf<lvl_t> level_;
+  // bitmap engine state
+  bool bitmap_ready_ = false;
+  DBuf<word_t> visited_, frontier_, next_, recv_, cand_;
+  DBuf<int64_t> seg_cnt_, seg_deg_, qscan_, qbase_, stats_;
+  DBuf<int32_t> blk_vstart_;
+  int64_t nseg_ = 0;
+  // reference-mode state
+  bool ref_ready_ = false;
+  DBuf<lvl_t> dist_;
+  DBuf<vid_t> queue_, buckets_, recvq_;
+  DBuf<int64_t> bucket_cnt_, qcount_;
+};
+
+}  // namespace dbfs

@@ -1,0 +1,213 @@
+// gfx950 graph-construction and validation kernels.
+//
+// The reference builds its CSR on the host from vector<vector<int>> and then
+// copies the FULL graph to every device (bfs.cu:346-351).  Here a
+// rank builds only its own shard on its own GPU, straight from the
+// counter-based generator (dbfs/rmat.hpp): pass 1 counts owned endpoint
+// degrees (device atomics), an exclusive scan turns degrees into row offsets,
+// pass 2 regenerates the same edges and scatters them (atomic cursors).  No
+// edge list is ever materialised, so RMAT-27 on 8 GPUs needs only the shard.
+#include <hip/hip_runtime.h>
+
+#include "launch.hpp"
+#include "wave.hpp"
+
+namespace dbfs {
+namespace kern {
+namespace {
+
+using namespace dev;
+
+constexpr int kBlock = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kBlock * kScanItems;
+
+__global__ __launch_bounds__(kBlock) void gen_count_kernel(GenParams p, int64_t lo, int64_t rows,
+                                                          unsigned long long* __restrict__ deg) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < p.m; i += stride) {
+    uint64_t u, v;
+    gen_edge(p, static_cast<uint64_t>(i), u, v);
+    const uint64_t ur = u - static_cast<uint64_t>(lo), vr = v - static_cast<uint64_t>(lo);
+    if (ur < static_cast<uint64_t>(rows)) atomicAdd(deg + ur, 1ull);
+    if (vr < static_cast<uint64_t>(rows)) atomicAdd(deg + vr, 1ull);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void gen_fill_kernel(GenParams p, int64_t lo, int64_t rows,
+                                                         unsigned long long* __restrict__ cursor,
+                                                         vid_t* __restrict__ col) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < p.m; i += stride) {
+    uint64_t u, v;
+    gen_edge(p, static_cast<uint64_t>(i), u, v);
+    const uint64_t ur = u - static_cast<uint64_t>(lo), vr = v - static_cast<uint64_t>(lo);
+    if (ur < static_cast<uint64_t>(rows)) col[atomicAdd(cursor + ur, 1ull)] = static_cast<vid_t>(v);
+    if (vr < static_cast<uint64_t>(rows)) col[atomicAdd(cursor + vr, 1ull)] = static_cast<vid_t>(u);
+  }
+}
+
+// Block-wide exclusive scan of `items` (kScanItems per thread, blocked layout).
+__device__ long long block_excl_scan(long long (&items)[kScanItems], long long* s_wave, long long& total) {
+  long long sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const long long x = items[k];
+    items[k] = sum;
+    sum += x;
+  }
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  const long long incl = wave_incl_scan(sum);
+  if (lane == kWave - 1) s_wave[wv] = incl;
+  __syncthreads();
+  long long off = incl - sum;
+  total = 0;
+  for (int k = 0; k < kBlock / kWave; ++k) {
+    if (k < wv) off += s_wave[k];
+    total += s_wave[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) items[k] += off;
+  return off;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_single_kernel(eid_t* data, int64_t n) {
+  __shared__ long long s_wave[kBlock / kWave];
+  long long items[kScanItems];
+  const int64_t base = static_cast<int64_t>(threadIdx.x) * kScanItems;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) items[k] = (base + k < n) ? data[base + k] : 0;
+  long long total;
+  block_excl_scan(items, s_wave, total);
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) data[base + k] = items[k];
+  if (threadIdx.x == 0) data[n] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const eid_t* __restrict__ data, int64_t n,
+                                                            eid_t* __restrict__ sums) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  long long s = 0;
+  for (int k = threadIdx.x; k < kScanTile; k += kBlock) {
+    const int64_t i = base + k;
+    if (i < n) s += data[i];
+  }
+  s = wave_sum(s);
+  __shared__ long long s_wave[kBlock / kWave];
+  if (lane_id() == 0) s_wave[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+    for (int k = 0; k < kBlock / kWave; ++k) t += s_wave[k];
+    sums[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void scan_apply_kernel(eid_t* data, int64_t n, const eid_t* __restrict__ offs,
+                                                           int64_t nb) {
+  __shared__ long long s_wave[kBlock / kWave];
+  long long items[kScanItems];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile + static_cast<int64_t>(threadIdx.x) * kScanItems;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) items[k] = (base + k < n) ? data[base + k] : 0;
+  long long total;
+  block_excl_scan(items, s_wave, total);
+  const long long off = offs[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k)
+    if (base + k < n) data[base + k] = items[k] + off;
+  if (blockIdx.x == 0 && threadIdx.x == 0) data[n] = offs[nb];
+}
+
+__global__ __launch_bounds__(kBlock) void validate_kernel(ValidateArgs a) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= a.g.rows) return;
+  const int64_t u = a.g.lo + r;
+  const lvl_t lu = a.level_global[u];
+  long long gap = 0, cross = 0;
+  bool has_parent = false;
+  for (eid_t e = a.g.row_off[r]; e < a.g.row_off[r + 1]; ++e) {
+    const lvl_t lv = a.level_global[a.g.col[e]];
+    if (lu == kUnreached && lv == kUnreached) continue;
+    if ((lu == kUnreached) != (lv == kUnreached)) { ++cross; continue; }
+    if (lu - lv > 1 || lv - lu > 1) ++gap;
+    if (lv == lu - 1) has_parent = true;
+  }
+  long long orphan = 0;
+  if (lu != kUnreached && u != a.src && !has_parent) orphan = 1;
+  if (u == a.src && lu != 0) orphan = 1;
+  if (gap) atomicAdd(reinterpret_cast<unsigned long long*>(a.out + 0), static_cast<unsigned long long>(gap));
+  if (cross) atomicAdd(reinterpret_cast<unsigned long long*>(a.out + 1), static_cast<unsigned long long>(cross));
+  if (orphan) atomicAdd(reinterpret_cast<unsigned long long*>(a.out + 2), 1ull);
+}
+
+__global__ __launch_bounds__(kBlock) void reached_deg_kernel(ShardView g, const lvl_t* __restrict__ level,
+                                                            int64_t* out2) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  long long c = 0, d = 0;
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; r < g.rows; r += stride) {
+    if (level[r] != kUnreached) { ++c; d += g.row_off[r + 1] - g.row_off[r]; }
+  }
+  c = wave_sum(c);
+  d = wave_sum(d);
+  if (lane_id() == 0) {
+    if (c) atomicAdd(reinterpret_cast<unsigned long long*>(out2 + 0), static_cast<unsigned long long>(c));
+    if (d) atomicAdd(reinterpret_cast<unsigned long long*>(out2 + 1), static_cast<unsigned long long>(d));
+  }
+}
+
+inline unsigned capped_grid(int64_t work, int64_t cap) {
+  int64_t g = (work + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<unsigned>(g);
+}
+
+}  // namespace
+
+void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg, hipStream_t st) {
+  if (p.m <= 0 || rows <= 0) return;
+  gen_count_kernel<<<capped_grid(p.m, 256 * 32), kBlock, 0, st>>>(p, lo, rows,
+                                                                  reinterpret_cast<unsigned long long*>(deg));
+}
+
+void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col, hipStream_t st) {
+  if (p.m <= 0 || rows <= 0) return;
+  gen_fill_kernel<<<capped_grid(p.m, 256 * 32), kBlock, 0, st>>>(
+      p, lo, rows, reinterpret_cast<unsigned long long*>(cursor), col);
+}
+
+int64_t scan_tmp_elems(int64_t n) {
+  int64_t total = 0;
+  while (n > kScanTile) {
+    const int64_t nb = (n + kScanTile - 1) / kScanTile;
+    total += nb + 1;
+    n = nb;
+  }
+  return total + 1;
+}
+
+void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st) {
+  if (n <= kScanTile) {
+    scan_single_kernel<<<1, kBlock, 0, st>>>(data, n);
+    return;
+  }
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  scan_reduce_kernel<<<static_cast<unsigned>(nb), kBlock, 0, st>>>(data, n, tmp);
+  exclusive_scan(tmp, nb, tmp + nb + 1, st);
+  scan_apply_kernel<<<static_cast<unsigned>(nb), kBlock, 0, st>>>(data, n, tmp, nb);
+}
+
+void validate_levels(const ValidateArgs& a, hipStream_t st) {
+  if (a.g.rows <= 0) return;
+  validate_kernel<<<static_cast<unsigned>((a.g.rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(a);
+}
+
+void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st) {
+  if (g.rows <= 0) return;
+  reached_deg_kernel<<<capped_grid(g.rows, 4096), kBlock, 0, st>>>(g, level, out2);
+}
+
+}  // namespace kern
+}  // namespace dbfs

@@ -1,0 +1,36 @@
+// Host-side launchers of the gfx950 kernels (defined in csrc/kernels/*.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "dbfs/backend.hpp"
+
+namespace dbfs {
+namespace kern {
+
+// bfs_kernels.hip
+void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st);
+void set_bit(word_t* bm, int64_t bit, hipStream_t st);
+void update_frontier(const UpdateArgs& a, hipStream_t st);
+void scan_segments(const ScanArgs& a, hipStream_t st);
+void compact_frontier(const CompactArgs& a, hipStream_t st);
+void td_expand(const TdArgs& a, hipStream_t st);
+void bu_step(const BuArgs& a, hipStream_t st);
+void status_expand(const StatusArgs& a, hipStream_t st);
+void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
+
+// ref_kernels.hip (reference-algorithm mode)
+void ref_expand(const RefExpandArgs& a, hipStream_t st);
+void ref_accept(const RefAcceptArgs& a, hipStream_t st);
+
+// graph_kernels.hip
+void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg, hipStream_t st);
+void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col, hipStream_t st);
+// in-place exclusive scan of n + 1 entries; `tmp` must hold scan_tmp_elems(n) entries
+int64_t scan_tmp_elems(int64_t n);
+void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st);
+void validate_levels(const ValidateArgs& a, hipStream_t st);
+void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
+
+}  // namespace kern
+}  // namespace dbfs

@@ -1,0 +1,63 @@
+// wave64 helpers for gfx950 (CDNA4).  A wave is 64 lanes: ballots are 64-bit,
+// one bitmap word (64 vertices) maps to one wave ballot.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "dbfs/common.hpp"
+
+namespace dbfs {
+namespace dev {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return static_cast<int>(__lane_id()); }
+
+// Number of set bits of `m` strictly below this lane (v_mbcnt_lo/hi).
+__device__ __forceinline__ unsigned mask_rank(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+}
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long x, int l) {
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x & 0xffffffffull), l));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), l));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ long long readlane_i64(long long x, int l) {
+  return static_cast<long long>(readlane64(static_cast<unsigned long long>(x), l));
+}
+
+__device__ __forceinline__ long long wave_incl_scan(long long x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const long long y = __shfl_up(x, off, kWave);
+    if (l >= off) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ int wave_incl_max(int x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int y = __shfl_up(x, off, kWave);
+    if (l >= off) x = max(x, y);
+  }
+  return x;
+}
+
+__device__ __forceinline__ long long wave_sum(long long x) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+  return x;
+}
+
+__device__ __forceinline__ bool test_bit(const word_t* bm, unsigned v) {
+  return (bm[v >> 6] >> (v & 63)) & 1ull;
+}
+
+}  // namespace dev
+}  // namespace dbfs

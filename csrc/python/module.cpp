@@ -1,0 +1,397 @@
+// Python bindings of the native core (pybind11, no libtorch dependency: the
+// module links the system ROCm 7.2 HIP runtime and RCCL directly, so a process
+// that uses it has exactly one HIP runtime).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "dbfs/engine.hpp"
+
+namespace py = pybind11;
+using namespace dbfs;
+
+namespace {
+
+template <class T>
+py::array_t<T> to_numpy(const std::vector<T>& v) {
+  py::array_t<T> a(static_cast<py::ssize_t>(v.size()));
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+template <class T>
+std::vector<T> from_numpy(const py::array_t<T, py::array::c_style | py::array::forcecast>& a) {
+  std::vector<T> v(static_cast<size_t>(a.size()));
+  if (!v.empty()) std::memcpy(v.data(), a.data(), v.size() * sizeof(T));
+  return v;
+}
+
+py::dict result_dict(const RunResult& r) {
+  py::dict d;
+  d["source"] = r.source;
+  d["ms"] = r.ms;
+  d["reached"] = r.reached;
+  d["edges"] = r.edges;
+  d["depth"] = r.depth;
+  d["gteps"] = r.gteps;
+  py::list lv;
+  for (const auto& l : r.levels) {
+    py::dict x;
+    x["level"] = l.level;
+    x["dir"] = std::string(1, l.direction);
+    x["frontier"] = l.frontier;
+    x["frontier_edges"] = l.frontier_edges;
+    x["discovered"] = l.discovered;
+    x["ms"] = l.ms;
+    lv.append(x);
+  }
+  d["levels"] = lv;
+  return d;
+}
+
+// Comm whose collectives are implemented in Python (torch.distributed / gloo).
+// Buffers are passed as integer addresses plus byte counts; only meaningful
+// with the CPU backend (host memory).
+class PyCommBase : public Comm {
+ public:
+  virtual void py_alltoall(uintptr_t send, uintptr_t recv, size_t bytes) = 0;
+  virtual void py_allgather(uintptr_t send, uintptr_t recv, size_t bytes) = 0;
+  virtual void py_allreduce_sum_i64(uintptr_t buf, size_t count) = 0;
+  virtual void py_alltoallv(uintptr_t send, std::vector<int64_t> sc, std::vector<int64_t> sd, uintptr_t recv,
+                            std::vector<int64_t> rc, std::vector<int64_t> rd, size_t elem_bytes) = 0;
+  virtual void py_barrier() = 0;
+
+  void alltoall(const void* s, void* r, size_t b) override {
+    py_alltoall(reinterpret_cast<uintptr_t>(s), reinterpret_cast<uintptr_t>(r), b);
+  }
+  void allgather(const void* s, void* r, size_t b) override {
+    py_allgather(reinterpret_cast<uintptr_t>(s), reinterpret_cast<uintptr_t>(r), b);
+  }
+  void allreduce_sum_i64(int64_t* buf, size_t count) override {
+    py_allreduce_sum_i64(reinterpret_cast<uintptr_t>(buf), count);
+  }
+  void alltoallv(const void* s, const int64_t* sc, const int64_t* sd, void* r, const int64_t* rc, const int64_t* rd,
+                 size_t eb) override {
+    const int n = size();
+    py_alltoallv(reinterpret_cast<uintptr_t>(s), std::vector<int64_t>(sc, sc + n), std::vector<int64_t>(sd, sd + n),
+                 reinterpret_cast<uintptr_t>(r), std::vector<int64_t>(rc, rc + n), std::vector<int64_t>(rd, rd + n),
+                 eb);
+  }
+  void barrier() override { py_barrier(); }
+  std::string name() const override { return "python"; }
+};
+
+class PyCommTrampoline : public PyCommBase {
+ public:
+  int rank() const override { PYBIND11_OVERRIDE_PURE(int, PyCommBase, rank, ); }
+  int size() const override { PYBIND11_OVERRIDE_PURE(int, PyCommBase, size, ); }
+  std::string name() const override { PYBIND11_OVERRIDE(std::string, PyCommBase, name, ); }
+  void py_alltoall(uintptr_t s, uintptr_t r, size_t b) override {
+    PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_alltoall, s, r, b);
+  }
+  void py_allgather(uintptr_t s, uintptr_t r, size_t b) override {
+    PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_allgather, s, r, b);
+  }
+  void py_allreduce_sum_i64(uintptr_t buf, size_t count) override {
+    PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_allreduce_sum_i64, buf, count);
+  }
+  void py_alltoallv(uintptr_t s, std::vector<int64_t> sc, std::vector<int64_t> sd, uintptr_t r,
+                    std::vector<int64_t> rc, std::vector<int64_t> rd, size_t eb) override {
+    PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_alltoallv, s, sc, sd, r, rc, rd, eb);
+  }
+  void py_barrier() override { PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_barrier, ); }
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_dbfs_native, m) {
+  m.doc() = "MI355X-native distributed BFS core (HIP/CDNA4 kernels, RCCL over xGMI)";
+  py::register_exception<Error>(m, "NativeError", PyExc_RuntimeError);
+
+  m.attr("UNREACHED") = py::int_(kUnreached);
+  m.attr("TD_EDGES_PER_BLOCK") = py::int_(kTdEdgesPerBlock);
+  m.attr("SEG_VERTICES") = py::int_(kSegVertices);
+
+  // ---- graphs ----
+  py::class_<HostCSR>(m, "HostCSR")
+      .def_readonly("n", &HostCSR::n)
+      .def_readonly("row_lo", &HostCSR::row_lo)
+      .def_readonly("rows", &HostCSR::rows)
+      .def_readonly("input_edges", &HostCSR::input_edges)
+      .def_property_readonly("directed_edges", &HostCSR::directed_edges)
+      .def_property_readonly("row_off", [](const HostCSR& g) { return to_numpy(g.row_off); })
+      .def_property_readonly("col", [](const HostCSR& g) { return to_numpy(g.col); })
+      .def("degree", [](const HostCSR& g, int64_t r) { return g.degree(r); });
+
+  m.def(
+      "read_graph",
+      [](const std::string& path, bool verbose) {
+        if (is_binary_csr(path)) return read_binary_csr(path);
+        ReadOptions ro;
+        ro.verbose_reference_lines = verbose;
+        return build_csr(read_edge_list(path, ro));
+      },
+      py::arg("path"), py::arg("verbose") = false, py::call_guard<py::gil_scoped_release>(),
+      "Read an edge list / MatrixMarket / binary-CSR file into a symmetrised CSR.");
+  m.def(
+      "read_edge_list",
+      [](const std::string& path) {
+        EdgeList el = read_edge_list(path);
+        return py::make_tuple(el.n, to_numpy(el.u), to_numpy(el.v));
+      },
+      py::arg("path"));
+  m.def("detect_format", [](const std::string& p) {
+    switch (detect_format(p)) {
+      case FileFormat::Binary: return std::string("binary");
+      case FileFormat::MatrixMarket: return std::string("mtx");
+      default: return std::string("edgelist");
+    }
+  });
+  m.def(
+      "build_csr",
+      [](int64_t n, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> u,
+         py::array_t<uint32_t, py::array::c_style | py::array::forcecast> v) {
+        EdgeList el;
+        el.n = n;
+        el.u = from_numpy<uint32_t>(u);
+        el.v = from_numpy<uint32_t>(v);
+        DBFS_CHECK(el.u.size() == el.v.size(), "u and v must have the same length");
+        for (size_t i = 0; i < el.u.size(); ++i)
+          DBFS_CHECK(el.u[i] < n && el.v[i] < n, "edge endpoint out of range");
+        return build_csr(el);
+      },
+      py::arg("n"), py::arg("u"), py::arg("v"));
+  m.def("write_binary_csr", &write_binary_csr, py::arg("path"), py::arg("csr"));
+  m.def("write_levels", [](const std::string& path, py::array_t<int32_t, py::array::c_style | py::array::forcecast> l) {
+    write_levels(path, from_numpy<int32_t>(l));
+  });
+  m.def(
+      "cpu_bfs",
+      [](const HostCSR& g, int64_t src) {
+        CpuBfsResult r;
+        {
+          py::gil_scoped_release rel;
+          r = cpu_bfs(g, src);
+        }
+        return py::make_tuple(to_numpy(r.level), to_numpy(r.parent_edge));
+      },
+      py::arg("csr"), py::arg("src"));
+
+  py::class_<GenParams>(m, "GenParams")
+      .def_readonly("n", &GenParams::n)
+      .def_readonly("m", &GenParams::m)
+      .def_readonly("scale", &GenParams::scale)
+      .def_readonly("seed", &GenParams::seed)
+      .def_readonly("uniform", &GenParams::uniform)
+      .def_readwrite("scramble", &GenParams::scramble);
+  m.def("rmat_params", &rmat_params, py::arg("scale"), py::arg("edge_factor") = 16, py::arg("seed") = 1);
+  m.def("uniform_params", &uniform_params, py::arg("n"), py::arg("m"), py::arg("seed") = 1);
+  m.def(
+      "generate_edges",
+      [](const GenParams& p, int64_t begin, int64_t end) {
+        if (end < 0) end = p.m;
+        DBFS_CHECK(0 <= begin && begin <= end && end <= p.m, "bad edge range");
+        std::vector<uint32_t> u(static_cast<size_t>(end - begin)), v(u.size());
+        {
+          py::gil_scoped_release rel;
+          for (int64_t i = begin; i < end; ++i) {
+            uint64_t a, b;
+            gen_edge(p, static_cast<uint64_t>(i), a, b);
+            u[i - begin] = static_cast<uint32_t>(a);
+            v[i - begin] = static_cast<uint32_t>(b);
+          }
+        }
+        return py::make_tuple(to_numpy(u), to_numpy(v));
+      },
+      py::arg("params"), py::arg("begin") = 0, py::arg("end") = -1,
+      "Host copy of the counter-based generator stream (bit-identical to the device).");
+  m.def("scramble_vertex", &scramble_vertex);
+
+  py::class_<Partition>(m, "Partition")
+      .def(py::init([](int64_t n, int nranks) { return Partition::block(n, nranks); }), py::arg("n"),
+           py::arg("nranks"))
+      .def_readonly("n", &Partition::n)
+      .def_readonly("nranks", &Partition::nranks)
+      .def_readonly("part", &Partition::part)
+      .def("owner", &Partition::owner)
+      .def("lo", &Partition::lo)
+      .def("hi", &Partition::hi)
+      .def("count", &Partition::count)
+      .def("slice_words", &Partition::slice_words)
+      .def("global_words", &Partition::global_words);
+
+  // ---- runtime ----
+  py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
+      .def_property_readonly("name", &Backend::name)
+      .def_property_readonly("device_id", &Backend::device_id)
+      .def_property_readonly("is_gpu", [](const Backend& b) { return b.kind() == DeviceKind::HIP; })
+      .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>());
+  m.def("cpu_backend", []() { return std::shared_ptr<Backend>(make_cpu_backend()); });
+  m.def("hip_backend", [](int dev) { return std::shared_ptr<Backend>(make_hip_backend(dev)); }, py::arg("device") = 0);
+  m.def("hip_device_count", &hip_device_count);
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("size", &Comm::size)
+      .def_property_readonly("name", &Comm::name)
+      .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("sum_host", &Comm::sum_host, py::call_guard<py::gil_scoped_release>())
+      .def("max_host", &Comm::max_host, py::call_guard<py::gil_scoped_release>())
+      .def("bind_backend", [](Comm& c, std::shared_ptr<Backend> be) { c.bind_backend(be.get()); },
+           py::keep_alive<1, 2>());
+  m.def(
+      "local_comm", [](std::shared_ptr<Backend> be) { return std::shared_ptr<Comm>(new LocalComm(*be)); },
+      py::keep_alive<0, 1>());
+  py::class_<VirtualGroup, std::shared_ptr<VirtualGroup>>(m, "VirtualGroup")
+      .def(py::init<int>())
+      .def_property_readonly("size", &VirtualGroup::size);
+  m.def(
+      "virtual_comm",
+      [](std::shared_ptr<VirtualGroup> g, int rank, std::shared_ptr<Backend> be) {
+        return std::shared_ptr<Comm>(new VirtualComm(g, rank, *be));
+      },
+      py::keep_alive<0, 3>());
+  m.def("nccl_unique_id", []() { return py::bytes(NcclComm::unique_id()); });
+  m.def(
+      "nccl_comm",
+      [](py::bytes uid, int rank, int nranks, std::shared_ptr<Backend> be) {
+        std::string u = uid;
+        py::gil_scoped_release rel;
+        return std::shared_ptr<Comm>(new NcclComm(u, rank, nranks, *be));
+      },
+      py::keep_alive<0, 4>());
+  m.def("nccl_init_all", [](std::vector<std::shared_ptr<Backend>> bes) {
+    std::vector<Backend*> raw;
+    for (auto& b : bes) raw.push_back(b.get());
+    auto comms = NcclComm::init_all(raw);
+    std::vector<std::shared_ptr<Comm>> out;
+    for (auto& c : comms) out.push_back(std::shared_ptr<Comm>(c.release()));
+    return out;
+  });
+  py::class_<PyCommBase, Comm, PyCommTrampoline, std::shared_ptr<PyCommBase>>(m, "PyComm")
+      .def(py::init<>())
+      .def("py_alltoall", &PyCommBase::py_alltoall)
+      .def("py_allgather", &PyCommBase::py_allgather)
+      .def("py_allreduce_sum_i64", &PyCommBase::py_allreduce_sum_i64)
+      .def("py_alltoallv", &PyCommBase::py_alltoallv)
+      .def("py_barrier", &PyCommBase::py_barrier);
+
+  py::class_<TcpBootstrap, std::shared_ptr<TcpBootstrap>>(m, "TcpBootstrap")
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("host"), py::arg("port"), py::arg("rank"),
+           py::arg("nranks"), py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &TcpBootstrap::rank)
+      .def_property_readonly("size", &TcpBootstrap::size)
+      .def(
+          "broadcast",
+          [](TcpBootstrap& b, py::bytes data) {
+            std::string s = data, r;
+            {
+              py::gil_scoped_release rel;
+              r = b.broadcast(s);
+            }
+            return py::bytes(r);
+          },
+          py::arg("data"))
+      .def("allgather",
+           [](TcpBootstrap& b, py::bytes data) {
+             std::string s = data;
+             std::vector<std::string> r;
+             {
+               py::gil_scoped_release rel;
+               r = b.allgather(s);
+             }
+             py::list out;
+             for (auto& x : r) out.append(py::bytes(x));
+             return out;
+           })
+      .def("barrier", &TcpBootstrap::barrier, py::call_guard<py::gil_scoped_release>());
+
+  // ---- engine ----
+  py::class_<DeviceGraph, std::shared_ptr<DeviceGraph>>(m, "DeviceGraph")
+      .def_static(
+          "from_host",
+          [](std::shared_ptr<Backend> be, const HostCSR& csr, const Partition& part, int rank) {
+            py::gil_scoped_release rel;
+            return std::shared_ptr<DeviceGraph>(DeviceGraph::from_host(*be, csr, part, rank));
+          },
+          py::arg("backend"), py::arg("csr"), py::arg("partition"), py::arg("rank"), py::keep_alive<0, 1>())
+      .def_static(
+          "generate",
+          [](std::shared_ptr<Backend> be, const GenParams& p, const Partition& part, int rank) {
+            py::gil_scoped_release rel;
+            return std::shared_ptr<DeviceGraph>(DeviceGraph::generate(*be, p, part, rank));
+          },
+          py::arg("backend"), py::arg("params"), py::arg("partition"), py::arg("rank"), py::keep_alive<0, 1>())
+      .def_property_readonly("n", &DeviceGraph::n)
+      .def_property_readonly("lo", &DeviceGraph::lo)
+      .def_property_readonly("rows", &DeviceGraph::rows)
+      .def_property_readonly("nnz", &DeviceGraph::nnz)
+      .def_property_readonly("input_edges", &DeviceGraph::input_edges)
+      .def_property_readonly("rank", &DeviceGraph::rank)
+      .def_property_readonly("partition", &DeviceGraph::partition)
+      .def("to_host", &DeviceGraph::to_host, py::call_guard<py::gil_scoped_release>())
+      .def("degrees_of", &DeviceGraph::degrees_of);
+
+  py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
+      .def(py::init([](std::shared_ptr<DeviceGraph> g, std::shared_ptr<Comm> c, const std::string& mode, double alpha,
+                       double beta, int bu_lane_limit, bool phase_timing) {
+             EngineOptions o;
+             o.mode = parse_mode(mode);
+             o.alpha = alpha;
+             o.beta = beta;
+             o.bu_lane_limit = bu_lane_limit;
+             o.phase_timing = phase_timing;
+             py::gil_scoped_release rel;
+             return std::make_shared<Engine>(*g, *c, o);
+           }),
+           py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 14.0, py::arg("beta") = 24.0,
+           py::arg("bu_lane_limit") = 8, py::arg("phase_timing") = false, py::keep_alive<1, 2>(),
+           py::keep_alive<1, 3>())
+      .def(
+          "run",
+          [](Engine& e, int64_t src) {
+            RunResult r;
+            {
+              py::gil_scoped_release rel;
+              r = e.run(src);
+            }
+            return result_dict(r);
+          },
+          py::arg("source"))
+      .def("levels_local",
+           [](const Engine& e) {
+             std::vector<lvl_t> v;
+             {
+               py::gil_scoped_release rel;
+               v = e.levels_local();
+             }
+             return to_numpy(v);
+           })
+      .def("gather_levels",
+           [](Engine& e) {
+             std::vector<lvl_t> v;
+             {
+               py::gil_scoped_release rel;
+               v = e.gather_levels();
+             }
+             return to_numpy(v);
+           })
+      .def("validate", &Engine::validate, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("global_directed_edges", &Engine::global_directed_edges)
+      .def_property(
+          "mode", [](const Engine& e) { return std::string(mode_name(e.options().mode)); },
+          [](Engine& e, const std::string& s) {
+            EngineOptions o = e.options();
+            o.mode = parse_mode(s);
+            e.set_options(o);
+          })
+      .def("set_heuristics", [](Engine& e, double alpha, double beta, int lane_limit) {
+        EngineOptions o = e.options();
+        o.alpha = alpha;
+        o.beta = beta;
+        o.bu_lane_limit = lane_limit;
+        e.set_options(o);
+      });
+}

@@ -1,0 +1,107 @@
+"""High-level distributed BFS.
+
+Reference entry points: ``main`` -> ``runCudaQueueBfs`` (bfs.cu:783-823,
+542-629) and the MPI variant (bfs_mpi.cu:797-856).  One ``BFS`` object holds
+this rank's CSR shard on its device and a native engine; ``run(src)`` is one
+level-synchronous traversal (all ranks call it collectively).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Union
+
+import numpy as np
+
+from .._native import N
+from ..parallel.runtime import Runtime, init_runtime
+
+MODES = ("ref", "td", "bu", "do", "simple")
+
+
+@dataclass
+class BFSResult:
+    source: int
+    ms: float
+    reached: int
+    edges: int
+    depth: int
+    gteps: float
+    levels: List[Dict[str, Any]] = field(default_factory=list)
+
+    @classmethod
+    def from_native(cls, d: Dict[str, Any]) -> "BFSResult":
+        return cls(source=d["source"], ms=d["ms"], reached=d["reached"], edges=d["edges"],
+                   depth=d["depth"], gteps=d["gteps"], levels=list(d["levels"]))
+
+
+class BFS:
+    """Distributed BFS over a graph given as a HostCSR, generator params, or a file path."""
+
+    def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
+                 alpha: float = 14.0, beta: float = 24.0, bu_lane_limit: int = 8, phase_timing: bool = False):
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        self.rt = runtime or init_runtime()
+        if isinstance(graph, str):
+            graph = N.read_graph(graph)
+        if isinstance(graph, N.GenParams):
+            self.n = graph.n
+            self.partition = N.Partition(graph.n, self.rt.world)
+            self.graph = N.DeviceGraph.generate(self.rt.backend, graph, self.partition, self.rt.rank)
+        elif isinstance(graph, N.HostCSR):
+            self.n = graph.n
+            self.partition = N.Partition(graph.n, self.rt.world)
+            self.graph = N.DeviceGraph.from_host(self.rt.backend, graph, self.partition, self.rt.rank)
+        else:
+            raise TypeError("graph must be a path, HostCSR or GenParams")
+        self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
+                               bu_lane_limit=bu_lane_limit, phase_timing=phase_timing)
+
+    @property
+    def mode(self) -> str:
+        return self.engine.mode
+
+    @mode.setter
+    def mode(self, m: str) -> None:
+        if m not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        self.engine.mode = m
+
+    def run(self, source: int) -> BFSResult:
+        return BFSResult.from_native(self.engine.run(int(source)))
+
+    def levels(self) -> np.ndarray:
+        """Full per-vertex level array of the last run (collective)."""
+        return self.engine.gather_levels()
+
+    def local_levels(self) -> np.ndarray:
+        return self.engine.levels_local()
+
+    def validate(self, source: int) -> bool:
+        """Graph500-style level validation of the last run on the device (collective)."""
+        gap, cross, orphan = self.engine.validate(int(source))
+        return gap == 0 and cross == 0 and orphan == 0
+
+    def degree(self, v: int) -> int:
+        """Degree of global vertex v (collective: the owner contributes)."""
+        own = self.partition.owner(int(v))
+        d = 0
+        if own == self.rt.rank:
+            d = self.graph.degrees_of([int(v) - self.partition.lo(own)])[0]
+        return int(self.rt.comm.sum_host(int(d))) if self.rt.world > 1 else int(d)
+
+    def sample_roots(self, k: int, seed: int = 1) -> List[int]:
+        """Graph500 root sampling: k distinct random vertices of degree >= 1 (collective)."""
+        rng = np.random.default_rng(seed)
+        roots: List[int] = []
+        seen = set()
+        tries = 0
+        while len(roots) < k and tries < 64 * k + 64:
+            tries += 1
+            v = int(rng.integers(0, self.n))
+            if v in seen:
+                continue
+            seen.add(v)
+            if self.degree(v) > 0:
+                roots.append(v)
+        return roots

@@ -1,0 +1,63 @@
+"""Graph construction, synthetic generators and the CPU oracle.
+
+Reference counterparts: ``readGraphFromFile`` (bfs.cu:829-880, edge list only),
+the dead random generator ``readGraph`` (bfs.cu:882-920) and the sequential
+oracle ``bfsCPU`` (bfs.cu:923-945).  All heavy lifting is native C++.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .._native import N
+
+
+def read_graph(path: str, verbose: bool = False):
+    """Edge list (``n m`` + ``u v`` lines), MatrixMarket (.mtx) or binary CSR -> HostCSR."""
+    return N.read_graph(path, verbose)
+
+
+def read_edge_list(path: str):
+    """Return ``(n, u, v)`` numpy arrays of the undirected input edges."""
+    return N.read_edge_list(path)
+
+
+def detect_format(path: str) -> str:
+    return N.detect_format(path)
+
+
+def build_csr(n: int, u, v):
+    """Symmetrised CSR in the reference's adjacency order (dups and self-loops kept)."""
+    return N.build_csr(int(n), np.ascontiguousarray(u, dtype=np.uint32), np.ascontiguousarray(v, dtype=np.uint32))
+
+
+def rmat_params(scale: int, edge_factor: int = 16, seed: int = 1, scramble: bool = True):
+    p = N.rmat_params(int(scale), int(edge_factor), int(seed))
+    p.scramble = bool(scramble)
+    return p
+
+
+def uniform_params(n: int, m: int, seed: int = 1):
+    return N.uniform_params(int(n), int(m), int(seed))
+
+
+def generate_edges(params, begin: int = 0, end: int = -1):
+    """Host copy of the counter-based edge stream (bit-identical to the device generator)."""
+    return N.generate_edges(params, int(begin), int(end))
+
+
+def host_csr_from_params(params):
+    u, v = generate_edges(params)
+    return build_csr(params.n, u, v)
+
+
+def cpu_bfs(csr, src: int):
+    """Sequential oracle: returns ``(levels int32, parent_edge int64)``; unreached = INT32_MAX."""
+    return N.cpu_bfs(csr, int(src))
+
+
+def write_binary_csr(path: str, csr) -> None:
+    N.write_binary_csr(path, csr)
+
+
+def write_levels(path: str, levels) -> None:
+    N.write_levels(path, np.ascontiguousarray(levels, dtype=np.int32))

@@ -1,0 +1,103 @@
+"""Per-process runtime: one backend (GPU or CPU) plus the rank's communicator.
+
+Execution models:
+  * one process per GPU (``torch.distributed.run`` / any launcher exporting
+    RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT) -> RCCL communicator
+    bootstrapped over TCP (the reference used CUDA-aware MPI, bfs_mpi.cu:800-808);
+  * one process, P virtual ranks as threads on one device -> ``run_virtual_ranks``;
+  * CPU multi-process over torch.distributed/gloo -> ``TorchComm``.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass
+from typing import Any, Callable, List, Optional
+
+from .._native import N
+
+
+@dataclass
+class Runtime:
+    backend: Any
+    comm: Any
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+
+    @property
+    def is_gpu(self) -> bool:
+        return bool(self.backend.is_gpu)
+
+    def barrier(self) -> None:
+        self.comm.barrier()
+
+
+def _env_int(k: str, d: int) -> int:
+    v = os.environ.get(k)
+    return int(v) if v not in (None, "") else d
+
+
+def make_backend(device: str = "auto", local_rank: int = 0):
+    if device == "auto":
+        device = "hip" if N.hip_device_count() > 0 else "cpu"
+    if device in ("hip", "gpu", "cuda"):
+        return N.hip_backend(local_rank)
+    if device == "cpu":
+        return N.cpu_backend()
+    raise ValueError(f"unknown device {device!r} (hip|cpu|auto)")
+
+
+def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
+    """Create this process's backend and communicator from the launcher's environment."""
+    world = _env_int("WORLD_SIZE", 1)
+    rank = _env_int("RANK", 0)
+    local_rank = _env_int("LOCAL_RANK", rank if world > 1 else 0)
+    backend = make_backend(device, local_rank)
+    if comm is None:
+        if world == 1:
+            comm = N.local_comm(backend)
+        elif backend.is_gpu:
+            addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            port = _env_int("DBFS_BOOTSTRAP_PORT", _env_int("MASTER_PORT", 29500) + 1)
+            boot = N.TcpBootstrap(addr, port, rank, world)
+            uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
+            comm = N.nccl_comm(uid, rank, world, backend)
+            del boot
+        else:
+            from .torch_comm import TorchComm
+            comm = TorchComm()
+    comm.bind_backend(backend)
+    return Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)
+
+
+def run_virtual_ranks(nranks: int, fn: Callable[[Runtime], Any], device: str = "auto",
+                      device_id: int = 0) -> List[Any]:
+    """Run ``fn(runtime)`` for P virtual ranks (threads) sharing one device.
+
+    All ranks run the real partitioned code path (shards, owner routing,
+    collectives); only the transport is an in-process copy.
+    """
+    group = N.VirtualGroup(int(nranks))
+    rts = []
+    for r in range(nranks):
+        be = make_backend(device, device_id)
+        rts.append(Runtime(backend=be, comm=N.virtual_comm(group, r, be), rank=r, world=nranks))
+    out: List[Any] = [None] * nranks
+    errs: List[Optional[BaseException]] = [None] * nranks
+
+    def body(r: int) -> None:
+        try:
+            out[r] = fn(rts[r])
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
