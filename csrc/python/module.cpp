@@ -85,9 +85,11 @@ class PyCommBase : public Comm {
 
 class PyCommTrampoline : public PyCommBase {
  public:
-  int rank() const override { PYBIND11_OVERRIDE_PURE(int, PyCommBase, rank, ); }
-  int size() const override { PYBIND11_OVERRIDE_PURE(int, PyCommBase, size, ); }
-  std::string name() const override { PYBIND11_OVERRIDE(std::string, PyCommBase, name, ); }
+  // Python implements get_rank / get_size / get_name (plain `rank` / `size` /
+  // `name` are the read-only properties every Comm exposes).
+  int rank() const override { PYBIND11_OVERRIDE_PURE_NAME(int, PyCommBase, "get_rank", rank, ); }
+  int size() const override { PYBIND11_OVERRIDE_PURE_NAME(int, PyCommBase, "get_size", size, ); }
+  std::string name() const override { PYBIND11_OVERRIDE_NAME(std::string, PyCommBase, "get_name", name, ); }
   void py_alltoall(uintptr_t s, uintptr_t r, size_t b) override {
     PYBIND11_OVERRIDE_PURE(void, PyCommBase, py_alltoall, s, r, b);
   }

@@ -36,13 +36,13 @@ class TorchComm(N.PyComm):
         self._rank = dist.get_rank(group)
         self._size = dist.get_world_size(group)
 
-    def rank(self) -> int:
+    def get_rank(self) -> int:
         return self._rank
 
-    def size(self) -> int:
+    def get_size(self) -> int:
         return self._size
 
-    def name(self) -> str:
+    def get_name(self) -> str:
         return "torch." + str(self._dist.get_backend(self._group))
 
     def py_alltoall(self, send: int, recv: int, nbytes: int) -> None:

@@ -1,0 +1,117 @@
+"""TCP bootstrap (RCCL unique-id exchange), the reference-compatible CLI, and
+the bench.py output contract -- all on CPU."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BFS_BIN = os.path.join(REPO, "bin", "bfs")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _boot_worker(rank, world, port, q):
+    import distributed_cuda_bfs_amd as dbfs
+
+    b = dbfs.native.TcpBootstrap("127.0.0.1", port, rank, world, 60.0)
+    got = b.broadcast(b"uid-128-bytes" if rank == 0 else b"")
+    gathered = b.allgather(f"r{rank}".encode())
+    b.barrier()
+    q.put((rank, got, gathered))
+
+
+def test_tcp_bootstrap_three_ranks():
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_boot_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    outs = [q.get(timeout=60) for _ in range(3)]
+    for p in ps:
+        p.join(timeout=30)
+    for rank, got, gathered in outs:
+        assert got == b"uid-128-bytes"
+        assert gathered == [b"r0", b"r1", b"r2"]
+
+
+def _run(args, **kw):
+    return subprocess.run([BFS_BIN] + args, capture_output=True, text=True, timeout=120, **kw)
+
+
+def test_cli_reference_stdout(data_dir):
+    path = os.path.join(data_dir, "chain8.txt")
+    out = _run(["0", path, "--cpu"])
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    # SURVEY Appendix A line set, in order (GPU-only peer-access line omitted on --cpu)
+    expect_prefix = [path, "nodes num: 8", "edge num: 7", "finish load graph", "Number of vertices 8",
+                     "Number of edges 14", "", "Starting sequential bfs."]
+    assert lines[:8] == expect_prefix
+    assert lines[8].startswith("Elapsed time in milliseconds : ") and lines[8].endswith(" ms.")
+    assert "Starting queue parallel bfs." in lines
+    assert out.stdout.endswith("Output OK!\n\n")  # bfs.cu:383 prints a trailing blank line
+
+
+def test_cli_levels_out_and_json(tmp_path, data_dir):
+    lv = tmp_path / "levels.txt"
+    out = _run(["3", os.path.join(data_dir, "two_components.txt"), "--cpu", "--quiet", "--json",
+                "--levels-out", str(lv), "--validate"])
+    assert out.returncode == 0, out.stderr
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["reached"] == 3 and rec["edges"] == 3
+    assert lv.read_text().split() == ["2147483647"] * 3 + ["0", "1", "2"] + ["2147483647"] * 4
+
+
+@pytest.mark.parametrize("mode", ["ref", "td", "bu", "do", "simple"])
+def test_cli_modes_rmat_virtual(mode):
+    out = _run(["--rmat", "10", "5", "--cpu", "--mode", mode, "--virtual-ranks", "3", "--quiet", "--validate"])
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_cli_errors(tmp_path):
+    out = _run(["0", str(tmp_path / "nope.txt"), "--cpu"])
+    assert out.returncode != 0 and "not open" in out.stderr
+    out = _run(["0"])
+    assert out.returncode == 2
+    bad = tmp_path / "g.txt"
+    bad.write_text("2 1\n0 1\n")
+    out = _run(["5", str(bad), "--cpu", "--quiet"])
+    assert out.returncode != 0 and "out of range" in out.stderr
+
+
+def test_cli_roots_and_cache(tmp_path):
+    cache = tmp_path / "g.csr"
+    out = _run(["--rmat", "9", "0", "--cpu", "--quiet", "--cache", str(cache), "--roots", "3"])
+    assert out.returncode == 0, out.stderr
+    assert "harmonic-mean GTEPS" in out.stdout
+    out = _run(["0", str(cache), "--cpu", "--quiet"])
+    assert out.returncode == 0, out.stderr
+
+
+def test_bench_contract_cpu():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--scale", "10",
+                          "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec
+    assert rec["steps"] == 3 and rec["warmup"] == 1 and rec["n_gpus"] == 1
+    assert rec["value"] > 0 and rec["validated"] is True
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in rec["config"]

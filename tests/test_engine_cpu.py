@@ -1,0 +1,133 @@
+"""Engine orchestration on the CPU backend (same C++ engine the GPU runs).
+
+Covers every mode, the direction-optimising switch, P virtual ranks with N not
+divisible by P (reference defect D5), isolated / last-vertex sources, and the
+device-side Graph500 validation.
+"""
+import numpy as np
+import pytest
+
+import distributed_cuda_bfs_amd as dbfs
+from distributed_cuda_bfs_amd.parallel.runtime import init_runtime, run_virtual_ranks
+
+MODES = list(dbfs.MODES)
+
+
+@pytest.fixture(scope="module")
+def rt():
+    return init_runtime("cpu")
+
+
+def _oracle(csr, src):
+    return dbfs.cpu_bfs(csr, src)[0]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_modes_match_oracle(rt, mode):
+    p = dbfs.rmat_params(11, 16, 7)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    for src in bfs.sample_roots(4, seed=1):
+        res = bfs.run(src)
+        exp = _oracle(csr, src)
+        assert np.array_equal(bfs.levels(), exp)
+        deg = np.diff(np.asarray(csr.row_off))
+        assert res.reached == int((exp != dbfs.UNREACHED).sum())
+        assert res.edges == int(deg[exp != dbfs.UNREACHED].sum()) // 2
+        assert res.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
+        assert bfs.validate(src)
+
+
+def test_direction_switches(rt):
+    p = dbfs.rmat_params(12, 16, 3)
+    bfs = dbfs.BFS(p, rt, mode="do")
+    src = bfs.sample_roots(1, seed=5)[0]
+    res = bfs.run(src)
+    dirs = "".join(l["dir"] for l in res.levels)
+    assert "T" in dirs and "B" in dirs, dirs
+    assert dirs[0] == "T"
+
+
+def test_heuristic_extremes_still_exact(rt):
+    p = dbfs.rmat_params(11, 16, 9)
+    csr = dbfs.host_csr_from_params(p)
+    for alpha, beta in [(1e9, 1e9), (1e-9, 1e-9), (2.0, 2.0)]:
+        bfs = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=beta, bu_lane_limit=1)
+        bfs.run(17)
+        assert np.array_equal(bfs.levels(), _oracle(csr, 17))
+
+
+def test_isolated_and_last_source(rt):
+    p = dbfs.uniform_params(3001, 2000, 5)  # many isolated vertices, odd n
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    iso = int(np.nonzero(deg == 0)[0][0])
+    for mode in MODES:
+        bfs = dbfs.BFS(csr, rt, mode=mode)
+        for src in (iso, csr.n - 1, 0):
+            res = bfs.run(src)
+            assert np.array_equal(bfs.levels(), _oracle(csr, src))
+        res = bfs.run(iso)
+        assert res.reached == 1 and res.edges == 0 and res.depth == 1
+
+
+def test_self_loops_and_duplicates(rt, data_dir):
+    csr = dbfs.read_graph(f"{data_dir}/dup_self.mtx")
+    for mode in MODES:
+        bfs = dbfs.BFS(csr, rt, mode=mode)
+        bfs.run(2)
+        assert np.array_equal(bfs.levels(), _oracle(csr, 2))
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("mode", MODES)
+def test_virtual_ranks(P, mode):
+    p = dbfs.rmat_params(10, 16, 13)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [3, 1000, 1023]
+    exp = [_oracle(csr, s) for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(csr, rt, mode=mode)
+        out = []
+        for s in srcs:
+            r = bfs.run(s)
+            out.append((bfs.levels(), r.reached, r.edges, bfs.validate(s)))
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for (lv, reached, edges, ok), e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+            assert reached == int((e != dbfs.UNREACHED).sum())
+            assert ok
+
+
+def test_virtual_ranks_odd_n_generated_shards():
+    # generated shards (device generator path) with N % P != 0 via uniform graph
+    p = dbfs.uniform_params(777, 3000, 21)
+    csr = dbfs.host_csr_from_params(p)
+    exp = _oracle(csr, 776)
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode="do")
+        bfs.run(776)
+        return bfs.levels(), bfs.local_levels(), bfs.graph.lo, bfs.graph.rows
+
+    outs = run_virtual_ranks(5, body, device="cpu")
+    total_rows = 0
+    for lv, loc, lo, rows in outs:
+        assert np.array_equal(lv, exp)
+        assert np.array_equal(loc, exp[lo:lo + rows])
+        total_rows += rows
+    assert total_rows == 777
+
+
+def test_mode_switch_on_same_engine(rt):
+    p = dbfs.rmat_params(10, 16, 2)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode="ref")
+    for m in MODES:
+        bfs.mode = m
+        assert bfs.mode == m
+        bfs.run(9)
+        assert np.array_equal(bfs.levels(), _oracle(csr, 9))

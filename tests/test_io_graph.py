@@ -1,0 +1,138 @@
+"""Graph ingestion, CSR construction, generators and the CPU oracle (CPU only).
+
+Reference behaviour pinned here: readGraphFromFile (bfs.cu:829-880) symmetrises
+every input edge in file order, keeps duplicates and self-loops (a self-loop
+appears twice), numEdges = 2m; bfsCPU (bfs.cu:923-945) gives the exact levels.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import distributed_cuda_bfs_amd as dbfs
+from distributed_cuda_bfs_amd.utils.validate import check_levels_against_oracle, levels_are_consistent
+
+U = dbfs.UNREACHED
+
+
+def test_chain8_levels(data_dir):
+    csr = dbfs.read_graph(os.path.join(data_dir, "chain8.txt"))
+    assert csr.n == 8 and csr.input_edges == 7 and csr.directed_edges == 14
+    lv, par = dbfs.cpu_bfs(csr, 0)
+    assert lv.tolist() == list(range(8))
+    assert par[0] == -1
+
+
+def test_reference_adjacency_order(data_dir):
+    csr = dbfs.read_graph(os.path.join(data_dir, "two_components.txt"))
+    ro, col = np.asarray(csr.row_off), np.asarray(csr.col)
+    # adj[u] += v ; adj[v] += u per input edge in file order (bfs.cu:860-861)
+    assert col[ro[0]:ro[1]].tolist() == [1, 0 + 2]  # edges (0,1) then (2,0)
+    assert col[ro[2]:ro[3]].tolist() == [1, 0]
+    assert col[ro[5]:ro[6]].tolist() == [4, 5, 5]  # self-loop appears twice
+    assert csr.directed_edges == 14
+
+
+def test_two_components_unreached(data_dir):
+    csr = dbfs.read_graph(os.path.join(data_dir, "two_components.txt"))
+    lv, _ = dbfs.cpu_bfs(csr, 3)
+    assert lv.tolist() == [U, U, U, 0, 1, 2, U, U, U, U]
+    assert levels_are_consistent(csr, lv, 3)
+
+
+def test_matrix_market(data_dir):
+    p = os.path.join(data_dir, "dup_self.mtx")
+    assert dbfs.detect_format(p) == "mtx"
+    n, u, v = dbfs.read_edge_list(p)
+    assert n == 7 and len(u) == 9
+    assert (u[0], v[0]) == (0, 1)  # 1-based -> 0-based
+    csr = dbfs.read_graph(p)
+    lv, _ = dbfs.cpu_bfs(csr, 0)
+    assert lv.tolist() == [0, 1, 2, 3, 3, 2, 1]
+
+
+def test_bad_inputs(tmp_path):
+    bad = tmp_path / "bad.txt"
+    bad.write_text("3 2\n0 1\n1 7\n")
+    with pytest.raises(RuntimeError, match="out of range"):
+        dbfs.read_graph(str(bad))
+    trunc = tmp_path / "trunc.txt"
+    trunc.write_text("3 5\n0 1\n")
+    with pytest.raises(RuntimeError, match="truncated"):
+        dbfs.read_graph(str(trunc))
+    with pytest.raises(RuntimeError, match="not open"):
+        dbfs.read_graph(str(tmp_path / "missing.txt"))
+
+
+def test_binary_cache_roundtrip(tmp_path):
+    p = dbfs.rmat_params(10, 8, 4)
+    csr = dbfs.host_csr_from_params(p)
+    f = str(tmp_path / "g.csr")
+    dbfs.ops.write_binary_csr(f, csr)
+    assert dbfs.detect_format(f) == "binary"
+    back = dbfs.read_graph(f)
+    assert np.array_equal(np.asarray(back.row_off), np.asarray(csr.row_off))
+    assert np.array_equal(np.asarray(back.col), np.asarray(csr.col))
+    assert back.input_edges == csr.input_edges
+
+
+def test_levels_out_format(tmp_path):
+    f = str(tmp_path / "l.txt")
+    dbfs.ops.write_levels(f, np.array([0, 1, U], dtype=np.int32))
+    assert open(f).read() == "0\n1\n2147483647\n"
+
+
+def test_generator_deterministic_and_scrambled():
+    p = dbfs.rmat_params(14, 16, 1)
+    u1, v1 = dbfs.generate_edges(p, 0, 1000)
+    u2, v2 = dbfs.generate_edges(p, 500, 1000)
+    assert np.array_equal(u1[500:], u2) and np.array_equal(v1[500:], v2)
+    assert u1.max() < p.n and v1.max() < p.n
+    # scramble spreads the hubs: vertex 0 is not the top-degree vertex
+    u, v = dbfs.generate_edges(p)
+    deg = np.bincount(np.concatenate([u, v]), minlength=p.n)
+    assert deg.sum() == 2 * p.m
+    assert int(np.argmax(deg)) != 0
+    # a different seed gives a different graph
+    q = dbfs.rmat_params(14, 16, 2)
+    u3, _ = dbfs.generate_edges(q, 0, 1000)
+    assert not np.array_equal(u1, u3)
+
+
+def test_scramble_is_bijective():
+    N = dbfs.native
+    for scale in (1, 5, 10):
+        xs = [N.scramble_vertex(x, scale, 42) for x in range(1 << scale)]
+        assert sorted(xs) == list(range(1 << scale))
+
+
+def test_rmat_skew():
+    p = dbfs.rmat_params(12, 16, 3)
+    u, v = dbfs.generate_edges(p)
+    deg = np.bincount(np.concatenate([u, v]), minlength=p.n)
+    assert deg.max() > 20 * deg.mean()  # power-law hubs
+
+
+def test_uniform_generator():
+    p = dbfs.uniform_params(1000, 5000, 3)
+    u, v = dbfs.generate_edges(p)
+    assert len(u) == 5000 and u.max() < 1000 and v.max() < 1000
+
+
+def test_check_levels_against_oracle():
+    assert check_levels_against_oracle([0, 1, 2], [0, 1, 2]) is None
+    assert check_levels_against_oracle([0, 2, 2], [0, 1, 2]) == (1, 2, 1)
+
+
+def test_partition_block_rounding():
+    N = dbfs.native
+    p = N.Partition(1000, 3)
+    assert p.part % 64 == 0 and p.part * 3 >= 1000
+    owners = [p.owner(v) for v in range(1000)]
+    assert min(owners) == 0 and max(owners) == 2
+    assert sum(p.count(r) for r in range(3)) == 1000
+    assert p.lo(0) == 0 and p.hi(2) == 1000
+    # N % P != 0 with tiny N: every vertex still has a valid owner (reference defect D5)
+    q = N.Partition(5, 4)
+    assert all(0 <= q.owner(v) < 4 for v in range(5))
+    assert sum(q.count(r) for r in range(4)) == 5
