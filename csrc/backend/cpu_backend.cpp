@@ -200,6 +200,22 @@ class CpuBackend final : public Backend {
     a.out[2] += orphan;
   }
 
+  void compute_parents(const ParentArgs& a) override {
+    for (int64_t r = 0; r < a.g.rows; ++r) {
+      const int64_t v = a.g.lo + r;
+      const lvl_t lv = a.level_global[v];
+      int64_t par = -1;
+      if (v == a.src) {
+        par = v;
+      } else if (lv != kUnreached) {
+        for (eid_t e = a.g.row_off[r]; e < a.g.row_off[r + 1]; ++e) {
+          if (a.level_global[a.g.col[e]] == lv - 1) { par = a.g.col[e]; break; }
+        }
+      }
+      a.parent[r] = par;
+    }
+  }
+
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     for (int64_t i = 0; i < p.m; ++i) {
       uint64_t u, v;

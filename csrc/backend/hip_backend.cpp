@@ -121,6 +121,7 @@ class HipBackend final : public Backend {
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
   void ref_accept(const RefAcceptArgs& a) override { on(); kern::ref_accept(a, st_); chk(); }
   void validate_levels(const ValidateArgs& a) override { on(); kern::validate_levels(a, st_); chk(); }
+  void compute_parents(const ParentArgs& a) override { on(); kern::compute_parents(a, st_); chk(); }
 
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     on();

@@ -474,13 +474,49 @@ std::vector<lvl_t> Engine::gather_levels() {
   return h;
 }
 
-std::vector<int64_t> Engine::validate(int64_t source) {
+void Engine::gather_levels_device(DBuf<lvl_t>& full) {
   const int P = part_.nranks;
   const int64_t part = part_.part;
-  DBuf<lvl_t> send(be_, static_cast<size_t>(part)), full(be_, static_cast<size_t>(P * part));
+  DBuf<lvl_t> send(be_, static_cast<size_t>(part));
+  full = DBuf<lvl_t>(be_, static_cast<size_t>(P * part));
   be_.fill_level(send.data(), part, kUnreached);
   be_.copy_async(send.data(), level_.data(), static_cast<size_t>(g_.rows()) * sizeof(lvl_t));
   comm_.allgather(send.data(), full.data(), static_cast<size_t>(part) * sizeof(lvl_t));
+}
+
+std::vector<int64_t> Engine::parents_local(int64_t source) {
+  DBuf<lvl_t> full;
+  gather_levels_device(full);
+  DBuf<int64_t> par(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
+  ParentArgs pa;
+  pa.g = g_.view();
+  pa.level_global = full.data();
+  pa.src = source;
+  pa.parent = par.data();
+  be_.compute_parents(pa);
+  std::vector<int64_t> h(static_cast<size_t>(g_.rows()));
+  if (!h.empty()) be_.to_host(h.data(), par.data(), h.size() * sizeof(int64_t));
+  else be_.synchronize();
+  return h;
+}
+
+std::vector<int64_t> Engine::gather_parents(int64_t source) {
+  const int P = part_.nranks;
+  const int64_t part = part_.part;
+  std::vector<int64_t> mine = parents_local(source);
+  mine.resize(static_cast<size_t>(part), -1);
+  DBuf<int64_t> send(be_, static_cast<size_t>(part)), recv(be_, static_cast<size_t>(P * part));
+  be_.to_device(send.data(), mine.data(), mine.size() * sizeof(int64_t));
+  comm_.allgather(send.data(), recv.data(), static_cast<size_t>(part) * sizeof(int64_t));
+  std::vector<int64_t> h(static_cast<size_t>(P * part));
+  be_.to_host(h.data(), recv.data(), h.size() * sizeof(int64_t));
+  h.resize(static_cast<size_t>(part_.n));
+  return h;
+}
+
+std::vector<int64_t> Engine::validate(int64_t source) {
+  DBuf<lvl_t> full;
+  gather_levels_device(full);
   DBuf<int64_t> out(be_, 3);
   be_.memset_async(out.data(), 0, out.bytes());
   ValidateArgs va;

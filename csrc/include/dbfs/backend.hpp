@@ -158,6 +158,16 @@ struct ValidateArgs {
   int64_t* out = nullptr;               // 3 counters (device)
 };
 
+// Graph500 parent tree from levels: parent[v] = first neighbour u with
+// level[u] == level[v] - 1 (global vertex id), parent[src] = src, -1 if
+// unreached.  Computed after a run from the all-gathered level array.
+struct ParentArgs {
+  ShardView g;
+  const lvl_t* level_global = nullptr;  // n entries
+  int64_t src = 0;
+  int64_t* parent = nullptr;            // rows (owned slice)
+};
+
 // ---- backend ----------------------------------------------------------------
 
 class Backend {
@@ -195,6 +205,7 @@ class Backend {
   virtual void ref_expand(const RefExpandArgs& a) = 0;
   virtual void ref_accept(const RefAcceptArgs& a) = 0;
   virtual void validate_levels(const ValidateArgs& a) = 0;
+  virtual void compute_parents(const ParentArgs& a) = 0;
 
   // graph construction on the device
   // deg[r] += number of edge endpoints owned in rows [lo, lo + rows) (deg zeroed by caller)

@@ -97,6 +97,10 @@ class Engine {
   // Graph500-style device validation of the last run; returns violation counts
   // {depth-gap, reached-unreached, orphan} summed over ranks (all must be 0).
   std::vector<int64_t> validate(int64_t source);
+  // Graph500 parent tree of the last run (global vertex ids; -1 unreached):
+  // owned slice, and the full array (all ranks participate in both).
+  std::vector<int64_t> parents_local(int64_t source);
+  std::vector<int64_t> gather_parents(int64_t source);
   int64_t global_directed_edges() const { return total_directed_; }
   const EngineOptions& options() const { return opt_; }
   void set_options(const EngineOptions& o) { opt_ = o; }
@@ -106,6 +110,7 @@ class Engine {
   RunResult run_ref(int64_t source);
   void alloc_bitmap_state();
   void alloc_ref_state();
+  void gather_levels_device(DBuf<lvl_t>& full);
 
   DeviceGraph& g_;
   Comm& comm_;

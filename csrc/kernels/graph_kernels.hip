@@ -142,6 +142,37 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(ValidateArgs a) {
   if (orphan) atomicAdd(reinterpret_cast<unsigned long long*>(a.out + 2), 1ull);
 }
 
+// One wave per owned vertex: 64 neighbours per step, first match by ballot.
+__global__ __launch_bounds__(kBlock) void parent_kernel(ParentArgs a) {
+  const int lane = lane_id();
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= a.g.rows) return;
+  const int64_t v = a.g.lo + r;
+  const lvl_t lv = a.level_global[v];
+  if (v == a.src || lv == kUnreached) {
+    if (lane == 0) a.parent[r] = (v == a.src) ? v : -1;
+    return;
+  }
+  const eid_t b = a.g.row_off[r], e = a.g.row_off[r + 1];
+  long long par = -1;
+  for (eid_t base = b; base < e; base += kWave) {
+    const eid_t idx = base + lane;
+    vid_t u = 0;
+    bool hit = false;
+    if (idx < e) {
+      u = a.g.col[idx];
+      hit = a.level_global[u] == lv - 1;
+    }
+    const unsigned long long m = __ballot(hit);
+    if (m) {
+      const int l = __ffsll(static_cast<long long>(m)) - 1;
+      par = __shfl(static_cast<int>(u), l, kWave);
+      break;
+    }
+  }
+  if (lane == 0) a.parent[r] = par;
+}
+
 __global__ __launch_bounds__(kBlock) void reached_deg_kernel(ShardView g, const lvl_t* __restrict__ level,
                                                             int64_t* out2) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
@@ -202,6 +233,12 @@ void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st) {
 void validate_levels(const ValidateArgs& a, hipStream_t st) {
   if (a.g.rows <= 0) return;
   validate_kernel<<<static_cast<unsigned>((a.g.rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(a);
+}
+
+void compute_parents(const ParentArgs& a, hipStream_t st) {
+  if (a.g.rows <= 0) return;
+  const int64_t wpb = kBlock / kWave;
+  parent_kernel<<<static_cast<unsigned>((a.g.rows + wpb - 1) / wpb), kBlock, 0, st>>>(a);
 }
 
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st) {

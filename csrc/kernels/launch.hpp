@@ -30,6 +30,7 @@ void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t
 int64_t scan_tmp_elems(int64_t n);
 void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st);
 void validate_levels(const ValidateArgs& a, hipStream_t st);
+void compute_parents(const ParentArgs& a, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
 
 }  // namespace kern

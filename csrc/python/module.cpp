@@ -381,6 +381,23 @@ PYBIND11_MODULE(_dbfs_native, m) {
              return to_numpy(v);
            })
       .def("validate", &Engine::validate, py::call_guard<py::gil_scoped_release>())
+      .def("parents_local",
+           [](Engine& e, int64_t src) {
+             std::vector<int64_t> v;
+             {
+               py::gil_scoped_release rel;
+               v = e.parents_local(src);
+             }
+             return to_numpy(v);
+           })
+      .def("gather_parents", [](Engine& e, int64_t src) {
+        std::vector<int64_t> v;
+        {
+          py::gil_scoped_release rel;
+          v = e.gather_parents(src);
+        }
+        return to_numpy(v);
+      })
       .def_property_readonly("global_directed_edges", &Engine::global_directed_edges)
       .def_property(
           "mode", [](const Engine& e) { return std::string(mode_name(e.options().mode)); },

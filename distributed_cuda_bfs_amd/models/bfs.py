@@ -77,6 +77,15 @@ class BFS:
     def local_levels(self) -> np.ndarray:
         return self.engine.levels_local()
 
+    def parents(self, source: int) -> np.ndarray:
+        """Graph500 parent tree of the last run from ``source`` (collective).
+
+        parent[v] is a neighbour one level closer to the source (global vertex
+        id), parent[source] = source, -1 for unreached vertices.  The reference
+        records edge indices as parents and never gathers them (bfs.cu:147,439).
+        """
+        return self.engine.gather_parents(int(source))
+
     def validate(self, source: int) -> bool:
         """Graph500-style level validation of the last run on the device (collective)."""
         gap, cross, orphan = self.engine.validate(int(source))

@@ -46,3 +46,27 @@ def levels_are_consistent(csr, levels, src: int) -> bool:
     reached = lv != UNREACHED
     reached[src] = False
     return bool(np.all(has_parent[reached]))
+
+
+def parents_are_valid(csr, levels, parents, src: int) -> bool:
+    """Graph500 parent-tree check: every reached v != src has an edge to
+    parent[v] and level[parent[v]] == level[v] - 1; unreached have -1."""
+    lv = np.asarray(levels, dtype=np.int64)
+    par = np.asarray(parents, dtype=np.int64)
+    ro = np.asarray(csr.row_off)
+    col = np.asarray(csr.col)
+    if par[src] != src:
+        return False
+    for v in range(csr.n):
+        if v == src:
+            continue
+        if lv[v] == UNREACHED:
+            if par[v] != -1:
+                return False
+            continue
+        p = par[v]
+        if p < 0 or lv[p] != lv[v] - 1:
+            return False
+        if p not in col[ro[v]:ro[v + 1]]:
+            return False
+    return True

@@ -131,3 +131,30 @@ def test_mode_switch_on_same_engine(rt):
         assert bfs.mode == m
         bfs.run(9)
         assert np.array_equal(bfs.levels(), _oracle(csr, 9))
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_parent_tree(rt, mode):
+    from distributed_cuda_bfs_amd.utils.validate import parents_are_valid
+
+    p = dbfs.rmat_params(10, 8, 4)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    src = bfs.sample_roots(1, seed=2)[0]
+    bfs.run(src)
+    assert parents_are_valid(csr, bfs.levels(), bfs.parents(src), src)
+
+
+def test_parent_tree_virtual_ranks():
+    from distributed_cuda_bfs_amd.utils.validate import parents_are_valid
+
+    p = dbfs.rmat_params(9, 8, 6)
+    csr = dbfs.host_csr_from_params(p)
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode="do")
+        bfs.run(1)
+        return bfs.levels(), bfs.parents(1)
+
+    for lv, par in run_virtual_ranks(3, body, device="cpu"):
+        assert parents_are_valid(csr, lv, par, 1)

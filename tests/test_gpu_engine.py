@@ -106,3 +106,28 @@ def test_virtual_ranks_on_one_gpu(P, mode):
     outs = run_virtual_ranks(P, body, device="hip")
     for o in outs:
         assert np.array_equal(o, exp)
+
+
+@pytest.mark.parametrize("mode", ["do", "ref"])
+def test_parent_tree_gpu(gpu_runtime, mode):
+    from distributed_cuda_bfs_amd.utils.validate import parents_are_valid
+
+    p = dbfs.rmat_params(12, 16, 21)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    src = bfs.sample_roots(1, seed=8)[0]
+    bfs.run(src)
+    assert parents_are_valid(csr, bfs.levels(), bfs.parents(src), src)
+
+
+def test_cli_gpu_reference_stdout(data_dir):
+    import os
+    import subprocess
+
+    repo = os.path.dirname(data_dir.rstrip("/").rsplit("/", 1)[0] + "/")
+    out = subprocess.run([os.path.join(os.path.dirname(os.path.dirname(data_dir)), "bin", "bfs"), "0",
+                          os.path.join(data_dir, "chain8.txt")], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "Enabling peer access between GPU0 and GPU1..." in out.stdout
+    assert out.stdout.endswith("Output OK!\n\n")
+    del repo
