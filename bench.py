@@ -107,11 +107,17 @@ def main() -> int:
     edges = sum(r.edges for r in results)
     bfs_ms = sum(r.ms for r in results)
     value = edges / (wall_ms * 1e6)
-    if rank == 0:
-        if args.per_level:
-            for lv in results[0].levels:
+    if args.per_level:
+        # one extra (untimed) traversal of the first timed root with per-level device events
+        bfs.engine.phase_timing = True
+        prof = bfs.run(timed[0])
+        bfs.engine.phase_timing = False
+        if rank == 0:
+            log(f"per-level profile of root {timed[0]} ({prof.ms:.3f} ms incl. event overhead):")
+            for lv in prof.levels:
                 log(f"  level {lv['level']} {lv['dir']} frontier {lv['frontier']} edges {lv['frontier_edges']}"
-                    f" new {lv['discovered']}")
+                    f" new {lv['discovered']} {lv['ms']:.3f} ms")
+    if rank == 0:
         out = {
             "metric": METRIC,
             "value": round(value, 4),

@@ -406,6 +406,13 @@ PYBIND11_MODULE(_dbfs_native, m) {
             o.mode = parse_mode(s);
             e.set_options(o);
           })
+      .def_property(
+          "phase_timing", [](const Engine& e) { return e.options().phase_timing; },
+          [](Engine& e, bool on) {
+            EngineOptions o = e.options();
+            o.phase_timing = on;
+            e.set_options(o);
+          })
       .def("set_heuristics", [](Engine& e, double alpha, double beta, int lane_limit) {
         EngineOptions o = e.options();
         o.alpha = alpha;

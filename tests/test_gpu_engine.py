@@ -124,10 +124,9 @@ def test_cli_gpu_reference_stdout(data_dir):
     import os
     import subprocess
 
-    repo = os.path.dirname(data_dir.rstrip("/").rsplit("/", 1)[0] + "/")
-    out = subprocess.run([os.path.join(os.path.dirname(os.path.dirname(data_dir)), "bin", "bfs"), "0",
-                          os.path.join(data_dir, "chain8.txt")], capture_output=True, text=True, timeout=120)
+    repo = os.path.dirname(os.path.dirname(data_dir))  # data_dir = <repo>/tests/data
+    out = subprocess.run([os.path.join(repo, "bin", "bfs"), "0", os.path.join(data_dir, "chain8.txt")],
+                         capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "Enabling peer access between GPU0 and GPU1..." in out.stdout
     assert out.stdout.endswith("Output OK!\n\n")
-    del repo
