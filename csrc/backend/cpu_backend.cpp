@@ -50,15 +50,16 @@ class CpuBackend final : public Backend {
   void set_bit(word_t* bm, int64_t bit) override { bm[bit >> 6] |= 1ull << (bit & 63); }
 
   void update_frontier(const UpdateArgs& a) override {
-    const int64_t nseg = div_up(a.words, kSegWords);
-    for (int64_t s = 0; s < nseg; ++s) {
+    const int64_t nunits = div_up(a.words, kUnitWords);
+    for (int64_t u = 0; u < nunits; ++u) {
       int64_t cnt = 0, deg = 0;
-      for (int64_t w = s * kSegWords; w < std::min<int64_t>(a.words, (s + 1) * kSegWords); ++w) {
+      for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
         for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
-        const word_t nb = c & ~a.visited[w];
+        const word_t nb = a.force ? c : (c & ~a.visited[w]);
         a.visited[w] |= nb;
         a.frontier[w] = nb;
+        if (a.clear_cand) a.cand[w] = 0;
         word_t x = nb;
         while (x) {
           const int b = __builtin_ctzll(x);
@@ -69,30 +70,50 @@ class CpuBackend final : public Backend {
           if (d > 0) { ++cnt; deg += d; }
         }
       }
-      a.seg_cnt[s] = cnt;
-      a.seg_deg[s] = deg;
+      a.unit_cnt[u] = cnt;
+      a.unit_deg[u] = deg;
     }
   }
 
-  void scan_segments(const ScanArgs& a) override {
+  void scan_units(const ScanArgs& a) override {
+    const int64_t nchunks = div_up(a.nunits, kScanChunk);
     int64_t c = 0, d = 0;
-    for (int64_t s = 0; s < a.nseg; ++s) {
-      const int64_t tc = a.seg_cnt[s], td = a.seg_deg[s];
-      a.seg_cnt[s] = c;
-      a.seg_deg[s] = d;
-      c += tc;
-      d += td;
+    for (int64_t k = 0; k < nchunks; ++k) {
+      int64_t ic = 0, id = 0;
+      for (int64_t u = k * kScanChunk; u < std::min<int64_t>(a.nunits, (k + 1) * kScanChunk); ++u) {
+        const int64_t tc = a.unit_cnt[u], td = a.unit_deg[u];
+        a.unit_cnt[u] = ic;
+        a.unit_deg[u] = id;
+        ic += tc;
+        id += td;
+      }
+      a.part_cnt[k] = c;
+      a.part_deg[k] = d;
+      c += ic;
+      d += id;
     }
     a.stats[0] = a.stats[2] = c;
     a.stats[1] = a.stats[3] = d;
     a.qscan[c] = d;
   }
 
+  void zero_degree_mask(const ZeroDegArgs& a) override {
+    for (int64_t w = 0; w < a.words; ++w) {
+      word_t m = 0;
+      for (int b = 0; b < 64; ++b) {
+        const int64_t v = w * 64 + b;
+        if (v >= a.g.rows || a.g.row_off[v + 1] == a.g.row_off[v]) m |= 1ull << b;
+      }
+      a.out[w] = m;
+    }
+  }
+
   void compact_frontier(const CompactArgs& a) override {
-    const int64_t nseg = div_up(a.words, kSegWords);
-    for (int64_t s = 0; s < nseg; ++s) {
-      int64_t pos = a.seg_cnt_off[s], off = a.seg_deg_off[s];
-      for (int64_t w = s * kSegWords; w < std::min<int64_t>(a.words, (s + 1) * kSegWords); ++w) {
+    const int64_t nunits = div_up(a.words, kUnitWords);
+    for (int64_t u = 0; u < nunits; ++u) {
+      int64_t pos = a.unit_cnt_off[u] + a.part_cnt[u / kScanChunk];
+      int64_t off = a.unit_deg_off[u] + a.part_deg[u / kScanChunk];
+      for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t x = a.frontier[w];
         while (x) {
           const int b = __builtin_ctzll(x);
@@ -122,17 +143,30 @@ class CpuBackend final : public Backend {
   }
 
   void bu_step(const BuArgs& a) override {
-    for (int64_t w = 0; w < a.words; ++w) {
-      word_t out = 0;
-      const word_t vis = a.visited[w];
-      for (int b = 0; b < 64; ++b) {
-        const int64_t v = w * 64 + b;
-        if (v >= a.g.rows || ((vis >> b) & 1ull)) continue;
-        for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
-          if (test_bit(a.frontier, a.g.col[e])) { out |= 1ull << b; break; }
+    const int64_t nunits = div_up(a.words, kUnitWords);
+    for (int64_t u = 0; u < nunits; ++u) {
+      int64_t cnt = 0, deg = 0;
+      for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
+        word_t out = 0;
+        const word_t vis = a.visited[w];
+        for (int b = 0; b < 64; ++b) {
+          const int64_t v = w * 64 + b;
+          if (v >= a.g.rows || ((vis >> b) & 1ull)) continue;
+          for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
+            if (test_bit(a.frontier, a.g.col[e])) {
+              out |= 1ull << b;
+              a.level[v] = a.new_level;
+              ++cnt;
+              deg += a.g.row_off[v + 1] - a.g.row_off[v];
+              break;
+            }
+          }
         }
+        a.visited[w] = vis | out;
+        a.new_frontier[w] = out;
       }
-      a.cand[w] = out;
+      a.unit_cnt[u] = cnt;
+      a.unit_deg[u] = deg;
     }
   }
 

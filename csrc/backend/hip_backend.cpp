@@ -112,7 +112,8 @@ class HipBackend final : public Backend {
   void fill_level(lvl_t* level, int64_t n, lvl_t value) override { on(); kern::fill_level(level, n, value, st_); chk(); }
   void set_bit(word_t* bm, int64_t bit) override { on(); kern::set_bit(bm, bit, st_); chk(); }
   void update_frontier(const UpdateArgs& a) override { on(); kern::update_frontier(a, st_); chk(); }
-  void scan_segments(const ScanArgs& a) override { on(); kern::scan_segments(a, st_); chk(); }
+  void scan_units(const ScanArgs& a) override { on(); kern::scan_units(a, st_); chk(); }
+  void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }

@@ -156,17 +156,32 @@ void Engine::alloc_bitmap_state() {
   const int64_t W = part_.slice_words(), GW = part_.global_words();
   const int P = part_.nranks;
   visited_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
-  frontier_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  zdeg_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  frontier_[0] = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  frontier_[1] = DBuf<word_t>(be_, static_cast<size_t>(GW));
   next_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
   if (P > 1) recv_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
   cand_ = DBuf<word_t>(be_, static_cast<size_t>(W));
-  nseg_ = div_up(W, kSegWords);
-  seg_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(nseg_ + 1));
-  seg_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(nseg_ + 1));
+  nunits_ = div_up(W, kUnitWords);
+  unit_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(nunits_ + 1));
+  unit_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(nunits_ + 1));
+  part_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(nunits_, kScanChunk) + 1));
+  part_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(nunits_, kScanChunk) + 1));
+  ticket_ = DBuf<unsigned>(be_, 4);
+  be_.memset_async(ticket_.data(), 0, ticket_.bytes());
   qscan_ = DBuf<int64_t>(be_, static_cast<size_t>(g_.rows() + 1));
   qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
   stats_ = DBuf<int64_t>(be_, 8);
+  // Zero-degree (and padding) vertices can never be discovered: they start out
+  // visited, so bottom-up steps skip them without touching row_off.
+  ZeroDegArgs za;
+  za.g = g_.view();
+  za.out = zdeg_.data() + comm_.rank() * W;
+  za.words = W;
+  be_.zero_degree_mask(za);
+  if (P > 1) comm_.allgather(za.out, zdeg_.data(), static_cast<size_t>(W) * sizeof(word_t));
+  be_.synchronize();
   bitmap_ready_ = true;
 }
 
@@ -212,7 +227,12 @@ RunResult Engine::run_bitmap(int64_t source) {
   const int64_t lo = g_.lo();
   const ShardView gv = g_.view();
   word_t* vis_own = visited_.data() + me * W;
-  word_t* fr_own = frontier_.data() + me * W;
+  // Frontier double buffer: `cur` is the frontier being expanded (global after
+  // the all-gather), `nxt` receives the next one (bottom-up reads `cur` while
+  // it writes `nxt`, so they must differ).
+  int cur = 0;
+  auto fr_cur = [&]() { return frontier_[cur].data(); };
+  auto fr_nxt_own = [&]() { return frontier_[cur ^ 1].data() + me * W; };
 
   RunResult res;
   res.source = source;
@@ -222,42 +242,54 @@ RunResult Engine::run_bitmap(int64_t source) {
 
   // ---- init (inside the timed window) ----
   be_.fill_level(level_.data(), g_.rows(), kUnreached);
-  be_.memset_async(visited_.data(), 0, visited_.bytes());
+  be_.copy_async(visited_.data(), zdeg_.data(), visited_.bytes());
   be_.memset_async(cand_.data(), 0, cand_.bytes());
+  be_.memset_async(next_.data(), 0, next_.bytes());
   if (part_.owner(source) == me) be_.set_bit(cand_.data(), source - lo);
 
-  auto update_and_exchange = [&](const word_t* cand, int nchunks, int64_t stride, lvl_t new_level,
-                                 int64_t* host_stats) {
-    UpdateArgs ua;
-    ua.g = gv;
-    ua.cand = cand;
-    ua.nchunks = nchunks;
-    ua.cand_stride = stride;
-    ua.visited = vis_own;
-    ua.frontier = fr_own;
-    ua.level = level_.data();
-    ua.new_level = new_level;
-    ua.words = W;
-    ua.seg_cnt = seg_cnt_.data();
-    ua.seg_deg = seg_deg_.data();
-    be_.update_frontier(ua);
+  // Scan the unit statistics of the new frontier, publish it (all-gather, P > 1),
+  // merge it into the replicated visited bitmap, reduce the totals to the host.
+  auto finish_level = [&](int64_t* host_stats) {
     ScanArgs sa;
-    sa.seg_cnt = seg_cnt_.data();
-    sa.seg_deg = seg_deg_.data();
-    sa.nseg = nseg_;
+    sa.unit_cnt = unit_cnt_.data();
+    sa.unit_deg = unit_deg_.data();
+    sa.nunits = nunits_;
+    sa.part_cnt = part_cnt_.data();
+    sa.part_deg = part_deg_.data();
+    sa.ticket = ticket_.data();
     sa.stats = stats_.data();
     sa.qscan = qscan_.data();
-    be_.scan_segments(sa);
+    be_.scan_units(sa);
+    cur ^= 1;
     if (P > 1) {
-      comm_.allgather(fr_own, frontier_.data(), static_cast<size_t>(W) * sizeof(word_t));
-      be_.bitmap_or(visited_.data(), frontier_.data(), GW);
+      comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
+      be_.bitmap_or(visited_.data(), fr_cur(), GW);
     }
     comm_.allreduce_sum_i64(stats_.data() + 2, 2);
     be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
   };
+  auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level) {
+    UpdateArgs ua;
+    ua.g = gv;
+    ua.cand = cand;
+    ua.nchunks = nchunks;
+    ua.cand_stride = W;
+    ua.clear_cand = clear;
+    ua.force = force;
+    ua.visited = vis_own;
+    ua.frontier = fr_nxt_own();
+    ua.level = level_.data();
+    ua.new_level = new_level;
+    ua.words = W;
+    ua.unit_cnt = unit_cnt_.data();
+    ua.unit_deg = unit_deg_.data();
+    be_.update_frontier(ua);
+  };
 
   int64_t hs[4];
-  update_and_exchange(cand_.data(), 1, W, 0, hs);
+  // Seed: the source is forced in even when it has degree 0 (pre-visited).
+  update(cand_.data(), 1, false, true, 0);
+  finish_level(hs);
   int64_t q_local = hs[0], m_local = hs[1], n_f = hs[2], m_f = hs[3];
   int64_t vis_deg = m_f;
   int64_t prev_nf = 0;
@@ -280,18 +312,19 @@ RunResult Engine::run_bitmap(int64_t source) {
       }
     }
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    const word_t* cand = nullptr;
-    int nchunks = 1;
     if (dir == 'T' || dir == 'S') {
-      be_.memset_async(next_.data(), 0, next_.bytes());
+      // `next` is all-zero here: cleared at init and by every consuming update
+      // (P == 1), or re-zeroed right after the exchange below (P > 1).
       if (dir == 'T') {
         if (q_local > 0) {
           CompactArgs ca;
           ca.g = gv;
-          ca.frontier = fr_own;
+          ca.frontier = fr_cur() + me * W;
           ca.words = W;
-          ca.seg_cnt_off = seg_cnt_.data();
-          ca.seg_deg_off = seg_deg_.data();
+          ca.unit_cnt_off = unit_cnt_.data();
+          ca.unit_deg_off = unit_deg_.data();
+          ca.part_cnt = part_cnt_.data();
+          ca.part_deg = part_deg_.data();
           ca.qscan = qscan_.data();
           ca.qbase = qbase_.data();
           ca.blk_vstart = blk_vstart_.data();
@@ -318,23 +351,26 @@ RunResult Engine::run_bitmap(int64_t source) {
       }
       if (P > 1) {
         comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
-        cand = recv_.data();
-        nchunks = P;
+        be_.memset_async(next_.data(), 0, next_.bytes());
+        update(recv_.data(), P, false, false, L + 1);
       } else {
-        cand = next_.data();
+        update(next_.data(), 1, true, false, L + 1);
       }
     } else {
       BuArgs ba;
       ba.g = gv;
       ba.visited = vis_own;
-      ba.frontier = frontier_.data();
-      ba.cand = cand_.data();
+      ba.frontier = fr_cur();
+      ba.new_frontier = fr_nxt_own();
+      ba.level = level_.data();
+      ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
+      ba.unit_cnt = unit_cnt_.data();
+      ba.unit_deg = unit_deg_.data();
       be_.bu_step(ba);
-      cand = cand_.data();
     }
-    update_and_exchange(cand, nchunks, W, L + 1, hs);
+    finish_level(hs);
     LevelRecord rec;
     rec.level = L;
     rec.direction = dir;

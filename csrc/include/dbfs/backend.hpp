@@ -35,39 +35,51 @@ struct ShardView {
   int64_t n = 0, lo = 0, rows = 0, nnz = 0;
 };
 
-// Frontier bookkeeping is organised in "segments" of 64 bitmap words
-// (4096 vertices) -- one wave64 per segment in the HIP kernels.
-constexpr int kSegWords = 64;
-constexpr int kSegVertices = kSegWords * kWordBits;
+// Frontier bookkeeping is organised in "units" of 16 bitmap words (1024
+// vertices): one 1024-thread workgroup per unit, one wave64 per word, in the
+// HIP kernels.  Per-unit counts are scanned by a multi-block scan whose chunks
+// hold kScanChunk units.
+constexpr int kUnitWords = 16;
+constexpr int kUnitVertices = kUnitWords * kWordBits;
+constexpr int kScanChunk = 1024;
 // Top-down expansion handles kTdEdgesPerBlock frontier edges per workgroup.
 constexpr int kTdThreads = 256;
 constexpr int kTdItems = 8;
 constexpr int kTdEdgesPerBlock = kTdThreads * kTdItems;
 
-// new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice:
-// visited |= new; frontier = new; level[v] = new_level for v in new;
-// seg_cnt[s] / seg_deg[s] = count / degree-sum of new vertices with degree > 0.
+// new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
+// (force: new = cand, used to seed the source):  visited |= new;
+// frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
+// = count / degree-sum of new vertices with degree > 0.  clear_cand zeroes the
+// consumed cand words (single-chunk top-down: keeps `next` clean).
 struct UpdateArgs {
   ShardView g;
-  const word_t* cand = nullptr;
+  word_t* cand = nullptr;
   int nchunks = 1;
   int64_t cand_stride = 0;       // words between chunks
+  bool clear_cand = false;
+  bool force = false;
   word_t* visited = nullptr;     // owned slice of the global visited bitmap
-  word_t* frontier = nullptr;    // owned slice of the global frontier bitmap
+  word_t* frontier = nullptr;    // owned slice of the NEXT global frontier bitmap
   lvl_t* level = nullptr;        // rows
   lvl_t new_level = 0;
   int64_t words = 0;             // words of the owned slice
-  int64_t* seg_cnt = nullptr;    // nseg
-  int64_t* seg_deg = nullptr;    // nseg
+  int64_t* unit_cnt = nullptr;   // nunits
+  int64_t* unit_deg = nullptr;   // nunits
 };
 
-// In-place exclusive scan of seg_cnt / seg_deg (nseg entries); writes totals to
-// stats[0..1] and stats[2..3] (the latter is all-reduced by the engine), and the
-// end sentinel qscan[total_cnt] = total_deg.
+// Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
+// kScanChunk units) plus chunk prefixes (part_cnt / part_deg, exclusive).  The
+// last workgroup to finish (ticket, agent-scope release/acquire) scans the
+// chunk totals and writes stats[0..1] = stats[2..3] = (count, degree sum) and
+// the work-list end sentinel qscan[count] = degree sum.
 struct ScanArgs {
-  int64_t* seg_cnt = nullptr;
-  int64_t* seg_deg = nullptr;
-  int64_t nseg = 0;
+  int64_t* unit_cnt = nullptr;
+  int64_t* unit_deg = nullptr;
+  int64_t nunits = 0;
+  int64_t* part_cnt = nullptr;   // ceil(nunits / kScanChunk)
+  int64_t* part_deg = nullptr;
+  unsigned* ticket = nullptr;    // zero before the first launch; reset by the last block
   int64_t* stats = nullptr;
   int64_t* qscan = nullptr;
 };
@@ -79,8 +91,10 @@ struct CompactArgs {
   ShardView g;
   const word_t* frontier = nullptr;
   int64_t words = 0;
-  const int64_t* seg_cnt_off = nullptr;
-  const int64_t* seg_deg_off = nullptr;
+  const int64_t* unit_cnt_off = nullptr;  // scanned (in-chunk) unit offsets
+  const int64_t* unit_deg_off = nullptr;
+  const int64_t* part_cnt = nullptr;      // chunk prefixes
+  const int64_t* part_deg = nullptr;
   int64_t* qscan = nullptr;
   int64_t* qbase = nullptr;
   int32_t* blk_vstart = nullptr;
@@ -98,14 +112,28 @@ struct TdArgs {
   word_t* next = nullptr;           // global
 };
 
-// For every owned unvisited v: if some neighbour u has frontier[u]: cand[v] = 1.
+// Bottom-up step fused with the frontier update: for every owned unvisited v,
+// if some neighbour u has frontier[u], v joins the new frontier: visited[v],
+// new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
 struct BuArgs {
   ShardView g;
-  const word_t* visited = nullptr;   // owned slice
-  const word_t* frontier = nullptr;  // global
-  word_t* cand = nullptr;            // owned slice (fully overwritten)
+  word_t* visited = nullptr;         // owned slice
+  const word_t* frontier = nullptr;  // current frontier, global
+  word_t* new_frontier = nullptr;    // owned slice of the next frontier (fully overwritten)
+  lvl_t* level = nullptr;
+  lvl_t new_level = 0;
   int64_t words = 0;
-  int lane_limit = 8;                // neighbours scanned per lane before wave cooperation
+  int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
+  int64_t* unit_cnt = nullptr;
+  int64_t* unit_deg = nullptr;
+};
+
+// Bits of the owned slice for vertices with degree 0 or beyond the shard
+// (padding): they can never be discovered, so they start out "visited".
+struct ZeroDegArgs {
+  ShardView g;
+  word_t* out = nullptr;  // owned slice
+  int64_t words = 0;
 };
 
 // Vertex-centric ("status array") top-down: every owned v with level[v] == cur
@@ -196,7 +224,8 @@ class Backend {
   virtual void fill_level(lvl_t* level, int64_t n, lvl_t value) = 0;
   virtual void set_bit(word_t* bitmap, int64_t bit) = 0;
   virtual void update_frontier(const UpdateArgs& a) = 0;
-  virtual void scan_segments(const ScanArgs& a) = 0;
+  virtual void scan_units(const ScanArgs& a) = 0;
+  virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;

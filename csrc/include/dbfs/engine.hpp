@@ -62,7 +62,7 @@ struct EngineOptions {
   Mode mode = Mode::DirOpt;
   double alpha = 14.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
-  int bu_lane_limit = 8;
+  int bu_lane_limit = 32;
   bool phase_timing = false;  // per-level device timing (adds events)
 };
 
@@ -122,10 +122,11 @@ class Engine {
   DBuf<lvl_t> level_;
   // bitmap engine state
   bool bitmap_ready_ = false;
-  DBuf<word_t> visited_, frontier_, next_, recv_, cand_;
-  DBuf<int64_t> seg_cnt_, seg_deg_, qscan_, qbase_, stats_;
+  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_;
+  DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
+  DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;
-  int64_t nseg_ = 0;
+  int64_t nunits_ = 0;
   // reference-mode state
   bool ref_ready_ = false;
   DBuf<lvl_t> dist_;

@@ -1,6 +1,6 @@
 // gfx950 BFS primitives: frontier update (visited-bitmap update + level write),
-// segment scan, frontier compaction (wave prefix sums), load-balanced top-down
-// neighbour gather, bottom-up parent search.
+// multi-block unit scan, frontier compaction (wave prefix sums), load-balanced
+// top-down neighbour gather, fused bottom-up parent search.
 //
 // Reference counterpart: the single live kernel queueBfs (bfs.cu:134-165) --
 // thread-per-frontier-vertex serial neighbour loop, atomicMin claim on an int
@@ -10,14 +10,18 @@
 // device-scope counter (~88 returning atomics/us per word, MI355X_MICROARCH
 // "dequeue" row).  Here:
 //   * discoveries are bits (atomicOr on a 64-bit word, no counter at all);
-//   * the next work list is built by wave prefix sums over bitmap segments
-//     (one wave64 ballot per 64 vertices) -- deterministic, atomic-free;
+//   * one wave64 owns one bitmap word (64 vertices): ballots build words,
+//     mbcnt gives slots, wave prefix sums give edge offsets -- no atomics;
+//   * per-unit (16 words) counts are scanned by a multi-block scan that hands
+//     its chunk totals to the last-arriving workgroup (agent-scope release /
+//     acquire, cdna_hip_programming.md Guideline 16);
 //   * top-down work is split into equal edge ranges per workgroup
 //     (kTdEdgesPerBlock) with an LDS owner map, so hubs and leaves cost the same
 //     per edge and col[] is read fully coalesced;
 //   * bottom-up scans each owned unvisited vertex's neighbours for a frontier
 //     bit, per lane for the first few, then wave-cooperatively (64 neighbours per
-//     step, ballot early exit) for the long ones.
+//     step, ballot early exit) for the long ones, and writes the new frontier,
+//     visited word, levels and unit stats itself (no separate update pass).
 #include <hip/hip_runtime.h>
 
 #include "launch.hpp"
@@ -30,7 +34,8 @@ namespace {
 using namespace dev;
 
 constexpr int kBlock = 256;
-constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kUnitThreads = kUnitWords * kWave;  // 1024: one wave per word
+static_assert(kUnitThreads == 1024, "unit = 16 waves");
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void fill_level_kernel(lvl_t* __restrict__ level, int64_t n, lvl_t value,
@@ -48,123 +53,195 @@ __global__ void set_bit_kernel(word_t* bm, int64_t bit) {
   if (threadIdx.x == 0) bm[bit >> 6] |= 1ull << (bit & 63);
 }
 
+// Sum (cnt, deg) of the 16 waves of a unit workgroup; thread 0 writes them.
+__device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
+                                                 int64_t* unit_deg) {
+  __shared__ long long s_c[kUnitWords], s_d[kUnitWords];
+  cnt = wave_sum(cnt);
+  deg = wave_sum(deg);
+  const int wv = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    s_c[wv] = cnt;
+    s_d[wv] = deg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long c = 0, d = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitWords; ++k) {
+      c += s_c[k];
+      d += s_d[k];
+    }
+    unit_cnt[unit] = c;
+    unit_deg[unit] = d;
+  }
+}
+
 // ---------------------------------------------------------------------------
-// One wave per segment of 64 words.  Lane l owns word s*64+l for the bitmap
-// update; then, for every non-zero new word (ballot over lanes), the wave
-// switches to lane-per-vertex so level stores and row_off loads are coalesced.
-__global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
+// Frontier update: one wave per owned word; lane l handles vertex w*64+l so the
+// level stores and row_off loads of a word are one coalesced access each.
+__global__ __launch_bounds__(kUnitThreads) void update_kernel(UpdateArgs a) {
   const int lane = lane_id();
-  const int64_t s = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t nseg = (a.words + kSegWords - 1) / kSegWords;
-  if (s >= nseg) return;
-  const int64_t w = s * kSegWords + lane;
-  word_t nb = 0;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6);
+  long long cnt = 0, deg = 0;
   if (w < a.words) {
     word_t c = 0;
     for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
     const word_t vis = a.visited[w];
-    nb = c & ~vis;
-    if (nb) a.visited[w] = vis | nb;
-    a.frontier[w] = nb;
-  }
-  long long cnt = 0, deg = 0;
-  unsigned long long nz = __ballot(nb != 0);
-  const eid_t* __restrict__ ro = a.g.row_off;
-  while (nz) {
-    const int j = __ffsll(static_cast<long long>(nz)) - 1;
-    nz &= nz - 1;
-    const word_t word = readlane64(nb, j);
-    if ((word >> lane) & 1ull) {
-      const int64_t v = (s * kSegWords + j) * 64 + lane;
+    const word_t nb = a.force ? c : (c & ~vis);
+    if (lane == 0) {
+      if (nb) a.visited[w] = vis | nb;
+      a.frontier[w] = nb;
+      if (a.clear_cand && c) a.cand[w] = 0;
+    }
+    if ((nb >> lane) & 1ull) {
+      const int64_t v = w * 64 + lane;
       a.level[v] = a.new_level;
-      const eid_t d = ro[v + 1] - ro[v];
-      if (d > 0) { cnt += 1; deg += d; }
+      const eid_t d = a.g.row_off[v + 1] - a.g.row_off[v];
+      if (d > 0) {
+        cnt = 1;
+        deg = d;
+      }
     }
   }
-  cnt = wave_sum(cnt);
-  deg = wave_sum(deg);
-  if (lane == 0) {
-    a.seg_cnt[s] = cnt;
-    a.seg_deg[s] = deg;
-  }
+  unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
 }
 
 // ---------------------------------------------------------------------------
-// Single workgroup exclusive scan over the segment counters (nseg is at most
-// a few tens of thousands: 4096 vertices per segment).
-constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void scan_segments_kernel(ScanArgs a) {
-  __shared__ long long s_c[kScanThreads / kWave];
-  __shared__ long long s_d[kScanThreads / kWave];
+// Multi-block scan.  Workgroup b scans units [b*CH, (b+1)*CH) in place
+// (exclusive, in-chunk) and publishes its chunk total; the last workgroup to
+// arrive scans the chunk totals.  Hand-off: chunk totals stored by thread 0,
+// `s_waitcnt vmcnt(0)`, agent release fence, `s_waitcnt vmcnt(0)` (compiler
+// hazard, MI355X_MICROARCH), then the ticket atomic; the last arriver runs an
+// agent acquire fence before any thread reads the totals.
+__global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
+  __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
+  __shared__ int s_last;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
-  const int64_t per = (a.nseg + kScanThreads - 1) / kScanThreads;
-  const int64_t b = t * per;
-  const int64_t e = min(a.nseg, b + per);
-  long long c = 0, d = 0;
-  for (int64_t i = b; i < e; ++i) { c += a.seg_cnt[i]; d += a.seg_deg[i]; }
-  const long long ic = wave_incl_scan(c);
-  const long long id = wave_incl_scan(d);
-  if (lane == kWave - 1) { s_c[wv] = ic; s_d[wv] = id; }
-  __syncthreads();
-  long long oc = 0, od = 0;
-  for (int k = 0; k < wv; ++k) { oc += s_c[k]; od += s_d[k]; }
-  long long rc = oc + ic - c, rd = od + id - d;
-  for (int64_t i = b; i < e; ++i) {
-    const long long tc = a.seg_cnt[i], td = a.seg_deg[i];
-    a.seg_cnt[i] = rc;
-    a.seg_deg[i] = rd;
-    rc += tc;
-    rd += td;
+  const int64_t u = static_cast<int64_t>(blockIdx.x) * kScanChunk + t;
+  const long long c = u < a.nunits ? a.unit_cnt[u] : 0;
+  const long long d = u < a.nunits ? a.unit_deg[u] : 0;
+  const long long ic = wave_incl_scan(c), id = wave_incl_scan(d);
+  if (lane == kWave - 1) {
+    s_c[wv] = ic;
+    s_d[wv] = id;
   }
-  if (t == kScanThreads - 1) {
-    a.stats[0] = a.stats[2] = rc;
-    a.stats[1] = a.stats[3] = rd;
-    a.qscan[rc] = rd;
+  __syncthreads();
+  long long oc = 0, od = 0, tc = 0, td = 0;
+#pragma unroll
+  for (int k = 0; k < kScanChunk / kWave; ++k) {
+    if (k < wv) {
+      oc += s_c[k];
+      od += s_d[k];
+    }
+    tc += s_c[k];
+    td += s_d[k];
+  }
+  if (u < a.nunits) {
+    a.unit_cnt[u] = oc + ic - c;
+    a.unit_deg[u] = od + id - d;
+  }
+  const unsigned nblk = gridDim.x;
+  if (t == 0) {
+    // chunk totals: agent-scope (sc1, write-through) stores
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.part_cnt + blockIdx.x),
+                       static_cast<unsigned long long>(tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.part_deg + blockIdx.x),
+                       static_cast<unsigned long long>(td), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = (prev == nblk - 1) ? 1 : 0;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // Last workgroup: exclusive scan of the chunk totals (loop for > 1024 chunks).
+  long long carry_c = 0, carry_d = 0;
+  for (unsigned base = 0; base < nblk; base += kScanChunk) {
+    const unsigned i = base + t;
+    // agent-scope loads of the other workgroups' chunk totals (behind the acquire)
+    const long long pc = i < nblk ? static_cast<long long>(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(a.part_cnt + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0;
+    const long long pd = i < nblk ? static_cast<long long>(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(a.part_deg + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0;
+    const long long jc = wave_incl_scan(pc), jd = wave_incl_scan(pd);
+    __syncthreads();
+    if (lane == kWave - 1) {
+      s_c[wv] = jc;
+      s_d[wv] = jd;
+    }
+    __syncthreads();
+    long long qc = 0, qd = 0, sc = 0, sd = 0;
+#pragma unroll
+    for (int k = 0; k < kScanChunk / kWave; ++k) {
+      if (k < wv) {
+        qc += s_c[k];
+        qd += s_d[k];
+      }
+      sc += s_c[k];
+      sd += s_d[k];
+    }
+    if (i < nblk) {
+      a.part_cnt[i] = carry_c + qc + jc - pc;
+      a.part_deg[i] = carry_d + qd + jd - pd;
+    }
+    carry_c += sc;
+    carry_d += sd;
+  }
+  if (t == 0) {
+    a.stats[0] = a.stats[2] = carry_c;
+    a.stats[1] = a.stats[3] = carry_d;
+    a.qscan[carry_c] = carry_d;
+    *a.ticket = 0u;  // next launch is stream-ordered after this one
   }
 }
 
 // ---------------------------------------------------------------------------
-// Frontier compaction: one wave per segment; per non-zero word, a wave-wide
-// ballot gives each set bit its slot (mbcnt) and a wave prefix sum of degrees
-// gives its edge offset.  Writes the top-down work list and the per-block start
-// entries (blk_vstart) of the edge-balanced expansion.
-__global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
+// Frontier compaction: one wave per owned word, 16 waves per unit.  The unit's
+// base comes from the scan; the waves' offsets inside the unit from an LDS
+// scan of their (count, degree) totals; each set bit's slot from mbcnt and its
+// edge offset from a wave prefix sum of degrees.
+__global__ __launch_bounds__(kUnitThreads) void compact_kernel(CompactArgs a) {
+  __shared__ long long s_c[kUnitWords], s_d[kUnitWords];
   const int lane = lane_id();
-  const int64_t s = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
-  const int64_t nseg = (a.words + kSegWords - 1) / kSegWords;
-  if (s >= nseg) return;
-  const int64_t w = s * kSegWords + lane;
-  const word_t mine = (w < a.words) ? a.frontier[w] : 0ull;
-  long long pos = a.seg_cnt_off[s];
-  long long off = a.seg_deg_off[s];
-  unsigned long long nz = __ballot(mine != 0);
-  const eid_t* __restrict__ ro = a.g.row_off;
-  while (nz) {
-    const int j = __ffsll(static_cast<long long>(nz)) - 1;
-    nz &= nz - 1;
-    const word_t word = readlane64(mine, j);
-    const int64_t v = (s * kSegWords + j) * 64 + lane;
-    eid_t rs = 0, d = 0;
-    if ((word >> lane) & 1ull) {
-      rs = ro[v];
-      d = ro[v + 1] - rs;
-    }
-    const bool take = d > 0;
-    const unsigned long long tm = __ballot(take);
-    const long long incl = wave_incl_scan(d);
-    if (take) {
-      const long long p = pos + mask_rank(tm);
-      const long long qs = off + incl - d;
-      a.qscan[p] = qs;
-      a.qbase[p] = rs - qs;
-      for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
-           blk * kTdEdgesPerBlock < qs + d; ++blk)
-        a.blk_vstart[blk] = static_cast<int32_t>(p);
-    }
-    pos += __popcll(tm);
-    off += readlane_i64(incl, kWave - 1);
+  const int wv = threadIdx.x >> 6;
+  const int64_t unit = blockIdx.x;
+  const int64_t w = unit * kUnitWords + wv;
+  const word_t word = (w < a.words) ? a.frontier[w] : 0ull;
+  const int64_t v = w * 64 + lane;
+  eid_t rs = 0, d = 0;
+  if ((word >> lane) & 1ull) {
+    rs = a.g.row_off[v];
+    d = a.g.row_off[v + 1] - rs;
+  }
+  const bool take = d > 0;
+  const unsigned long long tm = __ballot(take);
+  const long long incl = wave_incl_scan(d);
+  if (lane == kWave - 1) {
+    s_c[wv] = __popcll(tm);
+    s_d[wv] = incl;
+  }
+  __syncthreads();
+  long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
+  long long off = a.unit_deg_off[unit] + a.part_deg[unit / kScanChunk];
+  for (int k = 0; k < wv; ++k) {
+    pos += s_c[k];
+    off += s_d[k];
+  }
+  if (take) {
+    const long long p = pos + mask_rank(tm);
+    const long long qs = off + incl - d;
+    a.qscan[p] = qs;
+    a.qbase[p] = rs - qs;
+    for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
+      a.blk_vstart[blk] = static_cast<int32_t>(p);
   }
 }
 
@@ -173,7 +250,9 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // [b*EPB, (b+1)*EPB).  The entries covering that range are [blk_vstart[b],
 // blk_vstart[b+1]]; their start positions are scattered into an LDS owner map
 // and max-scanned so every edge finds its entry with one LDS read.  col[] is
-// then read in 256-lane coalesced sweeps.
+// then read in 256-lane coalesced sweeps.  A discovered vertex costs one
+// atomicOr only if neither `visited` nor the (possibly stale, only-growing)
+// `next` word already has its bit.
 __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
@@ -227,67 +306,94 @@ __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
       const int i = s_owner[idx];
       const vid_t v = col[e0 + idx + s_base[i]];
       const word_t bit = 1ull << (v & 63);
-      if (!(visited[v >> 6] & bit)) atomicOr(a.next + (v >> 6), bit);
+      const word_t seen = visited[v >> 6] | a.next[v >> 6];
+      if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Bottom-up parent search: one wave per owned bitmap word (64 vertices).
+// Fused bottom-up step: one wave per owned bitmap word (64 vertices).
 // Phase 1: each unvisited lane checks its first `lane_limit` neighbours (loads
 // batched 4-wide for memory-level parallelism).  Phase 2: lanes still
 // unresolved are scanned by the whole wave, 64 neighbours per step, ballot
-// early exit.  The result word is assembled by a ballot: no atomics.
-__global__ __launch_bounds__(kBlock) void bu_kernel(BuArgs a) {
+// early exit.  The result word is assembled by a ballot (no atomics) and the
+// wave writes the new frontier word, the visited word, the new levels and the
+// unit statistics directly.
+__global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
   const int lane = lane_id();
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6);
+  long long cnt = 0, deg = 0;
+  if (w < a.words) {
+    const word_t vis = a.visited[w];
+    word_t res = 0;
+    if (vis != ~0ull) {
+      const int64_t v = w * 64 + lane;
+      const eid_t* __restrict__ ro = a.g.row_off;
+      const vid_t* __restrict__ col = a.g.col;
+      const word_t* __restrict__ fr = a.frontier;
+      eid_t rs = 0, e = 0;
+      if (!((vis >> lane) & 1ull)) {  // padding / zero-degree bits are pre-set in visited
+        rs = ro[v];
+        e = ro[v + 1];
+      }
+      eid_t p = rs;
+      bool found = false;
+      const eid_t lim = min(e, p + static_cast<eid_t>(a.lane_limit));
+      while (p < lim && !found) {
+        vid_t u[4];
+        bool ok[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ok[k] = p + k < lim;
+          u[k] = ok[k] ? col[p + k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) found |= ok[k] && test_bit(fr, u[k]);
+        p += 4;
+      }
+      if (p > lim) p = lim;
+      unsigned long long pending = __ballot(!found && p < e);
+      while (pending) {
+        const int l = __ffsll(static_cast<long long>(pending)) - 1;
+        pending &= pending - 1;
+        const long long ps = __shfl(static_cast<long long>(p), l, kWave);
+        const long long pe = __shfl(static_cast<long long>(e), l, kWave);
+        bool f = false;
+        for (long long base = ps; base < pe; base += kWave) {
+          const long long idx = base + lane;
+          bool hit = false;
+          if (idx < pe) hit = test_bit(fr, col[idx]);
+          if (__ballot(hit)) {
+            f = true;
+            break;
+          }
+        }
+        if (lane == l) found = f;
+      }
+      res = __ballot(found);
+      if (found) {
+        a.level[v] = a.new_level;
+        cnt = 1;
+        deg = e - rs;
+      }
+      if (lane == 0 && res) a.visited[w] = vis | res;
+    }
+    if (lane == 0) a.new_frontier[w] = res;
+  }
+  unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
+}
+
+// Zero-degree / padding mask of the owned slice (computed once per graph).
+__global__ __launch_bounds__(kBlock) void zero_degree_kernel(ZeroDegArgs a) {
+  const int lane = lane_id();
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
   if (w >= a.words) return;
-  const word_t vis = a.visited[w];
-  if (vis == ~0ull) {
-    if (lane == 0) a.cand[w] = 0;
-    return;
-  }
   const int64_t v = w * 64 + lane;
-  const eid_t* __restrict__ ro = a.g.row_off;
-  const vid_t* __restrict__ col = a.g.col;
-  const word_t* __restrict__ fr = a.frontier;
-  eid_t p = 0, e = 0;
-  if (v < a.g.rows && !((vis >> lane) & 1ull)) {
-    p = ro[v];
-    e = ro[v + 1];
-  }
-  bool found = false;
-  const eid_t lim = min(e, p + static_cast<eid_t>(a.lane_limit));
-  while (p < lim && !found) {
-    vid_t u[4];
-    bool ok[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      ok[k] = p + k < lim;
-      u[k] = ok[k] ? col[p + k] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) found |= ok[k] && test_bit(fr, u[k]);
-    p += 4;
-  }
-  if (p > lim) p = lim;
-  unsigned long long pending = __ballot(!found && p < e);
-  while (pending) {
-    const int l = __ffsll(static_cast<long long>(pending)) - 1;
-    pending &= pending - 1;
-    const long long ps = __shfl(static_cast<long long>(p), l, kWave);
-    const long long pe = __shfl(static_cast<long long>(e), l, kWave);
-    bool f = false;
-    for (long long base = ps; base < pe; base += kWave) {
-      const long long idx = base + lane;
-      bool hit = false;
-      if (idx < pe) hit = test_bit(fr, col[idx]);
-      if (__ballot(hit)) { f = true; break; }
-    }
-    if (lane == l) found = f;
-  }
-  const word_t res = __ballot(found);
-  if (lane == 0) a.cand[w] = res;
+  bool dead = true;
+  if (v < a.g.rows) dead = a.g.row_off[v + 1] == a.g.row_off[v];
+  const word_t m = __ballot(dead);
+  if (lane == 0) a.out[w] = m;
 }
 
 // ---------------------------------------------------------------------------
@@ -328,19 +434,18 @@ void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st) {
 void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 0, st>>>(bm, bit); }
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
-  const int64_t nseg = (a.words + kSegWords - 1) / kSegWords;
-  if (nseg == 0) return;
-  update_kernel<<<grid_for(nseg, kWavesPerBlock), kBlock, 0, st>>>(a);
+  if (a.words <= 0) return;
+  update_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
 }
 
-void scan_segments(const ScanArgs& a, hipStream_t st) {
-  scan_segments_kernel<<<1, kScanThreads, 0, st>>>(a);
+void scan_units(const ScanArgs& a, hipStream_t st) {
+  if (a.nunits <= 0) return;
+  scan_units_kernel<<<grid_for(a.nunits, kScanChunk), kScanChunk, 0, st>>>(a);
 }
 
 void compact_frontier(const CompactArgs& a, hipStream_t st) {
-  const int64_t nseg = (a.words + kSegWords - 1) / kSegWords;
-  if (nseg == 0) return;
-  compact_kernel<<<grid_for(nseg, kWavesPerBlock), kBlock, 0, st>>>(a);
+  if (a.words <= 0) return;
+  compact_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
 }
 
 void td_expand(const TdArgs& a, hipStream_t st) {
@@ -350,7 +455,12 @@ void td_expand(const TdArgs& a, hipStream_t st) {
 
 void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  bu_kernel<<<grid_for(a.words, kWavesPerBlock), kBlock, 0, st>>>(a);
+  bu_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+}
+
+void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st) {
+  if (a.words <= 0) return;
+  zero_degree_kernel<<<grid_for(a.words, kBlock / kWave), kBlock, 0, st>>>(a);
 }
 
 void status_expand(const StatusArgs& a, hipStream_t st) {

@@ -12,7 +12,8 @@ namespace kern {
 void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st);
 void set_bit(word_t* bm, int64_t bit, hipStream_t st);
 void update_frontier(const UpdateArgs& a, hipStream_t st);
-void scan_segments(const ScanArgs& a, hipStream_t st);
+void scan_units(const ScanArgs& a, hipStream_t st);
+void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);

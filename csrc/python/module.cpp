@@ -114,7 +114,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
 
   m.attr("UNREACHED") = py::int_(kUnreached);
   m.attr("TD_EDGES_PER_BLOCK") = py::int_(kTdEdgesPerBlock);
-  m.attr("SEG_VERTICES") = py::int_(kSegVertices);
+  m.attr("UNIT_VERTICES") = py::int_(kUnitVertices);
 
   // ---- graphs ----
   py::class_<HostCSR>(m, "HostCSR")
@@ -349,7 +349,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
              return std::make_shared<Engine>(*g, *c, o);
            }),
            py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 14.0, py::arg("beta") = 24.0,
-           py::arg("bu_lane_limit") = 8, py::arg("phase_timing") = false, py::keep_alive<1, 2>(),
+           py::arg("bu_lane_limit") = 32, py::arg("phase_timing") = false, py::keep_alive<1, 2>(),
            py::keep_alive<1, 3>())
       .def(
           "run",
