@@ -35,11 +35,14 @@ struct ShardView {
   int64_t n = 0, lo = 0, rows = 0, nnz = 0;
 };
 
-// Frontier bookkeeping is organised in "units" of 16 bitmap words (1024
-// vertices): one 1024-thread workgroup per unit, one wave64 per word, in the
-// HIP kernels.  Per-unit counts are scanned by a multi-block scan whose chunks
-// hold kScanChunk units.
-constexpr int kUnitWords = 16;
+// Frontier bookkeeping is organised in "units" of 64 bitmap words (4096
+// vertices): one 256-thread workgroup (4 waves) per unit, 16 consecutive words
+// per wave64, in the HIP kernels.  (One wave per word would launch 1M waves for
+// RMAT-26: dispatch alone then costs ~300 us per kernel on MI355X.)  Per-unit
+// counts are scanned by a multi-block scan whose chunks hold kScanChunk units.
+constexpr int kWaveWords = 16;
+constexpr int kUnitWaves = 4;
+constexpr int kUnitWords = kWaveWords * kUnitWaves;
 constexpr int kUnitVertices = kUnitWords * kWordBits;
 constexpr int kScanChunk = 1024;
 // Top-down expansion handles kTdEdgesPerBlock frontier edges per workgroup.

@@ -34,8 +34,8 @@ namespace {
 using namespace dev;
 
 constexpr int kBlock = 256;
-constexpr int kUnitThreads = kUnitWords * kWave;  // 1024: one wave per word
-static_assert(kUnitThreads == 1024, "unit = 16 waves");
+constexpr int kUnitThreads = kUnitWaves * kWave;  // 256: 4 waves x 16 words
+static_assert(kUnitThreads == 256 && kWaveWords <= kWave, "unit geometry");
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void fill_level_kernel(lvl_t* __restrict__ level, int64_t n, lvl_t value,
@@ -53,10 +53,10 @@ __global__ void set_bit_kernel(word_t* bm, int64_t bit) {
   if (threadIdx.x == 0) bm[bit >> 6] |= 1ull << (bit & 63);
 }
 
-// Sum (cnt, deg) of the 16 waves of a unit workgroup; thread 0 writes them.
+// Sum (cnt, deg) of the 4 waves of a unit workgroup; thread 0 writes them.
 __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
                                                  int64_t* unit_deg) {
-  __shared__ long long s_c[kUnitWords], s_d[kUnitWords];
+  __shared__ long long s_c[kUnitWaves], s_d[kUnitWaves];
   cnt = wave_sum(cnt);
   deg = wave_sum(deg);
   const int wv = threadIdx.x >> 6;
@@ -68,7 +68,7 @@ __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, i
   if (threadIdx.x == 0) {
     long long c = 0, d = 0;
 #pragma unroll
-    for (int k = 0; k < kUnitWords; ++k) {
+    for (int k = 0; k < kUnitWaves; ++k) {
       c += s_c[k];
       d += s_d[k];
     }
@@ -78,29 +78,38 @@ __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, i
 }
 
 // ---------------------------------------------------------------------------
-// Frontier update: one wave per owned word; lane l handles vertex w*64+l so the
-// level stores and row_off loads of a word are one coalesced access each.
+// Frontier update: a wave owns 16 consecutive words.  Lanes 0..15 update the
+// bitmap words (one coalesced 128-B access per array); then, for every
+// non-zero new word, the wave switches to lane-per-vertex so the level stores
+// and row_off loads of that word are one coalesced access each.
 __global__ __launch_bounds__(kUnitThreads) void update_kernel(UpdateArgs a) {
   const int lane = lane_id();
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6);
-  long long cnt = 0, deg = 0;
-  if (w < a.words) {
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
+  const int64_t wl = w0 + lane;
+  word_t nb = 0;
+  if (lane < kWaveWords && wl < a.words) {
     word_t c = 0;
-    for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
-    const word_t vis = a.visited[w];
-    const word_t nb = a.force ? c : (c & ~vis);
-    if (lane == 0) {
-      if (nb) a.visited[w] = vis | nb;
-      a.frontier[w] = nb;
-      if (a.clear_cand && c) a.cand[w] = 0;
-    }
-    if ((nb >> lane) & 1ull) {
-      const int64_t v = w * 64 + lane;
+    for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
+    const word_t vis = a.visited[wl];
+    nb = a.force ? c : (c & ~vis);
+    if (nb) a.visited[wl] = vis | nb;
+    a.frontier[wl] = nb;
+    if (a.clear_cand && c) a.cand[wl] = 0;
+  }
+  long long cnt = 0, deg = 0;
+  unsigned long long nz = __ballot(nb != 0);
+  const eid_t* __restrict__ ro = a.g.row_off;
+  while (nz) {
+    const int j = __ffsll(static_cast<long long>(nz)) - 1;
+    nz &= nz - 1;
+    const word_t word = readlane64(nb, j);
+    if ((word >> lane) & 1ull) {
+      const int64_t v = (w0 + j) * 64 + lane;
       a.level[v] = a.new_level;
-      const eid_t d = a.g.row_off[v + 1] - a.g.row_off[v];
+      const eid_t d = ro[v + 1] - ro[v];
       if (d > 0) {
-        cnt = 1;
-        deg = d;
+        cnt += 1;
+        deg += d;
       }
     }
   }
@@ -209,24 +218,33 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
 // scan of their (count, degree) totals; each set bit's slot from mbcnt and its
 // edge offset from a wave prefix sum of degrees.
 __global__ __launch_bounds__(kUnitThreads) void compact_kernel(CompactArgs a) {
-  __shared__ long long s_c[kUnitWords], s_d[kUnitWords];
+  __shared__ long long s_c[kUnitWaves], s_d[kUnitWaves];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   const int64_t unit = blockIdx.x;
-  const int64_t w = unit * kUnitWords + wv;
-  const word_t word = (w < a.words) ? a.frontier[w] : 0ull;
-  const int64_t v = w * 64 + lane;
-  eid_t rs = 0, d = 0;
-  if ((word >> lane) & 1ull) {
-    rs = a.g.row_off[v];
-    d = a.g.row_off[v + 1] - rs;
+  const int64_t w0 = unit * kUnitWords + wv * kWaveWords;
+  const word_t mine = (lane < kWaveWords && w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
+  const unsigned long long nzw = __ballot(mine != 0);
+  const eid_t* __restrict__ ro = a.g.row_off;
+  // Pass 1: this wave's (count, degree) totals, for the unit-internal offsets.
+  long long c1 = 0, d1 = 0;
+  for (unsigned long long nz = nzw; nz; nz &= nz - 1) {
+    const int j = __ffsll(static_cast<long long>(nz)) - 1;
+    const word_t word = readlane64(mine, j);
+    if ((word >> lane) & 1ull) {
+      const int64_t v = (w0 + j) * 64 + lane;
+      const eid_t d = ro[v + 1] - ro[v];
+      if (d > 0) {
+        c1 += 1;
+        d1 += d;
+      }
+    }
   }
-  const bool take = d > 0;
-  const unsigned long long tm = __ballot(take);
-  const long long incl = wave_incl_scan(d);
-  if (lane == kWave - 1) {
-    s_c[wv] = __popcll(tm);
-    s_d[wv] = incl;
+  c1 = wave_sum(c1);
+  d1 = wave_sum(d1);
+  if (lane == 0) {
+    s_c[wv] = c1;
+    s_d[wv] = d1;
   }
   __syncthreads();
   long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
@@ -235,13 +253,29 @@ __global__ __launch_bounds__(kUnitThreads) void compact_kernel(CompactArgs a) {
     pos += s_c[k];
     off += s_d[k];
   }
-  if (take) {
-    const long long p = pos + mask_rank(tm);
-    const long long qs = off + incl - d;
-    a.qscan[p] = qs;
-    a.qbase[p] = rs - qs;
-    for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
-      a.blk_vstart[blk] = static_cast<int32_t>(p);
+  // Pass 2 (row_off now L2-warm): slots by mbcnt, edge offsets by wave prefix sums.
+  for (unsigned long long nz = nzw; nz; nz &= nz - 1) {
+    const int j = __ffsll(static_cast<long long>(nz)) - 1;
+    const word_t word = readlane64(mine, j);
+    const int64_t v = (w0 + j) * 64 + lane;
+    eid_t rs = 0, d = 0;
+    if ((word >> lane) & 1ull) {
+      rs = ro[v];
+      d = ro[v + 1] - rs;
+    }
+    const bool take = d > 0;
+    const unsigned long long tm = __ballot(take);
+    const long long incl = wave_incl_scan(d);
+    if (take) {
+      const long long p = pos + mask_rank(tm);
+      const long long qs = off + incl - d;
+      a.qscan[p] = qs;
+      a.qbase[p] = rs - qs;
+      for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
+        a.blk_vstart[blk] = static_cast<int32_t>(p);
+    }
+    pos += __popcll(tm);
+    off += readlane_i64(incl, kWave - 1);
   }
 }
 
@@ -313,19 +347,23 @@ __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused bottom-up step: one wave per owned bitmap word (64 vertices).
-// Phase 1: each unvisited lane checks its first `lane_limit` neighbours (loads
-// batched 4-wide for memory-level parallelism).  Phase 2: lanes still
-// unresolved are scanned by the whole wave, 64 neighbours per step, ballot
-// early exit.  The result word is assembled by a ballot (no atomics) and the
-// wave writes the new frontier word, the visited word, the new levels and the
-// unit statistics directly.
+// Fused bottom-up step: a wave owns 16 consecutive bitmap words and walks them
+// one word (64 vertices, one per lane) at a time; fully visited words cost one
+// uniform branch.  Phase 1: each unvisited lane checks its first `lane_limit`
+// neighbours (loads batched 4-wide for memory-level parallelism).  Phase 2:
+// lanes still unresolved are scanned by the whole wave, 64 neighbours per
+// step, ballot early exit.  The result word is assembled by a ballot (no
+// atomics) and the wave writes the new frontier word, the visited word, the new
+// levels and the unit statistics directly.
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
   const int lane = lane_id();
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6);
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
+  const word_t vis_l = (lane < kWaveWords && w0 + lane < a.words) ? a.visited[w0 + lane] : ~0ull;
   long long cnt = 0, deg = 0;
-  if (w < a.words) {
-    const word_t vis = a.visited[w];
+  for (int j = 0; j < kWaveWords; ++j) {
+    const int64_t w = w0 + j;
+    if (w >= a.words) break;
+    const word_t vis = readlane64(vis_l, j);
     word_t res = 0;
     if (vis != ~0ull) {
       const int64_t v = w * 64 + lane;
@@ -374,8 +412,8 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
       res = __ballot(found);
       if (found) {
         a.level[v] = a.new_level;
-        cnt = 1;
-        deg = e - rs;
+        cnt += 1;
+        deg += e - rs;
       }
       if (lane == 0 && res) a.visited[w] = vis | res;
     }
