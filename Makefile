@@ -24,7 +24,8 @@ LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -lpthread
 HOST_SRC  := csrc/graph/io.cpp csrc/graph/csr.cpp csrc/backend/cpu_backend.cpp \
              csrc/backend/hip_backend.cpp csrc/comm/comm.cpp csrc/comm/nccl_comm.cpp \
              csrc/comm/tcp_bootstrap.cpp csrc/engine/engine.cpp
-HIP_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/graph_kernels.hip csrc/kernels/ref_kernels.hip
+HIP_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/graph_kernels.hip csrc/kernels/ref_kernels.hip \
+             csrc/kernels/graph_sort.hip
 
 HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC))
 HIP_OBJ   := $(patsubst csrc/%.hip,$(BUILD)/%.o,$(HIP_SRC))

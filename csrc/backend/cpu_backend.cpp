@@ -250,6 +250,24 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void degrees_u32(const eid_t* ro, int64_t rows, uint32_t* out) override {
+    for (int64_t r = 0; r < rows; ++r) {
+      const eid_t d = ro[r + 1] - ro[r];
+      out[r] = d > 0xFFFFFFFFll ? 0xFFFFFFFFu : static_cast<uint32_t>(d);
+    }
+  }
+
+  void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {
+    // Same policy as the device: rows of 2..4096 entries, (degree desc, id asc).
+    for (int64_t r = 0; r < rows; ++r) {
+      const eid_t len = ro[r + 1] - ro[r];
+      if (len < 2 || len > 4096) continue;
+      std::sort(col + ro[r], col + ro[r + 1], [&](vid_t x, vid_t y) {
+        return key_deg[x] != key_deg[y] ? key_deg[x] > key_deg[y] : x < y;
+      });
+    }
+  }
+
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     for (int64_t i = 0; i < p.m; ++i) {
       uint64_t u, v;

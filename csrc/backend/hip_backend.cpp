@@ -123,6 +123,23 @@ class HipBackend final : public Backend {
   void ref_accept(const RefAcceptArgs& a) override { on(); kern::ref_accept(a, st_); chk(); }
   void validate_levels(const ValidateArgs& a) override { on(); kern::validate_levels(a, st_); chk(); }
   void compute_parents(const ParentArgs& a) override { on(); kern::compute_parents(a, st_); chk(); }
+  void degrees_u32(const eid_t* ro, int64_t rows, uint32_t* out) override {
+    on();
+    kern::degrees_u32(ro, rows, out, st_);
+    chk();
+  }
+  void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {
+    on();
+    int64_t* list = nullptr;
+    unsigned long long* count = nullptr;
+    HIP_CHECK(hipMalloc(&list, static_cast<size_t>(std::max<int64_t>(rows, 1)) * sizeof(int64_t)));
+    HIP_CHECK(hipMalloc(&count, sizeof(unsigned long long)));
+    kern::sort_neighbors(ro, col, rows, key_deg, list, count, st_);
+    chk();
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipFree(list));
+    HIP_CHECK(hipFree(count));
+  }
 
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     on();

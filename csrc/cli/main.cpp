@@ -56,6 +56,7 @@ struct Args {
   bool json = false;
   bool quiet = false;
   bool phase_timing = false;
+  bool hub_sort = true;
 };
 
 [[noreturn]] void usage(const char* msg = nullptr) {
@@ -108,6 +109,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--json") a.json = true;
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--phase-timing") a.phase_timing = true;
+    else if (s == "--no-hub-sort") a.hub_sort = false;
     else if (s == "-h" || s == "--help") usage();
     else if (!s.empty() && s[0] == '-' && s.size() > 1 && !std::isdigit(static_cast<unsigned char>(s[1])))
       usage(("unknown flag " + s).c_str());
@@ -299,6 +301,7 @@ int main(int argc, char** argv) {
       const int rk = multiproc ? wrank : i;
       if (synth) rc.graph = DeviceGraph::generate(*rc.be, gp, part, rk);
       else rc.graph = DeviceGraph::from_host(*rc.be, full, part, rk);
+      if (a.hub_sort) rc.graph->sort_neighbors_by_degree(*rc.comm);
       rc.engine = std::make_unique<Engine>(*rc.graph, *rc.comm, eo);
     });
 

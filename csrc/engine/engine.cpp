@@ -137,6 +137,20 @@ std::vector<eid_t> DeviceGraph::degrees_of(const std::vector<int64_t>& local_row
   return out;
 }
 
+void DeviceGraph::sort_neighbors_by_degree(Comm& comm) {
+  DBFS_CHECK(comm.size() == part_.nranks && comm.rank() == rank_, "communicator does not match the shard");
+  comm.bind_backend(be_);
+  const int P = part_.nranks;
+  const int64_t part = part_.part;
+  DBuf<uint32_t> mine(*be_, static_cast<size_t>(part)), all(*be_, static_cast<size_t>(P * part));
+  be_->memset_async(mine.data(), 0, mine.bytes());
+  be_->degrees_u32(row_off_.data(), rows_, mine.data());
+  comm.allgather(mine.data(), all.data(), static_cast<size_t>(part) * sizeof(uint32_t));
+  be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
+  be_->synchronize();
+  hub_sorted_ = true;
+}
+
 // ---- Engine ----------------------------------------------------------------------
 
 Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)

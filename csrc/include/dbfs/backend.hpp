@@ -239,6 +239,11 @@ class Backend {
   virtual void validate_levels(const ValidateArgs& a) = 0;
   virtual void compute_parents(const ParentArgs& a) = 0;
 
+  // Hub-first adjacency: out[r] = degree of local row r (saturated to uint32);
+  // then sort every row by (key_deg[neighbour] descending, neighbour ascending).
+  virtual void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out) = 0;
+  virtual void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg) = 0;
+
   // graph construction on the device
   // deg[r] += number of edge endpoints owned in rows [lo, lo + rows) (deg zeroed by caller)
   virtual void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) = 0;

@@ -48,12 +48,17 @@ class DeviceGraph {
   int64_t nnz() const { return nnz_; }
   int64_t input_edges() const { return input_edges_; }
   std::vector<eid_t> degrees_of(const std::vector<int64_t>& local_rows) const;
+  // Reorder every row hub-first (neighbour degree descending); collective over
+  // `comm` (all ranks need every vertex's degree).  One-time preprocessing.
+  void sort_neighbors_by_degree(Comm& comm);
+  bool hub_sorted() const { return hub_sorted_; }
 
  private:
   Backend* be_ = nullptr;
   Partition part_;
   int rank_ = 0;
   int64_t lo_ = 0, rows_ = 0, nnz_ = 0, input_edges_ = 0;
+  bool hub_sorted_ = false;
   DBuf<eid_t> row_off_;
   DBuf<vid_t> col_;
 };

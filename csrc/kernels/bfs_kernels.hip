@@ -382,31 +382,23 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
       e = ro[v + 1];
     }
   };
-  auto fetch_cols = [&](eid_t rs, eid_t e, vid_t (&u)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) u[k] = (rs + k < e) ? col[rs + k] : 0u;
-  };
   eid_t n_rs, n_e;
-  vid_t n_u[4];
   fetch_rows(0, n_rs, n_e);
-  fetch_cols(n_rs, n_e, n_u);
+  vid_t n_u = n_rs < n_e ? col[n_rs] : 0u;
 
   for (int j = 0; j < nw; ++j) {
     const int64_t w = w0 + j;
     const word_t vis = readlane64(vis_l, j);
     const eid_t rs = n_rs, e = n_e;
-    vid_t u0[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) u0[k] = n_u[k];
-    fetch_rows(j + 1, n_rs, n_e);  // in flight during this word's bit tests
-    bool found = false;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) found |= (rs + k < e) && test_bit(fr, u0[k]);
-    fetch_cols(n_rs, n_e, n_u);    // in flight during this word's tail
+    const vid_t u0 = n_u;
+    fetch_rows(j + 1, n_rs, n_e);  // in flight during this word's bit test
+    // First probe: the row's first (highest-degree, hub-first order) neighbour.
+    bool found = (rs < e) && test_bit(fr, u0);
+    n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
     word_t res = 0;
     if (vis != ~0ull) {
       const int64_t v = w * 64 + lane;
-      eid_t p = min(e, rs + 4);
+      eid_t p = min(e, rs + 1);
       const eid_t lim = min(e, rs + static_cast<eid_t>(a.lane_limit));
       while (p < lim && !found) {
         vid_t u[4];

@@ -32,6 +32,12 @@ int64_t scan_tmp_elems(int64_t n);
 void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st);
 void validate_levels(const ValidateArgs& a, hipStream_t st);
 void compute_parents(const ParentArgs& a, hipStream_t st);
+
+// graph_sort.hip
+void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st);
+// list must hold `rows` entries; count is one device counter
+void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
+                    unsigned long long* count, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
 
 }  // namespace kern

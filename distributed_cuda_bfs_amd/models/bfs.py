@@ -38,7 +38,11 @@ class BFS:
     """Distributed BFS over a graph given as a HostCSR, generator params, or a file path."""
 
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
-                 alpha: float = 14.0, beta: float = 24.0, bu_lane_limit: int = 32, phase_timing: bool = False):
+                 alpha: float = 14.0, beta: float = 24.0, bu_lane_limit: int = 32, phase_timing: bool = False,
+                 hub_sort: bool = True):
+        """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
+        once, before any traversal: levels are unchanged, bottom-up probes find a
+        frontier parent sooner (see csrc/kernels/graph_sort.hip)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.rt = runtime or init_runtime()
@@ -54,6 +58,8 @@ class BFS:
             self.graph = N.DeviceGraph.from_host(self.rt.backend, graph, self.partition, self.rt.rank)
         else:
             raise TypeError("graph must be a path, HostCSR or GenParams")
+        if hub_sort:
+            self.graph.sort_neighbors_by_degree(self.rt.comm)
         self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
                                bu_lane_limit=bu_lane_limit, phase_timing=phase_timing)
 

@@ -158,3 +158,23 @@ def test_parent_tree_virtual_ranks():
 
     for lv, par in run_virtual_ranks(3, body, device="cpu"):
         assert parents_are_valid(csr, lv, par, 1)
+
+
+def test_hub_sort_orders_rows_and_keeps_levels(rt):
+    p = dbfs.rmat_params(11, 16, 12)
+    csr = dbfs.host_csr_from_params(p)
+    exp = _oracle(csr, 4)
+    bfs = dbfs.BFS(p, rt, mode="do", hub_sort=True)
+    assert bfs.graph.hub_sorted
+    g = bfs.graph.to_host()
+    ro, col = np.asarray(g.row_off), np.asarray(g.col)
+    deg = np.diff(np.asarray(csr.row_off))
+    for r in range(0, g.rows, 37):
+        row = col[ro[r]:ro[r + 1]]
+        if 2 <= len(row) <= 4096:
+            keys = list(zip(-deg[row], row))
+            assert keys == sorted(keys)
+        # same multiset as the unsorted CSR
+        assert sorted(row.tolist()) == sorted(np.asarray(csr.col)[ro[r]:ro[r + 1]].tolist())
+    bfs.run(4)
+    assert np.array_equal(bfs.levels(), exp)

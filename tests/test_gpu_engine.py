@@ -130,3 +130,19 @@ def test_cli_gpu_reference_stdout(data_dir):
     assert out.returncode == 0, out.stderr
     assert "Enabling peer access between GPU0 and GPU1..." in out.stdout
     assert out.stdout.endswith("Output OK!\n\n")
+
+
+def test_hub_sort_gpu_matches_cpu(gpu_runtime):
+    from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
+
+    p = dbfs.rmat_params(15, 16, 12)
+    gpu = dbfs.BFS(p, gpu_runtime, hub_sort=True)
+    cpu = dbfs.BFS(p, init_runtime("cpu"), hub_sort=True)
+    g, c = gpu.graph.to_host(), cpu.graph.to_host()
+    assert np.array_equal(np.asarray(g.row_off), np.asarray(c.row_off))
+    ro = np.asarray(g.row_off)
+    gc, cc = np.asarray(g.col), np.asarray(c.col)
+    for r in range(g.rows):
+        n = ro[r + 1] - ro[r]
+        if 2 <= n <= 4096:
+            assert np.array_equal(gc[ro[r]:ro[r + 1]], cc[ro[r]:ro[r + 1]]), r
