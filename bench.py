@@ -46,9 +46,9 @@ def main() -> int:
     ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--root-seed", type=int, default=12345)
-    ap.add_argument("--alpha", type=float, default=14.0)
+    ap.add_argument("--alpha", type=float, default=24.0)
     ap.add_argument("--beta", type=float, default=24.0)
-    ap.add_argument("--bu-lane-limit", type=int, default=32)
+    ap.add_argument("--bu-lane-limit", type=int, default=8)
     ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--baseline-gteps", type=float, default=None)

@@ -65,9 +65,12 @@ class DeviceGraph {
 
 struct EngineOptions {
   Mode mode = Mode::DirOpt;
-  double alpha = 14.0;  // TD -> BU when m_f > m_u / alpha
+  // Beamer's direction switch.  Defaults tuned on MI355X / RMAT-26 (sweep in
+  // profiles/): BU is cheap enough here that switching earlier than Beamer's
+  // CPU value (14) pays.
+  double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
-  int bu_lane_limit = 32;
+  int bu_lane_limit = 8;
   bool phase_timing = false;  // per-level device timing (adds events)
 };
 

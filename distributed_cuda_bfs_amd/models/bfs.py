@@ -38,7 +38,7 @@ class BFS:
     """Distributed BFS over a graph given as a HostCSR, generator params, or a file path."""
 
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
-                 alpha: float = 14.0, beta: float = 24.0, bu_lane_limit: int = 32, phase_timing: bool = False,
+                 alpha: float = 24.0, beta: float = 24.0, bu_lane_limit: int = 8, phase_timing: bool = False,
                  hub_sort: bool = True):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
