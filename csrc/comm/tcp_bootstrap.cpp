@@ -158,3 +158,74 @@ std::vector<std::string> TcpBootstrap::allgather(const std::string& data) {
 void TcpBootstrap::barrier() { allgather(std::string()); }
 
 }  // namespace dbfs
+
+// ---- TcpComm --------------------------------------------------------------------
+
+namespace dbfs {
+
+TcpComm::TcpComm(std::shared_ptr<TcpBootstrap> boot, Backend& be) : boot_(std::move(boot)) { bind_backend(&be); }
+int TcpComm::rank() const { return boot_->rank(); }
+int TcpComm::size() const { return boot_->size(); }
+
+std::string TcpComm::fetch(const void* p, size_t bytes) {
+  std::string s(bytes, '\0');
+  if (bytes) be_->to_host(&s[0], p, bytes);
+  return s;
+}
+
+void TcpComm::store(void* p, const std::string& s, size_t off, size_t bytes) {
+  if (bytes) be_->to_device(p, s.data() + off, bytes);
+}
+
+void TcpComm::alltoall(const void* send, void* recv, size_t bytes) {
+  const int P = size(), me = rank();
+  auto all = boot_->allgather(fetch(send, bytes * P));
+  for (int r = 0; r < P; ++r) store(static_cast<char*>(recv) + r * bytes, all[r], me * bytes, bytes);
+}
+
+void TcpComm::allgather(const void* send, void* recv, size_t bytes) {
+  auto all = boot_->allgather(fetch(send, bytes));
+  for (int r = 0; r < size(); ++r) store(static_cast<char*>(recv) + r * bytes, all[r], 0, bytes);
+}
+
+void TcpComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  auto all = boot_->allgather(fetch(buf, count * sizeof(int64_t)));
+  std::vector<int64_t> acc(count, 0);
+  for (const auto& s : all)
+    for (size_t i = 0; i < count; ++i) {
+      int64_t x;
+      std::memcpy(&x, s.data() + i * sizeof(int64_t), sizeof(x));
+      acc[i] += x;
+    }
+  be_->to_device(buf, acc.data(), count * sizeof(int64_t));
+}
+
+void TcpComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                        const int64_t* rd, size_t eb) {
+  const int P = size(), me = rank();
+  // message: P (offset, count) pairs, then the concatenated pieces
+  std::string msg(static_cast<size_t>(P) * 2 * sizeof(int64_t), '\0');
+  int64_t off = 0;
+  std::string data;
+  for (int r = 0; r < P; ++r) {
+    const int64_t hdr[2] = {off, sc[r]};
+    std::memcpy(&msg[static_cast<size_t>(r) * 2 * sizeof(int64_t)], hdr, sizeof(hdr));
+    data += fetch(static_cast<const char*>(send) + sd[r] * eb, static_cast<size_t>(sc[r]) * eb);
+    off += sc[r];
+  }
+  auto all = boot_->allgather(msg + data);
+  for (int r = 0; r < P; ++r) {
+    int64_t hdr[2];
+    std::memcpy(hdr, all[r].data() + static_cast<size_t>(me) * 2 * sizeof(int64_t), sizeof(hdr));
+    DBFS_CHECK(hdr[1] == rc[r], "TcpComm alltoallv count mismatch");
+    const size_t base = static_cast<size_t>(P) * 2 * sizeof(int64_t) + static_cast<size_t>(hdr[0]) * eb;
+    store(static_cast<char*>(recv) + rd[r] * eb, all[r], base, static_cast<size_t>(hdr[1]) * eb);
+  }
+}
+
+void TcpComm::barrier() {
+  be_->synchronize();
+  boot_->barrier();
+}
+
+}  // namespace dbfs

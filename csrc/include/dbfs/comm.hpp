@@ -147,6 +147,30 @@ class NcclComm final : public Comm {
 
 // Minimal TCP bootstrap (rank 0 hosts) used to ship the RCCL unique id and for
 // host barriers when no MPI / torch store is wanted.  Single- or multi-node.
+class TcpBootstrap;
+
+// Host collectives over the TCP bootstrap (star through rank 0).  Device
+// buffers are staged through host memory, so it works with any backend: used
+// for multi-process CPU runs and as a debug fallback transport (DBFS_COMM=tcp).
+class TcpComm final : public Comm {
+ public:
+  TcpComm(std::shared_ptr<TcpBootstrap> boot, Backend& be);
+  int rank() const override;
+  int size() const override;
+  std::string name() const override { return "tcp"; }
+  void alltoall(const void* send, void* recv, size_t bytes) override;
+  void allgather(const void* send, void* recv, size_t bytes) override;
+  void allreduce_sum_i64(int64_t* buf, size_t count) override;
+  void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv,
+                 const int64_t* rc, const int64_t* rd, size_t eb) override;
+  void barrier() override;
+
+ private:
+  std::string fetch(const void* p, size_t bytes);
+  void store(void* p, const std::string& s, size_t off, size_t bytes);
+  std::shared_ptr<TcpBootstrap> boot_;
+};
+
 class TcpBootstrap {
  public:
   TcpBootstrap(const std::string& host, int port, int rank, int nranks, double timeout_s = 300.0);

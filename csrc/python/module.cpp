@@ -255,6 +255,12 @@ PYBIND11_MODULE(_dbfs_native, m) {
         return std::shared_ptr<Comm>(new VirtualComm(g, rank, *be));
       },
       py::keep_alive<0, 3>());
+  m.def(
+      "tcp_comm",
+      [](std::shared_ptr<TcpBootstrap> boot, std::shared_ptr<Backend> be) {
+        return std::shared_ptr<Comm>(new TcpComm(boot, *be));
+      },
+      py::keep_alive<0, 2>());
   m.def("nccl_unique_id", []() { return py::bytes(NcclComm::unique_id()); });
   m.def(
       "nccl_comm",

@@ -38,6 +38,15 @@ def _env_int(k: str, d: int) -> int:
     return int(v) if v not in (None, "") else d
 
 
+def _torch_dist_ready() -> bool:
+    """True only if torch is already imported AND a process group exists (this
+    module never imports torch itself: GPU processes keep a single HIP runtime)."""
+    import sys
+
+    dist = sys.modules.get("torch.distributed")
+    return bool(dist is not None and dist.is_available() and dist.is_initialized())
+
+
 def make_backend(device: str = "auto", local_rank: int = 0):
     if device == "auto":
         device = "hip" if N.hip_device_count() > 0 else "cpu"
@@ -55,18 +64,22 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
     local_rank = _env_int("LOCAL_RANK", rank if world > 1 else 0)
     backend = make_backend(device, local_rank)
     if comm is None:
+        kind = os.environ.get("DBFS_COMM", "")
         if world == 1:
             comm = N.local_comm(backend)
-        elif backend.is_gpu:
+        elif kind == "torch" or (not kind and not backend.is_gpu and _torch_dist_ready()):
+            from .torch_comm import TorchComm
+            comm = TorchComm()
+        else:
             addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
             port = _env_int("DBFS_BOOTSTRAP_PORT", _env_int("MASTER_PORT", 29500) + 1)
             boot = N.TcpBootstrap(addr, port, rank, world)
-            uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
-            comm = N.nccl_comm(uid, rank, world, backend)
-            del boot
-        else:
-            from .torch_comm import TorchComm
-            comm = TorchComm()
+            if kind == "tcp" or (not kind and not backend.is_gpu):
+                comm = N.tcp_comm(boot, backend)  # host collectives (CPU runs / debug fallback)
+            else:
+                uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
+                comm = N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
+                del boot
     comm.bind_backend(backend)
     return Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)
 

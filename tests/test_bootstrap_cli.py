@@ -115,3 +115,22 @@ def test_bench_contract_cpu():
     assert rec["value"] > 0 and rec["validated"] is True
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in rec["config"]
+
+
+@pytest.mark.parametrize("nproc,mode", [(2, "do"), (3, "ref")])
+def test_bench_torchrun_multiprocess_cpu(nproc, mode):
+    """The driver's N>1 launch (torch.distributed.run, one process per rank,
+    127.0.0.1 rendezvous) on the CPU backend: bootstrap + TCP collectives +
+    rank-0-only JSON line."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", str(nproc), "--device", "cpu", "--scale", "10", "--steps", "2", "--warmup", "1",
+           "--mode", mode]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == nproc and rec["validated"] is True
+    assert rec["config"]["parallelism"] == f"1d-vertex-partition x{nproc}"
