@@ -174,7 +174,7 @@ void Engine::alloc_bitmap_state() {
   frontier_[0] = DBuf<word_t>(be_, static_cast<size_t>(GW));
   frontier_[1] = DBuf<word_t>(be_, static_cast<size_t>(GW));
   next_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
-  if (P > 1) recv_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
+  if (exchange()) recv_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
   cand_ = DBuf<word_t>(be_, static_cast<size_t>(W));
   nunits_ = div_up(W, kUnitWords);
   unit_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(nunits_ + 1));
@@ -194,7 +194,7 @@ void Engine::alloc_bitmap_state() {
   za.out = zdeg_.data() + comm_.rank() * W;
   za.words = W;
   be_.zero_degree_mask(za);
-  if (P > 1) comm_.allgather(za.out, zdeg_.data(), static_cast<size_t>(W) * sizeof(word_t));
+  if (exchange()) comm_.allgather(za.out, zdeg_.data(), static_cast<size_t>(W) * sizeof(word_t));
   be_.synchronize();
   bitmap_ready_ = true;
 }
@@ -275,7 +275,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     sa.qscan = qscan_.data();
     be_.scan_units(sa);
     cur ^= 1;
-    if (P > 1) {
+    if (exchange()) {
       comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
       be_.bitmap_or(visited_.data(), fr_cur(), GW);
     }
@@ -363,7 +363,7 @@ RunResult Engine::run_bitmap(int64_t source) {
         sa.next = next_.data();
         be_.status_expand(sa);
       }
-      if (P > 1) {
+      if (exchange()) {
         comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
         be_.memset_async(next_.data(), 0, next_.bytes());
         update(recv_.data(), P, false, false, L + 1);
@@ -456,7 +456,7 @@ RunResult Engine::run_ref(int64_t source) {
     ea.bucket_cap = cap;
     be_.ref_expand(ea);
     be_.to_host(hcnt.data(), bucket_cnt_.data(), static_cast<size_t>(P) * sizeof(int64_t));
-    if (P == 1) {
+    if (!exchange()) {
       be_.copy_async(queue_.data(), buckets_.data(), static_cast<size_t>(hcnt[0]) * sizeof(vid_t));
       q = hcnt[0];
     } else {
@@ -487,7 +487,7 @@ RunResult Engine::run_ref(int64_t source) {
     rec.level = L;
     rec.direction = 'R';
     rec.frontier = total_q;
-    total_q = (P == 1) ? q : comm_.sum_host(q);
+    total_q = exchange() ? comm_.sum_host(q) : q;
     rec.discovered = total_q;
     if (opt_.phase_timing) {
       const int ev1 = be_.record_event();

@@ -72,6 +72,10 @@ struct EngineOptions {
   double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
   int bu_lane_limit = 8;
   bool phase_timing = false;  // per-level device timing (adds events)
+  // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
+  // with one rank: lets a 1-rank RCCL communicator exercise every collective
+  // call on a single GPU (tests).
+  bool force_exchange = false;
 };
 
 struct LevelRecord {
@@ -119,6 +123,7 @@ class Engine {
   void alloc_bitmap_state();
   void alloc_ref_state();
   void gather_levels_device(DBuf<lvl_t>& full);
+  bool exchange() const { return part_.nranks > 1 || opt_.force_exchange; }
 
   DeviceGraph& g_;
   Comm& comm_;

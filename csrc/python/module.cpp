@@ -347,18 +347,20 @@ PYBIND11_MODULE(_dbfs_native, m) {
 
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](std::shared_ptr<DeviceGraph> g, std::shared_ptr<Comm> c, const std::string& mode, double alpha,
-                       double beta, int bu_lane_limit, bool phase_timing) {
+                       double beta, int bu_lane_limit, bool phase_timing, bool force_exchange) {
              EngineOptions o;
              o.mode = parse_mode(mode);
              o.alpha = alpha;
              o.beta = beta;
              o.bu_lane_limit = bu_lane_limit;
              o.phase_timing = phase_timing;
+             o.force_exchange = force_exchange;
              py::gil_scoped_release rel;
              return std::make_shared<Engine>(*g, *c, o);
            }),
            py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 24.0, py::arg("beta") = 24.0,
-           py::arg("bu_lane_limit") = 8, py::arg("phase_timing") = false, py::keep_alive<1, 2>(),
+           py::arg("bu_lane_limit") = 8, py::arg("phase_timing") = false, py::arg("force_exchange") = false,
+           py::keep_alive<1, 2>(),
            py::keep_alive<1, 3>())
       .def(
           "run",

@@ -39,7 +39,7 @@ class BFS:
 
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
                  alpha: float = 24.0, beta: float = 24.0, bu_lane_limit: int = 8, phase_timing: bool = False,
-                 hub_sort: bool = True):
+                 hub_sort: bool = True, force_exchange: bool = False):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
         frontier parent sooner (see csrc/kernels/graph_sort.hip)."""
@@ -61,7 +61,8 @@ class BFS:
         if hub_sort:
             self.graph.sort_neighbors_by_degree(self.rt.comm)
         self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
-                               bu_lane_limit=bu_lane_limit, phase_timing=phase_timing)
+                               bu_lane_limit=bu_lane_limit, phase_timing=phase_timing,
+                               force_exchange=force_exchange)
 
     @property
     def mode(self) -> str:

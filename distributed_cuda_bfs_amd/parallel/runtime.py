@@ -62,7 +62,8 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local_rank = _env_int("LOCAL_RANK", rank if world > 1 else 0)
-    backend = make_backend(device, local_rank)
+    # DBFS_DEVICE pins every rank to one device id (debug: several ranks on one GPU).
+    backend = make_backend(device, _env_int("DBFS_DEVICE", local_rank))
     if comm is None:
         kind = os.environ.get("DBFS_COMM", "")
         if world == 1:

@@ -160,6 +160,17 @@ def test_parent_tree_virtual_ranks():
         assert parents_are_valid(csr, lv, par, 1)
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_force_exchange_single_rank(rt, mode):
+    # the multi-rank exchange path (alltoall / allgather / alltoallv) with P = 1
+    p = dbfs.rmat_params(10, 16, 17)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+    for src in bfs.sample_roots(2, seed=3):
+        bfs.run(src)
+        assert np.array_equal(bfs.levels(), _oracle(csr, src))
+
+
 def test_hub_sort_orders_rows_and_keeps_levels(rt):
     p = dbfs.rmat_params(11, 16, 12)
     csr = dbfs.host_csr_from_params(p)

@@ -132,6 +132,26 @@ def test_cli_gpu_reference_stdout(data_dir):
     assert out.stdout.endswith("Output OK!\n\n")
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_rccl_single_rank_exchange_path(gpu_runtime, mode):
+    """RCCL communicator (1 rank) driving the full exchange path: ncclAllToAll,
+    in-place ncclAllGather, ncclAllReduce, grouped ncclSend/ncclRecv."""
+    from distributed_cuda_bfs_amd.parallel.runtime import Runtime
+
+    N = dbfs.native
+    be = gpu_runtime.backend
+    comm = N.nccl_comm(N.nccl_unique_id(), 0, 1, be)
+    assert comm.name == "rccl"
+    rt = Runtime(backend=be, comm=comm)
+    p = dbfs.rmat_params(14, 16, 23)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+    for src in bfs.sample_roots(2, seed=6):
+        _check(bfs, csr, src)
+    assert comm.sum_host(41) == 41 and comm.max_host(2.5) == 2.5
+    comm.barrier()
+
+
 def test_hub_sort_gpu_matches_cpu(gpu_runtime):
     from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
 
