@@ -268,6 +268,10 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head) override {
+    for (int64_t r = 0; r < rows; ++r) head[r] = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;
+  }
+
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     for (int64_t i = 0; i < p.m; ++i) {
       uint64_t u, v;

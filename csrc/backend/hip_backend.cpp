@@ -128,6 +128,11 @@ class HipBackend final : public Backend {
     kern::degrees_u32(ro, rows, out, st_);
     chk();
   }
+  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head) override {
+    on();
+    kern::row_heads(ro, col, rows, head, st_);
+    chk();
+  }
   void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {
     on();
     int64_t* list = nullptr;

@@ -71,6 +71,7 @@ std::unique_ptr<DeviceGraph> DeviceGraph::from_host(Backend& be, const HostCSR& 
   g->col_ = DBuf<vid_t>(be, static_cast<size_t>(std::max<int64_t>(g->nnz_, 1)));
   be.to_device(g->row_off_.data(), ro, static_cast<size_t>(g->rows_ + 1) * sizeof(eid_t));
   if (g->nnz_) be.to_device(g->col_.data(), col, static_cast<size_t>(g->nnz_) * sizeof(vid_t));
+  g->build_heads();
   return g;
 }
 
@@ -98,6 +99,7 @@ std::unique_ptr<DeviceGraph> DeviceGraph::generate(Backend& be, const GenParams&
     be.gen_fill(p, g->lo_, g->rows_, cursor.data(), g->col_.data());
     be.synchronize();
   }
+  g->build_heads();
   return g;
 }
 
@@ -109,6 +111,7 @@ ShardView DeviceGraph::view() const {
   v.lo = lo_;
   v.rows = rows_;
   v.nnz = nnz_;
+  v.head = head_.data();
   return v;
 }
 
@@ -147,8 +150,15 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm) {
   be_->degrees_u32(row_off_.data(), rows_, mine.data());
   comm.allgather(mine.data(), all.data(), static_cast<size_t>(part) * sizeof(uint32_t));
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
-  be_->synchronize();
+  build_heads();
   hub_sorted_ = true;
+}
+
+void DeviceGraph::build_heads() {
+  if (head_.size() < static_cast<size_t>(std::max<int64_t>(rows_, 1)))
+    head_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(rows_, 1)));
+  be_->row_heads(row_off_.data(), col_.data(), rows_, head_.data());
+  be_->synchronize();
 }
 
 // ---- Engine ----------------------------------------------------------------------

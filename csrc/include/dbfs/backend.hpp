@@ -33,6 +33,10 @@ struct ShardView {
   const eid_t* row_off = nullptr;  // rows + 1 (local)
   const vid_t* col = nullptr;      // row_off[rows]
   int64_t n = 0, lo = 0, rows = 0, nnz = 0;
+  // Optional per-row copy of the first neighbour (col[row_off[r]]; any value
+  // for empty rows), laid out per vertex so a wave's 64 first probes are one
+  // coalesced 256-B load instead of 64 scattered col[] lines.
+  const vid_t* head = nullptr;
 };
 
 // Frontier bookkeeping is organised in "units" of 64 bitmap words (4096
@@ -243,6 +247,8 @@ class Backend {
   // then sort every row by (key_deg[neighbour] descending, neighbour ascending).
   virtual void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out) = 0;
   virtual void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg) = 0;
+  // head[r] = col[row_off[r]] (0 for empty rows)
+  virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head) = 0;
 
   // graph construction on the device
   // deg[r] += number of edge endpoints owned in rows [lo, lo + rows) (deg zeroed by caller)

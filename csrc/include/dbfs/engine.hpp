@@ -59,6 +59,8 @@ class DeviceGraph {
   int rank_ = 0;
   int64_t lo_ = 0, rows_ = 0, nnz_ = 0, input_edges_ = 0;
   bool hub_sorted_ = false;
+  void build_heads();
+  DBuf<vid_t> head_;
   DBuf<eid_t> row_off_;
   DBuf<vid_t> col_;
 };

@@ -373,28 +373,35 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
 
   // Rows of word j for this lane (0, 0 when visited: padding and zero-degree
   // vertices are pre-set in visited).
-  auto fetch_rows = [&](int j, eid_t& rs, eid_t& e) {
+  // The row head (first, i.e. highest-degree, neighbour) comes from the
+  // per-vertex head[] array when present: a coalesced load issued together
+  // with the row offsets, no dependent col[] line.
+  const vid_t* __restrict__ head = a.g.head;
+  auto fetch_rows = [&](int j, eid_t& rs, eid_t& e, vid_t& u) {
     rs = 0;
     e = 0;
+    u = 0;
     if (j < nw && !((readlane64(vis_l, j) >> lane) & 1ull)) {
       const int64_t v = (w0 + j) * 64 + lane;
       rs = ro[v];
       e = ro[v + 1];
+      if (head) u = head[v];
     }
   };
   eid_t n_rs, n_e;
-  fetch_rows(0, n_rs, n_e);
-  vid_t n_u = n_rs < n_e ? col[n_rs] : 0u;
+  vid_t n_u;
+  fetch_rows(0, n_rs, n_e, n_u);
+  if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;
 
   for (int j = 0; j < nw; ++j) {
     const int64_t w = w0 + j;
     const word_t vis = readlane64(vis_l, j);
     const eid_t rs = n_rs, e = n_e;
     const vid_t u0 = n_u;
-    fetch_rows(j + 1, n_rs, n_e);  // in flight during this word's bit test
+    fetch_rows(j + 1, n_rs, n_e, n_u);  // in flight during this word's bit test
     // First probe: the row's first (highest-degree, hub-first order) neighbour.
     bool found = (rs < e) && test_bit(fr, u0);
-    n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
+    if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
     word_t res = 0;
     if (vis != ~0ull) {
       const int64_t v = w * 64 + lane;

@@ -120,7 +120,18 @@ __global__ __launch_bounds__(kBlock) void sort_medium_rows_kernel(const eid_t* _
   }
 }
 
+__global__ __launch_bounds__(kBlock) void row_heads_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ col,
+                                                          int64_t rows, vid_t* __restrict__ head) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r < rows) head[r] = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;
+}
+
 }  // namespace
+
+void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, hipStream_t st) {
+  if (rows <= 0) return;
+  row_heads_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, col, rows, head);
+}
 
 void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st) {
   if (rows <= 0) return;

@@ -35,6 +35,7 @@ void compute_parents(const ParentArgs& a, hipStream_t st);
 
 // graph_sort.hip
 void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st);
+void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, hipStream_t st);
 // list must hold `rows` entries; count is one device counter
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);
