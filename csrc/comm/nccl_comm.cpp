@@ -112,6 +112,9 @@ void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd,
   NCCL_CHECK(ncclGroupEnd());
 }
 
+void NcclComm::group_start() { NCCL_CHECK(ncclGroupStart()); }
+void NcclComm::group_end() { NCCL_CHECK(ncclGroupEnd()); }
+
 void NcclComm::barrier() {
   DBuf<int64_t> b(*be_, 1);
   be_->memset_async(b.data(), 0, sizeof(int64_t));

@@ -178,7 +178,6 @@ Engine::~Engine() = default;
 void Engine::alloc_bitmap_state() {
   if (bitmap_ready_) return;
   const int64_t W = part_.slice_words(), GW = part_.global_words();
-  const int P = part_.nranks;
   visited_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
   zdeg_ = DBuf<word_t>(be_, static_cast<size_t>(GW));
   frontier_[0] = DBuf<word_t>(be_, static_cast<size_t>(GW));
@@ -286,10 +285,13 @@ RunResult Engine::run_bitmap(int64_t source) {
     be_.scan_units(sa);
     cur ^= 1;
     if (exchange()) {
+      // one RCCL group: frontier all-gather + totals all-reduce share a launch
+      comm_.group_start();
       comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
+      comm_.allreduce_sum_i64(stats_.data() + 2, 2);
+      comm_.group_end();
       be_.bitmap_or(visited_.data(), fr_cur(), GW);
     }
-    comm_.allreduce_sum_i64(stats_.data() + 2, 2);
     be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
   };
   auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level) {

@@ -49,6 +49,10 @@ class Comm {
                          void* recv, const int64_t* recv_counts, const int64_t* recv_displs,
                          size_t elem_bytes) = 0;
   virtual void barrier() = 0;
+  // Collectives issued between group_start/group_end may be fused into one
+  // launch (ncclGroupStart/End); other communicators execute them in order.
+  virtual void group_start() {}
+  virtual void group_end() {}
 
   // Host-value helpers built on the device collectives.
   virtual int64_t sum_host(int64_t x);
@@ -138,6 +142,8 @@ class NcclComm final : public Comm {
   void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv,
                  const int64_t* rc, const int64_t* rd, size_t eb) override;
   void barrier() override;
+  void group_start() override;
+  void group_end() override;
 
  private:
   NcclComm() = default;
