@@ -82,12 +82,32 @@ __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, i
 // bitmap words (one coalesced 128-B access per array); then, for every
 // non-zero new word, the wave switches to lane-per-vertex so the level stores
 // and row_off loads of that word are one coalesced access each.
-__global__ __launch_bounds__(kUnitThreads) void update_kernel(UpdateArgs a) {
+//
+// Geometry: one wave per 64-word unit (lane l owns word l of the unit), 4
+// units per workgroup -- a sparse level then costs ~4K workgroups of dispatch
+// instead of 16K, and the unit statistics need no cross-wave reduction.
+constexpr int kUnitsPerBlock = kBlock / kWave;
+static_assert(kUnitWords == kWave, "one word per lane in update/compact");
+
+__device__ __forceinline__ void wave_unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
+                                                      int64_t* unit_deg) {
+  cnt = wave_sum(cnt);
+  deg = wave_sum(deg);
+  if (lane_id() == 0) {
+    unit_cnt[unit] = cnt;
+    unit_deg[unit] = deg;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   const int lane = lane_id();
-  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if (unit >= nunits) return;
+  const int64_t w0 = unit * kUnitWords;
   const int64_t wl = w0 + lane;
   word_t nb = 0;
-  if (lane < kWaveWords && wl < a.words) {
+  if (wl < a.words) {
     word_t c = 0;
     for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
     const word_t vis = a.visited[wl];
@@ -113,7 +133,7 @@ __global__ __launch_bounds__(kUnitThreads) void update_kernel(UpdateArgs a) {
       }
     }
   }
-  unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
+  wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
 }
 
 // ---------------------------------------------------------------------------
@@ -213,47 +233,22 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Frontier compaction: one wave per owned word, 16 waves per unit.  The unit's
-// base comes from the scan; the waves' offsets inside the unit from an LDS
-// scan of their (count, degree) totals; each set bit's slot from mbcnt and its
-// edge offset from a wave prefix sum of degrees.
-__global__ __launch_bounds__(kUnitThreads) void compact_kernel(CompactArgs a) {
-  __shared__ long long s_c[kUnitWaves], s_d[kUnitWaves];
+// Frontier compaction: one wave per 64-word unit (lane l loads word l), 4
+// units per workgroup.  The unit's base slot and edge offset come from the
+// scan; each set bit's slot from mbcnt and its edge offset from a wave prefix
+// sum of degrees.
+__global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   const int lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  const int64_t unit = blockIdx.x;
-  const int64_t w0 = unit * kUnitWords + wv * kWaveWords;
-  const word_t mine = (lane < kWaveWords && w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if (unit >= nunits) return;
+  const int64_t w0 = unit * kUnitWords;
+  const word_t mine = (w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
   const unsigned long long nzw = __ballot(mine != 0);
+  if (!nzw) return;
   const eid_t* __restrict__ ro = a.g.row_off;
-  // Pass 1: this wave's (count, degree) totals, for the unit-internal offsets.
-  long long c1 = 0, d1 = 0;
-  for (unsigned long long nz = nzw; nz; nz &= nz - 1) {
-    const int j = __ffsll(static_cast<long long>(nz)) - 1;
-    const word_t word = readlane64(mine, j);
-    if ((word >> lane) & 1ull) {
-      const int64_t v = (w0 + j) * 64 + lane;
-      const eid_t d = ro[v + 1] - ro[v];
-      if (d > 0) {
-        c1 += 1;
-        d1 += d;
-      }
-    }
-  }
-  c1 = wave_sum(c1);
-  d1 = wave_sum(d1);
-  if (lane == 0) {
-    s_c[wv] = c1;
-    s_d[wv] = d1;
-  }
-  __syncthreads();
   long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
   long long off = a.unit_deg_off[unit] + a.part_deg[unit / kScanChunk];
-  for (int k = 0; k < wv; ++k) {
-    pos += s_c[k];
-    off += s_d[k];
-  }
-  // Pass 2 (row_off now L2-warm): slots by mbcnt, edge offsets by wave prefix sums.
   for (unsigned long long nz = nzw; nz; nz &= nz - 1) {
     const int j = __ffsll(static_cast<long long>(nz)) - 1;
     const word_t word = readlane64(mine, j);
@@ -502,7 +497,7 @@ void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  update_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+  update_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
 }
 
 void scan_units(const ScanArgs& a, hipStream_t st) {
@@ -512,7 +507,7 @@ void scan_units(const ScanArgs& a, hipStream_t st) {
 
 void compact_frontier(const CompactArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  compact_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+  compact_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
 }
 
 void td_expand(const TdArgs& a, hipStream_t st) {
