@@ -19,7 +19,7 @@ EXT_SUFFIX:= $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_v
 COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-result
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib -lpthread
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib -lpthread
 
 HOST_SRC  := csrc/graph/io.cpp csrc/graph/csr.cpp csrc/backend/cpu_backend.cpp \
              csrc/backend/hip_backend.cpp csrc/comm/comm.cpp csrc/comm/nccl_comm.cpp \

@@ -13,10 +13,12 @@
 // serialized peer copies per (i, j), host reads of managed counters, memset.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
 #include "dbfs/engine.hpp"
+#include "dbfs/trace.hpp"
 
 namespace dbfs {
 
@@ -244,6 +246,7 @@ RunResult Engine::run(int64_t source) {
 
 RunResult Engine::run_bitmap(int64_t source) {
   alloc_bitmap_state();
+  TraceRange trace_run(std::string("bfs.run mode=") + mode_name(opt_.mode) + " src=" + std::to_string(source));
   const int P = part_.nranks;
   const int me = comm_.rank();
   const int64_t W = part_.slice_words(), GW = part_.global_words();
@@ -338,6 +341,9 @@ RunResult Engine::run_bitmap(int64_t source) {
       }
     }
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    char trace_name[48];
+    std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
+    TraceRange trace_level(trace_name);
     if (dir == 'T' || dir == 'S') {
       // `next` is all-zero here: cleared at init and by every consuming update
       // (P == 1), or re-zeroed right after the exchange below (P > 1).
