@@ -273,8 +273,8 @@ RunResult Engine::run_bitmap(int64_t source) {
   be_.memset_async(next_.data(), 0, next_.bytes());
   if (part_.owner(source) == me) be_.set_bit(cand_.data(), source - lo);
 
-  // Scan the unit statistics of the new frontier, publish it (all-gather, P > 1),
-  // merge it into the replicated visited bitmap, reduce the totals to the host.
+  // Scan the unit statistics of the new frontier and reduce the totals to the
+  // host (termination + direction decision).
   auto finish_level = [&](int64_t* host_stats) {
     ScanArgs sa;
     sa.unit_cnt = unit_cnt_.data();
@@ -287,15 +287,19 @@ RunResult Engine::run_bitmap(int64_t source) {
     sa.qscan = qscan_.data();
     be_.scan_units(sa);
     cur ^= 1;
-    if (exchange()) {
-      // one RCCL group: frontier all-gather + totals all-reduce share a launch
-      comm_.group_start();
-      comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
-      comm_.allreduce_sum_i64(stats_.data() + 2, 2);
-      comm_.group_end();
-      be_.bitmap_or(visited_.data(), fr_cur(), GW);
-    }
+    if (exchange()) comm_.allreduce_sum_i64(stats_.data() + 2, 2);
     be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
+  };
+  // Publish the new frontier (all-gather of the owned slices) and merge it into
+  // the replicated visited bitmap.  Bottom-up needs the global frontier; a
+  // top-down level only reads its owned slice, and a stale remote `visited`
+  // only lets some already-visited candidates through to their owners (which
+  // filter them), so the direction-optimising engine skips the all-gather
+  // before a top-down level.
+  auto publish = [&](char next_dir) {
+    if (!exchange() || (next_dir == 'T' && opt_.mode == Mode::DirOpt)) return;
+    comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
+    be_.bitmap_or(visited_.data(), fr_cur(), GW);
   };
   auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level) {
     UpdateArgs ua;
@@ -329,17 +333,21 @@ RunResult Engine::run_bitmap(int64_t source) {
     case Mode::Simple: dir = 'S'; break;
     default: dir = 'T'; break;
   }
-  lvl_t L = 0;
   const double n_d = static_cast<double>(part_.n);
-  while (n_f > 0) {
-    if (opt_.mode == Mode::DirOpt) {
-      const double m_u = static_cast<double>(total_directed_ - vis_deg);
-      if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha) {
-        dir = 'B';
-      } else if (dir == 'B' && static_cast<double>(n_f) < n_d / opt_.beta && n_f < prev_nf) {
-        dir = 'T';
-      }
+  // Beamer's switch, evaluated on global totals (identical on every rank).
+  auto decide = [&]() {
+    if (opt_.mode != Mode::DirOpt) return;
+    const double m_u = static_cast<double>(total_directed_ - vis_deg);
+    if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha) {
+      dir = 'B';
+    } else if (dir == 'B' && static_cast<double>(n_f) < n_d / opt_.beta && n_f < prev_nf) {
+      dir = 'T';
     }
+  };
+  decide();
+  if (n_f > 0) publish(dir);
+  lvl_t L = 0;
+  while (n_f > 0) {
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
@@ -421,6 +429,10 @@ RunResult Engine::run_bitmap(int64_t source) {
     m_f = hs[3];
     vis_deg += m_f;
     ++L;
+    if (n_f > 0) {
+      decide();
+      publish(dir);
+    }
   }
   be_.synchronize();
   const auto t1 = std::chrono::steady_clock::now();
