@@ -108,6 +108,11 @@ def main() -> int:
     wall_ms = (time.perf_counter() - t_start) * 1e3
     wall_ms = rt.comm.max_host(wall_ms)
 
+    if rank == 0:
+        for r in results:
+            dirs = "".join(lv["dir"] for lv in r.levels)
+            log(f"timed root {r.source}: {r.ms:.3f} ms {r.gteps:.1f} GTEPS levels {dirs} "
+                f"frontier-edges {[lv['frontier_edges'] for lv in r.levels]}")
     edges = sum(r.edges for r in results)
     bfs_ms = sum(r.ms for r in results)
     value = edges / (wall_ms * 1e6)
