@@ -338,7 +338,10 @@ RunResult Engine::run_bitmap(int64_t source) {
   auto decide = [&]() {
     if (opt_.mode != Mode::DirOpt) return;
     const double m_u = static_cast<double>(total_directed_ - vis_deg);
-    if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha) {
+    // T -> B only while the frontier grows: in the tail m_u is just the edges
+    // of unreachable components, and m_u / alpha would flip tiny frontiers to a
+    // full bottom-up sweep.
+    if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha && n_f > prev_nf) {
       dir = 'B';
     } else if (dir == 'B' && static_cast<double>(n_f) < n_d / opt_.beta && n_f < prev_nf) {
       dir = 'T';
