@@ -117,12 +117,16 @@ def main() -> int:
     bfs_ms = sum(r.ms for r in results)
     value = edges / (wall_ms * 1e6)
     if args.per_level:
-        # one extra (untimed) traversal of the first timed root with per-level device events
+        # extra (untimed) traversals of the fastest and the slowest timed root with
+        # per-level device events
+        order = sorted(results, key=lambda r: r.ms)
         bfs.engine.phase_timing = True
-        prof = bfs.run(timed[0])
+        profs = [bfs.run(order[0].source), bfs.run(order[-1].source)]
         bfs.engine.phase_timing = False
-        if rank == 0:
-            log(f"per-level profile of root {timed[0]} ({prof.ms:.3f} ms incl. event overhead):")
+        for prof in profs:
+            if rank != 0:
+                break
+            log(f"per-level profile of root {prof.source} ({prof.ms:.3f} ms incl. event overhead):")
             for lv in prof.levels:
                 log(f"  level {lv['level']} {lv['dir']} frontier {lv['frontier']} edges {lv['frontier_edges']}"
                     f" new {lv['discovered']} {lv['ms']:.3f} ms")
