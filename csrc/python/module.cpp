@@ -278,6 +278,62 @@ PYBIND11_MODULE(_dbfs_native, m) {
     for (auto& c : comms) out.push_back(std::shared_ptr<Comm>(c.release()));
     return out;
   });
+  // Run one collective on numpy data through a communicator (unit tests of the
+  // Comm implementations).  The data is staged into backend memory first.
+  m.def(
+      "comm_exercise",
+      [](std::shared_ptr<Comm> comm, std::shared_ptr<Backend> be, const std::string& op,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> data, std::vector<int64_t> send_counts,
+         std::vector<int64_t> recv_counts) {
+        std::vector<int64_t> in = from_numpy<int64_t>(data);
+        const int P = comm->size();
+        std::vector<int64_t> out;
+        {
+          py::gil_scoped_release rel;
+          DBuf<int64_t> s(*be, std::max<size_t>(in.size(), 1));
+          if (!in.empty()) be->to_device(s.data(), in.data(), in.size() * sizeof(int64_t));
+          if (op == "allreduce") {
+            comm->allreduce_sum_i64(s.data(), in.size());
+            out.resize(in.size());
+          } else if (op == "allgather") {
+            out.resize(in.size() * static_cast<size_t>(P));
+            DBuf<int64_t> r(*be, std::max<size_t>(out.size(), 1));
+            comm->allgather(s.data(), r.data(), in.size() * sizeof(int64_t));
+            be->to_host(out.data(), r.data(), out.size() * sizeof(int64_t));
+          } else if (op == "alltoall") {
+            DBFS_CHECK(in.size() % static_cast<size_t>(P) == 0, "alltoall input must be P equal chunks");
+            out.resize(in.size());
+            DBuf<int64_t> r(*be, std::max<size_t>(out.size(), 1));
+            comm->alltoall(s.data(), r.data(), in.size() / P * sizeof(int64_t));
+            be->to_host(out.data(), r.data(), out.size() * sizeof(int64_t));
+          } else if (op == "alltoallv") {
+            DBFS_CHECK(static_cast<int>(send_counts.size()) == P && static_cast<int>(recv_counts.size()) == P,
+                       "alltoallv needs P send and P recv counts");
+            std::vector<int64_t> sd(P), rd(P);
+            int64_t so = 0, ro = 0;
+            for (int r = 0; r < P; ++r) {
+              sd[r] = so;
+              rd[r] = ro;
+              so += send_counts[r];
+              ro += recv_counts[r];
+            }
+            DBFS_CHECK(so == static_cast<int64_t>(in.size()), "send counts must cover the input");
+            out.resize(static_cast<size_t>(ro));
+            DBuf<int64_t> r(*be, std::max<size_t>(out.size(), 1));
+            comm->alltoallv(s.data(), send_counts.data(), sd.data(), r.data(), recv_counts.data(), rd.data(),
+                            sizeof(int64_t));
+            if (!out.empty()) be->to_host(out.data(), r.data(), out.size() * sizeof(int64_t));
+          } else {
+            throw Error("unknown op " + op);
+          }
+          if (op == "allreduce" && !out.empty()) be->to_host(out.data(), s.data(), out.size() * sizeof(int64_t));
+          be->synchronize();
+        }
+        return to_numpy(out);
+      },
+      py::arg("comm"), py::arg("backend"), py::arg("op"), py::arg("data"),
+      py::arg("send_counts") = std::vector<int64_t>(), py::arg("recv_counts") = std::vector<int64_t>());
+
   py::class_<PyCommBase, Comm, PyCommTrampoline, std::shared_ptr<PyCommBase>>(m, "PyComm")
       .def(py::init<>())
       .def("py_alltoall", &PyCommBase::py_alltoall)

@@ -152,6 +152,20 @@ def test_rccl_single_rank_exchange_path(gpu_runtime, mode):
     comm.barrier()
 
 
+def test_rccl_and_virtual_comm_patterns_gpu(gpu_runtime):
+    """Communicator unit exercise (tests/test_comm.py) on device memory: RCCL
+    (1 rank) and VirtualComm ranks on one GPU."""
+    from test_comm import _check, _exercise
+
+    N = dbfs.native
+    be = gpu_runtime.backend
+    comm = N.nccl_comm(N.nccl_unique_id(), 0, 1, be)
+    _check(_exercise(comm, be, 1, 0), 1, 0)
+    outs = run_virtual_ranks(3, lambda rt: _exercise(rt.comm, rt.backend, 3, rt.rank), device="hip")
+    for me, res in enumerate(outs):
+        _check(res, 3, me)
+
+
 def test_hub_sort_gpu_matches_cpu(gpu_runtime):
     from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
 
