@@ -16,7 +16,13 @@ namespace dbfs {
 namespace {
 
 inline bool test_bit(const word_t* bm, uint64_t v) { return (bm[v >> 6] >> (v & 63)) & 1ull; }
-inline int popc(word_t w) { return __builtin_popcountll(w); }
+inline word_t gather_bytes(uint8_t* p) {
+  word_t bits = 0;
+  for (int b = 0; b < 64; ++b)
+    if (p[b]) bits |= 1ull << b;
+  if (bits) std::memset(p, 0, 64);
+  return bits;
+}
 
 class CpuBackend final : public Backend {
  public:
@@ -55,11 +61,15 @@ class CpuBackend final : public Backend {
       int64_t cnt = 0, deg = 0;
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
-        for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
+        if (a.cand_bytes) {
+          c = gather_bytes(a.cand_bytes + w * 64);
+        } else {
+          for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
+          if (a.clear_cand) a.cand[w] = 0;
+        }
         const word_t nb = a.force ? c : (c & ~a.visited[w]);
         a.visited[w] |= nb;
         a.frontier[w] = nb;
-        if (a.clear_cand) a.cand[w] = 0;
         word_t x = nb;
         while (x) {
           const int b = __builtin_ctzll(x);
@@ -137,9 +147,15 @@ class CpuBackend final : public Backend {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
       for (int64_t k = b; k < e; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
-        if (!test_bit(a.visited, v)) a.next[v >> 6] |= 1ull << (v & 63);
+        if (test_bit(a.visited, v)) continue;
+        if (a.next_bytes) a.next_bytes[v] = 1;
+        else a.next[v >> 6] |= 1ull << (v & 63);
       }
     }
+  }
+
+  void pack_bytes(const PackArgs& a) override {
+    for (int64_t w = 0; w < a.words; ++w) a.next[w] |= gather_bytes(a.bytes + w * 64);
   }
 
   void bu_step(const BuArgs& a) override {

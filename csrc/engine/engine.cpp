@@ -301,10 +301,12 @@ RunResult Engine::run_bitmap(int64_t source) {
     comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
     be_.bitmap_or(visited_.data(), fr_cur(), GW);
   };
-  auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level) {
+  auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level,
+                    uint8_t* cand_bytes = nullptr) {
     UpdateArgs ua;
     ua.g = gv;
     ua.cand = cand;
+    ua.cand_bytes = cand_bytes;
     ua.nchunks = nchunks;
     ua.cand_stride = W;
     ua.clear_cand = clear;
@@ -355,6 +357,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
     TraceRange trace_level(trace_name);
+    bool bytes_mode = false;
     if (dir == 'T' || dir == 'S') {
       // `next` is all-zero here: cleared at init and by every consuming update
       // (P == 1), or re-zeroed right after the exchange below (P > 1).
@@ -381,6 +384,14 @@ RunResult Engine::run_bitmap(int64_t source) {
           ta.m = m_local;
           ta.visited = visited_.data();
           ta.next = next_.data();
+          if (m_local >= opt_.td_byte_edges) {
+            if (!next_bytes_.data()) {
+              next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(GW) * kWordBits);
+              be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
+            }
+            ta.next_bytes = next_bytes_.data();
+            bytes_mode = true;
+          }
           be_.td_expand(ta);
         }
       } else {
@@ -393,9 +404,18 @@ RunResult Engine::run_bitmap(int64_t source) {
         be_.status_expand(sa);
       }
       if (exchange()) {
+        if (bytes_mode) {
+          PackArgs pa;
+          pa.bytes = next_bytes_.data();
+          pa.next = next_.data();
+          pa.words = GW;
+          be_.pack_bytes(pa);
+        }
         comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
         be_.memset_async(next_.data(), 0, next_.bytes());
         update(recv_.data(), P, false, false, L + 1);
+      } else if (bytes_mode) {
+        update(nullptr, 1, false, false, L + 1, next_bytes_.data());
       } else {
         update(next_.data(), 1, true, false, L + 1);
       }

@@ -62,6 +62,9 @@ constexpr int kTdEdgesPerBlock = kTdThreads * kTdItems;
 struct UpdateArgs {
   ShardView g;
   word_t* cand = nullptr;
+  // Byte-map candidates (one byte per vertex, 0/1) instead of `cand`: used
+  // after a byte-map top-down step on one rank; the bytes are cleared.
+  uint8_t* cand_bytes = nullptr;
   int nchunks = 1;
   int64_t cand_stride = 0;       // words between chunks
   bool clear_cand = false;
@@ -117,6 +120,18 @@ struct TdArgs {
   int64_t m = 0;        // work-list edges (qscan[q])
   const word_t* visited = nullptr;  // global
   word_t* next = nullptr;           // global
+  // Byte-map mode (large levels): next_bytes[v] = 1 with a plain byte store
+  // instead of a scattered 64-bit atomicOr on next (the atomics bound the
+  // top-down rate at ~40 G edges/s on MI355X).
+  uint8_t* next_bytes = nullptr;
+};
+
+// next[w] |= bits of bytes[64 w .. 64 w + 63]; bytes cleared (multi-rank
+// byte-map top-down: the exchange stays a bitmap all-to-all).
+struct PackArgs {
+  uint8_t* bytes = nullptr;
+  word_t* next = nullptr;
+  int64_t words = 0;
 };
 
 // Bottom-up step fused with the frontier update: for every owned unvisited v,
@@ -235,6 +250,7 @@ class Backend {
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
+  virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;

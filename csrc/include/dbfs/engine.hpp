@@ -73,6 +73,9 @@ struct EngineOptions {
   double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
   int bu_lane_limit = 8;
+  // Top-down levels with at least this many local frontier edges mark
+  // discoveries in a byte map (plain stores) instead of bitmap atomics.
+  int64_t td_byte_edges = int64_t(1) << 22;
   bool phase_timing = false;  // per-level device timing (adds events)
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
@@ -138,6 +141,7 @@ class Engine {
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_;
+  DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;

@@ -99,6 +99,29 @@ __device__ __forceinline__ void wave_unit_stats_store(long long cnt, long long d
   }
 }
 
+// 64 candidate bytes (0/1, 64-byte aligned) -> one bitmap word; the bytes are
+// cleared when any is set.  Four 16-B loads / stores per lane.
+__device__ __forceinline__ word_t gather_byte_bits(uint8_t* p) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  word_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 x = q[k];
+    const unsigned v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((v[j] >> (8 * b)) & 0xFFu) bits |= 1ull << (k * 16 + j * 4 + b);
+    }
+  }
+  if (bits) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  return bits;
+}
+
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
@@ -109,7 +132,11 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   word_t nb = 0;
   if (wl < a.words) {
     word_t c = 0;
-    for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
+    if (a.cand_bytes) {
+      c = gather_byte_bits(a.cand_bytes + wl * 64);
+    } else {
+      for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
+    }
     const word_t vis = a.visited[wl];
     nb = a.force ? c : (c & ~vis);
     if (nb) a.visited[wl] = vis | nb;
@@ -282,6 +309,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // then read in 256-lane coalesced sweeps.  A discovered vertex costs one
 // atomicOr only if neither `visited` nor the (possibly stale, only-growing)
 // `next` word already has its bit.
+template <bool kBytes>
 __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
@@ -335,10 +363,22 @@ __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
       const int i = s_owner[idx];
       const vid_t v = col[e0 + idx + s_base[i]];
       const word_t bit = 1ull << (v & 63);
-      const word_t seen = visited[v >> 6] | a.next[v >> 6];
-      if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
+      if constexpr (kBytes) {
+        if (!(visited[v >> 6] & bit)) a.next_bytes[v] = 1;
+      } else {
+        const word_t seen = visited[v >> 6] | a.next[v >> 6];
+        if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
+      }
     }
   }
+}
+
+// Byte map -> bitmap for the multi-rank exchange (words of 64 vertices).
+__global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (w >= a.words) return;
+  const word_t bits = gather_byte_bits(a.bytes + w * 64);
+  if (bits) a.next[w] |= bits;
 }
 
 // ---------------------------------------------------------------------------
@@ -512,7 +552,15 @@ void compact_frontier(const CompactArgs& a, hipStream_t st) {
 
 void td_expand(const TdArgs& a, hipStream_t st) {
   if (a.m <= 0 || a.q <= 0) return;
-  td_expand_kernel<<<grid_for(a.m, kTdEdgesPerBlock), kTdThreads, 0, st>>>(a);
+  if (a.next_bytes)
+    td_expand_kernel<true><<<grid_for(a.m, kTdEdgesPerBlock), kTdThreads, 0, st>>>(a);
+  else
+    td_expand_kernel<false><<<grid_for(a.m, kTdEdgesPerBlock), kTdThreads, 0, st>>>(a);
+}
+
+void pack_bytes(const PackArgs& a, hipStream_t st) {
+  if (a.words <= 0) return;
+  pack_bytes_kernel<<<grid_for(a.words, kBlock), kBlock, 0, st>>>(a);
 }
 
 void bu_step(const BuArgs& a, hipStream_t st) {

@@ -480,11 +480,16 @@ PYBIND11_MODULE(_dbfs_native, m) {
             o.phase_timing = on;
             e.set_options(o);
           })
-      .def("set_heuristics", [](Engine& e, double alpha, double beta, int lane_limit) {
-        EngineOptions o = e.options();
-        o.alpha = alpha;
-        o.beta = beta;
-        o.bu_lane_limit = lane_limit;
-        e.set_options(o);
-      });
+      .def(
+          "set_heuristics",
+          [](Engine& e, double alpha, double beta, int lane_limit, int64_t td_byte_edges) {
+            EngineOptions o = e.options();
+            o.alpha = alpha;
+            o.beta = beta;
+            o.bu_lane_limit = lane_limit;
+            if (td_byte_edges >= 0) o.td_byte_edges = td_byte_edges;
+            e.set_options(o);
+          },
+          py::arg("alpha"), py::arg("beta"), py::arg("lane_limit"), py::arg("td_byte_edges") = -1)
+      .def_property_readonly("td_byte_edges", [](const Engine& e) { return e.options().td_byte_edges; });
 }

@@ -171,6 +171,30 @@ def test_force_exchange_single_rank(rt, mode):
         assert np.array_equal(bfs.levels(), _oracle(csr, src))
 
 
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_td_byte_map_mode(P, mode):
+    # td_byte_edges = 0: every top-down level uses the byte map (+ pack for P > 1)
+    p = dbfs.rmat_params(11, 16, 29)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [0, 5, 2047]
+    exp = [_oracle(csr, s) for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        bfs.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+        assert bfs.engine.td_byte_edges == 0
+        out = []
+        for s in srcs:
+            bfs.run(s)
+            out.append(bfs.levels())
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for lv, e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+
+
 def test_hub_sort_orders_rows_and_keeps_levels(rt):
     p = dbfs.rmat_params(11, 16, 12)
     csr = dbfs.host_csr_from_params(p)

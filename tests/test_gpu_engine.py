@@ -166,6 +166,28 @@ def test_rccl_and_virtual_comm_patterns_gpu(gpu_runtime):
         _check(res, 3, me)
 
 
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_td_byte_map_mode_gpu(P, mode):
+    p = dbfs.rmat_params(16, 16, 29)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [0, 5, 40000]
+    exp = [dbfs.cpu_bfs(csr, s)[0] for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        bfs.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+        out = []
+        for s in srcs:
+            bfs.run(s)
+            out.append(bfs.levels())
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="hip"):
+        for lv, e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+
+
 def test_hub_sort_gpu_matches_cpu(gpu_runtime):
     from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
 
