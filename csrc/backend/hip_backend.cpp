@@ -7,6 +7,7 @@
 // comma-expression idiom that discards them (bfs.cu:336-351, D3).
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -37,12 +38,14 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
+    HIP_CHECK(hipHostMalloc(&pinned_, kPinned, hipHostMallocDefault));
   }
   ~HipBackend() override {
     hipSetDevice(dev_);
     hipStreamSynchronize(st_);
     for (hipEvent_t e : events_) hipEventDestroy(e);
     if (scan_tmp_) hipFree(scan_tmp_);
+    if (pinned_) hipHostFree(pinned_);
     hipStreamDestroy(st_);
   }
 
@@ -77,6 +80,13 @@ class HipBackend final : public Backend {
   }
   void to_host(void* d, const void* s, size_t bytes) override {
     on();
+    if (bytes && bytes <= kPinned) {
+      // small (per-level statistics) copies: DMA into pinned memory, no staging
+      HIP_CHECK(hipMemcpyAsync(pinned_, s, bytes, hipMemcpyDeviceToHost, st_));
+      HIP_CHECK(hipStreamSynchronize(st_));
+      std::memcpy(d, pinned_, bytes);
+      return;
+    }
     if (bytes) HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
   }
@@ -182,7 +192,9 @@ class HipBackend final : public Backend {
   void on() { HIP_CHECK(hipSetDevice(dev_)); }
   static void chk() { HIP_CHECK(hipGetLastError()); }
 
+  static constexpr size_t kPinned = 4096;
   int dev_;
+  void* pinned_ = nullptr;
   hipStream_t st_ = nullptr;
   std::string arch_;
   int cus_ = 0;

@@ -11,23 +11,27 @@
 
 namespace dbfs {
 
-int64_t Comm::sum_host(int64_t x) {
+int64_t* Comm::scratch(size_t n) {
   DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
-  DBuf<int64_t> b(*be_, 1);
-  be_->to_device(b.data(), &x, sizeof(x));
-  allreduce_sum_i64(b.data(), 1);
-  be_->to_host(&x, b.data(), sizeof(x));
+  if (scratch_.size() < n) scratch_ = DBuf<int64_t>(*be_, std::max<size_t>(n, 64));
+  return scratch_.data();
+}
+
+int64_t Comm::sum_host(int64_t x) {
+  int64_t* b = scratch(1);
+  be_->to_device(b, &x, sizeof(x));
+  allreduce_sum_i64(b, 1);
+  be_->to_host(&x, b, sizeof(x));
   return x;
 }
 
 double Comm::max_host(double x) {
-  DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
   const int n = size();
-  DBuf<double> s(*be_, 1), r(*be_, static_cast<size_t>(n));
-  be_->to_device(s.data(), &x, sizeof(x));
-  allgather(s.data(), r.data(), sizeof(double));
+  int64_t* b = scratch(static_cast<size_t>(n) + 1);
+  be_->to_device(b, &x, sizeof(x));
+  allgather(b, b + 1, sizeof(double));
   std::vector<double> h(static_cast<size_t>(n));
-  be_->to_host(h.data(), r.data(), h.size() * sizeof(double));
+  be_->to_host(h.data(), b + 1, h.size() * sizeof(double));
   return *std::max_element(h.begin(), h.end());
 }
 

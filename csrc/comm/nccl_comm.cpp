@@ -116,9 +116,8 @@ void NcclComm::group_start() { NCCL_CHECK(ncclGroupStart()); }
 void NcclComm::group_end() { NCCL_CHECK(ncclGroupEnd()); }
 
 void NcclComm::barrier() {
-  DBuf<int64_t> b(*be_, 1);
-  be_->memset_async(b.data(), 0, sizeof(int64_t));
-  allreduce_sum_i64(b.data(), 1);
+  int64_t* b = scratch(1);
+  allreduce_sum_i64(b, 1);  // value irrelevant: completion on every rank is the barrier
   be_->synchronize();
 }
 

@@ -57,10 +57,17 @@ class Comm {
   // Host-value helpers built on the device collectives.
   virtual int64_t sum_host(int64_t x);
   virtual double max_host(double x);
-  void bind_backend(Backend* be) { be_ = be; }
+  void bind_backend(Backend* be) {
+    if (be != be_) scratch_.reset();
+    be_ = be;
+  }
 
  protected:
+  // Small persistent device scratch for the host-value helpers and barriers
+  // (no hipMalloc/hipFree -- which synchronise the device -- per call).
+  int64_t* scratch(size_t n_int64);
   Backend* be_ = nullptr;
+  DBuf<int64_t> scratch_;
 };
 
 class LocalComm final : public Comm {
