@@ -148,8 +148,24 @@ class CpuBackend final : public Backend {
       for (int64_t k = b; k < e; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
         if (test_bit(a.visited, v)) continue;
-        if (a.next_bytes) a.next_bytes[v] = 1;
-        else a.next[v >> 6] |= 1ull << (v & 63);
+        if (a.lists) {
+          vid_t* list = a.lists + static_cast<int64_t>(v / a.part) * (a.list_cap + 1);
+          list[1 + list[0]++] = v;
+        } else if (a.next_bytes) {
+          a.next_bytes[v] = 1;
+        } else {
+          a.next[v >> 6] |= 1ull << (v & 63);
+        }
+      }
+    }
+  }
+
+  void list_scatter(const ListScatterArgs& a) override {
+    for (int r = 0; r < a.nranks; ++r) {
+      const vid_t* list = a.lists + static_cast<int64_t>(r) * (a.list_cap + 1);
+      for (vid_t k = 0; k < list[0]; ++k) {
+        const int64_t v = static_cast<int64_t>(list[1 + k]) - a.lo;
+        a.cand[v >> 6] |= 1ull << (v & 63);
       }
     }
   }

@@ -127,6 +127,7 @@ class HipBackend final : public Backend {
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }
+  void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }

@@ -323,7 +323,7 @@ RunResult Engine::run_bitmap(int64_t source) {
 
   int64_t hs[4];
   // Seed: the source is forced in even when it has degree 0 (pre-visited).
-  update(cand_.data(), 1, false, true, 0);
+  update(cand_.data(), 1, true, true, 0);
   finish_level(hs);
   int64_t q_local = hs[0], m_local = hs[1], n_f = hs[2], m_f = hs[3];
   int64_t vis_deg = m_f;
@@ -358,6 +358,24 @@ RunResult Engine::run_bitmap(int64_t source) {
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
     TraceRange trace_level(trace_name);
     bool bytes_mode = false;
+    // Sparse exchange: every rank sends at most m_f (global frontier edges)
+    // candidates to any peer, so owner lists of capacity m_f cannot overflow;
+    // used when they are smaller than half a bitmap slice.
+    const bool list_mode =
+        exchange() && dir == 'T' && m_f <= opt_.sparse_max_edges &&
+        (!opt_.sparse_size_check ||
+         (m_f + 1) * static_cast<int64_t>(sizeof(vid_t)) * 2 <= W * static_cast<int64_t>(sizeof(word_t)));
+    const int64_t list_cap = m_f;
+    if (list_mode) {
+      if (send_lists_.size() < static_cast<size_t>(P) * (list_cap + 1)) {
+        // grow geometrically (bounded by the option) so a run allocates O(1) times
+        const int64_t per = std::min(opt_.sparse_max_edges, std::max<int64_t>(2 * list_cap, 4096));
+        const size_t cap = static_cast<size_t>(P) * static_cast<size_t>(std::max(per, list_cap) + 1);
+        send_lists_ = DBuf<vid_t>(be_, cap);
+        recv_lists_ = DBuf<vid_t>(be_, cap);
+      }
+      be_.memset_async(send_lists_.data(), 0, static_cast<size_t>(P) * (list_cap + 1) * sizeof(vid_t));
+    }
     if (dir == 'T' || dir == 'S') {
       // `next` is all-zero here: cleared at init and by every consuming update
       // (P == 1), or re-zeroed right after the exchange below (P > 1).
@@ -384,7 +402,11 @@ RunResult Engine::run_bitmap(int64_t source) {
           ta.m = m_local;
           ta.visited = visited_.data();
           ta.next = next_.data();
-          if (m_local >= opt_.td_byte_edges) {
+          if (list_mode) {
+            ta.lists = send_lists_.data();
+            ta.list_cap = list_cap;
+            ta.part = part_.part;
+          } else if (m_local >= opt_.td_byte_edges) {
             if (!next_bytes_.data()) {
               next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(GW) * kWordBits);
               be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
@@ -403,7 +425,17 @@ RunResult Engine::run_bitmap(int64_t source) {
         sa.next = next_.data();
         be_.status_expand(sa);
       }
-      if (exchange()) {
+      if (list_mode) {
+        comm_.alltoall(send_lists_.data(), recv_lists_.data(), static_cast<size_t>(list_cap + 1) * sizeof(vid_t));
+        ListScatterArgs la;
+        la.lists = recv_lists_.data();
+        la.nranks = P;
+        la.list_cap = list_cap;
+        la.lo = lo;
+        la.cand = cand_.data();
+        be_.list_scatter(la);
+        update(cand_.data(), 1, true, false, L + 1);
+      } else if (exchange()) {
         if (bytes_mode) {
           PackArgs pa;
           pa.bytes = next_bytes_.data();

@@ -124,6 +124,23 @@ struct TdArgs {
   // instead of a scattered 64-bit atomicOr on next (the atomics bound the
   // top-down rate at ~40 G edges/s on MI355X).
   uint8_t* next_bytes = nullptr;
+  // List mode (small levels, multi-rank): candidate v is appended to its
+  // owner's list lists[o * (list_cap + 1) + 1 + k]; slot 0 of each list is its
+  // count (wave-aggregated atomics, at most nranks per wave instruction).
+  // list_cap >= global frontier edges guarantees no overflow.
+  vid_t* lists = nullptr;
+  int64_t list_cap = 0;
+  int64_t part = 0;   // owner(v) = v / part
+};
+
+// Received candidate lists (nranks lists of list_cap + 1 words, count first)
+// -> bits in cand (owned slice), local index v - lo.
+struct ListScatterArgs {
+  const vid_t* lists = nullptr;
+  int nranks = 1;
+  int64_t list_cap = 0;
+  int64_t lo = 0;
+  word_t* cand = nullptr;
 };
 
 // next[w] |= bits of bytes[64 w .. 64 w + 63]; bytes cleared (multi-rank
@@ -251,6 +268,7 @@ class Backend {
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
   virtual void pack_bytes(const PackArgs& a) = 0;
+  virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;

@@ -76,6 +76,12 @@ struct EngineOptions {
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;
+  // Multi-rank top-down levels whose global frontier has at most this many
+  // edges exchange owner lists instead of bitmap slices.
+  int64_t sparse_max_edges = int64_t(1) << 17;
+  // ... and only when the lists are smaller than half a bitmap slice (tests
+  // switch this off to exercise the list path on small graphs).
+  bool sparse_size_check = true;
   bool phase_timing = false;  // per-level device timing (adds events)
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
@@ -142,6 +148,7 @@ class Engine {
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
+  DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;

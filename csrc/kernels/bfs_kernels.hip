@@ -309,7 +309,9 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // then read in 256-lane coalesced sweeps.  A discovered vertex costs one
 // atomicOr only if neither `visited` nor the (possibly stale, only-growing)
 // `next` word already has its bit.
-template <bool kBytes>
+enum class TdOut { Bits, Bytes, Lists };
+
+template <TdOut kOut>
 __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
@@ -359,17 +361,50 @@ __global__ __launch_bounds__(kTdThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
   for (int k = 0; k < kTdItems; ++k) {
     const int idx = k * kTdThreads + t;
-    if (idx < cnt) {
+    if constexpr (kOut == TdOut::Lists) {
+      // wave-aggregated append to the owner lists (uniform loop over owners)
+      vid_t v = 0;
+      bool act = false;
+      if (idx < cnt) {
+        v = col[e0 + idx + s_base[s_owner[idx]]];
+        act = !(visited[v >> 6] & (1ull << (v & 63)));
+      }
+      const int owner = act ? static_cast<int>(v / a.part) : -1;
+      unsigned long long pending = __ballot(act);
+      while (pending) {
+        const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+        const int o = __shfl(owner, leader, kWave);
+        const unsigned long long m = __ballot(owner == o);
+        unsigned base = 0;
+        vid_t* list = a.lists + static_cast<int64_t>(o) * (a.list_cap + 1);
+        if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(m)));
+        base = __shfl(base, leader, kWave);
+        if (owner == o) list[1 + base + mask_rank(m)] = v;
+        pending &= ~m;
+      }
+    } else if (idx < cnt) {
       const int i = s_owner[idx];
       const vid_t v = col[e0 + idx + s_base[i]];
       const word_t bit = 1ull << (v & 63);
-      if constexpr (kBytes) {
+      if constexpr (kOut == TdOut::Bytes) {
         if (!(visited[v >> 6] & bit)) a.next_bytes[v] = 1;
       } else {
         const word_t seen = visited[v >> 6] | a.next[v >> 6];
         if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
       }
     }
+  }
+}
+
+// Received owner lists -> candidate bits of the owned slice.
+__global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a) {
+  const int r = blockIdx.y;
+  const vid_t* list = a.lists + static_cast<int64_t>(r) * (a.list_cap + 1);
+  const int64_t n = list[0];
+  for (int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; k < n;
+       k += static_cast<int64_t>(gridDim.x) * kBlock) {
+    const int64_t v = static_cast<int64_t>(list[1 + k]) - a.lo;
+    atomicOr(a.cand + (v >> 6), 1ull << (v & 63));
   }
 }
 
@@ -552,10 +587,19 @@ void compact_frontier(const CompactArgs& a, hipStream_t st) {
 
 void td_expand(const TdArgs& a, hipStream_t st) {
   if (a.m <= 0 || a.q <= 0) return;
-  if (a.next_bytes)
-    td_expand_kernel<true><<<grid_for(a.m, kTdEdgesPerBlock), kTdThreads, 0, st>>>(a);
+  const unsigned grid = grid_for(a.m, kTdEdgesPerBlock);
+  if (a.lists)
+    td_expand_kernel<TdOut::Lists><<<grid, kTdThreads, 0, st>>>(a);
+  else if (a.next_bytes)
+    td_expand_kernel<TdOut::Bytes><<<grid, kTdThreads, 0, st>>>(a);
   else
-    td_expand_kernel<false><<<grid_for(a.m, kTdEdgesPerBlock), kTdThreads, 0, st>>>(a);
+    td_expand_kernel<TdOut::Bits><<<grid, kTdThreads, 0, st>>>(a);
+}
+
+void list_scatter(const ListScatterArgs& a, hipStream_t st) {
+  if (a.nranks <= 0 || a.list_cap <= 0) return;
+  const unsigned gx = grid_for(a.list_cap, kBlock, 256);
+  list_scatter_kernel<<<dim3(gx, static_cast<unsigned>(a.nranks)), kBlock, 0, st>>>(a);
 }
 
 void pack_bytes(const PackArgs& a, hipStream_t st) {

@@ -17,6 +17,7 @@ void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
+void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);

@@ -482,14 +482,18 @@ PYBIND11_MODULE(_dbfs_native, m) {
           })
       .def(
           "set_heuristics",
-          [](Engine& e, double alpha, double beta, int lane_limit, int64_t td_byte_edges) {
+          [](Engine& e, double alpha, double beta, int lane_limit, int64_t td_byte_edges, int64_t sparse_max_edges,
+             int sparse_size_check) {
             EngineOptions o = e.options();
             o.alpha = alpha;
             o.beta = beta;
             o.bu_lane_limit = lane_limit;
             if (td_byte_edges >= 0) o.td_byte_edges = td_byte_edges;
+            if (sparse_max_edges >= 0) o.sparse_max_edges = sparse_max_edges;
+            if (sparse_size_check >= 0) o.sparse_size_check = sparse_size_check != 0;
             e.set_options(o);
           },
-          py::arg("alpha"), py::arg("beta"), py::arg("lane_limit"), py::arg("td_byte_edges") = -1)
+          py::arg("alpha"), py::arg("beta"), py::arg("lane_limit"), py::arg("td_byte_edges") = -1,
+          py::arg("sparse_max_edges") = -1, py::arg("sparse_size_check") = -1)
       .def_property_readonly("td_byte_edges", [](const Engine& e) { return e.options().td_byte_edges; });
 }

@@ -195,6 +195,30 @@ def test_td_byte_map_mode(P, mode):
             assert np.array_equal(lv, e)
 
 
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("sparse_max", [0, 64, 1 << 40])
+def test_sparse_list_exchange(P, mode, sparse_max):
+    # sparse_max_edges decides which top-down levels use the owner-list exchange
+    p = dbfs.rmat_params(11, 16, 31)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [1, 7, 2000]
+    exp = [_oracle(csr, s) for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        bfs.engine.set_heuristics(24.0, 24.0, 8, sparse_max_edges=sparse_max, sparse_size_check=0)
+        out = []
+        for s in srcs:
+            bfs.run(s)
+            out.append(bfs.levels())
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for lv, e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+
+
 def test_hub_sort_orders_rows_and_keeps_levels(rt):
     p = dbfs.rmat_params(11, 16, 12)
     csr = dbfs.host_csr_from_params(p)

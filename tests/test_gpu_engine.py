@@ -188,6 +188,38 @@ def test_td_byte_map_mode_gpu(P, mode):
             assert np.array_equal(lv, e)
 
 
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_sparse_list_exchange_gpu(gpu_runtime, P, mode):
+    """Owner-list exchange for every top-down level (P=1 through a 1-rank RCCL
+    communicator with force_exchange, P=3 through virtual ranks on one GPU)."""
+    from distributed_cuda_bfs_amd.parallel.runtime import Runtime
+
+    p = dbfs.rmat_params(16, 16, 31)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [1, 7, 50000]
+    exp = [dbfs.cpu_bfs(csr, s)[0] for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+        bfs.engine.set_heuristics(24.0, 24.0, 8, sparse_max_edges=1 << 40, sparse_size_check=0)
+        out = []
+        for s in srcs:
+            bfs.run(s)
+            out.append(bfs.levels())
+        return out
+
+    if P == 1:
+        N = dbfs.native
+        be = gpu_runtime.backend
+        outs = [body(Runtime(backend=be, comm=N.nccl_comm(N.nccl_unique_id(), 0, 1, be)))]
+    else:
+        outs = run_virtual_ranks(P, body, device="hip")
+    for rank_out in outs:
+        for lv, e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+
+
 def test_hub_sort_gpu_matches_cpu(gpu_runtime):
     from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
 
