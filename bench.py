@@ -47,7 +47,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edge-factor", type=int, default=16)
-    ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple"])
+    ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple", "scan"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--root-seed", type=int, default=12345)
     ap.add_argument("--alpha", type=float, default=24.0)

@@ -245,6 +245,44 @@ class CpuBackend final : public Backend {
     }
   }
 
+  // Scan mode: the same four passes as the HIP kernels (sequential, so the
+  // claim is simply the first edge in queue order).
+  void scan_relax(const ScanBfsArgs& a) override {
+    for (int64_t i = 0; i < a.q; ++i) {
+      const int64_t u = static_cast<int64_t>(a.queue[i]) - a.g.lo;
+      for (eid_t e = a.g.row_off[u]; e < a.g.row_off[u + 1]; ++e) {
+        const vid_t v = a.g.col[e];
+        if (a.dist[v] == kUnreached) {
+          a.dist[v] = a.next_level;
+          a.claim[v] = e;
+        }
+      }
+    }
+  }
+  void scan_count(const ScanBfsArgs& a) override {
+    for (int64_t i = 0; i < a.q * a.nranks; ++i) a.offs[i] = 0;
+    for (int64_t i = 0; i < a.q; ++i) {
+      const int64_t u = static_cast<int64_t>(a.queue[i]) - a.g.lo;
+      for (eid_t e = a.g.row_off[u]; e < a.g.row_off[u + 1]; ++e) {
+        const vid_t v = a.g.col[e];
+        if (a.dist[v] == a.next_level && a.claim[v] == e) ++a.offs[(v / a.part) * a.q + i];
+      }
+    }
+  }
+  void scan_bounds(const ScanBfsArgs& a) override {
+    for (int o = 0; o <= a.nranks; ++o) a.bounds[o] = a.offs[o * a.q];
+    for (int o = 0; o < a.nranks; ++o) a.counts[o] = a.bounds[o + 1] - a.bounds[o];
+  }
+  void scan_assign(const ScanBfsArgs& a) override {
+    for (int64_t i = 0; i < a.q; ++i) {
+      const int64_t u = static_cast<int64_t>(a.queue[i]) - a.g.lo;
+      for (eid_t e = a.g.row_off[u]; e < a.g.row_off[u + 1]; ++e) {
+        const vid_t v = a.g.col[e];
+        if (a.dist[v] == a.next_level && a.claim[v] == e) a.out[a.offs[(v / a.part) * a.q + i]++] = v;
+      }
+    }
+  }
+
   void validate_levels(const ValidateArgs& a) override {
     int64_t gap = 0, cross = 0, orphan = 0;
     for (int64_t r = 0; r < a.g.rows; ++r) {

@@ -133,6 +133,10 @@ class HipBackend final : public Backend {
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
   void ref_accept(const RefAcceptArgs& a) override { on(); kern::ref_accept(a, st_); chk(); }
+  void scan_relax(const ScanBfsArgs& a) override { on(); kern::scan_relax(a, st_); chk(); }
+  void scan_count(const ScanBfsArgs& a) override { on(); kern::scan_count(a, st_); chk(); }
+  void scan_bounds(const ScanBfsArgs& a) override { on(); kern::scan_bounds(a, st_); chk(); }
+  void scan_assign(const ScanBfsArgs& a) override { on(); kern::scan_assign(a, st_); chk(); }
   void validate_levels(const ValidateArgs& a) override { on(); kern::validate_levels(a, st_); chk(); }
   void compute_parents(const ParentArgs& a) override { on(); kern::compute_parents(a, st_); chk(); }
   void degrees_u32(const eid_t* ro, int64_t rows, uint32_t* out) override {

@@ -65,7 +65,7 @@ struct Args {
                "usage: bfs <src> <edge-list|.mtx|.csr> [flags]\n"
                "       bfs --rmat SCALE[:EF] [<src>] [flags]\n"
                "flags: --gpus P | --virtual-ranks P | --cpu | --device D\n"
-               "       --mode ref|td|bu|do|simple  --alpha A --beta B --bu-lane-limit K\n"
+               "       --mode ref|td|bu|do|simple|scan  --alpha A --beta B --bu-lane-limit K\n"
                "       --rmat SCALE[:EF] | --uniform N:M   --seed S\n"
                "       --roots K (random sources, GTEPS summary)  --no-oracle  --validate\n"
                "       --levels-out FILE  --cache FILE (write binary CSR)  --json  --quiet  --phase-timing\n");

@@ -28,7 +28,8 @@ Mode parse_mode(const std::string& s) {
   if (s == "bu" || s == "bottomup" || s == "bottom-up") return Mode::BottomUp;
   if (s == "do" || s == "diropt" || s == "direction-optimizing" || s == "hybrid") return Mode::DirOpt;
   if (s == "simple" || s == "status") return Mode::Simple;
-  throw Error("unknown mode '" + s + "' (expected ref|td|bu|do|simple)");
+  if (s == "scan") return Mode::Scan;
+  throw Error("unknown mode '" + s + "' (expected ref|td|bu|do|simple|scan)");
 }
 
 const char* mode_name(Mode m) {
@@ -38,6 +39,7 @@ const char* mode_name(Mode m) {
     case Mode::BottomUp: return "bu";
     case Mode::DirOpt: return "do";
     case Mode::Simple: return "simple";
+    case Mode::Scan: return "scan";
   }
   return "?";
 }
@@ -211,14 +213,20 @@ void Engine::alloc_bitmap_state() {
 }
 
 void Engine::alloc_ref_state() {
-  if (ref_ready_) return;
   const int P = part_.nranks;
   const int64_t cap = part_.part;
-  dist_ = DBuf<lvl_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.n, 1)));
+  if (opt_.mode == Mode::Scan && claim_.size() == 0) {
+    DBFS_CHECK(P <= 64, "scan mode supports at most 64 ranks");
+    claim_ = DBuf<eid_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.n, 1)));
+    scan_offs_ = DBuf<eid_t>(be_, static_cast<size_t>(P * cap + 1));
+  }
+  if (ref_ready_) return;
+  dist_ =DBuf<lvl_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.n, 1)));
   queue_ = DBuf<vid_t>(be_, static_cast<size_t>(std::max<int64_t>(cap, 1)));
   buckets_ = DBuf<vid_t>(be_, static_cast<size_t>(P * cap));
   recvq_ = DBuf<vid_t>(be_, static_cast<size_t>(P * cap));
-  bucket_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * P));
+  // [0, P) send counts, [P, 2P) receive counts, [2P, 3P] scan-mode bounds
+  bucket_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(3 * P + 1));
   qcount_ = DBuf<int64_t>(be_, 1);
   ref_ready_ = true;
 }
@@ -226,7 +234,7 @@ void Engine::alloc_ref_state() {
 RunResult Engine::run(int64_t source) {
   DBFS_CHECK(source >= 0 && source < part_.n, "source vertex out of range");
   RunResult r;
-  if (opt_.mode == Mode::Ref) {
+  if (opt_.mode == Mode::Ref || opt_.mode == Mode::Scan) {
     r = run_ref(source);
     // Traversed-edge accounting (Graph500), outside the timed region.
     DBuf<int64_t> acc(be_, 2);
@@ -525,24 +533,58 @@ RunResult Engine::run_ref(int64_t source) {
   int64_t total_q = 1;
   lvl_t L = 0;
   std::vector<int64_t> hcnt(static_cast<size_t>(P)), hrc(static_cast<size_t>(P)), sd(static_cast<size_t>(P)),
-      rd(static_cast<size_t>(P));
+      rd(static_cast<size_t>(P)), hbuf(static_cast<size_t>(3 * P + 1));
+  const bool scan = opt_.mode == Mode::Scan;
   while (total_q > 0) {
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    be_.memset_async(bucket_cnt_.data(), 0, static_cast<size_t>(P) * sizeof(int64_t));
-    RefExpandArgs ea;
-    ea.g = gv;
-    ea.queue = queue_.data();
-    ea.q = q;
-    ea.next_level = L + 1;
-    ea.dist = dist_.data();
-    ea.part = part_.part;
-    ea.bucket_cnt = bucket_cnt_.data();
-    ea.buckets = buckets_.data();
-    ea.bucket_cap = cap;
-    be_.ref_expand(ea);
-    be_.to_host(hcnt.data(), bucket_cnt_.data(), static_cast<size_t>(P) * sizeof(int64_t));
+    if (scan) {
+      // relax -> count -> scan -> bounds -> assign: children land owner-major in
+      // buckets_, bucket o at [bounds[o], bounds[o + 1])
+      ScanBfsArgs sa;
+      sa.g = gv;
+      sa.queue = queue_.data();
+      sa.q = q;
+      sa.next_level = L + 1;
+      sa.dist = dist_.data();
+      sa.claim = claim_.data();
+      sa.part = part_.part;
+      sa.nranks = P;
+      sa.offs = scan_offs_.data();
+      sa.counts = bucket_cnt_.data();
+      sa.bounds = bucket_cnt_.data() + 2 * P;
+      sa.out = buckets_.data();
+      be_.scan_relax(sa);
+      be_.scan_count(sa);
+      be_.exclusive_scan(sa.offs, P * q);
+      be_.scan_bounds(sa);
+      be_.scan_assign(sa);
+      be_.to_host(hbuf.data(), bucket_cnt_.data(), hbuf.size() * sizeof(int64_t));
+      for (int r = 0; r < P; ++r) {
+        hcnt[r] = hbuf[r];
+        sd[r] = hbuf[2 * P + r];
+      }
+    } else {
+      be_.memset_async(bucket_cnt_.data(), 0, static_cast<size_t>(P) * sizeof(int64_t));
+      RefExpandArgs ea;
+      ea.g = gv;
+      ea.queue = queue_.data();
+      ea.q = q;
+      ea.next_level = L + 1;
+      ea.dist = dist_.data();
+      ea.part = part_.part;
+      ea.bucket_cnt = bucket_cnt_.data();
+      ea.buckets = buckets_.data();
+      ea.bucket_cap = cap;
+      be_.ref_expand(ea);
+      be_.to_host(hcnt.data(), bucket_cnt_.data(), static_cast<size_t>(P) * sizeof(int64_t));
+      for (int r = 0; r < P; ++r) sd[r] = r * cap;
+    }
     if (!exchange()) {
-      be_.copy_async(queue_.data(), buckets_.data(), static_cast<size_t>(hcnt[0]) * sizeof(vid_t));
+      if (scan) {
+        std::swap(queue_, buckets_);  // P == 1: both hold cap entries
+      } else {
+        be_.copy_async(queue_.data(), buckets_.data(), static_cast<size_t>(hcnt[0]) * sizeof(vid_t));
+      }
       q = hcnt[0];
     } else {
       // count exchange (the reference reads the peers' managed counters)
@@ -550,7 +592,6 @@ RunResult Engine::run_ref(int64_t source) {
       be_.to_host(hrc.data(), bucket_cnt_.data() + P, static_cast<size_t>(P) * sizeof(int64_t));
       int64_t tot = 0;
       for (int r = 0; r < P; ++r) {
-        sd[r] = r * cap;
         rd[r] = tot;
         tot += hrc[r];
       }
@@ -570,7 +611,7 @@ RunResult Engine::run_ref(int64_t source) {
     }
     LevelRecord rec;
     rec.level = L;
-    rec.direction = 'R';
+    rec.direction = scan ? 'C' : 'R';
     rec.frontier = total_q;
     total_q = exchange() ? comm_.sum_host(q) : q;
     rec.discovered = total_q;

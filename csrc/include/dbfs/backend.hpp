@@ -214,6 +214,28 @@ struct RefAcceptArgs {
   int64_t* qcount = nullptr;
 };
 
+// Scan-mode BFS (the reference's single-GPU "scan" pipeline nextLayer /
+// countDegrees / scanDegrees / assignVerticesNextQueue, bfs.cu:706-781 and
+// H16c in SURVEY.md): an atomic-free frontier build.  relax writes
+// dist[v] = next_level and claim[v] = e (shard-local edge index, last writer
+// wins) with plain stores; count gives every frontier vertex i, per owner o,
+// the number of edges e it won (offs[o * q + i]); an exclusive scan turns the
+// counts into an owner-major output layout; assign writes the children there.
+struct ScanBfsArgs {
+  ShardView g;
+  const vid_t* queue = nullptr;  // global ids of owned frontier vertices
+  int64_t q = 0;
+  lvl_t next_level = 0;
+  lvl_t* dist = nullptr;         // replicated, n entries
+  eid_t* claim = nullptr;        // replicated, n entries (no reset needed)
+  int64_t part = 0;              // owner(v) = v / part
+  int nranks = 1;
+  eid_t* offs = nullptr;         // nranks * q + 1 entries
+  eid_t* bounds = nullptr;       // scan_bounds: offs[o * q] for o in [0, nranks]
+  int64_t* counts = nullptr;     // scan_bounds: per-owner child counts
+  vid_t* out = nullptr;          // children, owner-major
+};
+
 // Graph500-style validation of a full level array against a shard: counts
 // violations of (a) |level[u] - level[v]| <= 1 over every edge with both ends
 // reached, (b) reached-unreached edges, (c) reached v != src without a
@@ -274,6 +296,10 @@ class Backend {
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;
   virtual void ref_expand(const RefExpandArgs& a) = 0;
   virtual void ref_accept(const RefAcceptArgs& a) = 0;
+  virtual void scan_relax(const ScanBfsArgs& a) = 0;
+  virtual void scan_count(const ScanBfsArgs& a) = 0;   // then exclusive_scan(offs, nranks * q)
+  virtual void scan_bounds(const ScanBfsArgs& a) = 0;
+  virtual void scan_assign(const ScanBfsArgs& a) = 0;  // consumes offs
   virtual void validate_levels(const ValidateArgs& a) = 0;
   virtual void compute_parents(const ParentArgs& a) = 0;
 

@@ -25,7 +25,7 @@
 
 namespace dbfs {
 
-enum class Mode { Ref, TopDown, BottomUp, DirOpt, Simple };
+enum class Mode { Ref, TopDown, BottomUp, DirOpt, Simple, Scan };
 Mode parse_mode(const std::string& s);
 const char* mode_name(Mode m);
 
@@ -91,7 +91,7 @@ struct EngineOptions {
 
 struct LevelRecord {
   int level = 0;
-  char direction = 'T';       // 'T' top-down, 'B' bottom-up, 'R' reference, 'S' simple
+  char direction = 'T';  // 'T' top-down, 'B' bottom-up, 'R' reference, 'S' simple, 'C' scan
   int64_t frontier = 0;       // global frontier vertices expanded at this level
   int64_t frontier_edges = 0; // global sum of their degrees
   int64_t discovered = 0;     // global new vertices
@@ -158,6 +158,7 @@ class Engine {
   DBuf<lvl_t> dist_;
   DBuf<vid_t> queue_, buckets_, recvq_;
   DBuf<int64_t> bucket_cnt_, qcount_;
+  DBuf<eid_t> claim_, scan_offs_;  // scan mode
 };
 
 }  // namespace dbfs

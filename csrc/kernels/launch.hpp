@@ -25,6 +25,10 @@ void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 // ref_kernels.hip (reference-algorithm mode)
 void ref_expand(const RefExpandArgs& a, hipStream_t st);
 void ref_accept(const RefAcceptArgs& a, hipStream_t st);
+void scan_relax(const ScanBfsArgs& a, hipStream_t st);
+void scan_count(const ScanBfsArgs& a, hipStream_t st);
+void scan_bounds(const ScanBfsArgs& a, hipStream_t st);
+void scan_assign(const ScanBfsArgs& a, hipStream_t st);
 
 // graph_kernels.hip
 void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg, hipStream_t st);

@@ -7,7 +7,7 @@ search, bitmap frontier update, wave-prefix-sum compaction), direction
 optimisation, and an RCCL all-to-all / all-gather frontier exchange over xGMI.
 
 Layout
-  models/    BFS front-ends (the engine modes: ref, td, bu, do, simple)
+  models/    BFS front-ends (the engine modes: ref, td, bu, do, simple, scan)
   ops/       graph construction / generation / oracle operations
   parallel/  partitioning, communicators (RCCL, virtual ranks, torch.distributed)
   utils/     file I/O, Graph500 root sampling, GTEPS accounting, validation

@@ -7,5 +7,7 @@ traversal algorithms the engine implements:
   bu      bottom-up parent search every level
   do      direction-optimising (Beamer alpha/beta switch between td and bu)
   simple  vertex-centric status-array scan (the reference's dead multiBfs)
+  scan    atomic-free queue build: relax / count / prefix-scan / assign (the
+          reference's driver-API "scan" pipeline, bfs.cu:706-781)
 """
 from .bfs import BFS, BFSResult, MODES  # noqa: F401

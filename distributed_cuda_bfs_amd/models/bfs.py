@@ -15,7 +15,7 @@ import numpy as np
 from .._native import N
 from ..parallel.runtime import Runtime, init_runtime
 
-MODES = ("ref", "td", "bu", "do", "simple")
+MODES = ("ref", "td", "bu", "do", "simple", "scan")
 
 
 @dataclass
