@@ -7,6 +7,7 @@
 // comma-expression idiom that discards them (bfs.cu:336-351, D3).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -83,21 +84,42 @@ class HipBackend final : public Backend {
     if (bytes && bytes <= kPinned) {
       // small (per-level statistics) copies: DMA into pinned memory, no staging
       HIP_CHECK(hipMemcpyAsync(pinned_, s, bytes, hipMemcpyDeviceToHost, st_));
-      HIP_CHECK(hipStreamSynchronize(st_));
+      wait_stream();
       std::memcpy(d, pinned_, bytes);
       return;
     }
     if (bytes) HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st_));
-    HIP_CHECK(hipStreamSynchronize(st_));
+    wait_stream();
   }
   void to_device(void* d, const void* s, size_t bytes) override {
     on();
     if (bytes) HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st_));
-    HIP_CHECK(hipStreamSynchronize(st_));
+    wait_stream();
   }
   void synchronize() override {
     on();
-    HIP_CHECK(hipStreamSynchronize(st_));
+    wait_stream();
+  }
+
+  // Blocking wait on the stream.  With a wait watch installed (RCCL), poll so
+  // the watch can inspect the communicator while a collective is in flight.
+  void wait_stream() {
+    if (!wait_watch_) {
+      HIP_CHECK(hipStreamSynchronize(st_));
+      return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    double next = wait_period_;
+    for (;;) {
+      const hipError_t e = hipStreamQuery(st_);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+      const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (waited >= next) {
+        wait_watch_(waited);
+        next = waited + wait_period_;
+      }
+    }
   }
 
   int record_event() override {

@@ -145,7 +145,10 @@ struct RankCtx {
   std::unique_ptr<Engine> engine;
 };
 
-void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCtx&)>& fn) {
+// One thread per local rank.  A rank that throws aborts the virtual group so
+// its peers fail at their next collective instead of waiting forever.
+void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCtx&)>& fn,
+               VirtualGroup* group = nullptr) {
   if (ranks.size() == 1) {
     fn(0, ranks[0]);
     return;
@@ -156,8 +159,12 @@ void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCt
     th.emplace_back([&, r] {
       try {
         fn(static_cast<int>(r), ranks[r]);
+      } catch (const std::exception& e) {
+        errs[r] = std::current_exception();
+        if (group) group->abort("rank " + std::to_string(r) + ": " + e.what());
       } catch (...) {
         errs[r] = std::current_exception();
+        if (group) group->abort("rank " + std::to_string(r) + " failed");
       }
     });
   for (auto& t : th) t.join();
@@ -277,9 +284,15 @@ int main(int argc, char** argv) {
     if (multiproc) {
       const char* addr = std::getenv("MASTER_ADDR");
       const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
-      TcpBootstrap boot(addr ? addr : "127.0.0.1", port, wrank, world);
-      std::string uid = boot.broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
-      ranks[0].comm = std::make_unique<NcclComm>(uid, wrank, world, *ranks[0].be);
+      auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
+      const char* cm = std::getenv("DBFS_COMM");
+      if (a.cpu || (cm && std::string(cm) == "tcp")) {
+        // host transport (CPU ranks, or GPU ranks without RCCL)
+        ranks[0].comm = std::make_unique<TcpComm>(boot, *ranks[0].be);
+      } else {
+        std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+        ranks[0].comm = std::make_unique<NcclComm>(uid, wrank, world, *ranks[0].be);
+      }
     } else if (vgroup) {
       for (int i = 0; i < P; ++i) ranks[i].comm = std::make_unique<VirtualComm>(vgroup, i, *ranks[i].be);
     } else if (P > 1) {
@@ -303,7 +316,7 @@ int main(int argc, char** argv) {
       else rc.graph = DeviceGraph::from_host(*rc.be, full, part, rk);
       if (a.hub_sort) rc.graph->sort_neighbors_by_degree(*rc.comm);
       rc.engine = std::make_unique<Engine>(*rc.graph, *rc.comm, eo);
-    });
+    }, vgroup.get());
 
     // ---- the reference's single run from <src> ----
     std::vector<RunResult> res(static_cast<size_t>(nlocal));
@@ -315,7 +328,7 @@ int main(int argc, char** argv) {
       std::vector<lvl_t> lv = rc.engine->gather_levels();
       if (i == 0) got = std::move(lv);
       if (a.validate) viol[i] = rc.engine->validate(a.src);
-    });
+    }, vgroup.get());
     if (ref_lines) std::printf("Elapsed time in milliseconds : %li ms.\n", static_cast<long>(res[0].ms));
     int rc_exit = 0;
     if (leader && !expected.empty()) {
@@ -366,7 +379,7 @@ int main(int argc, char** argv) {
       double inv_sum = 0, ms_sum = 0;
       int64_t e_sum = 0;
       for (int64_t root : roots) {
-        run_ranks(ranks, [&](int i, RankCtx& rc) { res[i] = rc.engine->run(root); });
+        run_ranks(ranks, [&](int i, RankCtx& rc) { res[i] = rc.engine->run(root); }, vgroup.get());
         inv_sum += res[0].gteps > 0 ? 1.0 / res[0].gteps : 0;
         ms_sum += res[0].ms;
         e_sum += res[0].edges;

@@ -5,11 +5,19 @@
 // on a single GPU or on the CPU, which the reference cannot do (its multi-GPU
 // path needs >= 2 real GPUs with peer access).
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <vector>
 
 #include "dbfs/comm.hpp"
 
 namespace dbfs {
+
+double comm_timeout_s() {
+  const char* e = std::getenv("DBFS_COMM_TIMEOUT_S");
+  if (!e || !*e) return 600.0;
+  return std::max(0.0, std::atof(e));
+}
 
 int64_t* Comm::scratch(size_t n) {
   DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
@@ -59,14 +67,40 @@ VirtualGroup::VirtualGroup(int nranks) : n_(nranks), slots_(static_cast<size_t>(
 
 void VirtualGroup::barrier() {
   std::unique_lock<std::mutex> lk(mu_);
+  if (aborted_) throw Error("virtual rank group aborted: " + reason_);
   const uint64_t gen = generation_;
   if (++arrived_ == n_) {
     arrived_ = 0;
     ++generation_;
     cv_.notify_all();
-  } else {
-    cv_.wait(lk, [&] { return generation_ != gen; });
+    return;
   }
+  auto done = [&] { return generation_ != gen || aborted_; };
+  const double limit = comm_timeout_s();
+  if (limit > 0) {
+    if (!cv_.wait_for(lk, std::chrono::duration<double>(limit), done)) {
+      aborted_ = true;
+      reason_ = "barrier timed out after " + std::to_string(limit) + " s (a rank stopped participating)";
+      cv_.notify_all();
+    }
+  } else {
+    cv_.wait(lk, done);
+  }
+  if (generation_ == gen) throw Error("virtual rank group aborted: " + reason_);
+}
+
+void VirtualGroup::abort(const std::string& reason) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!aborted_) {
+    aborted_ = true;
+    reason_ = reason;
+  }
+  cv_.notify_all();
+}
+
+bool VirtualGroup::aborted() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return aborted_;
 }
 
 VirtualComm::VirtualComm(std::shared_ptr<VirtualGroup> g, int rank, Backend& be) : g_(std::move(g)), rank_(rank) {

@@ -55,6 +55,28 @@ NcclComm::NcclComm(const std::string& uid, int rank, int nranks, Backend& be) : 
   ncclComm_t c = nullptr;
   NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
   comm_ = c;
+  install_watchdog();
+}
+
+// Failure detection: while the host waits on the stream, poll
+// ncclCommGetAsyncError and bound the wait by comm_timeout_s(); on either, the
+// communicator is aborted (ncclCommAbort releases the stuck kernels) and the
+// wait throws, so a dead or hung peer ends the run with an error.
+void NcclComm::install_watchdog() {
+  const double limit = comm_timeout_s();
+  be_->set_wait_watch([this, limit](double waited) {
+    if (!comm_) return;
+    ncclResult_t st = ncclSuccess;
+    ncclCommGetAsyncError(C(comm_), &st);
+    std::string why;
+    if (st != ncclSuccess && st != ncclInProgress) why = std::string("RCCL async error: ") + ncclGetErrorString(st);
+    else if (limit > 0 && waited > limit)
+      why = "RCCL collective did not complete within " + std::to_string(limit) + " s (DBFS_COMM_TIMEOUT_S)";
+    if (why.empty()) return;
+    ncclCommAbort(C(comm_));
+    comm_ = nullptr;
+    throw Error(why + " on rank " + std::to_string(rank_));
+  });
 }
 
 std::vector<std::unique_ptr<NcclComm>> NcclComm::init_all(const std::vector<Backend*>& bes) {
@@ -73,32 +95,42 @@ std::vector<std::unique_ptr<NcclComm>> NcclComm::init_all(const std::vector<Back
     c->rank_ = i;
     c->size_ = n;
     c->bind_backend(bes[i]);
+    c->install_watchdog();
     out.push_back(std::move(c));
   }
   return out;
 }
 
 NcclComm::~NcclComm() {
+  if (be_) be_->set_wait_watch(nullptr);
   if (comm_) ncclCommDestroy(C(comm_));
 }
 
+void NcclComm::check_alive() const {
+  DBFS_CHECK(comm_ != nullptr, "RCCL communicator was aborted after a failure");
+}
+
 void NcclComm::alltoall(const void* send, void* recv, size_t bytes) {
+  check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allgather(const void* send, void* recv, size_t bytes) {
+  check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, C(comm_), S(be_)));
 }
 
 void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                          const int64_t* rd, size_t eb) {
+  check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclGroupStart());
   for (int r = 0; r < size_; ++r) {

@@ -8,7 +8,9 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -37,9 +39,26 @@ void read_all(int fd, void* p, size_t n) {
   while (n) {
     ssize_t k = ::recv(fd, c, n, 0);
     if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) throw Error("bootstrap peer closed the connection");
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
+      throw Error("bootstrap peer timed out after " + std::to_string(comm_timeout_s()) +
+                  " s (DBFS_COMM_TIMEOUT_S); a rank stopped participating");
+    if (k <= 0) throw Error("bootstrap peer closed the connection (a rank failed)");
     c += k;
     n -= static_cast<size_t>(k);
+  }
+}
+
+// Connected sockets: no Nagle, and a receive timeout so a hung peer turns into
+// an error (failure detection).
+void tune_socket(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  const double t = comm_timeout_s();
+  if (t > 0) {
+    timeval tv{};
+    tv.tv_sec = static_cast<time_t>(t);
+    tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
   }
 }
 
@@ -93,9 +112,15 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
     if (::listen(listen_fd_, nranks) != 0) throw Error("bootstrap listen failed");
     peers_.assign(static_cast<size_t>(nranks), -1);
     for (int k = 1; k < nranks; ++k) {
+      const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+      pollfd pfd{listen_fd_, POLLIN, 0};
+      const int pr = left.count() > 0 ? ::poll(&pfd, 1, static_cast<int>(left.count())) : 0;
+      if (pr <= 0)
+        throw Error("bootstrap: only " + std::to_string(k - 1) + " of " + std::to_string(nranks - 1) +
+                    " peers connected within " + std::to_string(timeout_s) + " s");
       int fd = ::accept(listen_fd_, nullptr, nullptr);
       if (fd < 0) throw Error("bootstrap accept failed");
-      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      tune_socket(fd);
       int32_t r = -1;
       read_all(fd, &r, sizeof(r));
       if (r <= 0 || r >= nranks || peers_[r] != -1) throw Error("bootstrap got bad rank " + std::to_string(r));
@@ -113,8 +138,7 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
         throw Error("bootstrap connect to " + host + ":" + std::to_string(port) + " timed out");
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }
-    int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    tune_socket(fd);
     const int32_t r = rank;
     write_all(fd, &r, sizeof(r));
     peers_.assign(1, fd);

@@ -14,7 +14,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "dbfs/engine.hpp"
@@ -168,7 +170,7 @@ void DeviceGraph::build_heads() {
 // ---- Engine ----------------------------------------------------------------------
 
 Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
-    : g_(g), comm_(comm), be_(g.backend()), opt_(opt), part_(g.partition()) {
+    : g_(g), comm_(comm), be_(g.backend()), opt_(opt), part_(g.partition()), fault_(FaultSpec::from_env()) {
   DBFS_CHECK(comm.size() == part_.nranks, "communicator size does not match the partition");
   DBFS_CHECK(comm.rank() == g.rank(), "communicator rank does not match the shard");
   comm_.bind_backend(&be_);
@@ -178,6 +180,50 @@ Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
 }
 
 Engine::~Engine() = default;
+
+// ---- fault injection -------------------------------------------
+// DBFS_FAULT_INJECT="rank=R,level=L[,kind=throw|exit|hang]" makes rank R fail
+// at the start of level L of every run: `throw` raises an Error (in-process
+// ranks abort their group), `exit` ends the process with status 17 (a crashed
+// rank), `hang` stops participating (peers must time out).  Used by the
+// failure-detection tests; unset in normal runs.
+FaultSpec FaultSpec::from_env() {
+  FaultSpec f;
+  const char* e = std::getenv("DBFS_FAULT_INJECT");
+  if (!e || !*e) return f;
+  std::string s(e);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t comma = s.find(',', pos);
+    if (comma == std::string::npos) comma = s.size();
+    const std::string kv = s.substr(pos, comma - pos);
+    const size_t eq = kv.find('=');
+    DBFS_CHECK(eq != std::string::npos, "DBFS_FAULT_INJECT: expected key=value, got '" + kv + "'");
+    const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    if (k == "rank") f.rank = std::stoi(v);
+    else if (k == "level") f.level = std::stoi(v);
+    else if (k == "kind") f.kind = v;
+    else DBFS_CHECK(false, "DBFS_FAULT_INJECT: unknown key '" + k + "'");
+    pos = comma + 1;
+  }
+  DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang",
+             "DBFS_FAULT_INJECT: kind must be throw|exit|hang");
+  return f;
+}
+
+void Engine::inject_fault(int level) {
+  if (fault_.rank != comm_.rank() || fault_.level != level) return;
+  const std::string what = "injected fault (" + fault_.kind + ") at level " + std::to_string(level) + " on rank " +
+                           std::to_string(fault_.rank);
+  std::fprintf(stderr, "[dbfs] %s\n", what.c_str());
+  std::fflush(stderr);
+  if (fault_.kind == "exit") std::_Exit(17);
+  if (fault_.kind == "hang") {
+    // bounded, so an unattended run still ends eventually
+    for (int i = 0; i < 3600; ++i) std::this_thread::sleep_for(std::chrono::seconds(1));
+  }
+  throw Error(what);
+}
 
 void Engine::alloc_bitmap_state() {
   if (bitmap_ready_) return;
@@ -361,6 +407,7 @@ RunResult Engine::run_bitmap(int64_t source) {
   if (n_f > 0) publish(dir);
   lvl_t L = 0;
   while (n_f > 0) {
+    inject_fault(L);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
@@ -536,6 +583,7 @@ RunResult Engine::run_ref(int64_t source) {
       rd(static_cast<size_t>(P)), hbuf(static_cast<size_t>(3 * P + 1));
   const bool scan = opt_.mode == Mode::Scan;
   while (total_q > 0) {
+    inject_fault(L);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
     if (scan) {
       // relax -> count -> scan -> bounds -> assign: children land owner-major in

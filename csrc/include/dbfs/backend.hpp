@@ -15,6 +15,7 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <memory>
 #include <string>
 #include <utility>
@@ -267,6 +268,15 @@ class Backend {
   virtual int device_id() const { return -1; }
   virtual void* stream_handle() { return nullptr; }
 
+  // Host waits on the device (to_host, to_device, synchronize) call
+  // watch(seconds waited) about every period_s while the stream is still busy;
+  // the watch may throw to abandon the wait.  A communicator installs one to
+  // turn a dead peer into an error instead of a hang.
+  void set_wait_watch(std::function<void(double)> watch, double period_s = 0.05) {
+    wait_watch_ = std::move(watch);
+    wait_period_ = period_s;
+  }
+
   // memory (alloc/free are synchronous; copies/memsets are stream-ordered)
   virtual void* alloc(size_t bytes) = 0;
   virtual void dealloc(void* p) = 0;
@@ -319,6 +329,10 @@ class Backend {
   virtual void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) = 0;
   // sum of degrees of vertices with level != kUnreached (device scalar out)
   virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
+
+ protected:
+  std::function<void(double)> wait_watch_;
+  double wait_period_ = 0.05;
 };
 
 std::unique_ptr<Backend> make_cpu_backend();

@@ -30,6 +30,11 @@
 
 namespace dbfs {
 
+// Failure detection: a collective that waits longer than this
+// for its peers fails with an error instead of hanging.  DBFS_COMM_TIMEOUT_S,
+// default 600 s; 0 disables the limit.
+double comm_timeout_s();
+
 class Comm {
  public:
   virtual ~Comm() = default;
@@ -91,7 +96,12 @@ class VirtualGroup {
  public:
   explicit VirtualGroup(int nranks);
   int size() const { return n_; }
+  // Throws if the group was aborted (a rank failed) or the wait exceeds
+  // comm_timeout_s().
   void barrier();
+  // Mark the group failed and wake every waiting rank (they throw).
+  void abort(const std::string& reason);
+  bool aborted() const;
   struct Slot {
     const void* send = nullptr;
     void* recv = nullptr;
@@ -104,10 +114,12 @@ class VirtualGroup {
 
  private:
   int n_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::condition_variable cv_;
   int arrived_ = 0;
   uint64_t generation_ = 0;
+  bool aborted_ = false;
+  std::string reason_;
   std::vector<Slot> slots_;
   std::vector<double> scratch_;
 };
@@ -154,6 +166,8 @@ class NcclComm final : public Comm {
 
  private:
   NcclComm() = default;
+  void install_watchdog();
+  void check_alive() const;
   void* comm_ = nullptr;  // ncclComm_t
   int rank_ = 0, size_ = 1;
 };

@@ -108,6 +108,13 @@ struct RunResult {
   std::vector<LevelRecord> levels;
 };
 
+// Fault injection for failure-detection tests (see Engine::inject_fault).
+struct FaultSpec {
+  int rank = -1, level = -1;
+  std::string kind = "throw";
+  static FaultSpec from_env();
+};
+
 class Engine {
  public:
   Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt = {});
@@ -135,12 +142,14 @@ class Engine {
   void alloc_ref_state();
   void gather_levels_device(DBuf<lvl_t>& full);
   bool exchange() const { return part_.nranks > 1 || opt_.force_exchange; }
+  void inject_fault(int level);
 
   DeviceGraph& g_;
   Comm& comm_;
   Backend& be_;
   EngineOptions opt_;
   Partition part_;
+  FaultSpec fault_;
   int64_t total_directed_ = 0;
 
   DBuf<lvl_t> level_;

@@ -248,7 +248,9 @@ PYBIND11_MODULE(_dbfs_native, m) {
       py::keep_alive<0, 1>());
   py::class_<VirtualGroup, std::shared_ptr<VirtualGroup>>(m, "VirtualGroup")
       .def(py::init<int>())
-      .def_property_readonly("size", &VirtualGroup::size);
+      .def_property_readonly("size", &VirtualGroup::size)
+      .def("abort", &VirtualGroup::abort, py::arg("reason"))
+      .def_property_readonly("aborted", &VirtualGroup::aborted);
   m.def(
       "virtual_comm",
       [](std::shared_ptr<VirtualGroup> g, int rank, std::shared_ptr<Backend> be) {

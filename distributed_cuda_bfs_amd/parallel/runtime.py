@@ -105,13 +105,17 @@ def run_virtual_ranks(nranks: int, fn: Callable[[Runtime], Any], device: str = "
             out[r] = fn(rts[r])
         except BaseException as e:  # noqa: BLE001 - re-raised below
             errs[r] = e
+            # wake the peers blocked in a collective (they raise too)
+            group.abort(f"rank {r}: {e}")
 
     th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
     for t in th:
         t.start()
     for t in th:
         t.join()
-    for e in errs:
-        if e is not None:
-            raise e
+    # report the root cause: the first rank whose failure was not a peer abort
+    first = [e for e in errs if e is not None]
+    if first:
+        roots = [e for e in first if "virtual rank group aborted" not in str(e)]
+        raise (roots or first)[0]
     return out
