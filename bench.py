@@ -53,6 +53,8 @@ def main() -> int:
     ap.add_argument("--alpha", type=float, default=24.0)
     ap.add_argument("--beta", type=float, default=24.0)
     ap.add_argument("--bu-lane-limit", type=int, default=8)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine tuning option (see Engine.get_options()), repeatable")
     ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--baseline-gteps", type=float, default=None)
@@ -78,6 +80,9 @@ def main() -> int:
     t0 = time.time()
     bfs = dbfs.BFS(params, rt, mode=args.mode, alpha=args.alpha, beta=args.beta,
                    bu_lane_limit=args.bu_lane_limit)
+    for kv in args.opt:
+        name, _, val = kv.partition("=")
+        bfs.engine.set_option(name, float(val))
     rt.backend.synchronize()
     rt.barrier()
     gen_s = time.time() - t0

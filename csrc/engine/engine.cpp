@@ -46,6 +46,33 @@ const char* mode_name(Mode m) {
   return "?";
 }
 
+void set_engine_option(EngineOptions& o, const std::string& name, double v) {
+  if (name == "alpha") o.alpha = v;
+  else if (name == "beta") o.beta = v;
+  else if (name == "bu_lane_limit") o.bu_lane_limit = static_cast<int>(v);
+  else if (name == "td_byte_edges") o.td_byte_edges = static_cast<int64_t>(v);
+  else if (name == "td_check_visited_min") o.td_check_visited_min = v;
+  else if (name == "td_wide_below_blocks") o.td_wide_below_blocks = static_cast<int64_t>(v);
+  else if (name == "sparse_max_edges") o.sparse_max_edges = static_cast<int64_t>(v);
+  else if (name == "sparse_size_check") o.sparse_size_check = v != 0;
+  else if (name == "force_exchange") o.force_exchange = v != 0;
+  else if (name == "phase_timing") o.phase_timing = v != 0;
+  else throw Error("unknown engine option '" + name + "'");
+}
+
+std::vector<std::pair<std::string, double>> engine_option_map(const EngineOptions& o) {
+  return {{"alpha", o.alpha},
+          {"beta", o.beta},
+          {"bu_lane_limit", o.bu_lane_limit},
+          {"td_byte_edges", static_cast<double>(o.td_byte_edges)},
+          {"td_check_visited_min", o.td_check_visited_min},
+          {"td_wide_below_blocks", static_cast<double>(o.td_wide_below_blocks)},
+          {"sparse_max_edges", static_cast<double>(o.sparse_max_edges)},
+          {"sparse_size_check", o.sparse_size_check ? 1.0 : 0.0},
+          {"force_exchange", o.force_exchange ? 1.0 : 0.0},
+          {"phase_timing", o.phase_timing ? 1.0 : 0.0}};
+}
+
 // ---- DeviceGraph ----------------------------------------------------------------
 
 std::unique_ptr<DeviceGraph> DeviceGraph::from_host(Backend& be, const HostCSR& csr, const Partition& part,
@@ -467,8 +494,10 @@ RunResult Engine::run_bitmap(int64_t source) {
               be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
             }
             ta.next_bytes = next_bytes_.data();
+            ta.check_visited = static_cast<double>(vis_deg) >= opt_.td_check_visited_min * static_cast<double>(total_directed_);
             bytes_mode = true;
           }
+          ta.wide_below_blocks = opt_.td_wide_below_blocks;
           be_.td_expand(ta);
         }
       } else {

@@ -132,6 +132,10 @@ struct TdArgs {
   vid_t* lists = nullptr;
   int64_t list_cap = 0;
   int64_t part = 0;   // owner(v) = v / part
+  // Byte mode only: skip the visited pre-check (few vertices visited yet).
+  bool check_visited = true;
+  // Launch 1024-thread workgroups when the grid has fewer blocks than this.
+  int64_t wide_below_blocks = 0;
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)

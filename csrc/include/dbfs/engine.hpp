@@ -16,6 +16,7 @@
 
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dbfs/backend.hpp"
@@ -76,6 +77,11 @@ struct EngineOptions {
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;
+  // Byte-map levels skip the visited pre-check while the visited vertices
+  // hold less than this fraction of all adjacency entries.
+  double td_check_visited_min = 0.02;
+  // Top-down grids of fewer workgroups than this use 1024-thread workgroups.
+  int64_t td_wide_below_blocks = 2048;
   // Multi-rank top-down levels whose global frontier has at most this many
   // edges exchange owner lists instead of bitmap slices.
   int64_t sparse_max_edges = int64_t(1) << 17;
@@ -88,6 +94,12 @@ struct EngineOptions {
   // call on a single GPU (tests).
   bool force_exchange = false;
 };
+
+// Named access to the numeric tuning options (alpha, beta, bu_lane_limit,
+// td_byte_edges, td_wide_below_blocks, td_check_visited_min, sparse_max_edges,
+// sparse_size_check, force_exchange, phase_timing); throws on unknown names.
+void set_engine_option(EngineOptions& o, const std::string& name, double value);
+std::vector<std::pair<std::string, double>> engine_option_map(const EngineOptions& o);
 
 struct LevelRecord {
   int level = 0;

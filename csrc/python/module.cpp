@@ -497,5 +497,13 @@ PYBIND11_MODULE(_dbfs_native, m) {
           },
           py::arg("alpha"), py::arg("beta"), py::arg("lane_limit"), py::arg("td_byte_edges") = -1,
           py::arg("sparse_max_edges") = -1, py::arg("sparse_size_check") = -1)
-      .def_property_readonly("td_byte_edges", [](const Engine& e) { return e.options().td_byte_edges; });
+      .def_property_readonly("td_byte_edges", [](const Engine& e) { return e.options().td_byte_edges; })
+      // Generic tuning knob access (bench.py --opt NAME=VALUE, sweeps).
+      .def("set_option",
+           [](Engine& e, const std::string& name, double v) {
+             EngineOptions o = e.options();
+             set_engine_option(o, name, v);
+             e.set_options(o);
+           })
+      .def("get_options", [](const Engine& e) { return engine_option_map(e.options()); });
 }

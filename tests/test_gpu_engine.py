@@ -12,7 +12,7 @@ from distributed_cuda_bfs_amd.parallel.runtime import run_virtual_ranks
 
 pytestmark = pytest.mark.gpu
 
-MODES = ["do", "td", "bu", "ref", "simple"]
+MODES = ["do", "td", "bu", "ref", "simple", "scan"]
 
 
 def _check(bfs, csr, src):
@@ -168,7 +168,11 @@ def test_rccl_and_virtual_comm_patterns_gpu(gpu_runtime):
 
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("mode", ["td", "do"])
-def test_td_byte_map_mode_gpu(P, mode):
+@pytest.mark.parametrize("knobs", [{}, {"td_check_visited_min": 2.0, "td_wide_below_blocks": 1 << 30},
+                                   {"td_check_visited_min": 0.0, "td_wide_below_blocks": 0}])
+def test_td_byte_map_mode_gpu(P, mode, knobs):
+    # byte map on every top-down level; with / without the visited pre-check,
+    # 256- and 1024-thread workgroups
     p = dbfs.rmat_params(16, 16, 29)
     csr = dbfs.host_csr_from_params(p)
     srcs = [0, 5, 40000]
@@ -177,6 +181,8 @@ def test_td_byte_map_mode_gpu(P, mode):
     def body(rt):
         bfs = dbfs.BFS(p, rt, mode=mode)
         bfs.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+        for k, v in knobs.items():
+            bfs.engine.set_option(k, v)
         out = []
         for s in srcs:
             bfs.run(s)
