@@ -56,12 +56,17 @@ class CpuBackend final : public Backend {
   void set_bit(word_t* bm, int64_t bit) override { bm[bit >> 6] |= 1ull << (bit & 63); }
 
   void update_frontier(const UpdateArgs& a) override {
+    bool use_bytes = a.cand_bytes != nullptr;
+    if (a.ctrl) {
+      if (a.ctrl->done || a.ctrl->dir != 'T') return;
+      use_bytes = a.ctrl->bytes != 0;
+    }
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
       int64_t cnt = 0, deg = 0;
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
-        if (a.cand_bytes) {
+        if (use_bytes) {
           c = gather_bytes(a.cand_bytes + w * 64);
         } else {
           for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
@@ -85,7 +90,17 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override { *c = init; }
+  void* alloc_mapped(size_t bytes, void** dptr) override {
+    void* h = std::calloc(1, std::max<size_t>(bytes, 1));
+    DBFS_CHECK(h != nullptr, "host allocation failed");
+    *dptr = h;
+    return h;
+  }
+  void free_mapped(void* h) override { std::free(h); }
+
   void scan_units(const ScanArgs& a) override {
+    if (a.ctrl && a.ctrl->done) return;
     const int64_t nchunks = div_up(a.nunits, kScanChunk);
     int64_t c = 0, d = 0;
     for (int64_t k = 0; k < nchunks; ++k) {
@@ -105,6 +120,14 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = c;
     a.stats[1] = a.stats[3] = d;
     a.qscan[c] = d;
+    if (a.ctrl) {
+      level_ctrl_finish(*a.ctrl, c, d, a.seed, a.seed ? nullptr : a.rec + a.level);
+      if (a.mailbox) {
+        a.mailbox->done = a.ctrl->done;
+        a.mailbox->vis_deg = a.ctrl->vis_deg;
+        a.mailbox->level = a.level;
+      }
+    }
   }
 
   void zero_degree_mask(const ZeroDegArgs& a) override {
@@ -119,6 +142,7 @@ class CpuBackend final : public Backend {
   }
 
   void compact_frontier(const CompactArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T')) return;
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
       int64_t pos = a.unit_cnt_off[u] + a.part_cnt[u / kScanChunk];
@@ -143,7 +167,14 @@ class CpuBackend final : public Backend {
   }
 
   void td_expand(const TdArgs& a) override {
-    for (int64_t i = 0; i < a.q; ++i) {
+    int64_t q = a.q;
+    bool bytes = a.next_bytes != nullptr;
+    if (a.ctrl) {
+      if (a.ctrl->done || a.ctrl->dir != 'T') return;
+      q = a.dev_stats[0];
+      bytes = a.ctrl->bytes != 0;
+    }
+    for (int64_t i = 0; i < q; ++i) {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
       for (int64_t k = b; k < e; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
@@ -151,7 +182,7 @@ class CpuBackend final : public Backend {
         if (a.lists) {
           vid_t* list = a.lists + static_cast<int64_t>(v / a.part) * (a.list_cap + 1);
           list[1 + list[0]++] = v;
-        } else if (a.next_bytes) {
+        } else if (bytes) {
           a.next_bytes[v] = 1;
         } else {
           a.next[v >> 6] |= 1ull << (v & 63);
@@ -175,6 +206,7 @@ class CpuBackend final : public Backend {
   }
 
   void bu_step(const BuArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
       int64_t cnt = 0, deg = 0;

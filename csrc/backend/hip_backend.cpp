@@ -100,6 +100,12 @@ class HipBackend final : public Backend {
     on();
     wait_stream();
   }
+  bool stream_idle() override {
+    const hipError_t e = hipStreamQuery(st_);
+    if (e == hipSuccess) return true;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    return false;
+  }
 
   // Blocking wait on the stream.  With a wait watch installed (RCCL), poll so
   // the watch can inspect the communicator while a collective is in flight.
@@ -145,6 +151,25 @@ class HipBackend final : public Backend {
   void set_bit(word_t* bm, int64_t bit) override { on(); kern::set_bit(bm, bit, st_); chk(); }
   void update_frontier(const UpdateArgs& a) override { on(); kern::update_frontier(a, st_); chk(); }
   void scan_units(const ScanArgs& a) override { on(); kern::scan_units(a, st_); chk(); }
+  void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override {
+    on();
+    kern::level_ctrl_init(c, init, st_);
+    chk();
+  }
+  void* alloc_mapped(size_t bytes, void** dptr) override {
+    on();
+    void* h = nullptr;
+    HIP_CHECK(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h, 0, bytes);
+    HIP_CHECK(hipHostGetDevicePointer(dptr, h, 0));
+    return h;
+  }
+  void free_mapped(void* h) override {
+    if (!h) return;
+    on();
+    hipStreamSynchronize(st_);
+    hipHostFree(h);
+  }
   void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }

@@ -57,6 +57,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "sparse_size_check") o.sparse_size_check = v != 0;
   else if (name == "force_exchange") o.force_exchange = v != 0;
   else if (name == "phase_timing") o.phase_timing = v != 0;
+  else if (name == "device_loop") o.device_loop = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -70,7 +71,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"sparse_max_edges", static_cast<double>(o.sparse_max_edges)},
           {"sparse_size_check", o.sparse_size_check ? 1.0 : 0.0},
           {"force_exchange", o.force_exchange ? 1.0 : 0.0},
-          {"phase_timing", o.phase_timing ? 1.0 : 0.0}};
+          {"phase_timing", o.phase_timing ? 1.0 : 0.0},
+          {"device_loop", o.device_loop ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -206,7 +208,9 @@ Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
   be_.fill_level(level_.data(), g.rows(), kUnreached);
 }
 
-Engine::~Engine() = default;
+Engine::~Engine() {
+  if (mailbox_host_) be_.free_mapped(mailbox_host_);
+}
 
 // ---- fault injection -------------------------------------------
 // DBFS_FAULT_INJECT="rank=R,level=L[,kind=throw|exit|hang]" makes rank R fail
@@ -319,7 +323,7 @@ RunResult Engine::run(int64_t source) {
     r.edges = h[1] / 2;
   } else {
     // The bitmap engine already knows sum(deg) of every level's new vertices.
-    r = run_bitmap(source);
+    r = use_device_loop() ? run_bitmap_device(source) : run_bitmap(source);
   }
   r.gteps = r.ms > 0 ? static_cast<double>(r.edges) / (r.ms * 1e6) : 0.0;
   return r;
@@ -581,6 +585,208 @@ RunResult Engine::run_bitmap(int64_t source) {
   res.edges = vis_deg / 2;
   res.reached = 1;
   for (const auto& l : res.levels) res.reached += l.discovered;
+  return res;
+}
+
+bool Engine::use_device_loop() const {
+  return opt_.device_loop && !exchange() &&
+         (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
+}
+
+// Device-driven level loop (one rank).  Same kernels and decisions as
+// run_bitmap, but every level is enqueued as the full predicated chain
+//   compact -> td_expand -> update   (run when ctrl->dir == 'T')
+//   bu_step                          (run when ctrl->dir == 'B')
+//   scan (+ level_ctrl_finish)       (skipped once ctrl->done)
+// and the host enqueues level L+1 before it waits for level L's mailbox stamp:
+// the GPU never idles for a host round trip.  After the frontier empties, the
+// one level enqueued ahead costs a handful of early-exit launches.
+RunResult Engine::run_bitmap_device(int64_t source) {
+  alloc_bitmap_state();
+  TraceRange trace_run(std::string("bfs.run(device loop) mode=") + mode_name(opt_.mode) + " src=" +
+                       std::to_string(source));
+  const int64_t W = part_.slice_words();
+  const int64_t lo = g_.lo();
+  const ShardView gv = g_.view();
+  if (!ctrl_.data()) ctrl_ = DBuf<LevelCtrl>(be_, 1);
+  if (rec_.size() < 64) rec_ = DBuf<LevelRecDev>(be_, 64);
+  if (!mailbox_host_) {
+    void* dptr = nullptr;
+    mailbox_host_ = static_cast<LevelMailbox*>(be_.alloc_mapped(sizeof(LevelMailbox) * kMailboxSlots, &dptr));
+    mailbox_dev_ = static_cast<LevelMailbox*>(dptr);
+  }
+  const bool bytes_ok = opt_.mode != Mode::BottomUp && opt_.td_byte_edges <= total_directed_;
+  if (bytes_ok && !next_bytes_.data()) {
+    next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
+    be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
+  }
+  // the previous run has completed (it ended with a synchronize): stamps can be reset
+  for (int i = 0; i < kMailboxSlots; ++i) {
+    volatile LevelMailbox* mb = mailbox_host_ + i;
+    mb->level = -2;
+  }
+  auto slot = [](int level) { return (level + 1) % kMailboxSlots; };
+  // Wait until level `lv` (-1 = seed) has stamped its mailbox slot.
+  auto wait_stamp = [&](int lv) -> const volatile LevelMailbox* {
+    const volatile LevelMailbox* mb = mailbox_host_ + slot(lv);
+    for (uint64_t spin = 0;; ++spin) {
+      if (__atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) == lv) return mb;
+      if ((spin & 0xFFFF) == 0xFFFF && be_.stream_idle() && __atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) != lv)
+        throw Error("device level loop: level " + std::to_string(lv) + " finished without its mailbox stamp");
+    }
+  };
+
+  RunResult res;
+  res.source = source;
+  be_.reset_events();
+  comm_.barrier();
+  const auto t0 = std::chrono::steady_clock::now();
+
+  be_.fill_level(level_.data(), g_.rows(), kUnreached);
+  be_.copy_async(visited_.data(), zdeg_.data(), visited_.bytes());
+  be_.memset_async(cand_.data(), 0, cand_.bytes());
+  be_.memset_async(next_.data(), 0, next_.bytes());
+  be_.set_bit(cand_.data(), source - lo);
+  LevelCtrl init;
+  init.mode = opt_.mode == Mode::TopDown ? 0 : opt_.mode == Mode::BottomUp ? 1 : 2;
+  init.alpha = opt_.alpha;
+  init.beta = opt_.beta;
+  init.n = static_cast<double>(part_.n);
+  init.total_directed = static_cast<double>(total_directed_);
+  init.td_byte_edges = bytes_ok ? static_cast<double>(opt_.td_byte_edges) : 1e300;
+  init.check_visited_min = opt_.td_check_visited_min;
+  init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
+  be_.level_ctrl_init(ctrl_.data(), init);
+
+  int cur = 0;
+  auto scan = [&](int level, bool seed) {
+    ScanArgs sa;
+    sa.unit_cnt = unit_cnt_.data();
+    sa.unit_deg = unit_deg_.data();
+    sa.nunits = nunits_;
+    sa.part_cnt = part_cnt_.data();
+    sa.part_deg = part_deg_.data();
+    sa.ticket = ticket_.data();
+    sa.stats = stats_.data();
+    sa.qscan = qscan_.data();
+    sa.ctrl = ctrl_.data();
+    sa.rec = rec_.data();
+    sa.mailbox = mailbox_dev_ + slot(level);
+    sa.level = level;
+    sa.seed = seed;
+    be_.scan_units(sa);
+  };
+  UpdateArgs ua;
+  ua.g = gv;
+  ua.cand = cand_.data();
+  ua.nchunks = 1;
+  ua.cand_stride = W;
+  ua.clear_cand = true;
+  ua.force = true;  // the source counts even with degree 0
+  ua.visited = visited_.data();
+  ua.frontier = frontier_[cur ^ 1].data();
+  ua.level = level_.data();
+  ua.new_level = 0;
+  ua.words = W;
+  ua.unit_cnt = unit_cnt_.data();
+  ua.unit_deg = unit_deg_.data();
+  be_.update_frontier(ua);
+  scan(-1, true);
+  cur ^= 1;
+
+  const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), 2048));
+  std::vector<std::pair<int, int>> evs;
+  int nlev = 0;
+  for (int L = 0;; ++L) {
+    inject_fault(L);
+    if (static_cast<size_t>(L) >= rec_.size()) {
+      // grow the record array (stream-ordered copy; the old one is freed after a sync)
+      DBuf<LevelRecDev> bigger(be_, rec_.size() * 2);
+      be_.copy_async(bigger.data(), rec_.data(), rec_.bytes());
+      rec_ = std::move(bigger);
+    }
+    const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    CompactArgs ca;
+    ca.g = gv;
+    ca.frontier = frontier_[cur].data();
+    ca.words = W;
+    ca.unit_cnt_off = unit_cnt_.data();
+    ca.unit_deg_off = unit_deg_.data();
+    ca.part_cnt = part_cnt_.data();
+    ca.part_deg = part_deg_.data();
+    ca.qscan = qscan_.data();
+    ca.qbase = qbase_.data();
+    ca.blk_vstart = blk_vstart_.data();
+    ca.ctrl = ctrl_.data();
+    if (opt_.mode != Mode::BottomUp) {
+      be_.compact_frontier(ca);
+      TdArgs ta;
+      ta.g = gv;
+      ta.qscan = qscan_.data();
+      ta.qbase = qbase_.data();
+      ta.blk_vstart = blk_vstart_.data();
+      ta.visited = visited_.data();
+      ta.next = next_.data();
+      ta.next_bytes = next_bytes_.data();
+      ta.ctrl = ctrl_.data();
+      ta.dev_stats = stats_.data();
+      ta.grid = td_grid;
+      be_.td_expand(ta);
+      UpdateArgs tu = ua;
+      tu.cand = next_.data();
+      tu.cand_bytes = next_bytes_.data();
+      tu.force = false;
+      tu.frontier = frontier_[cur ^ 1].data();
+      tu.new_level = L + 1;
+      tu.ctrl = ctrl_.data();
+      be_.update_frontier(tu);
+    }
+    if (opt_.mode != Mode::TopDown) {
+      BuArgs ba;
+      ba.g = gv;
+      ba.visited = visited_.data();
+      ba.frontier = frontier_[cur].data();
+      ba.new_frontier = frontier_[cur ^ 1].data();
+      ba.level = level_.data();
+      ba.new_level = L + 1;
+      ba.words = W;
+      ba.lane_limit = opt_.bu_lane_limit;
+      ba.unit_cnt = unit_cnt_.data();
+      ba.unit_deg = unit_deg_.data();
+      ba.ctrl = ctrl_.data();
+      be_.bu_step(ba);
+    }
+    scan(L, false);
+    if (opt_.phase_timing) evs.emplace_back(ev0, be_.record_event());
+    cur ^= 1;
+    const volatile LevelMailbox* mb = wait_stamp(L - 1);
+    if (mb->done) {
+      nlev = L;
+      break;
+    }
+  }
+  be_.synchronize();
+  const auto t1 = std::chrono::steady_clock::now();
+  res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  const int64_t vis_deg = mailbox_host_[slot(nlev - 1)].vis_deg;
+
+  // per-level records (outside the timed window)
+  std::vector<LevelRecDev> recs(static_cast<size_t>(nlev));
+  if (nlev > 0) be_.to_host(recs.data(), rec_.data(), recs.size() * sizeof(LevelRecDev));
+  res.reached = 1;
+  for (int L = 0; L < nlev; ++L) {
+    LevelRecord r;
+    r.level = L;
+    r.direction = static_cast<char>(recs[L].dir);
+    r.frontier = recs[L].n_f;
+    r.frontier_edges = recs[L].m_f;
+    r.discovered = recs[L].discovered;
+    if (opt_.phase_timing && static_cast<size_t>(L) < evs.size()) r.ms = be_.elapsed_ms(evs[L].first, evs[L].second);
+    res.reached += r.discovered;
+    res.levels.push_back(r);
+  }
+  res.depth = nlev == 0 ? 1 : nlev;
+  res.edges = vis_deg / 2;
   return res;
 }
 

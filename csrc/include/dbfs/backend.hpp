@@ -55,6 +55,70 @@ constexpr int kTdThreads = 256;
 constexpr int kTdItems = 8;
 constexpr int kTdEdgesPerBlock = kTdThreads * kTdItems;
 
+// ---- device-driven level loop (one rank) -------------------------------------
+// The host enqueues level L+1 before level L has finished; every kernel of a
+// level reads this block at entry and returns at once when the level is not
+// its direction (or the traversal is done).  The scan's last workgroup turns
+// the new frontier's totals into the next level's decision (level_ctrl_finish,
+// the same Beamer switch as the host loop), so no per-level host round trip
+// (~19 us of idle GPU on MI355X: D2H, host wake-up, next launch) remains.
+struct LevelCtrl {
+  // configuration (written once per run)
+  int32_t mode = 2;             // 0 top-down only, 1 bottom-up only, 2 direction-optimising
+  int32_t pad0 = 0;
+  double alpha = 24.0, beta = 24.0;
+  double n = 0.0, total_directed = 0.0;
+  double td_byte_edges = 0.0, check_visited_min = 0.0;
+  // state after the last finished level
+  int32_t dir = 'T';            // direction of the next level
+  int32_t bytes = 0;            // next top-down level writes the byte map
+  int32_t check_visited = 1;    // ... with the visited pre-check
+  int32_t done = 0;             // frontier empty: every later kernel returns
+  int64_t n_f = 0, m_f = 0, prev_nf = 0, vis_deg = 0;
+};
+
+// One record per finished level (device array; read after the run).
+struct LevelRecDev {
+  int32_t dir = 0, pad = 0;
+  int64_t n_f = 0, m_f = 0, discovered = 0;
+};
+
+// Host-visible mailbox slot (pinned, device-mapped), written by the scan's
+// last workgroup of level L into slot L % kMailboxSlots.
+struct LevelMailbox {
+  int32_t level = -2;           // level that wrote this slot
+  int32_t done = 0;
+  int64_t vis_deg = 0;
+};
+constexpr int kMailboxSlots = 8;
+
+// Shared host/device decision logic (also used by the CPU backend).
+DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool seed, LevelRecDev* rec) {
+  if (seed) {
+    c.prev_nf = 0;
+    c.vis_deg = degsum;
+  } else {
+    rec->dir = c.dir;
+    rec->n_f = c.n_f;
+    rec->m_f = c.m_f;
+    rec->discovered = count;
+    c.prev_nf = c.n_f;
+    c.vis_deg += degsum;
+  }
+  c.n_f = count;
+  c.m_f = degsum;
+  c.done = count == 0 ? 1 : 0;
+  if (!c.done && c.mode == 2) {
+    const double m_u = c.total_directed - static_cast<double>(c.vis_deg);
+    if (c.dir == 'T' && static_cast<double>(c.m_f) > m_u / c.alpha && c.n_f > c.prev_nf)
+      c.dir = 'B';
+    else if (c.dir == 'B' && static_cast<double>(c.n_f) < c.n / c.beta && c.n_f < c.prev_nf)
+      c.dir = 'T';
+  }
+  c.bytes = (c.dir == 'T' && static_cast<double>(c.m_f) >= c.td_byte_edges) ? 1 : 0;
+  c.check_visited = static_cast<double>(c.vis_deg) >= c.check_visited_min * c.total_directed ? 1 : 0;
+}
+
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -77,6 +141,9 @@ struct UpdateArgs {
   int64_t words = 0;             // words of the owned slice
   int64_t* unit_cnt = nullptr;   // nunits
   int64_t* unit_deg = nullptr;   // nunits
+  // Device loop: runs only when ctrl->dir == 'T'; reads cand_bytes when
+  // ctrl->bytes, else cand (both given).
+  const LevelCtrl* ctrl = nullptr;
 };
 
 // Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
@@ -93,6 +160,13 @@ struct ScanArgs {
   unsigned* ticket = nullptr;    // zero before the first launch; reset by the last block
   int64_t* stats = nullptr;
   int64_t* qscan = nullptr;
+  // device-driven loop: skip everything when ctrl->done at entry; the last
+  // workgroup runs level_ctrl_finish and fills rec / the mailbox slot
+  LevelCtrl* ctrl = nullptr;
+  LevelRecDev* rec = nullptr;
+  LevelMailbox* mailbox = nullptr;  // device-mapped pinned slot
+  int32_t level = 0;
+  bool seed = false;
 };
 
 // Owned frontier bitmap -> load-balanced top-down work list:
@@ -109,6 +183,7 @@ struct CompactArgs {
   int64_t* qscan = nullptr;
   int64_t* qbase = nullptr;
   int32_t* blk_vstart = nullptr;
+  const LevelCtrl* ctrl = nullptr;  // device loop: runs only when ctrl->dir == 'T'
 };
 
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
@@ -136,6 +211,11 @@ struct TdArgs {
   bool check_visited = true;
   // Launch 1024-thread workgroups when the grid has fewer blocks than this.
   int64_t wide_below_blocks = 0;
+  // Device loop: q / m come from dev_stats[0..1], bits vs bytes and the
+  // visited pre-check from ctrl; the fixed grid loops over the edge blocks.
+  const LevelCtrl* ctrl = nullptr;
+  const int64_t* dev_stats = nullptr;
+  int64_t grid = 0;
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)
@@ -170,6 +250,7 @@ struct BuArgs {
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
+  const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'
 };
 
 // Bits of the owned slice for vertices with degree 0 or beyond the shard
@@ -289,6 +370,12 @@ class Backend {
   virtual void to_host(void* host_dst, const void* dev_src, size_t bytes) = 0;   // blocking
   virtual void to_device(void* dev_dst, const void* host_src, size_t bytes) = 0; // blocking
   virtual void synchronize() = 0;
+  // Non-blocking: true when all enqueued work has completed (raises on a
+  // device error).
+  virtual bool stream_idle() {
+    synchronize();
+    return true;
+  }
 
   // timing: ms between two recorded points (events on HIP)
   virtual int record_event() = 0;
@@ -300,6 +387,11 @@ class Backend {
   virtual void set_bit(word_t* bitmap, int64_t bit) = 0;
   virtual void update_frontier(const UpdateArgs& a) = 0;
   virtual void scan_units(const ScanArgs& a) = 0;
+  // *ctrl = init (stream-ordered)
+  virtual void level_ctrl_init(LevelCtrl* ctrl, const LevelCtrl& init) = 0;
+  // Pinned host memory the device can store to (nullptr-safe free).
+  virtual void* alloc_mapped(size_t bytes, void** device_ptr) = 0;
+  virtual void free_mapped(void* host_ptr) = 0;
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;

@@ -89,6 +89,9 @@ struct EngineOptions {
   // switch this off to exercise the list path on small graphs).
   bool sparse_size_check = true;
   bool phase_timing = false;  // per-level device timing (adds events)
+  // One rank, td/bu/do modes: device-driven level loop (LevelCtrl): the host
+  // enqueues the next level before the current one finishes.
+  bool device_loop = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -149,6 +152,8 @@ class Engine {
 
  private:
   RunResult run_bitmap(int64_t source);
+  RunResult run_bitmap_device(int64_t source);
+  bool use_device_loop() const;
   RunResult run_ref(int64_t source);
   void alloc_bitmap_state();
   void alloc_ref_state();
@@ -174,6 +179,11 @@ class Engine {
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;
   int64_t nunits_ = 0;
+  // device-driven loop state
+  DBuf<LevelCtrl> ctrl_;
+  DBuf<LevelRecDev> rec_;
+  LevelMailbox* mailbox_host_ = nullptr;  // pinned, device-mapped
+  LevelMailbox* mailbox_dev_ = nullptr;
   // reference-mode state
   bool ref_ready_ = false;
   DBuf<lvl_t> dist_;

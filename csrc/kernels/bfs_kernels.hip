@@ -49,6 +49,10 @@ __global__ __launch_bounds__(kBlock) void fill_level_kernel(lvl_t* __restrict__ 
     level[i] = value;
 }
 
+__global__ void ctrl_init_kernel(LevelCtrl* c, LevelCtrl init) {
+  if (threadIdx.x == 0) *c = init;
+}
+
 __global__ void set_bit_kernel(word_t* bm, int64_t bit) {
   if (threadIdx.x == 0) bm[bit >> 6] |= 1ull << (bit & 63);
 }
@@ -123,6 +127,11 @@ __device__ __forceinline__ word_t gather_byte_bits(uint8_t* p) {
 }
 
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
+  bool use_bytes = a.cand_bytes != nullptr;
+  if (a.ctrl) {
+    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    use_bytes = a.ctrl->bytes != 0;
+  }
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   word_t nb = 0;
   if (wl < a.words) {
     word_t c = 0;
-    if (a.cand_bytes) {
+    if (use_bytes) {
       c = gather_byte_bits(a.cand_bytes + wl * 64);
     } else {
       for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
@@ -141,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     nb = a.force ? c : (c & ~vis);
     if (nb) a.visited[wl] = vis | nb;
     a.frontier[wl] = nb;
-    if (a.clear_cand && c) a.cand[wl] = 0;
+    if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
   long long cnt = 0, deg = 0;
   unsigned long long nz = __ballot(nb != 0);
@@ -173,6 +182,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
 __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;
+  if (a.ctrl && a.ctrl->done) return;  // uniform: no block takes a ticket
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
@@ -256,6 +266,18 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     a.stats[1] = a.stats[3] = carry_d;
     a.qscan[carry_c] = carry_d;
     *a.ticket = 0u;  // next launch is stream-ordered after this one
+    if (a.ctrl) {
+      LevelCtrl c = *a.ctrl;
+      level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec + a.level);
+      *a.ctrl = c;
+      if (a.mailbox) {
+        // host-mapped pinned slot: system-scope stores, level last
+        __hip_atomic_store(&a.mailbox->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
+                           static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.mailbox->level, a.level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -265,6 +287,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
 // scan; each set bit's slot from mbcnt and its edge offset from a wave prefix
 // sum of degrees.
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T')) return;
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
@@ -309,95 +332,110 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // then read in 256-lane coalesced sweeps.  A discovered vertex costs one
 // atomicOr only if neither `visited` nor the (possibly stale, only-growing)
 // `next` word already has its bit.
-enum class TdOut { Bits, Bytes, Lists };
+enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->bytes
 
 // kThreads: 256 (8 edges per thread) for big levels; 1024 (2 per thread) when
 // the grid is too small to fill the chip -- 4x the waves in flight to cover the
-// latency of the scattered loads/atomics.
+// latency of the scattered loads/atomics.  The grid may be smaller than the
+// number of edge blocks (device loop: fixed grid): workgroups stride over them.
 template <TdOut kOut, int kThreads>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
+  long long q = a.q, m = a.m;
+  bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
+  if (a.ctrl) {
+    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    bytes = a.ctrl->bytes != 0;
+    check = a.ctrl->check_visited != 0;
+    q = a.dev_stats[0];
+    m = a.dev_stats[1];
+  }
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
-  const long long e0 = static_cast<long long>(blockIdx.x) * kTdEdgesPerBlock;
-  const long long e1 = min(static_cast<long long>(a.m), e0 + kTdEdgesPerBlock);
-  const int cnt = static_cast<int>(e1 - e0);
-  const long long v0 = a.blk_vstart[blockIdx.x];
-  const long long vlast = (blockIdx.x + 1 < gridDim.x) ? a.blk_vstart[blockIdx.x + 1] : a.q - 1;
-  const int nv = static_cast<int>(vlast - v0 + 1);
-
-#pragma unroll
-  for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
-  __syncthreads();
-  // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
-  for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
-    const long long qs = a.qscan[v0 + i];
-    s_base[i] = a.qbase[v0 + i];
-    const long long p = (qs > e0 ? qs : e0) - e0;
-    if (p < cnt) s_owner[p] = i;
-  }
-  __syncthreads();
-  // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
-  int vals[kItems];
-  int run = 0;
-#pragma unroll
-  for (int k = 0; k < kItems; ++k) {
-    run = max(run, s_owner[t * kItems + k]);
-    vals[k] = run;
-  }
-  const int incl = wave_incl_max(run);
-  if (lane == kWave - 1) s_wmax[wv] = incl;
-  __syncthreads();
-  int carry = 0;
-  for (int k = 0; k < wv; ++k) carry = max(carry, s_wmax[k]);
-  const int prev = __shfl_up(incl, 1, kWave);
-  const int excl = lane > 0 ? max(carry, prev) : carry;
-#pragma unroll
-  for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
-  __syncthreads();
-
   const vid_t* __restrict__ col = a.g.col;
   const word_t* __restrict__ visited = a.visited;
+
+  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const long long e1 = min(m, e0 + kTdEdgesPerBlock);
+    const int cnt = static_cast<int>(e1 - e0);
+    const long long v0 = a.blk_vstart[b];
+    const long long vlast = (b + 1 < nblocks) ? a.blk_vstart[b + 1] : q - 1;
+    const int nv = static_cast<int>(vlast - v0 + 1);
+
+    __syncthreads();  // LDS reuse across iterations
 #pragma unroll
-  for (int k = 0; k < kItems; ++k) {
-    const int idx = k * kThreads + t;
-    if constexpr (kOut == TdOut::Lists) {
-      // wave-aggregated append to the owner lists (uniform loop over owners)
-      vid_t v = 0;
-      bool act = false;
-      if (idx < cnt) {
-        v = col[e0 + idx + s_base[s_owner[idx]]];
-        act = !(visited[v >> 6] & (1ull << (v & 63)));
-      }
-      const int owner = act ? static_cast<int>(v / a.part) : -1;
-      unsigned long long pending = __ballot(act);
-      while (pending) {
-        const int leader = __ffsll(static_cast<long long>(pending)) - 1;
-        const int o = __shfl(owner, leader, kWave);
-        const unsigned long long m = __ballot(owner == o);
-        unsigned base = 0;
-        vid_t* list = a.lists + static_cast<int64_t>(o) * (a.list_cap + 1);
-        if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(m)));
-        base = __shfl(base, leader, kWave);
-        if (owner == o) list[1 + base + mask_rank(m)] = v;
-        pending &= ~m;
-      }
-    } else if (idx < cnt) {
-      const int i = s_owner[idx];
-      const vid_t v = col[e0 + idx + s_base[i]];
-      const word_t bit = 1ull << (v & 63);
-      if constexpr (kOut == TdOut::Bytes) {
-        // with few visited vertices the check costs more than the store it
-        // saves (random loads ~120 G/s vs byte stores ~88 G/s on MI355X);
-        // the consuming update masks with ~visited anyway
-        if (!a.check_visited || !(visited[v >> 6] & bit)) a.next_bytes[v] = 1;
-      } else {
-        const word_t seen = visited[v >> 6] | a.next[v >> 6];
-        if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
+    for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
+    __syncthreads();
+    // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
+    for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
+      const long long qs = a.qscan[v0 + i];
+      s_base[i] = a.qbase[v0 + i];
+      const long long p = (qs > e0 ? qs : e0) - e0;
+      if (p < cnt) s_owner[p] = i;
+    }
+    __syncthreads();
+    // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
+    int vals[kItems];
+    int run = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      run = max(run, s_owner[t * kItems + k]);
+      vals[k] = run;
+    }
+    const int incl = wave_incl_max(run);
+    if (lane == kWave - 1) s_wmax[wv] = incl;
+    __syncthreads();
+    int carry = 0;
+    for (int k = 0; k < wv; ++k) carry = max(carry, s_wmax[k]);
+    const int prev = __shfl_up(incl, 1, kWave);
+    const int excl = lane > 0 ? max(carry, prev) : carry;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
+    __syncthreads();
+
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kThreads + t;
+      if constexpr (kOut == TdOut::Lists) {
+        // wave-aggregated append to the owner lists (uniform loop over owners)
+        vid_t v = 0;
+        bool act = false;
+        if (idx < cnt) {
+          v = col[e0 + idx + s_base[s_owner[idx]]];
+          act = !(visited[v >> 6] & (1ull << (v & 63)));
+        }
+        const int owner = act ? static_cast<int>(v / a.part) : -1;
+        unsigned long long pending = __ballot(act);
+        while (pending) {
+          const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+          const int o = __shfl(owner, leader, kWave);
+          const unsigned long long msk = __ballot(owner == o);
+          unsigned base = 0;
+          vid_t* list = a.lists + static_cast<int64_t>(o) * (a.list_cap + 1);
+          if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
+          base = __shfl(base, leader, kWave);
+          if (owner == o) list[1 + base + mask_rank(msk)] = v;
+          pending &= ~msk;
+        }
+      } else if (idx < cnt) {
+        const int i = s_owner[idx];
+        const vid_t v = col[e0 + idx + s_base[i]];
+        const word_t bit = 1ull << (v & 63);
+        if (bytes) {
+          // with few visited vertices the check costs more than the store it
+          // saves (random loads ~120 G/s vs byte stores ~88 G/s on MI355X);
+          // the consuming update masks with ~visited anyway
+          if (!check || !(visited[v >> 6] & bit)) a.next_bytes[v] = 1;
+        } else {
+          const word_t seen = visited[v >> 6] | a.next[v >> 6];
+          if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
+        }
       }
     }
   }
@@ -438,6 +476,7 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // column ids are loaded right after -- the critical path per word is then about
 // one memory round-trip instead of three (row_off -> col -> bitmap).
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   const int lane = lane_id();
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
   const word_t vis_l = (lane < kWaveWords && w0 + lane < a.words) ? a.visited[w0 + lane] : ~0ull;
@@ -577,6 +616,8 @@ void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st) {
 
 void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 0, st>>>(bm, bit); }
 
+void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
+
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
   update_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
@@ -593,6 +634,12 @@ void compact_frontier(const CompactArgs& a, hipStream_t st) {
 }
 
 void td_expand(const TdArgs& a, hipStream_t st) {
+  if (a.ctrl) {
+    // device loop: fixed grid, size and output mode read on the device
+    if (a.grid <= 0) return;
+    td_expand_kernel<TdOut::Dyn, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+    return;
+  }
   if (a.m <= 0 || a.q <= 0) return;
   const unsigned grid = grid_for(a.m, kTdEdgesPerBlock);
   const bool wide = static_cast<int64_t>(grid) < a.wide_below_blocks;

@@ -237,3 +237,22 @@ def test_hub_sort_orders_rows_and_keeps_levels(rt):
         assert sorted(row.tolist()) == sorted(np.asarray(csr.col)[ro[r]:ro[r + 1]].tolist())
     bfs.run(4)
     assert np.array_equal(bfs.levels(), exp)
+
+
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_device_loop_matches_host_loop(rt, mode):
+    # the device-driven level loop (LevelCtrl decisions on the device) must
+    # take exactly the host loop's decisions: same levels, same per-level records
+    p = dbfs.rmat_params(12, 16, 41)
+    csr = dbfs.host_csr_from_params(p)
+    dev = dbfs.BFS(p, rt, mode=mode)
+    host = dbfs.BFS(p, rt, mode=mode)
+    host.engine.set_option("device_loop", 0)
+    assert dict(dev.engine.get_options())["device_loop"] == 1.0
+    for src in dev.sample_roots(4, seed=3) + [0]:
+        a, b = dev.run(src), host.run(src)
+        assert np.array_equal(dev.levels(), _oracle(csr, src))
+        assert np.array_equal(host.levels(), dev.levels())
+        strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+        assert strip(a) == strip(b)
+        assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)

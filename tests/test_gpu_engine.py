@@ -240,3 +240,27 @@ def test_hub_sort_gpu_matches_cpu(gpu_runtime):
         n = ro[r + 1] - ro[r]
         if 2 <= n <= 4096:
             assert np.array_equal(gc[ro[r]:ro[r + 1]], cc[ro[r]:ro[r + 1]]), r
+
+
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+@pytest.mark.parametrize("byte_edges", [-1, 0])
+def test_device_loop_matches_host_loop_gpu(gpu_runtime, mode, byte_edges):
+    """Device-driven level loop (predicated kernels + LevelCtrl decisions in
+    the scan's last workgroup + mailbox stamps) against the host loop."""
+    p = dbfs.rmat_params(16, 16, 43)
+    csr = dbfs.host_csr_from_params(p)
+    dev = dbfs.BFS(p, gpu_runtime, mode=mode)
+    host = dbfs.BFS(p, gpu_runtime, mode=mode)
+    host.engine.set_option("device_loop", 0)
+    for b in (dev, host):
+        b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=byte_edges)
+        b.engine.phase_timing = True
+    for src in dev.sample_roots(4, seed=5):
+        a = dev.run(src)
+        exp = dbfs.cpu_bfs(csr, src)[0]
+        assert np.array_equal(dev.levels(), exp)
+        r = host.run(src)
+        strip = lambda x: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in x.levels]
+        assert strip(a) == strip(r)
+        assert (a.reached, a.edges, a.depth) == (r.reached, r.edges, r.depth)
+        assert all(l["ms"] > 0 for l in a.levels)
