@@ -58,6 +58,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "force_exchange") o.force_exchange = v != 0;
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
+  else if (name == "bu_packed") o.bu_packed = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -72,7 +73,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"sparse_size_check", o.sparse_size_check ? 1.0 : 0.0},
           {"force_exchange", o.force_exchange ? 1.0 : 0.0},
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
-          {"device_loop", o.device_loop ? 1.0 : 0.0}};
+          {"device_loop", o.device_loop ? 1.0 : 0.0},
+          {"bu_packed", o.bu_packed ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -549,6 +551,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
+      ba.packed = opt_.bu_packed;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       be_.bu_step(ba);
@@ -751,6 +754,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
+      ba.packed = opt_.bu_packed;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();

@@ -74,6 +74,9 @@ struct EngineOptions {
   double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
   int bu_lane_limit = 8;
+  // Bottom-up rows still unresolved after the per-lane phase are scanned as
+  // one packed edge stream per wave (else one row at a time).
+  bool bu_packed = true;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -476,6 +476,7 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // column ids are loaded right after -- the critical path per word is then about
 // one memory round-trip instead of three (row_off -> col -> bitmap).
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
+  __shared__ int s_bu_owner[kUnitThreads];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   const int lane = lane_id();
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
@@ -536,23 +537,57 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
         p += 4;
       }
       if (p > lim) p = lim;
-      unsigned long long pending = __ballot(!found && p < e);
-      while (pending) {
-        const int l = __ffsll(static_cast<long long>(pending)) - 1;
-        pending &= pending - 1;
-        const long long ps = __shfl(static_cast<long long>(p), l, kWave);
-        const long long pe = __shfl(static_cast<long long>(e), l, kWave);
-        bool f = false;
-        for (long long base = ps; base < pe; base += kWave) {
-          const long long idx = base + lane;
+      if (a.packed) {
+        // Phase 2, packed: the remaining rows of all unresolved lanes form one
+        // edge stream (lane order); every step the wave tests its next 64
+        // edges, whatever rows they belong to, then drops the rows that hit or
+        // ran out.  Steps = ceil(sum of remaining lengths / 64) instead of one
+        // or more dependent steps per unresolved vertex.
+        int* own = s_bu_owner + (threadIdx.x & ~(kWave - 1));
+        for (;;) {
+          const long long rem = (!found && p < e) ? static_cast<long long>(e - p) : 0;
+          if (!__ballot(rem > 0)) break;
+          const long long incl = wave_incl_scan(rem);
+          const long long excl = incl - rem;
+          own[lane] = -1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          if (rem > 0 && excl < kWave) own[excl] = lane;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          const int o = wave_incl_max(own[lane]);  // owner lane of edge slot `lane`
+          const long long total = readlane_i64(incl, kWave - 1);
+          const long long o_excl = __shfl(excl, o, kWave);
+          const long long o_p = __shfl(static_cast<long long>(p), o, kWave);
           bool hit = false;
-          if (idx < pe) hit = test_bit(fr, col[idx]);
-          if (__ballot(hit)) {
-            f = true;
-            break;
-          }
+          if (lane < total) hit = test_bit(fr, col[o_p + (lane - o_excl)]);
+          // owners with a hit: set bit o of a wave mask
+          unsigned long long hitmask = hit ? (1ull << o) : 0ull;
+#pragma unroll
+          for (int off = 1; off < kWave; off <<= 1) hitmask |= __shfl_xor(hitmask, off, kWave);
+          if ((hitmask >> lane) & 1ull) found = true;
+          const long long took = rem > 0 ? max(0LL, min(rem, static_cast<long long>(kWave) - excl)) : 0;
+          p += took;
         }
-        if (lane == l) found = f;
+      } else {
+        unsigned long long pending = __ballot(!found && p < e);
+        while (pending) {
+          const int l = __ffsll(static_cast<long long>(pending)) - 1;
+          pending &= pending - 1;
+          const long long ps = __shfl(static_cast<long long>(p), l, kWave);
+          const long long pe = __shfl(static_cast<long long>(e), l, kWave);
+          bool f = false;
+          for (long long base = ps; base < pe; base += kWave) {
+            const long long idx = base + lane;
+            bool hit = false;
+            if (idx < pe) hit = test_bit(fr, col[idx]);
+            if (__ballot(hit)) {
+              f = true;
+              break;
+            }
+          }
+          if (lane == l) found = f;
+        }
       }
       res = __ballot(found);
       if (found) {

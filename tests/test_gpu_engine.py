@@ -264,3 +264,17 @@ def test_device_loop_matches_host_loop_gpu(gpu_runtime, mode, byte_edges):
         assert strip(a) == strip(r)
         assert (a.reached, a.edges, a.depth) == (r.reached, r.edges, r.depth)
         assert all(l["ms"] > 0 for l in a.levels)
+
+
+@pytest.mark.parametrize("packed", [0, 1])
+@pytest.mark.parametrize("lane_limit", [1, 8, 64])
+def test_bottom_up_variants_gpu(gpu_runtime, packed, lane_limit):
+    """Bottom-up phase 2 (packed multi-row edge stream vs one row at a time)
+    at several per-lane phase lengths, pure BU and direction-optimising."""
+    p = dbfs.rmat_params(17, 16, 47)
+    csr = dbfs.host_csr_from_params(p)
+    for mode in ["bu", "do"]:
+        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, bu_lane_limit=lane_limit)
+        bfs.engine.set_option("bu_packed", packed)
+        for src in bfs.sample_roots(3, seed=lane_limit):
+            _check(bfs, csr, src)
