@@ -35,9 +35,24 @@ CLI       := bin/bfs
 
 HEADERS   := $(wildcard csrc/include/dbfs/*.hpp) $(wildcard csrc/kernels/*.hpp)
 
-.PHONY: all clean lib
+.PHONY: all clean lib asan
 all: $(CLI) $(PYMOD)
 lib: $(CORE_LIB)
+
+# Host sanitizers: bin/bfs_asan, every host translation unit
+# built with AddressSanitizer + UBSan (g++), device code unchanged.  GPU
+# sanitizers are not available on this pool: run it with --cpu.
+ASAN_BUILD := build-asan
+ASANFLAGS  := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+              -std=c++17 -Icsrc/include -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+ASAN_OBJ   := $(patsubst csrc/%.cpp,$(ASAN_BUILD)/%.o,$(HOST_SRC) csrc/cli/main.cpp)
+asan: bin/bfs_asan
+$(ASAN_BUILD)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ASANFLAGS) -c $< -o $@
+bin/bfs_asan: $(ASAN_OBJ) $(HIP_OBJ)
+	@mkdir -p bin
+	$(CXX) -fsanitize=address,undefined $^ -o $@ $(LDLIBS)
 
 $(BUILD)/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
@@ -67,4 +82,4 @@ $(PYMOD): $(BUILD)/python/module.o $(CORE_LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -shared $^ -o $@ $(LDLIBS)
 
 clean:
-	rm -rf $(BUILD) bin $(PKG)/_dbfs_native*.so
+	rm -rf $(BUILD) $(ASAN_BUILD) bin $(PKG)/_dbfs_native*.so
