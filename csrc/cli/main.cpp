@@ -54,6 +54,7 @@ struct Args {
   std::string levels_out;
   std::string cache_out;
   bool json = false;
+  std::string level_csv;
   bool quiet = false;
   bool phase_timing = false;
   bool hub_sort = true;
@@ -68,7 +69,8 @@ struct Args {
                "       --mode ref|td|bu|do|simple|scan  --alpha A --beta B --bu-lane-limit K\n"
                "       --rmat SCALE[:EF] | --uniform N:M   --seed S\n"
                "       --roots K (random sources, GTEPS summary)  --no-oracle  --validate\n"
-               "       --levels-out FILE  --cache FILE (write binary CSR)  --json  --quiet  --phase-timing\n");
+               "       --levels-out FILE  --cache FILE (write binary CSR)  --json  --quiet  --phase-timing\n"
+               "       --level-csv FILE (per-level records of every run: root,level,dir,frontier,...,ms)\n");
   std::exit(2);
 }
 
@@ -107,6 +109,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--levels-out") a.levels_out = next();
     else if (s == "--cache") a.cache_out = next();
     else if (s == "--json") a.json = true;
+    else if (s == "--level-csv") a.level_csv = next();
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--phase-timing") a.phase_timing = true;
     else if (s == "--no-hub-sort") a.hub_sort = false;
@@ -352,6 +355,21 @@ int main(int argc, char** argv) {
       }
     }
     if (!a.levels_out.empty() && leader) write_levels(a.levels_out, got);
+    // Per-level profile CSV: one row per level of every run.
+    std::FILE* csv = nullptr;
+    if (!a.level_csv.empty() && leader) {
+      csv = std::fopen(a.level_csv.c_str(), "w");
+      DBFS_CHECK(csv != nullptr, "cannot write " + a.level_csv);
+      std::fprintf(csv, "root,level,dir,frontier,frontier_edges,discovered,ms,run_ms\n");
+    }
+    auto csv_run = [&](const RunResult& r) {
+      if (!csv) return;
+      for (const auto& l : r.levels)
+        std::fprintf(csv, "%lld,%d,%c,%lld,%lld,%lld,%.4f,%.4f\n", static_cast<long long>(r.source), l.level,
+                     l.direction, static_cast<long long>(l.frontier), static_cast<long long>(l.frontier_edges),
+                     static_cast<long long>(l.discovered), l.ms, r.ms);
+    };
+    csv_run(res[0]);
     const std::string bname = ranks[0].be->name();
     if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
 
@@ -384,6 +402,7 @@ int main(int argc, char** argv) {
         ms_sum += res[0].ms;
         e_sum += res[0].edges;
         if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
+        csv_run(res[0]);
       }
       if (leader && !roots.empty()) {
         const double hm = inv_sum > 0 ? roots.size() / inv_sum : 0.0;
@@ -391,6 +410,7 @@ int main(int argc, char** argv) {
                     ms_sum / roots.size(), hm, ms_sum > 0 ? e_sum / (ms_sum * 1e6) : 0.0);
       }
     }
+    if (csv) std::fclose(csv);
     return rc_exit;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "bfs: %s\n", e.what());

@@ -134,3 +134,16 @@ def test_bench_torchrun_multiprocess_cpu(nproc, mode):
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == nproc and rec["validated"] is True
     assert rec["config"]["parallelism"] == f"1d-vertex-partition x{nproc}"
+
+
+def test_cli_level_csv(tmp_path):
+    csv_path = tmp_path / "levels.csv"
+    out = _run(["--rmat", "10", "3", "--cpu", "--quiet", "--roots", "3", "--json", "--phase-timing",
+                "--level-csv", str(csv_path)])
+    assert out.returncode == 0, out.stderr
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    rows = csv_path.read_text().strip().splitlines()
+    assert rows[0] == "root,level,dir,frontier,frontier_edges,discovered,ms,run_ms"
+    assert len(rows) - 1 == sum(len(r["levels"]) for r in recs)
+    first = rows[1].split(",")
+    assert int(first[0]) == recs[0]["source"] and first[1] == "0" and first[2] in "TB"
