@@ -278,3 +278,18 @@ def test_bottom_up_variants_gpu(gpu_runtime, packed, lane_limit):
         bfs.engine.set_option("bu_packed", packed)
         for src in bfs.sample_roots(3, seed=lane_limit):
             _check(bfs, csr, src)
+
+
+def test_perf_regression_do_vs_ref_gpu(gpu_runtime):
+    """SURVEY §7.4 perf guard: on RMAT-18 the direction-optimising engine must
+    stay far ahead of the reference algorithm on the same GPU (measured
+    ~100x at RMAT-26; require 10x here to stay robust on a shared box)."""
+    p = dbfs.rmat_params(18, 16, 3)
+    ref = dbfs.BFS(p, gpu_runtime, mode="ref")
+    do = dbfs.BFS(p, gpu_runtime, mode="do")
+    roots = do.sample_roots(4, seed=2)
+    for b in (ref, do):
+        b.run(roots[0])  # warm-up
+    t_ref = sum(ref.run(r).ms for r in roots)
+    t_do = sum(do.run(r).ms for r in roots)
+    assert t_do * 10 < t_ref, (t_do, t_ref)
