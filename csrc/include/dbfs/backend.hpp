@@ -248,7 +248,7 @@ struct BuArgs {
   lvl_t new_level = 0;
   int64_t words = 0;
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
-  bool packed = true;                // wave cooperation over a packed multi-row edge stream
+  bool packed = false;               // wave cooperation over a packed multi-row edge stream
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'

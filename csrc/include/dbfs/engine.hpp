@@ -76,7 +76,7 @@ struct EngineOptions {
   int bu_lane_limit = 8;
   // Bottom-up rows still unresolved after the per-lane phase are scanned as
   // one packed edge stream per wave (else one row at a time).
-  bool bu_packed = true;
+  bool bu_packed = false;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -475,8 +475,9 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // are in flight, word j+1's row offsets are loaded, and word j+1's first four
 // column ids are loaded right after -- the critical path per word is then about
 // one memory round-trip instead of three (row_off -> col -> bitmap).
+template <bool kPacked>
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
-  __shared__ int s_bu_owner[kUnitThreads];
+  __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   const int lane = lane_id();
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
         p += 4;
       }
       if (p > lim) p = lim;
-      if (a.packed) {
+      if constexpr (kPacked) {
         // Phase 2, packed: the remaining rows of all unresolved lanes form one
         // edge stream (lane order); every step the wave tests its next 64
         // edges, whatever rows they belong to, then drops the rows that hit or
@@ -707,7 +708,10 @@ void pack_bytes(const PackArgs& a, hipStream_t st) {
 
 void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  bu_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+  if (a.packed)
+    bu_kernel<true><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+  else
+    bu_kernel<false><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
 }
 
 void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st) {
