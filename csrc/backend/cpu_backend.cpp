@@ -100,7 +100,7 @@ class CpuBackend final : public Backend {
   void free_mapped(void* h) override { std::free(h); }
 
   void scan_units(const ScanArgs& a) override {
-    if (a.ctrl && a.ctrl->done) return;
+    if (a.ctrl && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
     const int64_t nchunks = div_up(a.nunits, kScanChunk);
     int64_t c = 0, d = 0;
     for (int64_t k = 0; k < nchunks; ++k) {
@@ -125,6 +125,7 @@ class CpuBackend final : public Backend {
       if (a.mailbox) {
         a.mailbox->done = a.ctrl->done;
         a.mailbox->vis_deg = a.ctrl->vis_deg;
+        a.mailbox->next_dir = a.ctrl->dir;
         a.mailbox->level = a.level;
       }
     }

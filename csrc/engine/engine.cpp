@@ -661,8 +661,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
   be_.level_ctrl_init(ctrl_.data(), init);
 
-  int cur = 0;
-  auto scan = [&](int level, bool seed) {
+  auto scan = [&](int level, bool seed, char expect_dir) {
     ScanArgs sa;
     sa.unit_cnt = unit_cnt_.data();
     sa.unit_deg = unit_deg_.data();
@@ -677,8 +676,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.mailbox = mailbox_dev_ + slot(level);
     sa.level = level;
     sa.seed = seed;
+    sa.expect_dir = expect_dir;
     be_.scan_units(sa);
   };
+  // Frontier double buffer: the seed writes frontier_[1]; level L reads
+  // frontier_[(L + 1) & 1] and writes the other one.
   UpdateArgs ua;
   ua.g = gv;
   ua.cand = cand_.data();
@@ -687,41 +689,52 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   ua.clear_cand = true;
   ua.force = true;  // the source counts even with degree 0
   ua.visited = visited_.data();
-  ua.frontier = frontier_[cur ^ 1].data();
+  ua.frontier = frontier_[1].data();
   ua.level = level_.data();
   ua.new_level = 0;
   ua.words = W;
   ua.unit_cnt = unit_cnt_.data();
   ua.unit_deg = unit_deg_.data();
   be_.update_frontier(ua);
-  scan(-1, true);
-  cur ^= 1;
+  scan(-1, true, 0);
 
   const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), 2048));
   std::vector<std::pair<int, int>> evs;
-  int nlev = 0;
-  for (int L = 0;; ++L) {
-    inject_fault(L);
+  std::vector<char> enq_dir;  // direction each level was (last) enqueued with
+  // Enqueue level L's chain for direction d: top-down = compact + td_expand +
+  // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
+  // so a chain enqueued for the wrong direction is a handful of no-op launches.
+  auto enqueue_level = [&](int L, char d) {
     if (static_cast<size_t>(L) >= rec_.size()) {
       // grow the record array (stream-ordered copy; the old one is freed after a sync)
       DBuf<LevelRecDev> bigger(be_, rec_.size() * 2);
       be_.copy_async(bigger.data(), rec_.data(), rec_.bytes());
       rec_ = std::move(bigger);
     }
+    if (static_cast<size_t>(L) >= enq_dir.size()) {
+      inject_fault(L);
+      enq_dir.resize(static_cast<size_t>(L) + 1);
+      evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
+    }
+    enq_dir[L] = d;
+    const int cur = (L + 1) & 1;
+    char trace_name[48];
+    std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
+    TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    CompactArgs ca;
-    ca.g = gv;
-    ca.frontier = frontier_[cur].data();
-    ca.words = W;
-    ca.unit_cnt_off = unit_cnt_.data();
-    ca.unit_deg_off = unit_deg_.data();
-    ca.part_cnt = part_cnt_.data();
-    ca.part_deg = part_deg_.data();
-    ca.qscan = qscan_.data();
-    ca.qbase = qbase_.data();
-    ca.blk_vstart = blk_vstart_.data();
-    ca.ctrl = ctrl_.data();
-    if (opt_.mode != Mode::BottomUp) {
+    if (d == 'T') {
+      CompactArgs ca;
+      ca.g = gv;
+      ca.frontier = frontier_[cur].data();
+      ca.words = W;
+      ca.unit_cnt_off = unit_cnt_.data();
+      ca.unit_deg_off = unit_deg_.data();
+      ca.part_cnt = part_cnt_.data();
+      ca.part_deg = part_deg_.data();
+      ca.qscan = qscan_.data();
+      ca.qbase = qbase_.data();
+      ca.blk_vstart = blk_vstart_.data();
+      ca.ctrl = ctrl_.data();
       be_.compact_frontier(ca);
       TdArgs ta;
       ta.g = gv;
@@ -743,8 +756,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.new_level = L + 1;
       tu.ctrl = ctrl_.data();
       be_.update_frontier(tu);
-    }
-    if (opt_.mode != Mode::TopDown) {
+    } else {
       BuArgs ba;
       ba.g = gv;
       ba.visited = visited_.data();
@@ -760,13 +772,27 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.ctrl = ctrl_.data();
       be_.bu_step(ba);
     }
-    scan(L, false);
-    if (opt_.phase_timing) evs.emplace_back(ev0, be_.record_event());
-    cur ^= 1;
+    scan(L, false, d);
+    if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
+  };
+
+  // Host loop, one level ahead of the device.  The direction of level L + 1 is
+  // predicted to be level L's (directions change about twice per traversal);
+  // the stamp of level L - 1 carries the real direction of level L, and a
+  // mispredicted level (a no-op chain, its scan skipped too) is enqueued again.
+  int nlev = 0;
+  enqueue_level(0, static_cast<char>(init.dir));
+  for (int L = 0;; ++L) {
+    enqueue_level(L + 1, enq_dir[L]);
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
     if (mb->done) {
       nlev = L;
       break;
+    }
+    const char actual = static_cast<char>(mb->next_dir);
+    if (actual != enq_dir[L]) {
+      enqueue_level(L, actual);
+      enqueue_level(L + 1, actual);
     }
   }
   be_.synchronize();

@@ -89,6 +89,8 @@ struct LevelMailbox {
   int32_t level = -2;           // level that wrote this slot
   int32_t done = 0;
   int64_t vis_deg = 0;
+  int32_t next_dir = 0;         // direction decided for the following level
+  int32_t pad = 0;
 };
 constexpr int kMailboxSlots = 8;
 
@@ -167,6 +169,9 @@ struct ScanArgs {
   LevelMailbox* mailbox = nullptr;  // device-mapped pinned slot
   int32_t level = 0;
   bool seed = false;
+  // Device loop: the level's chain was enqueued for this direction (0: any);
+  // when ctrl->dir differs, the chain was a no-op and so is the scan.
+  int32_t expect_dir = 0;
 };
 
 // Owned frontier bitmap -> load-balanced top-down work list:

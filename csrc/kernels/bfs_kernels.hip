@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
 __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;
-  if (a.ctrl && a.ctrl->done) return;  // uniform: no block takes a ticket
+  // uniform: no block takes a ticket
+  if (a.ctrl && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
         __hip_atomic_store(&a.mailbox->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
                            static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.mailbox->level, a.level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
