@@ -134,7 +134,14 @@ def main() -> int:
             log(f"per-level profile of root {prof.source} ({prof.ms:.3f} ms incl. event overhead):")
             for lv in prof.levels:
                 log(f"  level {lv['level']} {lv['dir']} frontier {lv['frontier']} edges {lv['frontier_edges']}"
-                    f" new {lv['discovered']} {lv['ms']:.3f} ms")
+                    f" new {lv['discovered']} {lv['ms']:.3f} ms (collectives {lv.get('comm_ms', 0.0):.3f} ms)")
+    # One extra (untimed) traversal of the median timed root with per-level
+    # device events: where the time goes (collectives vs kernels) at this N.
+    med = sorted(results, key=lambda r: r.ms)[len(results) // 2]
+    bfs.engine.phase_timing = True
+    prof = bfs.run(med.source)
+    bfs.engine.phase_timing = False
+    level_profile = [[lv["dir"], round(lv["ms"], 4), round(lv.get("comm_ms", 0.0), 4)] for lv in prof.levels]
     baseline = args.baseline_gteps
     if baseline is None and args.edge_factor == 16 and args.mode != "ref":
         baseline = MEASURED_REF_GTEPS.get((args.scale, nranks))
@@ -169,6 +176,8 @@ def main() -> int:
             "depth_mean": sum(r.depth for r in results) / len(results),
             "validated": validated,
             "generate_s": round(gen_s, 3),
+            "level_profile": {"root": med.source, "levels": level_profile,
+                              "columns": ["dir", "ms", "comm_ms"]},
         }
         print(json.dumps(out), flush=True)
     return 0

@@ -91,6 +91,10 @@ class CpuBackend final : public Backend {
   }
 
   void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override { *c = init; }
+  void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) override {
+    for (int k = 0; k < 4; ++k) mb->v[k] = stats[k];
+    __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
+  }
   void* alloc_mapped(size_t bytes, void** dptr) override {
     void* h = std::calloc(1, std::max<size_t>(bytes, 1));
     DBFS_CHECK(h != nullptr, "host allocation failed");

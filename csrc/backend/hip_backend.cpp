@@ -156,6 +156,11 @@ class HipBackend final : public Backend {
     kern::level_ctrl_init(c, init, st_);
     chk();
   }
+  void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) override {
+    on();
+    kern::publish_stats(stats, mb, seq, st_);
+    chk();
+  }
   void* alloc_mapped(size_t bytes, void** dptr) override {
     on();
     void* h = nullptr;

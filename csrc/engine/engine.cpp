@@ -58,6 +58,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "force_exchange") o.force_exchange = v != 0;
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
+  else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
@@ -74,6 +75,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"force_exchange", o.force_exchange ? 1.0 : 0.0},
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
+          {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0}};
 }
 
@@ -212,6 +214,50 @@ Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
 
 Engine::~Engine() {
   if (mailbox_host_) be_.free_mapped(mailbox_host_);
+  if (stats_mb_host_) be_.free_mapped(stats_mb_host_);
+}
+
+namespace {
+// Spin until `ready()` (a store of the device into pinned, mapped memory).
+// Every wait-watch period: the backend's watch runs (RCCL: async errors and
+// the collective timeout), and a stream that has drained without `ready()`
+// is an error (the stamping kernel did not run).
+template <class Ready>
+void spin_until(Backend& be, Ready ready, const char* what) {
+  if (ready()) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  const double period = be.wait_watch_period();
+  double next = period;
+  for (uint64_t spin = 1;; ++spin) {
+    if (ready()) return;
+    if ((spin & 0x3FF) != 0) continue;
+    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (waited < next) continue;
+    if (be.stream_idle() && !ready()) throw Error(what);
+    be.poll_wait_watch(waited);
+    next = waited + period;
+  }
+}
+}  // namespace
+
+// Totals of the level just scanned (stats[0..3]: local count, local degree
+// sum, global count, global degree sum) to the host.
+void Engine::read_level_stats(int64_t* host_stats) {
+  if (!opt_.stats_mailbox) {
+    be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
+    return;
+  }
+  if (!stats_mb_host_) {
+    void* dptr = nullptr;
+    stats_mb_host_ = static_cast<StatsMailbox*>(be_.alloc_mapped(sizeof(StatsMailbox), &dptr));
+    stats_mb_dev_ = static_cast<StatsMailbox*>(dptr);
+  }
+  const int64_t seq = ++stats_seq_;
+  be_.publish_stats(stats_.data(), stats_mb_dev_, seq);
+  StatsMailbox* mb = stats_mb_host_;
+  spin_until(be_, [&] { return __atomic_load_n(&mb->seq, __ATOMIC_ACQUIRE) == seq; },
+             "level statistics mailbox: stream drained without the stamp");
+  for (int k = 0; k < 4; ++k) host_stats[k] = __atomic_load_n(&mb->v[k], __ATOMIC_RELAXED);
 }
 
 // ---- fault injection -------------------------------------------
@@ -360,6 +406,18 @@ RunResult Engine::run_bitmap(int64_t source) {
   be_.memset_async(next_.data(), 0, next_.bytes());
   if (part_.owner(source) == me) be_.set_bit(cand_.data(), source - lo);
 
+  // Collectives of the current level, bracketed by events when phase timing is
+  // on (LevelRecord::comm_ms).
+  std::vector<std::pair<int, int>> comm_evs;
+  auto timed_comm = [&](auto&& fn) {
+    if (!opt_.phase_timing) {
+      fn();
+      return;
+    }
+    const int a = be_.record_event();
+    fn();
+    comm_evs.emplace_back(a, be_.record_event());
+  };
   // Scan the unit statistics of the new frontier and reduce the totals to the
   // host (termination + direction decision).
   auto finish_level = [&](int64_t* host_stats) {
@@ -374,8 +432,8 @@ RunResult Engine::run_bitmap(int64_t source) {
     sa.qscan = qscan_.data();
     be_.scan_units(sa);
     cur ^= 1;
-    if (exchange()) comm_.allreduce_sum_i64(stats_.data() + 2, 2);
-    be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
+    if (exchange()) timed_comm([&] { comm_.allreduce_sum_i64(stats_.data() + 2, 2); });
+    read_level_stats(host_stats);
   };
   // Publish the new frontier (all-gather of the owned slices) and merge it into
   // the replicated visited bitmap.  Bottom-up needs the global frontier; a
@@ -385,7 +443,7 @@ RunResult Engine::run_bitmap(int64_t source) {
   // before a top-down level.
   auto publish = [&](char next_dir) {
     if (!exchange() || (next_dir == 'T' && opt_.mode == Mode::DirOpt)) return;
-    comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t));
+    timed_comm([&] { comm_.allgather(fr_cur() + me * W, fr_cur(), static_cast<size_t>(W) * sizeof(word_t)); });
     be_.bitmap_or(visited_.data(), fr_cur(), GW);
   };
   auto update = [&](word_t* cand, int nchunks, bool clear, bool force, lvl_t new_level,
@@ -437,11 +495,19 @@ RunResult Engine::run_bitmap(int64_t source) {
     }
   };
   decide();
-  if (n_f > 0) publish(dir);
+  // A level's timing starts before the all-gather that publishes its frontier.
+  int next_ev0 = -1;
+  auto begin_next = [&]() {
+    comm_evs.clear();
+    if (opt_.phase_timing) next_ev0 = be_.record_event();
+    publish(dir);
+  };
+  if (n_f > 0) begin_next();
   lvl_t L = 0;
   while (n_f > 0) {
     inject_fault(L);
-    const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    const int ev0 = opt_.phase_timing ? (next_ev0 >= 0 ? next_ev0 : be_.record_event()) : -1;
+    next_ev0 = -1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c", L, dir);
     TraceRange trace_level(trace_name);
@@ -516,7 +582,9 @@ RunResult Engine::run_bitmap(int64_t source) {
         be_.status_expand(sa);
       }
       if (list_mode) {
-        comm_.alltoall(send_lists_.data(), recv_lists_.data(), static_cast<size_t>(list_cap + 1) * sizeof(vid_t));
+        timed_comm([&] {
+          comm_.alltoall(send_lists_.data(), recv_lists_.data(), static_cast<size_t>(list_cap + 1) * sizeof(vid_t));
+        });
         ListScatterArgs la;
         la.lists = recv_lists_.data();
         la.nranks = P;
@@ -533,7 +601,7 @@ RunResult Engine::run_bitmap(int64_t source) {
           pa.words = GW;
           be_.pack_bytes(pa);
         }
-        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
+        timed_comm([&] { comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t)); });
         be_.memset_async(next_.data(), 0, next_.bytes());
         update(recv_.data(), P, false, false, L + 1);
       } else if (bytes_mode) {
@@ -566,6 +634,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     if (opt_.phase_timing) {
       const int ev1 = be_.record_event();
       rec.ms = be_.elapsed_ms(ev0, ev1);
+      for (const auto& ce : comm_evs) rec.comm_ms += be_.elapsed_ms(ce.first, ce.second);
     }
     res.levels.push_back(rec);
     prev_nf = n_f;
@@ -577,7 +646,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     ++L;
     if (n_f > 0) {
       decide();
-      publish(dir);
+      begin_next();
     }
   }
   be_.synchronize();
@@ -632,11 +701,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // Wait until level `lv` (-1 = seed) has stamped its mailbox slot.
   auto wait_stamp = [&](int lv) -> const volatile LevelMailbox* {
     const volatile LevelMailbox* mb = mailbox_host_ + slot(lv);
-    for (uint64_t spin = 0;; ++spin) {
-      if (__atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) == lv) return mb;
-      if ((spin & 0xFFFF) == 0xFFFF && be_.stream_idle() && __atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) != lv)
-        throw Error("device level loop: level " + std::to_string(lv) + " finished without its mailbox stamp");
-    }
+    spin_until(be_, [&] { return __atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) == lv; },
+               "device level loop: a level finished without its mailbox stamp");
+    return mb;
   };
 
   RunResult res;

@@ -174,6 +174,17 @@ struct ScanArgs {
   int32_t expect_dir = 0;
 };
 
+// Host-loop statistics mailbox (pinned, device-mapped).  After a level's
+// totals are final (scan, plus the all-reduce on several ranks) one tiny
+// kernel copies stats[0..3] here with system-scope stores and then writes
+// `seq` with release semantics; the host spins on `seq`.  This replaces a
+// D2H copy + stream synchronisation per level (a copy-engine round trip and a
+// host wake-up) by a store the spinning host sees within a microsecond.
+struct StatsMailbox {
+  int64_t seq = 0;
+  int64_t v[4] = {0, 0, 0, 0};
+};
+
 // Owned frontier bitmap -> load-balanced top-down work list:
 // qscan[i] = exclusive prefix of degrees, qbase[i] = row_off[v_i] - qscan[i],
 // blk_vstart[b] = index of the entry covering edge b * kTdEdgesPerBlock.
@@ -395,6 +406,15 @@ class Backend {
   virtual void scan_units(const ScanArgs& a) = 0;
   // *ctrl = init (stream-ordered)
   virtual void level_ctrl_init(LevelCtrl* ctrl, const LevelCtrl& init) = 0;
+  // mb->v[0..3] = stats[0..3], then mb->seq = seq (release); mb is the device
+  // pointer of an alloc_mapped block.
+  virtual void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) = 0;
+  // Give an installed wait watch a chance to inspect a host-side wait that does
+  // not go through the stream (mailbox spins).
+  void poll_wait_watch(double waited) {
+    if (wait_watch_) wait_watch_(waited);
+  }
+  double wait_watch_period() const { return wait_period_; }
   // Pinned host memory the device can store to (nullptr-safe free).
   virtual void* alloc_mapped(size_t bytes, void** device_ptr) = 0;
   virtual void free_mapped(void* host_ptr) = 0;

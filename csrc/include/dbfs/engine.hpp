@@ -95,6 +95,10 @@ struct EngineOptions {
   // One rank, td/bu/do modes: device-driven level loop (LevelCtrl): the host
   // enqueues the next level before the current one finishes.
   bool device_loop = true;
+  // Host loop (several ranks, or device_loop off): read each level's totals
+  // through a device-mapped mailbox the host spins on, instead of a D2H copy
+  // plus a stream synchronisation.
+  bool stats_mailbox = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -114,6 +118,7 @@ struct LevelRecord {
   int64_t frontier_edges = 0; // global sum of their degrees
   int64_t discovered = 0;     // global new vertices
   double ms = 0.0;            // device time of the level (phase_timing only)
+  double comm_ms = 0.0;       // ... of which in collectives (host loop, phase_timing only)
 };
 
 struct RunResult {
@@ -187,6 +192,11 @@ class Engine {
   DBuf<LevelRecDev> rec_;
   LevelMailbox* mailbox_host_ = nullptr;  // pinned, device-mapped
   LevelMailbox* mailbox_dev_ = nullptr;
+  // host-loop statistics mailbox
+  StatsMailbox* stats_mb_host_ = nullptr;
+  StatsMailbox* stats_mb_dev_ = nullptr;
+  int64_t stats_seq_ = 0;
+  void read_level_stats(int64_t* host_stats);
   // reference-mode state
   bool ref_ready_ = false;
   DBuf<lvl_t> dist_;

@@ -57,6 +57,19 @@ __global__ void set_bit_kernel(word_t* bm, int64_t bit) {
   if (threadIdx.x == 0) bm[bit >> 6] |= 1ull << (bit & 63);
 }
 
+// Level totals -> host-mapped mailbox: values first (system scope), then the
+// sequence number with release semantics, so a host that observes `seq` reads
+// the values of that level.
+__global__ void publish_stats_kernel(const int64_t* __restrict__ stats, StatsMailbox* mb, int64_t seq) {
+  if (threadIdx.x != 0) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->v[k]), static_cast<unsigned long long>(stats[k]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->seq), static_cast<unsigned long long>(seq),
+                     __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Sum (cnt, deg) of the 4 waves of a unit workgroup; thread 0 writes them.
 __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
                                                  int64_t* unit_deg) {
@@ -655,6 +668,10 @@ void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st) {
 void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 0, st>>>(bm, bit); }
 
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
+
+void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st) {
+  publish_stats_kernel<<<1, 64, 0, st>>>(stats, mb, seq);
+}
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;

@@ -45,6 +45,7 @@ py::dict result_dict(const RunResult& r) {
     x["frontier_edges"] = l.frontier_edges;
     x["discovered"] = l.discovered;
     x["ms"] = l.ms;
+    x["comm_ms"] = l.comm_ms;
     lv.append(x);
   }
   d["levels"] = lv;

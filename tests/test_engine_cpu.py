@@ -256,3 +256,30 @@ def test_device_loop_matches_host_loop(rt, mode):
         strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
         assert strip(a) == strip(b)
         assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+
+
+@pytest.mark.parametrize("mailbox", [0, 1])
+def test_host_loop_stats_mailbox(mailbox):
+    # host loop on 3 virtual ranks: level totals read through the mapped
+    # mailbox (or a plain copy) give the oracle's levels; with phase timing
+    # every level reports its collective time (comm_ms <= ms)
+    p = dbfs.rmat_params(11, 16, 19)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    srcs = [int(v) for v in np.nonzero(deg > 0)[0][[0, 50, 400]]]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode="do")
+        bfs.engine.set_option("stats_mailbox", mailbox)
+        bfs.engine.phase_timing = True
+        out = []
+        for s in srcs:
+            res = bfs.run(s)
+            out.append((bfs.levels(), res.levels))
+        return out
+
+    for rank_out in run_virtual_ranks(3, body, device="cpu"):
+        for (lv, levels), s in zip(rank_out, srcs):
+            assert np.array_equal(lv, _oracle(csr, s))
+            assert levels and all(0.0 <= l["comm_ms"] <= l["ms"] + 1e-6 for l in levels)
+            assert any(l["comm_ms"] > 0 for l in levels)
