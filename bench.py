@@ -55,6 +55,8 @@ def main() -> int:
     ap.add_argument("--bu-lane-limit", type=int, default=8)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning option (see Engine.get_options()), repeatable")
+    ap.add_argument("--no-hubs", action="store_true", help="bottom-up without the LDS hub frontier")
+    ap.add_argument("--max-hubs", type=int, default=None)
     ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--baseline-gteps", type=float, default=None)
@@ -79,7 +81,7 @@ def main() -> int:
     params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
     t0 = time.time()
     bfs = dbfs.BFS(params, rt, mode=args.mode, alpha=args.alpha, beta=args.beta,
-                   bu_lane_limit=args.bu_lane_limit)
+                   bu_lane_limit=args.bu_lane_limit, hubs=not args.no_hubs, max_hubs=args.max_hubs)
     for kv in args.opt:
         name, _, val = kv.partition("=")
         bfs.engine.set_option(name, float(val))

@@ -375,8 +375,34 @@ class CpuBackend final : public Backend {
     }
   }
 
-  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head) override {
-    for (int64_t r = 0; r < rows; ++r) head[r] = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;
+  int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
+                      uint32_t* hub_idx) override {
+    int64_t k = 0;
+    for (int64_t v = 0; v < n; ++v) {
+      if (deg[v] >= min_deg) {
+        hub_vertex[k] = static_cast<vid_t>(v);
+        hub_idx[v] = static_cast<uint32_t>(k++);
+      } else {
+        hub_idx[v] = 0xFFFFFFFFu;
+      }
+    }
+    return k;
+  }
+  void hub_gather(const HubGatherArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    for (int64_t w = 0; w < div_up(a.g.nhubs, 64); ++w) {
+      word_t m = 0;
+      for (int b = 0; b < 64 && w * 64 + b < a.g.nhubs; ++b)
+        if (test_bit(a.frontier, a.g.hub_vertex[w * 64 + b])) m |= 1ull << b;
+      a.hub_front[w] = m;
+    }
+  }
+  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx) override {
+    for (int64_t r = 0; r < rows; ++r) {
+      vid_t h = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;
+      if (hub_idx && ro[r + 1] > ro[r] && hub_idx[h] != 0xFFFFFFFFu) h = kHubFlag | hub_idx[h];
+      head[r] = h;
+    }
   }
 
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {

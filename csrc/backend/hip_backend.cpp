@@ -181,6 +181,7 @@ class HipBackend final : public Backend {
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
+  void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
@@ -196,10 +197,24 @@ class HipBackend final : public Backend {
     kern::degrees_u32(ro, rows, out, st_);
     chk();
   }
-  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head) override {
+  void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx) override {
     on();
-    kern::row_heads(ro, col, rows, head, st_);
+    kern::row_heads(ro, col, rows, head, hub_idx, st_);
     chk();
+  }
+  int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
+                      uint32_t* hub_idx) override {
+    on();
+    unsigned long long* count = nullptr;
+    HIP_CHECK(hipMalloc(&count, sizeof(unsigned long long)));
+    HIP_CHECK(hipMemsetAsync(count, 0, sizeof(unsigned long long), st_));
+    kern::select_hubs(deg, n, min_deg, hub_vertex, hub_idx, count, st_);
+    chk();
+    unsigned long long h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, count, sizeof(h), hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipFree(count));
+    return static_cast<int64_t>(h);
   }
   void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {
     on();

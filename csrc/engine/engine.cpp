@@ -151,6 +151,8 @@ ShardView DeviceGraph::view() const {
   v.rows = rows_;
   v.nnz = nnz_;
   v.head = head_.data();
+  v.hub_vertex = hub_vertex_.data();
+  v.nhubs = nhubs_;
   return v;
 }
 
@@ -179,24 +181,60 @@ std::vector<eid_t> DeviceGraph::degrees_of(const std::vector<int64_t>& local_row
   return out;
 }
 
-void DeviceGraph::sort_neighbors_by_degree(Comm& comm) {
+// Smallest degree d >= 1 with |{v : deg(v) >= d}| <= cap (0: no vertex has
+// degree >= 1).
+static uint32_t hub_min_degree(const std::vector<uint32_t>& deg, int64_t cap) {
+  constexpr uint32_t kCapDeg = 1u << 20;  // histogram range; larger degrees share the top bucket
+  std::vector<int64_t> hist(kCapDeg + 1, 0);
+  for (uint32_t d : deg) ++hist[std::min(d, kCapDeg)];
+  int64_t acc = 0;
+  uint32_t best = 0;
+  for (uint32_t d = kCapDeg; d >= 1; --d) {
+    acc += hist[d];
+    if (acc > cap) break;
+    best = d;
+  }
+  return best;
+}
+
+void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hubs) {
+  DBFS_CHECK(max_hubs >= 0 && max_hubs <= kMaxHubs, "max_hubs out of range");
   DBFS_CHECK(comm.size() == part_.nranks && comm.rank() == rank_, "communicator does not match the shard");
   comm.bind_backend(be_);
   const int P = part_.nranks;
   const int64_t part = part_.part;
-  DBuf<uint32_t> mine(*be_, static_cast<size_t>(part)), all(*be_, static_cast<size_t>(P * part));
+  const int64_t nall = static_cast<int64_t>(P) * part;
+  DBuf<uint32_t> mine(*be_, static_cast<size_t>(part)), all(*be_, static_cast<size_t>(nall));
   be_->memset_async(mine.data(), 0, mine.bytes());
   be_->degrees_u32(row_off_.data(), rows_, mine.data());
   comm.allgather(mine.data(), all.data(), static_cast<size_t>(part) * sizeof(uint32_t));
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
-  build_heads();
+  nhubs_ = 0;
+  hub_vertex_.reset();
+  // Hub encoding needs a free flag bit in the vertex ids.
+  if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
+    std::vector<uint32_t> deg(static_cast<size_t>(nall));
+    be_->to_host(deg.data(), all.data(), deg.size() * sizeof(uint32_t));
+    const uint32_t min_deg = hub_min_degree(deg, max_hubs);
+    if (min_deg > 0) {
+      DBuf<uint32_t> hub_idx(*be_, static_cast<size_t>(nall));
+      hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(max_hubs, 1)));
+      nhubs_ = be_->select_hubs(all.data(), nall, min_deg, hub_vertex_.data(), hub_idx.data());
+      DBFS_CHECK(nhubs_ >= 0 && nhubs_ <= max_hubs, "hub selection exceeded its capacity");
+      build_heads(hub_idx.data());
+    } else {
+      build_heads();
+    }
+  } else {
+    build_heads();
+  }
   hub_sorted_ = true;
 }
 
-void DeviceGraph::build_heads() {
+void DeviceGraph::build_heads(const uint32_t* hub_idx) {
   if (head_.size() < static_cast<size_t>(std::max<int64_t>(rows_, 1)))
     head_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(rows_, 1)));
-  be_->row_heads(row_off_.data(), col_.data(), rows_, head_.data());
+  be_->row_heads(row_off_.data(), col_.data(), rows_, head_.data(), hub_idx);
   be_->synchronize();
 }
 
@@ -325,6 +363,7 @@ void Engine::alloc_bitmap_state() {
   qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
   stats_ = DBuf<int64_t>(be_, 8);
+  if (g_.nhubs() > 0) hub_front_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(g_.nhubs(), kWordBits)));
   // Zero-degree (and padding) vertices can never be discovered: they start out
   // visited, so bottom-up steps skip them without touching row_off.
   ZeroDegArgs za;
@@ -622,6 +661,14 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.packed = opt_.bu_packed;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
+      if (gv.nhubs > 0) {
+        HubGatherArgs hg;
+        hg.g = gv;
+        hg.frontier = fr_cur();
+        hg.hub_front = hub_front_.data();
+        be_.hub_gather(hg);
+        ba.hub_front = hub_front_.data();
+      }
       be_.bu_step(ba);
     }
     finish_level(hs);
@@ -837,6 +884,15 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();
+      if (gv.nhubs > 0) {
+        HubGatherArgs hg;
+        hg.g = gv;
+        hg.frontier = frontier_[cur].data();
+        hg.hub_front = hub_front_.data();
+        hg.ctrl = ctrl_.data();
+        be_.hub_gather(hg);
+        ba.hub_front = hub_front_.data();
+      }
       be_.bu_step(ba);
     }
     scan(L, false, d);

@@ -38,7 +38,18 @@ struct ShardView {
   // for empty rows), laid out per vertex so a wave's 64 first probes are one
   // coalesced 256-B load instead of 64 scattered col[] lines.
   const vid_t* head = nullptr;
+  // Hub-encoded heads (nhubs > 0): the nhubs highest-degree vertices of the
+  // whole graph get compact indices; head[r] = kHubFlag | index when the row's
+  // first neighbour is a hub (hub_vertex[index] = its vertex id), else the
+  // vertex id.  Bottom-up keeps the hubs' frontier bits in LDS.
+  const vid_t* hub_vertex = nullptr;
+  int64_t nhubs = 0;
 };
+
+// At most kMaxHubs hubs: their frontier bitmap (64 KiB) is staged in LDS by
+// every bottom-up workgroup (two 1024-thread workgroups per CU fit in 160 KiB).
+constexpr int64_t kMaxHubs = int64_t(1) << 19;
+constexpr vid_t kHubFlag = 0x80000000u;
 
 // Frontier bookkeeping is organised in "units" of 64 bitmap words (4096
 // vertices): one 256-thread workgroup (4 waves) per unit, 16 consecutive words
@@ -257,6 +268,8 @@ struct PackArgs {
 // new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
 struct BuArgs {
   ShardView g;
+  // Hub frontier bits (g.nhubs bits, from hub_gather), staged in LDS.
+  const word_t* hub_front = nullptr;
   word_t* visited = nullptr;         // owned slice
   const word_t* frontier = nullptr;  // current frontier, global
   word_t* new_frontier = nullptr;    // owned slice of the next frontier (fully overwritten)
@@ -268,6 +281,15 @@ struct BuArgs {
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'
+};
+
+// hub_front bit h = frontier bit of g.hub_vertex[h] (frontier global); in the
+// device loop only when ctrl->dir == 'B'.
+struct HubGatherArgs {
+  ShardView g;
+  const word_t* frontier = nullptr;
+  word_t* hub_front = nullptr;  // ceil(nhubs / 64) words
+  const LevelCtrl* ctrl = nullptr;
 };
 
 // Bits of the owned slice for vertices with degree 0 or beyond the shard
@@ -424,6 +446,7 @@ class Backend {
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
+  virtual void hub_gather(const HubGatherArgs& a) = 0;
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;
   virtual void ref_expand(const RefExpandArgs& a) = 0;
@@ -439,8 +462,15 @@ class Backend {
   // then sort every row by (key_deg[neighbour] descending, neighbour ascending).
   virtual void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out) = 0;
   virtual void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg) = 0;
-  // head[r] = col[row_off[r]] (0 for empty rows)
-  virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head) = 0;
+  // head[r] = col[row_off[r]] (0 for empty rows); with hub_idx (one entry per
+  // vertex, UINT32_MAX for non-hubs) a hub head is stored as kHubFlag | index.
+  virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head,
+                         const uint32_t* hub_idx = nullptr) = 0;
+  // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex
+  // receives their ids (in some order), hub_idx[v] their index or UINT32_MAX;
+  // returns the count (blocking).
+  virtual int64_t select_hubs(const uint32_t* deg_all, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
+                              uint32_t* hub_idx) = 0;
 
   // graph construction on the device
   // deg[r] += number of edge endpoints owned in rows [lo, lo + rows) (deg zeroed by caller)

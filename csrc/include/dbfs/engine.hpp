@@ -51,8 +51,11 @@ class DeviceGraph {
   std::vector<eid_t> degrees_of(const std::vector<int64_t>& local_rows) const;
   // Reorder every row hub-first (neighbour degree descending); collective over
   // `comm` (all ranks need every vertex's degree).  One-time preprocessing.
-  void sort_neighbors_by_degree(Comm& comm);
+  // With `hubs`, the (up to kMaxHubs) highest-degree vertices of the graph are
+  // also indexed and every row head naming one is hub-encoded (ShardView).
+  void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs);
   bool hub_sorted() const { return hub_sorted_; }
+  int64_t nhubs() const { return nhubs_; }
 
  private:
   Backend* be_ = nullptr;
@@ -60,8 +63,9 @@ class DeviceGraph {
   int rank_ = 0;
   int64_t lo_ = 0, rows_ = 0, nnz_ = 0, input_edges_ = 0;
   bool hub_sorted_ = false;
-  void build_heads();
-  DBuf<vid_t> head_;
+  int64_t nhubs_ = 0;
+  void build_heads(const uint32_t* hub_idx = nullptr);
+  DBuf<vid_t> head_, hub_vertex_;
   DBuf<eid_t> row_off_;
   DBuf<vid_t> col_;
 };
@@ -180,7 +184,7 @@ class Engine {
   DBuf<lvl_t> level_;
   // bitmap engine state
   bool bitmap_ready_ = false;
-  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_;
+  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;

@@ -490,19 +490,19 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // are in flight, word j+1's row offsets are loaded, and word j+1's first four
 // column ids are loaded right after -- the critical path per word is then about
 // one memory round-trip instead of three (row_off -> col -> bitmap).
-template <bool kPacked>
-__global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
-  __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+// One wave's 16 words starting at w0 (any w0: words past the slice are
+// skipped).  `own` is the wave's 64-int LDS scratch (packed phase 2), `s_hub`
+// the LDS copy of the hub frontier bits (kHub: heads may be hub-encoded).
+template <bool kPacked, bool kHub>
+__device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, const word_t* s_hub, long long& cnt,
+                                        long long& deg) {
   const int lane = lane_id();
-  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
   const word_t vis_l = (lane < kWaveWords && w0 + lane < a.words) ? a.visited[w0 + lane] : ~0ull;
   const int64_t left = a.words - w0;
   const int nw = left < kWaveWords ? static_cast<int>(left) : kWaveWords;
   const eid_t* __restrict__ ro = a.g.row_off;
   const vid_t* __restrict__ col = a.g.col;
   const word_t* __restrict__ fr = a.frontier;
-  long long cnt = 0, deg = 0;
 
   // Rows of word j for this lane (0, 0 when visited: padding and zero-degree
   // vertices are pre-set in visited).
@@ -533,7 +533,15 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
     const vid_t u0 = n_u;
     fetch_rows(j + 1, n_rs, n_e, n_u);  // in flight during this word's bit test
     // First probe: the row's first (highest-degree, hub-first order) neighbour.
-    bool found = (rs < e) && test_bit(fr, u0);
+    bool found = false;
+    if (rs < e) {
+      if constexpr (kHub) {
+        const vid_t hb = u0 & ~kHubFlag;
+        found = (u0 & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u0);
+      } else {
+        found = test_bit(fr, u0);
+      }
+    }
     if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
     word_t res = 0;
     if (vis != ~0ull) {
@@ -559,7 +567,6 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
         // edges, whatever rows they belong to, then drops the rows that hit or
         // ran out.  Steps = ceil(sum of remaining lengths / 64) instead of one
         // or more dependent steps per unresolved vertex.
-        int* own = s_bu_owner + (threadIdx.x & ~(kWave - 1));
         for (;;) {
           const long long rem = (!found && p < e) ? static_cast<long long>(e - p) : 0;
           if (!__ballot(rem > 0)) break;
@@ -615,7 +622,78 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
     }
     if (lane == 0) a.new_frontier[w] = res;
   }
+}
+
+template <bool kPacked>
+__global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
+  __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  long long cnt = 0, deg = 0;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
+  bu_wave<kPacked, false>(a, w0, s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0), nullptr, cnt, deg);
   unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
+}
+
+// Hub variant: persistent 1024-thread workgroups (two per CU: 32 waves) that
+// first stage the hub frontier bits (<= kMaxHubs bits, 64 KiB) in LDS; a
+// hub-encoded head is then probed in LDS instead of by a scattered load of the
+// 8 MiB (RMAT-26) frontier bitmap -- at the dominant bottom-up level ~80% of
+// the unvisited vertices resolve at their head, ~85% of heads are hubs.  Four
+// unit groups of 4 waves walk the units; every workgroup runs the same number
+// of iterations (barriers stay uniform).
+constexpr int kHubBuThreads = 1024;
+constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
+
+template <bool kPacked>
+__global__ __launch_bounds__(kHubBuThreads, 8) void bu_hub_kernel(BuArgs a) {
+  __shared__ word_t s_hub[kHubWords];
+  __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
+  __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
+  for (int64_t i = threadIdx.x; i < hw; i += kHubBuThreads) s_hub[i] = a.hub_front[i];
+  __syncthreads();
+  constexpr int kGroups = kHubBuThreads / kUnitThreads;
+  const int wave = threadIdx.x >> 6;
+  const int group = wave / kUnitWaves;
+  const int wg = wave % kUnitWaves;
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
+    const int64_t u = base + group;
+    long long cnt = 0, deg = 0;
+    if (u < nunits)
+      bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords,
+                             s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0), s_hub, cnt, deg);
+    cnt = wave_sum(cnt);
+    deg = wave_sum(deg);
+    if (lane_id() == 0) {
+      s_c[wave] = cnt;
+      s_d[wave] = deg;
+    }
+    __syncthreads();
+    if ((threadIdx.x & (kUnitThreads - 1)) == 0 && u < nunits) {
+      long long c = 0, d = 0;
+#pragma unroll
+      for (int k = 0; k < kUnitWaves; ++k) {
+        c += s_c[group * kUnitWaves + k];
+        d += s_d[group * kUnitWaves + k];
+      }
+      a.unit_cnt[u] = c;
+      a.unit_deg[u] = d;
+    }
+    __syncthreads();
+  }
+}
+
+// hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word.
+__global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int64_t h = w * kWave + lane_id();
+  const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);
+  const word_t m = __ballot(bit);
+  if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
 }
 
 // Zero-degree / padding mask of the owned slice (computed once per graph).
@@ -725,12 +803,40 @@ void pack_bytes(const PackArgs& a, hipStream_t st) {
   pack_bytes_kernel<<<grid_for(a.words, kBlock), kBlock, 0, st>>>(a);
 }
 
+// Compute units of the current device (cached per device id).
+int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
+  if (a.g.nhubs > 0 && a.hub_front) {
+    const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+    const unsigned grid = grid_for(nunits, kHubBuThreads / kUnitThreads, 2 * device_cus());
+    if (a.packed)
+      bu_hub_kernel<true><<<grid, kHubBuThreads, 0, st>>>(a);
+    else
+      bu_hub_kernel<false><<<grid, kHubBuThreads, 0, st>>>(a);
+    return;
+  }
   if (a.packed)
     bu_kernel<true><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
   else
     bu_kernel<false><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+}
+
+void hub_gather(const HubGatherArgs& a, hipStream_t st) {
+  if (a.g.nhubs <= 0) return;
+  hub_gather_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
 }
 
 void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st) {

@@ -121,16 +121,56 @@ __global__ __launch_bounds__(kBlock) void sort_medium_rows_kernel(const eid_t* _
 }
 
 __global__ __launch_bounds__(kBlock) void row_heads_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ col,
-                                                          int64_t rows, vid_t* __restrict__ head) {
+                                                          int64_t rows, vid_t* __restrict__ head,
+                                                          const uint32_t* __restrict__ hub_idx) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (r < rows) head[r] = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;
+  if (r >= rows) return;
+  vid_t h = 0;
+  if (ro[r + 1] > ro[r]) {
+    h = col[ro[r]];
+    if (hub_idx) {
+      const uint32_t k = hub_idx[h];
+      if (k != 0xFFFFFFFFu) h = kHubFlag | k;
+    }
+  }
+  head[r] = h;
+}
+
+// Hubs = vertices of degree >= min_deg, indexed in wave-ballot order (one
+// atomic per wave).
+__global__ __launch_bounds__(kBlock) void select_hubs_kernel(const uint32_t* __restrict__ deg, int64_t n,
+                                                            uint32_t min_deg, vid_t* __restrict__ hub_vertex,
+                                                            uint32_t* __restrict__ hub_idx,
+                                                            unsigned long long* count) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool hub = v < n && deg[v] >= min_deg;
+  const unsigned long long m = __ballot(hub);
+  const int lane = lane_id();
+  unsigned long long base = 0;
+  const int leader = m ? __ffsll(static_cast<long long>(m)) - 1 : 0;
+  if (m && lane == leader) base = atomicAdd(count, static_cast<unsigned long long>(__popcll(m)));
+  base = __shfl(base, leader, kWave);
+  if (v < n) {
+    const unsigned long long slot = base + mask_rank(m);
+    if (hub) hub_vertex[slot] = static_cast<vid_t>(v);
+    hub_idx[v] = hub ? static_cast<uint32_t>(slot) : 0xFFFFFFFFu;
+  }
 }
 
 }  // namespace
 
-void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, hipStream_t st) {
+void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx,
+               hipStream_t st) {
   if (rows <= 0) return;
-  row_heads_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, col, rows, head);
+  row_heads_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, col, rows, head,
+                                                                                          hub_idx);
+}
+
+void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex, uint32_t* hub_idx,
+                 unsigned long long* count, hipStream_t st) {
+  if (n <= 0) return;
+  select_hubs_kernel<<<static_cast<unsigned>((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(deg, n, min_deg, hub_vertex,
+                                                                                         hub_idx, count);
 }
 
 void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st) {

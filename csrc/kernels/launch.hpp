@@ -21,6 +21,7 @@ void td_expand(const TdArgs& a, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
 void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
+void hub_gather(const HubGatherArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 
@@ -43,7 +44,11 @@ void compute_parents(const ParentArgs& a, hipStream_t st);
 
 // graph_sort.hip
 void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st);
-void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, hipStream_t st);
+void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx,
+               hipStream_t st);
+// count must be zeroed by the caller
+void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex, uint32_t* hub_idx,
+                 unsigned long long* count, hipStream_t st);
 // list must hold `rows` entries; count is one device counter
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);

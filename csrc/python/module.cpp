@@ -400,8 +400,9 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("partition", &DeviceGraph::partition)
       .def("to_host", &DeviceGraph::to_host, py::call_guard<py::gil_scoped_release>())
       .def("sort_neighbors_by_degree", &DeviceGraph::sort_neighbors_by_degree, py::arg("comm"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("hubs") = true, py::arg("max_hubs") = kMaxHubs, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
+      .def_property_readonly("nhubs", &DeviceGraph::nhubs)
       .def("degrees_of", &DeviceGraph::degrees_of);
 
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")

@@ -39,10 +39,13 @@ class BFS:
 
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
                  alpha: float = 24.0, beta: float = 24.0, bu_lane_limit: int = 8, phase_timing: bool = False,
-                 hub_sort: bool = True, force_exchange: bool = False):
+                 hub_sort: bool = True, force_exchange: bool = False, hubs: bool = True,
+                 max_hubs: Optional[int] = None):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
-        frontier parent sooner (see csrc/kernels/graph_sort.hip)."""
+        frontier parent sooner (see csrc/kernels/graph_sort.hip).  ``hubs`` also
+        indexes the highest-degree vertices so that bottom-up probes of them test
+        an LDS-resident copy of their frontier bits (needs ``hub_sort``)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.rt = runtime or init_runtime()
@@ -59,7 +62,10 @@ class BFS:
         else:
             raise TypeError("graph must be a path, HostCSR or GenParams")
         if hub_sort:
-            self.graph.sort_neighbors_by_degree(self.rt.comm)
+            if max_hubs is None:
+                self.graph.sort_neighbors_by_degree(self.rt.comm, hubs)
+            else:
+                self.graph.sort_neighbors_by_degree(self.rt.comm, hubs, int(max_hubs))
         self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
                                bu_lane_limit=bu_lane_limit, phase_timing=phase_timing,
                                force_exchange=force_exchange)

@@ -293,3 +293,46 @@ def test_perf_regression_do_vs_ref_gpu(gpu_runtime):
     t_ref = sum(ref.run(r).ms for r in roots)
     t_do = sum(do.run(r).ms for r in roots)
     assert t_do * 10 < t_ref, (t_do, t_ref)
+
+
+@pytest.mark.parametrize("max_hubs", [None, 64, 3000, 0])
+@pytest.mark.parametrize("packed", [0, 1])
+def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed):
+    """Bottom-up with hub-encoded heads probed in the LDS copy of the hub
+    frontier bits: every vertex a hub (default cap on a small graph), a few
+    hubs (mixed LDS / global head probes), no hubs (plain kernel)."""
+    p = dbfs.rmat_params(16, 16, 53)
+    csr = dbfs.host_csr_from_params(p)
+    for mode in ["bu", "do"]:
+        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, max_hubs=max_hubs)
+        if max_hubs is not None:
+            assert bfs.graph.nhubs <= max_hubs
+        if max_hubs != 0:
+            assert bfs.graph.nhubs > 0
+        bfs.engine.set_option("bu_packed", packed)
+        for src in bfs.sample_roots(3, seed=11):
+            _check(bfs, csr, src)
+        bfs.engine.set_option("device_loop", 0)
+        _check(bfs, csr, bfs.sample_roots(1, seed=12)[0])
+
+
+def test_hub_lds_virtual_ranks_gpu():
+    """Hub path on 3 virtual ranks: the hub frontier bits are gathered from the
+    all-gathered global frontier of every rank."""
+    p = dbfs.rmat_params(15, 16, 59)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [2, 900, 20000]
+    exp = [dbfs.cpu_bfs(csr, s)[0] for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode="do", max_hubs=2000)
+        assert 0 < bfs.graph.nhubs <= 2000
+        out = []
+        for s in srcs:
+            bfs.run(s)
+            out.append(bfs.levels())
+        return out
+
+    for rank_out in run_virtual_ranks(3, body, device="hip"):
+        for lv, e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
