@@ -60,6 +60,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "device_loop") o.device_loop = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
+  else if (name == "bu_compact") o.bu_compact = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -76,7 +77,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
-          {"bu_packed", o.bu_packed ? 1.0 : 0.0}};
+          {"bu_packed", o.bu_packed ? 1.0 : 0.0},
+          {"bu_compact", o.bu_compact ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -659,6 +661,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
+      ba.compact = opt_.bu_compact;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       if (gv.nhubs > 0) {
@@ -881,6 +884,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
+      ba.compact = opt_.bu_compact;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();

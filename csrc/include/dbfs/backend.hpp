@@ -278,6 +278,7 @@ struct BuArgs {
   int64_t words = 0;
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
   bool packed = false;               // wave cooperation over a packed multi-row edge stream
+  bool compact = true;               // waves process their unvisited vertices 64 at a time
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'

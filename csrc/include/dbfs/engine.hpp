@@ -81,6 +81,9 @@ struct EngineOptions {
   // Bottom-up rows still unresolved after the per-lane phase are scanned as
   // one packed edge stream per wave (else one row at a time).
   bool bu_packed = false;
+  // Bottom-up waves number their unvisited vertices and take 64 per step
+  // (else one bitmap word per step).
+  bool bu_compact = true;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -476,6 +476,90 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
   if (bits) a.next[w] |= bits;
 }
 
+// Rest of a bottom-up row after the head probe: phase 1, each unresolved lane
+// checks its next `lane_limit` neighbours (loads batched 4-wide); phase 2,
+// rows still unresolved are scanned by the whole wave (64 neighbours per step,
+// ballot early exit; kPacked: several rows as one packed edge stream).
+// Wave-uniform call (phase 2 is cooperative); returns the lane's `found`.
+template <bool kPacked>
+__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own) {
+  const int lane = lane_id();
+  const vid_t* __restrict__ col = a.g.col;
+  const word_t* __restrict__ fr = a.frontier;
+  // positions relative to the row start: 32-bit (a row never holds 2^32 entries)
+  const vid_t* __restrict__ row = col + rs;
+  const uint32_t len = static_cast<uint32_t>(e - rs);
+  uint32_t p = min(len, 1u);
+  const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
+  while (p < lim && !found) {
+    vid_t u[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ok[k] = p + k < lim;
+      u[k] = ok[k] ? row[p + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) found |= ok[k] && test_bit(fr, u[k]);
+    p += 4;
+  }
+  if (p > lim) p = lim;
+  if constexpr (kPacked) {
+    // Phase 2, packed: the remaining rows of all unresolved lanes form one
+    // edge stream (lane order); every step the wave tests its next 64
+    // edges, whatever rows they belong to, then drops the rows that hit or
+    // ran out.  Steps = ceil(sum of remaining lengths / 64) instead of one
+    // or more dependent steps per unresolved vertex.
+    for (;;) {
+      const long long rem = (!found && p < len) ? static_cast<long long>(len - p) : 0;
+      if (!__ballot(rem > 0)) break;
+      const long long incl = wave_incl_scan(rem);
+      const long long excl = incl - rem;
+      own[lane] = -1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (rem > 0 && excl < kWave) own[excl] = lane;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int o = wave_incl_max(own[lane]);  // owner lane of edge slot `lane`
+      const long long total = readlane_i64(incl, kWave - 1);
+      const long long o_excl = __shfl(excl, o, kWave);
+      const long long o_p = __shfl(static_cast<long long>(rs + p), o, kWave);
+      bool hit = false;
+      if (lane < total) hit = test_bit(fr, col[o_p + (lane - o_excl)]);
+      // owners with a hit: set bit o of a wave mask
+      unsigned long long hitmask = hit ? (1ull << o) : 0ull;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) hitmask |= __shfl_xor(hitmask, off, kWave);
+      if ((hitmask >> lane) & 1ull) found = true;
+      const long long took = rem > 0 ? max(0LL, min(rem, static_cast<long long>(kWave) - excl)) : 0;
+      p += static_cast<uint32_t>(took);
+    }
+  } else {
+    // Phase 2: the wave scans each still-unresolved row in turn, 64
+    // neighbours per step.
+    unsigned long long pending = __ballot(!found && p < len);
+    while (pending) {
+      const int l = __ffsll(static_cast<long long>(pending)) - 1;
+      pending &= pending - 1;
+      const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
+      const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
+      bool f = false;
+      for (uint32_t base = ps; base < pe; base += kWave) {
+        const uint32_t idx = base + lane;
+        bool hit = false;
+        if (idx < pe) hit = test_bit(fr, r[idx]);
+        if (__ballot(hit)) {
+          f = true;
+          break;
+        }
+      }
+      if (lane == l) found = f;
+    }
+  }
+  return found;
+}
+
 // ---------------------------------------------------------------------------
 // Fused bottom-up step: a wave owns 16 consecutive bitmap words and walks them
 // one word (64 vertices, one per lane) at a time; fully visited words cost one
@@ -546,72 +630,7 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
     word_t res = 0;
     if (vis != ~0ull) {
       const int64_t v = w * 64 + lane;
-      eid_t p = min(e, rs + 1);
-      const eid_t lim = min(e, rs + static_cast<eid_t>(a.lane_limit));
-      while (p < lim && !found) {
-        vid_t u[4];
-        bool ok[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          ok[k] = p + k < lim;
-          u[k] = ok[k] ? col[p + k] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) found |= ok[k] && test_bit(fr, u[k]);
-        p += 4;
-      }
-      if (p > lim) p = lim;
-      if constexpr (kPacked) {
-        // Phase 2, packed: the remaining rows of all unresolved lanes form one
-        // edge stream (lane order); every step the wave tests its next 64
-        // edges, whatever rows they belong to, then drops the rows that hit or
-        // ran out.  Steps = ceil(sum of remaining lengths / 64) instead of one
-        // or more dependent steps per unresolved vertex.
-        for (;;) {
-          const long long rem = (!found && p < e) ? static_cast<long long>(e - p) : 0;
-          if (!__ballot(rem > 0)) break;
-          const long long incl = wave_incl_scan(rem);
-          const long long excl = incl - rem;
-          own[lane] = -1;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          if (rem > 0 && excl < kWave) own[excl] = lane;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          const int o = wave_incl_max(own[lane]);  // owner lane of edge slot `lane`
-          const long long total = readlane_i64(incl, kWave - 1);
-          const long long o_excl = __shfl(excl, o, kWave);
-          const long long o_p = __shfl(static_cast<long long>(p), o, kWave);
-          bool hit = false;
-          if (lane < total) hit = test_bit(fr, col[o_p + (lane - o_excl)]);
-          // owners with a hit: set bit o of a wave mask
-          unsigned long long hitmask = hit ? (1ull << o) : 0ull;
-#pragma unroll
-          for (int off = 1; off < kWave; off <<= 1) hitmask |= __shfl_xor(hitmask, off, kWave);
-          if ((hitmask >> lane) & 1ull) found = true;
-          const long long took = rem > 0 ? max(0LL, min(rem, static_cast<long long>(kWave) - excl)) : 0;
-          p += took;
-        }
-      } else {
-        unsigned long long pending = __ballot(!found && p < e);
-        while (pending) {
-          const int l = __ffsll(static_cast<long long>(pending)) - 1;
-          pending &= pending - 1;
-          const long long ps = __shfl(static_cast<long long>(p), l, kWave);
-          const long long pe = __shfl(static_cast<long long>(e), l, kWave);
-          bool f = false;
-          for (long long base = ps; base < pe; base += kWave) {
-            const long long idx = base + lane;
-            bool hit = false;
-            if (idx < pe) hit = test_bit(fr, col[idx]);
-            if (__ballot(hit)) {
-              f = true;
-              break;
-            }
-          }
-          if (lane == l) found = f;
-        }
-      }
+      found = bu_scan_row<kPacked>(a, rs, e, found, own);
       res = __ballot(found);
       if (found) {
         a.level[v] = a.new_level;
@@ -624,13 +643,136 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
   }
 }
 
-template <bool kPacked>
+// Position of the r-th (0-based) set bit of x (r < popcount(x)).
+__device__ __forceinline__ int select_bit(word_t x, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int width = 32; width >= 1; width >>= 1) {
+    const int c = __popcll(x & ((1ull << width) - 1ull));
+    if (r >= c) {
+      r -= c;
+      x >>= width;
+      pos += width;
+    }
+  }
+  return pos;
+}
+
+// Compacted variant of bu_wave: the unvisited vertices of the wave's 16 words
+// are numbered (per-word popcount prefix) and processed 64 at a time, one per
+// lane, whatever word they sit in -- instead of one word (64 lanes, many of
+// them visited) per step.  The per-step cost of a bottom-up wave is a chain of
+// dependent memory round trips nearly independent of how many lanes are
+// active, so steps = ceil(unvisited / 64) instead of the number of words
+// with any unvisited vertex: at the dense first bottom-up level of RMAT-26
+// (~half the lanes unvisited) half the steps, at the later levels (a few per
+// word) a fraction.  Found bits are OR-ed into a per-wave LDS copy of the 16
+// result words (s_res), written out once.
+template <bool kPacked, bool kHub>
+__device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int* own, word_t* s_res,
+                                                const word_t* s_hub, long long& cnt, long long& deg) {
+  const int lane = lane_id();
+  const int64_t left = a.words - w0;
+  const int nw = left <= 0 ? 0 : (left < kWaveWords ? static_cast<int>(left) : kWaveWords);
+  // unvisited bits of word `lane` (0 past the words); visited = ~um
+  const word_t um = lane < nw ? ~a.visited[w0 + lane] : 0ull;
+  const int incl = static_cast<int>(wave_incl_scan(__popcll(um)));
+  const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  if (lane < kWaveWords) s_res[lane] = 0ull;
+  if (total == 0) {
+    if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const vid_t* __restrict__ col = a.g.col;
+  const word_t* __restrict__ fr = a.frontier;
+  const vid_t* __restrict__ head = a.g.head;
+  // Unvisited vertex number 64 b + lane -> its position loc = 64 j + bit in the
+  // wave's 1024 vertices (-1: no vertex), row bounds and head.
+  // (row start, 32-bit length) keep the prefetched state small: the hub
+  // kernel runs at 64 VGPRs (two 1024-thread workgroups per CU).
+  auto fetch = [&](int b, int& loc, eid_t& rs, uint32_t& len, vid_t& u) {
+    loc = -1;
+    rs = 0;
+    len = 0;
+    u = 0;
+    const int idx = b * kWave + lane;
+    if (b * kWave >= total) return;  // uniform
+    // word j = number of words ending at or before idx; ex = where j starts
+    int j = 0, ex = 0;
+    for (int i = 0; i < nw; ++i) {
+      const int end_i = __builtin_amdgcn_readlane(incl, i);
+      if (end_i <= idx) {
+        ++j;
+        ex = end_i;
+      }
+    }
+    j = min(j, nw - 1);
+    const word_t umj = static_cast<word_t>(__shfl(static_cast<long long>(um), j, kWave));
+    if (idx < total) {
+      loc = j * 64 + select_bit(umj, idx - ex);
+      const int64_t v = w0 * 64 + loc;
+      rs = ro[v];
+      len = static_cast<uint32_t>(ro[v + 1] - rs);
+      if (head) u = head[v];
+    }
+  };
+  const int nb = (total + kWave - 1) / kWave;
+  int n_loc;
+  eid_t n_rs;
+  uint32_t n_len;
+  vid_t n_u;
+  fetch(0, n_loc, n_rs, n_len, n_u);
+  if (!head) n_u = n_len ? col[n_rs] : 0u;
+  int cnt32 = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int loc = n_loc;
+    const eid_t rs = n_rs, e = n_rs + n_len;
+    const vid_t u0 = n_u;
+    fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
+    bool found = false;
+    if (rs < e) {
+      if constexpr (kHub) {
+        const vid_t hb = u0 & ~kHubFlag;
+        found = (u0 & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u0);
+      } else {
+        found = test_bit(fr, u0);
+      }
+    }
+    if (!head) n_u = n_len ? col[n_rs] : 0u;
+    found = bu_scan_row<kPacked>(a, rs, e, found, own);
+    if (found) {
+      a.level[w0 * 64 + loc] = a.new_level;
+      cnt32 += 1;
+      deg += e - rs;
+      __hip_atomic_fetch_or(s_res + (loc >> 6), 1ull << (loc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
+  cnt += cnt32;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < nw) {
+    const word_t res = s_res[lane];
+    a.new_frontier[w0 + lane] = res;
+    if (res) a.visited[w0 + lane] = ~um | res;
+  }
+}
+
+template <bool kPacked, bool kCompact>
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
   __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
+  __shared__ word_t s_res[kCompact ? kUnitWaves * kWaveWords : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   long long cnt = 0, deg = 0;
-  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + (threadIdx.x >> 6) * kWaveWords;
-  bu_wave<kPacked, false>(a, w0, s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0), nullptr, cnt, deg);
+  const int wave = threadIdx.x >> 6;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + wave * kWaveWords;
+  int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
+  if constexpr (kCompact)
+    bu_wave_compact<kPacked, false>(a, w0, own, s_res + wave * kWaveWords, nullptr, cnt, deg);
+  else
+    bu_wave<kPacked, false>(a, w0, own, nullptr, cnt, deg);
   unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
 }
 
@@ -644,10 +786,11 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
 constexpr int kHubBuThreads = 1024;
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
-template <bool kPacked>
+template <bool kPacked, bool kCompact>
 __global__ __launch_bounds__(kHubBuThreads, 8) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
+  __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kWaveWords : 1];
   __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
@@ -662,9 +805,14 @@ __global__ __launch_bounds__(kHubBuThreads, 8) void bu_hub_kernel(BuArgs a) {
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
-    if (u < nunits)
-      bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords,
-                             s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0), s_hub, cnt, deg);
+    if (u < nunits) {
+      int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
+      if constexpr (kCompact)
+        bu_wave_compact<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_res + wave * kWaveWords, s_hub,
+                                       cnt, deg);
+      else
+        bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_hub, cnt, deg);
+    }
     cnt = wave_sum(cnt);
     deg = wave_sum(deg);
     if (lane_id() == 0) {
@@ -822,16 +970,21 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
     const unsigned grid = grid_for(nunits, kHubBuThreads / kUnitThreads, 2 * device_cus());
+#define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
     if (a.packed)
-      bu_hub_kernel<true><<<grid, kHubBuThreads, 0, st>>>(a);
+      a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
     else
-      bu_hub_kernel<false><<<grid, kHubBuThreads, 0, st>>>(a);
+      a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);
+#undef DBFS_BU_HUB
     return;
   }
+  const unsigned grid = grid_for(a.words, kUnitWords);
+#define DBFS_BU(P, C) bu_kernel<P, C><<<grid, kUnitThreads, 0, st>>>(a)
   if (a.packed)
-    bu_kernel<true><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+    a.compact ? DBFS_BU(true, true) : DBFS_BU(true, false);
   else
-    bu_kernel<false><<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+    a.compact ? DBFS_BU(false, true) : DBFS_BU(false, false);
+#undef DBFS_BU
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {
