@@ -18,7 +18,7 @@ EXT_SUFFIX:= $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_v
 
 COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-result
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
-HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics
+HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib -lpthread
 
 HOST_SRC  := csrc/graph/io.cpp csrc/graph/csr.cpp csrc/backend/cpu_backend.cpp \

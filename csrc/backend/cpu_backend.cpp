@@ -91,6 +91,37 @@ class CpuBackend final : public Backend {
   }
 
   void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override { *c = init; }
+  void init_run(const InitRunArgs& a) override {
+    const int64_t src = a.src_local;
+    for (int64_t i = 0; i < a.g.rows; ++i) a.level[i] = i == src ? 0 : kUnreached;
+    for (int64_t w = 0; w < a.gwords; ++w) a.visited[w] = a.zdeg[w];
+    for (int64_t w = 0; w < a.words; ++w) a.frontier[w] = 0;
+    int64_t cnt = 0, deg = 0;
+    if (src >= 0) {
+      const word_t bit = 1ull << (src & 63);
+      a.visited[a.vis_word_base + (src >> 6)] |= bit;
+      a.frontier[src >> 6] = bit;
+      const eid_t d = a.g.row_off[src + 1] - a.g.row_off[src];
+      if (d > 0) { cnt = 1; deg = d; }
+      const int64_t unit = (src >> 6) / kUnitWords;
+      a.unit_cnt[unit] = a.unit_deg[unit] = 0;
+      a.part_cnt[unit / kScanChunk] = a.part_deg[unit / kScanChunk] = 0;
+    }
+    a.stats[0] = a.stats[2] = cnt;
+    a.stats[1] = a.stats[3] = deg;
+    a.qscan[cnt] = deg;
+    if (a.ctrl) {
+      LevelCtrl c = a.ctrl_init;
+      level_ctrl_finish(c, cnt, deg, true, nullptr);
+      *a.ctrl = c;
+      if (a.mailbox) {
+        a.mailbox->done = c.done;
+        a.mailbox->vis_deg = c.vis_deg;
+        a.mailbox->next_dir = c.dir;
+        a.mailbox->level = -1;
+      }
+    }
+  }
   void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) override {
     for (int k = 0; k < 4; ++k) mb->v[k] = stats[k];
     __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);

@@ -156,6 +156,7 @@ class HipBackend final : public Backend {
     kern::level_ctrl_init(c, init, st_);
     chk();
   }
+  void init_run(const InitRunArgs& a) override { on(); kern::init_run(a, st_); chk(); }
   void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) override {
     on();
     kern::publish_stats(stats, mb, seq, st_);

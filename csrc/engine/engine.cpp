@@ -418,6 +418,44 @@ RunResult Engine::run(int64_t source) {
   return r;
 }
 
+// Scratch bitmaps every consumer leaves zeroed (`next` bits cleared by the
+// consuming update or re-zeroed after the exchange, the byte map by its
+// gather, `cand` by its update): only a run that ended early (an error,
+// injected fault) leaves them dirty, and then they are cleared here.
+void Engine::begin_run_scratch() {
+  if (scratch_dirty_) {
+    be_.memset_async(cand_.data(), 0, cand_.bytes());
+    be_.memset_async(next_.data(), 0, next_.bytes());
+    if (next_bytes_.data()) be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
+  }
+  scratch_dirty_ = true;  // until the run completes
+}
+
+InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
+                              LevelMailbox* mailbox) {
+  const int me = comm_.rank();
+  InitRunArgs ia;
+  ia.g = g_.view();
+  ia.level = level_.data();
+  ia.zdeg = zdeg_.data();
+  ia.visited = visited_.data();
+  ia.gwords = part_.global_words();
+  ia.frontier = seed_frontier;
+  ia.words = part_.slice_words();
+  ia.src_local = part_.owner(source) == me ? source - g_.lo() : -1;
+  ia.vis_word_base = static_cast<int64_t>(me) * part_.slice_words();
+  ia.unit_cnt = unit_cnt_.data();
+  ia.unit_deg = unit_deg_.data();
+  ia.part_cnt = part_cnt_.data();
+  ia.part_deg = part_deg_.data();
+  ia.stats = stats_.data();
+  ia.qscan = qscan_.data();
+  ia.ctrl = ctrl;
+  ia.ctrl_init = ctrl_init;
+  ia.mailbox = mailbox;
+  return ia;
+}
+
 RunResult Engine::run_bitmap(int64_t source) {
   alloc_bitmap_state();
   TraceRange trace_run(std::string("bfs.run mode=") + mode_name(opt_.mode) + " src=" + std::to_string(source));
@@ -440,12 +478,9 @@ RunResult Engine::run_bitmap(int64_t source) {
   comm_.barrier();
   const auto t0 = std::chrono::steady_clock::now();
 
-  // ---- init (inside the timed window) ----
-  be_.fill_level(level_.data(), g_.rows(), kUnreached);
-  be_.copy_async(visited_.data(), zdeg_.data(), visited_.bytes());
-  be_.memset_async(cand_.data(), 0, cand_.bytes());
-  be_.memset_async(next_.data(), 0, next_.bytes());
-  if (part_.owner(source) == me) be_.set_bit(cand_.data(), source - lo);
+  // ---- init (inside the timed window): one fused pass, seed totals included ----
+  begin_run_scratch();
+  be_.init_run(init_args(source, frontier_[1].data() + me * W, nullptr, LevelCtrl(), nullptr));
 
   // Collectives of the current level, bracketed by events when phase timing is
   // on (LevelRecord::comm_ms).
@@ -508,9 +543,10 @@ RunResult Engine::run_bitmap(int64_t source) {
   };
 
   int64_t hs[4];
-  // Seed: the source is forced in even when it has degree 0 (pre-visited).
-  update(cand_.data(), 1, true, true, 0);
-  finish_level(hs);
+  // Seed totals (written by init_run; the source counts with degree > 0 only).
+  cur ^= 1;
+  if (exchange()) timed_comm([&] { comm_.allreduce_sum_i64(stats_.data() + 2, 2); });
+  read_level_stats(hs);
   int64_t q_local = hs[0], m_local = hs[1], n_f = hs[2], m_f = hs[3];
   int64_t vis_deg = m_f;
   int64_t prev_nf = 0;
@@ -701,6 +737,7 @@ RunResult Engine::run_bitmap(int64_t source) {
   }
   be_.synchronize();
   const auto t1 = std::chrono::steady_clock::now();
+  scratch_dirty_ = false;
   const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   res.ms = comm_.max_host(ms);
   res.depth = res.levels.empty() ? 1 : static_cast<int>(res.levels.size());
@@ -728,7 +765,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   TraceRange trace_run(std::string("bfs.run(device loop) mode=") + mode_name(opt_.mode) + " src=" +
                        std::to_string(source));
   const int64_t W = part_.slice_words();
-  const int64_t lo = g_.lo();
   const ShardView gv = g_.view();
   if (!ctrl_.data()) ctrl_ = DBuf<LevelCtrl>(be_, 1);
   if (rec_.size() < 64) rec_ = DBuf<LevelRecDev>(be_, 64);
@@ -762,11 +798,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   comm_.barrier();
   const auto t0 = std::chrono::steady_clock::now();
 
-  be_.fill_level(level_.data(), g_.rows(), kUnreached);
-  be_.copy_async(visited_.data(), zdeg_.data(), visited_.bytes());
-  be_.memset_async(cand_.data(), 0, cand_.bytes());
-  be_.memset_async(next_.data(), 0, next_.bytes());
-  be_.set_bit(cand_.data(), source - lo);
+  begin_run_scratch();
   LevelCtrl init;
   init.mode = opt_.mode == Mode::TopDown ? 0 : opt_.mode == Mode::BottomUp ? 1 : 2;
   init.alpha = opt_.alpha;
@@ -776,7 +808,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   init.td_byte_edges = bytes_ok ? static_cast<double>(opt_.td_byte_edges) : 1e300;
   init.check_visited_min = opt_.td_check_visited_min;
   init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
-  be_.level_ctrl_init(ctrl_.data(), init);
+  // one fused pass: levels, visited, the seed frontier (frontier_[1]), its
+  // totals, the seeded LevelCtrl and the mailbox stamp of level -1
+  be_.init_run(init_args(source, frontier_[1].data(), ctrl_.data(), init, mailbox_dev_ + slot(-1)));
 
   auto scan = [&](int level, bool seed, char expect_dir) {
     ScanArgs sa;
@@ -796,24 +830,18 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.expect_dir = expect_dir;
     be_.scan_units(sa);
   };
-  // Frontier double buffer: the seed writes frontier_[1]; level L reads
+  // Frontier double buffer: the seed is frontier_[1]; level L reads
   // frontier_[(L + 1) & 1] and writes the other one.
   UpdateArgs ua;
   ua.g = gv;
-  ua.cand = cand_.data();
   ua.nchunks = 1;
   ua.cand_stride = W;
   ua.clear_cand = true;
-  ua.force = true;  // the source counts even with degree 0
   ua.visited = visited_.data();
-  ua.frontier = frontier_[1].data();
   ua.level = level_.data();
-  ua.new_level = 0;
   ua.words = W;
   ua.unit_cnt = unit_cnt_.data();
   ua.unit_deg = unit_deg_.data();
-  be_.update_frontier(ua);
-  scan(-1, true, 0);
 
   const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), 2048));
   std::vector<std::pair<int, int>> evs;
@@ -924,6 +952,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   }
   be_.synchronize();
   const auto t1 = std::chrono::steady_clock::now();
+  scratch_dirty_ = false;
   res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   const int64_t vis_deg = mailbox_host_[slot(nlev - 1)].vis_deg;
 

@@ -132,6 +132,36 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
   c.check_visited = static_cast<double>(c.vis_deg) >= c.check_visited_min * c.total_directed ? 1 : 0;
 }
 
+// Per-run initialisation of the bitmap engine in one pass (replaces a level
+// fill, a visited copy, the seed update and its scan: ~8 dependent launches):
+//   level[r] = kUnreached (0 for the source), visited = zdeg (+ source bit),
+//   frontier (owned slice) = source bit only, and the seed's totals --
+//   stats[0..3] = (count, degree sum) of {source} counting degree > 0 only,
+//   qscan[count] = degree sum, the source unit's scan offsets = 0 -- exactly
+//   what update + scan leave for a one-vertex frontier.  With ctrl, the
+//   device-loop state is *ctrl = level_ctrl_finish(ctrl_init, seed) and the
+//   mailbox slot of level -1 is stamped.
+struct InitRunArgs {
+  ShardView g;
+  lvl_t* level = nullptr;          // rows
+  const word_t* zdeg = nullptr;    // global
+  word_t* visited = nullptr;       // global
+  int64_t gwords = 0;
+  word_t* frontier = nullptr;      // owned slice of the seed frontier
+  int64_t words = 0;
+  int64_t src_local = -1;          // source row on this rank, -1 if not owned
+  int64_t vis_word_base = 0;       // global word index of the owned slice
+  int64_t* unit_cnt = nullptr;
+  int64_t* unit_deg = nullptr;
+  int64_t* part_cnt = nullptr;
+  int64_t* part_deg = nullptr;
+  int64_t* stats = nullptr;
+  int64_t* qscan = nullptr;
+  LevelCtrl* ctrl = nullptr;
+  LevelCtrl ctrl_init;
+  LevelMailbox* mailbox = nullptr;
+};
+
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -429,6 +459,7 @@ class Backend {
   virtual void scan_units(const ScanArgs& a) = 0;
   // *ctrl = init (stream-ordered)
   virtual void level_ctrl_init(LevelCtrl* ctrl, const LevelCtrl& init) = 0;
+  virtual void init_run(const InitRunArgs& a) = 0;
   // mb->v[0..3] = stats[0..3], then mb->seq = seq (release); mb is the device
   // pointer of an alloc_mapped block.
   virtual void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq) = 0;

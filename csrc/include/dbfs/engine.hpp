@@ -171,6 +171,10 @@ class Engine {
   bool use_device_loop() const;
   RunResult run_ref(int64_t source);
   void alloc_bitmap_state();
+  void begin_run_scratch();
+  InitRunArgs init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
+                        LevelMailbox* mailbox);
+  bool scratch_dirty_ = true;  // cand / next / byte map may hold stale bits
   void alloc_ref_state();
   void gather_levels_device(DBuf<lvl_t>& full);
   bool exchange() const { return part_.nranks > 1 || opt_.force_exchange; }

@@ -24,6 +24,8 @@
 //     visited word, levels and unit stats itself (no separate update pass).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "launch.hpp"
 #include "wave.hpp"
 
@@ -55,6 +57,65 @@ __global__ void ctrl_init_kernel(LevelCtrl* c, LevelCtrl init) {
 
 __global__ void set_bit_kernel(word_t* bm, int64_t bit) {
   if (threadIdx.x == 0) bm[bit >> 6] |= 1ull << (bit & 63);
+}
+
+// Fused per-run initialisation (InitRunArgs).  Grid-stride over the level
+// array (16-B stores), the global visited words and the owned frontier words;
+// the element holding the source is written with its seeded value by the same
+// thread that fills it, so no ordering between threads is needed.  Thread 0 of
+// block 0 writes the seed's totals / work-list offsets / device-loop state.
+__global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const int64_t rows = a.g.rows;
+  const int64_t src = a.src_local;
+  // level: rows / 4 int4 stores (+ tail)
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(a.level) & 15u) == 0 ? rows / 4 : 0;
+  int4* l4 = reinterpret_cast<int4*>(a.level);
+  for (int64_t i = t0; i < n4; i += stride) {
+    int4 v = make_int4(kUnreached, kUnreached, kUnreached, kUnreached);
+    if (src >= 0 && (src >> 2) == i) {
+      if ((src & 3) == 0) v.x = 0;
+      else if ((src & 3) == 1) v.y = 0;
+      else if ((src & 3) == 2) v.z = 0;
+      else v.w = 0;
+    }
+    l4[i] = v;
+  }
+  for (int64_t i = n4 * 4 + t0; i < rows; i += stride) a.level[i] = i == src ? 0 : kUnreached;
+  const int64_t sw = src >= 0 ? a.vis_word_base + (src >> 6) : -1;
+  const word_t sbit = src >= 0 ? (1ull << (src & 63)) : 0ull;
+  for (int64_t w = t0; w < a.gwords; w += stride) a.visited[w] = a.zdeg[w] | (w == sw ? sbit : 0ull);
+  for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? sbit : 0ull;
+  if (t0 != 0) return;
+  int64_t cnt = 0, deg = 0;
+  if (src >= 0) {
+    const eid_t d = a.g.row_off[src + 1] - a.g.row_off[src];
+    if (d > 0) {
+      cnt = 1;
+      deg = d;
+    }
+    const int64_t unit = (src >> 6) / kUnitWords;
+    a.unit_cnt[unit] = 0;
+    a.unit_deg[unit] = 0;
+    a.part_cnt[unit / kScanChunk] = 0;
+    a.part_deg[unit / kScanChunk] = 0;
+  }
+  a.stats[0] = a.stats[2] = cnt;
+  a.stats[1] = a.stats[3] = deg;
+  a.qscan[cnt] = deg;
+  if (a.ctrl) {
+    LevelCtrl c = a.ctrl_init;
+    level_ctrl_finish(c, cnt, deg, true, nullptr);
+    *a.ctrl = c;
+    if (a.mailbox) {
+      __hip_atomic_store(&a.mailbox->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
+                         static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.mailbox->level, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // Level totals -> host-mapped mailbox: values first (system scope), then the
@@ -481,6 +542,11 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // rows still unresolved are scanned by the whole wave (64 neighbours per step,
 // ballot early exit; kPacked: several rows as one packed edge stream).
 // Wave-uniform call (phase 2 is cooperative); returns the lane's `found`.
+#ifndef DBFS_BU_BATCH
+#define DBFS_BU_BATCH 4
+#endif
+constexpr int kBuBatch = DBFS_BU_BATCH;  // phase-1 column loads in flight per lane
+
 template <bool kPacked>
 __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own) {
   const int lane = lane_id();
@@ -492,16 +558,16 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
   uint32_t p = min(len, 1u);
   const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
   while (p < lim && !found) {
-    vid_t u[4];
-    bool ok[4];
+    vid_t u[kBuBatch];
+    bool ok[kBuBatch];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kBuBatch; ++k) {
       ok[k] = p + k < lim;
       u[k] = ok[k] ? row[p + k] : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) found |= ok[k] && test_bit(fr, u[k]);
-    p += 4;
+    for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && test_bit(fr, u[k]);
+    p += kBuBatch;
   }
   if (p > lim) p = lim;
   if constexpr (kPacked) {
@@ -894,6 +960,13 @@ void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st) {
 void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 0, st>>>(bm, bit); }
 
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
+
+int device_cus();
+
+void init_run(const InitRunArgs& a, hipStream_t st) {
+  const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
+  init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
+}
 
 void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st) {
   publish_stats_kernel<<<1, 64, 0, st>>>(stats, mb, seq);

@@ -13,6 +13,7 @@ void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st);
 void set_bit(word_t* bm, int64_t bit, hipStream_t st);
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st);
 void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st);
+void init_run(const InitRunArgs& a, hipStream_t st);
 void update_frontier(const UpdateArgs& a, hipStream_t st);
 void scan_units(const ScanArgs& a, hipStream_t st);
 void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
