@@ -849,11 +849,15 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
 // the unvisited vertices resolve at their head, ~85% of heads are hubs.  Four
 // unit groups of 4 waves walk the units; every workgroup runs the same number
 // of iterations (barriers stay uniform).
-constexpr int kHubBuThreads = 1024;
+#ifndef DBFS_HUB_BU_THREADS
+#define DBFS_HUB_BU_THREADS 1024
+#endif
+constexpr int kHubBuThreads = DBFS_HUB_BU_THREADS;
+static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
 template <bool kPacked, bool kCompact>
-__global__ __launch_bounds__(kHubBuThreads, 8) void bu_hub_kernel(BuArgs a) {
+__global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
   __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kWaveWords : 1];
