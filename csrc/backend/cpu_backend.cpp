@@ -406,6 +406,26 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void nz_word_counts(const eid_t* ro, int64_t rows, int64_t words, eid_t* counts) override {
+    for (int64_t w = 0; w < words; ++w) {
+      eid_t c = 0;
+      for (int64_t v = w * 64; v < std::min<int64_t>(rows, (w + 1) * 64); ++v) c += ro[v + 1] > ro[v] ? 1 : 0;
+      counts[w] = c;
+    }
+  }
+  void nz_fill(const eid_t* ro, const vid_t* head, int64_t rows, const eid_t* pref, eid_t* nz_ro,
+               vid_t* nz_head) override {
+    int64_t k = 0;
+    for (int64_t v = 0; v < rows; ++v) {
+      if (ro[v + 1] > ro[v]) {
+        nz_ro[k] = ro[v];
+        nz_head[k] = head[v];
+        ++k;
+      }
+    }
+    nz_ro[k] = rows > 0 ? ro[rows] : 0;
+    (void)pref;
+  }
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {
     int64_t k = 0;

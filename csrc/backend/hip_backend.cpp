@@ -203,6 +203,17 @@ class HipBackend final : public Backend {
     kern::row_heads(ro, col, rows, head, hub_idx, st_);
     chk();
   }
+  void nz_word_counts(const eid_t* ro, int64_t rows, int64_t words, eid_t* counts) override {
+    on();
+    kern::nz_word_counts(ro, rows, words, counts, st_);
+    chk();
+  }
+  void nz_fill(const eid_t* ro, const vid_t* head, int64_t rows, const eid_t* pref, eid_t* nz_ro,
+               vid_t* nz_head) override {
+    on();
+    kern::nz_fill(ro, head, rows, div_up(rows, kWordBits), pref, nz_ro, nz_head, st_);
+    chk();
+  }
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {
     on();

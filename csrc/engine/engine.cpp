@@ -61,6 +61,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "bu_compact") o.bu_compact = v != 0;
+  else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -78,7 +79,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"device_loop", o.device_loop ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
-          {"bu_compact", o.bu_compact ? 1.0 : 0.0}};
+          {"bu_compact", o.bu_compact ? 1.0 : 0.0},
+          {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -155,6 +157,9 @@ ShardView DeviceGraph::view() const {
   v.head = head_.data();
   v.hub_vertex = hub_vertex_.data();
   v.nhubs = nhubs_;
+  v.nz_pref = nz_pref_.data();
+  v.nz_row_off = nz_row_off_.data();
+  v.nz_head = nz_head_.data();
   return v;
 }
 
@@ -237,7 +242,23 @@ void DeviceGraph::build_heads(const uint32_t* hub_idx) {
   if (head_.size() < static_cast<size_t>(std::max<int64_t>(rows_, 1)))
     head_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(rows_, 1)));
   be_->row_heads(row_off_.data(), col_.data(), rows_, head_.data(), hub_idx);
+  build_nz_view();
   be_->synchronize();
+}
+
+// Dense copies of row_off / head over the non-empty rows (ShardView::nz_*),
+// rebuilt whenever the heads change.
+void DeviceGraph::build_nz_view() {
+  const int64_t words = div_up(std::max<int64_t>(rows_, 1), kWordBits);
+  nz_pref_ = DBuf<eid_t>(*be_, static_cast<size_t>(words + 1));
+  be_->memset_async(nz_pref_.data(), 0, nz_pref_.bytes());
+  be_->nz_word_counts(row_off_.data(), rows_, words, nz_pref_.data());
+  be_->exclusive_scan(nz_pref_.data(), words);
+  eid_t nzrows = 0;
+  be_->to_host(&nzrows, nz_pref_.data() + words, sizeof(eid_t));
+  nz_row_off_ = DBuf<eid_t>(*be_, static_cast<size_t>(nzrows + 1));
+  nz_head_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<eid_t>(nzrows, 1)));
+  be_->nz_fill(row_off_.data(), head_.data(), rows_, nz_pref_.data(), nz_row_off_.data(), nz_head_.data());
 }
 
 // ---- Engine ----------------------------------------------------------------------
@@ -698,6 +719,8 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
       ba.compact = opt_.bu_compact;
+      ba.zdeg = zdeg_.data() + comm_.rank() * W;
+      if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       if (gv.nhubs > 0) {
@@ -913,6 +936,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
       ba.compact = opt_.bu_compact;
+      ba.zdeg = zdeg_.data() + comm_.rank() * W;
+      if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();

@@ -44,6 +44,14 @@ struct ShardView {
   // vertex id.  Bottom-up keeps the hubs' frontier bits in LDS.
   const vid_t* hub_vertex = nullptr;
   int64_t nhubs = 0;
+  // Optional non-empty-row view (Graph500 RMAT: about half the vertices have
+  // no edges): nz_pref[w] = number of non-empty rows before bitmap word w,
+  // nz_row_off / nz_head = row_off / head of the non-empty rows only (dense,
+  // so a bottom-up wave touches half the cache lines).  Row k of the view is
+  // [nz_row_off[k], nz_row_off[k + 1]).
+  const eid_t* nz_pref = nullptr;
+  const eid_t* nz_row_off = nullptr;
+  const vid_t* nz_head = nullptr;
 };
 
 // At most kMaxHubs hubs: their frontier bitmap (64 KiB) is staged in LDS by
@@ -298,6 +306,8 @@ struct PackArgs {
 // new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
 struct BuArgs {
   ShardView g;
+  // Zero-degree / padding bits of the owned slice (needed with g.nz_pref).
+  const word_t* zdeg = nullptr;
   // Hub frontier bits (g.nhubs bits, from hub_gather), staged in LDS.
   const word_t* hub_front = nullptr;
   word_t* visited = nullptr;         // owned slice
@@ -498,6 +508,12 @@ class Backend {
   // vertex, UINT32_MAX for non-hubs) a hub head is stored as kHubFlag | index.
   virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head,
                          const uint32_t* hub_idx = nullptr) = 0;
+  // Non-empty-row view: counts[w] = non-empty rows of bitmap word w (words
+  // entries), then (after an exclusive scan into nz_pref) the dense row_off /
+  // head copies.
+  virtual void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts) = 0;
+  virtual void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, eid_t* nz_row_off,
+                       vid_t* nz_head) = 0;
   // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex
   // receives their ids (in some order), hub_idx[v] their index or UINT32_MAX;
   // returns the count (blocking).

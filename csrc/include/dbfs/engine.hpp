@@ -65,7 +65,9 @@ class DeviceGraph {
   bool hub_sorted_ = false;
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
-  DBuf<vid_t> head_, hub_vertex_;
+  DBuf<vid_t> head_, hub_vertex_, nz_head_;
+  DBuf<eid_t> nz_pref_, nz_row_off_;
+  void build_nz_view();
   DBuf<eid_t> row_off_;
   DBuf<vid_t> col_;
 };
@@ -84,6 +86,8 @@ struct EngineOptions {
   // Bottom-up waves number their unvisited vertices and take 64 per step
   // (else one bitmap word per step).
   bool bu_compact = true;
+  // ... reading row bounds and heads from the dense non-empty-row view.
+  bool bu_nz_view = true;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -755,6 +755,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   const vid_t* __restrict__ col = a.g.col;
   const word_t* __restrict__ fr = a.frontier;
   const vid_t* __restrict__ head = a.g.head;
+  const eid_t* __restrict__ nz_ro = (head && a.g.nz_pref && a.zdeg) ? a.g.nz_row_off : nullptr;
   // Unvisited vertex number 64 b + lane -> its position loc = 64 j + bit in the
   // wave's 1024 vertices (-1: no vertex), row bounds and head.
   // (row start, 32-bit length) keep the prefetched state small: the hub
@@ -778,11 +779,22 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     j = min(j, nw - 1);
     const word_t umj = static_cast<word_t>(__shfl(static_cast<long long>(um), j, kWave));
     if (idx < total) {
-      loc = j * 64 + select_bit(umj, idx - ex);
-      const int64_t v = w0 * 64 + loc;
-      rs = ro[v];
-      len = static_cast<uint32_t>(ro[v + 1] - rs);
-      if (head) u = head[v];
+      const int bit = select_bit(umj, idx - ex);
+      loc = j * 64 + bit;
+      if (nz_ro) {
+        // dense non-empty-row view: rank = non-empty rows before the word +
+        // those below this bit (the word's prefix and zero-degree mask are
+        // L1-resident: every lane of the wave reads one of <= 16 words)
+        const int64_t k = a.g.nz_pref[w0 + j] + __popcll(~a.zdeg[w0 + j] & ((1ull << bit) - 1ull));
+        rs = nz_ro[k];
+        len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
+        u = a.g.nz_head[k];
+      } else {
+        const int64_t v = w0 * 64 + loc;
+        rs = ro[v];
+        len = static_cast<uint32_t>(ro[v + 1] - rs);
+        if (head) u = head[v];
+      }
     }
   };
   const int nb = (total + kWave - 1) / kWave;

@@ -136,6 +136,33 @@ __global__ __launch_bounds__(kBlock) void row_heads_kernel(const eid_t* __restri
   head[r] = h;
 }
 
+// Non-empty rows per bitmap word: one wave per word.
+__global__ __launch_bounds__(kBlock) void nz_count_kernel(const eid_t* __restrict__ ro, int64_t rows, int64_t words,
+                                                         eid_t* __restrict__ counts) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  if (w >= words) return;
+  const int64_t v = w * kWave + lane_id();
+  const bool nz = v < rows && ro[v + 1] > ro[v];
+  const unsigned long long m = __ballot(nz);
+  if (lane_id() == 0) counts[w] = __popcll(m);
+}
+
+__global__ __launch_bounds__(kBlock) void nz_fill_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ head,
+                                                        int64_t rows, int64_t words, const eid_t* __restrict__ pref,
+                                                        eid_t* __restrict__ nz_ro, vid_t* __restrict__ nz_head) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  if (w >= words) return;
+  const int64_t v = w * kWave + lane_id();
+  const bool nz = v < rows && ro[v + 1] > ro[v];
+  const unsigned long long m = __ballot(nz);
+  if (nz) {
+    const int64_t k = pref[w] + mask_rank(m);
+    nz_ro[k] = ro[v];
+    nz_head[k] = head[v];
+  }
+  if (w == words - 1 && lane_id() == 0) nz_ro[pref[words]] = ro[rows];
+}
+
 // Hubs = vertices of degree >= min_deg, indexed in wave-ballot order (one
 // atomic per wave).
 __global__ __launch_bounds__(kBlock) void select_hubs_kernel(const uint32_t* __restrict__ deg, int64_t n,
@@ -164,6 +191,18 @@ void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head
   if (rows <= 0) return;
   row_heads_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, col, rows, head,
                                                                                           hub_idx);
+}
+
+void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts, hipStream_t st) {
+  if (words <= 0) return;
+  nz_count_kernel<<<static_cast<unsigned>((words + 3) / 4), kBlock, 0, st>>>(row_off, rows, words, counts);
+}
+
+void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t words, const eid_t* nz_pref,
+             eid_t* nz_row_off, vid_t* nz_head, hipStream_t st) {
+  if (words <= 0) return;
+  nz_fill_kernel<<<static_cast<unsigned>((words + 3) / 4), kBlock, 0, st>>>(row_off, head, rows, words, nz_pref,
+                                                                          nz_row_off, nz_head);
 }
 
 void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex, uint32_t* hub_idx,
