@@ -406,6 +406,9 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
+    for (int64_t e = 0; e < nnz; ++e) out[e] = hub_idx[col[e]] != 0xFFFFFFFFu ? (kHubFlag | hub_idx[col[e]]) : col[e];
+  }
   void nz_word_counts(const eid_t* ro, int64_t rows, int64_t words, eid_t* counts) override {
     for (int64_t w = 0; w < words; ++w) {
       eid_t c = 0;

@@ -203,6 +203,11 @@ class HipBackend final : public Backend {
     kern::row_heads(ro, col, rows, head, hub_idx, st_);
     chk();
   }
+  void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
+    on();
+    kern::encode_hub_cols(col, nnz, hub_idx, out, st_);
+    chk();
+  }
   void nz_word_counts(const eid_t* ro, int64_t rows, int64_t words, eid_t* counts) override {
     on();
     kern::nz_word_counts(ro, rows, words, counts, st_);

@@ -62,6 +62,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "bu_compact") o.bu_compact = v != 0;
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
+  else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -80,7 +81,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
-          {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0}};
+          {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
+          {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -157,6 +159,7 @@ ShardView DeviceGraph::view() const {
   v.head = head_.data();
   v.hub_vertex = hub_vertex_.data();
   v.nhubs = nhubs_;
+  v.hub_col = hub_col_.data();
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -218,6 +221,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
   nhubs_ = 0;
   hub_vertex_.reset();
+  hub_col_.reset();
   // Hub encoding needs a free flag bit in the vertex ids.
   if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
     std::vector<uint32_t> deg(static_cast<size_t>(nall));
@@ -228,6 +232,10 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(max_hubs, 1)));
       nhubs_ = be_->select_hubs(all.data(), nall, min_deg, hub_vertex_.data(), hub_idx.data());
       DBFS_CHECK(nhubs_ >= 0 && nhubs_ <= max_hubs, "hub selection exceeded its capacity");
+      // bottom-up's hub-encoded adjacency copy (one more nnz x 4 B: RMAT-26
+      // 8.6 GB of the 288 GB HBM3E)
+      hub_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
+      be_->encode_hub_cols(col_.data(), nnz_, hub_idx.data(), hub_col_.data());
       build_heads(hub_idx.data());
     } else {
       build_heads();
@@ -721,6 +729,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.compact = opt_.bu_compact;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
+      if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       if (gv.nhubs > 0) {
@@ -938,6 +947,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.compact = opt_.bu_compact;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
+      if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();

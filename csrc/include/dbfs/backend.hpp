@@ -44,6 +44,9 @@ struct ShardView {
   // vertex id.  Bottom-up keeps the hubs' frontier bits in LDS.
   const vid_t* hub_vertex = nullptr;
   int64_t nhubs = 0;
+  // Hub-encoded copy of col (same layout; hub neighbours as kHubFlag | index),
+  // read by bottom-up so that probes of hub neighbours hit LDS too.
+  const vid_t* hub_col = nullptr;
   // Optional non-empty-row view (Graph500 RMAT: about half the vertices have
   // no edges): nz_pref[w] = number of non-empty rows before bitmap word w,
   // nz_row_off / nz_head = row_off / head of the non-empty rows only (dense,
@@ -514,6 +517,8 @@ class Backend {
   virtual void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts) = 0;
   virtual void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, eid_t* nz_row_off,
                        vid_t* nz_head) = 0;
+  // out[e] = kHubFlag | hub_idx[col[e]] for hub neighbours, else col[e].
+  virtual void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) = 0;
   // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex
   // receives their ids (in some order), hub_idx[v] their index or UINT32_MAX;
   // returns the count (blocking).

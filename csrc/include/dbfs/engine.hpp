@@ -65,7 +65,7 @@ class DeviceGraph {
   bool hub_sorted_ = false;
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
-  DBuf<vid_t> head_, hub_vertex_, nz_head_;
+  DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_;
   DBuf<eid_t> nz_pref_, nz_row_off_;
   void build_nz_view();
   DBuf<eid_t> row_off_;
@@ -88,6 +88,8 @@ struct EngineOptions {
   bool bu_compact = true;
   // ... reading row bounds and heads from the dense non-empty-row view.
   bool bu_nz_view = true;
+  // ... and scanning rows in the hub-encoded adjacency copy (LDS hub probes).
+  bool bu_hub_col = true;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -547,10 +547,24 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 #endif
 constexpr int kBuBatch = DBFS_BU_BATCH;  // phase-1 column loads in flight per lane
 
-template <bool kPacked>
-__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own) {
+// Frontier test of a neighbour id that may be hub-encoded (kHub): hubs in the
+// LDS copy of their frontier bits, the rest in the global bitmap.
+template <bool kHub>
+__device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const word_t* s_hub, vid_t u) {
+  if constexpr (kHub) {
+    const vid_t hb = u & ~kHubFlag;
+    return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u);
+  } else {
+    return test_bit(fr, u);
+  }
+}
+
+template <bool kPacked, bool kHub>
+__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own,
+                                            const word_t* s_hub) {
   const int lane = lane_id();
-  const vid_t* __restrict__ col = a.g.col;
+  // hub-encoded copy of the adjacency when present (kHub kernels only)
+  const vid_t* __restrict__ col = (kHub && a.g.hub_col) ? a.g.hub_col : a.g.col;
   const word_t* __restrict__ fr = a.frontier;
   // positions relative to the row start: 32-bit (a row never holds 2^32 entries)
   const vid_t* __restrict__ row = col + rs;
@@ -566,7 +580,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       u[k] = ok[k] ? row[p + k] : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && test_bit(fr, u[k]);
+    for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && bu_probe<kHub>(fr, s_hub, u[k]);
     p += kBuBatch;
   }
   if (p > lim) p = lim;
@@ -592,7 +606,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       const long long o_excl = __shfl(excl, o, kWave);
       const long long o_p = __shfl(static_cast<long long>(rs + p), o, kWave);
       bool hit = false;
-      if (lane < total) hit = test_bit(fr, col[o_p + (lane - o_excl)]);
+      if (lane < total) hit = bu_probe<kHub>(fr, s_hub, col[o_p + (lane - o_excl)]);
       // owners with a hit: set bit o of a wave mask
       unsigned long long hitmask = hit ? (1ull << o) : 0ull;
 #pragma unroll
@@ -614,7 +628,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       for (uint32_t base = ps; base < pe; base += kWave) {
         const uint32_t idx = base + lane;
         bool hit = false;
-        if (idx < pe) hit = test_bit(fr, r[idx]);
+        if (idx < pe) hit = bu_probe<kHub>(fr, s_hub, r[idx]);
         if (__ballot(hit)) {
           f = true;
           break;
@@ -685,18 +699,13 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
     // First probe: the row's first (highest-degree, hub-first order) neighbour.
     bool found = false;
     if (rs < e) {
-      if constexpr (kHub) {
-        const vid_t hb = u0 & ~kHubFlag;
-        found = (u0 & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u0);
-      } else {
-        found = test_bit(fr, u0);
-      }
+      found = bu_probe<kHub>(fr, s_hub, u0);
     }
     if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
     word_t res = 0;
     if (vis != ~0ull) {
       const int64_t v = w * 64 + lane;
-      found = bu_scan_row<kPacked>(a, rs, e, found, own);
+      found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
       res = __ballot(found);
       if (found) {
         a.level[v] = a.new_level;
@@ -812,15 +821,10 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
     bool found = false;
     if (rs < e) {
-      if constexpr (kHub) {
-        const vid_t hb = u0 & ~kHubFlag;
-        found = (u0 & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u0);
-      } else {
-        found = test_bit(fr, u0);
-      }
+      found = bu_probe<kHub>(fr, s_hub, u0);
     }
     if (!head) n_u = n_len ? col[n_rs] : 0u;
-    found = bu_scan_row<kPacked>(a, rs, e, found, own);
+    found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
     if (found) {
       a.level[w0 * 64 + loc] = a.new_level;
       cnt32 += 1;

@@ -15,6 +15,8 @@
 // their rows are never probed bottom-up.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "launch.hpp"
 #include "wave.hpp"
 
@@ -136,6 +138,17 @@ __global__ __launch_bounds__(kBlock) void row_heads_kernel(const eid_t* __restri
   head[r] = h;
 }
 
+__global__ __launch_bounds__(kBlock) void encode_hub_cols_kernel(const vid_t* __restrict__ col, int64_t nnz,
+                                                                const uint32_t* __restrict__ hub_idx,
+                                                                vid_t* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; e < nnz; e += stride) {
+    const vid_t v = col[e];
+    const uint32_t k = hub_idx[v];
+    out[e] = k != 0xFFFFFFFFu ? (kHubFlag | k) : v;
+  }
+}
+
 // Non-empty rows per bitmap word: one wave per word.
 __global__ __launch_bounds__(kBlock) void nz_count_kernel(const eid_t* __restrict__ ro, int64_t rows, int64_t words,
                                                          eid_t* __restrict__ counts) {
@@ -191,6 +204,12 @@ void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head
   if (rows <= 0) return;
   row_heads_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, col, rows, head,
                                                                                           hub_idx);
+}
+
+void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out, hipStream_t st) {
+  if (nnz <= 0) return;
+  encode_hub_cols_kernel<<<static_cast<unsigned>(std::min<int64_t>((nnz + kBlock - 1) / kBlock, 1 << 16)), kBlock, 0,
+                           st>>>(col, nnz, hub_idx, out);
 }
 
 void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts, hipStream_t st) {
