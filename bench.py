@@ -45,6 +45,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--graph", default=None, metavar="PATH",
+                    help="real graph instead of RMAT: edge list / .mtx / binary .csr cache (e.g. soc-LiveJournal1; "
+                         "no dataset ships with the repo and the GPU pool has no network)")
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple", "scan"])
@@ -78,7 +81,15 @@ def main() -> int:
     rank, nranks = rt.rank, rt.world
     log(f"backend {rt.backend.name}, comm {rt.comm.name}, ranks {nranks}")
 
-    params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
+    if args.graph:
+        params = dbfs.read_graph(args.graph)  # every rank reads the file, shards its rows
+        graph_name = os.path.basename(args.graph)
+        n_vertices, n_input_edges = params.n, params.input_edges
+    else:
+        params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
+        graph_name = (f"RMAT-{args.scale} (Graph500 Kronecker a=.57 b=.19 c=.19, "
+                      f"edge factor {args.edge_factor})")
+        n_vertices, n_input_edges = params.n, params.m
     t0 = time.time()
     bfs = dbfs.BFS(params, rt, mode=args.mode, alpha=args.alpha, beta=args.beta,
                    bu_lane_limit=args.bu_lane_limit, hubs=not args.no_hubs, max_hubs=args.max_hubs)
@@ -88,7 +99,7 @@ def main() -> int:
     rt.backend.synchronize()
     rt.barrier()
     gen_s = time.time() - t0
-    log(f"generated RMAT-{args.scale} shard: rows {bfs.graph.rows} nnz {bfs.graph.nnz} in {gen_s:.2f}s")
+    log(f"built {graph_name} shard: rows {bfs.graph.rows} nnz {bfs.graph.nnz} in {gen_s:.2f}s")
 
     roots = bfs.sample_roots(args.warmup + args.steps, seed=args.root_seed)
     if len(roots) < args.warmup + args.steps:
@@ -145,7 +156,7 @@ def main() -> int:
     bfs.engine.phase_timing = False
     level_profile = [[lv["dir"], round(lv["ms"], 4), round(lv.get("comm_ms", 0.0), 4)] for lv in prof.levels]
     baseline = args.baseline_gteps
-    if baseline is None and args.edge_factor == 16 and args.mode != "ref":
+    if baseline is None and not args.graph and args.edge_factor == 16 and args.mode != "ref":
         baseline = MEASURED_REF_GTEPS.get((args.scale, nranks))
     if rank == 0:
         out = {
@@ -161,15 +172,16 @@ def main() -> int:
             "vs_baseline": (round(value / baseline, 2) if baseline else None),
             "baseline": ("reference algorithm (--mode ref) on MI355X, BASELINE.md" if baseline else None),
             "dtype": "int32",
-            "data": "synthetic (Graph500 RMAT generated on device, random roots)",
+            "data": (f"file {graph_name}, random roots" if args.graph
+                     else "synthetic (Graph500 RMAT generated on device, random roots)"),
             "config": {
-                "model": f"RMAT-{args.scale} (Graph500 Kronecker a=.57 b=.19 c=.19, edge factor {args.edge_factor})",
+                "model": graph_name,
                 "global_batch": 1,
                 "seq_len": None,
                 "parallelism": f"1d-vertex-partition x{nranks}",
                 "mode": args.mode,
-                "vertices": params.n,
-                "input_edges": params.m,
+                "vertices": n_vertices,
+                "input_edges": n_input_edges,
                 "directed_edges": bfs.engine.global_directed_edges,
             },
             "bfs_ms_mean": round(bfs_ms / len(results), 4),

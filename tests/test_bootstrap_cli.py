@@ -6,6 +6,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -115,6 +116,23 @@ def test_bench_contract_cpu():
     assert rec["value"] > 0 and rec["validated"] is True
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in rec["config"]
+
+
+def test_bench_graph_file_cpu(tmp_path):
+    # bench on a real graph file (the soc-LiveJournal1 / Friendster path;
+    # here a small random edge list in the reference's `n m` + `u v` format)
+    rng = np.random.default_rng(5)
+    n, m = 2000, 12000
+    path = tmp_path / "g.txt"
+    e = rng.integers(0, n, size=(m, 2))
+    path.write_text(f"{n} {m}\n" + "".join(f"{u} {v}\n" for u, v in e))
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--graph", str(path),
+                          "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert rec["config"]["model"] == "g.txt" and rec["config"]["vertices"] == n
+    assert rec["config"]["input_edges"] == m and rec["validated"] is True
+    assert rec["data"].startswith("file g.txt") and rec["vs_baseline"] is None
 
 
 @pytest.mark.parametrize("nproc,mode", [(2, "do"), (3, "ref")])
