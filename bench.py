@@ -188,6 +188,7 @@ def main() -> int:
             "harmonic_mean_gteps": round(harmonic_mean([r.gteps for r in results]), 4),
             "traversed_edges_mean": edges // len(results),
             "depth_mean": sum(r.depth for r in results) / len(results),
+            "mispredicted_levels": sum(r.mispredicts for r in results),
             "validated": validated,
             "generate_s": round(gen_s, 3),
             "level_profile": {"root": med.source, "levels": level_profile,

@@ -118,6 +118,8 @@ class CpuBackend final : public Backend {
         a.mailbox->done = c.done;
         a.mailbox->vis_deg = c.vis_deg;
         a.mailbox->next_dir = c.dir;
+        a.mailbox->n_f = c.n_f;
+        a.mailbox->m_f = c.m_f;
         a.mailbox->level = -1;
       }
     }
@@ -161,6 +163,8 @@ class CpuBackend final : public Backend {
         a.mailbox->done = a.ctrl->done;
         a.mailbox->vis_deg = a.ctrl->vis_deg;
         a.mailbox->next_dir = a.ctrl->dir;
+        a.mailbox->n_f = a.ctrl->n_f;
+        a.mailbox->m_f = a.ctrl->m_f;
         a.mailbox->level = a.level;
       }
     }

@@ -58,6 +58,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "force_exchange") o.force_exchange = v != 0;
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
+  else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "bu_compact") o.bu_compact = v != 0;
@@ -78,6 +79,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"force_exchange", o.force_exchange ? 1.0 : 0.0},
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
+          {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
@@ -966,24 +968,57 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
   };
 
-  // Host loop, one level ahead of the device.  The direction of level L + 1 is
-  // predicted to be level L's (directions change about twice per traversal);
-  // the stamp of level L - 1 carries the real direction of level L, and a
-  // mispredicted level (a no-op chain, its scan skipped too) is enqueued again.
+  // Host loop, one level ahead of the device.  The stamp of level L - 1
+  // carries the real direction of level L and its frontier; a mispredicted
+  // level (a no-op chain, its scan skipped too) is enqueued again.
+  //   device_loop_predict: after that stamp, level L + 1 is enqueued with the
+  //     direction the device will choose if the frontier keeps its growth rate
+  //     (n_f and m_f extrapolated geometrically, run through the same
+  //     level_ctrl_finish): the Beamer switches of RMAT traversals are
+  //     predicted exactly, so no chain is wasted.
+  //   otherwise: level L + 1 is enqueued before the stamp, predicted to keep
+  //     level L's direction (two wasted chains per direction change).
   int nlev = 0;
+  LevelCtrl hc = init;  // host mirror for the prediction
+  int64_t prev_nf = 0, prev_mf = 0;
   enqueue_level(0, static_cast<char>(init.dir));
   for (int L = 0;; ++L) {
-    enqueue_level(L + 1, enq_dir[L]);
+    if (!opt_.device_loop_predict) enqueue_level(L + 1, enq_dir[L]);
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
     if (mb->done) {
       nlev = L;
       break;
     }
     const char actual = static_cast<char>(mb->next_dir);
-    if (actual != enq_dir[L]) {
-      enqueue_level(L, actual);
-      enqueue_level(L + 1, actual);
+    if (actual != enq_dir[L]) ++res.mispredicts;
+    if (!opt_.device_loop_predict) {
+      if (actual != enq_dir[L]) {
+        enqueue_level(L, actual);
+        enqueue_level(L + 1, actual);
+      }
+      continue;
     }
+    if (actual != enq_dir[L]) enqueue_level(L, actual);
+    const int64_t nf = mb->n_f, mf = mb->m_f;
+    // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
+    auto grow = [](int64_t cur, int64_t prev) {
+      if (prev <= 0) return static_cast<double>(cur) * static_cast<double>(cur);
+      return static_cast<double>(cur) * (static_cast<double>(cur) / static_cast<double>(prev));
+    };
+    hc.dir = actual;
+    hc.n_f = nf;
+    hc.m_f = mf;
+    hc.vis_deg = mb->vis_deg;
+    hc.done = 0;
+    LevelRecDev scratch;
+    const double cap = static_cast<double>(part_.n);
+    const double enf = std::min(grow(nf, prev_nf), cap);
+    const double emf = std::min(grow(mf, prev_mf), static_cast<double>(total_directed_));
+    level_ctrl_finish(hc, std::max<int64_t>(1, static_cast<int64_t>(enf)), static_cast<int64_t>(emf), false,
+                      &scratch);
+    prev_nf = nf;
+    prev_mf = mf;
+    enqueue_level(L + 1, static_cast<char>(hc.dir));
   }
   be_.synchronize();
   const auto t1 = std::chrono::steady_clock::now();

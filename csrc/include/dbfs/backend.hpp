@@ -113,6 +113,7 @@ struct LevelMailbox {
   int64_t vis_deg = 0;
   int32_t next_dir = 0;         // direction decided for the following level
   int32_t pad = 0;
+  int64_t n_f = 0, m_f = 0;     // the following level's frontier (vertices, edges)
 };
 constexpr int kMailboxSlots = 8;
 

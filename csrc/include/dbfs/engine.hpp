@@ -108,6 +108,9 @@ struct EngineOptions {
   // One rank, td/bu/do modes: device-driven level loop (LevelCtrl): the host
   // enqueues the next level before the current one finishes.
   bool device_loop = true;
+  // ... enqueueing each level with an extrapolated direction prediction (else:
+  // the previous level's direction, one more level ahead).
+  bool device_loop_predict = true;
   // Host loop (several ranks, or device_loop off): read each level's totals
   // through a device-mapped mailbox the host spins on, instead of a D2H copy
   // plus a stream synchronisation.
@@ -141,6 +144,7 @@ struct RunResult {
   int64_t edges = 0;           // traversed undirected edges (Graph500)
   int depth = 0;               // number of levels (max level + 1)
   double gteps = 0.0;
+  int mispredicts = 0;         // device loop: level chains enqueued for the wrong direction
   std::vector<LevelRecord> levels;
 };
 

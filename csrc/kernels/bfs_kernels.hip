@@ -113,6 +113,10 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
                          static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->n_f), static_cast<unsigned long long>(c.n_f),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->m_f), static_cast<unsigned long long>(c.m_f),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&a.mailbox->level, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
@@ -351,6 +355,10 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
                            static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->n_f),
+                           static_cast<unsigned long long>(c.n_f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->m_f),
+                           static_cast<unsigned long long>(c.m_f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&a.mailbox->level, a.level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }

@@ -36,6 +36,7 @@ py::dict result_dict(const RunResult& r) {
   d["edges"] = r.edges;
   d["depth"] = r.depth;
   d["gteps"] = r.gteps;
+  d["mispredicts"] = r.mispredicts;
   py::list lv;
   for (const auto& l : r.levels) {
     py::dict x;

@@ -27,11 +27,13 @@ class BFSResult:
     depth: int
     gteps: float
     levels: List[Dict[str, Any]] = field(default_factory=list)
+    mispredicts: int = 0  # device loop: level chains enqueued for the wrong direction
 
     @classmethod
     def from_native(cls, d: Dict[str, Any]) -> "BFSResult":
         return cls(source=d["source"], ms=d["ms"], reached=d["reached"], edges=d["edges"],
-                   depth=d["depth"], gteps=d["gteps"], levels=list(d["levels"]))
+                   depth=d["depth"], gteps=d["gteps"], levels=list(d["levels"]),
+                   mispredicts=int(d.get("mispredicts", 0)))
 
 
 class BFS:

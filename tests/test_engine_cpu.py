@@ -239,13 +239,16 @@ def test_hub_sort_orders_rows_and_keeps_levels(rt):
     assert np.array_equal(bfs.levels(), exp)
 
 
+@pytest.mark.parametrize("predict", [1, 0])
 @pytest.mark.parametrize("mode", ["td", "bu", "do"])
-def test_device_loop_matches_host_loop(rt, mode):
+def test_device_loop_matches_host_loop(rt, mode, predict):
     # the device-driven level loop (LevelCtrl decisions on the device) must
     # take exactly the host loop's decisions: same levels, same per-level records
+    # (with either direction predictor: mispredictions only cost no-op chains)
     p = dbfs.rmat_params(12, 16, 41)
     csr = dbfs.host_csr_from_params(p)
     dev = dbfs.BFS(p, rt, mode=mode)
+    dev.engine.set_option("device_loop_predict", predict)
     host = dbfs.BFS(p, rt, mode=mode)
     host.engine.set_option("device_loop", 0)
     assert dict(dev.engine.get_options())["device_loop"] == 1.0
