@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 
 #include "launch.hpp"
 #include "wave.hpp"
@@ -555,6 +556,21 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 #endif
 constexpr int kBuBatch = DBFS_BU_BATCH;  // phase-1 column loads in flight per lane
 
+#ifdef DBFS_BU_STATS
+// Diagnostic build only (-DDBFS_BU_STATS, tools/gpu_bu_stats.sh): wave-level
+// event counters of the bottom-up kernel, printed per dispatch by bu_step.
+__device__ unsigned long long g_bu_stats[8];
+#define BU_STAT(i, x)                                                   \
+  do {                                                                  \
+    const unsigned long long v_ = (x);                                  \
+    if (lane_id() == 0 && v_) atomicAdd(&g_bu_stats[i], v_);            \
+  } while (0)
+#else
+#define BU_STAT(i, x) \
+  do {                \
+  } while (0)
+#endif
+
 // Frontier test of a neighbour id that may be hub-encoded (kHub): hubs in the
 // LDS copy of their frontier bits, the rest in the global bitmap.
 template <bool kHub>
@@ -579,7 +595,9 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
   const uint32_t len = static_cast<uint32_t>(e - rs);
   uint32_t p = min(len, 1u);
   const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
+  BU_STAT(3, __popcll(__ballot(p < lim && !found)));
   while (p < lim && !found) {
+    BU_STAT(4, 1);
     vid_t u[kBuBatch];
     bool ok[kBuBatch];
 #pragma unroll
@@ -627,6 +645,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
     // Phase 2: the wave scans each still-unresolved row in turn, 64
     // neighbours per step.
     unsigned long long pending = __ballot(!found && p < len);
+    BU_STAT(5, __popcll(pending));
     while (pending) {
       const int l = __ffsll(static_cast<long long>(pending)) - 1;
       pending &= pending - 1;
@@ -634,6 +653,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
       bool f = false;
       for (uint32_t base = ps; base < pe; base += kWave) {
+        BU_STAT(6, 1);
         const uint32_t idx = base + lane;
         bool hit = false;
         if (idx < pe) hit = bu_probe<kHub>(fr, s_hub, r[idx]);
@@ -831,8 +851,12 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     if (rs < e) {
       found = bu_probe<kHub>(fr, s_hub, u0);
     }
+    BU_STAT(0, 1);
+    BU_STAT(1, __popcll(__ballot(loc >= 0)));
+    BU_STAT(2, __popcll(__ballot(found)));
     if (!head) n_u = n_len ? col[n_rs] : 0u;
     found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
+    BU_STAT(7, __popcll(__ballot(found)));
     if (found) {
       a.level[w0 * 64 + loc] = a.new_level;
       cnt32 += 1;
@@ -1066,7 +1090,28 @@ int device_cus() {
   return cus[dev];
 }
 
+#ifdef DBFS_BU_STATS
+static void bu_stats_report(hipStream_t st) {
+  unsigned long long h[8] = {0};
+  (void)hipStreamSynchronize(st);
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bu_stats), sizeof(h));
+  const unsigned long long z[8] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bu_stats), z, sizeof(z));
+  if (h[0])
+    std::fprintf(stderr,
+                 "[bu-stats] batches %llu active-lanes %llu head-found %llu p1-lanes %llu p1-iters %llu "
+                 "p2-rows %llu p2-steps %llu found %llu\n",
+                 h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+}
+#endif
+
 void bu_step(const BuArgs& a, hipStream_t st) {
+#ifdef DBFS_BU_STATS
+  struct Report {
+    hipStream_t st;
+    ~Report() { bu_stats_report(st); }
+  } report{st};
+#endif
   if (a.words <= 0) return;
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
