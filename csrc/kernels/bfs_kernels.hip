@@ -231,15 +231,18 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     a.frontier[wl] = nb;
     if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
+  // New vertices of the unit, 64 per step (one per lane, whatever word they
+  // sit in): a sparse level has about one new vertex per word, and one word
+  // per step would cost a dependent row_off round trip per new vertex.
   long long cnt = 0, deg = 0;
-  unsigned long long nz = __ballot(nb != 0);
+  const int incl = static_cast<int>(wave_incl_scan(__popcll(nb)));
+  const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   const eid_t* __restrict__ ro = a.g.row_off;
-  while (nz) {
-    const int j = __ffsll(static_cast<long long>(nz)) - 1;
-    nz &= nz - 1;
-    const word_t word = readlane64(nb, j);
-    if ((word >> lane) & 1ull) {
-      const int64_t v = (w0 + j) * 64 + lane;
+  for (int base = 0; base < total; base += kWave) {
+    const int idx = base + lane;
+    const int pos = wave_set_position(nb, incl, idx);
+    if (idx < total) {
+      const int64_t v = w0 * 64 + pos;
       a.level[v] = a.new_level;
       const eid_t d = ro[v + 1] - ro[v];
       if (d > 0) {
@@ -379,17 +382,20 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
   const word_t mine = (w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
-  const unsigned long long nzw = __ballot(mine != 0);
-  if (!nzw) return;
+  if (!__ballot(mine != 0)) return;
   const eid_t* __restrict__ ro = a.g.row_off;
   long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
   long long off = a.unit_deg_off[unit] + a.part_deg[unit / kScanChunk];
-  for (unsigned long long nz = nzw; nz; nz &= nz - 1) {
-    const int j = __ffsll(static_cast<long long>(nz)) - 1;
-    const word_t word = readlane64(mine, j);
-    const int64_t v = (w0 + j) * 64 + lane;
+  // Frontier vertices of the unit in (word, bit) order, 64 per step (one per
+  // lane, whatever word they sit in), so the work-list order is unchanged.
+  const int fincl = static_cast<int>(wave_incl_scan(__popcll(mine)));
+  const int ftotal = __builtin_amdgcn_readlane(fincl, kWave - 1);
+  for (int base = 0; base < ftotal; base += kWave) {
+    const int idx = base + lane;
+    const int vpos = wave_set_position(mine, fincl, idx);
     eid_t rs = 0, d = 0;
-    if ((word >> lane) & 1ull) {
+    if (idx < ftotal) {
+      const int64_t v = w0 * 64 + vpos;
       rs = ro[v];
       d = ro[v + 1] - rs;
     }
@@ -746,20 +752,6 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
   }
 }
 
-// Position of the r-th (0-based) set bit of x (r < popcount(x)).
-__device__ __forceinline__ int select_bit(word_t x, int r) {
-  int pos = 0;
-#pragma unroll
-  for (int width = 32; width >= 1; width >>= 1) {
-    const int c = __popcll(x & ((1ull << width) - 1ull));
-    if (r >= c) {
-      r -= c;
-      x >>= width;
-      pos += width;
-    }
-  }
-  return pos;
-}
 
 // Compacted variant of bu_wave: the unvisited vertices of the wave's 16 words
 // are numbered (per-word popcount prefix) and processed 64 at a time, one per

@@ -59,5 +59,36 @@ __device__ __forceinline__ bool test_bit(const word_t* bm, unsigned v) {
   return (bm[v >> 6] >> (v & 63)) & 1ull;
 }
 
+// Position of the r-th (0-based) set bit of x (r < popcount(x)).
+__device__ __forceinline__ int select_bit(unsigned long long x, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int width = 32; width >= 1; width >>= 1) {
+    const int c = __popcll(x & ((1ull << width) - 1ull));
+    if (r >= c) {
+      r -= c;
+      x >>= width;
+      pos += width;
+    }
+  }
+  return pos;
+}
+
+// Compaction of a wave's bit set: lane l holds word l's bits `m` (64 words,
+// 4096 positions) and `incl` = inclusive prefix of popcounts over the lanes.
+// Element idx (< total) of the set -> position 64 j + bit.  Binary search over
+// the lanes' prefixes (6 shuffles) + select in the word.
+__device__ __forceinline__ int wave_set_position(unsigned long long m, int incl, int idx) {
+  int j = 0;
+#pragma unroll
+  for (int step = 32; step >= 1; step >>= 1)
+    if (__shfl(incl, j + step - 1, kWave) <= idx) j += step;
+  // (every lane shuffles: a source lane must be active for its value to be read)
+  const int prev = __shfl(incl, j > 0 ? j - 1 : 0, kWave);
+  const int ex = j > 0 ? prev : 0;
+  const unsigned long long mj = static_cast<unsigned long long>(__shfl(static_cast<long long>(m), j, kWave));
+  return j * 64 + select_bit(mj, idx - ex);
+}
+
 }  // namespace dev
 }  // namespace dbfs
