@@ -763,17 +763,19 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
 // (~half the lanes unvisited) half the steps, at the later levels (a few per
 // word) a fraction.  Found bits are OR-ed into a per-wave LDS copy of the 16
 // result words (s_res), written out once.
-template <bool kPacked, bool kHub>
+// kWords: the wave's share, 16 words (a quarter unit) or 64 (a whole unit).
+template <bool kPacked, bool kHub, int kWords = kWaveWords>
 __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int* own, word_t* s_res,
                                                 const word_t* s_hub, long long& cnt, long long& deg) {
+  static_assert(kWords <= kWave, "one word per lane");
   const int lane = lane_id();
   const int64_t left = a.words - w0;
-  const int nw = left <= 0 ? 0 : (left < kWaveWords ? static_cast<int>(left) : kWaveWords);
+  const int nw = left <= 0 ? 0 : (left < kWords ? static_cast<int>(left) : kWords);
   // unvisited bits of word `lane` (0 past the words); visited = ~um
   const word_t um = lane < nw ? ~a.visited[w0 + lane] : 0ull;
   const int incl = static_cast<int>(wave_incl_scan(__popcll(um)));
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
-  if (lane < kWaveWords) s_res[lane] = 0ull;
+  if (lane < kWords) s_res[lane] = 0ull;
   if (total == 0) {
     if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
     return;
@@ -796,19 +798,27 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     u = 0;
     const int idx = b * kWave + lane;
     if (b * kWave >= total) return;  // uniform
-    // word j = number of words ending at or before idx; ex = where j starts
-    int j = 0, ex = 0;
-    for (int i = 0; i < nw; ++i) {
-      const int end_i = __builtin_amdgcn_readlane(incl, i);
-      if (end_i <= idx) {
-        ++j;
-        ex = end_i;
+    int j, bit;
+    if constexpr (kWords == kWave) {
+      const int p = wave_set_position(um, incl, idx);
+      j = p >> 6;
+      bit = p & 63;
+    } else {
+      // word j = number of words ending at or before idx; ex = where j starts
+      int ex = 0;
+      j = 0;
+      for (int i = 0; i < nw; ++i) {
+        const int end_i = __builtin_amdgcn_readlane(incl, i);
+        if (end_i <= idx) {
+          ++j;
+          ex = end_i;
+        }
       }
+      j = min(j, nw - 1);
+      const word_t umj = static_cast<word_t>(__shfl(static_cast<long long>(um), j, kWave));
+      bit = select_bit(umj, idx - ex);
     }
-    j = min(j, nw - 1);
-    const word_t umj = static_cast<word_t>(__shfl(static_cast<long long>(um), j, kWave));
     if (idx < total) {
-      const int bit = select_bit(umj, idx - ex);
       loc = j * 64 + bit;
       if (nz_ro) {
         // dense non-empty-row view: rank = non-empty rows before the word +
@@ -900,17 +910,31 @@ template <bool kPacked, bool kCompact>
 __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
-  __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kWaveWords : 1];
+  __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   for (int64_t i = threadIdx.x; i < hw; i += kHubBuThreads) s_hub[i] = a.hub_front[i];
   __syncthreads();
-  constexpr int kGroups = kHubBuThreads / kUnitThreads;
   const int wave = threadIdx.x >> 6;
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if constexpr (kCompact && !kPacked) {
+    // compacted: one whole 64-word unit per wave (its statistics need no
+    // cross-wave reduction, so waves run independently: no barrier)
+    constexpr int kWavesPerBlock = kHubBuThreads / kWave;
+    int* own = s_bu_owner;
+    for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+         u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
+      long long cnt = 0, deg = 0;
+      bu_wave_compact<kPacked, true, kUnitWords>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub, cnt,
+                                                 deg);
+      wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg);
+    }
+    return;
+  }
+  constexpr int kGroups = kHubBuThreads / kUnitThreads;
   const int group = wave / kUnitWaves;
   const int wg = wave % kUnitWaves;
-  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
     const int64_t u = base + group;
