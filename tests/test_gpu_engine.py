@@ -4,11 +4,15 @@ Every test compares the GPU levels against the sequential CPU oracle (the
 reference's bfsCPU, bfs.cu:923-945) element-wise -- the reference's own
 checkOutput contract (bfs.cu:374-384).
 """
+import os
+
 import numpy as np
 import pytest
 
 import distributed_cuda_bfs_amd as dbfs
 from distributed_cuda_bfs_amd.parallel.runtime import run_virtual_ranks
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -336,3 +340,27 @@ def test_hub_lds_virtual_ranks_gpu():
     for rank_out in run_virtual_ranks(3, body, device="hip"):
         for lv, e in zip(rank_out, exp):
             assert np.array_equal(lv, e)
+
+
+def test_multiprocess_ranks_share_one_gpu_tcp():
+    """The one-process-per-rank launch (torch.distributed.run, as the driver
+    runs bench.py on 8 GPUs) with 2 ranks on this one GPU: every rank runs the
+    real HIP kernels on its shard; collectives go through the TCP communicator
+    (RCCL refuses two ranks on one device).  The traversal must validate."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="tcp")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "18",
+           "--steps", "2", "--warmup", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["validated"] is True
