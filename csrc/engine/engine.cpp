@@ -62,6 +62,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "bu_compact") o.bu_compact = v != 0;
+  else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
   else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
   else throw Error("unknown engine option '" + name + "'");
@@ -83,6 +84,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
+          {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0}};
 }
@@ -729,6 +731,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
       ba.compact = opt_.bu_compact;
+      ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
@@ -947,6 +950,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.lane_limit = opt_.bu_lane_limit;
       ba.packed = opt_.bu_packed;
       ba.compact = opt_.bu_compact;
+      ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;

@@ -86,6 +86,9 @@ struct EngineOptions {
   // Bottom-up waves number their unvisited vertices and take 64 per step
   // (else one bitmap word per step).
   bool bu_compact = true;
+  // ... a whole 64-word unit per wave (1), 16 words (-1), or by shard size (0:
+  // whole units when they fill every resident wave slot).
+  int bu_whole_units = 0;
   // ... reading row bounds and heads from the dense non-empty-row view.
   bool bu_nz_view = true;
   // ... and scanning rows in the hub-encoded adjacency copy (LDS hub probes).

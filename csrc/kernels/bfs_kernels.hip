@@ -906,7 +906,7 @@ constexpr int kHubBuThreads = DBFS_HUB_BU_THREADS;
 static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
-template <bool kPacked, bool kCompact>
+template <bool kPacked, bool kCompact, bool kWhole = false>
 __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
@@ -918,9 +918,11 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-  if constexpr (kCompact && !kPacked) {
+  if constexpr (kWhole) {
     // compacted: one whole 64-word unit per wave (its statistics need no
-    // cross-wave reduction, so waves run independently: no barrier)
+    // cross-wave reduction, so waves run independently: no barrier).  Chosen
+    // when the shard has enough units to fill the chip this way (one GPU);
+    // small shards (many ranks) keep 16 words per wave for parallelism.
     constexpr int kWavesPerBlock = kHubBuThreads / kWave;
     int* own = s_bu_owner;
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
@@ -1131,9 +1133,17 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-    const unsigned grid = grid_for(nunits, kHubBuThreads / kUnitThreads, 2 * device_cus());
+    // compacted: a whole 64-word unit per wave when the shard has enough units
+    // to fill every resident wave slot (one GPU); small shards (many ranks)
+    // keep 16 words per wave for parallelism
+    const int64_t slots = 2 * static_cast<int64_t>(device_cus()) * (kHubBuThreads / kWave);
+    const bool whole = a.compact && !a.packed && (a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots));
+    const unsigned grid = grid_for(nunits, whole ? kHubBuThreads / kWave : kHubBuThreads / kUnitThreads,
+                                   2 * device_cus());
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
-    if (a.packed)
+    if (whole)
+      bu_hub_kernel<false, true, true><<<grid, kHubBuThreads, 0, st>>>(a);
+    else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
     else
       a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);

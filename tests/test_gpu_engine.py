@@ -299,9 +299,10 @@ def test_perf_regression_do_vs_ref_gpu(gpu_runtime):
     assert t_do * 10 < t_ref, (t_do, t_ref)
 
 
+@pytest.mark.parametrize("whole", [1, -1])
 @pytest.mark.parametrize("max_hubs", [None, 64, 3000, 0])
 @pytest.mark.parametrize("packed", [0, 1])
-def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed):
+def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed, whole):
     """Bottom-up with hub-encoded heads probed in the LDS copy of the hub
     frontier bits: every vertex a hub (default cap on a small graph), a few
     hubs (mixed LDS / global head probes), no hubs (plain kernel)."""
@@ -314,6 +315,7 @@ def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed):
         if max_hubs != 0:
             assert bfs.graph.nhubs > 0
         bfs.engine.set_option("bu_packed", packed)
+        bfs.engine.set_option("bu_whole_units", whole)  # 64 / 16 words per wave (compacted hub kernel)
         for src in bfs.sample_roots(3, seed=11):
             _check(bfs, csr, src)
         bfs.engine.set_option("device_loop", 0)

@@ -13,6 +13,6 @@ fi
 echo "== bench x${REPS:-3}"
 : > gpurun_out/quick.txt
 for rep in $(seq ${REPS:-3}); do
-  timeout -k 10 240 python bench.py --steps ${STEPS:-16} --warmup 3 --no-validate ${BENCH_ARGS} > gpurun_out/quick_run.json 2> gpurun_out/quick_run.err || { tail -20 gpurun_out/quick_run.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/quick_run.json').read().strip().splitlines()[-1]); print('%8.1f GTEPS %7.3f ms/step  levels %s' % (d['value'], d['ms_per_step'], [(l[0], l[1]) for l in d['level_profile']['levels']]))" | tee -a gpurun_out/quick.txt
+  timeout -k 10 240 python bench.py --steps ${STEPS:-16} --warmup 3 ${BENCH_ARGS} > gpurun_out/quick_run.json 2> gpurun_out/quick_run.err || { tail -20 gpurun_out/quick_run.err; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/quick_run.json').read().strip().splitlines()[-1]); print('%8.1f GTEPS %7.3f ms/step validated %s levels %s' % (d['value'], d['ms_per_step'], d['validated'], [(l[0], l[1]) for l in d['level_profile']['levels']]))" | tee -a gpurun_out/quick.txt
 done
