@@ -175,7 +175,7 @@ class CpuBackend final : public Backend {
       word_t m = 0;
       for (int b = 0; b < 64; ++b) {
         const int64_t v = w * 64 + b;
-        if (v >= a.g.rows || a.g.row_off[v + 1] == a.g.row_off[v]) m |= 1ull << b;
+        if (v >= a.g.rows || (!a.padding_only && a.g.row_off[v + 1] == a.g.row_off[v])) m |= 1ull << b;
       }
       a.out[w] = m;
     }

@@ -58,18 +58,21 @@ struct Args {
   bool quiet = false;
   bool phase_timing = false;
   bool hub_sort = true;
+  bool directed = false;
 };
 
 [[noreturn]] void usage(const char* msg = nullptr) {
   if (msg) std::fprintf(stderr, "error: %s\n\n", msg);
   std::fprintf(stderr,
-               "usage: bfs <src> <edge-list|.mtx|.csr> [flags]\n"
+               "usage: bfs <src> <edge-list|.mtx|.csr|-> [flags]   (- = standard input)\n"
                "       bfs --rmat SCALE[:EF] [<src>] [flags]\n"
                "flags: --gpus P | --virtual-ranks P | --cpu | --device D\n"
                "       --mode ref|td|bu|do|simple|scan  --alpha A --beta B --bu-lane-limit K\n"
                "       --rmat SCALE[:EF] | --uniform N:M   --seed S\n"
                "       --roots K (random sources, GTEPS summary)  --no-oracle  --validate\n"
                "       --levels-out FILE  --cache FILE (write binary CSR)  --json  --quiet  --phase-timing\n"
+               "       --directed (edge list as directed u->v pairs, like the reference's stdin reader;\n"
+               "                   top-down modes only)\n"
                "       --level-csv FILE (per-level records of every run: root,level,dir,frontier,...,ms)\n");
   std::exit(2);
 }
@@ -113,6 +116,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--phase-timing") a.phase_timing = true;
     else if (s == "--no-hub-sort") a.hub_sort = false;
+    else if (s == "--directed") a.directed = true;
     else if (s == "-h" || s == "--help") usage();
     else if (!s.empty() && s[0] == '-' && s.size() > 1 && !std::isdigit(static_cast<unsigned char>(s[1])))
       usage(("unknown flag " + s).c_str());
@@ -132,6 +136,14 @@ Args parse(int argc, char** argv) {
     a.src_given = true;
   }
   if (a.gpus < 1) usage("--gpus must be >= 1");
+  if (a.directed) {
+    // bottom-up searches in-edges, which a directed CSR does not hold; the
+    // Graph500 checks assume an undirected graph
+    if (synth) usage("--directed applies to edge-list input only");
+    if (a.mode == "bu") usage("--directed needs a top-down mode (td, ref, simple, scan)");
+    if (a.mode == "do") a.mode = "td";
+    if (a.validate) usage("--validate checks undirected graphs only (the oracle comparison stays on)");
+  }
   return a;
 }
 
@@ -211,13 +223,13 @@ int main(int argc, char** argv) {
     if (!a.path.empty()) {
       gname = a.path;
       if (ref_lines) std::printf("%s\n", a.path.c_str());
-      if (is_binary_csr(a.path)) {
+      if (a.path != "-" && is_binary_csr(a.path)) {
         full = read_binary_csr(a.path);
       } else {
         ReadOptions ro;
         ro.verbose_reference_lines = ref_lines;
         EdgeList el = read_edge_list(a.path, ro);
-        full = build_csr(el);
+        full = build_csr(el, a.directed);
       }
       have_host = true;
       if (ref_lines) std::printf("finish load graph\n");
@@ -313,6 +325,7 @@ int main(int argc, char** argv) {
     eo.beta = a.beta;
     eo.bu_lane_limit = a.bu_lane_limit;
     eo.phase_timing = a.phase_timing;
+    eo.directed = a.directed;
     run_ranks(ranks, [&](int i, RankCtx& rc) {
       const int rk = multiproc ? wrank : i;
       if (synth) rc.graph = DeviceGraph::generate(*rc.be, gp, part, rk);

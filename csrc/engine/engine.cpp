@@ -61,6 +61,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
+  else if (name == "directed") o.directed = v != 0;
   else if (name == "bu_compact") o.bu_compact = v != 0;
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
@@ -83,6 +84,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
+          {"directed", o.directed ? 1.0 : 0.0},
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
@@ -403,6 +405,7 @@ void Engine::alloc_bitmap_state() {
   // visited, so bottom-up steps skip them without touching row_off.
   ZeroDegArgs za;
   za.g = g_.view();
+  za.padding_only = opt_.directed;  // a directed vertex without out-edges can still be reached
   za.out = zdeg_.data() + comm_.rank() * W;
   za.words = W;
   be_.zero_degree_mask(za);
@@ -432,20 +435,22 @@ void Engine::alloc_ref_state() {
 
 RunResult Engine::run(int64_t source) {
   DBFS_CHECK(source >= 0 && source < part_.n, "source vertex out of range");
+  DBFS_CHECK(!opt_.directed || (opt_.mode != Mode::BottomUp && opt_.mode != Mode::DirOpt),
+             "directed graphs need a top-down mode (bottom-up searches in-edges)");
   RunResult r;
-  if (opt_.mode == Mode::Ref || opt_.mode == Mode::Scan) {
-    r = run_ref(source);
-    // Traversed-edge accounting (Graph500), outside the timed region.
+  const bool ref = opt_.mode == Mode::Ref || opt_.mode == Mode::Scan;
+  r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
+  if (ref || opt_.directed) {
+    // Traversed-edge accounting outside the timed region (the bitmap engine
+    // otherwise knows sum(deg) of every level's new vertices): Graph500's
+    // undirected convention, or all out-edges of reached vertices (directed).
     DBuf<int64_t> acc(be_, 2);
     be_.reached_degree_sum(g_.view(), level_.data(), acc.data());
     comm_.allreduce_sum_i64(acc.data(), 2);
     int64_t h[2];
     be_.to_host(h, acc.data(), sizeof(h));
     r.reached = h[0];
-    r.edges = h[1] / 2;
-  } else {
-    // The bitmap engine already knows sum(deg) of every level's new vertices.
-    r = use_device_loop() ? run_bitmap_device(source) : run_bitmap(source);
+    r.edges = opt_.directed ? h[1] : h[1] / 2;
   }
   r.gteps = r.ms > 0 ? static_cast<double>(r.edges) / (r.ms * 1e6) : 0.0;
   return r;

@@ -11,7 +11,7 @@
 
 namespace dbfs {
 
-HostCSR build_csr(const EdgeList& el) {
+HostCSR build_csr(const EdgeList& el, bool directed) {
   HostCSR g;
   g.n = el.n;
   g.row_lo = 0;
@@ -21,7 +21,7 @@ HostCSR build_csr(const EdgeList& el) {
   const int64_t m = el.m();
   for (int64_t i = 0; i < m; ++i) {
     ++g.row_off[el.u[i] + 1];
-    ++g.row_off[el.v[i] + 1];
+    if (!directed) ++g.row_off[el.v[i] + 1];
   }
   for (int64_t r = 0; r < el.n; ++r) g.row_off[r + 1] += g.row_off[r];
   g.col.resize(static_cast<size_t>(g.row_off[el.n]));
@@ -29,7 +29,7 @@ HostCSR build_csr(const EdgeList& el) {
   for (int64_t i = 0; i < m; ++i) {
     const vid_t a = el.u[i], b = el.v[i];
     g.col[cur[a]++] = b;
-    g.col[cur[b]++] = a;
+    if (!directed) g.col[cur[b]++] = a;
   }
   return g;
 }

@@ -183,6 +183,18 @@ bool is_binary_csr(const std::string& path) {
 }
 
 EdgeList read_edge_list(const std::string& path, const ReadOptions& opt) {
+  if (path == "-") {
+    // standard input (the reference's readGraph, bfs.cu:882-920): slurp, then parse
+    std::string buf;
+    char tmp[1 << 16];
+    size_t k;
+    while ((k = std::fread(tmp, 1, sizeof(tmp), stdin)) > 0) buf.append(tmp, k);
+    Cursor c{buf.data(), buf.data() + buf.size()};
+    const bool mm = opt.format == FileFormat::MatrixMarket ||
+                    (opt.format == FileFormat::Auto && starts_with(buf.data(), buf.size(), "%%MatrixMarket"));
+    if (mm) return parse_matrix_market(c, "<stdin>", opt.verbose_reference_lines);
+    return parse_reference(c, "<stdin>", opt.verbose_reference_lines);
+  }
   FileFormat fmt = opt.format == FileFormat::Auto ? detect_format(path) : opt.format;
   if (fmt == FileFormat::Binary) throw Error("binary CSR cache is not an edge list: " + path);
   MappedFile mf(path);

@@ -344,6 +344,7 @@ struct ZeroDegArgs {
   ShardView g;
   word_t* out = nullptr;  // owned slice
   int64_t words = 0;
+  bool padding_only = false;  // directed graphs: only the padding past the shard
 };
 
 // Vertex-centric ("status array") top-down: every owned v with level[v] == cur

@@ -122,6 +122,10 @@ struct EngineOptions {
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
   bool force_exchange = false;
+  // Directed input (CSR holds out-edges only): top-down modes only; vertices
+  // without out-edges are not pre-marked visited; traversed edges = out-edges
+  // of the reached vertices.
+  bool directed = false;
 };
 
 // Named access to the numeric tuning options (alpha, beta, bu_lane_limit,

@@ -44,11 +44,15 @@ struct ReadOptions {
 // Reference-format `n m` + m lines `u v` (0-based), or MatrixMarket
 // (%%MatrixMarket header, % comments, 1-based, optional value column), or the
 // binary CSR cache (see write_binary_csr).  Throws dbfs::Error on failure.
+// path "-" reads the reference format (or MatrixMarket) from standard input.
 EdgeList read_edge_list(const std::string& path, const ReadOptions& opt = {});
 FileFormat detect_format(const std::string& path);
 
 // Build a symmetrised CSR in reference adjacency order (stable counting sort).
-HostCSR build_csr(const EdgeList& el);
+// directed: u -> v entries only -- the reference's stdin reader `readGraph`
+// (bfs.cu:882-920, dead there: main calls readGraphFromFile) reads the pairs as
+// directed edges without symmetrising.
+HostCSR build_csr(const EdgeList& el, bool directed = false);
 // Rows [lo, hi) of a full CSR (shard extraction; column ids stay global).
 HostCSR slice_rows(const HostCSR& full, int64_t lo, int64_t hi);
 

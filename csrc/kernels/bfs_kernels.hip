@@ -987,7 +987,7 @@ __global__ __launch_bounds__(kBlock) void zero_degree_kernel(ZeroDegArgs a) {
   if (w >= a.words) return;
   const int64_t v = w * 64 + lane;
   bool dead = true;
-  if (v < a.g.rows) dead = a.g.row_off[v + 1] == a.g.row_off[v];
+  if (v < a.g.rows) dead = !a.padding_only && a.g.row_off[v + 1] == a.g.row_off[v];
   const word_t m = __ballot(dead);
   if (lane == 0) a.out[w] = m;
 }

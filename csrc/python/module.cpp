@@ -131,14 +131,16 @@ PYBIND11_MODULE(_dbfs_native, m) {
 
   m.def(
       "read_graph",
-      [](const std::string& path, bool verbose) {
-        if (is_binary_csr(path)) return read_binary_csr(path);
+      [](const std::string& path, bool verbose, bool directed) {
+        if (path != "-" && is_binary_csr(path)) return read_binary_csr(path);
         ReadOptions ro;
         ro.verbose_reference_lines = verbose;
-        return build_csr(read_edge_list(path, ro));
+        return build_csr(read_edge_list(path, ro), directed);
       },
-      py::arg("path"), py::arg("verbose") = false, py::call_guard<py::gil_scoped_release>(),
-      "Read an edge list / MatrixMarket / binary-CSR file into a symmetrised CSR.");
+      py::arg("path"), py::arg("verbose") = false, py::arg("directed") = false,
+      py::call_guard<py::gil_scoped_release>(),
+      "Read an edge list / MatrixMarket / binary-CSR file (\"-\": standard input) into a CSR, symmetrised "
+      "unless directed.");
   m.def(
       "read_edge_list",
       [](const std::string& path) {
@@ -156,7 +158,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
   m.def(
       "build_csr",
       [](int64_t n, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> u,
-         py::array_t<uint32_t, py::array::c_style | py::array::forcecast> v) {
+         py::array_t<uint32_t, py::array::c_style | py::array::forcecast> v, bool directed) {
         EdgeList el;
         el.n = n;
         el.u = from_numpy<uint32_t>(u);
@@ -164,9 +166,9 @@ PYBIND11_MODULE(_dbfs_native, m) {
         DBFS_CHECK(el.u.size() == el.v.size(), "u and v must have the same length");
         for (size_t i = 0; i < el.u.size(); ++i)
           DBFS_CHECK(el.u[i] < n && el.v[i] < n, "edge endpoint out of range");
-        return build_csr(el);
+        return build_csr(el, directed);
       },
-      py::arg("n"), py::arg("u"), py::arg("v"));
+      py::arg("n"), py::arg("u"), py::arg("v"), py::arg("directed") = false);
   m.def("write_binary_csr", &write_binary_csr, py::arg("path"), py::arg("csr"));
   m.def("write_levels", [](const std::string& path, py::array_t<int32_t, py::array::c_style | py::array::forcecast> l) {
     write_levels(path, from_numpy<int32_t>(l));

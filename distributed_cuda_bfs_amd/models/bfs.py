@@ -42,7 +42,7 @@ class BFS:
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
                  alpha: float = 24.0, beta: float = 24.0, bu_lane_limit: int = 8, phase_timing: bool = False,
                  hub_sort: bool = True, force_exchange: bool = False, hubs: bool = True,
-                 max_hubs: Optional[int] = None):
+                 max_hubs: Optional[int] = None, directed: bool = False):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
         frontier parent sooner (see csrc/kernels/graph_sort.hip).  ``hubs`` also
@@ -51,8 +51,10 @@ class BFS:
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.rt = runtime or init_runtime()
+        if directed and mode in ("bu", "do"):
+            raise ValueError("directed graphs need a top-down mode (td, ref, simple, scan)")
         if isinstance(graph, str):
-            graph = N.read_graph(graph)
+            graph = N.read_graph(graph, False, directed)
         if isinstance(graph, N.GenParams):
             self.n = graph.n
             self.partition = N.Partition(graph.n, self.rt.world)
@@ -71,6 +73,8 @@ class BFS:
         self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
                                bu_lane_limit=bu_lane_limit, phase_timing=phase_timing,
                                force_exchange=force_exchange)
+        if directed:  # the CSR holds out-edges only (see build_csr / read_graph)
+            self.engine.set_option("directed", 1)
 
     @property
     def mode(self) -> str:

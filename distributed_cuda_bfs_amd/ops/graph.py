@@ -11,9 +11,11 @@ import numpy as np
 from .._native import N
 
 
-def read_graph(path: str, verbose: bool = False):
-    """Edge list (``n m`` + ``u v`` lines), MatrixMarket (.mtx) or binary CSR -> HostCSR."""
-    return N.read_graph(path, verbose)
+def read_graph(path: str, verbose: bool = False, directed: bool = False):
+    """Edge list (``n m`` + ``u v`` lines), MatrixMarket (.mtx) or binary CSR -> HostCSR
+    (``"-"`` reads standard input).  ``directed`` keeps the pairs as u -> v edges (the
+    reference's stdin reader ``readGraph``, bfs.cu:882-920) instead of symmetrising."""
+    return N.read_graph(path, verbose, directed)
 
 
 def read_edge_list(path: str):
@@ -25,9 +27,10 @@ def detect_format(path: str) -> str:
     return N.detect_format(path)
 
 
-def build_csr(n: int, u, v):
-    """Symmetrised CSR in the reference's adjacency order (dups and self-loops kept)."""
-    return N.build_csr(int(n), np.ascontiguousarray(u, dtype=np.uint32), np.ascontiguousarray(v, dtype=np.uint32))
+def build_csr(n: int, u, v, directed: bool = False):
+    """CSR in the reference's adjacency order (dups and self-loops kept), symmetrised unless directed."""
+    return N.build_csr(int(n), np.ascontiguousarray(u, dtype=np.uint32), np.ascontiguousarray(v, dtype=np.uint32),
+                       bool(directed))
 
 
 def rmat_params(scale: int, edge_factor: int = 16, seed: int = 1, scramble: bool = True):

@@ -12,6 +12,8 @@ import pytest
 import distributed_cuda_bfs_amd as dbfs
 from distributed_cuda_bfs_amd.utils.validate import check_levels_against_oracle, levels_are_consistent
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 U = dbfs.UNREACHED
 
 
@@ -136,3 +138,36 @@ def test_partition_block_rounding():
     q = N.Partition(5, 4)
     assert all(0 <= q.owner(v) < 4 for v in range(5))
     assert sum(q.count(r) for r in range(4)) == 5
+
+
+def test_directed_stdin_reader_and_engine(tmp_path):
+    # the reference's stdin reader (readGraph, bfs.cu:882-920): pairs as
+    # directed edges, no symmetrisation; top-down modes on the CSR of out-edges
+    import subprocess
+    import sys
+
+    import distributed_cuda_bfs_amd as dbfs
+    from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
+
+    text = "6 5\n0 1\n1 2\n3 2\n2 4\n4 0\n"
+    path = tmp_path / "d.txt"
+    path.write_text(text)
+    g = dbfs.read_graph(str(path), directed=True)
+    assert g.directed_edges == 5 and np.diff(np.asarray(g.row_off)).tolist() == [1, 1, 1, 1, 1, 0]
+    exp, _ = dbfs.cpu_bfs(g, 0)
+    assert exp.tolist() == [0, 1, 2, dbfs.UNREACHED, 3, dbfs.UNREACHED]
+    rt = init_runtime("cpu")
+    for mode in ("td", "ref", "simple", "scan"):
+        for P in (1,):
+            bfs = dbfs.BFS(g, rt, mode=mode, directed=True)
+            res = bfs.run(0)
+            assert np.array_equal(bfs.levels(), exp), mode
+            assert res.reached == 4 and res.edges == 4, (mode, res.reached, res.edges)
+    with pytest.raises(ValueError):
+        dbfs.BFS(g, rt, mode="do", directed=True)
+    # CLI, edge list on standard input
+    out = subprocess.run([os.path.join(REPO, "bin", "bfs"), "0", "-", "--cpu", "--directed", "--quiet",
+                          "--levels-out", str(tmp_path / "lv.txt")], input=text, capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert (tmp_path / "lv.txt").read_text().split() == ["0", "1", "2", "2147483647", "3", "2147483647"]
