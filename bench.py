@@ -193,6 +193,12 @@ def main() -> int:
             "generate_s": round(gen_s, 3),
             "level_profile": {"root": med.source, "levels": level_profile,
                               "columns": ["dir", "ms", "comm_ms"]},
+            # the timed traversal of the same root, from the device clock the
+            # kernels stamp (device loop only): level time and the idle gap
+            # before its first kernel
+            "level_clock": {"levels": [[lv["dir"], round(lv["ms"], 4), round(lv.get("gap_ms", -1.0), 4)]
+                                       for lv in med.levels],
+                            "columns": ["dir", "ms", "gap_ms"]},
         }
         print(json.dumps(out), flush=True)
     return 0

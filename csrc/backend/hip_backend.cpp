@@ -39,6 +39,9 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
     cus_ = prop.multiProcessorCount;
+    int khz = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_));
+    clock_khz_ = khz;
     HIP_CHECK(hipHostMalloc(&pinned_, kPinned, hipHostMallocDefault));
   }
   ~HipBackend() override {
@@ -55,6 +58,7 @@ class HipBackend final : public Backend {
     return "hip:" + std::to_string(dev_) + " (" + arch_ + ", " + std::to_string(cus_) + " CUs)";
   }
   int device_id() const override { return dev_; }
+  double wall_clock_khz() const override { return clock_khz_; }
   void* stream_handle() override { return st_; }
 
   void* alloc(size_t bytes) override {
@@ -287,6 +291,7 @@ class HipBackend final : public Backend {
   hipStream_t st_ = nullptr;
   std::string arch_;
   int cus_ = 0;
+  double clock_khz_ = 0.0;
   std::vector<hipEvent_t> events_;
   size_t ev_used_ = 0;
   eid_t* scan_tmp_ = nullptr;

@@ -891,7 +891,18 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // Enqueue level L's chain for direction d: top-down = compact + td_expand +
   // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
   // so a chain enqueued for the wrong direction is a handful of no-op launches.
+  // DBFS_HOST_TIMING=1: host-side enqueue / stamp-wait timeline to stderr
+  static const bool host_timing = [] {
+    const char* e = std::getenv("DBFS_HOST_TIMING");
+    return e && *e == '1';
+  }();
+  std::vector<std::pair<std::string, double>> htl;
+  auto hmark = [&](const std::string& what) {
+    if (host_timing)
+      htl.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  };
   auto enqueue_level = [&](int L, char d) {
+    hmark("enqueue " + std::to_string(L) + d);
     if (static_cast<size_t>(L) >= rec_.size()) {
       // grow the record array (stream-ordered copy; the old one is freed after a sync)
       DBuf<LevelRecDev> bigger(be_, rec_.size() * 2);
@@ -975,6 +986,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     }
     scan(L, false, d);
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
+    hmark("enqueued " + std::to_string(L));
   };
 
   // Host loop, one level ahead of the device.  The stamp of level L - 1
@@ -994,6 +1006,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   for (int L = 0;; ++L) {
     if (!opt_.device_loop_predict) enqueue_level(L + 1, enq_dir[L]);
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
+    hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {
       nlev = L;
       break;
@@ -1033,6 +1046,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   const auto t1 = std::chrono::steady_clock::now();
   scratch_dirty_ = false;
   res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (host_timing) {
+    hmark("synchronized");
+    std::string line = "[host timing]";
+    for (auto& [w, us] : htl) line += " " + w + "@" + std::to_string(static_cast<int>(us));
+    std::fprintf(stderr, "%s\n", line.c_str());
+  }
   const int64_t vis_deg = mailbox_host_[slot(nlev - 1)].vis_deg;
 
   // per-level records (outside the timed window)
@@ -1047,6 +1066,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     r.frontier_edges = recs[L].m_f;
     r.discovered = recs[L].discovered;
     if (opt_.phase_timing && static_cast<size_t>(L) < evs.size()) r.ms = be_.elapsed_ms(evs[L].first, evs[L].second);
+    // device-clock times (kernels stamp them; no events, no overhead)
+    const double khz = be_.wall_clock_khz();
+    if (khz > 0 && recs[L].t0 != 0 && recs[L].t1 >= recs[L].t0) {
+      if (!opt_.phase_timing) r.ms = static_cast<double>(recs[L].t1 - recs[L].t0) / khz;
+      if (L > 0 && recs[L - 1].t1 != 0)
+        r.gap_ms = (static_cast<double>(recs[L].t0) - static_cast<double>(recs[L - 1].t1)) / khz;
+    }
     res.reached += r.discovered;
     res.levels.push_back(r);
   }

@@ -97,12 +97,16 @@ struct LevelCtrl {
   int32_t check_visited = 1;    // ... with the visited pre-check
   int32_t done = 0;             // frontier empty: every later kernel returns
   int64_t n_f = 0, m_f = 0, prev_nf = 0, vis_deg = 0;
+  // device wall clock (Backend::wall_clock_khz) when the running level's
+  // first kernel started
+  uint64_t t_start = 0;
 };
 
 // One record per finished level (device array; read after the run).
 struct LevelRecDev {
   int32_t dir = 0, pad = 0;
   int64_t n_f = 0, m_f = 0, discovered = 0;
+  uint64_t t0 = 0, t1 = 0;  // device wall clock: first kernel started, scan finished
 };
 
 // Host-visible mailbox slot (pinned, device-mapped), written by the scan's
@@ -438,6 +442,9 @@ class Backend {
   virtual std::string name() const = 0;
   virtual int device_id() const { return -1; }
   virtual void* stream_handle() { return nullptr; }
+  // Rate of the device wall clock the kernels stamp level records with (ticks
+  // per ms; 0: no device clock, records carry no times).
+  virtual double wall_clock_khz() const { return 0.0; }
 
   // Host waits on the device (to_host, to_device, synchronize) call
   // watch(seconds waited) about every period_s while the stream is still busy;

@@ -142,6 +142,9 @@ struct LevelRecord {
   int64_t discovered = 0;     // global new vertices
   double ms = 0.0;            // device time of the level (phase_timing only)
   double comm_ms = 0.0;       // ... of which in collectives (host loop, phase_timing only)
+  // Device loop, device clock: idle time between the previous level's scan
+  // and this level's first kernel (launch gaps; -1 when unknown).
+  double gap_ms = -1.0;
 };
 
 struct RunResult {

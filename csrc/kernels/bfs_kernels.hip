@@ -36,6 +36,14 @@ namespace {
 
 using namespace dev;
 
+// First kernel of a device-loop level chain: record its start (device wall
+// clock) for the level's record (scan_units_kernel copies it to rec[L].t0).
+// (The argument blocks carry the control block as const; this field is the
+// one a level's kernels write.)
+__device__ __forceinline__ void stamp_level_start(const LevelCtrl* c) {
+  if (c && blockIdx.x == 0 && threadIdx.x == 0) const_cast<LevelCtrl*>(c)->t_start = wall_clock64();
+}
+
 constexpr int kBlock = 256;
 constexpr int kUnitThreads = kUnitWaves * kWave;  // 256: 4 waves x 16 words
 static_assert(kUnitThreads == 256 && kWaveWords <= kWave, "unit geometry");
@@ -352,6 +360,10 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     if (a.ctrl) {
       LevelCtrl c = *a.ctrl;
       level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec + a.level);
+      if (!a.seed) {
+        a.rec[a.level].t0 = c.t_start;
+        a.rec[a.level].t1 = wall_clock64();
+      }
       *a.ctrl = c;
       if (a.mailbox) {
         // host-mapped pinned slot: system-scope stores, level last
@@ -376,6 +388,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
 // sum of degrees.
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T')) return;
+  stamp_level_start(a.ctrl);
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
@@ -881,6 +894,7 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
   __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
   __shared__ word_t s_res[kCompact ? kUnitWaves * kWaveWords : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  if (!a.hub_front) stamp_level_start(a.ctrl);
   long long cnt = 0, deg = 0;
   const int wave = threadIdx.x >> 6;
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + wave * kWaveWords;
@@ -913,6 +927,7 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
   __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   for (int64_t i = threadIdx.x; i < hw; i += kHubBuThreads) s_hub[i] = a.hub_front[i];
   __syncthreads();
@@ -973,6 +988,7 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
 // hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word.
 __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  stamp_level_start(a.ctrl);
   const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
   const int64_t h = w * kWave + lane_id();
   const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);

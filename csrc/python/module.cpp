@@ -47,6 +47,7 @@ py::dict result_dict(const RunResult& r) {
     x["discovered"] = l.discovered;
     x["ms"] = l.ms;
     x["comm_ms"] = l.comm_ms;
+    x["gap_ms"] = l.gap_ms;
     lv.append(x);
   }
   d["levels"] = lv;
