@@ -110,6 +110,14 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = cnt;
     a.stats[1] = a.stats[3] = deg;
     a.qscan[cnt] = deg;
+    if (a.frontier_clear)
+      for (int64_t w = 0; w < a.words; ++w) a.frontier_clear[w] = 0;
+    if (cnt && a.qbase) {
+      a.qscan[0] = 0;
+      a.qbase[0] = a.g.row_off[src];
+      a.qv[0] = static_cast<vid_t>(src);
+      for (int64_t b = 0; b * kTdEdgesPerBlock < deg; ++b) a.blk_vstart[b] = 0;
+    }
     if (a.ctrl) {
       LevelCtrl c = a.ctrl_init;
       level_ctrl_finish(c, cnt, deg, true, nullptr);
@@ -189,6 +197,7 @@ class CpuBackend final : public Backend {
       int64_t off = a.unit_deg_off[u] + a.part_deg[u / kScanChunk];
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t x = a.frontier[w];
+        if (a.clear) a.clear[w] = 0;
         while (x) {
           const int b = __builtin_ctzll(x);
           x &= x - 1;
@@ -197,6 +206,7 @@ class CpuBackend final : public Backend {
           if (d <= 0) continue;
           a.qscan[pos] = off;
           a.qbase[pos] = rs - off;
+          if (a.qv) a.qv[pos] = static_cast<vid_t>(v);
           for (int64_t blk = div_up(off, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < off + d; ++blk)
             a.blk_vstart[blk] = static_cast<int32_t>(pos);
           ++pos;
@@ -213,6 +223,8 @@ class CpuBackend final : public Backend {
       if (a.ctrl->done || a.ctrl->dir != 'T') return;
       q = a.dev_stats[0];
       bytes = a.ctrl->bytes != 0;
+      if (a.clear_qv)
+        for (int64_t i = 0; i < q; ++i) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
     }
     for (int64_t i = 0; i < q; ++i) {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
@@ -228,6 +240,44 @@ class CpuBackend final : public Backend {
           a.next[v >> 6] |= 1ull << (v & 63);
         }
       }
+    }
+  }
+
+  void td_sparse(const TdSparseArgs& a) override {
+    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    const int64_t q = a.dev_stats[0];
+    for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
+    int64_t cnt = 0, deg = 0;
+    for (int64_t i = 0; i < q; ++i) {
+      for (int64_t k = a.qscan[i]; k < a.qscan[i + 1]; ++k) {
+        const vid_t v = a.g.col[k + a.qbase[i]];
+        if (test_bit(a.visited, v)) continue;
+        a.visited[v >> 6] |= 1ull << (v & 63);
+        const int64_t r = static_cast<int64_t>(v) - a.g.lo;
+        a.level[r] = a.new_level;
+        const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
+        if (d <= 0) continue;
+        a.frontier_out[r >> 6] |= 1ull << (r & 63);
+        a.oscan[cnt] = deg;
+        a.obase[cnt] = rs - deg;
+        a.oqv[cnt] = static_cast<vid_t>(r);
+        for (int64_t blk = div_up(deg, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < deg + d; ++blk)
+          a.oblk[blk] = static_cast<int32_t>(cnt);
+        ++cnt;
+        deg += d;
+      }
+    }
+    a.stats[0] = a.stats[2] = cnt;
+    a.stats[1] = a.stats[3] = deg;
+    a.oscan[cnt] = deg;
+    level_ctrl_finish(*a.ctrl, cnt, deg, false, a.rec + a.level_index);
+    if (a.mailbox) {
+      a.mailbox->done = a.ctrl->done;
+      a.mailbox->vis_deg = a.ctrl->vis_deg;
+      a.mailbox->next_dir = a.ctrl->dir;
+      a.mailbox->n_f = a.ctrl->n_f;
+      a.mailbox->m_f = a.ctrl->m_f;
+      a.mailbox->level = a.level_index;
     }
   }
 
@@ -494,6 +544,14 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void degree_square_sum(const ShardView& g, int64_t* out1) override {
+    int64_t s = 0;
+    for (int64_t r = 0; r < g.rows; ++r) {
+      const int64_t d = g.row_off[r + 1] - g.row_off[r];
+      s += d * d;
+    }
+    out1[0] = s;
+  }
   void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) override {
     int64_t c = 0, d = 0;
     for (int64_t r = 0; r < g.rows; ++r)

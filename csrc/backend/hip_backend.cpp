@@ -182,6 +182,7 @@ class HipBackend final : public Backend {
   }
   void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
+  void td_sparse(const TdSparseArgs& a) override { on(); kern::td_sparse(a, st_); chk(); }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
@@ -270,6 +271,12 @@ class HipBackend final : public Backend {
   void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) override {
     on();
     kern::gen_fill(p, lo, rows, cursor, col, st_);
+    chk();
+  }
+  void degree_square_sum(const ShardView& g, int64_t* out1) override {
+    on();
+    HIP_CHECK(hipMemsetAsync(out1, 0, sizeof(int64_t), st_));
+    kern::degree_square_sum(g, out1, st_);
     chk();
   }
   void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) override {

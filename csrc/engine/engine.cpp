@@ -66,6 +66,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
   else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
+  else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
+  else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -87,6 +89,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"directed", o.directed ? 1.0 : 0.0},
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
+          {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
+          {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0}};
 }
@@ -789,6 +793,13 @@ RunResult Engine::run_bitmap(int64_t source) {
   return res;
 }
 
+// Sparse top-down levels (device loop): the packed output counter holds
+// 64 - kSparseEdgeBits bits of entries and kSparseEdgeBits of edges.
+bool Engine::sparse_enabled() const {
+  return opt_.td_sparse_edges > 0 && opt_.mode != Mode::BottomUp && g_.rows() < (int64_t(1) << (64 - kSparseEdgeBits)) &&
+         g_.nnz() < (int64_t(1) << kSparseEdgeBits);
+}
+
 bool Engine::use_device_loop() const {
   return opt_.device_loop && !exchange() &&
          (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
@@ -820,6 +831,30 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
     be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
   }
+  const bool sparse = sparse_enabled();
+  if (sparse && !sparse_ready_) {
+    const size_t rows = static_cast<size_t>(std::max<int64_t>(g_.rows(), 1));
+    qscan2_ = DBuf<int64_t>(be_, rows + 1);
+    qbase2_ = DBuf<int64_t>(be_, rows);
+    blk_vstart2_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
+    qv_[0] = DBuf<vid_t>(be_, rows);
+    qv_[1] = DBuf<vid_t>(be_, rows);
+    sparse_cnt_ = DBuf<unsigned long long>(be_, 2);
+    sparse_ticket_ = DBuf<unsigned>(be_, 1);
+    be_.memset_async(sparse_cnt_.data(), 0, sparse_cnt_.bytes());
+    be_.memset_async(sparse_ticket_.data(), 0, sparse_ticket_.bytes());
+    // mean degree of an edge's endpoint (sum deg^2 / sum deg): predicts the
+    // edges of level 1's frontier (the source's neighbours) from the source's degree
+    be_.degree_square_sum(gv, stats_.data() + 4);
+    int64_t sq = 0;
+    be_.to_host(&sq, stats_.data() + 4, sizeof(sq));
+    excess_degree_ = total_directed_ > 0 ? static_cast<double>(sq) / static_cast<double>(total_directed_) : 0.0;
+    sparse_ready_ = true;
+  }
+  // work-list set k (level L reads set L & 1; one set without sparse levels)
+  auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
+  auto qbase_set = [&](int k) { return sparse && (k & 1) ? qbase2_.data() : qbase_.data(); };
+  auto blk_set = [&](int k) { return sparse && (k & 1) ? blk_vstart2_.data() : blk_vstart_.data(); };
   // the previous run has completed (it ended with a synchronize): stamps can be reset
   for (int i = 0; i < kMailboxSlots; ++i) {
     volatile LevelMailbox* mb = mailbox_host_ + i;
@@ -852,7 +887,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
   // one fused pass: levels, visited, the seed frontier (frontier_[1]), its
   // totals, the seeded LevelCtrl and the mailbox stamp of level -1
-  be_.init_run(init_args(source, frontier_[1].data(), ctrl_.data(), init, mailbox_dev_ + slot(-1)));
+  // (+ with sparse levels: the seed's work-list entry in set 0 and a clean
+  // frontier_[0] for a sparse level 0 to write)
+  InitRunArgs ia = init_args(source, frontier_[1].data(), ctrl_.data(), init, mailbox_dev_ + slot(-1));
+  if (sparse) {
+    ia.qbase = qbase_.data();
+    ia.blk_vstart = blk_vstart_.data();
+    ia.qv = qv_[0].data();
+    ia.frontier_clear = frontier_[0].data();
+  }
+  be_.init_run(ia);
 
   auto scan = [&](int level, bool seed, char expect_dir) {
     ScanArgs sa;
@@ -863,7 +907,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.part_deg = part_deg_.data();
     sa.ticket = ticket_.data();
     sa.stats = stats_.data();
-    sa.qscan = qscan_.data();
+    sa.qscan = qscan_set(level + 1);
     sa.ctrl = ctrl_.data();
     sa.rec = rec_.data();
     sa.mailbox = mailbox_dev_ + slot(level);
@@ -887,7 +931,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
 
   const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), 2048));
   std::vector<std::pair<int, int>> evs;
-  std::vector<char> enq_dir;  // direction each level was (last) enqueued with
+  std::vector<char> enq_dir;   // direction each level was (last) enqueued with
+  std::vector<char> enq_form;  // ... and its chain form ('T', 'S', 'B')
   // Enqueue level L's chain for direction d: top-down = compact + td_expand +
   // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
   // so a chain enqueued for the wrong direction is a handful of no-op launches.
@@ -912,15 +957,23 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (static_cast<size_t>(L) >= enq_dir.size()) {
       inject_fault(L);
       enq_dir.resize(static_cast<size_t>(L) + 1);
+      enq_form.resize(static_cast<size_t>(L) + 1);
       evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
     }
-    enq_dir[L] = d;
+    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up; the
+    // previous level's form decides what hands this one its work list
+    const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
+    enq_dir[L] = d == 'B' ? 'B' : 'T';
+    enq_form[L] = d;
     const int cur = (L + 1) & 1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    if (d == 'T') {
+    // the frontier bitmap -> work list (set L & 1); with sparse levels also
+    // its vertex map, and the bitmap is zeroed as read (a later sparse level
+    // writes into it)
+    auto compact = [&] {
       CompactArgs ca;
       ca.g = gv;
       ca.frontier = frontier_[cur].data();
@@ -929,16 +982,57 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ca.unit_deg_off = unit_deg_.data();
       ca.part_cnt = part_cnt_.data();
       ca.part_deg = part_deg_.data();
-      ca.qscan = qscan_.data();
-      ca.qbase = qbase_.data();
-      ca.blk_vstart = blk_vstart_.data();
+      ca.qscan = qscan_set(L);
+      ca.qbase = qbase_set(L);
+      ca.blk_vstart = blk_set(L);
+      if (sparse) {
+        ca.qv = qv_[L & 1].data();
+        ca.clear = frontier_[cur].data();
+      }
       ca.ctrl = ctrl_.data();
       be_.compact_frontier(ca);
+    };
+    if (d == 'S') {
+      DBFS_CHECK(sparse && pf != 'B', "sparse top-down level after a bottom-up level");
+      if (pf == 'T') compact();
+      TdSparseArgs sp;
+      sp.g = gv;
+      sp.qscan = qscan_set(L);
+      sp.qbase = qbase_set(L);
+      sp.blk_vstart = blk_set(L);
+      sp.qv = qv_[L & 1].data();
+      sp.dev_stats = stats_.data();
+      sp.frontier_in = frontier_[cur].data();
+      sp.frontier_out = frontier_[cur ^ 1].data();
+      sp.visited = visited_.data();
+      sp.level = level_.data();
+      sp.new_level = L + 1;
+      sp.oscan = qscan_set(L + 1);
+      sp.obase = qbase_set(L + 1);
+      sp.oblk = blk_set(L + 1);
+      sp.oqv = qv_[(L + 1) & 1].data();
+      sp.counter = sparse_cnt_.data() + ((L + 1) & 1);
+      sp.ticket = sparse_ticket_.data();
+      sp.stats = stats_.data();
+      sp.ctrl = ctrl_.data();
+      sp.rec = rec_.data();
+      sp.mailbox = mailbox_dev_ + slot(L);
+      sp.level_index = L;
+      sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
+      be_.td_sparse(sp);
+    } else if (d == 'T') {
+      // a sparse level (or the seed) already handed over the work list
+      const bool listed = sparse && (pf == 'S' || pf == 'I');
+      if (!listed) compact();
       TdArgs ta;
       ta.g = gv;
-      ta.qscan = qscan_.data();
-      ta.qbase = qbase_.data();
-      ta.blk_vstart = blk_vstart_.data();
+      ta.qscan = qscan_set(L);
+      ta.qbase = qbase_set(L);
+      ta.blk_vstart = blk_set(L);
+      if (listed) {
+        ta.clear_qv = qv_[L & 1].data();
+        ta.clear_frontier = frontier_[cur].data();
+      }
       ta.visited = visited_.data();
       ta.next = next_.data();
       ta.next_bytes = next_bytes_.data();
@@ -984,7 +1078,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       }
       be_.bu_step(ba);
     }
-    scan(L, false, d);
+    if (d != 'S') scan(L, false, enq_dir[L]);
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
     hmark("enqueued " + std::to_string(L));
   };
@@ -1002,9 +1096,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   int nlev = 0;
   LevelCtrl hc = init;  // host mirror for the prediction
   int64_t prev_nf = 0, prev_mf = 0;
-  enqueue_level(0, static_cast<char>(init.dir));
+  // top-down form of level L whose frontier has (about) mf edges: sparse when
+  // small, and never right after a bottom-up level (its input bitmap is
+  // still set, so a sparse level would have no clean bitmap to write)
+  auto td_form = [&](int L, double mf) {
+    const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
+    return sparse && pf != 'B' && mf <= static_cast<double>(opt_.td_sparse_edges) ? 'S' : 'T';
+  };
+  enqueue_level(0, init.dir == 'B' ? 'B' : td_form(0, 0.0));
   for (int L = 0;; ++L) {
-    if (!opt_.device_loop_predict) enqueue_level(L + 1, enq_dir[L]);
+    if (!opt_.device_loop_predict) enqueue_level(L + 1, enq_dir[L]);  // dense top-down or bottom-up
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
     hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {
@@ -1020,8 +1121,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       }
       continue;
     }
-    if (actual != enq_dir[L]) enqueue_level(L, actual);
     const int64_t nf = mb->n_f, mf = mb->m_f;
+    if (actual != enq_dir[L]) enqueue_level(L, actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf)));
     // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
     auto grow = [](int64_t cur, int64_t prev) {
       if (prev <= 0) return static_cast<double>(cur) * static_cast<double>(cur);
@@ -1035,12 +1136,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     LevelRecDev scratch;
     const double cap = static_cast<double>(part_.n);
     const double enf = std::min(grow(nf, prev_nf), cap);
-    const double emf = std::min(grow(mf, prev_mf), static_cast<double>(total_directed_));
+    // level 1's frontier edges: the source's neighbours have the mean endpoint degree
+    const double emf = std::min(L == 0 ? static_cast<double>(mf) * std::max(1.0, excess_degree_) : grow(mf, prev_mf),
+                                static_cast<double>(total_directed_));
     level_ctrl_finish(hc, std::max<int64_t>(1, static_cast<int64_t>(enf)), static_cast<int64_t>(emf), false,
                       &scratch);
     prev_nf = nf;
     prev_mf = mf;
-    enqueue_level(L + 1, static_cast<char>(hc.dir));
+    enqueue_level(L + 1, hc.dir == 'B' ? 'B' : td_form(L + 1, emf));
   }
   be_.synchronize();
   const auto t1 = std::chrono::steady_clock::now();

@@ -173,6 +173,13 @@ struct InitRunArgs {
   int64_t* part_deg = nullptr;
   int64_t* stats = nullptr;
   int64_t* qscan = nullptr;
+  // Device loop: the seed's work-list entry (source vertex, qbase, the edge
+  // blocks it covers) so a sparse first level can run without a compaction,
+  // and frontier_clear (the first level's output bitmap) zeroed.
+  int64_t* qbase = nullptr;
+  int32_t* blk_vstart = nullptr;
+  vid_t* qv = nullptr;
+  word_t* frontier_clear = nullptr;
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;
@@ -256,7 +263,47 @@ struct CompactArgs {
   int64_t* qscan = nullptr;
   int64_t* qbase = nullptr;
   int32_t* blk_vstart = nullptr;
+  vid_t* qv = nullptr;              // optional: work-list entry -> vertex (local row)
+  word_t* clear = nullptr;          // optional: zero the frontier words once read (== frontier)
   const LevelCtrl* ctrl = nullptr;  // device loop: runs only when ctrl->dir == 'T'
+};
+
+// Sparse top-down level (device loop, one rank): one kernel instead of
+// compact + td_expand + update + scan.  Expands the work list (qscan / qbase /
+// blk_vstart / qv, totals in dev_stats[0..1]) edge-balanced like td_expand,
+// claims each new vertex with a fetch-or on `visited`, writes its level, sets
+// its bit in frontier_out (clean on entry) and appends it -- wave-aggregated,
+// one packed atomic (count << kSparseEdgeBits | edges) per wave, so entries
+// stay ordered by edge offset -- to the output work list (oscan / obase / oblk
+// / oqv) the next level expands directly.  The input vertices' bits are
+// cleared from frontier_in (keeps the bitmap the next sparse level writes
+// clean).  The last workgroup publishes the totals (stats[0..3], oscan[q]),
+// runs level_ctrl_finish and stamps rec / the mailbox like the scan.
+constexpr int kSparseEdgeBits = 36;
+struct TdSparseArgs {
+  ShardView g;
+  const int64_t* qscan = nullptr;
+  const int64_t* qbase = nullptr;
+  const int32_t* blk_vstart = nullptr;
+  const vid_t* qv = nullptr;
+  const int64_t* dev_stats = nullptr;  // [0] entries, [1] edges of the input list
+  word_t* frontier_in = nullptr;       // owned slice
+  word_t* frontier_out = nullptr;      // owned slice, zero on entry
+  word_t* visited = nullptr;           // global
+  lvl_t* level = nullptr;              // rows
+  int32_t new_level = 0;
+  int64_t* oscan = nullptr;
+  int64_t* obase = nullptr;
+  int32_t* oblk = nullptr;
+  vid_t* oqv = nullptr;
+  unsigned long long* counter = nullptr;  // zero on entry; reset by the last workgroup
+  unsigned* ticket = nullptr;             // zero on entry; reset by the last workgroup
+  int64_t* stats = nullptr;
+  LevelCtrl* ctrl = nullptr;
+  LevelRecDev* rec = nullptr;
+  LevelMailbox* mailbox = nullptr;
+  int32_t level_index = 0;
+  int64_t grid = 0;
 };
 
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
@@ -289,6 +336,10 @@ struct TdArgs {
   const LevelCtrl* ctrl = nullptr;
   const int64_t* dev_stats = nullptr;
   int64_t grid = 0;
+  // Device loop, work list handed over by a sparse level (no compaction ran):
+  // zero the input vertices' words of clear_frontier (clear_qv: entry -> row).
+  const vid_t* clear_qv = nullptr;
+  word_t* clear_frontier = nullptr;
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)
@@ -497,6 +548,7 @@ class Backend {
   virtual void free_mapped(void* host_ptr) = 0;
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
+  virtual void td_sparse(const TdSparseArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;
@@ -544,6 +596,8 @@ class Backend {
   virtual void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) = 0;
   // sum of degrees of vertices with level != kUnreached (device scalar out)
   virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
+  // sum over the shard's rows of degree^2 (device scalar out)
+  virtual void degree_square_sum(const ShardView& g, int64_t* out1) = 0;
 
  protected:
   std::function<void(double)> wait_watch_;

@@ -118,6 +118,12 @@ struct EngineOptions {
   // through a device-mapped mailbox the host spins on, instead of a D2H copy
   // plus a stream synchronisation.
   bool stats_mailbox = true;
+  // Device loop: top-down levels whose frontier is predicted to have at most
+  // this many edges run as one sparse kernel (TdSparseArgs: direct claims, work list
+  // handed to the next level) instead of compact + td_expand + update + scan;
+  // 0 disables.  td_sparse_grid: its workgroups.
+  int64_t td_sparse_edges = int64_t(1) << 16;
+  int64_t td_sparse_grid = 256;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -217,6 +223,16 @@ class Engine {
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;
+  // device loop, sparse top-down levels: a second work-list set (level L
+  // reads set L & 1), entry -> vertex maps, output counters, a ticket
+  bool sparse_ready_ = false;
+  double excess_degree_ = 0.0;  // sum deg^2 / sum deg (level-1 edge prediction)
+  DBuf<int64_t> qscan2_, qbase2_;
+  DBuf<int32_t> blk_vstart2_;
+  DBuf<vid_t> qv_[2];
+  DBuf<unsigned long long> sparse_cnt_;
+  DBuf<unsigned> sparse_ticket_;
+  bool sparse_enabled() const;
   int64_t nunits_ = 0;
   // device-driven loop state
   DBuf<LevelCtrl> ctrl_;

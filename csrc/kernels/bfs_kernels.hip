@@ -44,6 +44,21 @@ __device__ __forceinline__ void stamp_level_start(const LevelCtrl* c) {
   if (c && blockIdx.x == 0 && threadIdx.x == 0) const_cast<LevelCtrl*>(c)->t_start = wall_clock64();
 }
 
+// Level-end stamp of the host-mapped mailbox slot: values first (system
+// scope), then the level with release semantics, so a host that observes the
+// level reads that level's values.
+__device__ __forceinline__ void stamp_mailbox(LevelMailbox* mb, const LevelCtrl& c, int32_t level) {
+  __hip_atomic_store(&mb->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->vis_deg), static_cast<unsigned long long>(c.vis_deg),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&mb->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->n_f), static_cast<unsigned long long>(c.n_f),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->m_f), static_cast<unsigned long long>(c.m_f),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&mb->level, level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr int kBlock = 256;
 constexpr int kUnitThreads = kUnitWaves * kWave;  // 256: 4 waves x 16 words
 static_assert(kUnitThreads == 256 && kWaveWords <= kWave, "unit geometry");
@@ -96,6 +111,13 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   const word_t sbit = src >= 0 ? (1ull << (src & 63)) : 0ull;
   for (int64_t w = t0; w < a.gwords; w += stride) a.visited[w] = a.zdeg[w] | (w == sw ? sbit : 0ull);
   for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? sbit : 0ull;
+  if (a.frontier_clear)
+    for (int64_t w = t0; w < a.words; w += stride) a.frontier_clear[w] = 0ull;
+  // the seed's work-list entry: edge blocks [0, ceil(d / EPB)) all start in it
+  if (a.blk_vstart && src >= 0) {
+    const eid_t d = a.g.row_off[src + 1] - a.g.row_off[src];
+    for (int64_t b = t0; b * kTdEdgesPerBlock < d; b += stride) a.blk_vstart[b] = 0;
+  }
   if (t0 != 0) return;
   int64_t cnt = 0, deg = 0;
   if (src >= 0) {
@@ -113,21 +135,16 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   a.stats[0] = a.stats[2] = cnt;
   a.stats[1] = a.stats[3] = deg;
   a.qscan[cnt] = deg;
+  if (cnt && a.qbase) {
+    a.qscan[0] = 0;
+    a.qbase[0] = a.g.row_off[src];
+    a.qv[0] = static_cast<vid_t>(src);
+  }
   if (a.ctrl) {
     LevelCtrl c = a.ctrl_init;
     level_ctrl_finish(c, cnt, deg, true, nullptr);
     *a.ctrl = c;
-    if (a.mailbox) {
-      __hip_atomic_store(&a.mailbox->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
-                         static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->n_f), static_cast<unsigned long long>(c.n_f),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->m_f), static_cast<unsigned long long>(c.m_f),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.mailbox->level, -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (a.mailbox) stamp_mailbox(a.mailbox, c, -1);
   }
 }
 
@@ -365,18 +382,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
         a.rec[a.level].t1 = wall_clock64();
       }
       *a.ctrl = c;
-      if (a.mailbox) {
-        // host-mapped pinned slot: system-scope stores, level last
-        __hip_atomic_store(&a.mailbox->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->vis_deg),
-                           static_cast<unsigned long long>(c.vis_deg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.mailbox->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->n_f),
-                           static_cast<unsigned long long>(c.n_f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(&a.mailbox->m_f),
-                           static_cast<unsigned long long>(c.m_f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.mailbox->level, a.level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
     }
   }
 }
@@ -396,6 +402,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   const int64_t w0 = unit * kUnitWords;
   const word_t mine = (w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
   if (!__ballot(mine != 0)) return;
+  if (a.clear && mine) a.clear[w0 + lane] = 0ull;  // read once: the next sparse level writes here
   const eid_t* __restrict__ ro = a.g.row_off;
   long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
   long long off = a.unit_deg_off[unit] + a.part_deg[unit / kScanChunk];
@@ -420,6 +427,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
       const long long qs = off + incl - d;
       a.qscan[p] = qs;
       a.qbase[p] = rs - qs;
+      if (a.qv) a.qv[p] = static_cast<vid_t>(w0 * 64 + vpos);
       for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
         a.blk_vstart[blk] = static_cast<int32_t>(p);
     }
@@ -437,6 +445,60 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
 // atomicOr only if neither `visited` nor the (possibly stale, only-growing)
 // `next` word already has its bit.
 enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->bytes
+
+// Work-list owner map of edge block b (edges [b*EPB, min(m, (b+1)*EPB))):
+// the entries covering the block are [blk_vstart[b], blk_vstart[b+1]]; their
+// start positions are scattered into s_owner and max-scanned, so s_owner[i]
+// is the block-local entry of edge i and s_base[entry] its qbase (col index =
+// edge + qbase).  Returns the block's edge count; ends with a barrier.
+template <int kThreads>
+__device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qscan, const int64_t* __restrict__ qbase,
+                                                  const int32_t* __restrict__ blk_vstart, long long b,
+                                                  long long nblocks, long long q, long long m, int32_t* s_owner,
+                                                  long long* s_base, int32_t* s_wmax) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = t >> 6;
+  const long long e0 = b * kTdEdgesPerBlock;
+  const long long e1 = min(m, e0 + kTdEdgesPerBlock);
+  const int cnt = static_cast<int>(e1 - e0);
+  const long long v0 = blk_vstart[b];
+  const long long vlast = (b + 1 < nblocks) ? blk_vstart[b + 1] : q - 1;
+  const int nv = static_cast<int>(vlast - v0 + 1);
+
+  __syncthreads();  // LDS reuse across iterations
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
+  __syncthreads();
+  // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
+  for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
+    const long long qs = qscan[v0 + i];
+    s_base[i] = qbase[v0 + i];
+    const long long p = (qs > e0 ? qs : e0) - e0;
+    if (p < cnt) s_owner[p] = i;
+  }
+  __syncthreads();
+  // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
+  int vals[kItems];
+  int run = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    run = max(run, s_owner[t * kItems + k]);
+    vals[k] = run;
+  }
+  const int incl = wave_incl_max(run);
+  if (lane == kWave - 1) s_wmax[wv] = incl;
+  __syncthreads();
+  int carry = 0;
+  for (int k = 0; k < wv; ++k) carry = max(carry, s_wmax[k]);
+  const int prev = __shfl_up(incl, 1, kWave);
+  const int excl = lane > 0 ? max(carry, prev) : carry;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
+  __syncthreads();
+  return cnt;
+}
 
 // kThreads: 256 (8 edges per thread) for big levels; 1024 (2 per thread) when
 // the grid is too small to fill the chip -- 4x the waves in flight to cover the
@@ -456,52 +518,22 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     check = a.ctrl->check_visited != 0;
     q = a.dev_stats[0];
     m = a.dev_stats[1];
+    if (a.clear_qv) stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
+    if (a.clear_qv)
+      for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < q;
+           i += static_cast<int64_t>(gridDim.x) * kThreads)
+        a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const int t = threadIdx.x;
   const int lane = lane_id();
-  const int wv = t >> 6;
   const vid_t* __restrict__ col = a.g.col;
   const word_t* __restrict__ visited = a.visited;
 
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
     const long long e0 = b * kTdEdgesPerBlock;
-    const long long e1 = min(m, e0 + kTdEdgesPerBlock);
-    const int cnt = static_cast<int>(e1 - e0);
-    const long long v0 = a.blk_vstart[b];
-    const long long vlast = (b + 1 < nblocks) ? a.blk_vstart[b + 1] : q - 1;
-    const int nv = static_cast<int>(vlast - v0 + 1);
-
-    __syncthreads();  // LDS reuse across iterations
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
-    __syncthreads();
-    // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
-    for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
-      const long long qs = a.qscan[v0 + i];
-      s_base[i] = a.qbase[v0 + i];
-      const long long p = (qs > e0 ? qs : e0) - e0;
-      if (p < cnt) s_owner[p] = i;
-    }
-    __syncthreads();
-    // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
-    int vals[kItems];
-    int run = 0;
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      run = max(run, s_owner[t * kItems + k]);
-      vals[k] = run;
-    }
-    const int incl = wave_incl_max(run);
-    if (lane == kWave - 1) s_wmax[wv] = incl;
-    __syncthreads();
-    int carry = 0;
-    for (int k = 0; k < wv; ++k) carry = max(carry, s_wmax[k]);
-    const int prev = __shfl_up(incl, 1, kWave);
-    const int excl = lane > 0 ? max(carry, prev) : carry;
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
-    __syncthreads();
+    const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
+                                                 s_wmax);
 
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
@@ -543,6 +575,139 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       }
     }
   }
+}
+
+// Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
+// claimed vertex is finished in place (level, frontier bit, output entry), so
+// the level is one launch.  kThreads = 256: 8 edges per thread per block.
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
+  __shared__ int32_t s_owner[kTdEdgesPerBlock];
+  __shared__ long long s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_wmax[kThreads / kWave];
+  __shared__ int s_last;
+  // uniform: the whole grid returns, no workgroup takes a ticket
+  if (a.ctrl->done || a.ctrl->dir != 'T') return;
+  stamp_level_start(a.ctrl);
+  const long long q = a.dev_stats[0], m = a.dev_stats[1];
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
+  const int64_t gstride = static_cast<int64_t>(gridDim.x) * kThreads;
+  // the input vertices' frontier bits (the bitmap is not read here)
+  for (int64_t i = gtid; i < q; i += gstride) a.frontier_in[a.qv[i] >> 6] = 0ull;
+
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  const vid_t* __restrict__ col = a.g.col;
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const int64_t lo = a.g.lo;
+  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
+                                                 s_wmax);
+    // (A) all items' claims in flight together: col, visited, fetch-or
+    vid_t v[kItems];
+    word_t seen[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kThreads + t;
+      v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) seen[k] = k * kThreads + t < cnt ? a.visited[v[k] >> 6] : ~0ull;
+    unsigned claimed = 0;  // bit k: item k claimed by this lane
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const word_t bit = 1ull << (v[k] & 63);
+      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+    }
+    if (!__ballot(claimed != 0)) continue;
+    // (B) finish the wave's claimed vertices: level, degree, frontier bit,
+    // then one packed append for all of them
+    eid_t rs[kItems], re[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      rs[k] = re[k] = 0;
+      if (claimed & (1u << k)) {
+        const int64_t r = static_cast<int64_t>(v[k]) - lo;
+        a.level[r] = a.new_level;
+        rs[k] = ro[r];
+        re[k] = ro[r + 1];
+      }
+    }
+    unsigned long long tm[kItems];
+    long long incl[kItems], cbase[kItems], ebase[kItems];
+    long long ctot = 0, etot = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const long long d = static_cast<long long>(re[k] - rs[k]);
+      const bool take = d > 0;  // claimed (else rs == re)
+      tm[k] = __ballot(take);
+      if (take) {
+        const int64_t r = static_cast<int64_t>(v[k]) - lo;
+        atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
+      }
+      incl[k] = wave_incl_scan(take ? d : 0ll);
+      cbase[k] = ctot;
+      ebase[k] = etot;
+      ctot += __popcll(tm[k]);
+      etot += readlane_i64(incl[k], kWave - 1);
+    }
+    if (!ctot) continue;
+    unsigned long long old = 0;
+    if (lane == 0)
+      old = atomicAdd(a.counter, (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
+                                     static_cast<unsigned long long>(etot));
+    old = __shfl(old, 0, kWave);
+    const long long p0 = static_cast<long long>(old >> kSparseEdgeBits);
+    const long long q0 = static_cast<long long>(old & kEdgeMask);
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const long long d = static_cast<long long>(re[k] - rs[k]);
+      if (d > 0) {
+        const long long p = p0 + cbase[k] + mask_rank(tm[k]);
+        const long long qs = q0 + ebase[k] + incl[k] - d;
+        a.oscan[p] = qs;
+        a.obase[p] = rs[k] - qs;
+        a.oqv[p] = static_cast<vid_t>(static_cast<int64_t>(v[k]) - lo);
+        for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
+          a.oblk[blk] = static_cast<int32_t>(p);
+      }
+    }
+  }
+
+  // last workgroup: the level's totals and decision (as scan_units_kernel)
+  __syncthreads();
+  if (t == 0) {
+    // every wave's counter atomic has returned; hand-off as in scan_units_kernel
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = (prev == gridDim.x - 1) ? 1 : 0;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last || t != 0) return;
+  const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long cnt = static_cast<long long>(tot >> kSparseEdgeBits);
+  const long long deg = static_cast<long long>(tot & kEdgeMask);
+  *a.counter = 0ull;
+  *a.ticket = 0u;
+  a.stats[0] = a.stats[2] = cnt;
+  a.stats[1] = a.stats[3] = deg;
+  a.oscan[cnt] = deg;
+  LevelCtrl c = *a.ctrl;
+  level_ctrl_finish(c, cnt, deg, false, a.rec + a.level_index);
+  a.rec[a.level_index].t0 = c.t_start;
+  a.rec[a.level_index].t1 = wall_clock64();
+  *a.ctrl = c;
+  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
 }
 
 // Received owner lists -> candidate bits of the owned slice.
@@ -1097,6 +1262,10 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   else
     DBFS_TD_LAUNCH(TdOut::Bits);
 #undef DBFS_TD_LAUNCH
+}
+
+void td_sparse(const TdSparseArgs& a, hipStream_t st) {
+  td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
 }
 
 void list_scatter(const ListScatterArgs& a, hipStream_t st) {

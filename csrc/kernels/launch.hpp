@@ -19,6 +19,7 @@ void scan_units(const ScanArgs& a, hipStream_t st);
 void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
+void td_sparse(const TdSparseArgs& a, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
 void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
@@ -58,6 +59,7 @@ void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_ve
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
+void degree_square_sum(const ShardView& g, int64_t* out1, hipStream_t st);
 
 }  // namespace kern
 }  // namespace dbfs

@@ -286,3 +286,35 @@ def test_host_loop_stats_mailbox(mailbox):
             assert np.array_equal(lv, _oracle(csr, s))
             assert levels and all(0.0 <= l["comm_ms"] <= l["ms"] + 1e-6 for l in levels)
             assert any(l["comm_ms"] > 0 for l in levels)
+
+
+def _mixed_graph(n=20000, seed=7):
+    """Hub + long path + random blob: sparse, dense and bottom-up levels in one
+    traversal from vertex 0 (degree 3000 > one 2048-edge block)."""
+    rng = np.random.default_rng(seed)
+    u = [np.zeros(3000, np.int64), np.arange(3000, 6000), rng.integers(6000, n, 40000)]
+    v = [np.arange(1, 3001), np.arange(3001, 6001), rng.integers(6000, n, 40000)]
+    return n, np.concatenate(u), np.concatenate(v)
+
+
+@pytest.mark.parametrize("predict", [1, 0])
+@pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("sparse_edges", [0, 1, 64, 4096, 1 << 40])
+def test_sparse_top_down_levels(rt, mode, predict, sparse_edges):
+    # sparse top-down levels (one kernel: direct claims, work list handed to
+    # the next level) mixed with dense and bottom-up levels in any order: the
+    # levels and per-level records equal the host loop's
+    n, u, v = _mixed_graph()
+    g = dbfs.build_csr(n, u, v)
+    dev = dbfs.BFS(g, rt, mode=mode)
+    dev.engine.set_option("device_loop_predict", predict)
+    dev.engine.set_option("td_sparse_edges", sparse_edges)
+    host = dbfs.BFS(g, rt, mode=mode)
+    host.engine.set_option("device_loop", 0)
+    for src in (0, 2999, 4500, 12345):
+        a, b = dev.run(src), host.run(src)
+        assert np.array_equal(dev.levels(), dbfs.cpu_bfs(g, src)[0])
+        strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+        assert strip(a) == strip(b)
+        assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+    assert dev.validate(12345)

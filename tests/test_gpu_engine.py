@@ -366,3 +366,34 @@ def test_multiprocess_ranks_share_one_gpu_tcp():
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["validated"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("sparse_edges", [0, 64, 1 << 16, 1 << 40])
+def test_sparse_top_down_levels_gpu(gpu_runtime, mode, sparse_edges):
+    """Sparse top-down levels (td_sparse_kernel: fetch-or claims, wave-
+    aggregated packed append, last-workgroup level decision) interleaved with
+    dense and bottom-up levels: hub root (> one edge block), 3000-level path,
+    random blob; and RMAT-16 roots.  Same levels and records as the host loop."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_engine_cpu import _mixed_graph
+    n, u, v = _mixed_graph()
+    graphs = [(dbfs.build_csr(n, u, v), [0, 2999, 4500, 12345])]
+    p = dbfs.rmat_params(16, 16, 47)
+    csr = dbfs.host_csr_from_params(p)
+    graphs.append((p, None))
+    for g, roots in graphs:
+        dev = dbfs.BFS(g, gpu_runtime, mode=mode)
+        dev.engine.set_option("td_sparse_edges", sparse_edges)
+        host = dbfs.BFS(g, gpu_runtime, mode=mode)
+        host.engine.set_option("device_loop", 0)
+        ref = g if roots is not None else csr
+        for src in roots or dev.sample_roots(4, seed=9):
+            a, b = dev.run(src), host.run(src)
+            assert np.array_equal(dev.levels(), dbfs.cpu_bfs(ref, src)[0])
+            strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+            assert strip(a) == strip(b)
+            assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+            assert all(l["ms"] > 0 for l in a.levels)

@@ -19,5 +19,5 @@ for v in "${VS[@]}"; do
   fi
   timeout -k 10 240 python bench.py --scale $SCALE --steps $STEPS --warmup 3 --no-validate "${args[@]}" ${BENCH_ARGS} \
     > gpurun_out/ab_run.json 2> gpurun_out/ab_run.err || { echo "variant $v failed"; tail -20 gpurun_out/ab_run.err; exit 1; }
-  python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_run.json').read().strip().splitlines()[-1]); print('%-40s %8.1f GTEPS %7.3f ms/step hm %7.1f' % (sys.argv[1], d['value'], d['ms_per_step'], d['harmonic_mean_gteps']))" "$v" | tee -a gpurun_out/ab.txt
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_run.json').read().strip().splitlines()[-1]); print('%-40s %8.1f GTEPS %7.3f ms/step hm %7.1f clock %s' % (sys.argv[1], d['value'], d['ms_per_step'], d['harmonic_mean_gteps'], [(l[0], round(l[1] * 1e3, 1)) for l in d.get('level_clock', {}).get('levels', [])]))" "$v" | tee -a gpurun_out/ab.txt
 done
