@@ -15,6 +15,12 @@
 namespace dbfs {
 namespace {
 
+// Level of a new vertex in the wide or the narrow array (HIP: store_level).
+inline void put_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level) {
+  if (narrow) narrow[i] = level <= kNarrowMaxLevel ? static_cast<uint8_t>(level) : kNarrowUnreached;
+  else wide[i] = level;
+}
+
 inline bool test_bit(const word_t* bm, uint64_t v) { return (bm[v >> 6] >> (v & 63)) & 1ull; }
 inline word_t gather_bytes(uint8_t* p) {
   word_t bits = 0;
@@ -80,7 +86,7 @@ class CpuBackend final : public Backend {
           const int b = __builtin_ctzll(x);
           x &= x - 1;
           const int64_t v = w * 64 + b;
-          a.level[v] = a.new_level;
+          put_level(a.level, a.level8, v, a.new_level);
           const eid_t d = a.g.row_off[v + 1] - a.g.row_off[v];
           if (d > 0) { ++cnt; deg += d; }
         }
@@ -93,7 +99,10 @@ class CpuBackend final : public Backend {
   void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override { *c = init; }
   void init_run(const InitRunArgs& a) override {
     const int64_t src = a.src_local;
-    for (int64_t i = 0; i < a.g.rows; ++i) a.level[i] = i == src ? 0 : kUnreached;
+    for (int64_t i = 0; i < a.g.rows; ++i) {
+      if (a.level8) a.level8[i] = i == src ? 0 : kNarrowUnreached;
+      else a.level[i] = i == src ? 0 : kUnreached;
+    }
     for (int64_t w = 0; w < a.gwords; ++w) a.visited[w] = a.zdeg[w];
     for (int64_t w = 0; w < a.words; ++w) a.frontier[w] = 0;
     int64_t cnt = 0, deg = 0;
@@ -254,7 +263,7 @@ class CpuBackend final : public Backend {
         if (test_bit(a.visited, v)) continue;
         a.visited[v >> 6] |= 1ull << (v & 63);
         const int64_t r = static_cast<int64_t>(v) - a.g.lo;
-        a.level[r] = a.new_level;
+        put_level(a.level, a.level8, r, a.new_level);
         const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
         if (d <= 0) continue;
         a.frontier_out[r >> 6] |= 1ull << (r & 63);
@@ -309,7 +318,7 @@ class CpuBackend final : public Backend {
           for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
             if (test_bit(a.frontier, a.g.col[e])) {
               out |= 1ull << b;
-              a.level[v] = a.new_level;
+              put_level(a.level, a.level8, v, a.new_level);
               ++cnt;
               deg += a.g.row_off[v + 1] - a.g.row_off[v];
               break;
@@ -544,6 +553,9 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) override {
+    for (int64_t i = 0; i < n; ++i) out[i] = in[i] == kNarrowUnreached ? kUnreached : static_cast<lvl_t>(in[i]);
+  }
   void degree_square_sum(const ShardView& g, int64_t* out1) override {
     int64_t s = 0;
     for (int64_t r = 0; r < g.rows; ++r) {

@@ -66,6 +66,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
   else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
+  else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else throw Error("unknown engine option '" + name + "'");
@@ -90,6 +91,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
+          {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0}};
@@ -443,8 +445,21 @@ RunResult Engine::run(int64_t source) {
              "directed graphs need a top-down mode (bottom-up searches in-edges)");
   RunResult r;
   const bool ref = opt_.mode == Mode::Ref || opt_.mode == Mode::Scan;
+  run_narrow_ = !ref && use_narrow();
+  if (run_narrow_ && level8_.size() == 0) level8_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
+  levels_narrow_ = run_narrow_;
+  if (run_narrow_ && r.depth - 1 > kNarrowMaxLevel) {
+    // deeper than the narrow levels hold (identical decision on every rank):
+    // rerun with 32-bit levels; the reported time includes both traversals
+    narrow_failed_ = true;
+    run_narrow_ = levels_narrow_ = false;
+    const double first_ms = r.ms;
+    r = use_device_loop() ? run_bitmap_device(source) : run_bitmap(source);
+    r.ms += first_ms;
+  }
   if (ref || opt_.directed) {
+    ensure_wide_levels();
     // Traversed-edge accounting outside the timed region (the bitmap engine
     // otherwise knows sum(deg) of every level's new vertices): Graph500's
     // undirected convention, or all out-edges of reached vertices (directed).
@@ -458,6 +473,18 @@ RunResult Engine::run(int64_t source) {
   }
   r.gteps = r.ms > 0 ? static_cast<double>(r.edges) / (r.ms * 1e6) : 0.0;
   return r;
+}
+
+bool Engine::use_narrow() const {
+  return opt_.narrow_levels && !narrow_failed_ &&
+         (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
+}
+
+// The last run's levels into level_ (32-bit) if it kept them narrow.
+void Engine::ensure_wide_levels() const {
+  if (!levels_narrow_) return;
+  be_.widen_levels(level8_.data(), level_.data(), g_.rows());
+  levels_narrow_ = false;
 }
 
 // Scratch bitmaps every consumer leaves zeroed (`next` bits cleared by the
@@ -479,6 +506,7 @@ InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* 
   InitRunArgs ia;
   ia.g = g_.view();
   ia.level = level_.data();
+  ia.level8 = run_narrow_ ? level8_.data() : nullptr;
   ia.zdeg = zdeg_.data();
   ia.visited = visited_.data();
   ia.gwords = part_.global_words();
@@ -577,6 +605,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     ua.visited = vis_own;
     ua.frontier = fr_nxt_own();
     ua.level = level_.data();
+    ua.level8 = run_narrow_ ? level8_.data() : nullptr;
     ua.new_level = new_level;
     ua.words = W;
     ua.unit_cnt = unit_cnt_.data();
@@ -735,6 +764,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.frontier = fr_cur();
       ba.new_frontier = fr_nxt_own();
       ba.level = level_.data();
+      ba.level8 = run_narrow_ ? level8_.data() : nullptr;
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
@@ -925,6 +955,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   ua.clear_cand = true;
   ua.visited = visited_.data();
   ua.level = level_.data();
+  ua.level8 = run_narrow_ ? level8_.data() : nullptr;
   ua.words = W;
   ua.unit_cnt = unit_cnt_.data();
   ua.unit_deg = unit_deg_.data();
@@ -1006,6 +1037,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.frontier_out = frontier_[cur ^ 1].data();
       sp.visited = visited_.data();
       sp.level = level_.data();
+      sp.level8 = run_narrow_ ? level8_.data() : nullptr;
       sp.new_level = L + 1;
       sp.oscan = qscan_set(L + 1);
       sp.obase = qbase_set(L + 1);
@@ -1055,6 +1087,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.frontier = frontier_[cur].data();
       ba.new_frontier = frontier_[cur ^ 1].data();
       ba.level = level_.data();
+      ba.level8 = run_narrow_ ? level8_.data() : nullptr;
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
@@ -1309,12 +1342,14 @@ RunResult Engine::run_ref(int64_t source) {
 }
 
 std::vector<lvl_t> Engine::levels_local() const {
+  ensure_wide_levels();
   std::vector<lvl_t> h(static_cast<size_t>(g_.rows()));
   if (!h.empty()) be_.to_host(h.data(), level_.data(), h.size() * sizeof(lvl_t));
   return h;
 }
 
 std::vector<lvl_t> Engine::gather_levels() {
+  ensure_wide_levels();
   const int P = part_.nranks;
   const int64_t part = part_.part;
   DBuf<lvl_t> send(be_, static_cast<size_t>(part)), recv(be_, static_cast<size_t>(P * part));
@@ -1328,6 +1363,7 @@ std::vector<lvl_t> Engine::gather_levels() {
 }
 
 void Engine::gather_levels_device(DBuf<lvl_t>& full) {
+  ensure_wide_levels();
   const int P = part_.nranks;
   const int64_t part = part_.part;
   DBuf<lvl_t> send(be_, static_cast<size_t>(part));

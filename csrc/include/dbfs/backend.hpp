@@ -61,6 +61,9 @@ struct ShardView {
 // every bottom-up workgroup (two 1024-thread workgroups per CU fit in 160 KiB).
 constexpr int64_t kMaxHubs = int64_t(1) << 19;
 constexpr vid_t kHubFlag = 0x80000000u;
+// Narrow (8-bit) level arrays: 0xFF = unreached, levels 0 .. 254.
+constexpr uint8_t kNarrowUnreached = 0xFF;
+constexpr int kNarrowMaxLevel = 254;
 
 // Frontier bookkeeping is organised in "units" of 64 bitmap words (4096
 // vertices): one 256-thread workgroup (4 waves) per unit, 16 consecutive words
@@ -160,6 +163,10 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
 struct InitRunArgs {
   ShardView g;
   lvl_t* level = nullptr;          // rows
+  // Narrow level array (one byte per vertex, kNarrowUnreached = not reached;
+  // levels up to kNarrowMaxLevel): written instead of `level` when set, here
+  // and by every bitmap-engine kernel that writes levels.
+  uint8_t* level8 = nullptr;
   const word_t* zdeg = nullptr;    // global
   word_t* visited = nullptr;       // global
   int64_t gwords = 0;
@@ -203,6 +210,7 @@ struct UpdateArgs {
   word_t* visited = nullptr;     // owned slice of the global visited bitmap
   word_t* frontier = nullptr;    // owned slice of the NEXT global frontier bitmap
   lvl_t* level = nullptr;        // rows
+  uint8_t* level8 = nullptr;     // narrow levels (see InitRunArgs)
   lvl_t new_level = 0;
   int64_t words = 0;             // words of the owned slice
   int64_t* unit_cnt = nullptr;   // nunits
@@ -291,6 +299,7 @@ struct TdSparseArgs {
   word_t* frontier_out = nullptr;      // owned slice, zero on entry
   word_t* visited = nullptr;           // global
   lvl_t* level = nullptr;              // rows
+  uint8_t* level8 = nullptr;           // narrow levels (see InitRunArgs)
   int32_t new_level = 0;
   int64_t* oscan = nullptr;
   int64_t* obase = nullptr;
@@ -373,6 +382,7 @@ struct BuArgs {
   const word_t* frontier = nullptr;  // current frontier, global
   word_t* new_frontier = nullptr;    // owned slice of the next frontier (fully overwritten)
   lvl_t* level = nullptr;
+  uint8_t* level8 = nullptr;         // narrow levels (see InitRunArgs)
   lvl_t new_level = 0;
   int64_t words = 0;
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
@@ -598,6 +608,8 @@ class Backend {
   virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
   // sum over the shard's rows of degree^2 (device scalar out)
   virtual void degree_square_sum(const ShardView& g, int64_t* out1) = 0;
+  // out[i] = in[i] (narrow levels; kNarrowUnreached -> kUnreached)
+  virtual void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) = 0;
 
  protected:
   std::function<void(double)> wait_watch_;

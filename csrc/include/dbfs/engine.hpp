@@ -124,6 +124,11 @@ struct EngineOptions {
   // 0 disables.  td_sparse_grid: its workgroups.
   int64_t td_sparse_edges = int64_t(1) << 16;
   int64_t td_sparse_grid = 256;
+  // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
+  // during the traversal (a quarter of the per-run initialisation traffic),
+  // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
+  // rerun with 32-bit levels (and later runs keep them).
+  bool narrow_levels = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -215,6 +220,12 @@ class Engine {
   int64_t total_directed_ = 0;
 
   DBuf<lvl_t> level_;
+  DBuf<uint8_t> level8_;
+  bool narrow_failed_ = false;        // a traversal overflowed the narrow levels
+  bool run_narrow_ = false;           // the current run writes level8_
+  mutable bool levels_narrow_ = false;  // level_ is stale: level8_ holds the last run's levels
+  bool use_narrow() const;
+  void ensure_wide_levels() const;
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_;

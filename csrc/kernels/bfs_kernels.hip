@@ -59,6 +59,16 @@ __device__ __forceinline__ void stamp_mailbox(LevelMailbox* mb, const LevelCtrl&
   __hip_atomic_store(&mb->level, level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A new vertex's level: the narrow array when the run uses one (uniform
+// branch), else the 32-bit array.  Narrow overflow (level > kNarrowMaxLevel)
+// stores kNarrowUnreached; the engine reruns such a traversal with wide levels.
+__device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level) {
+  if (narrow)
+    narrow[i] = level <= kNarrowMaxLevel ? static_cast<uint8_t>(level) : kNarrowUnreached;
+  else
+    wide[i] = level;
+}
+
 constexpr int kBlock = 256;
 constexpr int kUnitThreads = kUnitWaves * kWave;  // 256: 4 waves x 16 words
 static_assert(kUnitThreads == 256 && kWaveWords <= kWave, "unit geometry");
@@ -93,20 +103,39 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const int64_t rows = a.g.rows;
   const int64_t src = a.src_local;
-  // level: rows / 4 int4 stores (+ tail)
-  const int64_t n4 = (reinterpret_cast<uintptr_t>(a.level) & 15u) == 0 ? rows / 4 : 0;
-  int4* l4 = reinterpret_cast<int4*>(a.level);
-  for (int64_t i = t0; i < n4; i += stride) {
-    int4 v = make_int4(kUnreached, kUnreached, kUnreached, kUnreached);
-    if (src >= 0 && (src >> 2) == i) {
-      if ((src & 3) == 0) v.x = 0;
-      else if ((src & 3) == 1) v.y = 0;
-      else if ((src & 3) == 2) v.z = 0;
-      else v.w = 0;
+  if (a.level8) {
+    // narrow levels: rows / 16 uint4 stores of 0xFF (+ tail), the source's byte after
+    const int64_t n16 = (reinterpret_cast<uintptr_t>(a.level8) & 15u) == 0 ? rows / 16 : 0;
+    uint4* l16 = reinterpret_cast<uint4*>(a.level8);
+    for (int64_t i = t0; i < n16; i += stride) {
+      uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
+      if (src >= 0 && (src >> 4) == i) {
+        const unsigned clear = ~(0xFFu << (8 * (src & 3)));
+        const int word = static_cast<int>((src >> 2) & 3);
+        if (word == 0) v.x &= clear;
+        else if (word == 1) v.y &= clear;
+        else if (word == 2) v.z &= clear;
+        else v.w &= clear;
+      }
+      l16[i] = v;
     }
-    l4[i] = v;
+    for (int64_t i = n16 * 16 + t0; i < rows; i += stride) a.level8[i] = i == src ? 0 : kNarrowUnreached;
+  } else {
+    // level: rows / 4 int4 stores (+ tail)
+    const int64_t n4 = (reinterpret_cast<uintptr_t>(a.level) & 15u) == 0 ? rows / 4 : 0;
+    int4* l4 = reinterpret_cast<int4*>(a.level);
+    for (int64_t i = t0; i < n4; i += stride) {
+      int4 v = make_int4(kUnreached, kUnreached, kUnreached, kUnreached);
+      if (src >= 0 && (src >> 2) == i) {
+        if ((src & 3) == 0) v.x = 0;
+        else if ((src & 3) == 1) v.y = 0;
+        else if ((src & 3) == 2) v.z = 0;
+        else v.w = 0;
+      }
+      l4[i] = v;
+    }
+    for (int64_t i = n4 * 4 + t0; i < rows; i += stride) a.level[i] = i == src ? 0 : kUnreached;
   }
-  for (int64_t i = n4 * 4 + t0; i < rows; i += stride) a.level[i] = i == src ? 0 : kUnreached;
   const int64_t sw = src >= 0 ? a.vis_word_base + (src >> 6) : -1;
   const word_t sbit = src >= 0 ? (1ull << (src & 63)) : 0ull;
   for (int64_t w = t0; w < a.gwords; w += stride) a.visited[w] = a.zdeg[w] | (w == sw ? sbit : 0ull);
@@ -268,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     const int pos = wave_set_position(nb, incl, idx);
     if (idx < total) {
       const int64_t v = w0 * 64 + pos;
-      a.level[v] = a.new_level;
+      store_level(a.level, a.level8, v, a.new_level);
       const eid_t d = ro[v + 1] - ro[v];
       if (d > 0) {
         cnt += 1;
@@ -632,7 +661,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       rs[k] = re[k] = 0;
       if (claimed & (1u << k)) {
         const int64_t r = static_cast<int64_t>(v[k]) - lo;
-        a.level[r] = a.new_level;
+        store_level(a.level, a.level8, r, a.new_level);
         rs[k] = ro[r];
         re[k] = ro[r + 1];
       }
@@ -708,6 +737,16 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   a.rec[a.level_index].t1 = wall_clock64();
   *a.ctrl = c;
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+}
+
+// Narrow levels -> 32-bit levels (outside the timed traversal, on demand).
+__global__ __launch_bounds__(kBlock) void widen_levels_kernel(const uint8_t* __restrict__ in, lvl_t* __restrict__ out,
+                                                              int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    const uint8_t v = in[i];
+    out[i] = v == kNarrowUnreached ? kUnreached : static_cast<lvl_t>(v);
+  }
 }
 
 // Received owner lists -> candidate bits of the owned slice.
@@ -920,7 +959,7 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
       found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
       res = __ballot(found);
       if (found) {
-        a.level[v] = a.new_level;
+        store_level(a.level, a.level8, v, a.new_level);
         cnt += 1;
         deg += e - rs;
       }
@@ -1038,7 +1077,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
     BU_STAT(7, __popcll(__ballot(found)));
     if (found) {
-      a.level[w0 * 64 + loc] = a.new_level;
+      store_level(a.level, a.level8, w0 * 64 + loc, a.new_level);
       cnt32 += 1;
       deg += e - rs;
       __hip_atomic_fetch_or(s_res + (loc >> 6), 1ull << (loc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -1266,6 +1305,11 @@ void td_expand(const TdArgs& a, hipStream_t st) {
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+}
+
+void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n);
 }
 
 void list_scatter(const ListScatterArgs& a, hipStream_t st) {

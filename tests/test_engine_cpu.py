@@ -318,3 +318,32 @@ def test_sparse_top_down_levels(rt, mode, predict, sparse_edges):
         assert strip(a) == strip(b)
         assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
     assert dev.validate(12345)
+
+
+@pytest.mark.parametrize("device_loop", [1, 0])
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_narrow_levels(rt, mode, device_loop):
+    # one-byte levels during the traversal, widened on read: same levels as
+    # the 32-bit array; a path deeper than 254 levels is rerun with 32-bit
+    # levels (reported time covers both runs) and later runs stay wide
+    p = dbfs.rmat_params(11, 16, 5)
+    csr = dbfs.host_csr_from_params(p)
+    narrow, wide = dbfs.BFS(p, rt, mode=mode), dbfs.BFS(p, rt, mode=mode)
+    wide.engine.set_option("narrow_levels", 0)
+    for b in (narrow, wide):
+        b.engine.set_option("device_loop", device_loop)
+    for src in narrow.sample_roots(3, seed=2):
+        a, b = narrow.run(src), wide.run(src)
+        assert np.array_equal(narrow.local_levels(), wide.local_levels())
+        assert np.array_equal(narrow.levels(), _oracle(csr, src))
+        assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+        assert narrow.validate(src)
+    n = 700
+    path = dbfs.build_csr(n, np.arange(n - 1), np.arange(1, n))
+    deep = dbfs.BFS(path, rt, mode=mode)
+    deep.engine.set_option("device_loop", device_loop)
+    for src in (0, 350):
+        r = deep.run(src)
+        exp = np.abs(np.arange(n) - src)
+        assert np.array_equal(deep.levels(), exp)
+        assert r.depth == exp.max() + 1 and r.reached == n

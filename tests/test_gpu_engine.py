@@ -397,3 +397,28 @@ def test_sparse_top_down_levels_gpu(gpu_runtime, mode, sparse_edges):
             assert strip(a) == strip(b)
             assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
             assert all(l["ms"] > 0 for l in a.levels)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_narrow_levels_gpu(gpu_runtime, mode):
+    """One-byte levels (init_run uint4 fill, store_level in update / bottom-up /
+    sparse kernels, widen_levels on read) equal the 32-bit path; a 700-level
+    path overflows them and is rerun with 32-bit levels."""
+    p = dbfs.rmat_params(16, 16, 13)
+    csr = dbfs.host_csr_from_params(p)
+    narrow, wide = dbfs.BFS(p, gpu_runtime, mode=mode), dbfs.BFS(p, gpu_runtime, mode=mode)
+    wide.engine.set_option("narrow_levels", 0)
+    for src in narrow.sample_roots(3, seed=4) + [17]:
+        a, b = narrow.run(src), wide.run(src)
+        assert np.array_equal(narrow.local_levels(), wide.local_levels())
+        assert np.array_equal(narrow.levels(), dbfs.cpu_bfs(csr, src)[0])
+        assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+        assert narrow.validate(src)
+    n = 700
+    path = dbfs.build_csr(n, np.arange(n - 1), np.arange(1, n))
+    deep = dbfs.BFS(path, gpu_runtime, mode=mode)
+    for src in (0, 350):
+        r = deep.run(src)
+        assert np.array_equal(deep.levels(), np.abs(np.arange(n) - src))
+        assert r.reached == n
