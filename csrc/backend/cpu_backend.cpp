@@ -65,7 +65,7 @@ class CpuBackend final : public Backend {
     bool use_bytes = a.cand_bytes != nullptr;
     if (a.ctrl) {
       if (a.ctrl->done || a.ctrl->dir != 'T') return;
-      use_bytes = a.ctrl->bytes != 0;
+      use_bytes = use_bytes && a.ctrl->bytes != 0;
     }
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
@@ -174,7 +174,7 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = c;
     a.stats[1] = a.stats[3] = d;
     a.qscan[c] = d;
-    if (a.ctrl) {
+    if (a.ctrl && a.finish) {
       level_ctrl_finish(*a.ctrl, c, d, a.seed, a.seed ? nullptr : a.rec + a.level);
       if (a.mailbox) {
         a.mailbox->done = a.ctrl->done;
@@ -252,6 +252,21 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void level_finish(const LevelFinishArgs& a) override {
+    if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+    LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
+    level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec + a.level);
+    *a.ctrl = c;
+    if (a.mailbox) {
+      a.mailbox->done = c.done;
+      a.mailbox->vis_deg = c.vis_deg;
+      a.mailbox->next_dir = c.dir;
+      a.mailbox->n_f = c.n_f;
+      a.mailbox->m_f = c.m_f;
+      a.mailbox->level = a.seed ? -1 : a.level;
+    }
+  }
+
   void td_sparse(const TdSparseArgs& a) override {
     if (a.ctrl->done || a.ctrl->dir != 'T') return;
     const int64_t q = a.dev_stats[0];
@@ -301,6 +316,7 @@ class CpuBackend final : public Backend {
   }
 
   void pack_bytes(const PackArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T' || !a.ctrl->bytes)) return;
     for (int64_t w = 0; w < a.words; ++w) a.next[w] |= gather_bytes(a.bytes + w * 64);
   }
 

@@ -59,6 +59,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
   else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
+  else if (name == "device_loop_ranks") o.device_loop_ranks = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "directed") o.directed = v != 0;
@@ -85,6 +86,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
           {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
+          {"device_loop_ranks", o.device_loop_ranks ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"bu_packed", o.bu_packed ? 1.0 : 0.0},
           {"directed", o.directed ? 1.0 : 0.0},
@@ -400,6 +402,12 @@ void Engine::alloc_bitmap_state() {
   unit_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(nunits_ + 1));
   part_cnt_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(nunits_, kScanChunk) + 1));
   part_deg_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(nunits_, kScanChunk) + 1));
+  // (never read before written by a scan, except by a compaction of an empty
+  // owned frontier, which ignores them: zeroed anyway)
+  be_.memset_async(unit_cnt_.data(), 0, unit_cnt_.bytes());
+  be_.memset_async(unit_deg_.data(), 0, unit_deg_.bytes());
+  be_.memset_async(part_cnt_.data(), 0, part_cnt_.bytes());
+  be_.memset_async(part_deg_.data(), 0, part_deg_.bytes());
   ticket_ = DBuf<unsigned>(be_, 4);
   be_.memset_async(ticket_.data(), 0, ticket_.bytes());
   qscan_ = DBuf<int64_t>(be_, static_cast<size_t>(g_.rows() + 1));
@@ -831,7 +839,7 @@ bool Engine::sparse_enabled() const {
 }
 
 bool Engine::use_device_loop() const {
-  return opt_.device_loop && !exchange() &&
+  return opt_.device_loop && (!exchange() || opt_.device_loop_ranks) &&
          (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
 }
 
@@ -847,7 +855,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   alloc_bitmap_state();
   TraceRange trace_run(std::string("bfs.run(device loop) mode=") + mode_name(opt_.mode) + " src=" +
                        std::to_string(source));
-  const int64_t W = part_.slice_words();
+  const int64_t W = part_.slice_words(), GW = part_.global_words();
+  const int me = comm_.rank();
+  // several ranks (or a forced exchange): every chain also carries its
+  // collectives -- enqueued blindly, the same sequence on every rank (the
+  // host decisions are functions of the all-reduced totals in the mailbox)
+  const bool xc = exchange();
+  auto fr_own = [&](int k) { return frontier_[k].data() + me * W; };
+  word_t* const vis_own = visited_.data() + me * W;
   const ShardView gv = g_.view();
   if (!ctrl_.data()) ctrl_ = DBuf<LevelCtrl>(be_, 1);
   if (rec_.size() < 64) rec_ = DBuf<LevelRecDev>(be_, 64);
@@ -861,7 +876,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
     be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
   }
-  const bool sparse = sparse_enabled();
+  const bool sparse = sparse_enabled() && !xc;
   if (sparse && !sparse_ready_) {
     const size_t rows = static_cast<size_t>(std::max<int64_t>(g_.rows(), 1));
     qscan2_ = DBuf<int64_t>(be_, rows + 1);
@@ -919,7 +934,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // totals, the seeded LevelCtrl and the mailbox stamp of level -1
   // (+ with sparse levels: the seed's work-list entry in set 0 and a clean
   // frontier_[0] for a sparse level 0 to write)
-  InitRunArgs ia = init_args(source, frontier_[1].data(), ctrl_.data(), init, mailbox_dev_ + slot(-1));
+  // (several ranks: the seed totals are all-reduced first, then level_finish
+  // seeds the LevelCtrl and stamps level -1)
+  InitRunArgs ia = init_args(source, fr_own(1), xc ? nullptr : ctrl_.data(), init,
+                             xc ? nullptr : mailbox_dev_ + slot(-1));
   if (sparse) {
     ia.qbase = qbase_.data();
     ia.blk_vstart = blk_vstart_.data();
@@ -927,6 +945,20 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     ia.frontier_clear = frontier_[0].data();
   }
   be_.init_run(ia);
+  auto finish_ranks = [&](int level, bool seed, char expect_dir) {
+    comm_.allreduce_sum_i64(stats_.data() + 2, 2);
+    LevelFinishArgs fa;
+    fa.stats = stats_.data();
+    fa.ctrl = ctrl_.data();
+    fa.ctrl_init = init;
+    fa.rec = rec_.data();
+    fa.mailbox = mailbox_dev_ + slot(level);
+    fa.level = level;
+    fa.seed = seed;
+    fa.expect_dir = expect_dir;
+    be_.level_finish(fa);
+  };
+  if (xc) finish_ranks(-1, true, 0);
 
   auto scan = [&](int level, bool seed, char expect_dir) {
     ScanArgs sa;
@@ -944,16 +976,18 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.level = level;
     sa.seed = seed;
     sa.expect_dir = expect_dir;
+    sa.finish = !xc;
     be_.scan_units(sa);
+    if (xc) finish_ranks(level, seed, expect_dir);
   };
   // Frontier double buffer: the seed is frontier_[1]; level L reads
   // frontier_[(L + 1) & 1] and writes the other one.
   UpdateArgs ua;
   ua.g = gv;
-  ua.nchunks = 1;
+  ua.nchunks = xc ? part_.nranks : 1;
   ua.cand_stride = W;
-  ua.clear_cand = true;
-  ua.visited = visited_.data();
+  ua.clear_cand = !xc;
+  ua.visited = vis_own;
   ua.level = level_.data();
   ua.level8 = run_narrow_ ? level8_.data() : nullptr;
   ua.words = W;
@@ -1001,13 +1035,22 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    // several ranks: the level's input frontier to every rank (all-gather of
+    // the owned slices) and into the replicated visited bitmap -- before a
+    // bottom-up level, and before top-down levels of the td mode (fewer
+    // candidates); not predicated: on a no-op chain it only refreshes bits
+    // every owner already has
+    if (xc && (d == 'B' || opt_.mode != Mode::DirOpt)) {
+      comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
+      be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
+    }
     // the frontier bitmap -> work list (set L & 1); with sparse levels also
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
     // writes into it)
     auto compact = [&] {
       CompactArgs ca;
       ca.g = gv;
-      ca.frontier = frontier_[cur].data();
+      ca.frontier = fr_own(cur);
       ca.words = W;
       ca.unit_cnt_off = unit_cnt_.data();
       ca.unit_deg_off = unit_deg_.data();
@@ -1075,17 +1118,33 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       UpdateArgs tu = ua;
       tu.cand = next_.data();
       tu.cand_bytes = next_bytes_.data();
+      if (xc) {
+        // candidates to their owners: the byte map (if this level used it)
+        // packed into `next`, one bitmap slice per peer, `next` re-zeroed
+        if (next_bytes_.data()) {
+          PackArgs pa;
+          pa.bytes = next_bytes_.data();
+          pa.next = next_.data();
+          pa.words = GW;
+          pa.ctrl = ctrl_.data();
+          be_.pack_bytes(pa);
+        }
+        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
+        be_.memset_async(next_.data(), 0, next_.bytes());
+        tu.cand = recv_.data();
+        tu.cand_bytes = nullptr;
+      }
       tu.force = false;
-      tu.frontier = frontier_[cur ^ 1].data();
+      tu.frontier = fr_own(cur ^ 1);
       tu.new_level = L + 1;
       tu.ctrl = ctrl_.data();
       be_.update_frontier(tu);
     } else {
       BuArgs ba;
       ba.g = gv;
-      ba.visited = visited_.data();
+      ba.visited = vis_own;
       ba.frontier = frontier_[cur].data();
-      ba.new_frontier = frontier_[cur ^ 1].data();
+      ba.new_frontier = fr_own(cur ^ 1);
       ba.level = level_.data();
       ba.level8 = run_narrow_ ? level8_.data() : nullptr;
       ba.new_level = L + 1;
@@ -1182,6 +1241,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   const auto t1 = std::chrono::steady_clock::now();
   scratch_dirty_ = false;
   res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  if (xc) res.ms = comm_.max_host(res.ms);
   if (host_timing) {
     hmark("synchronized");
     std::string line = "[host timing]";

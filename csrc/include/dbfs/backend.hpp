@@ -244,6 +244,23 @@ struct ScanArgs {
   // Device loop: the level's chain was enqueued for this direction (0: any);
   // when ctrl->dir differs, the chain was a no-op and so is the scan.
   int32_t expect_dir = 0;
+  // Device loop: run level_ctrl_finish here (one rank); several ranks reduce
+  // the totals first and finish in level_finish.
+  bool finish = true;
+};
+
+// Device loop, several ranks: after the totals' all-reduce (stats[2..3] =
+// global count / degree sum), one thread runs level_ctrl_finish (seed: from
+// ctrl_init) and stamps rec / the mailbox, as the one-rank scan does.
+struct LevelFinishArgs {
+  const int64_t* stats = nullptr;
+  LevelCtrl* ctrl = nullptr;
+  LevelCtrl ctrl_init;
+  LevelRecDev* rec = nullptr;
+  LevelMailbox* mailbox = nullptr;
+  int32_t level = 0;
+  bool seed = false;
+  int32_t expect_dir = 0;
 };
 
 // Host-loop statistics mailbox (pinned, device-mapped).  After a level's
@@ -367,6 +384,8 @@ struct PackArgs {
   uint8_t* bytes = nullptr;
   word_t* next = nullptr;
   int64_t words = 0;
+  // device loop: runs only on a byte-map top-down level (ctrl->bytes)
+  const LevelCtrl* ctrl = nullptr;
 };
 
 // Bottom-up step fused with the frontier update: for every owned unvisited v,
@@ -559,6 +578,7 @@ class Backend {
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_sparse(const TdSparseArgs& a) = 0;
+  virtual void level_finish(const LevelFinishArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;

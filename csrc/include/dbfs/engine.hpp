@@ -111,6 +111,10 @@ struct EngineOptions {
   // One rank, td/bu/do modes: device-driven level loop (LevelCtrl): the host
   // enqueues the next level before the current one finishes.
   bool device_loop = true;
+  // ... also with several ranks: each level's chain carries its collectives
+  // (frontier all-gather, candidate all-to-all, totals all-reduce), enqueued
+  // ahead like the kernels; level_finish decides on the reduced totals.
+  bool device_loop_ranks = true;
   // ... enqueueing each level with an extrapolated direction prediction (else:
   // the previous level's direction, one more level ahead).
   bool device_loop_predict = true;

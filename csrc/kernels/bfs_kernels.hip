@@ -177,6 +177,19 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   }
 }
 
+__global__ void level_finish_kernel(LevelFinishArgs a) {
+  if (threadIdx.x != 0) return;
+  if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+  LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
+  level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec + a.level);
+  if (!a.seed) {
+    a.rec[a.level].t0 = c.t_start;
+    a.rec[a.level].t1 = wall_clock64();
+  }
+  *a.ctrl = c;
+  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.seed ? -1 : a.level);
+}
+
 // Level totals -> host-mapped mailbox: values first (system scope), then the
 // sequence number with release semantics, so a host that observes `seq` reads
 // the values of that level.
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
     if (a.ctrl->done || a.ctrl->dir != 'T') return;
-    use_bytes = a.ctrl->bytes != 0;
+    use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     a.stats[1] = a.stats[3] = carry_d;
     a.qscan[carry_c] = carry_d;
     *a.ticket = 0u;  // next launch is stream-ordered after this one
-    if (a.ctrl) {
+    if (a.ctrl && a.finish) {
       LevelCtrl c = *a.ctrl;
       level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec + a.level);
       if (!a.seed) {
@@ -763,6 +776,7 @@ __global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a)
 
 // Byte map -> bitmap for the multi-rank exchange (words of 64 vertices).
 __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T' || !a.ctrl->bytes)) return;
   const int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (w >= a.words) return;
   const word_t bits = gather_byte_bits(a.bytes + w * 64);
@@ -1311,6 +1325,8 @@ void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, hipStream_t st) {
   if (n <= 0) return;
   widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n);
 }
+
+void level_finish(const LevelFinishArgs& a, hipStream_t st) { level_finish_kernel<<<1, 64, 0, st>>>(a); }
 
 void list_scatter(const ListScatterArgs& a, hipStream_t st) {
   if (a.nranks <= 0 || a.list_cap <= 0) return;

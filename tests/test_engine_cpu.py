@@ -273,6 +273,7 @@ def test_host_loop_stats_mailbox(mailbox):
 
     def body(rt):
         bfs = dbfs.BFS(p, rt, mode="do")
+        bfs.engine.set_option("device_loop", 0)  # the host loop (several ranks default to the device loop)
         bfs.engine.set_option("stats_mailbox", mailbox)
         bfs.engine.phase_timing = True
         out = []
@@ -347,3 +348,34 @@ def test_narrow_levels(rt, mode, device_loop):
         exp = np.abs(np.arange(n) - src)
         assert np.array_equal(deep.levels(), exp)
         assert r.depth == exp.max() + 1 and r.reached == n
+
+
+@pytest.mark.parametrize("predict", [1, 0])
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+@pytest.mark.parametrize("P", [2, 3])
+def test_device_loop_several_ranks(P, mode, predict):
+    # the device-driven loop with collectives in every level chain (all-gather,
+    # all-to-all, totals all-reduce + level_finish) takes the host loop's
+    # decisions on every rank: same levels, records, reached / edges / depth
+    p = dbfs.rmat_params(11, 16, 29)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    srcs = [int(v) for v in np.nonzero(deg > 0)[0][[0, 77, 901]]]
+
+    def body(rt):
+        dev, host = dbfs.BFS(p, rt, mode=mode), dbfs.BFS(p, rt, mode=mode)
+        dev.engine.set_option("device_loop_predict", predict)
+        dev.engine.set_option("td_byte_edges", 1 << 10)  # byte-map levels (pack + exchange) too
+        host.engine.set_option("device_loop", 0)
+        out = []
+        for s in srcs:
+            a, b = dev.run(s), host.run(s)
+            strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+            out.append((dev.levels(), host.levels(), strip(a), strip(b), (a.reached, a.edges, a.depth),
+                        (b.reached, b.edges, b.depth)))
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for (ld, lh, ra, rb, ta, tb), s in zip(rank_out, srcs):
+            assert np.array_equal(ld, _oracle(csr, s)) and np.array_equal(lh, ld)
+            assert ra == rb and ta == tb

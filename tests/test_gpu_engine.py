@@ -422,3 +422,45 @@ def test_narrow_levels_gpu(gpu_runtime, mode):
         r = deep.run(src)
         assert np.array_equal(deep.levels(), np.abs(np.arange(n) - src))
         assert r.reached == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_device_loop_several_ranks_gpu(gpu_runtime, mode):
+    """Device loop with collectives in the level chains: RCCL (1 rank, forced
+    exchange: the stream-ordered ncclAllGather / ncclAllToAll / ncclAllReduce
+    between predicated kernels, level_finish on the reduced totals) and three
+    virtual ranks on one GPU, against the host loop."""
+    from distributed_cuda_bfs_amd.parallel.runtime import Runtime
+
+    N = dbfs.native
+    be = gpu_runtime.backend
+    comm = N.nccl_comm(N.nccl_unique_id(), 0, 1, be)
+    rt = Runtime(backend=be, comm=comm)
+    p = dbfs.rmat_params(15, 16, 31)
+    csr = dbfs.host_csr_from_params(p)
+    strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+    dev = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+    dev.engine.set_option("td_byte_edges", 1 << 12)
+    host = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+    host.engine.set_option("device_loop", 0)
+    for src in dev.sample_roots(3, seed=12):
+        a, b = dev.run(src), host.run(src)
+        assert np.array_equal(dev.levels(), dbfs.cpu_bfs(csr, src)[0])
+        assert strip(a) == strip(b) and (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+    comm.barrier()
+
+    srcs = [5, 1234]
+
+    def body(r):
+        d, h = dbfs.BFS(p, r, mode=mode), dbfs.BFS(p, r, mode=mode)
+        h.engine.set_option("device_loop", 0)
+        out = []
+        for s in srcs:
+            x, y = d.run(s), h.run(s)
+            out.append((d.levels(), strip(x) == strip(y)))
+        return out
+
+    for rank_out in run_virtual_ranks(3, body, device="hip"):
+        for (lv, same), s in zip(rank_out, srcs):
+            assert same and np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
