@@ -175,7 +175,7 @@ class CpuBackend final : public Backend {
     a.stats[1] = a.stats[3] = d;
     a.qscan[c] = d;
     if (a.ctrl && a.finish) {
-      level_ctrl_finish(*a.ctrl, c, d, a.seed, a.seed ? nullptr : a.rec + a.level);
+      level_ctrl_finish(*a.ctrl, c, d, a.seed, a.seed ? nullptr : a.rec);
       if (a.mailbox) {
         a.mailbox->done = a.ctrl->done;
         a.mailbox->vis_deg = a.ctrl->vis_deg;
@@ -255,7 +255,7 @@ class CpuBackend final : public Backend {
   void level_finish(const LevelFinishArgs& a) override {
     if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
-    level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec + a.level);
+    level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
     *a.ctrl = c;
     if (a.mailbox) {
       a.mailbox->done = c.done;
@@ -294,7 +294,7 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = cnt;
     a.stats[1] = a.stats[3] = deg;
     a.oscan[cnt] = deg;
-    level_ctrl_finish(*a.ctrl, cnt, deg, false, a.rec + a.level_index);
+    level_ctrl_finish(*a.ctrl, cnt, deg, false, a.rec);
     if (a.mailbox) {
       a.mailbox->done = a.ctrl->done;
       a.mailbox->vis_deg = a.ctrl->vis_deg;

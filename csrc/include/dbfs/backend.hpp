@@ -237,7 +237,7 @@ struct ScanArgs {
   // device-driven loop: skip everything when ctrl->done at entry; the last
   // workgroup runs level_ctrl_finish and fills rec / the mailbox slot
   LevelCtrl* ctrl = nullptr;
-  LevelRecDev* rec = nullptr;
+  LevelRecDev* rec = nullptr;       // this level's record
   LevelMailbox* mailbox = nullptr;  // device-mapped pinned slot
   int32_t level = 0;
   bool seed = false;

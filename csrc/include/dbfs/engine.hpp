@@ -251,7 +251,12 @@ class Engine {
   int64_t nunits_ = 0;
   // device-driven loop state
   DBuf<LevelCtrl> ctrl_;
-  DBuf<LevelRecDev> rec_;
+  // per-level records in pinned, device-mapped segments of kRecSeg levels
+  // (host pointer, device pointer): the host reads them after the last stamp
+  // without a copy or a stream synchronisation
+  static constexpr int kRecSeg = 1024;
+  std::vector<std::pair<LevelRecDev*, LevelRecDev*>> rec_segs_;
+  LevelRecDev* rec_at(int level);  // device pointer of level's record
   LevelMailbox* mailbox_host_ = nullptr;  // pinned, device-mapped
   LevelMailbox* mailbox_dev_ = nullptr;
   // host-loop statistics mailbox

@@ -181,10 +181,10 @@ __global__ void level_finish_kernel(LevelFinishArgs a) {
   if (threadIdx.x != 0) return;
   if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
   LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
-  level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec + a.level);
+  level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
   if (!a.seed) {
-    a.rec[a.level].t0 = c.t_start;
-    a.rec[a.level].t1 = wall_clock64();
+    a.rec->t0 = c.t_start;
+    a.rec->t1 = wall_clock64();
   }
   *a.ctrl = c;
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.seed ? -1 : a.level);
@@ -418,10 +418,10 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     *a.ticket = 0u;  // next launch is stream-ordered after this one
     if (a.ctrl && a.finish) {
       LevelCtrl c = *a.ctrl;
-      level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec + a.level);
+      level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
       if (!a.seed) {
-        a.rec[a.level].t0 = c.t_start;
-        a.rec[a.level].t1 = wall_clock64();
+        a.rec->t0 = c.t_start;
+        a.rec->t1 = wall_clock64();
       }
       *a.ctrl = c;
       if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
@@ -745,9 +745,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   a.stats[1] = a.stats[3] = deg;
   a.oscan[cnt] = deg;
   LevelCtrl c = *a.ctrl;
-  level_ctrl_finish(c, cnt, deg, false, a.rec + a.level_index);
-  a.rec[a.level_index].t0 = c.t_start;
-  a.rec[a.level_index].t1 = wall_clock64();
+  level_ctrl_finish(c, cnt, deg, false, a.rec);
+  a.rec->t0 = c.t_start;
+  a.rec->t1 = wall_clock64();
   *a.ctrl = c;
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
 }
