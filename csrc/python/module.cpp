@@ -28,15 +28,9 @@ std::vector<T> from_numpy(const py::array_t<T, py::array::c_style | py::array::f
   return v;
 }
 
-py::dict result_dict(const RunResult& r) {
-  py::dict d;
-  d["source"] = r.source;
-  d["ms"] = r.ms;
-  d["reached"] = r.reached;
-  d["edges"] = r.edges;
-  d["depth"] = r.depth;
-  d["gteps"] = r.gteps;
-  d["mispredicts"] = r.mispredicts;
+// Per-level records as a list of dicts (built on demand: converting them on
+// every run cost more host time than a short GPU level).
+py::list level_dicts(const RunResult& r) {
   py::list lv;
   for (const auto& l : r.levels) {
     py::dict x;
@@ -50,8 +44,7 @@ py::dict result_dict(const RunResult& r) {
     x["gap_ms"] = l.gap_ms;
     lv.append(x);
   }
-  d["levels"] = lv;
-  return d;
+  return lv;
 }
 
 // Comm whose collectives are implemented in Python (torch.distributed / gloo).
@@ -409,6 +402,16 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
       .def("degrees_of", &DeviceGraph::degrees_of);
 
+  py::class_<RunResult>(m, "RunResult")
+      .def_readonly("source", &RunResult::source)
+      .def_readonly("ms", &RunResult::ms)
+      .def_readonly("reached", &RunResult::reached)
+      .def_readonly("edges", &RunResult::edges)
+      .def_readonly("depth", &RunResult::depth)
+      .def_readonly("gteps", &RunResult::gteps)
+      .def_readonly("mispredicts", &RunResult::mispredicts)
+      .def("level_dicts", &level_dicts);
+
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")
       .def(py::init([](std::shared_ptr<DeviceGraph> g, std::shared_ptr<Comm> c, const std::string& mode, double alpha,
                        double beta, int bu_lane_limit, bool phase_timing, bool force_exchange) {
@@ -434,7 +437,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
               py::gil_scoped_release rel;
               r = e.run(src);
             }
-            return result_dict(r);
+            return r;
           },
           py::arg("source"))
       .def("levels_local",

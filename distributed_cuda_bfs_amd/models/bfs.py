@@ -7,7 +7,6 @@ level-synchronous traversal (all ranks call it collectively).
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Union
 
 import numpy as np
@@ -18,22 +17,35 @@ from ..parallel.runtime import Runtime, init_runtime
 MODES = ("ref", "td", "bu", "do", "simple", "scan")
 
 
-@dataclass
 class BFSResult:
-    source: int
-    ms: float
-    reached: int
-    edges: int
-    depth: int
-    gteps: float
-    levels: List[Dict[str, Any]] = field(default_factory=list)
-    mispredicts: int = 0  # device loop: level chains enqueued for the wrong direction
+    """One traversal: totals, plus per-level records (list of dicts with level,
+    dir, frontier, frontier_edges, discovered, ms, comm_ms, gap_ms) converted
+    from the native record on first access."""
+
+    __slots__ = ("source", "ms", "reached", "edges", "depth", "gteps", "mispredicts", "_native", "_levels")
+
+    def __init__(self, source: int, ms: float, reached: int, edges: int, depth: int, gteps: float,
+                 levels: Optional[List[Dict[str, Any]]] = None, mispredicts: int = 0, native: Any = None):
+        self.source, self.ms, self.reached, self.edges = source, ms, reached, edges
+        self.depth, self.gteps, self.mispredicts = depth, gteps, mispredicts
+        self._native, self._levels = native, levels
+
+    @property
+    def levels(self) -> List[Dict[str, Any]]:
+        if self._levels is None:
+            self._levels = list(self._native.level_dicts()) if self._native is not None else []
+        return self._levels
+
+    def __repr__(self) -> str:
+        return (f"BFSResult(source={self.source}, ms={self.ms:.4f}, reached={self.reached}, edges={self.edges}, "
+                f"depth={self.depth}, gteps={self.gteps:.2f})")
 
     @classmethod
-    def from_native(cls, d: Dict[str, Any]) -> "BFSResult":
-        return cls(source=d["source"], ms=d["ms"], reached=d["reached"], edges=d["edges"],
-                   depth=d["depth"], gteps=d["gteps"], levels=list(d["levels"]),
-                   mispredicts=int(d.get("mispredicts", 0)))
+    def from_native(cls, r: Any) -> "BFSResult":
+        if isinstance(r, dict):
+            return cls(r["source"], r["ms"], r["reached"], r["edges"], r["depth"], r["gteps"],
+                       levels=list(r["levels"]), mispredicts=int(r.get("mispredicts", 0)))
+        return cls(r.source, r.ms, r.reached, r.edges, r.depth, r.gteps, mispredicts=r.mispredicts, native=r)
 
 
 class BFS:
