@@ -609,7 +609,9 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
           // with few visited vertices the check costs more than the store it
           // saves (random loads ~120 G/s vs byte stores ~88 G/s on MI355X);
           // the consuming update masks with ~visited anyway
-          if (!check || !(visited[v >> 6] & bit)) a.next_bytes[v] = 1;
+          // (a byte already marked is not stored again: RMAT rows repeat the
+          // same hubs, and a read hit is cheaper than a byte write)
+          if ((!check || !(visited[v >> 6] & bit)) && !a.next_bytes[v]) a.next_bytes[v] = 1;
         } else {
           const word_t seen = visited[v >> 6] | a.next[v >> 6];
           if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
