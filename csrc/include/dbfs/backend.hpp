@@ -59,7 +59,12 @@ struct ShardView {
 
 // At most kMaxHubs hubs: their frontier bitmap (64 KiB) is staged in LDS by
 // every bottom-up workgroup (two 1024-thread workgroups per CU fit in 160 KiB).
-constexpr int64_t kMaxHubs = int64_t(1) << 19;
+// (2^19 - 2^12: the 512 B below 64 KiB leave room for a 64-entry deferred-scan
+// queue per wave next to the hub bits in two workgroups' LDS, see bu_hub_kernel)
+#ifndef DBFS_MAX_HUBS
+#define DBFS_MAX_HUBS ((int64_t(1) << 19) - (int64_t(1) << 12))
+#endif
+constexpr int64_t kMaxHubs = DBFS_MAX_HUBS;
 constexpr vid_t kHubFlag = 0x80000000u;
 // Narrow (8-bit) level arrays: 0xFF = unreached, levels 0 .. 254.
 constexpr uint8_t kNarrowUnreached = 0xFF;

@@ -997,9 +997,15 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
 // word) a fraction.  Found bits are OR-ed into a per-wave LDS copy of the 16
 // result words (s_res), written out once.
 // kWords: the wave's share, 16 words (a quarter unit) or 64 (a whole unit).
-template <bool kPacked, bool kHub, int kWords = kWaveWords>
+// kQueue > 0: rows whose head probe failed are not scanned in the step that
+// probed them (a handful of lanes per step, the rest idle through the scan's
+// dependent loads) but queued in LDS (s_q, kQueue entries of row offset
+// relative to the unit's first row / length / position) and scanned kQueue at
+// a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in place.
+template <bool kPacked, bool kHub, int kWords = kWaveWords, int kQueue = 0>
 __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int* own, word_t* s_res,
-                                                const word_t* s_hub, long long& cnt, long long& deg) {
+                                                const word_t* s_hub, long long& cnt, long long& deg,
+                                                unsigned long long* s_q = nullptr) {
   static_assert(kWords <= kWave, "one word per lane");
   const int lane = lane_id();
   const int64_t left = a.words - w0;
@@ -1077,6 +1083,47 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   fetch(0, n_loc, n_rs, n_len, n_u);
   if (!head) n_u = n_len ? col[n_rs] : 0u;
   int cnt32 = 0;
+  // deferred row scans (kQueue): base = the unit's first row offset
+  eid_t q_base = 0;
+  bool q_span_ok = false;
+  int qn = 0;
+  if constexpr (kQueue > 0) {
+    const int64_t wend = w0 + nw;
+    if (nz_ro) {
+      q_base = nz_ro[a.g.nz_pref[w0]];
+      q_span_ok = nz_ro[a.g.nz_pref[wend]] - q_base < (eid_t(1) << 32);
+    } else {
+      const int64_t vend = min(wend * 64, a.g.rows);
+      q_base = ro[w0 * 64];
+      q_span_ok = ro[vend] - q_base < (eid_t(1) << 32);
+    }
+  }
+  auto settle = [&](bool f, int l, eid_t r0, eid_t r1) {
+    if (f) {
+      store_level(a.level, a.level8, w0 * 64 + l, a.new_level);
+      cnt32 += 1;
+      deg += r1 - r0;
+      __hip_atomic_fetch_or(s_res + (l >> 6), 1ull << (l & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  };
+  // scan the queued rows, one per lane (wave-uniform)
+  auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int ql = 0;
+    eid_t qrs = 0, qe = 0;
+    if (lane < qn) {
+      const unsigned long long ent = s_q[lane];
+      ql = static_cast<int>(ent & 0xFFFu);
+      qrs = q_base + static_cast<eid_t>(ent >> 32);
+      qe = qrs + static_cast<eid_t>((ent >> 12) & 0xFFFFFu);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const bool f = bu_scan_row<kPacked, kHub>(a, qrs, qe, lane >= qn, own, s_hub);
+    settle(lane < qn && f, ql, qrs, qe);
+    qn = 0;
+  };
   for (int b = 0; b < nb; ++b) {
     const int loc = n_loc;
     const eid_t rs = n_rs, e = n_rs + n_len;
@@ -1090,14 +1137,38 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     BU_STAT(1, __popcll(__ballot(loc >= 0)));
     BU_STAT(2, __popcll(__ballot(found)));
     if (!head) n_u = n_len ? col[n_rs] : 0u;
-    found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
-    BU_STAT(7, __popcll(__ballot(found)));
-    if (found) {
-      store_level(a.level, a.level8, w0 * 64 + loc, a.new_level);
-      cnt32 += 1;
-      deg += e - rs;
-      __hip_atomic_fetch_or(s_res + (loc >> 6), 1ull << (loc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if constexpr (kQueue > 0) {
+      // found by the head: settled now; unresolved rows with more neighbours
+      // are queued (huge rows / spans scanned in place)
+      const bool need = !found && e - rs > 1;
+      const bool fits = q_span_ok && e - rs < (eid_t(1) << 20);
+      // more unresolved rows than the queue holds (a sparse-hit level): all in place
+      const bool direct = __popcll(__ballot(need && fits)) > kQueue;
+      const bool inplace = need && (direct || !fits);
+      if (__ballot(inplace)) {
+        // (lanes not scanned here pass as resolved and keep their result)
+        const bool f = bu_scan_row<kPacked, kHub>(a, rs, e, found || !inplace, own, s_hub);
+        if (inplace) found = f;
+      }
+      settle(found, loc, rs, e);
+      const bool defer = need && !inplace;
+      const unsigned long long dm = __ballot(defer);
+      const int k = __popcll(dm);
+      if (qn + k > kQueue) flush();
+      if (defer)
+        s_q[qn + mask_rank(dm)] = (static_cast<unsigned long long>(rs - q_base) << 32) |
+                                  (static_cast<unsigned long long>(e - rs) << 12) | static_cast<unsigned>(loc);
+      qn += k;
+    } else {
+#ifndef DBFS_BU_HEAD_ONLY  // diagnostic timing build: head probes only (wrong levels)
+      found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
+#endif
+      BU_STAT(7, __popcll(__ballot(found)));
+      settle(found, loc, rs, e);
     }
+  }
+  if constexpr (kQueue > 0) {
+    if (qn) flush();
   }
   cnt += cnt32;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1139,6 +1210,14 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
 constexpr int kHubBuThreads = DBFS_HUB_BU_THREADS;
 static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
+// Deferred row-scan queue entries per wave (whole-unit hub waves; 0 = scan
+// in the probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
+// (kMaxHubs / 8 B) and the 8 KiB result words, two workgroups per CU.
+#ifndef DBFS_BU_QUEUE
+#define DBFS_BU_QUEUE 64
+#endif
+constexpr int kBuQueue = DBFS_BU_QUEUE;
+static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
 
 template <bool kPacked, bool kCompact, bool kWhole = false>
 __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
@@ -1146,6 +1225,7 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
   __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
   __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
+  __shared__ unsigned long long s_q[kWhole && kBuQueue > 0 ? (kHubBuThreads / kWave) * kBuQueue : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
@@ -1163,8 +1243,8 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<kPacked, true, kUnitWords>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub, cnt,
-                                                 deg);
+      bu_wave_compact<kPacked, true, kUnitWords, kBuQueue>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
+                                                           cnt, deg, s_q + wave * kBuQueue);
       wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg);
     }
     return;
