@@ -795,6 +795,19 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 #endif
 constexpr int kBuBatch = DBFS_BU_BATCH;  // phase-1 column loads in flight per lane
 
+// Deferred row-scan queue entries per wave (whole-unit hub waves; 0 = scan
+// in the probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
+// (kMaxHubs / 8 B) and the 8 KiB result words, two workgroups per CU.
+#ifndef DBFS_BU_QUEUE
+#define DBFS_BU_QUEUE 64
+#endif
+constexpr int kBuQueue = DBFS_BU_QUEUE;
+#ifndef DBFS_BU_QUEUE_DIRECT
+#define DBFS_BU_QUEUE_DIRECT DBFS_BU_QUEUE
+#endif
+constexpr int kQueueDirect = DBFS_BU_QUEUE_DIRECT < kBuQueue ? DBFS_BU_QUEUE_DIRECT : kBuQueue;
+static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
+
 #ifdef DBFS_BU_STATS
 // Diagnostic build only (-DDBFS_BU_STATS, tools/gpu_bu_stats.sh): wave-level
 // event counters of the bottom-up kernel, printed per dispatch by bu_step.
@@ -1142,8 +1155,9 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
       // are queued (huge rows / spans scanned in place)
       const bool need = !found && e - rs > 1;
       const bool fits = q_span_ok && e - rs < (eid_t(1) << 20);
-      // more unresolved rows than the queue holds (a sparse-hit level): all in place
-      const bool direct = __popcll(__ballot(need && fits)) > kQueue;
+      // more unresolved rows than kQueueDirect (a sparse-hit level: most lanes
+      // scan anyway, deferring gains nothing): all in place
+      const bool direct = __popcll(__ballot(need && fits)) > kQueueDirect;
       const bool inplace = need && (direct || !fits);
       if (__ballot(inplace)) {
         // (lanes not scanned here pass as resolved and keep their result)
@@ -1210,14 +1224,7 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
 constexpr int kHubBuThreads = DBFS_HUB_BU_THREADS;
 static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
-// Deferred row-scan queue entries per wave (whole-unit hub waves; 0 = scan
-// in the probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
-// (kMaxHubs / 8 B) and the 8 KiB result words, two workgroups per CU.
-#ifndef DBFS_BU_QUEUE
-#define DBFS_BU_QUEUE 64
-#endif
-constexpr int kBuQueue = DBFS_BU_QUEUE;
-static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
+
 
 template <bool kPacked, bool kCompact, bool kWhole = false>
 __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
