@@ -781,6 +781,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.compact = opt_.bu_compact;
       ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
+      ba.follow_up = !res.levels.empty() && res.levels.back().direction == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
@@ -1159,6 +1160,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.compact = opt_.bu_compact;
       ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
+      ba.follow_up = pf == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
       if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();

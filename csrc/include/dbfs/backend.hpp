@@ -412,6 +412,7 @@ struct BuArgs {
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
   bool packed = false;               // wave cooperation over a packed multi-row edge stream
   bool compact = true;               // waves process their unvisited vertices 64 at a time
+  bool follow_up = false;            // the previous level was bottom-up too (launch shape)
   int whole_units = 0;               // hub kernel, compacted: 64 words per wave (1), 16 (-1), by shard size (0)
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;

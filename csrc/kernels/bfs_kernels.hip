@@ -1226,17 +1226,17 @@ static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
 
-template <bool kPacked, bool kCompact, bool kWhole = false>
-__global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub_kernel(BuArgs a) {
+template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads>
+__global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
-  __shared__ int s_bu_owner[kPacked ? kHubBuThreads : 1];
-  __shared__ word_t s_res[kCompact ? (kHubBuThreads / kWave) * kUnitWords : 1];
-  __shared__ long long s_c[kHubBuThreads / kWave], s_d[kHubBuThreads / kWave];
-  __shared__ unsigned long long s_q[kWhole && kBuQueue > 0 ? (kHubBuThreads / kWave) * kBuQueue : 1];
+  __shared__ int s_bu_owner[kPacked ? kThreads : 1];
+  __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
+  __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
+  __shared__ unsigned long long s_q[kWhole && kBuQueue > 0 ? (kThreads / kWave) * kBuQueue : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
-  for (int64_t i = threadIdx.x; i < hw; i += kHubBuThreads) s_hub[i] = a.hub_front[i];
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) s_hub[i] = a.hub_front[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
     // cross-wave reduction, so waves run independently: no barrier).  Chosen
     // when the shard has enough units to fill the chip this way (one GPU);
     // small shards (many ranks) keep 16 words per wave for parallelism.
-    constexpr int kWavesPerBlock = kHubBuThreads / kWave;
+    constexpr int kWavesPerBlock = kThreads / kWave;
     int* own = s_bu_owner;
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
@@ -1256,7 +1256,7 @@ __global__ __launch_bounds__(kHubBuThreads, 2 * kHubBuThreads / 256) void bu_hub
     }
     return;
   }
-  constexpr int kGroups = kHubBuThreads / kUnitThreads;
+  constexpr int kGroups = kThreads / kUnitThreads;
   const int group = wave / kUnitWaves;
   const int wg = wave % kUnitWaves;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
@@ -1472,10 +1472,15 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // keep 16 words per wave for parallelism
     const int64_t slots = 2 * static_cast<int64_t>(device_cus()) * (kHubBuThreads / kWave);
     const bool whole = a.compact && !a.packed && (a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots));
-    const unsigned grid = grid_for(nunits, whole ? kHubBuThreads / kWave : kHubBuThreads / kUnitThreads,
-                                   2 * device_cus());
+    // a bottom-up level after another one (few unvisited vertices left, most
+    // of them scanning rows): 768-thread workgroups, 80 VGPRs instead of 64
+    constexpr int kFollowThreads = 768;
+    const int threads = whole && a.follow_up ? kFollowThreads : kHubBuThreads;
+    const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
-    if (whole)
+    if (whole && a.follow_up)
+      bu_hub_kernel<false, true, true, kFollowThreads><<<grid, kFollowThreads, 0, st>>>(a);
+    else if (whole)
       bu_hub_kernel<false, true, true><<<grid, kHubBuThreads, 0, st>>>(a);
     else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
