@@ -1226,13 +1226,13 @@ static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
 
-template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads>
+template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads, int kQ = kBuQueue>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ int s_bu_owner[kPacked ? kThreads : 1];
   __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
-  __shared__ unsigned long long s_q[kWhole && kBuQueue > 0 ? (kThreads / kWave) * kBuQueue : 1];
+  __shared__ unsigned long long s_q[kWhole && kQ > 0 ? (kThreads / kWave) * kQ : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
@@ -1250,8 +1250,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<kPacked, true, kUnitWords, kBuQueue>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
-                                                           cnt, deg, s_q + wave * kBuQueue);
+      bu_wave_compact<kPacked, true, kUnitWords, kQ>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub, cnt,
+                                                     deg, s_q + wave * kQ);
       wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg);
     }
     return;
@@ -1474,12 +1474,19 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     const bool whole = a.compact && !a.packed && (a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots));
     // a bottom-up level after another one (few unvisited vertices left, most
     // of them scanning rows): 768-thread workgroups, 80 VGPRs instead of 64
-    constexpr int kFollowThreads = 768;
+#ifndef DBFS_BU_FOLLOW_THREADS
+#define DBFS_BU_FOLLOW_THREADS 768
+#endif
+    constexpr int kFollowThreads = DBFS_BU_FOLLOW_THREADS;
+#ifndef DBFS_BU_FOLLOW_QUEUE
+#define DBFS_BU_FOLLOW_QUEUE DBFS_BU_QUEUE
+#endif
+    constexpr int kFollowQueue = DBFS_BU_FOLLOW_QUEUE;
     const int threads = whole && a.follow_up ? kFollowThreads : kHubBuThreads;
     const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
     if (whole && a.follow_up)
-      bu_hub_kernel<false, true, true, kFollowThreads><<<grid, kFollowThreads, 0, st>>>(a);
+      bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue><<<grid, kFollowThreads, 0, st>>>(a);
     else if (whole)
       bu_hub_kernel<false, true, true><<<grid, kHubBuThreads, 0, st>>>(a);
     else if (a.packed)
