@@ -1232,7 +1232,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   __shared__ int s_bu_owner[kPacked ? kThreads : 1];
   __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
-  __shared__ unsigned long long s_q[kWhole && kQ > 0 ? (kThreads / kWave) * kQ : 1];
+  constexpr int kQueueLen = (kCompact && !kPacked) ? kQ : 0;
+  __shared__ unsigned long long s_q[kQueueLen > 0 ? (kThreads / kWave) * kQueueLen : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
@@ -1250,8 +1251,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<kPacked, true, kUnitWords, kQ>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub, cnt,
-                                                     deg, s_q + wave * kQ);
+      bu_wave_compact<kPacked, true, kUnitWords, kQueueLen>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
+                                                            cnt, deg, s_q + wave * kQueueLen);
       wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg);
     }
     return;
@@ -1266,8 +1267,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     if (u < nunits) {
       int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
       if constexpr (kCompact)
-        bu_wave_compact<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_res + wave * kWaveWords, s_hub,
-                                       cnt, deg);
+        bu_wave_compact<kPacked, true, kWaveWords, kQueueLen>(a, u * kUnitWords + wg * kWaveWords, own,
+                                                              s_res + wave * kWaveWords, s_hub, cnt, deg,
+                                                              s_q + wave * kQueueLen);
       else
         bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_hub, cnt, deg);
     }
@@ -1491,6 +1493,8 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       bu_hub_kernel<false, true, true><<<grid, kHubBuThreads, 0, st>>>(a);
     else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
+    else if (a.compact && a.follow_up)  // scan-heavy later level: no deferral (measured)
+      bu_hub_kernel<false, true, false, kHubBuThreads, 0><<<grid, kHubBuThreads, 0, st>>>(a);
     else
       a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);
 #undef DBFS_BU_HUB
