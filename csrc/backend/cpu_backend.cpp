@@ -137,6 +137,7 @@ class CpuBackend final : public Backend {
         a.mailbox->next_dir = c.dir;
         a.mailbox->n_f = c.n_f;
         a.mailbox->m_f = c.m_f;
+        a.mailbox->reached = c.reached;
         a.mailbox->level = -1;
       }
     }
@@ -182,6 +183,7 @@ class CpuBackend final : public Backend {
         a.mailbox->next_dir = a.ctrl->dir;
         a.mailbox->n_f = a.ctrl->n_f;
         a.mailbox->m_f = a.ctrl->m_f;
+        a.mailbox->reached = a.ctrl->reached;
         a.mailbox->level = a.level;
       }
     }
@@ -263,6 +265,7 @@ class CpuBackend final : public Backend {
       a.mailbox->next_dir = c.dir;
       a.mailbox->n_f = c.n_f;
       a.mailbox->m_f = c.m_f;
+      a.mailbox->reached = c.reached;
       a.mailbox->level = a.seed ? -1 : a.level;
     }
   }
@@ -301,6 +304,7 @@ class CpuBackend final : public Backend {
       a.mailbox->next_dir = a.ctrl->dir;
       a.mailbox->n_f = a.ctrl->n_f;
       a.mailbox->m_f = a.ctrl->m_f;
+      a.mailbox->reached = a.ctrl->reached;
       a.mailbox->level = a.level_index;
     }
   }
@@ -572,13 +576,15 @@ class CpuBackend final : public Backend {
   void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) override {
     for (int64_t i = 0; i < n; ++i) out[i] = in[i] == kNarrowUnreached ? kUnreached : static_cast<lvl_t>(in[i]);
   }
-  void degree_square_sum(const ShardView& g, int64_t* out1) override {
-    int64_t s = 0;
+  void degree_moments(const ShardView& g, int64_t* out2) override {
+    int64_t s = 0, c = 0;
     for (int64_t r = 0; r < g.rows; ++r) {
       const int64_t d = g.row_off[r + 1] - g.row_off[r];
       s += d * d;
+      c += d > 0 ? 1 : 0;
     }
-    out1[0] = s;
+    out2[0] = s;
+    out2[1] = c;
   }
   void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) override {
     int64_t c = 0, d = 0;

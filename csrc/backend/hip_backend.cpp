@@ -275,10 +275,10 @@ class HipBackend final : public Backend {
     kern::gen_fill(p, lo, rows, cursor, col, st_);
     chk();
   }
-  void degree_square_sum(const ShardView& g, int64_t* out1) override {
+  void degree_moments(const ShardView& g, int64_t* out2) override {
     on();
-    HIP_CHECK(hipMemsetAsync(out1, 0, sizeof(int64_t), st_));
-    kern::degree_square_sum(g, out1, st_);
+    HIP_CHECK(hipMemsetAsync(out2, 0, 2 * sizeof(int64_t), st_));
+    kern::degree_moments(g, out2, st_);
     chk();
   }
   void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) override {

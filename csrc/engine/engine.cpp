@@ -899,13 +899,19 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sparse_ticket_ = DBuf<unsigned>(be_, 1);
     be_.memset_async(sparse_cnt_.data(), 0, sparse_cnt_.bytes());
     be_.memset_async(sparse_ticket_.data(), 0, sparse_ticket_.bytes());
-    // mean degree of an edge's endpoint (sum deg^2 / sum deg): predicts the
-    // edges of level 1's frontier (the source's neighbours) from the source's degree
-    be_.degree_square_sum(gv, stats_.data() + 4);
-    int64_t sq = 0;
-    be_.to_host(&sq, stats_.data() + 4, sizeof(sq));
-    excess_degree_ = total_directed_ > 0 ? static_cast<double>(sq) / static_cast<double>(total_directed_) : 0.0;
     sparse_ready_ = true;
+  }
+  if (n_active_ < 0) {
+    // (outside the timed window, once) the mean degree of an edge's endpoint
+    // (sum deg^2 / sum deg) predicts the edges of level 1's frontier (the
+    // source's neighbours) from the source's degree; the number of vertices
+    // with edges bounds every later frontier by those not reached yet
+    be_.degree_moments(gv, stats_.data() + 4);
+    if (xc) comm_.allreduce_sum_i64(stats_.data() + 4, 2);
+    int64_t mom[2] = {0, 0};
+    be_.to_host(mom, stats_.data() + 4, sizeof(mom));
+    excess_degree_ = total_directed_ > 0 ? static_cast<double>(mom[0]) / static_cast<double>(total_directed_) : 0.0;
+    n_active_ = mom[1];
   }
   // work-list set k (level L reads set L & 1; one set without sparse levels)
   auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
@@ -1100,6 +1106,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.mailbox = mailbox_dev_ + slot(L);
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
+      sp.first = pf != 'T';
       be_.td_sparse(sp);
     } else if (d == 'T') {
       // a sparse level (or the seed) already handed over the work list
@@ -1234,7 +1241,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     hc.done = 0;
     LevelRecDev scratch;
     const double cap = static_cast<double>(part_.n);
-    const double enf = std::min(grow(nf, prev_nf), cap);
+    // (never more than the vertices with edges not reached yet)
+    const double enf = std::min({grow(nf, prev_nf), cap, static_cast<double>(std::max<int64_t>(0, n_active_ - mb->reached))});
     // level 1's frontier edges: the source's neighbours have the mean endpoint degree
     const double emf = std::min(L == 0 ? static_cast<double>(mf) * std::max(1.0, excess_degree_) : grow(mf, prev_mf),
                                 static_cast<double>(total_directed_));

@@ -105,6 +105,7 @@ struct LevelCtrl {
   int32_t check_visited = 1;    // ... with the visited pre-check
   int32_t done = 0;             // frontier empty: every later kernel returns
   int64_t n_f = 0, m_f = 0, prev_nf = 0, vis_deg = 0;
+  int64_t reached = 0;          // vertices with degree > 0 reached so far (counts summed)
   // device wall clock (Backend::wall_clock_khz) when the running level's
   // first kernel started
   uint64_t t_start = 0;
@@ -126,6 +127,7 @@ struct LevelMailbox {
   int32_t next_dir = 0;         // direction decided for the following level
   int32_t pad = 0;
   int64_t n_f = 0, m_f = 0;     // the following level's frontier (vertices, edges)
+  int64_t reached = 0;          // LevelCtrl::reached
 };
 constexpr int kMailboxSlots = 8;
 
@@ -134,6 +136,7 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
   if (seed) {
     c.prev_nf = 0;
     c.vis_deg = degsum;
+    c.reached = count;
   } else {
     rec->dir = c.dir;
     rec->n_f = c.n_f;
@@ -141,6 +144,7 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
     rec->discovered = count;
     c.prev_nf = c.n_f;
     c.vis_deg += degsum;
+    c.reached += count;
   }
   c.n_f = count;
   c.m_f = degsum;
@@ -335,6 +339,7 @@ struct TdSparseArgs {
   LevelMailbox* mailbox = nullptr;
   int32_t level_index = 0;
   int64_t grid = 0;
+  bool first = true;  // first kernel of the level (else a compaction ran before it)
 };
 
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
@@ -632,8 +637,8 @@ class Backend {
   virtual void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) = 0;
   // sum of degrees of vertices with level != kUnreached (device scalar out)
   virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
-  // sum over the shard's rows of degree^2 (device scalar out)
-  virtual void degree_square_sum(const ShardView& g, int64_t* out1) = 0;
+  // over the shard's rows: out2[0] = sum of degree^2, out2[1] = rows with degree > 0
+  virtual void degree_moments(const ShardView& g, int64_t* out2) = 0;
   // out[i] = in[i] (narrow levels; kNarrowUnreached -> kUnreached)
   virtual void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) = 0;
 

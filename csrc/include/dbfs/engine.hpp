@@ -242,6 +242,7 @@ class Engine {
   // reads set L & 1), entry -> vertex maps, output counters, a ticket
   bool sparse_ready_ = false;
   double excess_degree_ = 0.0;  // sum deg^2 / sum deg (level-1 edge prediction)
+  int64_t n_active_ = -1;       // vertices with degree > 0 (global; -1: not computed yet)
   DBuf<int64_t> qscan2_, qbase2_;
   DBuf<int32_t> blk_vstart2_;
   DBuf<vid_t> qv_[2];

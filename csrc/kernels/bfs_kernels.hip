@@ -56,6 +56,8 @@ __device__ __forceinline__ void stamp_mailbox(LevelMailbox* mb, const LevelCtrl&
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->m_f), static_cast<unsigned long long>(c.m_f),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->reached), static_cast<unsigned long long>(c.reached),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&mb->level, level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -634,7 +636,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   __shared__ int s_last;
   // uniform: the whole grid returns, no workgroup takes a ticket
   if (a.ctrl->done || a.ctrl->dir != 'T') return;
-  stamp_level_start(a.ctrl);
+  if (a.first) stamp_level_start(a.ctrl);
   const long long q = a.dev_stats[0], m = a.dev_stats[1];
   const int t = threadIdx.x;
   const int lane = lane_id();

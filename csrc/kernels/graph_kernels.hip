@@ -188,15 +188,18 @@ __global__ __launch_bounds__(kBlock) void reached_deg_kernel(ShardView g, const 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void degree_square_kernel(ShardView g, int64_t* out1) {
+__global__ __launch_bounds__(kBlock) void degree_moments_kernel(ShardView g, int64_t* out2) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  long long s = 0;
+  long long s = 0, c = 0;
   for (int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; r < g.rows; r += stride) {
     const long long d = g.row_off[r + 1] - g.row_off[r];
     s += d * d;
+    c += d > 0 ? 1 : 0;
   }
   s = wave_sum(s);
-  if (lane_id() == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(out1), static_cast<unsigned long long>(s));
+  c = wave_sum(c);
+  if (lane_id() == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(out2), static_cast<unsigned long long>(s));
+  if (lane_id() == 0 && c) atomicAdd(reinterpret_cast<unsigned long long*>(out2 + 1), static_cast<unsigned long long>(c));
 }
 
 inline unsigned capped_grid(int64_t work, int64_t cap) {
@@ -252,9 +255,9 @@ void compute_parents(const ParentArgs& a, hipStream_t st) {
   parent_kernel<<<static_cast<unsigned>((a.g.rows + wpb - 1) / wpb), kBlock, 0, st>>>(a);
 }
 
-void degree_square_sum(const ShardView& g, int64_t* out1, hipStream_t st) {
+void degree_moments(const ShardView& g, int64_t* out2, hipStream_t st) {
   if (g.rows <= 0) return;
-  degree_square_kernel<<<capped_grid(g.rows, 4096), kBlock, 0, st>>>(g, out1);
+  degree_moments_kernel<<<capped_grid(g.rows, 4096), kBlock, 0, st>>>(g, out2);
 }
 
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st) {

@@ -61,7 +61,7 @@ void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_ve
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
-void degree_square_sum(const ShardView& g, int64_t* out1, hipStream_t st);
+void degree_moments(const ShardView& g, int64_t* out2, hipStream_t st);
 
 }  // namespace kern
 }  // namespace dbfs
