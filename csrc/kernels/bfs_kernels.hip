@@ -1103,7 +1103,9 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   bool q_span_ok = false;
   int qn = 0;
   if constexpr (kQueue > 0) {
-    const int64_t wend = w0 + nw;
+    // (the non-empty-row view covers ceil(rows / 64) words; a shard's bitmap
+    // slice may be longer -- padding words, all visited)
+    const int64_t wend = min(w0 + nw, (a.g.rows + kWordBits - 1) / kWordBits);
     if (nz_ro) {
       q_base = nz_ro[a.g.nz_pref[w0]];
       q_span_ok = nz_ro[a.g.nz_pref[wend]] - q_base < (eid_t(1) << 32);
