@@ -431,6 +431,26 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   }
 }
 
+// blk[b] = p for every edge block b (kTdEdgesPerBlock edges) that starts in the
+// entry's edge range [qs, qs + d) -- wave-uniform call.  Short ranges are
+// written by their lane; long ones (a hub's row spans hundreds of blocks) by
+// the whole wave, 64 blocks per step, instead of one lane looping alone.
+__device__ __forceinline__ void wave_fill_blocks(int32_t* __restrict__ blk, bool take, long long qs, long long d,
+                                                 long long p) {
+  const long long b0 = take ? (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock : 0;
+  const long long b1 = take ? (qs + d + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock : 0;
+  const bool wide = b1 - b0 > 4;
+  if (!wide)
+    for (long long b = b0; b < b1; ++b) blk[b] = static_cast<int32_t>(p);
+  unsigned long long pending = __ballot(wide);
+  while (pending) {
+    const int l = __ffsll(static_cast<long long>(pending)) - 1;
+    pending &= pending - 1;
+    const long long lo = readlane_i64(b0, l), hi = readlane_i64(b1, l), pl = readlane_i64(p, l);
+    for (long long b = lo + lane_id(); b < hi; b += kWave) blk[b] = static_cast<int32_t>(pl);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Frontier compaction: one wave per 64-word unit (lane l loads word l), 4
 // units per workgroup.  The unit's base slot and edge offset come from the
@@ -466,15 +486,14 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     const bool take = d > 0;
     const unsigned long long tm = __ballot(take);
     const long long incl = wave_incl_scan(d);
+    const long long p = pos + mask_rank(tm);
+    const long long qs = off + incl - d;
     if (take) {
-      const long long p = pos + mask_rank(tm);
-      const long long qs = off + incl - d;
       a.qscan[p] = qs;
       a.qbase[p] = rs - qs;
       if (a.qv) a.qv[p] = static_cast<vid_t>(w0 * 64 + vpos);
-      for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
-        a.blk_vstart[blk] = static_cast<int32_t>(p);
     }
+    wave_fill_blocks(a.blk_vstart, take, qs, d, p);
     pos += __popcll(tm);
     off += readlane_i64(incl, kWave - 1);
   }
@@ -712,15 +731,14 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const long long d = static_cast<long long>(re[k] - rs[k]);
+      const long long p = p0 + cbase[k] + mask_rank(tm[k]);
+      const long long qs = q0 + ebase[k] + incl[k] - d;
       if (d > 0) {
-        const long long p = p0 + cbase[k] + mask_rank(tm[k]);
-        const long long qs = q0 + ebase[k] + incl[k] - d;
         a.oscan[p] = qs;
         a.obase[p] = rs[k] - qs;
         a.oqv[p] = static_cast<vid_t>(static_cast<int64_t>(v[k]) - lo);
-        for (long long blk = (qs + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock; blk * kTdEdgesPerBlock < qs + d; ++blk)
-          a.oblk[blk] = static_cast<int32_t>(p);
       }
+      wave_fill_blocks(a.oblk, d > 0, qs, d, p);
     }
   }
 
