@@ -1382,7 +1382,10 @@ int device_cus();
 
 void init_run(const InitRunArgs& a, hipStream_t st) {
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
-  init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
+#ifndef DBFS_INIT_BLOCKS_PER_CU
+#define DBFS_INIT_BLOCKS_PER_CU 8
+#endif
+  init_run_kernel<<<grid_for(work, kBlock, DBFS_INIT_BLOCKS_PER_CU * device_cus()), kBlock, 0, st>>>(a);
 }
 
 void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st) {
