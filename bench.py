@@ -54,7 +54,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--root-seed", type=int, default=12345)
     ap.add_argument("--alpha", type=float, default=24.0)
-    ap.add_argument("--beta", type=float, default=24.0)
+    ap.add_argument("--beta", type=float, default=96.0)
     ap.add_argument("--bu-lane-limit", type=int, default=8)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning option (see Engine.get_options()), repeatable")

@@ -96,7 +96,7 @@ struct LevelCtrl {
   // configuration (written once per run)
   int32_t mode = 2;             // 0 top-down only, 1 bottom-up only, 2 direction-optimising
   int32_t pad0 = 0;
-  double alpha = 24.0, beta = 24.0;
+  double alpha = 24.0, beta = 96.0;
   double n = 0.0, total_directed = 0.0;
   double td_byte_edges = 0.0, check_visited_min = 0.0;
   // state after the last finished level

@@ -78,7 +78,7 @@ struct EngineOptions {
   // profiles/): BU is cheap enough here that switching earlier than Beamer's
   // CPU value (14) pays.
   double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
-  double beta = 24.0;   // BU -> TD when n_f < n / beta (and shrinking)
+  double beta = 96.0;   // BU -> TD when n_f < n / beta (and shrinking)
   int bu_lane_limit = 8;
   // Bottom-up rows still unresolved after the per-lane phase are scanned as
   // one packed edge stream per wave (else one row at a time).
