@@ -1509,13 +1509,18 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 #define DBFS_BU_FOLLOW_QUEUE DBFS_BU_QUEUE
 #endif
     constexpr int kFollowQueue = DBFS_BU_FOLLOW_QUEUE;
-    const int threads = whole && a.follow_up ? kFollowThreads : kHubBuThreads;
+    // first bottom-up level, whole units (any multiple of 64 threads: no unit groups)
+#ifndef DBFS_BU_FIRST_THREADS
+#define DBFS_BU_FIRST_THREADS DBFS_HUB_BU_THREADS
+#endif
+    constexpr int kFirstThreads = DBFS_BU_FIRST_THREADS;
+    const int threads = whole ? (a.follow_up ? kFollowThreads : kFirstThreads) : kHubBuThreads;
     const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
     if (whole && a.follow_up)
       bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue><<<grid, kFollowThreads, 0, st>>>(a);
     else if (whole)
-      bu_hub_kernel<false, true, true><<<grid, kHubBuThreads, 0, st>>>(a);
+      bu_hub_kernel<false, true, true, kFirstThreads><<<grid, kFirstThreads, 0, st>>>(a);
     else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
     else if (a.compact && a.follow_up)  // scan-heavy later level: no deferral (measured)
