@@ -379,3 +379,26 @@ def test_device_loop_several_ranks(P, mode, predict):
         for (ld, lh, ra, rb, ta, tb), s in zip(rank_out, srcs):
             assert np.array_equal(ld, _oracle(csr, s)) and np.array_equal(lh, ld)
             assert ra == rb and ta == tb
+
+
+@pytest.mark.parametrize("case", [(1, [], [], 0), (2, [0], [1], 1), (5, [0, 1], [1, 2], 4),
+                                  (130, list(range(128)), list(range(1, 129)), 129),
+                                  (130, list(range(128)), list(range(1, 129)), 0)])
+def test_tiny_and_isolated_sources(rt, case):
+    # one-vertex graph, isolated sources, a slice boundary inside a path: every
+    # mode (device loop: sparse levels, narrow levels) on one rank and three
+    n, u, v, src = case
+    g = dbfs.build_csr(n, np.array(u, dtype=np.int64), np.array(v, dtype=np.int64))
+    exp = dbfs.cpu_bfs(g, src)[0]
+    for mode in ("td", "bu", "do"):
+        b = dbfs.BFS(g, rt, mode=mode)
+        b.run(src)
+        assert np.array_equal(b.levels(), exp)
+
+    def body(r):
+        b = dbfs.BFS(g, r, mode="do")
+        b.run(src)
+        return b.levels()
+
+    for lv in run_virtual_ranks(3, body, device="cpu"):
+        assert np.array_equal(lv, exp)
