@@ -1,28 +1,48 @@
 #!/usr/bin/env python3
 """Headline benchmark: Graph500-style BFS GTEPS on RMAT-26 over N MI355X GPUs.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` -- for N > 1
-launched with ``torch.distributed.run`` (one process per GPU; RANK, LOCAL_RANK,
-WORLD_SIZE, MASTER_ADDR, MASTER_PORT from the environment).  One *step* = one
-complete BFS traversal from a fresh random root (degree >= 1) on the fixed
-RMAT-26 graph (strong scaling: the graph is 1D-partitioned over the N GPUs).
-W untimed warm-up traversals, then EXACTLY K traversals timed between a
-barrier + device synchronisation on both sides, max over ranks; rank 0 prints
-one JSON line.  value = total traversed edges of the K traversals / timed wall
-time (whole job, all GPUs).  The graph is generated on the GPUs with the
-Graph500 Kronecker parameters (a=.57 b=.19 c=.19, edge factor 16, scrambled
-vertex labels); weights/data are synthetic by construction (no dataset).
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.
 
-The reference (xxcclong/Distributed-CUDA-BFS) publishes no number
-(BASELINE.md), so vs_baseline is null unless --baseline-gteps is given.
-This process never imports torch: it uses the native core's own HIP runtime
-and RCCL communicator.
+* N > 1 under ``torch.distributed.run`` (RANK / LOCAL_RANK / WORLD_SIZE /
+  MASTER_ADDR / MASTER_PORT in the environment): this process is one rank.
+* N > 1 without a launcher (no WORLD_SIZE): the process starts N fresh child
+  processes of itself (``subprocess``, never ``exec``), one per GPU, with the
+  launcher's variables set, before it imports the native module or touches
+  HIP; rank 0's JSON line is the output, the exit status is the worst child's.
+  (The reference's 2-rank launch was ``mpirun -np 2 osu_bw``, README.md:18-23,
+  bfs_mpi.cu:797-809.)
+
+One *step* = one complete BFS traversal from a fresh random root (degree >= 1)
+on the fixed RMAT-26 graph (strong scaling: the graph is 1D-partitioned over
+the N GPUs).  W untimed warm-up traversals, then EXACTLY K traversals timed
+between a barrier + device synchronisation on both sides, max over ranks;
+rank 0 prints one JSON line.  value = total traversed input edges of the K
+traversals / timed wall time (whole job, all GPUs).  The graph is generated on
+the GPUs with the Graph500 Kronecker parameters (a=.57 b=.19 c=.19, edge
+factor 16, scrambled vertex labels): synthetic by construction (no dataset).
+
+Honesty fields:
+  * ``level_state_dtype``: the engine keeps one-byte levels during a traversal
+    (widened to the reference's int32 when read, outside the timer);
+    ``value_int32_levels`` is a second timed pass of the same K roots with
+    32-bit levels written by every kernel (``narrow_levels=0``).
+  * ``validated_roots``: after the timed windows every timed root is traversed
+    again and checked by the device Graph500 validator.
+  * ``vs_baseline``: value / the reference algorithm's GTEPS (``--mode ref``, a
+    HIP re-implementation of bfs.cu:134-165).  With ``--baseline-live`` it is
+    measured in this process on the same graph; otherwise the number measured
+    on MI355X in round 1 is used for the 1-GPU RMAT-26
+    configuration and vs_baseline is null elsewhere.
+  * ``comm`` / ``comm_ranks`` / ``devices``: the communicator the ranks formed
+    (rccl for N > 1 GPUs) and each rank's HIP device.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,7 +52,7 @@ sys.path.insert(0, REPO)
 METRIC = "GTEPS (traversed edges/sec) on RMAT-26 + soc-LiveJournal1 at 1/2/4/8 MI355X"
 
 # The reference publishes no number.  Its algorithm, re-implemented
-# in HIP (`--mode ref`), measured on MI355X in this repo: (scale, n_gpus) -> GTEPS.
+# in HIP (`--mode ref`), measured on MI355X in round 1: (scale, n_gpus) -> GTEPS.
 MEASURED_REF_GTEPS = {(26, 1): 0.8088}
 
 
@@ -40,7 +60,7 @@ def log(msg: str) -> None:
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=16)
@@ -50,6 +70,8 @@ def main() -> int:
                          "no dataset ships with the repo and the GPU pool has no network)")
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: RMAT scale = --scale + log2(N) (per-GPU shard size fixed)")
     ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple", "scan"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--root-seed", type=int, default=12345)
@@ -62,32 +84,110 @@ def main() -> int:
     ap.add_argument("--max-hubs", type=int, default=None)
     ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-int32-pass", action="store_true",
+                    help="skip the second timed pass with 32-bit level arrays")
     ap.add_argument("--baseline-gteps", type=float, default=None)
+    ap.add_argument("--baseline-live", action="store_true",
+                    help="measure the reference algorithm (--mode ref) on the same graph in this process")
+    ap.add_argument("--baseline-roots", type=int, default=2)
     ap.add_argument("--per-level", action="store_true", help="print per-level records of the first timed run")
-    args = ap.parse_args()
+    ap.add_argument("--spawn-timeout", type=float, default=1500.0,
+                    help="self-spawned ranks: seconds before the children are killed")
+    return ap.parse_args(argv)
 
+
+# ---- self-spawn (no launcher) -------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv, timeout_s: float) -> int:
+    """Start n child processes of this script, one rank each (RANK = LOCAL_RANK
+    = i, WORLD_SIZE = n, MASTER_* = 127.0.0.1 and a free port).  The parent
+    never touches the GPU.  If a child fails the others are given 30 s to
+    notice (their collectives time out or see the closed peer) and are then
+    killed; the exit status is the first failing child's (0 if all succeed)."""
+    port = _free_port()
+    boot_port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   DBFS_BOOTSTRAP_PORT=str(boot_port), DBFS_SPAWNED="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    t0 = time.time()
+    rc = 0
+    failed_at = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and failed_at is None:
+            failed_at = time.time()
+            rc = bad[0]
+            log(f"a rank exited with status {rc}; waiting 30 s for the others")
+        if all(c is not None for c in codes):
+            break
+        now = time.time()
+        if (failed_at is not None and now - failed_at > 30) or now - t0 > timeout_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            return rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+# ---- measurement ---------------------------------------------------------------
+
+def timed_pass(bfs, rt, roots):
+    rt.barrier()
+    rt.backend.synchronize()
+    t_start = time.perf_counter()
+    results = [bfs.run(r) for r in roots]
+    rt.backend.synchronize()
+    rt.barrier()
+    wall_ms = (time.perf_counter() - t_start) * 1e3
+    return results, rt.comm.max_host(wall_ms)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv, args.spawn_timeout)
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            log(f"--gpus {args.gpus} requested but WORLD_SIZE=1: launch with torch.distributed.run "
-                f"--nproc-per-node {args.gpus}")
-            return 2
+        log(f"--gpus {args.gpus} but WORLD_SIZE={world}: the launcher's world size wins")
+
     import distributed_cuda_bfs_amd as dbfs
     from distributed_cuda_bfs_amd.parallel.runtime import init_runtime
     from distributed_cuda_bfs_amd.utils.metrics import harmonic_mean
 
-    N = dbfs.native
     rt = init_runtime(args.device)
     rank, nranks = rt.rank, rt.world
-    log(f"backend {rt.backend.name}, comm {rt.comm.name}, ranks {nranks}")
+    devices = rt.comm.allgather_host_i64(int(rt.backend.device_id))
+    log(f"backend {rt.backend.name}, comm {rt.comm.name}, ranks {nranks}, devices {devices}")
 
+    scale = args.scale
+    if args.weak and not args.graph:
+        lg = nranks.bit_length() - 1
+        if 1 << lg != nranks:
+            log("--weak needs a power-of-two number of ranks")
+            return 2
+        scale += lg
     if args.graph:
-        params = dbfs.read_graph(args.graph)  # every rank reads the file, shards its rows
+        params = dbfs.read_graph(args.graph)
         graph_name = os.path.basename(args.graph)
         n_vertices, n_input_edges = params.n, params.input_edges
     else:
-        params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
-        graph_name = (f"RMAT-{args.scale} (Graph500 Kronecker a=.57 b=.19 c=.19, "
+        params = dbfs.rmat_params(scale, args.edge_factor, args.seed)
+        graph_name = (f"RMAT-{scale} (Graph500 Kronecker a=.57 b=.19 c=.19, "
                       f"edge factor {args.edge_factor})")
         n_vertices, n_input_edges = params.n, params.m
     t0 = time.time()
@@ -107,24 +207,11 @@ def main() -> int:
         return 3
     warm, timed = roots[:args.warmup], roots[args.warmup:]
 
-    validated = None
-    for i, r in enumerate(warm):
+    for r in warm:
         res = bfs.run(r)
-        if i == 0 and not args.no_validate:
-            validated = bfs.validate(r)
-            log(f"validation of root {r}: {'OK' if validated else 'FAILED'}")
-            if not validated:
-                return 4
         log(f"warmup root {r}: {res.ms:.3f} ms, {res.gteps:.2f} GTEPS, depth {res.depth}")
 
-    rt.barrier()
-    rt.backend.synchronize()
-    t_start = time.perf_counter()
-    results = [bfs.run(r) for r in timed]
-    rt.backend.synchronize()
-    rt.barrier()
-    wall_ms = (time.perf_counter() - t_start) * 1e3
-    wall_ms = rt.comm.max_host(wall_ms)
+    results, wall_ms = timed_pass(bfs, rt, timed)
 
     if rank == 0:
         for r in results:
@@ -134,9 +221,32 @@ def main() -> int:
     edges = sum(r.edges for r in results)
     bfs_ms = sum(r.ms for r in results)
     value = edges / (wall_ms * 1e6)
+
+    # Second timed pass: the same roots with 32-bit levels written by the kernels.
+    narrow = bool(dict(bfs.engine.get_options()).get("narrow_levels", 0)) and args.mode in ("td", "bu", "do")
+    value_i32 = None
+    if narrow and not args.no_int32_pass:
+        bfs.engine.set_option("narrow_levels", 0)
+        bfs.run(warm[0] if warm else timed[0])
+        res32, wall32 = timed_pass(bfs, rt, timed)
+        value_i32 = sum(r.edges for r in res32) / (wall32 * 1e6)
+        bfs.engine.set_option("narrow_levels", 1)
+        log(f"int32-level pass: {value_i32:.2f} GTEPS ({wall32 / len(timed):.4f} ms/step)")
+
+    # Validation of every timed root (re-traversed after the timed windows).
+    validated = None
+    n_valid = 0
+    if not args.no_validate:
+        for r in timed:
+            bfs.run(r)
+            ok = bfs.validate(r)
+            n_valid += int(ok)
+            if not ok:
+                log(f"validation of root {r}: FAILED")
+        validated = n_valid == len(timed)
+        log(f"validated {n_valid}/{len(timed)} timed roots")
+
     if args.per_level:
-        # extra (untimed) traversals of the fastest and the slowest timed root with
-        # per-level device events
         order = sorted(results, key=lambda r: r.ms)
         bfs.engine.phase_timing = True
         profs = [bfs.run(order[0].source), bfs.run(order[-1].source)]
@@ -155,9 +265,23 @@ def main() -> int:
     prof = bfs.run(med.source)
     bfs.engine.phase_timing = False
     level_profile = [[lv["dir"], round(lv["ms"], 4), round(lv.get("comm_ms", 0.0), 4)] for lv in prof.levels]
+
     baseline = args.baseline_gteps
+    baseline_src = "--baseline-gteps" if baseline else None
+    if args.baseline_live and args.mode != "ref":
+        mode = bfs.mode
+        bfs.mode = "ref"
+        ref_roots = timed[:max(1, args.baseline_roots)]
+        bfs.run(ref_roots[0])
+        ref_res, ref_wall = timed_pass(bfs, rt, ref_roots)
+        bfs.mode = mode
+        baseline = sum(r.edges for r in ref_res) / (ref_wall * 1e6)
+        baseline_src = f"reference algorithm (--mode ref) measured live, {len(ref_roots)} roots, same graph"
+        log(f"live baseline: {baseline:.4f} GTEPS")
     if baseline is None and not args.graph and args.edge_factor == 16 and args.mode != "ref":
-        baseline = MEASURED_REF_GTEPS.get((args.scale, nranks))
+        baseline = MEASURED_REF_GTEPS.get((scale, nranks))
+        if baseline:
+            baseline_src = "reference algorithm (--mode ref) on MI355X, measured round 1 (BASELINE.md)"
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -168,10 +292,13 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(wall_ms / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if args.weak else "strong",
             "vs_baseline": (round(value / baseline, 2) if baseline else None),
-            "baseline": ("reference algorithm (--mode ref) on MI355X, BASELINE.md" if baseline else None),
+            "baseline": baseline_src,
+            "baseline_gteps": (round(baseline, 4) if baseline else None),
             "dtype": "int32",
+            "level_state_dtype": "uint8" if narrow else "int32",
+            "value_int32_levels": (round(value_i32, 4) if value_i32 is not None else None),
             "data": (f"file {graph_name}, random roots" if args.graph
                      else "synthetic (Graph500 RMAT generated on device, random roots)"),
             "config": {
@@ -184,12 +311,16 @@ def main() -> int:
                 "input_edges": n_input_edges,
                 "directed_edges": bfs.engine.global_directed_edges,
             },
+            "comm": rt.comm.name,
+            "comm_ranks": rt.comm.size,
+            "devices": [f"{'hip' if rt.is_gpu else 'cpu'}:{d}" for d in devices],
             "bfs_ms_mean": round(bfs_ms / len(results), 4),
             "harmonic_mean_gteps": round(harmonic_mean([r.gteps for r in results]), 4),
             "traversed_edges_mean": edges // len(results),
             "depth_mean": sum(r.depth for r in results) / len(results),
             "mispredicted_levels": sum(r.mispredicts for r in results),
             "validated": validated,
+            "validated_roots": (f"{n_valid}/{len(timed)}" if validated is not None else None),
             "generate_s": round(gen_s, 3),
             "level_profile": {"root": med.source, "levels": level_profile,
                               "columns": ["dir", "ms", "comm_ms"]},
@@ -201,7 +332,7 @@ def main() -> int:
                             "columns": ["dir", "ms", "gap_ms"]},
         }
         print(json.dumps(out), flush=True)
-    return 0
+    return 0 if validated in (None, True) else 4
 
 
 if __name__ == "__main__":

@@ -43,6 +43,16 @@ double Comm::max_host(double x) {
   return *std::max_element(h.begin(), h.end());
 }
 
+std::vector<int64_t> Comm::allgather_host_i64(int64_t x) {
+  const int n = size();
+  int64_t* b = scratch(static_cast<size_t>(n) + 1);
+  be_->to_device(b, &x, sizeof(x));
+  allgather(b, b + 1, sizeof(int64_t));
+  std::vector<int64_t> h(static_cast<size_t>(n));
+  be_->to_host(h.data(), b + 1, h.size() * sizeof(int64_t));
+  return h;
+}
+
 // ---- LocalComm ----------------------------------------------------------------
 
 void LocalComm::alltoall(const void* send, void* recv, size_t bytes) {

@@ -15,6 +15,7 @@
 
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -68,9 +69,27 @@ void send_msg(int fd, const std::string& s) {
   if (n) write_all(fd, s.data(), n);
 }
 
+// Largest message a peer may announce (DBFS_BOOTSTRAP_MAX_MSG bytes, default
+// 4 GiB): a bogus length from a stray or hostile connection is an error, not
+// a huge allocation.
+uint64_t max_msg_bytes() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("DBFS_BOOTSTRAP_MAX_MSG");
+    return e && *e ? std::strtoull(e, nullptr, 10) : (uint64_t(1) << 32);
+  }();
+  return v;
+}
+
+// First bytes every connecting rank sends (then its rank): rejects
+// connections that are not from this program.
+constexpr uint64_t kHelloMagic = 0x31544f4f42534642ull;  // "BFSBOOT1"
+
 std::string recv_msg(int fd) {
   uint64_t n = 0;
   read_all(fd, &n, sizeof(n));
+  if (n > max_msg_bytes())
+    throw Error("bootstrap peer announced a " + std::to_string(n) + "-byte message (limit " +
+                std::to_string(max_msg_bytes()) + ", DBFS_BOOTSTRAP_MAX_MSG)");
   std::string s(n, '\0');
   if (n) read_all(fd, &s[0], n);
   return s;
@@ -106,7 +125,8 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_port = htons(static_cast<uint16_t>(port));
-    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    // listen on the rendezvous address only (not every interface)
+    a.sin_addr = resolve(host, port).sin_addr;
     if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
       throw Error("bootstrap bind to port " + std::to_string(port) + " failed: " + std::strerror(errno));
     if (::listen(listen_fd_, nranks) != 0) throw Error("bootstrap listen failed");
@@ -121,7 +141,15 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
       int fd = ::accept(listen_fd_, nullptr, nullptr);
       if (fd < 0) throw Error("bootstrap accept failed");
       tune_socket(fd);
+      uint64_t hello = 0;
       int32_t r = -1;
+      read_all(fd, &hello, sizeof(hello));
+      if (hello != kHelloMagic) {
+        // not one of our ranks: drop it and keep waiting for the real peers
+        ::close(fd);
+        --k;
+        continue;
+      }
       read_all(fd, &r, sizeof(r));
       if (r <= 0 || r >= nranks || peers_[r] != -1) throw Error("bootstrap got bad rank " + std::to_string(r));
       peers_[r] = fd;
@@ -139,7 +167,9 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }
     tune_socket(fd);
+    const uint64_t hello = kHelloMagic;
     const int32_t r = rank;
+    write_all(fd, &hello, sizeof(hello));
     write_all(fd, &r, sizeof(r));
     peers_.assign(1, fd);
   }

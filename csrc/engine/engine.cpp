@@ -917,7 +917,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
   auto qbase_set = [&](int k) { return sparse && (k & 1) ? qbase2_.data() : qbase_.data(); };
   auto blk_set = [&](int k) { return sparse && (k & 1) ? blk_vstart2_.data() : blk_vstart_.data(); };
-  // the previous run has completed (it ended with a synchronize): stamps can be reset
+  // Mailbox stamps can be reset although the previous run did not end with a
+  // synchronize: its trailing (speculative) chain may still be executing, but
+  // every kernel that stamps a mailbox slot (scan_units, level_finish,
+  // td_sparse, init_run with a ctrl) returns at entry once ctrl->done is set,
+  // and the previous run's last stamp set it -- so nothing of that run writes
+  // a slot again.  (tests/test_gpu_engine.py::test_back_to_back_runs_*)
   for (int i = 0; i < kMailboxSlots; ++i) {
     volatile LevelMailbox* mb = mailbox_host_ + i;
     mb->level = -2;

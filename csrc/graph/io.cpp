@@ -12,6 +12,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -209,59 +211,173 @@ uint64_t fnv1a(const void* data, size_t bytes, uint64_t h = 1469598103934665603u
   for (size_t i = 0; i < bytes; ++i) { h ^= p[i]; h *= 1099511628211ull; }
   return h;
 }
-struct BinHeader {
+// Version 1 (round 1): header + row_off + col, one checksum over row_off.
+struct BinHeaderV1 {
   char magic[8];
   uint32_t version;
   uint32_t reserved;
   int64_t n, row_lo, rows, nnz, input_edges;
   uint64_t checksum;  // FNV-1a over row_off
 };
+// Version 2: header (with its own checksum) + row_off + col + per-block
+// checksums of row_off (kRowBlock entries each) and col (kColBlock entries
+// each), so a rank can map and verify only the rows it owns
+// (read_binary_csr_rows) instead of reading and hashing the whole file.
+struct BinHeaderV2 {
+  char magic[8];
+  uint32_t version;
+  uint32_t reserved;
+  int64_t n, row_lo, rows, nnz, input_edges;
+  int64_t row_block, col_block;
+  uint64_t header_sum;  // FNV-1a over the bytes before it
+};
+constexpr int64_t kRowBlock = int64_t(1) << 16;
+constexpr int64_t kColBlock = int64_t(1) << 20;
+
+// a + b * c in size_t, or an Error on overflow / negative inputs.
+size_t checked_span(size_t a, int64_t b, size_t c, const std::string& path) {
+  size_t bc = 0, out = 0;
+  if (b < 0 || __builtin_mul_overflow(static_cast<size_t>(b), c, &bc) || __builtin_add_overflow(a, bc, &out))
+    throw Error("corrupt binary CSR header (size overflow) " + path);
+  return out;
+}
+
+// Structural checks of a row range [r0, r1) of a CSR whose offsets are `ro`
+// (ro[r0 .. r1] readable) and columns `col` (global offsets): monotone offsets
+// inside [0, nnz], column ids < n.
+void check_rows(const eid_t* ro, int64_t r0, int64_t r1, const vid_t* col, int64_t nnz, int64_t n,
+                const std::string& path) {
+  for (int64_t r = r0; r < r1; ++r)
+    if (ro[r] < 0 || ro[r] > ro[r + 1] || ro[r + 1] > nnz)
+      throw Error("corrupt binary CSR: row offsets not monotone at row " + std::to_string(r) + " in " + path);
+  for (eid_t e = ro[r0]; e < ro[r1]; ++e)
+    if (static_cast<int64_t>(col[e]) >= n)
+      throw Error("corrupt binary CSR: column id " + std::to_string(col[e]) + " >= n at entry " +
+                  std::to_string(e) + " in " + path);
+}
 }  // namespace
 
 void write_binary_csr(const std::string& path, const HostCSR& g) {
-  BinHeader h{};
+  BinHeaderV2 h{};
   std::memcpy(h.magic, kBinaryMagic, 8);
-  h.version = 1;
+  h.version = 2;
   h.n = g.n;
   h.row_lo = g.row_lo;
   h.rows = g.rows;
   h.nnz = g.directed_edges();
   h.input_edges = g.input_edges;
-  h.checksum = fnv1a(g.row_off.data(), g.row_off.size() * sizeof(eid_t));
+  h.row_block = kRowBlock;
+  h.col_block = kColBlock;
+  h.header_sum = fnv1a(&h, offsetof(BinHeaderV2, header_sum));
+  std::vector<uint64_t> sums;
+  for (size_t i = 0; i < g.row_off.size(); i += kRowBlock)
+    sums.push_back(fnv1a(g.row_off.data() + i, std::min<size_t>(kRowBlock, g.row_off.size() - i) * sizeof(eid_t)));
+  for (size_t i = 0; i < g.col.size(); i += kColBlock)
+    sums.push_back(fnv1a(g.col.data() + i, std::min<size_t>(kColBlock, g.col.size() - i) * sizeof(vid_t)));
   std::string tmp = path + ".tmp";
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) throw Error("cannot write " + tmp);
   bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
   ok = ok && std::fwrite(g.row_off.data(), sizeof(eid_t), g.row_off.size(), f) == g.row_off.size();
   if (!g.col.empty()) ok = ok && std::fwrite(g.col.data(), sizeof(vid_t), g.col.size(), f) == g.col.size();
+  if (!sums.empty()) ok = ok && std::fwrite(sums.data(), sizeof(uint64_t), sums.size(), f) == sums.size();
   ok = (std::fclose(f) == 0) && ok;
   if (!ok) throw Error("short write to " + tmp);
   if (std::rename(tmp.c_str(), path.c_str()) != 0) throw Error("cannot rename " + tmp + " -> " + path);
 }
 
-HostCSR read_binary_csr(const std::string& path) {
+BinaryCsrInfo binary_csr_info(const std::string& path) {
   MappedFile mf(path);
-  if (mf.size < sizeof(BinHeader)) throw Error("truncated binary CSR " + path);
-  BinHeader h;
-  std::memcpy(&h, mf.data, sizeof(h));
-  if (std::memcmp(h.magic, kBinaryMagic, 8) != 0 || h.version != 1) throw Error("bad binary CSR header " + path);
-  const size_t need = sizeof(BinHeader) + static_cast<size_t>(h.rows + 1) * sizeof(eid_t) +
-                      static_cast<size_t>(h.nnz) * sizeof(vid_t);
+  if (mf.size < sizeof(BinHeaderV1)) throw Error("truncated binary CSR " + path);
+  BinHeaderV1 h1;
+  std::memcpy(&h1, mf.data, sizeof(h1));
+  if (std::memcmp(h1.magic, kBinaryMagic, 8) != 0 || (h1.version != 1 && h1.version != 2))
+    throw Error("bad binary CSR header " + path);
+  BinaryCsrInfo info;
+  info.version = static_cast<int>(h1.version);
+  info.n = h1.n;
+  info.row_lo = h1.row_lo;
+  info.rows = h1.rows;
+  info.nnz = h1.nnz;
+  info.input_edges = h1.input_edges;
+  if (info.n < 0 || info.n > int64_t(UINT32_MAX) || info.rows < 0 || info.nnz < 0 || info.row_lo < 0 ||
+      info.row_lo > info.n - info.rows || info.input_edges < 0)
+    throw Error("corrupt binary CSR header (n / rows / nnz out of range) " + path);
+  return info;
+}
+
+HostCSR read_binary_csr_rows(const std::string& path, int64_t lo, int64_t hi) {
+  const BinaryCsrInfo info = binary_csr_info(path);
+  if (lo < info.row_lo || hi < lo || hi > info.row_lo + info.rows)
+    throw Error("row range [" + std::to_string(lo) + ", " + std::to_string(hi) + ") outside the rows of " + path);
+  MappedFile mf(path);
+  const int64_t r0 = lo - info.row_lo, r1 = hi - info.row_lo;  // file-local rows
+  size_t hdr = sizeof(BinHeaderV1);
+  int64_t row_block = 0, col_block = 0;
+  if (info.version == 2) {
+    if (mf.size < sizeof(BinHeaderV2)) throw Error("truncated binary CSR " + path);
+    BinHeaderV2 h;
+    std::memcpy(&h, mf.data, sizeof(h));
+    if (fnv1a(&h, offsetof(BinHeaderV2, header_sum)) != h.header_sum)
+      throw Error("binary CSR header checksum mismatch " + path);
+    if (h.row_block <= 0 || h.col_block <= 0) throw Error("corrupt binary CSR header (block sizes) " + path);
+    hdr = sizeof(BinHeaderV2);
+    row_block = h.row_block;
+    col_block = h.col_block;
+  }
+  const size_t off_row = hdr;
+  const size_t off_col = checked_span(off_row, info.rows + 1, sizeof(eid_t), path);
+  const size_t off_sum = checked_span(off_col, info.nnz, sizeof(vid_t), path);
+  const int64_t nrow_blocks = row_block ? (info.rows + 1 + row_block - 1) / row_block : 0;
+  const int64_t ncol_blocks = col_block ? (info.nnz + col_block - 1) / col_block : 0;
+  const size_t need = checked_span(off_sum, nrow_blocks + ncol_blocks, sizeof(uint64_t), path);
   if (mf.size < need) throw Error("truncated binary CSR " + path);
+  const eid_t* ro = reinterpret_cast<const eid_t*>(mf.data + off_row);
+  const vid_t* col = reinterpret_cast<const vid_t*>(mf.data + off_col);
+  const uint64_t* sums = reinterpret_cast<const uint64_t*>(mf.data + off_sum);
+  if (info.version == 1) {
+    // one checksum over all offsets: verify them all (a full read in practice)
+    BinHeaderV1 h1;
+    std::memcpy(&h1, mf.data, sizeof(h1));
+    if (fnv1a(ro, static_cast<size_t>(info.rows + 1) * sizeof(eid_t)) != h1.checksum)
+      throw Error("binary CSR checksum mismatch " + path);
+  } else {
+    // the blocks of row_off[r0 .. r1] (and, after the offset checks, of the
+    // column range they name)
+    for (int64_t b = r0 / row_block; b <= r1 / row_block && b < nrow_blocks; ++b) {
+      const int64_t a = b * row_block, e = std::min(info.rows + 1, a + row_block);
+      if (fnv1a(ro + a, static_cast<size_t>(e - a) * sizeof(eid_t)) != sums[b])
+        throw Error("binary CSR checksum mismatch (row offsets block " + std::to_string(b) + ") " + path);
+    }
+  }
+  if (ro[0] != 0 || ro[info.rows] != info.nnz)
+    throw Error("corrupt binary CSR: row offsets do not span [0, nnz] in " + path);
+  for (int64_t r = r0; r < r1; ++r)
+    if (ro[r] < 0 || ro[r] > ro[r + 1] || ro[r + 1] > info.nnz)
+      throw Error("corrupt binary CSR: row offsets not monotone at row " + std::to_string(r) + " in " + path);
+  const eid_t c0 = ro[r0], c1 = ro[r1];
+  if (info.version == 2 && c1 > c0) {
+    for (int64_t b = c0 / col_block; b <= (c1 - 1) / col_block; ++b) {
+      const int64_t a = b * col_block, e = std::min(info.nnz, a + col_block);
+      if (fnv1a(col + a, static_cast<size_t>(e - a) * sizeof(vid_t)) != sums[nrow_blocks + b])
+        throw Error("binary CSR checksum mismatch (columns block " + std::to_string(b) + ") " + path);
+    }
+  }
+  check_rows(ro, r0, r1, col, info.nnz, info.n, path);
   HostCSR g;
-  g.n = h.n;
-  g.row_lo = h.row_lo;
-  g.rows = h.rows;
-  g.input_edges = h.input_edges;
-  g.row_off.resize(static_cast<size_t>(h.rows + 1));
-  std::memcpy(g.row_off.data(), mf.data + sizeof(BinHeader), g.row_off.size() * sizeof(eid_t));
-  if (fnv1a(g.row_off.data(), g.row_off.size() * sizeof(eid_t)) != h.checksum)
-    throw Error("binary CSR checksum mismatch " + path);
-  g.col.resize(static_cast<size_t>(h.nnz));
-  if (h.nnz)
-    std::memcpy(g.col.data(), mf.data + sizeof(BinHeader) + g.row_off.size() * sizeof(eid_t),
-                g.col.size() * sizeof(vid_t));
+  g.n = info.n;
+  g.row_lo = lo;
+  g.rows = hi - lo;
+  g.input_edges = info.input_edges;
+  g.row_off.resize(static_cast<size_t>(g.rows + 1));
+  for (int64_t r = 0; r <= g.rows; ++r) g.row_off[r] = ro[r0 + r] - c0;
+  g.col.assign(col + c0, col + c1);
   return g;
+}
+
+HostCSR read_binary_csr(const std::string& path) {
+  const BinaryCsrInfo info = binary_csr_info(path);
+  return read_binary_csr_rows(path, info.row_lo, info.row_lo + info.rows);
 }
 
 void write_levels(const std::string& path, const std::vector<lvl_t>& levels) {

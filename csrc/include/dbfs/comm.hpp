@@ -62,6 +62,8 @@ class Comm {
   // Host-value helpers built on the device collectives.
   virtual int64_t sum_host(int64_t x);
   virtual double max_host(double x);
+  // Every rank's x, indexed by rank (one device all-gather).
+  virtual std::vector<int64_t> allgather_host_i64(int64_t x);
   void bind_backend(Backend* be) {
     if (be != be_) scratch_.reset();
     be_ = be;
@@ -89,6 +91,7 @@ class LocalComm final : public Comm {
   void barrier() override;
   int64_t sum_host(int64_t x) override { return x; }
   double max_host(double x) override { return x; }
+  std::vector<int64_t> allgather_host_i64(int64_t x) override { return {x}; }
 };
 
 // Shared state of a group of virtual ranks living in one process.

@@ -58,8 +58,18 @@ HostCSR slice_rows(const HostCSR& full, int64_t lo, int64_t hi);
 
 // Binary CSR cache: header {magic, version, n, rows, nnz, input_edges, checksum}
 // then row_off (int64) and col (uint32).  SURVEY §5.4.
+// Version 2 adds per-block checksums (row offsets and columns) so that a rank
+// maps and verifies only its own rows; every read checks the header ranges,
+// the offsets' monotonicity and span, and that column ids are < n.
 void write_binary_csr(const std::string& path, const HostCSR& g);
 HostCSR read_binary_csr(const std::string& path);
+struct BinaryCsrInfo {
+  int version = 0;
+  int64_t n = 0, row_lo = 0, rows = 0, nnz = 0, input_edges = 0;
+};
+BinaryCsrInfo binary_csr_info(const std::string& path);
+// Global rows [lo, hi) of the cache (a shard: row_lo = lo, rebased offsets).
+HostCSR read_binary_csr_rows(const std::string& path, int64_t lo, int64_t hi);
 bool is_binary_csr(const std::string& path);
 
 // Write per-vertex levels, one per line, 2147483647 for unreached.

@@ -166,7 +166,8 @@ __global__ __launch_bounds__(kBlock) void parent_kernel(ParentArgs a) {
     const unsigned long long m = __ballot(hit);
     if (m) {
       const int l = __ffsll(static_cast<long long>(m)) - 1;
-      par = __shfl(static_cast<int>(u), l, kWave);
+      // (ids up to 2^32 - 1: shuffled as unsigned, widened without sign)
+      par = static_cast<long long>(static_cast<unsigned>(__shfl(static_cast<int>(u), l, kWave)));
       break;
     }
   }

@@ -164,6 +164,23 @@ PYBIND11_MODULE(_dbfs_native, m) {
       },
       py::arg("n"), py::arg("u"), py::arg("v"), py::arg("directed") = false);
   m.def("write_binary_csr", &write_binary_csr, py::arg("path"), py::arg("csr"));
+  m.def(
+      "binary_csr_info",
+      [](const std::string& path) {
+        BinaryCsrInfo i = binary_csr_info(path);
+        py::dict d;
+        d["version"] = i.version;
+        d["n"] = i.n;
+        d["row_lo"] = i.row_lo;
+        d["rows"] = i.rows;
+        d["nnz"] = i.nnz;
+        d["input_edges"] = i.input_edges;
+        return d;
+      },
+      py::arg("path"));
+  m.def("read_binary_csr_rows", &read_binary_csr_rows, py::arg("path"), py::arg("lo"), py::arg("hi"),
+        py::call_guard<py::gil_scoped_release>(),
+        "Global rows [lo, hi) of a binary CSR cache as a shard (only those rows' blocks are read and verified).");
   m.def("write_levels", [](const std::string& path, py::array_t<int32_t, py::array::c_style | py::array::forcecast> l) {
     write_levels(path, from_numpy<int32_t>(l));
   });
@@ -239,6 +256,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
       .def("sum_host", &Comm::sum_host, py::call_guard<py::gil_scoped_release>())
       .def("max_host", &Comm::max_host, py::call_guard<py::gil_scoped_release>())
+      .def("allgather_host_i64", &Comm::allgather_host_i64, py::call_guard<py::gil_scoped_release>())
       .def("bind_backend", [](Comm& c, std::shared_ptr<Backend> be) { c.bind_backend(be.get()); },
            py::keep_alive<1, 2>());
   m.def(

@@ -78,6 +78,11 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
             if kind == "tcp" or (not kind and not backend.is_gpu):
                 comm = N.tcp_comm(boot, backend)  # host collectives (CPU runs / debug fallback)
             else:
+                # one GPU per rank: the backend made LOCAL_RANK current
+                # (hipSetDevice) before the communicator is created
+                if "DBFS_DEVICE" not in os.environ and backend.device_id != local_rank:
+                    raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, "
+                                       f"expected LOCAL_RANK {local_rank}")
                 uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
                 comm = N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
                 del boot

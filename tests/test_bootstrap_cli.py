@@ -48,6 +48,36 @@ def test_tcp_bootstrap_three_ranks():
         assert gathered == [b"r0", b"r1", b"r2"]
 
 
+def test_tcp_bootstrap_rejects_stray_connection():
+    """A connection that does not speak the bootstrap handshake is dropped;
+    the real ranks still form the group (any host could inject a
+    fake peer or announce a huge message)."""
+    import multiprocessing as mp
+    import time
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    root = ctx.Process(target=_boot_worker, args=(0, 2, port, q))
+    root.start()
+    stray = None
+    for _ in range(200):
+        try:
+            stray = socket.create_connection(("127.0.0.1", port), timeout=1)
+            break
+        except OSError:
+            time.sleep(0.05)
+    assert stray is not None
+    stray.sendall(b"\xff" * 8 + b"\x01\x00\x00\x00")  # wrong magic, then a plausible rank
+    stray.close()
+    peer = ctx.Process(target=_boot_worker, args=(1, 2, port, q))
+    peer.start()
+    outs = sorted([q.get(timeout=60) for _ in range(2)])
+    root.join(timeout=30)
+    peer.join(timeout=30)
+    assert [o[2] for o in outs] == [[b"r0", b"r1"]] * 2
+
+
 def _run(args, **kw):
     return subprocess.run([BFS_BIN] + args, capture_output=True, text=True, timeout=120, **kw)
 
@@ -116,6 +146,52 @@ def test_bench_contract_cpu():
     assert rec["value"] > 0 and rec["validated"] is True
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in rec["config"]
+
+
+def test_bench_self_spawn_cpu():
+    """``bench.py --gpus 3`` without a launcher starts 3 rank processes itself
+    (no torchrun): one JSON line from rank 0, the communicator really formed 3
+    ranks, every timed root validated, honesty fields present."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--device", "cpu",
+                          "--scale", "10", "--steps", "3", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 3 and rec["comm_ranks"] == 3 and rec["comm"] == "tcp"
+    assert rec["devices"] == ["cpu:-1"] * 3
+    assert rec["validated"] is True and rec["validated_roots"] == "3/3"
+    assert rec["level_state_dtype"] == "uint8" and rec["value_int32_levels"] > 0
+    assert rec["config"]["parallelism"] == "1d-vertex-partition x3"
+
+
+def test_bench_self_spawn_failure_propagates():
+    """A failing rank makes the self-spawned job fail (no hang, non-zero exit)."""
+    env = dict(os.environ, DBFS_FAULT_INJECT="rank=1,level=1,kind=exit", DBFS_COMM_TIMEOUT_S="20")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu",
+                          "--scale", "9", "--steps", "2", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode != 0
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_weak_scaling_cpu():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--device", "cpu",
+                          "--scale", "9", "--weak", "--steps", "2", "--warmup", "1", "--no-int32-pass"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["scaling"] == "weak" and rec["config"]["vertices"] == 1 << 10
+    assert rec["value_int32_levels"] is None
 
 
 def test_bench_graph_file_cpu(tmp_path):

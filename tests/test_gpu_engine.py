@@ -368,6 +368,30 @@ def test_multiprocess_ranks_share_one_gpu_tcp():
     assert rec["n_gpus"] == 2 and rec["validated"] is True
 
 
+def test_bench_self_spawned_ranks_share_one_gpu():
+    """bench.py --gpus 2 WITHOUT a launcher (the parent spawns the rank
+    processes itself, as when a driver runs `python bench.py --gpus 8`): both
+    ranks run the HIP kernels on device 0, TCP collectives, every timed root
+    validated, and the JSON reports the ranks the communicator formed."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="tcp")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "18", "--steps", "3",
+           "--warmup", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["comm_ranks"] == 2 and rec["comm"] == "tcp"
+    assert rec["devices"] == ["hip:0", "hip:0"]
+    assert rec["validated"] is True and rec["validated_roots"] == "3/3"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["td", "do"])
 @pytest.mark.parametrize("sparse_edges", [0, 64, 1 << 16, 1 << 40])
@@ -464,3 +488,23 @@ def test_device_loop_several_ranks_gpu(gpu_runtime, mode):
     for rank_out in run_virtual_ranks(3, body, device="hip"):
         for (lv, same), s in zip(rank_out, srcs):
             assert same and np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
+
+
+@pytest.mark.parametrize("mode,sparse_edges", [("bu", 0), ("td", 0), ("td", 1 << 16), ("do", 1 << 16)])
+def test_back_to_back_runs_trailing_chain_gpu(gpu_runtime, mode, sparse_edges):
+    """Runs issued back to back (the device loop ends without a synchronize,
+    so the speculative chain enqueued after the last level -- bottom-up 'B',
+    dense 'T' or sparse 'S' form -- is still in flight when the next run resets
+    the mailbox): no stale stamp may leak into the next run.  Every run is
+    compared with the CPU oracle, and its records with a fresh engine's."""
+    p = dbfs.rmat_params(15, 16, 21)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    bfs.engine.set_option("td_sparse_edges", sparse_edges)
+    roots = bfs.sample_roots(6, seed=4)
+    results = [bfs.run(r) for r in roots]  # no synchronize in between
+    for r, res in zip(roots, results):
+        again = bfs.run(r)
+        assert (res.reached, res.edges, res.depth) == (again.reached, again.edges, again.depth)
+        exp, _ = dbfs.cpu_bfs(csr, r)
+        assert np.array_equal(bfs.levels(), exp)

@@ -78,6 +78,94 @@ def test_binary_cache_roundtrip(tmp_path):
     assert back.input_edges == csr.input_edges
 
 
+def test_binary_cache_shard_reads(tmp_path):
+    """Version-2 cache: a rank reads only its rows (rebased offsets, global
+    column ids) and the shards concatenate to the whole graph."""
+    p = dbfs.rmat_params(12, 8, 5)
+    csr = dbfs.host_csr_from_params(p)
+    f = str(tmp_path / "g.csr")
+    dbfs.ops.write_binary_csr(f, csr)
+    info = dbfs.native.binary_csr_info(f)
+    assert info["version"] == 2 and info["n"] == csr.n and info["nnz"] == csr.directed_edges
+    ro, col = np.asarray(csr.row_off), np.asarray(csr.col)
+    part = dbfs.native.Partition(csr.n, 3)
+    cols = []
+    for r in range(3):
+        lo, hi = part.lo(r), part.hi(r)
+        sh = dbfs.native.read_binary_csr_rows(f, lo, hi)
+        assert sh.row_lo == lo and sh.rows == hi - lo and sh.n == csr.n
+        assert np.array_equal(np.asarray(sh.row_off), ro[lo:hi + 1] - ro[lo])
+        cols.append(np.asarray(sh.col))
+    assert np.array_equal(np.concatenate(cols), col)
+    with pytest.raises(RuntimeError, match="outside"):
+        dbfs.native.read_binary_csr_rows(f, 0, csr.n + 1)
+
+
+def _corrupt(src, dst, offset, data):
+    b = bytearray(open(src, "rb").read())
+    if offset is None:
+        b = b[:data]
+    else:
+        b[offset:offset + len(data)] = data
+    open(dst, "wb").write(bytes(b))
+
+
+def test_binary_cache_rejects_corruption(tmp_path):
+    """Truncated or corrupted caches raise instead of handing out-of-range ids
+    or offsets to the device (header trusted, col unchecked)."""
+    import struct
+    p = dbfs.rmat_params(10, 8, 4)
+    csr = dbfs.host_csr_from_params(p)
+    f = str(tmp_path / "g.csr")
+    dbfs.ops.write_binary_csr(f, csr)
+    hdr = 8 + 4 + 4 + 5 * 8 + 2 * 8 + 8
+    n_off = (csr.rows + 1) * 8
+    cases = {
+        "trunc": (None, hdr + 10),
+        "trunc_cols": (None, hdr + n_off + 16),
+        "header_rows": (16 + 16, struct.pack("<q", -5)),          # rows field (header checksum)
+        "header_nnz_huge": (16 + 24, struct.pack("<q", 1 << 62)),  # nnz field
+        "row_off": (hdr + 8 * 5, struct.pack("<q", 1 << 40)),      # an offset (block checksum)
+        "col": (hdr + n_off + 4 * 7, struct.pack("<I", 0xFFFFFFF0)),  # a column id
+    }
+    for name, (off, data) in cases.items():
+        g = str(tmp_path / f"{name}.csr")
+        _corrupt(f, g, off, data)
+        with pytest.raises(RuntimeError):
+            dbfs.read_graph(g)
+
+
+def test_binary_cache_v1_structural_checks(tmp_path):
+    """Round-1 (version 1) caches are still read, with the structural checks:
+    a column id >= n is rejected even though v1 checksums only the offsets."""
+    import struct
+    p = dbfs.rmat_params(9, 8, 3)
+    csr = dbfs.host_csr_from_params(p)
+    ro = np.asarray(csr.row_off, dtype=np.int64)
+    col = np.asarray(csr.col, dtype=np.uint32).copy()
+
+    def fnv(b):
+        h = 1469598103934665603
+        for x in b:
+            h = ((h ^ x) * 1099511628211) & (2 ** 64 - 1)
+        return h
+
+    def write(path, col_arr):
+        hdr = b"DBFSCSR1" + struct.pack("<II", 1, 0) + struct.pack(
+            "<qqqqq", csr.n, 0, csr.rows, csr.directed_edges, csr.input_edges) + struct.pack("<Q", fnv(ro.tobytes()))
+        open(path, "wb").write(hdr + ro.tobytes() + col_arr.tobytes())
+
+    good = str(tmp_path / "v1.csr")
+    write(good, col)
+    back = dbfs.read_graph(good)
+    assert np.array_equal(np.asarray(back.col), col)
+    col[3] = csr.n + 7
+    bad = str(tmp_path / "v1bad.csr")
+    write(bad, col)
+    with pytest.raises(RuntimeError, match="column id"):
+        dbfs.read_graph(bad)
+
+
 def test_levels_out_format(tmp_path):
     f = str(tmp_path / "l.txt")
     dbfs.ops.write_levels(f, np.array([0, 1, U], dtype=np.int32))
