@@ -64,7 +64,7 @@ class CpuBackend final : public Backend {
   void update_frontier(const UpdateArgs& a) override {
     bool use_bytes = a.cand_bytes != nullptr;
     if (a.ctrl) {
-      if (a.ctrl->done || a.ctrl->dir != 'T') return;
+      if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
       use_bytes = use_bytes && a.ctrl->bytes != 0;
     }
     const int64_t nunits = div_up(a.words, kUnitWords);
@@ -155,7 +155,7 @@ class CpuBackend final : public Backend {
   void free_mapped(void* h) override { std::free(h); }
 
   void scan_units(const ScanArgs& a) override {
-    if (a.ctrl && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+    if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
     const int64_t nchunks = div_up(a.nunits, kScanChunk);
     int64_t c = 0, d = 0;
     for (int64_t k = 0; k < nchunks; ++k) {
@@ -231,7 +231,7 @@ class CpuBackend final : public Backend {
     int64_t q = a.q;
     bool bytes = a.next_bytes != nullptr;
     if (a.ctrl) {
-      if (a.ctrl->done || a.ctrl->dir != 'T') return;
+      if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
       q = a.dev_stats[0];
       bytes = a.ctrl->bytes != 0;
       if (a.clear_qv)
@@ -255,7 +255,7 @@ class CpuBackend final : public Backend {
   }
 
   void level_finish(const LevelFinishArgs& a) override {
-    if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+    if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
     level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
     *a.ctrl = c;
@@ -310,6 +310,9 @@ class CpuBackend final : public Backend {
   }
 
   void list_scatter(const ListScatterArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    if (a.reset_lists)
+      for (int r = 0; r < a.nranks; ++r) a.reset_lists[static_cast<int64_t>(r) * (a.list_cap + 1)] = 0;
     for (int r = 0; r < a.nranks; ++r) {
       const vid_t* list = a.lists + static_cast<int64_t>(r) * (a.list_cap + 1);
       for (vid_t k = 0; k < list[0]; ++k) {
@@ -346,10 +349,59 @@ class CpuBackend final : public Backend {
           }
         }
         a.visited[w] = vis | out;
+        a.new_frontier[w] = a.merge ? (a.new_frontier[w] | out) : out;
+      }
+      a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + cnt : cnt;
+      a.unit_deg[u] = a.merge ? a.unit_deg[u] + deg : deg;
+    }
+  }
+
+  // Head pass of a split bottom-up level: only hub heads (all-reduced hub
+  // bits) and owned heads (owned frontier slice) are tested -- the global
+  // frontier is deliberately not read (on the GPU it is still in flight).
+  void bu_head(const BuHeadArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    const int64_t nunits = div_up(a.words, kUnitWords);
+    const int64_t lo = a.g.lo, hi = a.g.lo + a.g.rows;
+    for (int64_t u = 0; u < nunits; ++u) {
+      int64_t cnt = 0, deg = 0;
+      for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
+        const word_t vis = a.visited[w];
+        word_t out = 0;
+        for (int b = 0; b < 64; ++b) {
+          if ((vis >> b) & 1ull) continue;
+          const int64_t k = a.g.nz_pref[w] + __builtin_popcountll(~a.zdeg[w] & ((1ull << b) - 1ull));
+          const vid_t h = a.g.nz_head[k];
+          bool found = false;
+          if (h & kHubFlag) {
+            const vid_t x = h & ~kHubFlag;
+            found = (a.hub_front[x >> 6] >> (x & 63)) & 1ull;
+          } else if (h >= lo && h < hi) {
+            found = test_bit(a.frontier_own, static_cast<int64_t>(h) - lo);
+          }
+          if (!found) continue;
+          out |= 1ull << b;
+          put_level(a.level, a.level8, w * 64 + b, a.new_level);
+          ++cnt;
+          deg += a.g.nz_row_off[k + 1] - a.g.nz_row_off[k];
+        }
+        a.visited[w] = vis | out;
         a.new_frontier[w] = out;
       }
       a.unit_cnt[u] = cnt;
       a.unit_deg[u] = deg;
+    }
+  }
+
+  void hub_local(const HubLocalArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
+    for (int64_t w = 0; w < div_up(a.g.nhubs, 64); ++w) {
+      word_t m = 0;
+      for (int b = 0; b < 64 && w * 64 + b < a.g.nhubs; ++b) {
+        const int64_t r = static_cast<int64_t>(a.g.hub_vertex[w * 64 + b]) - a.g.lo;
+        if (r >= 0 && r < a.g.rows && test_bit(a.frontier_own, r)) m |= 1ull << b;
+      }
+      a.out[w] = m;
     }
   }
 

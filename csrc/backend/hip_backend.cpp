@@ -35,6 +35,9 @@ class HipBackend final : public Backend {
     DBFS_CHECK(dev >= 0 && dev < n, "HIP device " + std::to_string(dev) + " not present (" + std::to_string(n) + " visible)");
     HIP_CHECK(hipSetDevice(dev_));
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming));
     hipDeviceProp_t prop{};
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
@@ -47,7 +50,11 @@ class HipBackend final : public Backend {
   ~HipBackend() override {
     hipSetDevice(dev_);
     hipStreamSynchronize(st_);
+    hipStreamSynchronize(side_);
     for (hipEvent_t e : events_) hipEventDestroy(e);
+    hipEventDestroy(fork_ev_);
+    hipEventDestroy(join_ev_);
+    hipStreamDestroy(side_);
     if (scan_tmp_) hipFree(scan_tmp_);
     if (pinned_) hipHostFree(pinned_);
     hipStreamDestroy(st_);
@@ -60,6 +67,21 @@ class HipBackend final : public Backend {
   int device_id() const override { return dev_; }
   double wall_clock_khz() const override { return clock_khz_; }
   void* stream_handle() override { return st_; }
+  void* comm_stream_handle() override { return forked_ ? side_ : st_; }
+  void fork_side() override {
+    on();
+    DBFS_CHECK(!forked_, "fork_side: a side region is already open");
+    HIP_CHECK(hipEventRecord(fork_ev_, st_));
+    HIP_CHECK(hipStreamWaitEvent(side_, fork_ev_, 0));
+    forked_ = true;
+  }
+  void join_side() override {
+    on();
+    if (!forked_) return;
+    HIP_CHECK(hipEventRecord(join_ev_, side_));
+    HIP_CHECK(hipStreamWaitEvent(st_, join_ev_, 0));
+    forked_ = false;
+  }
 
   void* alloc(size_t bytes) override {
     on();
@@ -102,6 +124,7 @@ class HipBackend final : public Backend {
   }
   void synchronize() override {
     on();
+    join_side();
     wait_stream();
   }
   bool stream_idle() override {
@@ -190,6 +213,8 @@ class HipBackend final : public Backend {
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
+  void bu_head(const BuHeadArgs& a) override { on(); kern::bu_head(a, st_); chk(); }
+  void hub_local(const HubLocalArgs& a) override { on(); kern::hub_local(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
@@ -298,6 +323,10 @@ class HipBackend final : public Backend {
   int dev_;
   void* pinned_ = nullptr;
   hipStream_t st_ = nullptr;
+  // communication side stream (fork_side / join_side)
+  hipStream_t side_ = nullptr;
+  hipEvent_t fork_ev_ = nullptr, join_ev_ = nullptr;
+  bool forked_ = false;
   std::string arch_;
   int cus_ = 0;
   double clock_khz_ = 0.0;

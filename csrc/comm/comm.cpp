@@ -146,7 +146,8 @@ void VirtualComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   auto& sl = g_->slots();
   sl[rank_].send = buf;
   g_->barrier();
-  std::vector<int64_t> acc(count, 0), tmp(count);
+  // wrapping (two's-complement) sums, as RCCL's (see TcpComm::allreduce_sum_i64)
+  std::vector<uint64_t> acc(count, 0), tmp(count);
   for (int r = 0; r < size(); ++r) {
     be_->to_host(tmp.data(), sl[r].send, count * sizeof(int64_t));
     for (size_t i = 0; i < count; ++i) acc[i] += tmp[i];

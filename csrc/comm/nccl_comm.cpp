@@ -36,7 +36,9 @@ namespace dbfs {
 
 namespace {
 inline ncclComm_t C(void* p) { return static_cast<ncclComm_t>(p); }
-inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->stream_handle()); }
+// collectives go to the backend's communication stream (the compute stream
+// unless the engine opened a side region: Backend::fork_side)
+inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->comm_stream_handle()); }
 }  // namespace
 
 std::string NcclComm::unique_id() {

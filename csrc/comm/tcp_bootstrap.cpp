@@ -244,11 +244,13 @@ void TcpComm::allgather(const void* send, void* recv, size_t bytes) {
 
 void TcpComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   auto all = boot_->allgather(fetch(buf, count * sizeof(int64_t)));
-  std::vector<int64_t> acc(count, 0);
+  // two's-complement (wrapping) sums, as RCCL's: the engine also reduces
+  // disjoint bit sets (hub frontier words) and, on no-op chains, stale blocks
+  std::vector<uint64_t> acc(count, 0);
   for (const auto& s : all)
     for (size_t i = 0; i < count; ++i) {
-      int64_t x;
-      std::memcpy(&x, s.data() + i * sizeof(int64_t), sizeof(x));
+      uint64_t x;
+      std::memcpy(&x, s.data() + i * sizeof(uint64_t), sizeof(x));
       acc[i] += x;
     }
   be_->to_device(buf, acc.data(), count * sizeof(int64_t));

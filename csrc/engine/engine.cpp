@@ -70,6 +70,9 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
+  else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
+  else if (name == "list_cap_factor") o.list_cap_factor = v;
+  else if (name == "bu_split") o.bu_split = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -96,7 +99,10 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
-          {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0}};
+          {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
+          {"list_form_edges", static_cast<double>(o.list_form_edges)},
+          {"list_cap_factor", o.list_cap_factor},
+          {"bu_split", o.bu_split ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -414,7 +420,11 @@ void Engine::alloc_bitmap_state() {
   qscan_ = DBuf<int64_t>(be_, static_cast<size_t>(g_.rows() + 1));
   qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
-  stats_ = DBuf<int64_t>(be_, 8);
+  // several ranks: kStatsBlocks blocks of [local count, local degree sum,
+  // global count, global degree sum, hub frontier words] (see stats_block)
+  stats_stride_ = div_up(4 + div_up(g_.nhubs(), kWordBits), 8) * 8;
+  stats_ = DBuf<int64_t>(be_, static_cast<size_t>(exchange() ? kStatsBlocks * stats_stride_ : std::max<int64_t>(stats_stride_, 8)));
+  be_.memset_async(stats_.data(), 0, stats_.bytes());
   if (g_.nhubs() > 0) hub_front_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(g_.nhubs(), kWordBits)));
   // Zero-degree (and padding) vertices can never be discovered: they start out
   // visited, so bottom-up steps skip them without touching row_off.
@@ -901,6 +911,30 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     be_.memset_async(sparse_ticket_.data(), 0, sparse_ticket_.bytes());
     sparse_ready_ = true;
   }
+  // Several ranks, list form: owner lists at a fixed stride (list_stride_ + 1
+  // entries per peer, count first), exchanged cap + 1 entries per peer; the
+  // counts are zeroed once here and by each consuming list_scatter after.
+  const int P = part_.nranks;
+  const int64_t list_max = xc && opt_.list_form_edges > 0 && opt_.mode != Mode::BottomUp
+                               ? std::min<int64_t>(opt_.list_form_edges, std::max<int64_t>(W, 1024))
+                               : 0;
+  if (list_max > 0 && list_stride_ < list_max) {
+    list_stride_ = list_max;
+    const size_t n = static_cast<size_t>(P) * static_cast<size_t>(list_stride_ + 1);
+    dl_send_lists_ = DBuf<vid_t>(be_, n);
+    dl_recv_lists_ = DBuf<vid_t>(be_, n);
+    be_.memset_async(dl_send_lists_.data(), 0, dl_send_lists_.bytes());
+    be_.memset_async(dl_recv_lists_.data(), 0, dl_recv_lists_.bytes());
+  }
+  // Split bottom-up levels: hub frontier bits reduced with the totals (needs
+  // the hub-encoded non-empty-row view the head pass reads).
+  const bool split_ok = xc && opt_.bu_split && gv.nhubs > 0 && gv.nz_pref && gv.nz_head && opt_.bu_nz_view &&
+                        opt_.bu_compact && !opt_.bu_packed && opt_.mode != Mode::TopDown;
+  const int64_t hub_words = div_up(gv.nhubs, kWordBits);
+  // stats block of level L's output (L = -1: the seed); one block with one rank
+  auto sblk = [&](int L) {
+    return xc ? stats_.data() + static_cast<int64_t>((L + 1) % kStatsBlocks) * stats_stride_ : stats_.data();
+  };
   if (n_active_ < 0) {
     // (outside the timed window, once) the mean degree of an edge's endpoint
     // (sum deg^2 / sum deg) predicts the edges of level 1's frontier (the
@@ -961,6 +995,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // seeds the LevelCtrl and stamps level -1)
   InitRunArgs ia = init_args(source, fr_own(1), xc ? nullptr : ctrl_.data(), init,
                              xc ? nullptr : mailbox_dev_ + slot(-1));
+  ia.stats = sblk(-1);
   if (sparse) {
     ia.qbase = qbase_.data();
     ia.blk_vstart = blk_vstart_.data();
@@ -968,10 +1003,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     ia.frontier_clear = frontier_[0].data();
   }
   be_.init_run(ia);
-  auto finish_ranks = [&](int level, bool seed, char expect_dir) {
-    comm_.allreduce_sum_i64(stats_.data() + 2, 2);
+  // Several ranks: level `level`'s totals (stats block) all-reduced -- with the
+  // owned hubs' frontier bits when `carry` (a split bottom-up level may
+  // follow) -- then level_finish decides and stamps.
+  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool carry) {
+    int64_t* blk = sblk(level);
+    comm_.allreduce_sum_i64(blk + 2, static_cast<size_t>(2 + (carry ? hub_words : 0)));
     LevelFinishArgs fa;
-    fa.stats = stats_.data();
+    fa.stats = blk;
     fa.ctrl = ctrl_.data();
     fa.ctrl_init = init;
     fa.rec = seed ? nullptr : rec_at(level);
@@ -979,11 +1018,28 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     fa.level = level;
     fa.seed = seed;
     fa.expect_dir = expect_dir;
+    fa.expect_cap = cap;
     be_.level_finish(fa);
   };
-  if (xc) finish_ranks(-1, true, 0);
+  // owned hubs' bits of level `level`'s output frontier (own slice `fr`)
+  auto hub_bits = [&](int level, const word_t* fr, char expect_dir, int64_t cap, bool guard) {
+    HubLocalArgs hl;
+    hl.g = gv;
+    hl.frontier_own = fr;
+    hl.out = reinterpret_cast<word_t*>(sblk(level) + 4);
+    hl.ctrl = guard ? ctrl_.data() : nullptr;
+    hl.expect_dir = expect_dir;
+    hl.expect_cap = cap;
+    be_.hub_local(hl);
+  };
+  // the seed carries hub bits when level 0 is bottom-up (bu mode)
+  const bool seed_carry = split_ok && init.dir == 'B';
+  if (xc) {
+    if (seed_carry) hub_bits(-1, fr_own(1), 0, 0, false);
+    finish_ranks(-1, true, 0, 0, seed_carry);
+  }
 
-  auto scan = [&](int level, bool seed, char expect_dir) {
+  auto scan = [&](int level, bool seed, char expect_dir, int64_t cap) {
     ScanArgs sa;
     sa.unit_cnt = unit_cnt_.data();
     sa.unit_deg = unit_deg_.data();
@@ -991,7 +1047,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.part_cnt = part_cnt_.data();
     sa.part_deg = part_deg_.data();
     sa.ticket = ticket_.data();
-    sa.stats = stats_.data();
+    sa.stats = sblk(level);
     sa.qscan = qscan_set(level + 1);
     sa.ctrl = ctrl_.data();
     sa.rec = seed ? nullptr : rec_at(level);
@@ -999,9 +1055,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.level = level;
     sa.seed = seed;
     sa.expect_dir = expect_dir;
+    sa.expect_cap = cap;
     sa.finish = !xc;
     be_.scan_units(sa);
-    if (xc) finish_ranks(level, seed, expect_dir);
   };
   // Frontier double buffer: the seed is frontier_[1]; level L reads
   // frontier_[(L + 1) & 1] and writes the other one.
@@ -1019,8 +1075,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
 
   const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), 2048));
   std::vector<std::pair<int, int>> evs;
-  std::vector<char> enq_dir;   // direction each level was (last) enqueued with
-  std::vector<char> enq_form;  // ... and its chain form ('T', 'S', 'B')
+  std::vector<char> enq_dir;     // direction each level was (last) enqueued with
+  std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B'; several ranks: 'L' list form)
+  std::vector<int64_t> enq_cap;  // ... list form: the global frontier edges its lists hold
+  std::vector<char> enq_carry;   // ... several ranks: its reduction carries the hub bits
   // Enqueue level L's chain for direction d: top-down = compact + td_expand +
   // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
   // so a chain enqueued for the wrong direction is a handful of no-op launches.
@@ -1034,30 +1092,50 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (host_timing)
       htl.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   };
-  auto enqueue_level = [&](int L, char d) {
+  // List-form capacity for a level predicted to have mf frontier edges (0: dense)
+  auto list_cap_for = [&](double mf) -> int64_t {
+    if (list_max <= 0) return 0;
+    const double want = std::max(1024.0, mf * opt_.list_cap_factor);
+    if (want > static_cast<double>(list_max)) return 0;
+    int64_t c = 1024;
+    while (static_cast<double>(c) < want) c <<= 1;
+    return std::min(c, list_max);
+  };
+  auto enqueue_level = [&](int L, char d, int64_t cap) {
     hmark("enqueue " + std::to_string(L) + d);
     if (static_cast<size_t>(L) >= enq_dir.size()) {
       inject_fault(L);
       enq_dir.resize(static_cast<size_t>(L) + 1);
       enq_form.resize(static_cast<size_t>(L) + 1);
+      enq_cap.resize(static_cast<size_t>(L) + 1);
+      enq_carry.resize(static_cast<size_t>(L) + 1);
       evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
     }
-    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up; the
-    // previous level's form decides what hands this one its work list
+    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up, 'L' list
+    // top-down (several ranks); the previous level's form decides what hands
+    // this one its work list
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
+    const bool in_carry = L == 0 ? seed_carry : enq_carry[static_cast<size_t>(L - 1)] != 0;
     enq_dir[L] = d == 'B' ? 'B' : 'T';
     enq_form[L] = d;
+    enq_cap[L] = d == 'L' ? cap : 0;
+    // carry the hub bits out of dense and bottom-up chains (the ones a
+    // bottom-up level follows); list chains are the small levels
+    enq_carry[L] = split_ok && d != 'L';
+    const int64_t chain_cap = enq_cap[L];
     const int cur = (L + 1) & 1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
+    const bool split = xc && d == 'B' && split_ok && in_carry;
     // several ranks: the level's input frontier to every rank (all-gather of
     // the owned slices) and into the replicated visited bitmap -- before a
     // bottom-up level, and before top-down levels of the td mode (fewer
     // candidates); not predicated: on a no-op chain it only refreshes bits
-    // every owner already has
-    if (xc && (d == 'B' || opt_.mode != Mode::DirOpt)) {
+    // every owner already has.  A split bottom-up level runs its head pass
+    // while the all-gather is in flight (communication stream).
+    if (xc && !split && (d == 'B' || opt_.mode != Mode::DirOpt)) {
       comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
       be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
     }
@@ -1113,7 +1191,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
       sp.first = pf != 'T';
       be_.td_sparse(sp);
-    } else if (d == 'T') {
+    } else if (d == 'T' || d == 'L') {
       // a sparse level (or the seed) already handed over the work list
       const bool listed = sparse && (pf == 'S' || pf == 'I');
       if (!listed) compact();
@@ -1127,30 +1205,60 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ta.clear_frontier = frontier_[cur].data();
       }
       ta.visited = visited_.data();
-      ta.next = next_.data();
-      ta.next_bytes = next_bytes_.data();
       ta.ctrl = ctrl_.data();
-      ta.dev_stats = stats_.data();
+      ta.dev_stats = sblk(L - 1);
       ta.grid = td_grid;
-      be_.td_expand(ta);
       UpdateArgs tu = ua;
-      tu.cand = next_.data();
-      tu.cand_bytes = next_bytes_.data();
-      if (xc) {
-        // candidates to their owners: the byte map (if this level used it)
-        // packed into `next`, one bitmap slice per peer, `next` re-zeroed
-        if (next_bytes_.data()) {
-          PackArgs pa;
-          pa.bytes = next_bytes_.data();
-          pa.next = next_.data();
-          pa.words = GW;
-          pa.ctrl = ctrl_.data();
-          be_.pack_bytes(pa);
-        }
-        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
-        be_.memset_async(next_.data(), 0, next_.bytes());
-        tu.cand = recv_.data();
+      if (d == 'L') {
+        // owner-routed lists: candidates appended to their owner's list
+        // (capacity >= the global frontier edges while the chain is live)
+        DBFS_CHECK(xc && chain_cap > 0 && chain_cap <= list_stride_, "list-form chain without lists");
+        ta.lists = dl_send_lists_.data();
+        ta.list_cap = list_stride_;
+        ta.part = part_.part;
+        ta.max_mf = chain_cap;
+        be_.td_expand(ta);
+        std::vector<int64_t> cnt(static_cast<size_t>(P), chain_cap + 1), off(static_cast<size_t>(P));
+        for (int r = 0; r < P; ++r) off[r] = static_cast<int64_t>(r) * (list_stride_ + 1);
+        comm_.alltoallv(dl_send_lists_.data(), cnt.data(), off.data(), dl_recv_lists_.data(), cnt.data(), off.data(),
+                        sizeof(vid_t));
+        ListScatterArgs la;
+        la.lists = dl_recv_lists_.data();
+        la.nranks = P;
+        la.list_cap = list_stride_;
+        la.lo = g_.lo();
+        la.cand = cand_.data();
+        la.reset_lists = dl_send_lists_.data();
+        la.ctrl = ctrl_.data();
+        la.max_mf = chain_cap;
+        be_.list_scatter(la);
+        tu.cand = cand_.data();
         tu.cand_bytes = nullptr;
+        tu.nchunks = 1;
+        tu.clear_cand = true;
+        tu.max_mf = chain_cap;
+      } else {
+        ta.next = next_.data();
+        ta.next_bytes = next_bytes_.data();
+        be_.td_expand(ta);
+        tu.cand = next_.data();
+        tu.cand_bytes = next_bytes_.data();
+        if (xc) {
+          // candidates to their owners: the byte map (if this level used it)
+          // packed into `next`, one bitmap slice per peer, `next` re-zeroed
+          if (next_bytes_.data()) {
+            PackArgs pa;
+            pa.bytes = next_bytes_.data();
+            pa.next = next_.data();
+            pa.words = GW;
+            pa.ctrl = ctrl_.data();
+            be_.pack_bytes(pa);
+          }
+          comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
+          be_.memset_async(next_.data(), 0, next_.bytes());
+          tu.cand = recv_.data();
+          tu.cand_bytes = nullptr;
+        }
       }
       tu.force = false;
       tu.frontier = fr_own(cur ^ 1);
@@ -1178,18 +1286,52 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();
-      if (gv.nhubs > 0) {
-        HubGatherArgs hg;
-        hg.g = gv;
-        hg.frontier = frontier_[cur].data();
-        hg.hub_front = hub_front_.data();
-        hg.ctrl = ctrl_.data();
-        be_.hub_gather(hg);
-        ba.hub_front = hub_front_.data();
+      if (split) {
+        // head pass (hub bits from the previous level's reduction, owned
+        // slice of the frontier) overlapped with the all-gather on the side
+        // stream; the full pass merges after the join
+        const word_t* hub_in = reinterpret_cast<const word_t*>(sblk(L - 1) + 4);
+        be_.fork_side();
+        comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
+        BuHeadArgs bh;
+        bh.g = gv;
+        bh.zdeg = ba.zdeg;
+        bh.hub_front = hub_in;
+        bh.frontier_own = fr_own(cur);
+        bh.visited = vis_own;
+        bh.new_frontier = ba.new_frontier;
+        bh.level = ba.level;
+        bh.level8 = ba.level8;
+        bh.new_level = ba.new_level;
+        bh.words = W;
+        bh.unit_cnt = unit_cnt_.data();
+        bh.unit_deg = unit_deg_.data();
+        bh.ctrl = ctrl_.data();
+        be_.bu_head(bh);
+        be_.join_side();
+        ba.hub_front = hub_in;
+        ba.merge = true;
+        be_.bu_step(ba);
+        // remote slices into the replicated visited bitmap (top-down filter)
+        be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
+      } else {
+        if (gv.nhubs > 0) {
+          HubGatherArgs hg;
+          hg.g = gv;
+          hg.frontier = frontier_[cur].data();
+          hg.hub_front = hub_front_.data();
+          hg.ctrl = ctrl_.data();
+          be_.hub_gather(hg);
+          ba.hub_front = hub_front_.data();
+        }
+        be_.bu_step(ba);
       }
-      be_.bu_step(ba);
     }
-    if (d != 'S') scan(L, false, enq_dir[L]);
+    if (d != 'S') scan(L, false, enq_dir[L], chain_cap);
+    if (xc) {
+      if (enq_carry[L]) hub_bits(L, fr_own(cur ^ 1), enq_dir[L], chain_cap, true);
+      finish_ranks(L, false, enq_dir[L], chain_cap, enq_carry[L] != 0);
+    }
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
     hmark("enqueued " + std::to_string(L));
   };
@@ -1204,19 +1346,43 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   //     predicted exactly, so no chain is wasted.
   //   otherwise: level L + 1 is enqueued before the stamp, predicted to keep
   //     level L's direction (two wasted chains per direction change).
+  // Several ranks: a top-down chain also has a form -- list ('L', capacity
+  // from the predicted frontier edges) or dense ('T'); a list chain whose
+  // level turns out to have more frontier edges than its capacity is a no-op
+  // and is re-enqueued like a mispredicted direction.
   int nlev = 0;
   LevelCtrl hc = init;  // host mirror for the prediction
   int64_t prev_nf = 0, prev_mf = 0;
   // top-down form of level L whose frontier has (about) mf edges: sparse when
   // small, and never right after a bottom-up level (its input bitmap is
-  // still set, so a sparse level would have no clean bitmap to write)
-  auto td_form = [&](int L, double mf) {
+  // still set, so a sparse level would have no clean bitmap to write); with
+  // several ranks list form when the lists stay small
+  auto td_form = [&](int L, double mf, int64_t* cap) {
+    *cap = 0;
+    if (xc) {
+      *cap = list_cap_for(mf);
+      return *cap > 0 ? 'L' : 'T';
+    }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
     return sparse && pf != 'B' && mf <= static_cast<double>(opt_.td_sparse_edges) ? 'S' : 'T';
   };
-  enqueue_level(0, init.dir == 'B' ? 'B' : td_form(0, 0.0));
+  // the chain enqueued for level L is live for a level with direction `dir`
+  // and mf global frontier edges
+  auto chain_valid = [&](int L, char dir, int64_t mf) {
+    if (enq_dir[L] != dir) return false;
+    return enq_form[L] != 'L' || mf <= enq_cap[L];
+  };
+  {
+    int64_t cap0 = 0;
+    // level 0 (the source's row): list form with the largest lists
+    const char f0 = init.dir == 'B' ? 'B' : (xc ? (list_max > 0 ? 'L' : 'T') : td_form(0, 0.0, &cap0));
+    enqueue_level(0, f0, f0 == 'L' ? list_max : 0);
+  }
   for (int L = 0;; ++L) {
-    if (!opt_.device_loop_predict) enqueue_level(L + 1, enq_dir[L]);  // dense top-down or bottom-up
+    if (!opt_.device_loop_predict) {
+      // dense top-down or bottom-up, one more level ahead
+      enqueue_level(L + 1, enq_dir[L], 0);
+    }
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
     hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {
@@ -1224,16 +1390,21 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       break;
     }
     const char actual = static_cast<char>(mb->next_dir);
-    if (actual != enq_dir[L]) ++res.mispredicts;
+    const int64_t nf = mb->n_f, mf = mb->m_f;
+    const bool valid = chain_valid(L, actual, mf);
+    if (!valid) ++res.mispredicts;
     if (!opt_.device_loop_predict) {
-      if (actual != enq_dir[L]) {
-        enqueue_level(L, actual);
-        enqueue_level(L + 1, actual);
+      if (!valid) {
+        enqueue_level(L, actual, 0);
+        enqueue_level(L + 1, actual, 0);
       }
       continue;
     }
-    const int64_t nf = mb->n_f, mf = mb->m_f;
-    if (actual != enq_dir[L]) enqueue_level(L, actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf)));
+    if (!valid) {
+      int64_t cap = 0;
+      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap);
+      enqueue_level(L, f, cap);
+    }
     // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
     auto grow = [](int64_t cur, int64_t prev) {
       if (prev <= 0) return static_cast<double>(cur) * static_cast<double>(cur);
@@ -1255,7 +1426,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
                       &scratch);
     prev_nf = nf;
     prev_mf = mf;
-    enqueue_level(L + 1, hc.dir == 'B' ? 'B' : td_form(L + 1, emf));
+    int64_t lcap = 0;
+    const char f = hc.dir == 'B' ? 'B' : td_form(L + 1, emf, &lcap);
+    enqueue_level(L + 1, f, lcap);
   }
   // The traversal is complete once the last stamp is seen: the stamping
   // workgroup ran after all of that level's work (and every earlier level's).

@@ -227,6 +227,7 @@ struct UpdateArgs {
   // Device loop: runs only when ctrl->dir == 'T'; reads cand_bytes when
   // ctrl->bytes, else cand (both given).
   const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;  // list-form chain: live only while ctrl->m_f <= max_mf
 };
 
 // Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
@@ -253,6 +254,10 @@ struct ScanArgs {
   // Device loop: the level's chain was enqueued for this direction (0: any);
   // when ctrl->dir differs, the chain was a no-op and so is the scan.
   int32_t expect_dir = 0;
+  // ... and, for a multi-rank list-form top-down chain, only valid while the
+  // level's global frontier edges fit its lists (ctrl->m_f <= expect_cap;
+  // 0: no bound).
+  int64_t expect_cap = 0;
   // Device loop: run level_ctrl_finish here (one rank); several ranks reduce
   // the totals first and finish in level_finish.
   bool finish = true;
@@ -270,7 +275,15 @@ struct LevelFinishArgs {
   int32_t level = 0;
   bool seed = false;
   int32_t expect_dir = 0;
+  int64_t expect_cap = 0;  // see ScanArgs::expect_cap
 };
+
+// A device-loop chain's kernels run only when the chain is live: the level is
+// not done, its direction is the one the chain was enqueued for, and (list-form
+// top-down chains) the global frontier edges fit the chain's lists.
+DBFS_HD bool chain_live(const LevelCtrl& c, int32_t dir, int64_t cap) {
+  return !c.done && (dir == 0 || c.dir == dir) && (cap <= 0 || c.m_f <= cap);
+}
 
 // Host-loop statistics mailbox (pinned, device-mapped).  After a level's
 // totals are final (scan, plus the all-reduce on several ranks) one tiny
@@ -376,6 +389,10 @@ struct TdArgs {
   // zero the input vertices' words of clear_frontier (clear_qv: entry -> row).
   const vid_t* clear_qv = nullptr;
   word_t* clear_frontier = nullptr;
+  // Device loop, several ranks, list form (`lists` set): live only while the
+  // global frontier edges ctrl->m_f <= max_mf (= list_cap: no list can
+  // overflow, every rank decides alike); else a no-op the host re-enqueues.
+  int64_t max_mf = 0;
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)
@@ -386,6 +403,11 @@ struct ListScatterArgs {
   int64_t list_cap = 0;
   int64_t lo = 0;
   word_t* cand = nullptr;
+  // Device loop: the send lists' counts to zero once the exchange has read
+  // them (the next list-form chain appends from zero), and the chain guard.
+  vid_t* reset_lists = nullptr;
+  const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;
 };
 
 // next[w] |= bits of bytes[64 w .. 64 w + 63]; bytes cleared (multi-rank
@@ -422,6 +444,46 @@ struct BuArgs {
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'
+  // Second half of a split bottom-up level (BuHeadArgs ran first): the head
+  // pass's results stay -- new_frontier words are OR-ed, unit statistics
+  // added -- and its vertices are already visited.  Hub kernel, compacted.
+  bool merge = false;
+};
+
+// First half of a split bottom-up level (several ranks): while the frontier
+// all-gather is still in flight on the communication stream, every owned
+// unvisited vertex whose row head (its highest-degree neighbour) is a hub in
+// the frontier (hub bits all-reduced with the previous level's totals) or an
+// owned frontier vertex is settled.  Writes new_frontier (every owned word),
+// visited, levels and unit statistics like bu_step; bu_step(merge) then
+// finishes the level once the all-gather has landed.
+struct BuHeadArgs {
+  ShardView g;                       // needs the non-empty-row view and hub-encoded heads
+  const word_t* zdeg = nullptr;      // owned slice
+  const word_t* hub_front = nullptr; // all hubs' frontier bits (g.nhubs bits)
+  const word_t* frontier_own = nullptr;  // owned slice of the current frontier
+  word_t* visited = nullptr;         // owned slice
+  word_t* new_frontier = nullptr;    // owned slice (fully overwritten)
+  lvl_t* level = nullptr;
+  uint8_t* level8 = nullptr;
+  lvl_t new_level = 0;
+  int64_t words = 0;
+  int64_t* unit_cnt = nullptr;
+  int64_t* unit_deg = nullptr;
+  const LevelCtrl* ctrl = nullptr;   // runs only when ctrl->dir == 'B'
+};
+
+// Frontier bits of the hubs this rank owns (bit h = new frontier bit of
+// hub_vertex[h] when lo <= hub_vertex[h] < lo + rows, else 0), every hub word
+// written: summed over ranks (disjoint bits) it is the hubs' global frontier,
+// reduced together with the level totals.  Chain guard as ScanArgs.
+struct HubLocalArgs {
+  ShardView g;
+  const word_t* frontier_own = nullptr;  // owned slice of the new frontier
+  word_t* out = nullptr;                 // ceil(nhubs / 64) words
+  const LevelCtrl* ctrl = nullptr;
+  int32_t expect_dir = 0;
+  int64_t expect_cap = 0;
 };
 
 // hub_front bit h = frontier bit of g.hub_vertex[h] (frontier global); in the
@@ -533,6 +595,15 @@ class Backend {
   virtual std::string name() const = 0;
   virtual int device_id() const { return -1; }
   virtual void* stream_handle() { return nullptr; }
+  // Communication stream.  Collectives are enqueued on comm_stream_handle():
+  // the compute stream itself, unless a side region is open.  fork_side()
+  // makes the side stream wait for everything enqueued on the compute stream
+  // so far and routes the following collectives to it, so kernels enqueued
+  // meanwhile overlap them; join_side() makes the compute stream wait for the
+  // side stream's work and routes collectives back.  (CPU: no-ops.)
+  virtual void* comm_stream_handle() { return stream_handle(); }
+  virtual void fork_side() {}
+  virtual void join_side() {}
   // Rate of the device wall clock the kernels stamp level records with (ticks
   // per ms; 0: no device clock, records carry no times).
   virtual double wall_clock_khz() const { return 0.0; }
@@ -594,6 +665,8 @@ class Backend {
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
+  virtual void bu_head(const BuHeadArgs& a) = 0;
+  virtual void hub_local(const HubLocalArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;

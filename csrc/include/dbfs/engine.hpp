@@ -128,6 +128,20 @@ struct EngineOptions {
   // 0 disables.  td_sparse_grid: its workgroups.
   int64_t td_sparse_edges = int64_t(1) << 16;
   int64_t td_sparse_grid = 256;
+  // Device loop, several ranks: top-down levels whose frontier is predicted to
+  // have at most this many edges exchange owner-routed vertex lists (list
+  // form, per-peer capacity list_cap_factor x the prediction, rounded to a
+  // power of two, at most min(this, slice words)) instead of N/P-bit slices;
+  // a level whose global frontier edges exceed its chain's capacity is
+  // re-enqueued dense (every rank sees the same totals).  0 disables.
+  int64_t list_form_edges = int64_t(1) << 16;
+  double list_cap_factor = 4.0;
+  // Device loop, several ranks, hub LDS on: the hub frontier bits travel with
+  // each level's totals reduction, so a bottom-up level settles the vertices
+  // whose head is a frontier hub (or an owned frontier vertex) while the
+  // frontier all-gather is still in flight on the communication stream, and
+  // finishes the rest after it (bu_head + bu_step merge).
+  bool bu_split = true;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
@@ -236,6 +250,14 @@ class Engine {
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
+  // Several ranks (device loop): level L's totals (and carried hub bits) go to
+  // stats block (L + 1) % kStatsBlocks, so a mispredicted chain's
+  // (unpredicated) reduction never touches the block the re-enqueued chain
+  // reads.  stats_stride_: int64 entries per block.
+  static constexpr int kStatsBlocks = 3;
+  int64_t stats_stride_ = 8;
+  DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
+  int64_t list_stride_ = 0;
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;
   // device loop, sparse top-down levels: a second work-list set (level L

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
 
 __global__ void level_finish_kernel(LevelFinishArgs a) {
   if (threadIdx.x != 0) return;
-  if (!a.seed && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+  if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
   LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
   level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
   if (!a.seed) {
@@ -242,12 +242,12 @@ constexpr int kUnitsPerBlock = kBlock / kWave;
 static_assert(kUnitWords == kWave, "one word per lane in update/compact");
 
 __device__ __forceinline__ void wave_unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
-                                                      int64_t* unit_deg) {
+                                                      int64_t* unit_deg, bool add = false) {
   cnt = wave_sum(cnt);
   deg = wave_sum(deg);
   if (lane_id() == 0) {
-    unit_cnt[unit] = cnt;
-    unit_deg[unit] = deg;
+    unit_cnt[unit] = add ? unit_cnt[unit] + cnt : cnt;
+    unit_deg[unit] = add ? unit_deg[unit] + deg : deg;
   }
 }
 
@@ -277,7 +277,7 @@ __device__ __forceinline__ word_t gather_byte_bits(uint8_t* p) {
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
-    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int lane = lane_id();
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;
   // uniform: no block takes a ticket
-  if (a.ctrl && (a.ctrl->done || (a.expect_dir && a.ctrl->dir != a.expect_dir))) return;
+  if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   long long q = a.q, m = a.m;
   bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
   if (a.ctrl) {
-    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     bytes = a.ctrl->bytes != 0;
     check = a.ctrl->check_visited != 0;
     q = a.dev_stats[0];
@@ -786,7 +786,11 @@ __global__ __launch_bounds__(kBlock) void widen_levels_kernel(const uint8_t* __r
 
 // Received owner lists -> candidate bits of the owned slice.
 __global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
   const int r = blockIdx.y;
+  // the send lists were read by the exchange (stream-ordered before this
+  // kernel): their counts restart from zero for the next list-form chain
+  if (a.reset_lists && blockIdx.x == 0 && threadIdx.x == 0) a.reset_lists[static_cast<int64_t>(r) * (a.list_cap + 1)] = 0;
   const vid_t* list = a.lists + static_cast<int64_t>(r) * (a.list_cap + 1);
   const int64_t n = list[0];
   for (int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; k < n;
@@ -1049,7 +1053,8 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (lane < kWords) s_res[lane] = 0ull;
   if (total == 0) {
-    if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
+    // (merge: the head pass already wrote these words)
+    if (lane < nw && !a.merge) a.new_frontier[w0 + lane] = 0ull;
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1211,7 +1216,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   __builtin_amdgcn_wave_barrier();
   if (lane < nw) {
     const word_t res = s_res[lane];
-    a.new_frontier[w0 + lane] = res;
+    a.new_frontier[w0 + lane] = a.merge ? (res | a.new_frontier[w0 + lane]) : res;
     if (res) a.visited[w0 + lane] = ~um | res;
   }
 }
@@ -1275,7 +1280,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       long long cnt = 0, deg = 0;
       bu_wave_compact<kPacked, true, kUnitWords, kQueueLen>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
                                                             cnt, deg, s_q + wave * kQueueLen);
-      wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg);
+      wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg, a.merge);
     }
     return;
   }
@@ -1309,8 +1314,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
         c += s_c[group * kUnitWaves + k];
         d += s_d[group * kUnitWaves + k];
       }
-      a.unit_cnt[u] = c;
-      a.unit_deg[u] = d;
+      a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + c : c;
+      a.unit_deg[u] = a.merge ? a.unit_deg[u] + d : d;
     }
     __syncthreads();
   }
@@ -1325,6 +1330,75 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
   const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);
   const word_t m = __ballot(bit);
   if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
+}
+
+// Head pass of a split bottom-up level (BuHeadArgs): one wave per 64-word unit,
+// one word per step (lane = vertex).  An unvisited vertex's hub-encoded head
+// (dense non-empty-row view) is tested in the all-reduced hub frontier bits
+// (64 KiB, L2-resident) or, when it is an owned vertex, in the owned frontier
+// slice; anything else waits for bu_step(merge) after the all-gather.  Every
+// owned word of new_frontier and every unit's statistics are written.
+__global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  stamp_level_start(a.ctrl);
+  const int lane = lane_id();
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if (unit >= nunits) return;
+  const int64_t w0 = unit * kUnitWords;
+  const int64_t nw = min<int64_t>(kUnitWords, a.words - w0);
+  // the words of the unit, one per lane (visited includes zero-degree and padding)
+  const word_t vis_l = lane < nw ? a.visited[w0 + lane] : ~0ull;
+  const word_t zd_l = lane < nw ? a.zdeg[w0 + lane] : ~0ull;
+  const int64_t nzw = (a.g.rows + kWordBits - 1) / kWordBits;  // words of the non-empty-row view
+  const int64_t pref_l = (lane < nw && w0 + lane < nzw) ? a.g.nz_pref[w0 + lane] : 0;
+  const int64_t lo = a.g.lo, hi = a.g.lo + a.g.rows;
+  long long cnt = 0, deg = 0;
+  for (int j = 0; j < nw; ++j) {
+    const word_t vis = readlane64(vis_l, j);
+    word_t res = 0;
+    if (vis != ~0ull) {  // uniform
+      const word_t zd = readlane64(zd_l, j);
+      bool found = false;
+      eid_t d = 0;
+      if (!((vis >> lane) & 1ull)) {
+        // unvisited implies non-zero degree (zero-degree bits are pre-set)
+        const int64_t k = readlane_i64(pref_l, j) + __popcll(~zd & ((1ull << lane) - 1ull));
+        const vid_t u = a.g.nz_head[k];
+        if (u & kHubFlag) {
+          const vid_t h = u & ~kHubFlag;
+          found = (a.hub_front[h >> 6] >> (h & 63)) & 1ull;
+        } else if (u >= lo && u < hi) {
+          const int64_t r = static_cast<int64_t>(u) - lo;
+          found = (a.frontier_own[r >> 6] >> (r & 63)) & 1ull;
+        }
+        if (found) d = a.g.nz_row_off[k + 1] - a.g.nz_row_off[k];
+      }
+      res = __ballot(found);
+      if (found) {
+        store_level(a.level, a.level8, (w0 + j) * 64 + lane, a.new_level);
+        cnt += 1;
+        deg += d;
+      }
+      if (lane == 0 && res) a.visited[w0 + j] = vis | res;
+    }
+    if (lane == 0) a.new_frontier[w0 + j] = res;
+  }
+  wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
+}
+
+// Owned hubs' bits of the new frontier (HubLocalArgs): one wave per hub word.
+__global__ __launch_bounds__(kBlock) void hub_local_kernel(HubLocalArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int64_t h = w * kWave + lane_id();
+  bool bit = false;
+  if (h < a.g.nhubs) {
+    const int64_t r = static_cast<int64_t>(a.g.hub_vertex[h]) - a.g.lo;
+    bit = r >= 0 && r < a.g.rows && ((a.frontier_own[r >> 6] >> (r & 63)) & 1ull);
+  }
+  const word_t m = __ballot(bit);
+  if (lane_id() == 0 && w * kWave < a.g.nhubs) a.out[w] = m;
 }
 
 // Zero-degree / padding mask of the owned slice (computed once per graph).
@@ -1411,7 +1485,10 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   if (a.ctrl) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;
-    td_expand_kernel<TdOut::Dyn, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+    if (a.lists)
+      td_expand_kernel<TdOut::Lists, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+    else
+      td_expand_kernel<TdOut::Dyn, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
     return;
   }
   if (a.m <= 0 || a.q <= 0) return;
@@ -1537,6 +1614,16 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   else
     a.compact ? DBFS_BU(false, true) : DBFS_BU(false, false);
 #undef DBFS_BU
+}
+
+void bu_head(const BuHeadArgs& a, hipStream_t st) {
+  if (a.words <= 0) return;
+  bu_head_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
+}
+
+void hub_local(const HubLocalArgs& a, hipStream_t st) {
+  if (a.g.nhubs <= 0) return;
+  hub_local_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {

@@ -26,6 +26,8 @@ void pack_bytes(const PackArgs& a, hipStream_t st);
 void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
+void bu_head(const BuHeadArgs& a, hipStream_t st);
+void hub_local(const HubLocalArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 

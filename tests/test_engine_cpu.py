@@ -381,6 +381,67 @@ def test_device_loop_several_ranks(P, mode, predict):
             assert ra == rb and ta == tb
 
 
+@pytest.mark.parametrize("knobs", [
+    {},                                             # defaults: list form, split bottom-up
+    {"list_form_edges": 0},                         # dense top-down chains only
+    {"bu_split": 0},                                # unsplit bottom-up chains
+    {"list_cap_factor": 0.01},                      # capacities too small: list chains re-enqueued dense
+    {"device_loop_predict": 0},                     # no prediction: two wasted chains per switch
+])
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_device_loop_list_form_and_split_bottom_up(P, knobs):
+    """Several ranks, device loop: list-form top-down chains (owner lists
+    exchanged with a fixed-capacity all-to-all-v, capacity checked against the
+    global frontier edges on every rank) and split bottom-up levels (head pass
+    on the all-reduced hub bits while the frontier all-gather is in flight,
+    then the merging full pass) give the host loop's levels and records."""
+    p = dbfs.rmat_params(12, 16, 31)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    srcs = [int(v) for v in np.nonzero(deg > 0)[0][[0, 55, 700, 1500]]]
+
+    def body(rt):
+        dev, host = dbfs.BFS(p, rt, mode="do"), dbfs.BFS(p, rt, mode="do")
+        for k, v in knobs.items():
+            dev.engine.set_option(k, v)
+        host.engine.set_option("device_loop", 0)
+        assert dev.graph.nhubs > 0
+        out = []
+        for s in srcs:
+            a, b = dev.run(s), host.run(s)
+            strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+            out.append((dev.levels(), strip(a), strip(b), (a.reached, a.edges, a.depth), (b.reached, b.edges, b.depth),
+                        a.mispredicts))
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        mis = 0
+        for (ld, ra, rb, ta, tb, m), s in zip(rank_out, srcs):
+            assert np.array_equal(ld, _oracle(csr, s))
+            assert ra == rb and ta == tb
+            mis += m
+        if knobs.get("list_cap_factor", 1) < 1:
+            assert mis > 0  # undersized list chains were replaced
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_bottom_up_mode_split_several_ranks(P):
+    """bu mode on several ranks: the seed's reduction carries the hub bits, so
+    level 0 is already a split bottom-up level."""
+    p = dbfs.rmat_params(11, 16, 13)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    srcs = [int(v) for v in np.nonzero(deg > 0)[0][[3, 400]]]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="bu")
+        return [(b.run(s), b.levels())[1] for s in srcs]
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for lv, s in zip(rank_out, srcs):
+            assert np.array_equal(lv, _oracle(csr, s))
+
+
 @pytest.mark.parametrize("case", [(1, [], [], 0), (2, [0], [1], 1), (5, [0, 1], [1, 2], 4),
                                   (130, list(range(128)), list(range(1, 129)), 129),
                                   (130, list(range(128)), list(range(1, 129)), 0)])

@@ -508,3 +508,49 @@ def test_back_to_back_runs_trailing_chain_gpu(gpu_runtime, mode, sparse_edges):
         assert (res.reached, res.edges, res.depth) == (again.reached, again.edges, again.depth)
         exp, _ = dbfs.cpu_bfs(csr, r)
         assert np.array_equal(bfs.levels(), exp)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"list_cap_factor": 0.01}, {"bu_split": 0, "list_form_edges": 0}])
+def test_list_form_and_split_bottom_up_gpu(gpu_runtime, knobs):
+    """Several-rank device loop on the GPU kernels: list-form top-down chains
+    (td_expand lists under the chain guard, all-to-all-v, list_scatter with the
+    count reset) and split bottom-up levels (bu_head_kernel on the reduced hub
+    bits, the all-gather on the side stream, bu_hub_kernel merging) -- one RCCL
+    rank with the exchange forced (ncclSend/Recv and ncclAllGather on the side
+    stream) and 3 / 8 virtual ranks, against the CPU oracle and the host loop."""
+    from distributed_cuda_bfs_amd.parallel.runtime import Runtime
+
+    N = dbfs.native
+    be = gpu_runtime.backend
+    comm = N.nccl_comm(N.nccl_unique_id(), 0, 1, be)
+    rt = Runtime(backend=be, comm=comm)
+    p = dbfs.rmat_params(16, 16, 37)
+    csr = dbfs.host_csr_from_params(p)
+    strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+    dev = dbfs.BFS(p, rt, mode="do", force_exchange=True)
+    for k, v in knobs.items():
+        dev.engine.set_option(k, v)
+    host = dbfs.BFS(p, rt, mode="do", force_exchange=True)
+    host.engine.set_option("device_loop", 0)
+    mis = 0
+    for src in dev.sample_roots(4, seed=17):
+        a, b = dev.run(src), host.run(src)
+        mis += a.mispredicts
+        assert np.array_equal(dev.levels(), dbfs.cpu_bfs(csr, src)[0])
+        assert strip(a) == strip(b) and (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+    if knobs.get("list_cap_factor", 1) < 1:
+        assert mis > 0
+    comm.barrier()
+
+    srcs = [7, 4321, 60000]
+
+    def body(r):
+        d = dbfs.BFS(p, r, mode="do")
+        for k, v in knobs.items():
+            d.engine.set_option(k, v)
+        return [(d.run(s), d.levels())[1] for s in srcs]
+
+    for P in (3, 8):
+        for rank_out in run_virtual_ranks(P, body, device="hip"):
+            for lv, s in zip(rank_out, srcs):
+                assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
