@@ -254,15 +254,21 @@ class HipBackend final : public Backend {
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {
     on();
-    unsigned long long* count = nullptr;
-    HIP_CHECK(hipMalloc(&count, sizeof(unsigned long long)));
-    HIP_CHECK(hipMemsetAsync(count, 0, sizeof(unsigned long long), st_));
-    kern::select_hubs(deg, n, min_deg, hub_vertex, hub_idx, count, st_);
+    // indices in vertex order (identical on every rank): per-word counts,
+    // exclusive scan, assignment
+    const int64_t words = div_up(std::max<int64_t>(n, 1), kWordBits);
+    eid_t* cnt = nullptr;
+    HIP_CHECK(hipMalloc(&cnt, static_cast<size_t>(words + 1) * sizeof(eid_t)));
+    HIP_CHECK(hipMemsetAsync(cnt, 0, static_cast<size_t>(words + 1) * sizeof(eid_t), st_));
+    kern::hub_count(deg, n, min_deg, cnt, st_);
     chk();
-    unsigned long long h = 0;
-    HIP_CHECK(hipMemcpyAsync(&h, count, sizeof(h), hipMemcpyDeviceToHost, st_));
+    exclusive_scan(cnt, words);
+    kern::hub_assign(deg, n, min_deg, cnt, hub_vertex, hub_idx, st_);
+    chk();
+    eid_t h = 0;
+    HIP_CHECK(hipMemcpyAsync(&h, cnt + words, sizeof(h), hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
-    HIP_CHECK(hipFree(count));
+    HIP_CHECK(hipFree(cnt));
     return static_cast<int64_t>(h);
   }
   void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {

@@ -1307,6 +1307,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         bh.unit_cnt = unit_cnt_.data();
         bh.unit_deg = unit_deg_.data();
         bh.ctrl = ctrl_.data();
+        static const bool head_probe = [] {
+          const char* e = std::getenv("DBFS_DEBUG_BU_HEAD");
+          return !(e && *e == '0');
+        }();
+        bh.probe = head_probe;
         be_.bu_head(bh);
         be_.join_side();
         ba.hub_front = hub_in;
@@ -1357,10 +1362,17 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // small, and never right after a bottom-up level (its input bitmap is
   // still set, so a sparse level would have no clean bitmap to write); with
   // several ranks list form when the lists stay small
-  auto td_form = [&](int L, double mf, int64_t* cap) {
+  // (exact: mf is the level's actual frontier edges -- a re-enqueue, which
+  // must be live: the lists then hold at least mf entries, or the chain is dense)
+  auto td_form = [&](int L, double mf, int64_t* cap, bool exact) {
     *cap = 0;
     if (xc) {
       *cap = list_cap_for(mf);
+      if (exact && *cap > 0 && static_cast<double>(*cap) < mf) {
+        int64_t c = *cap;
+        while (static_cast<double>(c) < mf && c < list_max) c <<= 1;
+        *cap = static_cast<double>(std::min(c, list_max)) >= mf ? std::min(c, list_max) : 0;
+      }
       return *cap > 0 ? 'L' : 'T';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
@@ -1375,7 +1387,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   {
     int64_t cap0 = 0;
     // level 0 (the source's row): list form with the largest lists
-    const char f0 = init.dir == 'B' ? 'B' : (xc ? (list_max > 0 ? 'L' : 'T') : td_form(0, 0.0, &cap0));
+    const char f0 = init.dir == 'B' ? 'B' : (xc ? (list_max > 0 ? 'L' : 'T') : td_form(0, 0.0, &cap0, false));
     enqueue_level(0, f0, f0 == 'L' ? list_max : 0);
   }
   for (int L = 0;; ++L) {
@@ -1402,7 +1414,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     }
     if (!valid) {
       int64_t cap = 0;
-      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap);
+      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
       enqueue_level(L, f, cap);
     }
     // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
@@ -1427,7 +1439,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     prev_nf = nf;
     prev_mf = mf;
     int64_t lcap = 0;
-    const char f = hc.dir == 'B' ? 'B' : td_form(L + 1, emf, &lcap);
+    const char f = hc.dir == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
     enqueue_level(L + 1, f, lcap);
   }
   // The traversal is complete once the last stamp is seen: the stamping

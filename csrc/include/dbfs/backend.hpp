@@ -471,6 +471,7 @@ struct BuHeadArgs {
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // runs only when ctrl->dir == 'B'
+  bool probe = true;                 // false (diagnostics): settle nothing, only write the words
 };
 
 // Frontier bits of the hubs this rank owns (bit h = new frontier bit of

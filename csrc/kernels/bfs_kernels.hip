@@ -1359,11 +1359,12 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
     word_t res = 0;
     if (vis != ~0ull) {  // uniform
       const word_t zd = readlane64(zd_l, j);
+      const int64_t pref = readlane_i64(pref_l, j);
       bool found = false;
       eid_t d = 0;
-      if (!((vis >> lane) & 1ull)) {
+      if (a.probe && !((vis >> lane) & 1ull)) {
         // unvisited implies non-zero degree (zero-degree bits are pre-set)
-        const int64_t k = readlane_i64(pref_l, j) + __popcll(~zd & ((1ull << lane) - 1ull));
+        const int64_t k = pref + __popcll(~zd & ((1ull << lane) - 1ull));
         const vid_t u = a.g.nz_head[k];
         if (u & kHubFlag) {
           const vid_t h = u & ~kHubFlag;

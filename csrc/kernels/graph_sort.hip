@@ -178,20 +178,27 @@ __global__ __launch_bounds__(kBlock) void nz_fill_kernel(const eid_t* __restrict
 
 // Hubs = vertices of degree >= min_deg, indexed in wave-ballot order (one
 // atomic per wave).
-__global__ __launch_bounds__(kBlock) void select_hubs_kernel(const uint32_t* __restrict__ deg, int64_t n,
-                                                            uint32_t min_deg, vid_t* __restrict__ hub_vertex,
-                                                            uint32_t* __restrict__ hub_idx,
-                                                            unsigned long long* count) {
+// Hub selection in two passes so that every rank numbers the hubs alike (hub
+// index = number of hubs with a smaller vertex id): the split bottom-up levels
+// of several ranks all-reduce hub frontier bits by index.
+// Pass 1: hubs per 64-vertex word.
+__global__ __launch_bounds__(kBlock) void hub_count_kernel(const uint32_t* __restrict__ deg, int64_t n,
+                                                          uint32_t min_deg, eid_t* __restrict__ cnt) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const unsigned long long m = __ballot(v < n && deg[v] >= min_deg);
+  if (lane_id() == 0 && (v >> 6) * 64 < n) cnt[v >> 6] = __popcll(m);
+}
+
+// Pass 2 (cnt exclusive-scanned): index = hubs before the word + rank in it.
+__global__ __launch_bounds__(kBlock) void hub_assign_kernel(const uint32_t* __restrict__ deg, int64_t n,
+                                                           uint32_t min_deg, const eid_t* __restrict__ cnt,
+                                                           vid_t* __restrict__ hub_vertex,
+                                                           uint32_t* __restrict__ hub_idx) {
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool hub = v < n && deg[v] >= min_deg;
   const unsigned long long m = __ballot(hub);
-  const int lane = lane_id();
-  unsigned long long base = 0;
-  const int leader = m ? __ffsll(static_cast<long long>(m)) - 1 : 0;
-  if (m && lane == leader) base = atomicAdd(count, static_cast<unsigned long long>(__popcll(m)));
-  base = __shfl(base, leader, kWave);
   if (v < n) {
-    const unsigned long long slot = base + mask_rank(m);
+    const unsigned long long slot = static_cast<unsigned long long>(cnt[v >> 6]) + mask_rank(m);
     if (hub) hub_vertex[slot] = static_cast<vid_t>(v);
     hub_idx[v] = hub ? static_cast<uint32_t>(slot) : 0xFFFFFFFFu;
   }
@@ -224,11 +231,16 @@ void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t word
                                                                           nz_row_off, nz_head);
 }
 
-void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex, uint32_t* hub_idx,
-                 unsigned long long* count, hipStream_t st) {
+void hub_count(const uint32_t* deg, int64_t n, uint32_t min_deg, eid_t* cnt, hipStream_t st) {
   if (n <= 0) return;
-  select_hubs_kernel<<<static_cast<unsigned>((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(deg, n, min_deg, hub_vertex,
-                                                                                         hub_idx, count);
+  hub_count_kernel<<<static_cast<unsigned>((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(deg, n, min_deg, cnt);
+}
+
+void hub_assign(const uint32_t* deg, int64_t n, uint32_t min_deg, const eid_t* cnt, vid_t* hub_vertex,
+                uint32_t* hub_idx, hipStream_t st) {
+  if (n <= 0) return;
+  hub_assign_kernel<<<static_cast<unsigned>((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(deg, n, min_deg, cnt,
+                                                                                        hub_vertex, hub_idx);
 }
 
 void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out, hipStream_t st) {

@@ -56,9 +56,11 @@ void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid
 void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts, hipStream_t st);
 void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t words, const eid_t* nz_pref,
              eid_t* nz_row_off, vid_t* nz_head, hipStream_t st);
-// count must be zeroed by the caller
-void select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex, uint32_t* hub_idx,
-                 unsigned long long* count, hipStream_t st);
+// hub selection: cnt[w] = hubs among vertices [64 w, 64 w + 64) (ceil(n / 64)
+// entries); after an exclusive scan of cnt, hub index = hubs with a smaller id
+void hub_count(const uint32_t* deg, int64_t n, uint32_t min_deg, eid_t* cnt, hipStream_t st);
+void hub_assign(const uint32_t* deg, int64_t n, uint32_t min_deg, const eid_t* cnt, vid_t* hub_vertex,
+                uint32_t* hub_idx, hipStream_t st);
 // list must hold `rows` entries; count is one device counter
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);

@@ -16,7 +16,12 @@ DATA = os.path.join(REPO, "tests", "data")
 
 @pytest.fixture(scope="module")
 def asan_bin():
-    out = subprocess.run(["make", "-j8", "asan"], cwd=REPO, capture_output=True, text=True, timeout=900)
+    # (pytest-xdist workers each run this fixture: serialise the build)
+    import fcntl
+    os.makedirs(os.path.join(REPO, "build-asan"), exist_ok=True)
+    with open(os.path.join(REPO, "build-asan", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        out = subprocess.run(["make", "-j8", "asan"], cwd=REPO, capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     return ASAN_BIN
 
