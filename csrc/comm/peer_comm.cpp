@@ -1,0 +1,332 @@
+// Peer-memory communicator: collectives as stream-ordered kernels over
+// IPC-mapped windows (see dbfs/comm.hpp, csrc/kernels/peer_kernels.hip).
+//
+// Window layout (per rank, uncached device memory, exported over IPC):
+//   [0, 4096)                       flag words, one per sender (monotonic seq)
+//   4096 + ((parity * P) + s) * slot payload slot written by sender s
+// Collective number `seq` uses parity seq & 1.  A sender reuses a parity slot
+// (seq + 2) only after it has waited for every peer's seq + 1, which each peer
+// pushed after it had unpacked seq -- so two slots per sender suffice, provided
+// every collective involves every rank (all of these do) and a rank's
+// collectives are totally ordered on its streams (the engine joins the side
+// stream before issuing on the compute stream again).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dbfs/comm.hpp"
+#include "../kernels/launch.hpp"
+
+namespace dbfs {
+
+#define HIP_CHECK(expr)                                                                          \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      ::dbfs::raise_error(__FILE__, __LINE__, std::string("HIP error ") + hipGetErrorString(e_) + \
+                                                  " in " #expr);                                 \
+  } while (0)
+
+namespace {
+constexpr size_t kFlagBytes = 4096;
+inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->comm_stream_handle()); }
+}  // namespace
+
+PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes)
+    : boot_(std::move(boot)), inner_(std::move(inner)), slot_(slot_bytes) {
+  DBFS_CHECK(be.kind() == DeviceKind::HIP, "PeerComm requires a HIP backend");
+  DBFS_CHECK(boot_ && inner_, "PeerComm needs a bootstrap and an inner communicator");
+  rank_ = boot_->rank();
+  size_ = boot_->size();
+  DBFS_CHECK(size_ <= kern::kMaxPeers, "PeerComm supports at most 16 ranks");
+  DBFS_CHECK(inner_->rank() == rank_ && inner_->size() == size_, "inner communicator does not match the bootstrap");
+  DBFS_CHECK(slot_ >= 4096 && slot_ % 256 == 0, "PeerComm slot size must be a multiple of 256 B (>= 4 KiB)");
+  bind_backend(&be);
+  // Every step that can fail locally is agreed over the bootstrap, so all
+  // ranks either build the communicator or all throw (no rank is left waiting
+  // in a bootstrap exchange its peers never join).
+  std::string local_err;
+  hipIpcMemHandle_t h{};
+  try {
+    HIP_CHECK(hipSetDevice(be.device_id()));
+    const size_t total = kFlagBytes + 2 * static_cast<size_t>(size_) * slot_;
+    void* w = nullptr;
+    HIP_CHECK(hipExtMallocWithFlags(&w, total, hipDeviceMallocUncached));
+    win_ = static_cast<char*>(w);
+    HIP_CHECK(hipMemset(win_, 0, total));
+    HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&ticket_), sizeof(unsigned)));
+    HIP_CHECK(hipMemset(ticket_, 0, sizeof(unsigned)));
+    HIP_CHECK(hipDeviceSynchronize());
+    void* dptr = nullptr;
+    err_host_ = static_cast<uint64_t*>(be.alloc_mapped(sizeof(uint64_t), &dptr));
+    err_dev_ = static_cast<uint64_t*>(dptr);
+    HIP_CHECK(hipIpcGetMemHandle(&h, win_));
+  } catch (const std::exception& e) {
+    local_err = e.what();
+  }
+  const auto all = boot_->allgather(local_err.empty() ? std::string(reinterpret_cast<const char*>(&h), sizeof(h))
+                                                      : std::string());
+  auto agree = [&](const std::string& what) {
+    // every rank's status; throw on all ranks if any failed
+    const auto st = boot_->allgather(local_err);
+    for (int p = 0; p < size_; ++p)
+      if (!st[p].empty()) {
+        release();
+        throw Error("PeerComm " + what + " failed on rank " + std::to_string(p) + ": " + st[p]);
+      }
+  };
+  agree("window allocation / export");
+  peer_.assign(static_cast<size_t>(size_), nullptr);
+  try {
+    for (int p = 0; p < size_; ++p) {
+      if (p == rank_) {
+        peer_[p] = win_;
+        continue;
+      }
+      DBFS_CHECK(all[p].size() == sizeof(hipIpcMemHandle_t), "PeerComm: bad IPC handle from a peer");
+      hipIpcMemHandle_t ph;
+      std::memcpy(&ph, all[p].data(), sizeof(ph));
+      void* m = nullptr;
+      HIP_CHECK(hipIpcOpenMemHandle(&m, ph, hipIpcMemLazyEnablePeerAccess));
+      peer_[p] = static_cast<char*>(m);
+    }
+  } catch (const std::exception& e) {
+    local_err = e.what();
+  }
+  agree("window mapping");
+  // a wait kernel that timed out leaves its seq in the error word: the host's
+  // waits (stream synchronise, mailbox spins) turn it into an error
+  prev_watch_ = be.wait_watch();
+  auto prev = prev_watch_;
+  uint64_t* eh = err_host_;
+  const int me = rank_;
+  be.set_wait_watch([eh, prev, me](double waited) {
+    const uint64_t e = __atomic_load_n(eh, __ATOMIC_ACQUIRE);
+    if (e)
+      throw Error("peer communicator: collective " + std::to_string(e) + " timed out waiting for a peer on rank " +
+                  std::to_string(me) + " (DBFS_COMM_TIMEOUT_S)");
+    if (prev) prev(waited);
+  });
+  watch_installed_ = true;
+  boot_->barrier();  // every rank has mapped every window
+}
+
+PeerComm::~PeerComm() {
+  if (be_ && watch_installed_) {
+    hipStreamSynchronize(static_cast<hipStream_t>(be_->stream_handle()));
+    be_->set_wait_watch(prev_watch_);
+  }
+  release();
+}
+
+void PeerComm::release() {
+  for (int p = 0; p < static_cast<int>(peer_.size()); ++p)
+    if (p != rank_ && peer_[p]) hipIpcCloseMemHandle(peer_[p]);
+  peer_.clear();
+  if (ticket_) hipFree(ticket_);
+  ticket_ = nullptr;
+  if (win_) hipFree(win_);
+  win_ = nullptr;
+  if (be_ && err_host_) be_->free_mapped(err_host_);
+  err_host_ = nullptr;
+}
+
+std::string PeerComm::name() const { return "peer+" + inner_->name(); }
+
+char* PeerComm::slot_ptr(int owner, int parity, int sender) const {
+  return peer_[owner] + kFlagBytes + (static_cast<size_t>(parity) * size_ + sender) * slot_;
+}
+
+namespace {
+int unit_for(uintptr_t x) { return (x % 16 == 0) ? 16 : (x % 8 == 0) ? 8 : 4; }
+}  // namespace
+
+void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& recv, bool self_direct,
+                   int64_t sum_count, int64_t* sum_out) {
+  const int P = size_;
+  const uint64_t s = ++seq_;
+  const int b = static_cast<int>(s & 1);
+  const hipStream_t st = S(be_);
+  HIP_CHECK(hipSetDevice(be_->device_id()));
+  int unit = 16;
+  kern::PeerPushArgs pa;
+  pa.npeers = P;
+  pa.seq = s;
+  pa.ticket = ticket_;
+  for (int p = 0; p < P; ++p) {
+    const bool direct = self_direct && p == rank_;
+    pa.src[p] = send[p].src;
+    pa.bytes[p] = send[p].bytes;
+    pa.dst[p] = direct ? recv[p].dst : slot_ptr(p, b, rank_);
+    pa.flag[p] = direct ? nullptr : reinterpret_cast<uint64_t*>(peer_[p]) + rank_;
+    if (direct && pa.src[p] == pa.dst[p]) pa.bytes[p] = 0;  // in place
+    if (pa.bytes[p] > 0)
+      unit = std::min({unit, unit_for(reinterpret_cast<uintptr_t>(pa.src[p])),
+                       unit_for(reinterpret_cast<uintptr_t>(pa.dst[p])), unit_for(static_cast<uintptr_t>(pa.bytes[p]))});
+  }
+  kern::PeerUnpackArgs ua;
+  ua.npeers = P;
+  for (int p = 0; p < P; ++p) {
+    const bool direct = self_direct && p == rank_;
+    ua.src[p] = slot_ptr(rank_, b, p);
+    ua.dst[p] = recv[p].dst;
+    ua.bytes[p] = direct || sum_count > 0 ? 0 : recv[p].bytes;
+    if (ua.bytes[p] > 0)
+      unit = std::min({unit, unit_for(reinterpret_cast<uintptr_t>(ua.dst[p])), unit_for(static_cast<uintptr_t>(ua.bytes[p]))});
+  }
+  DBFS_CHECK(unit >= 4, "PeerComm payloads must be multiples of 4 bytes, 4-byte aligned");
+  pa.unit = ua.unit = unit;
+  ua.sum_count = sum_count;
+  ua.sum_out = sum_out;
+  kern::peer_push(pa, st);
+  HIP_CHECK(hipGetLastError());
+  kern::PeerWaitArgs wa;
+  wa.flags = reinterpret_cast<const uint64_t*>(win_);
+  wa.npeers = P;
+  wa.skip = self_direct ? rank_ : -1;
+  wa.seq = s;
+  // (a peer that is minutes late is dead: the device-side wait gives up after
+  // at most 60 s so a hung job frees the GPU and reports the error)
+  const double limit = comm_timeout_s() > 0 ? std::min(comm_timeout_s(), 60.0) : 60.0;
+  const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
+  wa.timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
+  wa.error = err_dev_;
+  kern::peer_wait(wa, st);
+  HIP_CHECK(hipGetLastError());
+  kern::peer_unpack(ua, st);
+  HIP_CHECK(hipGetLastError());
+  ++peer_ops_;
+}
+
+void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
+  if (bytes > slot_ || bytes % 4) {
+    ++inner_ops_;
+    inner_->alltoall(send, recv, bytes);
+    return;
+  }
+  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    sp[p] = {static_cast<const char*>(send) + p * bytes, nullptr, static_cast<int64_t>(bytes)};
+    rp[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+  }
+  run(sp, rp, true, 0, nullptr);
+}
+
+void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
+  if (bytes > slot_ || bytes % 4) {
+    ++inner_ops_;
+    inner_->allgather(send, recv, bytes);
+    return;
+  }
+  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    sp[p] = {send, nullptr, static_cast<int64_t>(bytes)};
+    rp[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+  }
+  run(sp, rp, true, 0, nullptr);
+}
+
+void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  const size_t bytes = count * sizeof(int64_t);
+  if (bytes > slot_ || count == 0) {
+    ++inner_ops_;
+    if (count) inner_->allreduce_sum_i64(buf, count);
+    return;
+  }
+  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    sp[p] = {buf, nullptr, static_cast<int64_t>(bytes)};
+    rp[p] = {nullptr, nullptr, static_cast<int64_t>(bytes)};
+  }
+  run(sp, rp, false, static_cast<int64_t>(count), buf);
+}
+
+void PeerComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                         const int64_t* rd, size_t eb) {
+  bool fits = eb % 4 == 0;
+  for (int p = 0; p < size_ && fits; ++p)
+    fits = static_cast<size_t>(std::max(sc[p], rc[p])) * eb <= slot_;
+  if (!fits) {
+    ++inner_ops_;
+    inner_->alltoallv(send, sc, sd, recv, rc, rd, eb);
+    return;
+  }
+  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    sp[p] = {static_cast<const char*>(send) + sd[p] * eb, nullptr, sc[p] * static_cast<int64_t>(eb)};
+    rp[p] = {nullptr, static_cast<char*>(recv) + rd[p] * eb, rc[p] * static_cast<int64_t>(eb)};
+  }
+  run(sp, rp, true, 0, nullptr);
+}
+
+bool PeerComm::self_test(std::string* why) {
+  const int P = size_, me = rank_;
+  std::string err;
+  auto pat = [](int from, int to, int64_t i, int round) {
+    return static_cast<int64_t>((static_cast<uint64_t>(from + 1) * 0x9E3779B97F4A7C15ull) ^
+                                (static_cast<uint64_t>(to + 3) << 40) ^ (static_cast<uint64_t>(i) * 2654435761ull) ^
+                                static_cast<uint64_t>(round));
+  };
+  try {
+    for (int round = 0; round < 4 && err.empty(); ++round) {
+      // per-peer words: tiny, odd, and a whole slot
+      const int64_t words = round == 0 ? 1 : round == 1 ? 257 : round == 2 ? 4099 : static_cast<int64_t>(slot_ / 8);
+      const size_t n = static_cast<size_t>(words) * P;
+      DBuf<int64_t> a(*be_, n), b(*be_, n);
+      std::vector<int64_t> h(n), g(n);
+      // alltoall
+      for (int p = 0; p < P; ++p)
+        for (int64_t i = 0; i < words; ++i) h[p * words + i] = pat(me, p, i, round);
+      be_->to_device(a.data(), h.data(), n * 8);
+      alltoall(a.data(), b.data(), static_cast<size_t>(words) * 8);
+      be_->to_host(g.data(), b.data(), n * 8);
+      for (int p = 0; p < P && err.empty(); ++p)
+        for (int64_t i = 0; i < words; ++i)
+          if (g[p * words + i] != pat(p, me, i, round)) {
+            err = "alltoall mismatch (round " + std::to_string(round) + ", from rank " + std::to_string(p) + ")";
+            break;
+          }
+      // in-place allgather
+      for (int64_t i = 0; i < words; ++i) h[me * words + i] = pat(me, -1, i, round);
+      be_->to_device(b.data() + me * words, h.data() + me * words, static_cast<size_t>(words) * 8);
+      allgather(b.data() + me * words, b.data(), static_cast<size_t>(words) * 8);
+      be_->to_host(g.data(), b.data(), n * 8);
+      for (int p = 0; p < P && err.empty(); ++p)
+        for (int64_t i = 0; i < words; ++i)
+          if (g[p * words + i] != pat(p, -1, i, round)) {
+            err = "allgather mismatch (round " + std::to_string(round) + ", from rank " + std::to_string(p) + ")";
+            break;
+          }
+      // all-reduce (wrapping sums)
+      const int64_t cnt = std::min<int64_t>(words, static_cast<int64_t>(slot_ / 8));
+      for (int64_t i = 0; i < cnt; ++i) h[i] = pat(me, -2, i, round);
+      be_->to_device(a.data(), h.data(), static_cast<size_t>(cnt) * 8);
+      allreduce_sum_i64(a.data(), static_cast<size_t>(cnt));
+      be_->to_host(g.data(), a.data(), static_cast<size_t>(cnt) * 8);
+      for (int64_t i = 0; i < cnt && err.empty(); ++i) {
+        uint64_t want = 0;
+        for (int p = 0; p < P; ++p) want += static_cast<uint64_t>(pat(p, -2, i, round));
+        if (static_cast<uint64_t>(g[i]) != want) err = "allreduce mismatch (round " + std::to_string(round) + ")";
+      }
+    }
+    be_->synchronize();
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  // agree over the inner communicator (the windows may be what is broken)
+  const int64_t bad = inner_->sum_host(err.empty() ? 0 : 1);
+  if (bad && err.empty()) err = "a peer's self-test failed";
+  if (why) *why = err;
+  return bad == 0;
+}
+
+void PeerComm::barrier() {
+  int64_t* b = scratch(1);
+  allreduce_sum_i64(b, 1);  // value irrelevant: completion on every rank is the barrier
+  be_->synchronize();
+}
+
+}  // namespace dbfs

@@ -613,6 +613,7 @@ class Backend {
   // watch(seconds waited) about every period_s while the stream is still busy;
   // the watch may throw to abandon the wait.  A communicator installs one to
   // turn a dead peer into an error instead of a hang.
+  const std::function<void(double)>& wait_watch() const { return wait_watch_; }
   void set_wait_watch(std::function<void(double)> watch, double period_s = 0.05) {
     wait_watch_ = std::move(watch);
     wait_period_ = period_s;

@@ -20,6 +20,7 @@
 #pragma once
 
 #include <condition_variable>
+#include <functional>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -173,6 +174,66 @@ class NcclComm final : public Comm {
   void check_alive() const;
   void* comm_ = nullptr;  // ncclComm_t
   int rank_ = 0, size_ = 1;
+};
+
+class TcpBootstrap;
+
+// Collectives through peer-mapped device memory (csrc/comm/peer_comm.cpp,
+// csrc/kernels/peer_kernels.hip): every rank exports a window of uncached
+// device memory over IPC and maps every peer's; a collective is a push kernel
+// (remote stores over xGMI + a flag per sender), a one-wave wait kernel and an
+// unpack kernel, all on the backend's communication stream -- a few
+// microseconds of latency instead of a library collective's protocol.
+// Payloads larger than a window slot go to `inner` (RCCL, or TCP when ranks
+// share a GPU).  Requires: one HIP backend per rank, every window mappable.
+class PeerComm final : public Comm {
+ public:
+  PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes);
+  ~PeerComm() override;
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  std::string name() const override;
+  void alltoall(const void* send, void* recv, size_t bytes) override;
+  void allgather(const void* send, void* recv, size_t bytes) override;
+  void allreduce_sum_i64(int64_t* buf, size_t count) override;
+  void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv,
+                 const int64_t* rc, const int64_t* rd, size_t eb) override;
+  void barrier() override;
+  size_t slot_bytes() const { return slot_; }
+  // Every collective through the windows with known patterns (sizes up to a
+  // full slot), checked on the host; the verdict is agreed over the inner
+  // communicator, so every rank returns the same answer.
+  bool self_test(std::string* why = nullptr);
+  // collectives issued through the windows / delegated to the inner communicator
+  int64_t peer_ops() const { return peer_ops_; }
+  int64_t inner_ops() const { return inner_ops_; }
+
+ private:
+  struct Piece {
+    const void* src = nullptr;
+    void* dst = nullptr;  // final destination of a delivered piece (unpack)
+    int64_t bytes = 0;
+  };
+  // One collective: send[p] goes to rank p; recv[p] is where rank p's piece
+  // lands here; `self_direct`: this rank's own piece is copied straight to
+  // recv[rank] by the push (no window round trip); sum_count > 0: all-reduce.
+  void run(const std::vector<Piece>& send, const std::vector<Piece>& recv, bool self_direct, int64_t sum_count,
+           int64_t* sum_out);
+  std::shared_ptr<TcpBootstrap> boot_;
+  std::shared_ptr<Comm> inner_;
+  int rank_ = 0, size_ = 1;
+  size_t slot_ = 0;
+  char* win_ = nullptr;                 // own window (uncached device memory)
+  std::vector<char*> peer_;             // every rank's window as mapped here (peer_[rank_] == win_)
+  unsigned* ticket_ = nullptr;
+  uint64_t* err_host_ = nullptr;        // host-mapped error word (wait timeouts)
+  uint64_t* err_dev_ = nullptr;
+  uint64_t seq_ = 0;
+  int64_t peer_ops_ = 0, inner_ops_ = 0;
+  std::function<void(double)> prev_watch_;
+  bool watch_installed_ = false;
+  char* slot_ptr(int owner, int parity, int sender) const;
+  void release();
 };
 
 // Minimal TCP bootstrap (rank 0 hosts) used to ship the RCCL unique id and for

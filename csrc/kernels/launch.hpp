@@ -31,6 +31,39 @@ void hub_local(const HubLocalArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 
+// peer_kernels.hip (PeerComm: collectives through peer-mapped windows)
+constexpr int kMaxPeers = 16;
+struct PeerPushArgs {
+  void* dst[kMaxPeers] = {};        // destination (a peer's window slot, or a local buffer)
+  const void* src[kMaxPeers] = {};
+  int64_t bytes[kMaxPeers] = {};
+  uint64_t* flag[kMaxPeers] = {};   // flag word this rank owns in each peer's window (nullptr: none)
+  int npeers = 0;
+  int unit = 4;                     // copy granule (4, 8, 16 B; every size and address a multiple)
+  uint64_t seq = 0;
+  unsigned* ticket = nullptr;       // zero on entry; reset by the last workgroup
+};
+struct PeerWaitArgs {
+  const uint64_t* flags = nullptr;  // this rank's window: one word per sender
+  int npeers = 0;
+  int skip = -1;                    // sender not waited for (this rank, when it sent itself nothing)
+  uint64_t seq = 0;
+  uint64_t timeout_ticks = 0;       // device wall-clock ticks
+  uint64_t* error = nullptr;        // host-mapped: set to seq on a timeout
+};
+struct PeerUnpackArgs {
+  void* dst[kMaxPeers] = {};
+  const void* src[kMaxPeers] = {};
+  int64_t bytes[kMaxPeers] = {};
+  int npeers = 0;
+  int unit = 4;
+  int64_t sum_count = 0;            // > 0: all-reduce -- sum_out[i] = sum_p src[p][i] (uint64, wrapping)
+  void* sum_out = nullptr;
+};
+void peer_push(const PeerPushArgs& a, hipStream_t st);
+void peer_wait(const PeerWaitArgs& a, hipStream_t st);
+void peer_unpack(const PeerUnpackArgs& a, hipStream_t st);
+
 // ref_kernels.hip (reference-algorithm mode)
 void ref_expand(const RefExpandArgs& a, hipStream_t st);
 void ref_accept(const RefAcceptArgs& a, hipStream_t st);

@@ -1,0 +1,158 @@
+// gfx950 kernels of the peer-memory communicator (PeerComm, csrc/comm/peer_comm.cpp).
+//
+// Every rank exports one window of uncached device memory (IPC) and maps its
+// peers' windows; a collective is three stream-ordered launches, no host in
+// the loop and no library protocol:
+//   push   -- each rank stores its per-peer payloads straight into the peers'
+//             windows over xGMI (slot [parity][sender]); the last workgroup to
+//             finish (ticket) publishes `seq` into every peer's flag word for
+//             this sender, behind a system-scope release;
+//   wait   -- one wave polls the P flag words of its own window (system-scope
+//             relaxed loads + s_sleep, bounded: a peer that never arrives sets
+//             the error word the host watches instead of hanging the GPU);
+//   unpack -- copy (or, for the all-reduce, sum) the landed slots into the
+//             caller's buffers.
+// The windows are uncached (hipDeviceMallocUncached), so the data a peer wrote
+// is read from memory, not from a stale L2 line; the consumer's caches are the
+// ordinary ones because unpack writes the caller's (cached) buffers.
+// Reference call sites replaced: the per-pair synchronous cudaMemcpyPeer of
+// bfs.cu:595-609 and MPI_Sendrecv of bfs_mpi.cu:614-621.
+#include <hip/hip_runtime.h>
+
+#include "launch.hpp"
+#include "wave.hpp"
+
+namespace dbfs {
+namespace kern {
+namespace {
+
+using namespace dev;
+
+constexpr int kBlock = 256;
+
+// Copy `bytes` (a multiple of `unit`, 4 / 8 / 16) with every thread of the
+// grid; `t` / `nt` = global thread index / count.
+__device__ __forceinline__ void grid_copy(void* __restrict__ dst, const void* __restrict__ src, int64_t bytes, int unit,
+                                          int64_t t, int64_t nt) {
+  if (unit == 16) {
+    uint4* d = static_cast<uint4*>(dst);
+    const uint4* s = static_cast<const uint4*>(src);
+    for (int64_t i = t; i < bytes / 16; i += nt) d[i] = s[i];
+  } else if (unit == 8) {
+    uint64_t* d = static_cast<uint64_t*>(dst);
+    const uint64_t* s = static_cast<const uint64_t*>(src);
+    for (int64_t i = t; i < bytes / 8; i += nt) d[i] = s[i];
+  } else {
+    uint32_t* d = static_cast<uint32_t*>(dst);
+    const uint32_t* s = static_cast<const uint32_t*>(src);
+    for (int64_t i = t; i < bytes / 4; i += nt) d[i] = s[i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void peer_push_kernel(PeerPushArgs a) {
+  __shared__ int s_last;
+  // Workgroups are dealt to peers round-robin (group g -> peer g % P), so
+  // every xGMI link carries its share at once instead of the grid streaming
+  // to one peer after another.
+  const int P = a.npeers;
+  const int groups = static_cast<int>(gridDim.x) / P;
+  if (groups > 0) {
+    const int p = static_cast<int>(blockIdx.x) % P;
+    const int g = static_cast<int>(blockIdx.x) / P;
+    if (g < groups && a.bytes[p] > 0)
+      grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, static_cast<int64_t>(g) * kBlock + threadIdx.x,
+                static_cast<int64_t>(groups) * kBlock);
+  } else {
+    const int64_t nt = static_cast<int64_t>(gridDim.x) * kBlock;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    for (int q = 0; q < P; ++q)
+      if (a.bytes[q] > 0) grid_copy(a.dst[q], a.src[q], a.bytes[q], a.unit, t, nt);
+  }
+  // every wave's stores complete, then the hand-off (cdna_hip_programming.md
+  // Guideline 16, at system scope: the stores went to other GPUs' memory)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = prev == gridDim.x - 1 ? 1 : 0;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x < a.npeers && a.flag[threadIdx.x])
+    __hip_atomic_store(a.flag[threadIdx.x], a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) *a.ticket = 0u;  // next push is stream-ordered after this one
+}
+
+// One wave: lane p waits until flags[p] >= seq (p < npeers, skip_self aside).
+__global__ void peer_wait_kernel(PeerWaitArgs a) {
+  const int lane = lane_id();
+  bool ok = true;
+  if (lane < a.npeers && lane != a.skip) {
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t spin = 0;; ++spin) {
+      if (__hip_atomic_load(a.flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= a.seq) break;
+      __builtin_amdgcn_s_sleep(2);
+      if ((spin & 255) == 255 && wall_clock64() - t0 > a.timeout_ticks) {
+        ok = false;
+        break;
+      }
+    }
+  }
+  if (!__all(ok)) {
+    if (lane == 0 && a.error) __hip_atomic_store(a.error, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+__global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
+  const int64_t nt = static_cast<int64_t>(gridDim.x) * kBlock;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (a.sum_count > 0) {
+    // all-reduce: out[i] = sum over ranks of slot[p][i] (wrapping, as RCCL)
+    for (int64_t i = t; i < a.sum_count; i += nt) {
+      uint64_t acc = 0;
+      for (int p = 0; p < a.npeers; ++p) acc += static_cast<const uint64_t*>(a.src[p])[i];
+      static_cast<uint64_t*>(a.sum_out)[i] = acc;
+    }
+    return;
+  }
+  for (int p = 0; p < a.npeers; ++p)
+    if (a.bytes[p] > 0) grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, t, nt);
+}
+
+inline unsigned grid_for_bytes(int64_t bytes, int unit) {
+  int64_t g = (bytes / unit + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > 1024) g = 1024;
+  return static_cast<unsigned>(g);
+}
+
+}  // namespace
+
+void peer_push(const PeerPushArgs& a, hipStream_t st) {
+  int64_t mx = 0;
+  for (int p = 0; p < a.npeers; ++p) mx = a.bytes[p] > mx ? a.bytes[p] : mx;
+  // one group of workgroups per peer, sized for the largest piece
+  const int64_t per = (mx / a.unit + kBlock - 1) / kBlock;
+  const int64_t groups = per < 1 ? 1 : (per > 128 ? 128 : per);
+  peer_push_kernel<<<static_cast<unsigned>(groups * a.npeers), kBlock, 0, st>>>(a);
+}
+
+void peer_wait(const PeerWaitArgs& a, hipStream_t st) { peer_wait_kernel<<<1, 64, 0, st>>>(a); }
+
+void peer_unpack(const PeerUnpackArgs& a, hipStream_t st) {
+  int64_t tot = a.sum_count * 8;
+  for (int p = 0; p < a.npeers && a.sum_count == 0; ++p) tot += a.bytes[p];
+  if (tot <= 0) return;
+  peer_unpack_kernel<<<grid_for_bytes(tot, a.sum_count > 0 ? 8 : a.unit), kBlock, 0, st>>>(a);
+}
+
+}  // namespace kern
+}  // namespace dbfs

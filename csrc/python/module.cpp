@@ -279,6 +279,28 @@ PYBIND11_MODULE(_dbfs_native, m) {
         return std::shared_ptr<Comm>(new TcpComm(boot, *be));
       },
       py::keep_alive<0, 2>());
+  py::class_<PeerComm, Comm, std::shared_ptr<PeerComm>>(m, "PeerComm")
+      .def_property_readonly("slot_bytes", &PeerComm::slot_bytes)
+      .def_property_readonly("peer_ops", &PeerComm::peer_ops)
+      .def_property_readonly("inner_ops", &PeerComm::inner_ops)
+      .def("self_test", [](PeerComm& c) {
+        std::string why;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = c.self_test(&why);
+        }
+        return py::make_tuple(ok, why);
+      });
+  m.def(
+      "peer_comm",
+      [](std::shared_ptr<TcpBootstrap> boot, std::shared_ptr<Backend> be, std::shared_ptr<Comm> inner,
+         size_t slot_bytes) {
+        py::gil_scoped_release rel;
+        return std::make_shared<PeerComm>(boot, *be, inner, slot_bytes);
+      },
+      py::arg("boot"), py::arg("backend"), py::arg("inner"), py::arg("slot_bytes") = size_t(16) << 20,
+      py::keep_alive<0, 2>(), py::keep_alive<0, 3>());
   m.def("nccl_unique_id", []() { return py::bytes(NcclComm::unique_id()); });
   m.def(
       "nccl_comm",

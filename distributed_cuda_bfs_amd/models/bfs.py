@@ -88,6 +88,19 @@ class BFS:
         if directed:  # the CSR holds out-edges only (see build_csr / read_graph)
             self.engine.set_option("directed", 1)
 
+    def use_comm(self, comm) -> None:
+        """Rebuild the engine on another communicator (same shard, same
+        options): e.g. the RCCL communicator a peer-memory one wraps."""
+        opts = dict(self.engine.get_options())
+        mode = self.engine.mode
+        self.rt.comm = comm
+        comm.bind_backend(self.rt.backend)
+        self.engine = N.Engine(self.graph, comm, mode=mode, alpha=opts["alpha"], beta=opts["beta"],
+                               bu_lane_limit=int(opts["bu_lane_limit"]), phase_timing=bool(opts["phase_timing"]),
+                               force_exchange=bool(opts["force_exchange"]))
+        for k, v in opts.items():
+            self.engine.set_option(k, v)
+
     @property
     def mode(self) -> str:
         return self.engine.mode

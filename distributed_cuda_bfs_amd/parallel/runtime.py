@@ -24,6 +24,9 @@ class Runtime:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
+    # the communicator a peer-memory communicator wraps (RCCL), kept as the
+    # fallback transport (bench.py re-measures on it if a traversal fails)
+    fallback_comm: Any = None
 
     @property
     def is_gpu(self) -> bool:
@@ -64,6 +67,7 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
     local_rank = _env_int("LOCAL_RANK", rank if world > 1 else 0)
     # DBFS_DEVICE pins every rank to one device id (debug: several ranks on one GPU).
     backend = make_backend(device, _env_int("DBFS_DEVICE", local_rank))
+    fallback = None
     if comm is None:
         kind = os.environ.get("DBFS_COMM", "")
         if world == 1:
@@ -75,19 +79,50 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
             addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
             port = _env_int("DBFS_BOOTSTRAP_PORT", _env_int("MASTER_PORT", 29500) + 1)
             boot = N.TcpBootstrap(addr, port, rank, world)
-            if kind == "tcp" or (not kind and not backend.is_gpu):
+            shared = "DBFS_DEVICE" in os.environ  # several ranks on one GPU (tests)
+            if kind == "tcp" or (not kind and (not backend.is_gpu or shared)):
                 comm = N.tcp_comm(boot, backend)  # host collectives (CPU runs / debug fallback)
             else:
-                # one GPU per rank: the backend made LOCAL_RANK current
-                # (hipSetDevice) before the communicator is created
-                if "DBFS_DEVICE" not in os.environ and backend.device_id != local_rank:
-                    raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, "
-                                       f"expected LOCAL_RANK {local_rank}")
-                uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
-                comm = N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
-                del boot
+                if shared:
+                    # RCCL refuses two ranks on one device: TCP carries what
+                    # does not fit the peer windows
+                    inner = N.tcp_comm(boot, backend)
+                else:
+                    # one GPU per rank: the backend made LOCAL_RANK current
+                    # (hipSetDevice) before the communicator is created
+                    if backend.device_id != local_rank:
+                        raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, "
+                                           f"expected LOCAL_RANK {local_rank}")
+                    uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
+                    inner = N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
+                comm = inner
+                if kind in ("", "peer"):
+                    comm, fallback = _try_peer(boot, backend, inner, rank, kind == "peer")
     comm.bind_backend(backend)
-    return Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)
+    rt = Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)
+    rt.fallback_comm = fallback
+    return rt
+
+
+def _try_peer(boot, backend, inner, rank: int, required: bool):
+    """The peer-memory communicator over `inner` if every rank can map every
+    window and its self-test passes on every rank (the verdict is agreed), else
+    `inner`.  Returns (comm, fallback)."""
+    import sys
+
+    slot = _env_int("DBFS_PEER_SLOT_MB", 16) << 20
+    try:
+        pc = N.peer_comm(boot, backend, inner, slot)
+        ok, why = pc.self_test()
+    except Exception as e:  # noqa: BLE001 - agreed on every rank by the native code
+        ok, why, pc = False, str(e), None
+    if ok:
+        return pc, inner
+    if required:
+        raise RuntimeError(f"DBFS_COMM=peer: peer communicator unavailable: {why}")
+    if rank == 0:
+        print(f"[dbfs] peer communicator unavailable ({why}); using {inner.name}", file=sys.stderr, flush=True)
+    return inner, None
 
 
 def run_virtual_ranks(nranks: int, fn: Callable[[Runtime], Any], device: str = "auto",

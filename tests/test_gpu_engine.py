@@ -554,3 +554,24 @@ def test_list_form_and_split_bottom_up_gpu(gpu_runtime, knobs):
         for rank_out in run_virtual_ranks(P, body, device="hip"):
             for lv, s in zip(rank_out, srcs):
                 assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
+
+
+def test_peer_comm_two_ranks_share_one_gpu():
+    """Peer-memory communicator: two self-spawned ranks on device 0 export
+    their uncached windows over IPC, map each other's, pass the self-test
+    (every collective with known patterns), then run the bench with the
+    collectives as push / wait / unpack kernels; every timed root validated."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "18", "--steps", "4",
+           "--warmup", "1"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["comm_note"] is None
+    assert rec["validated"] is True and rec["validated_roots"] == "4/4"
