@@ -70,6 +70,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
+  else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "bu_split") o.bu_split = v != 0;
@@ -98,6 +99,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
+          {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
@@ -931,6 +933,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   const bool split_ok = xc && opt_.bu_split && gv.nhubs > 0 && gv.nz_pref && gv.nz_head && opt_.bu_nz_view &&
                         opt_.bu_compact && !opt_.bu_packed && opt_.mode != Mode::TopDown;
   const int64_t hub_words = div_up(gv.nhubs, kWordBits);
+  // One rank: bottom-up levels may run a separate head pass (bu_head_pass).
+  const bool head_split_ok = !xc && opt_.bu_head_pass > 0 && gv.nhubs > 0 && gv.nz_pref && gv.nz_head &&
+                             opt_.bu_nz_view && opt_.bu_compact && !opt_.bu_packed;
   // stats block of level L's output (L = -1: the seed); one block with one rank
   auto sblk = [&](int L) {
     return xc ? stats_.data() + static_cast<int64_t>((L + 1) % kStatsBlocks) * stats_stride_ : stats_.data();
@@ -1328,6 +1333,30 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           hg.ctrl = ctrl_.data();
           be_.hub_gather(hg);
           ba.hub_front = hub_front_.data();
+        }
+        // one rank: the row heads of every unvisited vertex probed first in
+        // a pass of its own (loads of eight words in flight per wave), then
+        // the rows whose head missed are scanned by the merging full pass
+        const bool head_pass = head_split_ok && (opt_.bu_head_pass == 2 || (opt_.bu_head_pass == 1 && pf != 'B'));
+        if (head_pass) {
+          BuHeadArgs bh;
+          bh.g = gv;
+          bh.zdeg = ba.zdeg;
+          bh.hub_front = hub_front_.data();
+          bh.frontier_own = frontier_[cur].data();
+          bh.visited = vis_own;
+          bh.new_frontier = ba.new_frontier;
+          bh.level = ba.level;
+          bh.level8 = ba.level8;
+          bh.new_level = ba.new_level;
+          bh.words = W;
+          bh.unit_cnt = unit_cnt_.data();
+          bh.unit_deg = unit_deg_.data();
+          bh.ctrl = ctrl_.data();
+          bh.stamp = false;  // hub_gather stamped the level's start
+          be_.bu_head(bh);
+          ba.merge = true;
+          ba.heads_done = true;
         }
         be_.bu_step(ba);
       }

@@ -448,6 +448,10 @@ struct BuArgs {
   // pass's results stay -- new_frontier words are OR-ed, unit statistics
   // added -- and its vertices are already visited.  Hub kernel, compacted.
   bool merge = false;
+  // ... and the head pass saw the whole frontier (one rank): every head it did
+  // not settle is known to miss, so rows are not probed at their head again
+  // (rows of one entry are done, longer ones go straight to the row scan).
+  bool heads_done = false;
 };
 
 // First half of a split bottom-up level (several ranks): while the frontier
@@ -472,6 +476,7 @@ struct BuHeadArgs {
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // runs only when ctrl->dir == 'B'
   bool probe = true;                 // false (diagnostics): settle nothing, only write the words
+  bool stamp = true;                 // first kernel of the level: stamps its start
 };
 
 // Frontier bits of the hubs this rank owns (bit h = new frontier bit of

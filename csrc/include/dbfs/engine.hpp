@@ -142,6 +142,14 @@ struct EngineOptions {
   // frontier all-gather is still in flight on the communication stream, and
   // finishes the rest after it (bu_head + bu_step merge).
   bool bu_split = true;
+  // Device loop, one rank, hub LDS on: bottom-up levels settle the vertices
+  // whose row head is in the frontier in a head pass of their own (bu_head),
+  // then bu_step(merge) scans only the rows whose head missed: 0 off, 1 the
+  // first bottom-up level of a run of them, 2 every bottom-up level.  Off by
+  // default: measured on RMAT-26 the head pass alone (hub bits probed in L2,
+  // not LDS) took 342 us against 390 us for the whole fused level
+  // (profiles/README.md, round 2).
+  int bu_head_pass = 0;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is

@@ -598,17 +598,56 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
                                                  s_wmax);
 
+    // All items' loads in flight together (column ids, then their visited /
+    // next words), then the stores: the items of a thread are independent, but
+    // the compiler cannot move a load above an earlier item's atomic, so one
+    // item at a time costs kItems dependent round trips per block.
+    vid_t vk[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int idx = k * kThreads + t;
+      vk[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+    }
+    if constexpr (kOut != TdOut::Lists) {
+      if (!bytes) {
+        word_t seen[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          seen[k] = k * kThreads + t < cnt ? (visited[vk[k] >> 6] | a.next[vk[k] >> 6]) : ~0ull;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const word_t bit = 1ull << (vk[k] & 63);
+          if (!(seen[k] & bit)) atomicOr(a.next + (vk[k] >> 6), bit);
+        }
+        continue;
+      }
+      // byte map: with few visited vertices the check costs more than the
+      // store it saves (random loads ~120 G/s vs byte stores ~88 G/s on
+      // MI355X); the consuming update masks with ~visited anyway.  A byte
+      // already marked is not stored again (RMAT rows repeat the same hubs,
+      // and a read hit is cheaper than a byte write).
+      bool keep[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k)
+        keep[k] = k * kThreads + t < cnt && (!check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+      uint8_t mark[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) mark[k] = keep[k] ? a.next_bytes[vk[k]] : 1;
+#pragma unroll
+      for (int k = 0; k < kItems; ++k)
+        if (!mark[k]) a.next_bytes[vk[k]] = 1;
+      continue;
+    }
+    bool actk[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      actk[k] = k * kThreads + t < cnt && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
       if constexpr (kOut == TdOut::Lists) {
         // wave-aggregated append to the owner lists (uniform loop over owners)
-        vid_t v = 0;
-        bool act = false;
-        if (idx < cnt) {
-          v = col[e0 + idx + s_base[s_owner[idx]]];
-          act = !(visited[v >> 6] & (1ull << (v & 63)));
-        }
+        const vid_t v = vk[k];
+        const bool act = actk[k];
         const int owner = act ? static_cast<int>(v / a.part) : -1;
         unsigned long long pending = __ballot(act);
         while (pending) {
@@ -621,21 +660,6 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
           base = __shfl(base, leader, kWave);
           if (owner == o) list[1 + base + mask_rank(msk)] = v;
           pending &= ~msk;
-        }
-      } else if (idx < cnt) {
-        const int i = s_owner[idx];
-        const vid_t v = col[e0 + idx + s_base[i]];
-        const word_t bit = 1ull << (v & 63);
-        if (bytes) {
-          // with few visited vertices the check costs more than the store it
-          // saves (random loads ~120 G/s vs byte stores ~88 G/s on MI355X);
-          // the consuming update masks with ~visited anyway
-          // (a byte already marked is not stored again: RMAT rows repeat the
-          // same hubs, and a read hit is cheaper than a byte write)
-          if ((!check || !(visited[v >> 6] & bit)) && !a.next_bytes[v]) a.next_bytes[v] = 1;
-        } else {
-          const word_t seen = visited[v >> 6] | a.next[v >> 6];
-          if (!(seen & bit)) atomicOr(a.next + (v >> 6), bit);
         }
       }
     }
@@ -1104,7 +1128,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
         const int64_t k = a.g.nz_pref[w0 + j] + __popcll(~a.zdeg[w0 + j] & ((1ull << bit) - 1ull));
         rs = nz_ro[k];
         len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
-        u = a.g.nz_head[k];
+        if (!a.heads_done) u = a.g.nz_head[k];
       } else {
         const int64_t v = w0 * 64 + loc;
         rs = ro[v];
@@ -1170,7 +1194,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     const vid_t u0 = n_u;
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
     bool found = false;
-    if (rs < e) {
+    if (rs < e && !a.heads_done) {
       found = bu_probe<kHub>(fr, s_hub, u0);
     }
     BU_STAT(0, 1);
@@ -1338,52 +1362,93 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
 // (64 KiB, L2-resident) or, when it is an owned vertex, in the owned frontier
 // slice; anything else waits for bu_step(merge) after the all-gather.  Every
 // owned word of new_frontier and every unit's statistics are written.
+//
+// The pass is a chain of dependent loads per word (head -> frontier bit ->
+// row bounds), so the words are taken kHeadGroup at a time with every load of
+// the group in flight together (one word at a time left the first bottom-up
+// level of RMAT-26 latency-bound); the result words are collected in lane j's
+// register and written once per unit, coalesced.
+#ifndef DBFS_BU_HEAD_GROUP
+#define DBFS_BU_HEAD_GROUP 8
+#endif
+constexpr int kHeadGroup = DBFS_BU_HEAD_GROUP;
+static_assert(kUnitWords % kHeadGroup == 0, "head groups tile a unit");
+
 __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-  stamp_level_start(a.ctrl);
+  if (a.stamp) stamp_level_start(a.ctrl);
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
-  const int64_t nw = min<int64_t>(kUnitWords, a.words - w0);
+  const int nw = static_cast<int>(min<int64_t>(kUnitWords, a.words - w0));
   // the words of the unit, one per lane (visited includes zero-degree and padding)
   const word_t vis_l = lane < nw ? a.visited[w0 + lane] : ~0ull;
   const word_t zd_l = lane < nw ? a.zdeg[w0 + lane] : ~0ull;
   const int64_t nzw = (a.g.rows + kWordBits - 1) / kWordBits;  // words of the non-empty-row view
   const int64_t pref_l = (lane < nw && w0 + lane < nzw) ? a.g.nz_pref[w0 + lane] : 0;
   const int64_t lo = a.g.lo, hi = a.g.lo + a.g.rows;
+  const word_t below = (1ull << lane) - 1ull;
   long long cnt = 0, deg = 0;
-  for (int j = 0; j < nw; ++j) {
-    const word_t vis = readlane64(vis_l, j);
-    word_t res = 0;
-    if (vis != ~0ull) {  // uniform
-      const word_t zd = readlane64(zd_l, j);
-      const int64_t pref = readlane_i64(pref_l, j);
-      bool found = false;
-      eid_t d = 0;
-      if (a.probe && !((vis >> lane) & 1ull)) {
+  word_t res_l = 0;  // result word `lane` of the unit
+  for (int j0 = 0; j0 < nw; j0 += kHeadGroup) {
+    int64_t k[kHeadGroup];
+    vid_t u[kHeadGroup];
+    bool act[kHeadGroup];
+    // (1) heads of the group's unvisited vertices
+#pragma unroll
+    for (int i = 0; i < kHeadGroup; ++i) {
+      const int j = j0 + i;
+      const word_t vis = j < nw ? readlane64(vis_l, j) : ~0ull;
+      act[i] = a.probe && !((vis >> lane) & 1ull);
+      k[i] = 0;
+      u[i] = 0;
+      if (act[i]) {
         // unvisited implies non-zero degree (zero-degree bits are pre-set)
-        const int64_t k = pref + __popcll(~zd & ((1ull << lane) - 1ull));
-        const vid_t u = a.g.nz_head[k];
-        if (u & kHubFlag) {
-          const vid_t h = u & ~kHubFlag;
-          found = (a.hub_front[h >> 6] >> (h & 63)) & 1ull;
-        } else if (u >= lo && u < hi) {
-          const int64_t r = static_cast<int64_t>(u) - lo;
-          found = (a.frontier_own[r >> 6] >> (r & 63)) & 1ull;
-        }
-        if (found) d = a.g.nz_row_off[k + 1] - a.g.nz_row_off[k];
+        k[i] = readlane_i64(pref_l, j) + __popcll(~readlane64(zd_l, j) & below);
+        u[i] = a.g.nz_head[k[i]];
       }
-      res = __ballot(found);
-      if (found) {
-        store_level(a.level, a.level8, (w0 + j) * 64 + lane, a.new_level);
-        cnt += 1;
-        deg += d;
-      }
-      if (lane == 0 && res) a.visited[w0 + j] = vis | res;
     }
-    if (lane == 0) a.new_frontier[w0 + j] = res;
+    // (2) frontier bits of the heads
+    bool found[kHeadGroup];
+#pragma unroll
+    for (int i = 0; i < kHeadGroup; ++i) {
+      found[i] = false;
+      if (act[i]) {
+        if (u[i] & kHubFlag) {
+          const vid_t h = u[i] & ~kHubFlag;
+          found[i] = (a.hub_front[h >> 6] >> (h & 63)) & 1ull;
+        } else if (u[i] >= lo && u[i] < hi) {
+          const int64_t r = static_cast<int64_t>(u[i]) - lo;
+          found[i] = (a.frontier_own[r >> 6] >> (r & 63)) & 1ull;
+        }
+      }
+    }
+    // (3) settled vertices: row lengths (statistics) and levels
+    eid_t r0[kHeadGroup], r1[kHeadGroup];
+#pragma unroll
+    for (int i = 0; i < kHeadGroup; ++i) {
+      r0[i] = r1[i] = 0;
+      if (found[i]) {
+        r0[i] = a.g.nz_row_off[k[i]];
+        r1[i] = a.g.nz_row_off[k[i] + 1];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kHeadGroup; ++i) {
+      const word_t res = __ballot(found[i]);
+      if (lane == j0 + i) res_l = res;
+      if (found[i]) {
+        store_level(a.level, a.level8, (w0 + j0 + i) * 64 + lane, a.new_level);
+        cnt += 1;
+        deg += r1[i] - r0[i];
+      }
+    }
+  }
+  if (lane < nw) {
+    a.new_frontier[w0 + lane] = res_l;
+    if (res_l) a.visited[w0 + lane] = vis_l | res_l;
   }
   wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
 }

@@ -322,6 +322,42 @@ def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed, whole):
         _check(bfs, csr, bfs.sample_roots(1, seed=12)[0])
 
 
+@pytest.mark.parametrize("head_pass", [0, 1, 2])
+@pytest.mark.parametrize("max_hubs", [None, 3000])
+@pytest.mark.parametrize("whole", [1, -1])
+def test_bottom_up_head_pass_gpu(gpu_runtime, head_pass, max_hubs, whole):
+    """One rank, bottom-up levels split into a head pass (bu_head: every
+    unvisited vertex's row head probed, eight words in flight per wave) and the
+    merging full pass that only scans the rows whose head missed (heads_done):
+    off, first bottom-up level only, every bottom-up level."""
+    p = dbfs.rmat_params(16, 16, 71)
+    csr = dbfs.host_csr_from_params(p)
+    for mode in ["bu", "do"]:
+        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, max_hubs=max_hubs)
+        bfs.engine.set_option("bu_head_pass", head_pass)
+        bfs.engine.set_option("bu_whole_units", whole)
+        for src in bfs.sample_roots(3, seed=13):
+            _check(bfs, csr, src)
+
+
+@pytest.mark.parametrize("head_pass", [0, 1])
+def test_full_scale_rmat20_gpu(gpu_runtime, head_pass):
+    """RMAT-20 at the default thresholds, exact against the CPU oracle: whole
+    64-word units per wave chosen by occupancy (16 K units >= the resident wave
+    slots), 2^19 hubs, deferred row scans, sparse and dense top-down levels."""
+    p = dbfs.rmat_params(20, 16, 5)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode="do")
+    assert bfs.graph.nhubs > 1 << 16
+    bfs.engine.set_option("bu_head_pass", head_pass)
+    dirs = set()
+    for src in bfs.sample_roots(2, seed=21):
+        res = _check(bfs, csr, src)
+        dirs.update(lv["dir"] for lv in res.levels)
+        assert bfs.validate(src)
+    assert dirs == {"T", "B"}
+
+
 def test_hub_lds_virtual_ranks_gpu():
     """Hub path on 3 virtual ranks: the hub frontier bits are gathered from the
     all-gathered global frontier of every rank."""

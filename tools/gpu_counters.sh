@@ -7,7 +7,6 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 SCALE=${SCALE:-26}
-make -j16 > gpurun_out/make.log 2>&1 || { tail -30 gpurun_out/make.log; exit 1; }
 rm -rf gpurun_out/pmc1 gpurun_out/pmc2
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY FETCH_SIZE \
   -d gpurun_out/pmc1 -o run --output-format csv -- \

@@ -1,24 +1,32 @@
 #!/bin/bash
-# One GPU iteration: build, GPU tests, headline bench with per-level profile,
-# rocprofv3 kernel statistics.  Every GPU step has its own time limit; the
-# script stops at the first failure.
+# Iteration check: GPU tests, headline bench, top-down-only bench at RMAT-22,
+# kernel timeline of the last two traversals of a short RMAT-26 bench.
+#   SKIP_TESTS=1 to skip pytest; TD=0 to skip the td bench; TRACE=0 to skip the trace.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-SCALE=${SCALE:-26}
-make -j16 > gpurun_out/make.log 2>&1 || { tail -30 gpurun_out/make.log; exit 1; }
-if [ "${TESTS:-1}" = 1 ]; then
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
   echo "== pytest gpu"
-  timeout -k 10 600 python -m pytest tests/ -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-  tail -6 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 fi
-echo "== bench"
-timeout -k 10 300 python bench.py --scale $SCALE --steps 16 --warmup 3 --per-level ${BENCH_ARGS} > gpurun_out/bench.log 2>&1; rc=$?
-tail -14 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
-if [ "${PROF:-1}" = 1 ]; then
-  echo "== rocprofv3"
-  rm -rf gpurun_out/prof
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python3 bench.py --scale $SCALE --steps 8 --warmup 2 --no-validate ${BENCH_ARGS} > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
-  f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -16 "$f" | cut -c1-200
+summ() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], 'GTEPS', d['ms_per_step'], 'ms', d['validated_roots'], [(l[0], round(l[1]*1e3,1)) for l in d['level_clock']['levels']])" "$@"; }
+echo "== bench RMAT-26 do"
+timeout -k 10 240 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS} > gpurun_out/it_do26.json 2> gpurun_out/it_do26.err || { tail -20 gpurun_out/it_do26.err; exit 1; }
+summ gpurun_out/it_do26.json do26
+if [ "${TD:-1}" = 1 ]; then
+  echo "== bench RMAT-22 td"
+  timeout -k 10 240 python bench.py --scale 22 --mode td --steps 16 --warmup 3 --no-int32-pass > gpurun_out/it_td22.json 2> gpurun_out/it_td22.err || { tail -20 gpurun_out/it_td22.err; exit 1; }
+  summ gpurun_out/it_td22.json td22
+fi
+if [ "${TRACE:-1}" = 1 ]; then
+  echo "== trace"
+  rm -rf gpurun_out/trace
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/trace -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-validate --no-int32-pass ${TRACE_ARGS} > gpurun_out/trace.log 2>&1 || { tail -30 gpurun_out/trace.log; exit 1; }
+  f=$(find gpurun_out/trace -name "*kernel_trace.csv" | head -1)
+  python3 tools/trace_summary.py "$f" --runs 2 > gpurun_out/trace_summary.txt
+  gzip -f "$f"
+  tail -45 gpurun_out/trace_summary.txt
 fi

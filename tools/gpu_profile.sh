@@ -5,7 +5,6 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 SCALE=${SCALE:-26}
-make -j16 > gpurun_out/make.log 2>&1 || { tail -30 gpurun_out/make.log; exit 1; }
 echo "== per-level"
 timeout -k 10 300 python bench.py --scale $SCALE --steps 8 --warmup 2 --per-level > gpurun_out/perlevel.log 2>&1 || { tail -30 gpurun_out/perlevel.log; exit 1; }
 tail -14 gpurun_out/perlevel.log

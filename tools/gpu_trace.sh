@@ -6,7 +6,6 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 SCALE=${SCALE:-26}
-make -j16 > gpurun_out/make.log 2>&1 || { tail -30 gpurun_out/make.log; exit 1; }
 rm -rf gpurun_out/trace
 timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/trace -o run --output-format csv -- \
   python3 bench.py --scale $SCALE --steps ${STEPS:-2} --warmup 1 --no-validate ${BENCH_ARGS} > gpurun_out/trace.log 2>&1 \
