@@ -41,6 +41,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import socket
 import subprocess
 import sys
@@ -182,9 +183,10 @@ def main(argv=None) -> int:
             return 2
         scale += lg
     if args.graph:
-        params = dbfs.read_graph(args.graph)
+        # sharded: every rank parses only its byte range (or its rows of a
+        # binary cache) and builds its shard on its GPU
+        params = args.graph
         graph_name = os.path.basename(args.graph)
-        n_vertices, n_input_edges = params.n, params.input_edges
     else:
         params = dbfs.rmat_params(scale, args.edge_factor, args.seed)
         graph_name = (f"RMAT-{scale} (Graph500 Kronecker a=.57 b=.19 c=.19, "
@@ -199,6 +201,8 @@ def main(argv=None) -> int:
     rt.backend.synchronize()
     rt.barrier()
     gen_s = time.time() - t0
+    if args.graph:
+        n_vertices, n_input_edges = bfs.n, bfs.graph.input_edges
     log(f"built {graph_name} shard: rows {bfs.graph.rows} nnz {bfs.graph.nnz} in {gen_s:.2f}s")
 
     roots = bfs.sample_roots(args.warmup + args.steps, seed=args.root_seed)
@@ -249,7 +253,8 @@ def main(argv=None) -> int:
         for r in results:
             dirs = "".join(lv["dir"] for lv in r.levels)
             log(f"timed root {r.source}: {r.ms:.3f} ms {r.gteps:.1f} GTEPS levels {dirs} "
-                f"frontier-edges {[lv['frontier_edges'] for lv in r.levels]}")
+                f"frontier-edges {[lv['frontier_edges'] for lv in r.levels]} "
+                f"level-us {[round(lv['ms'] * 1e3, 1) for lv in r.levels]}")
     edges = sum(r.edges for r in results)
     bfs_ms = sum(r.ms for r in results)
     value = edges / (wall_ms * 1e6)
@@ -331,6 +336,8 @@ def main(argv=None) -> int:
             "validated": validated,
             "validated_roots": (f"{n_valid}/{len(timed)}" if validated is not None else None),
             "generate_s": round(gen_s, 3),
+            # peak resident host memory of rank 0's process (graph build included)
+            "host_peak_rss_gb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 3),
             "level_profile": {"root": med.source, "levels": level_profile,
                               "columns": ["dir", "ms", "comm_ms"]},
             # the timed traversal of the same root, from the device clock the

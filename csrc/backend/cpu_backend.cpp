@@ -613,6 +613,31 @@ class CpuBackend final : public Backend {
     data[n] = acc;
   }
 
+  void route_edges_count(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks,
+                         int64_t* counts) override {
+    for (int64_t i = 0; i < m; ++i) {
+      ++counts[u[i] / part];
+      ++counts[v[i] / part];
+    }
+    (void)nranks;
+  }
+  void route_edges_fill(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* cursor,
+                        uint64_t* out) override {
+    // edge order within every destination segment (the reference's adjacency
+    // order survives the exchange: segments arrive in rank = file order)
+    for (int64_t i = 0; i < m; ++i) {
+      out[cursor[u[i] / part]++] = (static_cast<uint64_t>(u[i]) << 32) | v[i];
+      out[cursor[v[i] / part]++] = (static_cast<uint64_t>(v[i]) << 32) | u[i];
+    }
+    (void)nranks;
+  }
+  void entries_count(const uint64_t* e, int64_t k, int64_t lo, eid_t* deg) override {
+    for (int64_t i = 0; i < k; ++i) ++deg[static_cast<int64_t>(e[i] >> 32) - lo];
+  }
+  void entries_fill(const uint64_t* e, int64_t k, int64_t lo, eid_t* cursor, vid_t* col) override {
+    for (int64_t i = 0; i < k; ++i)
+      col[cursor[static_cast<int64_t>(e[i] >> 32) - lo]++] = static_cast<vid_t>(e[i] & 0xFFFFFFFFull);
+  }
   void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) override {
     // Same order as build_csr (edge order, u-side then v-side).
     for (int64_t i = 0; i < p.m; ++i) {

@@ -301,6 +301,26 @@ class HipBackend final : public Backend {
     kern::exclusive_scan(data, n, scan_tmp_, st_);
     chk();
   }
+  void route_edges_count(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks,
+                         int64_t* counts) override {
+    DBFS_CHECK(nranks <= kern::route_max_ranks(), "edge routing supports at most 1024 ranks");
+    kern::route_edges_count(u, v, m, part, nranks, counts, st_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void route_edges_fill(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* cursor,
+                        uint64_t* out) override {
+    DBFS_CHECK(nranks <= kern::route_max_ranks(), "edge routing supports at most 1024 ranks");
+    kern::route_edges_fill(u, v, m, part, nranks, cursor, out, st_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void entries_count(const uint64_t* e, int64_t k, int64_t lo, eid_t* deg) override {
+    kern::entries_count(e, k, lo, deg, st_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void entries_fill(const uint64_t* e, int64_t k, int64_t lo, eid_t* cursor, vid_t* col) override {
+    kern::entries_fill(e, k, lo, cursor, col, st_);
+    HIP_CHECK(hipGetLastError());
+  }
   void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) override {
     on();
     kern::gen_fill(p, lo, rows, cursor, col, st_);

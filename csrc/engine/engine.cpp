@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "dbfs/engine.hpp"
+#include "dbfs/shard_reader.hpp"
 #include "dbfs/trace.hpp"
 
 namespace dbfs {
@@ -168,6 +169,93 @@ std::unique_ptr<DeviceGraph> DeviceGraph::generate(Backend& be, const GenParams&
   }
   g->build_heads();
   return g;
+}
+
+std::unique_ptr<DeviceGraph> DeviceGraph::from_edges(Backend& be, Comm& comm, const Partition& part, int rank,
+                                                     int64_t input_edges, const vid_t* u, const vid_t* v,
+                                                     int64_t m_local) {
+  DBFS_CHECK(comm.size() == part.nranks && comm.rank() == rank, "communicator does not match the partition");
+  DBFS_CHECK(m_local >= 0, "negative edge count");
+  comm.bind_backend(&be);
+  const int P = part.nranks;
+  auto g = std::unique_ptr<DeviceGraph>(new DeviceGraph());
+  g->be_ = &be;
+  g->part_ = part;
+  g->rank_ = rank;
+  g->lo_ = part.lo(rank);
+  g->rows_ = part.count(rank);
+  g->input_edges_ = input_edges;
+  // (1) this rank's edges -> entries per owner, grouped by owner
+  std::vector<int64_t> sc(static_cast<size_t>(P), 0), rc(static_cast<size_t>(P), 0);
+  DBuf<uint64_t> send;
+  {
+    DBuf<vid_t> du(be, static_cast<size_t>(std::max<int64_t>(m_local, 1)));
+    DBuf<vid_t> dv(be, static_cast<size_t>(std::max<int64_t>(m_local, 1)));
+    if (m_local) {
+      be.to_device(du.data(), u, static_cast<size_t>(m_local) * sizeof(vid_t));
+      be.to_device(dv.data(), v, static_cast<size_t>(m_local) * sizeof(vid_t));
+    }
+    DBuf<int64_t> cnt(be, static_cast<size_t>(P)), rcnt(be, static_cast<size_t>(P));
+    be.memset_async(cnt.data(), 0, cnt.bytes());
+    be.route_edges_count(du.data(), dv.data(), m_local, part.part, P, cnt.data());
+    // (2) entry counts to their owners
+    comm.alltoall(cnt.data(), rcnt.data(), sizeof(int64_t));
+    be.to_host(sc.data(), cnt.data(), cnt.bytes());
+    be.to_host(rc.data(), rcnt.data(), rcnt.bytes());
+    std::vector<int64_t> sd(static_cast<size_t>(P), 0);
+    for (int r = 1; r < P; ++r) sd[r] = sd[r - 1] + sc[r - 1];
+    const int64_t total = sd[P - 1] + sc[P - 1];
+    DBFS_CHECK(total == 2 * m_local, "edge routing lost entries");
+    send = DBuf<uint64_t>(be, static_cast<size_t>(std::max<int64_t>(total, 1)));
+    be.to_device(cnt.data(), sd.data(), sd.size() * sizeof(int64_t));  // cursors = segment starts
+    be.route_edges_fill(du.data(), dv.data(), m_local, part.part, P, cnt.data(), send.data());
+    be.synchronize();
+  }
+  // (3) all-to-all-v of the entries (in rank order: file order per owner)
+  std::vector<int64_t> sd(static_cast<size_t>(P), 0), rd(static_cast<size_t>(P), 0);
+  for (int r = 1; r < P; ++r) {
+    sd[r] = sd[r - 1] + sc[r - 1];
+    rd[r] = rd[r - 1] + rc[r - 1];
+  }
+  const int64_t nrecv = rd[P - 1] + rc[P - 1];
+  DBuf<uint64_t> recv(be, static_cast<size_t>(std::max<int64_t>(nrecv, 1)));
+  comm.alltoallv(send.data(), sc.data(), sd.data(), recv.data(), rc.data(), rd.data(), sizeof(uint64_t));
+  be.synchronize();
+  send.reset();
+  // (4) the shard: degrees -> offsets -> fill
+  g->row_off_ = DBuf<eid_t>(be, static_cast<size_t>(g->rows_ + 1));
+  be.memset_async(g->row_off_.data(), 0, g->row_off_.bytes());
+  be.entries_count(recv.data(), nrecv, g->lo_, g->row_off_.data());
+  be.exclusive_scan(g->row_off_.data(), g->rows_);
+  eid_t nnz = 0;
+  be.to_host(&nnz, g->row_off_.data() + g->rows_, sizeof(eid_t));
+  DBFS_CHECK(nnz == nrecv, "entries outside this rank's rows");
+  g->nnz_ = nnz;
+  g->col_ = DBuf<vid_t>(be, static_cast<size_t>(std::max<int64_t>(nnz, 1)));
+  {
+    DBuf<eid_t> cursor(be, static_cast<size_t>(std::max<int64_t>(g->rows_, 1)));
+    be.copy_async(cursor.data(), g->row_off_.data(), static_cast<size_t>(g->rows_) * sizeof(eid_t));
+    be.entries_fill(recv.data(), nrecv, g->lo_, cursor.data(), g->col_.data());
+    be.synchronize();
+  }
+  g->build_heads();
+  return g;
+}
+
+std::unique_ptr<DeviceGraph> DeviceGraph::from_file(Backend& be, Comm& comm, const std::string& path, int threads) {
+  comm.bind_backend(&be);
+  const int P = comm.size(), rank = comm.rank();
+  if (is_binary_csr(path)) {
+    const BinaryCsrInfo info = binary_csr_info(path);
+    DBFS_CHECK(info.row_lo == 0 && info.rows == info.n, "a sharded read needs a whole-graph binary cache: " + path);
+    const Partition part = Partition::block(info.n, P);
+    const HostCSR shard = read_binary_csr_rows(path, part.lo(rank), part.lo(rank) + part.count(rank));
+    return from_host(be, shard, part, rank);
+  }
+  const EdgeShard es = read_edge_shard(
+      path, rank, P, [&comm](int64_t x) { return comm.allgather_host_i64(x); }, threads);
+  const Partition part = Partition::block(es.n, P);
+  return from_edges(be, comm, part, rank, es.m, es.u.data(), es.v.data(), es.local_edges());
 }
 
 ShardView DeviceGraph::view() const {

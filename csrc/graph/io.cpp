@@ -17,9 +17,11 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <thread>
 #include <sstream>
 
 #include "dbfs/graph.hpp"
+#include "dbfs/rmat.hpp"
 
 namespace dbfs {
 
@@ -378,6 +380,51 @@ HostCSR read_binary_csr_rows(const std::string& path, int64_t lo, int64_t hi) {
 HostCSR read_binary_csr(const std::string& path) {
   const BinaryCsrInfo info = binary_csr_info(path);
   return read_binary_csr_rows(path, info.row_lo, info.row_lo + info.rows);
+}
+
+void write_generated_edge_list(const std::string& path, const GenParams& p, int threads) {
+  // `n m` then the generator's edges (edge i is a pure function of (seed, i)),
+  // formatted by `threads` threads in chunks written in edge order.
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw Error("cannot write " + path);
+  std::fprintf(f, "%lld %lld\n", static_cast<long long>(p.n), static_cast<long long>(p.m));
+  const int T = threads > 0 ? threads : static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+  constexpr int64_t kChunk = int64_t(1) << 22;  // edges per thread per round
+  std::vector<std::string> buf(static_cast<size_t>(T));
+  bool ok = true;
+  for (int64_t base = 0; base < p.m && ok; base += kChunk * T) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const int64_t b = base + kChunk * t, e = std::min(p.m, b + kChunk);
+        std::string& out = buf[t];
+        out.clear();
+        if (b >= e) return;
+        out.resize(static_cast<size_t>(e - b) * 22);
+        char* w = &out[0];
+        auto put = [&w](uint64_t x, char end) {
+          char d[20];
+          int k = 0;
+          do {
+            d[k++] = static_cast<char>('0' + x % 10);
+            x /= 10;
+          } while (x);
+          while (k) *w++ = d[--k];
+          *w++ = end;
+        };
+        for (int64_t i = b; i < e; ++i) {
+          uint64_t u, v;
+          gen_edge(p, static_cast<uint64_t>(i), u, v);
+          put(u, ' ');
+          put(v, '\n');
+        }
+        out.resize(static_cast<size_t>(w - out.data()));
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < T && ok; ++t)
+      ok = buf[t].empty() || std::fwrite(buf[t].data(), 1, buf[t].size(), f) == buf[t].size();
+  }
+  if (std::fclose(f) != 0 || !ok) throw Error("short write to " + path);
 }
 
 void write_levels(const std::string& path, const std::vector<lvl_t>& levels) {

@@ -1,0 +1,344 @@
+// Sharded, multi-threaded edge-list reader: rank r of P parses only its byte
+// range of the file (plus the one token past its end that completes its last
+// edge) with T host threads, so no rank holds or scans the whole graph.
+//
+// Reference being replaced: readGraphFromFile (bfs.cu:829-880) -- one thread
+// reads the whole file into vector<vector<int>> -- which bfs_mpi.cu:815 runs on
+// EVERY rank.  Here the edges a rank parsed go to the GPU and are routed to
+// their owners there (DeviceGraph::from_edges: count -> all-to-all-v -> count
+// -> scan -> fill).
+//
+// Formats (same semantics as the whole-file reader, io.cpp):
+//   * reference: `n m` then m pairs `u v` (0-based), any whitespace layout --
+//     the byte ranges are cut at token boundaries; edge i is tokens 2i, 2i+1
+//     of the body, emitted by the rank whose range holds token 2i;
+//   * MatrixMarket: banner, `%` comments, `rows cols nnz`, then one entry
+//     `i j [value]` per line (1-based) -- ranges cut at line starts.
+// Extra tokens / entries after the m-th edge are ignored, fewer are an error,
+// ids out of range are an error (every rank throws the same message).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+
+#include "dbfs/shard_reader.hpp"
+
+namespace dbfs {
+
+namespace {
+
+constexpr vid_t kBadId = 0xFFFFFFFFu;  // never a vertex: n <= 2^32 - 1
+
+struct Mapped {
+  const char* data = nullptr;
+  size_t size = 0;
+  int fd = -1;
+  explicit Mapped(const std::string& path) {
+    fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw Error("not open " + path);
+    struct stat st {};
+    if (::fstat(fd, &st) != 0) {
+      ::close(fd);
+      throw Error("cannot stat " + path);
+    }
+    size = static_cast<size_t>(st.st_size);
+    if (size > 0) {
+      void* p = ::mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (p == MAP_FAILED) {
+        ::close(fd);
+        throw Error("cannot mmap " + path);
+      }
+      data = static_cast<const char*>(p);
+    }
+  }
+  ~Mapped() {
+    if (data) ::munmap(const_cast<char*>(data), size);
+    if (fd >= 0) ::close(fd);
+  }
+  // only this rank's range is touched: tell the kernel to read ahead there
+  void advise(size_t b, size_t e) const {
+    if (!data || b >= e) return;
+    const size_t pg = static_cast<size_t>(::sysconf(_SC_PAGESIZE));
+    const size_t a = b / pg * pg;
+    ::madvise(const_cast<char*>(data) + a, e - a, MADV_SEQUENTIAL);
+    ::madvise(const_cast<char*>(data) + a, e - a, MADV_WILLNEED);
+  }
+};
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+
+// Header integers (reference `n m`; MatrixMarket size line after banner and comments).
+struct Header {
+  int64_t n = 0, m = 0;
+  size_t body = 0;  // first byte after the header
+  bool mtx = false;
+};
+
+bool read_header_int(const char* d, size_t size, size_t& p, int64_t& out) {
+  while (p < size && is_space(d[p])) ++p;
+  if (p >= size) return false;
+  bool neg = false;
+  if (d[p] == '-' || d[p] == '+') {
+    neg = d[p] == '-';
+    ++p;
+  }
+  if (p >= size || !is_digit(d[p])) return false;
+  int64_t v = 0;
+  while (p < size && is_digit(d[p])) {
+    if (v > (INT64_MAX - 9) / 10) return false;
+    v = v * 10 + (d[p] - '0');
+    ++p;
+  }
+  out = neg ? -v : v;
+  return true;
+}
+
+Header parse_header(const Mapped& f, const std::string& path) {
+  Header h;
+  const char* d = f.data;
+  const size_t size = f.size;
+  size_t p = 0;
+  if (size >= 14 && (std::memcmp(d, "%%MatrixMarket", 14) == 0 || std::memcmp(d, "%%matrixmarket", 14) == 0)) {
+    h.mtx = true;
+    // banner, then blank / '%' lines, then the size line
+    for (;;) {
+      while (p < size && d[p] != '\n') ++p;
+      if (p < size) ++p;
+      size_t q = p;
+      while (q < size && (d[q] == ' ' || d[q] == '\t' || d[q] == '\r')) ++q;
+      if (q < size && (d[q] == '%' || d[q] == '\n')) continue;
+      break;
+    }
+    int64_t rows = 0, cols = 0, nnz = 0;
+    if (!read_header_int(d, size, p, rows) || !read_header_int(d, size, p, cols) ||
+        !read_header_int(d, size, p, nnz))
+      throw Error("bad MatrixMarket size line in " + path);
+    while (p < size && d[p] != '\n') ++p;  // rest of the size line
+    h.n = std::max(rows, cols);
+    h.m = nnz;
+  } else {
+    if (!read_header_int(d, size, p, h.n) || !read_header_int(d, size, p, h.m))
+      throw Error("bad header (expected `n m`) in " + path);
+  }
+  if (h.n < 0 || h.m < 0) throw Error("negative n or m in " + path);
+  if (h.n > int64_t(UINT32_MAX)) throw Error("vertex count exceeds 2^32 in " + path);
+  h.body = p;
+  return h;
+}
+
+// Cut [body, size) into k ranges: reference format at token boundaries,
+// MatrixMarket at line starts.  Every caller computes the same cuts.
+size_t align_cut(const char* d, size_t size, size_t body, size_t pos, bool lines) {
+  if (pos <= body) return body;
+  if (pos >= size) return size;
+  if (lines) {
+    while (pos < size && d[pos - 1] != '\n') ++pos;
+  } else {
+    while (pos < size && !is_space(d[pos - 1]) && !is_space(d[pos])) ++pos;
+  }
+  return pos;
+}
+
+size_t cut(const char* d, size_t size, size_t body, int64_t i, int64_t k, bool lines) {
+  const size_t len = size - body;
+  const size_t pos = body + static_cast<size_t>((static_cast<unsigned __int128>(len) * static_cast<uint64_t>(i)) /
+                                                static_cast<uint64_t>(k));
+  return align_cut(d, size, body, pos, lines);
+}
+
+// One parsed integer token as a vertex id (kBadId: negative, too long, or >= n
+// after the 1-based shift).
+inline vid_t parse_token(const char* d, size_t e, size_t& p, int64_t n, int64_t shift, bool& malformed) {
+  bool neg = false;
+  if (d[p] == '-' || d[p] == '+') {
+    neg = d[p] == '-';
+    ++p;
+  }
+  if (p >= e || !is_digit(d[p])) {
+    malformed = true;
+    return kBadId;
+  }
+  uint64_t v = 0;
+  bool big = false;
+  while (p < e && is_digit(d[p])) {
+    if (v < (uint64_t(1) << 40)) v = v * 10 + static_cast<uint64_t>(d[p] - '0');
+    else big = true;
+    ++p;
+  }
+  if (p < e && !is_space(d[p])) malformed = true;  // e.g. "12x"
+  if (neg || big || malformed) return kBadId;
+  const int64_t id = static_cast<int64_t>(v) - shift;
+  return (id >= 0 && id < n) ? static_cast<vid_t>(id) : kBadId;
+}
+
+// A thread's tokens (reference format) or entry pairs u0 v0 u1 v1 ...
+// (MatrixMarket); kBadId marks a malformed or out-of-range id, an error only
+// if one of the m edges uses it.
+struct Piece {
+  std::vector<vid_t> tok;
+};
+
+void parse_tokens(const char* d, size_t b, size_t e, int64_t n, Piece& out) {
+  size_t p = b;
+  while (p < e) {
+    while (p < e && is_space(d[p])) ++p;
+    if (p >= e) break;
+    bool mal = false;
+    out.tok.push_back(parse_token(d, e, p, n, 0, mal));
+    while (p < e && !is_space(d[p])) ++p;
+  }
+}
+
+void parse_mtx_lines(const char* d, size_t b, size_t e, int64_t n, Piece& out) {
+  size_t p = b;
+  while (p < e) {
+    size_t q = p;
+    while (q < e && (d[q] == ' ' || d[q] == '\t' || d[q] == '\r')) ++q;
+    if (q >= e) break;
+    if (d[q] == '\n' || d[q] == '%') {  // blank or comment line
+      while (q < e && d[q] != '\n') ++q;
+      p = q + 1;
+      continue;
+    }
+    bool mal = false;
+    const vid_t a = parse_token(d, e, q, n, 1, mal);
+    while (q < e && (d[q] == ' ' || d[q] == '\t')) ++q;
+    vid_t c = kBadId;
+    if (q < e && d[q] != '\n' && d[q] != '\r') c = parse_token(d, e, q, n, 1, mal);
+    out.tok.push_back(a);
+    out.tok.push_back(c);
+    while (q < e && d[q] != '\n') ++q;  // value column(s)
+    p = q + 1;
+  }
+}
+
+}  // namespace
+
+EdgeShard read_edge_shard(const std::string& path, int rank, int nranks, const HostAllgather& allgather,
+                          int threads) {
+  DBFS_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
+  DBFS_CHECK(path != "-", "sharded reads need a file (standard input is read whole)");
+  Mapped f(path);
+  EdgeShard s;
+  std::string err;
+  Header h;
+  try {
+    h = parse_header(f, path);
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  // every rank reads the same header; a failure is agreed so no rank is left
+  // waiting in a later exchange
+  {
+    const auto st = allgather(err.empty() ? 0 : 1);
+    for (int64_t x : st)
+      if (x) throw Error(err.empty() ? "edge list header unreadable on another rank: " + path : err);
+  }
+  s.n = h.n;
+  s.m = h.m;
+  s.format = h.mtx ? FileFormat::MatrixMarket : FileFormat::EdgeList;
+  const char* d = f.data;
+  const size_t size = f.size;
+  const bool lines = h.mtx;
+  const size_t rb = cut(d, size, h.body, rank, nranks, lines);
+  const size_t re = cut(d, size, h.body, rank + 1, nranks, lines);
+  s.byte_begin = static_cast<int64_t>(rb);
+  s.byte_end = static_cast<int64_t>(re);
+  f.advise(rb, re);
+
+  int T = threads > 0 ? threads : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+  T = static_cast<int>(std::min<size_t>(static_cast<size_t>(T), std::max<size_t>(1, (re - rb) / 4096)));
+  std::vector<Piece> pieces(static_cast<size_t>(T));
+  {
+    std::vector<std::thread> th;
+    std::vector<size_t> cuts(static_cast<size_t>(T) + 1);
+    for (int t = 0; t <= T; ++t) {
+      const size_t pos = rb + static_cast<size_t>((static_cast<unsigned __int128>(re - rb) * static_cast<uint64_t>(t)) /
+                                                   static_cast<uint64_t>(T));
+      cuts[t] = t == 0 ? rb : t == T ? re : std::min(re, align_cut(d, size, h.body, pos, lines));
+    }
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        const size_t b = std::min(cuts[t], re), e = std::max(b, std::min(cuts[t + 1], re));
+        if (lines) parse_mtx_lines(d, b, e, h.n, pieces[t]);
+        else parse_tokens(d, b, e, h.n, pieces[t]);
+      });
+    for (auto& x : th) x.join();
+  }
+  int64_t ntok = 0;
+  for (const Piece& pc : pieces) ntok += static_cast<int64_t>(pc.tok.size());
+  // token (or entry-pair) counts of every rank -> this rank's global position
+  const std::vector<int64_t> counts = allgather(ntok);
+  int64_t before = 0, total = 0;
+  for (int r = 0; r < nranks; ++r) {
+    if (r < rank) before += counts[r];
+    total += counts[r];
+  }
+  const int64_t need = 2 * h.m;  // tokens of the m edges
+  if (total < need) {
+    throw Error(std::string(h.mtx ? "truncated MatrixMarket entries" : "truncated edge list") + " in " + path +
+                ": expected " + std::to_string(h.m) + " edges, got " + std::to_string(total / 2));
+  }
+  // this rank's edges: those whose first token it holds (global index even, < 2m)
+  const int64_t g0 = before + (before & 1);  // first even global token index held
+  const int64_t g_end = std::min(before + ntok, need);
+  const int64_t my_edges = g_end > g0 ? (g_end - g0 + 1) / 2 : 0;
+  s.first_edge = g0 / 2;
+  s.u.resize(static_cast<size_t>(my_edges));
+  s.v.resize(static_cast<size_t>(my_edges));
+  // walk the pieces' tokens in order
+  int64_t g = before, e = 0;
+  vid_t pending = 0;
+  bool have_pending = false;
+  int64_t bad_edge = -1;
+  for (const Piece& pc : pieces) {
+    for (vid_t x : pc.tok) {
+      if (g >= g0 && g < g_end) {
+        if (!have_pending) {
+          pending = x;
+          have_pending = true;
+        } else {
+          if ((pending == kBadId || x == kBadId) && bad_edge < 0) bad_edge = e;
+          s.u[e] = pending;
+          s.v[e] = x;
+          ++e;
+          have_pending = false;
+        }
+      }
+      ++g;
+    }
+  }
+  if (have_pending) {
+    // the second token of the last edge lies past the range: read ahead
+    size_t p = re;
+    vid_t x = kBadId;
+    if (lines) {
+      // (MatrixMarket entries are whole lines: a pair never straddles a cut)
+      throw Error("internal: MatrixMarket entry split across ranks in " + path);
+    }
+    while (p < size && is_space(d[p])) ++p;
+    bool mal = false;
+    if (p < size) x = parse_token(d, size, p, h.n, 0, mal);
+    if ((pending == kBadId || x == kBadId) && bad_edge < 0) bad_edge = e;
+    s.u[e] = pending;
+    s.v[e] = x;
+    ++e;
+  }
+  DBFS_CHECK(e == my_edges, "internal: edge count mismatch in the sharded reader");
+  // agree on errors (global edge index of the first bad edge)
+  const int64_t code = bad_edge >= 0 ? s.first_edge + bad_edge + 1 : 0;
+  const auto bad = allgather(code);
+  for (int64_t c : bad)
+    if (c) {
+      throw Error(std::string(h.mtx ? "MatrixMarket entry " : "edge ") + std::to_string(c - 1) +
+                  " out of range [0, " + std::to_string(h.n) + ") or malformed in " + path);
+    }
+  return s;
+}
+
+}  // namespace dbfs

@@ -715,6 +715,18 @@ class Backend {
   virtual void exclusive_scan(eid_t* data, int64_t n) = 0;
   // col[cursor[u - lo]++] = v for every generated endpoint u owned
   virtual void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col) = 0;
+  // CSR build from a file's edges (DeviceGraph::from_edges): every edge
+  // (u, v) gives the entries u -> v and v -> u, routed to rank x / part as
+  // (row << 32 | neighbour).  counts[r] += entries for rank r; then the
+  // entries scattered into per-rank segments (cursor[r] = segment start,
+  // advanced); at the owner deg[row - lo] += 1 per entry (deg zeroed by the
+  // caller) and, after the scan, col[cursor[row - lo]++] = neighbour.
+  virtual void route_edges_count(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks,
+                                 int64_t* counts) = 0;
+  virtual void route_edges_fill(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks,
+                                int64_t* cursor, uint64_t* out) = 0;
+  virtual void entries_count(const uint64_t* e, int64_t k, int64_t lo, eid_t* deg) = 0;
+  virtual void entries_fill(const uint64_t* e, int64_t k, int64_t lo, eid_t* cursor, vid_t* col) = 0;
   // sum of degrees of vertices with level != kUnreached (device scalar out)
   virtual void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2) = 0;
   // over the shard's rows: out2[0] = sum of degree^2, out2[1] = rows with degree > 0

@@ -37,6 +37,17 @@ class DeviceGraph {
   static std::unique_ptr<DeviceGraph> from_host(Backend& be, const HostCSR& csr, const Partition& part, int rank);
   // Generate this rank's shard of a synthetic graph directly on the device.
   static std::unique_ptr<DeviceGraph> generate(Backend& be, const GenParams& p, const Partition& part, int rank);
+  // Build this rank's shard on the device from the edges this rank read (any
+  // slice of the file, e.g. read_edge_shard): every edge's two entries are
+  // routed to their owners (count -> all-to-all-v of (row, neighbour) pairs),
+  // then count -> scan -> fill as generate().  Collective over `comm`.
+  // input_edges: edges of the whole input (Graph500 TEPS numerator).
+  static std::unique_ptr<DeviceGraph> from_edges(Backend& be, Comm& comm, const Partition& part, int rank,
+                                                 int64_t input_edges, const vid_t* u, const vid_t* v,
+                                                 int64_t m_local);
+  // A file read in shards: edge list / MatrixMarket through read_edge_shard +
+  // from_edges, a binary CSR cache through its rank's rows only.  Collective.
+  static std::unique_ptr<DeviceGraph> from_file(Backend& be, Comm& comm, const std::string& path, int threads = 0);
 
   ShardView view() const;
   HostCSR to_host() const;  // the shard, copied back

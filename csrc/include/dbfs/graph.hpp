@@ -72,6 +72,12 @@ BinaryCsrInfo binary_csr_info(const std::string& path);
 HostCSR read_binary_csr_rows(const std::string& path, int64_t lo, int64_t hi);
 bool is_binary_csr(const std::string& path);
 
+// Reference-format edge list of a synthetic graph (generator edges in order),
+// formatted by `threads` host threads (0: all cores).  Test / benchmark inputs
+// for the file readers at scale (no dataset can be downloaded on the pool).
+struct GenParams;
+void write_generated_edge_list(const std::string& path, const GenParams& p, int threads = 0);
+
 // Write per-vertex levels, one per line, 2147483647 for unreached.
 void write_levels(const std::string& path, const std::vector<lvl_t>& levels);
 

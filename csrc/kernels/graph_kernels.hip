@@ -47,6 +47,84 @@ __global__ __launch_bounds__(kBlock) void gen_fill_kernel(GenParams p, int64_t l
   }
 }
 
+// ---- CSR build from a file's edges (DeviceGraph::from_edges) ----------------
+// Every input edge (u, v) yields the entries u -> v (owned by rank u / part) and
+// v -> u (rank v / part).  Pass 1 counts the entries per destination rank,
+// pass 2 scatters them into per-rank segments of the send buffer; both count
+// in LDS first and touch the global counters once per workgroup and rank
+// (device-scope atomics run at the memory side on MI355X: one per entry would
+// cost more than the whole build).  Entry = row << 32 | neighbour.
+constexpr int kMaxRouteRanks = 1024;
+
+__global__ __launch_bounds__(kBlock) void route_count_kernel(const vid_t* __restrict__ u, const vid_t* __restrict__ v,
+                                                            int64_t m, int64_t part, int nranks,
+                                                            unsigned long long* __restrict__ counts) {
+  __shared__ unsigned s_cnt[kMaxRouteRanks];
+  for (int r = threadIdx.x; r < nranks; r += kBlock) s_cnt[r] = 0;
+  __syncthreads();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < m; i += stride) {
+    atomicAdd(&s_cnt[u[i] / part], 1u);
+    atomicAdd(&s_cnt[v[i] / part], 1u);
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nranks; r += kBlock)
+    if (s_cnt[r]) atomicAdd(counts + r, static_cast<unsigned long long>(s_cnt[r]));
+}
+
+// One tile of kBlock edges per step: LDS counts -> one reservation per rank
+// -> stores.
+__global__ __launch_bounds__(kBlock) void route_fill_kernel(const vid_t* __restrict__ u, const vid_t* __restrict__ v,
+                                                           int64_t m, int64_t part, int nranks,
+                                                           unsigned long long* __restrict__ cursor,
+                                                           unsigned long long* __restrict__ out) {
+  __shared__ unsigned s_cnt[kMaxRouteRanks];
+  __shared__ unsigned long long s_base[kMaxRouteRanks];
+  for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBlock; t0 < m; t0 += static_cast<int64_t>(gridDim.x) * kBlock) {
+    for (int r = threadIdx.x; r < nranks; r += kBlock) s_cnt[r] = 0;
+    __syncthreads();
+    const int64_t i = t0 + threadIdx.x;
+    int ra = -1, rb = -1;
+    unsigned ka = 0, kb = 0;
+    vid_t a = 0, b = 0;
+    if (i < m) {
+      a = u[i];
+      b = v[i];
+      ra = static_cast<int>(a / part);
+      rb = static_cast<int>(b / part);
+      ka = atomicAdd(&s_cnt[ra], 1u);
+      kb = atomicAdd(&s_cnt[rb], 1u);
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < nranks; r += kBlock)
+      s_base[r] = s_cnt[r] ? atomicAdd(cursor + r, static_cast<unsigned long long>(s_cnt[r])) : 0ull;
+    __syncthreads();
+    if (i < m) {
+      out[s_base[ra] + ka] = (static_cast<unsigned long long>(a) << 32) | b;
+      out[s_base[rb] + kb] = (static_cast<unsigned long long>(b) << 32) | a;
+    }
+    __syncthreads();
+  }
+}
+
+// Received entries -> row degrees of the shard (rows [lo, lo + rows)).
+__global__ __launch_bounds__(kBlock) void entries_count_kernel(const unsigned long long* __restrict__ e, int64_t k,
+                                                              int64_t lo, unsigned long long* __restrict__ deg) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < k; i += stride)
+    atomicAdd(deg + (static_cast<int64_t>(e[i] >> 32) - lo), 1ull);
+}
+
+__global__ __launch_bounds__(kBlock) void entries_fill_kernel(const unsigned long long* __restrict__ e, int64_t k,
+                                                             int64_t lo, unsigned long long* __restrict__ cursor,
+                                                             vid_t* __restrict__ col) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < k; i += stride) {
+    const unsigned long long x = e[i];
+    col[atomicAdd(cursor + (static_cast<int64_t>(x >> 32) - lo), 1ull)] = static_cast<vid_t>(x & 0xFFFFFFFFull);
+  }
+}
+
 // Block-wide exclusive scan of `items` (kScanItems per thread, blocked layout).
 __device__ long long block_excl_scan(long long (&items)[kScanItems], long long* s_wave, long long& total) {
   long long sum = 0;
@@ -223,6 +301,34 @@ void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t
   gen_fill_kernel<<<capped_grid(p.m, 256 * 32), kBlock, 0, st>>>(
       p, lo, rows, reinterpret_cast<unsigned long long*>(cursor), col);
 }
+
+void route_edges_count(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* counts,
+                       hipStream_t st) {
+  if (m <= 0) return;
+  route_count_kernel<<<capped_grid(m, 256 * 16), kBlock, 0, st>>>(u, v, m, part, nranks,
+                                                                  reinterpret_cast<unsigned long long*>(counts));
+}
+
+void route_edges_fill(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* cursor,
+                      uint64_t* out, hipStream_t st) {
+  if (m <= 0) return;
+  route_fill_kernel<<<capped_grid(m, 256 * 16), kBlock, 0, st>>>(
+      u, v, m, part, nranks, reinterpret_cast<unsigned long long*>(cursor), reinterpret_cast<unsigned long long*>(out));
+}
+
+void entries_count(const uint64_t* e, int64_t k, int64_t lo, eid_t* deg, hipStream_t st) {
+  if (k <= 0) return;
+  entries_count_kernel<<<capped_grid(k, 256 * 32), kBlock, 0, st>>>(
+      reinterpret_cast<const unsigned long long*>(e), k, lo, reinterpret_cast<unsigned long long*>(deg));
+}
+
+void entries_fill(const uint64_t* e, int64_t k, int64_t lo, eid_t* cursor, vid_t* col, hipStream_t st) {
+  if (k <= 0) return;
+  entries_fill_kernel<<<capped_grid(k, 256 * 32), kBlock, 0, st>>>(
+      reinterpret_cast<const unsigned long long*>(e), k, lo, reinterpret_cast<unsigned long long*>(cursor), col);
+}
+
+int route_max_ranks() { return kMaxRouteRanks; }
 
 int64_t scan_tmp_elems(int64_t n) {
   int64_t total = 0;

@@ -75,6 +75,16 @@ void scan_assign(const ScanBfsArgs& a, hipStream_t st);
 // graph_kernels.hip
 void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg, hipStream_t st);
 void gen_fill(const GenParams& p, int64_t lo, int64_t rows, eid_t* cursor, vid_t* col, hipStream_t st);
+// CSR build from file edges: per-destination entry counts (counts[nranks],
+// added to), the entries scattered by destination (cursor[r] = segment start,
+// advanced), then the owner's row degrees (added to) and the row fill.
+void route_edges_count(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* counts,
+                       hipStream_t st);
+void route_edges_fill(const vid_t* u, const vid_t* v, int64_t m, int64_t part, int nranks, int64_t* cursor,
+                      uint64_t* out, hipStream_t st);
+void entries_count(const uint64_t* e, int64_t k, int64_t lo, eid_t* deg, hipStream_t st);
+void entries_fill(const uint64_t* e, int64_t k, int64_t lo, eid_t* cursor, vid_t* col, hipStream_t st);
+int route_max_ranks();
 // in-place exclusive scan of n + 1 entries; `tmp` must hold scan_tmp_elems(n) entries
 int64_t scan_tmp_elems(int64_t n);
 void exclusive_scan(eid_t* data, int64_t n, eid_t* tmp, hipStream_t st);

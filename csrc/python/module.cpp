@@ -8,6 +8,7 @@
 #include <cstring>
 
 #include "dbfs/engine.hpp"
+#include "dbfs/shard_reader.hpp"
 
 namespace py = pybind11;
 using namespace dbfs;
@@ -412,6 +413,32 @@ PYBIND11_MODULE(_dbfs_native, m) {
            })
       .def("barrier", &TcpBootstrap::barrier, py::call_guard<py::gil_scoped_release>());
 
+  py::class_<EdgeShard>(m, "EdgeShard")
+      .def_readonly("n", &EdgeShard::n)
+      .def_readonly("m", &EdgeShard::m)
+      .def_readonly("first_edge", &EdgeShard::first_edge)
+      .def_readonly("byte_begin", &EdgeShard::byte_begin)
+      .def_readonly("byte_end", &EdgeShard::byte_end)
+      .def_property_readonly("local_edges", &EdgeShard::local_edges)
+      .def_property_readonly("u", [](const EdgeShard& e) { return py::array_t<vid_t>(e.u.size(), e.u.data()); })
+      .def_property_readonly("v", [](const EdgeShard& e) { return py::array_t<vid_t>(e.v.size(), e.v.data()); });
+  m.def(
+      "write_generated_edge_list",
+      [](const std::string& path, const GenParams& p, int threads) {
+        py::gil_scoped_release rel;
+        write_generated_edge_list(path, p, threads);
+      },
+      py::arg("path"), py::arg("params"), py::arg("threads") = 0);
+  m.def(
+      "read_edge_shard",
+      [](const std::string& path, Comm& comm, int threads) {
+        py::gil_scoped_release rel;
+        return read_edge_shard(
+            path, comm.rank(), comm.size(), [&comm](int64_t x) { return comm.allgather_host_i64(x); }, threads);
+      },
+      py::arg("path"), py::arg("comm"), py::arg("threads") = 0,
+      "This rank's edges of an edge list / MatrixMarket file (collective: rank r parses only its byte range).");
+
   // ---- engine ----
   py::class_<DeviceGraph, std::shared_ptr<DeviceGraph>>(m, "DeviceGraph")
       .def_static(
@@ -428,6 +455,27 @@ PYBIND11_MODULE(_dbfs_native, m) {
             return std::shared_ptr<DeviceGraph>(DeviceGraph::generate(*be, p, part, rank));
           },
           py::arg("backend"), py::arg("params"), py::arg("partition"), py::arg("rank"), py::keep_alive<0, 1>())
+      .def_static(
+          "from_edges",
+          [](std::shared_ptr<Backend> be, Comm& comm, const Partition& part, int rank, int64_t input_edges,
+             py::array_t<vid_t, py::array::c_style | py::array::forcecast> u,
+             py::array_t<vid_t, py::array::c_style | py::array::forcecast> v) {
+            DBFS_CHECK(u.size() == v.size(), "u and v must have the same length");
+            const vid_t* pu = u.data();
+            const vid_t* pv = v.data();
+            const int64_t m = static_cast<int64_t>(u.size());
+            py::gil_scoped_release rel;
+            return std::shared_ptr<DeviceGraph>(DeviceGraph::from_edges(*be, comm, part, rank, input_edges, pu, pv, m));
+          },
+          py::arg("backend"), py::arg("comm"), py::arg("partition"), py::arg("rank"), py::arg("input_edges"),
+          py::arg("u"), py::arg("v"), py::keep_alive<0, 1>())
+      .def_static(
+          "from_file",
+          [](std::shared_ptr<Backend> be, Comm& comm, const std::string& path, int threads) {
+            py::gil_scoped_release rel;
+            return std::shared_ptr<DeviceGraph>(DeviceGraph::from_file(*be, comm, path, threads));
+          },
+          py::arg("backend"), py::arg("comm"), py::arg("path"), py::arg("threads") = 0, py::keep_alive<0, 1>())
       .def_property_readonly("n", &DeviceGraph::n)
       .def_property_readonly("lo", &DeviceGraph::lo)
       .def_property_readonly("rows", &DeviceGraph::rows)

@@ -54,20 +54,32 @@ class BFS:
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
                  alpha: float = 24.0, beta: float = 96.0, bu_lane_limit: int = 8, phase_timing: bool = False,
                  hub_sort: bool = True, force_exchange: bool = False, hubs: bool = True,
-                 max_hubs: Optional[int] = None, directed: bool = False):
+                 max_hubs: Optional[int] = None, directed: bool = False, sharded: bool = True,
+                 read_threads: int = 0):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
         frontier parent sooner (see csrc/kernels/graph_sort.hip).  ``hubs`` also
         indexes the highest-degree vertices so that bottom-up probes of them test
-        an LDS-resident copy of their frontier bits (needs ``hub_sort``)."""
+        an LDS-resident copy of their frontier bits (needs ``hub_sort``).
+
+        A file path is read in shards (``sharded``, the default for undirected
+        files): every rank parses only its byte range of an edge list /
+        MatrixMarket file with ``read_threads`` host threads and the CSR shard
+        is built on its GPU (edges routed to their owners by an all-to-all-v),
+        or reads only its rows of a binary CSR cache.  ``sharded=False`` reads
+        the whole file on every rank (the reference's bfs_mpi.cu:815 pattern)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         self.rt = runtime or init_runtime()
         if directed and mode in ("bu", "do"):
             raise ValueError("directed graphs need a top-down mode (td, ref, simple, scan)")
-        if isinstance(graph, str):
+        if isinstance(graph, str) and not (sharded and not directed and graph != "-"):
             graph = N.read_graph(graph, False, directed)
-        if isinstance(graph, N.GenParams):
+        if isinstance(graph, str):
+            self.graph = N.DeviceGraph.from_file(self.rt.backend, self.rt.comm, graph, int(read_threads))
+            self.n = self.graph.n
+            self.partition = self.graph.partition
+        elif isinstance(graph, N.GenParams):
             self.n = graph.n
             self.partition = N.Partition(graph.n, self.rt.world)
             self.graph = N.DeviceGraph.generate(self.rt.backend, graph, self.partition, self.rt.rank)
