@@ -83,6 +83,8 @@ def parse_args(argv=None):
                     help="engine tuning option (see Engine.get_options()), repeatable")
     ap.add_argument("--no-hubs", action="store_true", help="bottom-up without the LDS hub frontier")
     ap.add_argument("--max-hubs", type=int, default=None)
+    ap.add_argument("--no-id-order", action="store_true",
+                    help="keep the top-down adjacency in hub-first order (not neighbour-id order)")
     ap.add_argument("--device", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-int32-pass", action="store_true",
@@ -194,7 +196,8 @@ def main(argv=None) -> int:
         n_vertices, n_input_edges = params.n, params.m
     t0 = time.time()
     bfs = dbfs.BFS(params, rt, mode=args.mode, alpha=args.alpha, beta=args.beta,
-                   bu_lane_limit=args.bu_lane_limit, hubs=not args.no_hubs, max_hubs=args.max_hubs)
+                   bu_lane_limit=args.bu_lane_limit, hubs=not args.no_hubs, max_hubs=args.max_hubs,
+                   id_order=not args.no_id_order)
     for kv in args.opt:
         name, _, val = kv.partition("=")
         bfs.engine.set_option(name, float(val))

@@ -541,6 +541,11 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void sort_rows_by_id(const eid_t* ro, vid_t* col, int64_t rows, int64_t n) override {
+    (void)n;
+    for (int64_t r = 0; r < rows; ++r) std::sort(col + ro[r], col + ro[r + 1]);
+  }
+
   void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
     for (int64_t e = 0; e < nnz; ++e) out[e] = hub_idx[col[e]] != 0xFFFFFFFFu ? (kHubFlag | hub_idx[col[e]]) : col[e];
   }

@@ -284,6 +284,25 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipFree(count));
   }
 
+  void sort_rows_by_id(const eid_t* ro, vid_t* col, int64_t rows, int64_t n) override {
+    on();
+    eid_t nnz = 0;
+    HIP_CHECK(hipMemcpyAsync(&nnz, ro + rows, sizeof(nnz), hipMemcpyDeviceToHost, st_));
+    HIP_CHECK(hipStreamSynchronize(st_));
+    int64_t* list = nullptr;
+    unsigned long long* count = nullptr;
+    vid_t* tmp = nullptr;
+    HIP_CHECK(hipMalloc(&list, static_cast<size_t>(std::max<int64_t>(rows, 1)) * sizeof(int64_t)));
+    HIP_CHECK(hipMalloc(&count, sizeof(unsigned long long)));
+    HIP_CHECK(hipMalloc(&tmp, static_cast<size_t>(std::max<eid_t>(nnz, 1)) * sizeof(vid_t)));
+    kern::sort_rows_by_id(ro, col, rows, n, list, count, tmp, st_);
+    chk();
+    HIP_CHECK(hipStreamSynchronize(st_));
+    HIP_CHECK(hipFree(list));
+    HIP_CHECK(hipFree(count));
+    HIP_CHECK(hipFree(tmp));
+  }
+
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
     on();
     kern::gen_count_degrees(p, lo, rows, deg, st_);

@@ -317,7 +317,7 @@ static uint32_t hub_min_degree(const std::vector<uint32_t>& deg, int64_t cap) {
   return best;
 }
 
-void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hubs) {
+void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hubs, bool id_order) {
   DBFS_CHECK(max_hubs >= 0 && max_hubs <= kMaxHubs, "max_hubs out of range");
   DBFS_CHECK(comm.size() == part_.nranks && comm.rank() == rank_, "communicator does not match the shard");
   comm.bind_backend(be_);
@@ -332,6 +332,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   nhubs_ = 0;
   hub_vertex_.reset();
   hub_col_.reset();
+  col_by_id_ = false;
   // Hub encoding needs a free flag bit in the vertex ids.
   if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
     std::vector<uint32_t> deg(static_cast<size_t>(nall));
@@ -347,6 +348,12 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       hub_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
       be_->encode_hub_cols(col_.data(), nnz_, hub_idx.data(), hub_col_.data());
       build_heads(hub_idx.data());
+      // (only when bottom-up has the hub kernels -- the only ones that scan
+      // hub_col -- i.e. at least one hub was selected)
+      if (id_order && nhubs_ > 0) {
+        be_->sort_rows_by_id(row_off_.data(), col_.data(), rows_, part_.n);
+        col_by_id_ = true;
+      }
     } else {
       build_heads();
     }
@@ -883,7 +890,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = !res.levels.empty() && res.levels.back().direction == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
-      if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
+      if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       if (gv.nhubs > 0) {
@@ -1375,7 +1382,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = pf == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
-      if (!opt_.bu_hub_col) ba.g.hub_col = nullptr;
+      if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.ctrl = ctrl_.data();

@@ -690,6 +690,9 @@ class Backend {
   // then sort every row by (key_deg[neighbour] descending, neighbour ascending).
   virtual void degrees_u32(const eid_t* row_off, int64_t rows, uint32_t* out) = 0;
   virtual void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg) = 0;
+  // Every row in neighbour-id order (n: vertex count; the device orders rows
+  // of more than 4096 entries by 4096 id buckets only).
+  virtual void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n) = 0;
   // head[r] = col[row_off[r]] (0 for empty rows); with hub_idx (one entry per
   // vertex, UINT32_MAX for non-hubs) a hub head is stored as kHubFlag | index.
   virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head,

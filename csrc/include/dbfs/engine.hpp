@@ -64,8 +64,13 @@ class DeviceGraph {
   // `comm` (all ranks need every vertex's degree).  One-time preprocessing.
   // With `hubs`, the (up to kMaxHubs) highest-degree vertices of the graph are
   // also indexed and every row head naming one is hub-encoded (ShardView).
-  void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs);
+  // With hubs and `id_order`, bottom-up keeps the hub-first order in its
+  // hub-encoded copy and `col` is then put in neighbour-id order for the
+  // top-down sweeps (neighbours of one row probe the bitmaps monotonically).
+  void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs, bool id_order = true);
   bool hub_sorted() const { return hub_sorted_; }
+  // col is in id order (bottom-up must scan hub_col, whose order is hub-first)
+  bool col_by_id() const { return col_by_id_; }
   int64_t nhubs() const { return nhubs_; }
 
  private:
@@ -74,6 +79,7 @@ class DeviceGraph {
   int rank_ = 0;
   int64_t lo_ = 0, rows_ = 0, nnz_ = 0, input_edges_ = 0;
   bool hub_sorted_ = false;
+  bool col_by_id_ = false;
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_;

@@ -32,6 +32,10 @@ constexpr int kMaxLds = 4096;
 __device__ __forceinline__ unsigned long long sort_key(uint32_t deg, vid_t v) {
   return (static_cast<unsigned long long>(0xFFFFFFFFu - deg) << 32) | v;
 }
+// key_deg == nullptr: plain id order (top-down copy of the adjacency)
+__device__ __forceinline__ unsigned long long row_key(const uint32_t* __restrict__ key_deg, vid_t v) {
+  return sort_key(key_deg ? key_deg[v] : 0u, v);
+}
 
 __global__ __launch_bounds__(kBlock) void degrees_kernel(const eid_t* __restrict__ ro, int64_t rows,
                                                         uint32_t* __restrict__ out) {
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(kBlock) void sort_short_rows_kernel(const eid_t* __
     unsigned long long k = ~0ull;
     if (lane < len) {
       const vid_t v = col[b + lane];
-      k = sort_key(key_deg[v], v);
+      k = row_key(key_deg, v);
     }
 #pragma unroll
     for (int size = 2; size <= kWave; size <<= 1) {
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void sort_medium_rows_kernel(const eid_t* _
     for (int t = threadIdx.x; t < n2; t += kBlock) {
       if (t < len) {
         const vid_t v = col[b + t];
-        s[t] = sort_key(key_deg[v], v);
+        s[t] = row_key(key_deg, v);
       } else {
         s[t] = ~0ull;
       }
@@ -118,6 +122,65 @@ __global__ __launch_bounds__(kBlock) void sort_medium_rows_kernel(const eid_t* _
       }
     }
     for (int t = threadIdx.x; t < len; t += kBlock) col[b + t] = static_cast<vid_t>(s[t] & 0xFFFFFFFFull);
+    __syncthreads();
+  }
+}
+
+// Rows longer than kMaxLds in id order, approximately: a counting sort by the
+// top 12 bits of the id range (4096 buckets, one workgroup per row, LDS
+// histogram, scatter through `tmp`, copy back).  Within a bucket ids stay in
+// arrival order; a bucket spans n / 4096 ids, so a top-down sweep of a hub's
+// row walks the visited bitmap monotonically one bucket (<= a few cache lines
+// at RMAT-22 ... 26) at a time.
+constexpr int kLongThreads = 1024;
+constexpr int kBuckets = 4096;
+
+__global__ __launch_bounds__(kBlock) void list_long_rows_kernel(const eid_t* __restrict__ ro, int64_t rows,
+                                                               int64_t* __restrict__ list,
+                                                               unsigned long long* __restrict__ count) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= rows) return;
+  if (ro[r + 1] - ro[r] > kMaxLds) list[atomicAdd(count, 1ull)] = r;
+}
+
+__global__ __launch_bounds__(kLongThreads) void bucket_long_rows_kernel(const eid_t* __restrict__ ro,
+                                                                       vid_t* __restrict__ col,
+                                                                       const int64_t* __restrict__ list,
+                                                                       const unsigned long long* __restrict__ count,
+                                                                       vid_t* __restrict__ tmp, int shift) {
+  __shared__ unsigned s_pos[kBuckets];
+  __shared__ unsigned s_wave[kLongThreads / kWave];
+  constexpr int kPer = kBuckets / kLongThreads;
+  const unsigned long long nrows = *count;
+  const int t = threadIdx.x;
+  for (unsigned long long i = blockIdx.x; i < nrows; i += gridDim.x) {
+    const int64_t r = list[i];
+    const eid_t b = ro[r], e = ro[r + 1];
+    for (int k = t; k < kBuckets; k += kLongThreads) s_pos[k] = 0;
+    __syncthreads();
+    for (eid_t x = b + t; x < e; x += kLongThreads) atomicAdd(&s_pos[col[x] >> shift], 1u);
+    __syncthreads();
+    // exclusive scan of the 4096 bucket sizes (kPer consecutive per thread)
+    unsigned loc[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      loc[k] = sum;
+      sum += s_pos[t * kPer + k];
+    }
+    const unsigned incl = static_cast<unsigned>(wave_incl_scan(static_cast<long long>(sum)));
+    if (lane_id() == kWave - 1) s_wave[t >> 6] = incl;
+    __syncthreads();
+    unsigned off = incl - sum;
+    for (int w = 0; w < (t >> 6); ++w) off += s_wave[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s_pos[t * kPer + k] = off + loc[k];
+    __syncthreads();
+    for (eid_t x = b + t; x < e; x += kLongThreads) {
+      const vid_t v = col[x];
+      tmp[b + atomicAdd(&s_pos[v >> shift], 1u)] = v;
+    }
+    __syncthreads();
+    for (eid_t x = b + t; x < e; x += kLongThreads) col[x] = tmp[x];
     __syncthreads();
   }
 }
@@ -256,6 +319,19 @@ void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32
   list_medium_rows_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, rows,
                                                                                                   list, count);
   sort_medium_rows_kernel<<<4096, kBlock, 0, st>>>(row_off, col, list, count, key_deg);
+}
+
+void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n, int64_t* list,
+                     unsigned long long* count, vid_t* tmp, hipStream_t st) {
+  if (rows <= 0) return;
+  sort_neighbors(row_off, col, rows, nullptr, list, count, st);
+  int bits = 0;
+  while ((int64_t(1) << bits) < n) ++bits;
+  const int shift = bits > 12 ? bits - 12 : 0;
+  (void)hipMemsetAsync(count, 0, sizeof(unsigned long long), st);
+  list_long_rows_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, rows, list,
+                                                                                                count);
+  bucket_long_rows_kernel<<<1024, kLongThreads, 0, st>>>(row_off, col, list, count, tmp, shift);
 }
 
 }  // namespace kern

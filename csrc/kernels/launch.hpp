@@ -107,6 +107,10 @@ void hub_assign(const uint32_t* deg, int64_t n, uint32_t min_deg, const eid_t* c
 // list must hold `rows` entries; count is one device counter
 void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32_t* key_deg, int64_t* list,
                     unsigned long long* count, hipStream_t st);
+// rows in id order (rows of 2..4096 exactly, longer rows by 4096 id buckets);
+// tmp holds nnz entries
+void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n, int64_t* list,
+                     unsigned long long* count, vid_t* tmp, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
 void degree_moments(const ShardView& g, int64_t* out2, hipStream_t st);
 

@@ -112,6 +112,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
   m.attr("UNREACHED") = py::int_(kUnreached);
   m.attr("TD_EDGES_PER_BLOCK") = py::int_(kTdEdgesPerBlock);
   m.attr("UNIT_VERTICES") = py::int_(kUnitVertices);
+  m.attr("MAX_HUBS") = py::int_(kMaxHubs);
 
   // ---- graphs ----
   py::class_<HostCSR>(m, "HostCSR")
@@ -485,7 +486,9 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("partition", &DeviceGraph::partition)
       .def("to_host", &DeviceGraph::to_host, py::call_guard<py::gil_scoped_release>())
       .def("sort_neighbors_by_degree", &DeviceGraph::sort_neighbors_by_degree, py::arg("comm"),
-           py::arg("hubs") = true, py::arg("max_hubs") = kMaxHubs, py::call_guard<py::gil_scoped_release>())
+           py::arg("hubs") = true, py::arg("max_hubs") = kMaxHubs, py::arg("id_order") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("col_by_id", &DeviceGraph::col_by_id)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
       .def("degrees_of", &DeviceGraph::degrees_of);

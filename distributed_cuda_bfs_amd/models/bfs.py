@@ -55,12 +55,14 @@ class BFS:
                  alpha: float = 24.0, beta: float = 96.0, bu_lane_limit: int = 8, phase_timing: bool = False,
                  hub_sort: bool = True, force_exchange: bool = False, hubs: bool = True,
                  max_hubs: Optional[int] = None, directed: bool = False, sharded: bool = True,
-                 read_threads: int = 0):
+                 read_threads: int = 0, id_order: bool = True):
         """``hub_sort`` reorders every adjacency row by neighbour degree (descending)
         once, before any traversal: levels are unchanged, bottom-up probes find a
         frontier parent sooner (see csrc/kernels/graph_sort.hip).  ``hubs`` also
         indexes the highest-degree vertices so that bottom-up probes of them test
-        an LDS-resident copy of their frontier bits (needs ``hub_sort``).
+        an LDS-resident copy of their frontier bits (needs ``hub_sort``); with
+        hubs and ``id_order`` the top-down copy of the adjacency is then put in
+        neighbour-id order (bottom-up keeps the hub-first order).
 
         A file path is read in shards (``sharded``, the default for undirected
         files): every rank parses only its byte range of an edge list /
@@ -90,10 +92,8 @@ class BFS:
         else:
             raise TypeError("graph must be a path, HostCSR or GenParams")
         if hub_sort:
-            if max_hubs is None:
-                self.graph.sort_neighbors_by_degree(self.rt.comm, hubs)
-            else:
-                self.graph.sort_neighbors_by_degree(self.rt.comm, hubs, int(max_hubs))
+            cap = N.MAX_HUBS if max_hubs is None else int(max_hubs)
+            self.graph.sort_neighbors_by_degree(self.rt.comm, hubs, cap, id_order)
         self.engine = N.Engine(self.graph, self.rt.comm, mode=mode, alpha=alpha, beta=beta,
                                bu_lane_limit=bu_lane_limit, phase_timing=phase_timing,
                                force_exchange=force_exchange)

@@ -223,8 +223,8 @@ def test_hub_sort_orders_rows_and_keeps_levels(rt):
     p = dbfs.rmat_params(11, 16, 12)
     csr = dbfs.host_csr_from_params(p)
     exp = _oracle(csr, 4)
-    bfs = dbfs.BFS(p, rt, mode="do", hub_sort=True)
-    assert bfs.graph.hub_sorted
+    bfs = dbfs.BFS(p, rt, mode="do", hub_sort=True, id_order=False)
+    assert bfs.graph.hub_sorted and not bfs.graph.col_by_id
     g = bfs.graph.to_host()
     ro, col = np.asarray(g.row_off), np.asarray(g.col)
     deg = np.diff(np.asarray(csr.row_off))
@@ -237,6 +237,35 @@ def test_hub_sort_orders_rows_and_keeps_levels(rt):
         assert sorted(row.tolist()) == sorted(np.asarray(csr.col)[ro[r]:ro[r + 1]].tolist())
     bfs.run(4)
     assert np.array_equal(bfs.levels(), exp)
+
+
+def test_id_order_top_down_copy_keeps_levels(rt):
+    """With hubs, `col` is put in neighbour-id order for the top-down sweeps
+    (bottom-up scans the hub-first, hub-encoded copy): every row sorted, same
+    multiset, levels unchanged in every mode and loop."""
+    p = dbfs.rmat_params(11, 16, 14)
+    csr = dbfs.host_csr_from_params(p)
+    # no hub selected (cap 0): the hub-free bottom-up kernels scan `col`
+    # head-first, so it keeps its order
+    assert not dbfs.BFS(p, rt, mode="do", max_hubs=0).graph.col_by_id
+    bfs = dbfs.BFS(p, rt, mode="do")
+    assert bfs.graph.col_by_id and bfs.graph.nhubs > 0
+    g = bfs.graph.to_host()
+    ro, col = np.asarray(g.row_off), np.asarray(g.col)
+    for r in range(g.rows):
+        row = col[ro[r]:ro[r + 1]]
+        assert np.all(row[:-1] <= row[1:])
+        assert np.array_equal(row, np.sort(np.asarray(csr.col)[ro[r]:ro[r + 1]]))
+    for mode in ("do", "td", "bu"):
+        bfs.mode = mode
+        for opt in ({}, {"bu_hub_col": 0}, {"device_loop": 0}):
+            for k, v in opt.items():
+                bfs.engine.set_option(k, v)
+            for s in (4, 77):
+                bfs.run(s)
+                assert np.array_equal(bfs.levels(), _oracle(csr, s))
+            for k in opt:
+                bfs.engine.set_option(k, 1)
 
 
 @pytest.mark.parametrize("predict", [1, 0])
