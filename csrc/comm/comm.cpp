@@ -119,6 +119,7 @@ VirtualComm::VirtualComm(std::shared_ptr<VirtualGroup> g, int rank, Backend& be)
 }
 
 void VirtualComm::alltoall(const void* send, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   be_->synchronize();
   auto& sl = g_->slots();
   sl[rank_].send = send;
@@ -131,6 +132,7 @@ void VirtualComm::alltoall(const void* send, void* recv, size_t bytes) {
 }
 
 void VirtualComm::allgather(const void* send, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   be_->synchronize();
   auto& sl = g_->slots();
   sl[rank_].send = send;
@@ -142,6 +144,7 @@ void VirtualComm::allgather(const void* send, void* recv, size_t bytes) {
 }
 
 void VirtualComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   be_->synchronize();
   auto& sl = g_->slots();
   sl[rank_].send = buf;
@@ -159,6 +162,7 @@ void VirtualComm::allreduce_sum_i64(int64_t* buf, size_t count) {
 
 void VirtualComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                             const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
   be_->synchronize();
   auto& sl = g_->slots();
   sl[rank_].send = send;
@@ -176,6 +180,7 @@ void VirtualComm::alltoallv(const void* send, const int64_t* sc, const int64_t* 
 }
 
 void VirtualComm::barrier() {
+  note(kBarrier, 0);
   be_->synchronize();
   g_->barrier();
 }

@@ -113,18 +113,21 @@ void NcclComm::check_alive() const {
 }
 
 void NcclComm::alltoall(const void* send, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allgather(const void* send, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, C(comm_), S(be_)));
@@ -132,6 +135,7 @@ void NcclComm::allreduce_sum_i64(int64_t* buf, size_t count) {
 
 void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                          const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
   NCCL_CHECK(ncclGroupStart());
@@ -150,6 +154,7 @@ void NcclComm::group_start() { NCCL_CHECK(ncclGroupStart()); }
 void NcclComm::group_end() { NCCL_CHECK(ncclGroupEnd()); }
 
 void NcclComm::barrier() {
+  note(kBarrier, 0);
   int64_t* b = scratch(1);
   allreduce_sum_i64(b, 1);  // value irrelevant: completion on every rank is the barrier
   be_->synchronize();

@@ -202,6 +202,7 @@ void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& rec
 }
 
 void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   if (bytes > slot_ || bytes % 4) {
     ++inner_ops_;
     inner_->alltoall(send, recv, bytes);
@@ -216,6 +217,7 @@ void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
 }
 
 void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   if (bytes > slot_ || bytes % 4) {
     ++inner_ops_;
     inner_->allgather(send, recv, bytes);
@@ -230,6 +232,7 @@ void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
 }
 
 void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   const size_t bytes = count * sizeof(int64_t);
   if (bytes > slot_ || count == 0) {
     ++inner_ops_;
@@ -246,6 +249,7 @@ void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
 
 void PeerComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                          const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
   bool fits = eb % 4 == 0;
   for (int p = 0; p < size_ && fits; ++p)
     fits = static_cast<size_t>(std::max(sc[p], rc[p])) * eb <= slot_;
@@ -324,6 +328,7 @@ bool PeerComm::self_test(std::string* why) {
 }
 
 void PeerComm::barrier() {
+  note(kBarrier, 0);
   int64_t* b = scratch(1);
   allreduce_sum_i64(b, 1);  // value irrelevant: completion on every rank is the barrier
   be_->synchronize();

@@ -232,17 +232,20 @@ void TcpComm::store(void* p, const std::string& s, size_t off, size_t bytes) {
 }
 
 void TcpComm::alltoall(const void* send, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   const int P = size(), me = rank();
   auto all = boot_->allgather(fetch(send, bytes * P));
   for (int r = 0; r < P; ++r) store(static_cast<char*>(recv) + r * bytes, all[r], me * bytes, bytes);
 }
 
 void TcpComm::allgather(const void* send, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   auto all = boot_->allgather(fetch(send, bytes));
   for (int r = 0; r < size(); ++r) store(static_cast<char*>(recv) + r * bytes, all[r], 0, bytes);
 }
 
 void TcpComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   auto all = boot_->allgather(fetch(buf, count * sizeof(int64_t)));
   // two's-complement (wrapping) sums, as RCCL's: the engine also reduces
   // disjoint bit sets (hub frontier words) and, on no-op chains, stale blocks
@@ -258,6 +261,7 @@ void TcpComm::allreduce_sum_i64(int64_t* buf, size_t count) {
 
 void TcpComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                         const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
   const int P = size(), me = rank();
   // message: P (offset, count) pairs, then the concatenated pieces
   std::string msg(static_cast<size_t>(P) * 2 * sizeof(int64_t), '\0');
@@ -280,6 +284,7 @@ void TcpComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, 
 }
 
 void TcpComm::barrier() {
+  note(kBarrier, 0);
   be_->synchronize();
   boot_->barrier();
 }

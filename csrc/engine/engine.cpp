@@ -1218,6 +1218,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     const bool in_carry = L == 0 ? seed_carry : enq_carry[static_cast<size_t>(L - 1)] != 0;
     enq_dir[L] = d == 'B' ? 'B' : 'T';
     enq_form[L] = d;
+    res.chains.push_back({L, d, d == 'L' ? cap : 0});
     enq_cap[L] = d == 'L' ? cap : 0;
     // carry the hub bits out of dense and bottom-up chains (the ones a
     // bottom-up level follows); list chains are the small levels

@@ -70,7 +70,31 @@ class Comm {
     be_ = be;
   }
 
+  // Traffic of this rank since reset_traffic(): calls per collective and the
+  // bytes this rank sends to the other ranks under a direct exchange --
+  // alltoall / allgather (P - 1) x the per-peer bytes, all-reduce (P - 1) x
+  // the vector, alltoallv the counts to other ranks; barriers count calls.
+  // (docs/ARCHITECTURE.md §4 models these per level; tests check the model.)
+  enum TrafficKind { kAllToAll = 0, kAllGather, kAllReduce, kAllToAllV, kBarrier, kTrafficKinds };
+  struct Traffic {
+    int64_t calls[kTrafficKinds] = {};
+    int64_t bytes[kTrafficKinds] = {};
+  };
+  const Traffic& traffic() const { return traffic_; }
+  void reset_traffic() { traffic_ = Traffic{}; }
+
  protected:
+  void note(TrafficKind k, int64_t bytes) {
+    ++traffic_.calls[k];
+    traffic_.bytes[k] += bytes;
+  }
+  void note_alltoallv(const int64_t* sc, size_t eb) {
+    int64_t b = 0;
+    for (int p = 0; p < size(); ++p)
+      if (p != rank()) b += sc[p] * static_cast<int64_t>(eb);
+    note(kAllToAllV, b);
+  }
+  Traffic traffic_;
   // Small persistent device scratch for the host-value helpers and barriers
   // (no hipMalloc/hipFree -- which synchronise the device -- per call).
   int64_t* scratch(size_t n_int64);

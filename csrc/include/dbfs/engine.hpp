@@ -201,6 +201,15 @@ struct LevelRecord {
   double gap_ms = -1.0;
 };
 
+// One level chain the device loop enqueued (mispredicted ones included):
+// form 'T' dense top-down, 'S' sparse top-down, 'L' list top-down (several
+// ranks, `cap` = global frontier edges its lists hold), 'B' bottom-up.
+struct ChainRecord {
+  int level = 0;
+  char form = 'T';
+  int64_t cap = 0;
+};
+
 struct RunResult {
   int64_t source = 0;
   double ms = 0.0;             // wall time of the traversal (max over ranks)
@@ -210,6 +219,7 @@ struct RunResult {
   double gteps = 0.0;
   int mispredicts = 0;         // device loop: level chains enqueued for the wrong direction
   std::vector<LevelRecord> levels;
+  std::vector<ChainRecord> chains;  // device loop: every chain enqueued, in order
 };
 
 // Fault injection for failure-detection tests (see Engine::inject_fault).

@@ -259,6 +259,17 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def("sum_host", &Comm::sum_host, py::call_guard<py::gil_scoped_release>())
       .def("max_host", &Comm::max_host, py::call_guard<py::gil_scoped_release>())
       .def("allgather_host_i64", &Comm::allgather_host_i64, py::call_guard<py::gil_scoped_release>())
+      .def("reset_traffic", &Comm::reset_traffic)
+      .def(
+          "traffic",
+          [](const Comm& c) {
+            // {kind: (calls, bytes sent to other ranks)}
+            static const char* names[] = {"alltoall", "allgather", "allreduce", "alltoallv", "barrier"};
+            py::dict d;
+            for (int k = 0; k < Comm::kTrafficKinds; ++k)
+              d[names[k]] = py::make_tuple(c.traffic().calls[k], c.traffic().bytes[k]);
+            return d;
+          })
       .def("bind_backend", [](Comm& c, std::shared_ptr<Backend> be) { c.bind_backend(be.get()); },
            py::keep_alive<1, 2>());
   m.def(
@@ -501,6 +512,13 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_readonly("depth", &RunResult::depth)
       .def_readonly("gteps", &RunResult::gteps)
       .def_readonly("mispredicts", &RunResult::mispredicts)
+      .def_property_readonly("chains",
+                             [](const RunResult& r) {
+                               py::list out;
+                               for (const auto& c : r.chains)
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap));
+                               return out;
+                             })
       .def("level_dicts", &level_dicts);
 
   py::class_<Engine, std::shared_ptr<Engine>>(m, "Engine")

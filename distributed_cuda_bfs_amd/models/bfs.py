@@ -31,6 +31,12 @@ class BFSResult:
         self._native, self._levels = native, levels
 
     @property
+    def chains(self) -> List[Any]:
+        """Device loop: every level chain enqueued, in order, as (level, form,
+        list capacity) -- form T / S / L / B (mispredicted chains included)."""
+        return list(self._native.chains) if self._native is not None else []
+
+    @property
     def levels(self) -> List[Dict[str, Any]]:
         if self._levels is None:
             self._levels = list(self._native.level_dicts()) if self._native is not None else []
