@@ -72,7 +72,10 @@ class CpuBackend final : public Backend {
       int64_t cnt = 0, deg = 0;
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
-        if (use_bytes) {
+        if (use_bytes && a.level_direct) {
+          for (int b = 0; b < 64; ++b)
+            if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.new_level)) c |= 1ull << b;
+        } else if (use_bytes) {
           c = gather_bytes(a.cand_bytes + w * 64);
         } else {
           for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + w];
@@ -245,6 +248,8 @@ class CpuBackend final : public Backend {
         if (a.lists) {
           vid_t* list = a.lists + static_cast<int64_t>(v / a.part) * (a.list_cap + 1);
           list[1 + list[0]++] = v;
+        } else if (bytes && a.level_direct) {
+          a.level_direct[v] = static_cast<uint8_t>(a.new_level);
         } else if (bytes) {
           a.next_bytes[v] = 1;
         } else {

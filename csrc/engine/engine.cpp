@@ -72,6 +72,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
+  else if (name == "td_direct") o.td_direct = v != 0;
+  else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "bu_split") o.bu_split = v != 0;
@@ -101,6 +103,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
+          {"td_direct", o.td_direct ? 1.0 : 0.0},
+          {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
@@ -562,7 +566,10 @@ RunResult Engine::run(int64_t source) {
   RunResult r;
   const bool ref = opt_.mode == Mode::Ref || opt_.mode == Mode::Scan;
   run_narrow_ = !ref && use_narrow();
-  if (run_narrow_ && level8_.size() == 0) level8_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
+  // (padded to whole bitmap words: a direct top-down update reads a word's
+  // 64 level bytes; padding vertices are pre-set visited, so masked)
+  if (run_narrow_ && level8_.size() == 0)
+    level8_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1)));
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
   levels_narrow_ = run_narrow_;
   if (run_narrow_ && r.depth - 1 > kNarrowMaxLevel) {
@@ -989,7 +996,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     mailbox_host_ = static_cast<LevelMailbox*>(be_.alloc_mapped(sizeof(LevelMailbox) * kMailboxSlots, &dptr));
     mailbox_dev_ = static_cast<LevelMailbox*>(dptr);
   }
-  const bool bytes_ok = opt_.mode != Mode::BottomUp && opt_.td_byte_edges <= total_directed_;
+  // one rank with narrow levels: byte-map levels write the levels directly
+  const bool direct = !xc && run_narrow_ && opt_.td_direct;
+  const int64_t byte_edges = direct ? opt_.td_direct_edges : opt_.td_byte_edges;
+  const bool bytes_ok = opt_.mode != Mode::BottomUp && byte_edges <= total_directed_;
   if (bytes_ok && !next_bytes_.data()) {
     next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
     be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
@@ -1084,7 +1094,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   init.beta = opt_.beta;
   init.n = static_cast<double>(part_.n);
   init.total_directed = static_cast<double>(total_directed_);
-  init.td_byte_edges = bytes_ok ? static_cast<double>(opt_.td_byte_edges) : 1e300;
+  init.td_byte_edges = bytes_ok ? static_cast<double>(byte_edges) : 1e300;
   init.check_visited_min = opt_.td_check_visited_min;
   init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
   // one fused pass: levels, visited, the seed frontier (frontier_[1]), its
@@ -1341,6 +1351,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       } else {
         ta.next = next_.data();
         ta.next_bytes = next_bytes_.data();
+        // (a level past kNarrowMaxLevel would store the unreached byte:
+        // the usual path flags the overflow and the run is repeated wide)
+        if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {
+          // byte-map levels write the level itself (nothing to clear after)
+          ta.level_direct = level8_.data();
+          ta.new_level = L + 1;
+          tu.level_direct = level8_.data();
+        }
         be_.td_expand(ta);
         tu.cand = next_.data();
         tu.cand_bytes = next_bytes_.data();

@@ -228,6 +228,10 @@ struct UpdateArgs {
   // ctrl->bytes, else cand (both given).
   const LevelCtrl* ctrl = nullptr;
   int64_t max_mf = 0;  // list-form chain: live only while ctrl->m_f <= max_mf
+  // With the byte-map levels of TdArgs::level_direct: candidates are the
+  // unvisited vertices whose level already reads new_level (level8, padded to
+  // whole words); cand_bytes is not read.
+  const uint8_t* level_direct = nullptr;
 };
 
 // Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
@@ -378,6 +382,13 @@ struct TdArgs {
   int64_t part = 0;   // owner(v) = v / part
   // Byte mode only: skip the visited pre-check (few vertices visited yet).
   bool check_visited = true;
+  // One rank, narrow levels, byte-map levels: instead of marking next_bytes,
+  // store new_level straight into the level array of every unvisited
+  // candidate (plain byte stores; the visited check is then always made) --
+  // update_frontier(level_direct) derives the new frontier from it, nothing to
+  // clear afterwards.
+  uint8_t* level_direct = nullptr;
+  lvl_t new_level = 0;
   // Launch 1024-thread workgroups when the grid has fewer blocks than this.
   int64_t wide_below_blocks = 0;
   // Device loop: q / m come from dev_stats[0..1], bits vs bytes and the

@@ -274,6 +274,24 @@ __device__ __forceinline__ word_t gather_byte_bits(uint8_t* p) {
   return bits;
 }
 
+// 64 level bytes (64-byte aligned) -> bit b set when byte b == lvl.
+__device__ __forceinline__ word_t gather_level_bits(const uint8_t* p, uint8_t lvl) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  word_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 x = q[k];
+    const unsigned v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if (((v[j] >> (8 * b)) & 0xFFu) == lvl) bits |= 1ull << (k * 16 + j * 4 + b);
+    }
+  }
+  return bits;
+}
+
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
@@ -289,7 +307,9 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   word_t nb = 0;
   if (wl < a.words) {
     word_t c = 0;
-    if (use_bytes) {
+    if (use_bytes && a.level_direct) {
+      c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+    } else if (use_bytes) {
       c = gather_byte_bits(a.cand_bytes + wl * 64);
     } else {
       for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
@@ -312,7 +332,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     const int pos = wave_set_position(nb, incl, idx);
     if (idx < total) {
       const int64_t v = w0 * 64 + pos;
-      store_level(a.level, a.level8, v, a.new_level);
+      if (!(use_bytes && a.level_direct)) store_level(a.level, a.level8, v, a.new_level);
       const eid_t d = ro[v + 1] - ro[v];
       if (d > 0) {
         cnt += 1;
@@ -619,6 +639,19 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
           const word_t bit = 1ull << (vk[k] & 63);
           if (!(seen[k] & bit)) atomicOr(a.next + (vk[k] >> 6), bit);
         }
+        continue;
+      }
+      if (a.level_direct) {
+        // the level itself, for unvisited candidates only (a visited vertex
+        // keeps its level); repeated targets store the same byte again
+        const uint8_t lv = static_cast<uint8_t>(a.new_level);
+        bool keep[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          keep[k] = k * kThreads + t < cnt && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          if (keep[k]) a.level_direct[vk[k]] = lv;
         continue;
       }
       // byte map: with few visited vertices the check costs more than the

@@ -492,3 +492,21 @@ def test_tiny_and_isolated_sources(rt, case):
 
     for lv in run_virtual_ranks(3, body, device="cpu"):
         assert np.array_equal(lv, exp)
+
+
+@pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("direct_edges", [0, 1 << 40])
+def test_td_direct_levels_cpu(rt, mode, direct_edges):
+    p = dbfs.rmat_params(12, 16, 38)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    bfs.engine.set_option("td_direct_edges", direct_edges)
+    for s in (0, 9, 3000):
+        bfs.run(s)
+        assert np.array_equal(bfs.levels(), _oracle(csr, s))
+    n = 400
+    chain = dbfs.build_csr(n, np.arange(n - 1, dtype=np.uint32), np.arange(1, n, dtype=np.uint32))
+    cb = dbfs.BFS(chain, rt, mode=mode)
+    cb.engine.set_option("td_direct_edges", direct_edges)
+    cb.run(0)
+    assert np.array_equal(cb.levels(), np.arange(n))

@@ -611,3 +611,23 @@ def test_peer_comm_two_ranks_share_one_gpu():
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["comm_note"] is None
     assert rec["validated"] is True and rec["validated_roots"] == "4/4"
+
+
+@pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("direct_edges", [0, 1 << 16, 1 << 40])
+def test_td_direct_levels_gpu(gpu_runtime, mode, direct_edges):
+    """One rank, narrow levels: top-down levels store the level byte of every
+    unvisited candidate directly (td_direct) from `direct_edges` frontier edges
+    on (0: every dense level, 2^40: never); exact against the oracle, also
+    with a long chain (levels past the narrow range fall back and rerun)."""
+    p = dbfs.rmat_params(17, 16, 37)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    bfs.engine.set_option("td_direct_edges", direct_edges)
+    for src in bfs.sample_roots(3, seed=41):
+        _check(bfs, csr, src)
+    n = 600
+    chain = dbfs.build_csr(n, np.arange(n - 1, dtype=np.uint32), np.arange(1, n, dtype=np.uint32))
+    cb = dbfs.BFS(chain, gpu_runtime, mode=mode)
+    cb.engine.set_option("td_direct_edges", direct_edges)
+    _check(cb, chain, 0)
