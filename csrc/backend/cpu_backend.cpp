@@ -204,7 +204,7 @@ class CpuBackend final : public Backend {
   }
 
   void compact_frontier(const CompactArgs& a) override {
-    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T')) return;
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
       int64_t pos = a.unit_cnt_off[u] + a.part_cnt[u / kScanChunk];
@@ -276,7 +276,7 @@ class CpuBackend final : public Backend {
   }
 
   void td_sparse(const TdSparseArgs& a) override {
-    if (a.ctrl->done || a.ctrl->dir != 'T') return;
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     const int64_t q = a.dev_stats[0];
     for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
     int64_t cnt = 0, deg = 0;

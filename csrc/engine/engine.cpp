@@ -73,6 +73,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
+  else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
@@ -104,6 +105,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
+          {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
@@ -1005,6 +1007,20 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
   }
   const bool sparse = sparse_enabled() && !xc;
+  // A sparse chain is live up to this many frontier edges; a level that turns
+  // out larger (a geometric prediction can be off by 100x on the second
+  // level) is re-enqueued dense: fetch-or claims on every edge cost more than
+  // a dense level's fixed passes from there on.
+  // (Only with the predicting loop, which enqueues one chain ahead: without
+  // prediction the next level's chain is already queued behind a chain found
+  // invalid, and a chain of the right direction would run out of turn -- so
+  // there only direction mismatches invalidate a chain, and level 0 is never
+  // a list chain.)
+  const int64_t sparse_cap = opt_.device_loop_predict && opt_.td_sparse_cap_factor > 0
+                                 ? std::max<int64_t>(opt_.td_sparse_edges,
+                                                     static_cast<int64_t>(opt_.td_sparse_cap_factor *
+                                                                          static_cast<double>(opt_.td_sparse_edges)))
+                                 : 0;
   if (sparse && !sparse_ready_) {
     const size_t rows = static_cast<size_t>(std::max<int64_t>(g_.rows(), 1));
     qscan2_ = DBuf<int64_t>(be_, rows + 1);
@@ -1270,6 +1286,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ca.clear = frontier_[cur].data();
       }
       ca.ctrl = ctrl_.data();
+      ca.max_mf = d == 'S' ? sparse_cap : 0;
       be_.compact_frontier(ca);
     };
     if (d == 'S') {
@@ -1301,6 +1318,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
       sp.first = pf != 'T';
+      sp.max_mf = sparse_cap;
       be_.td_sparse(sp);
     } else if (d == 'T' || d == 'L') {
       // a sparse level (or the seed) already handed over the work list
@@ -1525,12 +1543,15 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // and mf global frontier edges
   auto chain_valid = [&](int L, char dir, int64_t mf) {
     if (enq_dir[L] != dir) return false;
+    if (enq_form[L] == 'S') return sparse_cap <= 0 || mf <= sparse_cap;
     return enq_form[L] != 'L' || mf <= enq_cap[L];
   };
   {
     int64_t cap0 = 0;
     // level 0 (the source's row): list form with the largest lists
-    const char f0 = init.dir == 'B' ? 'B' : (xc ? (list_max > 0 ? 'L' : 'T') : td_form(0, 0.0, &cap0, false));
+    const char f0 = init.dir == 'B' ? 'B'
+                    : xc             ? (list_max > 0 && opt_.device_loop_predict ? 'L' : 'T')
+                                     : td_form(0, 0.0, &cap0, false);
     enqueue_level(0, f0, f0 == 'L' ? list_max : 0);
   }
   for (int L = 0;; ++L) {

@@ -317,6 +317,7 @@ struct CompactArgs {
   vid_t* qv = nullptr;              // optional: work-list entry -> vertex (local row)
   word_t* clear = nullptr;          // optional: zero the frontier words once read (== frontier)
   const LevelCtrl* ctrl = nullptr;  // device loop: runs only when ctrl->dir == 'T'
+  int64_t max_mf = 0;               // ... and ctrl->m_f <= max_mf (0: any; a sparse chain's compaction)
 };
 
 // Sparse top-down level (device loop, one rank): one kernel instead of
@@ -357,6 +358,9 @@ struct TdSparseArgs {
   int32_t level_index = 0;
   int64_t grid = 0;
   bool first = true;  // first kernel of the level (else a compaction ran before it)
+  // live only while ctrl->m_f <= max_mf (0: any): a sparse chain enqueued for
+  // a level that turns out large is a no-op and is re-enqueued dense
+  int64_t max_mf = 0;
 };
 
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.

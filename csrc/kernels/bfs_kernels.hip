@@ -477,7 +477,7 @@ __device__ __forceinline__ void wave_fill_blocks(int32_t* __restrict__ blk, bool
 // scan; each set bit's slot from mbcnt and its edge offset from a wave prefix
 // sum of degrees.
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T')) return;
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
   stamp_level_start(a.ctrl);
   const int lane = lane_id();
   const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
@@ -711,7 +711,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ int s_last;
   // uniform: the whole grid returns, no workgroup takes a ticket
-  if (a.ctrl->done || a.ctrl->dir != 'T') return;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
   if (a.first) stamp_level_start(a.ctrl);
   const long long q = a.dev_stats[0], m = a.dev_stats[1];
   const int t = threadIdx.x;
