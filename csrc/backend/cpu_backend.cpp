@@ -259,6 +259,23 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void td_binned(const BinArgs& a) override {
+    if (!chain_live(*a.ctrl, 'T', 0)) return;
+    const int64_t q = a.dev_stats[0];
+    if (a.clear_qv)
+      for (int64_t i = 0; i < q; ++i) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
+    std::vector<word_t> nb(static_cast<size_t>(a.words), 0);
+    for (int64_t i = 0; i < q; ++i)
+      for (int64_t k = a.qscan[i]; k < a.qscan[i + 1]; ++k) {
+        const vid_t v = a.g.col[k + a.qbase[i]];
+        if (!test_bit(a.visited, v)) nb[v >> 6] |= 1ull << (v & 63);
+      }
+    for (int64_t w = 0; w < a.words; ++w) {
+      a.frontier[w] = nb[w];
+      a.visited[w] |= nb[w];
+    }
+  }
+
   void level_finish(const LevelFinishArgs& a) override {
     if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;

@@ -209,6 +209,7 @@ class HipBackend final : public Backend {
   void level_finish(const LevelFinishArgs& a) override { on(); kern::level_finish(a, st_); chk(); }
   void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) override { on(); kern::widen_levels(in, out, n, st_); chk(); }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
+  void td_binned(const BinArgs& a) override { on(); kern::td_binned(a, st_); chk(); }
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }

@@ -73,6 +73,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
+  else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
@@ -105,6 +106,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
+          {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
@@ -1034,6 +1036,27 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     be_.memset_async(sparse_ticket_.data(), 0, sparse_ticket_.bytes());
     sparse_ready_ = true;
   }
+  // One rank, binned top-down levels: bins of 2^shift vertices (>= one
+  // 4096-vertex unit, <= 2^kBinMaxShift so a bin's visited slice fits LDS),
+  // about 256 of them (up to kBinMaxBins).
+  constexpr int kBinGrid = 256;
+  int bin_shift = 12;
+  {
+    int bits = 0;
+    while ((int64_t(1) << bits) < W * kWordBits) ++bits;
+    bin_shift = std::min(std::max(bits - 8, 12), kBinMaxShift);
+    while (bin_shift <= kBinMaxShift && div_up(W * kWordBits, int64_t(1) << bin_shift) > kBinMaxBins) ++bin_shift;
+  }
+  const int64_t nbins = div_up(W * kWordBits, int64_t(1) << bin_shift);
+  const bool binned = !xc && opt_.td_bin_edges > 0 && opt_.mode != Mode::BottomUp && bin_shift <= kBinMaxShift &&
+                      g_.nnz() > 0;
+  if (binned && bin_buf_.size() < static_cast<size_t>(g_.nnz())) {
+    bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins));
+    be_.memset_async(bin_total_.data(), 0, bin_total_.bytes());  // the scan re-zeroes it per level
+    bin_off_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins * kBinGrid));
+    bin_start_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins + 1));
+    bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz
+  }
   // Several ranks, list form: owner lists at a fixed stride (list_stride_ + 1
   // entries per peer, count first), exchanged cap + 1 entries per peer; the
   // counts are zeroed once here and by each consuming list_scatter after.
@@ -1291,7 +1314,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     };
     if (d == 'S') {
       DBFS_CHECK(sparse && pf != 'B', "sparse top-down level after a bottom-up level");
-      if (pf == 'T') compact();
+      if (pf == 'T' || pf == 'X') compact();
       TdSparseArgs sp;
       sp.g = gv;
       sp.qscan = qscan_set(L);
@@ -1320,6 +1343,44 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.first = pf != 'T';
       sp.max_mf = sparse_cap;
       be_.td_sparse(sp);
+    } else if (d == 'X') {
+      // binned top-down (one rank): a sparse level (or the seed) handed over
+      // the work list, else compact
+      const bool listed = sparse && (pf == 'S' || pf == 'I');
+      if (!listed) compact();
+      BinArgs xa;
+      xa.g = gv;
+      xa.qscan = qscan_set(L);
+      xa.qbase = qbase_set(L);
+      xa.blk_vstart = blk_set(L);
+      xa.dev_stats = sblk(L - 1);
+      if (listed) {
+        xa.clear_qv = qv_[L & 1].data();
+        xa.clear_frontier = frontier_[cur].data();
+      }
+      xa.ctrl = ctrl_.data();
+      xa.shift = bin_shift;
+      xa.nbins = static_cast<int>(nbins);
+      xa.grid = kBinGrid;
+      xa.bin_total = bin_total_.data();
+      xa.wg_off = bin_off_.data();
+      xa.bin_start = bin_start_.data();
+      xa.buf = bin_buf_.data();
+      xa.visited = vis_own;
+      xa.frontier = fr_own(cur ^ 1);
+      xa.words = W;
+      be_.td_binned(xa);
+      // levels and unit statistics of the new frontier (already claimed)
+      UpdateArgs tu = ua;
+      tu.cand = fr_own(cur ^ 1);
+      tu.cand_bytes = nullptr;
+      tu.nchunks = 1;
+      tu.clear_cand = false;
+      tu.force = true;
+      tu.frontier = fr_own(cur ^ 1);
+      tu.new_level = L + 1;
+      tu.ctrl = ctrl_.data();
+      be_.update_frontier(tu);
     } else if (d == 'T' || d == 'L') {
       // a sparse level (or the seed) already handed over the work list
       const bool listed = sparse && (pf == 'S' || pf == 'I');
@@ -1537,7 +1598,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       return *cap > 0 ? 'L' : 'T';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    return sparse && pf != 'B' && mf <= static_cast<double>(opt_.td_sparse_edges) ? 'S' : 'T';
+    if (sparse && pf != 'B' && mf <= static_cast<double>(opt_.td_sparse_edges)) return 'S';
+    return binned && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
   };
   // the chain enqueued for level L is live for a level with direction `dir`
   // and mf global frontier edges

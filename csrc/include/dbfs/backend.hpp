@@ -363,6 +363,46 @@ struct TdSparseArgs {
   int64_t max_mf = 0;
 };
 
+// Binned top-down level (one rank, large frontiers; propagation blocking):
+// instead of a random probe and a random store per frontier edge, the edges'
+// targets are first written into nbins contiguous bins by target range
+// (count pass: per-workgroup bin counts; scan; fill pass: each workgroup
+// writes its targets at its scanned positions), then one workgroup per bin
+// holds the bin's slice of `visited` in LDS, claims the unvisited targets with
+// LDS atomics and writes the bin's frontier / visited words, the new
+// vertices' levels and its units' statistics -- every random access of the
+// level lands in one bin's LDS / L2-resident range.  Replaces td_expand; an
+// update_frontier with force = true over the new frontier (cand = frontier)
+// then writes the levels and unit statistics.  Correct for any frontier size.
+struct BinArgs {
+  ShardView g;
+  const int64_t* qscan = nullptr;
+  const int64_t* qbase = nullptr;
+  const int32_t* blk_vstart = nullptr;
+  const int64_t* dev_stats = nullptr;  // [0] work-list entries, [1] frontier edges
+  // work list handed over by a sparse level: zero its vertices' input bits
+  const vid_t* clear_qv = nullptr;
+  word_t* clear_frontier = nullptr;
+  const LevelCtrl* ctrl = nullptr;     // runs only when ctrl->dir == 'T'
+  int shift = 12;                      // bin = vertex >> shift (bins align with 4096-vertex units)
+  int nbins = 0;
+  int grid = 0;                        // workgroups of the count / fill passes
+  // count pass: workgroup g reserves its targets of bin k with one returning
+  // atomic on bin_total[k] (zero on entry) and keeps the offset in
+  // wg_off[k * grid + g]; the scan turns bin_total into bin_start (and zeroes
+  // it for the next level)
+  int64_t* bin_total = nullptr;        // nbins
+  int64_t* wg_off = nullptr;           // nbins * grid
+  int64_t* bin_start = nullptr;        // nbins + 1
+  vid_t* buf = nullptr;                // >= frontier edges
+  word_t* visited = nullptr;
+  word_t* frontier = nullptr;          // next frontier (every word written)
+  int64_t words = 0;
+};
+// Largest bin span (vertices) and bin count the kernels support.
+constexpr int kBinMaxShift = 18;
+constexpr int kBinMaxBins = 4096;
+
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
 struct TdArgs {
   ShardView g;
@@ -684,6 +724,8 @@ class Backend {
   virtual void td_sparse(const TdSparseArgs& a) = 0;
   virtual void level_finish(const LevelFinishArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
+  // the passes of a binned top-down level (BinArgs), stream-ordered
+  virtual void td_binned(const BinArgs& a) = 0;
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;

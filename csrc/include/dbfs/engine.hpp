@@ -121,6 +121,10 @@ struct EngineOptions {
   // 1.7 M-edge level 115 -> 68 us).  Replaces td_byte_edges there.
   bool td_direct = true;
   int64_t td_direct_edges = int64_t(1) << 16;
+  // Device loop, one rank: top-down levels predicted to have at least this
+  // many frontier edges run binned (BinArgs: targets binned by vertex range,
+  // claimed per bin in LDS) instead of td_expand + update; 0 disables.
+  int64_t td_bin_edges = 0;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.
   double td_check_visited_min = 0.02;
@@ -303,6 +307,9 @@ class Engine {
   static constexpr int kStatsBlocks = 3;
   int64_t stats_stride_ = 8;
   DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
+  // binned top-down levels (one rank): bin counts / positions, bin starts, targets
+  DBuf<int64_t> bin_total_, bin_off_, bin_start_;
+  DBuf<vid_t> bin_buf_;
   int64_t list_stride_ = 0;
   DBuf<unsigned> ticket_;
   DBuf<int32_t> blk_vstart_;

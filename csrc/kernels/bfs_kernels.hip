@@ -831,6 +831,178 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
 }
 
+// ---------------------------------------------------------------------------
+// Binned top-down level (BinArgs).  Count and fill passes walk the same edge
+// blocks per workgroup (b = blockIdx.x, += gridDim.x) with the td_expand owner
+// map; a workgroup's targets of bin k land at bin_start[k] + wg_off[k * grid +
+// g] plus an LDS slot.  1024-thread workgroups, 2 edges per thread per block.
+constexpr int kBinThreads = 1024;
+constexpr int kAggRounds = 4;
+
+// slot = atomicAdd(&cnt[key], 1) for every active lane, with the lanes that
+// share a key served by one LDS atomic (rows in id order put runs of targets
+// in one bin, and 64 same-address LDS atomics serialise): up to kAggRounds
+// distinct keys per wave aggregated, the rest per lane.  Wave-uniform call.
+__device__ __forceinline__ unsigned lds_slot_add(unsigned* cnt, int key, bool active) {
+  const int lane = lane_id();
+  unsigned long long pending = __ballot(active);
+  unsigned slot = 0;
+#pragma unroll
+  for (int r = 0; r < kAggRounds; ++r) {
+    if (!pending) break;
+    const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+    const int k = __shfl(key, leader, kWave);
+    const unsigned long long m = __ballot(active && key == k) & pending;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[k], static_cast<unsigned>(__popcll(m)));
+    base = __shfl(base, leader, kWave);
+    if ((m >> lane) & 1ull) slot = base + mask_rank(m);
+    pending &= ~m;
+  }
+  if ((pending >> lane) & 1ull) slot = atomicAdd(&cnt[key], 1u);
+  return slot;
+}
+
+template <bool kFill>
+__global__ __launch_bounds__(kBinThreads) void bin_pass_kernel(BinArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kBinThreads;
+  __shared__ int32_t s_owner[kTdEdgesPerBlock];
+  __shared__ long long s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_wmax[kBinThreads / kWave];
+  __shared__ unsigned s_cnt[kBinMaxBins];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  const long long q = a.dev_stats[0], m = a.dev_stats[1];
+  const int t = threadIdx.x;
+  if (!kFill && a.clear_qv) {
+    stamp_level_start(a.ctrl);  // first kernel of the level (no compaction ran)
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBinThreads + t; i < q;
+         i += static_cast<int64_t>(gridDim.x) * kBinThreads)
+      a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
+  }
+  for (int k = t; k < a.nbins; k += kBinThreads) s_cnt[k] = 0;
+  // (td_block_owner_map starts with a barrier)
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  const vid_t* __restrict__ col = a.g.col;
+  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const int cnt = td_block_owner_map<kBinThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
+                                                    s_base, s_wmax);
+    vid_t v[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kBinThreads + t;
+      v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const bool act = k * kBinThreads + t < cnt;
+      const int bin = static_cast<int>(v[k] >> a.shift);
+      const unsigned slot = lds_slot_add(s_cnt, bin, act);
+      if constexpr (kFill) {
+        if (act) a.buf[a.bin_start[bin] + a.wg_off[static_cast<int64_t>(bin) * a.grid + blockIdx.x] + slot] = v[k];
+      }
+    }
+  }
+  if constexpr (!kFill) {
+    __syncthreads();
+    // this workgroup's share of every bin: one returning atomic per non-empty bin
+    for (int k = t; k < a.nbins; k += kBinThreads)
+      if (s_cnt[k])
+        a.wg_off[static_cast<int64_t>(k) * a.grid + blockIdx.x] = static_cast<int64_t>(
+            atomicAdd(reinterpret_cast<unsigned long long*>(a.bin_total + k), static_cast<unsigned long long>(s_cnt[k])));
+  }
+}
+
+// One workgroup: bin_start = exclusive scan of bin_total (<= kBinMaxBins
+// entries, 4 per thread); bin_total zeroed for the next level.
+__global__ __launch_bounds__(kBinThreads) void bin_scan_kernel(BinArgs a) {
+  __shared__ long long s_wave[kBinThreads / kWave];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  constexpr int kPer = kBinMaxBins / kBinThreads;
+  const int t = threadIdx.x;
+  long long c[kPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = t * kPer + k;
+    c[k] = i < a.nbins ? a.bin_total[i] : 0;
+    sum += c[k];
+  }
+  const long long incl = wave_incl_scan(sum);
+  if (lane_id() == kWave - 1) s_wave[t >> 6] = incl;
+  __syncthreads();
+  long long off = incl - sum, total = 0;
+  for (int k = 0; k < kBinThreads / kWave; ++k) {
+    if (k < (t >> 6)) off += s_wave[k];
+    total += s_wave[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int i = t * kPer + k;
+    if (i < a.nbins) {
+      a.bin_start[i] = off;
+      a.bin_total[i] = 0;
+    }
+    off += c[k];
+  }
+  if (t == 0) a.bin_start[a.nbins] = total;
+}
+
+// One workgroup per bin: the bin's visited slice in LDS, claims of the bin's
+// targets with LDS atomics (lanes on one word aggregated), then the bin's
+// frontier / visited words.
+__global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
+  constexpr int kMaxWords = (1 << kBinMaxShift) / kWordBits;
+  __shared__ word_t s_vis[kMaxWords];
+  __shared__ word_t s_new[kMaxWords];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int64_t bin = blockIdx.x;
+  const int64_t span_w = (int64_t(1) << a.shift) / kWordBits;
+  const int64_t w0 = bin * span_w;
+  const int nw = static_cast<int>(min<int64_t>(span_w, a.words - w0));
+  if (nw <= 0) return;
+  for (int w = t; w < nw; w += kBinThreads) {
+    s_vis[w] = a.visited[w0 + w];
+    s_new[w] = 0ull;
+  }
+  __syncthreads();
+  const int64_t vlo = w0 * kWordBits;
+  const int64_t b0 = a.bin_start[bin], b1 = a.bin_start[bin + 1];
+  // (the loop bound is uniform per wave: every lane runs every iteration)
+  for (int64_t i0 = b0; i0 < b1; i0 += kBinThreads) {
+    const int64_t i = i0 + t;
+    int w = 0;
+    word_t bit = 0;
+    if (i < b1) {
+      const int64_t l = static_cast<int64_t>(a.buf[i]) - vlo;
+      w = static_cast<int>(l >> 6);
+      bit = 1ull << (l & 63);
+      if (s_vis[w] & bit) bit = 0;  // visited: nothing to claim
+    }
+    unsigned long long pending = __ballot(bit != 0);
+#pragma unroll
+    for (int r = 0; r < kAggRounds; ++r) {
+      if (!pending) break;
+      const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+      const int k = __shfl(w, leader, kWave);
+      const unsigned long long msk = __ballot(bit != 0 && w == k) & pending;
+      word_t mine = ((msk >> lane) & 1ull) ? bit : 0ull;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) mine |= __shfl_xor(mine, off, kWave);
+      if (lane == leader) atomicOr(&s_new[k], mine);
+      pending &= ~msk;
+    }
+    if ((pending >> lane) & 1ull) atomicOr(&s_new[w], bit);
+  }
+  __syncthreads();
+  for (int w = t; w < nw; w += kBinThreads) {
+    const word_t nb = s_new[w];
+    a.frontier[w0 + w] = nb;
+    if (nb) a.visited[w0 + w] = s_vis[w] | nb;
+  }
+}
+
 // Narrow levels -> 32-bit levels (outside the timed traversal, on demand).
 __global__ __launch_bounds__(kBlock) void widen_levels_kernel(const uint8_t* __restrict__ in, lvl_t* __restrict__ out,
                                                               int64_t n) {
@@ -1607,6 +1779,14 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   else
     DBFS_TD_LAUNCH(TdOut::Bits);
 #undef DBFS_TD_LAUNCH
+}
+
+void td_binned(const BinArgs& a, hipStream_t st) {
+  if (a.nbins <= 0 || a.grid <= 0 || a.nbins > kBinMaxBins) return;
+  bin_pass_kernel<false><<<static_cast<unsigned>(a.grid), kBinThreads, 0, st>>>(a);
+  bin_scan_kernel<<<1, kBinThreads, 0, st>>>(a);
+  bin_pass_kernel<true><<<static_cast<unsigned>(a.grid), kBinThreads, 0, st>>>(a);
+  bin_apply_kernel<<<static_cast<unsigned>(a.nbins), kBinThreads, 0, st>>>(a);
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {

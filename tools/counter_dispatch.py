@@ -55,6 +55,8 @@ def main():
         extra = []
         if c.get("FETCH_SIZE"):
             extra.append(f"HBM read {c['FETCH_SIZE'] / 1e3 / us:.2f} TB/s ({c['FETCH_SIZE'] / 1e3:.0f} MB)")
+        if c.get("WRITE_SIZE"):
+            extra.append(f"written {c['WRITE_SIZE'] / 1e3:.0f} MB")
         if c.get("SQ_WAVE_CYCLES"):
             extra.append(f"wait {100 * c.get('SQ_WAIT_ANY', 0) / c['SQ_WAVE_CYCLES']:.0f}% of wave-cycles")
             extra.append(f"active-inst {100 * c.get('SQ_ACTIVE_INST_ANY', 0) / c['SQ_WAVE_CYCLES']:.0f}%")
