@@ -1039,7 +1039,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // One rank, binned top-down levels: bins of 2^shift vertices (>= one
   // 4096-vertex unit, <= 2^kBinMaxShift so a bin's visited slice fits LDS),
   // about 256 of them (up to kBinMaxBins).
-  constexpr int kBinGrid = 256;
+  constexpr int kBinGrid = 1024;
   int bin_shift = 12;
   {
     int bits = 0;
@@ -1052,9 +1052,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
                       g_.nnz() > 0;
   if (binned && bin_buf_.size() < static_cast<size_t>(g_.nnz())) {
     bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins));
-    be_.memset_async(bin_total_.data(), 0, bin_total_.bytes());  // the scan re-zeroes it per level
-    bin_off_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins * kBinGrid));
-    bin_start_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins + 1));
+    bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
     bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz
   }
   // Several ranks, list form: owner lists at a fixed stride (list_stride_ + 1
@@ -1363,8 +1361,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       xa.nbins = static_cast<int>(nbins);
       xa.grid = kBinGrid;
       xa.bin_total = bin_total_.data();
-      xa.wg_off = bin_off_.data();
-      xa.bin_start = bin_start_.data();
+      xa.cnt = bin_cnt_.data();
       xa.buf = bin_buf_.data();
       xa.visited = vis_own;
       xa.frontier = fr_own(cur ^ 1);

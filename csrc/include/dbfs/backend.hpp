@@ -387,13 +387,12 @@ struct BinArgs {
   int shift = 12;                      // bin = vertex >> shift (bins align with 4096-vertex units)
   int nbins = 0;
   int grid = 0;                        // workgroups of the count / fill passes
-  // count pass: workgroup g reserves its targets of bin k with one returning
-  // atomic on bin_total[k] (zero on entry) and keeps the offset in
-  // wg_off[k * grid + g]; the scan turns bin_total into bin_start (and zeroes
-  // it for the next level)
+  // count pass: cnt[k * grid + g] = targets of bin k in workgroup g's edges;
+  // the scan (one workgroup per bin) makes each bin's row exclusive and sets
+  // bin_total[k]; the fill pass and the apply derive the bin starts from
+  // bin_total themselves
+  uint32_t* cnt = nullptr;             // nbins * grid
   int64_t* bin_total = nullptr;        // nbins
-  int64_t* wg_off = nullptr;           // nbins * grid
-  int64_t* bin_start = nullptr;        // nbins + 1
   vid_t* buf = nullptr;                // >= frontier edges
   word_t* visited = nullptr;
   word_t* frontier = nullptr;          // next frontier (every word written)
@@ -401,7 +400,7 @@ struct BinArgs {
 };
 // Largest bin span (vertices) and bin count the kernels support.
 constexpr int kBinMaxShift = 18;
-constexpr int kBinMaxBins = 4096;
+constexpr int kBinMaxBins = 2048;
 
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
 struct TdArgs {

@@ -308,7 +308,8 @@ class Engine {
   int64_t stats_stride_ = 8;
   DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
   // binned top-down levels (one rank): bin counts / positions, bin starts, targets
-  DBuf<int64_t> bin_total_, bin_off_, bin_start_;
+  DBuf<int64_t> bin_total_;
+  DBuf<uint32_t> bin_cnt_;
   DBuf<vid_t> bin_buf_;
   int64_t list_stride_ = 0;
   DBuf<unsigned> ticket_;

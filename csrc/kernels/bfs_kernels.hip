@@ -864,96 +864,118 @@ __device__ __forceinline__ unsigned lds_slot_add(unsigned* cnt, int key, bool ac
 }
 
 template <bool kFill>
-__global__ __launch_bounds__(kBinThreads) void bin_pass_kernel(BinArgs a) {
-  constexpr int kItems = kTdEdgesPerBlock / kBinThreads;
+__global__ __launch_bounds__(kTdThreads) void bin_pass_kernel(BinArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kTdThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
-  __shared__ int32_t s_wmax[kBinThreads / kWave];
+  __shared__ int32_t s_wmax[kTdThreads / kWave];
   __shared__ unsigned s_cnt[kBinMaxBins];
+  __shared__ long long s_start[kFill ? kBinMaxBins : 1];
   if (!chain_live(*a.ctrl, 'T', 0)) return;
   const long long q = a.dev_stats[0], m = a.dev_stats[1];
   const int t = threadIdx.x;
   if (!kFill && a.clear_qv) {
     stamp_level_start(a.ctrl);  // first kernel of the level (no compaction ran)
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBinThreads + t; i < q;
-         i += static_cast<int64_t>(gridDim.x) * kBinThreads)
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kTdThreads + t; i < q;
+         i += static_cast<int64_t>(gridDim.x) * kTdThreads)
       a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
   }
-  for (int k = t; k < a.nbins; k += kBinThreads) s_cnt[k] = 0;
+  for (int k = t; k < a.nbins; k += kTdThreads) s_cnt[k] = 0;
+  if constexpr (kFill) {
+    // bin starts: exclusive scan of the bin totals (<= kBinMaxBins), serial
+    // per wave-chunk then across the 4 waves
+    __shared__ long long s_part[kTdThreads / kWave];
+    constexpr int kPer = kBinMaxBins / kTdThreads;
+    long long c[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = t * kPer + k;
+      c[k] = b < a.nbins ? a.bin_total[b] : 0;
+      sum += c[k];
+    }
+    const long long incl = wave_incl_scan(sum);
+    if (lane_id() == kWave - 1) s_part[t >> 6] = incl;
+    __syncthreads();
+    long long off = incl - sum;
+    for (int w = 0; w < (t >> 6); ++w) off += s_part[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = t * kPer + k;
+      if (b < a.nbins) s_start[b] = off + a.cnt[static_cast<int64_t>(b) * a.grid + blockIdx.x];
+      off += c[k];
+    }
+  }
   // (td_block_owner_map starts with a barrier)
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const vid_t* __restrict__ col = a.g.col;
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
     const long long e0 = b * kTdEdgesPerBlock;
-    const int cnt = td_block_owner_map<kBinThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
-                                                    s_base, s_wmax);
+    const int cnt = td_block_owner_map<kTdThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
+                                                   s_base, s_wmax);
     vid_t v[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
-      const int idx = k * kBinThreads + t;
+      const int idx = k * kTdThreads + t;
       v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
     }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
-      const bool act = k * kBinThreads + t < cnt;
+      const bool act = k * kTdThreads + t < cnt;
       const int bin = static_cast<int>(v[k] >> a.shift);
       const unsigned slot = lds_slot_add(s_cnt, bin, act);
       if constexpr (kFill) {
-        if (act) a.buf[a.bin_start[bin] + a.wg_off[static_cast<int64_t>(bin) * a.grid + blockIdx.x] + slot] = v[k];
+        if (act) a.buf[s_start[bin] + slot] = v[k];
       }
     }
   }
   if constexpr (!kFill) {
     __syncthreads();
-    // this workgroup's share of every bin: one returning atomic per non-empty bin
-    for (int k = t; k < a.nbins; k += kBinThreads)
-      if (s_cnt[k])
-        a.wg_off[static_cast<int64_t>(k) * a.grid + blockIdx.x] = static_cast<int64_t>(
-            atomicAdd(reinterpret_cast<unsigned long long*>(a.bin_total + k), static_cast<unsigned long long>(s_cnt[k])));
+    for (int k = t; k < a.nbins; k += kTdThreads) a.cnt[static_cast<int64_t>(k) * a.grid + blockIdx.x] = s_cnt[k];
   }
 }
 
-// One workgroup: bin_start = exclusive scan of bin_total (<= kBinMaxBins
-// entries, 4 per thread); bin_total zeroed for the next level.
-__global__ __launch_bounds__(kBinThreads) void bin_scan_kernel(BinArgs a) {
-  __shared__ long long s_wave[kBinThreads / kWave];
+// One workgroup per bin: its row of workgroup counts made exclusive, the
+// bin's total.
+__global__ __launch_bounds__(kTdThreads) void bin_scan_kernel(BinArgs a) {
+  __shared__ long long s_part[kTdThreads / kWave];
   if (!chain_live(*a.ctrl, 'T', 0)) return;
-  constexpr int kPer = kBinMaxBins / kBinThreads;
+  uint32_t* row = a.cnt + static_cast<int64_t>(blockIdx.x) * a.grid;
   const int t = threadIdx.x;
-  long long c[kPer], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = t * kPer + k;
-    c[k] = i < a.nbins ? a.bin_total[i] : 0;
-    sum += c[k];
+  const int per = (a.grid + kTdThreads - 1) / kTdThreads;
+  long long sum = 0;
+  for (int k = 0; k < per; ++k) {
+    const int g = t * per + k;
+    if (g < a.grid) sum += row[g];
   }
   const long long incl = wave_incl_scan(sum);
-  if (lane_id() == kWave - 1) s_wave[t >> 6] = incl;
+  if (lane_id() == kWave - 1) s_part[t >> 6] = incl;
   __syncthreads();
   long long off = incl - sum, total = 0;
-  for (int k = 0; k < kBinThreads / kWave; ++k) {
-    if (k < (t >> 6)) off += s_wave[k];
-    total += s_wave[k];
+  for (int w = 0; w < kTdThreads / kWave; ++w) {
+    if (w < (t >> 6)) off += s_part[w];
+    total += s_part[w];
   }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int i = t * kPer + k;
-    if (i < a.nbins) {
-      a.bin_start[i] = off;
-      a.bin_total[i] = 0;
+  for (int k = 0; k < per; ++k) {
+    const int g = t * per + k;
+    if (g < a.grid) {
+      const uint32_t c = row[g];
+      row[g] = static_cast<uint32_t>(off);  // (a bin holds < 2^32 targets per level)
+      off += c;
     }
-    off += c[k];
   }
-  if (t == 0) a.bin_start[a.nbins] = total;
+  if (t == 0) a.bin_total[blockIdx.x] = total;
 }
 
 // One workgroup per bin: the bin's visited slice in LDS, claims of the bin's
-// targets with LDS atomics (lanes on one word aggregated), then the bin's
-// frontier / visited words.
+// targets with LDS atomics (lanes on one word aggregated; kApplyItems loads
+// in flight per thread), then the bin's frontier / visited words.
+constexpr int kApplyItems = 8;
+
 __global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
   constexpr int kMaxWords = (1 << kBinMaxShift) / kWordBits;
   __shared__ word_t s_vis[kMaxWords];
   __shared__ word_t s_new[kMaxWords];
+  __shared__ long long s_part[kBinThreads / kWave];
   if (!chain_live(*a.ctrl, 'T', 0)) return;
   const int t = threadIdx.x;
   const int lane = lane_id();
@@ -962,38 +984,53 @@ __global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
   const int64_t w0 = bin * span_w;
   const int nw = static_cast<int>(min<int64_t>(span_w, a.words - w0));
   if (nw <= 0) return;
+  // this bin's start: the totals of the bins before it
+  long long before = 0;
+  for (int64_t b = t; b < bin; b += kBinThreads) before += a.bin_total[b];
+  before = wave_sum(before);
+  if (lane == 0) s_part[t >> 6] = before;
   for (int w = t; w < nw; w += kBinThreads) {
     s_vis[w] = a.visited[w0 + w];
     s_new[w] = 0ull;
   }
   __syncthreads();
+  long long b0 = 0;
+  for (int w = 0; w < kBinThreads / kWave; ++w) b0 += s_part[w];
+  const long long b1 = b0 + a.bin_total[bin];
   const int64_t vlo = w0 * kWordBits;
-  const int64_t b0 = a.bin_start[bin], b1 = a.bin_start[bin + 1];
-  // (the loop bound is uniform per wave: every lane runs every iteration)
-  for (int64_t i0 = b0; i0 < b1; i0 += kBinThreads) {
-    const int64_t i = i0 + t;
-    int w = 0;
-    word_t bit = 0;
-    if (i < b1) {
-      const int64_t l = static_cast<int64_t>(a.buf[i]) - vlo;
-      w = static_cast<int>(l >> 6);
-      bit = 1ull << (l & 63);
-      if (s_vis[w] & bit) bit = 0;  // visited: nothing to claim
-    }
-    unsigned long long pending = __ballot(bit != 0);
+  for (long long i0 = b0; i0 < b1; i0 += static_cast<long long>(kBinThreads) * kApplyItems) {
+    vid_t v[kApplyItems];
 #pragma unroll
-    for (int r = 0; r < kAggRounds; ++r) {
-      if (!pending) break;
-      const int leader = __ffsll(static_cast<long long>(pending)) - 1;
-      const int k = __shfl(w, leader, kWave);
-      const unsigned long long msk = __ballot(bit != 0 && w == k) & pending;
-      word_t mine = ((msk >> lane) & 1ull) ? bit : 0ull;
-#pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) mine |= __shfl_xor(mine, off, kWave);
-      if (lane == leader) atomicOr(&s_new[k], mine);
-      pending &= ~msk;
+    for (int k = 0; k < kApplyItems; ++k) {
+      const long long j = i0 + static_cast<long long>(k) * kBinThreads + t;
+      v[k] = j < b1 ? a.buf[j] : 0xFFFFFFFFu;
     }
-    if ((pending >> lane) & 1ull) atomicOr(&s_new[w], bit);
+#pragma unroll
+    for (int k = 0; k < kApplyItems; ++k) {
+      int w = 0;
+      word_t bit = 0;
+      if (v[k] != 0xFFFFFFFFu) {
+        const int64_t l = static_cast<int64_t>(v[k]) - vlo;
+        w = static_cast<int>(l >> 6);
+        bit = 1ull << (l & 63);
+        if (s_vis[w] & bit) bit = 0;  // visited: nothing to claim
+      }
+      unsigned long long pending = __ballot(bit != 0);
+#pragma unroll
+      for (int r = 0; r < kAggRounds; ++r) {
+        if (!pending) break;
+        const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+        const int kw = __shfl(w, leader, kWave);
+        const unsigned long long msk = __ballot(bit != 0 && w == kw) & pending;
+        if (__popcll(msk) == 1) break;  // no sharing left worth a reduction
+        word_t mine = ((msk >> lane) & 1ull) ? bit : 0ull;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) mine |= __shfl_xor(mine, off, kWave);
+        if (lane == leader) atomicOr(&s_new[kw], mine);
+        pending &= ~msk;
+      }
+      if ((pending >> lane) & 1ull) atomicOr(&s_new[w], bit);
+    }
   }
   __syncthreads();
   for (int w = t; w < nw; w += kBinThreads) {
@@ -1783,9 +1820,9 @@ void td_expand(const TdArgs& a, hipStream_t st) {
 
 void td_binned(const BinArgs& a, hipStream_t st) {
   if (a.nbins <= 0 || a.grid <= 0 || a.nbins > kBinMaxBins) return;
-  bin_pass_kernel<false><<<static_cast<unsigned>(a.grid), kBinThreads, 0, st>>>(a);
-  bin_scan_kernel<<<1, kBinThreads, 0, st>>>(a);
-  bin_pass_kernel<true><<<static_cast<unsigned>(a.grid), kBinThreads, 0, st>>>(a);
+  bin_pass_kernel<false><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+  bin_scan_kernel<<<static_cast<unsigned>(a.nbins), kTdThreads, 0, st>>>(a);
+  bin_pass_kernel<true><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
   bin_apply_kernel<<<static_cast<unsigned>(a.nbins), kBinThreads, 0, st>>>(a);
 }
 

@@ -658,3 +658,60 @@ def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     sb.engine.set_option("td_bin_edges", bin_edges)
     _check(sb, star, 0)
     _check(sb, star, 5)
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_eight_virtual_ranks_rmat18_gpu(mode):
+    """P = 8 virtual ranks on one GPU through the multi-rank device loop at
+    RMAT-18: list-form (owner-routed lists) and dense top-down chains, split
+    bottom-up levels with the hub bits carried in the totals reduction;
+    exact against the oracle and every chain form seen."""
+    p = dbfs.rmat_params(18, 16, 61)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    hub = int(np.argmax(deg))
+    reach = np.nonzero(dbfs.cpu_bfs(csr, hub)[0] != dbfs.UNREACHED)[0]
+    srcs = [int(reach[len(reach) // 3]), int(reach[-1])]  # two roots in the giant component
+    exp = [dbfs.cpu_bfs(csr, s)[0] for s in srcs]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode=mode)
+        out, forms = [], set()
+        for s in srcs:
+            r = b.run(s)
+            forms.update(c[1] for c in r.chains)
+            out.append(b.levels())
+        return out, forms
+
+    for levels, forms in run_virtual_ranks(8, body, device="hip"):
+        for got, e in zip(levels, exp):
+            assert np.array_equal(got, e)
+        assert "L" in forms and ("B" in forms if mode == "do" else "T" in forms)
+
+
+def test_bottom_up_long_row_scanned_in_place_gpu(gpu_runtime):
+    """A vertex with a 2^21-entry row whose only frontier neighbour sits at the
+    end of its (hub-first) row: every bottom-up level scans the whole row in
+    place (rows of >= 2^20 entries are not queued), and the level that reaches
+    that neighbour finds it last."""
+    p = dbfs.rmat_params(16, 16, 9)
+    u0, v0 = (np.asarray(x, dtype=np.int64) for x in dbfs.generate_edges(p))
+    n0 = p.n
+    k = 1 << 21
+    c = n0                                   # the star centre
+    leaves = np.arange(n0 + 1, n0 + 1 + k, dtype=np.int64)
+    # every leaf has degree 2 (the centre + a partner leaf), so the centre's
+    # row is ordered by id; the last leaf's partner is RMAT vertex 5, the one
+    # before it gets a pendant vertex instead
+    partners = n0 + 1 + ((leaves - n0 - 1) ^ 1)
+    partners[-1] = 5
+    partners[-2] = n0 + 1 + k
+    keep = (leaves < partners) | (np.arange(k) >= k - 2)
+    u = np.concatenate([u0, np.full(k, c), leaves[keep]])
+    v = np.concatenate([v0, leaves, partners[keep]])
+    n = n0 + 2 + k
+    csr = dbfs.build_csr(n, u.astype(np.uint32), v.astype(np.uint32))
+    for mode in ["bu", "do"]:
+        bfs = dbfs.BFS(csr, gpu_runtime, mode=mode)
+        _check(bfs, csr, 5)
+        _check(bfs, csr, 0)
