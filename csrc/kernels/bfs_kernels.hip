@@ -1125,6 +1125,18 @@ __device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const wo
   }
 }
 
+// Wave-cooperative row scan: DBFS_BU_SCAN_STEPS 64-neighbour steps whose
+// loads are issued together (measured on RMAT-26: 1 step 1231 / 1224 GTEPS,
+// 2 steps 1225 / 1224, 4 steps 1217 / 1210, 8 steps 1188 / 1185 -- the extra
+// registers cost more than the latency they hide); kNoVertex pads the tail
+// (never a vertex or a hub-encoded id: ids < 2^31, hub codes < kHubFlag +
+// kMaxHubs).
+#ifndef DBFS_BU_SCAN_STEPS
+#define DBFS_BU_SCAN_STEPS 1
+#endif
+constexpr int kBuScanSteps = DBFS_BU_SCAN_STEPS;
+constexpr vid_t kNoVertex = 0xFFFFFFFFu;
+
 template <bool kPacked, bool kHub>
 __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own,
                                             const word_t* s_hub) {
@@ -1184,8 +1196,11 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       p += static_cast<uint32_t>(took);
     }
   } else {
-    // Phase 2: the wave scans each still-unresolved row in turn, 64
-    // neighbours per step.
+    // Phase 2: the wave scans each still-unresolved row in turn,
+    // kBuScanSteps x 64 neighbours per step (the column loads of a step in
+    // flight together, then their probes): a row that scans to its end --
+    // most rows at a bottom-up level entered with a small frontier -- costs
+    // len / (64 kBuScanSteps) dependent round trips instead of len / 64.
     unsigned long long pending = __ballot(!found && p < len);
     BU_STAT(5, __popcll(pending));
     while (pending) {
@@ -1194,11 +1209,17 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
       const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
       bool f = false;
-      for (uint32_t base = ps; base < pe; base += kWave) {
+      for (uint32_t base = ps; base < pe; base += kWave * kBuScanSteps) {
         BU_STAT(6, 1);
-        const uint32_t idx = base + lane;
+        vid_t u[kBuScanSteps];
+#pragma unroll
+        for (int k = 0; k < kBuScanSteps; ++k) {
+          const uint32_t idx = base + k * kWave + lane;
+          u[k] = idx < pe ? r[idx] : kNoVertex;
+        }
         bool hit = false;
-        if (idx < pe) hit = bu_probe<kHub>(fr, s_hub, r[idx]);
+#pragma unroll
+        for (int k = 0; k < kBuScanSteps; ++k) hit |= u[k] != kNoVertex && bu_probe<kHub>(fr, s_hub, u[k]);
         if (__ballot(hit)) {
           f = true;
           break;
