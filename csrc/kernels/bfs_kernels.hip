@@ -1096,6 +1096,16 @@ constexpr int kBuQueue = DBFS_BU_QUEUE;
 #define DBFS_BU_QUEUE_DIRECT DBFS_BU_QUEUE
 #endif
 constexpr int kQueueDirect = DBFS_BU_QUEUE_DIRECT < kBuQueue ? DBFS_BU_QUEUE_DIRECT : kBuQueue;
+// DBFS_BU_PACK_FLUSH=1: queued rows still unresolved after their per-lane scan
+// are finished as one packed edge stream per wave (several short rows per
+// 64-lane step) instead of one row per step -- at a bottom-up level entered
+// with a small frontier (RMAT-26, 91 M of 2.1 B edges) 3.3 M rows reach that
+// phase.  Off: the packed scan lifts the 1024-thread kernel to 83 VGPRs (one
+// workgroup per CU), measured 1238 -> 1069 GTEPS.
+#ifndef DBFS_BU_PACK_FLUSH
+#define DBFS_BU_PACK_FLUSH 0
+#endif
+constexpr bool kPackFlush = DBFS_BU_PACK_FLUSH != 0;
 static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
 
 #ifdef DBFS_BU_STATS
@@ -1447,7 +1457,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const bool f = bu_scan_row<kPacked, kHub>(a, qrs, qe, lane >= qn, own, s_hub);
+    const bool f = bu_scan_row<kPacked || kPackFlush, kHub>(a, qrs, qe, lane >= qn, own, s_hub);
     settle(lane < qn && f, ql, qrs, qe);
     qn = 0;
   };
@@ -1543,7 +1553,9 @@ constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads, int kQ = kBuQueue>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
-  __shared__ int s_bu_owner[kPacked ? kThreads : 1];
+  // per-wave scratch of the packed row scans (kPacked, or the queue flushes)
+  constexpr bool kOwn = kPacked || (kCompact && kQ > 0 && kPackFlush);
+  __shared__ int s_bu_owner[kOwn ? kThreads : 1];
   __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
   constexpr int kQueueLen = (kCompact && !kPacked) ? kQ : 0;
@@ -1561,7 +1573,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     // when the shard has enough units to fill the chip this way (one GPU);
     // small shards (many ranks) keep 16 words per wave for parallelism.
     constexpr int kWavesPerBlock = kThreads / kWave;
-    int* own = s_bu_owner;
+    int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
@@ -1579,7 +1591,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
     if (u < nunits) {
-      int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
+      int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
       if constexpr (kCompact)
         bu_wave_compact<kPacked, true, kWaveWords, kQueueLen>(a, u * kUnitWords + wg * kWaveWords, own,
                                                               s_res + wave * kWaveWords, s_hub, cnt, deg,
