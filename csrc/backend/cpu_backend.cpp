@@ -613,6 +613,15 @@ class CpuBackend final : public Backend {
       a.hub_front[w] = m;
     }
   }
+  void hub_visited(const HubVisitedArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', 0)) return;
+    for (int64_t w = 0; w < div_up(a.g.td_nhubs, 64); ++w) {
+      word_t m = 0;
+      for (int b = 0; b < 64 && w * 64 + b < a.g.td_nhubs; ++b)
+        if (test_bit(a.visited, a.g.td_hub_vertex[w * 64 + b])) m |= 1ull << b;
+      a.out[w] = m;
+    }
+  }
   void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx) override {
     for (int64_t r = 0; r < rows; ++r) {
       vid_t h = ro[r + 1] > ro[r] ? col[ro[r]] : 0u;

@@ -74,6 +74,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
+  else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
+  else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
@@ -107,6 +109,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
+          {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
+          {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
@@ -281,6 +285,11 @@ ShardView DeviceGraph::view() const {
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
+  if (td_nhubs_ > 0) {
+    v.td_col = td_col_.data();
+    v.td_hub_vertex = td_hub_vertex_.data();
+    v.td_nhubs = td_nhubs_;
+  }
   return v;
 }
 
@@ -325,7 +334,7 @@ static uint32_t hub_min_degree(const std::vector<uint32_t>& deg, int64_t cap) {
   return best;
 }
 
-void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hubs, bool id_order) {
+void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hubs, bool id_order, bool td_hubs) {
   DBFS_CHECK(max_hubs >= 0 && max_hubs <= kMaxHubs, "max_hubs out of range");
   DBFS_CHECK(comm.size() == part_.nranks && comm.rank() == rank_, "communicator does not match the shard");
   comm.bind_backend(be_);
@@ -340,6 +349,9 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   nhubs_ = 0;
   hub_vertex_.reset();
   hub_col_.reset();
+  td_col_.reset();
+  td_hub_vertex_.reset();
+  td_nhubs_ = 0;
   col_by_id_ = false;
   // Hub encoding needs a free flag bit in the vertex ids.
   if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
@@ -361,6 +373,21 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       if (id_order && nhubs_ > 0) {
         be_->sort_rows_by_id(row_off_.data(), col_.data(), rows_, part_.n);
         col_by_id_ = true;
+        if (td_hubs) {
+          // top-down hubs: the kTdMaxHubs highest-degree vertices (their
+          // visited bits fit LDS next to the top-down owner map)
+          const uint32_t td_min = hub_min_degree(deg, std::min<int64_t>(kTdMaxHubs, max_hubs));
+          if (td_min > 0) {
+            DBuf<uint32_t> td_idx(*be_, static_cast<size_t>(nall));
+            td_hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(kTdMaxHubs));
+            td_nhubs_ = be_->select_hubs(all.data(), nall, td_min, td_hub_vertex_.data(), td_idx.data());
+            if (td_nhubs_ > 0) {
+              td_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
+              be_->encode_hub_cols(col_.data(), nnz_, td_idx.data(), td_col_.data());
+            }
+            be_->synchronize();
+          }
+        }
       }
     } else {
       build_heads();
@@ -1427,6 +1454,21 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       } else {
         ta.next = next_.data();
         ta.next_bytes = next_bytes_.data();
+        if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0) {
+          // large levels: the hubs' visited bits, staged in LDS by td_expand
+          if (!td_hub_vis_.data()) td_hub_vis_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(gv.td_nhubs, kWordBits)));
+          HubVisitedArgs hv;
+          hv.g = gv;
+          hv.visited = visited_.data();
+          hv.out = td_hub_vis_.data();
+          hv.ctrl = ctrl_.data();
+          hv.min_edges = opt_.td_hub_edges;
+          hv.vis_frac = opt_.td_hub_vis_frac;
+          be_.hub_visited(hv);
+          ta.td_hub_vis = td_hub_vis_.data();
+          ta.td_hub_min_edges = opt_.td_hub_edges;
+          ta.td_hub_vis_frac = opt_.td_hub_vis_frac;
+        }
         // (a level past kNarrowMaxLevel would store the unreached byte:
         // the usual path flags the overflow and the run is repeated wide)
         if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {

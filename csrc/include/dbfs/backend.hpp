@@ -55,7 +55,18 @@ struct ShardView {
   const eid_t* nz_pref = nullptr;
   const eid_t* nz_row_off = nullptr;
   const vid_t* nz_head = nullptr;
+  // Top-down copy of col (same layout, neighbour-id order) with the
+  // td_nhubs highest-degree vertices encoded as kHubFlag | index
+  // (td_hub_vertex[index] = the vertex): a large top-down level tests them in
+  // an LDS copy of their visited bits and reads no visited word for them.
+  const vid_t* td_col = nullptr;
+  const vid_t* td_hub_vertex = nullptr;
+  int64_t td_nhubs = 0;
 };
+
+// At most kTdMaxHubs top-down hubs (their visited bits, 16 KiB, sit in LDS
+// next to the top-down owner map: three 256-thread workgroups per CU).
+constexpr int64_t kTdMaxHubs = int64_t(1) << 17;
 
 // At most kMaxHubs hubs: their frontier bitmap (64 KiB) is staged in LDS by
 // every bottom-up workgroup (two 1024-thread workgroups per CU fit in 160 KiB).
@@ -432,6 +443,15 @@ struct TdArgs {
   // clear afterwards.
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
+  // Levels of at least td_hub_min_edges frontier edges read g.td_col and test
+  // hub targets in an LDS copy of td_hub_vis (visited bits of the top-down
+  // hubs, this level's snapshot: hub_visited); not with owner lists.
+  const word_t* td_hub_vis = nullptr;
+  int64_t td_hub_min_edges = 0;
+  // ... and only once the visited vertices hold this fraction of all
+  // adjacency entries (device loop: ctrl->vis_deg; earlier, most hub
+  // targets are unvisited and decoding them costs a dependent load)
+  double td_hub_vis_frac = 0.0;
   // Launch 1024-thread workgroups when the grid has fewer blocks than this.
   int64_t wide_below_blocks = 0;
   // Device loop: q / m come from dev_stats[0..1], bits vs bytes and the
@@ -544,6 +564,18 @@ struct HubLocalArgs {
   const LevelCtrl* ctrl = nullptr;
   int32_t expect_dir = 0;
   int64_t expect_cap = 0;
+};
+
+// out bit h = visited bit of g.td_hub_vertex[h] (visited global): the
+// snapshot a top-down level filters hub targets with; device loop: runs only
+// when ctrl->dir == 'T' (and ctrl->m_f >= min_edges).
+struct HubVisitedArgs {
+  ShardView g;
+  const word_t* visited = nullptr;
+  word_t* out = nullptr;
+  const LevelCtrl* ctrl = nullptr;
+  int64_t min_edges = 0;
+  double vis_frac = 0.0;  // as TdArgs::td_hub_vis_frac
 };
 
 // hub_front bit h = frontier bit of g.hub_vertex[h] (frontier global); in the
@@ -731,6 +763,7 @@ class Backend {
   virtual void bu_head(const BuHeadArgs& a) = 0;
   virtual void hub_local(const HubLocalArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
+  virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;
   virtual void ref_expand(const RefExpandArgs& a) = 0;

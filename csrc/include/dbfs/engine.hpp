@@ -67,7 +67,10 @@ class DeviceGraph {
   // With hubs and `id_order`, bottom-up keeps the hub-first order in its
   // hub-encoded copy and `col` is then put in neighbour-id order for the
   // top-down sweeps (neighbours of one row probe the bitmaps monotonically).
-  void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs, bool id_order = true);
+  // ... and with `td_hubs` also the hub-encoded top-down copy td_col (the
+  // kTdMaxHubs highest-degree vertices encoded; one more nnz x 4 B).
+  void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs, bool id_order = true,
+                                bool td_hubs = true);
   bool hub_sorted() const { return hub_sorted_; }
   // col is in id order (bottom-up must scan hub_col, whose order is hub-first)
   bool col_by_id() const { return col_by_id_; }
@@ -82,7 +85,8 @@ class DeviceGraph {
   bool col_by_id_ = false;
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
-  DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_;
+  DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
+  int64_t td_nhubs_ = 0;
   DBuf<eid_t> nz_pref_, nz_row_off_;
   void build_nz_view();
   DBuf<eid_t> row_off_;
@@ -125,6 +129,16 @@ struct EngineOptions {
   // many frontier edges run binned (BinArgs: targets binned by vertex range,
   // claimed per bin in LDS) instead of td_expand + update; 0 disables.
   int64_t td_bin_edges = 0;
+  // Dense top-down levels with at least this many frontier edges test hub
+  // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
+  // 0 disables.
+  // (RMAT-22 top-down-only, per root: levels of 75-90 M edges 440-511 ->
+  // 397-474 us, the 43-58 M-edge levels before the visited fraction is
+  // reached unchanged; below ~16 M edges the hub snapshot and its LDS staging
+  // cost what they save)
+  int64_t td_hub_edges = int64_t(1) << 24;
+  // ... once the visited vertices hold this fraction of the adjacency
+  double td_hub_vis_frac = 0.75;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.
   double td_check_visited_min = 0.02;
@@ -296,7 +310,7 @@ class Engine {
   void ensure_wide_levels() const;
   // bitmap engine state
   bool bitmap_ready_ = false;
-  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_;
+  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;

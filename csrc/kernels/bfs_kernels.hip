@@ -590,9 +590,11 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
 template <TdOut kOut, int kThreads>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  constexpr bool kHubFilter = kOut != TdOut::Lists && kThreads == kTdThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
+  __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
   long long q = a.q, m = a.m;
   bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
   if (a.ctrl) {
@@ -610,8 +612,20 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const int t = threadIdx.x;
   const int lane = lane_id();
-  const vid_t* __restrict__ col = a.g.col;
   const word_t* __restrict__ visited = a.visited;
+  // large levels: hub targets tested in an LDS copy of the hubs' visited bits
+  // (uniform: every workgroup sees the same m)
+  bool filter = false;
+  if constexpr (kHubFilter) {
+    filter = a.td_hub_vis && a.g.td_col && m >= a.td_hub_min_edges && blockIdx.x < nblocks &&
+             (!a.ctrl || static_cast<double>(a.ctrl->vis_deg) >= a.td_hub_vis_frac * a.ctrl->total_directed);
+    if (filter) {
+      const int64_t hw = (a.g.td_nhubs + kWordBits - 1) / kWordBits;
+      for (int64_t i = t; i < hw; i += kThreads) s_hubvis[i] = a.td_hub_vis[i];
+      // (td_block_owner_map starts with a barrier)
+    }
+  }
+  const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
 
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
     const long long e0 = b * kTdEdgesPerBlock;
@@ -623,17 +637,31 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     // the compiler cannot move a load above an earlier item's atomic, so one
     // item at a time costs kItems dependent round trips per block.
     vid_t vk[kItems];
+    bool live[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int idx = k * kThreads + t;
       vk[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+      live[k] = idx < cnt;
+    }
+    if constexpr (kHubFilter) {
+      if (filter) {
+        // a visited hub is done here; an unvisited one is decoded
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          if (live[k] && (vk[k] & kHubFlag)) {
+            const vid_t h = vk[k] & ~kHubFlag;
+            if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) live[k] = false;
+            else vk[k] = a.g.td_hub_vertex[h];
+          }
+        }
+      }
     }
     if constexpr (kOut != TdOut::Lists) {
       if (!bytes) {
         word_t seen[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k)
-          seen[k] = k * kThreads + t < cnt ? (visited[vk[k] >> 6] | a.next[vk[k] >> 6]) : ~0ull;
+        for (int k = 0; k < kItems; ++k) seen[k] = live[k] ? (visited[vk[k] >> 6] | a.next[vk[k] >> 6]) : ~0ull;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
           const word_t bit = 1ull << (vk[k] & 63);
@@ -647,8 +675,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         const uint8_t lv = static_cast<uint8_t>(a.new_level);
         bool keep[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k)
-          keep[k] = k * kThreads + t < cnt && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
+        for (int k = 0; k < kItems; ++k) keep[k] = live[k] && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           if (keep[k]) a.level_direct[vk[k]] = lv;
@@ -662,7 +689,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       bool keep[kItems];
 #pragma unroll
       for (int k = 0; k < kItems; ++k)
-        keep[k] = k * kThreads + t < cnt && (!check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+        keep[k] = live[k] && (!check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
       uint8_t mark[kItems];
 #pragma unroll
       for (int k = 0; k < kItems; ++k) mark[k] = keep[k] ? a.next_bytes[vk[k]] : 1;
@@ -1631,6 +1658,18 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
   if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
 }
 
+// out bit h = visited bit of td_hub_vertex[h]: one wave per hub word.
+__global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
+  if (a.ctrl && (!chain_live(*a.ctrl, 'T', 0) || a.ctrl->m_f < a.min_edges ||
+                 static_cast<double>(a.ctrl->vis_deg) < a.vis_frac * a.ctrl->total_directed))
+    return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int64_t h = w * kWave + lane_id();
+  const bool bit = h < a.g.td_nhubs && test_bit(a.visited, a.g.td_hub_vertex[h]);
+  const word_t m = __ballot(bit);
+  if (lane_id() == 0 && w * kWave < a.g.td_nhubs) a.out[w] = m;
+}
+
 // Head pass of a split bottom-up level (BuHeadArgs): one wave per 64-word unit,
 // one word per step (lane = vertex).  An unvisited vertex's hub-encoded head
 // (dense non-empty-row view) is tested in the all-reduced hub frontier bits
@@ -1973,6 +2012,11 @@ void bu_head(const BuHeadArgs& a, hipStream_t st) {
 void hub_local(const HubLocalArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
   hub_local_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+}
+
+void hub_visited(const HubVisitedArgs& a, hipStream_t st) {
+  if (a.g.td_nhubs <= 0) return;
+  hub_visited_kernel<<<grid_for((a.g.td_nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {

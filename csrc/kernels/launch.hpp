@@ -27,6 +27,7 @@ void pack_bytes(const PackArgs& a, hipStream_t st);
 void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
+void hub_visited(const HubVisitedArgs& a, hipStream_t st);
 void bu_head(const BuHeadArgs& a, hipStream_t st);
 void hub_local(const HubLocalArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);

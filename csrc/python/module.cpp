@@ -498,6 +498,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def("to_host", &DeviceGraph::to_host, py::call_guard<py::gil_scoped_release>())
       .def("sort_neighbors_by_degree", &DeviceGraph::sort_neighbors_by_degree, py::arg("comm"),
            py::arg("hubs") = true, py::arg("max_hubs") = kMaxHubs, py::arg("id_order") = true,
+           py::arg("td_hubs") = true,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("col_by_id", &DeviceGraph::col_by_id)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
