@@ -35,9 +35,23 @@ CLI       := bin/bfs
 
 HEADERS   := $(wildcard csrc/include/dbfs/*.hpp) $(wildcard csrc/kernels/*.hpp)
 
-.PHONY: all clean lib asan
-all: $(CLI) $(PYMOD)
+.PHONY: all clean lib asan checked
+all: $(CLI) $(PYMOD) bin/bfs_checked
 lib: $(CORE_LIB)
+
+# Device-checked build: bin/bfs_checked, the traversal kernels
+# built with -DDBFS_CHECKED (work-list, owner-list and vertex-id bounds
+# verified on the device; the first violation fails the run on the host,
+# HipBackend::take_device_check).  Host code and the other kernels unchanged.
+CHECKED_BUILD := build-checked
+CHECKED_OBJ   := $(CHECKED_BUILD)/kernels/bfs_kernels.o
+checked: bin/bfs_checked
+$(CHECKED_OBJ): csrc/kernels/bfs_kernels.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DDBFS_CHECKED -c $< -o $@
+bin/bfs_checked: $(BUILD)/cli/main.o $(HOST_OBJ) $(CHECKED_OBJ) $(filter-out $(BUILD)/kernels/bfs_kernels.o,$(HIP_OBJ))
+	@mkdir -p bin
+	$(HIPCC) --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 
 # Host sanitizers: bin/bfs_asan, every host translation unit
 # built with AddressSanitizer + UBSan (g++), device code unchanged.  GPU
@@ -82,4 +96,4 @@ $(PYMOD): $(BUILD)/python/module.o $(CORE_LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -shared $^ -o $@ $(LDLIBS)
 
 clean:
-	rm -rf $(BUILD) $(ASAN_BUILD) bin $(PKG)/_dbfs_native*.so
+	rm -rf $(BUILD) $(ASAN_BUILD) $(CHECKED_BUILD) bin $(PKG)/_dbfs_native*.so

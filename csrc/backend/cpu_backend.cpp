@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "dbfs/backend.hpp"
@@ -330,6 +331,12 @@ class CpuBackend final : public Backend {
       a.mailbox->level = a.level_index;
     }
   }
+
+  // (no device checks in the CPU kernels; the injected violation exercises
+  // the engine's failure path on the CPU)
+  uint64_t take_device_check() override { return std::exchange(check_, 0); }
+  void inject_device_check() override { check_ = 99ull << 48; }
+  uint64_t check_ = 0;
 
   void list_scatter(const ListScatterArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

@@ -212,6 +212,12 @@ class HipBackend final : public Backend {
   void td_binned(const BinArgs& a) override { on(); kern::td_binned(a, st_); chk(); }
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
+  bool device_checks_enabled() const override { return kern::checks_enabled(); }
+  uint64_t take_device_check() override {
+    synchronize();
+    return kern::take_check_error();
+  }
+  void inject_device_check() override { on(); kern::inject_check_failure(st_); chk(); }
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }

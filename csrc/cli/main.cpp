@@ -383,7 +383,7 @@ int main(int argc, char** argv) {
                      static_cast<long long>(l.discovered), l.ms, r.ms);
     };
     csv_run(res[0]);
-    const std::string bname = ranks[0].be->name();
+    const std::string bname = ranks[0].be->name() + (ranks[0].be->device_checks_enabled() ? "+checked" : "");
     if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
 
     // ---- optional K random roots (Graph500-style GTEPS) ----

@@ -486,7 +486,8 @@ void Engine::read_level_stats(int64_t* host_stats) {
 // DBFS_FAULT_INJECT="rank=R,level=L[,kind=throw|exit|hang]" makes rank R fail
 // at the start of level L of every run: `throw` raises an Error (in-process
 // ranks abort their group), `exit` ends the process with status 17 (a crashed
-// rank), `hang` stops participating (peers must time out).  Used by the
+// rank), `hang` stops participating (peers must time out), `device` records
+// a device-check violation (the run fails when it ends).  Used by the
 // failure-detection tests; unset in normal runs.
 FaultSpec FaultSpec::from_env() {
   FaultSpec f;
@@ -507,13 +508,30 @@ FaultSpec FaultSpec::from_env() {
     else DBFS_CHECK(false, "DBFS_FAULT_INJECT: unknown key '" + k + "'");
     pos = comma + 1;
   }
-  DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang",
-             "DBFS_FAULT_INJECT: kind must be throw|exit|hang");
+  DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang" || f.kind == "device",
+             "DBFS_FAULT_INJECT: kind must be throw|exit|hang|device");
   return f;
+}
+
+// Device-checked build: the first bounds violation a kernel recorded during
+// the traversal fails the run (codes: DBFS_DCHECK sites in bfs_kernels.hip).
+void Engine::check_device() {
+  const uint64_t v = be_.take_device_check();
+  if (v == 0) return;
+  char buf[160];
+  std::snprintf(buf, sizeof(buf), "device check failed on rank %d: code %llu, detail %llu", comm_.rank(),
+                static_cast<unsigned long long>(v >> 48), static_cast<unsigned long long>(v & 0xFFFFFFFFFFFFull));
+  throw Error(buf);
 }
 
 void Engine::inject_fault(int level) {
   if (fault_.rank != comm_.rank() || fault_.level != level) return;
+  if (fault_.kind == "device") {
+    // a kernel-side bounds violation (recorded, not raised: the traversal
+    // completes and Engine::check_device fails it afterwards)
+    be_.inject_device_check();
+    return;
+  }
   const std::string what = "injected fault (" + fault_.kind + ") at level " + std::to_string(level) + " on rank " +
                            std::to_string(fault_.rank);
   std::fprintf(stderr, "[dbfs] %s\n", what.c_str());
@@ -602,6 +620,7 @@ RunResult Engine::run(int64_t source) {
   if (run_narrow_ && level8_.size() == 0)
     level8_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1)));
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
+  check_device();
   levels_narrow_ = run_narrow_;
   if (run_narrow_ && r.depth - 1 > kNarrowMaxLevel) {
     // deeper than the narrow levels hold (identical decision on every rank):
@@ -610,6 +629,7 @@ RunResult Engine::run(int64_t source) {
     run_narrow_ = levels_narrow_ = false;
     const double first_ms = r.ms;
     r = use_device_loop() ? run_bitmap_device(source) : run_bitmap(source);
+    check_device();
     r.ms += first_ms;
   }
   if (ref || opt_.directed) {
@@ -893,6 +913,7 @@ RunResult Engine::run_bitmap(int64_t source) {
         la.list_cap = list_cap;
         la.lo = lo;
         la.cand = cand_.data();
+        la.words = part_.slice_words();
         be_.list_scatter(la);
         update(cand_.data(), 1, true, false, L + 1);
       } else if (exchange()) {
@@ -1442,6 +1463,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         la.list_cap = list_stride_;
         la.lo = g_.lo();
         la.cand = cand_.data();
+        la.words = part_.slice_words();
         la.reset_lists = dl_send_lists_.data();
         la.ctrl = ctrl_.data();
         la.max_mf = chain_cap;

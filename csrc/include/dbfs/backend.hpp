@@ -477,6 +477,7 @@ struct ListScatterArgs {
   int64_t list_cap = 0;
   int64_t lo = 0;
   word_t* cand = nullptr;
+  int64_t words = 0;  // words of cand (bounds check of the checked build; 0: unchecked)
   // Device loop: the send lists' counts to zero once the exchange has read
   // them (the next list-form chain appends from zero), and the chain guard.
   vid_t* reset_lists = nullptr;
@@ -764,6 +765,12 @@ class Backend {
   virtual void hub_local(const HubLocalArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
+  // Device-checked build (make checked): whether the kernels verify their
+  // bounds, the first recorded violation (code << 48 | detail; 0: none;
+  // synchronises, clears), and a hook recording violation 99 (fault tests).
+  virtual bool device_checks_enabled() const { return false; }
+  virtual uint64_t take_device_check() { return 0; }
+  virtual void inject_device_check() {}
   virtual void status_expand(const StatusArgs& a) = 0;
   virtual void bitmap_or(word_t* dst, const word_t* src, int64_t words) = 0;
   virtual void ref_expand(const RefExpandArgs& a) = 0;

@@ -292,6 +292,7 @@ class Engine {
   void gather_levels_device(DBuf<lvl_t>& full);
   bool exchange() const { return part_.nranks > 1 || opt_.force_exchange; }
   void inject_fault(int level);
+  void check_device();
 
   DeviceGraph& g_;
   Comm& comm_;

@@ -36,6 +36,26 @@ namespace {
 
 using namespace dev;
 
+// Device-checked build (make checked, -DDBFS_CHECKED): bounds
+// of the work lists, owner lists and vertex ids are verified in the kernels
+// and the first violation is recorded (code << 48 | detail) in g_check --
+// never a trap: the host reads the word after every traversal and throws
+// (HipBackend::device_checks), the GPU keeps running.  Off: no code.
+#ifdef DBFS_CHECKED
+__device__ unsigned long long g_check;
+#define DBFS_DCHECK(cond, code, detail)                                                               \
+  do {                                                                                                \
+    if (!(cond))                                                                                      \
+      atomicCAS(&g_check, 0ull,                                                                       \
+                (static_cast<unsigned long long>(code) << 48) |                                       \
+                    (static_cast<unsigned long long>(detail) & 0xFFFFFFFFFFFFull));                   \
+  } while (0)
+#else
+#define DBFS_DCHECK(cond, code, detail) \
+  do {                                  \
+  } while (0)
+#endif
+
 // First kernel of a device-loop level chain: record its start (device wall
 // clock) for the level's record (scan_units_kernel copies it to rec[L].t0).
 // (The argument blocks carry the control block as const; this field is the
@@ -434,6 +454,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     carry_d += sd;
   }
   if (t == 0) {
+    DBFS_DCHECK(carry_c <= a.nunits * kUnitVertices, 7, carry_c);
     a.stats[0] = a.stats[2] = carry_c;
     a.stats[1] = a.stats[3] = carry_d;
     a.qscan[carry_c] = carry_d;
@@ -508,6 +529,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     const long long incl = wave_incl_scan(d);
     const long long p = pos + mask_rank(tm);
     const long long qs = off + incl - d;
+    DBFS_DCHECK(!take || p < a.g.rows, 1, p);
     if (take) {
       a.qscan[p] = qs;
       a.qbase[p] = rs - qs;
@@ -657,6 +679,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         }
       }
     }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
     if constexpr (kOut != TdOut::Lists) {
       if (!bytes) {
         word_t seen[kItems];
@@ -718,6 +742,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
           vid_t* list = a.lists + static_cast<int64_t>(o) * (a.list_cap + 1);
           if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
           base = __shfl(base, leader, kWave);
+          DBFS_DCHECK(base + __popcll(msk) <= static_cast<unsigned long long>(a.list_cap), 3, base);
           if (owner == o) list[1 + base + mask_rank(msk)] = v;
           pending &= ~msk;
         }
@@ -817,6 +842,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       const long long d = static_cast<long long>(re[k] - rs[k]);
       const long long p = p0 + cbase[k] + mask_rank(tm[k]);
       const long long qs = q0 + ebase[k] + incl[k] - d;
+      DBFS_DCHECK(d <= 0 || p < a.g.rows, 4, p);
       if (d > 0) {
         a.oscan[p] = qs;
         a.obase[p] = rs[k] - qs;
@@ -949,6 +975,7 @@ __global__ __launch_bounds__(kTdThreads) void bin_pass_kernel(BinArgs a) {
     for (int k = 0; k < kItems; ++k) {
       const bool act = k * kTdThreads + t < cnt;
       const int bin = static_cast<int>(v[k] >> a.shift);
+      DBFS_DCHECK(!act || bin < a.nbins, 8, v[k]);
       const unsigned slot = lds_slot_add(s_cnt, bin, act);
       if constexpr (kFill) {
         if (act) a.buf[s_start[bin] + slot] = v[k];
@@ -1086,9 +1113,11 @@ __global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a)
   if (a.reset_lists && blockIdx.x == 0 && threadIdx.x == 0) a.reset_lists[static_cast<int64_t>(r) * (a.list_cap + 1)] = 0;
   const vid_t* list = a.lists + static_cast<int64_t>(r) * (a.list_cap + 1);
   const int64_t n = list[0];
+  DBFS_DCHECK(n <= a.list_cap, 5, n);
   for (int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; k < n;
        k += static_cast<int64_t>(gridDim.x) * kBlock) {
     const int64_t v = static_cast<int64_t>(list[1 + k]) - a.lo;
+    DBFS_DCHECK(v >= 0 && (a.words <= 0 || (v >> 6) < a.words), 6, list[1 + k]);
     atomicOr(a.cand + (v >> 6), 1ull << (v & 63));
   }
 }
@@ -2012,6 +2041,37 @@ void bu_head(const BuHeadArgs& a, hipStream_t st) {
 void hub_local(const HubLocalArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
   hub_local_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+}
+
+#ifdef DBFS_CHECKED
+__global__ void check_fail_kernel(unsigned long long code) { DBFS_DCHECK(false, code, 0); }
+#endif
+
+void inject_check_failure(hipStream_t st) {
+#ifdef DBFS_CHECKED
+  check_fail_kernel<<<1, 1, 0, st>>>(99);
+#else
+  (void)st;
+#endif
+}
+
+bool checks_enabled() {
+#ifdef DBFS_CHECKED
+  return true;
+#else
+  return false;
+#endif
+}
+
+unsigned long long take_check_error() {
+#ifdef DBFS_CHECKED
+  unsigned long long h = 0, z = 0;
+  (void)hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_check), sizeof(h));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_check), &z, sizeof(z));
+  return h;
+#else
+  return 0;
+#endif
 }
 
 void hub_visited(const HubVisitedArgs& a, hipStream_t st) {

@@ -28,6 +28,12 @@ void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
 void hub_visited(const HubVisitedArgs& a, hipStream_t st);
+// device-checked build (DBFS_CHECKED): whether checks are compiled in, the
+// first recorded violation (code << 48 | detail, 0: none; cleared), and a
+// test hook recording code 99
+bool checks_enabled();
+unsigned long long take_check_error();
+void inject_check_failure(hipStream_t st);
 void bu_head(const BuHeadArgs& a, hipStream_t st);
 void hub_local(const HubLocalArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);

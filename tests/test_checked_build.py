@@ -1,0 +1,56 @@
+"""Device-checked build: bin/bfs_checked is the CLI with the
+traversal kernels compiled with -DDBFS_CHECKED (`make checked`, part of
+`make all`).  Kernels verify the bounds of their work lists, owner lists and
+vertex ids (DBFS_DCHECK sites in csrc/kernels/bfs_kernels.hip) and record the
+first violation; the engine reads it after every traversal
+(Engine::check_device) and fails the run.  DBFS_FAULT_INJECT kind=device
+records violation 99 to exercise that path."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import distributed_cuda_bfs_amd as dbfs
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHECKED_BIN = os.path.join(REPO, "bin", "bfs_checked")
+
+
+def test_injected_device_violation_fails_run_cpu(monkeypatch):
+    monkeypatch.setenv("DBFS_FAULT_INJECT", "rank=0,level=1,kind=device")
+    p = dbfs.rmat_params(10, 16, 3)
+    bfs = dbfs.BFS(p, dbfs.init_runtime("cpu"))
+    with pytest.raises(Exception, match="device check failed on rank 0: code 99"):
+        bfs.run(bfs.sample_roots(1, seed=1)[0])
+    # the violation is consumed: the next clean traversal passes
+    monkeypatch.delenv("DBFS_FAULT_INJECT")
+    bfs2 = dbfs.BFS(p, dbfs.init_runtime("cpu"))
+    bfs2.run(bfs2.sample_roots(1, seed=1)[0])
+
+
+def _run(args, env=None, timeout=180):
+    assert os.path.exists(CHECKED_BIN), "bin/bfs_checked missing: run `make checked` (make all builds it)"
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([CHECKED_BIN] + args, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["do", "td", "bu", "ref"])
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_checked_build_clean(mode, ranks):
+    args = ["--rmat", "16", "--roots", "4", "--validate", "--mode", mode, "--json", "--quiet"]
+    if ranks > 1:
+        args += ["--virtual-ranks", str(ranks)]
+    out = _run(args)
+    assert out.returncode == 0, out.stderr[-4000:]
+    runs = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert runs and all(r["backend"].endswith("+checked") for r in runs), out.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_checked_build_reports_violation():
+    out = _run(["--rmat", "14", "--roots", "2", "--quiet"], env={"DBFS_FAULT_INJECT": "rank=0,level=0,kind=device"})
+    assert out.returncode != 0
+    assert "device check failed on rank 0: code 99" in out.stderr, out.stderr[-4000:]
