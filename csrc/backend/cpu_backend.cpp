@@ -213,6 +213,7 @@ class CpuBackend final : public Backend {
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t x = a.frontier[w];
         if (a.clear) a.clear[w] = 0;
+        if (a.clear_all) a.clear_all[w] = 0;
         while (x) {
           const int b = __builtin_ctzll(x);
           x &= x - 1;

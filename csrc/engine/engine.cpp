@@ -70,6 +70,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
+  else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -104,6 +105,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_compact", o.bu_compact ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
+          {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -1338,7 +1340,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     // the frontier bitmap -> work list (set L & 1); with sparse levels also
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
     // writes into it)
-    auto compact = [&] {
+    auto compact = [&](word_t* clear_all) {
       CompactArgs ca;
       ca.g = gv;
       ca.frontier = fr_own(cur);
@@ -1354,13 +1356,17 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ca.qv = qv_[L & 1].data();
         ca.clear = frontier_[cur].data();
       }
+      ca.clear_all = clear_all;
       ca.ctrl = ctrl_.data();
       ca.max_mf = d == 'S' ? sparse_cap : 0;
       be_.compact_frontier(ca);
     };
     if (d == 'S') {
-      DBFS_CHECK(sparse && pf != 'B', "sparse top-down level after a bottom-up level");
-      if (pf == 'T' || pf == 'X') compact();
+      DBFS_CHECK(sparse, "sparse top-down level without sparse support");
+      // after a bottom-up level the output bitmap is that level's input:
+      // zeroed by the compaction (every other form leaves it clean)
+      const bool compacted = pf == 'T' || pf == 'X' || pf == 'B';
+      if (compacted) compact(pf == 'B' ? frontier_[cur ^ 1].data() : nullptr);
       TdSparseArgs sp;
       sp.g = gv;
       sp.qscan = qscan_set(L);
@@ -1386,14 +1392,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.mailbox = mailbox_dev_ + slot(L);
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
-      sp.first = pf != 'T';
+      sp.first = !compacted;
       sp.max_mf = sparse_cap;
       be_.td_sparse(sp);
     } else if (d == 'X') {
       // binned top-down (one rank): a sparse level (or the seed) handed over
       // the work list, else compact
       const bool listed = sparse && (pf == 'S' || pf == 'I');
-      if (!listed) compact();
+      if (!listed) compact(nullptr);
       BinArgs xa;
       xa.g = gv;
       xa.qscan = qscan_set(L);
@@ -1429,7 +1435,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     } else if (d == 'T' || d == 'L') {
       // a sparse level (or the seed) already handed over the work list
       const bool listed = sparse && (pf == 'S' || pf == 'I');
-      if (!listed) compact();
+      if (!listed) compact(nullptr);
       TdArgs ta;
       ta.g = gv;
       ta.qscan = qscan_set(L);
@@ -1642,9 +1648,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   LevelCtrl hc = init;  // host mirror for the prediction
   int64_t prev_nf = 0, prev_mf = 0;
   // top-down form of level L whose frontier has (about) mf edges: sparse when
-  // small, and never right after a bottom-up level (its input bitmap is
-  // still set, so a sparse level would have no clean bitmap to write); with
-  // several ranks list form when the lists stay small
+  // small (right after a bottom-up level too: the compaction then zeroes the
+  // bottom-up input bitmap the sparse level writes into); with several ranks
+  // list form when the lists stay small
   // (exact: mf is the level's actual frontier edges -- a re-enqueue, which
   // must be live: the lists then hold at least mf entries, or the chain is dense)
   auto td_form = [&](int L, double mf, int64_t* cap, bool exact) {
@@ -1659,7 +1665,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       return *cap > 0 ? 'L' : 'T';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    if (sparse && pf != 'B' && mf <= static_cast<double>(opt_.td_sparse_edges)) return 'S';
+    const int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
+    if (sparse && mf <= static_cast<double>(lim)) return 'S';
     return binned && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
   };
   // the chain enqueued for level L is live for a level with direction `dir`

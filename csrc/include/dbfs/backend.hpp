@@ -327,6 +327,9 @@ struct CompactArgs {
   int32_t* blk_vstart = nullptr;
   vid_t* qv = nullptr;              // optional: work-list entry -> vertex (local row)
   word_t* clear = nullptr;          // optional: zero the frontier words once read (== frontier)
+  // optional: zero every word of this bitmap (a sparse level after a
+  // bottom-up one writes its output into the bottom-up level's input)
+  word_t* clear_all = nullptr;
   const LevelCtrl* ctrl = nullptr;  // device loop: runs only when ctrl->dir == 'T'
   int64_t max_mf = 0;               // ... and ctrl->m_f <= max_mf (0: any; a sparse chain's compaction)
 };

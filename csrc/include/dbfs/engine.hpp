@@ -174,6 +174,9 @@ struct EngineOptions {
   // A sparse chain stays live up to td_sparse_cap_factor x td_sparse_edges
   // frontier edges (0: any size); a larger level is re-enqueued dense.
   double td_sparse_cap_factor = 8.0;
+  // The sparse threshold for the first top-down level after a bottom-up one
+  // (the extrapolated prediction of a shrinking frontier overshoots).
+  int64_t td_sparse_bu_edges = int64_t(1) << 18;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a

@@ -506,6 +506,7 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
   const word_t mine = (w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
+  if (a.clear_all && w0 + lane < a.words) a.clear_all[w0 + lane] = 0ull;
   if (!__ballot(mine != 0)) return;
   if (a.clear && mine) a.clear[w0 + lane] = 0ull;  // read once: the next sparse level writes here
   const eid_t* __restrict__ ro = a.g.row_off;
@@ -1231,35 +1232,36 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
   }
   if (p > lim) p = lim;
   if constexpr (kPacked) {
-    // Phase 2, packed: the remaining rows of all unresolved lanes form one
-    // edge stream (lane order); every step the wave tests its next 64
-    // edges, whatever rows they belong to, then drops the rows that hit or
-    // ran out.  Steps = ceil(sum of remaining lengths / 64) instead of one
-    // or more dependent steps per unresolved vertex.
+    // Phase 2, packed: the remaining neighbours of all unresolved lanes form
+    // one edge stream (lane order); every step the wave tests the stream's
+    // next 64 entries, whatever rows they belong to (owner lane of slot s:
+    // the first lane whose inclusive prefix exceeds s, a 6-shuffle search),
+    // then drops the rows that hit and advances the rest.  Steps ~ ceil(sum
+    // of remaining lengths / 64) instead of one or more dependent steps per
+    // unresolved row.  32-bit stream positions (queued rows hold < 2^20
+    // entries; a step covers 64 of them).
     for (;;) {
-      const long long rem = (!found && p < len) ? static_cast<long long>(len - p) : 0;
+      const uint32_t rem = (!found && p < len) ? len - p : 0u;
       if (!__ballot(rem > 0)) break;
-      const long long incl = wave_incl_scan(rem);
-      const long long excl = incl - rem;
-      own[lane] = -1;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (rem > 0 && excl < kWave) own[excl] = lane;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const int o = wave_incl_max(own[lane]);  // owner lane of edge slot `lane`
-      const long long total = readlane_i64(incl, kWave - 1);
-      const long long o_excl = __shfl(excl, o, kWave);
-      const long long o_p = __shfl(static_cast<long long>(rs + p), o, kWave);
-      bool hit = false;
-      if (lane < total) hit = bu_probe<kHub>(fr, s_hub, col[o_p + (lane - o_excl)]);
-      // owners with a hit: set bit o of a wave mask
-      unsigned long long hitmask = hit ? (1ull << o) : 0ull;
+      BU_STAT(6, 1);
+      const uint32_t incl = wave_incl_scan_u32(rem);
+      const uint32_t excl = incl - rem;
+      const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
+      const uint32_t slot = static_cast<uint32_t>(lane);
+      int o = 0;
 #pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) hitmask |= __shfl_xor(hitmask, off, kWave);
-      if ((hitmask >> lane) & 1ull) found = true;
-      const long long took = rem > 0 ? max(0LL, min(rem, static_cast<long long>(kWave) - excl)) : 0;
-      p += static_cast<uint32_t>(took);
+      for (int step = 32; step >= 1; step >>= 1)
+        if (static_cast<uint32_t>(__shfl(static_cast<int>(incl), o + step - 1, kWave)) <= slot) o += step;
+      o = min(o, kWave - 1);
+      const uint32_t o_excl = static_cast<uint32_t>(__shfl(static_cast<int>(excl), o, kWave));
+      const vid_t* o_next = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row + p), o, kWave));
+      bool hit = false;
+      if (slot < total) hit = bu_probe<kHub>(fr, s_hub, o_next[slot - o_excl]);
+      unsigned long long hm = hit ? (1ull << o) : 0ull;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) hm |= __shfl_xor(hm, off, kWave);
+      if ((hm >> lane) & 1ull) found = true;
+      p += (rem > 0 && excl < static_cast<uint32_t>(kWave)) ? min(rem, static_cast<uint32_t>(kWave) - excl) : 0u;
     }
   } else {
     // Phase 2: the wave scans each still-unresolved row in turn,
@@ -1267,7 +1269,11 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
     // flight together, then their probes): a row that scans to its end --
     // most rows at a bottom-up level entered with a small frontier -- costs
     // len / (64 kBuScanSteps) dependent round trips instead of len / 64.
+#ifdef DBFS_BU_NO_P2  // diagnostic timing build: no phase-2 scans (wrong levels)
+    unsigned long long pending = 0;
+#else
     unsigned long long pending = __ballot(!found && p < len);
+#endif
     BU_STAT(5, __popcll(pending));
     while (pending) {
       const int l = __ffsll(static_cast<long long>(pending)) - 1;
@@ -1610,7 +1616,7 @@ template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubB
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   // per-wave scratch of the packed row scans (kPacked, or the queue flushes)
-  constexpr bool kOwn = kPacked || (kCompact && kQ > 0 && kPackFlush);
+  constexpr bool kOwn = kPacked;
   __shared__ int s_bu_owner[kOwn ? kThreads : 1];
   __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];

@@ -39,6 +39,16 @@ __device__ __forceinline__ long long wave_incl_scan(long long x) {
   return x;
 }
 
+__device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const unsigned y = __shfl_up(x, off, kWave);
+    if (l >= off) x += y;
+  }
+  return x;
+}
+
 __device__ __forceinline__ int wave_incl_max(int x) {
   const int l = lane_id();
 #pragma unroll
