@@ -103,9 +103,13 @@ class CpuBackend final : public Backend {
   void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init) override { *c = init; }
   void init_run(const InitRunArgs& a) override {
     const int64_t src = a.src_local;
-    for (int64_t i = 0; i < a.g.rows; ++i) {
-      if (a.level8) a.level8[i] = i == src ? 0 : kNarrowUnreached;
-      else a.level[i] = i == src ? 0 : kUnreached;
+    if (a.level8 && a.level8_filled) {
+      if (src >= 0) a.level8[src] = 0;
+    } else {
+      for (int64_t i = 0; i < a.g.rows; ++i) {
+        if (a.level8) a.level8[i] = i == src ? 0 : kNarrowUnreached;
+        else a.level[i] = i == src ? 0 : kUnreached;
+      }
     }
     for (int64_t w = 0; w < a.gwords; ++w) a.visited[w] = a.zdeg[w];
     for (int64_t w = 0; w < a.words; ++w) a.frontier[w] = 0;

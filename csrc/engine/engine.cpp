@@ -71,6 +71,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
+  else if (name == "level_prefill") o.level_prefill = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -106,6 +107,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
+          {"level_prefill", o.level_prefill ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -619,8 +621,21 @@ RunResult Engine::run(int64_t source) {
   run_narrow_ = !ref && use_narrow();
   // (padded to whole bitmap words: a direct top-down update reads a word's
   // 64 level bytes; padding vertices are pre-set visited, so masked)
-  if (run_narrow_ && level8_.size() == 0)
-    level8_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1)));
+  const size_t l8_bytes = static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1));
+  if (run_narrow_ && level8_.size() == 0) level8_ = DBuf<uint8_t>(be_, l8_bytes);
+  level8_filled_ = false;
+  if (run_narrow_ && opt_.level_prefill && comm_.size() == 1) {
+    // the buffer filled under the previous run becomes this run's; the
+    // previous run's levels are overwritten by the fill for the next one
+    if (level8_next_ready_) {
+      std::swap(level8_, level8_next_);
+      be_.prefill_wait();
+      level8_filled_ = true;
+    }
+    if (level8_next_.size() == 0) level8_next_ = DBuf<uint8_t>(be_, l8_bytes);
+    be_.prefill_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
+    level8_next_ready_ = true;
+  }
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
   check_device();
   levels_narrow_ = run_narrow_;
@@ -683,6 +698,7 @@ InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* 
   ia.g = g_.view();
   ia.level = level_.data();
   ia.level8 = run_narrow_ ? level8_.data() : nullptr;
+  ia.level8_filled = level8_filled_;
   ia.zdeg = zdeg_.data();
   ia.visited = visited_.data();
   ia.gwords = part_.global_words();
@@ -1665,7 +1681,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       return *cap > 0 ? 'L' : 'T';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    const int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
+    int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
+    if (sparse_cap > 0) lim = std::min(lim, sparse_cap);  // (a sparse chain must stay live for mf)
     if (sparse && mf <= static_cast<double>(lim)) return 'S';
     return binned && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
   };

@@ -187,6 +187,7 @@ struct InitRunArgs {
   // levels up to kNarrowMaxLevel): written instead of `level` when set, here
   // and by every bitmap-engine kernel that writes levels.
   uint8_t* level8 = nullptr;
+  bool level8_filled = false;      // level8 already holds kNarrowUnreached (prefilled): only the source's byte
   const word_t* zdeg = nullptr;    // global
   word_t* visited = nullptr;       // global
   int64_t gwords = 0;
@@ -700,6 +701,12 @@ class Backend {
   virtual void* comm_stream_handle() { return stream_handle(); }
   virtual void fork_side() {}
   virtual void join_side() {}
+  // Fill `bytes` at dst with `value` on the side stream once everything
+  // enqueued on the compute stream so far has run (a buffer the next
+  // traversal uses, prepared under this one); prefill_wait() orders the
+  // compute stream after the last such fill.  (CPU: immediate.)
+  virtual void prefill_async(void* dst, int value, size_t bytes) { memset_async(dst, value, bytes); }
+  virtual void prefill_wait() {}
   // Rate of the device wall clock the kernels stamp level records with (ticks
   // per ms; 0: no device clock, records carry no times).
   virtual double wall_clock_khz() const { return 0.0; }

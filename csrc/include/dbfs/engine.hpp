@@ -177,6 +177,13 @@ struct EngineOptions {
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;
+  // One rank, narrow levels: the level bytes are double-buffered and the next
+  // run's buffer is filled on the side stream while this run traverses (its
+  // first levels are latency-bound), instead of by the run's init kernel.
+  // Off: measured slower on RMAT-26 (1219 / 1192 against 1238 / 1261 GTEPS,
+  // alternating runs): the cross-stream fill and event waits cost more than
+  // the 64 MiB fill (~13 us) they take off the critical path.
+  bool level_prefill = false;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a
@@ -307,6 +314,11 @@ class Engine {
 
   DBuf<lvl_t> level_;
   DBuf<uint8_t> level8_;
+  // one rank: the next run's level bytes, filled with kNarrowUnreached on the
+  // side stream under the current run (EngineOptions::level_prefill)
+  DBuf<uint8_t> level8_next_;
+  bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
+  bool level8_filled_ = false;        // level8_ was prefilled for the current run
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels
   bool run_narrow_ = false;           // the current run writes level8_
   mutable bool levels_narrow_ = false;  // level_ is stale: level8_ holds the last run's levels

@@ -125,7 +125,10 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const int64_t rows = a.g.rows;
   const int64_t src = a.src_local;
-  if (a.level8) {
+  if (a.level8 && a.level8_filled) {
+    // prefilled on the side stream: the source's byte only
+    if (src >= 0 && t0 == 0) a.level8[src] = 0;
+  } else if (a.level8) {
     // narrow levels: rows / 16 uint4 stores of 0xFF (+ tail), the source's byte after
     const int64_t n16 = (reinterpret_cast<uintptr_t>(a.level8) & 15u) == 0 ? rows / 16 : 0;
     uint4* l16 = reinterpret_cast<uint4*>(a.level8);

@@ -510,3 +510,16 @@ def test_td_direct_levels_cpu(rt, mode, direct_edges):
     cb.engine.set_option("td_direct_edges", direct_edges)
     cb.run(0)
     assert np.array_equal(cb.levels(), np.arange(n))
+
+
+@pytest.mark.parametrize("mode", ["do", "td", "bu"])
+def test_level_prefill_cpu(rt, mode):
+    # double-buffered level bytes (the next run's buffer prefilled): exact
+    # over consecutive runs
+    p = dbfs.rmat_params(11, 16, 9)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    bfs.engine.set_option("level_prefill", 1)
+    for src in bfs.sample_roots(4, seed=3):
+        bfs.run(src)
+        assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
