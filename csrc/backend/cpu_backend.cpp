@@ -362,6 +362,19 @@ class CpuBackend final : public Backend {
   }
 
   void bu_step(const BuArgs& a) override {
+    if (a.fuse_scan) {
+      // totals and finish right after the step; the unit statistics stay
+      // unscanned (as the HIP kernel's fused finish leaves them)
+      BuArgs b = a;
+      b.fuse_scan = false;
+      bu_step(b);
+      const int64_t n = a.scan.nunits;
+      std::vector<int64_t> c(a.scan.unit_cnt, a.scan.unit_cnt + n), d(a.scan.unit_deg, a.scan.unit_deg + n);
+      scan_units(a.scan);
+      std::copy(c.begin(), c.end(), a.scan.unit_cnt);
+      std::copy(d.begin(), d.end(), a.scan.unit_deg);
+      return;
+    }
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {

@@ -72,6 +72,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "level_prefill") o.level_prefill = v != 0;
+  else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -108,6 +109,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"level_prefill", o.level_prefill ? 1.0 : 0.0},
+          {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -1252,7 +1254,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     finish_ranks(-1, true, 0, 0, seed_carry);
   }
 
-  auto scan = [&](int level, bool seed, char expect_dir, int64_t cap) {
+  auto scan_args = [&](int level, bool seed, char expect_dir, int64_t cap) {
     ScanArgs sa;
     sa.unit_cnt = unit_cnt_.data();
     sa.unit_deg = unit_deg_.data();
@@ -1270,7 +1272,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     sa.expect_dir = expect_dir;
     sa.expect_cap = cap;
     sa.finish = !xc;
-    be_.scan_units(sa);
+    return sa;
+  };
+  auto scan = [&](int level, bool seed, char expect_dir, int64_t cap) {
+    be_.scan_units(scan_args(level, seed, expect_dir, cap));
   };
   // Frontier double buffer: the seed is frontier_[1]; level L reads
   // frontier_[(L + 1) & 1] and writes the other one.
@@ -1292,6 +1297,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B'; several ranks: 'L' list form)
   std::vector<int64_t> enq_cap;  // ... list form: the global frontier edges its lists hold
   std::vector<char> enq_carry;   // ... several ranks: its reduction carries the hub bits
+  std::vector<char> enq_fused;   // ... bottom-up: finished in the kernel (unit prefixes not scanned)
   // Enqueue level L's chain for direction d: top-down = compact + td_expand +
   // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
   // so a chain enqueued for the wrong direction is a handful of no-op launches.
@@ -1314,7 +1320,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     while (static_cast<double>(c) < want) c <<= 1;
     return std::min(c, list_max);
   };
-  auto enqueue_level = [&](int L, char d, int64_t cap) {
+  // mf_hint: the level's predicted (or, re-enqueued, actual) frontier edges;
+  // < 0 unknown
+  auto enqueue_level = [&](int L, char d, int64_t cap, double mf_hint = -1.0) {
     hmark("enqueue " + std::to_string(L) + d);
     if (static_cast<size_t>(L) >= enq_dir.size()) {
       inject_fault(L);
@@ -1322,6 +1330,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       enq_form.resize(static_cast<size_t>(L) + 1);
       enq_cap.resize(static_cast<size_t>(L) + 1);
       enq_carry.resize(static_cast<size_t>(L) + 1);
+      enq_fused.resize(static_cast<size_t>(L) + 1);
       evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
     }
     // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up, 'L' list
@@ -1343,6 +1352,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
     const bool split = xc && d == 'B' && split_ok && in_carry;
+    bool fused_scan = false;  // the bottom-up kernel runs the level's scan
     // several ranks: the level's input frontier to every rank (all-gather of
     // the owned slices) and into the replicated visited bitmap -- before a
     // bottom-up level, and before top-down levels of the td mode (fewer
@@ -1357,6 +1367,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
     // writes into it)
     auto compact = [&](word_t* clear_all) {
+      if (pf == 'B' && enq_fused[static_cast<size_t>(L - 1)]) {
+        // the bottom-up level only finished its totals: its unit prefixes
+        // now (no finish; a no-op unless this chain is live)
+        ScanArgs sa = scan_args(L - 1, false, 'T', d == 'S' ? sparse_cap : 0);
+        sa.finish = false;
+        be_.scan_units(sa);
+      }
       CompactArgs ca;
       ca.g = gv;
       ca.frontier = fr_own(cur);
@@ -1498,7 +1515,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       } else {
         ta.next = next_.data();
         ta.next_bytes = next_bytes_.data();
-        if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0) {
+        // (skipped for levels predicted well below the filter's threshold:
+        // the snapshot kernel would only find its gate closed)
+        if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
+            (mf_hint < 0 || mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
           // large levels: the hubs' visited bits, staged in LDS by td_expand
           if (!td_hub_vis_.data()) td_hub_vis_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(gv.td_nhubs, kWordBits)));
           HubVisitedArgs hv;
@@ -1634,10 +1654,23 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           ba.merge = true;
           ba.heads_done = true;
         }
+        if (!xc && opt_.bu_fused_scan && !ba.merge) {
+          // the level's totals and finish in the bottom-up kernel's last
+          // workgroup; the unit prefixes only if a top-down chain follows
+          if (!bu_tot_.data()) {
+            bu_tot_ = DBuf<int64_t>(be_, 2);
+            be_.memset_async(bu_tot_.data(), 0, bu_tot_.bytes());
+          }
+          ba.fuse_scan = true;
+          ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
+          ba.tot = bu_tot_.data();
+          fused_scan = true;
+        }
         be_.bu_step(ba);
       }
     }
-    if (d != 'S') scan(L, false, enq_dir[L], chain_cap);
+    if (d != 'S' && !fused_scan) scan(L, false, enq_dir[L], chain_cap);
+    enq_fused[L] = fused_scan;
     if (xc) {
       if (enq_carry[L]) hub_bits(L, fr_own(cur ^ 1), enq_dir[L], chain_cap, true);
       finish_ranks(L, false, enq_dir[L], chain_cap, enq_carry[L] != 0);
@@ -1726,7 +1759,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (!valid) {
       int64_t cap = 0;
       const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
-      enqueue_level(L, f, cap);
+      enqueue_level(L, f, cap, static_cast<double>(mf));
     }
     // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
     auto grow = [](int64_t cur, int64_t prev) {
@@ -1751,7 +1784,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     prev_mf = mf;
     int64_t lcap = 0;
     const char f = hc.dir == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
-    enqueue_level(L + 1, f, lcap);
+    enqueue_level(L + 1, f, lcap, emf);
   }
   // The traversal is complete once the last stamp is seen: the stamping
   // workgroup ran after all of that level's work (and every earlier level's).

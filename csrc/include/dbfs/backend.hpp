@@ -531,6 +531,16 @@ struct BuArgs {
   // not settle is known to miss, so rows are not probed at their head again
   // (rows of one entry are done, longer ones go straight to the row scan).
   bool heads_done = false;
+  // One rank, device loop: the level's totals and finish (ScanArgs: stats,
+  // direction decision, record, mailbox) run in the bottom-up kernel's
+  // last-arriving workgroup instead of a scan launch: workgroups add their
+  // totals into tot[0..1] (zero; reset by the last one).  The per-unit
+  // prefixes are left to a scan_units (finish off) in the next chain, only
+  // when it compacts the frontier (a top-down level).  Kernels without the
+  // epilogue launch scan_units after themselves.
+  bool fuse_scan = false;
+  ScanArgs scan;
+  int64_t* tot = nullptr;
 };
 
 // First half of a split bottom-up level (several ranks): while the frontier

@@ -184,6 +184,10 @@ struct EngineOptions {
   // alternating runs): the cross-stream fill and event waits cost more than
   // the 64 MiB fill (~13 us) they take off the critical path.
   bool level_prefill = false;
+  // One rank, device loop: a bottom-up level's unit scan (totals, direction
+  // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
+  // workgroup instead of a kernel of its own.
+  bool bu_fused_scan = true;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a
@@ -317,6 +321,7 @@ class Engine {
   // one rank: the next run's level bytes, filled with kNarrowUnreached on the
   // side stream under the current run (EngineOptions::level_prefill)
   DBuf<uint8_t> level8_next_;
+  DBuf<int64_t> bu_tot_;  // fused bottom-up finish: the level's totals (BuArgs::tot)
   bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
   bool level8_filled_ = false;        // level8_ was prefilled for the current run
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels

@@ -373,6 +373,55 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
 // `s_waitcnt vmcnt(0)`, agent release fence, `s_waitcnt vmcnt(0)` (compiler
 // hazard, MI355X_MICROARCH), then the ticket atomic; the last arriver runs an
 // agent acquire fence before any thread reads the totals.
+// The level's totals (count, degree sum of the new frontier) -> stats, the
+// work list's end marker, the ticket reset and (device loop) the direction
+// decision, level record and mailbox stamp.  One thread.
+__device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c, long long carry_d) {
+  DBFS_DCHECK(carry_c <= a.nunits * kUnitVertices, 7, carry_c);
+  a.stats[0] = a.stats[2] = carry_c;
+  a.stats[1] = a.stats[3] = carry_d;
+  a.qscan[carry_c] = carry_d;
+  *a.ticket = 0u;  // next launch is stream-ordered after this one
+  if (a.ctrl && a.finish) {
+    LevelCtrl c = *a.ctrl;
+    level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
+    if (!a.seed) {
+      a.rec->t0 = c.t_start;
+      a.rec->t1 = wall_clock64();
+    }
+    *a.ctrl = c;
+    if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
+  }
+}
+
+// Totals and finish of a level whose unit statistics stay unscanned (the
+// fused bottom-up finish of kernels without the epilogue): one workgroup
+// sums the units, thread 0 finishes.
+__global__ __launch_bounds__(kScanChunk) void totals_finish_kernel(ScanArgs a) {
+  __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
+  if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
+  long long c = 0, d = 0;
+  for (int64_t u = threadIdx.x; u < a.nunits; u += kScanChunk) {
+    c += a.unit_cnt[u];
+    d += a.unit_deg[u];
+  }
+  c = wave_sum(c);
+  d = wave_sum(d);
+  const int wv = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    s_c[wv] = c;
+    s_d[wv] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  long long tc = 0, td = 0;
+  for (int k = 0; k < kScanChunk / kWave; ++k) {
+    tc += s_c[k];
+    td += s_d[k];
+  }
+  scan_finish(a, tc, td);
+}
+
 __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;
@@ -456,24 +505,9 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     carry_c += sc;
     carry_d += sd;
   }
-  if (t == 0) {
-    DBFS_DCHECK(carry_c <= a.nunits * kUnitVertices, 7, carry_c);
-    a.stats[0] = a.stats[2] = carry_c;
-    a.stats[1] = a.stats[3] = carry_d;
-    a.qscan[carry_c] = carry_d;
-    *a.ticket = 0u;  // next launch is stream-ordered after this one
-    if (a.ctrl && a.finish) {
-      LevelCtrl c = *a.ctrl;
-      level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
-      if (!a.seed) {
-        a.rec->t0 = c.t_start;
-        a.rec->t1 = wall_clock64();
-      }
-      *a.ctrl = c;
-      if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
-    }
-  }
+  if (t == 0) scan_finish(a, carry_c, carry_d);
 }
+
 
 // blk[b] = p for every edge block b (kTdEdgesPerBlock edges) that starts in the
 // entry's edge range [qs, qs + d) -- wave-uniform call.  Short ranges are
@@ -1639,12 +1673,49 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     // small shards (many ranks) keep 16 words per wave for parallelism.
     constexpr int kWavesPerBlock = kThreads / kWave;
     int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
+    // (fused finish: this wave's totals accumulate in its LDS slots)
+    if (lane_id() == 0) {
+      s_c[wave] = 0;
+      s_d[wave] = 0;
+    }
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
       bu_wave_compact<kPacked, true, kUnitWords, kQueueLen>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
                                                             cnt, deg, s_q + wave * kQueueLen);
-      wave_unit_stats_store(cnt, deg, u, a.unit_cnt, a.unit_deg, a.merge);
+      cnt = wave_sum(cnt);
+      deg = wave_sum(deg);
+      if (lane_id() == 0) {
+        a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + cnt : cnt;
+        a.unit_deg[u] = a.merge ? a.unit_deg[u] + deg : deg;
+        s_c[wave] += cnt;
+        s_d[wave] += deg;
+      }
+    }
+    if (!a.fuse_scan) return;
+    // fused finish: the workgroup's totals into tot (device atomics, one
+    // pair per workgroup), a ticket; the last workgroup finishes the level
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long c = 0, d = 0;
+      for (int k = 0; k < kWavesPerBlock; ++k) {
+        c += s_c[k];
+        d += s_d[k];
+      }
+      if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot), static_cast<unsigned long long>(c));
+      if (d) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot + 1), static_cast<unsigned long long>(d));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+      if (prev == gridDim.x - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const long long tc = static_cast<long long>(
+            __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const long long td = static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 1),
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        a.tot[0] = 0;
+        a.tot[1] = 0;
+        scan_finish(a.scan, tc, td);  // (resets the ticket)
+      }
     }
     return;
   }
@@ -2024,6 +2095,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue><<<grid, kFollowThreads, 0, st>>>(a);
     else if (whole)
       bu_hub_kernel<false, true, true, kFirstThreads><<<grid, kFirstThreads, 0, st>>>(a);
+    if (whole) return;  // (the whole-unit kernels run a fused scan themselves)
     else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
     else if (a.compact && a.follow_up)  // scan-heavy later level: no deferral (measured)
@@ -2031,6 +2103,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     else
       a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);
 #undef DBFS_BU_HUB
+    if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
     return;
   }
   const unsigned grid = grid_for(a.words, kUnitWords);
@@ -2040,6 +2113,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   else
     a.compact ? DBFS_BU(false, true) : DBFS_BU(false, false);
 #undef DBFS_BU
+  if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
 }
 
 void bu_head(const BuHeadArgs& a, hipStream_t st) {
