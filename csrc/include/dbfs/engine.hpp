@@ -138,6 +138,7 @@ struct EngineOptions {
   // cost what they save)
   int64_t td_hub_edges = int64_t(1) << 24;
   // ... once the visited vertices hold this fraction of the adjacency
+  // (measured: 0, i.e. also the earlier big levels, 58.9 against 63.5 GTEPS)
   double td_hub_vis_frac = 0.75;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.

@@ -704,15 +704,26 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       vk[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
       live[k] = idx < cnt;
     }
+    // hub targets tested in the LDS snapshot: a visited hub is done here; an
+    // unvisited one is decoded and needs no global visited probe (unvisited
+    // at the level's start).  (Measured: claiming hubs in LDS as well, to
+    // store each once per workgroup, is slower -- few repeats per workgroup,
+    // LDS atomics on popular hubs serialise.)
+    bool hubnew[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) hubnew[k] = false;
     if constexpr (kHubFilter) {
       if (filter) {
-        // a visited hub is done here; an unvisited one is decoded
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
           if (live[k] && (vk[k] & kHubFlag)) {
             const vid_t h = vk[k] & ~kHubFlag;
-            if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) live[k] = false;
-            else vk[k] = a.g.td_hub_vertex[h];
+            if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) {
+              live[k] = false;
+            } else {
+              vk[k] = a.g.td_hub_vertex[h];
+              hubnew[k] = true;
+            }
           }
         }
       }
@@ -723,7 +734,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       if (!bytes) {
         word_t seen[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) seen[k] = live[k] ? (visited[vk[k] >> 6] | a.next[vk[k] >> 6]) : ~0ull;
+        for (int k = 0; k < kItems; ++k)
+          seen[k] = live[k] ? (hubnew[k] ? 0ull : (visited[vk[k] >> 6] | a.next[vk[k] >> 6])) : ~0ull;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
           const word_t bit = 1ull << (vk[k] & 63);
@@ -737,7 +749,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         const uint8_t lv = static_cast<uint8_t>(a.new_level);
         bool keep[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = live[k] && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
+        for (int k = 0; k < kItems; ++k)
+          keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           if (keep[k]) a.level_direct[vk[k]] = lv;
@@ -751,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       bool keep[kItems];
 #pragma unroll
       for (int k = 0; k < kItems; ++k)
-        keep[k] = live[k] && (!check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+        keep[k] = live[k] && (hubnew[k] || !check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
       uint8_t mark[kItems];
 #pragma unroll
       for (int k = 0; k < kItems; ++k) mark[k] = keep[k] ? a.next_bytes[vk[k]] : 1;
