@@ -78,7 +78,7 @@ def parse_args(argv=None):
     ap.add_argument("--root-seed", type=int, default=12345)
     ap.add_argument("--alpha", type=float, default=24.0)
     ap.add_argument("--beta", type=float, default=96.0)
-    ap.add_argument("--bu-lane-limit", type=int, default=8)
+    ap.add_argument("--bu-lane-limit", type=int, default=16)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning option (see Engine.get_options()), repeatable")
     ap.add_argument("--no-hubs", action="store_true", help="bottom-up without the LDS hub frontier")

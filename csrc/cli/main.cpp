@@ -44,7 +44,7 @@ struct Args {
   bool cpu = false;
   std::string mode = "do";
   double alpha = 24.0, beta = 96.0;
-  int bu_lane_limit = 8;
+  int bu_lane_limit = 16;
   int rmat_scale = 0, rmat_ef = 16;
   int64_t uni_n = 0, uni_m = 0;
   uint64_t seed = 1;

@@ -100,7 +100,10 @@ struct EngineOptions {
   // CPU value (14) pays.
   double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 96.0;   // BU -> TD when n_f < n / beta (and shrinking)
-  int bu_lane_limit = 8;
+  // neighbours a lane checks itself before rows go to wave-cooperative scans
+  // (16: a first bottom-up level entered with a small frontier resolves more
+  // rows per lane; RMAT-26 1240 -> 1259 GTEPS, 8 and 32 worse)
+  int bu_lane_limit = 16;
   // Bottom-up rows still unresolved after the per-lane phase are scanned as
   // one packed edge stream per wave (else one row at a time).
   bool bu_packed = false;
