@@ -616,6 +616,20 @@ class CpuBackend final : public Backend {
     nz_ro[k] = rows > 0 ? ro[rows] : 0;
     (void)pref;
   }
+  void nz_records(const eid_t* ro, const vid_t* head, int64_t rows, const eid_t* pref, NzRec* rec,
+                  eid_t* unit_base) override {
+    const int64_t nunits = div_up(std::max<int64_t>(rows, 1), kUnitVertices);
+    for (int64_t u = 0; u <= nunits; ++u) unit_base[u] = ro[std::min<int64_t>(u * kUnitVertices, rows)];
+    int64_t k = 0;
+    for (int64_t v = 0; v < rows; ++v) {
+      if (ro[v + 1] > ro[v]) {
+        rec[k].off = static_cast<uint32_t>(ro[v] - unit_base[v / kUnitVertices]);
+        rec[k].head = head[v];
+        ++k;
+      }
+    }
+    (void)pref;
+  }
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {
     int64_t k = 0;

@@ -274,6 +274,12 @@ class HipBackend final : public Backend {
     kern::nz_word_counts(ro, rows, words, counts, st_);
     chk();
   }
+  void nz_records(const eid_t* ro, const vid_t* head, int64_t rows, const eid_t* pref, NzRec* rec,
+                  eid_t* unit_base) override {
+    on();
+    kern::nz_records(ro, head, rows, div_up(rows, kWordBits), pref, rec, unit_base, st_);
+    chk();
+  }
   void nz_fill(const eid_t* ro, const vid_t* head, int64_t rows, const eid_t* pref, eid_t* nz_ro,
                vid_t* nz_head) override {
     on();

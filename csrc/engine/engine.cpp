@@ -73,6 +73,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "level_prefill") o.level_prefill = v != 0;
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
+  else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -110,6 +111,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"level_prefill", o.level_prefill ? 1.0 : 0.0},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
+          {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -291,6 +293,8 @@ ShardView DeviceGraph::view() const {
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
+  v.nz_rec = nz_rec_.data();
+  v.unit_base = unit_base_.data();
   if (td_nhubs_ > 0) {
     v.td_col = td_col_.data();
     v.td_hub_vertex = td_hub_vertex_.data();
@@ -425,6 +429,22 @@ void DeviceGraph::build_nz_view() {
   nz_row_off_ = DBuf<eid_t>(*be_, static_cast<size_t>(nzrows + 1));
   nz_head_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<eid_t>(nzrows, 1)));
   be_->nz_fill(row_off_.data(), head_.data(), rows_, nz_pref_.data(), nz_row_off_.data(), nz_head_.data());
+  // packed records, when every unit's edges fit 32-bit relative offsets
+  nz_rec_ = DBuf<NzRec>();
+  unit_base_ = DBuf<eid_t>();
+  if (rows_ <= 0) return;
+  const int64_t nunits = div_up(rows_, kUnitVertices);
+  unit_base_ = DBuf<eid_t>(*be_, static_cast<size_t>(nunits + 1));
+  nz_rec_ = DBuf<NzRec>(*be_, static_cast<size_t>(std::max<eid_t>(nzrows, 1)));
+  be_->nz_records(row_off_.data(), head_.data(), rows_, nz_pref_.data(), nz_rec_.data(), unit_base_.data());
+  std::vector<eid_t> ub(static_cast<size_t>(nunits + 1));
+  be_->to_host(ub.data(), unit_base_.data(), ub.size() * sizeof(eid_t));
+  for (int64_t u = 0; u < nunits; ++u)
+    if (ub[static_cast<size_t>(u + 1)] - ub[static_cast<size_t>(u)] >= (eid_t(1) << 32)) {
+      nz_rec_ = DBuf<NzRec>();
+      unit_base_ = DBuf<eid_t>();
+      break;
+    }
 }
 
 // ---- Engine ----------------------------------------------------------------------
@@ -969,6 +989,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = !res.levels.empty() && res.levels.back().direction == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
+      if (!opt_.bu_nz_rec) ba.g.nz_rec = nullptr;
       if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
@@ -1583,6 +1604,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = pf == 'B';
       if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
+      if (!opt_.bu_nz_rec) ba.g.nz_rec = nullptr;
       if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();

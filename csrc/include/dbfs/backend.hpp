@@ -30,6 +30,12 @@ enum class DeviceKind { CPU, HIP };
 // ---- kernel argument blocks -------------------------------------------------
 
 // Local CSR shard: rows [lo, lo + rows) of an n-vertex graph, global column ids.
+// Packed row record of the non-empty-row view (ShardView::nz_rec).
+struct alignas(8) NzRec {
+  uint32_t off;   // row start - unit_base[unit]
+  vid_t head;     // the row's head (hub-encoded like ShardView::head)
+};
+
 struct ShardView {
   const eid_t* row_off = nullptr;  // rows + 1 (local)
   const vid_t* col = nullptr;      // row_off[rows]
@@ -55,6 +61,13 @@ struct ShardView {
   const eid_t* nz_pref = nullptr;
   const eid_t* nz_row_off = nullptr;
   const vid_t* nz_head = nullptr;
+  // Packed non-empty-row records (optional, with the view): nz_rec[k] = {row
+  // start relative to unit_base[U], head} for row k of unit U (4096
+  // vertices); row k ends where row k + 1 starts, or at unit_base[U + 1] for
+  // the unit's last non-empty row.  8 bytes per row instead of the view's
+  // 8-byte offset + 4-byte head; present when every unit spans < 2^32 edges.
+  const struct NzRec* nz_rec = nullptr;
+  const eid_t* unit_base = nullptr;  // ceil(rows / 4096) + 1 entries: row_off of each unit's first vertex
   // Top-down copy of col (same layout, neighbour-id order) with the
   // td_nhubs highest-degree vertices encoded as kHubFlag | index
   // (td_hub_vertex[index] = the vertex): a large top-down level tests them in
@@ -819,6 +832,10 @@ class Backend {
   virtual void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts) = 0;
   virtual void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, eid_t* nz_row_off,
                        vid_t* nz_head) = 0;
+  // Packed records of the view (ShardView::nz_rec) and the unit bases
+  // (ceil(rows / 4096) + 1 entries).
+  virtual void nz_records(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, NzRec* rec,
+                          eid_t* unit_base) = 0;
   // out[e] = kHubFlag | hub_idx[col[e]] for hub neighbours, else col[e].
   virtual void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) = 0;
   // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex

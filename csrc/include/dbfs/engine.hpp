@@ -88,6 +88,8 @@ class DeviceGraph {
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
   int64_t td_nhubs_ = 0;
   DBuf<eid_t> nz_pref_, nz_row_off_;
+  DBuf<NzRec> nz_rec_;      // packed view records (empty when a unit spans >= 2^32 edges)
+  DBuf<eid_t> unit_base_;
   void build_nz_view();
   DBuf<eid_t> row_off_;
   DBuf<vid_t> col_;
@@ -192,6 +194,9 @@ struct EngineOptions {
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.
   bool bu_fused_scan = true;
+  // Bottom-up rows from the packed 8-byte records (ShardView::nz_rec) instead
+  // of the view's 8-byte offsets + 4-byte heads.
+  bool bu_nz_rec = true;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a

@@ -1448,7 +1448,7 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
 // dependent loads) but queued in LDS (s_q, kQueue entries of row offset
 // relative to the unit's first row / length / position) and scanned kQueue at
 // a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in place.
-template <bool kPacked, bool kHub, int kWords = kWaveWords, int kQueue = 0>
+template <bool kPacked, bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false>
 __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int* own, word_t* s_res,
                                                 const word_t* s_hub, long long& cnt, long long& deg,
                                                 unsigned long long* s_q = nullptr) {
@@ -1473,6 +1473,22 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   const word_t* __restrict__ fr = a.frontier;
   const vid_t* __restrict__ head = a.g.head;
   const eid_t* __restrict__ nz_ro = (head && a.g.nz_pref && a.zdeg) ? a.g.nz_row_off : nullptr;
+  // packed records: the unit's base offset, span and end of its non-empty
+  // rows are wave-uniform (one unit per wave range)
+  // (kRec: the launcher checked that the view and its records exist)
+  const NzRec* __restrict__ nz_rec = kRec ? a.g.nz_rec : nullptr;
+  eid_t u_base = 0;
+  uint32_t u_span = 0;
+  int64_t u_nzend = 0;
+  if constexpr (kRec) {
+    // (readfirstlane: wave-uniform values in scalar registers)
+    const int64_t unit = w0 / kUnitWords;
+    const int64_t row_words = (a.g.rows + kWordBits - 1) / kWordBits;
+    u_base = static_cast<eid_t>(readlane64(static_cast<unsigned long long>(a.g.unit_base[unit]), 0));
+    u_span = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a.g.unit_base[unit + 1] - u_base)));
+    u_nzend = static_cast<int64_t>(readlane64(
+        static_cast<unsigned long long>(a.g.nz_pref[min((unit + 1) * kUnitWords, row_words)]), 0));
+  }
   // Unvisited vertex number 64 b + lane -> its position loc = 64 j + bit in the
   // wave's 1024 vertices (-1: no vertex), row bounds and head.
   // (row start, 32-bit length) keep the prefetched state small: the hub
@@ -1506,14 +1522,22 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     }
     if (idx < total) {
       loc = j * 64 + bit;
-      if (nz_ro) {
+      if (kRec || nz_ro) {
         // dense non-empty-row view: rank = non-empty rows before the word +
         // those below this bit (the word's prefix and zero-degree mask are
         // L1-resident: every lane of the wave reads one of <= 16 words)
         const int64_t k = a.g.nz_pref[w0 + j] + __popcll(~a.zdeg[w0 + j] & ((1ull << bit) - 1ull));
-        rs = nz_ro[k];
-        len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
-        if (!a.heads_done) u = a.g.nz_head[k];
+        if constexpr (kRec) {
+          const NzRec r = nz_rec[k];
+          const uint32_t end = k + 1 < u_nzend ? nz_rec[k + 1].off : u_span;
+          rs = u_base + r.off;
+          len = end - r.off;
+          if (!a.heads_done) u = r.head;
+        } else {
+          rs = nz_ro[k];
+          len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
+          if (!a.heads_done) u = a.g.nz_head[k];
+        }
       } else {
         const int64_t v = w0 * 64 + loc;
         rs = ro[v];
@@ -1538,7 +1562,10 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     // (the non-empty-row view covers ceil(rows / 64) words; a shard's bitmap
     // slice may be longer -- padding words, all visited)
     const int64_t wend = min(w0 + nw, (a.g.rows + kWordBits - 1) / kWordBits);
-    if (nz_ro) {
+    if constexpr (kRec) {
+      q_base = u_base;  // (every row of the unit starts at or after it; span < 2^32)
+      q_span_ok = true;
+    } else if (nz_ro) {
       q_base = nz_ro[a.g.nz_pref[w0]];
       q_span_ok = nz_ro[a.g.nz_pref[wend]] - q_base < (eid_t(1) << 32);
     } else {
@@ -1662,7 +1689,8 @@ static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
 
-template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads, int kQ = kBuQueue>
+template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads, int kQ = kBuQueue,
+          bool kRec = false>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   // per-wave scratch of the packed row scans (kPacked, or the queue flushes)
@@ -1677,7 +1705,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   for (int64_t i = threadIdx.x; i < hw; i += kThreads) s_hub[i] = a.hub_front[i];
   __syncthreads();
-  const int wave = threadIdx.x >> 6;
+  // (readfirstlane: the wave index, and the unit and word offsets derived
+  // from it, are wave-uniform -- scalar registers, not vector ones)
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if constexpr (kWhole) {
     // compacted: one whole 64-word unit per wave (its statistics need no
@@ -1694,8 +1724,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<kPacked, true, kUnitWords, kQueueLen>(a, u * kUnitWords, own, s_res + wave * kUnitWords, s_hub,
-                                                            cnt, deg, s_q + wave * kQueueLen);
+      bu_wave_compact<kPacked, true, kUnitWords, kQueueLen, kRec>(a, u * kUnitWords, own, s_res + wave * kUnitWords,
+                                                                  s_hub, cnt, deg, s_q + wave * kQueueLen);
       cnt = wave_sum(cnt);
       deg = wave_sum(deg);
       if (lane_id() == 0) {
@@ -2104,8 +2134,14 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     const int threads = whole ? (a.follow_up ? kFollowThreads : kFirstThreads) : kHubBuThreads;
     const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
-    if (whole && a.follow_up)
+    // packed row records (compile-time path: the view's fallback costs registers)
+    const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
+    if (whole && a.follow_up && rec)
+      bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue, true><<<grid, kFollowThreads, 0, st>>>(a);
+    else if (whole && a.follow_up)
       bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue><<<grid, kFollowThreads, 0, st>>>(a);
+    else if (whole && rec)
+      bu_hub_kernel<false, true, true, kFirstThreads, kBuQueue, true><<<grid, kFirstThreads, 0, st>>>(a);
     else if (whole)
       bu_hub_kernel<false, true, true, kFirstThreads><<<grid, kFirstThreads, 0, st>>>(a);
     if (whole) return;  // (the whole-unit kernels run a fused scan themselves)

@@ -239,6 +239,31 @@ __global__ __launch_bounds__(kBlock) void nz_fill_kernel(const eid_t* __restrict
   if (w == words - 1 && lane_id() == 0) nz_ro[pref[words]] = ro[rows];
 }
 
+// Packed records of the non-empty-row view: row k of unit U (vertices
+// [4096 U, 4096 U + 4096)) -> {row start - unit_base[U], head}.
+__global__ __launch_bounds__(kBlock) void nz_rec_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ head,
+                                                       int64_t rows, int64_t words, const eid_t* __restrict__ pref,
+                                                       NzRec* __restrict__ rec) {
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  if (w >= words) return;
+  const int64_t v = w * kWave + lane_id();
+  const bool nz = v < rows && ro[v + 1] > ro[v];
+  const unsigned long long m = __ballot(nz);
+  if (nz) {
+    const int64_t k = pref[w] + mask_rank(m);
+    NzRec r;
+    r.off = static_cast<uint32_t>(ro[v] - ro[(v / kUnitVertices) * kUnitVertices]);
+    r.head = head[v];
+    rec[k] = r;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void unit_base_kernel(const eid_t* __restrict__ ro, int64_t rows, int64_t nunits,
+                                                          eid_t* __restrict__ unit_base) {
+  const int64_t u = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (u <= nunits) unit_base[u] = ro[min(u * kUnitVertices, rows)];
+}
+
 // Hubs = vertices of degree >= min_deg, indexed in wave-ballot order (one
 // atomic per wave).
 // Hub selection in two passes so that every rank numbers the hubs alike (hub
@@ -292,6 +317,15 @@ void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t word
   if (words <= 0) return;
   nz_fill_kernel<<<static_cast<unsigned>((words + 3) / 4), kBlock, 0, st>>>(row_off, head, rows, words, nz_pref,
                                                                           nz_row_off, nz_head);
+}
+
+void nz_records(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t words, const eid_t* nz_pref,
+                NzRec* rec, eid_t* unit_base, hipStream_t st) {
+  if (rows <= 0) return;
+  const int64_t nunits = (rows + kUnitVertices - 1) / kUnitVertices;
+  unit_base_kernel<<<static_cast<unsigned>((nunits + 1 + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, rows, nunits,
+                                                                                                unit_base);
+  nz_rec_kernel<<<static_cast<unsigned>((words + 3) / 4), kBlock, 0, st>>>(row_off, head, rows, words, nz_pref, rec);
 }
 
 void hub_count(const uint32_t* deg, int64_t n, uint32_t min_deg, eid_t* cnt, hipStream_t st) {

@@ -105,6 +105,8 @@ void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head
                hipStream_t st);
 void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out, hipStream_t st);
 void nz_word_counts(const eid_t* row_off, int64_t rows, int64_t words, eid_t* counts, hipStream_t st);
+void nz_records(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t words, const eid_t* nz_pref,
+                NzRec* rec, eid_t* unit_base, hipStream_t st);
 void nz_fill(const eid_t* row_off, const vid_t* head, int64_t rows, int64_t words, const eid_t* nz_pref,
              eid_t* nz_row_off, vid_t* nz_head, hipStream_t st);
 // hub selection: cnt[w] = hubs among vertices [64 w, 64 w + 64) (ceil(n / 64)
