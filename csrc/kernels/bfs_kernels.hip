@@ -322,7 +322,8 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
@@ -538,7 +539,8 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
   stamp_level_start(a.ctrl);
   const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
@@ -647,10 +649,12 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
 // the grid is too small to fill the chip -- 4x the waves in flight to cover the
 // latency of the scattered loads/atomics.  The grid may be smaller than the
 // number of edge blocks (device loop: fixed grid): workgroups stride over them.
-template <TdOut kOut, int kThreads>
+// kFilter: the hub-filter variant (16 KiB more LDS: 4 instead of 6 resident
+// workgroups per CU -- launched only for levels that may use it).
+template <TdOut kOut, int kThreads, bool kFilter = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
-  constexpr bool kHubFilter = kOut != TdOut::Lists && kThreads == kTdThreads;
+  constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
@@ -1664,7 +1668,7 @@ __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   long long cnt = 0, deg = 0;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + wave * kWaveWords;
   int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
   if constexpr (kCompact)
@@ -1844,7 +1848,8 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (a.stamp) stamp_level_start(a.ctrl);
   const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + (threadIdx.x >> 6);
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if (unit >= nunits) return;
   const int64_t w0 = unit * kUnitWords;
@@ -2019,6 +2024,8 @@ void td_expand(const TdArgs& a, hipStream_t st) {
     if (a.grid <= 0) return;
     if (a.lists)
       td_expand_kernel<TdOut::Lists, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+    else if (a.td_hub_vis)
+      td_expand_kernel<TdOut::Dyn, kTdThreads, true><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
     else
       td_expand_kernel<TdOut::Dyn, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
     return;
