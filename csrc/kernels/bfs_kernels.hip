@@ -1776,9 +1776,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     if (u < nunits) {
       int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
       if constexpr (kCompact)
-        bu_wave_compact<kPacked, true, kWaveWords, kQueueLen>(a, u * kUnitWords + wg * kWaveWords, own,
-                                                              s_res + wave * kWaveWords, s_hub, cnt, deg,
-                                                              s_q + wave * kQueueLen);
+        bu_wave_compact<kPacked, true, kWaveWords, kQueueLen, kRec>(a, u * kUnitWords + wg * kWaveWords, own,
+                                                                    s_res + wave * kWaveWords, s_hub, cnt, deg,
+                                                                    s_q + wave * kQueueLen);
       else
         bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_hub, cnt, deg);
     }
@@ -2154,8 +2154,12 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     if (whole) return;  // (the whole-unit kernels run a fused scan themselves)
     else if (a.packed)
       a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
-    else if (a.compact && a.follow_up)  // scan-heavy later level: no deferral (measured)
+    else if (a.compact && a.follow_up && rec)  // scan-heavy later level: no deferral (measured)
+      bu_hub_kernel<false, true, false, kHubBuThreads, 0, true><<<grid, kHubBuThreads, 0, st>>>(a);
+    else if (a.compact && a.follow_up)
       bu_hub_kernel<false, true, false, kHubBuThreads, 0><<<grid, kHubBuThreads, 0, st>>>(a);
+    else if (a.compact && rec)
+      bu_hub_kernel<false, true, false, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
     else
       a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);
 #undef DBFS_BU_HUB
