@@ -74,8 +74,11 @@ class CpuBackend final : public Backend {
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
         if (use_bytes && a.level_direct) {
-          for (int b = 0; b < 64; ++b)
-            if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.new_level)) c |= 1ull << b;
+          if (!a.dirty || a.dirty[w]) {
+            for (int b = 0; b < 64; ++b)
+              if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.new_level)) c |= 1ull << b;
+            if (a.dirty) a.dirty[w] = 0;
+          }
         } else if (use_bytes) {
           c = gather_bytes(a.cand_bytes + w * 64);
         } else {
@@ -256,6 +259,7 @@ class CpuBackend final : public Backend {
           list[1 + list[0]++] = v;
         } else if (bytes && a.level_direct) {
           a.level_direct[v] = static_cast<uint8_t>(a.new_level);
+          if (a.dirty) a.dirty[v >> 6] = 1;
         } else if (bytes) {
           a.next_bytes[v] = 1;
         } else {

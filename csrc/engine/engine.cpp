@@ -74,6 +74,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "level_prefill") o.level_prefill = v != 0;
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
+  else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -112,6 +113,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"level_prefill", o.level_prefill ? 1.0 : 0.0},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
+          {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -709,6 +711,7 @@ void Engine::begin_run_scratch() {
     be_.memset_async(cand_.data(), 0, cand_.bytes());
     be_.memset_async(next_.data(), 0, next_.bytes());
     if (next_bytes_.data()) be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
+    if (td_dirty_.data()) be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
   }
   scratch_dirty_ = true;  // until the run completes
 }
@@ -1561,6 +1564,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           ta.level_direct = level8_.data();
           ta.new_level = L + 1;
           tu.level_direct = level8_.data();
+          // a level predicted to touch few words: the update gathers only
+          // the words td_expand marked
+          if (opt_.td_dirty_words && mf_hint >= 0 && mf_hint * 8.0 < static_cast<double>(W * kWordBits)) {
+            if (!td_dirty_.data()) {
+              td_dirty_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(W, 1)));
+              be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
+            }
+            ta.dirty = td_dirty_.data();
+            tu.dirty = td_dirty_.data();
+          }
         }
         be_.td_expand(ta);
         tu.cand = next_.data();

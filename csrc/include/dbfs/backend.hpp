@@ -257,6 +257,9 @@ struct UpdateArgs {
   // unvisited vertices whose level already reads new_level (level8, padded to
   // whole words); cand_bytes is not read.
   const uint8_t* level_direct = nullptr;
+  // Optional with level_direct (TdArgs::dirty): only words whose byte is set
+  // are gathered; the bytes are cleared as read.
+  uint8_t* dirty = nullptr;
 };
 
 // Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
@@ -460,6 +463,10 @@ struct TdArgs {
   // clear afterwards.
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
+  // Optional with level_direct: byte w set for every bitmap word w that got a
+  // level byte (a small level's update then gathers only those words
+  // instead of every level byte).
+  uint8_t* dirty = nullptr;
   // Levels of at least td_hub_min_edges frontier edges read g.td_col and test
   // hub targets in an LDS copy of td_hub_vis (visited bits of the top-down
   // hubs, this level's snapshot: hub_visited); not with owner lists.

@@ -197,6 +197,11 @@ struct EngineOptions {
   // Bottom-up rows from the packed 8-byte records (ShardView::nz_rec) instead
   // of the view's 8-byte offsets + 4-byte heads.
   bool bu_nz_rec = true;
+  // Direct-level top-down levels predicted at < N/8 frontier edges mark the
+  // bitmap words they store level bytes into; the update gathers only those.
+  // Off: the level-1 update gains ~2 us, the traversal loses ~1 % (1330 against
+  // 1343-1348 GTEPS on RMAT-26, alternating runs).
+  bool td_dirty_words = false;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a
@@ -330,7 +335,8 @@ class Engine {
   // one rank: the next run's level bytes, filled with kNarrowUnreached on the
   // side stream under the current run (EngineOptions::level_prefill)
   DBuf<uint8_t> level8_next_;
-  DBuf<int64_t> bu_tot_;  // fused bottom-up finish: the level's totals (BuArgs::tot)
+  DBuf<int64_t> bu_tot_;
+  DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)  // fused bottom-up finish: the level's totals (BuArgs::tot)
   bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
   bool level8_filled_ = false;        // level8_ was prefilled for the current run
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels

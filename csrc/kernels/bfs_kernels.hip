@@ -332,7 +332,12 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   if (wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
-      c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+      if (!a.dirty) {
+        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+      } else if (a.dirty[wl]) {
+        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+        a.dirty[wl] = 0;
+      }
     } else if (use_bytes) {
       c = gather_byte_bits(a.cand_bytes + wl * 64);
     } else {
@@ -757,7 +762,10 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
           keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-          if (keep[k]) a.level_direct[vk[k]] = lv;
+          if (keep[k]) {
+            a.level_direct[vk[k]] = lv;
+            if (a.dirty) a.dirty[vk[k] >> 6] = 1;
+          }
         continue;
       }
       // byte map: with few visited vertices the check costs more than the
