@@ -523,3 +523,16 @@ def test_level_prefill_cpu(rt, mode):
     for src in bfs.sample_roots(4, seed=3):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_td_dirty_words_cpu(rt, mode):
+    # dirty-word marking of small direct top-down levels: exact
+    p = dbfs.rmat_params(12, 16, 61)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    bfs.engine.set_option("td_dirty_words", 1)
+    bfs.engine.set_option("td_direct_edges", 0)
+    for src in bfs.sample_roots(3, seed=5):
+        bfs.run(src)
+        assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])

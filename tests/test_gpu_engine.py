@@ -734,3 +734,16 @@ def test_level_prefill_gpu(gpu_runtime, mode):
     cb.engine.set_option("level_prefill", 1)
     _check(cb, chain, 0)
     _check(cb, chain, 5)
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_td_dirty_words_gpu(gpu_runtime, mode):
+    """td_dirty_words: small direct top-down levels mark the words they store
+    into and the update gathers only those; exact against the oracle."""
+    p = dbfs.rmat_params(17, 16, 61)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    bfs.engine.set_option("td_dirty_words", 1)
+    bfs.engine.set_option("td_direct_edges", 0)
+    for src in bfs.sample_roots(3, seed=5):
+        _check(bfs, csr, src)
