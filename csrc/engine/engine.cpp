@@ -71,7 +71,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
-  else if (name == "level_prefill") o.level_prefill = v != 0;
+  else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
@@ -110,7 +110,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
-          {"level_prefill", o.level_prefill ? 1.0 : 0.0},
+          {"level_prefill", static_cast<double>(o.level_prefill)},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
@@ -648,19 +648,29 @@ RunResult Engine::run(int64_t source) {
   const size_t l8_bytes = static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1));
   if (run_narrow_ && level8_.size() == 0) level8_ = DBuf<uint8_t>(be_, l8_bytes);
   level8_filled_ = false;
-  if (run_narrow_ && opt_.level_prefill && comm_.size() == 1) {
-    // the buffer filled under the previous run becomes this run's; the
-    // previous run's levels are overwritten by the fill for the next one
+  const bool prefill = run_narrow_ && opt_.level_prefill > 0 && comm_.size() == 1;
+  if (prefill) {
+    // the buffer filled under / after the previous run becomes this run's;
+    // the previous run's levels are overwritten by the fill for the next one
     if (level8_next_ready_) {
       std::swap(level8_, level8_next_);
-      be_.prefill_wait();
+      if (opt_.level_prefill == 1) be_.prefill_wait();
       level8_filled_ = true;
+      level8_next_ready_ = false;
     }
     if (level8_next_.size() == 0) level8_next_ = DBuf<uint8_t>(be_, l8_bytes);
-    be_.prefill_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
-    level8_next_ready_ = true;
+    if (opt_.level_prefill == 1) {
+      be_.prefill_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
+      level8_next_ready_ = true;
+    }
   }
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
+  if (prefill && opt_.level_prefill == 2) {
+    // behind the traversal on its stream: runs while the host returns the
+    // result and sets up the next traversal
+    be_.memset_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
+    level8_next_ready_ = true;
+  }
   check_device();
   levels_narrow_ = run_narrow_;
   if (run_narrow_ && r.depth - 1 > kNarrowMaxLevel) {

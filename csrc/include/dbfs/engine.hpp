@@ -184,12 +184,13 @@ struct EngineOptions {
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;
   // One rank, narrow levels: the level bytes are double-buffered and the next
-  // run's buffer is filled on the side stream while this run traverses (its
-  // first levels are latency-bound), instead of by the run's init kernel.
-  // Off: measured slower on RMAT-26 (1219 / 1192 against 1238 / 1261 GTEPS,
-  // alternating runs): the cross-stream fill and event waits cost more than
-  // the 64 MiB fill (~13 us) they take off the critical path.
-  bool level_prefill = false;
+  // run's buffer is filled ahead instead of by the run's init kernel -- 1: on
+  // the side stream while this run traverses (measured slower on RMAT-26:
+  // 1219 / 1192 against 1238 / 1261 GTEPS, the cross-stream fill and event
+  // waits cost more than the 64 MiB fill they take off the critical path);
+  // 2: on the stream right behind this run (overlapping the host's return
+  // and the next run's setup); 0: off.
+  int level_prefill = 0;
   // One rank, device loop: a bottom-up level's unit scan (totals, direction
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.

@@ -512,14 +512,15 @@ def test_td_direct_levels_cpu(rt, mode, direct_edges):
     assert np.array_equal(cb.levels(), np.arange(n))
 
 
+@pytest.mark.parametrize("prefill", [1, 2])
 @pytest.mark.parametrize("mode", ["do", "td", "bu"])
-def test_level_prefill_cpu(rt, mode):
+def test_level_prefill_cpu(rt, mode, prefill):
     # double-buffered level bytes (the next run's buffer prefilled): exact
     # over consecutive runs
     p = dbfs.rmat_params(11, 16, 9)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, rt, mode=mode)
-    bfs.engine.set_option("level_prefill", 1)
+    bfs.engine.set_option("level_prefill", prefill)
     for src in bfs.sample_roots(4, seed=3):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])

@@ -717,21 +717,22 @@ def test_bottom_up_long_row_scanned_in_place_gpu(gpu_runtime):
         _check(bfs, csr, 0)
 
 
+@pytest.mark.parametrize("prefill", [1, 2])
 @pytest.mark.parametrize("mode", ["do", "td", "bu"])
-def test_level_prefill_gpu(gpu_runtime, mode):
+def test_level_prefill_gpu(gpu_runtime, mode, prefill):
     """level_prefill: the next run's level bytes filled on the side stream
     under the current run (double buffer); consecutive runs stay exact, also
     across a deep chain that falls back to 32-bit levels."""
     p = dbfs.rmat_params(16, 16, 53)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
-    bfs.engine.set_option("level_prefill", 1)
+    bfs.engine.set_option("level_prefill", prefill)
     for src in bfs.sample_roots(4, seed=7):
         _check(bfs, csr, src)
     n = 400
     chain = dbfs.build_csr(n, np.arange(n - 1, dtype=np.uint32), np.arange(1, n, dtype=np.uint32))
     cb = dbfs.BFS(chain, gpu_runtime, mode="td" if mode == "bu" else mode)
-    cb.engine.set_option("level_prefill", 1)
+    cb.engine.set_option("level_prefill", prefill)
     _check(cb, chain, 0)
     _check(cb, chain, 5)
 
