@@ -63,6 +63,18 @@ class CpuBackend final : public Backend {
   void set_bit(word_t* bm, int64_t bit) override { bm[bit >> 6] |= 1ull << (bit & 63); }
 
   void update_frontier(const UpdateArgs& a) override {
+    if (a.fuse_scan) {
+      // totals and finish right after the update, unit statistics unscanned
+      UpdateArgs b = a;
+      b.fuse_scan = false;
+      update_frontier(b);
+      const int64_t n = a.scan.nunits;
+      std::vector<int64_t> c(a.scan.unit_cnt, a.scan.unit_cnt + n), d(a.scan.unit_deg, a.scan.unit_deg + n);
+      scan_units(a.scan);
+      std::copy(c.begin(), c.end(), a.scan.unit_cnt);
+      std::copy(d.begin(), d.end(), a.scan.unit_deg);
+      return;
+    }
     bool use_bytes = a.cand_bytes != nullptr;
     if (a.ctrl) {
       if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;

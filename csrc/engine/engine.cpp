@@ -75,6 +75,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
+  else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
@@ -114,6 +115,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
+          {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
@@ -1401,8 +1403,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
     // writes into it)
     auto compact = [&](word_t* clear_all) {
-      if (pf == 'B' && enq_fused[static_cast<size_t>(L - 1)]) {
-        // the bottom-up level only finished its totals: its unit prefixes
+      if (L > 0 && enq_fused[static_cast<size_t>(L - 1)]) {
+        // the previous level only finished its totals: its unit prefixes
         // now (no finish; a no-op unless this chain is live)
         ScanArgs sa = scan_args(L - 1, false, 'T', d == 'S' ? sparse_cap : 0);
         sa.finish = false;
@@ -1609,6 +1611,17 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.frontier = fr_own(cur ^ 1);
       tu.new_level = L + 1;
       tu.ctrl = ctrl_.data();
+      if (!xc && opt_.td_fused_finish) {
+        // totals and finish in the update's last workgroup (as bottom-up)
+        if (!bu_tot_.data()) {
+          bu_tot_ = DBuf<int64_t>(be_, 2);
+          be_.memset_async(bu_tot_.data(), 0, bu_tot_.bytes());
+        }
+        tu.fuse_scan = true;
+        tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
+        tu.tot = bu_tot_.data();
+        fused_scan = true;
+      }
       be_.update_frontier(tu);
     } else {
       BuArgs ba;

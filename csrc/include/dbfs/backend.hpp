@@ -226,6 +226,39 @@ struct InitRunArgs {
   LevelMailbox* mailbox = nullptr;
 };
 
+// Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
+// kScanChunk units) plus chunk prefixes (part_cnt / part_deg, exclusive).  The
+// last workgroup to finish (ticket, agent-scope release/acquire) scans the
+// chunk totals and writes stats[0..1] = stats[2..3] = (count, degree sum) and
+// the work-list end sentinel qscan[count] = degree sum.
+struct ScanArgs {
+  int64_t* unit_cnt = nullptr;
+  int64_t* unit_deg = nullptr;
+  int64_t nunits = 0;
+  int64_t* part_cnt = nullptr;   // ceil(nunits / kScanChunk)
+  int64_t* part_deg = nullptr;
+  unsigned* ticket = nullptr;    // zero before the first launch; reset by the last block
+  int64_t* stats = nullptr;
+  int64_t* qscan = nullptr;
+  // device-driven loop: skip everything when ctrl->done at entry; the last
+  // workgroup runs level_ctrl_finish and fills rec / the mailbox slot
+  LevelCtrl* ctrl = nullptr;
+  LevelRecDev* rec = nullptr;       // this level's record
+  LevelMailbox* mailbox = nullptr;  // device-mapped pinned slot
+  int32_t level = 0;
+  bool seed = false;
+  // Device loop: the level's chain was enqueued for this direction (0: any);
+  // when ctrl->dir differs, the chain was a no-op and so is the scan.
+  int32_t expect_dir = 0;
+  // ... and, for a multi-rank list-form top-down chain, only valid while the
+  // level's global frontier edges fit its lists (ctrl->m_f <= expect_cap;
+  // 0: no bound).
+  int64_t expect_cap = 0;
+  // Device loop: run level_ctrl_finish here (one rank); several ranks reduce
+  // the totals first and finish in level_finish.
+  bool finish = true;
+};
+
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -260,40 +293,14 @@ struct UpdateArgs {
   // Optional with level_direct (TdArgs::dirty): only words whose byte is set
   // are gathered; the bytes are cleared as read.
   uint8_t* dirty = nullptr;
+  // One rank, device loop (as BuArgs::fuse_scan): totals and finish in the
+  // last-arriving workgroup, unit statistics left unscanned (a following
+  // compaction scans them first); tot[0..1] zero, reset by the last one.
+  bool fuse_scan = false;
+  ScanArgs scan;
+  int64_t* tot = nullptr;
 };
 
-// Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of
-// kScanChunk units) plus chunk prefixes (part_cnt / part_deg, exclusive).  The
-// last workgroup to finish (ticket, agent-scope release/acquire) scans the
-// chunk totals and writes stats[0..1] = stats[2..3] = (count, degree sum) and
-// the work-list end sentinel qscan[count] = degree sum.
-struct ScanArgs {
-  int64_t* unit_cnt = nullptr;
-  int64_t* unit_deg = nullptr;
-  int64_t nunits = 0;
-  int64_t* part_cnt = nullptr;   // ceil(nunits / kScanChunk)
-  int64_t* part_deg = nullptr;
-  unsigned* ticket = nullptr;    // zero before the first launch; reset by the last block
-  int64_t* stats = nullptr;
-  int64_t* qscan = nullptr;
-  // device-driven loop: skip everything when ctrl->done at entry; the last
-  // workgroup runs level_ctrl_finish and fills rec / the mailbox slot
-  LevelCtrl* ctrl = nullptr;
-  LevelRecDev* rec = nullptr;       // this level's record
-  LevelMailbox* mailbox = nullptr;  // device-mapped pinned slot
-  int32_t level = 0;
-  bool seed = false;
-  // Device loop: the level's chain was enqueued for this direction (0: any);
-  // when ctrl->dir differs, the chain was a no-op and so is the scan.
-  int32_t expect_dir = 0;
-  // ... and, for a multi-rank list-form top-down chain, only valid while the
-  // level's global frontier edges fit its lists (ctrl->m_f <= expect_cap;
-  // 0: no bound).
-  int64_t expect_cap = 0;
-  // Device loop: run level_ctrl_finish here (one rank); several ranks reduce
-  // the totals first and finish in level_finish.
-  bool finish = true;
-};
 
 // Device loop, several ranks: after the totals' all-reduce (stats[2..3] =
 // global count / degree sum), one thread runs level_ctrl_finish (seed: from

@@ -203,6 +203,11 @@ struct EngineOptions {
   // Off: the level-1 update gains ~2 us, the traversal loses ~1 % (1330 against
   // 1343-1348 GTEPS on RMAT-26, alternating runs).
   bool td_dirty_words = false;
+  // One rank, device loop: a dense top-down level's update finishes the
+  // level itself (as bu_fused_scan): no scan launch unless a compaction follows.
+  // Off: the update's ~4K workgroups' totals / ticket atomics on three
+  // addresses serialise (level 1 of RMAT-26 38 -> 117 us).
+  bool td_fused_finish = false;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a

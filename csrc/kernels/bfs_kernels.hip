@@ -336,6 +336,27 @@ __device__ __forceinline__ word_t gather_level_bits(const uint8_t* p, uint8_t lv
   return bits;
 }
 
+// The level's totals (count, degree sum of the new frontier) -> stats, the
+// work list's end marker, the ticket reset and (device loop) the direction
+// decision, level record and mailbox stamp.  One thread.
+__device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c, long long carry_d) {
+  DBFS_DCHECK(carry_c <= a.nunits * kUnitVertices, 7, carry_c);
+  a.stats[0] = a.stats[2] = carry_c;
+  a.stats[1] = a.stats[3] = carry_d;
+  a.qscan[carry_c] = carry_d;
+  *a.ticket = 0u;  // next launch is stream-ordered after this one
+  if (a.ctrl && a.finish) {
+    LevelCtrl c = *a.ctrl;
+    level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
+    if (!a.seed) {
+      a.rec->t0 = c.t_start;
+      a.rec->t1 = wall_clock64();
+    }
+    *a.ctrl = c;
+    if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
@@ -343,14 +364,16 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
-                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-  if (unit >= nunits) return;
+  // (with the fused finish every wave reaches the barrier below)
+  if (unit >= nunits && !a.fuse_scan) return;
+  const bool have = unit < nunits;
   const int64_t w0 = unit * kUnitWords;
   const int64_t wl = w0 + lane;
   word_t nb = 0;
-  if (wl < a.words) {
+  if (have && wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
       if (!a.dirty) {
@@ -390,36 +413,48 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
       }
     }
   }
-  wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
-}
-
-// ---------------------------------------------------------------------------
-// Multi-block scan.  Workgroup b scans units [b*CH, (b+1)*CH) in place
-// (exclusive, in-chunk) and publishes its chunk total; the last workgroup to
-// arrive scans the chunk totals.  Hand-off: chunk totals stored by thread 0,
-// `s_waitcnt vmcnt(0)`, agent release fence, `s_waitcnt vmcnt(0)` (compiler
-// hazard, MI355X_MICROARCH), then the ticket atomic; the last arriver runs an
-// agent acquire fence before any thread reads the totals.
-// The level's totals (count, degree sum of the new frontier) -> stats, the
-// work list's end marker, the ticket reset and (device loop) the direction
-// decision, level record and mailbox stamp.  One thread.
-__device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c, long long carry_d) {
-  DBFS_DCHECK(carry_c <= a.nunits * kUnitVertices, 7, carry_c);
-  a.stats[0] = a.stats[2] = carry_c;
-  a.stats[1] = a.stats[3] = carry_d;
-  a.qscan[carry_c] = carry_d;
-  *a.ticket = 0u;  // next launch is stream-ordered after this one
-  if (a.ctrl && a.finish) {
-    LevelCtrl c = *a.ctrl;
-    level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
-    if (!a.seed) {
-      a.rec->t0 = c.t_start;
-      a.rec->t1 = wall_clock64();
+  if (!a.fuse_scan) {
+    wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
+    return;
+  }
+  // fused finish (as the whole-unit bottom-up kernel's): raw unit statistics,
+  // the workgroup's totals into tot, a ticket; the last workgroup finishes
+  __shared__ long long s_c[kUnitsPerBlock], s_d[kUnitsPerBlock];
+  cnt = wave_sum(cnt);
+  deg = wave_sum(deg);
+  if (lane == 0) {
+    if (have) {
+      a.unit_cnt[unit] = cnt;
+      a.unit_deg[unit] = deg;
     }
-    *a.ctrl = c;
-    if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
+    s_c[wv] = cnt;
+    s_d[wv] = deg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long c = 0, d = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitsPerBlock; ++k) {
+      c += s_c[k];
+      d += s_d[k];
+    }
+    if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot), static_cast<unsigned long long>(c));
+    if (d) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot + 1), static_cast<unsigned long long>(d));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+    if (prev == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const long long tc = static_cast<long long>(
+          __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const long long td = static_cast<long long>(
+          __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      a.tot[0] = 0;
+      a.tot[1] = 0;
+      scan_finish(a.scan, tc, td);
+    }
   }
 }
+
 
 // Totals and finish of a level whose unit statistics stay unscanned (the
 // fused bottom-up finish of kernels without the epilogue): one workgroup
@@ -449,6 +484,13 @@ __global__ __launch_bounds__(kScanChunk) void totals_finish_kernel(ScanArgs a) {
   scan_finish(a, tc, td);
 }
 
+// ---------------------------------------------------------------------------
+// Multi-block scan.  Workgroup b scans units [b*CH, (b+1)*CH) in place
+// (exclusive, in-chunk) and publishes its chunk total; the last workgroup to
+// arrive scans the chunk totals.  Hand-off: chunk totals stored by thread 0,
+// `s_waitcnt vmcnt(0)`, agent release fence, `s_waitcnt vmcnt(0)` (compiler
+// hazard, MI355X_MICROARCH), then the ticket atomic; the last arriver runs an
+// agent acquire fence before any thread reads the totals.
 __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;

@@ -537,3 +537,16 @@ def test_td_dirty_words_cpu(rt, mode):
     for src in bfs.sample_roots(3, seed=5):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_td_fused_finish_cpu(rt, mode):
+    # dense top-down levels finished in the update (unit prefixes deferred to
+    # the next compaction): exact
+    p = dbfs.rmat_params(12, 16, 67)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode=mode)
+    bfs.engine.set_option("td_fused_finish", 1)
+    for src in bfs.sample_roots(3, seed=9):
+        bfs.run(src)
+        assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])

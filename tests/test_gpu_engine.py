@@ -748,3 +748,15 @@ def test_td_dirty_words_gpu(gpu_runtime, mode):
     bfs.engine.set_option("td_direct_edges", 0)
     for src in bfs.sample_roots(3, seed=5):
         _check(bfs, csr, src)
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_td_fused_finish_gpu(gpu_runtime, mode):
+    """td_fused_finish: the update's last workgroup finishes dense top-down
+    levels; exact against the oracle."""
+    p = dbfs.rmat_params(17, 16, 67)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    bfs.engine.set_option("td_fused_finish", 1)
+    for src in bfs.sample_roots(3, seed=9):
+        _check(bfs, csr, src)
