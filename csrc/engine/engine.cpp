@@ -1613,13 +1613,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.ctrl = ctrl_.data();
       if (!xc && opt_.td_fused_finish) {
         // totals and finish in the update's last workgroup (as bottom-up)
-        if (!bu_tot_.data()) {
-          bu_tot_ = DBuf<int64_t>(be_, 2);
-          be_.memset_async(bu_tot_.data(), 0, bu_tot_.bytes());
+        if (!td_tot_.data()) {
+          td_tot_ = DBuf<int64_t>(be_, 2);
+          be_.memset_async(td_tot_.data(), 0, td_tot_.bytes());
         }
         tu.fuse_scan = true;
         tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
-        tu.tot = bu_tot_.data();
+        tu.tot = td_tot_.data();
         fused_scan = true;
       }
       be_.update_frontier(tu);
@@ -1715,10 +1715,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         if (!xc && opt_.bu_fused_scan && !ba.merge) {
           // the level's totals and finish in the bottom-up kernel's last
           // workgroup; the unit prefixes only if a top-down chain follows
-          if (!bu_tot_.data()) {
-            bu_tot_ = DBuf<int64_t>(be_, 2);
-            be_.memset_async(bu_tot_.data(), 0, bu_tot_.bytes());
-          }
+          if (!bu_tot_.data()) bu_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
           ba.fuse_scan = true;
           ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
           ba.tot = bu_tot_.data();

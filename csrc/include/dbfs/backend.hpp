@@ -529,6 +529,9 @@ struct PackArgs {
 // Bottom-up step fused with the frontier update: for every owned unvisited v,
 // if some neighbour u has frontier[u], v joins the new frontier: visited[v],
 // new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
+// Slots of BuArgs::tot (one pair per workgroup of a fused bottom-up finish).
+constexpr int kMaxFusedGrid = 4096;
+
 struct BuArgs {
   ShardView g;
   // Zero-degree / padding bits of the owned slice (needed with g.nz_pref).
@@ -560,8 +563,8 @@ struct BuArgs {
   bool heads_done = false;
   // One rank, device loop: the level's totals and finish (ScanArgs: stats,
   // direction decision, record, mailbox) run in the bottom-up kernel's
-  // last-arriving workgroup instead of a scan launch: workgroups add their
-  // totals into tot[0..1] (zero; reset by the last one).  The per-unit
+  // last-arriving workgroup instead of a scan launch: workgroup g stores its
+  // totals in tot[2g], tot[2g + 1] (kMaxFusedGrid slots).  The per-unit
   // prefixes are left to a scan_units (finish off) in the next chain, only
   // when it compacts the frontier (a top-down level).  Kernels without the
   // epilogue launch scan_units after themselves.

@@ -341,8 +341,9 @@ class Engine {
   // one rank: the next run's level bytes, filled with kNarrowUnreached on the
   // side stream under the current run (EngineOptions::level_prefill)
   DBuf<uint8_t> level8_next_;
-  DBuf<int64_t> bu_tot_;
-  DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)  // fused bottom-up finish: the level's totals (BuArgs::tot)
+  DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
+  DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
+  DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)
   bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
   bool level8_filled_ = false;        // level8_ was prefilled for the current run
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels

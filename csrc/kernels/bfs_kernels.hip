@@ -1844,8 +1844,10 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       }
     }
     if (!a.fuse_scan) return;
-    // fused finish: the workgroup's totals into tot (device atomics, one
-    // pair per workgroup), a ticket; the last workgroup finishes the level
+    // fused finish: the workgroup's totals into its own slot of tot
+    // (agent-scope stores: no same-address atomics but the ticket's), a
+    // ticket; the last workgroup sums the slots and finishes the level
+    __shared__ int s_last;
     __syncthreads();
     if (threadIdx.x == 0) {
       long long c = 0, d = 0;
@@ -1853,20 +1855,39 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
         c += s_c[k];
         d += s_d[k];
       }
-      if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot), static_cast<unsigned long long>(c));
-      if (d) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot + 1), static_cast<unsigned long long>(d));
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x), static_cast<unsigned long long>(c),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
+                         static_cast<unsigned long long>(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned prev = atomicAdd(a.scan.ticket, 1u);
-      if (prev == gridDim.x - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const long long tc = static_cast<long long>(
-            __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        const long long td = static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 1),
-                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        a.tot[0] = 0;
-        a.tot[1] = 0;
-        scan_finish(a.scan, tc, td);  // (resets the ticket)
+      s_last = prev == gridDim.x - 1;
+      if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!s_last) return;
+    long long c = 0, d = 0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
+      c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i + 1),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    c = wave_sum(c);
+    d = wave_sum(d);
+    __syncthreads();  // (s_c / s_d reused)
+    if (lane_id() == 0) {
+      s_c[wave] = c;
+      s_d[wave] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long tc = 0, td = 0;
+      for (int k = 0; k < kWavesPerBlock; ++k) {
+        tc += s_c[k];
+        td += s_d[k];
       }
+      scan_finish(a.scan, tc, td);  // (resets the ticket)
     }
     return;
   }
@@ -2247,6 +2268,14 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
+    if (whole && a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
+      // (more workgroups than totals slots: finish in a kernel of its own)
+      BuArgs b = a;
+      b.fuse_scan = false;
+      bu_step(b, st);
+      totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
+      return;
+    }
     if (whole && a.follow_up && rec)
       bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue, true><<<grid, kFollowThreads, 0, st>>>(a);
     else if (whole && a.follow_up)
