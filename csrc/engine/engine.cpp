@@ -1613,10 +1613,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.ctrl = ctrl_.data();
       if (!xc && opt_.td_fused_finish) {
         // totals and finish in the update's last workgroup (as bottom-up)
-        if (!td_tot_.data()) {
-          td_tot_ = DBuf<int64_t>(be_, 2);
-          be_.memset_async(td_tot_.data(), 0, td_tot_.bytes());
-        }
+        if (!td_tot_.data()) td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
         tu.fuse_scan = true;
         tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
         tu.tot = td_tot_.data();

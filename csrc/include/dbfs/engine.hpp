@@ -204,10 +204,12 @@ struct EngineOptions {
   // 1343-1348 GTEPS on RMAT-26, alternating runs).
   bool td_dirty_words = false;
   // One rank, device loop: a dense top-down level's update finishes the
-  // level itself (as bu_fused_scan): no scan launch unless a compaction follows.
-  // Off: the update's ~4K workgroups' totals / ticket atomics on three
-  // addresses serialise (level 1 of RMAT-26 38 -> 117 us).
-  bool td_fused_finish = false;
+  // level itself (as bu_fused_scan; 512 workgroups striding over the units,
+  // per-workgroup totals slots): no scan launch unless a compaction follows.
+  // RMAT-26 1344 / 1341 -> 1363 / 1353 GTEPS; top-down only equal within noise.
+  // (A first version with one workgroup per 4 units and totals atomics on
+  // one address: level 1 of RMAT-26 38 -> 117 us.)
+  bool td_fused_finish = true;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a

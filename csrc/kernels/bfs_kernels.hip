@@ -357,23 +357,15 @@ __device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c
   }
 }
 
-__global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
-  bool use_bytes = a.cand_bytes != nullptr;
-  if (a.ctrl) {
-    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-    use_bytes = use_bytes && a.ctrl->bytes != 0;
-  }
+// One wave per 64-word unit, kUnitsPerBlock units per workgroup; with the
+// fused finish a smaller grid strides over the units (fewer ticket arrivals).
+__device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, bool use_bytes, long long& cnt,
+                                            long long& deg) {
   const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;  // (wave-uniform)
-  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-  // (with the fused finish every wave reaches the barrier below)
-  if (unit >= nunits && !a.fuse_scan) return;
-  const bool have = unit < nunits;
   const int64_t w0 = unit * kUnitWords;
   const int64_t wl = w0 + lane;
   word_t nb = 0;
-  if (have && wl < a.words) {
+  if (wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
       if (!a.dirty) {
@@ -396,7 +388,8 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   // New vertices of the unit, 64 per step (one per lane, whatever word they
   // sit in): a sparse level has about one new vertex per word, and one word
   // per step would cost a dependent row_off round trip per new vertex.
-  long long cnt = 0, deg = 0;
+  cnt = 0;
+  deg = 0;
   const int incl = static_cast<int>(wave_incl_scan(__popcll(nb)));
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   const eid_t* __restrict__ ro = a.g.row_off;
@@ -413,22 +406,45 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
       }
     }
   }
-  if (!a.fuse_scan) {
-    wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
-    return;
-  }
-  // fused finish (as the whole-unit bottom-up kernel's): raw unit statistics,
-  // the workgroup's totals into tot, a ticket; the last workgroup finishes
-  __shared__ long long s_c[kUnitsPerBlock], s_d[kUnitsPerBlock];
   cnt = wave_sum(cnt);
   deg = wave_sum(deg);
   if (lane == 0) {
-    if (have) {
-      a.unit_cnt[unit] = cnt;
-      a.unit_deg[unit] = deg;
-    }
-    s_c[wv] = cnt;
-    s_d[wv] = deg;
+    a.unit_cnt[unit] = cnt;
+    a.unit_deg[unit] = deg;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
+  bool use_bytes = a.cand_bytes != nullptr;
+  if (a.ctrl) {
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    use_bytes = use_bytes && a.ctrl->bytes != 0;
+  }
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if (!a.fuse_scan) {
+    const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;
+    if (unit >= nunits) return;
+    long long cnt, deg;
+    update_unit(a, unit, use_bytes, cnt, deg);
+    return;
+  }
+  // fused finish (as the whole-unit bottom-up kernel's): raw unit statistics,
+  // the workgroup's totals in its slot of tot, a ticket; the last workgroup
+  // sums the slots and finishes the level
+  __shared__ long long s_c[kUnitsPerBlock], s_d[kUnitsPerBlock];
+  __shared__ int s_last;
+  long long wc = 0, wd = 0;
+  for (int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; unit < nunits;
+       unit += static_cast<int64_t>(gridDim.x) * kUnitsPerBlock) {
+    long long cnt, deg;
+    update_unit(a, unit, use_bytes, cnt, deg);
+    wc += cnt;
+    wd += deg;
+  }
+  if (lane_id() == 0) {
+    s_c[wv] = wc;
+    s_d[wv] = wd;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -438,20 +454,40 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
       c += s_c[k];
       d += s_d[k];
     }
-    if (c) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot), static_cast<unsigned long long>(c));
-    if (d) atomicAdd(reinterpret_cast<unsigned long long*>(a.tot + 1), static_cast<unsigned long long>(d));
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x), static_cast<unsigned long long>(c),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
+                       static_cast<unsigned long long>(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.scan.ticket, 1u);
-    if (prev == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const long long tc = static_cast<long long>(
-          __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const long long td = static_cast<long long>(
-          __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      a.tot[0] = 0;
-      a.tot[1] = 0;
-      scan_finish(a.scan, tc, td);
+    s_last = prev == gridDim.x - 1;
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;
+  long long c = 0, d = 0;
+  for (unsigned g = threadIdx.x; g < gridDim.x; g += kBlock) {
+    c += static_cast<long long>(
+        __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * g + 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  c = wave_sum(c);
+  d = wave_sum(d);
+  __syncthreads();  // (s_c / s_d reused)
+  if (lane_id() == 0) {
+    s_c[wv] = c;
+    s_d[wv] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long tc = 0, td = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitsPerBlock; ++k) {
+      tc += s_c[k];
+      td += s_d[k];
     }
+    scan_finish(a.scan, tc, td);
   }
 }
 
@@ -2130,7 +2166,10 @@ void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStrea
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  update_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
+  // fused finish: at most kMaxFusedGrid / 8 workgroups striding over the units
+  const unsigned grid = a.fuse_scan ? grid_for(a.words, kUnitWords * kUnitsPerBlock, kMaxFusedGrid / 8)
+                                    : grid_for(a.words, kUnitWords * kUnitsPerBlock);
+  update_kernel<<<grid, kBlock, 0, st>>>(a);
 }
 
 void scan_units(const ScanArgs& a, hipStream_t st) {
