@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,6 +42,7 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
   DBFS_CHECK(boot_ && inner_, "PeerComm needs a bootstrap and an inner communicator");
   rank_ = boot_->rank();
   size_ = boot_->size();
+  if (const char* e = std::getenv("DBFS_PEER_FUSED")) fused_small_ = std::string(e) != "0";
   DBFS_CHECK(size_ <= kern::kMaxPeers, "PeerComm supports at most 16 ranks");
   DBFS_CHECK(inner_->rank() == rank_ && inner_->size() == size_, "inner communicator does not match the bootstrap");
   DBFS_CHECK(slot_ >= 4096 && slot_ % 256 == 0, "PeerComm slot size must be a multiple of 256 B (>= 4 KiB)");
@@ -181,8 +183,13 @@ void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& rec
   pa.unit = ua.unit = unit;
   ua.sum_count = sum_count;
   ua.sum_out = sum_out;
-  kern::peer_push(pa, st);
-  HIP_CHECK(hipGetLastError());
+  int64_t largest = 0;
+  for (int p = 0; p < P; ++p) largest = std::max({largest, pa.bytes[p], ua.bytes[p]});
+  const bool fused = fused_small_ && largest <= kern::kPeerFusedMaxBytes;
+  if (!fused) {
+    kern::peer_push(pa, st);
+    HIP_CHECK(hipGetLastError());
+  }
   kern::PeerWaitArgs wa;
   wa.flags = reinterpret_cast<const uint64_t*>(win_);
   wa.npeers = P;
@@ -194,6 +201,12 @@ void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& rec
   const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
   wa.timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
   wa.error = err_dev_;
+  if (fused) {
+    kern::peer_fused(pa, wa, ua, st);
+    HIP_CHECK(hipGetLastError());
+    ++peer_ops_;
+    return;
+  }
   kern::peer_wait(wa, st);
   HIP_CHECK(hipGetLastError());
   kern::peer_unpack(ua, st);

@@ -1,8 +1,9 @@
 // gfx950 kernels of the peer-memory communicator (PeerComm, csrc/comm/peer_comm.cpp).
 //
 // Every rank exports one window of uncached device memory (IPC) and maps its
-// peers' windows; a collective is three stream-ordered launches, no host in
-// the loop and no library protocol:
+// peers' windows; a collective is three stream-ordered launches (one, fused,
+// for payloads of at most 64 KiB per peer), no host in the loop and no
+// library protocol:
 //   push   -- each rank stores its per-peer payloads straight into the peers'
 //             windows over xGMI (slot [parity][sender]); the last workgroup to
 //             finish (ticket) publishes `seq` into every peer's flag word for
@@ -127,6 +128,55 @@ __global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
     if (a.bytes[p] > 0) grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, t, nt);
 }
 
+// A small collective in one workgroup (the three launches above fused): the
+// push by every thread, the flags behind a system-scope release, the wait by
+// the first npeers threads (bounded as peer_wait_kernel), an acquire, the
+// unpack by every thread.  One workgroup is resident by itself, so the
+// spinning threads never keep the pushing ones from running.
+constexpr int kFusedThreads = 256;
+__global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs pa, PeerWaitArgs wa, PeerUnpackArgs ua) {
+  __shared__ int s_ok;
+  const int t = threadIdx.x;
+  if (t == 0) s_ok = 1;
+  for (int q = 0; q < pa.npeers; ++q)
+    if (pa.bytes[q] > 0) grid_copy(pa.dst[q], pa.src[q], pa.bytes[q], pa.unit, t, kFusedThreads);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (t < pa.npeers && pa.flag[t]) __hip_atomic_store(pa.flag[t], pa.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < wa.npeers && t != wa.skip) {
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t spin = 0;; ++spin) {
+      if (__hip_atomic_load(wa.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= wa.seq) break;
+      __builtin_amdgcn_s_sleep(2);
+      if ((spin & 255) == 255 && wall_clock64() - t0 > wa.timeout_ticks) {
+        s_ok = 0;  // (benign race: every writer stores 0)
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (!s_ok) {
+    if (t == 0 && wa.error) __hip_atomic_store(wa.error, wa.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (ua.sum_count > 0) {
+    for (int64_t i = t; i < ua.sum_count; i += kFusedThreads) {
+      uint64_t acc = 0;
+      for (int p = 0; p < ua.npeers; ++p) acc += static_cast<const uint64_t*>(ua.src[p])[i];
+      static_cast<uint64_t*>(ua.sum_out)[i] = acc;
+    }
+    return;
+  }
+  for (int p = 0; p < ua.npeers; ++p)
+    if (ua.bytes[p] > 0) grid_copy(ua.dst[p], ua.src[p], ua.bytes[p], ua.unit, t, kFusedThreads);
+}
+
 inline unsigned grid_for_bytes(int64_t bytes, int unit) {
   int64_t g = (bytes / unit + kBlock - 1) / kBlock;
   if (g < 1) g = 1;
@@ -146,6 +196,10 @@ void peer_push(const PeerPushArgs& a, hipStream_t st) {
 }
 
 void peer_wait(const PeerWaitArgs& a, hipStream_t st) { peer_wait_kernel<<<1, 64, 0, st>>>(a); }
+
+void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUnpackArgs& unpack, hipStream_t st) {
+  peer_fused_kernel<<<1, kFusedThreads, 0, st>>>(push, wait, unpack);
+}
 
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st) {
   int64_t tot = a.sum_count * 8;
