@@ -100,9 +100,12 @@ __device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_
 #define DBFS_NT_BU 0
 #endif
 // Direct top-down levels test the visited bit (1), the level byte (0: a
-// target claimed earlier in the level is not stored again) or both (2).
-// Measured, RMAT-22 top-down only: 65.0 / 60.0 / 58.0 GTEPS; RMAT-26: equal
-// within noise.
+// target claimed earlier in the level is not stored again), both (2), or the
+// visited and `next` words with claims in `next` (3).  Measured, RMAT-22
+// top-down only: 65.0 / 60.0 / 58.0 / 55.3 GTEPS; RMAT-26: 1, 0, 2 equal within
+// noise, 3 -2.5 %.  (Counters, tools/gpu_td_stats_roots.sh: the 43 M-edge level
+// stores 29.8 M level bytes for ~2 M new vertices and writes 1.1 GB; removing
+// the repeats with extra reads costs more L2 requests than the writes cost.)
 #ifndef DBFS_TD_DIRECT_PROBE_VISITED
 #define DBFS_TD_DIRECT_PROBE_VISITED 1
 #endif
@@ -368,6 +371,9 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
   if (wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
+#if DBFS_TD_DIRECT_PROBE_VISITED == 3
+      if (a.cand && a.cand[wl]) a.cand[wl] = 0;  // the claim bits of the level
+#endif
       if (!a.dirty) {
         c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
       } else if (a.dirty[wl]) {
@@ -753,6 +759,21 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
 // the grid is too small to fill the chip -- 4x the waves in flight to cover the
 // latency of the scattered loads/atomics.  The grid may be smaller than the
 // number of edge blocks (device loop: fixed grid): workgroups stride over them.
+#ifdef DBFS_TD_STATS
+// Diagnostic build only (-DDBFS_TD_STATS): per-dispatch top-down counters
+// (live edges, hub targets decoded unvisited, direct stores, filter on).
+__device__ unsigned long long g_td_stats[4];
+#define TD_STAT(i, x)                                              \
+  do {                                                             \
+    const unsigned long long v_ = (x);                             \
+    if (lane_id() == 0 && v_) atomicAdd(&g_td_stats[i], v_);       \
+  } while (0)
+#else
+#define TD_STAT(i, x) \
+  do {                \
+  } while (0)
+#endif
+
 // kFilter: the hub-filter variant (16 KiB more LDS: 4 instead of 6 resident
 // workgroups per CU -- launched only for levels that may use it).
 template <TdOut kOut, int kThreads, bool kFilter = false>
@@ -837,7 +858,12 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       }
     }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
+    for (int k = 0; k < kItems; ++k) {
+      DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
+      TD_STAT(0, __popcll(__ballot(live[k])));
+      TD_STAT(1, __popcll(__ballot(hubnew[k])));
+    }
+    TD_STAT(3, filter && t == 0 && b == blockIdx.x ? 1 : 0);
     if constexpr (kOut != TdOut::Lists) {
       if (!bytes) {
         word_t seen[kItems];
@@ -864,6 +890,22 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+#elif DBFS_TD_DIRECT_PROBE_VISITED == 3
+        // visited and `next` words loaded together: a target already claimed
+        // at this level (its bit in next, plain racy stores: a lost bit only
+        // repeats a store) is not stored again; update zeroes next
+        word_t nxt[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const int64_t w = vk[k] >> 6;
+          nxt[k] = live[k] ? a.next[w] : ~0ull;
+          keep[k] = live[k] && (hubnew[k] || !(visited[w] & (1ull << (vk[k] & 63))));
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) keep[k] = keep[k] && !(nxt[k] & (1ull << (vk[k] & 63)));
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          if (keep[k]) a.next[vk[k] >> 6] = nxt[k] | (1ull << (vk[k] & 63));
 #elif DBFS_TD_DIRECT_PROBE_VISITED == 2
         // visited bit first (dense), then the level byte of the unvisited
         // candidates (a target claimed earlier in this level is not stored again)
@@ -882,6 +924,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k) keep[k] = live[k] && cur[k] == kNarrowUnreached;
 #endif
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           if (keep[k]) {
@@ -1372,6 +1416,9 @@ template <bool kHub>
 __device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const word_t* s_hub, vid_t u) {
   if constexpr (kHub) {
     const vid_t hb = u & ~kHubFlag;
+#ifdef DBFS_DIAG_SMALL_PROBES  // diagnostic timing build: non-hub probes in a 512 KiB window (wrong levels)
+    return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u & ((1u << 22) - 1));
+#endif
     return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u);
   } else {
     return test_bit(fr, u);
@@ -2182,7 +2229,26 @@ void compact_frontier(const CompactArgs& a, hipStream_t st) {
   compact_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
 }
 
+#ifdef DBFS_TD_STATS
+static void td_stats_report(hipStream_t st) {
+  unsigned long long h[4] = {0};
+  (void)hipStreamSynchronize(st);
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_td_stats), sizeof(h));
+  const unsigned long long z[4] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_td_stats), z, sizeof(z));
+  if (h[0])
+    std::fprintf(stderr, "[td-stats] live %llu hub-unvisited %llu direct-stores %llu filter-wgs %llu\n", h[0], h[1],
+                 h[2], h[3]);
+}
+#endif
+
 void td_expand(const TdArgs& a, hipStream_t st) {
+#ifdef DBFS_TD_STATS
+  struct Report {
+    hipStream_t st;
+    ~Report() { td_stats_report(st); }
+  } report{st};
+#endif
   if (a.ctrl) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;
