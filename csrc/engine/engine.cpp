@@ -1651,6 +1651,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
         BuHeadArgs bh;
         bh.g = gv;
+        if (!opt_.bu_nz_rec) bh.g.nz_rec = nullptr;
         bh.zdeg = ba.zdeg;
         bh.hub_front = hub_in;
         bh.frontier_own = fr_own(cur);
@@ -1692,6 +1693,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         if (head_pass) {
           BuHeadArgs bh;
           bh.g = gv;
+          if (!opt_.bu_nz_rec) bh.g.nz_rec = nullptr;
           bh.zdeg = ba.zdeg;
           bh.hub_front = hub_front_.data();
           bh.frontier_own = frontier_[cur].data();

@@ -2066,6 +2066,9 @@ __global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
 constexpr int kHeadGroup = DBFS_BU_HEAD_GROUP;
 static_assert(kUnitWords % kHeadGroup == 0, "head groups tile a unit");
 
+// kRec: heads and row lengths from the packed row records (ShardView::nz_rec;
+// 32-bit lengths, one 8-byte record load per head).
+template <bool kRec>
 __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (a.stamp) stamp_level_start(a.ctrl);
@@ -2085,6 +2088,15 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
   const word_t below = (1ull << lane) - 1ull;
   long long cnt = 0, deg = 0;
   word_t res_l = 0;  // result word `lane` of the unit
+  // packed records: the unit's span and end of its non-empty rows (uniform)
+  uint32_t u_span = 0;
+  int64_t u_nzend = 0;
+  if constexpr (kRec) {
+    u_span = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(a.g.unit_base[unit + 1] - a.g.unit_base[unit])));
+    u_nzend = static_cast<int64_t>(readlane64(
+        static_cast<unsigned long long>(a.g.nz_pref[min((unit + 1) * kUnitWords, nzw)]), 0));
+  }
   for (int j0 = 0; j0 < nw; j0 += kHeadGroup) {
     int64_t k[kHeadGroup];
     vid_t u[kHeadGroup];
@@ -2100,7 +2112,7 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
       if (act[i]) {
         // unvisited implies non-zero degree (zero-degree bits are pre-set)
         k[i] = readlane_i64(pref_l, j) + __popcll(~readlane64(zd_l, j) & below);
-        u[i] = a.g.nz_head[k[i]];
+        u[i] = kRec ? a.g.nz_rec[k[i]].head : a.g.nz_head[k[i]];
       }
     }
     // (2) frontier bits of the heads
@@ -2119,13 +2131,18 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
       }
     }
     // (3) settled vertices: row lengths (statistics) and levels
-    eid_t r0[kHeadGroup], r1[kHeadGroup];
+    eid_t len[kHeadGroup];
 #pragma unroll
     for (int i = 0; i < kHeadGroup; ++i) {
-      r0[i] = r1[i] = 0;
+      len[i] = 0;
       if (found[i]) {
-        r0[i] = a.g.nz_row_off[k[i]];
-        r1[i] = a.g.nz_row_off[k[i] + 1];
+        if constexpr (kRec) {
+          const uint32_t s0 = a.g.nz_rec[k[i]].off;
+          const uint32_t s1 = k[i] + 1 < u_nzend ? a.g.nz_rec[k[i] + 1].off : u_span;
+          len[i] = s1 - s0;
+        } else {
+          len[i] = a.g.nz_row_off[k[i] + 1] - a.g.nz_row_off[k[i]];
+        }
       }
     }
 #pragma unroll
@@ -2135,7 +2152,7 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
       if (found[i]) {
         store_level(a.level, a.level8, (w0 + j0 + i) * 64 + lane, a.new_level);
         cnt += 1;
-        deg += r1[i] - r0[i];
+        deg += len[i];
       }
     }
   }
@@ -2430,7 +2447,11 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 
 void bu_head(const BuHeadArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  bu_head_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
+  const unsigned grid = grid_for(a.words, kUnitWords * kUnitsPerBlock);
+  if (a.g.nz_rec && a.g.unit_base)
+    bu_head_kernel<true><<<grid, kBlock, 0, st>>>(a);
+  else
+    bu_head_kernel<false><<<grid, kBlock, 0, st>>>(a);
 }
 
 void hub_local(const HubLocalArgs& a, hipStream_t st) {
