@@ -42,7 +42,7 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
   DBFS_CHECK(boot_ && inner_, "PeerComm needs a bootstrap and an inner communicator");
   rank_ = boot_->rank();
   size_ = boot_->size();
-  if (const char* e = std::getenv("DBFS_PEER_FUSED")) fused_small_ = std::string(e) != "0";
+  if (const char* e = std::getenv("DBFS_PEER_FUSED")) fused_ = std::string(e) != "0";
   DBFS_CHECK(size_ <= kern::kMaxPeers, "PeerComm supports at most 16 ranks");
   DBFS_CHECK(inner_->rank() == rank_ && inner_->size() == size_, "inner communicator does not match the bootstrap");
   DBFS_CHECK(slot_ >= 4096 && slot_ % 256 == 0, "PeerComm slot size must be a multiple of 256 B (>= 4 KiB)");
@@ -183,9 +183,7 @@ void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& rec
   pa.unit = ua.unit = unit;
   ua.sum_count = sum_count;
   ua.sum_out = sum_out;
-  int64_t largest = 0;
-  for (int p = 0; p < P; ++p) largest = std::max({largest, pa.bytes[p], ua.bytes[p]});
-  const bool fused = fused_small_ && largest <= kern::kPeerFusedMaxBytes;
+  const bool fused = fused_;
   if (!fused) {
     kern::peer_push(pa, st);
     HIP_CHECK(hipGetLastError());

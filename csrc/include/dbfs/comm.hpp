@@ -254,9 +254,8 @@ class PeerComm final : public Comm {
   uint64_t* err_dev_ = nullptr;
   uint64_t seq_ = 0;
   int64_t peer_ops_ = 0, inner_ops_ = 0;
-  // payloads of at most kern::kPeerFusedMaxBytes per peer as one launch
-  // (DBFS_PEER_FUSED=0: always push / wait / unpack)
-  bool fused_small_ = true;
+  // every collective as one launch (DBFS_PEER_FUSED=0: push / wait / unpack)
+  bool fused_ = true;
   std::function<void(double)> prev_watch_;
   bool watch_installed_ = false;
   char* slot_ptr(int owner, int parity, int sender) const;

@@ -71,9 +71,9 @@ struct PeerUnpackArgs {
 void peer_push(const PeerPushArgs& a, hipStream_t st);
 void peer_wait(const PeerWaitArgs& a, hipStream_t st);
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st);
-// Small collectives as ONE launch (one workgroup: push, flags, wait, unpack)
-// instead of three; every piece at most kPeerFusedMaxBytes.
-constexpr int64_t kPeerFusedMaxBytes = int64_t(64) << 10;
+// A collective as ONE launch (push, flags, wait, unpack fused) instead of
+// three; up to kPeerFusedGroups workgroups per peer.
+constexpr int64_t kPeerFusedGroups = 32;
 void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUnpackArgs& unpack, hipStream_t st);
 
 // ref_kernels.hip (reference-algorithm mode)

@@ -1,9 +1,9 @@
 // gfx950 kernels of the peer-memory communicator (PeerComm, csrc/comm/peer_comm.cpp).
 //
 // Every rank exports one window of uncached device memory (IPC) and maps its
-// peers' windows; a collective is three stream-ordered launches (one, fused,
-// for payloads of at most 64 KiB per peer), no host in the loop and no
-// library protocol:
+// peers' windows; a collective is one launch (peer_fused_kernel: the three
+// steps below in one grid; DBFS_PEER_FUSED=0 launches them separately), no
+// host in the loop and no library protocol:
 //   push   -- each rank stores its per-peer payloads straight into the peers'
 //             windows over xGMI (slot [parity][sender]); the last workgroup to
 //             finish (ticket) publishes `seq` into every peer's flag word for
@@ -128,26 +128,49 @@ __global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
     if (a.bytes[p] > 0) grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, t, nt);
 }
 
-// A small collective in one workgroup (the three launches above fused): the
-// push by every thread, the flags behind a system-scope release, the wait by
-// the first npeers threads (bounded as peer_wait_kernel), an acquire, the
-// unpack by every thread.  One workgroup is resident by itself, so the
-// spinning threads never keep the pushing ones from running.
+// A collective as ONE launch (the three above fused): push by every
+// workgroup (groups dealt to peers round-robin), the ticket hand-off whose
+// last workgroup publishes the flags behind a system-scope release, then
+// every workgroup waits for the peers' flags itself (bounded as
+// peer_wait_kernel) and unpacks its share after an acquire.  No workgroup
+// waits for another workgroup of this launch (only for the peers, whose
+// flags do not depend on it), so the grid need not be co-resident.
 constexpr int kFusedThreads = 256;
 __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs pa, PeerWaitArgs wa, PeerUnpackArgs ua) {
-  __shared__ int s_ok;
+  __shared__ int s_last, s_ok;
   const int t = threadIdx.x;
-  if (t == 0) s_ok = 1;
-  for (int q = 0; q < pa.npeers; ++q)
-    if (pa.bytes[q] > 0) grid_copy(pa.dst[q], pa.src[q], pa.bytes[q], pa.unit, t, kFusedThreads);
+  const int P = pa.npeers;
+  const int groups = static_cast<int>(gridDim.x) / P;
+  if (groups > 0) {
+    const int p = static_cast<int>(blockIdx.x) % P;
+    const int g = static_cast<int>(blockIdx.x) / P;
+    if (g < groups && pa.bytes[p] > 0)
+      grid_copy(pa.dst[p], pa.src[p], pa.bytes[p], pa.unit, static_cast<int64_t>(g) * kFusedThreads + t,
+                static_cast<int64_t>(groups) * kFusedThreads);
+  } else {
+    const int64_t nt = static_cast<int64_t>(gridDim.x) * kFusedThreads;
+    const int64_t gt = static_cast<int64_t>(blockIdx.x) * kFusedThreads + t;
+    for (int q = 0; q < P; ++q)
+      if (pa.bytes[q] > 0) grid_copy(pa.dst[q], pa.src[q], pa.bytes[q], pa.unit, gt, nt);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
+    s_ok = 1;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(pa.ticket, 1u);
+    s_last = prev == gridDim.x - 1 ? 1 : 0;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
-  if (t < pa.npeers && pa.flag[t]) __hip_atomic_store(pa.flag[t], pa.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (s_last) {
+    if (t < P && pa.flag[t]) __hip_atomic_store(pa.flag[t], pa.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) *pa.ticket = 0u;  // next collective is stream-ordered after this one
+  }
   if (t < wa.npeers && t != wa.skip) {
     const uint64_t t0 = wall_clock64();
     for (uint32_t spin = 0;; ++spin) {
@@ -165,8 +188,10 @@ __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs 
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int64_t nt = static_cast<int64_t>(gridDim.x) * kFusedThreads;
+  const int64_t gt = static_cast<int64_t>(blockIdx.x) * kFusedThreads + t;
   if (ua.sum_count > 0) {
-    for (int64_t i = t; i < ua.sum_count; i += kFusedThreads) {
+    for (int64_t i = gt; i < ua.sum_count; i += nt) {
       uint64_t acc = 0;
       for (int p = 0; p < ua.npeers; ++p) acc += static_cast<const uint64_t*>(ua.src[p])[i];
       static_cast<uint64_t*>(ua.sum_out)[i] = acc;
@@ -174,7 +199,7 @@ __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs 
     return;
   }
   for (int p = 0; p < ua.npeers; ++p)
-    if (ua.bytes[p] > 0) grid_copy(ua.dst[p], ua.src[p], ua.bytes[p], ua.unit, t, kFusedThreads);
+    if (ua.bytes[p] > 0) grid_copy(ua.dst[p], ua.src[p], ua.bytes[p], ua.unit, gt, nt);
 }
 
 inline unsigned grid_for_bytes(int64_t bytes, int unit) {
@@ -198,7 +223,15 @@ void peer_push(const PeerPushArgs& a, hipStream_t st) {
 void peer_wait(const PeerWaitArgs& a, hipStream_t st) { peer_wait_kernel<<<1, 64, 0, st>>>(a); }
 
 void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUnpackArgs& unpack, hipStream_t st) {
-  peer_fused_kernel<<<1, kFusedThreads, 0, st>>>(push, wait, unpack);
+  int64_t mx = 0;
+  for (int p = 0; p < push.npeers; ++p) mx = push.bytes[p] > mx ? push.bytes[p] : mx;
+  for (int p = 0; p < unpack.npeers; ++p) mx = unpack.bytes[p] > mx ? unpack.bytes[p] : mx;
+  if (unpack.sum_count * 8 > mx) mx = unpack.sum_count * 8;
+  // one group of workgroups per peer, sized for the largest piece (at most
+  // kPeerFusedGroups per peer: the push of 1 MiB per peer keeps every link busy)
+  const int64_t per = (mx / push.unit + kFusedThreads - 1) / kFusedThreads;
+  const int64_t groups = per < 1 ? 1 : (per > kPeerFusedGroups ? kPeerFusedGroups : per);
+  peer_fused_kernel<<<static_cast<unsigned>(groups * push.npeers), kFusedThreads, 0, st>>>(push, wait, unpack);
 }
 
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st) {
