@@ -5,6 +5,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <cstring>
 
 #include "dbfs/engine.hpp"
@@ -331,6 +332,34 @@ PYBIND11_MODULE(_dbfs_native, m) {
     for (auto& c : comms) out.push_back(std::shared_ptr<Comm>(c.release()));
     return out;
   });
+  // Collective latency: `iters` back-to-back collectives of `bytes` per peer
+  // on device buffers, one barrier + synchronize around them; returns the
+  // mean microseconds per collective (tools/peer_latency.py).
+  m.def(
+      "comm_latency",
+      [](std::shared_ptr<Comm> comm, std::shared_ptr<Backend> be, const std::string& op, int64_t bytes,
+         int iters) {
+        py::gil_scoped_release rel;
+        const int P = comm->size();
+        const int64_t words = std::max<int64_t>(bytes / 8, 1);
+        DBuf<int64_t> a(*be, static_cast<size_t>(words * P)), b(*be, static_cast<size_t>(words * P));
+        be->memset_async(a.data(), 0, a.bytes());
+        auto one = [&] {
+          if (op == "allreduce") comm->allreduce_sum_i64(a.data(), static_cast<size_t>(words));
+          else if (op == "allgather") comm->allgather(a.data(), b.data(), static_cast<size_t>(words) * 8);
+          else if (op == "alltoall") comm->alltoall(a.data(), b.data(), static_cast<size_t>(words) * 8);
+          else DBFS_CHECK(false, "comm_latency: op must be allreduce / allgather / alltoall");
+        };
+        for (int i = 0; i < 3; ++i) one();  // warm-up
+        be->synchronize();
+        comm->barrier();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < iters; ++i) one();
+        be->synchronize();
+        const auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double, std::micro>(t1 - t0).count() / std::max(iters, 1);
+      },
+      py::arg("comm"), py::arg("backend"), py::arg("op"), py::arg("bytes"), py::arg("iters") = 200);
   // Run one collective on numpy data through a communicator (unit tests of the
   // Comm implementations).  The data is staged into backend memory first.
   m.def(
