@@ -17,8 +17,8 @@ namespace dbfs {
 namespace {
 
 // Level of a new vertex in the wide or the narrow array (HIP: store_level).
-inline void put_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level) {
-  if (narrow) narrow[i] = level <= kNarrowMaxLevel ? static_cast<uint8_t>(level) : kNarrowUnreached;
+inline void put_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level, uint8_t base) {
+  if (narrow) narrow[i] = static_cast<uint8_t>(base + (level <= kNarrowMaxLevel ? level : kNarrowMaxLevel + 1));
   else wide[i] = level;
 }
 
@@ -88,7 +88,7 @@ class CpuBackend final : public Backend {
         if (use_bytes && a.level_direct) {
           if (!a.dirty || a.dirty[w]) {
             for (int b = 0; b < 64; ++b)
-              if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.new_level)) c |= 1ull << b;
+              if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.narrow_base + a.new_level)) c |= 1ull << b;
             if (a.dirty) a.dirty[w] = 0;
           }
         } else if (use_bytes) {
@@ -105,7 +105,7 @@ class CpuBackend final : public Backend {
           const int b = __builtin_ctzll(x);
           x &= x - 1;
           const int64_t v = w * 64 + b;
-          put_level(a.level, a.level8, v, a.new_level);
+          put_level(a.level, a.level8, v, a.new_level, a.narrow_base);
           const eid_t d = a.g.row_off[v + 1] - a.g.row_off[v];
           if (d > 0) { ++cnt; deg += d; }
         }
@@ -119,10 +119,10 @@ class CpuBackend final : public Backend {
   void init_run(const InitRunArgs& a) override {
     const int64_t src = a.src_local;
     if (a.level8 && a.level8_filled) {
-      if (src >= 0) a.level8[src] = 0;
+      if (src >= 0) a.level8[src] = a.narrow_base;
     } else {
       for (int64_t i = 0; i < a.g.rows; ++i) {
-        if (a.level8) a.level8[i] = i == src ? 0 : kNarrowUnreached;
+        if (a.level8) a.level8[i] = i == src ? a.narrow_base : kNarrowUnreached;
         else a.level[i] = i == src ? 0 : kUnreached;
       }
     }
@@ -270,7 +270,7 @@ class CpuBackend final : public Backend {
           vid_t* list = a.lists + static_cast<int64_t>(v / a.part) * (a.list_cap + 1);
           list[1 + list[0]++] = v;
         } else if (bytes && a.level_direct) {
-          a.level_direct[v] = static_cast<uint8_t>(a.new_level);
+          a.level_direct[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
           if (a.dirty) a.dirty[v >> 6] = 1;
         } else if (bytes) {
           a.next_bytes[v] = 1;
@@ -325,7 +325,7 @@ class CpuBackend final : public Backend {
         if (test_bit(a.visited, v)) continue;
         a.visited[v >> 6] |= 1ull << (v & 63);
         const int64_t r = static_cast<int64_t>(v) - a.g.lo;
-        put_level(a.level, a.level8, r, a.new_level);
+        put_level(a.level, a.level8, r, a.new_level, a.narrow_base);
         const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
         if (d <= 0) continue;
         a.frontier_out[r >> 6] |= 1ull << (r & 63);
@@ -404,7 +404,7 @@ class CpuBackend final : public Backend {
           for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
             if (test_bit(a.frontier, a.g.col[e])) {
               out |= 1ull << b;
-              put_level(a.level, a.level8, v, a.new_level);
+              put_level(a.level, a.level8, v, a.new_level, a.narrow_base);
               ++cnt;
               deg += a.g.row_off[v + 1] - a.g.row_off[v];
               break;
@@ -444,7 +444,7 @@ class CpuBackend final : public Backend {
           }
           if (!found) continue;
           out |= 1ull << b;
-          put_level(a.level, a.level8, w * 64 + b, a.new_level);
+          put_level(a.level, a.level8, w * 64 + b, a.new_level, a.narrow_base);
           ++cnt;
           deg += a.g.nz_row_off[k + 1] - a.g.nz_row_off[k];
         }
@@ -741,8 +741,11 @@ class CpuBackend final : public Backend {
     }
   }
 
-  void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) override {
-    for (int64_t i = 0; i < n; ++i) out[i] = in[i] == kNarrowUnreached ? kUnreached : static_cast<lvl_t>(in[i]);
+  void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base) override {
+    for (int64_t i = 0; i < n; ++i) {
+      const uint8_t v = static_cast<uint8_t>(in[i] - base);
+      out[i] = v > kNarrowMaxLevel ? kUnreached : static_cast<lvl_t>(v);
+    }
   }
   void degree_moments(const ShardView& g, int64_t* out2) override {
     int64_t s = 0, c = 0;

@@ -228,7 +228,11 @@ class HipBackend final : public Backend {
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_sparse(const TdSparseArgs& a) override { on(); kern::td_sparse(a, st_); chk(); }
   void level_finish(const LevelFinishArgs& a) override { on(); kern::level_finish(a, st_); chk(); }
-  void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) override { on(); kern::widen_levels(in, out, n, st_); chk(); }
+  void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base) override {
+    on();
+    kern::widen_levels(in, out, n, base, st_);
+    chk();
+  }
   void td_expand(const TdArgs& a) override { on(); kern::td_expand(a, st_); chk(); }
   void td_binned(const BinArgs& a) override { on(); kern::td_binned(a, st_); chk(); }
   void pack_bytes(const PackArgs& a) override { on(); kern::pack_bytes(a, st_); chk(); }

@@ -69,6 +69,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
   else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
+  else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
@@ -117,6 +118,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
+          {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
@@ -648,9 +650,24 @@ RunResult Engine::run(int64_t source) {
   // (padded to whole bitmap words: a direct top-down update reads a word's
   // 64 level bytes; padding vertices are pre-set visited, so masked)
   const size_t l8_bytes = static_cast<size_t>(std::max<int64_t>(part_.slice_words() * kWordBits, 1));
-  if (run_narrow_ && level8_.size() == 0) level8_ = DBuf<uint8_t>(be_, l8_bytes);
+  bool fresh = false;
+  if (run_narrow_ && level8_.size() == 0) {
+    level8_ = DBuf<uint8_t>(be_, l8_bytes);
+    fresh = true;
+  }
   level8_filled_ = false;
+  narrow_base_ = 0;
   const bool prefill = run_narrow_ && opt_.level_prefill > 0 && comm_.size() == 1;
+  if (run_narrow_ && !prefill && opt_.narrow_epochs) {
+    // Level bytes are stored as base + level with base cycling through
+    // kNarrowEpochs values: the previous epochs' bytes (and the 0xFF fill)
+    // lie outside this run's [base, base + kNarrowMaxLevel], so they already
+    // read as unreached and only epoch 0 pays for the fill.
+    if (fresh) narrow_run_ = 0;
+    const int epoch = static_cast<int>(narrow_run_++ % kNarrowEpochs);
+    narrow_base_ = static_cast<uint8_t>(epoch * (kNarrowMaxLevel + 2));
+    level8_filled_ = epoch != 0;
+  }
   if (prefill) {
     // the buffer filled under / after the previous run becomes this run's;
     // the previous run's levels are overwritten by the fill for the next one
@@ -710,7 +727,7 @@ bool Engine::use_narrow() const {
 // The last run's levels into level_ (32-bit) if it kept them narrow.
 void Engine::ensure_wide_levels() const {
   if (!levels_narrow_) return;
-  be_.widen_levels(level8_.data(), level_.data(), g_.rows());
+  be_.widen_levels(level8_.data(), level_.data(), g_.rows(), narrow_base_);
   levels_narrow_ = false;
 }
 
@@ -736,6 +753,7 @@ InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* 
   ia.level = level_.data();
   ia.level8 = run_narrow_ ? level8_.data() : nullptr;
   ia.level8_filled = level8_filled_;
+  ia.narrow_base = narrow_base_;
   ia.zdeg = zdeg_.data();
   ia.visited = visited_.data();
   ia.gwords = part_.global_words();
@@ -835,6 +853,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     ua.frontier = fr_nxt_own();
     ua.level = level_.data();
     ua.level8 = run_narrow_ ? level8_.data() : nullptr;
+    ua.narrow_base = narrow_base_;
     ua.new_level = new_level;
     ua.words = W;
     ua.unit_cnt = unit_cnt_.data();
@@ -995,6 +1014,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.new_frontier = fr_nxt_own();
       ba.level = level_.data();
       ba.level8 = run_narrow_ ? level8_.data() : nullptr;
+      ba.narrow_base = narrow_base_;
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
@@ -1323,6 +1343,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   ua.visited = vis_own;
   ua.level = level_.data();
   ua.level8 = run_narrow_ ? level8_.data() : nullptr;
+  ua.narrow_base = narrow_base_;
   ua.words = W;
   ua.unit_cnt = unit_cnt_.data();
   ua.unit_deg = unit_deg_.data();
@@ -1448,6 +1469,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.visited = visited_.data();
       sp.level = level_.data();
       sp.level8 = run_narrow_ ? level8_.data() : nullptr;
+      sp.narrow_base = narrow_base_;
       sp.new_level = L + 1;
       sp.oscan = qscan_set(L + 1);
       sp.obase = qbase_set(L + 1);
@@ -1574,8 +1596,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {
           // byte-map levels write the level itself (nothing to clear after)
           ta.level_direct = level8_.data();
+          ta.narrow_base = narrow_base_;
           ta.new_level = L + 1;
           tu.level_direct = level8_.data();
+          tu.narrow_base = narrow_base_;
           // a level predicted to touch few words: the update gathers only
           // the words td_expand marked
           if (opt_.td_dirty_words && mf_hint >= 0 && mf_hint * 8.0 < static_cast<double>(W * kWordBits)) {
@@ -1628,6 +1652,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.new_frontier = fr_own(cur ^ 1);
       ba.level = level_.data();
       ba.level8 = run_narrow_ ? level8_.data() : nullptr;
+      ba.narrow_base = narrow_base_;
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
@@ -1659,6 +1684,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         bh.new_frontier = ba.new_frontier;
         bh.level = ba.level;
         bh.level8 = ba.level8;
+        bh.narrow_base = narrow_base_;
         bh.new_level = ba.new_level;
         bh.words = W;
         bh.unit_cnt = unit_cnt_.data();
@@ -1701,6 +1727,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           bh.new_frontier = ba.new_frontier;
           bh.level = ba.level;
           bh.level8 = ba.level8;
+          bh.narrow_base = narrow_base_;
           bh.new_level = ba.new_level;
           bh.words = W;
           bh.unit_cnt = unit_cnt_.data();

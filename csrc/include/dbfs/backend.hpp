@@ -92,7 +92,13 @@ constexpr int64_t kMaxHubs = DBFS_MAX_HUBS;
 constexpr vid_t kHubFlag = 0x80000000u;
 // Narrow (8-bit) level arrays: 0xFF = unreached, levels 0 .. 254.
 constexpr uint8_t kNarrowUnreached = 0xFF;
-constexpr int kNarrowMaxLevel = 254;
+// One-byte levels are stored as base + level, base = 64 x (run number mod
+// kNarrowEpochs): a byte outside [base, base + kNarrowMaxLevel] reads as
+// unreached, so the array is refilled with 0xFF only every kNarrowEpochs runs
+// (base + 63 marks a level too deep for the narrow array: the traversal is
+// repeated with 32-bit levels).
+constexpr int kNarrowMaxLevel = 62;
+constexpr int kNarrowEpochs = 4;
 
 // Frontier bookkeeping is organised in "units" of 64 bitmap words (4096
 // vertices): one 256-thread workgroup (4 waves) per unit, 16 consecutive words
@@ -200,6 +206,7 @@ struct InitRunArgs {
   // levels up to kNarrowMaxLevel): written instead of `level` when set, here
   // and by every bitmap-engine kernel that writes levels.
   uint8_t* level8 = nullptr;
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
   bool level8_filled = false;      // level8 already holds kNarrowUnreached (prefilled): only the source's byte
   const word_t* zdeg = nullptr;    // global
   word_t* visited = nullptr;       // global
@@ -278,6 +285,7 @@ struct UpdateArgs {
   word_t* frontier = nullptr;    // owned slice of the NEXT global frontier bitmap
   lvl_t* level = nullptr;        // rows
   uint8_t* level8 = nullptr;     // narrow levels (see InitRunArgs)
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
   lvl_t new_level = 0;
   int64_t words = 0;             // words of the owned slice
   int64_t* unit_cnt = nullptr;   // nunits
@@ -382,6 +390,7 @@ struct TdSparseArgs {
   word_t* visited = nullptr;           // global
   lvl_t* level = nullptr;              // rows
   uint8_t* level8 = nullptr;           // narrow levels (see InitRunArgs)
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
   int32_t new_level = 0;
   int64_t* oscan = nullptr;
   int64_t* obase = nullptr;
@@ -470,6 +479,7 @@ struct TdArgs {
   // clear afterwards.
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
+  uint8_t narrow_base = 0;  // (level_direct stores narrow_base + new_level)
   // Optional with level_direct: byte w set for every bitmap word w that got a
   // level byte (a small level's update then gathers only those words
   // instead of every level byte).
@@ -543,6 +553,7 @@ struct BuArgs {
   word_t* new_frontier = nullptr;    // owned slice of the next frontier (fully overwritten)
   lvl_t* level = nullptr;
   uint8_t* level8 = nullptr;         // narrow levels (see InitRunArgs)
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
   lvl_t new_level = 0;
   int64_t words = 0;
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
@@ -589,6 +600,7 @@ struct BuHeadArgs {
   word_t* new_frontier = nullptr;    // owned slice (fully overwritten)
   lvl_t* level = nullptr;
   uint8_t* level8 = nullptr;
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
   lvl_t new_level = 0;
   int64_t words = 0;
   int64_t* unit_cnt = nullptr;
@@ -885,7 +897,7 @@ class Backend {
   // over the shard's rows: out2[0] = sum of degree^2, out2[1] = rows with degree > 0
   virtual void degree_moments(const ShardView& g, int64_t* out2) = 0;
   // out[i] = in[i] (narrow levels; kNarrowUnreached -> kUnreached)
-  virtual void widen_levels(const uint8_t* in, lvl_t* out, int64_t n) = 0;
+  virtual void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base) = 0;
 
  protected:
   std::function<void(double)> wait_watch_;

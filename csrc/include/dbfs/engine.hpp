@@ -237,6 +237,10 @@ struct EngineOptions {
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
   // rerun with 32-bit levels (and later runs keep them).
   bool narrow_levels = true;
+  // Narrow level bytes stored as base + level with the base cycling through
+  // kNarrowEpochs values, so only one run in kNarrowEpochs fills the byte
+  // array (the others read the earlier epochs' bytes as unreached).
+  bool narrow_epochs = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -347,7 +351,9 @@ class Engine {
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)
   bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
-  bool level8_filled_ = false;        // level8_ was prefilled for the current run
+  bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill
+  uint8_t narrow_base_ = 0;           // the current run's level byte base (narrow_epochs)
+  int64_t narrow_run_ = 0;            // narrow runs since level8_ was allocated
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels
   bool run_narrow_ = false;           // the current run writes level8_
   mutable bool levels_narrow_ = false;  // level_ is stale: level8_ holds the last run's levels

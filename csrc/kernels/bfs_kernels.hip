@@ -84,9 +84,10 @@ __device__ __forceinline__ void stamp_mailbox(LevelMailbox* mb, const LevelCtrl&
 // A new vertex's level: the narrow array when the run uses one (uniform
 // branch), else the 32-bit array.  Narrow overflow (level > kNarrowMaxLevel)
 // stores kNarrowUnreached; the engine reruns such a traversal with wide levels.
-__device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level) {
+// (narrow: base + level; base + 63 flags a level too deep for the bytes)
+__device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_t i, lvl_t level, uint8_t base) {
   if (narrow)
-    narrow[i] = level <= kNarrowMaxLevel ? static_cast<uint8_t>(level) : kNarrowUnreached;
+    narrow[i] = static_cast<uint8_t>(base + (level <= kNarrowMaxLevel ? level : kNarrowMaxLevel + 1));
   else
     wide[i] = level;
 }
@@ -156,8 +157,9 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   const int64_t rows = a.g.rows;
   const int64_t src = a.src_local;
   if (a.level8 && a.level8_filled) {
-    // prefilled on the side stream: the source's byte only
-    if (src >= 0 && t0 == 0) a.level8[src] = 0;
+    // already reads unreached for this run (prefilled, or an earlier epoch's
+    // bytes): the source's byte only
+    if (src >= 0 && t0 == 0) a.level8[src] = a.narrow_base;
   } else if (a.level8) {
     // narrow levels: rows / 16 uint4 stores of 0xFF (+ tail), the source's byte after
     const int64_t n16 = (reinterpret_cast<uintptr_t>(a.level8) & 15u) == 0 ? rows / 16 : 0;
@@ -166,15 +168,16 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
       uint4 v = make_uint4(~0u, ~0u, ~0u, ~0u);
       if (src >= 0 && (src >> 4) == i) {
         const unsigned clear = ~(0xFFu << (8 * (src & 3)));
+        const unsigned set = static_cast<unsigned>(a.narrow_base) << (8 * (src & 3));
         const int word = static_cast<int>((src >> 2) & 3);
-        if (word == 0) v.x &= clear;
-        else if (word == 1) v.y &= clear;
-        else if (word == 2) v.z &= clear;
-        else v.w &= clear;
+        if (word == 0) v.x = (v.x & clear) | set;
+        else if (word == 1) v.y = (v.y & clear) | set;
+        else if (word == 2) v.z = (v.z & clear) | set;
+        else v.w = (v.w & clear) | set;
       }
       l16[i] = v;
     }
-    for (int64_t i = n16 * 16 + t0; i < rows; i += stride) a.level8[i] = i == src ? 0 : kNarrowUnreached;
+    for (int64_t i = n16 * 16 + t0; i < rows; i += stride) a.level8[i] = i == src ? a.narrow_base : kNarrowUnreached;
   } else {
     // level: rows / 4 int4 stores (+ tail)
     const int64_t n4 = (reinterpret_cast<uintptr_t>(a.level) & 15u) == 0 ? rows / 4 : 0;
@@ -381,9 +384,9 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
       if (a.cand && a.cand[wl]) a.cand[wl] = 0;  // the claim bits of the level
 #endif
       if (!a.dirty) {
-        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
       } else if (a.dirty[wl]) {
-        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.new_level));
+        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
         a.dirty[wl] = 0;
       }
     } else if (use_bytes) {
@@ -410,7 +413,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
     const int pos = wave_set_position(nb, incl, idx);
     if (idx < total) {
       const int64_t v = w0 * 64 + pos;
-      if (!(use_bytes && a.level_direct)) store_level(a.level, a.level8, v, a.new_level);
+      if (!(use_bytes && a.level_direct)) store_level(a.level, a.level8, v, a.new_level, a.narrow_base);
       const eid_t d = ro[v + 1] - ro[v];
       if (d > 0) {
         cnt += 1;
@@ -898,7 +901,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         // a target hit by many edges is stored about once instead of once per
         // edge (stores cost more than reads; a stale read in another XCD's L2
         // only repeats the same store)
-        const uint8_t lv = static_cast<uint8_t>(a.new_level);
+        const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
         bool keep[kItems];
 #if DBFS_TD_DIRECT_PROBE_VISITED == 1
 #pragma unroll
@@ -930,13 +933,13 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k) cur[k] = keep[k] ? a.level_direct[vk[k]] : 0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = keep[k] && cur[k] == kNarrowUnreached;
+        for (int k = 0; k < kItems; ++k) keep[k] = keep[k] && static_cast<uint8_t>(cur[k] - a.narrow_base) > kNarrowMaxLevel;
 #else
         uint8_t cur[kItems];
 #pragma unroll
         for (int k = 0; k < kItems; ++k) cur[k] = live[k] ? a.level_direct[vk[k]] : 0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = live[k] && cur[k] == kNarrowUnreached;
+        for (int k = 0; k < kItems; ++k) keep[k] = live[k] && static_cast<uint8_t>(cur[k] - a.narrow_base) > kNarrowMaxLevel;
 #endif
 #pragma unroll
         for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
@@ -1051,7 +1054,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       rs[k] = re[k] = 0;
       if (claimed & (1u << k)) {
         const int64_t r = static_cast<int64_t>(v[k]) - lo;
-        store_level(a.level, a.level8, r, a.new_level);
+        store_level(a.level, a.level8, r, a.new_level, a.narrow_base);
         rs[k] = ro[r];
         re[k] = ro[r + 1];
       }
@@ -1341,11 +1344,11 @@ __global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
 
 // Narrow levels -> 32-bit levels (outside the timed traversal, on demand).
 __global__ __launch_bounds__(kBlock) void widen_levels_kernel(const uint8_t* __restrict__ in, lvl_t* __restrict__ out,
-                                                              int64_t n) {
+                                                              int64_t n, uint8_t base) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    const uint8_t v = in[i];
-    out[i] = v == kNarrowUnreached ? kUnreached : static_cast<lvl_t>(v);
+    const uint8_t v = static_cast<uint8_t>(in[i] - base);
+    out[i] = v > kNarrowMaxLevel ? kUnreached : static_cast<lvl_t>(v);
   }
 }
 
@@ -1618,7 +1621,7 @@ __device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, c
       found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
       res = __ballot(found);
       if (found) {
-        store_level(a.level, a.level8, v, a.new_level);
+        store_level(a.level, a.level8, v, a.new_level, a.narrow_base);
         cnt += 1;
         deg += e - rs;
       }
@@ -1781,7 +1784,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   }
   auto settle = [&](bool f, int l, eid_t r0, eid_t r1) {
     if (f) {
-      store_level(a.level, a.level8, w0 * 64 + l, a.new_level);
+      store_level(a.level, a.level8, w0 * 64 + l, a.new_level, a.narrow_base);
       cnt32 += 1;
       deg += r1 - r0;
       __hip_atomic_fetch_or(s_res + (l >> 6), 1ull << (l & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -2150,7 +2153,7 @@ __global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
       const word_t res = __ballot(found[i]);
       if (lane == j0 + i) res_l = res;
       if (found[i]) {
-        store_level(a.level, a.level8, (w0 + j0 + i) * 64 + lane, a.new_level);
+        store_level(a.level, a.level8, (w0 + j0 + i) * 64 + lane, a.new_level, a.narrow_base);
         cnt += 1;
         deg += len[i];
       }
@@ -2322,9 +2325,9 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
 }
 
-void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, hipStream_t st) {
+void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st) {
   if (n <= 0) return;
-  widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n);
+  widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n, base);
 }
 
 void level_finish(const LevelFinishArgs& a, hipStream_t st) { level_finish_kernel<<<1, 64, 0, st>>>(a); }

@@ -22,7 +22,7 @@ void td_expand(const TdArgs& a, hipStream_t st);
 void td_sparse(const TdSparseArgs& a, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
 void level_finish(const LevelFinishArgs& a, hipStream_t st);
-void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, hipStream_t st);
+void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
 void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);

@@ -350,11 +350,33 @@ def test_sparse_top_down_levels(rt, mode, predict, sparse_edges):
     assert dev.validate(12345)
 
 
+@pytest.mark.parametrize("epochs", [1, 0])
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_narrow_epochs_stale_bytes(rt, mode, epochs):
+    # level bytes are base + level with a base per run (narrow_epochs): runs
+    # alternate between two components (a 62-level path: the deepest narrow
+    # traversal, and a 40-level one) so every run meets the other
+    # component's and its own earlier epochs' bytes; levels must match the
+    # oracle every time (depth 62 fits the bytes: no fallback to wide levels)
+    n1, n2 = 63, 41
+    src_e = np.concatenate([np.arange(n1 - 1), n1 + np.arange(n2 - 1)])
+    dst_e = src_e + 1
+    csr = dbfs.build_csr(n1 + n2, src_e, dst_e)
+    b = dbfs.BFS(csr, rt, mode=mode)
+    b.engine.set_option("narrow_epochs", epochs)
+    for i in range(11):
+        src = (0, n1, n1 - 1, n1 + 20)[i % 4]
+        r = b.run(src)
+        exp = _oracle(csr, src)
+        assert np.array_equal(b.levels(), exp), (i, src)
+        assert r.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
+
+
 @pytest.mark.parametrize("device_loop", [1, 0])
 @pytest.mark.parametrize("mode", ["td", "bu", "do"])
 def test_narrow_levels(rt, mode, device_loop):
     # one-byte levels during the traversal, widened on read: same levels as
-    # the 32-bit array; a path deeper than 254 levels is rerun with 32-bit
+    # the 32-bit array; a path deeper than 62 levels is rerun with 32-bit
     # levels (reported time covers both runs) and later runs stay wide
     p = dbfs.rmat_params(11, 16, 5)
     csr = dbfs.host_csr_from_params(p)
@@ -362,7 +384,7 @@ def test_narrow_levels(rt, mode, device_loop):
     wide.engine.set_option("narrow_levels", 0)
     for b in (narrow, wide):
         b.engine.set_option("device_loop", device_loop)
-    for src in narrow.sample_roots(3, seed=2):
+    for src in narrow.sample_roots(9, seed=2):  # > kNarrowEpochs: cycles the byte base
         a, b = narrow.run(src), wide.run(src)
         assert np.array_equal(narrow.local_levels(), wide.local_levels())
         assert np.array_equal(narrow.levels(), _oracle(csr, src))

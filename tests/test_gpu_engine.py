@@ -464,12 +464,13 @@ def test_sparse_top_down_levels_gpu(gpu_runtime, mode, sparse_edges):
 def test_narrow_levels_gpu(gpu_runtime, mode):
     """One-byte levels (init_run uint4 fill, store_level in update / bottom-up /
     sparse kernels, widen_levels on read) equal the 32-bit path; a 700-level
-    path overflows them and is rerun with 32-bit levels."""
+    path overflows them and is rerun with 32-bit levels.  Nine roots cycle
+    the per-run byte base (narrow_epochs) twice."""
     p = dbfs.rmat_params(16, 16, 13)
     csr = dbfs.host_csr_from_params(p)
     narrow, wide = dbfs.BFS(p, gpu_runtime, mode=mode), dbfs.BFS(p, gpu_runtime, mode=mode)
     wide.engine.set_option("narrow_levels", 0)
-    for src in narrow.sample_roots(3, seed=4) + [17]:
+    for src in narrow.sample_roots(8, seed=4) + [17]:
         a, b = narrow.run(src), wide.run(src)
         assert np.array_equal(narrow.local_levels(), wide.local_levels())
         assert np.array_equal(narrow.levels(), dbfs.cpu_bfs(csr, src)[0])
@@ -482,6 +483,32 @@ def test_narrow_levels_gpu(gpu_runtime, mode):
         r = deep.run(src)
         assert np.array_equal(deep.levels(), np.abs(np.arange(n) - src))
         assert r.reached == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["td", "bu", "do"])
+def test_narrow_epochs_stale_bytes_gpu(gpu_runtime, mode):
+    """Runs alternate between an RMAT component and a 62-level path (the
+    deepest narrow traversal): each meets level bytes that the other component
+    and earlier epochs left behind, which must read as unreached."""
+    p = dbfs.rmat_params(14, 16, 3)
+    rm = dbfs.host_csr_from_params(p)
+    n0 = int(rm.n)
+    deg = np.diff(np.asarray(rm.row_off))
+    rows = np.repeat(np.arange(n0), deg)
+    cols = np.asarray(rm.col)
+    n1 = 63
+    src_e = np.concatenate([rows, n0 + np.arange(n1 - 1)])
+    dst_e = np.concatenate([cols, n0 + np.arange(1, n1)])
+    csr = dbfs.build_csr(n0 + n1, src_e, dst_e)
+    b = dbfs.BFS(csr, gpu_runtime, mode=mode)
+    roots = np.nonzero(deg)[0][::997][:5].tolist()
+    for i in range(10):
+        src = roots[i // 2] if i % 2 == 0 else n0 + (0 if i % 4 == 1 else n1 - 1)
+        r = b.run(src)
+        exp = dbfs.cpu_bfs(csr, src)[0]
+        assert np.array_equal(b.levels(), exp), (i, src)
+        assert r.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
 
 
 @pytest.mark.gpu
