@@ -17,7 +17,7 @@ PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())
 EXT_SUFFIX:= $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
 
 COMMON    := -O3 -std=c++17 -fPIC -Icsrc/include -Wall -Wno-unused-result
-HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $(EXTRA_HIPFLAGS)
 HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib -lpthread
 

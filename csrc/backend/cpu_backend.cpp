@@ -668,6 +668,16 @@ class CpuBackend final : public Backend {
       a.hub_front[w] = m;
     }
   }
+  void hub_apply(const HubApplyArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    for (int64_t h = 0; h < a.g.td_nhubs; ++h) {
+      if (!a.mark[h]) continue;
+      const vid_t v = a.g.td_hub_vertex[h];
+      a.level8[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
+      if (a.dirty) a.dirty[v >> 6] = 1;
+      a.mark[h] = 0;
+    }
+  }
   void hub_visited(const HubVisitedArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', 0)) return;
     for (int64_t w = 0; w < div_up(a.g.td_nhubs, 64); ++w) {

@@ -83,6 +83,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
+  else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
@@ -125,6 +126,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
+          {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
@@ -741,6 +743,7 @@ void Engine::begin_run_scratch() {
     be_.memset_async(next_.data(), 0, next_.bytes());
     if (next_bytes_.data()) be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
     if (td_dirty_.data()) be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
+    if (td_hub_mark_.data()) be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
   }
   scratch_dirty_ = true;  // until the run completes
 }
@@ -1610,8 +1613,27 @@ RunResult Engine::run_bitmap_device(int64_t source) {
             ta.dirty = td_dirty_.data();
             tu.dirty = td_dirty_.data();
           }
+          if (ta.td_hub_vis && opt_.td_hub_mark) {
+            if (!td_hub_mark_.data()) {
+              td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
+              be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
+            }
+            ta.td_hub_mark = td_hub_mark_.data();
+          }
         }
         be_.td_expand(ta);
+        if (ta.td_hub_mark) {
+          HubApplyArgs ha;
+          ha.g = gv;
+          ha.mark = ta.td_hub_mark;
+          ha.level8 = ta.level_direct;
+          ha.narrow_base = ta.narrow_base;
+          ha.new_level = ta.new_level;
+          ha.dirty = ta.dirty;
+          ha.ctrl = ctrl_.data();
+          ha.max_mf = ta.max_mf;
+          be_.hub_apply(ha);
+        }
         tu.cand = next_.data();
         tu.cand_bytes = next_bytes_.data();
         if (xc) {

@@ -77,9 +77,14 @@ struct ShardView {
   int64_t td_nhubs = 0;
 };
 
-// At most kTdMaxHubs top-down hubs (their visited bits, 16 KiB, sit in LDS
-// next to the top-down owner map: three 256-thread workgroups per CU).
-constexpr int64_t kTdMaxHubs = int64_t(1) << 17;
+// At most kTdMaxHubs top-down hubs (their visited bits, 8 KiB, sit in LDS
+// next to the top-down owner map: five 256-thread workgroups per CU).
+// Measured (RMAT-22 top-down only, hub marks on): 2^13 / 2^14 / 2^15 / 2^16
+// / 2^17 / 2^18 hubs: 60 / 62 / 71 / 77 / 69 / 60 GTEPS.
+#ifndef DBFS_TD_MAX_HUBS_LOG2
+#define DBFS_TD_MAX_HUBS_LOG2 16
+#endif
+constexpr int64_t kTdMaxHubs = int64_t(1) << DBFS_TD_MAX_HUBS_LOG2;
 
 // At most kMaxHubs hubs: their frontier bitmap (64 KiB) is staged in LDS by
 // every bottom-up workgroup (two 1024-thread workgroups per CU fit in 160 KiB).
@@ -493,6 +498,11 @@ struct TdArgs {
   // adjacency entries (device loop: ctrl->vis_deg; earlier, most hub
   // targets are unvisited and decoding them costs a dependent load)
   double td_hub_vis_frac = 0.0;
+  // With the filter and level_direct: a hub target unvisited at the level's
+  // start is claimed by a byte store here (kTdMaxHubs bytes, L2-resident,
+  // no decode of the hub id) instead of a level byte store scattered over
+  // the whole level array; hub_apply turns the marks into level bytes.
+  uint8_t* td_hub_mark = nullptr;
   // Launch 1024-thread workgroups when the grid has fewer blocks than this.
   int64_t wide_below_blocks = 0;
   // Device loop: q / m come from dev_stats[0..1], bits vs bytes and the
@@ -633,6 +643,20 @@ struct HubVisitedArgs {
   const LevelCtrl* ctrl = nullptr;
   int64_t min_edges = 0;
   double vis_frac = 0.0;  // as TdArgs::td_hub_vis_frac
+};
+
+// level8[td_hub_vertex[h]] = narrow_base + new_level (and dirty[v >> 6] = 1)
+// for every h with mark[h] != 0, which is cleared: td_expand's hub claims
+// (TdArgs::td_hub_mark).  mark holds kTdMaxHubs bytes.
+struct HubApplyArgs {
+  ShardView g;
+  uint8_t* mark = nullptr;
+  uint8_t* level8 = nullptr;
+  uint8_t narrow_base = 0;
+  lvl_t new_level = 0;
+  uint8_t* dirty = nullptr;
+  const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;  // chain predicate, as TdArgs::max_mf
 };
 
 // hub_front bit h = frontier bit of g.hub_vertex[h] (frontier global); in the
@@ -827,6 +851,7 @@ class Backend {
   virtual void hub_local(const HubLocalArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
+  virtual void hub_apply(const HubApplyArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their
   // bounds, the first recorded violation (code << 48 | detail; 0: none;
   // synchronises, clears), and a hook recording violation 99 (fault tests).

@@ -142,9 +142,15 @@ struct EngineOptions {
   // reached unchanged; below ~16 M edges the hub snapshot and its LDS staging
   // cost what they save)
   int64_t td_hub_edges = int64_t(1) << 24;
-  // ... once the visited vertices hold this fraction of the adjacency
-  // (measured: 0, i.e. also the earlier big levels, 58.9 against 63.5 GTEPS)
-  double td_hub_vis_frac = 0.75;
+  // ... once the visited vertices hold this fraction of the adjacency.
+  // Without hub marks (td_hub_mark) 0, i.e. also the earlier big levels, was
+  // slower (58.9 against 63.5 GTEPS: decoding unvisited hubs costs a
+  // dependent load); with them 0 is faster (69.0 against 65.9).
+  double td_hub_vis_frac = 0.0;
+  // Direct-level top-down: hub targets claimed as one byte per hub (an
+  // L2-resident 128 KiB array) and turned into level bytes after the
+  // expansion (TdArgs::td_hub_mark, hub_apply).
+  bool td_hub_mark = true;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.
   double td_check_visited_min = 0.02;
@@ -349,6 +355,7 @@ class Engine {
   DBuf<uint8_t> level8_next_;
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
+  DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
   DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)
   bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill

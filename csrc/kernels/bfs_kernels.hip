@@ -866,6 +866,9 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
             if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) {
 #endif
               live[k] = false;
+            } else if (a.td_hub_mark) {
+              a.td_hub_mark[h] = 1;  // claimed; hub_apply stores its level byte
+              live[k] = false;
             } else {
               vk[k] = a.g.td_hub_vertex[h];
               hubnew[k] = true;
@@ -2051,6 +2054,29 @@ __global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
   if (lane_id() == 0 && w * kWave < a.g.td_nhubs) a.out[w] = m;
 }
 
+// HubApplyArgs: 16 marks per thread (kTdMaxHubs is a multiple of 16; the
+// marks past td_nhubs stay zero).
+__global__ __launch_bounds__(kBlock) void hub_apply_kernel(HubApplyArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * 16;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 16; i < a.g.td_nhubs; i += stride) {
+    uint4* p = reinterpret_cast<uint4*>(a.mark + i);
+    const uint4 m = *p;
+    if ((m.x | m.y | m.z | m.w) == 0u) continue;
+    const unsigned w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) {
+        DBFS_DCHECK(i + j < a.g.td_nhubs, 9, i + j);
+        const vid_t v = a.g.td_hub_vertex[i + j];
+        a.level8[v] = lv;
+        if (a.dirty) a.dirty[v >> 6] = 1;
+      }
+    *p = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 // Head pass of a split bottom-up level (BuHeadArgs): one wave per 64-word unit,
 // one word per step (lane = vertex).  An unvisited vertex's hub-encoded head
 // (dense non-empty-row view) is tested in the all-reduced hub frontier bits
@@ -2496,6 +2522,11 @@ unsigned long long take_check_error() {
 void hub_visited(const HubVisitedArgs& a, hipStream_t st) {
   if (a.g.td_nhubs <= 0) return;
   hub_visited_kernel<<<grid_for((a.g.td_nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+}
+
+void hub_apply(const HubApplyArgs& a, hipStream_t st) {
+  if (a.g.td_nhubs <= 0 || a.g.td_nhubs > kTdMaxHubs) return;  // (select_hubs: at most kTdMaxHubs)
+  hub_apply_kernel<<<grid_for((a.g.td_nhubs + 15) / 16, kBlock), kBlock, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {

@@ -486,6 +486,29 @@ def test_narrow_levels_gpu(gpu_runtime, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mark", [1, 0])
+@pytest.mark.parametrize("vis_frac", [0.0, 0.75])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_td_hub_filter_gpu(gpu_runtime, mode, vis_frac, mark):
+    """Top-down hub filter (hubs' visited bits in LDS, hub-encoded td_col) on
+    every dense level (td_hub_edges=1), with hub targets claimed through the
+    hub marks + hub_apply or decoded and stored directly: exact levels."""
+    p = dbfs.rmat_params(17, 16, 21)
+    csr = dbfs.host_csr_from_params(p)
+    b = dbfs.BFS(p, gpu_runtime, mode=mode)
+    b.engine.set_option("td_hub_edges", 1)
+    b.engine.set_option("td_hub_vis_frac", vis_frac)
+    b.engine.set_option("td_hub_mark", mark)
+    b.engine.set_option("td_direct_edges", 1)
+    for src in b.sample_roots(5, seed=3):
+        r = b.run(src)
+        exp = dbfs.cpu_bfs(csr, src)[0]
+        assert np.array_equal(b.levels(), exp), src
+        assert r.reached == int((exp != dbfs.UNREACHED).sum())
+        assert b.validate(src)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["td", "bu", "do"])
 def test_narrow_epochs_stale_bytes_gpu(gpu_runtime, mode):
     """Runs alternate between an RMAT component and a 62-level path (the
