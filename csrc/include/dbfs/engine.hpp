@@ -186,6 +186,9 @@ struct EngineOptions {
   // A sparse chain stays live up to td_sparse_cap_factor x td_sparse_edges
   // frontier edges (0: any size); a larger level is re-enqueued dense.
   double td_sparse_cap_factor = 8.0;
+  // Device loop: workgroups of the dense top-down expansion grid (at most;
+  // they stride over the level's edge blocks).
+  int64_t td_grid_max = 2048;
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;

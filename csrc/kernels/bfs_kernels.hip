@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 
 #include "launch.hpp"
@@ -715,11 +716,13 @@ enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->b
 // start positions are scattered into s_owner and max-scanned, so s_owner[i]
 // is the block-local entry of edge i and s_base[entry] its qbase (col index =
 // edge + qbase).  Returns the block's edge count; ends with a barrier.
-template <int kThreads>
+// BaseT uint32_t: qbase kept modulo 2^32 (enough while the column array has
+// at most 2^32 entries: the column index is then (edge + qbase) mod 2^32).
+template <int kThreads, typename BaseT = long long>
 __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qscan, const int64_t* __restrict__ qbase,
                                                   const int32_t* __restrict__ blk_vstart, long long b,
                                                   long long nblocks, long long q, long long m, int32_t* s_owner,
-                                                  long long* s_base, int32_t* s_wmax) {
+                                                  BaseT* s_base, int32_t* s_wmax) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   const int t = threadIdx.x;
   const int lane = lane_id();
@@ -738,7 +741,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
   // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
   for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
     const long long qs = qscan[v0 + i];
-    s_base[i] = qbase[v0 + i];
+    s_base[i] = static_cast<BaseT>(qbase[v0 + i]);
     const long long p = (qs > e0 ? qs : e0) - e0;
     if (p < cnt) s_owner[p] = i;
   }
@@ -783,14 +786,21 @@ __device__ unsigned long long g_td_stats[4];
   } while (0)
 #endif
 
-// kFilter: the hub-filter variant (16 KiB more LDS: 4 instead of 6 resident
-// workgroups per CU -- launched only for levels that may use it).
-template <TdOut kOut, int kThreads, bool kFilter = false>
+// kFilter: the hub-filter variant (kTdMaxHubs / 8 bytes more LDS --
+// launched only for levels that may use it).  kBase32: the owner map's column
+// bases in 32 bits (graphs of at most 2^32 adjacency entries): 16 instead of
+// 24 KiB of LDS per workgroup, 8 resident workgroups per CU instead of 6 (5
+// instead of 4 with the filter).
+#ifndef DBFS_TD_BASE32
+#define DBFS_TD_BASE32 1
+#endif
+template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
+  using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
-  __shared__ long long s_base[kTdEdgesPerBlock + 1];
+  __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
   long long q = a.q, m = a.m;
@@ -827,8 +837,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
     const long long e0 = b * kTdEdgesPerBlock;
-    const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
-                                                 s_wmax);
+    const int cnt = td_block_owner_map<kThreads, BaseT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
+                                                        s_base, s_wmax);
 
     // All items' loads in flight together (column ids, then their visited /
     // next words), then the stores: the items of a thread are independent, but
@@ -839,7 +849,12 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const int idx = k * kThreads + t;
-      vk[k] = idx < cnt ? stream_load<DBFS_NT_TD != 0>(col + e0 + idx + s_base[s_owner[idx]]) : 0u;
+      int64_t ci;
+      if constexpr (kBase32)
+        ci = static_cast<uint32_t>(static_cast<uint32_t>(e0 + idx) + s_base[s_owner[idx]]);
+      else
+        ci = e0 + idx + s_base[s_owner[idx]];
+      vk[k] = idx < cnt ? stream_load<DBFS_NT_TD != 0>(col + ci) : 0u;
       live[k] = idx < cnt;
     }
     // hub targets tested in the LDS snapshot: a visited hub is done here; an
@@ -2302,6 +2317,23 @@ static void td_stats_report(hipStream_t st) {
 }
 #endif
 
+// Device-loop grid of a td_expand variant: at most the workgroups resident at
+// once (a.grid is a cap).  A grid past residency runs a partial second wave of
+// workgroups that start when the first ones finish their strided share: with
+// 2048 workgroups and six resident per CU, RMAT-22 top-down 70 against 83
+// GTEPS at 1536.
+template <TdOut kOut, bool kFilter, bool kBase32>
+unsigned td_resident_grid(int64_t cap) {
+  static const int per_cu = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kTdThreads, kFilter, kBase32>,
+                                                     kTdThreads, 0) != hipSuccess || n <= 0)
+      n = 1;
+    return n;
+  }();
+  return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(cap, static_cast<int64_t>(per_cu) * device_cus())));
+}
+
 void td_expand(const TdArgs& a, hipStream_t st) {
 #ifdef DBFS_TD_STATS
   struct Report {
@@ -2312,12 +2344,20 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   if (a.ctrl) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;
+    const bool b32 = DBFS_TD_BASE32 && a.g.nnz <= (int64_t(1) << 32);
+#define DBFS_TD_DEV(OUT, F, B) \
+  td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(a.grid), kTdThreads, 0, st>>>(a)
     if (a.lists)
-      td_expand_kernel<TdOut::Lists, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+      DBFS_TD_DEV(TdOut::Lists, false, false);
+    else if (a.td_hub_vis && b32)
+      DBFS_TD_DEV(TdOut::Dyn, true, true);
     else if (a.td_hub_vis)
-      td_expand_kernel<TdOut::Dyn, kTdThreads, true><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+      DBFS_TD_DEV(TdOut::Dyn, true, false);
+    else if (b32)
+      DBFS_TD_DEV(TdOut::Dyn, false, true);
     else
-      td_expand_kernel<TdOut::Dyn, kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+      DBFS_TD_DEV(TdOut::Dyn, false, false);
+#undef DBFS_TD_DEV
     return;
   }
   if (a.m <= 0 || a.q <= 0) return;
