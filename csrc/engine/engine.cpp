@@ -86,6 +86,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
+  else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
@@ -130,6 +131,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
+          {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
@@ -1353,8 +1355,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   ua.unit_cnt = unit_cnt_.data();
   ua.unit_deg = unit_deg_.data();
 
-  const int64_t td_grid =
-      std::max<int64_t>(1, std::min<int64_t>(div_up(g_.nnz(), kTdEdgesPerBlock), std::max<int64_t>(opt_.td_grid_max, 1)));
+  const int64_t td_blocks = div_up(g_.nnz(), kTdEdgesPerBlock);
+  const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_max, 1)));
+  const int64_t td_grid_filter =
+      std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_filter_max, 1)));
   std::vector<std::pair<int, int>> evs;
   std::vector<char> enq_dir;     // direction each level was (last) enqueued with
   std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B'; several ranks: 'L' list form)
@@ -1546,6 +1550,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ta.ctrl = ctrl_.data();
       ta.dev_stats = sblk(L - 1);
       ta.grid = td_grid;
+      ta.grid_filter = td_grid_filter;
       UpdateArgs tu = ua;
       if (d == 'L') {
         // owner-routed lists: candidates appended to their owner's list

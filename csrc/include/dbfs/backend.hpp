@@ -510,6 +510,7 @@ struct TdArgs {
   const LevelCtrl* ctrl = nullptr;
   const int64_t* dev_stats = nullptr;
   int64_t grid = 0;
+  int64_t grid_filter = 0;  // ... for the hub-filter variant (0: grid)
   // Device loop, work list handed over by a sparse level (no compaction ran):
   // zero the input vertices' words of clear_frontier (clear_qv: entry -> row).
   const vid_t* clear_qv = nullptr;

@@ -187,8 +187,13 @@ struct EngineOptions {
   // frontier edges (0: any size); a larger level is re-enqueued dense.
   double td_sparse_cap_factor = 8.0;
   // Device loop: workgroups of the dense top-down expansion grid (at most;
-  // they stride over the level's edge blocks).
-  int64_t td_grid_max = 2048;
+  // they stride over the level's edge blocks; the launcher also caps the grid
+  // at the kernel's residency), without and with the hub filter.  Measured:
+  // RMAT-26 (no filter levels) 1024 workgroups 1354 / 1334 against 1323 /
+  // 1318 GTEPS at 2048; RMAT-22 top-down only (filter levels) 1024 / 1280 /
+  // 1536 (= residency) 77 / 81 / 83 GTEPS.
+  int64_t td_grid_max = 1024;
+  int64_t td_grid_filter_max = 2048;
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;

@@ -2345,8 +2345,9 @@ void td_expand(const TdArgs& a, hipStream_t st) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;
     const bool b32 = DBFS_TD_BASE32 && a.g.nnz <= (int64_t(1) << 32);
+    const int64_t fgrid = a.grid_filter > 0 ? a.grid_filter : a.grid;
 #define DBFS_TD_DEV(OUT, F, B) \
-  td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(a.grid), kTdThreads, 0, st>>>(a)
+  td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
     if (a.lists)
       DBFS_TD_DEV(TdOut::Lists, false, false);
     else if (a.td_hub_vis && b32)
