@@ -572,3 +572,14 @@ def test_td_fused_finish_cpu(rt, mode):
     for src in bfs.sample_roots(3, seed=9):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
+
+
+def test_validator_counts(rt):
+    # Graph500 validator: clean levels -> no violations; validated against
+    # another source, exactly the two vertices with the wrong level-0 status
+    p = dbfs.rmat_params(11, 16, 9)
+    b = dbfs.BFS(p, rt, mode="do")
+    src, other = b.sample_roots(2, seed=8)
+    b.run(src)
+    assert list(b.engine.validate(int(src))) == [0, 0, 0]
+    assert list(b.engine.validate(int(other))) == [0, 0, 2]

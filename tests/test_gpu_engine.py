@@ -486,6 +486,21 @@ def test_narrow_levels_gpu(gpu_runtime, mode):
 
 
 @pytest.mark.gpu
+def test_validator_counts_gpu(gpu_runtime):
+    """Device Graph500 validator (thread-per-row, wave-per-long-row): clean
+    levels give no violations; validating against another source flags exactly
+    the two vertices whose level-0 status is wrong (RMAT hubs: rows > 64)."""
+    p = dbfs.rmat_params(16, 16, 9)
+    csr = dbfs.host_csr_from_params(p)
+    assert int(np.diff(np.asarray(csr.row_off)).max()) > 64
+    b = dbfs.BFS(p, gpu_runtime, mode="do")
+    src, other = b.sample_roots(2, seed=8)
+    b.run(src)
+    assert list(b.engine.validate(int(src))) == [0, 0, 0]
+    assert list(b.engine.validate(int(other))) == [0, 0, 2]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mark", [1, 0])
 @pytest.mark.parametrize("vis_frac", [0.0, 0.75])
 @pytest.mark.parametrize("mode", ["td", "do"])
