@@ -74,6 +74,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
+  else if (name == "bu_dyn_units") o.bu_dyn_units = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
@@ -117,6 +118,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"level_prefill", static_cast<double>(o.level_prefill)},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
+          {"bu_dyn_units", o.bu_dyn_units ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
@@ -748,8 +750,18 @@ void Engine::begin_run_scratch() {
     if (next_bytes_.data()) be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
     if (td_dirty_.data()) be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
     if (td_hub_mark_.data()) be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
+    if (bu_queue_.data()) be_.memset_async(bu_queue_.data(), 0, bu_queue_.bytes());
   }
   scratch_dirty_ = true;  // until the run completes
+}
+
+unsigned* Engine::bu_unit_queue() {
+  if (!opt_.bu_dyn_units) return nullptr;
+  if (!bu_queue_.data()) {
+    bu_queue_ = DBuf<uint32_t>(be_, static_cast<size_t>((kBuQueueGroups + 1) * kBuQueueStride));
+    be_.memset_async(bu_queue_.data(), 0, bu_queue_.bytes());
+  }
+  return bu_queue_.data();
 }
 
 InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
@@ -1035,6 +1047,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
+      ba.unit_queue = bu_unit_queue();
       if (gv.nhubs > 0) {
         HubGatherArgs hg;
         hg.g = gv;
@@ -1696,6 +1709,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
+      ba.unit_queue = bu_unit_queue();
       ba.ctrl = ctrl_.data();
       if (split) {
         // head pass (hub bits from the previous level's reduction, owned

@@ -552,6 +552,12 @@ struct PackArgs {
 // new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
 // Slots of BuArgs::tot (one pair per workgroup of a fused bottom-up finish).
 constexpr int kMaxFusedGrid = 4096;
+// Whole-unit bottom-up kernels with dynamic unit assignment: one counter per
+// workgroup group (blockIdx % kBuQueueGroups) plus an exit counter.
+constexpr int kBuQueueGroups = 8;
+// counters kBuQueueStride uints apart (one 128-B line each: counters sharing a
+// line serialise their atomics)
+constexpr int kBuQueueStride = 32;
 
 struct BuArgs {
   ShardView g;
@@ -593,6 +599,10 @@ struct BuArgs {
   bool fuse_scan = false;
   ScanArgs scan;
   int64_t* tot = nullptr;
+  // Whole-unit kernels: units beyond each wave's first taken from these
+  // kBuQueueGroups + 1 counters, kBuQueueStride apart (zero between launches; the kernel's last
+  // wave re-zeroes them); null: static stride over the units.
+  unsigned* unit_queue = nullptr;
 };
 
 // First half of a split bottom-up level (several ranks): while the frontier

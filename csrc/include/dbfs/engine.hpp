@@ -209,6 +209,12 @@ struct EngineOptions {
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.
   bool bu_fused_scan = true;
+  // Whole-unit bottom-up kernels hand out units beyond each wave's first
+  // dynamically (BuArgs::unit_queue) instead of a static stride.  Measured
+  // (RMAT-26, per level): 387 / 182 / 104 us against 346 / 137 / 30 with the
+  // static stride (counters on one 128-B line: 520 / 330 / 272) -- the
+  // returning device-scope atomics cost more than the stride's imbalance.
+  bool bu_dyn_units = false;
   // Bottom-up rows from the packed 8-byte records (ShardView::nz_rec) instead
   // of the view's 8-byte offsets + 4-byte heads.
   bool bu_nz_rec = true;
@@ -339,6 +345,7 @@ class Engine {
   RunResult run_ref(int64_t source);
   void alloc_bitmap_state();
   void begin_run_scratch();
+  unsigned* bu_unit_queue();  // BuArgs::unit_queue (null unless bu_dyn_units)
   InitRunArgs init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
                         LevelMailbox* mailbox);
   bool scratch_dirty_ = true;  // cand / next / byte map may hold stale bits
@@ -361,6 +368,7 @@ class Engine {
   // one rank: the next run's level bytes, filled with kNarrowUnreached on the
   // side stream under the current run (EngineOptions::level_prefill)
   DBuf<uint8_t> level8_next_;
+  DBuf<uint32_t> bu_queue_;  // BuArgs::unit_queue counters
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)

@@ -1947,8 +1947,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       s_c[wave] = 0;
       s_d[wave] = 0;
     }
-    for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
-         u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
+    auto unit = [&](int64_t u) {
       long long cnt = 0, deg = 0;
       bu_wave_compact<kPacked, true, kUnitWords, kQueueLen, kRec>(a, u * kUnitWords, own, s_res + wave * kUnitWords,
                                                                   s_hub, cnt, deg, s_q + wave * kQueueLen);
@@ -1960,6 +1959,37 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
         s_c[wave] += cnt;
         s_d[wave] += deg;
       }
+    };
+    if (a.unit_queue) {
+      // dynamic: a static stride gives every wave 2-3 units whose cost differs
+      // by their unvisited rows, and the level lasts as long as the slowest
+      // wave.  Here each wave takes its first unit statically (all waves
+      // starting at once would serialise on one counter), then further units
+      // from a device-scope counter of its workgroup group (blockIdx % 8: the
+      // round-robin XCD placement, so each counter serves one XCD's waves and
+      // takes ~1/8 of the dequeues).  The last wave to leave resets the
+      // counters for the next launch (every wave leaves once, after its last
+      // dequeue).
+      const int64_t waves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+      const unsigned ngroups = gridDim.x < kBuQueueGroups ? gridDim.x : kBuQueueGroups;
+      const unsigned grp = blockIdx.x % ngroups;
+      int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave;
+      while (u < nunits) {
+        unit(u);
+        unsigned got = 0;
+        if (lane_id() == 0) got = atomicAdd(a.unit_queue + grp * kBuQueueStride, 1u);
+        const int64_t k = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(got)));
+        u = waves + k * ngroups + grp;
+      }
+      if (lane_id() == 0) {
+        const unsigned left = atomicAdd(a.unit_queue + kBuQueueGroups * kBuQueueStride, 1u);
+        if (left == static_cast<unsigned>(waves) - 1u)
+          for (int i = 0; i <= kBuQueueGroups; ++i) atomicExch(a.unit_queue + i * kBuQueueStride, 0u);
+      }
+    } else {
+      for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+           u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock)
+        unit(u);
     }
     if (!a.fuse_scan) return;
     // fused finish: the workgroup's totals into its own slot of tot

@@ -340,16 +340,19 @@ def test_bottom_up_head_pass_gpu(gpu_runtime, head_pass, max_hubs, whole):
             _check(bfs, csr, src)
 
 
-@pytest.mark.parametrize("head_pass", [0, 1])
-def test_full_scale_rmat20_gpu(gpu_runtime, head_pass):
+@pytest.mark.parametrize("head_pass,dyn", [(0, 0), (1, 0), (0, 1)])
+def test_full_scale_rmat20_gpu(gpu_runtime, head_pass, dyn):
     """RMAT-20 at the default thresholds, exact against the CPU oracle: whole
     64-word units per wave chosen by occupancy (16 K units >= the resident wave
-    slots), 2^19 hubs, deferred row scans, sparse and dense top-down levels."""
+    slots), 2^19 hubs, deferred row scans, sparse and dense top-down levels;
+    also with units handed out dynamically (bu_dyn_units, whose counters the
+    last wave re-zeroes for the next launch)."""
     p = dbfs.rmat_params(20, 16, 5)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode="do")
     assert bfs.graph.nhubs > 1 << 16
     bfs.engine.set_option("bu_head_pass", head_pass)
+    bfs.engine.set_option("bu_dyn_units", dyn)
     dirs = set()
     for src in bfs.sample_roots(2, seed=21):
         res = _check(bfs, csr, src)
