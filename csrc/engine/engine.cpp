@@ -75,6 +75,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "bu_dyn_units") o.bu_dyn_units = v != 0;
+  else if (name == "bu_balanced_grid") o.bu_balanced_grid = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
@@ -119,6 +120,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"level_prefill", static_cast<double>(o.level_prefill)},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"bu_dyn_units", o.bu_dyn_units ? 1.0 : 0.0},
+          {"bu_balanced_grid", o.bu_balanced_grid ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
@@ -1048,6 +1050,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.unit_queue = bu_unit_queue();
+      ba.balanced_grid = opt_.bu_balanced_grid;
       if (gv.nhubs > 0) {
         HubGatherArgs hg;
         hg.g = gv;
@@ -1710,6 +1713,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
       ba.unit_queue = bu_unit_queue();
+      ba.balanced_grid = opt_.bu_balanced_grid;
       ba.ctrl = ctrl_.data();
       if (split) {
         // head pass (hub bits from the previous level's reduction, owned

@@ -603,6 +603,10 @@ struct BuArgs {
   // kBuQueueGroups + 1 counters, kBuQueueStride apart (zero between launches; the kernel's last
   // wave re-zeroes them); null: static stride over the units.
   unsigned* unit_queue = nullptr;
+  // Whole-unit kernels, static stride: grid trimmed so every wave takes the
+  // same number of units (e.g. 456 instead of 512 workgroups of 12 waves for
+  // 16 K units: 3 units per wave either way, fewer waves idle at the end).
+  bool balanced_grid = false;
 };
 
 // First half of a split bottom-up level (several ranks): while the frontier

@@ -215,6 +215,9 @@ struct EngineOptions {
   // static stride (counters on one 128-B line: 520 / 330 / 272) -- the
   // returning device-scope atomics cost more than the stride's imbalance.
   bool bu_dyn_units = false;
+  // ... or with the static stride's grid trimmed to an equal number of units
+  // per wave (BuArgs::balanced_grid).
+  bool bu_balanced_grid = false;
   // Bottom-up rows from the packed 8-byte records (ShardView::nz_rec) instead
   // of the view's 8-byte offsets + 4-byte heads.
   bool bu_nz_rec = true;

@@ -114,6 +114,22 @@ __device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_
 // noise, 3 -2.5 %.  (Counters, tools/gpu_td_stats_roots.sh: the 43 M-edge level
 // stores 29.8 M level bytes for ~2 M new vertices and writes 1.1 GB; removing
 // the repeats with extra reads costs more L2 requests than the writes cost.)
+// Last-arriver hand-offs (scan_units, fused finishes, td_sparse): the last
+// workgroup reads only values the others stored write-through (agent-scope
+// stores / atomics) and reads them with agent-scope loads, so it needs no
+// agent acquire fence (MI355X_MICROARCH, hand-off table, first row).  0 drops
+// it: measured no faster (RMAT-26 level times equal within noise), so the
+// fence stays.
+#ifndef DBFS_LAST_ACQUIRE
+#define DBFS_LAST_ACQUIRE 1
+#endif
+#define DBFS_LAST_ARRIVER_ACQUIRE()                                   \
+  do {                                                                \
+    if (DBFS_LAST_ACQUIRE) {                                          \
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");              \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                \
+    }                                                                 \
+  } while (0)
 #ifndef DBFS_TD_DIRECT_PROBE_VISITED
 #define DBFS_TD_DIRECT_PROBE_VISITED 1
 #endif
@@ -477,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.scan.ticket, 1u);
     s_last = prev == gridDim.x - 1;
-    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
   }
   __syncthreads();
   if (!s_last) return;
@@ -539,10 +555,11 @@ __global__ __launch_bounds__(kScanChunk) void totals_finish_kernel(ScanArgs a) {
 // ---------------------------------------------------------------------------
 // Multi-block scan.  Workgroup b scans units [b*CH, (b+1)*CH) in place
 // (exclusive, in-chunk) and publishes its chunk total; the last workgroup to
-// arrive scans the chunk totals.  Hand-off: chunk totals stored by thread 0,
-// `s_waitcnt vmcnt(0)`, agent release fence, `s_waitcnt vmcnt(0)` (compiler
-// hazard, MI355X_MICROARCH), then the ticket atomic; the last arriver runs an
-// agent acquire fence before any thread reads the totals.
+// arrive scans the chunk totals.  Hand-off: chunk totals stored agent-scope
+// (write-through) by thread 0, `s_waitcnt vmcnt(0)`, then the ticket atomic
+// (no agent release: it would write back the XCD's whole L2, microseconds on
+// the level's critical path); the last arriver runs an agent acquire fence
+// and reads the totals with agent-scope loads.
 __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   __shared__ long long s_c[kScanChunk / kWave], s_d[kScanChunk / kWave];
   __shared__ int s_last;
@@ -581,15 +598,12 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
                        static_cast<unsigned long long>(tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.part_deg + blockIdx.x),
                        static_cast<unsigned long long>(td), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // (no agent release: the totals are the only bytes handed off, stored
+    // write-through by this lane and read by agent-scope loads)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
     s_last = (prev == nblk - 1) ? 1 : 0;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
   }
   __syncthreads();
   if (!s_last) return;
@@ -597,7 +611,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
   long long carry_c = 0, carry_d = 0;
   for (unsigned base = 0; base < nblk; base += kScanChunk) {
     const unsigned i = base + t;
-    // agent-scope loads of the other workgroups' chunk totals (behind the acquire)
+    // agent-scope loads of the other workgroups' chunk totals
     const long long pc = i < nblk ? static_cast<long long>(__hip_atomic_load(
         reinterpret_cast<unsigned long long*>(a.part_cnt + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0;
     const long long pd = i < nblk ? static_cast<long long>(__hip_atomic_load(
@@ -1032,18 +1046,23 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
   if (a.first) stamp_level_start(a.ctrl);
   const long long q = a.dev_stats[0], m = a.dev_stats[1];
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  // Only the workgroups that have an edge block take part (at least one, for
+  // the finish): the others return before the ticket -- on a level of a few
+  // blocks, 256 workgroups queueing on one ticket address cost several us.
+  const unsigned active = static_cast<unsigned>(nblocks < 1 ? 1 : (nblocks < gridDim.x ? nblocks : gridDim.x));
+  if (blockIdx.x >= active) return;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
-  const int64_t gstride = static_cast<int64_t>(gridDim.x) * kThreads;
+  const int64_t gstride = static_cast<int64_t>(active) * kThreads;
   // the input vertices' frontier bits (the bitmap is not read here)
   for (int64_t i = gtid; i < q; i += gstride) a.frontier_in[a.qv[i] >> 6] = 0ull;
 
-  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const vid_t* __restrict__ col = a.g.col;
   const eid_t* __restrict__ ro = a.g.row_off;
   const int64_t lo = a.g.lo;
-  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+  for (long long b = blockIdx.x; b < nblocks; b += active) {
     const long long e0 = b * kTdEdgesPerBlock;
     const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
                                                  s_wmax);
@@ -1121,16 +1140,13 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   // last workgroup: the level's totals and decision (as scan_units_kernel)
   __syncthreads();
   if (t == 0) {
-    // every wave's counter atomic has returned; hand-off as in scan_units_kernel
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // every wave's counter atomic has returned.  (No release: the last
+    // workgroup reads only the counter, a device-scope atomic; the level's
+    // stores are read by later launches.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
-    s_last = (prev == gridDim.x - 1) ? 1 : 0;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    s_last = (prev == active - 1) ? 1 : 0;
+    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
   }
   __syncthreads();
   if (!s_last || t != 0) return;
@@ -2010,7 +2026,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned prev = atomicAdd(a.scan.ticket, 1u);
       s_last = prev == gridDim.x - 1;
-      if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
     }
     __syncthreads();
     if (!s_last) return;
@@ -2500,7 +2516,12 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 #endif
     constexpr int kFirstThreads = DBFS_BU_FIRST_THREADS;
     const int threads = whole ? (a.follow_up ? kFollowThreads : kFirstThreads) : kHubBuThreads;
-    const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
+    unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
+    if (whole && a.balanced_grid && !a.unit_queue) {
+      const int64_t wpb = threads / kWave;
+      const int64_t per_wave = (nunits + static_cast<int64_t>(grid) * wpb - 1) / (static_cast<int64_t>(grid) * wpb);
+      grid = grid_for(nunits, per_wave * wpb);
+    }
 #define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
