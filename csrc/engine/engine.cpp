@@ -75,6 +75,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "bu_dyn_units") o.bu_dyn_units = v != 0;
+  else if (name == "td_group_ticket") o.td_group_ticket = v != 0;
   else if (name == "bu_balanced_grid") o.bu_balanced_grid = v != 0;
   else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
   else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
@@ -120,6 +121,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"level_prefill", static_cast<double>(o.level_prefill)},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"bu_dyn_units", o.bu_dyn_units ? 1.0 : 0.0},
+          {"td_group_ticket", o.td_group_ticket ? 1.0 : 0.0},
           {"bu_balanced_grid", o.bu_balanced_grid ? 1.0 : 0.0},
           {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
           {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
@@ -753,6 +755,7 @@ void Engine::begin_run_scratch() {
     if (td_dirty_.data()) be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
     if (td_hub_mark_.data()) be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
     if (bu_queue_.data()) be_.memset_async(bu_queue_.data(), 0, bu_queue_.bytes());
+    if (td_group_ticket_.data()) be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
   }
   scratch_dirty_ = true;  // until the run completes
 }
@@ -1683,10 +1686,17 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.ctrl = ctrl_.data();
       if (!xc && opt_.td_fused_finish) {
         // totals and finish in the update's last workgroup (as bottom-up)
-        if (!td_tot_.data()) td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
+        if (!td_tot_.data()) td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
         tu.fuse_scan = true;
         tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
         tu.tot = td_tot_.data();
+        if (opt_.td_group_ticket) {
+          if (!td_group_ticket_.data()) {
+            td_group_ticket_ = DBuf<uint32_t>(be_, static_cast<size_t>(kFusedGroups * kBuQueueStride));
+            be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
+          }
+          tu.group_ticket = td_group_ticket_.data();
+        }
         fused_scan = true;
       }
       be_.update_frontier(tu);

@@ -312,6 +312,13 @@ struct UpdateArgs {
   bool fuse_scan = false;
   ScanArgs scan;
   int64_t* tot = nullptr;
+  // ... with the ticket two-level: workgroups of kFusedGroup consecutive ids
+  // share a group ticket (kBuQueueStride apart, zero between launches; the
+  // group's last workgroup re-zeroes it, sums the group's slots into
+  // tot[2 kMaxFusedGrid + 2 g] and takes the level ticket), so the grid can
+  // be large without thousands of same-address atomics.  Null: one ticket
+  // (grid capped at kMaxFusedGrid / 8).
+  unsigned* group_ticket = nullptr;
 };
 
 
@@ -558,6 +565,9 @@ constexpr int kBuQueueGroups = 8;
 // counters kBuQueueStride uints apart (one 128-B line each: counters sharing a
 // line serialise their atomics)
 constexpr int kBuQueueStride = 32;
+// Fused update finish, two-level ticket (UpdateArgs::group_ticket).
+constexpr int kFusedGroup = 64;
+constexpr int kFusedGroups = kMaxFusedGrid / kFusedGroup;
 
 struct BuArgs {
   ShardView g;

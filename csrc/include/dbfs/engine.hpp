@@ -233,6 +233,9 @@ struct EngineOptions {
   // (A first version with one workgroup per 4 units and totals atomics on
   // one address: level 1 of RMAT-26 38 -> 117 us.)
   bool td_fused_finish = true;
+  // ... with a two-level ticket (UpdateArgs::group_ticket): the update runs
+  // a full grid (up to kMaxFusedGrid workgroups) instead of kMaxFusedGrid / 8.
+  bool td_group_ticket = true;
   // Device loop, several ranks: top-down levels whose frontier is predicted to
   // have at most this many edges exchange owner-routed vertex lists (list
   // form, per-peer capacity list_cap_factor x the prediction, rounded to a
@@ -372,6 +375,7 @@ class Engine {
   // side stream under the current run (EngineOptions::level_prefill)
   DBuf<uint8_t> level8_next_;
   DBuf<uint32_t> bu_queue_;  // BuArgs::unit_queue counters
+  DBuf<uint32_t> td_group_ticket_;  // UpdateArgs::group_ticket
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)

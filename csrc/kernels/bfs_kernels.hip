@@ -465,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   // the workgroup's totals in its slot of tot, a ticket; the last workgroup
   // sums the slots and finishes the level
   __shared__ long long s_c[kUnitsPerBlock], s_d[kUnitsPerBlock];
-  __shared__ int s_last;
+  __shared__ int s_last, s_level_last;  // (separate: waves read s_last while wave 0 decides the level)
   long long wc = 0, wd = 0;
   for (int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; unit < nunits;
        unit += static_cast<int64_t>(gridDim.x) * kUnitsPerBlock) {
@@ -491,18 +491,62 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
                        static_cast<unsigned long long>(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(a.scan.ticket, 1u);
-    s_last = prev == gridDim.x - 1;
-    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+    if (a.group_ticket) {
+      // the group's last workgroup sums the group (below), then takes the
+      // level ticket
+      const unsigned grp = blockIdx.x / kFusedGroup;
+      const unsigned gsz = min(static_cast<unsigned>(kFusedGroup), gridDim.x - grp * kFusedGroup);
+      const unsigned prev = atomicAdd(a.group_ticket + grp * kBuQueueStride, 1u);
+      s_last = prev == gsz - 1;
+      if (s_last) {
+        atomicExch(a.group_ticket + grp * kBuQueueStride, 0u);
+        DBFS_LAST_ARRIVER_ACQUIRE();
+      }
+    } else {
+      const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+      s_last = prev == gridDim.x - 1;
+      if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+    }
   }
   __syncthreads();
   if (!s_last) return;
+  auto slot_sum = [&](const int64_t* slots, unsigned first, unsigned n, long long& c, long long& d) {
+    c = 0;
+    d = 0;
+    for (unsigned g = threadIdx.x; g < n; g += kBlock) {
+      c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(slots + 2 * (first + g)),
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      d += static_cast<long long>(__hip_atomic_load(
+          reinterpret_cast<const unsigned long long*>(slots + 2 * (first + g) + 1), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT));
+    }
+  };
   long long c = 0, d = 0;
-  for (unsigned g = threadIdx.x; g < gridDim.x; g += kBlock) {
-    c += static_cast<long long>(
-        __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * g + 1),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  if (a.group_ticket) {
+    // group total (kFusedGroup slots: the first wave), then the level ticket
+    const unsigned grp = blockIdx.x / kFusedGroup;
+    const unsigned ngroups = (gridDim.x + kFusedGroup - 1) / kFusedGroup;
+    if (wv == 0) {
+      slot_sum(a.tot, grp * kFusedGroup, min(static_cast<unsigned>(kFusedGroup), gridDim.x - grp * kFusedGroup), c, d);
+      c = wave_sum(c);
+      d = wave_sum(d);
+      if (lane_id() == 0) {
+        int64_t* gt = a.tot + 2 * kMaxFusedGrid;
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(gt + 2 * grp), static_cast<unsigned long long>(c),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(gt + 2 * grp + 1), static_cast<unsigned long long>(d),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+        s_level_last = prev == ngroups - 1;
+        if (s_level_last) DBFS_LAST_ARRIVER_ACQUIRE();
+      }
+    }
+    __syncthreads();
+    if (!s_level_last) return;
+    slot_sum(a.tot + 2 * kMaxFusedGrid, 0, ngroups, c, d);
+  } else {
+    slot_sum(a.tot, 0, gridDim.x, c, d);
   }
   c = wave_sum(c);
   d = wave_sum(d);
@@ -2335,7 +2379,9 @@ void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStrea
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
   // fused finish: at most kMaxFusedGrid / 8 workgroups striding over the units
-  const unsigned grid = a.fuse_scan ? grid_for(a.words, kUnitWords * kUnitsPerBlock, kMaxFusedGrid / 8)
+  // with one ticket; up to kMaxFusedGrid with the two-level ticket
+  const unsigned grid = a.fuse_scan ? grid_for(a.words, kUnitWords * kUnitsPerBlock,
+                                               a.group_ticket ? kMaxFusedGrid : kMaxFusedGrid / 8)
                                     : grid_for(a.words, kUnitWords * kUnitsPerBlock);
   update_kernel<<<grid, kBlock, 0, st>>>(a);
 }
