@@ -94,6 +94,8 @@ def parse_args(argv=None):
                     help="measure the reference algorithm (--mode ref) on the same graph in this process")
     ap.add_argument("--baseline-roots", type=int, default=2)
     ap.add_argument("--per-level", action="store_true", help="print per-level records of the first timed run")
+    ap.add_argument("--python-loop", action="store_true",
+                    help="time one bfs.run() call per root instead of one native run_many()")
     ap.add_argument("--spawn-timeout", type=float, default=1500.0,
                     help="self-spawned ranks: seconds before the children are killed")
     return ap.parse_args(argv)
@@ -149,11 +151,15 @@ def spawn_ranks(n: int, argv, timeout_s: float) -> int:
 
 # ---- measurement ---------------------------------------------------------------
 
+PYTHON_LOOP = False
+
+
 def timed_pass(bfs, rt, roots):
     rt.barrier()
     rt.backend.synchronize()
     t_start = time.perf_counter()
-    results = [bfs.run(r) for r in roots]
+    # back to back in native code (--python-loop: one bfs.run per root)
+    results = [bfs.run(r) for r in roots] if PYTHON_LOOP else bfs.run_many(roots)
     rt.backend.synchronize()
     rt.barrier()
     wall_ms = (time.perf_counter() - t_start) * 1e3
@@ -162,6 +168,8 @@ def timed_pass(bfs, rt, roots):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    global PYTHON_LOOP
+    PYTHON_LOOP = args.python_loop
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv, args.spawn_timeout)

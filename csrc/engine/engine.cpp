@@ -1271,7 +1271,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   RunResult res;
   res.source = source;
   be_.reset_events();
-  comm_.barrier();
+  // Several ranks: the runs start together.  One rank: no synchronize -- the
+  // previous run's speculative trailing chain may still be executing, and
+  // this run's initialisation queues right behind it on the stream instead of
+  // after a host wake-up (nothing below touches host-visible state the
+  // trailing chain writes: see the mailbox note above).
+  if (xc || opt_.phase_timing) comm_.barrier();
   const auto t0 = std::chrono::steady_clock::now();
 
   begin_run_scratch();

@@ -579,6 +579,20 @@ PYBIND11_MODULE(_dbfs_native, m) {
             return r;
           },
           py::arg("source"))
+      .def(
+          "run_many",
+          [](Engine& e, const std::vector<int64_t>& sources) {
+            // back-to-back traversals without a return to Python between them
+            // (each complete before the next one's initialisation runs)
+            std::vector<RunResult> out;
+            out.reserve(sources.size());
+            {
+              py::gil_scoped_release rel;
+              for (int64_t s : sources) out.push_back(e.run(s));
+            }
+            return out;
+          },
+          py::arg("sources"))
       .def("levels_local",
            [](const Engine& e) {
              std::vector<lvl_t> v;

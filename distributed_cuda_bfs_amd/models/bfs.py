@@ -132,6 +132,12 @@ class BFS:
     def run(self, source: int) -> BFSResult:
         return BFSResult.from_native(self.engine.run(int(source)))
 
+    def run_many(self, sources) -> List[BFSResult]:
+        """One complete traversal per source, back to back in native code (no
+        return to Python between them: the host gap between two traversals is
+        the engine's own).  Collective like run()."""
+        return [BFSResult.from_native(r) for r in self.engine.run_many([int(s) for s in sources])]
+
     def levels(self) -> np.ndarray:
         """Full per-vertex level array of the last run (collective)."""
         return self.engine.gather_levels()

@@ -583,3 +583,18 @@ def test_validator_counts(rt):
     b.run(src)
     assert list(b.engine.validate(int(src))) == [0, 0, 0]
     assert list(b.engine.validate(int(other))) == [0, 0, 2]
+
+
+def test_run_many_matches_single_runs(rt):
+    """run_many: back-to-back traversals in native code give the same per-run
+    results as one run() per source, and the last one's levels stay readable."""
+    p = dbfs.rmat_params(11, 16, 13)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, rt, mode="do")
+    srcs = bfs.sample_roots(5, seed=3)
+    singles = [bfs.run(s) for s in srcs]
+    many = bfs.run_many(srcs)
+    assert [r.source for r in many] == list(srcs)
+    for a, b in zip(singles, many):
+        assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
+    assert np.array_equal(bfs.levels(), _oracle(csr, srcs[-1]))

@@ -828,3 +828,21 @@ def test_td_fused_finish_gpu(gpu_runtime, mode):
     bfs.engine.set_option("td_fused_finish", 1)
     for src in bfs.sample_roots(3, seed=9):
         _check(bfs, csr, src)
+
+
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_run_many_gpu(gpu_runtime, mode):
+    """run_many on the GPU: back-to-back device-loop traversals without a
+    return to Python give the oracle's reach / depth per root, and the last
+    run's levels exactly."""
+    p = dbfs.rmat_params(17, 16, 29)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+    srcs = bfs.sample_roots(6, seed=31)
+    res = bfs.run_many(srcs)
+    for r, s in zip(res, srcs):
+        exp = dbfs.cpu_bfs(csr, s)[0]
+        assert r.source == s
+        assert r.reached == int(np.count_nonzero(exp != dbfs.UNREACHED))
+        assert r.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
+    assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, srcs[-1])[0])
