@@ -130,6 +130,11 @@ __device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                \
     }                                                                 \
   } while (0)
+// Bottom-up compacted waves: batches of row records prefetched ahead (1: the
+// next batch's while this one probes; 2: the next two).
+#ifndef DBFS_BU_PF
+#define DBFS_BU_PF 1
+#endif
 #ifndef DBFS_TD_DIRECT_PROBE_VISITED
 #define DBFS_TD_DIRECT_PROBE_VISITED 1
 #endif
@@ -1839,6 +1844,15 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   vid_t n_u;
   fetch(0, n_loc, n_rs, n_len, n_u);
   if (!head) n_u = n_len ? col[n_rs] : 0u;
+#if DBFS_BU_PF >= 2
+  // two batches' records in flight (the one after next as well)
+  int p_loc;
+  eid_t p_rs;
+  uint32_t p_len;
+  vid_t p_u;
+  fetch(1, p_loc, p_rs, p_len, p_u);
+  if (!head) p_u = p_len ? col[p_rs] : 0u;
+#endif
   int cnt32 = 0;
   // deferred row scans (kQueue): base = the unit's first row offset
   eid_t q_base = 0;
@@ -1890,7 +1904,15 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     const int loc = n_loc;
     const eid_t rs = n_rs, e = n_rs + n_len;
     const vid_t u0 = n_u;
+#if DBFS_BU_PF >= 2
+    n_loc = p_loc;
+    n_rs = p_rs;
+    n_len = p_len;
+    n_u = p_u;
+    fetch(b + 2, p_loc, p_rs, p_len, p_u);  // in flight during the next two batches
+#else
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
+#endif
     bool found = false;
     if (rs < e && !a.heads_done) {
       found = bu_probe<kHub>(fr, s_hub, u0);
@@ -1898,7 +1920,11 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     BU_STAT(0, 1);
     BU_STAT(1, __popcll(__ballot(loc >= 0)));
     BU_STAT(2, __popcll(__ballot(found)));
+#if DBFS_BU_PF >= 2
+    if (!head) p_u = p_len ? col[p_rs] : 0u;
+#else
     if (!head) n_u = n_len ? col[n_rs] : 0u;
+#endif
     if constexpr (kQueue > 0) {
       // found by the head: settled now; unresolved rows with more neighbours
       // are queued (huge rows / spans scanned in place)
