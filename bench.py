@@ -34,7 +34,13 @@ Honesty fields:
     on MI355X in round 1 is used for the 1-GPU RMAT-26
     configuration and vs_baseline is null elsewhere.
   * ``comm`` / ``comm_ranks`` / ``devices``: the communicator the ranks formed
-    (rccl for N > 1 GPUs) and each rank's HIP device.
+    (N > 1 GPUs: ``peer+rccl``, peer-memory collective kernels over xGMI with
+    RCCL for large payloads, or ``rccl`` if the peer self-test fails) and each
+    rank's HIP device.
+
+The K timed traversals run back to back in native code (``BFS.run_many``;
+``--python-loop`` times one ``bfs.run`` call per root instead); each one is
+complete before the next one's initialisation runs (stream order).
 """
 from __future__ import annotations
 
