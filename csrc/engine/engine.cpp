@@ -84,6 +84,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
+  else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
@@ -132,6 +133,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
+          {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
@@ -1199,7 +1201,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   }
   const int64_t nbins = div_up(W * kWordBits, int64_t(1) << bin_shift);
   const bool binned = !xc && opt_.td_bin_edges > 0 && opt_.mode != Mode::BottomUp && bin_shift <= kBinMaxShift &&
-                      g_.nnz() > 0;
+                      g_.nnz() > 0 && g_.rows() >= opt_.td_bin_min_rows;
   if (binned && bin_buf_.size() < static_cast<size_t>(g_.nnz())) {
     bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins));
     bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
@@ -1861,7 +1863,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
     if (sparse_cap > 0) lim = std::min(lim, sparse_cap);  // (a sparse chain must stay live for mf)
     if (sparse && mf <= static_cast<double>(lim)) return 'S';
-    return binned && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
+    bool after_bu = false;  // (binned only before the run's first bottom-up level)
+    for (int k = 0; k < L && !after_bu; ++k) after_bu = enq_form[static_cast<size_t>(k)] == 'B';
+    return binned && !after_bu && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
   };
   // the chain enqueued for level L is live for a level with direction `dir`
   // and mf global frontier edges

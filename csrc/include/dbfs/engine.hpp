@@ -132,8 +132,17 @@ struct EngineOptions {
   int64_t td_direct_edges = int64_t(1) << 16;
   // Device loop, one rank: top-down levels predicted to have at least this
   // many frontier edges run binned (BinArgs: targets binned by vertex range,
-  // claimed per bin in LDS) instead of td_expand + update; 0 disables.
-  int64_t td_bin_edges = 0;
+  // claimed per bin in LDS) instead of td_expand + update; 0 disables.  Only
+  // on graphs of at least td_bin_min_rows vertices (level bytes and visited
+  // bits far past the L2: a direct level's two random lines per edge go to
+  // HBM; below, the direct level is faster -- RMAT-22 top-down) and only
+  // before the run's first bottom-up level (the shrinking levels after it are
+  // predicted from a falling frontier and are mostly far smaller).
+  // Measured, RMAT-26 per root: a 28 M-edge second-level expansion 556 ->
+  // 402 us; 1354 -> 1368 GTEPS with the bottom-up gate missing (post-bottom-up
+  // levels of 200 K edges predicted at 2 M: 58 -> 80 us).
+  int64_t td_bin_edges = int64_t(1) << 21;
+  int64_t td_bin_min_rows = int64_t(1) << 24;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.

@@ -706,12 +706,13 @@ def test_td_direct_levels_gpu(gpu_runtime, mode, direct_edges):
 def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     """One rank, binned top-down levels (targets binned by vertex range, one
     workgroup per bin claims them in LDS): every non-sparse top-down level (1),
-    large ones only (default), none (0); exact against the oracle on RMAT and
+    large ones only (2^20), none (0); exact against the oracle on RMAT and
     on a star whose centre's row spans many edge blocks."""
     p = dbfs.rmat_params(18, 16, 43)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
     bfs.engine.set_option("td_bin_edges", bin_edges)
+    bfs.engine.set_option("td_bin_min_rows", 0)  # (default: graphs of >= 2^24 vertices only)
     forms = set()
     for src in bfs.sample_roots(3, seed=47):
         res = _check(bfs, csr, src)
@@ -724,6 +725,7 @@ def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     star = dbfs.build_csr(n, np.zeros(n - 1, dtype=np.uint32), np.arange(1, n, dtype=np.uint32))
     sb = dbfs.BFS(star, gpu_runtime, mode=mode)
     sb.engine.set_option("td_bin_edges", bin_edges)
+    sb.engine.set_option("td_bin_min_rows", 0)
     _check(sb, star, 0)
     _check(sb, star, 5)
 
