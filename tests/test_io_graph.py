@@ -259,3 +259,28 @@ def test_directed_stdin_reader_and_engine(tmp_path):
                          timeout=60)
     assert out.returncode == 0, out.stderr
     assert (tmp_path / "lv.txt").read_text().split() == ["0", "1", "2", "2147483647", "3", "2147483647"]
+
+
+def test_python_partition_vectorised_matches_native():
+    """The numpy forms of Partition (owners / to_local / to_global / route /
+    split / assemble) agree with the native per-vertex answers, including an
+    N that P does not divide (reference defect D5: no out-of-range owner)."""
+    import numpy as np
+    for n, p in [(1000, 3), (4847571, 8), (5, 4), (64, 1)]:
+        part = dbfs.Partition(n, p)
+        v = np.unique(np.concatenate([np.arange(min(n, 200)), np.linspace(0, n - 1, 200).astype(np.int64)]))
+        own = part.owners(v)
+        assert own.max() < p
+        assert all(int(o) == part.owner(int(x)) for o, x in zip(own, v))
+        loc = part.to_local(v)
+        assert all(int(part.to_global(int(o), [int(l)])[0]) == int(x) for o, l, x in zip(own, loc, v))
+        buckets = part.route(v[::-1])
+        assert sum(len(b) for b in buckets) == len(v)
+        for r, b in enumerate(buckets):
+            assert all(part.owner(int(x)) == r for x in b)
+            assert list(b) == sorted(b, reverse=True)  # input order kept
+        if n <= 5000:
+            full = np.arange(n) * 3
+            assert np.array_equal(part.assemble(part.split(full)), full)
+    with pytest.raises(ValueError):
+        dbfs.Partition(10, 2).owners([10])
