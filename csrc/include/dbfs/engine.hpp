@@ -236,8 +236,9 @@ struct EngineOptions {
   // 1343-1348 GTEPS on RMAT-26, alternating runs).
   bool td_dirty_words = false;
   // One rank, device loop: a dense top-down level's update finishes the
-  // level itself (as bu_fused_scan; 512 workgroups striding over the units,
-  // per-workgroup totals slots): no scan launch unless a compaction follows.
+  // level itself (as bu_fused_scan; per-workgroup totals slots, 512
+  // workgroups striding over the units with one ticket, the full grid with
+  // td_group_ticket): no scan launch unless a compaction follows.
   // RMAT-26 1344 / 1341 -> 1363 / 1353 GTEPS; top-down only equal within noise.
   // (A first version with one workgroup per 4 units and totals atomics on
   // one address: level 1 of RMAT-26 38 -> 117 us.)
