@@ -85,6 +85,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
+  else if (name == "td_bin_log2_bins") o.td_bin_log2_bins = static_cast<int64_t>(v);
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
@@ -134,6 +135,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
+          {"td_bin_log2_bins", static_cast<double>(o.td_bin_log2_bins)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
@@ -1196,13 +1198,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   {
     int bits = 0;
     while ((int64_t(1) << bits) < W * kWordBits) ++bits;
-    bin_shift = std::min(std::max(bits - 8, 12), kBinMaxShift);
+    bin_shift = std::min(std::max(bits - static_cast<int>(opt_.td_bin_log2_bins), 12), kBinMaxShift);
     while (bin_shift <= kBinMaxShift && div_up(W * kWordBits, int64_t(1) << bin_shift) > kBinMaxBins) ++bin_shift;
   }
   const int64_t nbins = div_up(W * kWordBits, int64_t(1) << bin_shift);
   const bool binned = !xc && opt_.td_bin_edges > 0 && opt_.mode != Mode::BottomUp && bin_shift <= kBinMaxShift &&
                       g_.nnz() > 0 && g_.rows() >= opt_.td_bin_min_rows;
-  if (binned && bin_buf_.size() < static_cast<size_t>(g_.nnz())) {
+  if (binned && (bin_buf_.size() < static_cast<size_t>(g_.nnz()) ||
+                 bin_cnt_.size() < static_cast<size_t>(nbins * kBinGrid))) {
     bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins));
     bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
     bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz

@@ -143,6 +143,11 @@ struct EngineOptions {
   // levels of 200 K edges predicted at 2 M: 58 -> 80 us).
   int64_t td_bin_edges = int64_t(1) << 21;
   int64_t td_bin_min_rows = int64_t(1) << 24;
+  // ... about 2^td_bin_log2_bins bins (of >= 4096 vertices, at most
+  // kBinMaxBins; each bin's visited slice must fit LDS).  RMAT-26, the 28 M-edge
+  // binned level: 256 / 512 / 1024 bins 407 / 417 / 441 us (more bins: the
+  // fill pass scatters into more open lines).
+  int64_t td_bin_log2_bins = 8;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
