@@ -142,7 +142,9 @@ struct EngineOptions {
   // 402 us; 1354 -> 1368 GTEPS with the bottom-up gate missing (post-bottom-up
   // levels of 200 K edges predicted at 2 M: 58 -> 80 us).
   int64_t td_bin_edges = int64_t(1) << 21;
-  int64_t td_bin_min_rows = int64_t(1) << 24;
+  // (2^26: RMAT-24, 2^24 vertices, measured 2 % slower binned -- 785 / 793
+  // against 815 / 800 GTEPS; RMAT-26 +2-4 %; RMAT-27 flat)
+  int64_t td_bin_min_rows = int64_t(1) << 26;
   // ... about 2^td_bin_log2_bins bins (of >= 4096 vertices, at most
   // kBinMaxBins; each bin's visited slice must fit LDS).  RMAT-26, the 28 M-edge
   // binned level: 256 / 512 / 1024 bins 407 / 417 / 441 us (more bins: the

@@ -712,7 +712,7 @@ def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
     bfs.engine.set_option("td_bin_edges", bin_edges)
-    bfs.engine.set_option("td_bin_min_rows", 0)  # (default: graphs of >= 2^24 vertices only)
+    bfs.engine.set_option("td_bin_min_rows", 0)  # (default: graphs of >= 2^26 vertices only)
     forms = set()
     for src in bfs.sample_roots(3, seed=47):
         res = _check(bfs, csr, src)
