@@ -53,6 +53,21 @@ std::vector<int64_t> Comm::allgather_host_i64(int64_t x) {
   return h;
 }
 
+void Comm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) {
+  const int P = size();
+  DBFS_CHECK(stride_words >= cap + 1, "alltoall_lists: stride below the list capacity");
+  std::vector<int64_t> cnt(static_cast<size_t>(P), static_cast<int64_t>(cap + 1)), off(static_cast<size_t>(P));
+  for (int p = 0; p < P; ++p) off[p] = static_cast<int64_t>(p) * static_cast<int64_t>(stride_words);
+  alltoallv(send, cnt.data(), off.data(), recv, cnt.data(), off.data(), sizeof(uint32_t));
+}
+
+void Comm::allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) {
+  group_start();
+  allgather(send, recv, bytes);
+  allreduce_sum_i64(buf, count);
+  group_end();
+}
+
 // ---- LocalComm ----------------------------------------------------------------
 
 void LocalComm::alltoall(const void* send, void* recv, size_t bytes) {

@@ -118,8 +118,18 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
 
 PeerComm::~PeerComm() {
   if (be_ && watch_installed_) {
+    // collectives run on the communication stream, the kernels that write
+    // into peers' windows directly on the compute stream: both drained
     hipStreamSynchronize(static_cast<hipStream_t>(be_->stream_handle()));
+    hipStreamSynchronize(S(be_));
     be_->set_wait_watch(prev_watch_);
+    // no rank unmaps or frees a window while a peer may still write into it
+    // or read it (a peer that failed closes its socket: the barrier throws at
+    // once and is ignored -- nothing of that peer is in flight any more)
+    try {
+      boot_->barrier();
+    } catch (const std::exception&) {
+    }
   }
   release();
 }
@@ -146,43 +156,74 @@ namespace {
 int unit_for(uintptr_t x) { return (x % 16 == 0) ? 16 : (x % 8 == 0) ? 8 : 4; }
 }  // namespace
 
-void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& recv, bool self_direct,
-                   int64_t sum_count, int64_t* sum_out) {
+void PeerComm::run(const Plan& plan) {
   const int P = size_;
   const uint64_t s = ++seq_;
   const int b = static_cast<int>(s & 1);
   const hipStream_t st = S(be_);
   HIP_CHECK(hipSetDevice(be_->device_id()));
+  const bool has_copy = !plan.send.empty();
+  const bool has_sum = plan.sum_count > 0;
+  // slot layout per sender: [segment 0 (copy), padded to 16 B][segment 1 (sum input)]
+  int64_t seg0_max = 0;
+  if (has_copy)
+    for (int p = 0; p < P; ++p) seg0_max = std::max(seg0_max, plan.send[p].bytes);
+  const int64_t off2 = has_copy ? (seg0_max + 15) / 16 * 16 : 0;
+  DBFS_CHECK(static_cast<size_t>(off2 + plan.sum_count * 8) <= slot_, "PeerComm: collective larger than a window slot");
+  // this rank's own segment 0 goes straight to its destination (self_direct);
+  // its all-reduce input goes through its own window like every peer's, so
+  // then it waits for its own flag too
+  const bool self_copy_direct = has_copy && plan.self_direct;
+  const bool self_flag = has_sum || !self_copy_direct;
   int unit = 16;
+  auto fit = [&](const void* x) { unit = std::min(unit, unit_for(reinterpret_cast<uintptr_t>(x))); };
   kern::PeerPushArgs pa;
   pa.npeers = P;
   pa.seq = s;
   pa.ticket = ticket_;
-  for (int p = 0; p < P; ++p) {
-    const bool direct = self_direct && p == rank_;
-    pa.src[p] = send[p].src;
-    pa.bytes[p] = send[p].bytes;
-    pa.dst[p] = direct ? recv[p].dst : slot_ptr(p, b, rank_);
-    pa.flag[p] = direct ? nullptr : reinterpret_cast<uint64_t*>(peer_[p]) + rank_;
-    if (direct && pa.src[p] == pa.dst[p]) pa.bytes[p] = 0;  // in place
-    if (pa.bytes[p] > 0)
-      unit = std::min({unit, unit_for(reinterpret_cast<uintptr_t>(pa.src[p])),
-                       unit_for(reinterpret_cast<uintptr_t>(pa.dst[p])), unit_for(static_cast<uintptr_t>(pa.bytes[p]))});
-  }
   kern::PeerUnpackArgs ua;
   ua.npeers = P;
+  ua.counted = plan.counted;
   for (int p = 0; p < P; ++p) {
-    const bool direct = self_direct && p == rank_;
-    ua.src[p] = slot_ptr(rank_, b, p);
-    ua.dst[p] = recv[p].dst;
-    ua.bytes[p] = direct || sum_count > 0 ? 0 : recv[p].bytes;
-    if (ua.bytes[p] > 0)
-      unit = std::min({unit, unit_for(reinterpret_cast<uintptr_t>(ua.dst[p])), unit_for(static_cast<uintptr_t>(ua.bytes[p]))});
+    char* slot = slot_ptr(p, b, rank_);
+    const bool direct = self_copy_direct && p == rank_;
+    if (has_copy) {
+      pa.src[p] = plan.send[p].src;
+      pa.bytes[p] = plan.send[p].bytes;
+      pa.dst[p] = direct ? plan.recv[p].dst : slot;
+      if (plan.counted) pa.count[p] = static_cast<const uint32_t*>(plan.send[p].src);
+      if (direct && pa.src[p] == pa.dst[p]) pa.bytes[p] = 0;  // in place
+      if (pa.bytes[p] > 0) {
+        fit(pa.src[p]);
+        fit(pa.dst[p]);
+        unit = std::min(unit, unit_for(static_cast<uintptr_t>(pa.bytes[p])));
+      }
+      // unpack: the piece rank p left in this rank's window
+      ua.src[p] = slot_ptr(rank_, b, p);
+      ua.dst[p] = plan.recv[p].dst;
+      ua.bytes[p] = (self_copy_direct && p == rank_) ? 0 : plan.recv[p].bytes;
+      if (ua.bytes[p] > 0) {
+        fit(ua.dst[p]);
+        unit = std::min(unit, unit_for(static_cast<uintptr_t>(ua.bytes[p])));
+      }
+    }
+    if (has_sum) {
+      pa.dst2[p] = slot + off2;
+      ua.sum_src[p] = slot_ptr(rank_, b, p) + off2;
+    }
+    pa.flag[p] = (p == rank_ && !self_flag) ? nullptr : reinterpret_cast<uint64_t*>(peer_[p]) + rank_;
+  }
+  if (has_sum) {
+    pa.src2 = plan.sum_buf;
+    pa.bytes2 = plan.sum_count * 8;
+    fit(plan.sum_buf);
+    unit = std::min(unit, 8);
+    ua.sum_count = plan.sum_count;
+    ua.sum_out = plan.sum_buf;
   }
   DBFS_CHECK(unit >= 4, "PeerComm payloads must be multiples of 4 bytes, 4-byte aligned");
+  DBFS_CHECK(!plan.counted || unit >= 4, "PeerComm: counted lists need 4-byte granules");
   pa.unit = ua.unit = unit;
-  ua.sum_count = sum_count;
-  ua.sum_out = sum_out;
   const bool fused = fused_;
   if (!fused) {
     kern::peer_push(pa, st);
@@ -191,7 +232,7 @@ void PeerComm::run(const std::vector<Piece>& send, const std::vector<Piece>& rec
   kern::PeerWaitArgs wa;
   wa.flags = reinterpret_cast<const uint64_t*>(win_);
   wa.npeers = P;
-  wa.skip = self_direct ? rank_ : -1;
+  wa.skip = self_flag ? -1 : rank_;
   wa.seq = s;
   // (a peer that is minutes late is dead: the device-side wait gives up after
   // at most 60 s so a hung job frees the GPU and reports the error)
@@ -219,12 +260,14 @@ void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
     inner_->alltoall(send, recv, bytes);
     return;
   }
-  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  Plan pl;
+  pl.send.resize(static_cast<size_t>(size_));
+  pl.recv.resize(static_cast<size_t>(size_));
   for (int p = 0; p < size_; ++p) {
-    sp[p] = {static_cast<const char*>(send) + p * bytes, nullptr, static_cast<int64_t>(bytes)};
-    rp[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+    pl.send[p] = {static_cast<const char*>(send) + p * bytes, nullptr, static_cast<int64_t>(bytes)};
+    pl.recv[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
   }
-  run(sp, rp, true, 0, nullptr);
+  run(pl);
 }
 
 void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
@@ -234,12 +277,14 @@ void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
     inner_->allgather(send, recv, bytes);
     return;
   }
-  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  Plan pl;
+  pl.send.resize(static_cast<size_t>(size_));
+  pl.recv.resize(static_cast<size_t>(size_));
   for (int p = 0; p < size_; ++p) {
-    sp[p] = {send, nullptr, static_cast<int64_t>(bytes)};
-    rp[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+    pl.send[p] = {send, nullptr, static_cast<int64_t>(bytes)};
+    pl.recv[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
   }
-  run(sp, rp, true, 0, nullptr);
+  run(pl);
 }
 
 void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
@@ -250,31 +295,89 @@ void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
     if (count) inner_->allreduce_sum_i64(buf, count);
     return;
   }
-  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
-  for (int p = 0; p < size_; ++p) {
-    sp[p] = {buf, nullptr, static_cast<int64_t>(bytes)};
-    rp[p] = {nullptr, nullptr, static_cast<int64_t>(bytes)};
-  }
-  run(sp, rp, false, static_cast<int64_t>(count), buf);
+  Plan pl;
+  pl.sum_count = static_cast<int64_t>(count);
+  pl.sum_buf = buf;
+  run(pl);
 }
 
 void PeerComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                          const int64_t* rd, size_t eb) {
   note_alltoallv(sc, eb);
-  bool fits = eb % 4 == 0;
-  for (int p = 0; p < size_ && fits; ++p)
-    fits = static_cast<size_t>(std::max(sc[p], rc[p])) * eb <= slot_;
+  // Window or inner communicator: the choice must be the same on every rank
+  // (a rank in the peer kernel waits for flags that a rank gone to the inner
+  // communicator never sends), but the counts are this rank's own: the pieces
+  // through the windows -- every one but the self piece, which the push copies
+  // directly -- are agreed over the inner communicator.  (Host counts imply a
+  // host round trip already; the engine's device-loop lists use
+  // alltoall_lists, whose choice depends only on the uniform capacity.)
+  int64_t mx = 0;
+  for (int p = 0; p < size_; ++p)
+    if (p != rank_) mx = std::max(mx, std::max(sc[p], rc[p]) * static_cast<int64_t>(eb));
+  const bool fits_here = eb % 4 == 0 && static_cast<size_t>(mx) <= slot_;
+  const bool fits = inner_->sum_host(fits_here ? 0 : 1) == 0;
   if (!fits) {
     ++inner_ops_;
     inner_->alltoallv(send, sc, sd, recv, rc, rd, eb);
     return;
   }
-  std::vector<Piece> sp(static_cast<size_t>(size_)), rp(static_cast<size_t>(size_));
+  Plan pl;
+  pl.send.resize(static_cast<size_t>(size_));
+  pl.recv.resize(static_cast<size_t>(size_));
   for (int p = 0; p < size_; ++p) {
-    sp[p] = {static_cast<const char*>(send) + sd[p] * eb, nullptr, sc[p] * static_cast<int64_t>(eb)};
-    rp[p] = {nullptr, static_cast<char*>(recv) + rd[p] * eb, rc[p] * static_cast<int64_t>(eb)};
+    pl.send[p] = {static_cast<const char*>(send) + sd[p] * eb, nullptr, sc[p] * static_cast<int64_t>(eb)};
+    pl.recv[p] = {nullptr, static_cast<char*>(recv) + rd[p] * eb, rc[p] * static_cast<int64_t>(eb)};
   }
-  run(sp, rp, true, 0, nullptr);
+  run(pl);
+}
+
+void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) {
+  const int64_t piece = static_cast<int64_t>(cap + 1) * 4;
+  // (the choice depends only on the capacity, the same on every rank)
+  if (static_cast<size_t>(piece) > slot_ || stride_words % 4 != 0 || stride_words < cap + 1) {
+    ++inner_ops_;
+    note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);
+    inner_->alltoall_lists(send, recv, stride_words, cap);  // cap + 1 words per peer over the inner communicator
+    return;
+  }
+  // (traffic accounted at the capacity, as the default exchange: the device
+  // counts are not read back)
+  note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);
+  // count-sized: each piece is its list's n + 1 words, read on the device
+  // (rounded up to 16 B, at most the stride)
+  const int64_t stride_b = static_cast<int64_t>(stride_words) * 4;
+  const int64_t cap_b = std::min<int64_t>((piece + 15) / 16 * 16, stride_b);
+  Plan pl;
+  pl.counted = true;
+  pl.send.resize(static_cast<size_t>(size_));
+  pl.recv.resize(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    pl.send[p] = {send + p * stride_words, nullptr, cap_b};
+    pl.recv[p] = {nullptr, recv + p * stride_words, cap_b};
+  }
+  run(pl);
+}
+
+void PeerComm::allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) {
+  const size_t need = (bytes + 15) / 16 * 16 + count * sizeof(int64_t);
+  if (need > slot_ || bytes % 4 || count == 0) {
+    allgather(send, recv, bytes);  // two collectives
+    allreduce_sum_i64(buf, count);
+    return;
+  }
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  note_fused();
+  Plan pl;
+  pl.send.resize(static_cast<size_t>(size_));
+  pl.recv.resize(static_cast<size_t>(size_));
+  for (int p = 0; p < size_; ++p) {
+    pl.send[p] = {send, nullptr, static_cast<int64_t>(bytes)};
+    pl.recv[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+  }
+  pl.sum_count = static_cast<int64_t>(count);
+  pl.sum_buf = buf;
+  run(pl);
 }
 
 bool PeerComm::self_test(std::string* why) {

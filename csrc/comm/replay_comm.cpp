@@ -1,0 +1,180 @@
+// Record / replay communicators: one rank of a P-rank job measured alone on
+// one GPU ("shadow rank").
+//
+// RecordComm wraps rank r's communicator in a real P-rank run (virtual ranks
+// on one GPU, or processes) and keeps every collective's OUTPUT on the host,
+// in call order: what the other ranks contributed, as this rank saw it.
+// ReplayComm then stands in for the whole job with rank r running alone: each
+// collective checks that it is the next recorded one (kind and sizes) and
+// writes the recorded output with one stream-ordered device copy.  Rank r's
+// kernels therefore see exactly the inputs they saw in the P-rank run (remote
+// frontier slices, candidates, all-reduced totals -- the traversal is
+// deterministic given them), but own the whole GPU: their times are the
+// per-rank compute of a P-GPU job, which no single-GPU box can otherwise
+// measure.  The per-device step of the reference being replaced is the
+// launch-per-device + synchronize of bfs.cu:577-591 / bfs_mpi.cu:586-593.
+#include <cstring>
+
+#include "dbfs/comm.hpp"
+
+namespace dbfs {
+
+namespace {
+const char* kind_name(int k) {
+  switch (k) {
+    case Comm::kAllToAll: return "alltoall";
+    case Comm::kAllGather: return "allgather";
+    case Comm::kAllReduce: return "allreduce";
+    case Comm::kAllToAllV: return "alltoallv";
+    case Comm::kBarrier: return "barrier";
+  }
+  return "?";
+}
+}  // namespace
+
+int64_t CommTape::bytes() const {
+  int64_t b = 0;
+  for (const auto& r : recs) b += static_cast<int64_t>(r.data.size());
+  return b;
+}
+
+// ---- RecordComm -------------------------------------------------------------
+
+RecordComm::RecordComm(std::shared_ptr<Comm> inner) : inner_(std::move(inner)), tape_(std::make_shared<CommTape>()) {
+  DBFS_CHECK(inner_ != nullptr, "RecordComm needs an inner communicator");
+  tape_->rank = inner_->rank();
+  tape_->size = inner_->size();
+}
+
+void RecordComm::push(int kind, int64_t a, int64_t b, const void* dev, size_t bytes) {
+  CommTape::Rec r;
+  r.kind = kind;
+  r.a = a;
+  r.b = b;
+  r.data.resize(bytes);
+  if (bytes) be_->to_host(&r.data[0], dev, bytes);  // (blocking: after the collective)
+  tape_->recs.push_back(std::move(r));
+}
+
+void RecordComm::alltoall(const void* send, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
+  inner_->alltoall(send, recv, bytes);
+  push(kAllToAll, static_cast<int64_t>(bytes), 0, recv, bytes * static_cast<size_t>(size()));
+}
+
+void RecordComm::allgather(const void* send, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
+  inner_->allgather(send, recv, bytes);
+  push(kAllGather, static_cast<int64_t>(bytes), 0, recv, bytes * static_cast<size_t>(size()));
+}
+
+void RecordComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  inner_->allreduce_sum_i64(buf, count);
+  push(kAllReduce, static_cast<int64_t>(count), 0, buf, count * sizeof(int64_t));
+}
+
+void RecordComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                           const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
+  inner_->alltoallv(send, sc, sd, recv, rc, rd, eb);
+  // the received pieces in rank order, concatenated
+  int64_t tot = 0;
+  for (int p = 0; p < size(); ++p) tot += rc[p];
+  CommTape::Rec r;
+  r.kind = kAllToAllV;
+  r.a = tot;
+  r.b = static_cast<int64_t>(eb);
+  r.data.resize(static_cast<size_t>(tot) * eb);
+  size_t off = 0;
+  for (int p = 0; p < size(); ++p) {
+    const size_t n = static_cast<size_t>(rc[p]) * eb;
+    if (n) be_->to_host(&r.data[off], static_cast<const char*>(recv) + rd[p] * eb, n);
+    off += n;
+  }
+  tape_->recs.push_back(std::move(r));
+}
+
+void RecordComm::barrier() {
+  note(kBarrier, 0);
+  inner_->barrier();
+  push(kBarrier, 0, 0, nullptr, 0);
+}
+
+double RecordComm::max_host(double x) { return inner_->max_host(x); }  // (timing only: not recorded)
+
+// ---- ReplayComm -------------------------------------------------------------
+
+ReplayComm::ReplayComm(std::shared_ptr<CommTape> tape, Backend& be) : tape_(std::move(tape)) {
+  DBFS_CHECK(tape_ != nullptr, "ReplayComm needs a tape");
+  bind_backend(&be);
+  // every recorded output in one device buffer: a replayed collective is then
+  // a device-to-device copy on the stream (no host round trip, no pinned
+  // staging that would stall the enqueue-ahead level loop)
+  const int64_t total = tape_->bytes();
+  dev_ = DBuf<char>(be, static_cast<size_t>(std::max<int64_t>(total, 16)));
+  off_.reserve(tape_->recs.size());
+  int64_t off = 0;
+  for (const auto& r : tape_->recs) {
+    off_.push_back(off);
+    if (!r.data.empty()) be.to_device(dev_.data() + off, r.data.data(), r.data.size());
+    off += static_cast<int64_t>(r.data.size());
+  }
+}
+
+const CommTape::Rec& ReplayComm::next(int kind, int64_t a, int64_t b, size_t* idx) {
+  DBFS_CHECK(pos_ < tape_->recs.size(), std::string("ReplayComm: tape exhausted at a ") + kind_name(kind) +
+                                            " (the replayed rank issued more collectives than it recorded)");
+  const auto& r = tape_->recs[pos_];
+  if (r.kind != kind || r.a != a || r.b != b)
+    throw Error("ReplayComm: collective " + std::to_string(pos_) + " is a " + kind_name(kind) + "(" + std::to_string(a) +
+                ", " + std::to_string(b) + ") but the tape has a " + kind_name(r.kind) + "(" + std::to_string(r.a) +
+                ", " + std::to_string(r.b) + ")");
+  *idx = pos_++;
+  return r;
+}
+
+void ReplayComm::alltoall(const void*, void* recv, size_t bytes) {
+  note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
+  size_t i = 0;
+  const auto& r = next(kAllToAll, static_cast<int64_t>(bytes), 0, &i);
+  be_->copy_async(recv, dev_.data() + off_[i], r.data.size());
+}
+
+void ReplayComm::allgather(const void*, void* recv, size_t bytes) {
+  note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
+  size_t i = 0;
+  const auto& r = next(kAllGather, static_cast<int64_t>(bytes), 0, &i);
+  be_->copy_async(recv, dev_.data() + off_[i], r.data.size());
+}
+
+void ReplayComm::allreduce_sum_i64(int64_t* buf, size_t count) {
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  size_t i = 0;
+  const auto& r = next(kAllReduce, static_cast<int64_t>(count), 0, &i);
+  be_->copy_async(buf, dev_.data() + off_[i], r.data.size());
+}
+
+void ReplayComm::alltoallv(const void*, const int64_t* sc, const int64_t*, void* recv, const int64_t* rc,
+                           const int64_t* rd, size_t eb) {
+  note_alltoallv(sc, eb);
+  int64_t tot = 0;
+  for (int p = 0; p < size(); ++p) tot += rc[p];
+  size_t i = 0;
+  next(kAllToAllV, tot, static_cast<int64_t>(eb), &i);
+  int64_t off = off_[i];
+  for (int p = 0; p < size(); ++p) {
+    const size_t n = static_cast<size_t>(rc[p]) * eb;
+    if (n) be_->copy_async(static_cast<char*>(recv) + rd[p] * eb, dev_.data() + off, n);
+    off += static_cast<int64_t>(n);
+  }
+}
+
+void ReplayComm::barrier() {
+  note(kBarrier, 0);
+  size_t i = 0;
+  next(kBarrier, 0, 0, &i);
+  be_->synchronize();
+}
+
+}  // namespace dbfs

@@ -54,13 +54,12 @@ void read_all(int fd, void* p, size_t n) {
 void tune_socket(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  const double t = comm_timeout_s();
-  if (t > 0) {
-    timeval tv{};
-    tv.tv_sec = static_cast<time_t>(t);
-    tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
-    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-  }
+  // (0: no limit -- also replaces the short hello timeout of an accepted socket)
+  const double t = comm_timeout_s() > 0 ? comm_timeout_s() : 0.0;
+  timeval tv{};
+  tv.tv_sec = static_cast<time_t>(t);
+  tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 
 void send_msg(int fd, const std::string& s) {
@@ -95,6 +94,20 @@ std::string recv_msg(int fd) {
   return s;
 }
 
+// Receive timeout of a freshly accepted connection's hello (a stray
+// connection that sends nothing must not stall the accept loop).
+void set_recv_timeout(int fd, double t) {
+  timeval tv{};
+  tv.tv_sec = static_cast<time_t>(t);
+  tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+}
+
+bool is_literal_ipv4(const std::string& host) {
+  in_addr x{};
+  return inet_pton(AF_INET, host.c_str(), &x) == 1;
+}
+
 sockaddr_in resolve(const std::string& host, int port) {
   sockaddr_in a{};
   a.sin_family = AF_INET;
@@ -125,8 +138,17 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_port = htons(static_cast<uint16_t>(port));
-    // listen on the rendezvous address only (not every interface)
+    // Listen on the rendezvous address only (not every interface) -- unless a
+    // host NAME resolves to a loopback address here (the usual 127.0.1.1
+    // /etc/hosts alias of the machine's own name): remote ranks reach that
+    // name at a routable address, so then every interface.
+    // DBFS_BOOTSTRAP_BIND=any|rendezvous overrides.
     a.sin_addr = resolve(host, port).sin_addr;
+    const bool loopback = (ntohl(a.sin_addr.s_addr) >> 24) == 127;
+    const char* bind_env = std::getenv("DBFS_BOOTSTRAP_BIND");
+    const std::string bind_mode = bind_env ? bind_env : "";
+    if (bind_mode == "any" || (bind_mode != "rendezvous" && loopback && !is_literal_ipv4(host)))
+      a.sin_addr.s_addr = htonl(INADDR_ANY);
     if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
       throw Error("bootstrap bind to port " + std::to_string(port) + " failed: " + std::strerror(errno));
     if (::listen(listen_fd_, nranks) != 0) throw Error("bootstrap listen failed");
@@ -140,17 +162,26 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
                     " peers connected within " + std::to_string(timeout_s) + " s");
       int fd = ::accept(listen_fd_, nullptr, nullptr);
       if (fd < 0) throw Error("bootstrap accept failed");
-      tune_socket(fd);
       uint64_t hello = 0;
       int32_t r = -1;
-      read_all(fd, &hello, sizeof(hello));
-      if (hello != kHelloMagic) {
-        // not one of our ranks: drop it and keep waiting for the real peers
+      // a rank sends its hello right after connecting: a connection silent
+      // for 10 s (or closed, or speaking another protocol) is not one of ours
+      // -- dropped, and the loop keeps waiting for the real peers
+      set_recv_timeout(fd, 10.0);
+      bool ours = false;
+      try {
+        read_all(fd, &hello, sizeof(hello));
+        ours = hello == kHelloMagic;
+        if (ours) read_all(fd, &r, sizeof(r));
+      } catch (const Error&) {
+        ours = false;
+      }
+      if (!ours) {
         ::close(fd);
         --k;
         continue;
       }
-      read_all(fd, &r, sizeof(r));
+      tune_socket(fd);
       if (r <= 0 || r >= nranks || peers_[r] != -1) throw Error("bootstrap got bad rank " + std::to_string(r));
       peers_[r] = fd;
     }

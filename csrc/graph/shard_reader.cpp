@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 #include "dbfs/shard_reader.hpp"
@@ -223,22 +224,26 @@ EdgeShard read_edge_shard(const std::string& path, int rank, int nranks, const H
                           int threads) {
   DBFS_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
   DBFS_CHECK(path != "-", "sharded reads need a file (standard input is read whole)");
-  Mapped f(path);
   EdgeShard s;
   std::string err;
   Header h;
+  // opening / mapping the file and its header: a failure on any rank (the
+  // file missing or unreadable on one node only) is agreed, so no rank is
+  // left waiting in a later exchange its peers never join
+  std::unique_ptr<Mapped> fm;
   try {
-    h = parse_header(f, path);
+    fm = std::make_unique<Mapped>(path);
+    h = parse_header(*fm, path);
   } catch (const std::exception& e) {
     err = e.what();
   }
-  // every rank reads the same header; a failure is agreed so no rank is left
-  // waiting in a later exchange
   {
     const auto st = allgather(err.empty() ? 0 : 1);
-    for (int64_t x : st)
-      if (x) throw Error(err.empty() ? "edge list header unreadable on another rank: " + path : err);
+    for (size_t r = 0; r < st.size(); ++r)
+      if (st[r])
+        throw Error(err.empty() ? "edge list unreadable on rank " + std::to_string(r) + ": " + path : err);
   }
+  const Mapped& f = *fm;
   s.n = h.n;
   s.m = h.m;
   s.format = h.mtx ? FileFormat::MatrixMarket : FileFormat::EdgeList;

@@ -60,6 +60,20 @@ class Comm {
   virtual void group_start() {}
   virtual void group_end() {}
 
+  // Owner lists whose lengths live on the device (no host round trip): rank
+  // r's list for peer p is the 32-bit words at send + p * stride_words -- word
+  // 0 its length n <= cap, then n entries -- and lands at recv + r *
+  // stride_words on peer p, length first.  The peer transport ships each
+  // list's n + 1 words, sized on the device (count-sized, as the reference's
+  // nextQueueSize-sized peer copies, bfs.cu:595-609 / bfs_mpi.cu:615-618);
+  // the default ships cap + 1 words per peer (an all-to-all-v of uniform
+  // counts).  The transport's choice may depend only on (stride, cap).
+  virtual void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap);
+  // allgather(send, recv, bytes) and allreduce_sum_i64(buf, count) as ONE
+  // collective where the transport can (peer windows: one launch, both
+  // payloads in one slot; RCCL: one group); in order otherwise.
+  virtual void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count);
+
   // Host-value helpers built on the device collectives.
   virtual int64_t sum_host(int64_t x);
   virtual double max_host(double x);
@@ -79,6 +93,9 @@ class Comm {
   struct Traffic {
     int64_t calls[kTrafficKinds] = {};
     int64_t bytes[kTrafficKinds] = {};
+    // collectives that shared another's launch (allgather_allreduce): the
+    // launches issued are sum(calls) - fused
+    int64_t fused = 0;
   };
   const Traffic& traffic() const { return traffic_; }
   void reset_traffic() { traffic_ = Traffic{}; }
@@ -88,6 +105,7 @@ class Comm {
     ++traffic_.calls[k];
     traffic_.bytes[k] += bytes;
   }
+  void note_fused() { ++traffic_.fused; }
   void note_alltoallv(const int64_t* sc, size_t eb) {
     int64_t b = 0;
     for (int p = 0; p < size(); ++p)
@@ -200,6 +218,69 @@ class NcclComm final : public Comm {
   int rank_ = 0, size_ = 1;
 };
 
+// Every collective output one rank saw, in call order (RecordComm ->
+// ReplayComm; csrc/comm/replay_comm.cpp).  kind: Comm::TrafficKind; (a, b):
+// the call's sizes (bytes per peer / count / total elements, element bytes).
+struct CommTape {
+  struct Rec {
+    int kind = 0;
+    int64_t a = 0, b = 0;
+    std::string data;
+  };
+  int rank = 0, size = 1;
+  std::vector<Rec> recs;
+  int64_t bytes() const;
+};
+
+// Forwards to `inner` and records every output on the host (blocking copies:
+// a recording run is not a timed one).
+class RecordComm final : public Comm {
+ public:
+  explicit RecordComm(std::shared_ptr<Comm> inner);
+  int rank() const override { return inner_->rank(); }
+  int size() const override { return inner_->size(); }
+  std::string name() const override { return "record+" + inner_->name(); }
+  void alltoall(const void* send, void* recv, size_t bytes) override;
+  void allgather(const void* send, void* recv, size_t bytes) override;
+  void allreduce_sum_i64(int64_t* buf, size_t count) override;
+  void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                 const int64_t* rd, size_t eb) override;
+  void barrier() override;
+  double max_host(double x) override;  // wall-time maxima: not part of the tape
+  std::shared_ptr<CommTape> tape() const { return tape_; }
+
+ private:
+  void push(int kind, int64_t a, int64_t b, const void* dev, size_t bytes);
+  std::shared_ptr<Comm> inner_;
+  std::shared_ptr<CommTape> tape_;
+};
+
+// Rank tape->rank of a tape->size-rank job, alone: every collective must be
+// the tape's next one and writes its recorded output (a device copy).
+class ReplayComm final : public Comm {
+ public:
+  ReplayComm(std::shared_ptr<CommTape> tape, Backend& be);
+  int rank() const override { return tape_->rank; }
+  int size() const override { return tape_->size; }
+  std::string name() const override { return "replay"; }
+  void alltoall(const void* send, void* recv, size_t bytes) override;
+  void allgather(const void* send, void* recv, size_t bytes) override;
+  void allreduce_sum_i64(int64_t* buf, size_t count) override;
+  void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
+                 const int64_t* rd, size_t eb) override;
+  void barrier() override;
+  double max_host(double x) override { return x; }  // this rank's own time
+  size_t position() const { return pos_; }
+  size_t length() const { return tape_->recs.size(); }
+
+ private:
+  const CommTape::Rec& next(int kind, int64_t a, int64_t b, size_t* idx);
+  std::shared_ptr<CommTape> tape_;
+  DBuf<char> dev_;
+  std::vector<int64_t> off_;
+  size_t pos_ = 0;
+};
+
 class TcpBootstrap;
 
 // Collectives through peer-mapped device memory (csrc/comm/peer_comm.cpp,
@@ -223,6 +304,8 @@ class PeerComm final : public Comm {
   void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv,
                  const int64_t* rc, const int64_t* rd, size_t eb) override;
   void barrier() override;
+  void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
+  void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
   size_t slot_bytes() const { return slot_; }
   // Every collective through the windows with known patterns (sizes up to a
   // full slot), checked on the host; the verdict is agreed over the inner
@@ -238,11 +321,20 @@ class PeerComm final : public Comm {
     void* dst = nullptr;  // final destination of a delivered piece (unpack)
     int64_t bytes = 0;
   };
-  // One collective: send[p] goes to rank p; recv[p] is where rank p's piece
-  // lands here; `self_direct`: this rank's own piece is copied straight to
-  // recv[rank] by the push (no window round trip); sum_count > 0: all-reduce.
-  void run(const std::vector<Piece>& send, const std::vector<Piece>& recv, bool self_direct, int64_t sum_count,
-           int64_t* sum_out);
+  // One collective launch: segment 0, send[p] goes to rank p and recv[p] is
+  // where rank p's piece lands here (empty: none; `counted`: pieces are owner
+  // lists sized on the device, bytes = the most they may be; `self_direct`:
+  // this rank's own piece is copied straight to recv[rank]); segment 1,
+  // sum_count > 0: all-reduce of sum_buf (every rank's input through the
+  // windows, summed in place).
+  struct Plan {
+    std::vector<Piece> send, recv;
+    bool self_direct = true;
+    bool counted = false;
+    int64_t sum_count = 0;
+    int64_t* sum_buf = nullptr;
+  };
+  void run(const Plan& plan);
   std::shared_ptr<TcpBootstrap> boot_;
   std::shared_ptr<Comm> inner_;
   int rank_ = 0, size_ = 1;

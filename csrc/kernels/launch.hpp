@@ -43,9 +43,19 @@ void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 // peer_kernels.hip (PeerComm: collectives through peer-mapped windows)
 constexpr int kMaxPeers = 16;
 struct PeerPushArgs {
-  void* dst[kMaxPeers] = {};        // destination (a peer's window slot, or a local buffer)
+  // segment 0 of the piece for peer p: src[p] -> dst[p] (a peer's window slot,
+  // or a local buffer for this rank's own piece)
+  void* dst[kMaxPeers] = {};
   const void* src[kMaxPeers] = {};
-  int64_t bytes[kMaxPeers] = {};
+  int64_t bytes[kMaxPeers] = {};    // (counted: the most it may be)
+  // counted segment 0 (owner lists): its length is read on the device -- the
+  // 32-bit word count[p] holds n, the piece is its n + 1 words (count first),
+  // rounded up to `unit`, at most bytes[p]
+  const uint32_t* count[kMaxPeers] = {};
+  // segment 1 (the all-reduce input, the same for every peer): src2 -> dst2[p]
+  void* dst2[kMaxPeers] = {};
+  const void* src2 = nullptr;
+  int64_t bytes2 = 0;
   uint64_t* flag[kMaxPeers] = {};   // flag word this rank owns in each peer's window (nullptr: none)
   int npeers = 0;
   int unit = 4;                     // copy granule (4, 8, 16 B; every size and address a multiple)
@@ -64,9 +74,11 @@ struct PeerUnpackArgs {
   void* dst[kMaxPeers] = {};
   const void* src[kMaxPeers] = {};
   int64_t bytes[kMaxPeers] = {};
+  bool counted = false;             // segment 0 counted (its first word holds n; n + 1 words, <= bytes[p])
   int npeers = 0;
   int unit = 4;
-  int64_t sum_count = 0;            // > 0: all-reduce -- sum_out[i] = sum_p src[p][i] (uint64, wrapping)
+  int64_t sum_count = 0;            // > 0: all-reduce -- sum_out[i] = sum_p sum_src[p][i] (uint64, wrapping)
+  const void* sum_src[kMaxPeers] = {};
   void* sum_out = nullptr;
 };
 void peer_push(const PeerPushArgs& a, hipStream_t st);

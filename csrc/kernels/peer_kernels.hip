@@ -50,25 +50,63 @@ __device__ __forceinline__ void grid_copy(void* __restrict__ dst, const void* __
   }
 }
 
-__global__ __launch_bounds__(kBlock) void peer_push_kernel(PeerPushArgs a) {
-  __shared__ int s_last;
-  // Workgroups are dealt to peers round-robin (group g -> peer g % P), so
-  // every xGMI link carries its share at once instead of the grid streaming
-  // to one peer after another.
+// Bytes of segment 0 for peer p: fixed, or counted from the list's first word
+// (n entries after it), rounded up to the copy granule, at most bytes[p].
+__device__ __forceinline__ int64_t seg_bytes(int64_t cap, const uint32_t* count, int unit) {
+  if (!count || cap <= 0) return cap;
+  const int64_t b = (static_cast<int64_t>(*count) + 1) * 4;
+  const int64_t r = (b + unit - 1) / unit * unit;
+  return r < cap ? r : cap;
+}
+
+// The push of every piece by the grid: workgroups are dealt to peers
+// round-robin (group g -> peer g % P), so every xGMI link carries its share at
+// once instead of the grid streaming to one peer after another.
+__device__ __forceinline__ void push_pieces(const PeerPushArgs& a, int nthreads) {
   const int P = a.npeers;
+  const int t = threadIdx.x;
   const int groups = static_cast<int>(gridDim.x) / P;
   if (groups > 0) {
     const int p = static_cast<int>(blockIdx.x) % P;
     const int g = static_cast<int>(blockIdx.x) / P;
-    if (g < groups && a.bytes[p] > 0)
-      grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, static_cast<int64_t>(g) * kBlock + threadIdx.x,
-                static_cast<int64_t>(groups) * kBlock);
+    if (g < groups) {
+      const int64_t gt = static_cast<int64_t>(g) * nthreads + t, nt = static_cast<int64_t>(groups) * nthreads;
+      const int64_t b = seg_bytes(a.bytes[p], a.count[p], a.unit);
+      if (b > 0) grid_copy(a.dst[p], a.src[p], b, a.unit, gt, nt);
+      if (a.bytes2 > 0 && a.dst2[p]) grid_copy(a.dst2[p], a.src2, a.bytes2, a.unit, gt, nt);
+    }
   } else {
-    const int64_t nt = static_cast<int64_t>(gridDim.x) * kBlock;
-    const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    for (int q = 0; q < P; ++q)
-      if (a.bytes[q] > 0) grid_copy(a.dst[q], a.src[q], a.bytes[q], a.unit, t, nt);
+    const int64_t nt = static_cast<int64_t>(gridDim.x) * nthreads;
+    const int64_t gt = static_cast<int64_t>(blockIdx.x) * nthreads + t;
+    for (int q = 0; q < P; ++q) {
+      const int64_t b = seg_bytes(a.bytes[q], a.count[q], a.unit);
+      if (b > 0) grid_copy(a.dst[q], a.src[q], b, a.unit, gt, nt);
+      if (a.bytes2 > 0 && a.dst2[q]) grid_copy(a.dst2[q], a.src2, a.bytes2, a.unit, gt, nt);
+    }
   }
+}
+
+// The unpack of the landed slots (after the flags and an acquire): segment 0
+// copied to the caller's buffers, segment 1 summed.
+__device__ __forceinline__ void unpack_pieces(const PeerUnpackArgs& a, int64_t gt, int64_t nt) {
+  if (a.sum_count > 0) {
+    // all-reduce: out[i] = sum over ranks of slot[p][i] (wrapping, as RCCL)
+    for (int64_t i = gt; i < a.sum_count; i += nt) {
+      uint64_t acc = 0;
+      for (int p = 0; p < a.npeers; ++p) acc += static_cast<const uint64_t*>(a.sum_src[p])[i];
+      static_cast<uint64_t*>(a.sum_out)[i] = acc;
+    }
+  }
+  for (int p = 0; p < a.npeers; ++p) {
+    const int64_t b =
+        seg_bytes(a.bytes[p], a.counted && a.bytes[p] > 0 ? static_cast<const uint32_t*>(a.src[p]) : nullptr, a.unit);
+    if (b > 0) grid_copy(a.dst[p], a.src[p], b, a.unit, gt, nt);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void peer_push_kernel(PeerPushArgs a) {
+  __shared__ int s_last;
+  push_pieces(a, kBlock);
   // every wave's stores complete, then the hand-off (cdna_hip_programming.md
   // Guideline 16, at system scope: the stores went to other GPUs' memory)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -113,46 +151,24 @@ __global__ void peer_wait_kernel(PeerWaitArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
-  const int64_t nt = static_cast<int64_t>(gridDim.x) * kBlock;
-  const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (a.sum_count > 0) {
-    // all-reduce: out[i] = sum over ranks of slot[p][i] (wrapping, as RCCL)
-    for (int64_t i = t; i < a.sum_count; i += nt) {
-      uint64_t acc = 0;
-      for (int p = 0; p < a.npeers; ++p) acc += static_cast<const uint64_t*>(a.src[p])[i];
-      static_cast<uint64_t*>(a.sum_out)[i] = acc;
-    }
-    return;
-  }
-  for (int p = 0; p < a.npeers; ++p)
-    if (a.bytes[p] > 0) grid_copy(a.dst[p], a.src[p], a.bytes[p], a.unit, t, nt);
+  unpack_pieces(a, static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x, static_cast<int64_t>(gridDim.x) * kBlock);
 }
 
 // A collective as ONE launch (the three above fused): push by every
 // workgroup (groups dealt to peers round-robin), the ticket hand-off whose
 // last workgroup publishes the flags behind a system-scope release, then
 // every workgroup waits for the peers' flags itself (bounded as
-// peer_wait_kernel) and unpacks its share after an acquire.  No workgroup
-// waits for another workgroup of this launch (only for the peers, whose
-// flags do not depend on it), so the grid need not be co-resident.
+// peer_wait_kernel) and unpacks its share after an acquire.  A workgroup
+// waits only for flags: the peers' (which do not depend on this launch), and
+// -- when this rank's own all-reduce input goes through its window -- its own,
+// published by this launch's last workgroup; the grid (<= kPeerFusedGroups
+// per peer) is far below the chip's residency, so that workgroup runs.
 constexpr int kFusedThreads = 256;
 __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs pa, PeerWaitArgs wa, PeerUnpackArgs ua) {
   __shared__ int s_last, s_ok;
   const int t = threadIdx.x;
   const int P = pa.npeers;
-  const int groups = static_cast<int>(gridDim.x) / P;
-  if (groups > 0) {
-    const int p = static_cast<int>(blockIdx.x) % P;
-    const int g = static_cast<int>(blockIdx.x) / P;
-    if (g < groups && pa.bytes[p] > 0)
-      grid_copy(pa.dst[p], pa.src[p], pa.bytes[p], pa.unit, static_cast<int64_t>(g) * kFusedThreads + t,
-                static_cast<int64_t>(groups) * kFusedThreads);
-  } else {
-    const int64_t nt = static_cast<int64_t>(gridDim.x) * kFusedThreads;
-    const int64_t gt = static_cast<int64_t>(blockIdx.x) * kFusedThreads + t;
-    for (int q = 0; q < P; ++q)
-      if (pa.bytes[q] > 0) grid_copy(pa.dst[q], pa.src[q], pa.bytes[q], pa.unit, gt, nt);
-  }
+  push_pieces(pa, kFusedThreads);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
@@ -188,18 +204,7 @@ __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs 
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  const int64_t nt = static_cast<int64_t>(gridDim.x) * kFusedThreads;
-  const int64_t gt = static_cast<int64_t>(blockIdx.x) * kFusedThreads + t;
-  if (ua.sum_count > 0) {
-    for (int64_t i = gt; i < ua.sum_count; i += nt) {
-      uint64_t acc = 0;
-      for (int p = 0; p < ua.npeers; ++p) acc += static_cast<const uint64_t*>(ua.src[p])[i];
-      static_cast<uint64_t*>(ua.sum_out)[i] = acc;
-    }
-    return;
-  }
-  for (int p = 0; p < ua.npeers; ++p)
-    if (ua.bytes[p] > 0) grid_copy(ua.dst[p], ua.src[p], ua.bytes[p], ua.unit, gt, nt);
+  unpack_pieces(ua, static_cast<int64_t>(blockIdx.x) * kFusedThreads + t, static_cast<int64_t>(gridDim.x) * kFusedThreads);
 }
 
 inline unsigned grid_for_bytes(int64_t bytes, int unit) {
@@ -213,7 +218,7 @@ inline unsigned grid_for_bytes(int64_t bytes, int unit) {
 
 void peer_push(const PeerPushArgs& a, hipStream_t st) {
   int64_t mx = 0;
-  for (int p = 0; p < a.npeers; ++p) mx = a.bytes[p] > mx ? a.bytes[p] : mx;
+  for (int p = 0; p < a.npeers; ++p) mx = a.bytes[p] + a.bytes2 > mx ? a.bytes[p] + a.bytes2 : mx;
   // one group of workgroups per peer, sized for the largest piece
   const int64_t per = (mx / a.unit + kBlock - 1) / kBlock;
   const int64_t groups = per < 1 ? 1 : (per > 128 ? 128 : per);
@@ -224,7 +229,7 @@ void peer_wait(const PeerWaitArgs& a, hipStream_t st) { peer_wait_kernel<<<1, 64
 
 void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUnpackArgs& unpack, hipStream_t st) {
   int64_t mx = 0;
-  for (int p = 0; p < push.npeers; ++p) mx = push.bytes[p] > mx ? push.bytes[p] : mx;
+  for (int p = 0; p < push.npeers; ++p) mx = push.bytes[p] + push.bytes2 > mx ? push.bytes[p] + push.bytes2 : mx;
   for (int p = 0; p < unpack.npeers; ++p) mx = unpack.bytes[p] > mx ? unpack.bytes[p] : mx;
   if (unpack.sum_count * 8 > mx) mx = unpack.sum_count * 8;
   // one group of workgroups per peer, sized for the largest piece (at most
@@ -236,9 +241,9 @@ void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUn
 
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st) {
   int64_t tot = a.sum_count * 8;
-  for (int p = 0; p < a.npeers && a.sum_count == 0; ++p) tot += a.bytes[p];
+  for (int p = 0; p < a.npeers; ++p) tot += a.bytes[p];
   if (tot <= 0) return;
-  peer_unpack_kernel<<<grid_for_bytes(tot, a.sum_count > 0 ? 8 : a.unit), kBlock, 0, st>>>(a);
+  peer_unpack_kernel<<<grid_for_bytes(tot, a.unit), kBlock, 0, st>>>(a);
 }
 
 }  // namespace kern

@@ -315,6 +315,41 @@ PYBIND11_MODULE(_dbfs_native, m) {
       },
       py::arg("boot"), py::arg("backend"), py::arg("inner"), py::arg("slot_bytes") = size_t(16) << 20,
       py::keep_alive<0, 2>(), py::keep_alive<0, 3>());
+  // shadow rank (csrc/comm/replay_comm.cpp): record one rank's collective
+  // outputs in a P-rank run, replay them with that rank alone on the GPU
+  py::class_<CommTape, std::shared_ptr<CommTape>>(m, "CommTape")
+      .def_readonly("rank", &CommTape::rank)
+      .def_readonly("size", &CommTape::size)
+      .def_property_readonly("bytes", &CommTape::bytes)
+      .def("__len__", [](const CommTape& t) { return t.recs.size(); })
+      .def("records", [](const CommTape& t) {
+        // (kind, a, b, output bytes) per collective
+        py::list out;
+        static const char* names[] = {"alltoall", "allgather", "allreduce", "alltoallv", "barrier"};
+        for (const auto& r : t.recs)
+          out.append(py::make_tuple(names[r.kind], r.a, r.b, static_cast<int64_t>(r.data.size())));
+        return out;
+      });
+  py::class_<RecordComm, Comm, std::shared_ptr<RecordComm>>(m, "RecordComm")
+      .def_property_readonly("tape", &RecordComm::tape);
+  m.def(
+      "record_comm",
+      [](std::shared_ptr<Comm> inner, std::shared_ptr<Backend> be) {
+        auto c = std::make_shared<RecordComm>(inner);
+        c->bind_backend(be.get());
+        return c;
+      },
+      py::keep_alive<0, 1>(), py::keep_alive<0, 2>());
+  py::class_<ReplayComm, Comm, std::shared_ptr<ReplayComm>>(m, "ReplayComm")
+      .def_property_readonly("position", &ReplayComm::position)
+      .def("__len__", &ReplayComm::length);
+  m.def(
+      "replay_comm",
+      [](std::shared_ptr<CommTape> tape, std::shared_ptr<Backend> be) {
+        py::gil_scoped_release rel;
+        return std::make_shared<ReplayComm>(tape, *be);
+      },
+      py::keep_alive<0, 2>());
   m.def("nccl_unique_id", []() { return py::bytes(NcclComm::unique_id()); });
   m.def(
       "nccl_comm",

@@ -146,6 +146,12 @@ def test_bench_contract_cpu():
     assert rec["value"] > 0 and rec["validated"] is True
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in rec["config"]
+    # honesty fields: what the timed kernels wrote, and the validated roots
+    # are the timed ones (totals cross-checked against the timed traversal)
+    assert rec["level_state_dtype"] in ("uint8", "int32")
+    assert rec["dtype"] == ("uint8 levels (int32 on read)" if rec["level_state_dtype"] == "uint8" else "int32")
+    assert rec["validated_roots"] == "3/3" and rec["primary"] is None
+    assert rec["value"] == pytest.approx(rec["traversed_edges_mean"] * 3 / (rec["ms_per_step"] * 3 * 1e6), rel=1e-2)
 
 
 def test_bench_self_spawn_cpu():

@@ -121,3 +121,38 @@ def test_process_comms(kind, world):
     for rank, res in out.items():
         assert not isinstance(res, str), res
         _check(res, world, rank)
+
+
+def test_bootstrap_ignores_a_silent_stray_connection():
+    """A connection that never sends the hello (a port scanner, a stale
+    client) is dropped after the short hello timeout instead of stalling rank
+    0's accept loop for the whole collective timeout."""
+    import socket
+    import threading
+    import time
+
+    N = dbfs.native
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    boots = [None, None]
+
+    def r0():
+        boots[0] = N.TcpBootstrap("127.0.0.1", port, 0, 2, 60.0)
+
+    t = threading.Thread(target=r0)
+    t.start()
+    stray = None
+    for _ in range(200):  # rank 0 listening
+        try:
+            stray = socket.create_connection(("127.0.0.1", port), timeout=1)
+            break
+        except OSError:
+            time.sleep(0.05)
+    assert stray is not None
+    t0 = time.time()
+    boots[1] = N.TcpBootstrap("127.0.0.1", port, 1, 2, 60.0)
+    t.join(timeout=60)
+    assert not t.is_alive() and boots[0] is not None
+    assert time.time() - t0 < 30
+    stray.close()
