@@ -314,34 +314,54 @@ class CpuBackend final : public Backend {
     }
   }
 
+  // Sparse top-down level (see the HIP kernel): claims in the replicated
+  // visited bitmap; owned claims settled into the next work list (the running
+  // totals in sparse_cnt_ / sparse_deg_), remote ones (several ranks) appended
+  // to their owners' lists; without lists the level is finished here.
+  void sparse_settle(const TdSparseArgs& a, vid_t v) {
+    const int64_t r = static_cast<int64_t>(v) - a.g.lo;
+    DBFS_CHECK(r >= 0 && r < a.g.rows, "sparse level: settled vertex outside this shard");
+    put_level(a.level, a.level8, r, a.new_level, a.narrow_base);
+    const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
+    if (d <= 0) return;
+    a.frontier_out[r >> 6] |= 1ull << (r & 63);
+    const int64_t cnt = sparse_cnt_, deg = sparse_deg_;
+    a.oscan[cnt] = deg;
+    a.obase[cnt] = rs - deg;
+    a.oqv[cnt] = static_cast<vid_t>(r);
+    for (int64_t blk = div_up(deg, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < deg + d; ++blk)
+      a.oblk[blk] = static_cast<int32_t>(cnt);
+    ++sparse_cnt_;
+    sparse_deg_ += d;
+  }
+  void sparse_finish_totals(const TdSparseArgs& a) {
+    a.stats[0] = a.stats[2] = sparse_cnt_;
+    a.stats[1] = a.stats[3] = sparse_deg_;
+    a.oscan[sparse_cnt_] = sparse_deg_;
+  }
   void td_sparse(const TdSparseArgs& a) override {
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     const int64_t q = a.dev_stats[0];
     for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
-    int64_t cnt = 0, deg = 0;
+    sparse_cnt_ = sparse_deg_ = 0;
     for (int64_t i = 0; i < q; ++i) {
       for (int64_t k = a.qscan[i]; k < a.qscan[i + 1]; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
         if (test_bit(a.visited, v)) continue;
         a.visited[v >> 6] |= 1ull << (v & 63);
         const int64_t r = static_cast<int64_t>(v) - a.g.lo;
-        put_level(a.level, a.level8, r, a.new_level, a.narrow_base);
-        const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
-        if (d <= 0) continue;
-        a.frontier_out[r >> 6] |= 1ull << (r & 63);
-        a.oscan[cnt] = deg;
-        a.obase[cnt] = rs - deg;
-        a.oqv[cnt] = static_cast<vid_t>(r);
-        for (int64_t blk = div_up(deg, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < deg + d; ++blk)
-          a.oblk[blk] = static_cast<int32_t>(cnt);
-        ++cnt;
-        deg += d;
+        if (a.lists && (r < 0 || r >= a.g.rows)) {
+          vid_t* list = a.lists + (static_cast<int64_t>(v) / a.part) * a.list_stride;
+          DBFS_CHECK(static_cast<int64_t>(list[0]) + 1 < a.list_stride, "owner list overflow");
+          list[1 + list[0]++] = v;
+          continue;
+        }
+        sparse_settle(a, v);
       }
     }
-    a.stats[0] = a.stats[2] = cnt;
-    a.stats[1] = a.stats[3] = deg;
-    a.oscan[cnt] = deg;
-    level_ctrl_finish(*a.ctrl, cnt, deg, false, a.rec);
+    if (a.lists) return;  // several ranks: td_sparse_apply finishes
+    sparse_finish_totals(a);
+    level_ctrl_finish(*a.ctrl, sparse_cnt_, sparse_deg_, false, a.rec);
     if (a.mailbox) {
       a.mailbox->done = a.ctrl->done;
       a.mailbox->vis_deg = a.ctrl->vis_deg;
@@ -352,6 +372,21 @@ class CpuBackend final : public Backend {
       a.mailbox->level = a.level_index;
     }
   }
+  void td_sparse_apply(const TdSparseArgs& a) override {
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    for (int r = 0; r < a.nranks; ++r) {
+      const vid_t* list = a.recv_lists + static_cast<int64_t>(r) * a.list_stride;
+      for (vid_t k = 0; k < list[0]; ++k) {
+        const vid_t v = list[1 + k];
+        if (test_bit(a.visited, v)) continue;
+        a.visited[v >> 6] |= 1ull << (v & 63);
+        sparse_settle(a, v);
+      }
+    }
+    for (int r = 0; r < a.nranks; ++r) a.lists[static_cast<int64_t>(r) * a.list_stride] = 0;
+    sparse_finish_totals(a);
+  }
+  int64_t sparse_cnt_ = 0, sparse_deg_ = 0;  // the current sparse level's settled entries / their edges
 
   // (no device checks in the CPU kernels; the injected violation exercises
   // the engine's failure path on the CPU)
@@ -667,6 +702,8 @@ class CpuBackend final : public Backend {
         if (test_bit(a.frontier, a.g.hub_vertex[w * 64 + b])) m |= 1ull << b;
       a.hub_front[w] = m;
     }
+    if (a.visited)
+      for (int64_t i = 0; i < a.words; ++i) a.visited[i] |= a.frontier[i];
   }
   void hub_apply(const HubApplyArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

@@ -227,6 +227,7 @@ class HipBackend final : public Backend {
   void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_sparse(const TdSparseArgs& a) override { on(); kern::td_sparse(a, st_); chk(); }
+  void td_sparse_apply(const TdSparseArgs& a) override { on(); kern::td_sparse_apply(a, st_); chk(); }
   void level_finish(const LevelFinishArgs& a) override { on(); kern::level_finish(a, st_); chk(); }
   void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base) override {
     on();

@@ -66,6 +66,7 @@ void Comm::allgather_allreduce(const void* send, void* recv, size_t bytes, int64
   allgather(send, recv, bytes);
   allreduce_sum_i64(buf, count);
   group_end();
+  if (groups()) note_fused();
 }
 
 // ---- LocalComm ----------------------------------------------------------------

@@ -418,6 +418,54 @@ bool PeerComm::self_test(std::string* why) {
             err = "allgather mismatch (round " + std::to_string(round) + ", from rank " + std::to_string(p) + ")";
             break;
           }
+      // owner lists, count-sized: rank me sends peer p a list of
+      // (me + p + round) % 37 ids (empty ones included), stride >= the most
+      const int64_t stride = 64, cap = 60;
+      {
+        std::vector<uint32_t> hl(static_cast<size_t>(P * stride), 0xDEADBEEFu), gl(hl.size());
+        for (int p = 0; p < P; ++p) {
+          const uint32_t n = static_cast<uint32_t>((me + p + round) % 37);
+          hl[p * stride] = n;
+          for (uint32_t k = 0; k < n; ++k) hl[p * stride + 1 + k] = static_cast<uint32_t>(pat(me, p, k, round));
+        }
+        DBuf<uint32_t> la(*be_, hl.size()), lb(*be_, hl.size());
+        be_->to_device(la.data(), hl.data(), hl.size() * 4);
+        be_->memset_async(lb.data(), 0, lb.bytes());
+        alltoall_lists(la.data(), lb.data(), static_cast<size_t>(stride), static_cast<size_t>(cap));
+        be_->to_host(gl.data(), lb.data(), gl.size() * 4);
+        for (int p = 0; p < P && err.empty(); ++p) {
+          const uint32_t n = static_cast<uint32_t>((p + me + round) % 37);
+          bool ok = gl[p * stride] == n;
+          for (uint32_t k = 0; k < n && ok; ++k) ok = gl[p * stride + 1 + k] == static_cast<uint32_t>(pat(p, me, k, round));
+          if (!ok) err = "alltoall_lists mismatch (round " + std::to_string(round) + ", from rank " + std::to_string(p) + ")";
+        }
+      }
+      // all-gather + all-reduce in one launch
+      {
+        const int64_t gw = words < 4096 ? words : 4096, cnt2 = 2 + round;
+        std::vector<int64_t> hg(static_cast<size_t>(gw * P)), hs(static_cast<size_t>(cnt2));
+        for (int64_t i = 0; i < gw; ++i) hg[me * gw + i] = pat(me, -3, i, round);
+        for (int64_t i = 0; i < cnt2; ++i) hs[i] = pat(me, -4, i, round);
+        DBuf<int64_t> ga(*be_, hg.size()), sa(*be_, hs.size());
+        be_->to_device(ga.data() + me * gw, hg.data() + me * gw, static_cast<size_t>(gw) * 8);
+        be_->to_device(sa.data(), hs.data(), hs.size() * 8);
+        allgather_allreduce(ga.data() + me * gw, ga.data(), static_cast<size_t>(gw) * 8, sa.data(),
+                            static_cast<size_t>(cnt2));
+        be_->to_host(hg.data(), ga.data(), hg.size() * 8);
+        be_->to_host(hs.data(), sa.data(), hs.size() * 8);
+        for (int p = 0; p < P && err.empty(); ++p)
+          for (int64_t i = 0; i < gw; ++i)
+            if (hg[p * gw + i] != pat(p, -3, i, round)) {
+              err = "allgather_allreduce gather mismatch (round " + std::to_string(round) + ")";
+              break;
+            }
+        for (int64_t i = 0; i < cnt2 && err.empty(); ++i) {
+          uint64_t want = 0;
+          for (int p = 0; p < P; ++p) want += static_cast<uint64_t>(pat(p, -4, i, round));
+          if (static_cast<uint64_t>(hs[i]) != want)
+            err = "allgather_allreduce sum mismatch (round " + std::to_string(round) + ")";
+        }
+      }
       // all-reduce (wrapping sums)
       const int64_t cnt = std::min<int64_t>(words, static_cast<int64_t>(slot_ / 8));
       for (int64_t i = 0; i < cnt; ++i) h[i] = pat(me, -2, i, round);

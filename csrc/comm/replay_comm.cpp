@@ -13,6 +13,8 @@
 // per-rank compute of a P-GPU job, which no single-GPU box can otherwise
 // measure.  The per-device step of the reference being replaced is the
 // launch-per-device + synchronize of bfs.cu:577-591 / bfs_mpi.cu:586-593.
+#include <algorithm>
+#include <climits>
 #include <cstring>
 
 #include "dbfs/comm.hpp"
@@ -78,19 +80,34 @@ void RecordComm::alltoallv(const void* send, const int64_t* sc, const int64_t* s
                            const int64_t* rd, size_t eb) {
   note_alltoallv(sc, eb);
   inner_->alltoallv(send, sc, sd, recv, rc, rd, eb);
-  // the received pieces in rank order, concatenated
-  int64_t tot = 0;
-  for (int p = 0; p < size(); ++p) tot += rc[p];
+  int64_t tot = 0, lo = INT64_MAX, hi = 0;
+  bool ordered = true;
+  for (int p = 0; p < size(); ++p) {
+    tot += rc[p];
+    if (rc[p] <= 0) continue;
+    if (rd[p] < hi) ordered = false;
+    lo = std::min(lo, rd[p]);
+    hi = std::max(hi, rd[p] + rc[p]);
+  }
   CommTape::Rec r;
   r.kind = kAllToAllV;
   r.a = tot;
   r.b = static_cast<int64_t>(eb);
-  r.data.resize(static_cast<size_t>(tot) * eb);
-  size_t off = 0;
-  for (int p = 0; p < size(); ++p) {
-    const size_t n = static_cast<size_t>(rc[p]) * eb;
-    if (n) be_->to_host(&r.data[off], static_cast<const char*>(recv) + rd[p] * eb, n);
-    off += n;
+  if (tot > 0 && ordered && hi - lo <= 2 * tot) {
+    // pieces in rank order with small gaps (owner lists at a fixed stride):
+    // the whole span, replayed as ONE copy (a gap is unused receive space)
+    r.span = lo * static_cast<int64_t>(eb);
+    r.data.resize(static_cast<size_t>(hi - lo) * eb);
+    be_->to_host(&r.data[0], static_cast<const char*>(recv) + r.span, r.data.size());
+  } else {
+    // the received pieces in rank order, concatenated
+    r.data.resize(static_cast<size_t>(tot) * eb);
+    size_t off = 0;
+    for (int p = 0; p < size(); ++p) {
+      const size_t n = static_cast<size_t>(rc[p]) * eb;
+      if (n) be_->to_host(&r.data[off], static_cast<const char*>(recv) + rd[p] * eb, n);
+      off += n;
+    }
   }
   tape_->recs.push_back(std::move(r));
 }
@@ -161,7 +178,11 @@ void ReplayComm::alltoallv(const void*, const int64_t* sc, const int64_t*, void*
   int64_t tot = 0;
   for (int p = 0; p < size(); ++p) tot += rc[p];
   size_t i = 0;
-  next(kAllToAllV, tot, static_cast<int64_t>(eb), &i);
+  const auto& r = next(kAllToAllV, tot, static_cast<int64_t>(eb), &i);
+  if (r.span >= 0) {
+    be_->copy_async(static_cast<char*>(recv) + r.span, dev_.data() + off_[i], r.data.size());
+    return;
+  }
   int64_t off = off_[i];
   for (int p = 0; p < size(); ++p) {
     const size_t n = static_cast<size_t>(rc[p]) * eb;

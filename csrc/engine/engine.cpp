@@ -94,8 +94,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
+  else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
-  else if (name == "bu_split") o.bu_split = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -146,8 +146,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
           {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
-          {"list_cap_factor", o.list_cap_factor},
-          {"bu_split", o.bu_split ? 1.0 : 0.0}};
+          {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
+          {"list_cap_factor", o.list_cap_factor}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -1162,7 +1162,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
     be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
   }
-  const bool sparse = sparse_enabled() && !xc;
+  // (several ranks too: remote claims travel as owner lists, td_sparse_apply
+  // settles them on their owner)
+  const bool sparse = sparse_enabled();
   // A sparse chain is live up to this many frontier edges; a level that turns
   // out larger (a geometric prediction can be off by 100x on the second
   // level) is re-enqueued dense: fetch-or claims on every edge cost more than
@@ -1177,6 +1179,24 @@ RunResult Engine::run_bitmap_device(int64_t source) {
                                                      static_cast<int64_t>(opt_.td_sparse_cap_factor *
                                                                           static_cast<double>(opt_.td_sparse_edges)))
                                  : 0;
+  // Several ranks: a sparse chain is live while the level's global frontier
+  // edges fit its owner lists (every rank sends any peer at most that many
+  // ids); predicted levels up to xsparse_lim go sparse.
+  const int P = part_.nranks;
+  const int64_t list_max = xc && sparse && opt_.list_form_edges > 0 ? opt_.list_form_edges : 0;
+  const int64_t xsparse_lim = std::min<int64_t>(opt_.xsparse_edges, list_max);
+  const bool counted = comm_.counted_lists();
+  if (list_max > 0 && list_stride_ < list_max + 1) {
+    // owner lists: count word + list_max ids, the stride a multiple of 4 words
+    // (16-byte pieces for the count-sized exchange); counts zeroed once here
+    // and by every td_sparse_apply after
+    list_stride_ = (list_max + 1 + 3) / 4 * 4;
+    const size_t n = static_cast<size_t>(P) * static_cast<size_t>(list_stride_);
+    dl_send_lists_ = DBuf<vid_t>(be_, n);
+    dl_recv_lists_ = DBuf<vid_t>(be_, n);
+    be_.memset_async(dl_send_lists_.data(), 0, dl_send_lists_.bytes());
+    be_.memset_async(dl_recv_lists_.data(), 0, dl_recv_lists_.bytes());
+  }
   if (sparse && !sparse_ready_) {
     const size_t rows = static_cast<size_t>(std::max<int64_t>(g_.rows(), 1));
     qscan2_ = DBuf<int64_t>(be_, rows + 1);
@@ -1210,26 +1230,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
     bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz
   }
-  // Several ranks, list form: owner lists at a fixed stride (list_stride_ + 1
-  // entries per peer, count first), exchanged cap + 1 entries per peer; the
-  // counts are zeroed once here and by each consuming list_scatter after.
-  const int P = part_.nranks;
-  const int64_t list_max = xc && opt_.list_form_edges > 0 && opt_.mode != Mode::BottomUp
-                               ? std::min<int64_t>(opt_.list_form_edges, std::max<int64_t>(W, 1024))
-                               : 0;
-  if (list_max > 0 && list_stride_ < list_max) {
-    list_stride_ = list_max;
-    const size_t n = static_cast<size_t>(P) * static_cast<size_t>(list_stride_ + 1);
-    dl_send_lists_ = DBuf<vid_t>(be_, n);
-    dl_recv_lists_ = DBuf<vid_t>(be_, n);
-    be_.memset_async(dl_send_lists_.data(), 0, dl_send_lists_.bytes());
-    be_.memset_async(dl_recv_lists_.data(), 0, dl_recv_lists_.bytes());
-  }
-  // Split bottom-up levels: hub frontier bits reduced with the totals (needs
-  // the hub-encoded non-empty-row view the head pass reads).
-  const bool split_ok = xc && opt_.bu_split && gv.nhubs > 0 && gv.nz_pref && gv.nz_head && opt_.bu_nz_view &&
-                        opt_.bu_compact && !opt_.bu_packed && opt_.mode != Mode::TopDown;
-  const int64_t hub_words = div_up(gv.nhubs, kWordBits);
   // One rank: bottom-up levels may run a separate head pass (bu_head_pass).
   const bool head_split_ok = !xc && opt_.bu_head_pass > 0 && gv.nhubs > 0 && gv.nz_pref && gv.nz_head &&
                              opt_.bu_nz_view && opt_.bu_compact && !opt_.bu_packed;
@@ -1307,15 +1307,23 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     ia.qbase = qbase_.data();
     ia.blk_vstart = blk_vstart_.data();
     ia.qv = qv_[0].data();
-    ia.frontier_clear = frontier_[0].data();
+    ia.frontier_clear = fr_own(0);
   }
   be_.init_run(ia);
-  // Several ranks: level `level`'s totals (stats block) all-reduced -- with the
-  // owned hubs' frontier bits when `carry` (a split bottom-up level may
-  // follow) -- then level_finish decides and stamps.
-  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool carry) {
+  // Several ranks: the level's ONE collective -- its totals (stats block)
+  // all-reduced, and with `gather` (the next level is predicted bottom-up, or
+  // td mode, whose top-down levels filter with the replicated visited bitmap)
+  // in the same launch the level's output frontier slice all-gathered
+  // (Comm::allgather_allreduce) -- then level_finish decides and stamps.
+  // (bfs_mpi.cu:615-621 pays a Sendrecv and an Allreduce per level.)
+  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool gather) {
     int64_t* blk = sblk(level);
-    comm_.allreduce_sum_i64(blk + 2, static_cast<size_t>(2 + (carry ? hub_words : 0)));
+    // level L writes frontier_[L & 1] (the seed: frontier_[1])
+    const int out = seed ? 1 : (level & 1);
+    if (gather)
+      comm_.allgather_allreduce(fr_own(out), frontier_[out].data(), static_cast<size_t>(W) * sizeof(word_t), blk + 2, 2);
+    else
+      comm_.allreduce_sum_i64(blk + 2, 2);
     LevelFinishArgs fa;
     fa.stats = blk;
     fa.ctrl = ctrl_.data();
@@ -1328,23 +1336,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     fa.expect_cap = cap;
     be_.level_finish(fa);
   };
-  // owned hubs' bits of level `level`'s output frontier (own slice `fr`)
-  auto hub_bits = [&](int level, const word_t* fr, char expect_dir, int64_t cap, bool guard) {
-    HubLocalArgs hl;
-    hl.g = gv;
-    hl.frontier_own = fr;
-    hl.out = reinterpret_cast<word_t*>(sblk(level) + 4);
-    hl.ctrl = guard ? ctrl_.data() : nullptr;
-    hl.expect_dir = expect_dir;
-    hl.expect_cap = cap;
-    be_.hub_local(hl);
-  };
-  // the seed carries hub bits when level 0 is bottom-up (bu mode)
-  const bool seed_carry = split_ok && init.dir == 'B';
-  if (xc) {
-    if (seed_carry) hub_bits(-1, fr_own(1), 0, 0, false);
-    finish_ranks(-1, true, 0, 0, seed_carry);
-  }
+  // the seed's frontier is gathered with its totals when level 0 is
+  // bottom-up (bu mode).  (Top-down levels read only their owned slice; the
+  // replicated visited bitmap filters candidates with whatever remote bits it
+  // has -- merged frontiers, and the remote targets this rank claimed and
+  // sent -- so a stale remote bit only costs an id its owner drops.)
+  const bool seed_gather = xc && init.dir == 'B';
+  if (xc) finish_ranks(-1, true, 0, 0, seed_gather);
 
   auto scan_args = [&](int level, bool seed, char expect_dir, int64_t cap) {
     ScanArgs sa;
@@ -1390,13 +1388,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_filter_max, 1)));
   std::vector<std::pair<int, int>> evs;
   std::vector<char> enq_dir;     // direction each level was (last) enqueued with
-  std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B'; several ranks: 'L' list form)
-  std::vector<int64_t> enq_cap;  // ... list form: the global frontier edges its lists hold
-  std::vector<char> enq_carry;   // ... several ranks: its reduction carries the hub bits
-  std::vector<char> enq_fused;   // ... bottom-up: finished in the kernel (unit prefixes not scanned)
-  // Enqueue level L's chain for direction d: top-down = compact + td_expand +
-  // update, bottom-up = bu_step; then the scan.  Every kernel checks ctrl->dir,
-  // so a chain enqueued for the wrong direction is a handful of no-op launches.
+  std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B', 'X')
+  std::vector<int64_t> enq_cap;  // ... sparse form: the global frontier edges it stays live for
+  std::vector<char> enq_gather;  // ... several ranks: its collective also all-gathered its output frontier
+  std::vector<char> enq_fused;   // ... finished in its last kernel (unit prefixes not scanned)
   // DBFS_HOST_TIMING=1: host-side enqueue / stamp-wait timeline to stderr
   static const bool host_timing = [] {
     const char* e = std::getenv("DBFS_HOST_TIMING");
@@ -1407,57 +1402,48 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (host_timing)
       htl.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   };
-  // List-form capacity for a level predicted to have mf frontier edges (0: dense)
-  auto list_cap_for = [&](double mf) -> int64_t {
-    if (list_max <= 0) return 0;
-    const double want = std::max(1024.0, mf * opt_.list_cap_factor);
-    if (want > static_cast<double>(list_max)) return 0;
-    int64_t c = 1024;
-    while (static_cast<double>(c) < want) c <<= 1;
-    return std::min(c, list_max);
-  };
-  // mf_hint: the level's predicted (or, re-enqueued, actual) frontier edges;
-  // < 0 unknown
-  auto enqueue_level = [&](int L, char d, int64_t cap, double mf_hint = -1.0) {
+  // mf_hint: the level's predicted (or, re-enqueued, actual) frontier edges
+  // (< 0 unknown); gather (several ranks): the chain's collective also
+  // all-gathers its output frontier, for a bottom-up level predicted next
+  auto enqueue_level = [&](int L, char d, int64_t cap, double mf_hint, bool gather) {
     hmark("enqueue " + std::to_string(L) + d);
     if (static_cast<size_t>(L) >= enq_dir.size()) {
       inject_fault(L);
       enq_dir.resize(static_cast<size_t>(L) + 1);
       enq_form.resize(static_cast<size_t>(L) + 1);
       enq_cap.resize(static_cast<size_t>(L) + 1);
-      enq_carry.resize(static_cast<size_t>(L) + 1);
+      enq_gather.resize(static_cast<size_t>(L) + 1);
       enq_fused.resize(static_cast<size_t>(L) + 1);
       evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
     }
-    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up, 'L' list
-    // top-down (several ranks); the previous level's form decides what hands
-    // this one its work list
+    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up, 'X'
+    // binned top-down (one rank); the previous level's form decides what
+    // hands this one its work list
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    const bool in_carry = L == 0 ? seed_carry : enq_carry[static_cast<size_t>(L - 1)] != 0;
+    // the input frontier is already global: all-gathered by the previous
+    // level's (or the seed's) collective
+    const bool in_gathered = L == 0 ? seed_gather : enq_gather[static_cast<size_t>(L - 1)] != 0;
     enq_dir[L] = d == 'B' ? 'B' : 'T';
     enq_form[L] = d;
-    res.chains.push_back({L, d, d == 'L' ? cap : 0});
-    enq_cap[L] = d == 'L' ? cap : 0;
-    // carry the hub bits out of dense and bottom-up chains (the ones a
-    // bottom-up level follows); list chains are the small levels
-    enq_carry[L] = split_ok && d != 'L';
+    enq_cap[L] = d == 'S' ? cap : 0;
+    enq_gather[L] = xc && gather;
+    res.chains.push_back({L, d, enq_cap[L], enq_gather[L] != 0});
     const int64_t chain_cap = enq_cap[L];
     const int cur = (L + 1) & 1;
     char trace_name[48];
     std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    const bool split = xc && d == 'B' && split_ok && in_carry;
-    bool fused_scan = false;  // the bottom-up kernel runs the level's scan
-    // several ranks: the level's input frontier to every rank (all-gather of
-    // the owned slices) and into the replicated visited bitmap -- before a
-    // bottom-up level, and before top-down levels of the td mode (fewer
-    // candidates); not predicated: on a no-op chain it only refreshes bits
-    // every owner already has.  A split bottom-up level runs its head pass
-    // while the all-gather is in flight (communication stream).
-    if (xc && !split && (d == 'B' || opt_.mode != Mode::DirOpt)) {
-      comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
-      be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
+    bool fused_scan = false;  // the chain's last kernel finishes the level (no scan launch)
+    // several ranks, bottom-up: the input frontier to every rank -- normally
+    // gathered already by the previous level's collective; a chain enqueued
+    // after a top-down prediction gathers it here (not predicated: on a no-op
+    // chain it only refreshes bits every owner already has)
+    if (xc && d == 'B') {
+      if (!in_gathered)
+        comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
+      // (with hubs, hub_gather merges the remote slices into visited)
+      if (gv.nhubs == 0) be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
     }
     // the frontier bitmap -> work list (set L & 1); with sparse levels also
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
@@ -1466,7 +1452,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       if (L > 0 && enq_fused[static_cast<size_t>(L - 1)]) {
         // the previous level only finished its totals: its unit prefixes
         // now (no finish; a no-op unless this chain is live)
-        ScanArgs sa = scan_args(L - 1, false, 'T', d == 'S' ? sparse_cap : 0);
+        ScanArgs sa = scan_args(L - 1, false, 'T', d == 'S' ? chain_cap : 0);
         sa.finish = false;
         be_.scan_units(sa);
       }
@@ -1483,11 +1469,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ca.blk_vstart = blk_set(L);
       if (sparse) {
         ca.qv = qv_[L & 1].data();
-        ca.clear = frontier_[cur].data();
+        ca.clear = fr_own(cur);
       }
       ca.clear_all = clear_all;
       ca.ctrl = ctrl_.data();
-      ca.max_mf = d == 'S' ? sparse_cap : 0;
+      ca.max_mf = d == 'S' ? chain_cap : 0;
       be_.compact_frontier(ca);
     };
     if (d == 'S') {
@@ -1495,16 +1481,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       // after a bottom-up level the output bitmap is that level's input:
       // zeroed by the compaction (every other form leaves it clean)
       const bool compacted = pf == 'T' || pf == 'X' || pf == 'B';
-      if (compacted) compact(pf == 'B' ? frontier_[cur ^ 1].data() : nullptr);
+      if (compacted) compact(pf == 'B' ? fr_own(cur ^ 1) : nullptr);
       TdSparseArgs sp;
       sp.g = gv;
       sp.qscan = qscan_set(L);
       sp.qbase = qbase_set(L);
       sp.blk_vstart = blk_set(L);
       sp.qv = qv_[L & 1].data();
-      sp.dev_stats = stats_.data();
-      sp.frontier_in = frontier_[cur].data();
-      sp.frontier_out = frontier_[cur ^ 1].data();
+      sp.dev_stats = sblk(L - 1);
+      sp.frontier_in = fr_own(cur);
+      sp.frontier_out = fr_own(cur ^ 1);
       sp.visited = visited_.data();
       sp.level = level_.data();
       sp.level8 = run_narrow_ ? level8_.data() : nullptr;
@@ -1516,15 +1502,34 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.oqv = qv_[(L + 1) & 1].data();
       sp.counter = sparse_cnt_.data() + ((L + 1) & 1);
       sp.ticket = sparse_ticket_.data();
-      sp.stats = stats_.data();
+      sp.stats = sblk(L);
       sp.ctrl = ctrl_.data();
       sp.rec = rec_at(L);
       sp.mailbox = mailbox_dev_ + slot(L);
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
       sp.first = !compacted;
-      sp.max_mf = sparse_cap;
-      be_.td_sparse(sp);
+      sp.max_mf = chain_cap;
+      if (xc) {
+        // remote claims to their owners' lists, the lists (count-sized) to
+        // their owners, the received ids settled there; the totals go to
+        // the collective below (no decision in the kernels)
+        DBFS_CHECK(list_max > 0 && chain_cap > 0 && chain_cap <= list_max, "sparse chain without owner lists");
+        sp.lists = dl_send_lists_.data();
+        sp.list_stride = list_stride_;
+        sp.part = part_.part;
+        sp.mailbox = nullptr;
+        be_.td_sparse(sp);
+        comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_),
+                             static_cast<size_t>(chain_cap));
+        sp.recv_lists = dl_recv_lists_.data();
+        sp.nranks = P;
+        sp.grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
+        be_.td_sparse_apply(sp);
+      } else {
+        be_.td_sparse(sp);
+      }
+      fused_scan = true;
     } else if (d == 'X') {
       // binned top-down (one rank): a sparse level (or the seed) handed over
       // the work list, else compact
@@ -1538,7 +1543,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       xa.dev_stats = sblk(L - 1);
       if (listed) {
         xa.clear_qv = qv_[L & 1].data();
-        xa.clear_frontier = frontier_[cur].data();
+        xa.clear_frontier = fr_own(cur);
       }
       xa.ctrl = ctrl_.data();
       xa.shift = bin_shift;
@@ -1562,7 +1567,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       tu.new_level = L + 1;
       tu.ctrl = ctrl_.data();
       be_.update_frontier(tu);
-    } else if (d == 'T' || d == 'L') {
+    } else if (d == 'T') {
       // a sparse level (or the seed) already handed over the work list
       const bool listed = sparse && (pf == 'S' || pf == 'I');
       if (!listed) compact(nullptr);
@@ -1573,7 +1578,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ta.blk_vstart = blk_set(L);
       if (listed) {
         ta.clear_qv = qv_[L & 1].data();
-        ta.clear_frontier = frontier_[cur].data();
+        ta.clear_frontier = fr_own(cur);
       }
       ta.visited = visited_.data();
       ta.ctrl = ctrl_.data();
@@ -1581,121 +1586,91 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ta.grid = td_grid;
       ta.grid_filter = td_grid_filter;
       UpdateArgs tu = ua;
-      if (d == 'L') {
-        // owner-routed lists: candidates appended to their owner's list
-        // (capacity >= the global frontier edges while the chain is live)
-        DBFS_CHECK(xc && chain_cap > 0 && chain_cap <= list_stride_, "list-form chain without lists");
-        ta.lists = dl_send_lists_.data();
-        ta.list_cap = list_stride_;
-        ta.part = part_.part;
-        ta.max_mf = chain_cap;
-        be_.td_expand(ta);
-        std::vector<int64_t> cnt(static_cast<size_t>(P), chain_cap + 1), off(static_cast<size_t>(P));
-        for (int r = 0; r < P; ++r) off[r] = static_cast<int64_t>(r) * (list_stride_ + 1);
-        comm_.alltoallv(dl_send_lists_.data(), cnt.data(), off.data(), dl_recv_lists_.data(), cnt.data(), off.data(),
-                        sizeof(vid_t));
-        ListScatterArgs la;
-        la.lists = dl_recv_lists_.data();
-        la.nranks = P;
-        la.list_cap = list_stride_;
-        la.lo = g_.lo();
-        la.cand = cand_.data();
-        la.words = part_.slice_words();
-        la.reset_lists = dl_send_lists_.data();
-        la.ctrl = ctrl_.data();
-        la.max_mf = chain_cap;
-        be_.list_scatter(la);
-        tu.cand = cand_.data();
+      ta.next = next_.data();
+      ta.next_bytes = next_bytes_.data();
+      // (skipped for levels predicted well below the filter's threshold:
+      // the snapshot kernel would only find its gate closed)
+      if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
+          (mf_hint < 0 || mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
+        // large levels: the hubs' visited bits, staged in LDS by td_expand
+        if (!td_hub_vis_.data()) td_hub_vis_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(gv.td_nhubs, kWordBits)));
+        HubVisitedArgs hv;
+        hv.g = gv;
+        hv.visited = visited_.data();
+        hv.out = td_hub_vis_.data();
+        hv.ctrl = ctrl_.data();
+        hv.min_edges = opt_.td_hub_edges;
+        hv.vis_frac = opt_.td_hub_vis_frac;
+        be_.hub_visited(hv);
+        ta.td_hub_vis = td_hub_vis_.data();
+        ta.td_hub_min_edges = opt_.td_hub_edges;
+        ta.td_hub_vis_frac = opt_.td_hub_vis_frac;
+      }
+      // (a level past kNarrowMaxLevel would store the unreached byte:
+      // the usual path flags the overflow and the run is repeated wide)
+      if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {
+        // byte-map levels write the level itself (nothing to clear after)
+        ta.level_direct = level8_.data();
+        ta.narrow_base = narrow_base_;
+        ta.new_level = L + 1;
+        tu.level_direct = level8_.data();
+        tu.narrow_base = narrow_base_;
+        // a level predicted to touch few words: the update gathers only
+        // the words td_expand marked
+        if (opt_.td_dirty_words && mf_hint >= 0 && mf_hint * 8.0 < static_cast<double>(W * kWordBits)) {
+          if (!td_dirty_.data()) {
+            td_dirty_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(W, 1)));
+            be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
+          }
+          ta.dirty = td_dirty_.data();
+          tu.dirty = td_dirty_.data();
+        }
+        if (ta.td_hub_vis && opt_.td_hub_mark) {
+          if (!td_hub_mark_.data()) {
+            td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
+            be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
+          }
+          ta.td_hub_mark = td_hub_mark_.data();
+        }
+      }
+      be_.td_expand(ta);
+      if (ta.td_hub_mark) {
+        HubApplyArgs ha;
+        ha.g = gv;
+        ha.mark = ta.td_hub_mark;
+        ha.level8 = ta.level_direct;
+        ha.narrow_base = ta.narrow_base;
+        ha.new_level = ta.new_level;
+        ha.dirty = ta.dirty;
+        ha.ctrl = ctrl_.data();
+        ha.max_mf = ta.max_mf;
+        be_.hub_apply(ha);
+      }
+      tu.cand = next_.data();
+      tu.cand_bytes = next_bytes_.data();
+      if (xc) {
+        // candidates to their owners: the byte map (if this level used it)
+        // packed into `next`, one bitmap slice per peer, `next` re-zeroed
+        if (next_bytes_.data()) {
+          PackArgs pa;
+          pa.bytes = next_bytes_.data();
+          pa.next = next_.data();
+          pa.words = GW;
+          pa.ctrl = ctrl_.data();
+          be_.pack_bytes(pa);
+        }
+        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
+        be_.memset_async(next_.data(), 0, next_.bytes());
+        tu.cand = recv_.data();
         tu.cand_bytes = nullptr;
-        tu.nchunks = 1;
-        tu.clear_cand = true;
-        tu.max_mf = chain_cap;
-      } else {
-        ta.next = next_.data();
-        ta.next_bytes = next_bytes_.data();
-        // (skipped for levels predicted well below the filter's threshold:
-        // the snapshot kernel would only find its gate closed)
-        if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
-            (mf_hint < 0 || mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
-          // large levels: the hubs' visited bits, staged in LDS by td_expand
-          if (!td_hub_vis_.data()) td_hub_vis_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(gv.td_nhubs, kWordBits)));
-          HubVisitedArgs hv;
-          hv.g = gv;
-          hv.visited = visited_.data();
-          hv.out = td_hub_vis_.data();
-          hv.ctrl = ctrl_.data();
-          hv.min_edges = opt_.td_hub_edges;
-          hv.vis_frac = opt_.td_hub_vis_frac;
-          be_.hub_visited(hv);
-          ta.td_hub_vis = td_hub_vis_.data();
-          ta.td_hub_min_edges = opt_.td_hub_edges;
-          ta.td_hub_vis_frac = opt_.td_hub_vis_frac;
-        }
-        // (a level past kNarrowMaxLevel would store the unreached byte:
-        // the usual path flags the overflow and the run is repeated wide)
-        if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {
-          // byte-map levels write the level itself (nothing to clear after)
-          ta.level_direct = level8_.data();
-          ta.narrow_base = narrow_base_;
-          ta.new_level = L + 1;
-          tu.level_direct = level8_.data();
-          tu.narrow_base = narrow_base_;
-          // a level predicted to touch few words: the update gathers only
-          // the words td_expand marked
-          if (opt_.td_dirty_words && mf_hint >= 0 && mf_hint * 8.0 < static_cast<double>(W * kWordBits)) {
-            if (!td_dirty_.data()) {
-              td_dirty_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(W, 1)));
-              be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
-            }
-            ta.dirty = td_dirty_.data();
-            tu.dirty = td_dirty_.data();
-          }
-          if (ta.td_hub_vis && opt_.td_hub_mark) {
-            if (!td_hub_mark_.data()) {
-              td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
-              be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
-            }
-            ta.td_hub_mark = td_hub_mark_.data();
-          }
-        }
-        be_.td_expand(ta);
-        if (ta.td_hub_mark) {
-          HubApplyArgs ha;
-          ha.g = gv;
-          ha.mark = ta.td_hub_mark;
-          ha.level8 = ta.level_direct;
-          ha.narrow_base = ta.narrow_base;
-          ha.new_level = ta.new_level;
-          ha.dirty = ta.dirty;
-          ha.ctrl = ctrl_.data();
-          ha.max_mf = ta.max_mf;
-          be_.hub_apply(ha);
-        }
-        tu.cand = next_.data();
-        tu.cand_bytes = next_bytes_.data();
-        if (xc) {
-          // candidates to their owners: the byte map (if this level used it)
-          // packed into `next`, one bitmap slice per peer, `next` re-zeroed
-          if (next_bytes_.data()) {
-            PackArgs pa;
-            pa.bytes = next_bytes_.data();
-            pa.next = next_.data();
-            pa.words = GW;
-            pa.ctrl = ctrl_.data();
-            be_.pack_bytes(pa);
-          }
-          comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
-          be_.memset_async(next_.data(), 0, next_.bytes());
-          tu.cand = recv_.data();
-          tu.cand_bytes = nullptr;
-        }
       }
       tu.force = false;
       tu.frontier = fr_own(cur ^ 1);
       tu.new_level = L + 1;
       tu.ctrl = ctrl_.data();
-      if (!xc && opt_.td_fused_finish) {
-        // totals and finish in the update's last workgroup (as bottom-up)
+      if (opt_.td_fused_finish) {
+        // totals (and with one rank the decision) in the update's last
+        // workgroup (as bottom-up)
         if (!td_tot_.data()) td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
         tu.fuse_scan = true;
         tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
@@ -1735,19 +1710,32 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.unit_queue = bu_unit_queue();
       ba.balanced_grid = opt_.bu_balanced_grid;
       ba.ctrl = ctrl_.data();
-      if (split) {
-        // head pass (hub bits from the previous level's reduction, owned
-        // slice of the frontier) overlapped with the all-gather on the side
-        // stream; the full pass merges after the join
-        const word_t* hub_in = reinterpret_cast<const word_t*>(sblk(L - 1) + 4);
-        be_.fork_side();
-        comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
+      if (gv.nhubs > 0) {
+        HubGatherArgs hg;
+        hg.g = gv;
+        hg.frontier = frontier_[cur].data();
+        hg.hub_front = hub_front_.data();
+        hg.ctrl = ctrl_.data();
+        // several ranks: the gathered remote slices merged into the
+        // replicated visited bitmap in the same launch
+        if (xc) {
+          hg.visited = visited_.data();
+          hg.words = GW;
+        }
+        be_.hub_gather(hg);
+        ba.hub_front = hub_front_.data();
+      }
+      // one rank: the row heads of every unvisited vertex probed first in
+      // a pass of its own (loads of eight words in flight per wave), then
+      // the rows whose head missed are scanned by the merging full pass
+      const bool head_pass = head_split_ok && (opt_.bu_head_pass == 2 || (opt_.bu_head_pass == 1 && pf != 'B'));
+      if (head_pass) {
         BuHeadArgs bh;
         bh.g = gv;
         if (!opt_.bu_nz_rec) bh.g.nz_rec = nullptr;
         bh.zdeg = ba.zdeg;
-        bh.hub_front = hub_in;
-        bh.frontier_own = fr_own(cur);
+        bh.hub_front = hub_front_.data();
+        bh.frontier_own = frontier_[cur].data();
         bh.visited = vis_own;
         bh.new_frontier = ba.new_frontier;
         bh.level = ba.level;
@@ -1758,72 +1746,26 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         bh.unit_cnt = unit_cnt_.data();
         bh.unit_deg = unit_deg_.data();
         bh.ctrl = ctrl_.data();
-        static const bool head_probe = [] {
-          const char* e = std::getenv("DBFS_DEBUG_BU_HEAD");
-          return !(e && *e == '0');
-        }();
-        bh.probe = head_probe;
+        bh.stamp = false;  // hub_gather stamped the level's start
         be_.bu_head(bh);
-        be_.join_side();
-        ba.hub_front = hub_in;
         ba.merge = true;
-        be_.bu_step(ba);
-        // remote slices into the replicated visited bitmap (top-down filter)
-        be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
-      } else {
-        if (gv.nhubs > 0) {
-          HubGatherArgs hg;
-          hg.g = gv;
-          hg.frontier = frontier_[cur].data();
-          hg.hub_front = hub_front_.data();
-          hg.ctrl = ctrl_.data();
-          be_.hub_gather(hg);
-          ba.hub_front = hub_front_.data();
-        }
-        // one rank: the row heads of every unvisited vertex probed first in
-        // a pass of its own (loads of eight words in flight per wave), then
-        // the rows whose head missed are scanned by the merging full pass
-        const bool head_pass = head_split_ok && (opt_.bu_head_pass == 2 || (opt_.bu_head_pass == 1 && pf != 'B'));
-        if (head_pass) {
-          BuHeadArgs bh;
-          bh.g = gv;
-          if (!opt_.bu_nz_rec) bh.g.nz_rec = nullptr;
-          bh.zdeg = ba.zdeg;
-          bh.hub_front = hub_front_.data();
-          bh.frontier_own = frontier_[cur].data();
-          bh.visited = vis_own;
-          bh.new_frontier = ba.new_frontier;
-          bh.level = ba.level;
-          bh.level8 = ba.level8;
-          bh.narrow_base = narrow_base_;
-          bh.new_level = ba.new_level;
-          bh.words = W;
-          bh.unit_cnt = unit_cnt_.data();
-          bh.unit_deg = unit_deg_.data();
-          bh.ctrl = ctrl_.data();
-          bh.stamp = false;  // hub_gather stamped the level's start
-          be_.bu_head(bh);
-          ba.merge = true;
-          ba.heads_done = true;
-        }
-        if (!xc && opt_.bu_fused_scan && !ba.merge) {
-          // the level's totals and finish in the bottom-up kernel's last
-          // workgroup; the unit prefixes only if a top-down chain follows
-          if (!bu_tot_.data()) bu_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
-          ba.fuse_scan = true;
-          ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
-          ba.tot = bu_tot_.data();
-          fused_scan = true;
-        }
-        be_.bu_step(ba);
+        ba.heads_done = true;
       }
+      if (opt_.bu_fused_scan && !ba.merge) {
+        // the level's totals (and with one rank its finish) in the
+        // bottom-up kernel's last workgroup; the unit prefixes only if a
+        // top-down chain follows
+        if (!bu_tot_.data()) bu_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
+        ba.fuse_scan = true;
+        ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
+        ba.tot = bu_tot_.data();
+        fused_scan = true;
+      }
+      be_.bu_step(ba);
     }
-    if (d != 'S' && !fused_scan) scan(L, false, enq_dir[L], chain_cap);
-    enq_fused[L] = fused_scan;
-    if (xc) {
-      if (enq_carry[L]) hub_bits(L, fr_own(cur ^ 1), enq_dir[L], chain_cap, true);
-      finish_ranks(L, false, enq_dir[L], chain_cap, enq_carry[L] != 0);
-    }
+    if (!fused_scan) scan(L, false, enq_dir[L], chain_cap);
+    enq_fused[L] = fused_scan && d != 'S';
+    if (xc) finish_ranks(L, false, enq_dir[L], chain_cap, enq_gather[L] != 0);
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
     hmark("enqueued " + std::to_string(L));
   };
@@ -1838,34 +1780,50 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   //     predicted exactly, so no chain is wasted.
   //   otherwise: level L + 1 is enqueued before the stamp, predicted to keep
   //     level L's direction (two wasted chains per direction change).
-  // Several ranks: a top-down chain also has a form -- list ('L', capacity
-  // from the predicted frontier edges) or dense ('T'); a list chain whose
-  // level turns out to have more frontier edges than its capacity is a no-op
-  // and is re-enqueued like a mispredicted direction.
+  // Several ranks: a top-down chain is sparse ('S': owner lists, live while
+  // the level's global frontier edges fit them) or dense ('T'); a sparse
+  // chain whose level turns out larger is a no-op and is re-enqueued dense,
+  // like a mispredicted direction.  Each chain's collective also all-gathers
+  // its output frontier when the level after it is predicted bottom-up (two
+  // levels ahead of the stamp: the prediction is extrapolated twice).
   int nlev = 0;
   LevelCtrl hc = init;  // host mirror for the prediction
   int64_t prev_nf = 0, prev_mf = 0;
   // top-down form of level L whose frontier has (about) mf edges: sparse when
   // small (right after a bottom-up level too: the compaction then zeroes the
-  // bottom-up input bitmap the sparse level writes into); with several ranks
-  // list form when the lists stay small
+  // bottom-up input bitmap the sparse level writes into); *cap: the global
+  // frontier edges a sparse chain stays live for
   // (exact: mf is the level's actual frontier edges -- a re-enqueue, which
-  // must be live: the lists then hold at least mf entries, or the chain is dense)
+  // must be live)
   auto td_form = [&](int L, double mf, int64_t* cap, bool exact) {
     *cap = 0;
     if (xc) {
-      *cap = list_cap_for(mf);
-      if (exact && *cap > 0 && static_cast<double>(*cap) < mf) {
-        int64_t c = *cap;
-        while (static_cast<double>(c) < mf && c < list_max) c <<= 1;
-        *cap = static_cast<double>(std::min(c, list_max)) >= mf ? std::min(c, list_max) : 0;
+      if (list_max <= 0) return 'T';
+      if (counted) {
+        // count-sized exchange: the largest lists cost nothing extra
+        if (mf > static_cast<double>(exact ? list_max : xsparse_lim)) return 'T';
+        *cap = list_max;
+        return 'S';
       }
-      return *cap > 0 ? 'L' : 'T';
+      // fixed-size exchange (cap + 1 ids per peer): lists sized for the
+      // level, list_cap_factor x the prediction (at least the actual edges
+      // of a re-enqueued level), a power of two >= 1024, and no larger than a
+      // bitmap slice's worth of ids (past that the dense form ships less)
+      const int64_t lim = std::min(list_max, std::max<int64_t>(W, 1024));
+      const double want = std::max(1024.0, exact ? mf : mf * opt_.list_cap_factor);
+      if (want > static_cast<double>(lim) || (!exact && mf > static_cast<double>(xsparse_lim))) return 'T';
+      int64_t c = 1024;
+      while (static_cast<double>(c) < want) c <<= 1;
+      *cap = std::min(c, lim);
+      return 'S';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
     int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
     if (sparse_cap > 0) lim = std::min(lim, sparse_cap);  // (a sparse chain must stay live for mf)
-    if (sparse && mf <= static_cast<double>(lim)) return 'S';
+    if (sparse && mf <= static_cast<double>(lim)) {
+      *cap = sparse_cap;
+      return 'S';
+    }
     bool after_bu = false;  // (binned only before the run's first bottom-up level)
     for (int k = 0; k < L && !after_bu; ++k) after_bu = enq_form[static_cast<size_t>(k)] == 'B';
     return binned && !after_bu && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
@@ -1874,21 +1832,32 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // and mf global frontier edges
   auto chain_valid = [&](int L, char dir, int64_t mf) {
     if (enq_dir[L] != dir) return false;
-    if (enq_form[L] == 'S') return sparse_cap <= 0 || mf <= sparse_cap;
-    return enq_form[L] != 'L' || mf <= enq_cap[L];
+    return enq_form[L] != 'S' || enq_cap[L] <= 0 || mf <= enq_cap[L];
+  };
+  // one prediction step: from a level with frontier (nf, mf), its
+  // predecessor's (pnf, pmf) and `reached` vertices so far, the next level's
+  // frontier extrapolated geometrically (never more than the vertices with
+  // edges not reached yet) and its direction through level_ctrl_finish (c
+  // holds the known level's direction and totals on entry)
+  auto grow = [](double cur, double prev) { return prev <= 0 ? cur * cur : cur * (cur / prev); };
+  auto predict = [&](LevelCtrl& c, double nf, double mf, double pnf, double pmf, double reached, bool first,
+                     double* enf, double* emf) {
+    *enf = std::min({grow(nf, pnf), static_cast<double>(part_.n),
+                     std::max(0.0, static_cast<double>(n_active_) - reached)});
+    // level 1's frontier edges: the source's neighbours have the mean endpoint degree
+    *emf = std::min(first ? mf * std::max(1.0, excess_degree_) : grow(mf, pmf), static_cast<double>(total_directed_));
+    LevelRecDev scratch;
+    level_ctrl_finish(c, std::max<int64_t>(1, static_cast<int64_t>(*enf)), static_cast<int64_t>(*emf), false, &scratch);
   };
   {
     int64_t cap0 = 0;
-    // level 0 (the source's row): list form with the largest lists
-    const char f0 = init.dir == 'B' ? 'B'
-                    : xc             ? (list_max > 0 && opt_.device_loop_predict ? 'L' : 'T')
-                                     : td_form(0, 0.0, &cap0, false);
-    enqueue_level(0, f0, f0 == 'L' ? list_max : 0);
+    const char f0 = init.dir == 'B' ? 'B' : td_form(0, 0.0, &cap0, false);
+    enqueue_level(0, f0, cap0, -1.0, init.dir == 'B');
   }
   for (int L = 0;; ++L) {
     if (!opt_.device_loop_predict) {
       // dense top-down or bottom-up, one more level ahead
-      enqueue_level(L + 1, enq_dir[L], 0);
+      enqueue_level(L + 1, enq_dir[L], 0, -1.0, enq_dir[L] == 'B');
     }
     const volatile LevelMailbox* mb = wait_stamp(L - 1);
     hmark("stamp " + std::to_string(L - 1));
@@ -1902,40 +1871,35 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (!valid) ++res.mispredicts;
     if (!opt_.device_loop_predict) {
       if (!valid) {
-        enqueue_level(L, actual, 0);
-        enqueue_level(L + 1, actual, 0);
+        enqueue_level(L, actual, 0, -1.0, actual == 'B');
+        enqueue_level(L + 1, actual, 0, -1.0, actual == 'B');
       }
       continue;
     }
-    if (!valid) {
-      int64_t cap = 0;
-      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
-      enqueue_level(L, f, cap, static_cast<double>(mf));
-    }
-    // frontier of L + 1, extrapolated from the frontiers of L - 1 and L
-    auto grow = [](int64_t cur, int64_t prev) {
-      if (prev <= 0) return static_cast<double>(cur) * static_cast<double>(cur);
-      return static_cast<double>(cur) * (static_cast<double>(cur) / static_cast<double>(prev));
-    };
+    // level L + 1 extrapolated from the frontiers of L - 1 and L, then L + 2
     hc.dir = actual;
     hc.n_f = nf;
     hc.m_f = mf;
     hc.vis_deg = mb->vis_deg;
     hc.done = 0;
-    LevelRecDev scratch;
-    const double cap = static_cast<double>(part_.n);
-    // (never more than the vertices with edges not reached yet)
-    const double enf = std::min({grow(nf, prev_nf), cap, static_cast<double>(std::max<int64_t>(0, n_active_ - mb->reached))});
-    // level 1's frontier edges: the source's neighbours have the mean endpoint degree
-    const double emf = std::min(L == 0 ? static_cast<double>(mf) * std::max(1.0, excess_degree_) : grow(mf, prev_mf),
-                                static_cast<double>(total_directed_));
-    level_ctrl_finish(hc, std::max<int64_t>(1, static_cast<int64_t>(enf)), static_cast<int64_t>(emf), false,
-                      &scratch);
+    double enf = 0, emf = 0, enf2 = 0, emf2 = 0;
+    predict(hc, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(prev_nf),
+            static_cast<double>(prev_mf), static_cast<double>(mb->reached), L == 0, &enf, &emf);
+    const char d1 = static_cast<char>(hc.dir);
+    LevelCtrl hc2 = hc;
+    predict(hc2, enf, emf, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(mb->reached) + enf,
+            false, &enf2, &emf2);
+    const char d2 = static_cast<char>(hc2.dir);
+    if (!valid) {
+      int64_t cap = 0;
+      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
+      enqueue_level(L, f, cap, static_cast<double>(mf), d1 == 'B');
+    }
     prev_nf = nf;
     prev_mf = mf;
     int64_t lcap = 0;
-    const char f = hc.dir == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
-    enqueue_level(L + 1, f, lcap, emf);
+    const char f = d1 == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
+    enqueue_level(L + 1, f, lcap, emf, d2 == 'B');
   }
   // The traversal is complete once the last stamp is seen: the stamping
   // workgroup ran after all of that level's work (and every earlier level's).

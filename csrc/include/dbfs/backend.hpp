@@ -420,6 +420,21 @@ struct TdSparseArgs {
   // live only while ctrl->m_f <= max_mf (0: any): a sparse chain enqueued for
   // a level that turns out large is a no-op and is re-enqueued dense
   int64_t max_mf = 0;
+  // Several ranks: every target is claimed in the replicated `visited`
+  // (fetch-or); an owned one is finished here, a remote one appended to its
+  // owner's list (lists + owner * list_stride: count, then the ids; wave-
+  // aggregated) -- claiming the remote bit too sends each target at most once
+  // per rank.  The lists then travel (Comm::alltoall_lists) and
+  // td_sparse_apply claims the received ids on their owner.  Only the apply
+  // kernel finishes the level (totals to stats, no decision: the totals are
+  // all-reduced first); with lists == nullptr td_sparse finishes it (one rank).
+  vid_t* lists = nullptr;
+  int64_t list_stride = 0;   // 32-bit words per owner list (count included)
+  int64_t part = 0;          // vertices per rank (owner = v / part)
+  // td_sparse_apply: the received lists (same layout, nranks of them) and the
+  // send lists whose counts it zeroes for the next list level
+  const vid_t* recv_lists = nullptr;
+  int nranks = 1;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -691,6 +706,10 @@ struct HubGatherArgs {
   const word_t* frontier = nullptr;
   word_t* hub_front = nullptr;  // ceil(nhubs / 64) words
   const LevelCtrl* ctrl = nullptr;
+  // several ranks: visited[0, words) |= frontier (the all-gathered remote
+  // slices into the replicated visited bitmap) in the same launch
+  word_t* visited = nullptr;
+  int64_t words = 0;
 };
 
 // Bits of the owned slice for vertices with degree 0 or beyond the shard
@@ -865,6 +884,7 @@ class Backend {
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_sparse(const TdSparseArgs& a) = 0;
+  virtual void td_sparse_apply(const TdSparseArgs& a) = 0;
   virtual void level_finish(const LevelFinishArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;
   // the passes of a binned top-down level (BinArgs), stream-ordered

@@ -59,6 +59,8 @@ class Comm {
   // launch (ncclGroupStart/End); other communicators execute them in order.
   virtual void group_start() {}
   virtual void group_end() {}
+  // group_start/group_end really fuse the collectives between them
+  virtual bool groups() const { return false; }
 
   // Owner lists whose lengths live on the device (no host round trip): rank
   // r's list for peer p is the 32-bit words at send + p * stride_words -- word
@@ -69,6 +71,9 @@ class Comm {
   // the default ships cap + 1 words per peer (an all-to-all-v of uniform
   // counts).  The transport's choice may depend only on (stride, cap).
   virtual void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap);
+  // alltoall_lists ships each list's own length (else the capacity): the
+  // engine then sizes its lists generously, otherwise by the prediction
+  virtual bool counted_lists() const { return false; }
   // allgather(send, recv, bytes) and allreduce_sum_i64(buf, count) as ONE
   // collective where the transport can (peer windows: one launch, both
   // payloads in one slot; RCCL: one group); in order otherwise.
@@ -209,6 +214,7 @@ class NcclComm final : public Comm {
   void barrier() override;
   void group_start() override;
   void group_end() override;
+  bool groups() const override { return true; }
 
  private:
   NcclComm() = default;
@@ -225,6 +231,10 @@ struct CommTape {
   struct Rec {
     int kind = 0;
     int64_t a = 0, b = 0;
+    // alltoallv: >= 0 -- data is the receive buffer's span [span, span +
+    // size) holding every piece (replayed as one copy); -1 -- the pieces
+    // concatenated in rank order
+    int64_t span = -1;
     std::string data;
   };
   int rank = 0, size = 1;
@@ -305,6 +315,7 @@ class PeerComm final : public Comm {
                  const int64_t* rc, const int64_t* rd, size_t eb) override;
   void barrier() override;
   void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
+  bool counted_lists() const override { return true; }
   void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
   size_t slot_bytes() const { return slot_; }
   // Every collective through the windows with known patterns (sizes up to a

@@ -253,20 +253,18 @@ struct EngineOptions {
   // ... with a two-level ticket (UpdateArgs::group_ticket): the update runs
   // a full grid (up to kMaxFusedGrid workgroups) instead of kMaxFusedGrid / 8.
   bool td_group_ticket = true;
-  // Device loop, several ranks: top-down levels whose frontier is predicted to
-  // have at most this many edges exchange owner-routed vertex lists (list
-  // form, per-peer capacity list_cap_factor x the prediction, rounded to a
-  // power of two, at most min(this, slice words)) instead of N/P-bit slices;
-  // a level whose global frontier edges exceed its chain's capacity is
-  // re-enqueued dense (every rank sees the same totals).  0 disables.
-  int64_t list_form_edges = int64_t(1) << 16;
+  // Device loop, several ranks: sparse top-down levels (td_sparse with owner
+  // lists, the lists exchanged count-sized, td_sparse_apply on the owners)
+  // for levels predicted at <= xsparse_edges global frontier edges; such a
+  // chain stays live up to list_form_edges (the owner lists' capacity: P x
+  // that many ids per rank, twice) and a larger level is re-enqueued dense.
+  // 0 disables (dense top-down chains only).
+  int64_t list_form_edges = int64_t(1) << 21;
+  int64_t xsparse_edges = int64_t(1) << 20;
+  // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
+  // the peer windows ship their lengths), a chain's lists hold
+  // list_cap_factor x the predicted edges (a power of two >= 1024)
   double list_cap_factor = 4.0;
-  // Device loop, several ranks, hub LDS on: the hub frontier bits travel with
-  // each level's totals reduction, so a bottom-up level settles the vertices
-  // whose head is a frontier hub (or an owned frontier vertex) while the
-  // frontier all-gather is still in flight on the communication stream, and
-  // finishes the rest after it (bu_head + bu_step merge).
-  bool bu_split = true;
   // Device loop, one rank, hub LDS on: bottom-up levels settle the vertices
   // whose row head is in the frontier in a head pass of their own (bu_head),
   // then bu_step(merge) scans only the rows whose head missed: 0 off, 1 the
@@ -314,12 +312,15 @@ struct LevelRecord {
 };
 
 // One level chain the device loop enqueued (mispredicted ones included):
-// form 'T' dense top-down, 'S' sparse top-down, 'L' list top-down (several
-// ranks, `cap` = global frontier edges its lists hold), 'B' bottom-up.
+// form 'T' dense top-down, 'S' sparse top-down (`cap`: the global frontier
+// edges it stays live for; several ranks: its owner lists' capacity), 'X'
+// binned top-down, 'B' bottom-up; `gather` (several ranks): the chain's
+// collective also all-gathered its output frontier.
 struct ChainRecord {
   int level = 0;
   char form = 'T';
   int64_t cap = 0;
+  bool gather = false;
 };
 
 struct RunResult {

@@ -1080,13 +1080,112 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   }
 }
 
+// Append v (act lanes) to its owner's list (lists + owner * stride: count
+// word, then the ids): one atomic per wave and owner.  Wave-uniform call.
+__device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, int64_t part, vid_t v, bool act) {
+  const int lane = lane_id();
+  const int owner = act ? static_cast<int>(static_cast<int64_t>(v) / part) : -1;
+  unsigned long long pending = __ballot(act);
+  while (pending) {
+    const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+    const int o = __shfl(owner, leader, kWave);
+    const unsigned long long msk = __ballot(owner == o);
+    unsigned base = 0;
+    vid_t* list = lists + static_cast<int64_t>(o) * stride;
+    if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
+    base = __shfl(base, leader, kWave);
+    DBFS_DCHECK(base + __popcll(msk) < static_cast<unsigned long long>(stride), 3, base);
+    if (owner == o) list[1 + base + mask_rank(msk)] = v;
+    pending &= ~msk;
+  }
+}
+
+// The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
+// of this shard): level, frontier bit, and the wave's work-list entries of
+// the next level with one packed atomic (count << kSparseEdgeBits | edges)
+// for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
+template <int kItems>
+__device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
+  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
+  if (!__ballot(claimed != 0)) return;
+  const int lane = lane_id();
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const int64_t lo = a.g.lo;
+  eid_t rs[kItems], re[kItems];
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    rs[k] = re[k] = 0;
+    if (claimed & (1u << k)) {
+      const int64_t r = static_cast<int64_t>(v[k]) - lo;
+      DBFS_DCHECK(r >= 0 && r < a.g.rows, 10, v[k]);
+      store_level(a.level, a.level8, r, a.new_level, a.narrow_base);
+      rs[k] = ro[r];
+      re[k] = ro[r + 1];
+    }
+  }
+  unsigned long long tm[kItems];
+  long long incl[kItems], cbase[kItems], ebase[kItems];
+  long long ctot = 0, etot = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const long long d = static_cast<long long>(re[k] - rs[k]);
+    const bool take = d > 0;  // claimed (else rs == re)
+    tm[k] = __ballot(take);
+    if (take) {
+      const int64_t r = static_cast<int64_t>(v[k]) - lo;
+      atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
+    }
+    incl[k] = wave_incl_scan(take ? d : 0ll);
+    cbase[k] = ctot;
+    ebase[k] = etot;
+    ctot += __popcll(tm[k]);
+    etot += readlane_i64(incl[k], kWave - 1);
+  }
+  if (!ctot) return;
+  unsigned long long old = 0;
+  if (lane == 0)
+    old = atomicAdd(a.counter, (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
+                                   static_cast<unsigned long long>(etot));
+  old = __shfl(old, 0, kWave);
+  const long long p0 = static_cast<long long>(old >> kSparseEdgeBits);
+  const long long q0 = static_cast<long long>(old & kEdgeMask);
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const long long d = static_cast<long long>(re[k] - rs[k]);
+    const long long p = p0 + cbase[k] + mask_rank(tm[k]);
+    const long long qs = q0 + ebase[k] + incl[k] - d;
+    DBFS_DCHECK(d <= 0 || p < a.g.rows, 4, p);
+    if (d > 0) {
+      a.oscan[p] = qs;
+      a.obase[p] = rs[k] - qs;
+      a.oqv[p] = static_cast<vid_t>(static_cast<int64_t>(v[k]) - lo);
+    }
+    wave_fill_blocks(a.oblk, d > 0, qs, d, p);
+  }
+}
+
+// The level's local totals from the packed counter (one thread of the last
+// workgroup): stats, the work list's end marker, counter and ticket reset.
+__device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg) {
+  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
+  const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  cnt = static_cast<long long>(tot >> kSparseEdgeBits);
+  deg = static_cast<long long>(tot & kEdgeMask);
+  *a.counter = 0ull;
+  *a.ticket = 0u;
+  a.stats[0] = a.stats[2] = cnt;
+  a.stats[1] = a.stats[3] = deg;
+  a.oscan[cnt] = deg;
+}
+
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
 // claimed vertex is finished in place (level, frontier bit, output entry), so
-// the level is one launch.  kThreads = 256: 8 edges per thread per block.
+// the level is one launch (one rank); with several ranks remote claims go to
+// their owners' lists and td_sparse_apply finishes the level after the
+// exchange.  kThreads = 256: 8 edges per thread per block.
 template <int kThreads>
 __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
-  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
@@ -1102,15 +1201,13 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   const unsigned active = static_cast<unsigned>(nblocks < 1 ? 1 : (nblocks < gridDim.x ? nblocks : gridDim.x));
   if (blockIdx.x >= active) return;
   const int t = threadIdx.x;
-  const int lane = lane_id();
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
   const int64_t gstride = static_cast<int64_t>(active) * kThreads;
   // the input vertices' frontier bits (the bitmap is not read here)
   for (int64_t i = gtid; i < q; i += gstride) a.frontier_in[a.qv[i] >> 6] = 0ull;
 
   const vid_t* __restrict__ col = a.g.col;
-  const eid_t* __restrict__ ro = a.g.row_off;
-  const int64_t lo = a.g.lo;
+  const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);
   for (long long b = blockIdx.x; b < nblocks; b += active) {
     const long long e0 = b * kTdEdgesPerBlock;
     const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
@@ -1131,60 +1228,22 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       const word_t bit = 1ull << (v[k] & 63);
       if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
     }
-    if (!__ballot(claimed != 0)) continue;
-    // (B) finish the wave's claimed vertices: level, degree, frontier bit,
-    // then one packed append for all of them
-    eid_t rs[kItems], re[kItems];
+    if (a.lists) {
+      // several ranks: claimed remote targets to their owners' lists
+      unsigned remote = 0;
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      rs[k] = re[k] = 0;
-      if (claimed & (1u << k)) {
-        const int64_t r = static_cast<int64_t>(v[k]) - lo;
-        store_level(a.level, a.level8, r, a.new_level, a.narrow_base);
-        rs[k] = ro[r];
-        re[k] = ro[r + 1];
+      for (int k = 0; k < kItems; ++k)
+        if (((claimed >> k) & 1u) && static_cast<uint64_t>(v[k]) - lo >= rows) remote |= 1u << k;
+      claimed &= ~remote;
+      if (__ballot(remote != 0)) {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u);
       }
     }
-    unsigned long long tm[kItems];
-    long long incl[kItems], cbase[kItems], ebase[kItems];
-    long long ctot = 0, etot = 0;
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      const long long d = static_cast<long long>(re[k] - rs[k]);
-      const bool take = d > 0;  // claimed (else rs == re)
-      tm[k] = __ballot(take);
-      if (take) {
-        const int64_t r = static_cast<int64_t>(v[k]) - lo;
-        atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
-      }
-      incl[k] = wave_incl_scan(take ? d : 0ll);
-      cbase[k] = ctot;
-      ebase[k] = etot;
-      ctot += __popcll(tm[k]);
-      etot += readlane_i64(incl[k], kWave - 1);
-    }
-    if (!ctot) continue;
-    unsigned long long old = 0;
-    if (lane == 0)
-      old = atomicAdd(a.counter, (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
-                                     static_cast<unsigned long long>(etot));
-    old = __shfl(old, 0, kWave);
-    const long long p0 = static_cast<long long>(old >> kSparseEdgeBits);
-    const long long q0 = static_cast<long long>(old & kEdgeMask);
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      const long long d = static_cast<long long>(re[k] - rs[k]);
-      const long long p = p0 + cbase[k] + mask_rank(tm[k]);
-      const long long qs = q0 + ebase[k] + incl[k] - d;
-      DBFS_DCHECK(d <= 0 || p < a.g.rows, 4, p);
-      if (d > 0) {
-        a.oscan[p] = qs;
-        a.obase[p] = rs[k] - qs;
-        a.oqv[p] = static_cast<vid_t>(static_cast<int64_t>(v[k]) - lo);
-      }
-      wave_fill_blocks(a.oblk, d > 0, qs, d, p);
-    }
+    // (B) finish the wave's claimed vertices
+    sparse_settle<kItems>(a, v, claimed);
   }
+  if (a.lists) return;  // several ranks: td_sparse_apply finishes the level
 
   // last workgroup: the level's totals and decision (as scan_units_kernel)
   __syncthreads();
@@ -1199,20 +1258,66 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   }
   __syncthreads();
   if (!s_last || t != 0) return;
-  const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const long long cnt = static_cast<long long>(tot >> kSparseEdgeBits);
-  const long long deg = static_cast<long long>(tot & kEdgeMask);
-  *a.counter = 0ull;
-  *a.ticket = 0u;
-  a.stats[0] = a.stats[2] = cnt;
-  a.stats[1] = a.stats[3] = deg;
-  a.oscan[cnt] = deg;
+  long long cnt = 0, deg = 0;
+  sparse_totals(a, cnt, deg);
   LevelCtrl c = *a.ctrl;
   level_ctrl_finish(c, cnt, deg, false, a.rec);
   a.rec->t0 = c.t_start;
   a.rec->t1 = wall_clock64();
   *a.ctrl = c;
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+}
+
+// Several ranks, after the list exchange: the ids the other ranks claimed for
+// this rank's vertices (recv_lists) are claimed here (fetch-or on the owned
+// slice of `visited`; a vertex sent by several ranks, or claimed by this
+// rank's own td_sparse, is settled once) and settled like td_sparse's owned
+// claims; the last workgroup writes the level's local totals and zeroes the
+// send lists' counts.  Grid-stride over each received list in turn.
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
+  constexpr int kItems = kTdItems;
+  __shared__ int s_last;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  const int t = threadIdx.x;
+  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
+  for (int r = 0; r < a.nranks; ++r) {
+    const vid_t* list = a.recv_lists + static_cast<int64_t>(r) * a.list_stride;
+    const int64_t n = list[0];
+    DBFS_DCHECK(n < a.list_stride, 5, n);
+    for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * span; i0 < n; i0 += static_cast<int64_t>(gridDim.x) * span) {
+      vid_t v[kItems];
+      word_t seen[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
+        v[k] = j < n ? list[1 + j] : 0u;
+        seen[k] = j < n ? a.visited[v[k] >> 6] : ~0ull;
+      }
+      unsigned claimed = 0;
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const word_t bit = 1ull << (v[k] & 63);
+        if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+      }
+      sparse_settle<kItems>(a, v, claimed);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = (prev == gridDim.x - 1) ? 1 : 0;
+    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the send lists were read by the exchange (stream-ordered before this
+  // kernel): their counts restart from zero for the next list level
+  if (t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
+  if (t != 0) return;
+  long long cnt = 0, deg = 0;
+  sparse_totals(a, cnt, deg);
 }
 
 // ---------------------------------------------------------------------------
@@ -2162,7 +2267,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   }
 }
 
-// hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word.
+// hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word;
+// several ranks: then the whole grid merges the frontier into visited.
 __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   stamp_level_start(a.ctrl);
@@ -2171,6 +2277,13 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
   const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);
   const word_t m = __ballot(bit);
   if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
+  if (a.visited) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.words; i += stride) {
+      const word_t f = a.frontier[i];
+      if (f) a.visited[i] |= f;
+    }
+  }
 }
 
 // out bit h = visited bit of td_hub_vertex[h]: one wave per hub word.
@@ -2510,6 +2623,10 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
 }
 
+void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {
+  td_sparse_apply_kernel<kTdThreads><<<static_cast<unsigned>(std::max<int64_t>(1, a.grid)), kTdThreads, 0, st>>>(a);
+}
+
 void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st) {
   if (n <= 0) return;
   widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n, base);
@@ -2695,7 +2812,9 @@ void hub_apply(const HubApplyArgs& a, hipStream_t st) {
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
-  hub_gather_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+  unsigned grid = grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave);
+  if (a.visited) grid = std::max(grid, grid_for(a.words, kBlock, 2048));
+  hub_gather_kernel<<<grid, kBlock, 0, st>>>(a);
 }
 
 void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st) {

@@ -20,6 +20,7 @@ void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void td_sparse(const TdSparseArgs& a, hipStream_t st);
+void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
 void level_finish(const LevelFinishArgs& a, hipStream_t st);
 void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st);

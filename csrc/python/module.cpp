@@ -269,6 +269,8 @@ PYBIND11_MODULE(_dbfs_native, m) {
             py::dict d;
             for (int k = 0; k < Comm::kTrafficKinds; ++k)
               d[names[k]] = py::make_tuple(c.traffic().calls[k], c.traffic().bytes[k]);
+            // collectives that shared another's launch (allgather_allreduce)
+            d["fused"] = py::make_tuple(c.traffic().fused, int64_t(0));
             return d;
           })
       .def("bind_backend", [](Comm& c, std::shared_ptr<Backend> be) { c.bind_backend(be.get()); },
@@ -581,7 +583,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
                              [](const RunResult& r) {
                                py::list out;
                                for (const auto& c : r.chains)
-                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap));
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather));
                                return out;
                              })
       .def("level_dicts", &level_dicts);

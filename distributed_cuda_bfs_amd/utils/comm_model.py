@@ -2,24 +2,36 @@
 
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
-collectives and bytes of a traversal can be predicted from its chain forms
-(``BFSResult.chains``) and checked against the communicators' traffic
-counters (``Comm.traffic()``, tests/test_comm_model.py).  ``table`` turns a
-1-GPU level profile into the per-level bytes / collectives table of
-docs/ARCHITECTURE.md §4.
+collectives and bytes of a traversal can be predicted from its chains
+(``BFSResult.chains``: level, form, capacity, gather) and checked against the
+communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
+``table`` turns a 1-GPU level profile into the per-level bytes / collectives
+table of docs/ARCHITECTURE.md §4.
+
+One collective per level, plus the payload a top-down level must move:
+
+* every chain ends with ONE collective: the level's totals all-reduced and --
+  when the next level is predicted bottom-up -- its output frontier slice
+  all-gathered in the same launch (``Comm.allgather_allreduce``);
+* a sparse top-down chain (``S``) exchanges owner lists, count-sized on the
+  peer transport (accounted here, as by the counters, at the lists' capacity);
+* a dense top-down chain (``T``) exchanges candidate bitmap slices;
+* a bottom-up chain (``B``) whose input frontier was not gathered by the
+  previous collective (a mispredicted switch) gathers it itself.
 
 Bytes are what one rank sends to the other ranks under a direct exchange:
 alltoall / allgather (P - 1) x the per-peer bytes, all-reduce (P - 1) x the
 vector, alltoallv the counts to other ranks.
 
 Reference being replaced: the per-level exchange of bfs.cu:587-609 (owner
-buckets copied peer to peer after a count exchange) and bfs_mpi.cu:601-621.
+buckets copied peer to peer after a count exchange, then a host sum) and
+bfs_mpi.cu:601-621 (Sendrecv + Allreduce).
 """
 from __future__ import annotations
 
 from collections import Counter
 from dataclasses import dataclass, field
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple
 
 WORD = 8  # bytes per bitmap word (64 vertices)
 
@@ -28,13 +40,9 @@ WORD = 8  # bytes per bitmap word (64 vertices)
 class ModelConfig:
     nranks: int
     slice_words: int              # Partition.slice_words(): words of one rank's bitmap slice
-    hub_words: int = 0            # ceil(nhubs / 64) (0: no hubs -> no split bottom-up levels)
     mode: str = "do"              # engine mode: do / td / bu
-    bu_split: bool = True         # EngineOptions.bu_split (needs hubs)
-
-    @property
-    def split_ok(self) -> bool:
-        return self.nranks > 1 and self.bu_split and self.hub_words > 0 and self.mode != "td"
+    fused: bool = False           # the transport runs allgather_allreduce as one launch (peer windows, RCCL group)
+    list_stride: int = 0          # owner-list stride in 32-bit words (EngineOptions.list_form_edges + 1, to 4)
 
 
 @dataclass
@@ -56,90 +64,101 @@ class ChainTraffic:
 
     @property
     def total_calls(self) -> int:
-        return sum(v for k, v in self.calls.items() if k != "barrier")
+        """Collective launches (fused ones count once)."""
+        return sum(v for k, v in self.calls.items() if k not in ("barrier", "fused")) - self.calls["fused"]
 
 
-def chain_traffic(cfg: ModelConfig, form: str, cap: int, in_carry: bool) -> Tuple[ChainTraffic, bool]:
-    """Collectives of one level chain; returns (traffic, carry) where carry says
-    whether its totals reduction carried the hub frontier bits."""
+def level_end(cfg: ModelConfig, gather: bool) -> ChainTraffic:
+    """The one collective that ends a level (or the seed)."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
-    split = form == "B" and cfg.split_ok and in_carry
-    if not split and (form == "B" or cfg.mode != "do"):
-        t.add("allgather", (P - 1) * W * WORD)             # frontier slices (+ visited merge)
-    if form == "L":
+    if gather:
+        t.add("allgather", (P - 1) * W * WORD)
+    t.add("allreduce", (P - 1) * 8 * 2)
+    if gather and cfg.fused:
+        t.add("fused", 0)
+    return t
+
+
+def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool) -> ChainTraffic:
+    """Collectives of one level chain."""
+    P, W = cfg.nranks, cfg.slice_words
+    t = ChainTraffic()
+    if form == "B" and not in_gathered:
+        t.add("allgather", (P - 1) * W * WORD)              # input frontier slices (+ visited merge)
+    if form == "S":
         t.add("alltoallv", (P - 1) * (cap + 1) * 4)         # owner lists, count first
     elif form == "T":
         t.add("alltoall", (P - 1) * W * WORD)               # candidate bitmap slices
-    elif form == "B" and split:
-        t.add("allgather", (P - 1) * W * WORD)              # on the side stream, under the head pass
-    carry = cfg.split_ok and form != "L"
-    t.add("allreduce", (P - 1) * 8 * (2 + (cfg.hub_words if carry else 0)))  # totals (+ hub bits)
-    return t, carry
+    t.merge(level_end(cfg, gather))
+    return t
 
 
-def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple[int, str, int]]) -> ChainTraffic:
-    """Traffic of one traversal from its enqueued chains (level, form, cap):
-    start barrier, seed totals, every chain, the wall-time max at the end."""
+def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
+    """Traffic of one traversal from its enqueued chains (level, form, cap,
+    gather): start barrier, the seed's collective, every chain, the wall-time
+    max at the end."""
     P = cfg.nranks
     tot = ChainTraffic()
     tot.add("barrier", 0)
-    seed_carry = cfg.split_ok and cfg.mode == "bu"
-    tot.add("allreduce", (P - 1) * 8 * (2 + (cfg.hub_words if seed_carry else 0)))
-    carry_of: Dict[int, bool] = {-1: seed_carry}
-    for level, form, cap in chains:
-        t, carry = chain_traffic(cfg, form, int(cap), carry_of.get(level - 1, False))
-        carry_of[level] = carry
-        tot.merge(t)
+    seed_gather = cfg.mode == "bu"
+    tot.merge(level_end(cfg, seed_gather))
+    gathered = {-1: seed_gather}
+    for level, form, cap, gather in chains:
+        tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False)))
+        gathered[level] = bool(gather)
     tot.add("allgather", (P - 1) * 8)  # max over ranks of the wall time
     return tot
 
 
-def list_cap_for(mf: float, list_max: int, factor: float = 4.0) -> int:
-    """The engine's list capacity for a predicted frontier of mf edges (0: dense)."""
-    if list_max <= 0:
-        return 0
-    want = max(1024.0, mf * factor)
-    if want > list_max:
-        return 0
-    c = 1024
-    while c < want:
-        c <<= 1
-    return min(c, list_max)
-
-
-def predicted_forms(levels: Sequence[Tuple[str, int]], cfg: ModelConfig,
-                    list_form_edges: int = 1 << 16) -> List[Tuple[int, str, int]]:
+def predicted_forms(levels: Sequence[Tuple[str, int]], cfg: ModelConfig, list_form_edges: int = 1 << 21,
+                    xsparse_edges: int = 1 << 20) -> List[Tuple[int, str, int, bool]]:
     """Chains of a perfectly predicted traversal with per-level (direction,
     frontier edges), plus the trailing no-op chain the loop enqueues ahead."""
-    list_max = min(list_form_edges, max(cfg.slice_words, 1024)) if cfg.mode != "bu" else 0
+    seq = list(levels) + [("T", 0)]
+    lim = min(xsparse_edges, list_form_edges) if cfg.mode != "bu" else -1
     out = []
-    for L, (d, mf) in enumerate(list(levels) + [("T", 0)]):
+    for L, (d, mf) in enumerate(seq):
+        nxt = seq[L + 1][0] if L + 1 < len(seq) else "T"
+        gather = nxt == "B"
         if d == "B":
-            out.append((L, "B", 0))
+            out.append((L, "B", 0, gather))
+        elif list_form_edges > 0 and mf <= lim:
+            out.append((L, "S", list_form_edges, gather))
         else:
-            cap = list_cap_for(mf, list_max)
-            out.append((L, "L" if cap else "T", cap))
+            out.append((L, "T", 0, gather))
     return out
 
 
-def table(levels: Sequence[Tuple[str, int]], n: int, nranks: int, nhubs: int = 1 << 19, mode: str = "do",
-          latency_us: float = 10.0, link_gbs: float = 45.0, links: Optional[int] = None) -> List[dict]:
+def table(levels: Sequence[Tuple[str, int]], n: int, nranks: int, mode: str = "do", latency_us: float = 10.0,
+          link_gbs: float = 45.0, links: Optional[int] = None, list_form_edges: int = 1 << 21,
+          avg_list_fill: float = 1.0) -> List[dict]:
     """Per-level rows for docs/ARCHITECTURE.md §4: direction, chain form,
-    collectives, MiB sent per rank and an estimate of the exchange time:
-    latency_us per collective + bytes over (P - 1) links of link_gbs GB/s each
-    (direct exchange over xGMI: each peer on its own link)."""
+    collective launches, MiB sent per rank and an estimate of the exchange
+    time: latency_us per launch + bytes over (P - 1) links of link_gbs GB/s
+    each (direct exchange over xGMI: each peer on its own link).  Sparse levels
+    ship count-sized lists: their bytes here are the frontier edges x 4 B x
+    (P - 1) / P (every edge's target an id to its owner, at most),
+    avg_list_fill scaling that bound."""
     part = max(64, -(-(-(-n // nranks)) // 64) * 64)
-    cfg = ModelConfig(nranks=nranks, slice_words=part // 64, hub_words=-(-nhubs // 64), mode=mode)
+    W = part // 64
+    cfg = ModelConfig(nranks=nranks, slice_words=W, mode=mode, fused=True)
     rows = []
-    carry_prev = cfg.split_ok and mode == "bu"
     links = links if links is not None else max(1, nranks - 1)
-    for level, form, cap in predicted_forms(levels, cfg):
-        t, carry_prev = chain_traffic(cfg, form, cap, carry_prev)
-        mib = t.total_bytes / 2**20
-        est = t.total_calls * latency_us + t.total_bytes / (links * link_gbs * 1e3)
-        d = levels[level][0] if level < len(levels) else "-"
+    gathered = mode == "bu"
+    for level, form, cap, gather in predicted_forms(levels, cfg, list_form_edges):
+        t = chain_traffic(cfg, form, cap, gather, gathered)
+        gathered = gather
         mf = levels[level][1] if level < len(levels) else 0
-        rows.append({"level": level, "dir": d, "frontier_edges": mf, "form": form, "collectives": t.total_calls,
-                     "kinds": dict(t.calls), "mib_per_rank": round(mib, 3), "est_us": round(est, 1)})
+        nbytes = t.total_bytes
+        if form == "S":
+            # count-sized: the ids actually sent, not the capacity
+            nbytes += int(mf * 4 * (nranks - 1) / nranks * avg_list_fill) - (nranks - 1) * (cap + 1) * 4
+        mib = nbytes / 2**20
+        est = t.total_calls * latency_us + nbytes / (links * link_gbs * 1e3)
+        d = levels[level][0] if level < len(levels) else "-"
+        rows.append({"level": level, "dir": d, "frontier_edges": mf, "form": form, "gather": gather,
+                     "collectives": t.total_calls,
+                     "kinds": {k: v for k, v in t.calls.items() if k != "fused"},
+                     "mib_per_rank": round(mib, 3), "est_us": round(est, 1)})
     return rows

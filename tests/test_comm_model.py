@@ -13,7 +13,7 @@ from distributed_cuda_bfs_amd.utils.comm_model import ModelConfig, run_traffic, 
 
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("mode", ["do", "td", "bu"])
-@pytest.mark.parametrize("knobs", [{}, {"bu_split": 0}, {"list_form_edges": 0}])
+@pytest.mark.parametrize("knobs", [{}, {"list_form_edges": 0}, {"list_cap_factor": 0.01}])
 def test_traffic_matches_model(P, mode, knobs):
     p = dbfs.rmat_params(12, 16, 17)
 
@@ -27,26 +27,39 @@ def test_traffic_matches_model(P, mode, knobs):
             rt.comm.reset_traffic()
             r = b.run(src)
             out.append((r.chains, rt.comm.traffic()))
-        return out, b.partition.slice_words(), b.graph.nhubs
+        return out, b.partition.slice_words()
 
-    for outs, W, nhubs in run_virtual_ranks(P, body, device="cpu"):
-        cfg = ModelConfig(nranks=P, slice_words=W, hub_words=-(-nhubs // 64), mode=mode,
-                          bu_split=knobs.get("bu_split", 1) != 0)
+    for outs, W in run_virtual_ranks(P, body, device="cpu"):
+        cfg = ModelConfig(nranks=P, slice_words=W, mode=mode)
         for chains, got in outs:
             want = run_traffic(cfg, chains)
             for kind, (calls, nbytes) in got.items():
                 assert calls == want.calls[kind], (kind, chains, got, dict(want.calls))
                 assert nbytes == want.bytes[kind], (kind, chains, got, dict(want.bytes))
+            # one collective per chain (its level's end), plus a top-down
+            # chain's payload exchange; a bottom-up chain's input frontier came
+            # with the previous collective unless that one mispredicted
+            fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True), chains)
+            n_td = sum(1 for c in chains if c[1] in "ST")
+            n_lone_b = sum(1 for i, c in enumerate(chains)
+                           if c[1] == "B" and not (chains[i - 1][3] if i else mode == "bu"))
+            assert fused.total_calls == 1 + len(chains) + n_td + n_lone_b + 1
 
 
 def test_table_shapes():
     levels = [("T", 5), ("T", 547726), ("B", 911126127), ("B", 1226480949), ("B", 9282057), ("T", 25207),
               ("T", 75)]
     rows = table(levels, 1 << 26, 8)
-    assert [r["form"] for r in rows] == ["L", "T", "B", "B", "B", "T", "L", "L"]
-    # a dense top-down level ships (P - 1) / P of an N-bit bitmap per rank,
-    # plus the totals all-reduce carrying the 2^19 hub frontier bits
-    assert rows[1]["mib_per_rank"] == pytest.approx((7 * (1 << 26) / 8 / 8 + 7 * 8 * (2 + 8192)) / 2**20, rel=0.01)
-    assert rows[1]["kinds"] == {"alltoall": 1, "allreduce": 1}
-    assert rows[2]["kinds"] == {"allgather": 1, "allreduce": 1}
+    assert [r["form"] for r in rows] == ["S", "S", "B", "B", "B", "S", "S", "S"]
+    # the level before a bottom-up one gathers its frontier in its collective
+    assert [r["gather"] for r in rows] == [False, True, True, True, False, False, False, False]
+    # sparse top-down levels: the owner lists, then the totals (+ frontier) in one launch
+    assert rows[1]["kinds"] == {"alltoallv": 1, "allgather": 1, "allreduce": 1}
+    assert rows[1]["collectives"] == 2
+    # bottom-up levels: ONE collective each (their input came with the previous one)
+    assert all(r["collectives"] == 1 for r in rows[2:5])
+    assert rows[2]["mib_per_rank"] == pytest.approx((7 * (1 << 26) / 8 / 8 + 7 * 16) / 2**20, rel=0.01)
+    # sparse levels ship count-sized lists: far below a bitmap slice
+    assert rows[5]["mib_per_rank"] < 0.2
+    assert sum(r["collectives"] for r in rows) <= len(rows) + 5
     assert all(np.isfinite(r["est_us"]) for r in rows)

@@ -433,19 +433,22 @@ def test_device_loop_several_ranks(P, mode, predict):
 
 
 @pytest.mark.parametrize("knobs", [
-    {},                                             # defaults: list form, split bottom-up
+    {},                                             # defaults: sparse list levels, gathered bottom-up inputs
     {"list_form_edges": 0},                         # dense top-down chains only
-    {"bu_split": 0},                                # unsplit bottom-up chains
-    {"list_cap_factor": 0.01},                      # capacities too small: list chains re-enqueued dense
+    {"list_cap_factor": 0.01},                      # lists too small: sparse chains re-enqueued dense
+    {"list_form_edges": 64},                        # list capacity below the minimum: dense only
+    {"xsparse_edges": 0},                           # only level 0 predicted sparse
     {"device_loop_predict": 0},                     # no prediction: two wasted chains per switch
+    {"bu_fused_scan": 0, "td_fused_finish": 0},     # separate scans
 ])
 @pytest.mark.parametrize("P", [2, 3, 8])
-def test_device_loop_list_form_and_split_bottom_up(P, knobs):
-    """Several ranks, device loop: list-form top-down chains (owner lists
-    exchanged with a fixed-capacity all-to-all-v, capacity checked against the
-    global frontier edges on every rank) and split bottom-up levels (head pass
-    on the all-reduced hub bits while the frontier all-gather is in flight,
-    then the merging full pass) give the host loop's levels and records."""
+def test_device_loop_sparse_lists_several_ranks(P, knobs):
+    """Several ranks, device loop: sparse top-down levels (owned targets
+    settled in place, remote ones appended to owner lists exchanged
+    count-sized, settled on their owners by td_sparse_apply; the lists'
+    capacity checked against the global frontier edges on every rank), the
+    frontier all-gathered by the collective of the level before a bottom-up
+    one, and fused finishes -- the host loop's levels and records."""
     p = dbfs.rmat_params(12, 16, 31)
     csr = dbfs.host_csr_from_params(p)
     deg = np.diff(np.asarray(csr.row_off))
@@ -462,17 +465,23 @@ def test_device_loop_list_form_and_split_bottom_up(P, knobs):
             a, b = dev.run(s), host.run(s)
             strip = lambda r: [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
             out.append((dev.levels(), strip(a), strip(b), (a.reached, a.edges, a.depth), (b.reached, b.edges, b.depth),
-                        a.mispredicts))
+                        a.mispredicts, [c[1] for c in a.chains]))
         return out
 
     for rank_out in run_virtual_ranks(P, body, device="cpu"):
         mis = 0
-        for (ld, ra, rb, ta, tb, m), s in zip(rank_out, srcs):
+        forms = ""
+        for (ld, ra, rb, ta, tb, m, fs), s in zip(rank_out, srcs):
             assert np.array_equal(ld, _oracle(csr, s))
             assert ra == rb and ta == tb
             mis += m
+            forms += "".join(fs)
         if knobs.get("list_cap_factor", 1) < 1:
-            assert mis > 0  # undersized list chains were replaced
+            assert mis > 0  # undersized sparse chains were replaced
+        if knobs.get("list_form_edges", 1) in (0, 64):
+            assert "S" not in forms
+        elif knobs.get("device_loop_predict", 1):
+            assert "S" in forms
 
 
 @pytest.mark.parametrize("P", [2, 3])

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import distributed_cuda_bfs_amd as dbfs
-from distributed_cuda_bfs_amd.parallel.runtime import run_virtual_ranks
+from distributed_cuda_bfs_amd.parallel.runtime import init_runtime, run_virtual_ranks
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -614,14 +614,15 @@ def test_back_to_back_runs_trailing_chain_gpu(gpu_runtime, mode, sparse_edges):
         assert np.array_equal(bfs.levels(), exp)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"list_cap_factor": 0.01}, {"bu_split": 0, "list_form_edges": 0}])
-def test_list_form_and_split_bottom_up_gpu(gpu_runtime, knobs):
-    """Several-rank device loop on the GPU kernels: list-form top-down chains
-    (td_expand lists under the chain guard, all-to-all-v, list_scatter with the
-    count reset) and split bottom-up levels (bu_head_kernel on the reduced hub
-    bits, the all-gather on the side stream, bu_hub_kernel merging) -- one RCCL
-    rank with the exchange forced (ncclSend/Recv and ncclAllGather on the side
-    stream) and 3 / 8 virtual ranks, against the CPU oracle and the host loop."""
+@pytest.mark.parametrize("knobs", [{}, {"list_cap_factor": 0.01}, {"list_form_edges": 0}])
+def test_sparse_lists_several_ranks_gpu(gpu_runtime, knobs):
+    """Several-rank device loop on the GPU kernels: sparse top-down chains
+    (td_sparse claiming owned targets in place and appending remote ones to
+    owner lists, the lists exchanged, td_sparse_apply settling them), dense
+    chains when the lists are off or too small (re-enqueued), bottom-up
+    chains fed by the previous level's fused gather + reduce -- one RCCL rank
+    with the exchange forced and 3 / 8 virtual ranks, against the CPU oracle
+    and the host loop."""
     from distributed_cuda_bfs_amd.parallel.runtime import Runtime
 
     N = dbfs.native
@@ -733,9 +734,9 @@ def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
 @pytest.mark.parametrize("mode", ["do", "td"])
 def test_eight_virtual_ranks_rmat18_gpu(mode):
     """P = 8 virtual ranks on one GPU through the multi-rank device loop at
-    RMAT-18: list-form (owner-routed lists) and dense top-down chains, split
-    bottom-up levels with the hub bits carried in the totals reduction;
-    exact against the oracle and every chain form seen."""
+    RMAT-18: sparse (owner lists) and dense top-down chains, bottom-up levels
+    fed by the fused gather + reduce; exact against the oracle and every chain
+    form seen."""
     p = dbfs.rmat_params(18, 16, 61)
     csr = dbfs.host_csr_from_params(p)
     deg = np.diff(np.asarray(csr.row_off))
@@ -756,7 +757,7 @@ def test_eight_virtual_ranks_rmat18_gpu(mode):
     for levels, forms in run_virtual_ranks(8, body, device="hip"):
         for got, e in zip(levels, exp):
             assert np.array_equal(got, e)
-        assert "L" in forms and ("B" in forms if mode == "do" else "T" in forms)
+        assert "S" in forms and ("B" in forms if mode == "do" else "T" in forms)
 
 
 def test_bottom_up_long_row_scanned_in_place_gpu(gpu_runtime):
@@ -848,3 +849,56 @@ def test_run_many_gpu(gpu_runtime, mode):
         assert r.reached == int(np.count_nonzero(exp != dbfs.UNREACHED))
         assert r.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
     assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, srcs[-1])[0])
+
+
+def test_eight_virtual_ranks_rmat22_defaults_gpu():
+    """P = 8 virtual ranks at RMAT-22 with the default thresholds: the shard
+    (2^19 vertices) takes the 16-word bottom-up waves, the hubs are the full
+    2^19, and sparse chains carry owner lists far past 1024 entries; the
+    levels equal the one-rank run's and the oracle's."""
+    p = dbfs.rmat_params(22, 16, 3)
+    csr = dbfs.host_csr_from_params(p)
+    one = dbfs.BFS(p, init_runtime("hip"), mode="do")
+    srcs = one.sample_roots(2, seed=11)
+    exp = []
+    for s in srcs:
+        one.run(s)
+        exp.append(one.levels())
+    del one
+    for s, e in zip(srcs, exp):
+        assert np.array_equal(e, dbfs.cpu_bfs(csr, s)[0])
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        out, caps = [], []
+        for s in srcs:
+            r = b.run(s)
+            caps += [c[2] for c in r.chains if c[1] == "S"]
+            out.append(b.levels())
+        return out, caps, b.graph.nhubs
+
+    for levels, caps, nhubs in run_virtual_ranks(8, body, device="hip"):
+        for got, e in zip(levels, exp):
+            assert np.array_equal(got, e)
+        assert caps and max(caps) > 1024
+        assert nhubs > 0
+
+
+def test_peer_comm_four_ranks_share_one_gpu_rmat20():
+    """Four self-spawned ranks on device 0 over the peer-memory transport at
+    RMAT-20: every collective (fused gather + reduce, count-sized owner lists,
+    candidate slices) through the IPC windows; every timed root validated."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "4", "--scale", "20", "--steps", "4",
+           "--warmup", "1", "--no-int32-pass"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["n_gpus"] == 4
+    assert rec["validated"] is True and rec["validated_roots"] == "4/4"
