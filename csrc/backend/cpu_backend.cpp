@@ -86,11 +86,8 @@ class CpuBackend final : public Backend {
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
         word_t c = 0;
         if (use_bytes && a.level_direct) {
-          if (!a.dirty || a.dirty[w]) {
-            for (int b = 0; b < 64; ++b)
-              if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.narrow_base + a.new_level)) c |= 1ull << b;
-            if (a.dirty) a.dirty[w] = 0;
-          }
+          for (int b = 0; b < 64; ++b)
+            if (a.level_direct[w * 64 + b] == static_cast<uint8_t>(a.narrow_base + a.new_level)) c |= 1ull << b;
         } else if (use_bytes) {
           c = gather_bytes(a.cand_bytes + w * 64);
         } else {
@@ -271,7 +268,6 @@ class CpuBackend final : public Backend {
           list[1 + list[0]++] = v;
         } else if (bytes && a.level_direct) {
           a.level_direct[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
-          if (a.dirty) a.dirty[v >> 6] = 1;
         } else if (bytes) {
           a.next_bytes[v] = 1;
         } else {
@@ -447,59 +443,10 @@ class CpuBackend final : public Backend {
           }
         }
         a.visited[w] = vis | out;
-        a.new_frontier[w] = a.merge ? (a.new_frontier[w] | out) : out;
-      }
-      a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + cnt : cnt;
-      a.unit_deg[u] = a.merge ? a.unit_deg[u] + deg : deg;
-    }
-  }
-
-  // Head pass of a split bottom-up level: only hub heads (all-reduced hub
-  // bits) and owned heads (owned frontier slice) are tested -- the global
-  // frontier is deliberately not read (on the GPU it is still in flight).
-  void bu_head(const BuHeadArgs& a) override {
-    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-    const int64_t nunits = div_up(a.words, kUnitWords);
-    const int64_t lo = a.g.lo, hi = a.g.lo + a.g.rows;
-    for (int64_t u = 0; u < nunits; ++u) {
-      int64_t cnt = 0, deg = 0;
-      for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
-        const word_t vis = a.visited[w];
-        word_t out = 0;
-        for (int b = 0; b < 64; ++b) {
-          if ((vis >> b) & 1ull) continue;
-          const int64_t k = a.g.nz_pref[w] + __builtin_popcountll(~a.zdeg[w] & ((1ull << b) - 1ull));
-          const vid_t h = a.g.nz_head[k];
-          bool found = false;
-          if (h & kHubFlag) {
-            const vid_t x = h & ~kHubFlag;
-            found = (a.hub_front[x >> 6] >> (x & 63)) & 1ull;
-          } else if (h >= lo && h < hi) {
-            found = test_bit(a.frontier_own, static_cast<int64_t>(h) - lo);
-          }
-          if (!found) continue;
-          out |= 1ull << b;
-          put_level(a.level, a.level8, w * 64 + b, a.new_level, a.narrow_base);
-          ++cnt;
-          deg += a.g.nz_row_off[k + 1] - a.g.nz_row_off[k];
-        }
-        a.visited[w] = vis | out;
         a.new_frontier[w] = out;
       }
       a.unit_cnt[u] = cnt;
       a.unit_deg[u] = deg;
-    }
-  }
-
-  void hub_local(const HubLocalArgs& a) override {
-    if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
-    for (int64_t w = 0; w < div_up(a.g.nhubs, 64); ++w) {
-      word_t m = 0;
-      for (int b = 0; b < 64 && w * 64 + b < a.g.nhubs; ++b) {
-        const int64_t r = static_cast<int64_t>(a.g.hub_vertex[w * 64 + b]) - a.g.lo;
-        if (r >= 0 && r < a.g.rows && test_bit(a.frontier_own, r)) m |= 1ull << b;
-      }
-      a.out[w] = m;
     }
   }
 
@@ -711,7 +658,6 @@ class CpuBackend final : public Backend {
       if (!a.mark[h]) continue;
       const vid_t v = a.g.td_hub_vertex[h];
       a.level8[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
-      if (a.dirty) a.dirty[v >> 6] = 1;
       a.mark[h] = 0;
     }
   }

@@ -38,8 +38,6 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&pre_fork_ev_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&pre_done_ev_, hipEventDisableTiming));
     hipDeviceProp_t prop{};
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
     arch_ = prop.gcnArchName;
@@ -56,8 +54,6 @@ class HipBackend final : public Backend {
     for (hipEvent_t e : events_) hipEventDestroy(e);
     hipEventDestroy(fork_ev_);
     hipEventDestroy(join_ev_);
-    hipEventDestroy(pre_fork_ev_);
-    hipEventDestroy(pre_done_ev_);
     hipStreamDestroy(side_);
     if (scan_tmp_) hipFree(scan_tmp_);
     if (pinned_) hipHostFree(pinned_);
@@ -87,22 +83,6 @@ class HipBackend final : public Backend {
     forked_ = false;
   }
 
-  void prefill_async(void* dst, int value, size_t bytes) override {
-    if (!bytes) return;
-    on();
-    HIP_CHECK(hipEventRecord(pre_fork_ev_, st_));
-    HIP_CHECK(hipStreamWaitEvent(side_, pre_fork_ev_, 0));
-    HIP_CHECK(hipMemsetAsync(dst, value, bytes, side_));
-    HIP_CHECK(hipEventRecord(pre_done_ev_, side_));
-    pre_pending_ = true;
-  }
-  void prefill_wait() override {
-    if (!pre_pending_) return;
-    on();
-    HIP_CHECK(hipStreamWaitEvent(st_, pre_done_ev_, 0));
-    pre_pending_ = false;
-  }
-
   void* alloc(size_t bytes) override {
     on();
     void* p = nullptr;
@@ -113,7 +93,7 @@ class HipBackend final : public Backend {
   void dealloc(void* p) override {
     on();
     hipStreamSynchronize(st_);
-    hipStreamSynchronize(side_);  // (a prefill may still target it)
+    hipStreamSynchronize(side_);
     hipFree(p);
   }
   void memset_async(void* p, int v, size_t bytes) override {
@@ -248,8 +228,6 @@ class HipBackend final : public Backend {
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
   void hub_apply(const HubApplyArgs& a) override { on(); kern::hub_apply(a, st_); chk(); }
-  void bu_head(const BuHeadArgs& a) override { on(); kern::bu_head(a, st_); chk(); }
-  void hub_local(const HubLocalArgs& a) override { on(); kern::hub_local(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }
@@ -411,8 +389,6 @@ class HipBackend final : public Backend {
   hipStream_t st_ = nullptr;
   // communication side stream (fork_side / join_side)
   hipStream_t side_ = nullptr;
-  hipEvent_t pre_fork_ev_ = nullptr, pre_done_ev_ = nullptr;  // prefill_async / prefill_wait
-  bool pre_pending_ = false;
   hipEvent_t fork_ev_ = nullptr, join_ev_ = nullptr;
   bool forked_ = false;
   std::string arch_;

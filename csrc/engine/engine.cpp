@@ -62,26 +62,16 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
   else if (name == "device_loop_ranks") o.device_loop_ranks = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
-  else if (name == "bu_packed") o.bu_packed = v != 0;
   else if (name == "directed") o.directed = v != 0;
-  else if (name == "bu_compact") o.bu_compact = v != 0;
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
-  else if (name == "bu_nz_view") o.bu_nz_view = v != 0;
-  else if (name == "bu_hub_col") o.bu_hub_col = v != 0;
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
-  else if (name == "level_prefill") o.level_prefill = static_cast<int>(v);
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
-  else if (name == "bu_dyn_units") o.bu_dyn_units = v != 0;
   else if (name == "td_group_ticket") o.td_group_ticket = v != 0;
-  else if (name == "bu_balanced_grid") o.bu_balanced_grid = v != 0;
-  else if (name == "bu_nz_rec") o.bu_nz_rec = v != 0;
-  else if (name == "td_dirty_words") o.td_dirty_words = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
-  else if (name == "bu_head_pass") o.bu_head_pass = static_cast<int>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
@@ -114,24 +104,16 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
           {"device_loop_ranks", o.device_loop_ranks ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
-          {"bu_packed", o.bu_packed ? 1.0 : 0.0},
           {"directed", o.directed ? 1.0 : 0.0},
-          {"bu_compact", o.bu_compact ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
-          {"level_prefill", static_cast<double>(o.level_prefill)},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
-          {"bu_dyn_units", o.bu_dyn_units ? 1.0 : 0.0},
           {"td_group_ticket", o.td_group_ticket ? 1.0 : 0.0},
-          {"bu_balanced_grid", o.bu_balanced_grid ? 1.0 : 0.0},
-          {"bu_nz_rec", o.bu_nz_rec ? 1.0 : 0.0},
-          {"td_dirty_words", o.td_dirty_words ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
-          {"bu_head_pass", static_cast<double>(o.bu_head_pass)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
@@ -143,8 +125,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
           {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
-          {"bu_nz_view", o.bu_nz_view ? 1.0 : 0.0},
-          {"bu_hub_col", o.bu_hub_col ? 1.0 : 0.0},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
           {"list_cap_factor", o.list_cap_factor}};
@@ -673,8 +653,7 @@ RunResult Engine::run(int64_t source) {
   }
   level8_filled_ = false;
   narrow_base_ = 0;
-  const bool prefill = run_narrow_ && opt_.level_prefill > 0 && comm_.size() == 1;
-  if (run_narrow_ && !prefill && opt_.narrow_epochs) {
+  if (run_narrow_ && opt_.narrow_epochs) {
     // Level bytes are stored as base + level with base cycling through
     // kNarrowEpochs values: the previous epochs' bytes (and the 0xFF fill)
     // lie outside this run's [base, base + kNarrowMaxLevel], so they already
@@ -684,28 +663,7 @@ RunResult Engine::run(int64_t source) {
     narrow_base_ = static_cast<uint8_t>(epoch * (kNarrowMaxLevel + 2));
     level8_filled_ = epoch != 0;
   }
-  if (prefill) {
-    // the buffer filled under / after the previous run becomes this run's;
-    // the previous run's levels are overwritten by the fill for the next one
-    if (level8_next_ready_) {
-      std::swap(level8_, level8_next_);
-      if (opt_.level_prefill == 1) be_.prefill_wait();
-      level8_filled_ = true;
-      level8_next_ready_ = false;
-    }
-    if (level8_next_.size() == 0) level8_next_ = DBuf<uint8_t>(be_, l8_bytes);
-    if (opt_.level_prefill == 1) {
-      be_.prefill_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
-      level8_next_ready_ = true;
-    }
-  }
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
-  if (prefill && opt_.level_prefill == 2) {
-    // behind the traversal on its stream: runs while the host returns the
-    // result and sets up the next traversal
-    be_.memset_async(level8_next_.data(), kNarrowUnreached, level8_next_.bytes());
-    level8_next_ready_ = true;
-  }
   check_device();
   levels_narrow_ = run_narrow_;
   if (run_narrow_ && r.depth - 1 > kNarrowMaxLevel) {
@@ -756,21 +714,10 @@ void Engine::begin_run_scratch() {
     be_.memset_async(cand_.data(), 0, cand_.bytes());
     be_.memset_async(next_.data(), 0, next_.bytes());
     if (next_bytes_.data()) be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
-    if (td_dirty_.data()) be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
     if (td_hub_mark_.data()) be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
-    if (bu_queue_.data()) be_.memset_async(bu_queue_.data(), 0, bu_queue_.bytes());
     if (td_group_ticket_.data()) be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
   }
   scratch_dirty_ = true;  // until the run completes
-}
-
-unsigned* Engine::bu_unit_queue() {
-  if (!opt_.bu_dyn_units) return nullptr;
-  if (!bu_queue_.data()) {
-    bu_queue_ = DBuf<uint32_t>(be_, static_cast<size_t>((kBuQueueGroups + 1) * kBuQueueStride));
-    be_.memset_async(bu_queue_.data(), 0, bu_queue_.bytes());
-  }
-  return bu_queue_.data();
 }
 
 InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
@@ -1046,18 +993,11 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
-      ba.packed = opt_.bu_packed;
-      ba.compact = opt_.bu_compact;
       ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = !res.levels.empty() && res.levels.back().direction == 'B';
-      if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
-      if (!opt_.bu_nz_rec) ba.g.nz_rec = nullptr;
-      if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
-      ba.unit_queue = bu_unit_queue();
-      ba.balanced_grid = opt_.bu_balanced_grid;
       if (gv.nhubs > 0) {
         HubGatherArgs hg;
         hg.g = gv;
@@ -1230,9 +1170,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
     bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz
   }
-  // One rank: bottom-up levels may run a separate head pass (bu_head_pass).
-  const bool head_split_ok = !xc && opt_.bu_head_pass > 0 && gv.nhubs > 0 && gv.nz_pref && gv.nz_head &&
-                             opt_.bu_nz_view && opt_.bu_compact && !opt_.bu_packed;
   // stats block of level L's output (L = -1: the seed); one block with one rank
   auto sblk = [&](int L) {
     return xc ? stats_.data() + static_cast<int64_t>((L + 1) % kStatsBlocks) * stats_stride_ : stats_.data();
@@ -1615,16 +1552,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ta.new_level = L + 1;
         tu.level_direct = level8_.data();
         tu.narrow_base = narrow_base_;
-        // a level predicted to touch few words: the update gathers only
-        // the words td_expand marked
-        if (opt_.td_dirty_words && mf_hint >= 0 && mf_hint * 8.0 < static_cast<double>(W * kWordBits)) {
-          if (!td_dirty_.data()) {
-            td_dirty_ = DBuf<uint8_t>(be_, static_cast<size_t>(std::max<int64_t>(W, 1)));
-            be_.memset_async(td_dirty_.data(), 0, td_dirty_.bytes());
-          }
-          ta.dirty = td_dirty_.data();
-          tu.dirty = td_dirty_.data();
-        }
         if (ta.td_hub_vis && opt_.td_hub_mark) {
           if (!td_hub_mark_.data()) {
             td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
@@ -1641,7 +1568,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ha.level8 = ta.level_direct;
         ha.narrow_base = ta.narrow_base;
         ha.new_level = ta.new_level;
-        ha.dirty = ta.dirty;
         ha.ctrl = ctrl_.data();
         ha.max_mf = ta.max_mf;
         be_.hub_apply(ha);
@@ -1697,18 +1623,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       ba.new_level = L + 1;
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
-      ba.packed = opt_.bu_packed;
-      ba.compact = opt_.bu_compact;
       ba.whole_units = opt_.bu_whole_units;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = pf == 'B';
-      if (!opt_.bu_nz_view) ba.g.nz_pref = nullptr;
-      if (!opt_.bu_nz_rec) ba.g.nz_rec = nullptr;
-      if (!opt_.bu_hub_col && !g_.col_by_id()) ba.g.hub_col = nullptr;
       ba.unit_cnt = unit_cnt_.data();
       ba.unit_deg = unit_deg_.data();
-      ba.unit_queue = bu_unit_queue();
-      ba.balanced_grid = opt_.bu_balanced_grid;
       ba.ctrl = ctrl_.data();
       if (gv.nhubs > 0) {
         HubGatherArgs hg;
@@ -1725,33 +1644,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         be_.hub_gather(hg);
         ba.hub_front = hub_front_.data();
       }
-      // one rank: the row heads of every unvisited vertex probed first in
-      // a pass of its own (loads of eight words in flight per wave), then
-      // the rows whose head missed are scanned by the merging full pass
-      const bool head_pass = head_split_ok && (opt_.bu_head_pass == 2 || (opt_.bu_head_pass == 1 && pf != 'B'));
-      if (head_pass) {
-        BuHeadArgs bh;
-        bh.g = gv;
-        if (!opt_.bu_nz_rec) bh.g.nz_rec = nullptr;
-        bh.zdeg = ba.zdeg;
-        bh.hub_front = hub_front_.data();
-        bh.frontier_own = frontier_[cur].data();
-        bh.visited = vis_own;
-        bh.new_frontier = ba.new_frontier;
-        bh.level = ba.level;
-        bh.level8 = ba.level8;
-        bh.narrow_base = narrow_base_;
-        bh.new_level = ba.new_level;
-        bh.words = W;
-        bh.unit_cnt = unit_cnt_.data();
-        bh.unit_deg = unit_deg_.data();
-        bh.ctrl = ctrl_.data();
-        bh.stamp = false;  // hub_gather stamped the level's start
-        be_.bu_head(bh);
-        ba.merge = true;
-        ba.heads_done = true;
-      }
-      if (opt_.bu_fused_scan && !ba.merge) {
+      if (opt_.bu_fused_scan) {
         // the level's totals (and with one rank its finish) in the
         // bottom-up kernel's last workgroup; the unit prefixes only if a
         // top-down chain follows

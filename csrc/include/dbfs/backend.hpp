@@ -303,9 +303,6 @@ struct UpdateArgs {
   // unvisited vertices whose level already reads new_level (level8, padded to
   // whole words); cand_bytes is not read.
   const uint8_t* level_direct = nullptr;
-  // Optional with level_direct (TdArgs::dirty): only words whose byte is set
-  // are gathered; the bytes are cleared as read.
-  uint8_t* dirty = nullptr;
   // One rank, device loop (as BuArgs::fuse_scan): totals and finish in the
   // last-arriving workgroup, unit statistics left unscanned (a following
   // compaction scans them first); tot[0..1] zero, reset by the last one.
@@ -507,10 +504,6 @@ struct TdArgs {
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
   uint8_t narrow_base = 0;  // (level_direct stores narrow_base + new_level)
-  // Optional with level_direct: byte w set for every bitmap word w that got a
-  // level byte (a small level's update then gathers only those words
-  // instead of every level byte).
-  uint8_t* dirty = nullptr;
   // Levels of at least td_hub_min_edges frontier edges read g.td_col and test
   // hub targets in an LDS copy of td_hub_vis (visited bits of the top-down
   // hubs, this level's snapshot: hub_visited); not with owner lists.
@@ -574,11 +567,8 @@ struct PackArgs {
 // new_frontier[v], level[v] = new_level, unit stats as in UpdateArgs.
 // Slots of BuArgs::tot (one pair per workgroup of a fused bottom-up finish).
 constexpr int kMaxFusedGrid = 4096;
-// Whole-unit bottom-up kernels with dynamic unit assignment: one counter per
-// workgroup group (blockIdx % kBuQueueGroups) plus an exit counter.
-constexpr int kBuQueueGroups = 8;
-// counters kBuQueueStride uints apart (one 128-B line each: counters sharing a
-// line serialise their atomics)
+// Group tickets kBuQueueStride uints apart (one 128-B line each: counters
+// sharing a line serialise their atomics).
 constexpr int kBuQueueStride = 32;
 // Fused update finish, two-level ticket (UpdateArgs::group_ticket).
 constexpr int kFusedGroup = 64;
@@ -599,21 +589,11 @@ struct BuArgs {
   lvl_t new_level = 0;
   int64_t words = 0;
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
-  bool packed = false;               // wave cooperation over a packed multi-row edge stream
-  bool compact = true;               // waves process their unvisited vertices 64 at a time
   bool follow_up = false;            // the previous level was bottom-up too (launch shape)
   int whole_units = 0;               // hub kernel, compacted: 64 words per wave (1), 16 (-1), by shard size (0)
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'
-  // Second half of a split bottom-up level (BuHeadArgs ran first): the head
-  // pass's results stay -- new_frontier words are OR-ed, unit statistics
-  // added -- and its vertices are already visited.  Hub kernel, compacted.
-  bool merge = false;
-  // ... and the head pass saw the whole frontier (one rank): every head it did
-  // not settle is known to miss, so rows are not probed at their head again
-  // (rows of one entry are done, longer ones go straight to the row scan).
-  bool heads_done = false;
   // One rank, device loop: the level's totals and finish (ScanArgs: stats,
   // direction decision, record, mailbox) run in the bottom-up kernel's
   // last-arriving workgroup instead of a scan launch: workgroup g stores its
@@ -624,53 +604,6 @@ struct BuArgs {
   bool fuse_scan = false;
   ScanArgs scan;
   int64_t* tot = nullptr;
-  // Whole-unit kernels: units beyond each wave's first taken from these
-  // kBuQueueGroups + 1 counters, kBuQueueStride apart (zero between launches; the kernel's last
-  // wave re-zeroes them); null: static stride over the units.
-  unsigned* unit_queue = nullptr;
-  // Whole-unit kernels, static stride: grid trimmed so every wave takes the
-  // same number of units (e.g. 456 instead of 512 workgroups of 12 waves for
-  // 16 K units: 3 units per wave either way, fewer waves idle at the end).
-  bool balanced_grid = false;
-};
-
-// First half of a split bottom-up level (several ranks): while the frontier
-// all-gather is still in flight on the communication stream, every owned
-// unvisited vertex whose row head (its highest-degree neighbour) is a hub in
-// the frontier (hub bits all-reduced with the previous level's totals) or an
-// owned frontier vertex is settled.  Writes new_frontier (every owned word),
-// visited, levels and unit statistics like bu_step; bu_step(merge) then
-// finishes the level once the all-gather has landed.
-struct BuHeadArgs {
-  ShardView g;                       // needs the non-empty-row view and hub-encoded heads
-  const word_t* zdeg = nullptr;      // owned slice
-  const word_t* hub_front = nullptr; // all hubs' frontier bits (g.nhubs bits)
-  const word_t* frontier_own = nullptr;  // owned slice of the current frontier
-  word_t* visited = nullptr;         // owned slice
-  word_t* new_frontier = nullptr;    // owned slice (fully overwritten)
-  lvl_t* level = nullptr;
-  uint8_t* level8 = nullptr;
-  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
-  lvl_t new_level = 0;
-  int64_t words = 0;
-  int64_t* unit_cnt = nullptr;
-  int64_t* unit_deg = nullptr;
-  const LevelCtrl* ctrl = nullptr;   // runs only when ctrl->dir == 'B'
-  bool probe = true;                 // false (diagnostics): settle nothing, only write the words
-  bool stamp = true;                 // first kernel of the level: stamps its start
-};
-
-// Frontier bits of the hubs this rank owns (bit h = new frontier bit of
-// hub_vertex[h] when lo <= hub_vertex[h] < lo + rows, else 0), every hub word
-// written: summed over ranks (disjoint bits) it is the hubs' global frontier,
-// reduced together with the level totals.  Chain guard as ScanArgs.
-struct HubLocalArgs {
-  ShardView g;
-  const word_t* frontier_own = nullptr;  // owned slice of the new frontier
-  word_t* out = nullptr;                 // ceil(nhubs / 64) words
-  const LevelCtrl* ctrl = nullptr;
-  int32_t expect_dir = 0;
-  int64_t expect_cap = 0;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the
@@ -685,7 +618,7 @@ struct HubVisitedArgs {
   double vis_frac = 0.0;  // as TdArgs::td_hub_vis_frac
 };
 
-// level8[td_hub_vertex[h]] = narrow_base + new_level (and dirty[v >> 6] = 1)
+// level8[td_hub_vertex[h]] = narrow_base + new_level
 // for every h with mark[h] != 0, which is cleared: td_expand's hub claims
 // (TdArgs::td_hub_mark).  mark holds kTdMaxHubs bytes.
 struct HubApplyArgs {
@@ -694,7 +627,6 @@ struct HubApplyArgs {
   uint8_t* level8 = nullptr;
   uint8_t narrow_base = 0;
   lvl_t new_level = 0;
-  uint8_t* dirty = nullptr;
   const LevelCtrl* ctrl = nullptr;
   int64_t max_mf = 0;  // chain predicate, as TdArgs::max_mf
 };
@@ -821,12 +753,6 @@ class Backend {
   virtual void* comm_stream_handle() { return stream_handle(); }
   virtual void fork_side() {}
   virtual void join_side() {}
-  // Fill `bytes` at dst with `value` on the side stream once everything
-  // enqueued on the compute stream so far has run (a buffer the next
-  // traversal uses, prepared under this one); prefill_wait() orders the
-  // compute stream after the last such fill.  (CPU: immediate.)
-  virtual void prefill_async(void* dst, int value, size_t bytes) { memset_async(dst, value, bytes); }
-  virtual void prefill_wait() {}
   // Rate of the device wall clock the kernels stamp level records with (ticks
   // per ms; 0: no device clock, records carry no times).
   virtual double wall_clock_khz() const { return 0.0; }
@@ -892,8 +818,6 @@ class Backend {
   virtual void pack_bytes(const PackArgs& a) = 0;
   virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
-  virtual void bu_head(const BuHeadArgs& a) = 0;
-  virtual void hub_local(const HubLocalArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;

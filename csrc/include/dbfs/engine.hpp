@@ -106,19 +106,9 @@ struct EngineOptions {
   // (16: a first bottom-up level entered with a small frontier resolves more
   // rows per lane; RMAT-26 1240 -> 1259 GTEPS, 8 and 32 worse)
   int bu_lane_limit = 16;
-  // Bottom-up rows still unresolved after the per-lane phase are scanned as
-  // one packed edge stream per wave (else one row at a time).
-  bool bu_packed = false;
-  // Bottom-up waves number their unvisited vertices and take 64 per step
-  // (else one bitmap word per step).
-  bool bu_compact = true;
-  // ... a whole 64-word unit per wave (1), 16 words (-1), or by shard size (0:
-  // whole units when they fill every resident wave slot).
+  // Bottom-up waves take a whole 64-word unit (1), 16 words (-1), or by shard
+  // size (0: whole units when they fill every resident wave slot).
   int bu_whole_units = 0;
-  // ... reading row bounds and heads from the dense non-empty-row view.
-  bool bu_nz_view = true;
-  // ... and scanning rows in the hub-encoded adjacency copy (LDS hub probes).
-  bool bu_hub_col = true;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;
@@ -213,36 +203,11 @@ struct EngineOptions {
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;
-  // One rank, narrow levels: the level bytes are double-buffered and the next
-  // run's buffer is filled ahead instead of by the run's init kernel -- 1: on
-  // the side stream while this run traverses (measured slower on RMAT-26:
-  // 1219 / 1192 against 1238 / 1261 GTEPS, the cross-stream fill and event
-  // waits cost more than the 64 MiB fill they take off the critical path);
-  // 2: on the stream right behind this run (overlapping the host's return
-  // and the next run's setup); 0: off.
-  int level_prefill = 0;
-  // One rank, device loop: a bottom-up level's unit scan (totals, direction
+  // Device loop: a bottom-up level's unit scan (totals; one rank: direction
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.
   bool bu_fused_scan = true;
-  // Whole-unit bottom-up kernels hand out units beyond each wave's first
-  // dynamically (BuArgs::unit_queue) instead of a static stride.  Measured
-  // (RMAT-26, per level): 387 / 182 / 104 us against 346 / 137 / 30 with the
-  // static stride (counters on one 128-B line: 520 / 330 / 272) -- the
-  // returning device-scope atomics cost more than the stride's imbalance.
-  bool bu_dyn_units = false;
-  // ... or with the static stride's grid trimmed to an equal number of units
-  // per wave (BuArgs::balanced_grid).
-  bool bu_balanced_grid = false;
-  // Bottom-up rows from the packed 8-byte records (ShardView::nz_rec) instead
-  // of the view's 8-byte offsets + 4-byte heads.
-  bool bu_nz_rec = true;
-  // Direct-level top-down levels predicted at < N/8 frontier edges mark the
-  // bitmap words they store level bytes into; the update gathers only those.
-  // Off: the level-1 update gains ~2 us, the traversal loses ~1 % (1330 against
-  // 1343-1348 GTEPS on RMAT-26, alternating runs).
-  bool td_dirty_words = false;
-  // One rank, device loop: a dense top-down level's update finishes the
+  // Device loop: a dense top-down level's update finishes the
   // level itself (as bu_fused_scan; per-workgroup totals slots, 512
   // workgroups striding over the units with one ticket, the full grid with
   // td_group_ticket): no scan launch unless a compaction follows.
@@ -265,14 +230,6 @@ struct EngineOptions {
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
   double list_cap_factor = 4.0;
-  // Device loop, one rank, hub LDS on: bottom-up levels settle the vertices
-  // whose row head is in the frontier in a head pass of their own (bu_head),
-  // then bu_step(merge) scans only the rows whose head missed: 0 off, 1 the
-  // first bottom-up level of a run of them, 2 every bottom-up level.  Off by
-  // default: measured on RMAT-26 the head pass alone (hub bits probed in L2,
-  // not LDS) took 342 us against 390 us for the whole fused level
-  // (profiles/README.md, round 2).
-  int bu_head_pass = 0;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
@@ -369,7 +326,6 @@ class Engine {
   RunResult run_ref(int64_t source);
   void alloc_bitmap_state();
   void begin_run_scratch();
-  unsigned* bu_unit_queue();  // BuArgs::unit_queue (null unless bu_dyn_units)
   InitRunArgs init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
                         LevelMailbox* mailbox);
   bool scratch_dirty_ = true;  // cand / next / byte map may hold stale bits
@@ -389,16 +345,10 @@ class Engine {
 
   DBuf<lvl_t> level_;
   DBuf<uint8_t> level8_;
-  // one rank: the next run's level bytes, filled with kNarrowUnreached on the
-  // side stream under the current run (EngineOptions::level_prefill)
-  DBuf<uint8_t> level8_next_;
-  DBuf<uint32_t> bu_queue_;  // BuArgs::unit_queue counters
   DBuf<uint32_t> td_group_ticket_;  // UpdateArgs::group_ticket
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
-  DBuf<uint8_t> td_dirty_;  // TdArgs::dirty (one byte per owned bitmap word; zero between levels)
-  bool level8_next_ready_ = false;    // level8_next_ has a fill enqueued
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill
   uint8_t narrow_base_ = 0;           // the current run's level byte base (narrow_epochs)
   int64_t narrow_run_ = 0;            // narrow runs since level8_ was allocated

@@ -93,55 +93,13 @@ __device__ __forceinline__ void store_level(lvl_t* wide, uint8_t* narrow, int64_
     wide[i] = level;
 }
 
-// Streaming loads (read once per level): DBFS_NT_TD / DBFS_NT_BU mark them
-// non-temporal so they do not push the level bytes / frontier bitmap out of L2.
-#ifndef DBFS_NT_TD
-#define DBFS_NT_TD 0
-#endif
-#ifndef DBFS_NT_BU
-#define DBFS_NT_BU 0
-#endif
-// DBFS_TD_HUB_CLAIM: hub targets of the filter claimed in LDS (plain RMW).
-// Measured (RMAT-22 top-down only): 60.3 against 58.7 GTEPS with the filter on
-// every large level, both below the default gate (65.0): off.
-#ifndef DBFS_TD_HUB_CLAIM
-#define DBFS_TD_HUB_CLAIM 0
-#endif
-// Direct top-down levels test the visited bit (1), the level byte (0: a
-// target claimed earlier in the level is not stored again), both (2), or the
-// visited and `next` words with claims in `next` (3).  Measured, RMAT-22
-// top-down only: 65.0 / 60.0 / 58.0 / 55.3 GTEPS; RMAT-26: 1, 0, 2 equal within
-// noise, 3 -2.5 %.  (Counters, tools/gpu_td_stats_roots.sh: the 43 M-edge level
-// stores 29.8 M level bytes for ~2 M new vertices and writes 1.1 GB; removing
-// the repeats with extra reads costs more L2 requests than the writes cost.)
 // Last-arriver hand-offs (scan_units, fused finishes, td_sparse): the last
 // workgroup reads only values the others stored write-through (agent-scope
-// stores / atomics) and reads them with agent-scope loads, so it needs no
-// agent acquire fence (MI355X_MICROARCH, hand-off table, first row).  0 drops
-// it: measured no faster (RMAT-26 level times equal within noise), so the
-// fence stays.
-#ifndef DBFS_LAST_ACQUIRE
-#define DBFS_LAST_ACQUIRE 1
-#endif
-#define DBFS_LAST_ARRIVER_ACQUIRE()                                   \
-  do {                                                                \
-    if (DBFS_LAST_ACQUIRE) {                                          \
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");              \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                \
-    }                                                                 \
-  } while (0)
-// Bottom-up compacted waves: batches of row records prefetched ahead (1: the
-// next batch's while this one probes; 2: the next two).
-#ifndef DBFS_BU_PF
-#define DBFS_BU_PF 1
-#endif
-#ifndef DBFS_TD_DIRECT_PROBE_VISITED
-#define DBFS_TD_DIRECT_PROBE_VISITED 1
-#endif
-template <bool kNt, typename T>
-__device__ __forceinline__ T stream_load(const T* p) {
-  if constexpr (kNt) return __builtin_nontemporal_load(p);
-  else return *p;
+// stores / atomics) with agent-scope loads; the agent acquire fence is kept
+// (measured no slower than without it).
+__device__ __forceinline__ void last_arriver_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 constexpr int kBlock = 256;
@@ -319,16 +277,6 @@ __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, i
 constexpr int kUnitsPerBlock = kBlock / kWave;
 static_assert(kUnitWords == kWave, "one word per lane in update/compact");
 
-__device__ __forceinline__ void wave_unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
-                                                      int64_t* unit_deg, bool add = false) {
-  cnt = wave_sum(cnt);
-  deg = wave_sum(deg);
-  if (lane_id() == 0) {
-    unit_cnt[unit] = add ? unit_cnt[unit] + cnt : cnt;
-    unit_deg[unit] = add ? unit_deg[unit] + deg : deg;
-  }
-}
-
 // 64 candidate bytes (0/1, 64-byte aligned) -> one bitmap word; the bytes are
 // cleared when any is set.  Four 16-B loads / stores per lane.
 __device__ __forceinline__ word_t gather_byte_bits(uint8_t* p) {
@@ -402,15 +350,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
   if (wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
-#if DBFS_TD_DIRECT_PROBE_VISITED == 3
-      if (a.cand && a.cand[wl]) a.cand[wl] = 0;  // the claim bits of the level
-#endif
-      if (!a.dirty) {
-        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
-      } else if (a.dirty[wl]) {
-        c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
-        a.dirty[wl] = 0;
-      }
+      c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
     } else if (use_bytes) {
       c = gather_byte_bits(a.cand_bytes + wl * 64);
     } else {
@@ -505,12 +445,12 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
       s_last = prev == gsz - 1;
       if (s_last) {
         atomicExch(a.group_ticket + grp * kBuQueueStride, 0u);
-        DBFS_LAST_ARRIVER_ACQUIRE();
+        last_arriver_acquire();
       }
     } else {
       const unsigned prev = atomicAdd(a.scan.ticket, 1u);
       s_last = prev == gridDim.x - 1;
-      if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+      if (s_last) last_arriver_acquire();
     }
   }
   __syncthreads();
@@ -544,7 +484,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = atomicAdd(a.scan.ticket, 1u);
         s_level_last = prev == ngroups - 1;
-        if (s_level_last) DBFS_LAST_ARRIVER_ACQUIRE();
+        if (s_level_last) last_arriver_acquire();
       }
     }
     __syncthreads();
@@ -652,7 +592,7 @@ __global__ __launch_bounds__(kScanChunk) void scan_units_kernel(ScanArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
     s_last = (prev == nblk - 1) ? 1 : 0;
-    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+    if (s_last) last_arriver_acquire();
   }
   __syncthreads();
   if (!s_last) return;
@@ -854,9 +794,6 @@ __device__ unsigned long long g_td_stats[4];
 // bases in 32 bits (graphs of at most 2^32 adjacency entries): 16 instead of
 // 24 KiB of LDS per workgroup, 8 resident workgroups per CU instead of 6 (5
 // instead of 4 with the filter).
-#ifndef DBFS_TD_BASE32
-#define DBFS_TD_BASE32 1
-#endif
 template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
@@ -917,7 +854,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         ci = static_cast<uint32_t>(static_cast<uint32_t>(e0 + idx) + s_base[s_owner[idx]]);
       else
         ci = e0 + idx + s_base[s_owner[idx]];
-      vk[k] = idx < cnt ? stream_load<DBFS_NT_TD != 0>(col + ci) : 0u;
+      vk[k] = idx < cnt ? col[ci] : 0u;
       live[k] = idx < cnt;
     }
     // hub targets tested in the LDS snapshot: a visited hub is done here; an
@@ -934,15 +871,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         for (int k = 0; k < kItems; ++k) {
           if (live[k] && (vk[k] & kHubFlag)) {
             const vid_t h = vk[k] & ~kHubFlag;
-#if DBFS_TD_HUB_CLAIM
-            // claimed in LDS by plain read-modify-write (a lost bit only
-            // repeats a store): later edges of this workgroup to the hub skip
-            const word_t hw = s_hubvis[h >> 6];
-            if (!((hw >> (h & 63)) & 1ull)) s_hubvis[h >> 6] = hw | (1ull << (h & 63));
-            if ((hw >> (h & 63)) & 1ull) {
-#else
             if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) {
-#endif
               live[k] = false;
             } else if (a.td_hub_mark) {
               a.td_hub_mark[h] = 1;  // claimed; hub_apply stores its level byte
@@ -982,56 +911,21 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         // a target hit by many edges is stored about once instead of once per
         // edge (stores cost more than reads; a stale read in another XCD's L2
         // only repeats the same store)
+        // The candidate's visited bit is tested (measured, RMAT-22 top-down
+        // only: 65.0 GTEPS, against 60.0 testing the level byte, 58.0 both,
+        // 55.3 with claims in `next`; the 43 M-edge level stores 29.8 M level
+        // bytes for ~2 M new vertices, and removing the repeats with extra
+        // reads costs more L2 requests than the writes, tools/gpu_td_stats_roots.sh).
         const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
         bool keep[kItems];
-#if DBFS_TD_DIRECT_PROBE_VISITED == 1
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
-#elif DBFS_TD_DIRECT_PROBE_VISITED == 3
-        // visited and `next` words loaded together: a target already claimed
-        // at this level (its bit in next, plain racy stores: a lost bit only
-        // repeats a store) is not stored again; update zeroes next
-        word_t nxt[kItems];
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-          const int64_t w = vk[k] >> 6;
-          nxt[k] = live[k] ? a.next[w] : ~0ull;
-          keep[k] = live[k] && (hubnew[k] || !(visited[w] & (1ull << (vk[k] & 63))));
-        }
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = keep[k] && !(nxt[k] & (1ull << (vk[k] & 63)));
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-          if (keep[k]) a.next[vk[k] >> 6] = nxt[k] | (1ull << (vk[k] & 63));
-#elif DBFS_TD_DIRECT_PROBE_VISITED == 2
-        // visited bit first (dense), then the level byte of the unvisited
-        // candidates (a target claimed earlier in this level is not stored again)
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-          keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
-        uint8_t cur[kItems];
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) cur[k] = keep[k] ? a.level_direct[vk[k]] : 0;
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = keep[k] && static_cast<uint8_t>(cur[k] - a.narrow_base) > kNarrowMaxLevel;
-#else
-        uint8_t cur[kItems];
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) cur[k] = live[k] ? a.level_direct[vk[k]] : 0;
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) keep[k] = live[k] && static_cast<uint8_t>(cur[k] - a.narrow_base) > kNarrowMaxLevel;
-#endif
 #pragma unroll
         for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-          if (keep[k]) {
-#ifndef DBFS_DIAG_NO_DIRECT_STORE  // diagnostic counter build only (wrong levels)
-            a.level_direct[vk[k]] = lv;
-#endif
-            if (a.dirty) a.dirty[vk[k] >> 6] = 1;
-          }
+          if (keep[k]) a.level_direct[vk[k]] = lv;
         continue;
       }
       // byte map: with few visited vertices the check costs more than the
@@ -1254,7 +1148,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
     s_last = (prev == active - 1) ? 1 : 0;
-    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+    if (s_last) last_arriver_acquire();
   }
   __syncthreads();
   if (!s_last || t != 0) return;
@@ -1308,7 +1202,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
     s_last = (prev == gridDim.x - 1) ? 1 : 0;
-    if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+    if (s_last) last_arriver_acquire();
   }
   __syncthreads();
   if (!s_last) return;
@@ -1568,36 +1462,20 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 }
 
 // Rest of a bottom-up row after the head probe: phase 1, each unresolved lane
-// checks its next `lane_limit` neighbours (loads batched 4-wide); phase 2,
-// rows still unresolved are scanned by the whole wave (64 neighbours per step,
-// ballot early exit; kPacked: several rows as one packed edge stream).
-// Wave-uniform call (phase 2 is cooperative); returns the lane's `found`.
-#ifndef DBFS_BU_BATCH
-#define DBFS_BU_BATCH 4
-#endif
-constexpr int kBuBatch = DBFS_BU_BATCH;  // phase-1 column loads in flight per lane
+// checks its next `lane_limit` neighbours (loads batched kBuBatch-wide);
+// phase 2, rows still unresolved are scanned by the whole wave, one row at a
+// time, 64 neighbours per step with a ballot early exit.  Wave-uniform call
+// (phase 2 is cooperative); returns the lane's `found`.
+// (Rejected, measured on RMAT-26 in rounds 1-2 and removed: phase 2 as one
+// packed multi-row edge stream -- 83 VGPRs, one workgroup per CU, 1238 ->
+// 1069 GTEPS; 2-8 phase-2 steps in flight -- 1231 -> 1225-1188; non-temporal
+// column loads; records prefetched two batches ahead.)
+constexpr int kBuBatch = 4;  // phase-1 column loads in flight per lane
 
-// Deferred row-scan queue entries per wave (whole-unit hub waves; 0 = scan
-// in the probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
+// Deferred row-scan queue entries per wave (hub waves; 0 = scan in the
+// probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
 // (kMaxHubs / 8 B) and the 8 KiB result words, two workgroups per CU.
-#ifndef DBFS_BU_QUEUE
-#define DBFS_BU_QUEUE 64
-#endif
-constexpr int kBuQueue = DBFS_BU_QUEUE;
-#ifndef DBFS_BU_QUEUE_DIRECT
-#define DBFS_BU_QUEUE_DIRECT DBFS_BU_QUEUE
-#endif
-constexpr int kQueueDirect = DBFS_BU_QUEUE_DIRECT < kBuQueue ? DBFS_BU_QUEUE_DIRECT : kBuQueue;
-// DBFS_BU_PACK_FLUSH=1: queued rows still unresolved after their per-lane scan
-// are finished as one packed edge stream per wave (several short rows per
-// 64-lane step) instead of one row per step -- at a bottom-up level entered
-// with a small frontier (RMAT-26, 91 M of 2.1 B edges) 3.3 M rows reach that
-// phase.  Off: the packed scan lifts the 1024-thread kernel to 83 VGPRs (one
-// workgroup per CU), measured 1238 -> 1069 GTEPS.
-#ifndef DBFS_BU_PACK_FLUSH
-#define DBFS_BU_PACK_FLUSH 0
-#endif
-constexpr bool kPackFlush = DBFS_BU_PACK_FLUSH != 0;
+constexpr int kBuQueue = 64;
 static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
 
 #ifdef DBFS_BU_STATS
@@ -1621,30 +1499,18 @@ template <bool kHub>
 __device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const word_t* s_hub, vid_t u) {
   if constexpr (kHub) {
     const vid_t hb = u & ~kHubFlag;
-#ifdef DBFS_DIAG_SMALL_PROBES  // diagnostic timing build: non-hub probes in a 512 KiB window (wrong levels)
-    return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u & ((1u << 22) - 1));
-#endif
     return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u);
   } else {
     return test_bit(fr, u);
   }
 }
 
-// Wave-cooperative row scan: DBFS_BU_SCAN_STEPS 64-neighbour steps whose
-// loads are issued together (measured on RMAT-26: 1 step 1231 / 1224 GTEPS,
-// 2 steps 1225 / 1224, 4 steps 1217 / 1210, 8 steps 1188 / 1185 -- the extra
-// registers cost more than the latency they hide); kNoVertex pads the tail
-// (never a vertex or a hub-encoded id: ids < 2^31, hub codes < kHubFlag +
-// kMaxHubs).
-#ifndef DBFS_BU_SCAN_STEPS
-#define DBFS_BU_SCAN_STEPS 1
-#endif
-constexpr int kBuScanSteps = DBFS_BU_SCAN_STEPS;
+// kNoVertex pads a phase-2 step's tail (never a vertex or a hub-encoded id:
+// ids < 2^31, hub codes < kHubFlag + kMaxHubs).
 constexpr vid_t kNoVertex = 0xFFFFFFFFu;
 
-template <bool kPacked, bool kHub>
-__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, int* own,
-                                            const word_t* s_hub) {
+template <bool kHub>
+__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, const word_t* s_hub) {
   const int lane = lane_id();
   // hub-encoded copy of the adjacency when present (kHub kernels only)
   const vid_t* __restrict__ col = (kHub && a.g.hub_col) ? a.g.hub_col : a.g.col;
@@ -1662,184 +1528,58 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
 #pragma unroll
     for (int k = 0; k < kBuBatch; ++k) {
       ok[k] = p + k < lim;
-      u[k] = ok[k] ? stream_load<DBFS_NT_BU != 0>(row + p + k) : 0u;
+      u[k] = ok[k] ? row[p + k] : 0u;
     }
 #pragma unroll
     for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && bu_probe<kHub>(fr, s_hub, u[k]);
     p += kBuBatch;
   }
   if (p > lim) p = lim;
-  if constexpr (kPacked) {
-    // Phase 2, packed: the remaining neighbours of all unresolved lanes form
-    // one edge stream (lane order); every step the wave tests the stream's
-    // next 64 entries, whatever rows they belong to (owner lane of slot s:
-    // the first lane whose inclusive prefix exceeds s, a 6-shuffle search),
-    // then drops the rows that hit and advances the rest.  Steps ~ ceil(sum
-    // of remaining lengths / 64) instead of one or more dependent steps per
-    // unresolved row.  32-bit stream positions (queued rows hold < 2^20
-    // entries; a step covers 64 of them).
-    for (;;) {
-      const uint32_t rem = (!found && p < len) ? len - p : 0u;
-      if (!__ballot(rem > 0)) break;
+  // Phase 2: the wave scans each still-unresolved row in turn
+  unsigned long long pending = __ballot(!found && p < len);
+  BU_STAT(5, __popcll(pending));
+  while (pending) {
+    const int l = __ffsll(static_cast<long long>(pending)) - 1;
+    pending &= pending - 1;
+    const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
+    const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
+    bool f = false;
+    for (uint32_t base = ps; base < pe; base += kWave) {
       BU_STAT(6, 1);
-      const uint32_t incl = wave_incl_scan_u32(rem);
-      const uint32_t excl = incl - rem;
-      const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
-      const uint32_t slot = static_cast<uint32_t>(lane);
-      int o = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1)
-        if (static_cast<uint32_t>(__shfl(static_cast<int>(incl), o + step - 1, kWave)) <= slot) o += step;
-      o = min(o, kWave - 1);
-      const uint32_t o_excl = static_cast<uint32_t>(__shfl(static_cast<int>(excl), o, kWave));
-      const vid_t* o_next = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row + p), o, kWave));
-      bool hit = false;
-      if (slot < total) hit = bu_probe<kHub>(fr, s_hub, o_next[slot - o_excl]);
-      unsigned long long hm = hit ? (1ull << o) : 0ull;
-#pragma unroll
-      for (int off = 1; off < kWave; off <<= 1) hm |= __shfl_xor(hm, off, kWave);
-      if ((hm >> lane) & 1ull) found = true;
-      p += (rem > 0 && excl < static_cast<uint32_t>(kWave)) ? min(rem, static_cast<uint32_t>(kWave) - excl) : 0u;
-    }
-  } else {
-    // Phase 2: the wave scans each still-unresolved row in turn,
-    // kBuScanSteps x 64 neighbours per step (the column loads of a step in
-    // flight together, then their probes): a row that scans to its end --
-    // most rows at a bottom-up level entered with a small frontier -- costs
-    // len / (64 kBuScanSteps) dependent round trips instead of len / 64.
-#ifdef DBFS_BU_NO_P2  // diagnostic timing build: no phase-2 scans (wrong levels)
-    unsigned long long pending = 0;
-#else
-    unsigned long long pending = __ballot(!found && p < len);
-#endif
-    BU_STAT(5, __popcll(pending));
-    while (pending) {
-      const int l = __ffsll(static_cast<long long>(pending)) - 1;
-      pending &= pending - 1;
-      const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
-      const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
-      bool f = false;
-      for (uint32_t base = ps; base < pe; base += kWave * kBuScanSteps) {
-        BU_STAT(6, 1);
-        vid_t u[kBuScanSteps];
-#pragma unroll
-        for (int k = 0; k < kBuScanSteps; ++k) {
-          const uint32_t idx = base + k * kWave + lane;
-          u[k] = idx < pe ? r[idx] : kNoVertex;
-        }
-        bool hit = false;
-#pragma unroll
-        for (int k = 0; k < kBuScanSteps; ++k) hit |= u[k] != kNoVertex && bu_probe<kHub>(fr, s_hub, u[k]);
-        if (__ballot(hit)) {
-          f = true;
-          break;
-        }
+      const uint32_t idx = base + lane;
+      const vid_t u = idx < pe ? r[idx] : kNoVertex;
+      if (__ballot(u != kNoVertex && bu_probe<kHub>(fr, s_hub, u))) {
+        f = true;
+        break;
       }
-      if (lane == l) found = f;
     }
+    if (lane == l) found = f;
   }
   return found;
 }
 
 // ---------------------------------------------------------------------------
-// Fused bottom-up step: a wave owns 16 consecutive bitmap words and walks them
-// one word (64 vertices, one per lane) at a time; fully visited words cost one
-// uniform branch.  Phase 1: each unvisited lane checks its first `lane_limit`
-// neighbours (loads batched 4-wide for memory-level parallelism).  Phase 2:
-// lanes still unresolved are scanned by the whole wave, 64 neighbours per
-// step, ballot early exit.  The result word is assembled by a ballot (no
-// atomics) and the wave writes the new frontier word, the visited word, the new
-// levels and the unit statistics directly.
-//
-// Software pipeline across the wave's words: while word j's frontier-bit tests
-// are in flight, word j+1's row offsets are loaded, and word j+1's first four
-// column ids are loaded right after -- the critical path per word is then about
-// one memory round-trip instead of three (row_off -> col -> bitmap).
-// One wave's 16 words starting at w0 (any w0: words past the slice are
-// skipped).  `own` is the wave's 64-int LDS scratch (packed phase 2), `s_hub`
-// the LDS copy of the hub frontier bits (kHub: heads may be hub-encoded).
-template <bool kPacked, bool kHub>
-__device__ __forceinline__ void bu_wave(const BuArgs& a, int64_t w0, int* own, const word_t* s_hub, long long& cnt,
-                                        long long& deg) {
-  const int lane = lane_id();
-  const word_t vis_l = (lane < kWaveWords && w0 + lane < a.words) ? a.visited[w0 + lane] : ~0ull;
-  const int64_t left = a.words - w0;
-  const int nw = left < kWaveWords ? static_cast<int>(left) : kWaveWords;
-  const eid_t* __restrict__ ro = a.g.row_off;
-  const vid_t* __restrict__ col = a.g.col;
-  const word_t* __restrict__ fr = a.frontier;
-
-  // Rows of word j for this lane (0, 0 when visited: padding and zero-degree
-  // vertices are pre-set in visited).
-  // The row head (first, i.e. highest-degree, neighbour) comes from the
-  // per-vertex head[] array when present: a coalesced load issued together
-  // with the row offsets, no dependent col[] line.
-  const vid_t* __restrict__ head = a.g.head;
-  auto fetch_rows = [&](int j, eid_t& rs, eid_t& e, vid_t& u) {
-    rs = 0;
-    e = 0;
-    u = 0;
-    if (j < nw && !((readlane64(vis_l, j) >> lane) & 1ull)) {
-      const int64_t v = (w0 + j) * 64 + lane;
-      rs = ro[v];
-      e = ro[v + 1];
-      if (head) u = head[v];
-    }
-  };
-  eid_t n_rs, n_e;
-  vid_t n_u;
-  fetch_rows(0, n_rs, n_e, n_u);
-  if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;
-
-  for (int j = 0; j < nw; ++j) {
-    const int64_t w = w0 + j;
-    const word_t vis = readlane64(vis_l, j);
-    const eid_t rs = n_rs, e = n_e;
-    const vid_t u0 = n_u;
-    fetch_rows(j + 1, n_rs, n_e, n_u);  // in flight during this word's bit test
-    // First probe: the row's first (highest-degree, hub-first order) neighbour.
-    bool found = false;
-    if (rs < e) {
-      found = bu_probe<kHub>(fr, s_hub, u0);
-    }
-    if (!head) n_u = n_rs < n_e ? col[n_rs] : 0u;  // in flight during this word's tail
-    word_t res = 0;
-    if (vis != ~0ull) {
-      const int64_t v = w * 64 + lane;
-      found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
-      res = __ballot(found);
-      if (found) {
-        store_level(a.level, a.level8, v, a.new_level, a.narrow_base);
-        cnt += 1;
-        deg += e - rs;
-      }
-      if (lane == 0 && res) a.visited[w] = vis | res;
-    }
-    if (lane == 0) a.new_frontier[w] = res;
-  }
-}
-
-
-// Compacted variant of bu_wave: the unvisited vertices of the wave's 16 words
-// are numbered (per-word popcount prefix) and processed 64 at a time, one per
-// lane, whatever word they sit in -- instead of one word (64 lanes, many of
-// them visited) per step.  The per-step cost of a bottom-up wave is a chain of
-// dependent memory round trips nearly independent of how many lanes are
-// active, so steps = ceil(unvisited / 64) instead of the number of words
-// with any unvisited vertex: at the dense first bottom-up level of RMAT-26
-// (~half the lanes unvisited) half the steps, at the later levels (a few per
-// word) a fraction.  Found bits are OR-ed into a per-wave LDS copy of the 16
-// result words (s_res), written out once.
-// kWords: the wave's share, 16 words (a quarter unit) or 64 (a whole unit).
+// Fused bottom-up step of one wave over kWords bitmap words from w0 (a whole
+// 64-word unit, or 16 words when the shard is too small to fill the chip
+// that way): the unvisited vertices of its words are numbered (per-word
+// popcount prefix) and processed 64 at a time, one per lane, whatever word
+// they sit in -- the per-step cost is a chain of dependent memory round trips
+// nearly independent of how many lanes are active, so steps =
+// ceil(unvisited / 64) instead of the words with any unvisited vertex.  Per
+// step: row bounds and head (prefetched one step ahead), head probe, then the
+// row scan.  Found bits are OR-ed into a per-wave LDS copy of the result words
+// (s_res), written out once with the visited update; levels and unit
+// statistics are written directly (no separate update pass).
 // kQueue > 0: rows whose head probe failed are not scanned in the step that
 // probed them (a handful of lanes per step, the rest idle through the scan's
 // dependent loads) but queued in LDS (s_q, kQueue entries of row offset
 // relative to the unit's first row / length / position) and scanned kQueue at
-// a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in place.
-template <bool kPacked, bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false>
-__device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int* own, word_t* s_res,
-                                                const word_t* s_hub, long long& cnt, long long& deg,
-                                                unsigned long long* s_q = nullptr) {
+// a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in
+// place.  kRec: row bounds and heads from the packed 8-byte records of the
+// non-empty-row view (ShardView::nz_rec).
+template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false>
+__device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, word_t* s_res, const word_t* s_hub,
+                                                long long& cnt, long long& deg, unsigned long long* s_q = nullptr) {
   static_assert(kWords <= kWave, "one word per lane");
   const int lane = lane_id();
   const int64_t left = a.words - w0;
@@ -1850,8 +1590,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (lane < kWords) s_res[lane] = 0ull;
   if (total == 0) {
-    // (merge: the head pass already wrote these words)
-    if (lane < nw && !a.merge) a.new_frontier[w0 + lane] = 0ull;
+    if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1878,7 +1617,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
         static_cast<unsigned long long>(a.g.nz_pref[min((unit + 1) * kUnitWords, row_words)]), 0));
   }
   // Unvisited vertex number 64 b + lane -> its position loc = 64 j + bit in the
-  // wave's 1024 vertices (-1: no vertex), row bounds and head.
+  // wave's vertices (-1: no vertex), row bounds and head.
   // (row start, 32-bit length) keep the prefetched state small: the hub
   // kernel runs at 64 VGPRs (two 1024-thread workgroups per CU).
   auto fetch = [&](int b, int& loc, eid_t& rs, uint32_t& len, vid_t& u) {
@@ -1916,23 +1655,15 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
         // L1-resident: every lane of the wave reads one of <= 16 words)
         const int64_t k = a.g.nz_pref[w0 + j] + __popcll(~a.zdeg[w0 + j] & ((1ull << bit) - 1ull));
         if constexpr (kRec) {
-          NzRec r;
-          if constexpr (DBFS_NT_BU >= 2) {
-            const unsigned long long raw =
-                __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(nz_rec + k));
-            r.off = static_cast<uint32_t>(raw);
-            r.head = static_cast<vid_t>(raw >> 32);
-          } else {
-            r = nz_rec[k];
-          }
+          const NzRec r = nz_rec[k];
           const uint32_t end = k + 1 < u_nzend ? nz_rec[k + 1].off : u_span;
           rs = u_base + r.off;
           len = end - r.off;
-          if (!a.heads_done) u = r.head;
+          u = r.head;
         } else {
           rs = nz_ro[k];
           len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
-          if (!a.heads_done) u = a.g.nz_head[k];
+          u = a.g.nz_head[k];
         }
       } else {
         const int64_t v = w0 * 64 + loc;
@@ -1949,15 +1680,6 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   vid_t n_u;
   fetch(0, n_loc, n_rs, n_len, n_u);
   if (!head) n_u = n_len ? col[n_rs] : 0u;
-#if DBFS_BU_PF >= 2
-  // two batches' records in flight (the one after next as well)
-  int p_loc;
-  eid_t p_rs;
-  uint32_t p_len;
-  vid_t p_u;
-  fetch(1, p_loc, p_rs, p_len, p_u);
-  if (!head) p_u = p_len ? col[p_rs] : 0u;
-#endif
   int cnt32 = 0;
   // deferred row scans (kQueue): base = the unit's first row offset
   eid_t q_base = 0;
@@ -2001,7 +1723,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const bool f = bu_scan_row<kPacked || kPackFlush, kHub>(a, qrs, qe, lane >= qn, own, s_hub);
+    const bool f = bu_scan_row<kHub>(a, qrs, qe, lane >= qn, s_hub);
     settle(lane < qn && f, ql, qrs, qe);
     qn = 0;
   };
@@ -2009,39 +1731,25 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
     const int loc = n_loc;
     const eid_t rs = n_rs, e = n_rs + n_len;
     const vid_t u0 = n_u;
-#if DBFS_BU_PF >= 2
-    n_loc = p_loc;
-    n_rs = p_rs;
-    n_len = p_len;
-    n_u = p_u;
-    fetch(b + 2, p_loc, p_rs, p_len, p_u);  // in flight during the next two batches
-#else
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
-#endif
     bool found = false;
-    if (rs < e && !a.heads_done) {
-      found = bu_probe<kHub>(fr, s_hub, u0);
-    }
+    if (rs < e) found = bu_probe<kHub>(fr, s_hub, u0);
     BU_STAT(0, 1);
     BU_STAT(1, __popcll(__ballot(loc >= 0)));
     BU_STAT(2, __popcll(__ballot(found)));
-#if DBFS_BU_PF >= 2
-    if (!head) p_u = p_len ? col[p_rs] : 0u;
-#else
     if (!head) n_u = n_len ? col[n_rs] : 0u;
-#endif
     if constexpr (kQueue > 0) {
       // found by the head: settled now; unresolved rows with more neighbours
       // are queued (huge rows / spans scanned in place)
       const bool need = !found && e - rs > 1;
       const bool fits = q_span_ok && e - rs < (eid_t(1) << 20);
-      // more unresolved rows than kQueueDirect (a sparse-hit level: most lanes
-      // scan anyway, deferring gains nothing): all in place
-      const bool direct = __popcll(__ballot(need && fits)) > kQueueDirect;
+      // more unresolved rows than the queue holds (a sparse-hit level: most
+      // lanes scan anyway, deferring gains nothing): all in place
+      const bool direct = __popcll(__ballot(need && fits)) > kQueue;
       const bool inplace = need && (direct || !fits);
       if (__ballot(inplace)) {
         // (lanes not scanned here pass as resolved and keep their result)
-        const bool f = bu_scan_row<kPacked, kHub>(a, rs, e, found || !inplace, own, s_hub);
+        const bool f = bu_scan_row<kHub>(a, rs, e, found || !inplace, s_hub);
         if (inplace) found = f;
       }
       settle(found, loc, rs, e);
@@ -2054,9 +1762,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
                                   (static_cast<unsigned long long>(e - rs) << 12) | static_cast<unsigned>(loc);
       qn += k;
     } else {
-#ifndef DBFS_BU_HEAD_ONLY  // diagnostic timing build: head probes only (wrong levels)
-      found = bu_scan_row<kPacked, kHub>(a, rs, e, found, own, s_hub);
-#endif
+      found = bu_scan_row<kHub>(a, rs, e, found, s_hub);
       BU_STAT(7, __popcll(__ballot(found)));
       settle(found, loc, rs, e);
     }
@@ -2069,54 +1775,42 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, int
   __builtin_amdgcn_wave_barrier();
   if (lane < nw) {
     const word_t res = s_res[lane];
-    a.new_frontier[w0 + lane] = a.merge ? (res | a.new_frontier[w0 + lane]) : res;
+    a.new_frontier[w0 + lane] = res;
     if (res) a.visited[w0 + lane] = ~um | res;
   }
 }
 
-template <bool kPacked, bool kCompact>
+// Graphs without hubs: a wave per 16 words, 4 waves (one unit) per workgroup.
 __global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
-  __shared__ int s_bu_owner[kPacked ? kUnitThreads : 1];
-  __shared__ word_t s_res[kCompact ? kUnitWaves * kWaveWords : 1];
+  __shared__ word_t s_res[kUnitWaves * kWaveWords];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-  if (!a.hub_front) stamp_level_start(a.ctrl);
+  stamp_level_start(a.ctrl);
   long long cnt = 0, deg = 0;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + wave * kWaveWords;
-  int* own = s_bu_owner + (kPacked ? (threadIdx.x & ~(kWave - 1)) : 0);
-  if constexpr (kCompact)
-    bu_wave_compact<kPacked, false>(a, w0, own, s_res + wave * kWaveWords, nullptr, cnt, deg);
-  else
-    bu_wave<kPacked, false>(a, w0, own, nullptr, cnt, deg);
+  bu_wave_compact<false>(a, w0, s_res + wave * kWaveWords, nullptr, cnt, deg);
   unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
 }
 
-// Hub variant: persistent 1024-thread workgroups (two per CU: 32 waves) that
-// first stage the hub frontier bits (<= kMaxHubs bits, 64 KiB) in LDS; a
-// hub-encoded head is then probed in LDS instead of by a scattered load of the
+// Hub variant: persistent workgroups (two per CU) that first stage the hub
+// frontier bits (<= kMaxHubs bits, 64 KiB) in LDS; a hub-encoded head or
+// neighbour is then probed in LDS instead of by a scattered load of the
 // 8 MiB (RMAT-26) frontier bitmap -- at the dominant bottom-up level ~80% of
-// the unvisited vertices resolve at their head, ~85% of heads are hubs.  Four
-// unit groups of 4 waves walk the units; every workgroup runs the same number
-// of iterations (barriers stay uniform).
-#ifndef DBFS_HUB_BU_THREADS
-#define DBFS_HUB_BU_THREADS 1024
-#endif
-constexpr int kHubBuThreads = DBFS_HUB_BU_THREADS;
+// the unvisited vertices resolve at their head, ~85% of heads are hubs.
+// kWhole: one whole 64-word unit per wave (its statistics need no cross-wave
+// reduction, so waves run independently) -- chosen when the shard has enough
+// units to fill the chip that way (one GPU); small shards (many ranks) keep
+// 16 words per wave, four waves per unit, for parallelism.
+constexpr int kHubBuThreads = 1024;
 static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
-
-template <bool kPacked, bool kCompact, bool kWhole = false, int kThreads = kHubBuThreads, int kQ = kBuQueue,
-          bool kRec = false>
+template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
-  // per-wave scratch of the packed row scans (kPacked, or the queue flushes)
-  constexpr bool kOwn = kPacked;
-  __shared__ int s_bu_owner[kOwn ? kThreads : 1];
-  __shared__ word_t s_res[kCompact ? (kThreads / kWave) * kUnitWords : 1];
+  __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
-  constexpr int kQueueLen = (kCompact && !kPacked) ? kQ : 0;
-  __shared__ unsigned long long s_q[kQueueLen > 0 ? (kThreads / kWave) * kQueueLen : 1];
+  __shared__ unsigned long long s_q[kQ > 0 ? (kThreads / kWave) * kQ : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
@@ -2127,60 +1821,28 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   if constexpr (kWhole) {
-    // compacted: one whole 64-word unit per wave (its statistics need no
-    // cross-wave reduction, so waves run independently: no barrier).  Chosen
-    // when the shard has enough units to fill the chip this way (one GPU);
-    // small shards (many ranks) keep 16 words per wave for parallelism.
     constexpr int kWavesPerBlock = kThreads / kWave;
-    int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
     // (fused finish: this wave's totals accumulate in its LDS slots)
     if (lane_id() == 0) {
       s_c[wave] = 0;
       s_d[wave] = 0;
     }
-    auto unit = [&](int64_t u) {
+    // Static stride over the units.  (A dynamic unit queue measured slower:
+    // RMAT-26 per level 387 / 182 / 104 against 346 / 137 / 30 us -- the
+    // returning device-scope atomics cost more than the stride's imbalance.)
+    for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+         u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<kPacked, true, kUnitWords, kQueueLen, kRec>(a, u * kUnitWords, own, s_res + wave * kUnitWords,
-                                                                  s_hub, cnt, deg, s_q + wave * kQueueLen);
+      bu_wave_compact<true, kUnitWords, kQ, kRec>(a, u * kUnitWords, s_res + wave * kUnitWords, s_hub, cnt, deg,
+                                                  s_q + wave * kQ);
       cnt = wave_sum(cnt);
       deg = wave_sum(deg);
       if (lane_id() == 0) {
-        a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + cnt : cnt;
-        a.unit_deg[u] = a.merge ? a.unit_deg[u] + deg : deg;
+        a.unit_cnt[u] = cnt;
+        a.unit_deg[u] = deg;
         s_c[wave] += cnt;
         s_d[wave] += deg;
       }
-    };
-    if (a.unit_queue) {
-      // dynamic: a static stride gives every wave 2-3 units whose cost differs
-      // by their unvisited rows, and the level lasts as long as the slowest
-      // wave.  Here each wave takes its first unit statically (all waves
-      // starting at once would serialise on one counter), then further units
-      // from a device-scope counter of its workgroup group (blockIdx % 8: the
-      // round-robin XCD placement, so each counter serves one XCD's waves and
-      // takes ~1/8 of the dequeues).  The last wave to leave resets the
-      // counters for the next launch (every wave leaves once, after its last
-      // dequeue).
-      const int64_t waves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-      const unsigned ngroups = gridDim.x < kBuQueueGroups ? gridDim.x : kBuQueueGroups;
-      const unsigned grp = blockIdx.x % ngroups;
-      int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave;
-      while (u < nunits) {
-        unit(u);
-        unsigned got = 0;
-        if (lane_id() == 0) got = atomicAdd(a.unit_queue + grp * kBuQueueStride, 1u);
-        const int64_t k = static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(got)));
-        u = waves + k * ngroups + grp;
-      }
-      if (lane_id() == 0) {
-        const unsigned left = atomicAdd(a.unit_queue + kBuQueueGroups * kBuQueueStride, 1u);
-        if (left == static_cast<unsigned>(waves) - 1u)
-          for (int i = 0; i <= kBuQueueGroups; ++i) atomicExch(a.unit_queue + i * kBuQueueStride, 0u);
-      }
-    } else {
-      for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
-           u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock)
-        unit(u);
     }
     if (!a.fuse_scan) return;
     // fused finish: the workgroup's totals into its own slot of tot
@@ -2201,7 +1863,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned prev = atomicAdd(a.scan.ticket, 1u);
       s_last = prev == gridDim.x - 1;
-      if (s_last) DBFS_LAST_ARRIVER_ACQUIRE();
+      if (s_last) last_arriver_acquire();
     }
     __syncthreads();
     if (!s_last) return;
@@ -2230,6 +1892,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     }
     return;
   }
+  // 16 words per wave: unit groups of 4 waves walk the units; every workgroup
+  // runs the same number of iterations (barriers stay uniform)
   constexpr int kGroups = kThreads / kUnitThreads;
   const int group = wave / kUnitWaves;
   const int wg = wave % kUnitWaves;
@@ -2237,15 +1901,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
-    if (u < nunits) {
-      int* own = s_bu_owner + (kOwn ? (threadIdx.x & ~(kWave - 1)) : 0);
-      if constexpr (kCompact)
-        bu_wave_compact<kPacked, true, kWaveWords, kQueueLen, kRec>(a, u * kUnitWords + wg * kWaveWords, own,
-                                                                    s_res + wave * kWaveWords, s_hub, cnt, deg,
-                                                                    s_q + wave * kQueueLen);
-      else
-        bu_wave<kPacked, true>(a, u * kUnitWords + wg * kWaveWords, own, s_hub, cnt, deg);
-    }
+    if (u < nunits)
+      bu_wave_compact<true, kWaveWords, kQ, kRec>(a, u * kUnitWords + wg * kWaveWords, s_res + wave * kWaveWords, s_hub,
+                                                  cnt, deg, s_q + wave * kQ);
     cnt = wave_sum(cnt);
     deg = wave_sum(deg);
     if (lane_id() == 0) {
@@ -2260,8 +1918,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
         c += s_c[group * kUnitWaves + k];
         d += s_d[group * kUnitWaves + k];
       }
-      a.unit_cnt[u] = a.merge ? a.unit_cnt[u] + c : c;
-      a.unit_deg[u] = a.merge ? a.unit_deg[u] + d : d;
+      a.unit_cnt[u] = c;
+      a.unit_deg[u] = d;
     }
     __syncthreads();
   }
@@ -2315,139 +1973,9 @@ __global__ __launch_bounds__(kBlock) void hub_apply_kernel(HubApplyArgs a) {
         DBFS_DCHECK(i + j < a.g.td_nhubs, 9, i + j);
         const vid_t v = a.g.td_hub_vertex[i + j];
         a.level8[v] = lv;
-        if (a.dirty) a.dirty[v >> 6] = 1;
       }
     *p = make_uint4(0u, 0u, 0u, 0u);
   }
-}
-
-// Head pass of a split bottom-up level (BuHeadArgs): one wave per 64-word unit,
-// one word per step (lane = vertex).  An unvisited vertex's hub-encoded head
-// (dense non-empty-row view) is tested in the all-reduced hub frontier bits
-// (64 KiB, L2-resident) or, when it is an owned vertex, in the owned frontier
-// slice; anything else waits for bu_step(merge) after the all-gather.  Every
-// owned word of new_frontier and every unit's statistics are written.
-//
-// The pass is a chain of dependent loads per word (head -> frontier bit ->
-// row bounds), so the words are taken kHeadGroup at a time with every load of
-// the group in flight together (one word at a time left the first bottom-up
-// level of RMAT-26 latency-bound); the result words are collected in lane j's
-// register and written once per unit, coalesced.
-#ifndef DBFS_BU_HEAD_GROUP
-#define DBFS_BU_HEAD_GROUP 8
-#endif
-constexpr int kHeadGroup = DBFS_BU_HEAD_GROUP;
-static_assert(kUnitWords % kHeadGroup == 0, "head groups tile a unit");
-
-// kRec: heads and row lengths from the packed row records (ShardView::nz_rec;
-// 32-bit lengths, one 8-byte record load per head).
-template <bool kRec>
-__global__ __launch_bounds__(kBlock) void bu_head_kernel(BuHeadArgs a) {
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-  if (a.stamp) stamp_level_start(a.ctrl);
-  const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
-                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
-  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-  if (unit >= nunits) return;
-  const int64_t w0 = unit * kUnitWords;
-  const int nw = static_cast<int>(min<int64_t>(kUnitWords, a.words - w0));
-  // the words of the unit, one per lane (visited includes zero-degree and padding)
-  const word_t vis_l = lane < nw ? a.visited[w0 + lane] : ~0ull;
-  const word_t zd_l = lane < nw ? a.zdeg[w0 + lane] : ~0ull;
-  const int64_t nzw = (a.g.rows + kWordBits - 1) / kWordBits;  // words of the non-empty-row view
-  const int64_t pref_l = (lane < nw && w0 + lane < nzw) ? a.g.nz_pref[w0 + lane] : 0;
-  const int64_t lo = a.g.lo, hi = a.g.lo + a.g.rows;
-  const word_t below = (1ull << lane) - 1ull;
-  long long cnt = 0, deg = 0;
-  word_t res_l = 0;  // result word `lane` of the unit
-  // packed records: the unit's span and end of its non-empty rows (uniform)
-  uint32_t u_span = 0;
-  int64_t u_nzend = 0;
-  if constexpr (kRec) {
-    u_span = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-        static_cast<int>(a.g.unit_base[unit + 1] - a.g.unit_base[unit])));
-    u_nzend = static_cast<int64_t>(readlane64(
-        static_cast<unsigned long long>(a.g.nz_pref[min((unit + 1) * kUnitWords, nzw)]), 0));
-  }
-  for (int j0 = 0; j0 < nw; j0 += kHeadGroup) {
-    int64_t k[kHeadGroup];
-    vid_t u[kHeadGroup];
-    bool act[kHeadGroup];
-    // (1) heads of the group's unvisited vertices
-#pragma unroll
-    for (int i = 0; i < kHeadGroup; ++i) {
-      const int j = j0 + i;
-      const word_t vis = j < nw ? readlane64(vis_l, j) : ~0ull;
-      act[i] = a.probe && !((vis >> lane) & 1ull);
-      k[i] = 0;
-      u[i] = 0;
-      if (act[i]) {
-        // unvisited implies non-zero degree (zero-degree bits are pre-set)
-        k[i] = readlane_i64(pref_l, j) + __popcll(~readlane64(zd_l, j) & below);
-        u[i] = kRec ? a.g.nz_rec[k[i]].head : a.g.nz_head[k[i]];
-      }
-    }
-    // (2) frontier bits of the heads
-    bool found[kHeadGroup];
-#pragma unroll
-    for (int i = 0; i < kHeadGroup; ++i) {
-      found[i] = false;
-      if (act[i]) {
-        if (u[i] & kHubFlag) {
-          const vid_t h = u[i] & ~kHubFlag;
-          found[i] = (a.hub_front[h >> 6] >> (h & 63)) & 1ull;
-        } else if (u[i] >= lo && u[i] < hi) {
-          const int64_t r = static_cast<int64_t>(u[i]) - lo;
-          found[i] = (a.frontier_own[r >> 6] >> (r & 63)) & 1ull;
-        }
-      }
-    }
-    // (3) settled vertices: row lengths (statistics) and levels
-    eid_t len[kHeadGroup];
-#pragma unroll
-    for (int i = 0; i < kHeadGroup; ++i) {
-      len[i] = 0;
-      if (found[i]) {
-        if constexpr (kRec) {
-          const uint32_t s0 = a.g.nz_rec[k[i]].off;
-          const uint32_t s1 = k[i] + 1 < u_nzend ? a.g.nz_rec[k[i] + 1].off : u_span;
-          len[i] = s1 - s0;
-        } else {
-          len[i] = a.g.nz_row_off[k[i] + 1] - a.g.nz_row_off[k[i]];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < kHeadGroup; ++i) {
-      const word_t res = __ballot(found[i]);
-      if (lane == j0 + i) res_l = res;
-      if (found[i]) {
-        store_level(a.level, a.level8, (w0 + j0 + i) * 64 + lane, a.new_level, a.narrow_base);
-        cnt += 1;
-        deg += len[i];
-      }
-    }
-  }
-  if (lane < nw) {
-    a.new_frontier[w0 + lane] = res_l;
-    if (res_l) a.visited[w0 + lane] = vis_l | res_l;
-  }
-  wave_unit_stats_store(cnt, deg, unit, a.unit_cnt, a.unit_deg);
-}
-
-// Owned hubs' bits of the new frontier (HubLocalArgs): one wave per hub word.
-__global__ __launch_bounds__(kBlock) void hub_local_kernel(HubLocalArgs a) {
-  if (a.ctrl && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
-  const int64_t h = w * kWave + lane_id();
-  bool bit = false;
-  if (h < a.g.nhubs) {
-    const int64_t r = static_cast<int64_t>(a.g.hub_vertex[h]) - a.g.lo;
-    bit = r >= 0 && r < a.g.rows && ((a.frontier_own[r >> 6] >> (r & 63)) & 1ull);
-  }
-  const word_t m = __ballot(bit);
-  if (lane_id() == 0 && w * kWave < a.g.nhubs) a.out[w] = m;
 }
 
 // Zero-degree / padding mask of the owned slice (computed once per graph).
@@ -2505,10 +2033,7 @@ int device_cus();
 
 void init_run(const InitRunArgs& a, hipStream_t st) {
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
-#ifndef DBFS_INIT_BLOCKS_PER_CU
-#define DBFS_INIT_BLOCKS_PER_CU 8
-#endif
-  init_run_kernel<<<grid_for(work, kBlock, DBFS_INIT_BLOCKS_PER_CU * device_cus()), kBlock, 0, st>>>(a);
+  init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
 }
 
 void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st) {
@@ -2575,27 +2100,27 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   if (a.ctrl) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;
-    const bool b32 = DBFS_TD_BASE32 && a.g.nnz <= (int64_t(1) << 32);
+    const bool b32 = a.g.nnz <= (int64_t(1) << 32);
     const int64_t fgrid = a.grid_filter > 0 ? a.grid_filter : a.grid;
-#define DBFS_TD_DEV(OUT, F, B) \
+#define LAUNCH_TD_DEV(OUT, F, B) \
   td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
     if (a.lists)
-      DBFS_TD_DEV(TdOut::Lists, false, false);
+      LAUNCH_TD_DEV(TdOut::Lists, false, false);
     else if (a.td_hub_vis && b32)
-      DBFS_TD_DEV(TdOut::Dyn, true, true);
+      LAUNCH_TD_DEV(TdOut::Dyn, true, true);
     else if (a.td_hub_vis)
-      DBFS_TD_DEV(TdOut::Dyn, true, false);
+      LAUNCH_TD_DEV(TdOut::Dyn, true, false);
     else if (b32)
-      DBFS_TD_DEV(TdOut::Dyn, false, true);
+      LAUNCH_TD_DEV(TdOut::Dyn, false, true);
     else
-      DBFS_TD_DEV(TdOut::Dyn, false, false);
-#undef DBFS_TD_DEV
+      LAUNCH_TD_DEV(TdOut::Dyn, false, false);
+#undef LAUNCH_TD_DEV
     return;
   }
   if (a.m <= 0 || a.q <= 0) return;
   const unsigned grid = grid_for(a.m, kTdEdgesPerBlock);
   const bool wide = static_cast<int64_t>(grid) < a.wide_below_blocks;
-#define DBFS_TD_LAUNCH(OUT)                                                  \
+#define LAUNCH_TD(OUT)                                                  \
   do {                                                                       \
     if (wide)                                                                \
       td_expand_kernel<OUT, 1024><<<grid, 1024, 0, st>>>(a);                 \
@@ -2603,12 +2128,12 @@ void td_expand(const TdArgs& a, hipStream_t st) {
       td_expand_kernel<OUT, kTdThreads><<<grid, kTdThreads, 0, st>>>(a);     \
   } while (0)
   if (a.lists)
-    DBFS_TD_LAUNCH(TdOut::Lists);
+    LAUNCH_TD(TdOut::Lists);
   else if (a.next_bytes)
-    DBFS_TD_LAUNCH(TdOut::Bytes);
+    LAUNCH_TD(TdOut::Bytes);
   else
-    DBFS_TD_LAUNCH(TdOut::Bits);
-#undef DBFS_TD_LAUNCH
+    LAUNCH_TD(TdOut::Bits);
+#undef LAUNCH_TD
 }
 
 void td_binned(const BinArgs& a, hipStream_t st) {
@@ -2684,34 +2209,17 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-    // compacted: a whole 64-word unit per wave when the shard has enough units
-    // to fill every resident wave slot (one GPU); small shards (many ranks)
-    // keep 16 words per wave for parallelism
+    // a whole 64-word unit per wave when the shard has enough units to fill
+    // every resident wave slot (one GPU); small shards (many ranks) keep 16
+    // words per wave for parallelism
     const int64_t slots = 2 * static_cast<int64_t>(device_cus()) * (kHubBuThreads / kWave);
-    const bool whole = a.compact && !a.packed && (a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots));
+    const bool whole = a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots);
     // a bottom-up level after another one (few unvisited vertices left, most
-    // of them scanning rows): 768-thread workgroups, 80 VGPRs instead of 64
-#ifndef DBFS_BU_FOLLOW_THREADS
-#define DBFS_BU_FOLLOW_THREADS 768
-#endif
-    constexpr int kFollowThreads = DBFS_BU_FOLLOW_THREADS;
-#ifndef DBFS_BU_FOLLOW_QUEUE
-#define DBFS_BU_FOLLOW_QUEUE DBFS_BU_QUEUE
-#endif
-    constexpr int kFollowQueue = DBFS_BU_FOLLOW_QUEUE;
-    // first bottom-up level, whole units (any multiple of 64 threads: no unit groups)
-#ifndef DBFS_BU_FIRST_THREADS
-#define DBFS_BU_FIRST_THREADS DBFS_HUB_BU_THREADS
-#endif
-    constexpr int kFirstThreads = DBFS_BU_FIRST_THREADS;
-    const int threads = whole ? (a.follow_up ? kFollowThreads : kFirstThreads) : kHubBuThreads;
-    unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
-    if (whole && a.balanced_grid && !a.unit_queue) {
-      const int64_t wpb = threads / kWave;
-      const int64_t per_wave = (nunits + static_cast<int64_t>(grid) * wpb - 1) / (static_cast<int64_t>(grid) * wpb);
-      grid = grid_for(nunits, per_wave * wpb);
-    }
-#define DBFS_BU_HUB(P, C) bu_hub_kernel<P, C><<<grid, kHubBuThreads, 0, st>>>(a)
+    // of them scanning rows): whole units in 768-thread workgroups (80 VGPRs
+    // instead of 64); 16-word waves without the row queue (measured)
+    constexpr int kFollowThreads = 768;
+    const int threads = whole ? (a.follow_up ? kFollowThreads : kHubBuThreads) : kHubBuThreads;
+    const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
     if (whole && a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
@@ -2722,51 +2230,31 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
       return;
     }
-    if (whole && a.follow_up && rec)
-      bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue, true><<<grid, kFollowThreads, 0, st>>>(a);
-    else if (whole && a.follow_up)
-      bu_hub_kernel<false, true, true, kFollowThreads, kFollowQueue><<<grid, kFollowThreads, 0, st>>>(a);
-    else if (whole && rec)
-      bu_hub_kernel<false, true, true, kFirstThreads, kBuQueue, true><<<grid, kFirstThreads, 0, st>>>(a);
-    else if (whole)
-      bu_hub_kernel<false, true, true, kFirstThreads><<<grid, kFirstThreads, 0, st>>>(a);
-    if (whole) return;  // (the whole-unit kernels run a fused scan themselves)
-    else if (a.packed)
-      a.compact ? DBFS_BU_HUB(true, true) : DBFS_BU_HUB(true, false);
-    else if (a.compact && a.follow_up && rec)  // scan-heavy later level: no deferral (measured)
-      bu_hub_kernel<false, true, false, kHubBuThreads, 0, true><<<grid, kHubBuThreads, 0, st>>>(a);
-    else if (a.compact && a.follow_up)
-      bu_hub_kernel<false, true, false, kHubBuThreads, 0><<<grid, kHubBuThreads, 0, st>>>(a);
-    else if (a.compact && rec)
-      bu_hub_kernel<false, true, false, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
+    if (whole) {
+      // (the whole-unit kernels run the fused finish themselves)
+      if (a.follow_up && rec)
+        bu_hub_kernel<true, kFollowThreads, kBuQueue, true><<<grid, kFollowThreads, 0, st>>>(a);
+      else if (a.follow_up)
+        bu_hub_kernel<true, kFollowThreads, kBuQueue><<<grid, kFollowThreads, 0, st>>>(a);
+      else if (rec)
+        bu_hub_kernel<true, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
+      else
+        bu_hub_kernel<true, kHubBuThreads, kBuQueue><<<grid, kHubBuThreads, 0, st>>>(a);
+      return;
+    }
+    if (a.follow_up && rec)
+      bu_hub_kernel<false, kHubBuThreads, 0, true><<<grid, kHubBuThreads, 0, st>>>(a);
+    else if (a.follow_up)
+      bu_hub_kernel<false, kHubBuThreads, 0><<<grid, kHubBuThreads, 0, st>>>(a);
+    else if (rec)
+      bu_hub_kernel<false, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
     else
-      a.compact ? DBFS_BU_HUB(false, true) : DBFS_BU_HUB(false, false);
-#undef DBFS_BU_HUB
+      bu_hub_kernel<false, kHubBuThreads, kBuQueue><<<grid, kHubBuThreads, 0, st>>>(a);
     if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
     return;
   }
-  const unsigned grid = grid_for(a.words, kUnitWords);
-#define DBFS_BU(P, C) bu_kernel<P, C><<<grid, kUnitThreads, 0, st>>>(a)
-  if (a.packed)
-    a.compact ? DBFS_BU(true, true) : DBFS_BU(true, false);
-  else
-    a.compact ? DBFS_BU(false, true) : DBFS_BU(false, false);
-#undef DBFS_BU
+  bu_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
   if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
-}
-
-void bu_head(const BuHeadArgs& a, hipStream_t st) {
-  if (a.words <= 0) return;
-  const unsigned grid = grid_for(a.words, kUnitWords * kUnitsPerBlock);
-  if (a.g.nz_rec && a.g.unit_base)
-    bu_head_kernel<true><<<grid, kBlock, 0, st>>>(a);
-  else
-    bu_head_kernel<false><<<grid, kBlock, 0, st>>>(a);
-}
-
-void hub_local(const HubLocalArgs& a, hipStream_t st) {
-  if (a.g.nhubs <= 0) return;
-  hub_local_kernel<<<grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
 }
 
 #ifdef DBFS_CHECKED

@@ -36,8 +36,6 @@ void hub_apply(const HubApplyArgs& a, hipStream_t st);
 bool checks_enabled();
 unsigned long long take_check_error();
 void inject_check_failure(hipStream_t st);
-void bu_head(const BuHeadArgs& a, hipStream_t st);
-void hub_local(const HubLocalArgs& a, hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
 

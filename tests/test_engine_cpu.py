@@ -258,7 +258,7 @@ def test_id_order_top_down_copy_keeps_levels(rt):
         assert np.array_equal(row, np.sort(np.asarray(csr.col)[ro[r]:ro[r + 1]]))
     for mode in ("do", "td", "bu"):
         bfs.mode = mode
-        for opt in ({}, {"bu_hub_col": 0}, {"device_loop": 0}):
+        for opt in ({}, {"device_loop": 0}):
             for k, v in opt.items():
                 bfs.engine.set_option(k, v)
             for s in (4, 77):
@@ -541,33 +541,6 @@ def test_td_direct_levels_cpu(rt, mode, direct_edges):
     cb.engine.set_option("td_direct_edges", direct_edges)
     cb.run(0)
     assert np.array_equal(cb.levels(), np.arange(n))
-
-
-@pytest.mark.parametrize("prefill", [1, 2])
-@pytest.mark.parametrize("mode", ["do", "td", "bu"])
-def test_level_prefill_cpu(rt, mode, prefill):
-    # double-buffered level bytes (the next run's buffer prefilled): exact
-    # over consecutive runs
-    p = dbfs.rmat_params(11, 16, 9)
-    csr = dbfs.host_csr_from_params(p)
-    bfs = dbfs.BFS(p, rt, mode=mode)
-    bfs.engine.set_option("level_prefill", prefill)
-    for src in bfs.sample_roots(4, seed=3):
-        bfs.run(src)
-        assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
-
-
-@pytest.mark.parametrize("mode", ["do", "td"])
-def test_td_dirty_words_cpu(rt, mode):
-    # dirty-word marking of small direct top-down levels: exact
-    p = dbfs.rmat_params(12, 16, 61)
-    csr = dbfs.host_csr_from_params(p)
-    bfs = dbfs.BFS(p, rt, mode=mode)
-    bfs.engine.set_option("td_dirty_words", 1)
-    bfs.engine.set_option("td_direct_edges", 0)
-    for src in bfs.sample_roots(3, seed=5):
-        bfs.run(src)
-        assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
 
 
 @pytest.mark.parametrize("mode", ["do", "td"])

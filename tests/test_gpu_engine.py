@@ -270,16 +270,14 @@ def test_device_loop_matches_host_loop_gpu(gpu_runtime, mode, byte_edges):
         assert all(l["ms"] > 0 for l in a.levels)
 
 
-@pytest.mark.parametrize("packed", [0, 1])
 @pytest.mark.parametrize("lane_limit", [1, 8, 64])
-def test_bottom_up_variants_gpu(gpu_runtime, packed, lane_limit):
-    """Bottom-up phase 2 (packed multi-row edge stream vs one row at a time)
-    at several per-lane phase lengths, pure BU and direction-optimising."""
+def test_bottom_up_variants_gpu(gpu_runtime, lane_limit):
+    """Bottom-up phase 2 (the wave scans unresolved rows one at a time) after
+    per-lane phases of several lengths, pure BU and direction-optimising."""
     p = dbfs.rmat_params(17, 16, 47)
     csr = dbfs.host_csr_from_params(p)
     for mode in ["bu", "do"]:
         bfs = dbfs.BFS(p, gpu_runtime, mode=mode, bu_lane_limit=lane_limit)
-        bfs.engine.set_option("bu_packed", packed)
         for src in bfs.sample_roots(3, seed=lane_limit):
             _check(bfs, csr, src)
 
@@ -301,8 +299,7 @@ def test_perf_regression_do_vs_ref_gpu(gpu_runtime):
 
 @pytest.mark.parametrize("whole", [1, -1])
 @pytest.mark.parametrize("max_hubs", [None, 64, 3000, 0])
-@pytest.mark.parametrize("packed", [0, 1])
-def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed, whole):
+def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, whole):
     """Bottom-up with hub-encoded heads probed in the LDS copy of the hub
     frontier bits: every vertex a hub (default cap on a small graph), a few
     hubs (mixed LDS / global head probes), no hubs (plain kernel)."""
@@ -314,7 +311,6 @@ def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed, whole):
             assert bfs.graph.nhubs <= max_hubs
         if max_hubs != 0:
             assert bfs.graph.nhubs > 0
-        bfs.engine.set_option("bu_packed", packed)
         bfs.engine.set_option("bu_whole_units", whole)  # 64 / 16 words per wave (compacted hub kernel)
         for src in bfs.sample_roots(3, seed=11):
             _check(bfs, csr, src)
@@ -322,37 +318,14 @@ def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, packed, whole):
         _check(bfs, csr, bfs.sample_roots(1, seed=12)[0])
 
 
-@pytest.mark.parametrize("head_pass", [0, 1, 2])
-@pytest.mark.parametrize("max_hubs", [None, 3000])
-@pytest.mark.parametrize("whole", [1, -1])
-def test_bottom_up_head_pass_gpu(gpu_runtime, head_pass, max_hubs, whole):
-    """One rank, bottom-up levels split into a head pass (bu_head: every
-    unvisited vertex's row head probed, eight words in flight per wave) and the
-    merging full pass that only scans the rows whose head missed (heads_done):
-    off, first bottom-up level only, every bottom-up level."""
-    p = dbfs.rmat_params(16, 16, 71)
-    csr = dbfs.host_csr_from_params(p)
-    for mode in ["bu", "do"]:
-        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, max_hubs=max_hubs)
-        bfs.engine.set_option("bu_head_pass", head_pass)
-        bfs.engine.set_option("bu_whole_units", whole)
-        for src in bfs.sample_roots(3, seed=13):
-            _check(bfs, csr, src)
-
-
-@pytest.mark.parametrize("head_pass,dyn", [(0, 0), (1, 0), (0, 1)])
-def test_full_scale_rmat20_gpu(gpu_runtime, head_pass, dyn):
+def test_full_scale_rmat20_gpu(gpu_runtime):
     """RMAT-20 at the default thresholds, exact against the CPU oracle: whole
     64-word units per wave chosen by occupancy (16 K units >= the resident wave
-    slots), 2^19 hubs, deferred row scans, sparse and dense top-down levels;
-    also with units handed out dynamically (bu_dyn_units, whose counters the
-    last wave re-zeroes for the next launch)."""
+    slots), 2^19 hubs, deferred row scans, sparse and dense top-down levels."""
     p = dbfs.rmat_params(20, 16, 5)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode="do")
     assert bfs.graph.nhubs > 1 << 16
-    bfs.engine.set_option("bu_head_pass", head_pass)
-    bfs.engine.set_option("bu_dyn_units", dyn)
     dirs = set()
     for src in bfs.sample_roots(2, seed=21):
         res = _check(bfs, csr, src)
@@ -788,39 +761,6 @@ def test_bottom_up_long_row_scanned_in_place_gpu(gpu_runtime):
         _check(bfs, csr, 0)
 
 
-@pytest.mark.parametrize("prefill", [1, 2])
-@pytest.mark.parametrize("mode", ["do", "td", "bu"])
-def test_level_prefill_gpu(gpu_runtime, mode, prefill):
-    """level_prefill: the next run's level bytes filled on the side stream
-    under the current run (double buffer); consecutive runs stay exact, also
-    across a deep chain that falls back to 32-bit levels."""
-    p = dbfs.rmat_params(16, 16, 53)
-    csr = dbfs.host_csr_from_params(p)
-    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
-    bfs.engine.set_option("level_prefill", prefill)
-    for src in bfs.sample_roots(4, seed=7):
-        _check(bfs, csr, src)
-    n = 400
-    chain = dbfs.build_csr(n, np.arange(n - 1, dtype=np.uint32), np.arange(1, n, dtype=np.uint32))
-    cb = dbfs.BFS(chain, gpu_runtime, mode="td" if mode == "bu" else mode)
-    cb.engine.set_option("level_prefill", prefill)
-    _check(cb, chain, 0)
-    _check(cb, chain, 5)
-
-
-@pytest.mark.parametrize("mode", ["do", "td"])
-def test_td_dirty_words_gpu(gpu_runtime, mode):
-    """td_dirty_words: small direct top-down levels mark the words they store
-    into and the update gathers only those; exact against the oracle."""
-    p = dbfs.rmat_params(17, 16, 61)
-    csr = dbfs.host_csr_from_params(p)
-    bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
-    bfs.engine.set_option("td_dirty_words", 1)
-    bfs.engine.set_option("td_direct_edges", 0)
-    for src in bfs.sample_roots(3, seed=5):
-        _check(bfs, csr, src)
-
-
 @pytest.mark.parametrize("mode", ["do", "td"])
 def test_td_fused_finish_gpu(gpu_runtime, mode):
     """td_fused_finish: the update's last workgroup finishes dense top-down
@@ -854,7 +794,7 @@ def test_run_many_gpu(gpu_runtime, mode):
 def test_eight_virtual_ranks_rmat22_defaults_gpu():
     """P = 8 virtual ranks at RMAT-22 with the default thresholds: the shard
     (2^19 vertices) takes the 16-word bottom-up waves, the hubs are the full
-    2^19, and sparse chains carry owner lists far past 1024 entries; the
+    2^19, and the small top-down levels are sparse chains with owner lists; the
     levels equal the one-rank run's and the oracle's."""
     p = dbfs.rmat_params(22, 16, 3)
     csr = dbfs.host_csr_from_params(p)
@@ -880,7 +820,7 @@ def test_eight_virtual_ranks_rmat22_defaults_gpu():
     for levels, caps, nhubs in run_virtual_ranks(8, body, device="hip"):
         for got, e in zip(levels, exp):
             assert np.array_equal(got, e)
-        assert caps and max(caps) > 1024
+        assert caps  # sparse chains with owner lists at P = 8
         assert nhubs > 0
 
 

@@ -15,5 +15,5 @@ timeout -k 10 300 python bench.py --steps 16 --warmup 3 > gpurun_out/${TAG}_benc
 python3 -c "import json; d=json.loads(open('gpurun_out/${TAG}_bench.json').read().strip().splitlines()[-1]); print('%8.1f GTEPS %7.3f ms/step validated %s' % (d['value'], d['ms_per_step'], d['validated_roots']))"
 if [ "${SHADOW:-1}" = 1 ]; then
   echo "== shadow"
-  CFGS="${CFGS:-26 8 0,7}" TAG=$TAG bash tools/gpu_shadow.sh
+  CFGS="${CFGS:-26:8:0,7}" TAG=$TAG bash tools/gpu_shadow.sh
 fi
