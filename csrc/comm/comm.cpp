@@ -69,6 +69,13 @@ void Comm::allgather_allreduce(const void* send, void* recv, size_t bytes, int64
   if (groups()) note_fused();
 }
 
+void Comm::level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                     const LevelFinishArgs& fin) {
+  if (gbytes > 0) allgather_allreduce(gsend, grecv, gbytes, buf, count);
+  else allreduce_sum_i64(buf, count);
+  be_->level_finish(fin);
+}
+
 // ---- LocalComm ----------------------------------------------------------------
 
 void LocalComm::alltoall(const void* send, void* recv, size_t bytes) {

@@ -220,6 +220,11 @@ void PeerComm::run(const Plan& plan) {
     unit = std::min(unit, 8);
     ua.sum_count = plan.sum_count;
     ua.sum_out = plan.sum_buf;
+    if (plan.finish) {
+      DBFS_CHECK(plan.sum_count <= kern::kPeerFinishMax, "PeerComm: a level end reduces at most 256 totals");
+      ua.has_finish = true;
+      ua.finish = *plan.finish;
+    }
   }
   DBFS_CHECK(unit >= 4, "PeerComm payloads must be multiples of 4 bytes, 4-byte aligned");
   DBFS_CHECK(!plan.counted || unit >= 4, "PeerComm: counted lists need 4-byte granules");
@@ -355,6 +360,33 @@ void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t strid
     pl.send[p] = {send + p * stride_words, nullptr, cap_b};
     pl.recv[p] = {nullptr, recv + p * stride_words, cap_b};
   }
+  run(pl);
+}
+
+void PeerComm::level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                         const LevelFinishArgs& fin) {
+  const size_t need = (gbytes + 15) / 16 * 16 + count * sizeof(int64_t);
+  if (need > slot_ || gbytes % 4 || count == 0 || static_cast<int64_t>(count) > kern::kPeerFinishMax) {
+    Comm::level_end(gsend, grecv, gbytes, buf, count, fin);
+    return;
+  }
+  // one launch: the frontier slices and the totals pushed, the flags, the
+  // slices unpacked, the totals summed and the level decided by one thread
+  Plan pl;
+  if (gbytes > 0) {
+    note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(gbytes));
+    note_fused();
+    pl.send.resize(static_cast<size_t>(size_));
+    pl.recv.resize(static_cast<size_t>(size_));
+    for (int p = 0; p < size_; ++p) {
+      pl.send[p] = {gsend, nullptr, static_cast<int64_t>(gbytes)};
+      pl.recv[p] = {nullptr, static_cast<char*>(grecv) + p * gbytes, static_cast<int64_t>(gbytes)};
+    }
+  }
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  pl.sum_count = static_cast<int64_t>(count);
+  pl.sum_buf = buf;
+  pl.finish = &fin;
   run(pl);
 }
 

@@ -1257,10 +1257,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     int64_t* blk = sblk(level);
     // level L writes frontier_[L & 1] (the seed: frontier_[1])
     const int out = seed ? 1 : (level & 1);
-    if (gather)
-      comm_.allgather_allreduce(fr_own(out), frontier_[out].data(), static_cast<size_t>(W) * sizeof(word_t), blk + 2, 2);
-    else
-      comm_.allreduce_sum_i64(blk + 2, 2);
     LevelFinishArgs fa;
     fa.stats = blk;
     fa.ctrl = ctrl_.data();
@@ -1271,7 +1267,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     fa.seed = seed;
     fa.expect_dir = expect_dir;
     fa.expect_cap = cap;
-    be_.level_finish(fa);
+    comm_.level_end(fr_own(out), frontier_[out].data(), gather ? static_cast<size_t>(W) * sizeof(word_t) : 0,
+                    blk + 2, 2, fa);
   };
   // the seed's frontier is gathered with its totals when level 0 is
   // bottom-up (bu mode).  (Top-down levels read only their owned slice; the

@@ -78,6 +78,13 @@ class Comm {
   // collective where the transport can (peer windows: one launch, both
   // payloads in one slot; RCCL: one group); in order otherwise.
   virtual void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count);
+  // A level's end on several ranks: its totals all-reduced (buf, count) --
+  // with gbytes > 0 also its output frontier slice all-gathered (gsend ->
+  // grecv) -- then the device continuation `fin`, the level's decision on the
+  // reduced totals (Backend::level_finish).  The peer transport runs all of
+  // it as ONE launch; the default is allgather_allreduce + level_finish.
+  virtual void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                         const LevelFinishArgs& fin);
 
   // Host-value helpers built on the device collectives.
   virtual int64_t sum_host(int64_t x);
@@ -317,6 +324,8 @@ class PeerComm final : public Comm {
   void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
   bool counted_lists() const override { return true; }
   void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
+  void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                 const LevelFinishArgs& fin) override;
   size_t slot_bytes() const { return slot_; }
   // Every collective through the windows with known patterns (sizes up to a
   // full slot), checked on the host; the verdict is agreed over the inner
@@ -344,6 +353,7 @@ class PeerComm final : public Comm {
     bool counted = false;
     int64_t sum_count = 0;
     int64_t* sum_buf = nullptr;
+    const LevelFinishArgs* finish = nullptr;  // then the level's decision (sum_count <= kPeerFinishMax)
   };
   void run(const Plan& plan);
   std::shared_ptr<TcpBootstrap> boot_;

@@ -29,6 +29,7 @@
 #include <cstdio>
 
 #include "launch.hpp"
+#include "level_device.hpp"
 #include "wave.hpp"
 
 namespace dbfs {
@@ -63,23 +64,6 @@ __device__ unsigned long long g_check;
 // one a level's kernels write.)
 __device__ __forceinline__ void stamp_level_start(const LevelCtrl* c) {
   if (c && blockIdx.x == 0 && threadIdx.x == 0) const_cast<LevelCtrl*>(c)->t_start = wall_clock64();
-}
-
-// Level-end stamp of the host-mapped mailbox slot: values first (system
-// scope), then the level with release semantics, so a host that observes the
-// level reads that level's values.
-__device__ __forceinline__ void stamp_mailbox(LevelMailbox* mb, const LevelCtrl& c, int32_t level) {
-  __hip_atomic_store(&mb->done, c.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->vis_deg), static_cast<unsigned long long>(c.vis_deg),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&mb->next_dir, c.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->n_f), static_cast<unsigned long long>(c.n_f),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->m_f), static_cast<unsigned long long>(c.m_f),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(&mb->reached), static_cast<unsigned long long>(c.reached),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&mb->level, level, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A new vertex's level: the narrow array when the run uses one (uniform
@@ -216,16 +200,7 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
 }
 
 __global__ void level_finish_kernel(LevelFinishArgs a) {
-  if (threadIdx.x != 0) return;
-  if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
-  LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
-  level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
-  if (!a.seed) {
-    a.rec->t0 = c.t_start;
-    a.rec->t1 = wall_clock64();
-  }
-  *a.ctrl = c;
-  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.seed ? -1 : a.level);
+  if (threadIdx.x == 0) level_finish_device(a);
 }
 
 // Level totals -> host-mapped mailbox: values first (system scope), then the

@@ -79,7 +79,12 @@ struct PeerUnpackArgs {
   int64_t sum_count = 0;            // > 0: all-reduce -- sum_out[i] = sum_p sum_src[p][i] (uint64, wrapping)
   const void* sum_src[kMaxPeers] = {};
   void* sum_out = nullptr;
+  // then a level's decision on the sums (sum_count <= kPeerFinishMax: the
+  // first workgroup sums everything, its thread 0 finishes the level)
+  bool has_finish = false;
+  LevelFinishArgs finish;
 };
+constexpr int64_t kPeerFinishMax = 256;
 void peer_push(const PeerPushArgs& a, hipStream_t st);
 void peer_wait(const PeerWaitArgs& a, hipStream_t st);
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st);

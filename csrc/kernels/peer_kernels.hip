@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "launch.hpp"
+#include "level_device.hpp"
 #include "wave.hpp"
 
 namespace dbfs {
@@ -89,7 +90,20 @@ __device__ __forceinline__ void push_pieces(const PeerPushArgs& a, int nthreads)
 // The unpack of the landed slots (after the flags and an acquire): segment 0
 // copied to the caller's buffers, segment 1 summed.
 __device__ __forceinline__ void unpack_pieces(const PeerUnpackArgs& a, int64_t gt, int64_t nt) {
-  if (a.sum_count > 0) {
+  if (a.has_finish) {
+    // a level's end: the first workgroup sums the (few) totals and its
+    // thread 0 makes the level's decision on them (the stamp the host and
+    // the next level's kernels read)
+    if (blockIdx.x == 0) {
+      for (int64_t i = threadIdx.x; i < a.sum_count; i += blockDim.x) {
+        uint64_t acc = 0;
+        for (int p = 0; p < a.npeers; ++p) acc += static_cast<const uint64_t*>(a.sum_src[p])[i];
+        static_cast<uint64_t*>(a.sum_out)[i] = acc;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) level_finish_device(a.finish);
+    }
+  } else if (a.sum_count > 0) {
     // all-reduce: out[i] = sum over ranks of slot[p][i] (wrapping, as RCCL)
     for (int64_t i = gt; i < a.sum_count; i += nt) {
       uint64_t acc = 0;
