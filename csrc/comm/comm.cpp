@@ -202,6 +202,23 @@ void VirtualComm::alltoallv(const void* send, const int64_t* sc, const int64_t* 
   g_->barrier();
 }
 
+void VirtualComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride, size_t cap) {
+  note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
+  be_->synchronize();
+  auto& sl = g_->slots();
+  sl[rank_].send = send;
+  g_->barrier();
+  for (int r = 0; r < size(); ++r) {
+    const uint32_t* src = static_cast<const uint32_t*>(sl[r].send) + static_cast<size_t>(rank_) * stride;
+    uint32_t n = 0;
+    be_->to_host(&n, src, sizeof(n));
+    DBFS_CHECK(n <= cap, "VirtualComm alltoall_lists: a list exceeds its capacity");
+    be_->copy_async(recv + static_cast<size_t>(r) * stride, src, (static_cast<size_t>(n) + 1) * sizeof(uint32_t));
+  }
+  be_->synchronize();
+  g_->barrier();
+}
+
 void VirtualComm::barrier() {
   note(kBarrier, 0);
   be_->synchronize();

@@ -29,6 +29,7 @@ const char* kind_name(int k) {
     case Comm::kAllReduce: return "allreduce";
     case Comm::kAllToAllV: return "alltoallv";
     case Comm::kBarrier: return "barrier";
+    case CommTape::kLists: return "alltoall_lists";
   }
   return "?";
 }
@@ -46,6 +47,7 @@ RecordComm::RecordComm(std::shared_ptr<Comm> inner) : inner_(std::move(inner)), 
   DBFS_CHECK(inner_ != nullptr, "RecordComm needs an inner communicator");
   tape_->rank = inner_->rank();
   tape_->size = inner_->size();
+  tape_->counted_lists = inner_->counted_lists();
 }
 
 void RecordComm::push(int kind, int64_t a, int64_t b, const void* dev, size_t bytes) {
@@ -110,6 +112,14 @@ void RecordComm::alltoallv(const void* send, const int64_t* sc, const int64_t* s
     }
   }
   tape_->recs.push_back(std::move(r));
+}
+
+void RecordComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride, size_t cap) {
+  note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
+  inner_->alltoall_lists(send, recv, stride, cap);
+  // the whole receive block (every list, count first), replayed as one copy
+  push(CommTape::kLists, static_cast<int64_t>(stride), static_cast<int64_t>(cap), recv,
+       stride * static_cast<size_t>(size()) * sizeof(uint32_t));
 }
 
 void RecordComm::barrier() {
@@ -189,6 +199,13 @@ void ReplayComm::alltoallv(const void*, const int64_t* sc, const int64_t*, void*
     if (n) be_->copy_async(static_cast<char*>(recv) + rd[p] * eb, dev_.data() + off, n);
     off += static_cast<int64_t>(n);
   }
+}
+
+void ReplayComm::alltoall_lists(const uint32_t*, uint32_t* recv, size_t stride, size_t cap) {
+  note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
+  size_t i = 0;
+  const auto& r = next(CommTape::kLists, static_cast<int64_t>(stride), static_cast<int64_t>(cap), &i);
+  be_->copy_async(recv, dev_.data() + off_[i], r.data.size());
 }
 
 void ReplayComm::barrier() {

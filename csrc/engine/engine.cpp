@@ -1123,7 +1123,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // edges fit its owner lists (every rank sends any peer at most that many
   // ids); predicted levels up to xsparse_lim go sparse.
   const int P = part_.nranks;
-  const int64_t list_max = xc && sparse && opt_.list_form_edges > 0 ? opt_.list_form_edges : 0;
+  // (a rank appends each remote vertex at most once per run -- it claims the
+  // vertex's bit in its replicated visited bitmap first -- so no list ever
+  // holds more than a rank's part: lists of that capacity never overflow)
+  const int64_t list_max =
+      xc && sparse && opt_.list_form_edges > 0 ? std::min<int64_t>(opt_.list_form_edges, part_.part) : 0;
+  const bool lists_unlimited = list_max > 0 && list_max >= part_.part;
   const int64_t xsparse_lim = std::min<int64_t>(opt_.xsparse_edges, list_max);
   const bool counted = comm_.counted_lists();
   if (list_max > 0 && list_stride_ < list_max + 1) {
@@ -1448,14 +1453,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         // remote claims to their owners' lists, the lists (count-sized) to
         // their owners, the received ids settled there; the totals go to
         // the collective below (no decision in the kernels)
-        DBFS_CHECK(list_max > 0 && chain_cap > 0 && chain_cap <= list_max, "sparse chain without owner lists");
+        DBFS_CHECK(list_max > 0 && chain_cap <= list_max, "sparse chain without owner lists");
         sp.lists = dl_send_lists_.data();
         sp.list_stride = list_stride_;
         sp.part = part_.part;
         sp.mailbox = nullptr;
         be_.td_sparse(sp);
         comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_),
-                             static_cast<size_t>(chain_cap));
+                             static_cast<size_t>(chain_cap > 0 ? chain_cap : list_max));
         sp.recv_lists = dl_recv_lists_.data();
         sp.nranks = P;
         sp.grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
@@ -1690,9 +1695,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (xc) {
       if (list_max <= 0) return 'T';
       if (counted) {
-        // count-sized exchange: the largest lists cost nothing extra
-        if (mf > static_cast<double>(exact ? list_max : xsparse_lim)) return 'T';
-        *cap = list_max;
+        // count-sized exchange: the largest lists cost nothing extra (cap 0:
+        // lists of a whole part, live for any level)
+        if (!exact && mf > static_cast<double>(xsparse_lim)) return 'T';
+        if (exact && !lists_unlimited && mf > static_cast<double>(list_max)) return 'T';
+        *cap = lists_unlimited ? 0 : list_max;
         return 'S';
       }
       // fixed-size exchange (cap + 1 ids per peer): lists sized for the

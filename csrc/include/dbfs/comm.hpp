@@ -194,6 +194,10 @@ class VirtualComm final : public Comm {
   void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv,
                  const int64_t* rc, const int64_t* rd, size_t eb) override;
   void barrier() override;
+  // count-sized, as the peer transport (so virtual ranks -- and the shadow
+  // rank's recording -- take the peer transport's schedule)
+  void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
+  bool counted_lists() const override { return true; }
 
  private:
   std::shared_ptr<VirtualGroup> g_;
@@ -245,8 +249,10 @@ struct CommTape {
     std::string data;
   };
   int rank = 0, size = 1;
+  bool counted_lists = false;  // the recorded communicator's Comm::counted_lists
   std::vector<Rec> recs;
   int64_t bytes() const;
+  static constexpr int kLists = 100;  // Rec::kind of an alltoall_lists (a = stride, b = cap)
 };
 
 // Forwards to `inner` and records every output on the host (blocking copies:
@@ -263,6 +269,8 @@ class RecordComm final : public Comm {
   void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                  const int64_t* rd, size_t eb) override;
   void barrier() override;
+  void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
+  bool counted_lists() const override { return inner_->counted_lists(); }
   double max_host(double x) override;  // wall-time maxima: not part of the tape
   std::shared_ptr<CommTape> tape() const { return tape_; }
 
@@ -286,6 +294,8 @@ class ReplayComm final : public Comm {
   void alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                  const int64_t* rd, size_t eb) override;
   void barrier() override;
+  void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
+  bool counted_lists() const override { return tape_->counted_lists; }
   double max_host(double x) override { return x; }  // this rank's own time
   size_t position() const { return pos_; }
   size_t length() const { return tape_->recs.size(); }

@@ -329,7 +329,8 @@ PYBIND11_MODULE(_dbfs_native, m) {
         py::list out;
         static const char* names[] = {"alltoall", "allgather", "allreduce", "alltoallv", "barrier"};
         for (const auto& r : t.recs)
-          out.append(py::make_tuple(names[r.kind], r.a, r.b, static_cast<int64_t>(r.data.size())));
+          out.append(py::make_tuple(r.kind == CommTape::kLists ? "alltoall_lists" : names[r.kind], r.a, r.b,
+                                    static_cast<int64_t>(r.data.size())));
         return out;
       });
   py::class_<RecordComm, Comm, std::shared_ptr<RecordComm>>(m, "RecordComm")

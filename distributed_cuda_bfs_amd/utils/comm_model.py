@@ -42,7 +42,13 @@ class ModelConfig:
     slice_words: int              # Partition.slice_words(): words of one rank's bitmap slice
     mode: str = "do"              # engine mode: do / td / bu
     fused: bool = False           # the transport runs allgather_allreduce as one launch (peer windows, RCCL group)
-    list_stride: int = 0          # owner-list stride in 32-bit words (EngineOptions.list_form_edges + 1, to 4)
+    list_form_edges: int = 1 << 21  # EngineOptions.list_form_edges
+
+    @property
+    def list_max(self) -> int:
+        """The owner lists' capacity: list_form_edges, at most a rank's part
+        (a sparse chain recorded with cap 0 exchanges lists of this size)."""
+        return min(self.list_form_edges, self.slice_words * 64)
 
 
 @dataclass
@@ -87,7 +93,7 @@ def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gather
     if form == "B" and not in_gathered:
         t.add("allgather", (P - 1) * W * WORD)              # input frontier slices (+ visited merge)
     if form == "S":
-        t.add("alltoallv", (P - 1) * (cap + 1) * 4)         # owner lists, count first
+        t.add("alltoallv", (P - 1) * ((cap or cfg.list_max) + 1) * 4)  # owner lists, count first
     elif form == "T":
         t.add("alltoall", (P - 1) * W * WORD)               # candidate bitmap slices
     t.merge(level_end(cfg, gather))

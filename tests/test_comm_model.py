@@ -13,7 +13,7 @@ from distributed_cuda_bfs_amd.utils.comm_model import ModelConfig, run_traffic, 
 
 @pytest.mark.parametrize("P", [2, 3, 4])
 @pytest.mark.parametrize("mode", ["do", "td", "bu"])
-@pytest.mark.parametrize("knobs", [{}, {"list_form_edges": 0}, {"list_cap_factor": 0.01}])
+@pytest.mark.parametrize("knobs", [{}, {"list_form_edges": 0}, {"list_form_edges": 64}])
 def test_traffic_matches_model(P, mode, knobs):
     p = dbfs.rmat_params(12, 16, 17)
 
@@ -30,7 +30,7 @@ def test_traffic_matches_model(P, mode, knobs):
         return out, b.partition.slice_words()
 
     for outs, W in run_virtual_ranks(P, body, device="cpu"):
-        cfg = ModelConfig(nranks=P, slice_words=W, mode=mode)
+        cfg = ModelConfig(nranks=P, slice_words=W, mode=mode, list_form_edges=knobs.get("list_form_edges", 1 << 21))
         for chains, got in outs:
             want = run_traffic(cfg, chains)
             for kind, (calls, nbytes) in got.items():
@@ -39,7 +39,8 @@ def test_traffic_matches_model(P, mode, knobs):
             # one collective per chain (its level's end), plus a top-down
             # chain's payload exchange; a bottom-up chain's input frontier came
             # with the previous collective unless that one mispredicted
-            fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True), chains)
+            fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True,
+                                            list_form_edges=cfg.list_form_edges), chains)
             n_td = sum(1 for c in chains if c[1] in "ST")
             n_lone_b = sum(1 for i, c in enumerate(chains)
                            if c[1] == "B" and not (chains[i - 1][3] if i else mode == "bu"))

@@ -435,8 +435,7 @@ def test_device_loop_several_ranks(P, mode, predict):
 @pytest.mark.parametrize("knobs", [
     {},                                             # defaults: sparse list levels, gathered bottom-up inputs
     {"list_form_edges": 0},                         # dense top-down chains only
-    {"list_cap_factor": 0.01},                      # lists too small: sparse chains re-enqueued dense
-    {"list_form_edges": 64},                        # list capacity below the minimum: dense only
+    {"list_form_edges": 64},                        # lists too small: sparse chains re-enqueued dense
     {"xsparse_edges": 0},                           # only level 0 predicted sparse
     {"device_loop_predict": 0},                     # no prediction: two wasted chains per switch
     {"bu_fused_scan": 0, "td_fused_finish": 0},     # separate scans
@@ -476,9 +475,9 @@ def test_device_loop_sparse_lists_several_ranks(P, knobs):
             assert ra == rb and ta == tb
             mis += m
             forms += "".join(fs)
-        if knobs.get("list_cap_factor", 1) < 1:
+        if knobs.get("list_form_edges", 1) == 64:
             assert mis > 0  # undersized sparse chains were replaced
-        if knobs.get("list_form_edges", 1) in (0, 64):
+        if knobs.get("list_form_edges", 1) == 0:
             assert "S" not in forms
         elif knobs.get("device_loop_predict", 1):
             assert "S" in forms
