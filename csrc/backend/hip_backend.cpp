@@ -106,6 +106,15 @@ class HipBackend final : public Backend {
     on();
     HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDefault, st_));
   }
+  void copy_pieces(const CopyPieces& c) override {
+    for (int i = 0; i < c.n; ++i)
+      DBFS_CHECK(c.bytes[i] % 4 == 0 && reinterpret_cast<uintptr_t>(c.dst[i]) % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(c.src[i]) % 4 == 0,
+                 "copy_pieces: 4-byte pieces only");
+    on();
+    kern::copy_pieces(c, st_);
+    chk();
+  }
   void to_host(void* d, const void* s, size_t bytes) override {
     on();
     if (bytes && bytes <= kPinned) {

@@ -108,6 +108,7 @@ void RecordComm::alltoallv(const void* send, const int64_t* sc, const int64_t* s
     for (int p = 0; p < size(); ++p) {
       const size_t n = static_cast<size_t>(rc[p]) * eb;
       if (n) be_->to_host(&r.data[off], static_cast<const char*>(recv) + rd[p] * eb, n);
+      r.pieces.push_back(static_cast<int64_t>(n));
       off += n;
     }
   }
@@ -117,9 +118,23 @@ void RecordComm::alltoallv(const void* send, const int64_t* sc, const int64_t* s
 void RecordComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride, size_t cap) {
   note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
   inner_->alltoall_lists(send, recv, stride, cap);
-  // the whole receive block (every list, count first), replayed as one copy
-  push(CommTape::kLists, static_cast<int64_t>(stride), static_cast<int64_t>(cap), recv,
-       stride * static_cast<size_t>(size()) * sizeof(uint32_t));
+  // every received list's count word and entries (count-sized), replayed as
+  // one multi-piece copy
+  CommTape::Rec r;
+  r.kind = CommTape::kLists;
+  r.a = static_cast<int64_t>(stride);
+  r.b = static_cast<int64_t>(cap);
+  for (int p = 0; p < size(); ++p) {
+    const uint32_t* list = recv + static_cast<size_t>(p) * stride;
+    uint32_t n = 0;
+    be_->to_host(&n, list, sizeof(n));
+    const size_t bytes = (static_cast<size_t>(n) + 1) * sizeof(uint32_t);
+    const size_t off = r.data.size();
+    r.data.resize(off + bytes);
+    be_->to_host(&r.data[off], list, bytes);
+    r.pieces.push_back(static_cast<int64_t>(bytes));
+  }
+  tape_->recs.push_back(std::move(r));
 }
 
 void RecordComm::barrier() {
@@ -194,18 +209,58 @@ void ReplayComm::alltoallv(const void*, const int64_t* sc, const int64_t*, void*
     return;
   }
   int64_t off = off_[i];
+  const bool words = eb % 4 == 0 && size() <= Backend::CopyPieces::kMax;
+  Backend::CopyPieces cp;
   for (int p = 0; p < size(); ++p) {
     const size_t n = static_cast<size_t>(rc[p]) * eb;
-    if (n) be_->copy_async(static_cast<char*>(recv) + rd[p] * eb, dev_.data() + off, n);
+    if (n && words) {
+      cp.dst[cp.n] = static_cast<char*>(recv) + rd[p] * eb;
+      cp.src[cp.n] = dev_.data() + off;
+      cp.bytes[cp.n++] = static_cast<int64_t>(n);
+    } else if (n) {
+      be_->copy_async(static_cast<char*>(recv) + rd[p] * eb, dev_.data() + off, n);
+    }
     off += static_cast<int64_t>(n);
   }
+  if (cp.n) be_->copy_pieces(cp);
 }
 
 void ReplayComm::alltoall_lists(const uint32_t*, uint32_t* recv, size_t stride, size_t cap) {
   note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
   size_t i = 0;
   const auto& r = next(CommTape::kLists, static_cast<int64_t>(stride), static_cast<int64_t>(cap), &i);
-  be_->copy_async(recv, dev_.data() + off_[i], r.data.size());
+  DBFS_CHECK(static_cast<int>(r.pieces.size()) == size() && size() <= Backend::CopyPieces::kMax,
+             "ReplayComm: malformed list record");
+  // one launch: every list at its stride, count-sized
+  Backend::CopyPieces cp;
+  int64_t off = off_[i];
+  for (int p = 0; p < size(); ++p) {
+    cp.dst[cp.n] = recv + static_cast<size_t>(p) * stride;
+    cp.src[cp.n] = dev_.data() + off;
+    cp.bytes[cp.n++] = r.pieces[p];
+    off += r.pieces[p];
+  }
+  be_->copy_pieces(cp);
+}
+
+void ReplayComm::level_end(const void*, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                           const LevelFinishArgs& fin) {
+  Backend::CopyPieces cp;
+  size_t i = 0;
+  if (gbytes > 0) {
+    note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(gbytes));
+    const auto& r = next(kAllGather, static_cast<int64_t>(gbytes), 0, &i);
+    cp.dst[cp.n] = grecv;
+    cp.src[cp.n] = dev_.data() + off_[i];
+    cp.bytes[cp.n++] = static_cast<int64_t>(r.data.size());
+  }
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  const auto& r = next(kAllReduce, static_cast<int64_t>(count), 0, &i);
+  cp.dst[cp.n] = buf;
+  cp.src[cp.n] = dev_.data() + off_[i];
+  cp.bytes[cp.n++] = static_cast<int64_t>(r.data.size());
+  be_->copy_pieces(cp);
+  be_->level_finish(fin);
 }
 
 void ReplayComm::barrier() {

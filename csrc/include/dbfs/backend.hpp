@@ -772,6 +772,18 @@ class Backend {
   virtual void dealloc(void* p) = 0;
   virtual void memset_async(void* p, int value, size_t bytes) = 0;
   virtual void copy_async(void* dst, const void* src, size_t bytes) = 0;
+  // Several device-to-device copies as one launch (4-byte multiples; the
+  // shadow rank's replayed collectives: ReplayComm).
+  struct CopyPieces {
+    static constexpr int kMax = 16;
+    void* dst[kMax] = {};
+    const void* src[kMax] = {};
+    int64_t bytes[kMax] = {};
+    int n = 0;
+  };
+  virtual void copy_pieces(const CopyPieces& c) {
+    for (int i = 0; i < c.n; ++i) copy_async(c.dst[i], c.src[i], static_cast<size_t>(c.bytes[i]));
+  }
   virtual void to_host(void* host_dst, const void* dev_src, size_t bytes) = 0;   // blocking
   virtual void to_device(void* dev_dst, const void* host_src, size_t bytes) = 0; // blocking
   virtual void synchronize() = 0;

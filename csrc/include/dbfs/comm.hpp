@@ -246,6 +246,9 @@ struct CommTape {
     // size) holding every piece (replayed as one copy); -1 -- the pieces
     // concatenated in rank order
     int64_t span = -1;
+    // alltoall_lists (and alltoallv without a span): the received pieces'
+    // byte sizes, concatenated in data in rank order
+    std::vector<int64_t> pieces;
     std::string data;
   };
   int rank = 0, size = 1;
@@ -296,6 +299,10 @@ class ReplayComm final : public Comm {
   void barrier() override;
   void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
   bool counted_lists() const override { return tape_->counted_lists; }
+  // the recorded frontier slices and totals as one multi-piece copy, then the
+  // level's decision (two launches; the peer transport's level end is one)
+  void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
+                 const LevelFinishArgs& fin) override;
   double max_host(double x) override { return x; }  // this rank's own time
   size_t position() const { return pos_; }
   size_t length() const { return tape_->recs.size(); }

@@ -1985,6 +1985,17 @@ __global__ __launch_bounds__(kBlock) void bitmap_or_kernel(word_t* __restrict__ 
     dst[i] |= src[i];
 }
 
+// blockIdx.y = piece; 4-byte words, grid-stride over the piece.
+__global__ __launch_bounds__(kBlock) void copy_pieces_kernel(Backend::CopyPieces c) {
+  const int i = blockIdx.y;
+  const int64_t n = c.bytes[i] / 4;
+  const uint32_t* s = static_cast<const uint32_t*>(c.src[i]);
+  uint32_t* d = static_cast<uint32_t*>(c.dst[i]);
+  for (int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; k < n;
+       k += static_cast<int64_t>(gridDim.x) * kBlock)
+    d[k] = s[k];
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap = 1 << 30) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -2288,6 +2299,13 @@ void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st) {
 void status_expand(const StatusArgs& a, hipStream_t st) {
   if (a.g.rows <= 0) return;
   status_kernel<<<grid_for(a.g.rows, kBlock), kBlock, 0, st>>>(a);
+}
+
+void copy_pieces(const Backend::CopyPieces& c, hipStream_t st) {
+  int64_t mx = 0;
+  for (int i = 0; i < c.n; ++i) mx = std::max(mx, c.bytes[i] / 4);
+  if (c.n <= 0 || mx <= 0) return;
+  copy_pieces_kernel<<<dim3(grid_for(mx, kBlock, 1024), static_cast<unsigned>(c.n)), kBlock, 0, st>>>(c);
 }
 
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st) {

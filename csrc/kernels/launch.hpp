@@ -38,6 +38,7 @@ unsigned long long take_check_error();
 void inject_check_failure(hipStream_t st);
 void status_expand(const StatusArgs& a, hipStream_t st);
 void bitmap_or(word_t* dst, const word_t* src, int64_t words, hipStream_t st);
+void copy_pieces(const Backend::CopyPieces& c, hipStream_t st);
 
 // peer_kernels.hip (PeerComm: collectives through peer-mapped windows)
 constexpr int kMaxPeers = 16;
