@@ -1142,41 +1142,59 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
 // slice of `visited`; a vertex sent by several ranks, or claimed by this
 // rank's own td_sparse, is settled once) and settled like td_sparse's owned
 // claims; the last workgroup writes the level's local totals and zeroes the
-// send lists' counts.  Grid-stride over each received list in turn.
+// send lists' counts.  The lists' counts are loaded together (one per
+// thread: they sit a stride apart, cold) and their entries form one index
+// space the grid strides over.
 template <int kThreads>
 __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdItems;
   __shared__ int s_last;
+  __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
   const int t = threadIdx.x;
-  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
-  for (int r = 0; r < a.nranks; ++r) {
-    const vid_t* list = a.recv_lists + static_cast<int64_t>(r) * a.list_stride;
-    const int64_t n = list[0];
+  if (t < kWave) {
+    const long long n = t < a.nranks ? static_cast<long long>(a.recv_lists[static_cast<int64_t>(t) * a.list_stride]) : 0;
     DBFS_DCHECK(n < a.list_stride, 5, n);
-    for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * span; i0 < n; i0 += static_cast<int64_t>(gridDim.x) * span) {
-      vid_t v[kItems];
-      word_t seen[kItems];
+    const long long incl = wave_incl_scan(n);
+    if (t < a.nranks) s_end[t] = incl;
+  }
+  __syncthreads();
+  const long long total = s_end[a.nranks - 1];
+  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
+  // only the workgroups with entries take part (at least one, for the finish)
+  const int64_t need = (total + span - 1) / span;
+  const unsigned active = static_cast<unsigned>(need < 1 ? 1 : (need < gridDim.x ? need : gridDim.x));
+  if (blockIdx.x >= active) return;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * span; i0 < total; i0 += static_cast<int64_t>(active) * span) {
+    vid_t v[kItems];
+    word_t seen[kItems];
 #pragma unroll
-      for (int k = 0; k < kItems; ++k) {
-        const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
-        v[k] = j < n ? list[1 + j] : 0u;
-        seen[k] = j < n ? a.visited[v[k] >> 6] : ~0ull;
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
+      v[k] = 0u;
+      if (j < total) {
+        int r = 0;
+        while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
+        const long long before = r > 0 ? s_end[r - 1] : 0;
+        v[k] = a.recv_lists[static_cast<int64_t>(r) * a.list_stride + 1 + (j - before)];
       }
-      unsigned claimed = 0;
-#pragma unroll
-      for (int k = 0; k < kItems; ++k) {
-        const word_t bit = 1ull << (v[k] & 63);
-        if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
-      }
-      sparse_settle<kItems>(a, v, claimed);
     }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      seen[k] = i0 + static_cast<int64_t>(k) * kThreads + t < total ? a.visited[v[k] >> 6] : ~0ull;
+    unsigned claimed = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const word_t bit = 1ull << (v[k] & 63);
+      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+    }
+    sparse_settle<kItems>(a, v, claimed);
   }
   __syncthreads();
   if (t == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(a.ticket, 1u);
-    s_last = (prev == gridDim.x - 1) ? 1 : 0;
+    s_last = (prev == active - 1) ? 1 : 0;
     if (s_last) last_arriver_acquire();
   }
   __syncthreads();
