@@ -7,15 +7,21 @@
 //
 // Execution models:
 //   default            1 GPU (HIP backend, device --device)
-//   --gpus P           P GPUs in one process, one host thread + one RCCL
-//                      communicator per GPU (ncclCommInitAll) -- replaces
-//                      the reference's intra-node bfs.cu
+//   --gpus P           P GPUs in one process, one host thread per GPU: the
+//                      peer-memory communicator (every rank's window shared
+//                      as a device pointer, peer access enabled) over one
+//                      RCCL communicator per GPU (ncclCommInitAll) --
+//                      replaces the reference's intra-node bfs.cu
 //   --virtual-ranks P  P partitions on ONE device (threads + VirtualComm):
 //                      exercises the distributed code path on one GPU
 //   --cpu              CPU backend (no GPU needed)
 //   WORLD_SIZE > 1     one process per GPU (torchrun / any launcher): TCP
-//                      bootstrap on MASTER_ADDR:MASTER_PORT+1, RCCL -- replaces
-//                      the reference's MPI build bfs_mpi.cu
+//                      bootstrap on MASTER_ADDR:MASTER_PORT+1, the peer-memory
+//                      communicator over RCCL (IPC windows) -- replaces the
+//                      reference's MPI build bfs_mpi.cu
+// DBFS_COMM = peer | rccl | tcp selects the transport (default: peer with an
+// agreed fallback to RCCL), DBFS_DEVICE pins every process to one device
+// (several ranks sharing a GPU: TCP carries what the windows do not).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -155,10 +161,27 @@ int env_int(const char* k, int dflt) {
 // One rank's state.
 struct RankCtx {
   std::unique_ptr<Backend> be;
-  std::unique_ptr<Comm> comm;
+  std::shared_ptr<Comm> comm;
   std::unique_ptr<DeviceGraph> graph;
   std::unique_ptr<Engine> engine;
 };
+
+// The peer-memory communicator over `inner` when every rank maps every window
+// and its self-test passes (both agreed over the bootstrap / inner), else
+// `inner` -- or an error when the peer transport was asked for.
+std::shared_ptr<Comm> try_peer(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr<Comm> inner,
+                               bool required, bool report) {
+  std::string why;
+  try {
+    auto pc = std::make_shared<PeerComm>(boot, be, inner, static_cast<size_t>(env_int("DBFS_PEER_SLOT_MB", 16)) << 20);
+    if (pc->self_test(&why)) return pc;
+  } catch (const std::exception& e) {
+    why = e.what();
+  }
+  if (required) throw Error("DBFS_COMM=peer: peer communicator unavailable: " + why);
+  if (report) std::fprintf(stderr, "[bfs] peer communicator unavailable (%s); using %s\n", why.c_str(), inner->name().c_str());
+  return inner;
+}
 
 // One thread per local rank.  A rank that throws aborts the virtual group so
 // its peers fail at their next collective instead of waiting forever.
@@ -188,10 +211,10 @@ void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCt
 }
 
 std::string json_run(const RunResult& r, const std::string& graph, int64_t n, int64_t m, int P, const char* mode,
-                     const std::string& backend) {
+                     const std::string& backend, const std::string& comm) {
   std::string s = "{\"graph\":\"" + graph + "\",\"n\":" + std::to_string(n) + ",\"m\":" + std::to_string(m) +
                   ",\"ranks\":" + std::to_string(P) + ",\"mode\":\"" + mode + "\",\"backend\":\"" + backend +
-                  "\",\"source\":" + std::to_string(r.source) + ",\"ms\":" + std::to_string(r.ms) +
+                  "\",\"comm\":\"" + comm + "\",\"source\":" + std::to_string(r.source) + ",\"ms\":" + std::to_string(r.ms) +
                   ",\"reached\":" + std::to_string(r.reached) + ",\"edges\":" + std::to_string(r.edges) +
                   ",\"gteps\":" + std::to_string(r.gteps) + ",\"depth\":" + std::to_string(r.depth) + ",\"levels\":[";
   for (size_t i = 0; i < r.levels.size(); ++i) {
@@ -290,9 +313,13 @@ int main(int argc, char** argv) {
     if (!a.cpu && ref_lines) std::printf("Enabling peer access between GPU0 and GPU1...\n");
     std::shared_ptr<VirtualGroup> vgroup;
     if (a.virtual_ranks > 0 && !multiproc) vgroup = std::make_shared<VirtualGroup>(P);
+    const char* dev_pin = std::getenv("DBFS_DEVICE");  // several processes on one GPU (tests)
+    const char* cm_env = std::getenv("DBFS_COMM");
+    const std::string cm = cm_env ? cm_env : "";
+    const bool want_peer = !a.cpu && (cm.empty() || cm == "peer");
     for (int i = 0; i < nlocal; ++i) {
       if (a.cpu) ranks[i].be = make_cpu_backend();
-      else if (multiproc) ranks[i].be = make_hip_backend(env_int("LOCAL_RANK", 0));
+      else if (multiproc) ranks[i].be = make_hip_backend(dev_pin ? std::atoi(dev_pin) : env_int("LOCAL_RANK", 0));
       else if (a.virtual_ranks > 0) ranks[i].be = make_hip_backend(a.device);
       else ranks[i].be = make_hip_backend(P > 1 ? i : a.device);
     }
@@ -300,23 +327,36 @@ int main(int argc, char** argv) {
       const char* addr = std::getenv("MASTER_ADDR");
       const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
       auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
-      const char* cm = std::getenv("DBFS_COMM");
-      if (a.cpu || (cm && std::string(cm) == "tcp")) {
-        // host transport (CPU ranks, or GPU ranks without RCCL)
-        ranks[0].comm = std::make_unique<TcpComm>(boot, *ranks[0].be);
+      if (a.cpu || cm == "tcp" || (cm.empty() && dev_pin)) {
+        // host transport (CPU ranks, GPU ranks without RCCL, shared GPU)
+        ranks[0].comm = std::make_shared<TcpComm>(boot, *ranks[0].be);
       } else {
-        std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
-        ranks[0].comm = std::make_unique<NcclComm>(uid, wrank, world, *ranks[0].be);
+        std::shared_ptr<Comm> inner;
+        if (dev_pin) {
+          // RCCL refuses two ranks on one device: TCP carries what does not
+          // fit the peer windows
+          inner = std::make_shared<TcpComm>(boot, *ranks[0].be);
+        } else {
+          std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+          inner = std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
+        }
+        ranks[0].comm = want_peer ? try_peer(boot, *ranks[0].be, inner, cm == "peer", leader) : inner;
       }
     } else if (vgroup) {
-      for (int i = 0; i < P; ++i) ranks[i].comm = std::make_unique<VirtualComm>(vgroup, i, *ranks[i].be);
+      for (int i = 0; i < P; ++i) ranks[i].comm = std::make_shared<VirtualComm>(vgroup, i, *ranks[i].be);
     } else if (P > 1) {
       std::vector<Backend*> bes;
       for (auto& r : ranks) bes.push_back(r.be.get());
       auto comms = NcclComm::init_all(bes);
       for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
+      if (want_peer) {
+        auto pgroup = std::make_shared<VirtualGroup>(P);
+        run_ranks(ranks, [&](int i, RankCtx& rc) {
+          rc.comm = try_peer(std::make_shared<GroupBootstrap>(pgroup, i), *rc.be, rc.comm, cm == "peer", i == 0);
+        }, pgroup.get());
+      }
     } else {
-      ranks[0].comm = std::make_unique<LocalComm>(*ranks[0].be);
+      ranks[0].comm = std::make_shared<LocalComm>(*ranks[0].be);
     }
 
     EngineOptions eo;
@@ -384,7 +424,7 @@ int main(int argc, char** argv) {
     };
     csv_run(res[0]);
     const std::string bname = ranks[0].be->name() + (ranks[0].be->device_checks_enabled() ? "+checked" : "");
-    if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
+    if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname, ranks[0].comm->name()).c_str());
 
     // ---- optional K random roots (Graph500-style GTEPS) ----
     if (a.roots > 0) {
@@ -414,7 +454,7 @@ int main(int argc, char** argv) {
         inv_sum += res[0].gteps > 0 ? 1.0 / res[0].gteps : 0;
         ms_sum += res[0].ms;
         e_sum += res[0].edges;
-        if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname).c_str());
+        if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname, ranks[0].comm->name()).c_str());
         csv_run(res[0]);
       }
       if (leader && !roots.empty()) {

@@ -136,6 +136,24 @@ bool VirtualGroup::aborted() const {
   return aborted_;
 }
 
+GroupBootstrap::GroupBootstrap(std::shared_ptr<VirtualGroup> g, int rank) : g_(std::move(g)), rank_(rank) {
+  DBFS_CHECK(g_ && rank >= 0 && rank < g_->size(), "group bootstrap: rank out of range");
+}
+
+std::vector<std::string> GroupBootstrap::allgather(const std::string& data) {
+  // (the group's slots are shared with its VirtualComms: every rank makes the
+  // same sequence of group calls, each ending in a barrier after the reads)
+  auto& sl = g_->slots();
+  sl[rank_].send = &data;
+  g_->barrier();
+  std::vector<std::string> out(static_cast<size_t>(size()));
+  for (int r = 0; r < size(); ++r) out[r] = *static_cast<const std::string*>(sl[r].send);
+  g_->barrier();
+  return out;
+}
+
+std::string GroupBootstrap::broadcast(const std::string& data, int root) { return allgather(data)[root]; }
+
 VirtualComm::VirtualComm(std::shared_ptr<VirtualGroup> g, int rank, Backend& be) : g_(std::move(g)), rank_(rank) {
   DBFS_CHECK(rank >= 0 && rank < g_->size(), "virtual rank out of range");
   bind_backend(&be);

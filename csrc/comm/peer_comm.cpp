@@ -36,12 +36,13 @@ constexpr size_t kFlagBytes = 4096;
 inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->comm_stream_handle()); }
 }  // namespace
 
-PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes)
+PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes)
     : boot_(std::move(boot)), inner_(std::move(inner)), slot_(slot_bytes) {
   DBFS_CHECK(be.kind() == DeviceKind::HIP, "PeerComm requires a HIP backend");
   DBFS_CHECK(boot_ && inner_, "PeerComm needs a bootstrap and an inner communicator");
   rank_ = boot_->rank();
   size_ = boot_->size();
+  ipc_ = !boot_->in_process();
   if (const char* e = std::getenv("DBFS_PEER_FUSED")) fused_ = std::string(e) != "0";
   DBFS_CHECK(size_ <= kern::kMaxPeers, "PeerComm supports at most 16 ranks");
   DBFS_CHECK(inner_->rank() == rank_ && inner_->size() == size_, "inner communicator does not match the bootstrap");
@@ -65,12 +66,26 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
     void* dptr = nullptr;
     err_host_ = static_cast<uint64_t*>(be.alloc_mapped(sizeof(uint64_t), &dptr));
     err_dev_ = static_cast<uint64_t*>(dptr);
-    HIP_CHECK(hipIpcGetMemHandle(&h, win_));
+    if (ipc_) HIP_CHECK(hipIpcGetMemHandle(&h, win_));
   } catch (const std::exception& e) {
     local_err = e.what();
   }
-  const auto all = boot_->allgather(local_err.empty() ? std::string(reinterpret_cast<const char*>(&h), sizeof(h))
-                                                      : std::string());
+  // what a peer needs to map this window: an IPC handle, or (one process)
+  // the pointer and its device
+  // (in-process: every rank keeps every window alive -- a window is freed
+  // with the group's last communicator, so no rank waits for the others on
+  // destruction)
+  struct Local {
+    char* win;
+    int device;
+    const std::shared_ptr<char>* keep;
+  };
+  if (!ipc_ && win_) win_keep_ = std::shared_ptr<char>(win_, [](char* w) { (void)hipFree(w); });
+  const Local loc{win_, be.device_id(), &win_keep_};
+  const std::string mine = !local_err.empty() ? std::string()
+                           : ipc_ ? std::string(reinterpret_cast<const char*>(&h), sizeof(h))
+                                  : std::string(reinterpret_cast<const char*>(&loc), sizeof(loc));
+  const auto all = boot_->allgather(mine);
   auto agree = [&](const std::string& what) {
     // every rank's status; throw on all ranks if any failed
     const auto st = boot_->allgather(local_err);
@@ -88,6 +103,29 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
         peer_[p] = win_;
         continue;
       }
+      if (!ipc_) {
+        DBFS_CHECK(all[p].size() == sizeof(Local), "PeerComm: bad window record from a peer");
+        Local pl;
+        std::memcpy(&pl, all[p].data(), sizeof(pl));
+        // threads of one process sharing a device cannot wait for each other in
+        // kernels: any device-wide synchronisation one of them makes (hipFree
+        // does) waits for the other's spinning collective
+        DBFS_CHECK(pl.device != be.device_id(), "PeerComm: in-process ranks " + std::to_string(rank_) + " and " +
+                                                    std::to_string(p) + " share device " + std::to_string(pl.device) +
+                                                    " (one device per rank, or one process per rank)");
+        {
+          int can = 0;
+          HIP_CHECK(hipDeviceCanAccessPeer(&can, be.device_id(), pl.device));
+          DBFS_CHECK(can, "PeerComm: device " + std::to_string(be.device_id()) + " cannot access device " +
+                              std::to_string(pl.device));
+          const hipError_t e = hipDeviceEnablePeerAccess(pl.device, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(e);
+          (void)hipGetLastError();  // (clear an already-enabled status)
+        }
+        peer_[p] = pl.win;
+        keep_.push_back(*pl.keep);
+        continue;
+      }
       DBFS_CHECK(all[p].size() == sizeof(hipIpcMemHandle_t), "PeerComm: bad IPC handle from a peer");
       hipIpcMemHandle_t ph;
       std::memcpy(&ph, all[p].data(), sizeof(ph));
@@ -99,6 +137,7 @@ PeerComm::PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_
     local_err = e.what();
   }
   agree("window mapping");
+  if (!ipc_) boot_->barrier();  // every rank holds every window before any may drop one
   // a wait kernel that timed out leaves its seq in the error word: the host's
   // waits (stream synchronise, mailbox spins) turn it into an error
   prev_watch_ = be.wait_watch();
@@ -125,10 +164,13 @@ PeerComm::~PeerComm() {
     be_->set_wait_watch(prev_watch_);
     // no rank unmaps or frees a window while a peer may still write into it
     // or read it (a peer that failed closes its socket: the barrier throws at
-    // once and is ignored -- nothing of that peer is in flight any more)
-    try {
-      boot_->barrier();
-    } catch (const std::exception&) {
+    // once and is ignored -- nothing of that peer is in flight any more).
+    // In-process the windows are shared-owned instead: the last rank frees.
+    if (ipc_) {
+      try {
+        boot_->barrier();
+      } catch (const std::exception&) {
+      }
     }
   }
   release();
@@ -136,11 +178,13 @@ PeerComm::~PeerComm() {
 
 void PeerComm::release() {
   for (int p = 0; p < static_cast<int>(peer_.size()); ++p)
-    if (p != rank_ && peer_[p]) hipIpcCloseMemHandle(peer_[p]);
+    if (ipc_ && p != rank_ && peer_[p]) hipIpcCloseMemHandle(peer_[p]);
   peer_.clear();
   if (ticket_) hipFree(ticket_);
   ticket_ = nullptr;
-  if (win_) hipFree(win_);
+  keep_.clear();
+  if (win_keep_) win_keep_.reset();  // (in-process: frees with the last holder)
+  else if (win_) hipFree(win_);
   win_ = nullptr;
   if (be_ && err_host_) be_->free_mapped(err_host_);
   err_host_ = nullptr;

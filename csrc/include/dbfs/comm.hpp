@@ -204,6 +204,38 @@ class VirtualComm final : public Comm {
   int rank_;
 };
 
+// Host-side rank group for setup exchanges (IPC handles, RCCL unique ids,
+// agreed verdicts): TCP between processes (TcpBootstrap) or threads of one
+// process (GroupBootstrap).
+class Bootstrap {
+ public:
+  virtual ~Bootstrap() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual std::string broadcast(const std::string& data, int root = 0) = 0;
+  virtual std::vector<std::string> allgather(const std::string& data) = 0;
+  virtual void barrier() = 0;
+  // every rank lives in this process: device pointers are shared directly
+  // (peer access) instead of through IPC handles
+  virtual bool in_process() const { return false; }
+};
+
+// The ranks of a VirtualGroup (one thread each) as a bootstrap.
+class GroupBootstrap final : public Bootstrap {
+ public:
+  GroupBootstrap(std::shared_ptr<VirtualGroup> g, int rank);
+  int rank() const override { return rank_; }
+  int size() const override { return g_->size(); }
+  std::string broadcast(const std::string& data, int root = 0) override;
+  std::vector<std::string> allgather(const std::string& data) override;
+  void barrier() override { g_->barrier(); }
+  bool in_process() const override { return true; }
+
+ private:
+  std::shared_ptr<VirtualGroup> g_;
+  int rank_;
+};
+
 // RCCL communicator (defined in csrc/comm/nccl_comm.cpp).
 class NcclComm final : public Comm {
  public:
@@ -327,7 +359,9 @@ class TcpBootstrap;
 // share a GPU).  Requires: one HIP backend per rank, every window mappable.
 class PeerComm final : public Comm {
  public:
-  PeerComm(std::shared_ptr<TcpBootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes);
+  // (an in-process bootstrap: the ranks' windows are shared as device
+  // pointers with peer access enabled between their devices)
+  PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr<Comm> inner, size_t slot_bytes);
   ~PeerComm() override;
   int rank() const override { return rank_; }
   int size() const override { return size_; }
@@ -373,7 +407,10 @@ class PeerComm final : public Comm {
     const LevelFinishArgs* finish = nullptr;  // then the level's decision (sum_count <= kPeerFinishMax)
   };
   void run(const Plan& plan);
-  std::shared_ptr<TcpBootstrap> boot_;
+  std::shared_ptr<Bootstrap> boot_;
+  bool ipc_ = true;                     // peers' windows IPC-mapped (closed on release)
+  std::shared_ptr<char> win_keep_;      // in-process: own window, shared-owned by the group
+  std::vector<std::shared_ptr<char>> keep_;  // in-process: the peers' windows
   std::shared_ptr<Comm> inner_;
   int rank_ = 0, size_ = 1;
   size_t slot_ = 0;
@@ -418,15 +455,15 @@ class TcpComm final : public Comm {
   std::shared_ptr<TcpBootstrap> boot_;
 };
 
-class TcpBootstrap {
+class TcpBootstrap final : public Bootstrap {
  public:
   TcpBootstrap(const std::string& host, int port, int rank, int nranks, double timeout_s = 300.0);
-  ~TcpBootstrap();
-  int rank() const { return rank_; }
-  int size() const { return size_; }
-  std::string broadcast(const std::string& data, int root = 0);
-  std::vector<std::string> allgather(const std::string& data);
-  void barrier();
+  ~TcpBootstrap() override;
+  int rank() const override { return rank_; }
+  int size() const override { return size_; }
+  std::string broadcast(const std::string& data, int root = 0) override;
+  std::vector<std::string> allgather(const std::string& data) override;
+  void barrier() override;
 
  private:
   int rank_, size_;

@@ -1462,7 +1462,13 @@ __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
 // (Rejected, measured on RMAT-26 in rounds 1-2 and removed: phase 2 as one
 // packed multi-row edge stream -- 83 VGPRs, one workgroup per CU, 1238 ->
 // 1069 GTEPS; 2-8 phase-2 steps in flight -- 1231 -> 1225-1188; non-temporal
-// column loads; records prefetched two batches ahead.)
+// column loads; records prefetched two batches ahead.  Round 3: the wave's
+// unresolved rows as one flattened stream, 128 entries per round found by a
+// binary search over the rows' prefixes, per-row cap 4 x 4^round: coalesced
+// loads and no serial phase 2, yet late-switch first levels 672 / 889 ->
+// 700 / 875 us and the bench flat -- that level is bound by the ~44 M L2
+// misses of its column lines and global frontier probes, not by the scan's
+// round trips.)
 constexpr int kBuBatch = 4;  // phase-1 column loads in flight per lane
 
 // Deferred row-scan queue entries per wave (hub waves; 0 = scan in the

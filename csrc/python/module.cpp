@@ -310,7 +310,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
       });
   m.def(
       "peer_comm",
-      [](std::shared_ptr<TcpBootstrap> boot, std::shared_ptr<Backend> be, std::shared_ptr<Comm> inner,
+      [](std::shared_ptr<Bootstrap> boot, std::shared_ptr<Backend> be, std::shared_ptr<Comm> inner,
          size_t slot_bytes) {
         py::gil_scoped_release rel;
         return std::make_shared<PeerComm>(boot, *be, inner, slot_bytes);
@@ -462,24 +462,23 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def("py_alltoallv", &PyCommBase::py_alltoallv)
       .def("py_barrier", &PyCommBase::py_barrier);
 
-  py::class_<TcpBootstrap, std::shared_ptr<TcpBootstrap>>(m, "TcpBootstrap")
-      .def(py::init<const std::string&, int, int, int, double>(), py::arg("host"), py::arg("port"), py::arg("rank"),
-           py::arg("nranks"), py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("rank", &TcpBootstrap::rank)
-      .def_property_readonly("size", &TcpBootstrap::size)
+  py::class_<Bootstrap, std::shared_ptr<Bootstrap>>(m, "Bootstrap")
+      .def_property_readonly("rank", &Bootstrap::rank)
+      .def_property_readonly("size", &Bootstrap::size)
+      .def_property_readonly("in_process", &Bootstrap::in_process)
       .def(
           "broadcast",
-          [](TcpBootstrap& b, py::bytes data) {
+          [](Bootstrap& b, py::bytes data, int root) {
             std::string s = data, r;
             {
               py::gil_scoped_release rel;
-              r = b.broadcast(s);
+              r = b.broadcast(s, root);
             }
             return py::bytes(r);
           },
-          py::arg("data"))
+          py::arg("data"), py::arg("root") = 0)
       .def("allgather",
-           [](TcpBootstrap& b, py::bytes data) {
+           [](Bootstrap& b, py::bytes data) {
              std::string s = data;
              std::vector<std::string> r;
              {
@@ -490,7 +489,16 @@ PYBIND11_MODULE(_dbfs_native, m) {
              for (auto& x : r) out.append(py::bytes(x));
              return out;
            })
-      .def("barrier", &TcpBootstrap::barrier, py::call_guard<py::gil_scoped_release>());
+      .def("barrier", &Bootstrap::barrier, py::call_guard<py::gil_scoped_release>());
+  // the ranks of a VirtualGroup (threads of this process) as a bootstrap: a
+  // peer communicator over it shares its windows as device pointers
+  m.def(
+      "group_bootstrap",
+      [](std::shared_ptr<VirtualGroup> g, int rank) { return std::shared_ptr<Bootstrap>(new GroupBootstrap(g, rank)); },
+      py::arg("group"), py::arg("rank"));
+  py::class_<TcpBootstrap, Bootstrap, std::shared_ptr<TcpBootstrap>>(m, "TcpBootstrap")
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("host"), py::arg("port"), py::arg("rank"),
+           py::arg("nranks"), py::arg("timeout_s") = 300.0, py::call_guard<py::gil_scoped_release>());
 
   py::class_<EdgeShard>(m, "EdgeShard")
       .def_readonly("n", &EdgeShard::n)

@@ -156,3 +156,35 @@ def test_bootstrap_ignores_a_silent_stray_connection():
     assert not t.is_alive() and boots[0] is not None
     assert time.time() - t0 < 30
     stray.close()
+
+
+def test_group_bootstrap_threads():
+    """The in-process bootstrap (GroupBootstrap: the ranks of a VirtualGroup,
+    one thread each) gathers every rank's bytes in rank order, broadcasts the
+    root's and shares the group with its virtual communicators."""
+    import threading
+
+    from distributed_cuda_bfs_amd._native import N
+
+    P = 4
+    group = N.VirtualGroup(P)
+    got = [None] * P
+
+    def body(r):
+        b = N.group_bootstrap(group, r)
+        assert b.in_process and b.rank == r and b.size == P
+        a = b.allgather(bytes([r]) * (r + 1))
+        c = b.broadcast(b"root%d" % r, root=2)
+        b.barrier()
+        d = b.allgather(b"")
+        got[r] = (a, c, d)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    for r in range(P):
+        a, c, d = got[r]
+        assert a == [bytes([q]) * (q + 1) for q in range(P)]
+        assert c == b"root2" and d == [b""] * P

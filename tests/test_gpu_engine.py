@@ -842,3 +842,77 @@ def test_peer_comm_four_ranks_share_one_gpu_rmat20():
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["n_gpus"] == 4
     assert rec["validated"] is True and rec["validated_roots"] == "4/4"
+
+
+def _free_port_pair():
+    import socket
+
+    while True:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        if port < 65000:
+            return port
+
+
+def test_cli_peer_two_processes_share_one_gpu():
+    """bin/bfs as two processes (WORLD_SIZE = 2, the reference's bfs_mpi.cu
+    model) on device 0 over the peer-memory transport: IPC windows, TCP for
+    what does not fit them (RCCL refuses a shared device); the reference's
+    output lines, Output OK! against the oracle, Graph500 checks."""
+    import json
+    import subprocess
+
+    port = _free_port_pair()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port - 1), DBFS_BOOTSTRAP_PORT=str(port), DBFS_DEVICE="0", DBFS_COMM="peer",
+                   DBFS_PEER_SLOT_MB="4", DBFS_COMM_TIMEOUT_S="60")
+        procs.append(subprocess.Popen([os.path.join(REPO, "bin", "bfs"), "--rmat", "16", "5", "--validate", "--json"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=110)
+        except subprocess.TimeoutExpired:
+            p.kill()  # exact child PID
+            o, e = p.communicate()
+        outs.append((p.returncode, o, e))
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+    o = outs[0][1]
+    assert "Output OK!" in o and "Validation OK" in o
+    rec = json.loads([l for l in o.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["ranks"] == 2
+
+
+def test_in_process_peer_refuses_a_shared_device():
+    """The in-process peer transport (GroupBootstrap, the --gpus P path: each
+    rank's window shared as a device pointer) needs one device per rank:
+    threads sharing a device cannot spin on each other's flags (a hipFree in
+    one waits for the other's collective).  On one GPU every rank refuses,
+    agreed, so every rank can fall back together."""
+    import threading
+
+    from distributed_cuda_bfs_amd._native import N
+    from distributed_cuda_bfs_amd.parallel.runtime import make_backend
+
+    P = 2
+    group = N.VirtualGroup(P)
+    errs = [None] * P
+
+    def body(r):
+        be = make_backend("hip", 0)
+        inner = N.virtual_comm(group, r, be)
+        try:
+            N.peer_comm(N.group_bootstrap(group, r), be, inner, 1 << 20)
+        except Exception as e:  # noqa: BLE001
+            errs[r] = str(e)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert all(e and "share device" in e for e in errs), errs
