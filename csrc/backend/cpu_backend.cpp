@@ -336,6 +336,7 @@ class CpuBackend final : public Backend {
     a.oscan[sparse_cnt_] = sparse_deg_;
   }
   void td_sparse(const TdSparseArgs& a) override {
+    DBFS_CHECK(!a.direct.active, "CpuBackend: no direct list exchange (peer windows are GPU memory)");
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     const int64_t q = a.dev_stats[0];
     for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
@@ -369,6 +370,7 @@ class CpuBackend final : public Backend {
     }
   }
   void td_sparse_apply(const TdSparseArgs& a) override {
+    DBFS_CHECK(!a.direct.active, "CpuBackend: no direct list exchange (peer windows are GPU memory)");
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     for (int r = 0; r < a.nranks; ++r) {
       const vid_t* list = a.recv_lists + static_cast<int64_t>(r) * a.list_stride;

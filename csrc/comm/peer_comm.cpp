@@ -138,6 +138,34 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   }
   agree("window mapping");
   if (!ipc_) boot_->barrier();  // every rank holds every window before any may drop one
+  // the direct exchange's tables (one per parity; DBFS_PEER_DIRECT=0: none)
+  const char* de = std::getenv("DBFS_PEER_DIRECT");
+  if (!de || std::string(de) != "0") {
+    static_assert(kMaxDirectRanks == kern::kMaxPeers, "direct exchange and peer kernels share the rank bound");
+    DirectTable t[2];
+    for (int b = 0; b < 2; ++b) {
+      std::memset(&t[b], 0, sizeof(DirectTable));
+      for (int p = 0; p < size_; ++p) {
+        const bool self = p == rank_;
+        t[b].dst[p] = self ? nullptr : reinterpret_cast<uint32_t*>(slot_ptr(p, b, rank_));
+        t[b].flag[p] = self ? nullptr : reinterpret_cast<uint64_t*>(peer_[p]) + rank_;
+        // (this rank's own claims are settled in place: its list is a zero
+        // word of the flag page, never written)
+        t[b].src[p] = self ? reinterpret_cast<const uint32_t*>(win_ + kFlagBytes - 16)
+                           : reinterpret_cast<const uint32_t*>(slot_ptr(rank_, b, p));
+      }
+      t[b].flags = reinterpret_cast<const uint64_t*>(win_);
+    }
+    try {
+      void* d = nullptr;
+      HIP_CHECK(hipMalloc(&d, sizeof(t)));
+      dtab_ = static_cast<DirectTable*>(d);
+      HIP_CHECK(hipMemcpy(d, t, sizeof(t), hipMemcpyHostToDevice));
+    } catch (const std::exception& e) {
+      local_err = e.what();
+    }
+  }
+  agree("direct exchange tables");  // (every rank has them, or none goes on)
   // a wait kernel that timed out leaves its seq in the error word: the host's
   // waits (stream synchronise, mailbox spins) turn it into an error
   prev_watch_ = be.wait_watch();
@@ -182,6 +210,8 @@ void PeerComm::release() {
   peer_.clear();
   if (ticket_) hipFree(ticket_);
   ticket_ = nullptr;
+  if (dtab_) hipFree(dtab_);
+  dtab_ = nullptr;
   keep_.clear();
   if (win_keep_) win_keep_.reset();  // (in-process: frees with the last holder)
   else if (win_) hipFree(win_);
@@ -405,6 +435,24 @@ void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t strid
     pl.recv[p] = {nullptr, recv + p * stride_words, cap_b};
   }
   run(pl);
+}
+
+bool PeerComm::direct_lists(size_t cap, DirectLists* x) {
+  const int64_t piece = static_cast<int64_t>(cap + 1) * 4;
+  if (static_cast<size_t>(piece) > slot_ || !dtab_) return false;
+  note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);  // (accounted at the capacity, as alltoall_lists)
+  const uint64_t s = ++seq_;
+  x->active = 1;
+  x->nranks = size_;
+  x->rank = rank_;
+  x->seq = s;
+  x->table = dtab_ + (s & 1);
+  const double limit = comm_timeout_s() > 0 ? std::min(comm_timeout_s(), 60.0) : 60.0;
+  const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
+  x->timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
+  x->error = err_dev_;
+  ++peer_ops_;
+  return true;
 }
 
 void PeerComm::level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,

@@ -162,6 +162,59 @@ ReplayComm::ReplayComm(std::shared_ptr<CommTape> tape, Backend& be) : tape_(std:
     if (!r.data.empty()) be.to_device(dev_.data() + off, r.data.data(), r.data.size());
     off += static_cast<int64_t>(r.data.size());
   }
+  // direct list exchanges (DirectLists): each recorded list exchange as a
+  // table whose sources are the recorded lists in dev_, whose destinations
+  // are one scratch buffer (what this rank sends is not replayed anywhere),
+  // and whose flags have all arrived (every word ~0)
+  if (be.kind() == DeviceKind::HIP && tape_->size <= kMaxDirectRanks) {
+    std::vector<DirectTable> tabs;
+    int64_t cap_max = 0;
+    for (const auto& r : tape_->recs)
+      if (r.kind == CommTape::kLists) cap_max = std::max(cap_max, r.b);
+    dscratch_ = DBuf<char>(be, static_cast<size_t>((cap_max + 1) * 4 + 16 * 8 + 16 * 8));
+    char* scr = dscratch_.data();
+    uint64_t* arrived = reinterpret_cast<uint64_t*>(scr + (cap_max + 1) * 4);
+    uint64_t* flag_sink = arrived + 16;
+    std::vector<uint64_t> ones(16, ~uint64_t(0));
+    be.to_device(arrived, ones.data(), ones.size() * sizeof(uint64_t));
+    for (size_t i = 0; i < tape_->recs.size(); ++i) {
+      const auto& r = tape_->recs[i];
+      if (r.kind != CommTape::kLists || static_cast<int>(r.pieces.size()) != tape_->size) continue;
+      DirectTable t;
+      std::memset(&t, 0, sizeof(t));
+      int64_t o = off_[i];
+      for (int p = 0; p < tape_->size; ++p) {
+        t.dst[p] = reinterpret_cast<uint32_t*>(scr);
+        t.flag[p] = flag_sink + p;
+        t.src[p] = reinterpret_cast<const uint32_t*>(dev_.data() + o);
+        o += r.pieces[p];
+      }
+      t.flags = arrived;
+      dtab_index_[i] = static_cast<int64_t>(tabs.size());
+      tabs.push_back(t);
+    }
+    if (!tabs.empty()) {
+      dtab_ = DBuf<char>(be, tabs.size() * sizeof(DirectTable));
+      be.to_device(dtab_.data(), tabs.data(), tabs.size() * sizeof(DirectTable));
+    }
+  }
+}
+
+bool ReplayComm::direct_lists(size_t cap, DirectLists* x) {
+  if (pos_ >= tape_->recs.size()) return false;
+  const auto& r = tape_->recs[pos_];
+  const auto it = dtab_index_.find(pos_);
+  if (r.kind != CommTape::kLists || r.b != static_cast<int64_t>(cap) || it == dtab_index_.end()) return false;
+  note(kAllToAllV, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(cap + 1) * 4);
+  x->active = 1;
+  x->nranks = size();
+  x->rank = rank();
+  x->seq = 1;  // (every flag reads ~0)
+  x->table = reinterpret_cast<const DirectTable*>(dtab_.data()) + it->second;
+  x->timeout_ticks = ~uint64_t(0) >> 1;
+  x->error = reinterpret_cast<uint64_t*>(dscratch_.data());  // (never written: no wait times out)
+  ++pos_;
+  return true;
 }
 
 const CommTape::Rec& ReplayComm::next(int kind, int64_t a, int64_t b, size_t* idx) {

@@ -86,6 +86,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
+  else if (name == "direct_lists") o.direct_lists = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -127,7 +128,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
-          {"list_cap_factor", o.list_cap_factor}};
+          {"list_cap_factor", o.list_cap_factor},
+          {"direct_lists", o.direct_lists ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -1458,10 +1460,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         sp.list_stride = list_stride_;
         sp.part = part_.part;
         sp.mailbox = nullptr;
+        // the exchange itself: by the two kernels through the peers'
+        // windows (direct), or a collective between them
+        const size_t lcap = static_cast<size_t>(chain_cap > 0 ? chain_cap : list_max);
+        const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
         be_.td_sparse(sp);
-        comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_),
-                             static_cast<size_t>(chain_cap > 0 ? chain_cap : list_max));
-        sp.recv_lists = dl_recv_lists_.data();
+        if (!direct)
+          comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_), lcap);
+        sp.recv_lists = direct ? nullptr : dl_recv_lists_.data();
         sp.nranks = P;
         sp.grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
         be_.td_sparse_apply(sp);

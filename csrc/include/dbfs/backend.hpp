@@ -387,6 +387,30 @@ struct CompactArgs {
 // clean).  The last workgroup publishes the totals (stats[0..3], oscan[q]),
 // runs level_ctrl_finish and stamps rec / the mailbox like the scan.
 constexpr int kSparseEdgeBits = 36;
+// Direct owner-list exchange (peer transport, Comm::direct_lists): the
+// producing kernel stores each remote claim straight into its owner's window
+// (the slot this rank owns there: count word, then the ids) and its last
+// workgroup publishes the counts and a flag per peer; the consuming kernel
+// waits for every peer's flag and reads the lists from its own window.  No
+// exchange launch in between.
+constexpr int kMaxDirectRanks = 16;
+// Where the lists go and come from, in device memory (the kernels index it
+// with a wave-uniform owner): one table per window parity.
+struct DirectTable {
+  uint32_t* dst[kMaxDirectRanks];        // rank p's window slot for this rank ([rank]: unused)
+  uint64_t* flag[kMaxDirectRanks];       // rank p's flag word for this rank ([rank]: unused)
+  const uint32_t* src[kMaxDirectRanks];  // this rank's window slot of sender p ([rank]: a zero word)
+  const uint64_t* flags;                 // this rank's flag words (index = sender)
+};
+struct DirectLists {
+  int active = 0;  // 0: the lists travel through Comm::alltoall_lists
+  int nranks = 1, rank = 0;
+  uint64_t seq = 0;                     // this exchange's flag value
+  const DirectTable* table = nullptr;   // device memory
+  uint64_t timeout_ticks = 0;           // a wait gives up after this many wall-clock ticks
+  uint64_t* error = nullptr;            // ... and stores seq here (the host watches it)
+};
+
 struct TdSparseArgs {
   ShardView g;
   const int64_t* qscan = nullptr;
@@ -432,6 +456,9 @@ struct TdSparseArgs {
   // send lists whose counts it zeroes for the next list level
   const vid_t* recv_lists = nullptr;
   int nranks = 1;
+  // direct.active: the lists go straight into the owners' windows (td_sparse)
+  // and are read from this rank's window (td_sparse_apply, after the flags)
+  DirectLists direct;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):

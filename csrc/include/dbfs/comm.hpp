@@ -25,6 +25,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "dbfs/backend.hpp"
@@ -78,6 +79,16 @@ class Comm {
   // collective where the transport can (peer windows: one launch, both
   // payloads in one slot; RCCL: one group); in order otherwise.
   virtual void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count);
+  // The next owner-list exchange (alltoall_lists of `cap` ids per peer) done
+  // by the kernels themselves (DirectLists: producer stores into the peers'
+  // windows, consumer waits for their flags): fills `x` and returns true, or
+  // false when this transport cannot (the caller uses alltoall_lists).  The
+  // choice depends only on `cap` (the same on every rank).
+  virtual bool direct_lists(size_t cap, DirectLists* x) {
+    (void)cap;
+    (void)x;
+    return false;
+  }
   // A level's end on several ranks: its totals all-reduced (buf, count) --
   // with gbytes > 0 also its output frontier slice all-gathered (gsend ->
   // grecv) -- then the device continuation `fin`, the level's decision on the
@@ -336,6 +347,9 @@ class ReplayComm final : public Comm {
   void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
                  const LevelFinishArgs& fin) override;
   double max_host(double x) override { return x; }  // this rank's own time
+  // a recorded list exchange as a direct one: the apply reads the recorded
+  // lists in place (no copy launch), the kernels' own stores land in scratch
+  bool direct_lists(size_t cap, DirectLists* x) override;
   size_t position() const { return pos_; }
   size_t length() const { return tape_->recs.size(); }
 
@@ -343,6 +357,8 @@ class ReplayComm final : public Comm {
   const CommTape::Rec& next(int kind, int64_t a, int64_t b, size_t* idx);
   std::shared_ptr<CommTape> tape_;
   DBuf<char> dev_;
+  DBuf<char> dtab_, dscratch_;                      // direct exchange tables / sinks
+  std::unordered_map<size_t, int64_t> dtab_index_;  // record -> table
   std::vector<int64_t> off_;
   size_t pos_ = 0;
 };
@@ -374,6 +390,7 @@ class PeerComm final : public Comm {
   void barrier() override;
   void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
   bool counted_lists() const override { return true; }
+  bool direct_lists(size_t cap, DirectLists* x) override;
   void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
   void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
                  const LevelFinishArgs& fin) override;
@@ -423,6 +440,9 @@ class PeerComm final : public Comm {
   int64_t peer_ops_ = 0, inner_ops_ = 0;
   // every collective as one launch (DBFS_PEER_FUSED=0: push / wait / unpack)
   bool fused_ = true;
+  // owner lists exchanged by the kernels themselves (DBFS_PEER_DIRECT=0: off):
+  // the device tables of DirectLists, one per parity
+  DirectTable* dtab_ = nullptr;
   std::function<void(double)> prev_watch_;
   bool watch_installed_ = false;
   char* slot_ptr(int owner, int parity, int sender) const;

@@ -230,6 +230,11 @@ struct EngineOptions {
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
   double list_cap_factor = 4.0;
+  // Sparse chains on a transport with a direct exchange (peer windows,
+  // Comm::direct_lists): td_sparse stores remote claims straight into their
+  // owners' windows and td_sparse_apply waits for the flags -- no exchange
+  // launch in between
+  bool direct_lists = true;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is

@@ -949,24 +949,98 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   }
 }
 
-// Append v (act lanes) to its owner's list (lists + owner * stride: count
-// word, then the ids): one atomic per wave and owner.  Wave-uniform call.
-__device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, int64_t part, vid_t v, bool act) {
+// Cross-GPU hand-off words (direct owner-list exchange): system-scope relaxed
+// accesses through global (not flat) instructions -- sc0 sc1 stores write
+// through to the owner's memory, sc0 sc1 loads read it -- so neither side
+// needs an L2 write-back or invalidate (MI355X_MICROARCH hand-off forms:
+// write-through stores, every storing wave's vmcnt(0) before the signal, the
+// reader's loads behind its poll and a workgroup barrier).
+using gu32 = __attribute__((address_space(1))) uint32_t;
+using gu64 = __attribute__((address_space(1))) uint64_t;
+__device__ __forceinline__ void sys_store_u32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store_u64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t sys_load_u32(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
+  return __hip_atomic_load((gu64*)(const_cast<uint64_t*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Append v (act lanes) to its owner's list: one atomic per wave and owner on
+// the count word (lists + owner * stride), the ids after it -- or, with a
+// direct exchange table, after the count word of the owner's window slot
+// (write-through stores over xGMI).  Wave-uniform call.
+__device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, int64_t part, vid_t v, bool act,
+                                                  const DirectTable* dt = nullptr) {
   const int lane = lane_id();
   const int owner = act ? static_cast<int>(static_cast<int64_t>(v) / part) : -1;
   unsigned long long pending = __ballot(act);
   while (pending) {
     const int leader = __ffsll(static_cast<long long>(pending)) - 1;
-    const int o = __shfl(owner, leader, kWave);
+    const int o = __builtin_amdgcn_readfirstlane(__shfl(owner, leader, kWave));
     const unsigned long long msk = __ballot(owner == o);
     unsigned base = 0;
     vid_t* list = lists + static_cast<int64_t>(o) * stride;
     if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
     base = __shfl(base, leader, kWave);
     DBFS_DCHECK(base + __popcll(msk) < static_cast<unsigned long long>(stride), 3, base);
-    if (owner == o) list[1 + base + mask_rank(msk)] = v;
+    if (owner == o) {
+      const unsigned at = 1 + base + mask_rank(msk);
+      if (dt) sys_store_u32(dt->dst[o] + at, v);
+      else list[at] = v;
+    }
     pending &= ~msk;
   }
+}
+
+// Direct exchange, producer side (one workgroup, after every producing
+// wave's stores have drained): thread p writes this rank's count for owner p
+// into the count word of p's window slot, zeroes the local count for the next
+// list level, waits for that store and raises p's flag for this rank.  A
+// chain that is not live publishes empty lists: the peers wait all the same.
+__device__ __forceinline__ void direct_publish(const DirectLists& d, vid_t* lists, int64_t stride, bool live) {
+  const int t = threadIdx.x;
+  if (t < d.nranks && t != d.rank) {
+    vid_t* cnt = lists + static_cast<int64_t>(t) * stride;
+    const vid_t n = live ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    *cnt = 0u;
+    sys_store_u32(d.table->dst[t], n);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sys_store_u64(d.table->flag[t], d.seq);
+  }
+}
+
+// Direct exchange, consumer side (every workgroup): threads p < nranks poll
+// sender p's flag in this rank's window until it reaches seq (bounded: a
+// timeout stores seq in the error word the host watches); false on timeout.
+// The lists are then read with sys_load_u32 behind the barrier.
+__device__ __forceinline__ bool direct_wait(const DirectLists& d) {
+  __shared__ int s_ok;
+  const int t = threadIdx.x;
+  if (t == 0) s_ok = 1;
+  __syncthreads();
+  if (t < d.nranks && t != d.rank) {
+    const uint64_t* fl = d.table->flags + t;
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t spin = 0;; ++spin) {
+      if (sys_load_u64(fl) >= d.seq) break;
+      __builtin_amdgcn_s_sleep(2);
+      if ((spin & 255) == 255 && wall_clock64() - t0 > d.timeout_ticks) {
+        s_ok = 0;  // (benign race: every writer stores 0)
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_ok) return true;
+  if (t == 0 && d.error) sys_store_u64(d.error, d.seq);
+  return false;
 }
 
 // The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
@@ -1059,8 +1133,13 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ int s_last;
-  // uniform: the whole grid returns, no workgroup takes a ticket
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  const bool dx = a.lists && a.direct.active;
+  // uniform: the whole grid returns, no workgroup takes a ticket (a direct
+  // exchange still publishes, empty)
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    if (dx && blockIdx.x == 0) direct_publish(a.direct, a.lists, a.list_stride, false);
+    return;
+  }
   if (a.first) stamp_level_start(a.ctrl);
   const long long q = a.dev_stats[0], m = a.dev_stats[1];
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
@@ -1106,13 +1185,29 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       claimed &= ~remote;
       if (__ballot(remote != 0)) {
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u);
+        for (int k = 0; k < kItems; ++k)
+          owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u, dx ? a.direct.table : nullptr);
       }
     }
     // (B) finish the wave's claimed vertices
     sparse_settle<kItems>(a, v, claimed);
   }
-  if (a.lists) return;  // several ranks: td_sparse_apply finishes the level
+  if (a.lists) {
+    // several ranks: td_sparse_apply finishes the level.  A direct exchange:
+    // every wave's write-through stores drained, the workgroups' ticket, and
+    // the last one publishes the counts and flags.
+    if (!dx) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned prev = atomicAdd(a.ticket, 1u);
+      s_last = (prev == active - 1) ? 1 : 0;
+      if (s_last) *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
+    }
+    __syncthreads();
+    if (s_last) direct_publish(a.direct, a.lists, a.list_stride, true);
+    return;
+  }
 
   // last workgroup: the level's totals and decision (as scan_units_kernel)
   __syncthreads();
@@ -1150,10 +1245,20 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   constexpr int kItems = kTdItems;
   __shared__ int s_last;
   __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
+  __shared__ const vid_t* s_src[kern::kMaxPeers];
+  // a direct exchange: the peers' flags first, live chain or not (every rank
+  // waits for every exchange: the window slots' reuse protocol)
+  const bool dx = a.direct.active;
+  if (dx && !direct_wait(a.direct)) return;
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
   const int t = threadIdx.x;
   if (t < kWave) {
-    const long long n = t < a.nranks ? static_cast<long long>(a.recv_lists[static_cast<int64_t>(t) * a.list_stride]) : 0;
+    long long n = 0;
+    if (t < a.nranks) {
+      const vid_t* src = dx ? a.direct.table->src[t] : a.recv_lists + static_cast<int64_t>(t) * a.list_stride;
+      s_src[t] = src;
+      n = dx ? static_cast<long long>(sys_load_u32(src)) : static_cast<long long>(*src);
+    }
     DBFS_DCHECK(n < a.list_stride, 5, n);
     const long long incl = wave_incl_scan(n);
     if (t < a.nranks) s_end[t] = incl;
@@ -1176,7 +1281,8 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
         int r = 0;
         while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
         const long long before = r > 0 ? s_end[r - 1] : 0;
-        v[k] = a.recv_lists[static_cast<int64_t>(r) * a.list_stride + 1 + (j - before)];
+        const vid_t* src = s_src[r] + 1 + (j - before);
+        v[k] = dx ? sys_load_u32(src) : *(const gu32*)(src);
       }
     }
 #pragma unroll
@@ -1200,8 +1306,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   __syncthreads();
   if (!s_last) return;
   // the send lists were read by the exchange (stream-ordered before this
-  // kernel): their counts restart from zero for the next list level
-  if (t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
+  // kernel): their counts restart from zero for the next list level (a
+  // direct exchange's publisher zeroed them)
+  if (!dx && t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
   if (t != 0) return;
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
