@@ -33,6 +33,8 @@ namespace dbfs {
 
 namespace {
 constexpr size_t kFlagBytes = 4096;
+constexpr size_t kCellBase = 1024;  // direct exchange cells in the flag page (flags: bytes [0, 8 P))
+static_assert(kCellBase + 2 * 16 * 16 <= kFlagBytes, "direct cells fit the flag page");
 inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->comm_stream_handle()); }
 }  // namespace
 
@@ -143,18 +145,19 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   if (!de || std::string(de) != "0") {
     static_assert(kMaxDirectRanks == kern::kMaxPeers, "direct exchange and peer kernels share the rank bound");
     DirectTable t[2];
+    // the direct exchanges' cells: flag page bytes [kCellBase, +2 x 16 x 16)
+    auto cell = [&](char* win, int parity, int sender) {
+      return reinterpret_cast<uint64_t*>(win + kCellBase + (static_cast<size_t>(parity) * kern::kMaxPeers + sender) * 16);
+    };
     for (int b = 0; b < 2; ++b) {
       std::memset(&t[b], 0, sizeof(DirectTable));
       for (int p = 0; p < size_; ++p) {
         const bool self = p == rank_;
         t[b].dst[p] = self ? nullptr : reinterpret_cast<uint32_t*>(slot_ptr(p, b, rank_));
-        t[b].flag[p] = self ? nullptr : reinterpret_cast<uint64_t*>(peer_[p]) + rank_;
-        // (this rank's own claims are settled in place: its list is a zero
-        // word of the flag page, never written)
-        t[b].src[p] = self ? reinterpret_cast<const uint32_t*>(win_ + kFlagBytes - 16)
-                           : reinterpret_cast<const uint32_t*>(slot_ptr(rank_, b, p));
+        t[b].cell_out[p] = self ? nullptr : cell(peer_[p], b, rank_);
+        t[b].src[p] = reinterpret_cast<const uint32_t*>(slot_ptr(rank_, b, p));
+        t[b].cell_in[p] = self ? nullptr : cell(win_, b, p);
       }
-      t[b].flags = reinterpret_cast<const uint64_t*>(win_);
     }
     try {
       void* d = nullptr;
@@ -437,7 +440,7 @@ void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t strid
   run(pl);
 }
 
-bool PeerComm::direct_lists(size_t cap, DirectLists* x) {
+bool PeerComm::direct_lists(size_t cap, DirectExchange* x) {
   const int64_t piece = static_cast<int64_t>(cap + 1) * 4;
   if (static_cast<size_t>(piece) > slot_ || !dtab_) return false;
   note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);  // (accounted at the capacity, as alltoall_lists)
@@ -451,6 +454,26 @@ bool PeerComm::direct_lists(size_t cap, DirectLists* x) {
   const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
   x->timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
   x->error = err_dev_;
+  ++peer_ops_;
+  return true;
+}
+
+bool PeerComm::direct_level_end(size_t count, DirectExchange* x) {
+  // (a level's totals: at most 2^32 new vertices and 2^40 of their degrees
+  // per rank -- the cells' payload widths)
+  if (!dtab_ || count != 2 || be_ == nullptr) return false;
+  note(kAllReduce, static_cast<int64_t>(size_ - 1) * static_cast<int64_t>(count) * 8);
+  const uint64_t s = ++seq_;
+  x->active = 1;
+  x->nranks = size_;
+  x->rank = rank_;
+  x->seq = s;
+  x->table = dtab_ + (s & 1);
+  const double limit = comm_timeout_s() > 0 ? std::min(comm_timeout_s(), 60.0) : 60.0;
+  const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
+  x->timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
+  x->error = err_dev_;
+  x->result = nullptr;
   ++peer_ops_;
   return true;
 }

@@ -162,45 +162,89 @@ ReplayComm::ReplayComm(std::shared_ptr<CommTape> tape, Backend& be) : tape_(std:
     if (!r.data.empty()) be.to_device(dev_.data() + off, r.data.data(), r.data.size());
     off += static_cast<int64_t>(r.data.size());
   }
-  // direct list exchanges (DirectLists): each recorded list exchange as a
-  // table whose sources are the recorded lists in dev_, whose destinations
-  // are one scratch buffer (what this rank sends is not replayed anywhere),
-  // and whose flags have all arrived (every word ~0)
+  // direct exchanges (DirectExchange, sequence number 1): each recorded list
+  // exchange as a table whose sources are the recorded lists in dev_ and
+  // whose incoming cells hold their counts; outgoing data and cells go to a
+  // sink (what this rank sends is not replayed anywhere); the level ends'
+  // table has cells that have arrived (the kernel takes the recorded sums)
   if (be.kind() == DeviceKind::HIP && tape_->size <= kMaxDirectRanks) {
-    std::vector<DirectTable> tabs;
-    int64_t cap_max = 0;
+    int64_t cap_max = 0, nlists = 0;
     for (const auto& r : tape_->recs)
-      if (r.kind == CommTape::kLists) cap_max = std::max(cap_max, r.b);
-    dscratch_ = DBuf<char>(be, static_cast<size_t>((cap_max + 1) * 4 + 16 * 8 + 16 * 8));
+      if (r.kind == CommTape::kLists && static_cast<int>(r.pieces.size()) == tape_->size) {
+        cap_max = std::max(cap_max, r.b);
+        ++nlists;
+      }
+    // [sink for ids / cells][cells: one 16-B cell per rank and list record,
+    // then the level ends' arrived cells]
+    const int64_t sink_b = (std::max<int64_t>((cap_max + 1) * 4, 64 * 16) + 15) / 16 * 16;
+    const int64_t ncells = (nlists + 1) * kMaxDirectRanks;
+    dscratch_ = DBuf<char>(be, static_cast<size_t>(sink_b + ncells * 16));
     char* scr = dscratch_.data();
-    uint64_t* arrived = reinterpret_cast<uint64_t*>(scr + (cap_max + 1) * 4);
-    uint64_t* flag_sink = arrived + 16;
-    std::vector<uint64_t> ones(16, ~uint64_t(0));
-    be.to_device(arrived, ones.data(), ones.size() * sizeof(uint64_t));
+    uint64_t* cells = reinterpret_cast<uint64_t*>(scr + sink_b);
+    std::vector<uint64_t> hcells(static_cast<size_t>(ncells * 2), 0);
+    std::vector<DirectTable> tabs;
+    auto sink_table = [&](DirectTable& t) {
+      std::memset(&t, 0, sizeof(t));
+      for (int p = 0; p < tape_->size; ++p) {
+        t.dst[p] = reinterpret_cast<uint32_t*>(scr);
+        t.cell_out[p] = reinterpret_cast<uint64_t*>(scr) + 2 * p;
+      }
+    };
     for (size_t i = 0; i < tape_->recs.size(); ++i) {
       const auto& r = tape_->recs[i];
       if (r.kind != CommTape::kLists || static_cast<int>(r.pieces.size()) != tape_->size) continue;
       DirectTable t;
-      std::memset(&t, 0, sizeof(t));
+      sink_table(t);
+      const int64_t c0 = static_cast<int64_t>(tabs.size()) * kMaxDirectRanks;
       int64_t o = off_[i];
+      size_t ho = 0;
       for (int p = 0; p < tape_->size; ++p) {
-        t.dst[p] = reinterpret_cast<uint32_t*>(scr);
-        t.flag[p] = flag_sink + p;
+        uint32_t n = 0;
+        std::memcpy(&n, r.data.data() + ho, sizeof(n));
         t.src[p] = reinterpret_cast<const uint32_t*>(dev_.data() + o);
+        t.cell_in[p] = cells + 2 * (c0 + p);
+        hcells[static_cast<size_t>(2 * (c0 + p))] = (uint64_t(1) << 32) | n;
         o += r.pieces[p];
+        ho += static_cast<size_t>(r.pieces[p]);
       }
-      t.flags = arrived;
       dtab_index_[i] = static_cast<int64_t>(tabs.size());
       tabs.push_back(t);
     }
-    if (!tabs.empty()) {
-      dtab_ = DBuf<char>(be, tabs.size() * sizeof(DirectTable));
-      be.to_device(dtab_.data(), tabs.data(), tabs.size() * sizeof(DirectTable));
+    DirectTable t;
+    sink_table(t);
+    const int64_t c0 = static_cast<int64_t>(tabs.size()) * kMaxDirectRanks;
+    for (int p = 0; p < tape_->size; ++p) {
+      t.src[p] = reinterpret_cast<const uint32_t*>(scr);
+      t.cell_in[p] = cells + 2 * (c0 + p);
+      hcells[static_cast<size_t>(2 * (c0 + p))] = uint64_t(1) << 32;
+      hcells[static_cast<size_t>(2 * (c0 + p) + 1)] = uint64_t(1) << 40;
     }
+    dtab_sink_ = static_cast<int64_t>(tabs.size());
+    tabs.push_back(t);
+    be.to_device(cells, hcells.data(), hcells.size() * sizeof(uint64_t));
+    dtab_ = DBuf<char>(be, tabs.size() * sizeof(DirectTable));
+    be.to_device(dtab_.data(), tabs.data(), tabs.size() * sizeof(DirectTable));
   }
 }
 
-bool ReplayComm::direct_lists(size_t cap, DirectLists* x) {
+bool ReplayComm::direct_level_end(size_t count, DirectExchange* x) {
+  if (dtab_sink_ < 0 || pos_ >= tape_->recs.size()) return false;
+  const auto& r = tape_->recs[pos_];
+  if (r.kind != kAllReduce || r.a != static_cast<int64_t>(count)) return false;
+  note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
+  x->active = 1;
+  x->nranks = size();
+  x->rank = rank();
+  x->seq = 1;  // (every flag reads ~0)
+  x->table = reinterpret_cast<const DirectTable*>(dtab_.data()) + dtab_sink_;
+  x->timeout_ticks = ~uint64_t(0) >> 1;
+  x->error = reinterpret_cast<uint64_t*>(dscratch_.data());
+  x->result = reinterpret_cast<const int64_t*>(dev_.data() + off_[pos_]);  // the recorded sums
+  ++pos_;
+  return true;
+}
+
+bool ReplayComm::direct_lists(size_t cap, DirectExchange* x) {
   if (pos_ >= tape_->recs.size()) return false;
   const auto& r = tape_->recs[pos_];
   const auto it = dtab_index_.find(pos_);

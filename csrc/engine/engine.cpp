@@ -87,6 +87,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
+  else if (name == "direct_level_end") o.direct_level_end = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -129,7 +130,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
           {"list_cap_factor", o.list_cap_factor},
-          {"direct_lists", o.direct_lists ? 1.0 : 0.0}};
+          {"direct_lists", o.direct_lists ? 1.0 : 0.0},
+          {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -1260,12 +1262,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // in the same launch the level's output frontier slice all-gathered
   // (Comm::allgather_allreduce) -- then level_finish decides and stamps.
   // (bfs_mpi.cu:615-621 pays a Sendrecv and an Allreduce per level.)
-  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool gather) {
-    int64_t* blk = sblk(level);
-    // level L writes frontier_[L & 1] (the seed: frontier_[1])
-    const int out = seed ? 1 : (level & 1);
+  auto finish_args = [&](int level, bool seed, char expect_dir, int64_t cap) {
     LevelFinishArgs fa;
-    fa.stats = blk;
+    fa.stats = sblk(level);
     fa.ctrl = ctrl_.data();
     fa.ctrl_init = init;
     fa.rec = seed ? nullptr : rec_at(level);
@@ -1274,6 +1273,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     fa.seed = seed;
     fa.expect_dir = expect_dir;
     fa.expect_cap = cap;
+    return fa;
+  };
+  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool gather) {
+    int64_t* blk = sblk(level);
+    // level L writes frontier_[L & 1] (the seed: frontier_[1])
+    const int out = seed ? 1 : (level & 1);
+    const LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
     comm_.level_end(fr_own(out), frontier_[out].data(), gather ? static_cast<size_t>(W) * sizeof(word_t) : 0,
                     blk + 2, 2, fa);
   };
@@ -1376,6 +1382,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     TraceRange trace_level(trace_name);
     const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
     bool fused_scan = false;  // the chain's last kernel finishes the level (no scan launch)
+    bool level_ended = false;  // ... and also ran its level end (several ranks, direct exchange)
     // several ranks, bottom-up: the input frontier to every rank -- normally
     // gathered already by the previous level's collective; a chain enqueued
     // after a top-down prediction gathers it here (not predicated: on a no-op
@@ -1470,6 +1477,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         sp.recv_lists = direct ? nullptr : dl_recv_lists_.data();
         sp.nranks = P;
         sp.grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
+        // the level's end folded into the apply's last workgroup (no frontier
+        // gather: that one is a bandwidth collective of its own)
+        // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
+        const bool cells_fit = g_.rows() < (int64_t(1) << 32) && g_.nnz() < (int64_t(1) << 40);
+        if (direct && opt_.direct_level_end && cells_fit && !enq_gather[L] && comm_.direct_level_end(2, &sp.end)) {
+          sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
+          level_ended = true;
+        }
         be_.td_sparse_apply(sp);
       } else {
         be_.td_sparse(sp);
@@ -1666,7 +1681,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     }
     if (!fused_scan) scan(L, false, enq_dir[L], chain_cap);
     enq_fused[L] = fused_scan && d != 'S';
-    if (xc) finish_ranks(L, false, enq_dir[L], chain_cap, enq_gather[L] != 0);
+    if (xc && !level_ended) finish_ranks(L, false, enq_dir[L], chain_cap, enq_gather[L] != 0);
     if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
     hmark("enqueued " + std::to_string(L));
   };

@@ -387,28 +387,37 @@ struct CompactArgs {
 // clean).  The last workgroup publishes the totals (stats[0..3], oscan[q]),
 // runs level_ctrl_finish and stamps rec / the mailbox like the scan.
 constexpr int kSparseEdgeBits = 36;
-// Direct owner-list exchange (peer transport, Comm::direct_lists): the
-// producing kernel stores each remote claim straight into its owner's window
-// (the slot this rank owns there: count word, then the ids) and its last
-// workgroup publishes the counts and a flag per peer; the consuming kernel
-// waits for every peer's flag and reads the lists from its own window.  No
-// exchange launch in between.
+// Direct exchanges (peer transport, Comm::direct_lists / direct_level_end):
+// the kernels themselves move the data through the peers' windows, no
+// exchange launch.  Every signal is a tagged cell of two 64-bit words in the
+// receiver's window -- each word carries the exchange's sequence number next
+// to its payload, so one write-through store publishes it and one poll both
+// observes it and delivers the payload:
+//   owner lists  word 0 = seq32 << 32 | count (the ids are in the slot,
+//                stored and drained before the cell)
+//   level end    word 0 = seq32 << 32 | new vertices (< 2^32 per rank),
+//                word 1 = seq24 << 40 | their degree sum (< 2^40 per rank)
+// The cells sit in the window's flag page, apart from every other
+// collective's payload: a stale cell holds an older sequence number.
 constexpr int kMaxDirectRanks = 16;
-// Where the lists go and come from, in device memory (the kernels index it
-// with a wave-uniform owner): one table per window parity.
+// Where the data goes and comes from, in device memory (the kernels index it
+// with a wave-uniform rank): one table per window parity.
 struct DirectTable {
-  uint32_t* dst[kMaxDirectRanks];        // rank p's window slot for this rank ([rank]: unused)
-  uint64_t* flag[kMaxDirectRanks];       // rank p's flag word for this rank ([rank]: unused)
-  const uint32_t* src[kMaxDirectRanks];  // this rank's window slot of sender p ([rank]: a zero word)
-  const uint64_t* flags;                 // this rank's flag words (index = sender)
+  uint32_t* dst[kMaxDirectRanks];            // rank p's window slot for this rank (ids from word 1; [rank]: unused)
+  uint64_t* cell_out[kMaxDirectRanks];       // rank p's cell for this rank ([rank]: unused)
+  const uint32_t* src[kMaxDirectRanks];      // this rank's window slot of sender p
+  const uint64_t* cell_in[kMaxDirectRanks];  // this rank's cell of sender p ([rank]: unused)
 };
-struct DirectLists {
-  int active = 0;  // 0: the lists travel through Comm::alltoall_lists
+struct DirectExchange {
+  int active = 0;  // 0: the exchange goes through a Comm collective instead
   int nranks = 1, rank = 0;
-  uint64_t seq = 0;                     // this exchange's flag value
+  uint64_t seq = 0;                     // this exchange's sequence number (the cells' tag)
   const DirectTable* table = nullptr;   // device memory
   uint64_t timeout_ticks = 0;           // a wait gives up after this many wall-clock ticks
   uint64_t* error = nullptr;            // ... and stores seq here (the host watches it)
+  // a level end: the all-reduced totals as recorded (shadow replay) instead
+  // of the peers' cells summed
+  const int64_t* result = nullptr;
 };
 
 struct TdSparseArgs {
@@ -458,7 +467,13 @@ struct TdSparseArgs {
   int nranks = 1;
   // direct.active: the lists go straight into the owners' windows (td_sparse)
   // and are read from this rank's window (td_sparse_apply, after the flags)
-  DirectLists direct;
+  DirectExchange direct;
+  // end.active (td_sparse_apply, several ranks): the level's end folded into
+  // its last workgroup -- the totals (stats[2..3]) pushed to every peer's
+  // window, the peers' awaited and summed, then the decision (`fin`), as
+  // Comm::level_end without a frontier gather; no collective launch after.
+  DirectExchange end;
+  LevelFinishArgs fin;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):

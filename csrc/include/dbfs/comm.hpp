@@ -80,12 +80,22 @@ class Comm {
   // payloads in one slot; RCCL: one group); in order otherwise.
   virtual void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count);
   // The next owner-list exchange (alltoall_lists of `cap` ids per peer) done
-  // by the kernels themselves (DirectLists: producer stores into the peers'
+  // by the kernels themselves (DirectExchange: producer stores into the peers'
   // windows, consumer waits for their flags): fills `x` and returns true, or
   // false when this transport cannot (the caller uses alltoall_lists).  The
   // choice depends only on `cap` (the same on every rank).
-  virtual bool direct_lists(size_t cap, DirectLists* x) {
+  virtual bool direct_lists(size_t cap, DirectExchange* x) {
     (void)cap;
+    (void)x;
+    return false;
+  }
+  // The next level end without a frontier gather -- level_end(nullptr,
+  // nullptr, 0, buf, count, fin) -- done by the last workgroup of the level's
+  // last kernel (DirectExchange: push the totals to every peer's window, wait
+  // for theirs, sum, decide): fills `x` and returns true, or false (the caller
+  // uses level_end).  The choice depends only on `count`.
+  virtual bool direct_level_end(size_t count, DirectExchange* x) {
+    (void)count;
     (void)x;
     return false;
   }
@@ -349,7 +359,8 @@ class ReplayComm final : public Comm {
   double max_host(double x) override { return x; }  // this rank's own time
   // a recorded list exchange as a direct one: the apply reads the recorded
   // lists in place (no copy launch), the kernels' own stores land in scratch
-  bool direct_lists(size_t cap, DirectLists* x) override;
+  bool direct_lists(size_t cap, DirectExchange* x) override;
+  bool direct_level_end(size_t count, DirectExchange* x) override;
   size_t position() const { return pos_; }
   size_t length() const { return tape_->recs.size(); }
 
@@ -359,6 +370,7 @@ class ReplayComm final : public Comm {
   DBuf<char> dev_;
   DBuf<char> dtab_, dscratch_;                      // direct exchange tables / sinks
   std::unordered_map<size_t, int64_t> dtab_index_;  // record -> table
+  int64_t dtab_sink_ = -1;                          // a table of sinks and arrived flags
   std::vector<int64_t> off_;
   size_t pos_ = 0;
 };
@@ -390,7 +402,8 @@ class PeerComm final : public Comm {
   void barrier() override;
   void alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) override;
   bool counted_lists() const override { return true; }
-  bool direct_lists(size_t cap, DirectLists* x) override;
+  bool direct_lists(size_t cap, DirectExchange* x) override;
+  bool direct_level_end(size_t count, DirectExchange* x) override;
   void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
   void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
                  const LevelFinishArgs& fin) override;
@@ -441,7 +454,7 @@ class PeerComm final : public Comm {
   // every collective as one launch (DBFS_PEER_FUSED=0: push / wait / unpack)
   bool fused_ = true;
   // owner lists exchanged by the kernels themselves (DBFS_PEER_DIRECT=0: off):
-  // the device tables of DirectLists, one per parity
+  // the device tables of DirectExchange, one per parity
   DirectTable* dtab_ = nullptr;
   std::function<void(double)> prev_watch_;
   bool watch_installed_ = false;

@@ -235,6 +235,9 @@ struct EngineOptions {
   // owners' windows and td_sparse_apply waits for the flags -- no exchange
   // launch in between
   bool direct_lists = true;
+  // ... and their level's end folded into td_sparse_apply's last workgroup
+  // (Comm::direct_level_end) when it gathers no frontier
+  bool direct_level_end = true;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is

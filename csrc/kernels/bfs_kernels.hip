@@ -999,48 +999,73 @@ __device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, 
   }
 }
 
-// Direct exchange, producer side (one workgroup, after every producing
-// wave's stores have drained): thread p writes this rank's count for owner p
-// into the count word of p's window slot, zeroes the local count for the next
-// list level, waits for that store and raises p's flag for this rank.  A
-// chain that is not live publishes empty lists: the peers wait all the same.
-__device__ __forceinline__ void direct_publish(const DirectLists& d, vid_t* lists, int64_t stride, bool live) {
+// Direct exchanges' tagged cells (backend.hpp DirectExchange).
+__device__ __forceinline__ uint64_t cell_word0(uint64_t seq, uint64_t v) { return (seq << 32) | (v & 0xffffffffull); }
+__device__ __forceinline__ uint64_t cell_word1(uint64_t seq, uint64_t v) {
+  return ((seq & 0xffffffull) << 40) | (v & ((1ull << 40) - 1));
+}
+__device__ __forceinline__ bool cell_ok0(uint64_t w, uint64_t seq) { return (w >> 32) == (seq & 0xffffffffull); }
+__device__ __forceinline__ bool cell_ok1(uint64_t w, uint64_t seq) { return (w >> 40) == (seq & 0xffffffull); }
+
+// Direct owner lists, producer side (one workgroup, after every producing
+// wave's write-through stores have drained): thread p publishes this rank's
+// count for owner p in p's cell -- one store -- and zeroes the local count for
+// the next list level.  A chain that is not live publishes empty lists: the
+// peers wait all the same.
+__device__ __forceinline__ void direct_publish(const DirectExchange& d, vid_t* lists, int64_t stride, bool live) {
   const int t = threadIdx.x;
   if (t < d.nranks && t != d.rank) {
     vid_t* cnt = lists + static_cast<int64_t>(t) * stride;
     const vid_t n = live ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     *cnt = 0u;
-    sys_store_u32(d.table->dst[t], n);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sys_store_u64(d.table->flag[t], d.seq);
+    sys_store_u64(d.table->cell_out[t], cell_word0(d.seq, n));
   }
 }
 
-// Direct exchange, consumer side (every workgroup): threads p < nranks poll
-// sender p's flag in this rank's window until it reaches seq (bounded: a
-// timeout stores seq in the error word the host watches); false on timeout.
-// The lists are then read with sys_load_u32 behind the barrier.
-__device__ __forceinline__ bool direct_wait(const DirectLists& d) {
-  __shared__ int s_ok;
+// Direct exchange, consumer side (every thread of the workgroup calls it):
+// threads p < nranks poll sender p's cell until both words asked for carry
+// this exchange's tag and leave its payload in out0 / out1 [p] (this rank's
+// own: 0).  Returns kWaitOk; kWaitTimeout after DirectExchange::timeout_ticks
+// (seq goes to the error word the host watches); kWaitLater when a cell
+// already carries a LATER exchange's tag: the peer has moved on, which it
+// does only after this rank's next signal -- so this exchange is over here
+// (a workgroup of the apply that started after the level's end: it has
+// nothing to do).  Data behind the cell is then read with sys loads.
+constexpr int kWaitOk = 1, kWaitTimeout = 0, kWaitLater = -1;
+__device__ __forceinline__ int direct_wait(const DirectExchange& d, uint64_t* out0, uint64_t* out1) {
+  __shared__ int s_st;
   const int t = threadIdx.x;
-  if (t == 0) s_ok = 1;
+  if (t == 0) s_st = kWaitOk;
   __syncthreads();
-  if (t < d.nranks && t != d.rank) {
-    const uint64_t* fl = d.table->flags + t;
-    const uint64_t t0 = wall_clock64();
-    for (uint32_t spin = 0;; ++spin) {
-      if (sys_load_u64(fl) >= d.seq) break;
-      __builtin_amdgcn_s_sleep(2);
-      if ((spin & 255) == 255 && wall_clock64() - t0 > d.timeout_ticks) {
-        s_ok = 0;  // (benign race: every writer stores 0)
-        break;
+  if (t < d.nranks) {
+    uint64_t w0 = 0, w1 = 0;
+    if (t != d.rank) {
+      const uint64_t* c = d.table->cell_in[t];
+      const uint64_t t0 = wall_clock64();
+      for (uint32_t spin = 0;; ++spin) {
+        w0 = sys_load_u64(c);
+        if (out1) w1 = sys_load_u64(c + 1);
+        if (cell_ok0(w0, d.seq) && (!out1 || cell_ok1(w1, d.seq))) break;
+        if (static_cast<int32_t>(static_cast<uint32_t>(w0 >> 32) - static_cast<uint32_t>(d.seq)) > 0) {
+          s_st = kWaitLater;  // (benign race: every writer stores the same)
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((spin & 255) == 255 && wall_clock64() - t0 > d.timeout_ticks) {
+          s_st = kWaitTimeout;
+          break;
+        }
       }
+      w0 &= 0xffffffffull;
+      w1 &= (1ull << 40) - 1;
     }
+    out0[t] = w0;
+    if (out1) out1[t] = w1;
   }
   __syncthreads();
-  if (s_ok) return true;
-  if (t == 0 && d.error) sys_store_u64(d.error, d.seq);
-  return false;
+  const int st = s_st;
+  if (st == kWaitTimeout && t == 0 && d.error) sys_store_u64(d.error, d.seq);
+  return st;
 }
 
 // The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
@@ -1119,6 +1144,40 @@ __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& 
   a.stats[0] = a.stats[2] = cnt;
   a.stats[1] = a.stats[3] = deg;
   a.oscan[cnt] = deg;
+}
+
+// The level's end in the last workgroup of its last kernel (DirectExchange
+// from Comm::direct_level_end; every thread of the workgroup calls it):
+// threads p < nranks publish this rank's totals (c new vertices, g their
+// degrees) in p's cell, every peer's cell is awaited, and thread 0 sums (or,
+// shadow replay, takes the recorded sums) into stats[2..3] and makes the
+// level's decision (level_finish_device, as Comm::level_end's).
+__device__ __forceinline__ void direct_level_end(const DirectExchange& d, int64_t c, int64_t g, int64_t* stats,
+                                                 const LevelFinishArgs& fin) {
+  __shared__ uint64_t s_c[kern::kMaxPeers], s_g[kern::kMaxPeers];
+  const int t = threadIdx.x;
+  DBFS_DCHECK(c >= 0 && c < (int64_t(1) << 32) && g >= 0 && g < (int64_t(1) << 40), 11, g);
+  if (t < d.nranks && t != d.rank) {
+    uint64_t* cell = d.table->cell_out[t];
+    sys_store_u64(cell, cell_word0(d.seq, static_cast<uint64_t>(c)));
+    sys_store_u64(cell + 1, cell_word1(d.seq, static_cast<uint64_t>(g)));
+  }
+  // (a level end is awaited by the one last workgroup of every rank: no peer
+  // passes it before this rank's cell is read, so kWaitLater cannot occur)
+  if (direct_wait(d, s_c, s_g) != kWaitOk || t != 0) return;
+  uint64_t sc = static_cast<uint64_t>(c), sg = static_cast<uint64_t>(g);
+  if (d.result) {
+    sc = static_cast<uint64_t>(d.result[0]);
+    sg = static_cast<uint64_t>(d.result[1]);
+  } else {
+    for (int p = 0; p < d.nranks; ++p) {
+      sc += s_c[p];  // (this rank's own entries are 0)
+      sg += s_g[p];
+    }
+  }
+  stats[2] = static_cast<int64_t>(sc);
+  stats[3] = static_cast<int64_t>(sg);
+  level_finish_device(fin);
 }
 
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
@@ -1246,18 +1305,23 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   __shared__ int s_last;
   __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
   __shared__ const vid_t* s_src[kern::kMaxPeers];
-  // a direct exchange: the peers' flags first, live chain or not (every rank
-  // waits for every exchange: the window slots' reuse protocol)
+  __shared__ uint64_t s_cnt[kern::kMaxPeers];
+  // a direct exchange: the peers' cells (their counts) first, live chain or
+  // not (every rank waits for every exchange: the window slots' reuse protocol)
   const bool dx = a.direct.active;
-  if (dx && !direct_wait(a.direct)) return;
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  if (dx && direct_wait(a.direct, s_cnt, nullptr) != kWaitOk) return;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if (a.end.active && blockIdx.x == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin);
+    return;
+  }
   const int t = threadIdx.x;
   if (t < kWave) {
     long long n = 0;
     if (t < a.nranks) {
       const vid_t* src = dx ? a.direct.table->src[t] : a.recv_lists + static_cast<int64_t>(t) * a.list_stride;
       s_src[t] = src;
-      n = dx ? static_cast<long long>(sys_load_u32(src)) : static_cast<long long>(*src);
+      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
     }
     DBFS_DCHECK(n < a.list_stride, 5, n);
     const long long incl = wave_incl_scan(n);
@@ -1309,9 +1373,16 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   // kernel): their counts restart from zero for the next list level (a
   // direct exchange's publisher zeroed them)
   if (!dx && t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
-  if (t != 0) return;
-  long long cnt = 0, deg = 0;
-  sparse_totals(a, cnt, deg);
+  __shared__ long long s_tot[2];
+  if (t == 0) {
+    long long cnt = 0, deg = 0;
+    sparse_totals(a, cnt, deg);
+    s_tot[0] = cnt;
+    s_tot[1] = deg;
+  }
+  if (!a.end.active) return;
+  __syncthreads();
+  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin);
 }
 
 // ---------------------------------------------------------------------------

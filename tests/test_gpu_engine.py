@@ -916,3 +916,29 @@ def test_in_process_peer_refuses_a_shared_device():
     for t in th:
         t.join(timeout=60)
     assert all(e and "share device" in e for e in errs), errs
+
+
+def test_peer_direct_exchange_long_chain(tmp_path):
+    """Two ranks on device 0 over the peer transport, on a 3000-vertex path
+    with a few shortcuts: thousands of sparse levels, each one direct owner-list
+    exchange (td_sparse -> the owner's window) and one level end folded into
+    td_sparse_apply's last workgroup -- the tagged cells reused every two
+    exchanges, workgroups of the apply that start after their level's end.
+    Every timed root validated (device validator + totals of the timed run)."""
+    import json
+    import subprocess
+    import sys
+
+    n = 3000
+    lines = [f"{i} {i + 1}" for i in range(n - 1)] + [f"{i} {i + 700}" for i in range(0, n - 700, 311)]
+    path = tmp_path / "chain.txt"
+    path.write_text(f"{n} {len(lines)}\n" + "\n".join(lines) + "\n")  # (the reference's header: n m)
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="4", DBFS_COMM_TIMEOUT_S="30")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--graph", str(path), "--steps", "3",
+           "--warmup", "1", "--no-int32-pass"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["validated_roots"] == "3/3"
