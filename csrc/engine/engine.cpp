@@ -1676,6 +1676,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
         ba.tot = bu_tot_.data();
         fused_scan = true;
+        // several ranks: the level's end in the kernel's last workgroup too
+        // (no frontier gather; the hub kernels' fused finish)
+        const bool cells_fit = g_.rows() < (int64_t(1) << 32) && g_.nnz() < (int64_t(1) << 40);
+        if (xc && opt_.direct_level_end && cells_fit && gv.nhubs > 0 && !enq_gather[L] &&
+            comm_.direct_level_end(2, &ba.end)) {
+          ba.fin = finish_args(L, false, enq_dir[L], chain_cap);
+          level_ended = true;
+        }
       }
       be_.bu_step(ba);
     }

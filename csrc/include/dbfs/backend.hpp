@@ -646,6 +646,10 @@ struct BuArgs {
   bool fuse_scan = false;
   ScanArgs scan;
   int64_t* tot = nullptr;
+  // several ranks, fuse_scan: the level's end folded into the last
+  // workgroup (Comm::direct_level_end; no frontier gather), as td_sparse_apply
+  DirectExchange end;
+  LevelFinishArgs fin;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the

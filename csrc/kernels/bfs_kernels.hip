@@ -1152,9 +1152,12 @@ __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& 
 // degrees) in p's cell, every peer's cell is awaited, and thread 0 sums (or,
 // shadow replay, takes the recorded sums) into stats[2..3] and makes the
 // level's decision (level_finish_device, as Comm::level_end's).
+// s_x: 2 x kMaxPeers words of LDS the caller lends (the bottom-up kernel has
+// none to spare: two workgroups per CU fill the LDS to within 0.5 KiB).
 __device__ __forceinline__ void direct_level_end(const DirectExchange& d, int64_t c, int64_t g, int64_t* stats,
-                                                 const LevelFinishArgs& fin) {
-  __shared__ uint64_t s_c[kern::kMaxPeers], s_g[kern::kMaxPeers];
+                                                 const LevelFinishArgs& fin, uint64_t* s_x) {
+  uint64_t* s_c = s_x;
+  uint64_t* s_g = s_x + kern::kMaxPeers;
   const int t = threadIdx.x;
   DBFS_DCHECK(c >= 0 && c < (int64_t(1) << 32) && g >= 0 && g < (int64_t(1) << 40), 11, g);
   if (t < d.nranks && t != d.rank) {
@@ -1306,13 +1309,14 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
   __shared__ const vid_t* s_src[kern::kMaxPeers];
   __shared__ uint64_t s_cnt[kern::kMaxPeers];
+  __shared__ uint64_t s_xend[2 * kern::kMaxPeers];
   // a direct exchange: the peers' cells (their counts) first, live chain or
   // not (every rank waits for every exchange: the window slots' reuse protocol)
   const bool dx = a.direct.active;
   if (dx && direct_wait(a.direct, s_cnt, nullptr) != kWaitOk) return;
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
     // a folded level end is a collective: it runs on a no-op chain too
-    if (a.end.active && blockIdx.x == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin);
+    if (a.end.active && blockIdx.x == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin, s_xend);
     return;
   }
   const int t = threadIdx.x;
@@ -1382,7 +1386,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
   }
   if (!a.end.active) return;
   __syncthreads();
-  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin);
+  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
 }
 
 // ---------------------------------------------------------------------------
@@ -1982,13 +1986,79 @@ constexpr int kHubBuThreads = 1024;
 static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
 constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
 
-template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false>
+// The fused finish of a bottom-up level (BuArgs::fuse_scan; every thread of
+// the workgroup calls it): thread 0's workgroup totals (wc, wd) go to the
+// workgroup's slot of tot (agent-scope stores: no same-address atomics but
+// the ticket's), a ticket; the last workgroup sums the slots and finishes the
+// level (scan_finish) -- and runs the level's end when it is folded in
+// (a.end, several ranks).  s_c / s_d: kThreads / 64 LDS slots, reused; s_x:
+// LDS for the level end (the kernel's result words, written out by then).
+template <int kThreads, bool kEnd>
+__device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, long long wd, long long* s_c,
+                                                long long* s_d, uint64_t* s_x) {
+  constexpr int kWaves = kThreads / kWave;
+  __shared__ int s_last;
+  const int wave = static_cast<int>(threadIdx.x >> 6);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x), static_cast<unsigned long long>(wc),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
+                       static_cast<unsigned long long>(wd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+    s_last = prev == gridDim.x - 1;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  long long c = 0, d = 0;
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
+    c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i + 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  c = wave_sum(c);
+  d = wave_sum(d);
+  __syncthreads();  // (s_c / s_d reused)
+  if (lane_id() == 0) {
+    s_c[wave] = c;
+    s_d[wave] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long tc = 0, td = 0;
+    for (int k = 0; k < kWaves; ++k) {
+      tc += s_c[k];
+      td += s_d[k];
+    }
+    scan_finish(a.scan, tc, td);  // (resets the ticket)
+    s_c[0] = tc;
+    s_d[0] = td;
+  }
+  if constexpr (kEnd) {
+    __syncthreads();
+    direct_level_end(a.end, s_c[0], s_d[0], a.scan.stats, a.fin, s_x);
+  }
+}
+
+// kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
+// code costs the one-rank kernels their spill-free 64 registers).
+template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
   __shared__ unsigned long long s_q[kQ > 0 ? (kThreads / kWave) * kQ : 1];
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if constexpr (kEnd) {
+      if (blockIdx.x == 0)
+        direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin,
+                         reinterpret_cast<uint64_t*>(s_res));
+    }
+    return;
+  }
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   for (int64_t i = threadIdx.x; i < hw; i += kThreads) s_hub[i] = a.hub_front[i];
@@ -2022,51 +2092,14 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       }
     }
     if (!a.fuse_scan) return;
-    // fused finish: the workgroup's totals into its own slot of tot
-    // (agent-scope stores: no same-address atomics but the ticket's), a
-    // ticket; the last workgroup sums the slots and finishes the level
-    __shared__ int s_last;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      long long c = 0, d = 0;
+    long long wc = 0, wd = 0;
+    if (threadIdx.x == 0)
       for (int k = 0; k < kWavesPerBlock; ++k) {
-        c += s_c[k];
-        d += s_d[k];
+        wc += s_c[k];
+        wd += s_d[k];
       }
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x), static_cast<unsigned long long>(c),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
-                         static_cast<unsigned long long>(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned prev = atomicAdd(a.scan.ticket, 1u);
-      s_last = prev == gridDim.x - 1;
-      if (s_last) last_arriver_acquire();
-    }
-    __syncthreads();
-    if (!s_last) return;
-    long long c = 0, d = 0;
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
-      c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i + 1),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    c = wave_sum(c);
-    d = wave_sum(d);
-    __syncthreads();  // (s_c / s_d reused)
-    if (lane_id() == 0) {
-      s_c[wave] = c;
-      s_d[wave] = d;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      long long tc = 0, td = 0;
-      for (int k = 0; k < kWavesPerBlock; ++k) {
-        tc += s_c[k];
-        td += s_d[k];
-      }
-      scan_finish(a.scan, tc, td);  // (resets the ticket)
-    }
+    bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
     return;
   }
   // 16 words per wave: unit groups of 4 waves walk the units; every workgroup
@@ -2075,6 +2108,10 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   const int group = wave / kUnitWaves;
   const int wg = wave % kUnitWaves;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
+  // the unit groups' totals for the fused finish, in LDS (registers live
+  // across the loop would spill)
+  __shared__ long long s_acc[2 * kGroups];
+  if (threadIdx.x < 2 * kGroups) s_acc[threadIdx.x] = 0;
   for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
@@ -2097,9 +2134,20 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       }
       a.unit_cnt[u] = c;
       a.unit_deg[u] = d;
+      s_acc[2 * group] += c;
+      s_acc[2 * group + 1] += d;
     }
     __syncthreads();
   }
+  if (!a.fuse_scan) return;
+  __syncthreads();  // (an empty loop: the accumulators' zeroing)
+  long long wc = 0, wd = 0;
+  if (threadIdx.x == 0)
+    for (int g = 0; g < kGroups; ++g) {
+      wc += s_acc[2 * g];
+      wd += s_acc[2 * g + 1];
+    }
+  bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
 }
 
 // hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word;
@@ -2410,7 +2458,8 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
-    if (whole && a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
+    if (a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
+      DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the fused finish");
       // (more workgroups than totals slots: finish in a kernel of its own)
       BuArgs b = a;
       b.fuse_scan = false;
@@ -2418,29 +2467,28 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
       return;
     }
+    // (every hub kernel runs the fused finish itself; a folded level end is
+    // compiled only into the kEnd variants)
+#define DBFS_BU_LAUNCH(W, T, Q, R)                                                          \
+  do {                                                                                    \
+    if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);            \
+    else bu_hub_kernel<W, T, Q, R, false><<<grid, T, 0, st>>>(a);                        \
+  } while (0)
     if (whole) {
-      // (the whole-unit kernels run the fused finish themselves)
-      if (a.follow_up && rec)
-        bu_hub_kernel<true, kFollowThreads, kBuQueue, true><<<grid, kFollowThreads, 0, st>>>(a);
-      else if (a.follow_up)
-        bu_hub_kernel<true, kFollowThreads, kBuQueue><<<grid, kFollowThreads, 0, st>>>(a);
-      else if (rec)
-        bu_hub_kernel<true, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
-      else
-        bu_hub_kernel<true, kHubBuThreads, kBuQueue><<<grid, kHubBuThreads, 0, st>>>(a);
+      if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);
+      else if (a.follow_up) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, false);
+      else if (rec) DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, true);
+      else DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, false);
       return;
     }
-    if (a.follow_up && rec)
-      bu_hub_kernel<false, kHubBuThreads, 0, true><<<grid, kHubBuThreads, 0, st>>>(a);
-    else if (a.follow_up)
-      bu_hub_kernel<false, kHubBuThreads, 0><<<grid, kHubBuThreads, 0, st>>>(a);
-    else if (rec)
-      bu_hub_kernel<false, kHubBuThreads, kBuQueue, true><<<grid, kHubBuThreads, 0, st>>>(a);
-    else
-      bu_hub_kernel<false, kHubBuThreads, kBuQueue><<<grid, kHubBuThreads, 0, st>>>(a);
-    if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
+    if (a.follow_up && rec) DBFS_BU_LAUNCH(false, kHubBuThreads, 0, true);
+    else if (a.follow_up) DBFS_BU_LAUNCH(false, kHubBuThreads, 0, false);
+    else if (rec) DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, true);
+    else DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, false);
+#undef DBFS_BU_LAUNCH
     return;
   }
+  DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the hub kernels' fused finish");
   bu_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
   if (a.fuse_scan) totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a.scan);
 }
