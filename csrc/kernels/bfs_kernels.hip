@@ -316,13 +316,18 @@ __device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c
 
 // One wave per 64-word unit, kUnitsPerBlock units per workgroup; with the
 // fused finish a smaller grid strides over the units (fewer ticket arrivals).
+// kSplit waves per unit (small graphs: 4, each over 16 of its words -- a
+// graph of few units would leave most wave slots idle while each wave walks
+// its unit's new vertices 64 per dependent step); `sub` = this wave's part.
+template <int kSplit = 1>
 __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, bool use_bytes, long long& cnt,
-                                            long long& deg) {
+                                            long long& deg, int sub = 0) {
+  constexpr int kWords = kUnitWords / kSplit;
   const int lane = lane_id();
-  const int64_t w0 = unit * kUnitWords;
+  const int64_t w0 = unit * kUnitWords + sub * kWords;
   const int64_t wl = w0 + lane;
   word_t nb = 0;
-  if (wl < a.words) {
+  if (lane < kWords && wl < a.words) {
     word_t c = 0;
     if (use_bytes && a.level_direct) {
       c = gather_level_bits(a.level_direct + wl * 64, static_cast<uint8_t>(a.narrow_base + a.new_level));
@@ -360,12 +365,37 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
   }
   cnt = wave_sum(cnt);
   deg = wave_sum(deg);
-  if (lane == 0) {
+  if (kSplit == 1 && lane == 0) {
     a.unit_cnt[unit] = cnt;
     a.unit_deg[unit] = deg;
   }
 }
 
+// A unit per workgroup, its kSplit (= kUnitsPerBlock) waves each over a part
+// (update_unit<kSplit>); the unit's statistics summed in LDS.
+__device__ __forceinline__ void update_unit_split(const UpdateArgs& a, int64_t unit, bool use_bytes, long long& cnt,
+                                                  long long& deg, long long* s_pc, long long* s_pd) {
+  const int wv = static_cast<int>(threadIdx.x >> 6);
+  update_unit<kUnitsPerBlock>(a, unit, use_bytes, cnt, deg, wv);
+  if (lane_id() == 0) {
+    s_pc[wv] = cnt;
+    s_pd[wv] = deg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long c = 0, d = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitsPerBlock; ++k) {
+      c += s_pc[k];
+      d += s_pd[k];
+    }
+    a.unit_cnt[unit] = c;
+    a.unit_deg[unit] = d;
+  }
+  __syncthreads();  // (s_pc / s_pd reused by the next unit)
+}
+
+template <bool kSplit>
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
@@ -374,11 +404,18 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   }
   const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  __shared__ long long s_pc[kUnitsPerBlock], s_pd[kUnitsPerBlock];
   if (!a.fuse_scan) {
-    const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;
-    if (unit >= nunits) return;
     long long cnt, deg;
-    update_unit(a, unit, use_bytes, cnt, deg);
+    if constexpr (kSplit) {
+      const int64_t unit = blockIdx.x;
+      if (unit >= nunits) return;
+      update_unit_split(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
+    } else {
+      const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;
+      if (unit >= nunits) return;
+      update_unit(a, unit, use_bytes, cnt, deg);
+    }
     return;
   }
   // fused finish (as the whole-unit bottom-up kernel's): raw unit statistics,
@@ -387,12 +424,21 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   __shared__ long long s_c[kUnitsPerBlock], s_d[kUnitsPerBlock];
   __shared__ int s_last, s_level_last;  // (separate: waves read s_last while wave 0 decides the level)
   long long wc = 0, wd = 0;
-  for (int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; unit < nunits;
-       unit += static_cast<int64_t>(gridDim.x) * kUnitsPerBlock) {
-    long long cnt, deg;
-    update_unit(a, unit, use_bytes, cnt, deg);
-    wc += cnt;
-    wd += deg;
+  if constexpr (kSplit) {
+    for (int64_t unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
+      long long cnt, deg;
+      update_unit_split(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
+      wc += cnt;  // (this wave's part: the workgroup's totals are the waves' sum, as below)
+      wd += deg;
+    }
+  } else {
+    for (int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; unit < nunits;
+         unit += static_cast<int64_t>(gridDim.x) * kUnitsPerBlock) {
+      long long cnt, deg;
+      update_unit(a, unit, use_bytes, cnt, deg);
+      wc += cnt;
+      wd += deg;
+    }
   }
   if (lane_id() == 0) {
     s_c[wv] = wc;
@@ -632,19 +678,25 @@ __device__ __forceinline__ void wave_fill_blocks(int32_t* __restrict__ blk, bool
 // Frontier compaction: one wave per 64-word unit (lane l loads word l), 4
 // units per workgroup.  The unit's base slot and edge offset come from the
 // scan; each set bit's slot from mbcnt and its edge offset from a wave prefix
-// sum of degrees.
+// sum of degrees.  kSplit (graphs of few units): a unit per workgroup, 16
+// words per wave; a first pass counts each part's entries and edges, the
+// parts' bases are prefix-summed in LDS, and the second pass (row offsets now
+// cache hits) writes -- twice the passes, a quarter of the steps each.
+template <bool kSplit>
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
   stamp_level_start(a.ctrl);
+  constexpr int kWords = kSplit ? kWaveWords : kUnitWords;
   const int lane = lane_id();
-  const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock +
-                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
+  const int64_t unit = kSplit ? static_cast<int64_t>(blockIdx.x) : static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
-  if (unit >= nunits) return;
-  const int64_t w0 = unit * kUnitWords;
-  const word_t mine = (w0 + lane < a.words) ? a.frontier[w0 + lane] : 0ull;
-  if (a.clear_all && w0 + lane < a.words) a.clear_all[w0 + lane] = 0ull;
-  if (!__ballot(mine != 0)) return;
+  if (unit >= nunits) return;  // (split: the whole workgroup)
+  const int64_t w0 = unit * kUnitWords + (kSplit ? wv * kWaveWords : 0);
+  const bool in = lane < kWords && w0 + lane < a.words;
+  const word_t mine = in ? a.frontier[w0 + lane] : 0ull;
+  if (a.clear_all && in) a.clear_all[w0 + lane] = 0ull;
+  if (!kSplit && !__ballot(mine != 0)) return;
   if (a.clear && mine) a.clear[w0 + lane] = 0ull;  // read once: the next sparse level writes here
   const eid_t* __restrict__ ro = a.g.row_off;
   long long pos = a.unit_cnt_off[unit] + a.part_cnt[unit / kScanChunk];
@@ -653,6 +705,31 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
   // lane, whatever word they sit in), so the work-list order is unchanged.
   const int fincl = static_cast<int>(wave_incl_scan(__popcll(mine)));
   const int ftotal = __builtin_amdgcn_readlane(fincl, kWave - 1);
+  if constexpr (kSplit) {
+    __shared__ long long s_pc[kUnitsPerBlock], s_pd[kUnitsPerBlock];
+    long long pc = 0, pd = 0;
+    for (int base = 0; base < ftotal; base += kWave) {
+      const int idx = base + lane;
+      const int vpos = wave_set_position(mine, fincl, idx);
+      if (idx < ftotal) {
+        const int64_t v = w0 * 64 + vpos;
+        const eid_t d = ro[v + 1] - ro[v];
+        pc += d > 0 ? 1 : 0;
+        pd += d;
+      }
+    }
+    pc = wave_sum(pc);
+    pd = wave_sum(pd);
+    if (lane == 0) {
+      s_pc[wv] = pc;
+      s_pd[wv] = pd;
+    }
+    __syncthreads();
+    for (int k = 0; k < wv; ++k) {
+      pos += s_pc[k];
+      off += s_pd[k];
+    }
+  }
   for (int base = 0; base < ftotal; base += kWave) {
     const int idx = base + lane;
     const int vpos = wave_set_position(mine, fincl, idx);
@@ -2276,14 +2353,22 @@ void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStrea
   publish_stats_kernel<<<1, 64, 0, st>>>(stats, mb, seq);
 }
 
+// A graph of fewer units than kSplitUnits: a unit per workgroup, 16 words per
+// wave (update_unit_split, compact_split) -- 4x the waves, a quarter of the
+// dependent row_off steps each.
+constexpr int64_t kSplitUnits = 4096;
+
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  const bool split = nunits < kSplitUnits;
+  const int64_t per = split ? kUnitWords : kUnitWords * kUnitsPerBlock;
   // fused finish: at most kMaxFusedGrid / 8 workgroups striding over the units
   // with one ticket; up to kMaxFusedGrid with the two-level ticket
-  const unsigned grid = a.fuse_scan ? grid_for(a.words, kUnitWords * kUnitsPerBlock,
-                                               a.group_ticket ? kMaxFusedGrid : kMaxFusedGrid / 8)
-                                    : grid_for(a.words, kUnitWords * kUnitsPerBlock);
-  update_kernel<<<grid, kBlock, 0, st>>>(a);
+  const unsigned grid = a.fuse_scan ? grid_for(a.words, per, a.group_ticket ? kMaxFusedGrid : kMaxFusedGrid / 8)
+                                    : grid_for(a.words, per);
+  if (split) update_kernel<true><<<grid, kBlock, 0, st>>>(a);
+  else update_kernel<false><<<grid, kBlock, 0, st>>>(a);
 }
 
 void scan_units(const ScanArgs& a, hipStream_t st) {
@@ -2293,7 +2378,9 @@ void scan_units(const ScanArgs& a, hipStream_t st) {
 
 void compact_frontier(const CompactArgs& a, hipStream_t st) {
   if (a.words <= 0) return;
-  compact_kernel<<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if (nunits < kSplitUnits) compact_kernel<true><<<grid_for(a.words, kUnitWords), kBlock, 0, st>>>(a);
+  else compact_kernel<false><<<grid_for(a.words, kUnitWords * kUnitsPerBlock), kBlock, 0, st>>>(a);
 }
 
 #ifdef DBFS_TD_STATS
