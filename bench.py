@@ -364,6 +364,9 @@ def main(argv=None) -> int:
                 "directed_edges": bfs.engine.global_directed_edges,
             },
             "comm": rt.comm.name,
+            # peer transport: the kernels exchange owner lists and level ends
+            # themselves (its self-test passed on every rank)
+            "comm_direct": bool(getattr(rt.comm, "direct_on", False)),
             "comm_note": comm_note,
             "primary": primary,
             "comm_ranks": rt.comm.size,

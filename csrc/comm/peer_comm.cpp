@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -633,7 +634,42 @@ bool PeerComm::self_test(std::string* why) {
   const int64_t bad = inner_->sum_host(err.empty() ? 0 : 1);
   if (bad && err.empty()) err = "a peer's self-test failed";
   if (why) *why = err;
+  if (bad == 0) direct_self_test();
   return bad == 0;
+}
+
+// The direct exchanges (kernels writing into the peers' windows, tagged
+// cells): four rounds of known lists and level ends on every rank; a failure
+// anywhere (agreed) turns them off on every rank -- the engine then runs the
+// collectives -- instead of failing the communicator.
+void PeerComm::direct_self_test() {
+  if (!dtab_) return;
+  std::string err;
+  try {
+    DBuf<unsigned> e(*be_, 1);
+    be_->memset_async(e.data(), 0, sizeof(unsigned));
+    for (int round = 0; round < 4; ++round) {
+      DirectExchange l, x;
+      DBFS_CHECK(direct_lists(4100, &l) && direct_level_end(2, &x), "direct exchange unavailable");
+      const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
+      l.timeout_ticks = x.timeout_ticks = static_cast<uint64_t>(10.0 * khz * 1000.0);  // (10 s)
+      kern::direct_selftest(l, x, round, e.data(), S(be_));
+      HIP_CHECK(hipGetLastError());
+    }
+    unsigned h = 0;
+    be_->to_host(&h, e.data(), sizeof(h));  // (synchronises)
+    if (h) err = std::to_string(h) + " mismatches / timeouts";
+  } catch (const std::exception& ex) {
+    err = ex.what();
+  }
+  if (err_host_) __atomic_store_n(err_host_, uint64_t(0), __ATOMIC_RELEASE);  // (a timed-out wait's mark)
+  const int64_t bad = inner_->sum_host(err.empty() ? 0 : 1);
+  if (bad == 0) return;
+  if (rank_ == 0)
+    std::fprintf(stderr, "[dbfs] peer communicator: direct exchanges off (self-test: %s)\n",
+                 err.empty() ? "failed on a peer" : err.c_str());
+  hipFree(dtab_);
+  dtab_ = nullptr;
 }
 
 void PeerComm::barrier() {

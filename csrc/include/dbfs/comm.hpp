@@ -415,6 +415,8 @@ class PeerComm final : public Comm {
   // collectives issued through the windows / delegated to the inner communicator
   int64_t peer_ops() const { return peer_ops_; }
   int64_t inner_ops() const { return inner_ops_; }
+  // the direct exchanges are on (off: DBFS_PEER_DIRECT=0, or their self-test failed)
+  bool direct_on() const { return dtab_ != nullptr; }
 
  private:
   struct Piece {
@@ -437,6 +439,7 @@ class PeerComm final : public Comm {
     const LevelFinishArgs* finish = nullptr;  // then the level's decision (sum_count <= kPeerFinishMax)
   };
   void run(const Plan& plan);
+  void direct_self_test();  // (self_test's second part)
   std::shared_ptr<Bootstrap> boot_;
   bool ipc_ = true;                     // peers' windows IPC-mapped (closed on release)
   std::shared_ptr<char> win_keep_;      // in-process: own window, shared-owned by the group

@@ -1260,6 +1260,67 @@ __device__ __forceinline__ void direct_level_end(const DirectExchange& d, int64_
   level_finish_device(fin);
 }
 
+// PeerComm::self_test of the direct exchanges (one workgroup): rank r sends
+// peer p an owner list of (r + p + round) % 37 ids (+ 4000 in round 3) of a
+// known pattern, then a level end of known totals; every count, id and sum
+// checked against the pattern, mismatches counted in *err.
+__device__ __forceinline__ uint32_t selftest_id(int from, int to, uint32_t i, int round) {
+  return (static_cast<uint32_t>(from + 1) * 0x9E3779B9u) ^ (static_cast<uint32_t>(to + 7) << 20) ^ (i * 2654435761u) ^
+         static_cast<uint32_t>(round * 977);
+}
+__device__ __forceinline__ uint32_t selftest_n(int from, int to, int round) {
+  return static_cast<uint32_t>((from + to + round) % 37) + (round == 3 ? 4000u : 0u);
+}
+__global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, DirectExchange e, int round,
+                                                              unsigned* err) {
+  __shared__ uint64_t s_n[kern::kMaxPeers], s_x[2 * kern::kMaxPeers];
+  const int t = threadIdx.x;
+  const int me = l.rank, P = l.nranks;
+  for (int p = 0; p < P; ++p) {
+    if (p == me) continue;
+    const uint32_t n = selftest_n(me, p, round);
+    for (uint32_t i = t; i < n; i += 256) sys_store_u32(l.table->dst[p] + 1 + i, selftest_id(me, p, i, round));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < P && t != me) sys_store_u64(l.table->cell_out[t], cell_word0(l.seq, selftest_n(me, t, round)));
+  if (direct_wait(l, s_n, nullptr) != kWaitOk) {
+    if (t == 0) atomicAdd(err, 1000000u);
+    return;
+  }
+  unsigned bad = 0;
+  for (int p = 0; p < P; ++p) {
+    if (p == me) continue;
+    const uint32_t n = selftest_n(p, me, round);
+    if (t == 0 && s_n[p] != n) ++bad;
+    const uint32_t m = min(static_cast<uint32_t>(s_n[p]), n);
+    for (uint32_t i = t; i < m; i += 256)
+      if (sys_load_u32(l.table->src[p] + 1 + i) != selftest_id(p, me, i, round)) ++bad;
+  }
+  // a level end of known totals: rank r contributes (r + round, r << 30 | round)
+  const int64_t c = me + round, g = (static_cast<int64_t>(me) << 30) | round;
+  if (t < P && t != me) {
+    uint64_t* cell = e.table->cell_out[t];
+    sys_store_u64(cell, cell_word0(e.seq, static_cast<uint64_t>(c)));
+    sys_store_u64(cell + 1, cell_word1(e.seq, static_cast<uint64_t>(g)));
+  }
+  if (direct_wait(e, s_x, s_x + kern::kMaxPeers) != kWaitOk) {
+    if (t == 0) atomicAdd(err, 1000000u);
+    return;
+  }
+  if (t == 0) {
+    int64_t sc = c, sg = g, wc = 0, wg = 0;
+    for (int p = 0; p < P; ++p) {
+      sc += p == me ? 0 : static_cast<int64_t>(s_x[p]);
+      sg += p == me ? 0 : static_cast<int64_t>(s_x[kern::kMaxPeers + p]);
+      wc += p + round;
+      wg += (static_cast<int64_t>(p) << 30) | round;
+    }
+    if (sc != wc || sg != wg) ++bad;
+  }
+  if (bad) atomicAdd(err, bad);
+}
+
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
 // claimed vertex is finished in place (level, frontier bit, output entry), so
 // the level is one launch (one rank); with several ranks remote claims go to
@@ -2469,6 +2530,11 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+}
+
+void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
+                     hipStream_t st) {
+  direct_selftest_kernel<<<1, 256, 0, st>>>(lists, end, round, err);
 }
 
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {

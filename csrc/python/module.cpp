@@ -299,6 +299,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("slot_bytes", &PeerComm::slot_bytes)
       .def_property_readonly("peer_ops", &PeerComm::peer_ops)
       .def_property_readonly("inner_ops", &PeerComm::inner_ops)
+      .def_property_readonly("direct_on", &PeerComm::direct_on)
       .def("self_test", [](PeerComm& c) {
         std::string why;
         bool ok;

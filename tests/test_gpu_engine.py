@@ -841,6 +841,7 @@ def test_peer_comm_four_ranks_share_one_gpu_rmat20():
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["n_gpus"] == 4
+    assert rec["comm_direct"] is True  # (the direct exchanges passed their self-test on every rank)
     assert rec["validated"] is True and rec["validated_roots"] == "4/4"
 
 
@@ -941,4 +942,4 @@ def test_peer_direct_exchange_long_chain(tmp_path):
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
-    assert rec["comm"] == "peer+tcp" and rec["validated_roots"] == "3/3"
+    assert rec["comm"] == "peer+tcp" and rec["comm_direct"] is True and rec["validated_roots"] == "3/3"
