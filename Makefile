@@ -24,7 +24,7 @@ LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,
 HOST_SRC  := csrc/graph/io.cpp csrc/graph/csr.cpp csrc/backend/cpu_backend.cpp \
              csrc/backend/hip_backend.cpp csrc/comm/comm.cpp csrc/comm/nccl_comm.cpp \
              csrc/comm/tcp_bootstrap.cpp csrc/comm/peer_comm.cpp csrc/comm/replay_comm.cpp csrc/engine/engine.cpp csrc/graph/shard_reader.cpp
-HIP_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/graph_kernels.hip csrc/kernels/ref_kernels.hip \
+HIP_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/td_kernels.hip csrc/kernels/bu_kernels.hip csrc/kernels/graph_kernels.hip csrc/kernels/ref_kernels.hip \
              csrc/kernels/graph_sort.hip csrc/kernels/peer_kernels.hip
 
 HOST_OBJ  := $(patsubst csrc/%.cpp,$(BUILD)/%.o,$(HOST_SRC))
@@ -44,12 +44,13 @@ lib: $(CORE_LIB)
 # verified on the device; the first violation fails the run on the host,
 # HipBackend::take_device_check).  Host code and the other kernels unchanged.
 CHECKED_BUILD := build-checked
-CHECKED_OBJ   := $(CHECKED_BUILD)/kernels/bfs_kernels.o
+CHECKED_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/td_kernels.hip csrc/kernels/bu_kernels.hip
+CHECKED_OBJ   := $(patsubst csrc/%.hip,$(CHECKED_BUILD)/%.o,$(CHECKED_SRC))
 checked: bin/bfs_checked
-$(CHECKED_OBJ): csrc/kernels/bfs_kernels.hip $(HEADERS)
+$(CHECKED_BUILD)/%.o: csrc/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DDBFS_CHECKED -c $< -o $@
-bin/bfs_checked: $(BUILD)/cli/main.o $(HOST_OBJ) $(CHECKED_OBJ) $(filter-out $(BUILD)/kernels/bfs_kernels.o,$(HIP_OBJ))
+bin/bfs_checked: $(BUILD)/cli/main.o $(HOST_OBJ) $(CHECKED_OBJ) $(filter-out $(patsubst csrc/%.hip,$(BUILD)/%.o,$(CHECKED_SRC)),$(HIP_OBJ))
 	@mkdir -p bin
 	$(HIPCC) --offload-arch=$(ARCH) $^ -o $@ $(LDLIBS)
 

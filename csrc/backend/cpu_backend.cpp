@@ -338,12 +338,26 @@ class CpuBackend final : public Backend {
   void td_sparse(const TdSparseArgs& a) override {
     DBFS_CHECK(!a.direct.active, "CpuBackend: no direct list exchange (peer windows are GPU memory)");
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-    const int64_t q = a.dev_stats[0];
-    for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
+    // the input frontier's rows [col_begin, col_end), in work-list order (a
+    // bitmap input: its set bits in (word, bit) order, as a compaction lists them)
+    std::vector<std::pair<eid_t, eid_t>> rows;
+    if (a.from_bits) {
+      for (int64_t w = 0; w < a.words; ++w) {
+        for (word_t m = a.frontier_in[w]; m; m &= m - 1) {
+          const int64_t r = w * kWordBits + __builtin_ctzll(m);
+          rows.emplace_back(a.g.row_off[r], a.g.row_off[r + 1]);
+        }
+        a.frontier_in[w] = 0;
+      }
+    } else {
+      const int64_t q = a.dev_stats[0];
+      for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
+      for (int64_t i = 0; i < q; ++i) rows.emplace_back(a.qscan[i] + a.qbase[i], a.qscan[i + 1] + a.qbase[i]);
+    }
     sparse_cnt_ = sparse_deg_ = 0;
-    for (int64_t i = 0; i < q; ++i) {
-      for (int64_t k = a.qscan[i]; k < a.qscan[i + 1]; ++k) {
-        const vid_t v = a.g.col[k + a.qbase[i]];
+    for (const auto& [cb, ce] : rows) {
+      for (eid_t k = cb; k < ce; ++k) {
+        const vid_t v = a.g.col[k];
         if (test_bit(a.visited, v)) continue;
         a.visited[v >> 6] |= 1ull << (v & 63);
         const int64_t r = static_cast<int64_t>(v) - a.g.lo;

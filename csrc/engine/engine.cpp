@@ -68,6 +68,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
+  else if (name == "td_sparse_bits") o.td_sparse_bits = v != 0;
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
   else if (name == "td_group_ticket") o.td_group_ticket = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
@@ -110,6 +111,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
+          {"td_sparse_bits", o.td_sparse_bits ? 1.0 : 0.0},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
           {"td_group_ticket", o.td_group_ticket ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
@@ -546,7 +548,7 @@ FaultSpec FaultSpec::from_env() {
 }
 
 // Device-checked build: the first bounds violation a kernel recorded during
-// the traversal fails the run (codes: DBFS_DCHECK sites in bfs_kernels.hip).
+// the traversal fails the run (codes: DBFS_DCHECK sites in the {bfs,td,bu}_kernels.hip files).
 void Engine::check_device() {
   const uint64_t v = be_.take_device_check();
   if (v == 0) return;
@@ -1197,6 +1199,15 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   }
   // work-list set k (level L reads set L & 1; one set without sparse levels)
   auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
+  // two-level tickets (fused update finish, sparse levels read from a bitmap):
+  // zero between launches, each user re-zeroes what it took
+  auto group_tickets = [&]() {
+    if (!td_group_ticket_.data()) {
+      td_group_ticket_ = DBuf<uint32_t>(be_, static_cast<size_t>(kFusedGroups * kBuQueueStride));
+      be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
+    }
+    return td_group_ticket_.data();
+  };
   auto qbase_set = [&](int k) { return sparse && (k & 1) ? qbase2_.data() : qbase_.data(); };
   auto blk_set = [&](int k) { return sparse && (k & 1) ? blk_vstart2_.data() : blk_vstart_.data(); };
   // Mailbox stamps can be reset although the previous run did not end with a
@@ -1429,7 +1440,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       // after a bottom-up level the output bitmap is that level's input:
       // zeroed by the compaction (every other form leaves it clean)
       const bool compacted = pf == 'T' || pf == 'X' || pf == 'B';
-      if (compacted) compact(pf == 'B' ? fr_own(cur ^ 1) : nullptr);
+      // right after a bottom-up level: the kernel reads that level's output
+      // bitmap itself (no unit scan, no compaction); only the stale output
+      // bitmap is cleared first
+      const bool from_bits = pf == 'B' && opt_.td_sparse_bits;
+      if (from_bits) be_.memset_async(fr_own(cur ^ 1), 0, static_cast<size_t>(W) * sizeof(word_t));
+      else if (compacted) compact(pf == 'B' ? fr_own(cur ^ 1) : nullptr);
       TdSparseArgs sp;
       sp.g = gv;
       sp.qscan = qscan_set(L);
@@ -1456,8 +1472,13 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       sp.mailbox = mailbox_dev_ + slot(L);
       sp.level_index = L;
       sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
-      sp.first = !compacted;
+      sp.first = !compacted || from_bits;
       sp.max_mf = chain_cap;
+      if (from_bits) {
+        sp.from_bits = true;
+        sp.words = W;
+        sp.group_ticket = group_tickets();
+      }
       if (xc) {
         // remote claims to their owners' lists, the lists (count-sized) to
         // their owners, the received ids settled there; the totals go to
@@ -1625,11 +1646,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
         tu.tot = td_tot_.data();
         if (opt_.td_group_ticket) {
-          if (!td_group_ticket_.data()) {
-            td_group_ticket_ = DBuf<uint32_t>(be_, static_cast<size_t>(kFusedGroups * kBuQueueStride));
-            be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
-          }
-          tu.group_ticket = td_group_ticket_.data();
+          tu.group_ticket = group_tickets();
         }
         fused_scan = true;
       }

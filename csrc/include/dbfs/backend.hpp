@@ -450,6 +450,15 @@ struct TdSparseArgs {
   // live only while ctrl->m_f <= max_mf (0: any): a sparse chain enqueued for
   // a level that turns out large is a no-op and is re-enqueued dense
   int64_t max_mf = 0;
+  // from_bits (a level right after a bottom-up one): the input frontier is the
+  // bitmap frontier_in itself (`words` owned words, zeroed as read), not a
+  // work list -- no unit scan, no compaction; qscan / qbase / blk_vstart / qv /
+  // dev_stats are unused and frontier_out must be zero on entry.  The kernel's
+  // workgroups end on a two-level ticket (group_ticket: kFusedGroups tickets
+  // kBuQueueStride apart, zero between launches).
+  bool from_bits = false;
+  int64_t words = 0;
+  unsigned* group_ticket = nullptr;
   // Several ranks: every target is claimed in the replicated `visited`
   // (fetch-or); an owned one is finished here, a remote one appended to its
   // owner's list (lists + owner * list_stride: count, then the ids; wave-

@@ -203,6 +203,10 @@ struct EngineOptions {
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots).
   int64_t td_sparse_bu_edges = int64_t(1) << 18;
+  // ... and that level reads the bottom-up level's output bitmap itself
+  // (TdSparseArgs::from_bits: one kernel after a clear of its output bitmap,
+  // instead of scan_units + compact + td_sparse).
+  bool td_sparse_bits = true;
   // Device loop: a bottom-up level's unit scan (totals; one rank: direction
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.

@@ -1,0 +1,665 @@
+// gfx950 bottom-up kernels: the fused parent search (bu_kernel, and the
+// persistent hub-LDS variants bu_hub_kernel with deferred row scans and the
+// fused level finish) and the hub frontier gather.
+//
+// Reference counterpart: none -- the reference traverses top-down only
+// (queueBfs, bfs.cu:134-165; the status scan, bfs.cu:102-125); the
+// direction-optimising search follows Beamer et al.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <type_traits>
+
+#include "kernel_common.hpp"
+#include "launch.hpp"
+#include "level_device.hpp"
+#include "wave.hpp"
+
+namespace dbfs {
+namespace kern {
+namespace {
+
+// Sum (cnt, deg) of the 4 waves of a unit workgroup; thread 0 writes them.
+__device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, int64_t unit, int64_t* unit_cnt,
+                                                 int64_t* unit_deg) {
+  __shared__ long long s_c[kUnitWaves], s_d[kUnitWaves];
+  cnt = wave_sum(cnt);
+  deg = wave_sum(deg);
+  const int wv = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    s_c[wv] = cnt;
+    s_d[wv] = deg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long c = 0, d = 0;
+#pragma unroll
+    for (int k = 0; k < kUnitWaves; ++k) {
+      c += s_c[k];
+      d += s_d[k];
+    }
+    unit_cnt[unit] = c;
+    unit_deg[unit] = d;
+  }
+}
+
+// Rest of a bottom-up row after the head probe: phase 1, each unresolved lane
+// checks its next `lane_limit` neighbours (loads batched kBuBatch-wide);
+// phase 2, rows still unresolved are scanned by the whole wave, one row at a
+// time, 64 neighbours per step with a ballot early exit.  Wave-uniform call
+// (phase 2 is cooperative); returns the lane's `found`.
+// (Rejected, measured on RMAT-26 in rounds 1-2 and removed: phase 2 as one
+// packed multi-row edge stream -- 83 VGPRs, one workgroup per CU, 1238 ->
+// 1069 GTEPS; 2-8 phase-2 steps in flight -- 1231 -> 1225-1188; non-temporal
+// column loads; records prefetched two batches ahead.  Round 3: the wave's
+// unresolved rows as one flattened stream, 128 entries per round found by a
+// binary search over the rows' prefixes, per-row cap 4 x 4^round: coalesced
+// loads and no serial phase 2, yet late-switch first levels 672 / 889 ->
+// 700 / 875 us and the bench flat -- that level is bound by the ~44 M L2
+// misses of its column lines and global frontier probes, not by the scan's
+// round trips.)
+constexpr int kBuBatch = 4;  // phase-1 column loads in flight per lane
+
+// Deferred row-scan queue entries per wave (hub waves; 0 = scan in the
+// probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
+// (kMaxHubs / 8 B) and the 8 KiB result words, two workgroups per CU.
+constexpr int kBuQueue = 64;
+static_assert(kBuQueue <= kWave, "one queued row per lane per flush");
+
+#ifdef DBFS_BU_STATS
+// Diagnostic build only (-DDBFS_BU_STATS, tools/gpu_bu_stats.sh): wave-level
+// event counters of the bottom-up kernel, printed per dispatch by bu_step.
+__device__ unsigned long long g_bu_stats[8];
+#define BU_STAT(i, x)                                                   \
+  do {                                                                  \
+    const unsigned long long v_ = (x);                                  \
+    if (lane_id() == 0 && v_) atomicAdd(&g_bu_stats[i], v_);            \
+  } while (0)
+#else
+#define BU_STAT(i, x) \
+  do {                \
+  } while (0)
+#endif
+
+// Frontier test of a neighbour id that may be hub-encoded (kHub): hubs in the
+// LDS copy of their frontier bits, the rest in the global bitmap.
+template <bool kHub>
+__device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const word_t* s_hub, vid_t u) {
+  if constexpr (kHub) {
+    const vid_t hb = u & ~kHubFlag;
+    return (u & kHubFlag) ? ((s_hub[hb >> 6] >> (hb & 63)) & 1ull) : test_bit(fr, u);
+  } else {
+    return test_bit(fr, u);
+  }
+}
+
+// kNoVertex pads a phase-2 step's tail (never a vertex or a hub-encoded id:
+// ids < 2^31, hub codes < kHubFlag + kMaxHubs).
+constexpr vid_t kNoVertex = 0xFFFFFFFFu;
+
+template <bool kHub>
+__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, const word_t* s_hub) {
+  const int lane = lane_id();
+  // hub-encoded copy of the adjacency when present (kHub kernels only)
+  const vid_t* __restrict__ col = (kHub && a.g.hub_col) ? a.g.hub_col : a.g.col;
+  const word_t* __restrict__ fr = a.frontier;
+  // positions relative to the row start: 32-bit (a row never holds 2^32 entries)
+  const vid_t* __restrict__ row = col + rs;
+  const uint32_t len = static_cast<uint32_t>(e - rs);
+  uint32_t p = min(len, 1u);
+  const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
+  BU_STAT(3, __popcll(__ballot(p < lim && !found)));
+  while (p < lim && !found) {
+    BU_STAT(4, 1);
+    vid_t u[kBuBatch];
+    bool ok[kBuBatch];
+#pragma unroll
+    for (int k = 0; k < kBuBatch; ++k) {
+      ok[k] = p + k < lim;
+      u[k] = ok[k] ? row[p + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && bu_probe<kHub>(fr, s_hub, u[k]);
+    p += kBuBatch;
+  }
+  if (p > lim) p = lim;
+  // Phase 2: the wave scans each still-unresolved row in turn
+  unsigned long long pending = __ballot(!found && p < len);
+  BU_STAT(5, __popcll(pending));
+  while (pending) {
+    const int l = __ffsll(static_cast<long long>(pending)) - 1;
+    pending &= pending - 1;
+    const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
+    const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
+    bool f = false;
+    for (uint32_t base = ps; base < pe; base += kWave) {
+      BU_STAT(6, 1);
+      const uint32_t idx = base + lane;
+      const vid_t u = idx < pe ? r[idx] : kNoVertex;
+      if (__ballot(u != kNoVertex && bu_probe<kHub>(fr, s_hub, u))) {
+        f = true;
+        break;
+      }
+    }
+    if (lane == l) found = f;
+  }
+  return found;
+}
+
+// ---------------------------------------------------------------------------
+// Fused bottom-up step of one wave over kWords bitmap words from w0 (a whole
+// 64-word unit, or 16 words when the shard is too small to fill the chip
+// that way): the unvisited vertices of its words are numbered (per-word
+// popcount prefix) and processed 64 at a time, one per lane, whatever word
+// they sit in -- the per-step cost is a chain of dependent memory round trips
+// nearly independent of how many lanes are active, so steps =
+// ceil(unvisited / 64) instead of the words with any unvisited vertex.  Per
+// step: row bounds and head (prefetched one step ahead), head probe, then the
+// row scan.  Found bits are OR-ed into a per-wave LDS copy of the result words
+// (s_res), written out once with the visited update; levels and unit
+// statistics are written directly (no separate update pass).
+// kQueue > 0: rows whose head probe failed are not scanned in the step that
+// probed them (a handful of lanes per step, the rest idle through the scan's
+// dependent loads) but queued in LDS (s_q, kQueue entries of row offset
+// relative to the unit's first row / length / position) and scanned kQueue at
+// a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in
+// place.  kRec: row bounds and heads from the packed 8-byte records of the
+// non-empty-row view (ShardView::nz_rec).
+template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false>
+__device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, word_t* s_res, const word_t* s_hub,
+                                                long long& cnt, long long& deg, unsigned long long* s_q = nullptr) {
+  static_assert(kWords <= kWave, "one word per lane");
+  const int lane = lane_id();
+  const int64_t left = a.words - w0;
+  const int nw = left <= 0 ? 0 : (left < kWords ? static_cast<int>(left) : kWords);
+  // unvisited bits of word `lane` (0 past the words); visited = ~um
+  const word_t um = lane < nw ? ~a.visited[w0 + lane] : 0ull;
+  const int incl = static_cast<int>(wave_incl_scan(__popcll(um)));
+  const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  if (lane < kWords) s_res[lane] = 0ull;
+  if (total == 0) {
+    if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const vid_t* __restrict__ col = a.g.col;
+  const word_t* __restrict__ fr = a.frontier;
+  const vid_t* __restrict__ head = a.g.head;
+  const eid_t* __restrict__ nz_ro = (head && a.g.nz_pref && a.zdeg) ? a.g.nz_row_off : nullptr;
+  // packed records: the unit's base offset, span and end of its non-empty
+  // rows are wave-uniform (one unit per wave range)
+  // (kRec: the launcher checked that the view and its records exist)
+  const NzRec* __restrict__ nz_rec = kRec ? a.g.nz_rec : nullptr;
+  eid_t u_base = 0;
+  uint32_t u_span = 0;
+  int64_t u_nzend = 0;
+  if constexpr (kRec) {
+    // (readfirstlane: wave-uniform values in scalar registers)
+    const int64_t unit = w0 / kUnitWords;
+    const int64_t row_words = (a.g.rows + kWordBits - 1) / kWordBits;
+    u_base = static_cast<eid_t>(readlane64(static_cast<unsigned long long>(a.g.unit_base[unit]), 0));
+    u_span = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a.g.unit_base[unit + 1] - u_base)));
+    u_nzend = static_cast<int64_t>(readlane64(
+        static_cast<unsigned long long>(a.g.nz_pref[min((unit + 1) * kUnitWords, row_words)]), 0));
+  }
+  // Unvisited vertex number 64 b + lane -> its position loc = 64 j + bit in the
+  // wave's vertices (-1: no vertex), row bounds and head.
+  // (row start, 32-bit length) keep the prefetched state small: the hub
+  // kernel runs at 64 VGPRs (two 1024-thread workgroups per CU).
+  auto fetch = [&](int b, int& loc, eid_t& rs, uint32_t& len, vid_t& u) {
+    loc = -1;
+    rs = 0;
+    len = 0;
+    u = 0;
+    const int idx = b * kWave + lane;
+    if (b * kWave >= total) return;  // uniform
+    int j, bit;
+    if constexpr (kWords == kWave) {
+      const int p = wave_set_position(um, incl, idx);
+      j = p >> 6;
+      bit = p & 63;
+    } else {
+      // word j = number of words ending at or before idx; ex = where j starts
+      int ex = 0;
+      j = 0;
+      for (int i = 0; i < nw; ++i) {
+        const int end_i = __builtin_amdgcn_readlane(incl, i);
+        if (end_i <= idx) {
+          ++j;
+          ex = end_i;
+        }
+      }
+      j = min(j, nw - 1);
+      const word_t umj = static_cast<word_t>(__shfl(static_cast<long long>(um), j, kWave));
+      bit = select_bit(umj, idx - ex);
+    }
+    if (idx < total) {
+      loc = j * 64 + bit;
+      if (kRec || nz_ro) {
+        // dense non-empty-row view: rank = non-empty rows before the word +
+        // those below this bit (the word's prefix and zero-degree mask are
+        // L1-resident: every lane of the wave reads one of <= 16 words)
+        const int64_t k = a.g.nz_pref[w0 + j] + __popcll(~a.zdeg[w0 + j] & ((1ull << bit) - 1ull));
+        if constexpr (kRec) {
+          const NzRec r = nz_rec[k];
+          const uint32_t end = k + 1 < u_nzend ? nz_rec[k + 1].off : u_span;
+          rs = u_base + r.off;
+          len = end - r.off;
+          u = r.head;
+        } else {
+          rs = nz_ro[k];
+          len = static_cast<uint32_t>(nz_ro[k + 1] - rs);
+          u = a.g.nz_head[k];
+        }
+      } else {
+        const int64_t v = w0 * 64 + loc;
+        rs = ro[v];
+        len = static_cast<uint32_t>(ro[v + 1] - rs);
+        if (head) u = head[v];
+      }
+    }
+  };
+  const int nb = (total + kWave - 1) / kWave;
+  int n_loc;
+  eid_t n_rs;
+  uint32_t n_len;
+  vid_t n_u;
+  fetch(0, n_loc, n_rs, n_len, n_u);
+  if (!head) n_u = n_len ? col[n_rs] : 0u;
+  int cnt32 = 0;
+  // deferred row scans (kQueue): base = the unit's first row offset
+  eid_t q_base = 0;
+  bool q_span_ok = false;
+  int qn = 0;
+  if constexpr (kQueue > 0) {
+    // (the non-empty-row view covers ceil(rows / 64) words; a shard's bitmap
+    // slice may be longer -- padding words, all visited)
+    const int64_t wend = min(w0 + nw, (a.g.rows + kWordBits - 1) / kWordBits);
+    if constexpr (kRec) {
+      q_base = u_base;  // (every row of the unit starts at or after it; span < 2^32)
+      q_span_ok = true;
+    } else if (nz_ro) {
+      q_base = nz_ro[a.g.nz_pref[w0]];
+      q_span_ok = nz_ro[a.g.nz_pref[wend]] - q_base < (eid_t(1) << 32);
+    } else {
+      const int64_t vend = min(wend * 64, a.g.rows);
+      q_base = ro[w0 * 64];
+      q_span_ok = ro[vend] - q_base < (eid_t(1) << 32);
+    }
+  }
+  auto settle = [&](bool f, int l, eid_t r0, eid_t r1) {
+    if (f) {
+      store_level(a.level, a.level8, w0 * 64 + l, a.new_level, a.narrow_base);
+      cnt32 += 1;
+      deg += r1 - r0;
+      __hip_atomic_fetch_or(s_res + (l >> 6), 1ull << (l & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  };
+  // scan the queued rows, one per lane (wave-uniform)
+  auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int ql = 0;
+    eid_t qrs = 0, qe = 0;
+    if (lane < qn) {
+      const unsigned long long ent = s_q[lane];
+      ql = static_cast<int>(ent & 0xFFFu);
+      qrs = q_base + static_cast<eid_t>(ent >> 32);
+      qe = qrs + static_cast<eid_t>((ent >> 12) & 0xFFFFFu);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const bool f = bu_scan_row<kHub>(a, qrs, qe, lane >= qn, s_hub);
+    settle(lane < qn && f, ql, qrs, qe);
+    qn = 0;
+  };
+  for (int b = 0; b < nb; ++b) {
+    const int loc = n_loc;
+    const eid_t rs = n_rs, e = n_rs + n_len;
+    const vid_t u0 = n_u;
+    fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
+    bool found = false;
+    if (rs < e) found = bu_probe<kHub>(fr, s_hub, u0);
+    BU_STAT(0, 1);
+    BU_STAT(1, __popcll(__ballot(loc >= 0)));
+    BU_STAT(2, __popcll(__ballot(found)));
+    if (!head) n_u = n_len ? col[n_rs] : 0u;
+    if constexpr (kQueue > 0) {
+      // found by the head: settled now; unresolved rows with more neighbours
+      // are queued (huge rows / spans scanned in place)
+      const bool need = !found && e - rs > 1;
+      const bool fits = q_span_ok && e - rs < (eid_t(1) << 20);
+      // more unresolved rows than the queue holds (a sparse-hit level: most
+      // lanes scan anyway, deferring gains nothing): all in place
+      const bool direct = __popcll(__ballot(need && fits)) > kQueue;
+      const bool inplace = need && (direct || !fits);
+      if (__ballot(inplace)) {
+        // (lanes not scanned here pass as resolved and keep their result)
+        const bool f = bu_scan_row<kHub>(a, rs, e, found || !inplace, s_hub);
+        if (inplace) found = f;
+      }
+      settle(found, loc, rs, e);
+      const bool defer = need && !inplace;
+      const unsigned long long dm = __ballot(defer);
+      const int k = __popcll(dm);
+      if (qn + k > kQueue) flush();
+      if (defer)
+        s_q[qn + mask_rank(dm)] = (static_cast<unsigned long long>(rs - q_base) << 32) |
+                                  (static_cast<unsigned long long>(e - rs) << 12) | static_cast<unsigned>(loc);
+      qn += k;
+    } else {
+      found = bu_scan_row<kHub>(a, rs, e, found, s_hub);
+      BU_STAT(7, __popcll(__ballot(found)));
+      settle(found, loc, rs, e);
+    }
+  }
+  if constexpr (kQueue > 0) {
+    if (qn) flush();
+  }
+  cnt += cnt32;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < nw) {
+    const word_t res = s_res[lane];
+    a.new_frontier[w0 + lane] = res;
+    if (res) a.visited[w0 + lane] = ~um | res;
+  }
+}
+
+// Graphs without hubs: a wave per 16 words, 4 waves (one unit) per workgroup.
+__global__ __launch_bounds__(kUnitThreads) void bu_kernel(BuArgs a) {
+  __shared__ word_t s_res[kUnitWaves * kWaveWords];
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  stamp_level_start(a.ctrl);
+  long long cnt = 0, deg = 0;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnitWords + wave * kWaveWords;
+  bu_wave_compact<false>(a, w0, s_res + wave * kWaveWords, nullptr, cnt, deg);
+  unit_stats_store(cnt, deg, blockIdx.x, a.unit_cnt, a.unit_deg);
+}
+
+// Hub variant: persistent workgroups (two per CU) that first stage the hub
+// frontier bits (<= kMaxHubs bits, 64 KiB) in LDS; a hub-encoded head or
+// neighbour is then probed in LDS instead of by a scattered load of the
+// 8 MiB (RMAT-26) frontier bitmap -- at the dominant bottom-up level ~80% of
+// the unvisited vertices resolve at their head, ~85% of heads are hubs.
+// kWhole: one whole 64-word unit per wave (its statistics need no cross-wave
+// reduction, so waves run independently) -- chosen when the shard has enough
+// units to fill the chip that way (one GPU); small shards (many ranks) keep
+// 16 words per wave, four waves per unit, for parallelism.
+constexpr int kHubBuThreads = 1024;
+static_assert(kHubBuThreads % kUnitThreads == 0, "hub workgroups hold whole unit groups");
+constexpr int kHubWords = static_cast<int>(kMaxHubs / kWordBits);
+
+// The fused finish of a bottom-up level (BuArgs::fuse_scan; every thread of
+// the workgroup calls it): thread 0's workgroup totals (wc, wd) go to the
+// workgroup's slot of tot (agent-scope stores: no same-address atomics but
+// the ticket's), a ticket; the last workgroup sums the slots and finishes the
+// level (scan_finish) -- and runs the level's end when it is folded in
+// (a.end, several ranks).  s_c / s_d: kThreads / 64 LDS slots, reused; s_x:
+// LDS for the level end (the kernel's result words, written out by then).
+template <int kThreads, bool kEnd>
+__device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, long long wd, long long* s_c,
+                                                long long* s_d, uint64_t* s_x) {
+  constexpr int kWaves = kThreads / kWave;
+  __shared__ int s_last;
+  const int wave = static_cast<int>(threadIdx.x >> 6);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x), static_cast<unsigned long long>(wc),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
+                       static_cast<unsigned long long>(wd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.scan.ticket, 1u);
+    s_last = prev == gridDim.x - 1;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  long long c = 0, d = 0;
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
+    c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    d += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i + 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  c = wave_sum(c);
+  d = wave_sum(d);
+  __syncthreads();  // (s_c / s_d reused)
+  if (lane_id() == 0) {
+    s_c[wave] = c;
+    s_d[wave] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long tc = 0, td = 0;
+    for (int k = 0; k < kWaves; ++k) {
+      tc += s_c[k];
+      td += s_d[k];
+    }
+    scan_finish(a.scan, tc, td);  // (resets the ticket)
+    s_c[0] = tc;
+    s_d[0] = td;
+  }
+  if constexpr (kEnd) {
+    __syncthreads();
+    direct_level_end(a.end, s_c[0], s_d[0], a.scan.stats, a.fin, s_x);
+  }
+}
+
+// kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
+// code costs the one-rank kernels their spill-free 64 registers).
+template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false>
+__global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
+  __shared__ word_t s_hub[kHubWords];
+  __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
+  __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
+  __shared__ unsigned long long s_q[kQ > 0 ? (kThreads / kWave) * kQ : 1];
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if constexpr (kEnd) {
+      if (blockIdx.x == 0)
+        direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin,
+                         reinterpret_cast<uint64_t*>(s_res));
+    }
+    return;
+  }
+  if (!a.hub_front) stamp_level_start(a.ctrl);
+  const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
+  for (int64_t i = threadIdx.x; i < hw; i += kThreads) s_hub[i] = a.hub_front[i];
+  __syncthreads();
+  // (readfirstlane: the wave index, and the unit and word offsets derived
+  // from it, are wave-uniform -- scalar registers, not vector ones)
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  if constexpr (kWhole) {
+    constexpr int kWavesPerBlock = kThreads / kWave;
+    // (fused finish: this wave's totals accumulate in its LDS slots)
+    if (lane_id() == 0) {
+      s_c[wave] = 0;
+      s_d[wave] = 0;
+    }
+    // Static stride over the units.  (A dynamic unit queue measured slower:
+    // RMAT-26 per level 387 / 182 / 104 against 346 / 137 / 30 us -- the
+    // returning device-scope atomics cost more than the stride's imbalance.)
+    for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+         u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
+      long long cnt = 0, deg = 0;
+      bu_wave_compact<true, kUnitWords, kQ, kRec>(a, u * kUnitWords, s_res + wave * kUnitWords, s_hub, cnt, deg,
+                                                  s_q + wave * kQ);
+      cnt = wave_sum(cnt);
+      deg = wave_sum(deg);
+      if (lane_id() == 0) {
+        a.unit_cnt[u] = cnt;
+        a.unit_deg[u] = deg;
+        s_c[wave] += cnt;
+        s_d[wave] += deg;
+      }
+    }
+    if (!a.fuse_scan) return;
+    __syncthreads();
+    long long wc = 0, wd = 0;
+    if (threadIdx.x == 0)
+      for (int k = 0; k < kWavesPerBlock; ++k) {
+        wc += s_c[k];
+        wd += s_d[k];
+      }
+    bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
+    return;
+  }
+  // 16 words per wave: unit groups of 4 waves walk the units; every workgroup
+  // runs the same number of iterations (barriers stay uniform)
+  constexpr int kGroups = kThreads / kUnitThreads;
+  const int group = wave / kUnitWaves;
+  const int wg = wave % kUnitWaves;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
+  // the unit groups' totals for the fused finish, in LDS (registers live
+  // across the loop would spill)
+  __shared__ long long s_acc[2 * kGroups];
+  if (threadIdx.x < 2 * kGroups) s_acc[threadIdx.x] = 0;
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
+    const int64_t u = base + group;
+    long long cnt = 0, deg = 0;
+    if (u < nunits)
+      bu_wave_compact<true, kWaveWords, kQ, kRec>(a, u * kUnitWords + wg * kWaveWords, s_res + wave * kWaveWords, s_hub,
+                                                  cnt, deg, s_q + wave * kQ);
+    cnt = wave_sum(cnt);
+    deg = wave_sum(deg);
+    if (lane_id() == 0) {
+      s_c[wave] = cnt;
+      s_d[wave] = deg;
+    }
+    __syncthreads();
+    if ((threadIdx.x & (kUnitThreads - 1)) == 0 && u < nunits) {
+      long long c = 0, d = 0;
+#pragma unroll
+      for (int k = 0; k < kUnitWaves; ++k) {
+        c += s_c[group * kUnitWaves + k];
+        d += s_d[group * kUnitWaves + k];
+      }
+      a.unit_cnt[u] = c;
+      a.unit_deg[u] = d;
+      s_acc[2 * group] += c;
+      s_acc[2 * group + 1] += d;
+    }
+    __syncthreads();
+  }
+  if (!a.fuse_scan) return;
+  __syncthreads();  // (an empty loop: the accumulators' zeroing)
+  long long wc = 0, wd = 0;
+  if (threadIdx.x == 0)
+    for (int g = 0; g < kGroups; ++g) {
+      wc += s_acc[2 * g];
+      wd += s_acc[2 * g + 1];
+    }
+  bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
+}
+
+// hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word;
+// several ranks: then the whole grid merges the frontier into visited.
+__global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  stamp_level_start(a.ctrl);
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int64_t h = w * kWave + lane_id();
+  const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);
+  const word_t m = __ballot(bit);
+  if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
+  if (a.visited) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.words; i += stride) {
+      const word_t f = a.frontier[i];
+      if (f) a.visited[i] |= f;
+    }
+  }
+}
+
+}  // namespace
+
+#ifdef DBFS_BU_STATS
+static void bu_stats_report(hipStream_t st) {
+  unsigned long long h[8] = {0};
+  (void)hipStreamSynchronize(st);
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bu_stats), sizeof(h));
+  const unsigned long long z[8] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bu_stats), z, sizeof(z));
+  if (h[0])
+    std::fprintf(stderr,
+                 "[bu-stats] batches %llu active-lanes %llu head-found %llu p1-lanes %llu p1-iters %llu "
+                 "p2-rows %llu p2-steps %llu found %llu\n",
+                 h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+}
+#endif
+
+void bu_step(const BuArgs& a, hipStream_t st) {
+#ifdef DBFS_BU_STATS
+  struct Report {
+    hipStream_t st;
+    ~Report() { bu_stats_report(st); }
+  } report{st};
+#endif
+  if (a.words <= 0) return;
+  if (a.g.nhubs > 0 && a.hub_front) {
+    const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+    // a whole 64-word unit per wave when the shard has enough units to fill
+    // every resident wave slot (one GPU); small shards (many ranks) keep 16
+    // words per wave for parallelism
+    const int64_t slots = 2 * static_cast<int64_t>(device_cus()) * (kHubBuThreads / kWave);
+    const bool whole = a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots);
+    // a bottom-up level after another one (few unvisited vertices left, most
+    // of them scanning rows): whole units in 768-thread workgroups (80 VGPRs
+    // instead of 64); 16-word waves without the row queue (measured)
+    constexpr int kFollowThreads = 768;
+    const int threads = whole ? (a.follow_up ? kFollowThreads : kHubBuThreads) : kHubBuThreads;
+    const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
+    // packed row records (compile-time path: the view's fallback costs registers)
+    const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
+    if (a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
+      DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the fused finish");
+      // (more workgroups than totals slots: finish in a kernel of its own)
+      BuArgs b = a;
+      b.fuse_scan = false;
+      bu_step(b, st);
+      totals_finish(a.scan, st);
+      return;
+    }
+    // (every hub kernel runs the fused finish itself; a folded level end is
+    // compiled only into the kEnd variants)
+#define DBFS_BU_LAUNCH(W, T, Q, R)                                                          \
+  do {                                                                                    \
+    if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);            \
+    else bu_hub_kernel<W, T, Q, R, false><<<grid, T, 0, st>>>(a);                        \
+  } while (0)
+    if (whole) {
+      if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);
+      else if (a.follow_up) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, false);
+      else if (rec) DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, true);
+      else DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, false);
+      return;
+    }
+    if (a.follow_up && rec) DBFS_BU_LAUNCH(false, kHubBuThreads, 0, true);
+    else if (a.follow_up) DBFS_BU_LAUNCH(false, kHubBuThreads, 0, false);
+    else if (rec) DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, true);
+    else DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, false);
+#undef DBFS_BU_LAUNCH
+    return;
+  }
+  DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the hub kernels' fused finish");
+  bu_kernel<<<grid_for(a.words, kUnitWords), kUnitThreads, 0, st>>>(a);
+  if (a.fuse_scan) totals_finish(a.scan, st);
+}
+
+void hub_gather(const HubGatherArgs& a, hipStream_t st) {
+  if (a.g.nhubs <= 0) return;
+  unsigned grid = grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave);
+  if (a.visited) grid = std::max(grid, grid_for(a.words, kBlock, 2048));
+  hub_gather_kernel<<<grid, kBlock, 0, st>>>(a);
+}
+
+unsigned long long take_check_bu() { return take_check_local(); }
+
+}  // namespace kern
+}  // namespace dbfs

@@ -8,7 +8,7 @@
 namespace dbfs {
 namespace kern {
 
-// bfs_kernels.hip
+// bfs_kernels.hip, td_kernels.hip, bu_kernels.hip
 void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st);
 void set_bit(word_t* bm, int64_t bit, hipStream_t st);
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st);

@@ -1,0 +1,1156 @@
+// gfx950 top-down kernels: edge-balanced expansion (td_expand), one-kernel
+// sparse levels from a work list or straight from a bottom-up level's bitmap
+// (td_sparse, td_sparse_bits), the owners' side of the owner-list exchange
+// (td_sparse_apply, direct exchanges and their self-test), binned levels
+// (propagation blocking) and the top-down hub marks.
+//
+// Reference counterpart: queueBfs (bfs.cu:134-165), a thread per frontier
+// vertex walking its row serially with an atomicMin claim per edge.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <type_traits>
+
+#include "kernel_common.hpp"
+#include "launch.hpp"
+#include "level_device.hpp"
+#include "wave.hpp"
+
+namespace dbfs {
+namespace kern {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Edge-balanced top-down expansion.  Workgroup b owns frontier edges
+// [b*EPB, (b+1)*EPB).  The entries covering that range are [blk_vstart[b],
+// blk_vstart[b+1]]; their start positions are scattered into an LDS owner map
+// and max-scanned so every edge finds its entry with one LDS read.  col[] is
+// then read in 256-lane coalesced sweeps.  A discovered vertex costs one
+// atomicOr only if neither `visited` nor the (possibly stale, only-growing)
+// `next` word already has its bit.
+enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->bytes
+
+// Work-list owner map of edge block b (edges [b*EPB, min(m, (b+1)*EPB))):
+// the entries covering the block are [blk_vstart[b], blk_vstart[b+1]]; their
+// start positions are scattered into s_owner and max-scanned, so s_owner[i]
+// is the block-local entry of edge i and s_base[entry] its qbase (col index =
+// edge + qbase).  Returns the block's edge count; ends with a barrier.
+// BaseT uint32_t: qbase kept modulo 2^32 (enough while the column array has
+// at most 2^32 entries: the column index is then (edge + qbase) mod 2^32).
+template <int kThreads, typename BaseT = long long>
+__device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qscan, const int64_t* __restrict__ qbase,
+                                                  const int32_t* __restrict__ blk_vstart, long long b,
+                                                  long long nblocks, long long q, long long m, int32_t* s_owner,
+                                                  BaseT* s_base, int32_t* s_wmax) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = t >> 6;
+  const long long e0 = b * kTdEdgesPerBlock;
+  const long long e1 = min(m, e0 + kTdEdgesPerBlock);
+  const int cnt = static_cast<int>(e1 - e0);
+  const long long v0 = blk_vstart[b];
+  const long long vlast = (b + 1 < nblocks) ? blk_vstart[b + 1] : q - 1;
+  const int nv = static_cast<int>(vlast - v0 + 1);
+
+  __syncthreads();  // LDS reuse across iterations
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
+  __syncthreads();
+  // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
+  for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
+    const long long qs = qscan[v0 + i];
+    s_base[i] = static_cast<BaseT>(qbase[v0 + i]);
+    const long long p = (qs > e0 ? qs : e0) - e0;
+    if (p < cnt) s_owner[p] = i;
+  }
+  __syncthreads();
+  // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
+  int vals[kItems];
+  int run = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    run = max(run, s_owner[t * kItems + k]);
+    vals[k] = run;
+  }
+  const int incl = wave_incl_max(run);
+  if (lane == kWave - 1) s_wmax[wv] = incl;
+  __syncthreads();
+  int carry = 0;
+  for (int k = 0; k < wv; ++k) carry = max(carry, s_wmax[k]);
+  const int prev = __shfl_up(incl, 1, kWave);
+  const int excl = lane > 0 ? max(carry, prev) : carry;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
+  __syncthreads();
+  return cnt;
+}
+
+// kThreads: 256 (8 edges per thread) for big levels; 1024 (2 per thread) when
+// the grid is too small to fill the chip -- 4x the waves in flight to cover the
+// latency of the scattered loads/atomics.  The grid may be smaller than the
+// number of edge blocks (device loop: fixed grid): workgroups stride over them.
+#ifdef DBFS_TD_STATS
+// Diagnostic build only (-DDBFS_TD_STATS): per-dispatch top-down counters
+// (live edges, hub targets decoded unvisited, direct stores, filter on).
+__device__ unsigned long long g_td_stats[4];
+#define TD_STAT(i, x)                                              \
+  do {                                                             \
+    const unsigned long long v_ = (x);                             \
+    if (lane_id() == 0 && v_) atomicAdd(&g_td_stats[i], v_);       \
+  } while (0)
+#else
+#define TD_STAT(i, x) \
+  do {                \
+  } while (0)
+#endif
+
+// kFilter: the hub-filter variant (kTdMaxHubs / 8 bytes more LDS --
+// launched only for levels that may use it).  kBase32: the owner map's column
+// bases in 32 bits (graphs of at most 2^32 adjacency entries): 16 instead of
+// 24 KiB of LDS per workgroup, 8 resident workgroups per CU instead of 6 (5
+// instead of 4 with the filter).
+template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false>
+__global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
+  using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
+  __shared__ int32_t s_owner[kTdEdgesPerBlock];
+  __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_wmax[kThreads / kWave];
+  __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
+  long long q = a.q, m = a.m;
+  bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
+  if (a.ctrl) {
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    bytes = a.ctrl->bytes != 0;
+    check = a.ctrl->check_visited != 0;
+    q = a.dev_stats[0];
+    m = a.dev_stats[1];
+    if (a.clear_qv) stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
+    if (a.clear_qv)
+      for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < q;
+           i += static_cast<int64_t>(gridDim.x) * kThreads)
+        a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
+  }
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const word_t* __restrict__ visited = a.visited;
+  // large levels: hub targets tested in an LDS copy of the hubs' visited bits
+  // (uniform: every workgroup sees the same m)
+  bool filter = false;
+  if constexpr (kHubFilter) {
+    filter = a.td_hub_vis && a.g.td_col && m >= a.td_hub_min_edges && blockIdx.x < nblocks &&
+             (!a.ctrl || static_cast<double>(a.ctrl->vis_deg) >= a.td_hub_vis_frac * a.ctrl->total_directed);
+    if (filter) {
+      const int64_t hw = (a.g.td_nhubs + kWordBits - 1) / kWordBits;
+      for (int64_t i = t; i < hw; i += kThreads) s_hubvis[i] = a.td_hub_vis[i];
+      // (td_block_owner_map starts with a barrier)
+    }
+  }
+  const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
+
+  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const int cnt = td_block_owner_map<kThreads, BaseT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
+                                                        s_base, s_wmax);
+
+    // All items' loads in flight together (column ids, then their visited /
+    // next words), then the stores: the items of a thread are independent, but
+    // the compiler cannot move a load above an earlier item's atomic, so one
+    // item at a time costs kItems dependent round trips per block.
+    vid_t vk[kItems];
+    bool live[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kThreads + t;
+      int64_t ci;
+      if constexpr (kBase32)
+        ci = static_cast<uint32_t>(static_cast<uint32_t>(e0 + idx) + s_base[s_owner[idx]]);
+      else
+        ci = e0 + idx + s_base[s_owner[idx]];
+      vk[k] = idx < cnt ? col[ci] : 0u;
+      live[k] = idx < cnt;
+    }
+    // hub targets tested in the LDS snapshot: a visited hub is done here; an
+    // unvisited one is decoded and needs no global visited probe (unvisited
+    // at the level's start).  (Measured: claiming hubs in LDS as well, to
+    // store each once per workgroup, is slower -- few repeats per workgroup,
+    // LDS atomics on popular hubs serialise.)
+    bool hubnew[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) hubnew[k] = false;
+    if constexpr (kHubFilter) {
+      if (filter) {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          if (live[k] && (vk[k] & kHubFlag)) {
+            const vid_t h = vk[k] & ~kHubFlag;
+            if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) {
+              live[k] = false;
+            } else if (a.td_hub_mark) {
+              a.td_hub_mark[h] = 1;  // claimed; hub_apply stores its level byte
+              live[k] = false;
+            } else {
+              vk[k] = a.g.td_hub_vertex[h];
+              hubnew[k] = true;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
+      TD_STAT(0, __popcll(__ballot(live[k])));
+      TD_STAT(1, __popcll(__ballot(hubnew[k])));
+    }
+    TD_STAT(3, filter && t == 0 && b == blockIdx.x ? 1 : 0);
+    if constexpr (kOut != TdOut::Lists) {
+      if (!bytes) {
+        word_t seen[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          seen[k] = live[k] ? (hubnew[k] ? 0ull : (visited[vk[k] >> 6] | a.next[vk[k] >> 6])) : ~0ull;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+          const word_t bit = 1ull << (vk[k] & 63);
+          if (!(seen[k] & bit)) atomicOr(a.next + (vk[k] >> 6), bit);
+        }
+        continue;
+      }
+      if (a.level_direct) {
+        // the level itself, for unreached candidates only: the level byte is
+        // read instead of the visited bit (a reached vertex -- earlier level,
+        // or claimed at this one -- reads something other than unreached), so
+        // a target hit by many edges is stored about once instead of once per
+        // edge (stores cost more than reads; a stale read in another XCD's L2
+        // only repeats the same store)
+        // The candidate's visited bit is tested (measured, RMAT-22 top-down
+        // only: 65.0 GTEPS, against 60.0 testing the level byte, 58.0 both,
+        // 55.3 with claims in `next`; the 43 M-edge level stores 29.8 M level
+        // bytes for ~2 M new vertices, and removing the repeats with extra
+        // reads costs more L2 requests than the writes, tools/gpu_td_stats_roots.sh).
+        const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
+        bool keep[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          if (keep[k]) a.level_direct[vk[k]] = lv;
+        continue;
+      }
+      // byte map: with few visited vertices the check costs more than the
+      // store it saves (random loads ~120 G/s vs byte stores ~88 G/s on
+      // MI355X); the consuming update masks with ~visited anyway.  A byte
+      // already marked is not stored again (RMAT rows repeat the same hubs,
+      // and a read hit is cheaper than a byte write).
+      bool keep[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k)
+        keep[k] = live[k] && (hubnew[k] || !check || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
+      uint8_t mark[kItems];
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) mark[k] = keep[k] ? a.next_bytes[vk[k]] : 1;
+#pragma unroll
+      for (int k = 0; k < kItems; ++k)
+        if (!mark[k]) a.next_bytes[vk[k]] = 1;
+      continue;
+    }
+    bool actk[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      actk[k] = k * kThreads + t < cnt && !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63)));
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      if constexpr (kOut == TdOut::Lists) {
+        // wave-aggregated append to the owner lists (uniform loop over owners)
+        const vid_t v = vk[k];
+        const bool act = actk[k];
+        const int owner = act ? static_cast<int>(v / a.part) : -1;
+        unsigned long long pending = __ballot(act);
+        while (pending) {
+          const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+          const int o = __shfl(owner, leader, kWave);
+          const unsigned long long msk = __ballot(owner == o);
+          unsigned base = 0;
+          vid_t* list = a.lists + static_cast<int64_t>(o) * (a.list_cap + 1);
+          if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
+          base = __shfl(base, leader, kWave);
+          DBFS_DCHECK(base + __popcll(msk) <= static_cast<unsigned long long>(a.list_cap), 3, base);
+          if (owner == o) list[1 + base + mask_rank(msk)] = v;
+          pending &= ~msk;
+        }
+      }
+    }
+  }
+}
+
+// The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
+// of this shard): level, frontier bit, and the wave's work-list entries of
+// the next level with one packed atomic (count << kSparseEdgeBits | edges)
+// for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
+template <int kItems>
+__device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
+  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
+  if (!__ballot(claimed != 0)) return;
+  const int lane = lane_id();
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const int64_t lo = a.g.lo;
+  eid_t rs[kItems], re[kItems];
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    rs[k] = re[k] = 0;
+    if (claimed & (1u << k)) {
+      const int64_t r = static_cast<int64_t>(v[k]) - lo;
+      DBFS_DCHECK(r >= 0 && r < a.g.rows, 10, v[k]);
+      store_level(a.level, a.level8, r, a.new_level, a.narrow_base);
+      rs[k] = ro[r];
+      re[k] = ro[r + 1];
+    }
+  }
+  unsigned long long tm[kItems];
+  long long incl[kItems], cbase[kItems], ebase[kItems];
+  long long ctot = 0, etot = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const long long d = static_cast<long long>(re[k] - rs[k]);
+    const bool take = d > 0;  // claimed (else rs == re)
+    tm[k] = __ballot(take);
+    if (take) {
+      const int64_t r = static_cast<int64_t>(v[k]) - lo;
+      atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
+    }
+    incl[k] = wave_incl_scan(take ? d : 0ll);
+    cbase[k] = ctot;
+    ebase[k] = etot;
+    ctot += __popcll(tm[k]);
+    etot += readlane_i64(incl[k], kWave - 1);
+  }
+  if (!ctot) return;
+  unsigned long long old = 0;
+  if (lane == 0)
+    old = atomicAdd(a.counter, (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
+                                   static_cast<unsigned long long>(etot));
+  old = __shfl(old, 0, kWave);
+  const long long p0 = static_cast<long long>(old >> kSparseEdgeBits);
+  const long long q0 = static_cast<long long>(old & kEdgeMask);
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const long long d = static_cast<long long>(re[k] - rs[k]);
+    const long long p = p0 + cbase[k] + mask_rank(tm[k]);
+    const long long qs = q0 + ebase[k] + incl[k] - d;
+    DBFS_DCHECK(d <= 0 || p < a.g.rows, 4, p);
+    if (d > 0) {
+      a.oscan[p] = qs;
+      a.obase[p] = rs[k] - qs;
+      a.oqv[p] = static_cast<vid_t>(static_cast<int64_t>(v[k]) - lo);
+    }
+    wave_fill_blocks(a.oblk, d > 0, qs, d, p);
+  }
+}
+
+// The level's local totals from the packed counter (one thread of the last
+// workgroup): stats, the work list's end marker, counter and ticket reset.
+__device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg) {
+  constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
+  const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  cnt = static_cast<long long>(tot >> kSparseEdgeBits);
+  deg = static_cast<long long>(tot & kEdgeMask);
+  *a.counter = 0ull;
+  *a.ticket = 0u;
+  a.stats[0] = a.stats[2] = cnt;
+  a.stats[1] = a.stats[3] = deg;
+  a.oscan[cnt] = deg;
+}
+
+// PeerComm::self_test of the direct exchanges (one workgroup): rank r sends
+// peer p an owner list of (r + p + round) % 37 ids (+ 4000 in round 3) of a
+// known pattern, then a level end of known totals; every count, id and sum
+// checked against the pattern, mismatches counted in *err.
+__device__ __forceinline__ uint32_t selftest_id(int from, int to, uint32_t i, int round) {
+  return (static_cast<uint32_t>(from + 1) * 0x9E3779B9u) ^ (static_cast<uint32_t>(to + 7) << 20) ^ (i * 2654435761u) ^
+         static_cast<uint32_t>(round * 977);
+}
+__device__ __forceinline__ uint32_t selftest_n(int from, int to, int round) {
+  return static_cast<uint32_t>((from + to + round) % 37) + (round == 3 ? 4000u : 0u);
+}
+__global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, DirectExchange e, int round,
+                                                              unsigned* err) {
+  __shared__ uint64_t s_n[kern::kMaxPeers], s_x[2 * kern::kMaxPeers];
+  const int t = threadIdx.x;
+  const int me = l.rank, P = l.nranks;
+  for (int p = 0; p < P; ++p) {
+    if (p == me) continue;
+    const uint32_t n = selftest_n(me, p, round);
+    for (uint32_t i = t; i < n; i += 256) sys_store_u32(l.table->dst[p] + 1 + i, selftest_id(me, p, i, round));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < P && t != me) sys_store_u64(l.table->cell_out[t], cell_word0(l.seq, selftest_n(me, t, round)));
+  if (direct_wait(l, s_n, nullptr) != kWaitOk) {
+    if (t == 0) atomicAdd(err, 1000000u);
+    return;
+  }
+  unsigned bad = 0;
+  for (int p = 0; p < P; ++p) {
+    if (p == me) continue;
+    const uint32_t n = selftest_n(p, me, round);
+    if (t == 0 && s_n[p] != n) ++bad;
+    const uint32_t m = min(static_cast<uint32_t>(s_n[p]), n);
+    for (uint32_t i = t; i < m; i += 256)
+      if (sys_load_u32(l.table->src[p] + 1 + i) != selftest_id(p, me, i, round)) ++bad;
+  }
+  // a level end of known totals: rank r contributes (r + round, r << 30 | round)
+  const int64_t c = me + round, g = (static_cast<int64_t>(me) << 30) | round;
+  if (t < P && t != me) {
+    uint64_t* cell = e.table->cell_out[t];
+    sys_store_u64(cell, cell_word0(e.seq, static_cast<uint64_t>(c)));
+    sys_store_u64(cell + 1, cell_word1(e.seq, static_cast<uint64_t>(g)));
+  }
+  if (direct_wait(e, s_x, s_x + kern::kMaxPeers) != kWaitOk) {
+    if (t == 0) atomicAdd(err, 1000000u);
+    return;
+  }
+  if (t == 0) {
+    int64_t sc = c, sg = g, wc = 0, wg = 0;
+    for (int p = 0; p < P; ++p) {
+      sc += p == me ? 0 : static_cast<int64_t>(s_x[p]);
+      sg += p == me ? 0 : static_cast<int64_t>(s_x[kern::kMaxPeers + p]);
+      wc += p + round;
+      wg += (static_cast<int64_t>(p) << 30) | round;
+    }
+    if (sc != wc || sg != wg) ++bad;
+  }
+  if (bad) atomicAdd(err, bad);
+}
+
+// Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
+// claimed vertex is finished in place (level, frontier bit, output entry), so
+// the level is one launch (one rank); with several ranks remote claims go to
+// their owners' lists and td_sparse_apply finishes the level after the
+// exchange.  kThreads = 256: 8 edges per thread per block.
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  __shared__ int32_t s_owner[kTdEdgesPerBlock];
+  __shared__ long long s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_wmax[kThreads / kWave];
+  __shared__ int s_last;
+  const bool dx = a.lists && a.direct.active;
+  // uniform: the whole grid returns, no workgroup takes a ticket (a direct
+  // exchange still publishes, empty)
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    if (dx && blockIdx.x == 0) direct_publish(a.direct, a.lists, a.list_stride, false);
+    return;
+  }
+  if (a.first) stamp_level_start(a.ctrl);
+  const long long q = a.dev_stats[0], m = a.dev_stats[1];
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  // Only the workgroups that have an edge block take part (at least one, for
+  // the finish): the others return before the ticket -- on a level of a few
+  // blocks, 256 workgroups queueing on one ticket address cost several us.
+  const unsigned active = static_cast<unsigned>(nblocks < 1 ? 1 : (nblocks < gridDim.x ? nblocks : gridDim.x));
+  if (blockIdx.x >= active) return;
+  const int t = threadIdx.x;
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
+  const int64_t gstride = static_cast<int64_t>(active) * kThreads;
+  // the input vertices' frontier bits (the bitmap is not read here)
+  for (int64_t i = gtid; i < q; i += gstride) a.frontier_in[a.qv[i] >> 6] = 0ull;
+
+  const vid_t* __restrict__ col = a.g.col;
+  const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);
+  for (long long b = blockIdx.x; b < nblocks; b += active) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const int cnt = td_block_owner_map<kThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner, s_base,
+                                                 s_wmax);
+    // (A) all items' claims in flight together: col, visited, fetch-or
+    vid_t v[kItems];
+    word_t seen[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kThreads + t;
+      v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) seen[k] = k * kThreads + t < cnt ? a.visited[v[k] >> 6] : ~0ull;
+    unsigned claimed = 0;  // bit k: item k claimed by this lane
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const word_t bit = 1ull << (v[k] & 63);
+      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+    }
+    if (a.lists) {
+      // several ranks: claimed remote targets to their owners' lists
+      unsigned remote = 0;
+#pragma unroll
+      for (int k = 0; k < kItems; ++k)
+        if (((claimed >> k) & 1u) && static_cast<uint64_t>(v[k]) - lo >= rows) remote |= 1u << k;
+      claimed &= ~remote;
+      if (__ballot(remote != 0)) {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+          owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u, dx ? a.direct.table : nullptr);
+      }
+    }
+    // (B) finish the wave's claimed vertices
+    sparse_settle<kItems>(a, v, claimed);
+  }
+  if (a.lists) {
+    // several ranks: td_sparse_apply finishes the level.  A direct exchange:
+    // every wave's write-through stores drained, the workgroups' ticket, and
+    // the last one publishes the counts and flags.
+    if (!dx) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const unsigned prev = atomicAdd(a.ticket, 1u);
+      s_last = (prev == active - 1) ? 1 : 0;
+      if (s_last) *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
+    }
+    __syncthreads();
+    if (s_last) direct_publish(a.direct, a.lists, a.list_stride, true);
+    return;
+  }
+
+  // last workgroup: the level's totals and decision (as scan_units_kernel)
+  __syncthreads();
+  if (t == 0) {
+    // every wave's counter atomic has returned.  (No release: the last
+    // workgroup reads only the counter, a device-scope atomic; the level's
+    // stores are read by later launches.)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = (prev == active - 1) ? 1 : 0;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last || t != 0) return;
+  long long cnt = 0, deg = 0;
+  sparse_totals(a, cnt, deg);
+  LevelCtrl c = *a.ctrl;
+  level_ctrl_finish(c, cnt, deg, false, a.rec);
+  a.rec->t0 = c.t_start;
+  a.rec->t1 = wall_clock64();
+  *a.ctrl = c;
+  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+}
+
+// Two-level last-arriver ticket (thread 0, the workgroup's stores drained):
+// the workgroups of a kFusedGroup group count on their group's ticket (its own
+// 128-B line), the group's last one re-zeroes it and counts on the level
+// ticket -- a grid of thousands of workgroups queues ~64 atomics per address
+// instead of all of them on one.  True in the level's last workgroup.
+__device__ __forceinline__ bool group_ticket_last(unsigned* group_ticket, unsigned* ticket) {
+  const unsigned grp = blockIdx.x / kFusedGroup;
+  const unsigned gsz = min(static_cast<unsigned>(kFusedGroup), gridDim.x - grp * kFusedGroup);
+  const unsigned ngroups = (gridDim.x + kFusedGroup - 1) / kFusedGroup;
+  unsigned* gt = group_ticket + grp * kBuQueueStride;
+  if (atomicAdd(gt, 1u) != gsz - 1) return false;
+  atomicExch(gt, 0u);
+  return atomicAdd(ticket, 1u) == ngroups - 1;
+}
+
+// Sparse top-down level read straight from the bitmap a bottom-up level left
+// (TdSparseArgs::from_bits) -- in place of scan_units + compact + td_sparse,
+// three launches whose scan must see every unit's count before any work list
+// exists.  A wave per 64-word unit, grid-strided, kBitsPre units' words loaded
+// at once (zeroed as read); a unit's frontier vertices 64 per step, their
+// edges expanded kItems x 64 per round from the wave's prefix sum of their
+// degrees (an edge's vertex by a binary search over the prefixes in LDS);
+// claims, owner lists and settling as td_sparse.  The level ends in the last
+// workgroup of a two-level ticket.
+constexpr int kBitsPre = 4;
+template <int kItems>
+__global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) {
+  __shared__ long long s_incl[kBlock];  // per wave: the step's inclusive degree prefixes
+  __shared__ eid_t s_rs[kBlock];        // ... and row starts
+  __shared__ int s_last;
+  const bool dx = a.lists && a.direct.active;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    if (dx && blockIdx.x == 0) direct_publish(a.direct, a.lists, a.list_stride, false);
+    return;
+  }
+  stamp_level_start(a.ctrl);
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(t >> 6));  // (wave-uniform)
+  long long* w_incl = s_incl + wv * kWave;
+  eid_t* w_rs = s_rs + wv * kWave;
+  const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  const int64_t wstride = static_cast<int64_t>(gridDim.x) * kUnitsPerBlock;
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const vid_t* __restrict__ col = a.g.col;
+  const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);
+  for (int64_t u0 = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; u0 < nunits; u0 += kBitsPre * wstride) {
+    word_t fw[kBitsPre];
+#pragma unroll
+    for (int p = 0; p < kBitsPre; ++p) {
+      const int64_t w = (u0 + p * wstride) * kUnitWords + lane;
+      fw[p] = u0 + p * wstride < nunits && w < a.words ? a.frontier_in[w] : 0ull;
+    }
+#pragma unroll
+    for (int p = 0; p < kBitsPre; ++p) {
+      const word_t mine = fw[p];
+      if (!__ballot(mine != 0)) continue;
+      const int64_t w0 = (u0 + p * wstride) * kUnitWords;
+      if (mine) a.frontier_in[w0 + lane] = 0ull;
+      const int fincl = static_cast<int>(wave_incl_scan_u32(static_cast<unsigned>(__popcll(mine))));
+      const int ftotal = __builtin_amdgcn_readlane(fincl, kWave - 1);
+      for (int base = 0; base < ftotal; base += kWave) {
+        const int idx = base + lane;
+        const int vpos = wave_set_position(mine, fincl, idx);
+        eid_t rs = 0, d = 0;
+        if (idx < ftotal) {
+          const int64_t r = w0 * 64 + vpos;
+          rs = ro[r];
+          d = ro[r + 1] - rs;
+        }
+        const long long incl = wave_incl_scan(static_cast<long long>(d));
+        const long long E = readlane_i64(incl, kWave - 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        w_incl[lane] = incl;
+        w_rs[lane] = rs;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (long long e0 = 0; e0 < E; e0 += kItems * kWave) {
+          // (A) all items' claims in flight together: col, visited, fetch-or
+          vid_t v[kItems];
+          word_t seen[kItems];
+#pragma unroll
+          for (int k = 0; k < kItems; ++k) {
+            const long long e = e0 + k * kWave + lane;
+            v[k] = 0u;
+            if (e < E) {
+              int j = 0;  // the first lane whose inclusive prefix passes e
+#pragma unroll
+              for (int step = kWave / 2; step >= 1; step >>= 1)
+                if (w_incl[j + step - 1] <= e) j += step;
+              const long long ex = j > 0 ? w_incl[j - 1] : 0;
+              v[k] = col[w_rs[j] + (e - ex)];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < kItems; ++k) seen[k] = e0 + k * kWave + lane < E ? a.visited[v[k] >> 6] : ~0ull;
+          unsigned claimed = 0;
+#pragma unroll
+          for (int k = 0; k < kItems; ++k) {
+            const word_t bit = 1ull << (v[k] & 63);
+            if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+          }
+          if (a.lists) {
+            unsigned remote = 0;
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+              if (((claimed >> k) & 1u) && static_cast<uint64_t>(v[k]) - lo >= rows) remote |= 1u << k;
+            claimed &= ~remote;
+            if (__ballot(remote != 0)) {
+#pragma unroll
+              for (int k = 0; k < kItems; ++k)
+                owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u,
+                                  dx ? a.direct.table : nullptr);
+            }
+          }
+          // (B) finish the wave's claimed vertices
+          sparse_settle<kItems>(a, v, claimed);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // (the next step overwrites w_incl / w_rs)
+      }
+    }
+  }
+  // every wave's stores and atomics drained, then the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    s_last = group_ticket_last(a.group_ticket, a.ticket) ? 1 : 0;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (a.lists) {
+    // several ranks: td_sparse_apply finishes the level (a direct exchange:
+    // the counts and flags published here)
+    if (t == 0) *a.ticket = 0u;
+    if (dx) direct_publish(a.direct, a.lists, a.list_stride, true);
+    return;
+  }
+  if (t != 0) return;
+  long long cnt = 0, deg = 0;
+  sparse_totals(a, cnt, deg);
+  LevelCtrl c = *a.ctrl;
+  level_ctrl_finish(c, cnt, deg, false, a.rec);
+  a.rec->t0 = c.t_start;
+  a.rec->t1 = wall_clock64();
+  *a.ctrl = c;
+  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+}
+
+// Several ranks, after the list exchange: the ids the other ranks claimed for
+// this rank's vertices (recv_lists) are claimed here (fetch-or on the owned
+// slice of `visited`; a vertex sent by several ranks, or claimed by this
+// rank's own td_sparse, is settled once) and settled like td_sparse's owned
+// claims; the last workgroup writes the level's local totals and zeroes the
+// send lists' counts.  The lists' counts are loaded together (one per
+// thread: they sit a stride apart, cold) and their entries form one index
+// space the grid strides over.
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
+  constexpr int kItems = kTdItems;
+  __shared__ int s_last;
+  __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
+  __shared__ const vid_t* s_src[kern::kMaxPeers];
+  __shared__ uint64_t s_cnt[kern::kMaxPeers];
+  __shared__ uint64_t s_xend[2 * kern::kMaxPeers];
+  // a direct exchange: the peers' cells (their counts) first, live chain or
+  // not (every rank waits for every exchange: the window slots' reuse protocol)
+  const bool dx = a.direct.active;
+  if (dx && direct_wait(a.direct, s_cnt, nullptr) != kWaitOk) return;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if (a.end.active && blockIdx.x == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin, s_xend);
+    return;
+  }
+  const int t = threadIdx.x;
+  if (t < kWave) {
+    long long n = 0;
+    if (t < a.nranks) {
+      const vid_t* src = dx ? a.direct.table->src[t] : a.recv_lists + static_cast<int64_t>(t) * a.list_stride;
+      s_src[t] = src;
+      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
+    }
+    DBFS_DCHECK(n < a.list_stride, 5, n);
+    const long long incl = wave_incl_scan(n);
+    if (t < a.nranks) s_end[t] = incl;
+  }
+  __syncthreads();
+  const long long total = s_end[a.nranks - 1];
+  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
+  // only the workgroups with entries take part (at least one, for the finish)
+  const int64_t need = (total + span - 1) / span;
+  const unsigned active = static_cast<unsigned>(need < 1 ? 1 : (need < gridDim.x ? need : gridDim.x));
+  if (blockIdx.x >= active) return;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * span; i0 < total; i0 += static_cast<int64_t>(active) * span) {
+    vid_t v[kItems];
+    word_t seen[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
+      v[k] = 0u;
+      if (j < total) {
+        int r = 0;
+        while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
+        const long long before = r > 0 ? s_end[r - 1] : 0;
+        const vid_t* src = s_src[r] + 1 + (j - before);
+        v[k] = dx ? sys_load_u32(src) : *(const gu32*)(src);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      seen[k] = i0 + static_cast<int64_t>(k) * kThreads + t < total ? a.visited[v[k] >> 6] : ~0ull;
+    unsigned claimed = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const word_t bit = 1ull << (v[k] & 63);
+      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+    }
+    sparse_settle<kItems>(a, v, claimed);
+  }
+  __syncthreads();
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    s_last = (prev == active - 1) ? 1 : 0;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the send lists were read by the exchange (stream-ordered before this
+  // kernel): their counts restart from zero for the next list level (a
+  // direct exchange's publisher zeroed them)
+  if (!dx && t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
+  __shared__ long long s_tot[2];
+  if (t == 0) {
+    long long cnt = 0, deg = 0;
+    sparse_totals(a, cnt, deg);
+    s_tot[0] = cnt;
+    s_tot[1] = deg;
+  }
+  if (!a.end.active) return;
+  __syncthreads();
+  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
+}
+
+// ---------------------------------------------------------------------------
+// Binned top-down level (BinArgs).  Count and fill passes walk the same edge
+// blocks per workgroup (b = blockIdx.x, += gridDim.x) with the td_expand owner
+// map; a workgroup's targets of bin k land at bin_start[k] + wg_off[k * grid +
+// g] plus an LDS slot.  1024-thread workgroups, 2 edges per thread per block.
+constexpr int kBinThreads = 1024;
+constexpr int kAggRounds = 4;
+
+// slot = atomicAdd(&cnt[key], 1) for every active lane, with the lanes that
+// share a key served by one LDS atomic (rows in id order put runs of targets
+// in one bin, and 64 same-address LDS atomics serialise): up to kAggRounds
+// distinct keys per wave aggregated, the rest per lane.  Wave-uniform call.
+__device__ __forceinline__ unsigned lds_slot_add(unsigned* cnt, int key, bool active) {
+  const int lane = lane_id();
+  unsigned long long pending = __ballot(active);
+  unsigned slot = 0;
+#pragma unroll
+  for (int r = 0; r < kAggRounds; ++r) {
+    if (!pending) break;
+    const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+    const int k = __shfl(key, leader, kWave);
+    const unsigned long long m = __ballot(active && key == k) & pending;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[k], static_cast<unsigned>(__popcll(m)));
+    base = __shfl(base, leader, kWave);
+    if ((m >> lane) & 1ull) slot = base + mask_rank(m);
+    pending &= ~m;
+  }
+  if ((pending >> lane) & 1ull) slot = atomicAdd(&cnt[key], 1u);
+  return slot;
+}
+
+template <bool kFill>
+__global__ __launch_bounds__(kTdThreads) void bin_pass_kernel(BinArgs a) {
+  constexpr int kItems = kTdEdgesPerBlock / kTdThreads;
+  __shared__ int32_t s_owner[kTdEdgesPerBlock];
+  __shared__ long long s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_wmax[kTdThreads / kWave];
+  __shared__ unsigned s_cnt[kBinMaxBins];
+  __shared__ long long s_start[kFill ? kBinMaxBins : 1];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  const long long q = a.dev_stats[0], m = a.dev_stats[1];
+  const int t = threadIdx.x;
+  if (!kFill && a.clear_qv) {
+    stamp_level_start(a.ctrl);  // first kernel of the level (no compaction ran)
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kTdThreads + t; i < q;
+         i += static_cast<int64_t>(gridDim.x) * kTdThreads)
+      a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
+  }
+  for (int k = t; k < a.nbins; k += kTdThreads) s_cnt[k] = 0;
+  if constexpr (kFill) {
+    // bin starts: exclusive scan of the bin totals (<= kBinMaxBins), serial
+    // per wave-chunk then across the 4 waves
+    __shared__ long long s_part[kTdThreads / kWave];
+    constexpr int kPer = kBinMaxBins / kTdThreads;
+    long long c[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = t * kPer + k;
+      c[k] = b < a.nbins ? a.bin_total[b] : 0;
+      sum += c[k];
+    }
+    const long long incl = wave_incl_scan(sum);
+    if (lane_id() == kWave - 1) s_part[t >> 6] = incl;
+    __syncthreads();
+    long long off = incl - sum;
+    for (int w = 0; w < (t >> 6); ++w) off += s_part[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int b = t * kPer + k;
+      if (b < a.nbins) s_start[b] = off + a.cnt[static_cast<int64_t>(b) * a.grid + blockIdx.x];
+      off += c[k];
+    }
+  }
+  // (td_block_owner_map starts with a barrier)
+  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  const vid_t* __restrict__ col = a.g.col;
+  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const long long e0 = b * kTdEdgesPerBlock;
+    const int cnt = td_block_owner_map<kTdThreads>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
+                                                   s_base, s_wmax);
+    vid_t v[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int idx = k * kTdThreads + t;
+      v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const bool act = k * kTdThreads + t < cnt;
+      const int bin = static_cast<int>(v[k] >> a.shift);
+      DBFS_DCHECK(!act || bin < a.nbins, 8, v[k]);
+      const unsigned slot = lds_slot_add(s_cnt, bin, act);
+      if constexpr (kFill) {
+        if (act) a.buf[s_start[bin] + slot] = v[k];
+      }
+    }
+  }
+  if constexpr (!kFill) {
+    __syncthreads();
+    for (int k = t; k < a.nbins; k += kTdThreads) a.cnt[static_cast<int64_t>(k) * a.grid + blockIdx.x] = s_cnt[k];
+  }
+}
+
+// One workgroup per bin: its row of workgroup counts made exclusive, the
+// bin's total.
+__global__ __launch_bounds__(kTdThreads) void bin_scan_kernel(BinArgs a) {
+  __shared__ long long s_part[kTdThreads / kWave];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  uint32_t* row = a.cnt + static_cast<int64_t>(blockIdx.x) * a.grid;
+  const int t = threadIdx.x;
+  const int per = (a.grid + kTdThreads - 1) / kTdThreads;
+  long long sum = 0;
+  for (int k = 0; k < per; ++k) {
+    const int g = t * per + k;
+    if (g < a.grid) sum += row[g];
+  }
+  const long long incl = wave_incl_scan(sum);
+  if (lane_id() == kWave - 1) s_part[t >> 6] = incl;
+  __syncthreads();
+  long long off = incl - sum, total = 0;
+  for (int w = 0; w < kTdThreads / kWave; ++w) {
+    if (w < (t >> 6)) off += s_part[w];
+    total += s_part[w];
+  }
+  for (int k = 0; k < per; ++k) {
+    const int g = t * per + k;
+    if (g < a.grid) {
+      const uint32_t c = row[g];
+      row[g] = static_cast<uint32_t>(off);  // (a bin holds < 2^32 targets per level)
+      off += c;
+    }
+  }
+  if (t == 0) a.bin_total[blockIdx.x] = total;
+}
+
+// One workgroup per bin: the bin's visited slice in LDS, claims of the bin's
+// targets with LDS atomics (lanes on one word aggregated; kApplyItems loads
+// in flight per thread), then the bin's frontier / visited words.
+constexpr int kApplyItems = 8;
+
+__global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
+  constexpr int kMaxWords = (1 << kBinMaxShift) / kWordBits;
+  __shared__ word_t s_vis[kMaxWords];
+  __shared__ word_t s_new[kMaxWords];
+  __shared__ long long s_part[kBinThreads / kWave];
+  if (!chain_live(*a.ctrl, 'T', 0)) return;
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  const int64_t bin = blockIdx.x;
+  const int64_t span_w = (int64_t(1) << a.shift) / kWordBits;
+  const int64_t w0 = bin * span_w;
+  const int nw = static_cast<int>(min<int64_t>(span_w, a.words - w0));
+  if (nw <= 0) return;
+  // this bin's start: the totals of the bins before it
+  long long before = 0;
+  for (int64_t b = t; b < bin; b += kBinThreads) before += a.bin_total[b];
+  before = wave_sum(before);
+  if (lane == 0) s_part[t >> 6] = before;
+  for (int w = t; w < nw; w += kBinThreads) {
+    s_vis[w] = a.visited[w0 + w];
+    s_new[w] = 0ull;
+  }
+  __syncthreads();
+  long long b0 = 0;
+  for (int w = 0; w < kBinThreads / kWave; ++w) b0 += s_part[w];
+  const long long b1 = b0 + a.bin_total[bin];
+  const int64_t vlo = w0 * kWordBits;
+  for (long long i0 = b0; i0 < b1; i0 += static_cast<long long>(kBinThreads) * kApplyItems) {
+    vid_t v[kApplyItems];
+#pragma unroll
+    for (int k = 0; k < kApplyItems; ++k) {
+      const long long j = i0 + static_cast<long long>(k) * kBinThreads + t;
+      v[k] = j < b1 ? a.buf[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < kApplyItems; ++k) {
+      int w = 0;
+      word_t bit = 0;
+      if (v[k] != 0xFFFFFFFFu) {
+        const int64_t l = static_cast<int64_t>(v[k]) - vlo;
+        w = static_cast<int>(l >> 6);
+        bit = 1ull << (l & 63);
+        if (s_vis[w] & bit) bit = 0;  // visited: nothing to claim
+      }
+      unsigned long long pending = __ballot(bit != 0);
+#pragma unroll
+      for (int r = 0; r < kAggRounds; ++r) {
+        if (!pending) break;
+        const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+        const int kw = __shfl(w, leader, kWave);
+        const unsigned long long msk = __ballot(bit != 0 && w == kw) & pending;
+        if (__popcll(msk) == 1) break;  // no sharing left worth a reduction
+        word_t mine = ((msk >> lane) & 1ull) ? bit : 0ull;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) mine |= __shfl_xor(mine, off, kWave);
+        if (lane == leader) atomicOr(&s_new[kw], mine);
+        pending &= ~msk;
+      }
+      if ((pending >> lane) & 1ull) atomicOr(&s_new[w], bit);
+    }
+  }
+  __syncthreads();
+  for (int w = t; w < nw; w += kBinThreads) {
+    const word_t nb = s_new[w];
+    a.frontier[w0 + w] = nb;
+    if (nb) a.visited[w0 + w] = s_vis[w] | nb;
+  }
+}
+
+// out bit h = visited bit of td_hub_vertex[h]: one wave per hub word.
+__global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
+  if (a.ctrl && (!chain_live(*a.ctrl, 'T', 0) || a.ctrl->m_f < a.min_edges ||
+                 static_cast<double>(a.ctrl->vis_deg) < a.vis_frac * a.ctrl->total_directed))
+    return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int64_t h = w * kWave + lane_id();
+  const bool bit = h < a.g.td_nhubs && test_bit(a.visited, a.g.td_hub_vertex[h]);
+  const word_t m = __ballot(bit);
+  if (lane_id() == 0 && w * kWave < a.g.td_nhubs) a.out[w] = m;
+}
+
+// HubApplyArgs: 16 marks per thread (kTdMaxHubs is a multiple of 16; the
+// marks past td_nhubs stay zero).
+__global__ __launch_bounds__(kBlock) void hub_apply_kernel(HubApplyArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock * 16;
+  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) * 16; i < a.g.td_nhubs; i += stride) {
+    uint4* p = reinterpret_cast<uint4*>(a.mark + i);
+    const uint4 m = *p;
+    if ((m.x | m.y | m.z | m.w) == 0u) continue;
+    const unsigned w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if ((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) {
+        DBFS_DCHECK(i + j < a.g.td_nhubs, 9, i + j);
+        const vid_t v = a.g.td_hub_vertex[i + j];
+        a.level8[v] = lv;
+      }
+    *p = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+}  // namespace
+
+#ifdef DBFS_TD_STATS
+static void td_stats_report(hipStream_t st) {
+  unsigned long long h[4] = {0};
+  (void)hipStreamSynchronize(st);
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_td_stats), sizeof(h));
+  const unsigned long long z[4] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_td_stats), z, sizeof(z));
+  if (h[0])
+    std::fprintf(stderr, "[td-stats] live %llu hub-unvisited %llu direct-stores %llu filter-wgs %llu\n", h[0], h[1],
+                 h[2], h[3]);
+}
+#endif
+
+// Device-loop grid of a td_expand variant: at most the workgroups resident at
+// once (a.grid is a cap).  A grid past residency runs a partial second wave of
+// workgroups that start when the first ones finish their strided share: with
+// 2048 workgroups and six resident per CU, RMAT-22 top-down 70 against 83
+// GTEPS at 1536.
+template <TdOut kOut, bool kFilter, bool kBase32>
+unsigned td_resident_grid(int64_t cap) {
+  static const int per_cu = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kTdThreads, kFilter, kBase32>,
+                                                     kTdThreads, 0) != hipSuccess || n <= 0)
+      n = 1;
+    return n;
+  }();
+  return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(cap, static_cast<int64_t>(per_cu) * device_cus())));
+}
+
+void td_expand(const TdArgs& a, hipStream_t st) {
+#ifdef DBFS_TD_STATS
+  struct Report {
+    hipStream_t st;
+    ~Report() { td_stats_report(st); }
+  } report{st};
+#endif
+  if (a.ctrl) {
+    // device loop: fixed grid, size and output mode read on the device
+    if (a.grid <= 0) return;
+    const bool b32 = a.g.nnz <= (int64_t(1) << 32);
+    const int64_t fgrid = a.grid_filter > 0 ? a.grid_filter : a.grid;
+#define LAUNCH_TD_DEV(OUT, F, B) \
+  td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
+    if (a.lists)
+      LAUNCH_TD_DEV(TdOut::Lists, false, false);
+    else if (a.td_hub_vis && b32)
+      LAUNCH_TD_DEV(TdOut::Dyn, true, true);
+    else if (a.td_hub_vis)
+      LAUNCH_TD_DEV(TdOut::Dyn, true, false);
+    else if (b32)
+      LAUNCH_TD_DEV(TdOut::Dyn, false, true);
+    else
+      LAUNCH_TD_DEV(TdOut::Dyn, false, false);
+#undef LAUNCH_TD_DEV
+    return;
+  }
+  if (a.m <= 0 || a.q <= 0) return;
+  const unsigned grid = grid_for(a.m, kTdEdgesPerBlock);
+  const bool wide = static_cast<int64_t>(grid) < a.wide_below_blocks;
+#define LAUNCH_TD(OUT)                                                  \
+  do {                                                                       \
+    if (wide)                                                                \
+      td_expand_kernel<OUT, 1024><<<grid, 1024, 0, st>>>(a);                 \
+    else                                                                     \
+      td_expand_kernel<OUT, kTdThreads><<<grid, kTdThreads, 0, st>>>(a);     \
+  } while (0)
+  if (a.lists)
+    LAUNCH_TD(TdOut::Lists);
+  else if (a.next_bytes)
+    LAUNCH_TD(TdOut::Bytes);
+  else
+    LAUNCH_TD(TdOut::Bits);
+#undef LAUNCH_TD
+}
+
+void td_binned(const BinArgs& a, hipStream_t st) {
+  if (a.nbins <= 0 || a.grid <= 0 || a.nbins > kBinMaxBins) return;
+  bin_pass_kernel<false><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+  bin_scan_kernel<<<static_cast<unsigned>(a.nbins), kTdThreads, 0, st>>>(a);
+  bin_pass_kernel<true><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+  bin_apply_kernel<<<static_cast<unsigned>(a.nbins), kBinThreads, 0, st>>>(a);
+}
+
+void td_sparse(const TdSparseArgs& a, hipStream_t st) {
+  if (a.from_bits) {
+    // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
+    // wave (RMAT-26, one rank: 1024 workgroups, 16 groups on the ticket)
+    const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+    DBFS_CHECK(a.group_ticket, "td_sparse from a bitmap needs the group tickets");
+    // (an empty shard still runs one workgroup: the level's finish)
+    const unsigned grid = grid_for(nunits, kUnitsPerBlock, std::min<int64_t>(kMaxFusedGrid, 1024));
+    td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
+    return;
+  }
+  td_sparse_kernel<kTdThreads><<<static_cast<unsigned>(a.grid), kTdThreads, 0, st>>>(a);
+}
+
+void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
+                     hipStream_t st) {
+  direct_selftest_kernel<<<1, 256, 0, st>>>(lists, end, round, err);
+}
+
+void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {
+  td_sparse_apply_kernel<kTdThreads><<<static_cast<unsigned>(std::max<int64_t>(1, a.grid)), kTdThreads, 0, st>>>(a);
+}
+
+void hub_visited(const HubVisitedArgs& a, hipStream_t st) {
+  if (a.g.td_nhubs <= 0) return;
+  hub_visited_kernel<<<grid_for((a.g.td_nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+}
+
+void hub_apply(const HubApplyArgs& a, hipStream_t st) {
+  if (a.g.td_nhubs <= 0 || a.g.td_nhubs > kTdMaxHubs) return;  // (select_hubs: at most kTdMaxHubs)
+  hub_apply_kernel<<<grid_for((a.g.td_nhubs + 15) / 16, kBlock), kBlock, 0, st>>>(a);
+}
+
+unsigned long long take_check_td() { return take_check_local(); }
+
+}  // namespace kern
+}  // namespace dbfs

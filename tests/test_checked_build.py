@@ -1,7 +1,7 @@
 """Device-checked build: bin/bfs_checked is the CLI with the
 traversal kernels compiled with -DDBFS_CHECKED (`make checked`, part of
 `make all`).  Kernels verify the bounds of their work lists, owner lists and
-vertex ids (DBFS_DCHECK sites in csrc/kernels/bfs_kernels.hip) and record the
+vertex ids (DBFS_DCHECK sites in csrc/kernels/{bfs,td,bu}_kernels.hip) and record the
 first violation; the engine reads it after every traversal
 (Engine::check_device) and fails the run.  DBFS_FAULT_INJECT kind=device
 records violation 99 to exercise that path."""

@@ -579,3 +579,38 @@ def test_run_many_matches_single_runs(rt):
     for a, b in zip(singles, many):
         assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
     assert np.array_equal(bfs.levels(), _oracle(csr, srcs[-1]))
+
+
+@pytest.mark.parametrize("bits", [1, 0])
+@pytest.mark.parametrize("P", [1, 3])
+def test_sparse_level_from_bitmap(P, bits):
+    """A sparse top-down level right after a bottom-up one reads the bottom-up
+    output bitmap itself (td_sparse_bits: no unit scan / compaction) or a
+    compacted work list (0): same levels and per-level records, exact against
+    the oracle, with one and several ranks; such a level occurs."""
+    p = dbfs.rmat_params(12, 16, 31)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    srcs = [int(v) for v in np.nonzero(deg > 0)[0][[3, 500, 1700]]]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        b.engine.set_option("td_sparse_bits", bits)
+        out = []
+        for s in srcs:
+            r = b.run(s)
+            forms = "".join(c[1] for c in r.chains)
+            out.append((b.levels(), [(l["dir"], l["frontier"], l["frontier_edges"]) for l in r.levels], forms))
+        return out
+
+    ref = None
+    if P == 1:
+        results = [body(init_runtime("cpu"))]
+    else:
+        results = run_virtual_ranks(P, body, device="cpu")
+    for rank_out in results:
+        for (lv, recs, forms), s in zip(rank_out, srcs):
+            assert np.array_equal(lv, _oracle(csr, s))
+        assert any("BS" in forms for _, _, forms in rank_out)
+        ref = ref or [recs for _, recs, _ in rank_out]
+        assert [recs for _, recs, _ in rank_out] == ref

@@ -943,3 +943,34 @@ def test_peer_direct_exchange_long_chain(tmp_path):
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["comm_direct"] is True and rec["validated_roots"] == "3/3"
+
+
+@pytest.mark.parametrize("bits", [1, 0])
+def test_sparse_level_from_bitmap_gpu(gpu_runtime, bits):
+    """td_sparse_bits: the sparse top-down level after a bottom-up one reads
+    the bottom-up output bitmap (a wave per unit, edges from the wave's degree
+    prefix, two-level ticket) instead of a compacted work list; exact against
+    the oracle on one rank (RMAT-18, RMAT-20: 16-unit grids up to the 1024-
+    workgroup cap) and on 3 virtual ranks (owner lists after it)."""
+    for scale in (18, 20):
+        p = dbfs.rmat_params(scale, 16, 71)
+        csr = dbfs.host_csr_from_params(p)
+        bfs = dbfs.BFS(p, gpu_runtime, mode="do")
+        bfs.engine.set_option("td_sparse_bits", bits)
+        forms = ""
+        for src in bfs.sample_roots(3, seed=5):
+            res = _check(bfs, csr, src)
+            forms += "".join(c[1] for c in res.chains) + "|"
+        assert "BS" in forms
+    p = dbfs.rmat_params(17, 16, 71)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [int(s) for s in dbfs.BFS(p, gpu_runtime, mode="do").sample_roots(2, seed=8)]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        b.engine.set_option("td_sparse_bits", bits)
+        return [(b.run(s), b.levels())[1] for s in srcs]
+
+    for rank_out in run_virtual_ranks(3, body, device="hip"):
+        for lv, s in zip(rank_out, srcs):
+            assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
