@@ -10,6 +10,8 @@ namespace kern {
 
 // bfs_kernels.hip, td_kernels.hip, bu_kernels.hip
 void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st);
+// zero `bytes` at p with 16-B stores (false: p or bytes not 16-B aligned)
+bool zero_fill(void* p, size_t bytes, hipStream_t st);
 void set_bit(word_t* bm, int64_t bit, hipStream_t st);
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st);
 void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStream_t st);
@@ -20,6 +22,8 @@ void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void td_sparse(const TdSparseArgs& a, hipStream_t st);
+void td_xcd(const TdArgs& a, hipStream_t st);
+int64_t td_xcd_grid();  // pass-1 workgroups of td_xcd (TdArgs::xcd_grid)
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 // PeerComm::self_test of the direct exchanges (`round` 0..3; mismatches and
 // timeouts counted in *err)
