@@ -78,7 +78,7 @@ class CpuBackend final : public Backend {
     bool use_bytes = a.cand_bytes != nullptr;
     if (a.ctrl) {
       if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-      use_bytes = use_bytes && (a.force_bytes || a.ctrl->bytes != 0);
+      use_bytes = use_bytes && a.ctrl->bytes != 0;
     }
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
@@ -275,20 +275,6 @@ class CpuBackend final : public Backend {
         }
       }
     }
-  }
-
-  // XCD-binned level: on the host simply the direct level-byte form
-  void td_xcd(const TdArgs& a) override {
-    DBFS_CHECK(a.ctrl && a.level_direct, "td_xcd: device loop and level bytes");
-    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-    const int64_t q = a.dev_stats[0];
-    if (a.clear_qv)
-      for (int64_t i = 0; i < q; ++i) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
-    for (int64_t i = 0; i < q; ++i)
-      for (int64_t k = a.qscan[i]; k < a.qscan[i + 1]; ++k) {
-        const vid_t v = a.g.col[k + a.qbase[i]];
-        if (!test_bit(a.visited, v)) a.level_direct[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
-      }
   }
 
   void td_binned(const BinArgs& a) override {

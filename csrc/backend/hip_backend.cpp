@@ -222,11 +222,6 @@ class HipBackend final : public Backend {
   void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
   void td_sparse(const TdSparseArgs& a) override { on(); kern::td_sparse(a, st_); chk(); }
-  void td_xcd(const TdArgs& a) override { on(); kern::td_xcd(a, st_); chk(); }
-  int64_t xcd_grid() override {
-    on();
-    return kern::td_xcd_grid();
-  }
   void td_sparse_apply(const TdSparseArgs& a) override { on(); kern::td_sparse_apply(a, st_); chk(); }
   void level_finish(const LevelFinishArgs& a) override { on(); kern::level_finish(a, st_); chk(); }
   void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base) override {

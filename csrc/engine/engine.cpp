@@ -84,7 +84,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
   else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
-  else if (name == "td_xcd_edges") o.td_xcd_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
@@ -130,7 +129,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
           {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
-          {"td_xcd_edges", static_cast<double>(o.td_xcd_edges)},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
           {"list_cap_factor", o.list_cap_factor},
@@ -1201,33 +1199,6 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   }
   // work-list set k (level L reads set L & 1; one set without sparse levels)
   auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
-  // XCD-binned levels: vertex-range bins of at most 2^20 vertices (a bin's
-  // level bytes fit one XCD's L2 next to the streams), at least 8 and at most
-  // 64 bins; the regions for the backend's pass-1 grid, twice the graph's
-  // entries (capped at 2^31: a full region falls back to direct stores)
-  auto setup_xcd = [&](TdArgs& ta) {
-    const int64_t rows = std::max<int64_t>(g_.rows(), 1);
-    int shift = 6, nb = 1;
-    while ((int64_t(1) << shift) * 8 < rows) ++shift;  // 8 bins of 2^shift cover the rows
-    nb = 8;
-    while (shift > 20 && nb < 64) {
-      --shift;
-      nb *= 2;
-    }
-    nb = static_cast<int>(std::max<int64_t>(1, div_up(rows, int64_t(1) << shift)));
-    const int64_t grid = be_.xcd_grid();
-    if (!xcd_fill_.data()) {
-      const int64_t want = 2 * (g_.nnz() + (grid + 1) * kTdEdgesPerBlock) + grid * 64 * 64;
-      xcd_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(std::min<int64_t>(want, int64_t(1) << 31)));
-      xcd_fill_ = DBuf<uint32_t>(be_, static_cast<size_t>(grid * 64));
-    }
-    ta.xcd_buf = xcd_buf_.data();
-    ta.xcd_fill = xcd_fill_.data();
-    ta.xcd_entries = static_cast<int64_t>(xcd_buf_.size());
-    ta.xcd_shift = shift;
-    ta.xcd_bins = nb;
-    ta.xcd_grid = grid;
-  };
   // two-level tickets (fused update finish, sparse levels read from a bitmap):
   // zero between launches, each user re-zeroes what it took
   auto group_tickets = [&]() {
@@ -1633,16 +1604,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           ta.td_hub_mark = td_hub_mark_.data();
         }
       }
-      // large levels: XCD-binned (the level bytes of a vertex range stored by
-      // the workgroups of one XCD); the update then reads the level bytes
-      const bool xcd = ta.level_direct && opt_.td_xcd_edges > 0 && mf_hint >= static_cast<double>(opt_.td_xcd_edges);
-      if (xcd) {
-        setup_xcd(ta);
-        tu.force_bytes = true;
-        be_.td_xcd(ta);
-      } else {
-        be_.td_expand(ta);
-      }
+      be_.td_expand(ta);
       if (ta.td_hub_mark) {
         HubApplyArgs ha;
         ha.g = gv;

@@ -303,9 +303,6 @@ struct UpdateArgs {
   // unvisited vertices whose level already reads new_level (level8, padded to
   // whole words); cand_bytes is not read.
   const uint8_t* level_direct = nullptr;
-  // ... read whatever ctrl->bytes says (an XCD-binned level always stores
-  // level bytes)
-  bool force_bytes = false;
   // One rank, device loop (as BuArgs::fuse_scan): totals and finish in the
   // last-arriving workgroup, unit statistics left unscanned (a following
   // compaction scans them first); tot[0..1] zero, reset by the last one.
@@ -588,20 +585,6 @@ struct TdArgs {
   // global frontier edges ctrl->m_f <= max_mf (= list_cap: no list can
   // overflow, every rank decides alike); else a no-op the host re-enqueues.
   int64_t max_mf = 0;
-  // XCD-binned level (Backend::td_xcd; one rank, level_direct): pass 1 reads
-  // the edge blocks as td_expand does and appends every unvisited target to
-  // this workgroup's region of its vertex-range bin (xcd_bins bins of
-  // 2^xcd_shift vertices; regions of xcd_cap(m) entries, xcd_buf holds
-  // xcd_entries; a full region falls back to the direct store); the fills go
-  // to xcd_fill[bin * xcd_grid + wg].  Pass 2's workgroup b stores the level
-  // bytes of bins b % 8, b % 8 + 8, ... -- one XCD per bin class under the
-  // round-robin placement, so a bin's level bytes stay in one XCD's L2.
-  vid_t* xcd_buf = nullptr;
-  uint32_t* xcd_fill = nullptr;
-  int64_t xcd_entries = 0;
-  int xcd_shift = 0;
-  int xcd_bins = 0;
-  int64_t xcd_grid = 0;  // pass-1 workgroups (set by the launcher)
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)
@@ -828,8 +811,6 @@ class Backend {
   // Rate of the device wall clock the kernels stamp level records with (ticks
   // per ms; 0: no device clock, records carry no times).
   virtual double wall_clock_khz() const { return 0.0; }
-  // Pass-1 workgroups of td_xcd (its regions are sized for them).
-  virtual int64_t xcd_grid() { return 8; }
 
   // Host waits on the device (to_host, to_device, synchronize) call
   // watch(seconds waited) about every period_s while the stream is still busy;
@@ -896,8 +877,6 @@ class Backend {
   virtual void zero_degree_mask(const ZeroDegArgs& a) = 0;
   virtual void compact_frontier(const CompactArgs& a) = 0;
   virtual void td_sparse(const TdSparseArgs& a) = 0;
-  // XCD-binned top-down level (TdArgs::xcd_*): the bin pass, then the apply
-  virtual void td_xcd(const TdArgs& a) = 0;
   virtual void td_sparse_apply(const TdSparseArgs& a) = 0;
   virtual void level_finish(const LevelFinishArgs& a) = 0;
   virtual void td_expand(const TdArgs& a) = 0;

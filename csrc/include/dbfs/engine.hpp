@@ -120,10 +120,6 @@ struct EngineOptions {
   // 1.7 M-edge level 115 -> 68 us).  Replaces td_byte_edges there.
   bool td_direct = true;
   int64_t td_direct_edges = int64_t(1) << 16;
-  // ... and levels predicted at >= td_xcd_edges frontier edges are
-  // XCD-binned (Backend::td_xcd: targets binned by vertex range, each bin's
-  // level bytes stored by the workgroups of one XCD); 0 disables.
-  int64_t td_xcd_edges = int64_t(1) << 22;
   // Device loop, one rank: top-down levels predicted to have at least this
   // many frontier edges run binned (BinArgs: targets binned by vertex range,
   // claimed per bin in LDS) instead of td_expand + update; 0 disables.  Only
@@ -364,8 +360,6 @@ class Engine {
   DBuf<uint32_t> td_group_ticket_;  // UpdateArgs::group_ticket
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
-  DBuf<vid_t> xcd_buf_;        // TdArgs::xcd_buf (XCD-binned levels)
-  DBuf<uint32_t> xcd_fill_;    // TdArgs::xcd_fill
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill
   uint8_t narrow_base_ = 0;           // the current run's level byte base (narrow_epochs)

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-    use_bytes = use_bytes && (a.force_bytes || a.ctrl->bytes != 0);
+    use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;

@@ -22,8 +22,6 @@ void zero_degree_mask(const ZeroDegArgs& a, hipStream_t st);
 void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void td_sparse(const TdSparseArgs& a, hipStream_t st);
-void td_xcd(const TdArgs& a, hipStream_t st);
-int64_t td_xcd_grid();  // pass-1 workgroups of td_xcd (TdArgs::xcd_grid)
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 // PeerComm::self_test of the direct exchanges (`round` 0..3; mismatches and
 // timeouts counted in *err)

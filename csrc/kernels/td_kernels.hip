@@ -1013,140 +1013,6 @@ __global__ __launch_bounds__(kBinThreads) void bin_apply_kernel(BinArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// XCD-binned top-down level (TdArgs::xcd_*; one rank, level bytes).  The
-// direct form stores each unvisited target's level byte wherever it lies, so
-// every XCD's L2 holds -- and writes back, over and over -- partial lines of
-// the whole level array (a 114 M-edge RMAT-22 level: 622 MB written for a
-// 4 MiB array, 85 % of wave-cycles waiting).  Here pass 1 reads the edge
-// blocks as td_expand does (owner map, hub filter, visited test) and appends
-// each unvisited target to this workgroup's region of its vertex-range bin
-// (LDS slots per bin, then contiguous runs of 4-B stores); pass 2's
-// workgroup b stores the level bytes of the bins of class b % 8, which the
-// round-robin placement keeps on one XCD (speed only: any placement is
-// correct), so a bin's bytes are written back once.
-constexpr int kXcdClasses = 8;
-constexpr int kXcdMaxBins = 64;
-constexpr double kXcdSlack = 2.0;
-
-// Entries per (bin, pass-1 workgroup) region for a level of m edges: twice
-// the workgroup's share of the level's edges over the bins (RMAT ids are
-// scrambled: near-uniform over the bins), at most what the buffer holds.
-__device__ __forceinline__ int64_t xcd_cap(const TdArgs& a, long long m) {
-  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
-  const long long per_wg = (nblocks + a.xcd_grid - 1) / a.xcd_grid * kTdEdgesPerBlock;
-  const int64_t want = static_cast<int64_t>(kXcdSlack * static_cast<double>(per_wg) / a.xcd_bins) + 64;
-  return min<int64_t>(want, a.xcd_entries / (a.xcd_grid * a.xcd_bins));
-}
-
-template <bool kFilter, bool kBase32>
-__global__ __launch_bounds__(kTdThreads) void td_xcd_bin_kernel(TdArgs a) {
-  constexpr int kThreads = kTdThreads;
-  constexpr int kItems = kTdEdgesPerBlock / kThreads;
-  using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
-  __shared__ int32_t s_owner[kTdEdgesPerBlock];
-  __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
-  __shared__ int32_t s_wmax[kThreads / kWave];
-  __shared__ word_t s_hubvis[kFilter ? kTdMaxHubs / kWordBits : 1];
-  __shared__ unsigned s_cnt[kXcdMaxBins], s_fill[kXcdMaxBins];
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-  const long long q = a.dev_stats[0], m = a.dev_stats[1];
-  if (a.clear_qv) {
-    stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < q;
-         i += static_cast<int64_t>(gridDim.x) * kThreads)
-      a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
-  }
-  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
-  const int t = threadIdx.x;
-  const int64_t cap = xcd_cap(a, m);
-  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
-  if (t < kXcdMaxBins) {
-    s_cnt[t] = 0;
-    s_fill[t] = 0;
-  }
-  bool filter = false;
-  if constexpr (kFilter) {
-    filter = a.td_hub_vis && a.g.td_col && m >= a.td_hub_min_edges && blockIdx.x < nblocks &&
-             static_cast<double>(a.ctrl->vis_deg) >= a.td_hub_vis_frac * a.ctrl->total_directed;
-    if (filter) {
-      const int64_t hw = (a.g.td_nhubs + kWordBits - 1) / kWordBits;
-      for (int64_t i = t; i < hw; i += kThreads) s_hubvis[i] = a.td_hub_vis[i];
-    }
-  }
-  const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
-  vid_t* __restrict__ region = a.xcd_buf + static_cast<int64_t>(blockIdx.x) * cap;  // bin k: + k * grid * cap
-  const int64_t bin_stride = static_cast<int64_t>(gridDim.x) * cap;
-  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    const long long e0 = b * kTdEdgesPerBlock;
-    // (starts with a barrier: the previous block's fills are final)
-    const int cnt = td_block_owner_map<kThreads, BaseT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
-                                                        s_base, s_wmax);
-    vid_t vk[kItems];
-    bool live[kItems], hubnew[kItems];
-    td_load_items<kThreads, kFilter, kBase32>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis, vk, live, hubnew);
-    bool keep[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
-      keep[k] = live[k] && (hubnew[k] || !(a.visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
-    }
-    unsigned slot[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) slot[k] = lds_slot_add(s_cnt, static_cast<int>(vk[k] >> a.xcd_shift), keep[k]);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      if (!keep[k]) continue;
-      const int bin = static_cast<int>(vk[k] >> a.xcd_shift);
-      const int64_t pos = static_cast<int64_t>(s_fill[bin]) + slot[k];
-      if (pos < cap) region[bin * bin_stride + pos] = vk[k];
-      else a.level_direct[vk[k]] = lv;  // (the region is full: the direct store)
-    }
-    __syncthreads();
-    if (t < a.xcd_bins) {
-      s_fill[t] = static_cast<unsigned>(min<int64_t>(cap, static_cast<int64_t>(s_fill[t]) + s_cnt[t]));
-      s_cnt[t] = 0;
-    }
-  }
-  __syncthreads();
-  if (t < a.xcd_bins) a.xcd_fill[static_cast<int64_t>(t) * gridDim.x + blockIdx.x] = s_fill[t];
-}
-
-// Pass 2: workgroup b stores the level bytes of bins b % 8, b % 8 + 8, ...,
-// each bin's regions split over the class's workgroups (gridDim.x is a
-// multiple of kXcdClasses); kXcdItems loads in flight per thread.
-constexpr int kXcdItems = 8;
-__global__ __launch_bounds__(kBlock) void td_xcd_apply_kernel(TdArgs a) {
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-  const long long m = a.dev_stats[1];
-  const int64_t cap = xcd_cap(a, m);
-  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
-  const int cls = static_cast<int>(blockIdx.x % kXcdClasses);
-  const int64_t idx = blockIdx.x / kXcdClasses, nper = gridDim.x / kXcdClasses;
-  const int t = threadIdx.x;
-  for (int bin = cls; bin < a.xcd_bins; bin += kXcdClasses) {
-    for (int64_t g = idx; g < a.xcd_grid; g += nper) {
-      const int64_t n = a.xcd_fill[static_cast<int64_t>(bin) * a.xcd_grid + g];
-      const vid_t* __restrict__ src = a.xcd_buf + (static_cast<int64_t>(bin) * a.xcd_grid + g) * cap;
-      for (int64_t i0 = 0; i0 < n; i0 += static_cast<int64_t>(kBlock) * kXcdItems) {
-        vid_t v[kXcdItems];
-#pragma unroll
-        for (int k = 0; k < kXcdItems; ++k) {
-          const int64_t i = i0 + k * kBlock + t;
-          v[k] = i < n ? src[i] : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int k = 0; k < kXcdItems; ++k)
-          if (v[k] != 0xFFFFFFFFu) {
-            DBFS_DCHECK((v[k] >> a.xcd_shift) == static_cast<vid_t>(bin), 12, v[k]);
-            a.level_direct[v[k]] = lv;
-          }
-      }
-    }
-  }
-}
-
 // out bit h = visited bit of td_hub_vertex[h]: one wave per hub word.
 __global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
   if (a.ctrl && (!chain_live(*a.ctrl, 'T', 0) || a.ctrl->m_f < a.min_edges ||
@@ -1257,34 +1123,6 @@ void td_expand(const TdArgs& a, hipStream_t st) {
   else
     LAUNCH_TD(TdOut::Bits);
 #undef LAUNCH_TD
-}
-
-void td_xcd(const TdArgs& a, hipStream_t st) {
-  DBFS_CHECK(a.ctrl && a.level_direct && a.xcd_buf && a.xcd_fill && a.xcd_bins > 0 && a.xcd_bins <= kXcdMaxBins &&
-                 a.xcd_grid > 0,
-             "td_xcd: device loop, level bytes and the bin buffers");
-  const bool b32 = a.g.nnz <= (int64_t(1) << 32);
-  const unsigned g1 = static_cast<unsigned>(a.xcd_grid);
-  if (a.td_hub_vis && b32) td_xcd_bin_kernel<true, true><<<g1, kTdThreads, 0, st>>>(a);
-  else if (a.td_hub_vis) td_xcd_bin_kernel<true, false><<<g1, kTdThreads, 0, st>>>(a);
-  else if (b32) td_xcd_bin_kernel<false, true><<<g1, kTdThreads, 0, st>>>(a);
-  else td_xcd_bin_kernel<false, false><<<g1, kTdThreads, 0, st>>>(a);
-  // pass 2: four workgroups per CU, a multiple of the classes
-  const unsigned g2 = static_cast<unsigned>(std::max(kXcdClasses, 4 * device_cus() / kXcdClasses * kXcdClasses));
-  td_xcd_apply_kernel<<<g2, kBlock, 0, st>>>(a);
-}
-
-// Pass-1 workgroups of an XCD-binned level: the bin kernel's residency (the
-// filter variant's, the larger LDS footprint), a multiple of the classes.
-int64_t td_xcd_grid() {
-  static const int per_cu = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_xcd_bin_kernel<true, false>, kTdThreads, 0) != hipSuccess ||
-        n <= 0)
-      n = 1;
-    return n;
-  }();
-  return std::max<int64_t>(kXcdClasses, static_cast<int64_t>(per_cu) * device_cus() / kXcdClasses * kXcdClasses);
 }
 
 void td_binned(const BinArgs& a, hipStream_t st) {
