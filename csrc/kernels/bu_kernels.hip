@@ -413,8 +413,9 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.tot + 2 * blockIdx.x + 1),
                        static_cast<unsigned long long>(wd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(a.scan.ticket, 1u);
-    s_last = prev == gridDim.x - 1;
+    // (measured: a two-level ticket here, as the update's, is no faster --
+    // the workgroups of a bottom-up level do not arrive together)
+    s_last = atomicAdd(a.scan.ticket, 1u) == gridDim.x - 1;
     if (s_last) last_arriver_acquire();
   }
   __syncthreads();

@@ -284,6 +284,21 @@ __device__ __forceinline__ void direct_level_end(const DirectExchange& d, int64_
   level_finish_device(fin);
 }
 
+// Two-level last-arriver ticket (thread 0, the workgroup's stores drained):
+// the workgroups of a kFusedGroup group count on their group's ticket (its own
+// 128-B line), the group's last one re-zeroes it and counts on the level
+// ticket -- a grid of thousands of workgroups queues ~64 atomics per address
+// instead of all of them on one.  True in the level's last workgroup.
+__device__ __forceinline__ bool group_ticket_last(unsigned* group_ticket, unsigned* ticket) {
+  const unsigned grp = blockIdx.x / kFusedGroup;
+  const unsigned gsz = min(static_cast<unsigned>(kFusedGroup), gridDim.x - grp * kFusedGroup);
+  const unsigned ngroups = (gridDim.x + kFusedGroup - 1) / kFusedGroup;
+  unsigned* gt = group_ticket + grp * kBuQueueStride;
+  if (atomicAdd(gt, 1u) != gsz - 1) return false;
+  atomicExch(gt, 0u);
+  return atomicAdd(ticket, 1u) == ngroups - 1;
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap = 1 << 30) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;

@@ -54,16 +54,36 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
   const long long vlast = (b + 1 < nblocks) ? blk_vstart[b + 1] : q - 1;
   const int nv = static_cast<int>(vlast - v0 + 1);
 
+  // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.  Every
+  // entry's work-list words are loaded at once (a block of low-degree
+  // vertices -- a sparse level's tail -- covers up to EPB + 1 entries, which
+  // a strided loop fetched one dependent round trip after another), in
+  // flight across the barriers of the owner map's zeroing.
+  constexpr int kMapIter = (kTdEdgesPerBlock + kThreads) / kThreads;
+  long long qs[kMapIter];
+  BaseT qb[kMapIter];
+#pragma unroll
+  for (int k = 0; k < kMapIter; ++k) {
+    const int i = t + k * kThreads;
+    qs[k] = 0;
+    qb[k] = 0;
+    if (i < nv && i <= kTdEdgesPerBlock) {
+      qs[k] = qscan[v0 + i];
+      qb[k] = static_cast<BaseT>(qbase[v0 + i]);
+    }
+  }
   __syncthreads();  // LDS reuse across iterations
 #pragma unroll
   for (int k = 0; k < kItems; ++k) s_owner[k * kThreads + t] = 0;
   __syncthreads();
-  // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.
-  for (int i = t; i < nv && i <= kTdEdgesPerBlock; i += kThreads) {
-    const long long qs = qscan[v0 + i];
-    s_base[i] = static_cast<BaseT>(qbase[v0 + i]);
-    const long long p = (qs > e0 ? qs : e0) - e0;
-    if (p < cnt) s_owner[p] = i;
+#pragma unroll
+  for (int k = 0; k < kMapIter; ++k) {
+    const int i = t + k * kThreads;
+    if (i < nv && i <= kTdEdgesPerBlock) {
+      s_base[i] = qb[k];
+      const long long p = (qs[k] > e0 ? qs[k] : e0) - e0;
+      if (p < cnt) s_owner[p] = i;
+    }
   }
   __syncthreads();
   // inclusive max-scan over s_owner: thread t owns entries [t*ITEMS, (t+1)*ITEMS)
@@ -547,21 +567,6 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   a.rec->t1 = wall_clock64();
   *a.ctrl = c;
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
-}
-
-// Two-level last-arriver ticket (thread 0, the workgroup's stores drained):
-// the workgroups of a kFusedGroup group count on their group's ticket (its own
-// 128-B line), the group's last one re-zeroes it and counts on the level
-// ticket -- a grid of thousands of workgroups queues ~64 atomics per address
-// instead of all of them on one.  True in the level's last workgroup.
-__device__ __forceinline__ bool group_ticket_last(unsigned* group_ticket, unsigned* ticket) {
-  const unsigned grp = blockIdx.x / kFusedGroup;
-  const unsigned gsz = min(static_cast<unsigned>(kFusedGroup), gridDim.x - grp * kFusedGroup);
-  const unsigned ngroups = (gridDim.x + kFusedGroup - 1) / kFusedGroup;
-  unsigned* gt = group_ticket + grp * kBuQueueStride;
-  if (atomicAdd(gt, 1u) != gsz - 1) return false;
-  atomicExch(gt, 0u);
-  return atomicAdd(ticket, 1u) == ngroups - 1;
 }
 
 // Sparse top-down level read straight from the bitmap a bottom-up level left

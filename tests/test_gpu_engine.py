@@ -974,3 +974,4 @@ def test_sparse_level_from_bitmap_gpu(gpu_runtime, bits):
     for rank_out in run_virtual_ranks(3, body, device="hip"):
         for lv, s in zip(rank_out, srcs):
             assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
+
