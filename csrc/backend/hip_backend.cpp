@@ -235,6 +235,10 @@ class HipBackend final : public Backend {
   void list_scatter(const ListScatterArgs& a) override { on(); kern::list_scatter(a, st_); chk(); }
   bool device_checks_enabled() const override { return kern::checks_enabled(); }
   uint64_t take_device_check() override {
+    // (only the checked build has a word to read: otherwise no synchronize --
+    // a traversal's speculative trailing chain keeps draining while the next
+    // one is enqueued behind it)
+    if (!kern::checks_enabled()) return 0;
     synchronize();
     return kern::take_check_error();
   }

@@ -1240,6 +1240,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   // trailing chain writes: see the mailbox note above).
   if (xc || opt_.phase_timing) comm_.barrier();
   const auto t0 = std::chrono::steady_clock::now();
+  // (host timing: the host's time from the previous traversal's last stamp
+  // to this one's start, i.e. the gap between back-to-back runs)
+  static thread_local std::chrono::steady_clock::time_point prev_done{};
 
   begin_run_scratch();
   LevelCtrl init;
@@ -1356,6 +1359,8 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     return e && *e == '1';
   }();
   std::vector<std::pair<std::string, double>> htl;
+  if (host_timing && prev_done.time_since_epoch().count() != 0)
+    htl.emplace_back("since_prev_done", std::chrono::duration<double, std::micro>(t0 - prev_done).count());
   auto hmark = [&](const std::string& what) {
     if (host_timing)
       htl.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
@@ -1854,6 +1859,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   if (xc) res.ms = comm_.max_host(res.ms);
   if (host_timing) {
+    prev_done = t1;
     hmark("done");
     std::string line = "[host timing]";
     for (auto& [w, us] : htl) line += " " + w + "@" + std::to_string(static_cast<int>(us));
