@@ -80,6 +80,9 @@ def parse_args(argv=None):
                     help="real graph instead of RMAT: edge list / .mtx / binary .csr cache (e.g. soc-LiveJournal1; "
                          "no dataset ships with the repo and the GPU pool has no network)")
     ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--uniform", default=None, metavar="N:M",
+                    help="uniform-random graph of N vertices and M input edges generated on the device "
+                         "(e.g. 4847571:68993773, soc-LiveJournal1's size) instead of RMAT")
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--weak", action="store_true",
                     help="weak scaling: RMAT scale = --scale + log2(N) (per-GPU shard size fixed)")
@@ -210,6 +213,11 @@ def main(argv=None) -> int:
         # binary cache) and builds its shard on its GPU
         params = args.graph
         graph_name = os.path.basename(args.graph)
+    elif args.uniform:
+        un, _, um = args.uniform.partition(":")
+        params = dbfs.uniform_params(int(un), int(um), args.seed)
+        graph_name = f"uniform random {int(un)} V / {int(um)} E"
+        n_vertices, n_input_edges = params.n, params.m
     else:
         params = dbfs.rmat_params(scale, args.edge_factor, args.seed)
         graph_name = (f"RMAT-{scale} (Graph500 Kronecker a=.57 b=.19 c=.19, "
@@ -327,7 +335,7 @@ def main(argv=None) -> int:
         baseline = sum(r.edges for r in ref_res) / (ref_wall * 1e6)
         baseline_src = f"reference algorithm (--mode ref) measured live, {len(ref_roots)} roots, same graph"
         log(f"live baseline: {baseline:.4f} GTEPS")
-    if baseline is None and not args.graph and args.edge_factor == 16 and args.mode != "ref":
+    if baseline is None and not args.graph and not args.uniform and args.edge_factor == 16 and args.mode != "ref":
         baseline = MEASURED_REF_GTEPS.get((scale, nranks))
         if baseline:
             baseline_src = "reference algorithm (--mode ref) on MI355X, measured round 1 (BASELINE.md)"
@@ -352,6 +360,7 @@ def main(argv=None) -> int:
             "level_state_dtype": "uint8" if narrow else "int32",
             "value_int32_levels": (round(value_i32, 4) if value_i32 is not None else None),
             "data": (f"file {graph_name}, random roots" if args.graph
+                     else "synthetic (uniform random graph generated on device, random roots)" if args.uniform
                      else "synthetic (Graph500 RMAT generated on device, random roots)"),
             "config": {
                 "model": graph_name,

@@ -86,6 +86,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
+  else if (name == "xfuse_edges") o.xfuse_edges = static_cast<int64_t>(v);
+  else if (name == "bu_merge_visited") o.bu_merge_visited = v != 0;
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
@@ -131,6 +133,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
+          {"xfuse_edges", static_cast<double>(o.xfuse_edges)},
+          {"bu_merge_visited", o.bu_merge_visited ? 1.0 : 0.0},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
@@ -1137,6 +1141,10 @@ RunResult Engine::run_bitmap_device(int64_t source) {
   const bool lists_unlimited = list_max > 0 && list_max >= part_.part;
   const int64_t xsparse_lim = std::min<int64_t>(opt_.xsparse_edges, list_max);
   const bool counted = comm_.counted_lists();
+  // tiny sparse chains (several ranks, counted lists): live up to fuse_cap
+  const int64_t fuse_cap = xc && counted && opt_.xfuse_edges > 0 && 4 * opt_.xfuse_edges < list_max
+                               ? 4 * opt_.xfuse_edges
+                               : 0;
   if (list_max > 0 && list_stride_ < list_max + 1) {
     // owner lists: count word + list_max ids, the stride a multiple of 4 words
     // (16-byte pieces for the count-sized exchange); counts zeroed once here
@@ -1406,8 +1414,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
     if (xc && d == 'B') {
       if (!in_gathered)
         comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
-      // (with hubs, hub_gather merges the remote slices into visited)
-      if (gv.nhubs == 0) be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
+      // (bu_merge_visited: the remote slices merged into the replicated
+      // visited bitmap -- by hub_gather with hubs)
+      if (opt_.bu_merge_visited && gv.nhubs == 0) be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
     }
     // the frontier bitmap -> work list (set L & 1); with sparse levels also
     // its vertex map, and the bitmap is zeroed as read (a later sparse level
@@ -1497,21 +1506,42 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         // windows (direct), or a collective between them
         const size_t lcap = static_cast<size_t>(chain_cap > 0 ? chain_cap : list_max);
         const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
-        be_.td_sparse(sp);
-        if (!direct)
-          comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_), lcap);
-        sp.recv_lists = direct ? nullptr : dl_recv_lists_.data();
         sp.nranks = P;
-        sp.grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
+        const int64_t apply_grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
         // the level's end folded into the apply's last workgroup (no frontier
         // gather: that one is a bandwidth collective of its own)
         // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
         const bool cells_fit = g_.rows() < (int64_t(1) << 32) && g_.nnz() < (int64_t(1) << 40);
-        if (direct && opt_.direct_level_end && cells_fit && !enq_gather[L] && comm_.direct_level_end(2, &sp.end)) {
-          sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
-          level_ended = true;
+        const bool end_ok = direct && opt_.direct_level_end && cells_fit && !enq_gather[L];
+        // a tiny level (its chain capped at fuse_cap): td_sparse's last
+        // workgroup also runs the owner side and the level end -- one launch
+        // (the direct level end is taken in the same order as unfused)
+        static const bool dbg_no_fuse = std::getenv("DBFS_DBG_NO_FUSE") != nullptr;  // (debug, temporary)
+        sp.fuse_apply = !dbg_no_fuse && end_ok && fuse_cap > 0 && chain_cap > 0 && chain_cap <= fuse_cap;
+        if (sp.fuse_apply) {
+          sp.recv_lists = nullptr;
+          if (comm_.direct_level_end(2, &sp.end)) {
+            sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
+            level_ended = true;
+          } else {
+            sp.fuse_apply = false;  // (not taken: the level ends in its collective)
+          }
+          be_.td_sparse(sp);
+          sp.grid = apply_grid;
+          if (!level_ended) be_.td_sparse_apply(sp);
+        } else {
+          be_.td_sparse(sp);
+          if (!direct)
+            comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_),
+                                 lcap);
+          sp.recv_lists = direct ? nullptr : dl_recv_lists_.data();
+          if (end_ok && comm_.direct_level_end(2, &sp.end)) {
+            sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
+            level_ended = true;
+          }
+          sp.grid = apply_grid;
+          be_.td_sparse_apply(sp);
         }
-        be_.td_sparse_apply(sp);
       } else {
         be_.td_sparse(sp);
       }
@@ -1680,9 +1710,9 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         hg.frontier = frontier_[cur].data();
         hg.hub_front = hub_front_.data();
         hg.ctrl = ctrl_.data();
-        // several ranks: the gathered remote slices merged into the
-        // replicated visited bitmap in the same launch
-        if (xc) {
+        // several ranks, bu_merge_visited: the gathered remote slices merged
+        // into the replicated visited bitmap in the same launch
+        if (xc && opt_.bu_merge_visited) {
           hg.visited = visited_.data();
           hg.words = GW;
         }
@@ -1751,6 +1781,11 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         if (!exact && mf > static_cast<double>(xsparse_lim)) return 'T';
         if (exact && !lists_unlimited && mf > static_cast<double>(list_max)) return 'T';
         *cap = lists_unlimited ? 0 : list_max;
+        // tiny levels: chains capped at fuse_cap (fused into one launch on a
+        // direct transport; the same chains on every transport, so a shadow
+        // replay follows its recording)
+        if (fuse_cap > 0 && (exact ? mf <= static_cast<double>(fuse_cap) : mf <= static_cast<double>(opt_.xfuse_edges)))
+          *cap = fuse_cap;
         return 'S';
       }
       // fixed-size exchange (cap + 1 ids per peer): lists sized for the
@@ -1807,7 +1842,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       // dense top-down or bottom-up, one more level ahead
       enqueue_level(L + 1, enq_dir[L], 0, -1.0, enq_dir[L] == 'B');
     }
-    const volatile LevelMailbox* mb = wait_stamp(L - 1);
+    const volatile LevelMailbox* mb = nullptr;
+    try {
+      mb = wait_stamp(L - 1);
+    } catch (const Error& e) {
+      // which level, and the chains enqueued so far (level, form, cap)
+      std::string chains;
+      for (const auto& c : res.chains)
+        chains += " " + std::to_string(c.level) + c.form + ":" + std::to_string(c.cap);
+      throw Error(std::string(e.what()) + " (waiting for level " + std::to_string(L - 1) + "; chains" + chains + ")");
+    }
     hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {
       nlev = L;

@@ -458,6 +458,11 @@ struct TdSparseArgs {
   // kBuQueueStride apart, zero between launches).
   bool from_bits = false;
   int64_t words = 0;
+  // Several ranks, direct exchange with a folded level end, a tiny level:
+  // td_sparse's last workgroup publishes the lists and then runs the owner
+  // side itself (td_sparse_apply's work on one workgroup: nranks, end, fin
+  // set) -- one launch per level instead of two.
+  bool fuse_apply = false;
   unsigned* group_ticket = nullptr;
   // Several ranks: every target is claimed in the replicated `visited`
   // (fetch-or); an owned one is finished here, a remote one appended to its

@@ -230,6 +230,15 @@ struct EngineOptions {
   // 0 disables (dense top-down chains only).
   int64_t list_form_edges = int64_t(1) << 21;
   int64_t xsparse_edges = int64_t(1) << 20;
+  // ... levels predicted at <= xfuse_edges (a chain then live up to 4x that):
+  // with a direct exchange and a folded level end, td_sparse's last workgroup
+  // runs the owner side too (TdSparseArgs::fuse_apply: one launch per level);
+  // 0 disables.
+  int64_t xfuse_edges = 0;  // (pending GPU validation: 2^12)
+  // Several ranks, bottom-up levels: merge the gathered frontier into the
+  // replicated visited bitmap (the remote slices).  Only top-down levels read
+  // remote visited bits, as a filter: a stale one sends an id its owner drops.
+  bool bu_merge_visited = true;  // (pending GPU validation: false)
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)

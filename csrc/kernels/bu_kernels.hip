@@ -470,7 +470,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   }
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
-  for (int64_t i = threadIdx.x; i < hw; i += kThreads) s_hub[i] = a.hub_front[i];
+  stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
   __syncthreads();
   // (readfirstlane: the wave index, and the unit and word offsets derived
   // from it, are wave-uniform -- scalar registers, not vector ones)

@@ -299,6 +299,26 @@ __device__ __forceinline__ bool group_ticket_last(unsigned* group_ticket, unsign
   return atomicAdd(ticket, 1u) == ngroups - 1;
 }
 
+// n (<= kMaxWords) words of global memory staged into LDS by a workgroup of
+// kThreads: every thread's words loaded at once, then stored -- one round
+// trip instead of one per kThreads words (the loop's trip count is not known
+// to the compiler, so it would not overlap them).
+template <int kThreads, int kMaxWords>
+__device__ __forceinline__ void stage_words(word_t* s, const word_t* __restrict__ g, int64_t n) {
+  constexpr int kPer = (kMaxWords + kThreads - 1) / kThreads;
+  word_t v[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(k) * kThreads;
+    v[k] = i < n ? g[i] : 0ull;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(k) * kThreads;
+    if (i < n) s[i] = v[k];
+  }
+}
+
 inline unsigned grid_for(int64_t work, int64_t per_block, int64_t cap = 1 << 30) {
   int64_t g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
              (!a.ctrl || static_cast<double>(a.ctrl->vis_deg) >= a.td_hub_vis_frac * a.ctrl->total_directed);
     if (filter) {
       const int64_t hw = (a.g.td_nhubs + kWordBits - 1) / kWordBits;
-      for (int64_t i = t; i < hw; i += kThreads) s_hubvis[i] = a.td_hub_vis[i];
+      stage_words<kThreads, kTdMaxHubs / kWordBits>(s_hubvis, a.td_hub_vis, hw);
       // (td_block_owner_map starts with a barrier)
     }
   }
@@ -458,6 +458,109 @@ __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, 
   if (bad) atomicAdd(err, bad);
 }
 
+// Several ranks, after the list exchange: the ids the other ranks claimed for
+// this rank's vertices (recv_lists) are claimed here (fetch-or on the owned
+// slice of `visited`; a vertex sent by several ranks, or claimed by this
+// rank's own td_sparse, is settled once) and settled like td_sparse's owned
+// claims; the last workgroup writes the level's local totals and zeroes the
+// send lists' counts.  The lists' counts are loaded together (one per
+// thread: they sit a stride apart, cold) and their entries form one index
+// space the grid strides over.
+// (bx / gx: this workgroup and the workgroups taking part -- the kernel's, or
+// the one last workgroup of a fused tiny level, TdSparseArgs::fuse_apply)
+template <int kThreads>
+__device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx) {
+  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  __shared__ int s_last;
+  __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
+  __shared__ const vid_t* s_src[kern::kMaxPeers];
+  __shared__ uint64_t s_cnt[kern::kMaxPeers];
+  __shared__ uint64_t s_xend[2 * kern::kMaxPeers];
+  // a direct exchange: the peers' cells (their counts) first, live chain or
+  // not (every rank waits for every exchange: the window slots' reuse protocol)
+  const bool dx = a.direct.active;
+  if (dx && direct_wait(a.direct, s_cnt, nullptr) != kWaitOk) return;
+  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if (a.end.active && bx == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin, s_xend);
+    return;
+  }
+  const int t = threadIdx.x;
+  if (t < kWave) {
+    long long n = 0;
+    if (t < a.nranks) {
+      const vid_t* src = dx ? a.direct.table->src[t] : a.recv_lists + static_cast<int64_t>(t) * a.list_stride;
+      s_src[t] = src;
+      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
+    }
+    DBFS_DCHECK(n < a.list_stride, 5, n);
+    const long long incl = wave_incl_scan(n);
+    if (t < a.nranks) s_end[t] = incl;
+  }
+  __syncthreads();
+  const long long total = s_end[a.nranks - 1];
+  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
+  // only the workgroups with entries take part (at least one, for the finish)
+  const int64_t need = (total + span - 1) / span;
+  const unsigned active = static_cast<unsigned>(need < 1 ? 1 : (need < gx ? need : gx));
+  if (bx >= active) return;
+  for (int64_t i0 = static_cast<int64_t>(bx) * span; i0 < total; i0 += static_cast<int64_t>(active) * span) {
+    vid_t v[kItems];
+    word_t seen[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
+      v[k] = 0u;
+      if (j < total) {
+        int r = 0;
+        while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
+        const long long before = r > 0 ? s_end[r - 1] : 0;
+        const vid_t* src = s_src[r] + 1 + (j - before);
+        v[k] = dx ? sys_load_u32(src) : *(const gu32*)(src);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      seen[k] = i0 + static_cast<int64_t>(k) * kThreads + t < total ? a.visited[v[k] >> 6] : ~0ull;
+    unsigned claimed = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const word_t bit = 1ull << (v[k] & 63);
+      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
+    }
+    sparse_settle<kItems>(a, v, claimed);
+  }
+  __syncthreads();
+  if (t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (one workgroup -- a fused tiny level's: trivially the last, no ticket)
+    const unsigned prev = gx == 1 ? 0u : atomicAdd(a.ticket, 1u);
+    s_last = (prev == active - 1) ? 1 : 0;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the send lists were read by the exchange (stream-ordered before this
+  // kernel): their counts restart from zero for the next list level (a
+  // direct exchange's publisher zeroed them)
+  if (!dx && t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
+  __shared__ long long s_tot[2];
+  if (t == 0) {
+    long long cnt = 0, deg = 0;
+    sparse_totals(a, cnt, deg);
+    s_tot[0] = cnt;
+    s_tot[1] = deg;
+  }
+  if (!a.end.active) return;
+  __syncthreads();
+  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
+}
+
+template <int kThreads>
+__global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
+  sparse_apply<kThreads>(a, blockIdx.x, gridDim.x);
+}
+
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
 // claimed vertex is finished in place (level, frontier bit, output entry), so
 // the level is one launch (one rank); with several ranks remote claims go to
@@ -475,7 +578,11 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   // uniform: the whole grid returns, no workgroup takes a ticket (a direct
   // exchange still publishes, empty)
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
-    if (dx && blockIdx.x == 0) direct_publish(a.direct, a.lists, a.list_stride, false);
+    if (dx && blockIdx.x == 0) {
+      direct_publish(a.direct, a.lists, a.list_stride, false);
+      // (the fused owner side waits for the peers all the same: a collective)
+      if (a.fuse_apply) sparse_apply<kThreads>(a, 0, 1);
+    }
     return;
   }
   if (a.first) stamp_level_start(a.ctrl);
@@ -543,7 +650,12 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       if (s_last) *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
     }
     __syncthreads();
-    if (s_last) direct_publish(a.direct, a.lists, a.list_stride, true);
+    if (!s_last) return;
+    direct_publish(a.direct, a.lists, a.list_stride, true);
+    // a tiny level (fuse_apply): this workgroup is also the owner side --
+    // the peers' lists, their claims and the folded level end -- instead of
+    // a td_sparse_apply launch
+    if (a.fuse_apply) sparse_apply<kThreads>(a, 0, 1);
     return;
   }
 
@@ -587,7 +699,10 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   __shared__ int s_last;
   const bool dx = a.lists && a.direct.active;
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
-    if (dx && blockIdx.x == 0) direct_publish(a.direct, a.lists, a.list_stride, false);
+    if (dx && blockIdx.x == 0) {
+      direct_publish(a.direct, a.lists, a.list_stride, false);
+      if (a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);  // (a collective: as td_sparse)
+    }
     return;
   }
   stamp_level_start(a.ctrl);
@@ -701,6 +816,8 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
     // the counts and flags published here)
     if (t == 0) *a.ticket = 0u;
     if (dx) direct_publish(a.direct, a.lists, a.list_stride, true);
+    // a tiny level (fuse_apply): the owner side and the level end here too
+    if (dx && a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);
     return;
   }
   if (t != 0) return;
@@ -714,100 +831,6 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
 }
 
-// Several ranks, after the list exchange: the ids the other ranks claimed for
-// this rank's vertices (recv_lists) are claimed here (fetch-or on the owned
-// slice of `visited`; a vertex sent by several ranks, or claimed by this
-// rank's own td_sparse, is settled once) and settled like td_sparse's owned
-// claims; the last workgroup writes the level's local totals and zeroes the
-// send lists' counts.  The lists' counts are loaded together (one per
-// thread: they sit a stride apart, cold) and their entries form one index
-// space the grid strides over.
-template <int kThreads>
-__global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
-  constexpr int kItems = kTdEdgesPerBlock / kThreads;
-  __shared__ int s_last;
-  __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
-  __shared__ const vid_t* s_src[kern::kMaxPeers];
-  __shared__ uint64_t s_cnt[kern::kMaxPeers];
-  __shared__ uint64_t s_xend[2 * kern::kMaxPeers];
-  // a direct exchange: the peers' cells (their counts) first, live chain or
-  // not (every rank waits for every exchange: the window slots' reuse protocol)
-  const bool dx = a.direct.active;
-  if (dx && direct_wait(a.direct, s_cnt, nullptr) != kWaitOk) return;
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
-    // a folded level end is a collective: it runs on a no-op chain too
-    if (a.end.active && blockIdx.x == 0) direct_level_end(a.end, a.stats[2], a.stats[3], a.stats, a.fin, s_xend);
-    return;
-  }
-  const int t = threadIdx.x;
-  if (t < kWave) {
-    long long n = 0;
-    if (t < a.nranks) {
-      const vid_t* src = dx ? a.direct.table->src[t] : a.recv_lists + static_cast<int64_t>(t) * a.list_stride;
-      s_src[t] = src;
-      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
-    }
-    DBFS_DCHECK(n < a.list_stride, 5, n);
-    const long long incl = wave_incl_scan(n);
-    if (t < a.nranks) s_end[t] = incl;
-  }
-  __syncthreads();
-  const long long total = s_end[a.nranks - 1];
-  const int64_t span = static_cast<int64_t>(kThreads) * kItems;
-  // only the workgroups with entries take part (at least one, for the finish)
-  const int64_t need = (total + span - 1) / span;
-  const unsigned active = static_cast<unsigned>(need < 1 ? 1 : (need < gridDim.x ? need : gridDim.x));
-  if (blockIdx.x >= active) return;
-  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * span; i0 < total; i0 += static_cast<int64_t>(active) * span) {
-    vid_t v[kItems];
-    word_t seen[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      const int64_t j = i0 + static_cast<int64_t>(k) * kThreads + t;
-      v[k] = 0u;
-      if (j < total) {
-        int r = 0;
-        while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
-        const long long before = r > 0 ? s_end[r - 1] : 0;
-        const vid_t* src = s_src[r] + 1 + (j - before);
-        v[k] = dx ? sys_load_u32(src) : *(const gu32*)(src);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-      seen[k] = i0 + static_cast<int64_t>(k) * kThreads + t < total ? a.visited[v[k] >> 6] : ~0ull;
-    unsigned claimed = 0;
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-      const word_t bit = 1ull << (v[k] & 63);
-      if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
-    }
-    sparse_settle<kItems>(a, v, claimed);
-  }
-  __syncthreads();
-  if (t == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(a.ticket, 1u);
-    s_last = (prev == active - 1) ? 1 : 0;
-    if (s_last) last_arriver_acquire();
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // the send lists were read by the exchange (stream-ordered before this
-  // kernel): their counts restart from zero for the next list level (a
-  // direct exchange's publisher zeroed them)
-  if (!dx && t < a.nranks) a.lists[static_cast<int64_t>(t) * a.list_stride] = 0u;
-  __shared__ long long s_tot[2];
-  if (t == 0) {
-    long long cnt = 0, deg = 0;
-    sparse_totals(a, cnt, deg);
-    s_tot[0] = cnt;
-    s_tot[1] = deg;
-  }
-  if (!a.end.active) return;
-  __syncthreads();
-  direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
-}
 
 // ---------------------------------------------------------------------------
 // Binned top-down level (BinArgs).  Count and fill passes walk the same edge

@@ -217,6 +217,20 @@ def test_bench_graph_file_cpu(tmp_path):
     assert rec["data"].startswith("file g.txt") and rec["vs_baseline"] is None
 
 
+def test_bench_uniform_graph_cpu():
+    # --uniform N:M: a uniform-random graph generated like RMAT (the
+    # soc-LiveJournal1-sized stand-in without the 1 GB text file); no RMAT
+    # baseline applies to it
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--uniform", "3001:20000",
+                          "--mode", "td", "--steps", "2", "--warmup", "1", "--no-int32-pass"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["config"]["vertices"] == 3001 and rec["config"]["input_edges"] == 20000
+    assert rec["data"].startswith("synthetic (uniform") and rec["vs_baseline"] is None
+    assert rec["validated"] is True
+
+
 @pytest.mark.parametrize("nproc,mode", [(2, "do"), (3, "ref")])
 def test_bench_torchrun_multiprocess_cpu(nproc, mode):
     """The driver's N>1 launch (torch.distributed.run, one process per rank,

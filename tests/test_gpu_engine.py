@@ -975,3 +975,17 @@ def test_sparse_level_from_bitmap_gpu(gpu_runtime, bits):
         for lv, s in zip(rank_out, srcs):
             assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
 
+
+
+@pytest.mark.parametrize("P", [4, 8])
+def test_shadow_replay_direct_gpu(P):
+    """Shadow ranks on the GPU: rank r of a P-rank traversal (recorded over
+    virtual ranks) replayed alone through the direct-exchange paths -- sparse
+    levels' lists read in place, tiny levels fused into one launch
+    (xfuse_edges), folded level ends -- computes the recorded levels."""
+    from distributed_cuda_bfs_amd.parallel.shadow import shadow_ranks
+
+    p = dbfs.rmat_params(17, 16, 5)
+    runs = shadow_ranks(p, P, [0, P - 1], [3, 777, 40000], mode="do", device="hip")
+    for s in runs:
+        assert s.exact, (s.rank, s.levels, s.recorded_levels)
