@@ -177,26 +177,69 @@ inline vid_t parse_token(const char* d, size_t e, size_t& p, int64_t n, int64_t 
   return (id >= 0 && id < n) ? static_cast<vid_t>(id) : kBadId;
 }
 
-// A thread's tokens (reference format) or entry pairs u0 v0 u1 v1 ...
-// (MatrixMarket); kBadId marks a malformed or out-of-range id, an error only
-// if one of the m edges uses it.
-struct Piece {
-  std::vector<vid_t> tok;
+// Pages of [b, e) that lie wholly inside it and that a parse has passed:
+// dropped from this process (MAP_PRIVATE, never written, so a later touch
+// just faults the page back in from the page cache).  Keeps the resident set
+// to the parsed arrays plus a window per thread, not the whole byte range.
+struct PageDropper {
+  const char* d;
+  size_t pg, lo, done;
+  PageDropper(const char* data, size_t b) : d(data), pg(static_cast<size_t>(::sysconf(_SC_PAGESIZE))) {
+    lo = (b + pg - 1) / pg * pg;  // first page wholly inside the range
+    done = lo;
+  }
+  void passed(size_t p, bool final = false) {
+    const size_t hi = p / pg * pg;
+    if (hi > done && (final || hi - done >= (size_t(64) << 20))) {
+      ::madvise(const_cast<char*>(d) + done, hi - done, MADV_DONTNEED);
+      done = hi;
+    }
+  }
 };
 
-void parse_tokens(const char* d, size_t b, size_t e, int64_t n, Piece& out) {
+// Reference-format tokens of [b, e): count them, then (second pass) hand
+// token j of the range to emit(j, id) (kBadId marks a malformed or
+// out-of-range id, an error only if one of the m edges uses it).
+int64_t count_tokens(const char* d, size_t b, size_t e) {
+  PageDropper drop(d, b);
+  int64_t c = 0;
+  bool prev_space = true;
+  for (size_t p0 = b; p0 < e; p0 += size_t(1) << 20) {
+    const size_t p1 = std::min(e, p0 + (size_t(1) << 20));
+    for (size_t p = p0; p < p1; ++p) {
+      const bool sp = is_space(d[p]);
+      c += prev_space && !sp;
+      prev_space = sp;
+    }
+    drop.passed(p1);
+  }
+  drop.passed(e, true);
+  return c;
+}
+
+template <class Emit>
+void parse_tokens(const char* d, size_t b, size_t e, int64_t n, Emit&& emit) {
+  PageDropper drop(d, b);
   size_t p = b;
+  int64_t j = 0;
   while (p < e) {
     while (p < e && is_space(d[p])) ++p;
     if (p >= e) break;
     bool mal = false;
-    out.tok.push_back(parse_token(d, e, p, n, 0, mal));
+    emit(j++, parse_token(d, e, p, n, 0, mal));
     while (p < e && !is_space(d[p])) ++p;
+    if ((j & 0xFFFF) == 0) drop.passed(p);
   }
+  drop.passed(e, true);
 }
 
-void parse_mtx_lines(const char* d, size_t b, size_t e, int64_t n, Piece& out) {
+// MatrixMarket entry lines of [b, e) as pairs (two tokens each); blank and
+// '%' lines skipped.  emit == nullptr-like counting when Count is true.
+template <bool Count, class Emit>
+int64_t parse_mtx_lines(const char* d, size_t b, size_t e, int64_t n, Emit&& emit) {
+  PageDropper drop(d, b);
   size_t p = b;
+  int64_t j = 0;
   while (p < e) {
     size_t q = p;
     while (q < e && (d[q] == ' ' || d[q] == '\t' || d[q] == '\r')) ++q;
@@ -206,16 +249,22 @@ void parse_mtx_lines(const char* d, size_t b, size_t e, int64_t n, Piece& out) {
       p = q + 1;
       continue;
     }
-    bool mal = false;
-    const vid_t a = parse_token(d, e, q, n, 1, mal);
-    while (q < e && (d[q] == ' ' || d[q] == '\t')) ++q;
-    vid_t c = kBadId;
-    if (q < e && d[q] != '\n' && d[q] != '\r') c = parse_token(d, e, q, n, 1, mal);
-    out.tok.push_back(a);
-    out.tok.push_back(c);
+    if constexpr (!Count) {
+      bool mal = false;
+      const vid_t a = parse_token(d, e, q, n, 1, mal);
+      while (q < e && (d[q] == ' ' || d[q] == '\t')) ++q;
+      vid_t c = kBadId;
+      if (q < e && d[q] != '\n' && d[q] != '\r') c = parse_token(d, e, q, n, 1, mal);
+      emit(j, a);
+      emit(j + 1, c);
+    }
+    if ((j & 0xFFFF) == 0) drop.passed(q);
+    j += 2;
     while (q < e && d[q] != '\n') ++q;  // value column(s)
     p = q + 1;
   }
+  drop.passed(e, true);
+  return j;
 }
 
 }  // namespace
@@ -258,25 +307,30 @@ EdgeShard read_edge_shard(const std::string& path, int rank, int nranks, const H
 
   int T = threads > 0 ? threads : static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
   T = static_cast<int>(std::min<size_t>(static_cast<size_t>(T), std::max<size_t>(1, (re - rb) / 4096)));
-  std::vector<Piece> pieces(static_cast<size_t>(T));
-  {
-    std::vector<std::thread> th;
-    std::vector<size_t> cuts(static_cast<size_t>(T) + 1);
-    for (int t = 0; t <= T; ++t) {
-      const size_t pos = rb + static_cast<size_t>((static_cast<unsigned __int128>(re - rb) * static_cast<uint64_t>(t)) /
-                                                   static_cast<uint64_t>(T));
-      cuts[t] = t == 0 ? rb : t == T ? re : std::min(re, align_cut(d, size, h.body, pos, lines));
-    }
-    for (int t = 0; t < T; ++t)
-      th.emplace_back([&, t] {
-        const size_t b = std::min(cuts[t], re), e = std::max(b, std::min(cuts[t + 1], re));
-        if (lines) parse_mtx_lines(d, b, e, h.n, pieces[t]);
-        else parse_tokens(d, b, e, h.n, pieces[t]);
-      });
-    for (auto& x : th) x.join();
+  std::vector<size_t> cuts(static_cast<size_t>(T) + 1);
+  for (int t = 0; t <= T; ++t) {
+    const size_t pos = rb + static_cast<size_t>((static_cast<unsigned __int128>(re - rb) * static_cast<uint64_t>(t)) /
+                                                 static_cast<uint64_t>(T));
+    cuts[t] = t == 0 ? rb : t == T ? re : std::min(re, align_cut(d, size, h.body, pos, lines));
   }
-  int64_t ntok = 0;
-  for (const Piece& pc : pieces) ntok += static_cast<int64_t>(pc.tok.size());
+  auto piece = [&](int t, size_t& b, size_t& e) {
+    b = std::min(cuts[t], re);
+    e = std::max(b, std::min(cuts[t + 1], re));
+  };
+  auto parallel = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { fn(t); });
+    for (auto& x : th) x.join();
+  };
+  // pass 1: token (entry-pair) counts per thread -- a byte scan, no storage
+  std::vector<int64_t> tcount(static_cast<size_t>(T) + 1, 0);
+  parallel([&](int t) {
+    size_t b, e;
+    piece(t, b, e);
+    tcount[t + 1] = lines ? parse_mtx_lines<true>(d, b, e, h.n, [](int64_t, vid_t) {}) : count_tokens(d, b, e);
+  });
+  for (int t = 0; t < T; ++t) tcount[t + 1] += tcount[t];
+  const int64_t ntok = tcount[T];
   // token (or entry-pair) counts of every rank -> this rank's global position
   const std::vector<int64_t> counts = allgather(ntok);
   int64_t before = 0, total = 0;
@@ -296,43 +350,43 @@ EdgeShard read_edge_shard(const std::string& path, int rank, int nranks, const H
   s.first_edge = g0 / 2;
   s.u.resize(static_cast<size_t>(my_edges));
   s.v.resize(static_cast<size_t>(my_edges));
-  // walk the pieces' tokens in order
-  int64_t g = before, e = 0;
-  vid_t pending = 0;
-  bool have_pending = false;
-  int64_t bad_edge = -1;
-  for (const Piece& pc : pieces) {
-    for (vid_t x : pc.tok) {
-      if (g >= g0 && g < g_end) {
-        if (!have_pending) {
-          pending = x;
-          have_pending = true;
-        } else {
-          if ((pending == kBadId || x == kBadId) && bad_edge < 0) bad_edge = e;
-          s.u[e] = pending;
-          s.v[e] = x;
-          ++e;
-          have_pending = false;
-        }
-      }
-      ++g;
-    }
-  }
-  if (have_pending) {
+  // pass 2: every thread parses its piece straight into u / v at its tokens'
+  // global positions (no per-thread token vectors, no copy)
+  std::vector<int64_t> tbad(static_cast<size_t>(T), INT64_MAX);
+  vid_t* const U = s.u.data();
+  vid_t* const V = s.v.data();
+  parallel([&](int t) {
+    size_t b, e;
+    piece(t, b, e);
+    const int64_t base = before + tcount[t];
+    int64_t bad = INT64_MAX;
+    auto emit = [&](int64_t j, vid_t x) {
+      const int64_t g = base + j;
+      if (g < g0 || g >= g_end) return;
+      const int64_t k = g - g0;
+      (k & 1 ? V : U)[k >> 1] = x;
+      if (x == kBadId && (k >> 1) < bad) bad = k >> 1;
+    };
+    if (lines) parse_mtx_lines<false>(d, b, e, h.n, emit);
+    else parse_tokens(d, b, e, h.n, emit);
+    tbad[t] = bad;
+  });
+  int64_t bad_edge = *std::min_element(tbad.begin(), tbad.end());
+  if (bad_edge == INT64_MAX) bad_edge = -1;
+  int64_t e = my_edges;
+  if (g_end > g0 && ((g_end - g0) & 1)) {
     // the second token of the last edge lies past the range: read ahead
-    size_t p = re;
-    vid_t x = kBadId;
     if (lines) {
       // (MatrixMarket entries are whole lines: a pair never straddles a cut)
       throw Error("internal: MatrixMarket entry split across ranks in " + path);
     }
+    size_t p = re;
+    vid_t x = kBadId;
     while (p < size && is_space(d[p])) ++p;
     bool mal = false;
     if (p < size) x = parse_token(d, size, p, h.n, 0, mal);
-    if ((pending == kBadId || x == kBadId) && bad_edge < 0) bad_edge = e;
-    s.u[e] = pending;
-    s.v[e] = x;
-    ++e;
+    if (x == kBadId && (bad_edge < 0 || my_edges - 1 < bad_edge)) bad_edge = my_edges - 1;
+    V[my_edges - 1] = x;
   }
   DBFS_CHECK(e == my_edges, "internal: edge count mismatch in the sharded reader");
   // agree on errors (global edge index of the first bad edge)
