@@ -439,17 +439,32 @@ class CpuBackend final : public Backend {
       return;
     }
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    // hub-cut level (as the HIP kernel): claimed vertices join the output
+    // unscanned, the others find parents among the frontier hubs only
+    const bool cut = a.cut_edges > 0 && *a.cut_flag;
     const int64_t nunits = div_up(a.words, kUnitWords);
     for (int64_t u = 0; u < nunits; ++u) {
       int64_t cnt = 0, deg = 0;
       for (int64_t w = u * kUnitWords; w < std::min<int64_t>(a.words, (u + 1) * kUnitWords); ++w) {
-        word_t out = 0;
-        const word_t vis = a.visited[w];
+        // claimed: unvisited with this level's level byte already
+        word_t pw = 0;
+        if (cut)
+          for (int b = 0; b < 64 && w * 64 + b < a.g.rows; ++b)
+            if (!((a.visited[w] >> b) & 1ull) &&
+                a.level8[w * 64 + b] == static_cast<uint8_t>(a.narrow_base + std::min<lvl_t>(a.new_level, kNarrowMaxLevel + 1)))
+              pw |= 1ull << b;
+        word_t out = pw;
+        const word_t vis = a.visited[w] | pw;
+        for (word_t m = pw; m; m &= m - 1) {
+          const int64_t v = w * 64 + __builtin_ctzll(m);
+          ++cnt;
+          deg += a.g.row_off[v + 1] - a.g.row_off[v];
+        }
         for (int b = 0; b < 64; ++b) {
           const int64_t v = w * 64 + b;
           if (v >= a.g.rows || ((vis >> b) & 1ull)) continue;
           for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
-            if (test_bit(a.frontier, a.g.col[e])) {
+            if (test_bit(a.frontier, a.g.col[e]) && (!cut || test_bit(a.g.hub_bits, a.g.col[e]))) {
               out |= 1ull << b;
               put_level(a.level, a.level8, v, a.new_level, a.narrow_base);
               ++cnt;
@@ -661,12 +676,36 @@ class CpuBackend final : public Backend {
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     for (int64_t w = 0; w < div_up(a.g.nhubs, 64); ++w) {
       word_t m = 0;
-      for (int b = 0; b < 64 && w * 64 + b < a.g.nhubs; ++b)
-        if (test_bit(a.frontier, a.g.hub_vertex[w * 64 + b])) m |= 1ull << b;
+      int64_t d = 0;
+      for (int b = 0; b < 64 && w * 64 + b < a.g.nhubs; ++b) {
+        const vid_t hv = a.g.hub_vertex[w * 64 + b];
+        if (test_bit(a.frontier, hv)) {
+          m |= 1ull << b;
+          if (a.cut_part) d += a.g.row_off[hv + 1] - a.g.row_off[hv];
+        }
+      }
       a.hub_front[w] = m;
+      if (a.cut_part) a.cut_part[w] = d;
+    }
+    if (a.cut_part) {
+      int64_t hub_edges = 0;
+      for (int64_t w = 0; w < div_up(a.g.nhubs, 64); ++w) hub_edges += a.cut_part[w];
+      *a.cut_flag = a.ctrl->m_f - hub_edges <= a.cut_edges ? 1 : 0;
     }
     if (a.visited)
       for (int64_t i = 0; i < a.words; ++i) a.visited[i] |= a.frontier[i];
+  }
+  void bu_cut_prep(const BuArgs& a) override {
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    if (!*a.cut_flag) return;
+    for (int64_t w = 0; w < a.words; ++w)
+      for (word_t m = a.frontier[w] & ~a.g.hub_bits[w]; m; m &= m - 1) {
+        const int64_t v = w * 64 + __builtin_ctzll(m);
+        for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
+          const vid_t t = a.g.col[e];
+          if (!test_bit(a.visited, t)) put_level(nullptr, a.level8, t, a.new_level, a.narrow_base);
+        }
+      }
   }
   void hub_apply(const HubApplyArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

@@ -88,6 +88,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "xfuse_edges") o.xfuse_edges = static_cast<int64_t>(v);
   else if (name == "bu_merge_visited") o.bu_merge_visited = v != 0;
+  else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
+  else if (name == "bu_cut_mf") o.bu_cut_mf = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
@@ -135,6 +137,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
           {"xfuse_edges", static_cast<double>(o.xfuse_edges)},
           {"bu_merge_visited", o.bu_merge_visited ? 1.0 : 0.0},
+          {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
+          {"bu_cut_mf", static_cast<double>(o.bu_cut_mf)},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
@@ -302,6 +306,7 @@ ShardView DeviceGraph::view() const {
   v.hub_vertex = hub_vertex_.data();
   v.nhubs = nhubs_;
   v.hub_col = hub_col_.data();
+  v.hub_bits = hub_bits_.data();
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -370,6 +375,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
   nhubs_ = 0;
   hub_vertex_.reset();
+  hub_bits_.reset();
   hub_col_.reset();
   td_col_.reset();
   td_hub_vertex_.reset();
@@ -385,6 +391,15 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(max_hubs, 1)));
       nhubs_ = be_->select_hubs(all.data(), nall, min_deg, hub_vertex_.data(), hub_idx.data());
       DBFS_CHECK(nhubs_ >= 0 && nhubs_ <= max_hubs, "hub selection exceeded its capacity");
+      if (nhubs_ > 0) {
+        // hub membership bitmap over all vertices (hub-cut bottom-up levels)
+        std::vector<vid_t> hv(static_cast<size_t>(nhubs_));
+        be_->to_host(hv.data(), hub_vertex_.data(), hv.size() * sizeof(vid_t));
+        std::vector<word_t> bits(static_cast<size_t>(part_.global_words()), 0ull);
+        for (vid_t v : hv) bits[v >> 6] |= 1ull << (v & 63);
+        hub_bits_ = DBuf<word_t>(*be_, bits.size());
+        be_->to_device(hub_bits_.data(), bits.data(), bits.size() * sizeof(word_t));
+      }
       // bottom-up's hub-encoded adjacency copy (one more nnz x 4 B: RMAT-26
       // 8.6 GB of the 288 GB HBM3E)
       hub_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
@@ -1716,8 +1731,33 @@ RunResult Engine::run_bitmap_device(int64_t source) {
           hg.visited = visited_.data();
           hg.words = GW;
         }
+        // one rank, a first bottom-up level: the hub cut (decided on the
+        // device from the frontier hubs' degrees hub_gather sums), enqueued
+        // for levels predicted at <= bu_cut_mf frontier edges (a first
+        // bottom-up level's non-hub frontier edges grow with its frontier:
+        // the larger ones never cut, and skip its launches)
+        const bool cut = !xc && run_narrow_ && opt_.bu_cut_edges > 0 && pf != 'B' &&
+                         (mf_hint < 0 || mf_hint <= static_cast<double>(opt_.bu_cut_mf)) && gv.hub_bits && gv.nz_rec && gv.unit_base &&
+                         gv.nz_pref && gv.nz_row_off && gv.head && ba.zdeg;
+        if (cut) {
+          if (!cut_part_.data()) {
+            cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(gv.nhubs, int64_t(64))));
+            cut_flag_ = DBuf<int>(be_, 1);
+            cut_ticket_ = DBuf<unsigned>(be_, 1);
+            be_.memset_async(cut_ticket_.data(), 0, cut_ticket_.bytes());
+          }
+          hg.cut_part = cut_part_.data();
+          hg.cut_edges = opt_.bu_cut_edges;
+          hg.cut_flag = cut_flag_.data();
+          hg.cut_ticket = cut_ticket_.data();
+        }
         be_.hub_gather(hg);
         ba.hub_front = hub_front_.data();
+        if (cut) {
+          ba.cut_edges = opt_.bu_cut_edges;
+          ba.cut_flag = cut_flag_.data();
+          be_.bu_cut_prep(ba);
+        }
       }
       if (opt_.bu_fused_scan) {
         // the level's totals (and with one rank its finish) in the

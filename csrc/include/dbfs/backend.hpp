@@ -75,6 +75,10 @@ struct ShardView {
   const vid_t* td_col = nullptr;
   const vid_t* td_hub_vertex = nullptr;
   int64_t td_nhubs = 0;
+  // One rank with hubs: bit v set when vertex v is a hub (the hubs are every
+  // vertex of degree >= the hub threshold, so a hub-first row's hubs are a
+  // prefix of it).  Read by the hub-cut bottom-up level (BuArgs::cut_edges).
+  const word_t* hub_bits = nullptr;
 };
 
 // At most kTdMaxHubs top-down hubs (their visited bits, 8 KiB, sit in LDS
@@ -664,6 +668,18 @@ struct BuArgs {
   // workgroup (Comm::direct_level_end; no frontier gather), as td_sparse_apply
   DirectExchange end;
   LevelFinishArgs fin;
+  // Hub-cut level (one rank, narrow levels, hub kernels with packed records,
+  // cut_edges > 0; bu_cut_prep before it): when the level's frontier edges
+  // outside the hubs -- ctrl->m_f minus the frontier hubs' degrees -- are at
+  // most cut_edges, hub_gather sets *cut_flag and bu_cut_prep writes the level
+  // byte of the non-hub frontier vertices' unvisited neighbours (top-down);
+  // every row scan of the level then stops at its first non-hub neighbour (a
+  // hub-first row's later neighbours cannot be in the frontier: rows with a
+  // non-hub frontier neighbour were claimed).  Claimed vertices (unvisited,
+  // level byte = this level) skip the scan and join the output with the
+  // found ones.  *cut_flag = 0: a plain level.
+  int64_t cut_edges = 0;
+  int* cut_flag = nullptr;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the
@@ -702,6 +718,13 @@ struct HubGatherArgs {
   // slices into the replicated visited bitmap) in the same launch
   word_t* visited = nullptr;
   int64_t words = 0;
+  // hub-cut levels (BuArgs::cut_edges): cut_part[b] = the summed degrees of
+  // the frontier hubs of workgroup b (kBlock hubs each); the last workgroup
+  // (cut_ticket, zero between levels) stores the decision in *cut_flag
+  int64_t* cut_part = nullptr;
+  int64_t cut_edges = 0;
+  int* cut_flag = nullptr;
+  unsigned* cut_ticket = nullptr;
 };
 
 // Bits of the owned slice for vertices with degree 0 or beyond the shard
@@ -891,6 +914,9 @@ class Backend {
   virtual void list_scatter(const ListScatterArgs& a) = 0;
   virtual void bu_step(const BuArgs& a) = 0;
   virtual void hub_gather(const HubGatherArgs& a) = 0;
+  // Hub-cut level's top-down part (BuArgs::cut_edges): the unvisited
+  // neighbours of the frontier's non-hub vertices claimed into a.pre.
+  virtual void bu_cut_prep(const BuArgs& a) = 0;
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their

@@ -86,6 +86,7 @@ class DeviceGraph {
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
+  DBuf<word_t> hub_bits_;  // global vertex bitmap of the hubs
   int64_t td_nhubs_ = 0;
   DBuf<eid_t> nz_pref_, nz_row_off_;
   DBuf<NzRec> nz_rec_;      // packed view records (empty when a unit spans >= 2^32 edges)
@@ -239,6 +240,16 @@ struct EngineOptions {
   // replicated visited bitmap (the remote slices).  Only top-down levels read
   // remote visited bits, as a filter: a stale one sends an id its owner drops.
   bool bu_merge_visited = true;  // (pending GPU validation: false)
+  // One rank, device loop, hubs: a first bottom-up level whose frontier has
+  // at most bu_cut_edges edges outside the hubs claims those vertices'
+  // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
+  // (BuArgs::cut_edges) -- the late-switch level, whose frontier is a few
+  // thousand vertices, mostly hubs.  0 disables.
+  int64_t bu_cut_edges = int64_t(1) << 22;
+  // ... enqueued (its decision and top-down launches) only for levels
+  // predicted at <= bu_cut_mf frontier edges (RMAT-26: the late-switch first
+  // bottom-up levels have 0.09-0.32 G, the others 0.8 G and more)
+  int64_t bu_cut_mf = int64_t(1) << 29;
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
@@ -381,6 +392,11 @@ class Engine {
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_;
+  // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
+  // decision and its ticket (zero between levels)
+  DBuf<int64_t> cut_part_;
+  DBuf<int> cut_flag_;
+  DBuf<unsigned> cut_ticket_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;

@@ -98,8 +98,11 @@ __device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const wo
 // ids < 2^31, hub codes < kHubFlag + kMaxHubs).
 constexpr vid_t kNoVertex = 0xFFFFFFFFu;
 
-template <bool kHub>
-__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, const word_t* s_hub) {
+// kCut (hub-cut level, `cut` set): the scan stops at the row's first non-hub
+// neighbour (BuArgs::cut_edges) -- only hub prefixes are read, probed in LDS.
+template <bool kHub, bool kCut = false>
+__device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, const word_t* s_hub,
+                                            bool cut = false) {
   const int lane = lane_id();
   // hub-encoded copy of the adjacency when present (kHub kernels only)
   const vid_t* __restrict__ col = (kHub && a.g.hub_col) ? a.g.hub_col : a.g.col;
@@ -110,6 +113,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
   uint32_t p = min(len, 1u);
   const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
   BU_STAT(3, __popcll(__ballot(p < lim && !found)));
+  bool past_hubs = false;  // (kCut) the scan reached a non-hub neighbour
   while (p < lim && !found) {
     BU_STAT(4, 1);
     vid_t u[kBuBatch];
@@ -119,13 +123,27 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       ok[k] = p + k < lim;
       u[k] = ok[k] ? row[p + k] : 0u;
     }
+    if constexpr (kCut) {
+      if (cut) {
+        bool stop = false;
+#pragma unroll
+        for (int k = 0; k < kBuBatch; ++k) {
+          const bool hub = (u[k] & kHubFlag) != 0;
+          found |= ok[k] && hub && ((s_hub[(u[k] & ~kHubFlag) >> 6] >> (u[k] & 63)) & 1ull);
+          stop |= ok[k] && !hub;
+        }
+        past_hubs = stop;
+        p = stop ? lim : p + kBuBatch;
+        continue;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < kBuBatch; ++k) found |= ok[k] && bu_probe<kHub>(fr, s_hub, u[k]);
     p += kBuBatch;
   }
   if (p > lim) p = lim;
   // Phase 2: the wave scans each still-unresolved row in turn
-  unsigned long long pending = __ballot(!found && p < len);
+  unsigned long long pending = __ballot(!found && !past_hubs && p < len);
   BU_STAT(5, __popcll(pending));
   while (pending) {
     const int l = __ffsll(static_cast<long long>(pending)) - 1;
@@ -137,6 +155,17 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
       BU_STAT(6, 1);
       const uint32_t idx = base + lane;
       const vid_t u = idx < pe ? r[idx] : kNoVertex;
+      if constexpr (kCut) {
+        if (cut) {
+          const bool hub = u != kNoVertex && (u & kHubFlag);
+          if (__ballot(hub && ((s_hub[(u & ~kHubFlag) >> 6] >> (u & 63)) & 1ull))) {
+            f = true;
+            break;
+          }
+          if (__ballot(u != kNoVertex && !hub)) break;  // past the hub prefix
+          continue;
+        }
+      }
       if (__ballot(u != kNoVertex && bu_probe<kHub>(fr, s_hub, u))) {
         f = true;
         break;
@@ -166,20 +195,67 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
 // a time; rows of 2^20+ entries (or units spanning 2^32 edges) are scanned in
 // place.  kRec: row bounds and heads from the packed 8-byte records of the
 // non-empty-row view (ShardView::nz_rec).
-template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false>
+// kCut: the hub-cut variant (BuArgs::cut_edges; `cut` = *a.cut_flag, read
+// once per kernel): vertices already claimed in a.pre are not scanned but
+// join the output (their statistics from their row bounds), heads and rows
+// stop at the first non-hub neighbour.
+template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false, bool kCut = false>
 __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, word_t* s_res, const word_t* s_hub,
-                                                long long& cnt, long long& deg, unsigned long long* s_q = nullptr) {
+                                                long long& cnt, long long& deg, unsigned long long* s_q = nullptr,
+                                                bool cut = false) {
   static_assert(kWords <= kWave, "one word per lane");
   const int lane = lane_id();
   const int64_t left = a.words - w0;
   const int nw = left <= 0 ? 0 : (left < kWords ? static_cast<int>(left) : kWords);
+  // claimed by the hub-cut level's top-down part (kCut): unvisited vertices
+  // whose level byte already holds this level (64 bytes per lane, 16-B loads)
+  word_t pw = 0;
+  if constexpr (kCut) {
+    if (cut && lane < nw) {
+      const uint4* lb = reinterpret_cast<const uint4*>(a.level8 + (w0 + lane) * 64);
+      const uint64_t cur = 0x0101010101010101ull * static_cast<uint8_t>(
+                               a.narrow_base + (a.new_level <= kNarrowMaxLevel ? a.new_level : kNarrowMaxLevel + 1));
+      uint4 q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = lb[k];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4& x = q[k >> 1];
+        const uint64_t y = (k & 1 ? (static_cast<uint64_t>(x.w) << 32 | x.z) : (static_cast<uint64_t>(x.y) << 32 | x.x)) ^ cur;
+        // high bit of each zero byte of y (exact), gathered into 8 bits
+        const uint64_t z = ~(((y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | y | 0x7F7F7F7F7F7F7F7Full);
+        pw |= (((z >> 7) * 0x0102040810204080ull) >> 56) << (8 * k);
+      }
+      pw &= ~a.visited[w0 + lane];
+    }
+  }
   // unvisited bits of word `lane` (0 past the words); visited = ~um
-  const word_t um = lane < nw ? ~a.visited[w0 + lane] : 0ull;
+  const word_t um = lane < nw ? ~a.visited[w0 + lane] & ~pw : 0ull;
   const int incl = static_cast<int>(wave_incl_scan(__popcll(um)));
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (lane < kWords) s_res[lane] = 0ull;
+  // the claimed vertices: counted, their row lengths summed
+  auto take_pre = [&]() {
+    if constexpr (kCut) {
+      if (pw) {
+        int c = 0;
+        long long d = 0;
+        for (word_t m = pw; m; m &= m - 1) {
+          const int64_t v = (w0 + lane) * 64 + __builtin_ctzll(m);
+          d += static_cast<long long>(a.g.row_off[v + 1] - a.g.row_off[v]);
+          ++c;
+        }
+        cnt += c;
+        deg += d;
+      }
+    }
+  };
   if (total == 0) {
-    if (lane < nw) a.new_frontier[w0 + lane] = 0ull;
+    if (lane < nw) {
+      a.new_frontier[w0 + lane] = pw;
+      if (pw) a.visited[w0 + lane] = ~um;  // (= visited | pw)
+    }
+    take_pre();
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -312,7 +388,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const bool f = bu_scan_row<kHub>(a, qrs, qe, lane >= qn, s_hub);
+    const bool f = bu_scan_row<kHub, kCut>(a, qrs, qe, lane >= qn, s_hub, cut);
     settle(lane < qn && f, ql, qrs, qe);
     qn = 0;
   };
@@ -322,7 +398,17 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     const vid_t u0 = n_u;
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
     bool found = false;
-    if (rs < e) found = bu_probe<kHub>(fr, s_hub, u0);
+    bool cut_row = false;  // (kCut) a non-hub head: no hub neighbour, nothing to scan
+    if constexpr (kCut) {
+      if (cut) {
+        cut_row = !(u0 & kHubFlag);
+        if (rs < e && !cut_row) found = (s_hub[(u0 & ~kHubFlag) >> 6] >> (u0 & 63)) & 1ull;
+      } else if (rs < e) {
+        found = bu_probe<kHub>(fr, s_hub, u0);
+      }
+    } else {
+      if (rs < e) found = bu_probe<kHub>(fr, s_hub, u0);
+    }
     BU_STAT(0, 1);
     BU_STAT(1, __popcll(__ballot(loc >= 0)));
     BU_STAT(2, __popcll(__ballot(found)));
@@ -330,7 +416,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     if constexpr (kQueue > 0) {
       // found by the head: settled now; unresolved rows with more neighbours
       // are queued (huge rows / spans scanned in place)
-      const bool need = !found && e - rs > 1;
+      const bool need = !found && e - rs > 1 && !cut_row;
       const bool fits = q_span_ok && e - rs < (eid_t(1) << 20);
       // more unresolved rows than the queue holds (a sparse-hit level: most
       // lanes scan anyway, deferring gains nothing): all in place
@@ -338,7 +424,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
       const bool inplace = need && (direct || !fits);
       if (__ballot(inplace)) {
         // (lanes not scanned here pass as resolved and keep their result)
-        const bool f = bu_scan_row<kHub>(a, rs, e, found || !inplace, s_hub);
+        const bool f = bu_scan_row<kHub, kCut>(a, rs, e, found || !inplace, s_hub, cut);
         if (inplace) found = f;
       }
       settle(found, loc, rs, e);
@@ -351,7 +437,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
                                   (static_cast<unsigned long long>(e - rs) << 12) | static_cast<unsigned>(loc);
       qn += k;
     } else {
-      found = bu_scan_row<kHub>(a, rs, e, found, s_hub);
+      found = bu_scan_row<kHub, kCut>(a, rs, e, found || cut_row, s_hub, cut) && !cut_row;
       BU_STAT(7, __popcll(__ballot(found)));
       settle(found, loc, rs, e);
     }
@@ -363,10 +449,11 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   if (lane < nw) {
-    const word_t res = s_res[lane];
+    const word_t res = s_res[lane] | pw;
     a.new_frontier[w0 + lane] = res;
-    if (res) a.visited[w0 + lane] = ~um | res;
+    if (res) a.visited[w0 + lane] = ~um | res;  // (~um holds pw)
   }
+  take_pre();
 }
 
 // Graphs without hubs: a wave per 16 words, 4 waves (one unit) per workgroup.
@@ -453,7 +540,9 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
 
 // kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
 // code costs the one-rank kernels their spill-free 64 registers).
-template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false>
+// kCut: the hub-cut variant (one rank, first bottom-up level of a run of them).
+template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false,
+          bool kCut = false>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
@@ -468,6 +557,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     }
     return;
   }
+  // a hub-cut level launches both variants; the decision picks one
+  if (a.cut_flag && (*a.cut_flag != 0) != kCut) return;
+  constexpr bool cut = kCut;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
@@ -489,8 +581,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
          u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
-      bu_wave_compact<true, kUnitWords, kQ, kRec>(a, u * kUnitWords, s_res + wave * kUnitWords, s_hub, cnt, deg,
-                                                  s_q + wave * kQ);
+      bu_wave_compact<true, kUnitWords, kQ, kRec, kCut>(a, u * kUnitWords, s_res + wave * kUnitWords, s_hub, cnt,
+                                                        deg, s_q + wave * kQ, cut);
       cnt = wave_sum(cnt);
       deg = wave_sum(deg);
       if (lane_id() == 0) {
@@ -525,8 +617,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
     if (u < nunits)
-      bu_wave_compact<true, kWaveWords, kQ, kRec>(a, u * kUnitWords + wg * kWaveWords, s_res + wave * kWaveWords, s_hub,
-                                                  cnt, deg, s_q + wave * kQ);
+      bu_wave_compact<true, kWaveWords, kQ, kRec, kCut>(a, u * kUnitWords + wg * kWaveWords,
+                                                        s_res + wave * kWaveWords, s_hub, cnt, deg, s_q + wave * kQ,
+                                                        cut);
     cnt = wave_sum(cnt);
     deg = wave_sum(deg);
     if (lane_id() == 0) {
@@ -559,6 +652,70 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
 }
 
+// hub_gather of a hub-cut level (one rank; BuArgs::cut_edges): 4 hubs per
+// thread (loads issued together), the frontier hubs' degrees summed per
+// workgroup; the last-arriving workgroup (of ~128) totals them and stores the
+// decision ctrl->m_f - hub edges <= cut_edges in *cut_flag.
+constexpr int kHgThreads = 1024, kHgPer = 4;
+__global__ __launch_bounds__(kHgThreads) void hub_gather_cut_kernel(HubGatherArgs a) {
+  if (a.ctrl->done || a.ctrl->dir != 'B') return;
+  stamp_level_start(a.ctrl);
+  __shared__ long long s_d[kHgThreads / kWave];
+  __shared__ int s_last;
+  const int lane = lane_id();
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * (kHgThreads * kHgPer);
+  vid_t hv[kHgPer];
+  bool bit[kHgPer];
+#pragma unroll
+  for (int k = 0; k < kHgPer; ++k) {
+    const int64_t h = base + k * kHgThreads + threadIdx.x;
+    hv[k] = h < a.g.nhubs ? a.g.hub_vertex[h] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kHgPer; ++k) {
+    const int64_t h = base + k * kHgThreads + threadIdx.x;
+    bit[k] = h < a.g.nhubs && test_bit(a.frontier, hv[k]);
+  }
+  long long d = 0;
+#pragma unroll
+  for (int k = 0; k < kHgPer; ++k) {
+    const int64_t h0 = base + k * kHgThreads + (threadIdx.x & ~(kWave - 1));
+    const word_t m = __ballot(bit[k]);
+    if (lane == 0 && h0 < a.g.nhubs) a.hub_front[h0 / kWave] = m;
+    if (bit[k]) d += static_cast<long long>(a.g.row_off[hv[k] + 1] - a.g.row_off[hv[k]]);
+  }
+  d = wave_sum(d);
+  if (lane == 0) s_d[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+#pragma unroll
+    for (int k = 0; k < kHgThreads / kWave; ++k) t += s_d[k];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.cut_part + blockIdx.x), static_cast<unsigned long long>(t),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = atomicAdd(a.cut_ticket, 1u) == gridDim.x - 1;
+    if (s_last) last_arriver_acquire();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  long long t = 0;
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kHgThreads)
+    t += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.cut_part + i),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  t = wave_sum(t);
+  __syncthreads();  // (s_d reused)
+  if (lane == 0) s_d[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long hub_edges = 0;
+#pragma unroll
+    for (int k = 0; k < kHgThreads / kWave; ++k) hub_edges += s_d[k];
+    *a.cut_flag = a.ctrl->m_f - hub_edges <= a.cut_edges ? 1 : 0;
+    *a.cut_ticket = 0u;
+  }
+}
+
 // hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word;
 // several ranks: then the whole grid merges the frontier into visited.
 __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
@@ -574,6 +731,49 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.words; i += stride) {
       const word_t f = a.frontier[i];
       if (f) a.visited[i] |= f;
+    }
+  }
+}
+
+// The hub-cut level's top-down part (BuArgs::cut_edges; hub_gather decided):
+// a wave per 64 frontier words finds their non-hub vertices and expands
+// their rows one after another, the lanes striding over the row (four column
+// loads, then four visited words, in flight per lane), writing the level
+// byte of every unvisited neighbour -- plain byte stores, repeats harmless;
+// the bottom-up kernel reads the claims back from the bytes.
+// Measured on RMAT-26 (3 K non-hub frontier vertices, 0.66 M edges): ~105 us
+// whatever the mapping (this one; a list of the vertices, a wave each: the
+// list's same-address appends alone took 109 us); claims in a bitmap by
+// device atomics 160 us.
+constexpr int kCutThreads = 1024;
+__global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+  if (!*a.cut_flag) return;
+  const vid_t* __restrict__ col = a.g.col;
+  const eid_t* __restrict__ ro = a.g.row_off;
+  const int lane = lane_id();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kCutThreads;
+  for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCutThreads + (threadIdx.x & ~(kWave - 1)); w0 < a.words;
+       w0 += stride) {
+    const int64_t w = w0 + lane;
+    word_t m = w < a.words ? a.frontier[w] & ~a.g.hub_bits[w] : 0ull;
+    for (unsigned long long bm = __ballot(m != 0); bm; bm = __ballot(m != 0)) {
+      const int l = __ffsll(static_cast<long long>(bm)) - 1;
+      const int64_t v = (w0 + l) * 64 + __builtin_ctzll(static_cast<word_t>(__shfl(static_cast<long long>(m), l, kWave)));
+      if (lane == l) m &= m - 1;
+      const eid_t rs = ro[v], re = ro[v + 1];
+      constexpr int kU = 4;
+      for (eid_t e0 = rs + lane; e0 < re; e0 += kU * kWave) {
+        vid_t t[kU];
+        word_t vw[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) t[k] = e0 + k * kWave < re ? col[e0 + k * kWave] : kNoVertex;
+#pragma unroll
+        for (int k = 0; k < kU; ++k) vw[k] = t[k] != kNoVertex ? a.visited[t[k] >> 6] : ~0ull;
+#pragma unroll
+        for (int k = 0; k < kU; ++k)
+          if (!((vw[k] >> (t[k] & 63)) & 1ull)) store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
+      }
     }
   }
 }
@@ -634,6 +834,15 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);            \
     else bu_hub_kernel<W, T, Q, R, false><<<grid, T, 0, st>>>(a);                        \
   } while (0)
+    if (a.cut_edges > 0) {
+      // a hub-cut level (one rank, a first bottom-up level: the engine only
+      // asks for it there): the cut variant, then the plain one -- whichever
+      // the device decision does not pick returns at once
+      DBFS_CHECK(rec && !a.follow_up && !a.end.active && a.cut_flag && a.level8 && a.g.hub_bits,
+                 "bu_step: hub-cut level without packed records / flag / narrow levels");
+      if (whole) bu_hub_kernel<true, kHubBuThreads, kBuQueue, true, false, true><<<grid, kHubBuThreads, 0, st>>>(a);
+      else bu_hub_kernel<false, kHubBuThreads, kBuQueue, true, false, true><<<grid, kHubBuThreads, 0, st>>>(a);
+    }
     if (whole) {
       if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);
       else if (a.follow_up) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, false);
@@ -653,8 +862,20 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   if (a.fuse_scan) totals_finish(a.scan, st);
 }
 
+void bu_cut_prep(const BuArgs& a, hipStream_t st) {
+  DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && a.level8 && a.g.hub_bits && a.ctrl,
+             "bu_cut_prep: hub-cut arguments missing (narrow levels needed)");
+  bu_cut_prep_kernel<<<grid_for(a.words, kCutThreads, 2 * device_cus()), kCutThreads, 0, st>>>(a);
+}
+
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
+  if (a.cut_part) {
+    DBFS_CHECK(!a.visited && a.cut_flag && a.cut_ticket && a.ctrl,
+               "hub_gather: the hub-cut decision needs one rank, a flag, a ticket and the level state");
+    hub_gather_cut_kernel<<<grid_for(a.g.nhubs, kHgThreads * kHgPer), kHgThreads, 0, st>>>(a);
+    return;
+  }
   unsigned grid = grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave);
   if (a.visited) grid = std::max(grid, grid_for(a.words, kBlock, 2048));
   hub_gather_kernel<<<grid, kBlock, 0, st>>>(a);

@@ -614,3 +614,30 @@ def test_sparse_level_from_bitmap(P, bits):
         assert any("BS" in forms for _, _, forms in rank_out)
         ref = ref or [recs for _, recs, _ in rank_out]
         assert [recs for _, recs, _ in rank_out] == ref
+
+
+@pytest.mark.parametrize("max_hubs", [300, None])
+@pytest.mark.parametrize("cut_edges", [0, 1 << 40])
+@pytest.mark.parametrize("alpha", [24.0, 1e9, 2.0])
+def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs):
+    """Hub-cut bottom-up levels (BuArgs::cut_edges): the non-hub frontier's
+    neighbours claimed top-down, rows resolved by frontier hubs only, the two
+    merged -- levels, reached vertices and edges exact, with the cut taken on
+    every first bottom-up level (1 << 40) or never (0); alpha moves the switch
+    from the first levels (1e9: bottom-up right after the root) to late ones;
+    300 hubs leave most frontier vertices to the top-down part, the default
+    cap makes every vertex with an edge a hub."""
+    p = dbfs.rmat_params(13, 16, 11)
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    bfs = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=24.0, max_hubs=max_hubs)
+    bfs.engine.set_option("bu_cut_edges", cut_edges)
+    assert bfs.graph.nhubs > 0
+    for src in bfs.sample_roots(6, seed=3):
+        res = bfs.run(src)
+        exp = _oracle(csr, src)
+        assert np.array_equal(bfs.levels(), exp)
+        assert res.reached == int((exp != dbfs.UNREACHED).sum())
+        assert res.edges == int(deg[exp != dbfs.UNREACHED].sum()) // 2
+        assert "B" in "".join(l["dir"] for l in res.levels)
+        assert bfs.validate(src)

@@ -989,3 +989,25 @@ def test_shadow_replay_direct_gpu(P):
     runs = shadow_ranks(p, P, [0, P - 1], [3, 777, 40000], mode="do", device="hip")
     for s in runs:
         assert s.exact, (s.rank, s.levels, s.recorded_levels)
+
+
+@pytest.mark.parametrize("whole", [1, -1])
+@pytest.mark.parametrize("max_hubs", [500, 4000, None])
+def test_hub_cut_bottom_up_gpu(gpu_runtime, max_hubs, whole):
+    """Hub-cut first bottom-up levels (bu_cut_prep + the kCut hub kernel):
+    the non-hub frontier's neighbours claimed top-down into the claim bitmap,
+    rows scanned up to their first non-hub neighbour, claimed vertices merged
+    into the output and their statistics -- exact against the oracle with the
+    cut on every first bottom-up level (1 << 40), at the default bound, and
+    off; bottom-up-only runs cut level 0 (the root's frontier)."""
+    p = dbfs.rmat_params(18, 16, 61)
+    csr = dbfs.host_csr_from_params(p)
+    for mode, alpha in [("do", 24.0), ("do", 2.0), ("do", 1e9), ("bu", 24.0)]:
+        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, alpha=alpha, max_hubs=max_hubs)
+        assert bfs.graph.nhubs > 0
+        bfs.engine.set_option("bu_whole_units", whole)
+        for cut in [None, 1 << 40, 0]:
+            if cut is not None:
+                bfs.engine.set_option("bu_cut_edges", cut)
+            for src in bfs.sample_roots(2, seed=17):
+                _check(bfs, csr, src)
