@@ -99,6 +99,9 @@ constexpr int64_t kTdMaxHubs = int64_t(1) << DBFS_TD_MAX_HUBS_LOG2;
 #endif
 constexpr int64_t kMaxHubs = DBFS_MAX_HUBS;
 constexpr vid_t kHubFlag = 0x80000000u;
+// Rows of up to kSortedRowMax entries are sorted hub-first (neighbour degree
+// descending, graph_sort); longer ones (a handful of hubs) keep their order.
+constexpr int kSortedRowMax = 4096;
 // Narrow (8-bit) level arrays: 0xFF = unreached, levels 0 .. 254.
 constexpr uint8_t kNarrowUnreached = 0xFF;
 // One-byte levels are stored as base + level, base = 64 x (run number mod

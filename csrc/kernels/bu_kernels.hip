@@ -99,7 +99,8 @@ __device__ __forceinline__ bool bu_probe(const word_t* __restrict__ fr, const wo
 constexpr vid_t kNoVertex = 0xFFFFFFFFu;
 
 // kCut (hub-cut level, `cut` set): the scan stops at the row's first non-hub
-// neighbour (BuArgs::cut_edges) -- only hub prefixes are read, probed in LDS.
+// neighbour (BuArgs::cut_edges) -- only hub prefixes are read, probed in LDS;
+// rows longer than kSortedRowMax are not hub-first and are scanned whole.
 template <bool kHub, bool kCut = false>
 __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, bool found, const word_t* s_hub,
                                             bool cut = false) {
@@ -111,7 +112,10 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
   const vid_t* __restrict__ row = col + rs;
   const uint32_t len = static_cast<uint32_t>(e - rs);
   uint32_t p = min(len, 1u);
-  const uint32_t lim = min(len, static_cast<uint32_t>(a.lane_limit));
+  // (kCut: a row too long to be hub-first goes straight to the wave scan,
+  // which decides per row)
+  const uint32_t lim = min(len, cut && len > static_cast<uint32_t>(kSortedRowMax) ? 1u
+                                                                                  : static_cast<uint32_t>(a.lane_limit));
   BU_STAT(3, __popcll(__ballot(p < lim && !found)));
   bool past_hubs = false;  // (kCut) the scan reached a non-hub neighbour
   while (p < lim && !found) {
@@ -150,13 +154,14 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
     pending &= pending - 1;
     const vid_t* r = reinterpret_cast<const vid_t*>(__shfl(reinterpret_cast<long long>(row), l, kWave));
     const uint32_t ps = __shfl(p, l, kWave), pe = __shfl(len, l, kWave);
+    const bool cut_row = cut && pe <= static_cast<uint32_t>(kSortedRowMax);  // (wave-uniform)
     bool f = false;
     for (uint32_t base = ps; base < pe; base += kWave) {
       BU_STAT(6, 1);
       const uint32_t idx = base + lane;
       const vid_t u = idx < pe ? r[idx] : kNoVertex;
       if constexpr (kCut) {
-        if (cut) {
+        if (cut_row) {
           const bool hub = u != kNoVertex && (u & kHubFlag);
           if (__ballot(hub && ((s_hub[(u & ~kHubFlag) >> 6] >> (u & 63)) & 1ull))) {
             f = true;
@@ -398,14 +403,10 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     const vid_t u0 = n_u;
     fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
     bool found = false;
-    bool cut_row = false;  // (kCut) a non-hub head: no hub neighbour, nothing to scan
+    bool cut_row = false;  // (kCut) a hub-first row with a non-hub head: nothing to scan
     if constexpr (kCut) {
-      if (cut) {
-        cut_row = !(u0 & kHubFlag);
-        if (rs < e && !cut_row) found = (s_hub[(u0 & ~kHubFlag) >> 6] >> (u0 & 63)) & 1ull;
-      } else if (rs < e) {
-        found = bu_probe<kHub>(fr, s_hub, u0);
-      }
+      cut_row = cut && !(u0 & kHubFlag) && e - rs <= static_cast<eid_t>(kSortedRowMax);
+      if (rs < e && !cut_row) found = bu_probe<kHub>(fr, s_hub, u0);
     } else {
       if (rs < e) found = bu_probe<kHub>(fr, s_hub, u0);
     }

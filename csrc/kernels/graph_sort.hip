@@ -27,7 +27,7 @@ namespace {
 using namespace dev;
 
 constexpr int kBlock = 256;
-constexpr int kMaxLds = 4096;
+constexpr int kMaxLds = kSortedRowMax;
 
 __device__ __forceinline__ unsigned long long sort_key(uint32_t deg, vid_t v) {
   return (static_cast<unsigned long long>(0xFFFFFFFFu - deg) << 32) | v;
