@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernel_common.hpp"
@@ -742,10 +743,10 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
 // loads, then four visited words, in flight per lane), writing the level
 // byte of every unvisited neighbour -- plain byte stores, repeats harmless;
 // the bottom-up kernel reads the claims back from the bytes.
-// Measured on RMAT-26 (3 K non-hub frontier vertices, 0.66 M edges): ~105 us
-// whatever the mapping (this one; a list of the vertices, a wave each: the
-// list's same-address appends alone took 109 us); claims in a bitmap by
-// device atomics 160 us.
+// Measured on RMAT-26 (3 K non-hub frontier vertices, 0.66 M edges): 35-40 us
+// (kernel trace; grid 256-4096 workgroups flat); a list of the vertices, a
+// wave each, spent 109 us in the list's same-address appends alone; claims
+// in a bitmap by device atomics 160 us.
 constexpr int kCutThreads = 1024;
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
@@ -866,6 +867,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 void bu_cut_prep(const BuArgs& a, hipStream_t st) {
   DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && a.level8 && a.g.hub_bits && a.ctrl,
              "bu_cut_prep: hub-cut arguments missing (narrow levels needed)");
+  // (grid measured flat from 256 to 4096 workgroups)
   bu_cut_prep_kernel<<<grid_for(a.words, kCutThreads, 2 * device_cus()), kCutThreads, 0, st>>>(a);
 }
 
