@@ -449,10 +449,20 @@ class CpuBackend final : public Backend {
         // claimed: unvisited with this level's level byte already
         word_t pw = 0;
         if (cut)
-          for (int b = 0; b < 64 && w * 64 + b < a.g.rows; ++b)
-            if (!((a.visited[w] >> b) & 1ull) &&
-                a.level8[w * 64 + b] == static_cast<uint8_t>(a.narrow_base + std::min<lvl_t>(a.new_level, kNarrowMaxLevel + 1)))
+          for (int b = 0; b < 64 && w * 64 + b < a.g.rows; ++b) {
+            const int64_t v = w * 64 + b;
+            const bool claimed =
+                a.cut_claim ? a.cut_claim[v] != 0
+                            : a.level8[v] == static_cast<uint8_t>(a.narrow_base +
+                                                                  std::min<lvl_t>(a.new_level, kNarrowMaxLevel + 1));
+            if (!((a.visited[w] >> b) & 1ull) && claimed) {
               pw |= 1ull << b;
+              if (a.cut_claim) {
+                a.cut_claim[v] = 0;
+                a.level[v] = a.new_level;
+              }
+            }
+          }
         word_t out = pw;
         const word_t vis = a.visited[w] | pw;
         for (word_t m = pw; m; m &= m - 1) {
@@ -703,7 +713,9 @@ class CpuBackend final : public Backend {
         const int64_t v = w * 64 + __builtin_ctzll(m);
         for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
           const vid_t t = a.g.col[e];
-          if (!test_bit(a.visited, t)) put_level(nullptr, a.level8, t, a.new_level, a.narrow_base);
+          if (test_bit(a.visited, t)) continue;
+          if (a.cut_claim) a.cut_claim[t] = 1;
+          else put_level(nullptr, a.level8, t, a.new_level, a.narrow_base);
         }
       }
   }

@@ -1736,7 +1736,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         // for levels predicted at <= bu_cut_mf frontier edges (a first
         // bottom-up level's non-hub frontier edges grow with its frontier:
         // the larger ones never cut, and skip its launches)
-        const bool cut = !xc && run_narrow_ && opt_.bu_cut_edges > 0 && pf != 'B' &&
+        const bool cut = !xc && opt_.bu_cut_edges > 0 && pf != 'B' &&
                          (mf_hint < 0 || mf_hint <= static_cast<double>(opt_.bu_cut_mf)) && gv.hub_bits && gv.nz_rec && gv.unit_base &&
                          gv.nz_pref && gv.nz_row_off && gv.head && ba.zdeg;
         if (cut) {
@@ -1756,6 +1756,14 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         if (cut) {
           ba.cut_edges = opt_.bu_cut_edges;
           ba.cut_flag = cut_flag_.data();
+          if (!run_narrow_) {
+            // wide levels: claims in a byte array of their own (kept zero)
+            if (!cut_claim_.data()) {
+              cut_claim_ = DBuf<uint8_t>(be_, static_cast<size_t>(W * kWordBits));
+              be_.memset_async(cut_claim_.data(), 0, cut_claim_.bytes());
+            }
+            ba.cut_claim = cut_claim_.data();
+          }
           be_.bu_cut_prep(ba);
         }
       }

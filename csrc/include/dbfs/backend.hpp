@@ -680,9 +680,12 @@ struct BuArgs {
   // hub-first row's later neighbours cannot be in the frontier: rows with a
   // non-hub frontier neighbour were claimed).  Claimed vertices (unvisited,
   // level byte = this level) skip the scan and join the output with the
-  // found ones.  *cut_flag = 0: a plain level.
+  // found ones.  *cut_flag = 0: a plain level.  Wide (32-bit) levels: the
+  // claims are non-zero bytes of cut_claim (one per vertex, all zero between
+  // levels), which the bottom-up kernel clears as it writes their levels.
   int64_t cut_edges = 0;
   int* cut_flag = nullptr;
+  uint8_t* cut_claim = nullptr;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the

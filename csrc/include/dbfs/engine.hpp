@@ -396,6 +396,7 @@ class Engine {
   // decision and its ticket (zero between levels)
   DBuf<int64_t> cut_part_;
   DBuf<int> cut_flag_;
+  DBuf<uint8_t> cut_claim_;  // wide-level runs' claims
   DBuf<unsigned> cut_ticket_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated

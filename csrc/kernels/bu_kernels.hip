@@ -61,6 +61,7 @@ __device__ __forceinline__ void unit_stats_store(long long cnt, long long deg, i
 // misses of its column lines and global frontier probes, not by the scan's
 // round trips.)
 constexpr int kBuBatch = 4;  // phase-1 column loads in flight per lane
+constexpr int kCutLevels = 1, kCutClaims = 2;  // hub-cut variants (bu_hub_kernel's kCut)
 
 // Deferred row-scan queue entries per wave (hub waves; 0 = scan in the
 // probing step).  LDS: 16 waves x kBuQueue x 8 B next to the hub bits
@@ -205,7 +206,7 @@ __device__ __forceinline__ bool bu_scan_row(const BuArgs& a, eid_t rs, eid_t e, 
 // once per kernel): vertices already claimed in a.pre are not scanned but
 // join the output (their statistics from their row bounds), heads and rows
 // stop at the first non-hub neighbour.
-template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false, bool kCut = false>
+template <bool kHub, int kWords = kWaveWords, int kQueue = 0, bool kRec = false, int kCut = 0>
 __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, word_t* s_res, const word_t* s_hub,
                                                 long long& cnt, long long& deg, unsigned long long* s_q = nullptr,
                                                 bool cut = false) {
@@ -214,13 +215,18 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   const int64_t left = a.words - w0;
   const int nw = left <= 0 ? 0 : (left < kWords ? static_cast<int>(left) : kWords);
   // claimed by the hub-cut level's top-down part (kCut): unvisited vertices
-  // whose level byte already holds this level (64 bytes per lane, 16-B loads)
+  // whose level byte already holds this level, or (wide levels) whose claim
+  // byte is set -- 64 bytes per lane, 16-B loads
   word_t pw = 0;
   if constexpr (kCut) {
     if (cut && lane < nw) {
-      const uint4* lb = reinterpret_cast<const uint4*>(a.level8 + (w0 + lane) * 64);
-      const uint64_t cur = 0x0101010101010101ull * static_cast<uint8_t>(
-                               a.narrow_base + (a.new_level <= kNarrowMaxLevel ? a.new_level : kNarrowMaxLevel + 1));
+      const uint8_t* src = kCut == kCutClaims ? a.cut_claim : a.level8;
+      const uint4* lb = reinterpret_cast<const uint4*>(src + (w0 + lane) * 64);
+      const uint64_t cur = kCut == kCutClaims ? 0ull
+                                       : 0x0101010101010101ull *
+                                             static_cast<uint8_t>(a.narrow_base + (a.new_level <= kNarrowMaxLevel
+                                                                                       ? a.new_level
+                                                                                       : kNarrowMaxLevel + 1));
       uint4 q[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) q[k] = lb[k];
@@ -232,6 +238,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
         const uint64_t z = ~(((y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | y | 0x7F7F7F7F7F7F7F7Full);
         pw |= (((z >> 7) * 0x0102040810204080ull) >> 56) << (8 * k);
       }
+      if constexpr (kCut == kCutClaims) pw = ~pw;  // (claim bytes: the non-zero ones)
       pw &= ~a.visited[w0 + lane];
     }
   }
@@ -240,15 +247,22 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   const int incl = static_cast<int>(wave_incl_scan(__popcll(um)));
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (lane < kWords) s_res[lane] = 0ull;
-  // the claimed vertices: counted, their row lengths summed
+  // the claimed vertices: counted, their row lengths summed (wide levels:
+  // their levels written and their claim bytes cleared)
   auto take_pre = [&]() {
     if constexpr (kCut) {
       if (pw) {
+        if constexpr (kCut == kCutClaims) {
+          uint4* cb = reinterpret_cast<uint4*>(a.cut_claim + (w0 + lane) * 64);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cb[k] = make_uint4(0u, 0u, 0u, 0u);
+        }
         int c = 0;
         long long d = 0;
         for (word_t m = pw; m; m &= m - 1) {
           const int64_t v = (w0 + lane) * 64 + __builtin_ctzll(m);
           d += static_cast<long long>(a.g.row_off[v + 1] - a.g.row_off[v]);
+          if constexpr (kCut == kCutClaims) a.level[v] = a.new_level;
           ++c;
         }
         cnt += c;
@@ -394,7 +408,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const bool f = bu_scan_row<kHub, kCut>(a, qrs, qe, lane >= qn, s_hub, cut);
+    const bool f = bu_scan_row<kHub, (kCut != 0)>(a, qrs, qe, lane >= qn, s_hub, cut);
     settle(lane < qn && f, ql, qrs, qe);
     qn = 0;
   };
@@ -426,7 +440,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
       const bool inplace = need && (direct || !fits);
       if (__ballot(inplace)) {
         // (lanes not scanned here pass as resolved and keep their result)
-        const bool f = bu_scan_row<kHub, kCut>(a, rs, e, found || !inplace, s_hub, cut);
+        const bool f = bu_scan_row<kHub, (kCut != 0)>(a, rs, e, found || !inplace, s_hub, cut);
         if (inplace) found = f;
       }
       settle(found, loc, rs, e);
@@ -439,7 +453,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
                                   (static_cast<unsigned long long>(e - rs) << 12) | static_cast<unsigned>(loc);
       qn += k;
     } else {
-      found = bu_scan_row<kHub, kCut>(a, rs, e, found || cut_row, s_hub, cut) && !cut_row;
+      found = bu_scan_row<kHub, (kCut != 0)>(a, rs, e, found || cut_row, s_hub, cut) && !cut_row;
       BU_STAT(7, __popcll(__ballot(found)));
       settle(found, loc, rs, e);
     }
@@ -542,9 +556,11 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
 
 // kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
 // code costs the one-rank kernels their spill-free 64 registers).
-// kCut: the hub-cut variant (one rank, first bottom-up level of a run of them).
+// kCut: the hub-cut variant (one rank, first bottom-up level of a run of them),
+// kCutLevels (claims in the narrow level bytes) or kCutClaims (wide levels:
+// claims in BuArgs::cut_claim).
 template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false,
-          bool kCut = false>
+          int kCut = 0>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
@@ -560,8 +576,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     return;
   }
   // a hub-cut level launches both variants; the decision picks one
-  if (a.cut_flag && (*a.cut_flag != 0) != kCut) return;
-  constexpr bool cut = kCut;
+  if (a.cut_flag && (*a.cut_flag != 0) != (kCut != 0)) return;
+  constexpr bool cut = kCut != 0;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
@@ -774,7 +790,10 @@ __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
         for (int k = 0; k < kU; ++k) vw[k] = t[k] != kNoVertex ? a.visited[t[k] >> 6] : ~0ull;
 #pragma unroll
         for (int k = 0; k < kU; ++k)
-          if (!((vw[k] >> (t[k] & 63)) & 1ull)) store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
+          if (!((vw[k] >> (t[k] & 63)) & 1ull)) {
+            if (a.cut_claim) a.cut_claim[t[k]] = 1;  // (wide levels: the bottom-up kernel writes them)
+            else store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
+          }
       }
     }
   }
@@ -840,10 +859,16 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       // a hub-cut level (one rank, a first bottom-up level: the engine only
       // asks for it there): the cut variant, then the plain one -- whichever
       // the device decision does not pick returns at once
-      DBFS_CHECK(rec && !a.follow_up && !a.end.active && a.cut_flag && a.level8 && a.g.hub_bits,
-                 "bu_step: hub-cut level without packed records / flag / narrow levels");
-      if (whole) bu_hub_kernel<true, kHubBuThreads, kBuQueue, true, false, true><<<grid, kHubBuThreads, 0, st>>>(a);
-      else bu_hub_kernel<false, kHubBuThreads, kBuQueue, true, false, true><<<grid, kHubBuThreads, 0, st>>>(a);
+      DBFS_CHECK(rec && !a.follow_up && !a.end.active && a.cut_flag && (a.level8 || (a.cut_claim && a.level)) &&
+                     a.g.hub_bits,
+                 "bu_step: hub-cut level without packed records / flag / claim bytes");
+      if (a.cut_claim) {
+        if (whole) bu_hub_kernel<true, kHubBuThreads, kBuQueue, true, false, kCutClaims><<<grid, kHubBuThreads, 0, st>>>(a);
+        else bu_hub_kernel<false, kHubBuThreads, kBuQueue, true, false, kCutClaims><<<grid, kHubBuThreads, 0, st>>>(a);
+      } else {
+        if (whole) bu_hub_kernel<true, kHubBuThreads, kBuQueue, true, false, kCutLevels><<<grid, kHubBuThreads, 0, st>>>(a);
+        else bu_hub_kernel<false, kHubBuThreads, kBuQueue, true, false, kCutLevels><<<grid, kHubBuThreads, 0, st>>>(a);
+      }
     }
     if (whole) {
       if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);
@@ -865,8 +890,8 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 }
 
 void bu_cut_prep(const BuArgs& a, hipStream_t st) {
-  DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && a.level8 && a.g.hub_bits && a.ctrl,
-             "bu_cut_prep: hub-cut arguments missing (narrow levels needed)");
+  DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && (a.level8 || a.cut_claim) && a.g.hub_bits && a.ctrl,
+             "bu_cut_prep: hub-cut arguments missing");
   // (grid measured flat from 256 to 4096 workgroups)
   bu_cut_prep_kernel<<<grid_for(a.words, kCutThreads, 2 * device_cus()), kCutThreads, 0, st>>>(a);
 }

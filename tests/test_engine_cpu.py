@@ -616,22 +616,25 @@ def test_sparse_level_from_bitmap(P, bits):
         assert [recs for _, recs, _ in rank_out] == ref
 
 
+@pytest.mark.parametrize("narrow", [1, 0])
 @pytest.mark.parametrize("max_hubs", [300, None])
 @pytest.mark.parametrize("cut_edges", [0, 1 << 40])
 @pytest.mark.parametrize("alpha", [24.0, 1e9, 2.0])
-def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs):
+def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs, narrow):
     """Hub-cut bottom-up levels (BuArgs::cut_edges): the non-hub frontier's
     neighbours claimed top-down, rows resolved by frontier hubs only, the two
     merged -- levels, reached vertices and edges exact, with the cut taken on
     every first bottom-up level (1 << 40) or never (0); alpha moves the switch
     from the first levels (1e9: bottom-up right after the root) to late ones;
     300 hubs leave most frontier vertices to the top-down part, the default
-    cap makes every vertex with an edge a hub."""
+    cap makes every vertex with an edge a hub; narrow levels keep the claims
+    in the level bytes, wide ones in a claim-byte array."""
     p = dbfs.rmat_params(13, 16, 11)
     csr = dbfs.host_csr_from_params(p)
     deg = np.diff(np.asarray(csr.row_off))
     bfs = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=24.0, max_hubs=max_hubs)
     bfs.engine.set_option("bu_cut_edges", cut_edges)
+    bfs.engine.set_option("narrow_levels", narrow)
     assert bfs.graph.nhubs > 0
     for src in bfs.sample_roots(6, seed=3):
         res = bfs.run(src)

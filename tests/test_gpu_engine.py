@@ -999,13 +999,16 @@ def test_hub_cut_bottom_up_gpu(gpu_runtime, max_hubs, whole):
     rows scanned up to their first non-hub neighbour, claimed vertices merged
     into the output and their statistics -- exact against the oracle with the
     cut on every first bottom-up level (1 << 40), at the default bound, and
-    off; bottom-up-only runs cut level 0 (the root's frontier)."""
+    off; bottom-up-only runs cut level 0 (the root's frontier); 32-bit levels
+    keep the claims in a byte array of their own (kCutClaims)."""
     p = dbfs.rmat_params(18, 16, 61)
     csr = dbfs.host_csr_from_params(p)
-    for mode, alpha in [("do", 24.0), ("do", 2.0), ("do", 1e9), ("bu", 24.0)]:
+    for mode, alpha, narrow in [("do", 24.0, 1), ("do", 2.0, 1), ("do", 1e9, 1), ("bu", 24.0, 1), ("do", 2.0, 0),
+                                ("bu", 24.0, 0)]:
         bfs = dbfs.BFS(p, gpu_runtime, mode=mode, alpha=alpha, max_hubs=max_hubs)
         assert bfs.graph.nhubs > 0
         bfs.engine.set_option("bu_whole_units", whole)
+        bfs.engine.set_option("narrow_levels", narrow)
         for cut in [None, 1 << 40, 0]:
             if cut is not None:
                 bfs.engine.set_option("bu_cut_edges", cut)
