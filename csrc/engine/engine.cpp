@@ -1849,10 +1849,16 @@ RunResult Engine::run_bitmap_device(int64_t source) {
       return 'S';
     }
     const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    int64_t lim = pf == 'B' ? std::max(opt_.td_sparse_edges, opt_.td_sparse_bu_edges) : opt_.td_sparse_edges;
-    if (sparse_cap > 0) lim = std::min(lim, sparse_cap);  // (a sparse chain must stay live for mf)
+    // right after a bottom-up level: sparse up to td_sparse_bu_edges, the
+    // chain live up to that many too (the prediction of a shrinking frontier
+    // overshoots, and that level reads the bottom-up output bitmap directly);
+    // elsewhere up to td_sparse_edges, live up to sparse_cap
+    const bool post_bu = pf == 'B' && opt_.td_sparse_bu_edges > opt_.td_sparse_edges;
+    int64_t lim = post_bu ? opt_.td_sparse_bu_edges : opt_.td_sparse_edges;
+    const int64_t live = post_bu && sparse_cap > 0 ? std::max(sparse_cap, opt_.td_sparse_bu_edges) : sparse_cap;
+    if (live > 0) lim = std::min(lim, live);  // (a sparse chain must stay live for mf)
     if (sparse && mf <= static_cast<double>(lim)) {
-      *cap = sparse_cap;
+      *cap = live;
       return 'S';
     }
     bool after_bu = false;  // (binned only before the run's first bottom-up level)

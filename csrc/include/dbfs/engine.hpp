@@ -202,8 +202,12 @@ struct EngineOptions {
   int64_t td_grid_max = 1024;
   int64_t td_grid_filter_max = 2048;
   // The sparse threshold for the first top-down level after a bottom-up one
-  // (the extrapolated prediction of a shrinking frontier overshoots).
-  int64_t td_sparse_bu_edges = int64_t(1) << 18;
+  // (the extrapolated prediction of a shrinking frontier overshoots), and
+  // how far such a chain stays live.  RMAT-26: the late-switch roots' level
+  // after three bottom-up levels (0.2-0.6 M edges, predicted 2-6 M) 52-58 ->
+  // 19-28 us sparse; a shared cap (td_sparse_cap_factor) would also keep
+  // mispredicted early chains sparse (measured: 112 -> 331 us).
+  int64_t td_sparse_bu_edges = int64_t(1) << 23;
   // ... and that level reads the bottom-up level's output bitmap itself
   // (TdSparseArgs::from_bits: one kernel after a clear of its output bitmap,
   // instead of scan_units + compact + td_sparse).
