@@ -89,7 +89,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "xfuse_edges") o.xfuse_edges = static_cast<int64_t>(v);
   else if (name == "bu_merge_visited") o.bu_merge_visited = v != 0;
   else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
-  else if (name == "bu_cut_mf") o.bu_cut_mf = static_cast<int64_t>(v);
+  else if (name == "bu_cut_mf_frac") o.bu_cut_mf_frac = v;
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
@@ -138,7 +138,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"xfuse_edges", static_cast<double>(o.xfuse_edges)},
           {"bu_merge_visited", o.bu_merge_visited ? 1.0 : 0.0},
           {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
-          {"bu_cut_mf", static_cast<double>(o.bu_cut_mf)},
+          {"bu_cut_mf_frac", o.bu_cut_mf_frac},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
@@ -1733,11 +1733,12 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         }
         // one rank, a first bottom-up level: the hub cut (decided on the
         // device from the frontier hubs' degrees hub_gather sums), enqueued
-        // for levels predicted at <= bu_cut_mf frontier edges (a first
+        // for levels predicted at <= bu_cut_mf_frac of the graph's edges (a first
         // bottom-up level's non-hub frontier edges grow with its frontier:
         // the larger ones never cut, and skip its launches)
         const bool cut = !xc && opt_.bu_cut_edges > 0 && pf != 'B' &&
-                         (mf_hint < 0 || mf_hint <= static_cast<double>(opt_.bu_cut_mf)) && gv.hub_bits && gv.nz_rec && gv.unit_base &&
+                         (mf_hint < 0 || mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(total_directed_)) &&
+                         gv.hub_bits && gv.nz_rec && gv.unit_base &&
                          gv.nz_pref && gv.nz_row_off && gv.head && ba.zdeg;
         if (cut) {
           if (!cut_part_.data()) {

@@ -251,9 +251,10 @@ struct EngineOptions {
   // thousand vertices, mostly hubs.  0 disables.
   int64_t bu_cut_edges = int64_t(1) << 22;
   // ... enqueued (its decision and top-down launches) only for levels
-  // predicted at <= bu_cut_mf frontier edges (RMAT-26: the late-switch first
-  // bottom-up levels have 0.09-0.32 G, the others 0.8 G and more)
-  int64_t bu_cut_mf = int64_t(1) << 29;
+  // predicted at <= bu_cut_mf_frac of the graph's directed edges (RMAT-26:
+  // the late-switch first bottom-up levels have 4-15 % of them, the others
+  // 37 % and more)
+  double bu_cut_mf_frac = 0.25;
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
