@@ -112,6 +112,16 @@ def parse_args(argv=None):
     ap.add_argument("--allow-fallback", action="store_true",
                     help="if the timed traversals fail validation on the peer-memory transport, measure again on "
                          "the RCCL communicator it wraps (the failure is kept in the record; exit status 4)")
+    ap.add_argument("--heldout-roots", type=int, default=64,
+                    help="after the headline pass, time this many roots drawn with --heldout-seed (a root sample "
+                         "no tuning saw), every one validated; 0 skips")
+    ap.add_argument("--heldout-seed", type=int, default=20261017)
+    ap.add_argument("--secondary", default="auto", metavar="N:M",
+                    help="the metric's second graph, separately timed in the same record: a uniform random graph "
+                         "of N vertices and M input edges in td (the reference's algorithm class) and do modes; "
+                         "'auto' = soc-LiveJournal1's size, 4847571:68993773 (the dataset is not on the pool), on "
+                         "GPUs and none on the CPU backend; 'none' skips")
+    ap.add_argument("--secondary-roots", type=int, default=16)
     ap.add_argument("--spawn-timeout", type=float, default=1500.0,
                     help="self-spawned ranks: seconds before the children are killed")
     return ap.parse_args(argv)
@@ -180,6 +190,44 @@ def timed_pass(bfs, rt, roots):
     rt.barrier()
     wall_ms = (time.perf_counter() - t_start) * 1e3
     return results, rt.comm.max_host(wall_ms)
+
+
+def validated_pass(bfs, rt, roots):
+    """Time `roots` back to back (timed_pass), then re-run and validate every
+    one (device Graph500 validator + totals equal to the timed run's).
+    Returns (GTEPS, ms per root, validated count, per-root results)."""
+    results, wall = timed_pass(bfs, rt, roots)
+    ok = 0
+    for r, tr in zip(roots, results):
+        res = bfs.run(r)
+        ok += int(bfs.validate(r) and (res.reached, res.edges, res.depth) == (tr.reached, tr.edges, tr.depth))
+    return sum(r.edges for r in results) / (wall * 1e6), wall / len(roots), ok, results
+
+
+def secondary_block(dbfs, rt, spec: str, nroots: int, seed: int, args):
+    """The metric's second graph (soc-LiveJournal1-sized uniform random graph,
+    generated on the device) in td and do modes: 2 warm-up roots, then
+    `nroots` timed and validated, per mode."""
+    un, _, um = spec.partition(":")
+    params = dbfs.uniform_params(int(un), int(um), seed)
+    t0 = time.time()
+    g = dbfs.BFS(params, rt, mode="td", alpha=args.alpha, beta=args.beta, bu_lane_limit=args.bu_lane_limit)
+    rt.barrier()
+    gen_s = time.time() - t0
+    roots = g.sample_roots(nroots + 2, seed=seed + 1)
+    out = {"graph": f"uniform random {int(un)} V / {int(um)} E " + ("(soc-LiveJournal1's size; synthetic)" if (int(un), int(um)) == (4847571, 68993773) else "(synthetic)"),
+           "generate_s": round(gen_s, 3), "roots": len(roots) - 2}
+    for mode in ("td", "do"):
+        g.mode = mode
+        for r in roots[:2]:
+            g.run(r)
+        gteps, ms, ok, res = validated_pass(g, rt, roots[2:])
+        out[mode] = {"value": round(gteps, 4), "ms_per_step": round(ms, 4),
+                     "harmonic_mean_gteps": round(len(res) / sum(1.0 / max(x.gteps, 1e-12) for x in res), 4),
+                     "validated_roots": f"{ok}/{len(res)}"}
+        log(f"secondary {spec} {mode}: {gteps:.2f} GTEPS ({ms:.4f} ms/root), validated {ok}/{len(res)}")
+    del g
+    return out
 
 
 def main(argv=None) -> int:
@@ -315,6 +363,30 @@ def main(argv=None) -> int:
             for lv in prof.levels:
                 log(f"  level {lv['level']} {lv['dir']} frontier {lv['frontier']} edges {lv['frontier_edges']}"
                     f" new {lv['discovered']} {lv['ms']:.3f} ms (collectives {lv.get('comm_ms', 0.0):.3f} ms)")
+    # A held-out root sample (another seed, never used for tuning): timed the
+    # same way, every root validated.  Reported next to the headline, which is
+    # the driver's K roots.
+    heldout = None
+    fast_mode = args.mode in ("td", "bu", "do")  # (ref / simple / scan take seconds per root)
+    if args.heldout_roots > 0 and fast_mode:
+        hroots = bfs.sample_roots(args.heldout_roots, seed=args.heldout_seed)
+        if hroots:
+            hv, hms, hok, _ = validated_pass(bfs, rt, hroots)
+            heldout = {"value": round(hv, 4), "ms_per_step": round(hms, 4), "roots": len(hroots),
+                       "seed": args.heldout_seed, "validated_roots": f"{hok}/{len(hroots)}"}
+            log(f"held-out roots (seed {args.heldout_seed}): {hv:.2f} GTEPS, validated {hok}/{len(hroots)}")
+            if hok != len(hroots):
+                validated = False
+    secondary = None
+    if args.secondary == "auto":
+        args.secondary = "4847571:68993773" if rt.is_gpu else "none"
+    if args.secondary and args.secondary != "none" and not args.graph and fast_mode:
+        secondary = {"lj_sized": secondary_block(dbfs, rt, args.secondary, args.secondary_roots, args.seed + 100,
+                                                 args)}
+        for m in ("td", "do"):
+            ok, tot = secondary["lj_sized"][m]["validated_roots"].split("/")
+            if ok != tot:
+                validated = False
     # One extra (untimed) traversal of the median timed root with per-level
     # device events: where the time goes (collectives vs kernels) at this N.
     med = sorted(results, key=lambda r: r.ms)[len(results) // 2]
@@ -379,6 +451,13 @@ def main(argv=None) -> int:
             "comm_note": comm_note,
             "primary": primary,
             "comm_ranks": rt.comm.size,
+            # peer transport: collectives through the IPC windows / handed to
+            # the wrapped communicator (RCCL) -- every payload size goes
+            # through the windows in slot-sized rounds, so 0 is expected
+            "comm_peer_ops": getattr(rt.comm, "peer_ops", None),
+            "comm_inner_ops": getattr(rt.comm, "inner_ops", None),
+            "heldout": heldout,
+            "secondary": secondary,
             "devices": [f"{'hip' if rt.is_gpu else 'cpu'}:{d}" for d in devices],
             "bfs_ms_mean": round(bfs_ms / len(results), 4),
             "harmonic_mean_gteps": round(harmonic_mean([r.gteps for r in results]), 4),

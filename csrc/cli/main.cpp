@@ -173,7 +173,11 @@ std::shared_ptr<Comm> try_peer(std::shared_ptr<Bootstrap> boot, Backend& be, std
                                bool required, bool report) {
   std::string why;
   try {
-    auto pc = std::make_shared<PeerComm>(boot, be, inner, static_cast<size_t>(env_int("DBFS_PEER_SLOT_MB", 16)) << 20);
+    // (DBFS_PEER_SLOT_KB, when set, overrides: small slots exercise the
+    // slot-sized rounds of large collectives in tests)
+    const size_t slot = std::getenv("DBFS_PEER_SLOT_KB") ? static_cast<size_t>(env_int("DBFS_PEER_SLOT_KB", 0)) << 10
+                                                         : static_cast<size_t>(env_int("DBFS_PEER_SLOT_MB", 16)) << 20;
+    auto pc = std::make_shared<PeerComm>(boot, be, inner, slot);
     if (pc->self_test(&why)) return pc;
   } catch (const std::exception& e) {
     why = e.what();
@@ -211,12 +215,13 @@ void run_ranks(std::vector<RankCtx>& ranks, const std::function<void(int, RankCt
 }
 
 std::string json_run(const RunResult& r, const std::string& graph, int64_t n, int64_t m, int P, const char* mode,
-                     const std::string& backend, const std::string& comm) {
+                     const std::string& backend, const std::string& comm, const std::string& ingest = "") {
   std::string s = "{\"graph\":\"" + graph + "\",\"n\":" + std::to_string(n) + ",\"m\":" + std::to_string(m) +
                   ",\"ranks\":" + std::to_string(P) + ",\"mode\":\"" + mode + "\",\"backend\":\"" + backend +
                   "\",\"comm\":\"" + comm + "\",\"source\":" + std::to_string(r.source) + ",\"ms\":" + std::to_string(r.ms) +
                   ",\"reached\":" + std::to_string(r.reached) + ",\"edges\":" + std::to_string(r.edges) +
-                  ",\"gteps\":" + std::to_string(r.gteps) + ",\"depth\":" + std::to_string(r.depth) + ",\"levels\":[";
+                  ",\"gteps\":" + std::to_string(r.gteps) + ",\"depth\":" + std::to_string(r.depth) +
+                  (ingest.empty() ? std::string() : ",\"ingest\":" + ingest) + ",\"levels\":[";
   for (size_t i = 0; i < r.levels.size(); ++i) {
     const auto& l = r.levels[i];
     if (i) s += ",";
@@ -237,6 +242,21 @@ int main(int argc, char** argv) {
   const bool leader = !multiproc || wrank == 0;
   const bool ref_lines = !a.quiet && leader;
   try {
+    // ranks of this job (P) and of this process (nlocal)
+    int P = 1;
+    if (multiproc) P = world;
+    else if (a.virtual_ranks > 0) P = a.virtual_ranks;
+    else if (!a.cpu) P = a.gpus;
+    const int nlocal = multiproc ? 1 : P;
+    // Several ranks reading an edge-list / .mtx file / binary cache: every rank
+    // parses only its byte range (or its rows) and builds its shard on its
+    // device (DeviceGraph::from_file).  The reference reads and builds the
+    // whole graph on every rank (bfs_mpi.cu:815); here only the leader reads
+    // the whole file, and only for the CPU oracle (--no-oracle: not at all;
+    // the device validator then checks the levels).
+    const bool sharded = !a.path.empty() && a.path != "-" && !a.directed && P > 1;
+    if (sharded && !a.oracle) a.validate = true;
+
     // ---- graph ingestion ----
     HostCSR full;
     bool have_host = false;
@@ -246,16 +266,18 @@ int main(int argc, char** argv) {
     if (!a.path.empty()) {
       gname = a.path;
       if (ref_lines) std::printf("%s\n", a.path.c_str());
-      if (a.path != "-" && is_binary_csr(a.path)) {
-        full = read_binary_csr(a.path);
-      } else {
-        ReadOptions ro;
-        ro.verbose_reference_lines = ref_lines;
-        EdgeList el = read_edge_list(a.path, ro);
-        full = build_csr(el, a.directed);
+      if (!sharded) {
+        if (a.path != "-" && is_binary_csr(a.path)) {
+          full = read_binary_csr(a.path);
+        } else {
+          ReadOptions ro;
+          ro.verbose_reference_lines = ref_lines;
+          EdgeList el = read_edge_list(a.path, ro);
+          full = build_csr(el, a.directed);
+        }
+        have_host = true;
+        if (ref_lines) std::printf("finish load graph\n");
       }
-      have_host = true;
-      if (ref_lines) std::printf("finish load graph\n");
     } else {
       synth = true;
       if (a.rmat_scale > 0) {
@@ -266,7 +288,7 @@ int main(int argc, char** argv) {
         gname = "uniform_n" + std::to_string(a.uni_n) + "_m" + std::to_string(a.uni_m);
       }
       // Host copy only when the CPU oracle / cache / CPU backend needs it.
-      if (a.oracle || !a.cache_out.empty()) {
+      if ((a.oracle && leader) || !a.cache_out.empty()) {
         EdgeList el;
         el.n = gp.n;
         el.u.resize(static_cast<size_t>(gp.m));
@@ -281,36 +303,43 @@ int main(int argc, char** argv) {
         have_host = true;
       }
     }
-    const int64_t n = have_host ? full.n : gp.n;
-    const int64_t m_in = have_host ? full.input_edges : gp.m;
-    if (ref_lines) {
-      std::printf("Number of vertices %lld\n", static_cast<long long>(n));
-      std::printf("Number of edges %lld\n\n", static_cast<long long>(have_host ? full.directed_edges() : 2 * gp.m));
-    }
-    if (!a.cache_out.empty() && leader) write_binary_csr(a.cache_out, full);
-    if (a.src < 0 || a.src >= n) throw Error("source vertex " + std::to_string(a.src) + " out of range [0, " + std::to_string(n) + ")");
-
-    // ---- CPU oracle (bfs.cu:798-802) ----
+    // the reference's lines after the load, and the CPU oracle
+    // (bfs.cu:789-802) on the leader
     std::vector<lvl_t> expected;
-    if (a.oracle && have_host && leader) {
-      if (ref_lines) std::printf("Starting sequential bfs.\n");
-      auto c0 = std::chrono::steady_clock::now();
-      expected = cpu_bfs(full, a.src).level;
-      auto c1 = std::chrono::steady_clock::now();
-      if (ref_lines)
-        std::printf("Elapsed time in milliseconds : %li ms.\n\n",
-                    static_cast<long>(std::chrono::duration_cast<std::chrono::milliseconds>(c1 - c0).count()));
-    }
+    auto print_graph_and_oracle = [&](int64_t n, int64_t directed_edges) {
+      if (ref_lines) {
+        std::printf("Number of vertices %lld\n", static_cast<long long>(n));
+        std::printf("Number of edges %lld\n\n", static_cast<long long>(directed_edges));
+      }
+      if (!a.cache_out.empty() && leader && have_host) write_binary_csr(a.cache_out, full);
+      if (a.src < 0 || a.src >= n)
+        throw Error("source vertex " + std::to_string(a.src) + " out of range [0, " + std::to_string(n) + ")");
+      if (a.oracle && leader) {
+        if (sharded && !have_host) {
+          // the whole graph on the leader only, for the oracle (not timed)
+          if (is_binary_csr(a.path)) {
+            full = read_binary_csr(a.path);
+          } else {
+            EdgeList el = read_edge_list(a.path, ReadOptions{});
+            full = build_csr(el, false);
+          }
+          have_host = true;
+        }
+        if (ref_lines) std::printf("Starting sequential bfs.\n");
+        auto c0 = std::chrono::steady_clock::now();
+        expected = cpu_bfs(full, a.src).level;
+        auto c1 = std::chrono::steady_clock::now();
+        if (ref_lines)
+          std::printf("Elapsed time in milliseconds : %li ms.\n\n",
+                      static_cast<long>(std::chrono::duration_cast<std::chrono::milliseconds>(c1 - c0).count()));
+      }
+    };
+    if (!sharded)
+      print_graph_and_oracle(have_host ? full.n : gp.n, have_host ? full.directed_edges() : 2 * gp.m);
 
     // ---- ranks / devices ----
-    int P = 1;
-    if (multiproc) P = world;
-    else if (a.virtual_ranks > 0) P = a.virtual_ranks;
-    else if (!a.cpu) P = a.gpus;
-    const Partition part = Partition::block(n, P);
-    const int nlocal = multiproc ? 1 : P;
     std::vector<RankCtx> ranks(static_cast<size_t>(nlocal));
-    if (!a.cpu && ref_lines) std::printf("Enabling peer access between GPU0 and GPU1...\n");
+    if (!a.cpu && ref_lines && !sharded) std::printf("Enabling peer access between GPU0 and GPU1...\n");
     std::shared_ptr<VirtualGroup> vgroup;
     if (a.virtual_ranks > 0 && !multiproc) vgroup = std::make_shared<VirtualGroup>(P);
     const char* dev_pin = std::getenv("DBFS_DEVICE");  // several processes on one GPU (tests)
@@ -359,6 +388,32 @@ int main(int argc, char** argv) {
       ranks[0].comm = std::make_shared<LocalComm>(*ranks[0].be);
     }
 
+    Partition part;
+    if (sharded) {
+      // every rank its byte range (host threads shared among this process's ranks)
+      const int threads = std::max(1, static_cast<int>(std::thread::hardware_concurrency()) / nlocal);
+      run_ranks(ranks, [&](int i, RankCtx& rc) {
+        rc.graph = DeviceGraph::from_file(*rc.be, *rc.comm, a.path, std::min(threads, 16));
+      }, vgroup.get());
+      const DeviceGraph& g0 = *ranks[0].graph;
+      part = g0.partition();
+      if (ref_lines) {
+        std::printf("nodes num: %lld\n", static_cast<long long>(g0.n()));
+        std::printf("edge num: %lld\n", static_cast<long long>(g0.input_edges()));
+        std::printf("finish load graph\n");
+      }
+      int64_t nnz = 0;
+      if (multiproc) nnz = ranks[0].comm->sum_host(g0.nnz());
+      else
+        for (auto& r : ranks) nnz += r.graph->nnz();
+      print_graph_and_oracle(g0.n(), nnz);
+      if (!a.cpu && ref_lines) std::printf("Enabling peer access between GPU0 and GPU1...\n");
+    } else {
+      part = Partition::block(have_host ? full.n : gp.n, P);
+    }
+    const int64_t n = part.n;
+    const int64_t m_in = sharded ? ranks[0].graph->input_edges() : have_host ? full.input_edges : gp.m;
+
     EngineOptions eo;
     eo.mode = parse_mode(a.mode);
     eo.alpha = a.alpha;
@@ -369,10 +424,32 @@ int main(int argc, char** argv) {
     run_ranks(ranks, [&](int i, RankCtx& rc) {
       const int rk = multiproc ? wrank : i;
       if (synth) rc.graph = DeviceGraph::generate(*rc.be, gp, part, rk);
-      else rc.graph = DeviceGraph::from_host(*rc.be, full, part, rk);
+      else if (!sharded) rc.graph = DeviceGraph::from_host(*rc.be, full, part, rk);
       if (a.hub_sort) rc.graph->sort_neighbors_by_degree(*rc.comm);
       rc.engine = std::make_unique<Engine>(*rc.graph, *rc.comm, eo);
     }, vgroup.get());
+    // what every rank parsed (sharded reads): [byte_begin, byte_end, edges] per rank
+    std::string ingest_json;
+    if (sharded) {
+      std::vector<int64_t> b, e, m;
+      if (multiproc) {
+        const auto& gi = ranks[0].graph->ingest();
+        b = ranks[0].comm->allgather_host_i64(gi.byte_begin);
+        e = ranks[0].comm->allgather_host_i64(gi.byte_end);
+        m = ranks[0].comm->allgather_host_i64(gi.edges);
+      } else {
+        for (auto& r : ranks) {
+          b.push_back(r.graph->ingest().byte_begin);
+          e.push_back(r.graph->ingest().byte_end);
+          m.push_back(r.graph->ingest().edges);
+        }
+      }
+      ingest_json = "[";
+      for (size_t r = 0; r < b.size(); ++r)
+        ingest_json += (r ? ",[" : "[") + std::to_string(b[r]) + "," + std::to_string(e[r]) + "," +
+                       std::to_string(m[r]) + "]";
+      ingest_json += "]";
+    }
 
     // ---- the reference's single run from <src> ----
     std::vector<RunResult> res(static_cast<size_t>(nlocal));
@@ -424,7 +501,8 @@ int main(int argc, char** argv) {
     };
     csv_run(res[0]);
     const std::string bname = ranks[0].be->name() + (ranks[0].be->device_checks_enabled() ? "+checked" : "");
-    if (a.json && leader) std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname, ranks[0].comm->name()).c_str());
+    if (a.json && leader)
+      std::printf("%s\n", json_run(res[0], gname, n, m_in, P, a.mode.c_str(), bname, ranks[0].comm->name(), ingest_json).c_str());
 
     // ---- optional K random roots (Graph500-style GTEPS) ----
     if (a.roots > 0) {

@@ -336,91 +336,126 @@ void PeerComm::run(const Plan& plan) {
   ++peer_ops_;
 }
 
+// Payloads larger than a window slot go through the windows in rounds of at
+// most one slot per peer (one launch each, in order on the comm stream; a
+// round's parity slots are reused two rounds later, after the peers' flags of
+// the round in between -- the same rule as any two consecutive collectives).
+// The round count is a function of sizes every rank knows (or agreed first),
+// so every rank issues the same sequence: RCCL is never needed for size.
+// src[p] / sb[p]: the piece for rank p; dst[p] / rb[p]: where rank p's lands.
+// (The reference copies each pair's bucket with one cudaMemcpyPeer,
+// bfs.cu:604-605.)
+void PeerComm::rounds(const std::vector<const char*>& src, const std::vector<int64_t>& sb,
+                      const std::vector<char*>& dst, const std::vector<int64_t>& rb, int64_t nrounds) {
+  const int64_t slot = static_cast<int64_t>(slot_);
+  for (int64_t k = 0; k < std::max<int64_t>(nrounds, 1); ++k) {
+    const int64_t off = k * slot;
+    auto piece = [&](int64_t total) { return std::max<int64_t>(0, std::min(slot, total - off)); };
+    Plan pl;
+    pl.send.resize(static_cast<size_t>(size_));
+    pl.recv.resize(static_cast<size_t>(size_));
+    for (int p = 0; p < size_; ++p) {
+      const int64_t sn = piece(sb[p]), rn = piece(rb[p]);
+      pl.send[p] = {src[p] + (sn > 0 ? off : 0), nullptr, sn};
+      pl.recv[p] = {nullptr, dst[p] + (rn > 0 ? off : 0), rn};
+    }
+    run(pl);
+  }
+}
+
+int64_t PeerComm::nrounds(int64_t bytes) const {
+  const int64_t slot = static_cast<int64_t>(slot_);
+  return std::max<int64_t>(1, (bytes + slot - 1) / slot);
+}
+
 void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
   note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
-  if (bytes > slot_ || bytes % 4) {
+  if (bytes % 4) {
     ++inner_ops_;
     inner_->alltoall(send, recv, bytes);
     return;
   }
-  Plan pl;
-  pl.send.resize(static_cast<size_t>(size_));
-  pl.recv.resize(static_cast<size_t>(size_));
+  std::vector<const char*> src(static_cast<size_t>(size_));
+  std::vector<char*> dst(static_cast<size_t>(size_));
+  std::vector<int64_t> n(static_cast<size_t>(size_), static_cast<int64_t>(bytes));
   for (int p = 0; p < size_; ++p) {
-    pl.send[p] = {static_cast<const char*>(send) + p * bytes, nullptr, static_cast<int64_t>(bytes)};
-    pl.recv[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
+    src[p] = static_cast<const char*>(send) + p * bytes;
+    dst[p] = static_cast<char*>(recv) + p * bytes;
   }
-  run(pl);
+  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)));
 }
 
 void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
   note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
-  if (bytes > slot_ || bytes % 4) {
+  if (bytes % 4) {
     ++inner_ops_;
     inner_->allgather(send, recv, bytes);
     return;
   }
-  Plan pl;
-  pl.send.resize(static_cast<size_t>(size_));
-  pl.recv.resize(static_cast<size_t>(size_));
-  for (int p = 0; p < size_; ++p) {
-    pl.send[p] = {send, nullptr, static_cast<int64_t>(bytes)};
-    pl.recv[p] = {nullptr, static_cast<char*>(recv) + p * bytes, static_cast<int64_t>(bytes)};
-  }
-  run(pl);
+  std::vector<const char*> src(static_cast<size_t>(size_), static_cast<const char*>(send));
+  std::vector<char*> dst(static_cast<size_t>(size_));
+  std::vector<int64_t> n(static_cast<size_t>(size_), static_cast<int64_t>(bytes));
+  for (int p = 0; p < size_; ++p) dst[p] = static_cast<char*>(recv) + p * bytes;
+  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)));
 }
 
 void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
-  const size_t bytes = count * sizeof(int64_t);
-  if (bytes > slot_ || count == 0) {
-    ++inner_ops_;
-    if (count) inner_->allreduce_sum_i64(buf, count);
-    return;
+  if (count == 0) return;
+  const size_t per = slot_ / sizeof(int64_t);
+  for (size_t off = 0; off < count; off += per) {
+    Plan pl;
+    pl.sum_count = static_cast<int64_t>(std::min(per, count - off));
+    pl.sum_buf = buf + off;
+    run(pl);
   }
-  Plan pl;
-  pl.sum_count = static_cast<int64_t>(count);
-  pl.sum_buf = buf;
-  run(pl);
 }
 
 void PeerComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
                          const int64_t* rd, size_t eb) {
   note_alltoallv(sc, eb);
-  // Window or inner communicator: the choice must be the same on every rank
-  // (a rank in the peer kernel waits for flags that a rank gone to the inner
-  // communicator never sends), but the counts are this rank's own: the pieces
-  // through the windows -- every one but the self piece, which the push copies
-  // directly -- are agreed over the inner communicator.  (Host counts imply a
-  // host round trip already; the engine's device-loop lists use
-  // alltoall_lists, whose choice depends only on the uniform capacity.)
-  int64_t mx = 0;
-  for (int p = 0; p < size_; ++p)
-    if (p != rank_) mx = std::max(mx, std::max(sc[p], rc[p]) * static_cast<int64_t>(eb));
-  const bool fits_here = eb % 4 == 0 && static_cast<size_t>(mx) <= slot_;
-  const bool fits = inner_->sum_host(fits_here ? 0 : 1) == 0;
-  if (!fits) {
+  // The element size is the same on every rank; the counts are this rank's
+  // own, so the number of rounds (the largest piece of any rank) is agreed
+  // through the windows first.  (Host counts imply a host round trip
+  // already; the engine's device-loop lists use alltoall_lists.)
+  if (eb % 4 != 0) {
     ++inner_ops_;
     inner_->alltoallv(send, sc, sd, recv, rc, rd, eb);
     return;
   }
-  Plan pl;
-  pl.send.resize(static_cast<size_t>(size_));
-  pl.recv.resize(static_cast<size_t>(size_));
+  const int64_t e = static_cast<int64_t>(eb);
+  std::vector<const char*> src(static_cast<size_t>(size_));
+  std::vector<char*> dst(static_cast<size_t>(size_));
+  std::vector<int64_t> sb(static_cast<size_t>(size_)), rb(static_cast<size_t>(size_));
+  int64_t mx = 0;
   for (int p = 0; p < size_; ++p) {
-    pl.send[p] = {static_cast<const char*>(send) + sd[p] * eb, nullptr, sc[p] * static_cast<int64_t>(eb)};
-    pl.recv[p] = {nullptr, static_cast<char*>(recv) + rd[p] * eb, rc[p] * static_cast<int64_t>(eb)};
+    src[p] = static_cast<const char*>(send) + sd[p] * e;
+    dst[p] = static_cast<char*>(recv) + rd[p] * e;
+    sb[p] = sc[p] * e;
+    rb[p] = rc[p] * e;
+    mx = std::max(mx, std::max(sb[p], rb[p]));
   }
-  run(pl);
+  int64_t gmx = 0;
+  for (int64_t x : allgather_host_i64(mx)) gmx = std::max(gmx, x);  // (one 8-byte round)
+  rounds(src, sb, dst, rb, nrounds(gmx));
 }
 
 void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) {
   const int64_t piece = static_cast<int64_t>(cap + 1) * 4;
   // (the choice depends only on the capacity, the same on every rank)
   if (static_cast<size_t>(piece) > slot_ || stride_words % 4 != 0 || stride_words < cap + 1) {
-    ++inner_ops_;
+    // cap + 1 words per peer (the capacity: the same on every rank), in
+    // slot-sized rounds through the windows
     note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);
-    inner_->alltoall_lists(send, recv, stride_words, cap);  // cap + 1 words per peer over the inner communicator
+    DBFS_CHECK(stride_words >= cap + 1, "alltoall_lists: stride below the list capacity");
+    std::vector<const char*> src(static_cast<size_t>(size_));
+    std::vector<char*> dst(static_cast<size_t>(size_));
+    std::vector<int64_t> n(static_cast<size_t>(size_), piece);
+    for (int p = 0; p < size_; ++p) {
+      src[p] = reinterpret_cast<const char*>(send + p * stride_words);
+      dst[p] = reinterpret_cast<char*>(recv + p * stride_words);
+    }
+    rounds(src, n, dst, n, nrounds(piece));
     return;
   }
   // (traffic accounted at the capacity, as the default exchange: the device
@@ -646,14 +681,14 @@ void PeerComm::direct_self_test() {
   if (!dtab_) return;
   std::string err;
   try {
-    DBuf<unsigned> e(*be_, 1);
-    be_->memset_async(e.data(), 0, sizeof(unsigned));
+    DBuf<unsigned> e(*be_, 2);  // [0] mismatches, [1] the producers' ticket
+    be_->memset_async(e.data(), 0, 2 * sizeof(unsigned));
     for (int round = 0; round < 4; ++round) {
       DirectExchange l, x;
       DBFS_CHECK(direct_lists(4100, &l) && direct_level_end(2, &x), "direct exchange unavailable");
       const double khz = be_->wall_clock_khz() > 0 ? be_->wall_clock_khz() : 100000.0;
       l.timeout_ticks = x.timeout_ticks = static_cast<uint64_t>(10.0 * khz * 1000.0);  // (10 s)
-      kern::direct_selftest(l, x, round, e.data(), S(be_));
+      kern::direct_selftest(l, x, round, e.data(), e.data() + 1, S(be_));
       HIP_CHECK(hipGetLastError());
     }
     unsigned h = 0;

@@ -16,6 +16,7 @@
 #include <cerrno>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 
@@ -138,17 +139,28 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_port = htons(static_cast<uint16_t>(port));
-    // Listen on the rendezvous address only (not every interface) -- unless a
-    // host NAME resolves to a loopback address here (the usual 127.0.1.1
-    // /etc/hosts alias of the machine's own name): remote ranks reach that
-    // name at a routable address, so then every interface.
-    // DBFS_BOOTSTRAP_BIND=any|rendezvous overrides.
+    // Listen on the rendezvous address only, never on every interface unless
+    // asked (DBFS_BOOTSTRAP_BIND=any): the handshake is a magic word and a
+    // rank number, so an open port would let any host take a rank slot.  A
+    // host NAME that resolves to a loopback address here (the usual 127.0.1.1
+    // /etc/hosts alias) is bound as such -- every rank of one node reaches it;
+    // ranks on other nodes need DBFS_BOOTSTRAP_BIND=any (said on stderr).
     a.sin_addr = resolve(host, port).sin_addr;
     const bool loopback = (ntohl(a.sin_addr.s_addr) >> 24) == 127;
     const char* bind_env = std::getenv("DBFS_BOOTSTRAP_BIND");
-    const std::string bind_mode = bind_env ? bind_env : "";
-    if (bind_mode == "any" || (bind_mode != "rendezvous" && loopback && !is_literal_ipv4(host)))
-      a.sin_addr.s_addr = htonl(INADDR_ANY);
+    const bool any = bind_env && std::string(bind_env) == "any";
+    if (any) a.sin_addr.s_addr = htonl(INADDR_ANY);
+    {
+      char ip[INET_ADDRSTRLEN] = {0};
+      inet_ntop(AF_INET, &a.sin_addr, ip, sizeof(ip));
+      const char* verbose = std::getenv("DBFS_BOOTSTRAP_VERBOSE");
+      if ((verbose && *verbose == '1') || (loopback && !any && !is_literal_ipv4(host)))
+        std::fprintf(stderr, "[dbfs] bootstrap: rank 0 listens on %s:%d%s\n", ip, port,
+                     loopback && !any && !is_literal_ipv4(host)
+                         ? " (the rendezvous name is a loopback alias here: ranks on other hosts need "
+                           "DBFS_BOOTSTRAP_BIND=any)"
+                         : "");
+    }
     if (::bind(listen_fd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
       throw Error("bootstrap bind to port " + std::to_string(port) + " failed: " + std::strerror(errno));
     if (::listen(listen_fd_, nranks) != 0) throw Error("bootstrap listen failed");

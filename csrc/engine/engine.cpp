@@ -286,12 +286,16 @@ std::unique_ptr<DeviceGraph> DeviceGraph::from_file(Backend& be, Comm& comm, con
     DBFS_CHECK(info.row_lo == 0 && info.rows == info.n, "a sharded read needs a whole-graph binary cache: " + path);
     const Partition part = Partition::block(info.n, P);
     const HostCSR shard = read_binary_csr_rows(path, part.lo(rank), part.lo(rank) + part.count(rank));
-    return from_host(be, shard, part, rank);
+    auto g = from_host(be, shard, part, rank);
+    g->ingest_.edges = shard.rows;
+    return g;
   }
   const EdgeShard es = read_edge_shard(
       path, rank, P, [&comm](int64_t x) { return comm.allgather_host_i64(x); }, threads);
   const Partition part = Partition::block(es.n, P);
-  return from_edges(be, comm, part, rank, es.m, es.u.data(), es.v.data(), es.local_edges());
+  auto g = from_edges(be, comm, part, rank, es.m, es.u.data(), es.v.data(), es.local_edges());
+  g->ingest_ = {es.byte_begin, es.byte_end, es.local_edges()};
+  return g;
 }
 
 ShardView DeviceGraph::view() const {
@@ -1531,8 +1535,7 @@ RunResult Engine::run_bitmap_device(int64_t source) {
         // a tiny level (its chain capped at fuse_cap): td_sparse's last
         // workgroup also runs the owner side and the level end -- one launch
         // (the direct level end is taken in the same order as unfused)
-        static const bool dbg_no_fuse = std::getenv("DBFS_DBG_NO_FUSE") != nullptr;  // (debug, temporary)
-        sp.fuse_apply = !dbg_no_fuse && end_ok && fuse_cap > 0 && chain_cap > 0 && chain_cap <= fuse_cap;
+        sp.fuse_apply = end_ok && fuse_cap > 0 && chain_cap > 0 && chain_cap <= fuse_cap;
         if (sp.fuse_apply) {
           sp.recv_lists = nullptr;
           if (comm_.direct_level_end(2, &sp.end)) {

@@ -383,8 +383,10 @@ class TcpBootstrap;
 // (remote stores over xGMI + a flag per sender), a one-wave wait kernel and an
 // unpack kernel, all on the backend's communication stream -- a few
 // microseconds of latency instead of a library collective's protocol.
-// Payloads larger than a window slot go to `inner` (RCCL, or TCP when ranks
-// share a GPU).  Requires: one HIP backend per rank, every window mappable.
+// Payloads larger than a window slot go through the windows in slot-sized
+// rounds; `inner` (RCCL, or TCP when ranks share a GPU) carries only the
+// setup agreements and payloads that are not whole 4-byte words.  Requires:
+// one HIP backend per rank, every window mappable.
 class PeerComm final : public Comm {
  public:
   // (an in-process bootstrap: the ranks' windows are shared as device
@@ -439,6 +441,10 @@ class PeerComm final : public Comm {
     const LevelFinishArgs* finish = nullptr;  // then the level's decision (sum_count <= kPeerFinishMax)
   };
   void run(const Plan& plan);
+  // pieces larger than a slot: nrounds launches of run(), slot-sized slices
+  void rounds(const std::vector<const char*>& src, const std::vector<int64_t>& sb, const std::vector<char*>& dst,
+              const std::vector<int64_t>& rb, int64_t nrounds);
+  int64_t nrounds(int64_t bytes) const;
   void direct_self_test();  // (self_test's second part)
   std::shared_ptr<Bootstrap> boot_;
   bool ipc_ = true;                     // peers' windows IPC-mapped (closed on release)

@@ -75,8 +75,15 @@ class DeviceGraph {
   // col is in id order (bottom-up must scan hub_col, whose order is hub-first)
   bool col_by_id() const { return col_by_id_; }
   int64_t nhubs() const { return nhubs_; }
+  // from_file: the byte range [begin, end) of the file this rank parsed and
+  // the edges it read (a binary cache: rows, -1 bytes); -1 when not from a file
+  struct IngestInfo {
+    int64_t byte_begin = -1, byte_end = -1, edges = -1;
+  };
+  const IngestInfo& ingest() const { return ingest_; }
 
  private:
+  IngestInfo ingest_;
   Backend* be_ = nullptr;
   Partition part_;
   int rank_ = 0;

@@ -26,7 +26,7 @@ void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 // PeerComm::self_test of the direct exchanges (`round` 0..3; mismatches and
 // timeouts counted in *err)
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
-                     hipStream_t st);
+                     unsigned* ticket, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
 void level_finish(const LevelFinishArgs& a, hipStream_t st);
 void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st);

@@ -408,18 +408,37 @@ __device__ __forceinline__ uint32_t selftest_id(int from, int to, uint32_t i, in
 __device__ __forceinline__ uint32_t selftest_n(int from, int to, int round) {
   return static_cast<uint32_t>((from + to + round) % 37) + (round == 3 ? 4000u : 0u);
 }
+// The producer side runs as td_sparse's does: kSelftestGroups workgroups each
+// store a strided share of every list (write-through, uneven: a workgroup's
+// share depends on the list length), drain them, take a ticket, and the last
+// arriver acquires and publishes the cells -- so the construction-time test
+// covers the multi-workgroup publish path the sparse levels take, over the
+// real links.  The last workgroup then runs the consumer side and the level end.
+constexpr int kSelftestGroups = 8;
 __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, DirectExchange e, int round,
-                                                              unsigned* err) {
+                                                              unsigned* err, unsigned* ticket) {
   __shared__ uint64_t s_n[kern::kMaxPeers], s_x[2 * kern::kMaxPeers];
+  __shared__ int s_last;
   const int t = threadIdx.x;
   const int me = l.rank, P = l.nranks;
+  const uint32_t g0 = blockIdx.x * 256 + t, gs = gridDim.x * 256;
   for (int p = 0; p < P; ++p) {
     if (p == me) continue;
     const uint32_t n = selftest_n(me, p, round);
-    for (uint32_t i = t; i < n; i += 256) sys_store_u32(l.table->dst[p] + 1 + i, selftest_id(me, p, i, round));
+    for (uint32_t i = g0; i < n; i += gs) sys_store_u32(l.table->dst[p] + 1 + i, selftest_id(me, p, i, round));
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (t == 0) {
+    const unsigned prev = atomicAdd(ticket, 1u);
+    s_last = prev == gridDim.x - 1 ? 1 : 0;
+    if (s_last) {
+      *ticket = 0u;
+      last_arriver_acquire();
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
   if (t < P && t != me) sys_store_u64(l.table->cell_out[t], cell_word0(l.seq, selftest_n(me, t, round)));
   if (direct_wait(l, s_n, nullptr) != kWaitOk) {
     if (t == 0) atomicAdd(err, 1000000u);
@@ -647,7 +666,15 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     if (t == 0) {
       const unsigned prev = atomicAdd(a.ticket, 1u);
       s_last = (prev == active - 1) ? 1 : 0;
-      if (s_last) *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
+      if (s_last) {
+        *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
+        // the counts the publish reads were added by every workgroup's
+        // waves; the ids are write-through stores every wave drained before
+        // its workgroup's ticket (the peers read them with system-scope loads
+        // behind the cell).  The acquire orders this workgroup's reads after
+        // the ticket, as every other last arriver's.
+        last_arriver_acquire();
+      }
     }
     __syncthreads();
     if (!s_last) return;
@@ -1181,8 +1208,8 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
 }
 
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
-                     hipStream_t st) {
-  direct_selftest_kernel<<<1, 256, 0, st>>>(lists, end, round, err);
+                     unsigned* ticket, hipStream_t st) {
+  direct_selftest_kernel<<<kSelftestGroups, 256, 0, st>>>(lists, end, round, err, ticket);
 }
 
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {

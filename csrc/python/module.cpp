@@ -579,6 +579,11 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("col_by_id", &DeviceGraph::col_by_id)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
+      // from_file: (byte_begin, byte_end, edges) this rank parsed
+      .def_property_readonly("ingest",
+                             [](const DeviceGraph& g) {
+                               return py::make_tuple(g.ingest().byte_begin, g.ingest().byte_end, g.ingest().edges);
+                             })
       .def("degrees_of", &DeviceGraph::degrees_of);
 
   py::class_<RunResult>(m, "RunResult")

@@ -111,6 +111,9 @@ def _try_peer(boot, backend, inner, rank: int, required: bool):
     import sys
 
     slot = _env_int("DBFS_PEER_SLOT_MB", 16) << 20
+    if os.environ.get("DBFS_PEER_SLOT_KB"):
+        # small slots: large collectives go through the windows in slot-sized rounds (tests)
+        slot = _env_int("DBFS_PEER_SLOT_KB", 0) << 10
     try:
         pc = N.peer_comm(boot, backend, inner, slot)
         ok, why = pc.self_test()

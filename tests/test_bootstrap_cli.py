@@ -261,3 +261,59 @@ def test_cli_level_csv(tmp_path):
     assert len(rows) - 1 == sum(len(r["levels"]) for r in recs)
     first = rows[1].split(",")
     assert int(first[0]) == recs[0]["source"] and first[1] == "0" and first[2] in "TB"
+
+
+def test_cli_sharded_ingest_three_processes(tmp_path):
+    """bin/bfs as 3 processes (WORLD_SIZE = 3, TCP, CPU backend) on an edge
+    list: every rank parses only its own byte range of the file (the ranges
+    tile the body, each rank reads about a third of the edges) and builds its
+    shard from the edges routed to it -- unlike the reference, where every
+    rank reads the whole file (bfs_mpi.cu:815).  Only the leader reads the
+    file whole, for the CPU oracle: Output OK!, and the Graph500 checks pass."""
+    rng = np.random.default_rng(11)
+    n, m = 5000, 40000
+    e = rng.integers(0, n, size=(m, 2))
+    path = tmp_path / "g.txt"
+    path.write_text(f"{n} {m}\n" + "".join(f"{u} {v}\n" for u, v in e))
+    size = path.stat().st_size
+    port = _free_port()
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, WORLD_SIZE="3", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port - 1), DBFS_BOOTSTRAP_PORT=str(port), DBFS_COMM_TIMEOUT_S="60")
+        procs.append(subprocess.Popen([BFS_BIN, "7", str(path), "--cpu", "--json", "--validate"], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, err = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            p.kill()  # exact child PID
+            o, err = p.communicate()
+        outs.append((p.returncode, o, err))
+    for rc, o, err in outs:
+        assert rc == 0, err[-3000:]
+    o = outs[0][1]
+    lines = o.splitlines()
+    assert lines[:6] == [str(path), f"nodes num: {n}", f"edge num: {m}", "finish load graph",
+                         f"Number of vertices {n}", f"Number of edges {2 * m}"]
+    assert "Output OK!" in o and "Validation OK" in o
+    assert not outs[1][1].strip() and not outs[2][1].strip()  # (the leader prints)
+    rec = json.loads([l for l in lines if l.startswith("{")][-1])
+    ing = rec["ingest"]
+    assert len(ing) == 3 and rec["ranks"] == 3
+    assert len(f"{n} {m}") <= ing[0][0] <= len(f"{n} {m}\n") and ing[-1][1] == size
+    for (b0, e0, _), (b1, _, _) in zip(ing, ing[1:]):
+        assert e0 == b1 and b0 < e0  # contiguous, disjoint byte ranges
+    assert sum(x[2] for x in ing) == m
+    assert all(abs(x[2] - m / 3) < m / 10 for x in ing)  # about a third each
+
+
+def test_cli_sharded_ingest_virtual_ranks_mtx(data_dir):
+    """--virtual-ranks with a MatrixMarket file: sharded read (lines cut at
+    line starts), levels equal the oracle's."""
+    out = _run(["0", os.path.join(data_dir, "dup_self.mtx"), "--cpu", "--virtual-ranks", "2", "--json"])
+    assert out.returncode == 0, out.stderr
+    assert "Output OK!" in out.stdout
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert len(rec["ingest"]) == 2
