@@ -23,7 +23,7 @@ LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -Wl,-rpath,
 
 HOST_SRC  := csrc/graph/io.cpp csrc/graph/csr.cpp csrc/backend/cpu_backend.cpp \
              csrc/backend/hip_backend.cpp csrc/comm/comm.cpp csrc/comm/nccl_comm.cpp \
-             csrc/comm/tcp_bootstrap.cpp csrc/comm/peer_comm.cpp csrc/comm/replay_comm.cpp csrc/engine/engine.cpp csrc/graph/shard_reader.cpp
+             csrc/comm/tcp_bootstrap.cpp csrc/comm/peer_comm.cpp csrc/comm/replay_comm.cpp csrc/engine/engine.cpp csrc/engine/device_loop.cpp csrc/graph/shard_reader.cpp
 HIP_SRC   := csrc/kernels/bfs_kernels.hip csrc/kernels/td_kernels.hip csrc/kernels/bu_kernels.hip csrc/kernels/graph_kernels.hip csrc/kernels/ref_kernels.hip \
              csrc/kernels/graph_sort.hip csrc/kernels/peer_kernels.hip
 
@@ -33,7 +33,7 @@ CORE_LIB  := $(BUILD)/libdbfs_core.a
 PYMOD     := $(PKG)/_dbfs_native$(EXT_SUFFIX)
 CLI       := bin/bfs
 
-HEADERS   := $(wildcard csrc/include/dbfs/*.hpp) $(wildcard csrc/kernels/*.hpp)
+HEADERS   := $(wildcard csrc/include/dbfs/*.hpp) $(wildcard csrc/kernels/*.hpp) $(wildcard csrc/engine/*.hpp)
 
 .PHONY: all clean lib asan checked
 all: $(CLI) $(PYMOD) bin/bfs_checked

@@ -22,6 +22,7 @@
 #include "dbfs/engine.hpp"
 #include "dbfs/shard_reader.hpp"
 #include "dbfs/trace.hpp"
+#include "spin.hpp"
 
 namespace dbfs {
 
@@ -496,28 +497,6 @@ Engine::~Engine() {
   if (stats_mb_host_) be_.free_mapped(stats_mb_host_);
 }
 
-namespace {
-// Spin until `ready()` (a store of the device into pinned, mapped memory).
-// Every wait-watch period: the backend's watch runs (RCCL: async errors and
-// the collective timeout), and a stream that has drained without `ready()`
-// is an error (the stamping kernel did not run).
-template <class Ready>
-void spin_until(Backend& be, Ready ready, const char* what) {
-  if (ready()) return;
-  const auto t0 = std::chrono::steady_clock::now();
-  const double period = be.wait_watch_period();
-  double next = period;
-  for (uint64_t spin = 1;; ++spin) {
-    if (ready()) return;
-    if ((spin & 0x3FF) != 0) continue;
-    const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (waited < next) continue;
-    if (be.stream_idle() && !ready()) throw Error(what);
-    be.poll_wait_watch(waited);
-    next = waited + period;
-  }
-}
-}  // namespace
 
 // Totals of the level just scanned (stats[0..3]: local count, local degree
 // sum, global count, global degree sum) to the host.
@@ -1094,914 +1073,6 @@ LevelRecDev* Engine::rec_at(int level) {
 bool Engine::use_device_loop() const {
   return opt_.device_loop && (!exchange() || opt_.device_loop_ranks) &&
          (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
-}
-
-// Device-driven level loop (one rank).  Same kernels and decisions as
-// run_bitmap, but every level is enqueued as the full predicated chain
-//   compact -> td_expand -> update   (run when ctrl->dir == 'T')
-//   bu_step                          (run when ctrl->dir == 'B')
-//   scan (+ level_ctrl_finish)       (skipped once ctrl->done)
-// and the host enqueues level L+1 before it waits for level L's mailbox stamp:
-// the GPU never idles for a host round trip.  After the frontier empties, the
-// one level enqueued ahead costs a handful of early-exit launches.
-RunResult Engine::run_bitmap_device(int64_t source) {
-  alloc_bitmap_state();
-  TraceRange trace_run(std::string("bfs.run(device loop) mode=") + mode_name(opt_.mode) + " src=" +
-                       std::to_string(source));
-  const int64_t W = part_.slice_words(), GW = part_.global_words();
-  const int me = comm_.rank();
-  // several ranks (or a forced exchange): every chain also carries its
-  // collectives -- enqueued blindly, the same sequence on every rank (the
-  // host decisions are functions of the all-reduced totals in the mailbox)
-  const bool xc = exchange();
-  auto fr_own = [&](int k) { return frontier_[k].data() + me * W; };
-  word_t* const vis_own = visited_.data() + me * W;
-  const ShardView gv = g_.view();
-  if (!ctrl_.data()) ctrl_ = DBuf<LevelCtrl>(be_, 1);
-  if (!mailbox_host_) {
-    void* dptr = nullptr;
-    mailbox_host_ = static_cast<LevelMailbox*>(be_.alloc_mapped(sizeof(LevelMailbox) * kMailboxSlots, &dptr));
-    mailbox_dev_ = static_cast<LevelMailbox*>(dptr);
-  }
-  // one rank with narrow levels: byte-map levels write the levels directly
-  const bool direct = !xc && run_narrow_ && opt_.td_direct;
-  const int64_t byte_edges = direct ? opt_.td_direct_edges : opt_.td_byte_edges;
-  const bool bytes_ok = opt_.mode != Mode::BottomUp && byte_edges <= total_directed_;
-  if (bytes_ok && !next_bytes_.data()) {
-    next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(part_.global_words()) * kWordBits);
-    be_.memset_async(next_bytes_.data(), 0, next_bytes_.bytes());
-  }
-  // (several ranks too: remote claims travel as owner lists, td_sparse_apply
-  // settles them on their owner)
-  const bool sparse = sparse_enabled();
-  // A sparse chain is live up to this many frontier edges; a level that turns
-  // out larger (a geometric prediction can be off by 100x on the second
-  // level) is re-enqueued dense: fetch-or claims on every edge cost more than
-  // a dense level's fixed passes from there on.
-  // (Only with the predicting loop, which enqueues one chain ahead: without
-  // prediction the next level's chain is already queued behind a chain found
-  // invalid, and a chain of the right direction would run out of turn -- so
-  // there only direction mismatches invalidate a chain, and level 0 is never
-  // a list chain.)
-  const int64_t sparse_cap = opt_.device_loop_predict && opt_.td_sparse_cap_factor > 0
-                                 ? std::max<int64_t>(opt_.td_sparse_edges,
-                                                     static_cast<int64_t>(opt_.td_sparse_cap_factor *
-                                                                          static_cast<double>(opt_.td_sparse_edges)))
-                                 : 0;
-  // Several ranks: a sparse chain is live while the level's global frontier
-  // edges fit its owner lists (every rank sends any peer at most that many
-  // ids); predicted levels up to xsparse_lim go sparse.
-  const int P = part_.nranks;
-  // (a rank appends each remote vertex at most once per run -- it claims the
-  // vertex's bit in its replicated visited bitmap first -- so no list ever
-  // holds more than a rank's part: lists of that capacity never overflow)
-  const int64_t list_max =
-      xc && sparse && opt_.list_form_edges > 0 ? std::min<int64_t>(opt_.list_form_edges, part_.part) : 0;
-  const bool lists_unlimited = list_max > 0 && list_max >= part_.part;
-  const int64_t xsparse_lim = std::min<int64_t>(opt_.xsparse_edges, list_max);
-  const bool counted = comm_.counted_lists();
-  // tiny sparse chains (several ranks, counted lists): live up to fuse_cap
-  const int64_t fuse_cap = xc && counted && opt_.xfuse_edges > 0 && 4 * opt_.xfuse_edges < list_max
-                               ? 4 * opt_.xfuse_edges
-                               : 0;
-  if (list_max > 0 && list_stride_ < list_max + 1) {
-    // owner lists: count word + list_max ids, the stride a multiple of 4 words
-    // (16-byte pieces for the count-sized exchange); counts zeroed once here
-    // and by every td_sparse_apply after
-    list_stride_ = (list_max + 1 + 3) / 4 * 4;
-    const size_t n = static_cast<size_t>(P) * static_cast<size_t>(list_stride_);
-    dl_send_lists_ = DBuf<vid_t>(be_, n);
-    dl_recv_lists_ = DBuf<vid_t>(be_, n);
-    be_.memset_async(dl_send_lists_.data(), 0, dl_send_lists_.bytes());
-    be_.memset_async(dl_recv_lists_.data(), 0, dl_recv_lists_.bytes());
-  }
-  if (sparse && !sparse_ready_) {
-    const size_t rows = static_cast<size_t>(std::max<int64_t>(g_.rows(), 1));
-    qscan2_ = DBuf<int64_t>(be_, rows + 1);
-    qbase2_ = DBuf<int64_t>(be_, rows);
-    blk_vstart2_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
-    qv_[0] = DBuf<vid_t>(be_, rows);
-    qv_[1] = DBuf<vid_t>(be_, rows);
-    sparse_cnt_ = DBuf<unsigned long long>(be_, 2);
-    sparse_ticket_ = DBuf<unsigned>(be_, 1);
-    be_.memset_async(sparse_cnt_.data(), 0, sparse_cnt_.bytes());
-    be_.memset_async(sparse_ticket_.data(), 0, sparse_ticket_.bytes());
-    sparse_ready_ = true;
-  }
-  // One rank, binned top-down levels: bins of 2^shift vertices (>= one
-  // 4096-vertex unit, <= 2^kBinMaxShift so a bin's visited slice fits LDS),
-  // about 256 of them (up to kBinMaxBins).
-  constexpr int kBinGrid = 1024;
-  int bin_shift = 12;
-  {
-    int bits = 0;
-    while ((int64_t(1) << bits) < W * kWordBits) ++bits;
-    bin_shift = std::min(std::max(bits - static_cast<int>(opt_.td_bin_log2_bins), 12), kBinMaxShift);
-    while (bin_shift <= kBinMaxShift && div_up(W * kWordBits, int64_t(1) << bin_shift) > kBinMaxBins) ++bin_shift;
-  }
-  const int64_t nbins = div_up(W * kWordBits, int64_t(1) << bin_shift);
-  const bool binned = !xc && opt_.td_bin_edges > 0 && opt_.mode != Mode::BottomUp && bin_shift <= kBinMaxShift &&
-                      g_.nnz() > 0 && g_.rows() >= opt_.td_bin_min_rows;
-  if (binned && (bin_buf_.size() < static_cast<size_t>(g_.nnz()) ||
-                 bin_cnt_.size() < static_cast<size_t>(nbins * kBinGrid))) {
-    bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins));
-    bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins * kBinGrid));
-    bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(g_.nnz()));  // a level's frontier edges <= nnz
-  }
-  // stats block of level L's output (L = -1: the seed); one block with one rank
-  auto sblk = [&](int L) {
-    return xc ? stats_.data() + static_cast<int64_t>((L + 1) % kStatsBlocks) * stats_stride_ : stats_.data();
-  };
-  if (n_active_ < 0) {
-    // (outside the timed window, once) the mean degree of an edge's endpoint
-    // (sum deg^2 / sum deg) predicts the edges of level 1's frontier (the
-    // source's neighbours) from the source's degree; the number of vertices
-    // with edges bounds every later frontier by those not reached yet
-    be_.degree_moments(gv, stats_.data() + 4);
-    if (xc) comm_.allreduce_sum_i64(stats_.data() + 4, 2);
-    int64_t mom[2] = {0, 0};
-    be_.to_host(mom, stats_.data() + 4, sizeof(mom));
-    excess_degree_ = total_directed_ > 0 ? static_cast<double>(mom[0]) / static_cast<double>(total_directed_) : 0.0;
-    n_active_ = mom[1];
-  }
-  // work-list set k (level L reads set L & 1; one set without sparse levels)
-  auto qscan_set = [&](int k) { return sparse && (k & 1) ? qscan2_.data() : qscan_.data(); };
-  // two-level tickets (fused update finish, sparse levels read from a bitmap):
-  // zero between launches, each user re-zeroes what it took
-  auto group_tickets = [&]() {
-    if (!td_group_ticket_.data()) {
-      td_group_ticket_ = DBuf<uint32_t>(be_, static_cast<size_t>(kFusedGroups * kBuQueueStride));
-      be_.memset_async(td_group_ticket_.data(), 0, td_group_ticket_.bytes());
-    }
-    return td_group_ticket_.data();
-  };
-  auto qbase_set = [&](int k) { return sparse && (k & 1) ? qbase2_.data() : qbase_.data(); };
-  auto blk_set = [&](int k) { return sparse && (k & 1) ? blk_vstart2_.data() : blk_vstart_.data(); };
-  // Mailbox stamps can be reset although the previous run did not end with a
-  // synchronize: its trailing (speculative) chain may still be executing, but
-  // every kernel that stamps a mailbox slot (scan_units, level_finish,
-  // td_sparse, init_run with a ctrl) returns at entry once ctrl->done is set,
-  // and the previous run's last stamp set it -- so nothing of that run writes
-  // a slot again.  (tests/test_gpu_engine.py::test_back_to_back_runs_*)
-  for (int i = 0; i < kMailboxSlots; ++i) {
-    volatile LevelMailbox* mb = mailbox_host_ + i;
-    mb->level = -2;
-  }
-  auto slot = [](int level) { return (level + 1) % kMailboxSlots; };
-  // Wait until level `lv` (-1 = seed) has stamped its mailbox slot.
-  auto wait_stamp = [&](int lv) -> const volatile LevelMailbox* {
-    const volatile LevelMailbox* mb = mailbox_host_ + slot(lv);
-    spin_until(be_, [&] { return __atomic_load_n(&mb->level, __ATOMIC_ACQUIRE) == lv; },
-               "device level loop: a level finished without its mailbox stamp");
-    return mb;
-  };
-
-  rec_at(0);  // the first record segment, outside the timed window
-  RunResult res;
-  res.source = source;
-  be_.reset_events();
-  // Several ranks: the runs start together.  One rank: no synchronize -- the
-  // previous run's speculative trailing chain may still be executing, and
-  // this run's initialisation queues right behind it on the stream instead of
-  // after a host wake-up (nothing below touches host-visible state the
-  // trailing chain writes: see the mailbox note above).
-  if (xc || opt_.phase_timing) comm_.barrier();
-  const auto t0 = std::chrono::steady_clock::now();
-  // (host timing: the host's time from the previous traversal's last stamp
-  // to this one's start, i.e. the gap between back-to-back runs)
-  static thread_local std::chrono::steady_clock::time_point prev_done{};
-
-  begin_run_scratch();
-  LevelCtrl init;
-  init.mode = opt_.mode == Mode::TopDown ? 0 : opt_.mode == Mode::BottomUp ? 1 : 2;
-  init.alpha = opt_.alpha;
-  init.beta = opt_.beta;
-  init.n = static_cast<double>(part_.n);
-  init.total_directed = static_cast<double>(total_directed_);
-  init.td_byte_edges = bytes_ok ? static_cast<double>(byte_edges) : 1e300;
-  init.check_visited_min = opt_.td_check_visited_min;
-  init.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
-  // one fused pass: levels, visited, the seed frontier (frontier_[1]), its
-  // totals, the seeded LevelCtrl and the mailbox stamp of level -1
-  // (+ with sparse levels: the seed's work-list entry in set 0 and a clean
-  // frontier_[0] for a sparse level 0 to write)
-  // (several ranks: the seed totals are all-reduced first, then level_finish
-  // seeds the LevelCtrl and stamps level -1)
-  InitRunArgs ia = init_args(source, fr_own(1), xc ? nullptr : ctrl_.data(), init,
-                             xc ? nullptr : mailbox_dev_ + slot(-1));
-  ia.stats = sblk(-1);
-  if (sparse) {
-    ia.qbase = qbase_.data();
-    ia.blk_vstart = blk_vstart_.data();
-    ia.qv = qv_[0].data();
-    ia.frontier_clear = fr_own(0);
-  }
-  be_.init_run(ia);
-  // Several ranks: the level's ONE collective -- its totals (stats block)
-  // all-reduced, and with `gather` (the next level is predicted bottom-up, or
-  // td mode, whose top-down levels filter with the replicated visited bitmap)
-  // in the same launch the level's output frontier slice all-gathered
-  // (Comm::allgather_allreduce) -- then level_finish decides and stamps.
-  // (bfs_mpi.cu:615-621 pays a Sendrecv and an Allreduce per level.)
-  auto finish_args = [&](int level, bool seed, char expect_dir, int64_t cap) {
-    LevelFinishArgs fa;
-    fa.stats = sblk(level);
-    fa.ctrl = ctrl_.data();
-    fa.ctrl_init = init;
-    fa.rec = seed ? nullptr : rec_at(level);
-    fa.mailbox = mailbox_dev_ + slot(level);
-    fa.level = level;
-    fa.seed = seed;
-    fa.expect_dir = expect_dir;
-    fa.expect_cap = cap;
-    return fa;
-  };
-  auto finish_ranks = [&](int level, bool seed, char expect_dir, int64_t cap, bool gather) {
-    int64_t* blk = sblk(level);
-    // level L writes frontier_[L & 1] (the seed: frontier_[1])
-    const int out = seed ? 1 : (level & 1);
-    const LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
-    comm_.level_end(fr_own(out), frontier_[out].data(), gather ? static_cast<size_t>(W) * sizeof(word_t) : 0,
-                    blk + 2, 2, fa);
-  };
-  // the seed's frontier is gathered with its totals when level 0 is
-  // bottom-up (bu mode).  (Top-down levels read only their owned slice; the
-  // replicated visited bitmap filters candidates with whatever remote bits it
-  // has -- merged frontiers, and the remote targets this rank claimed and
-  // sent -- so a stale remote bit only costs an id its owner drops.)
-  const bool seed_gather = xc && init.dir == 'B';
-  if (xc) finish_ranks(-1, true, 0, 0, seed_gather);
-
-  auto scan_args = [&](int level, bool seed, char expect_dir, int64_t cap) {
-    ScanArgs sa;
-    sa.unit_cnt = unit_cnt_.data();
-    sa.unit_deg = unit_deg_.data();
-    sa.nunits = nunits_;
-    sa.part_cnt = part_cnt_.data();
-    sa.part_deg = part_deg_.data();
-    sa.ticket = ticket_.data();
-    sa.stats = sblk(level);
-    sa.qscan = qscan_set(level + 1);
-    sa.ctrl = ctrl_.data();
-    sa.rec = seed ? nullptr : rec_at(level);
-    sa.mailbox = mailbox_dev_ + slot(level);
-    sa.level = level;
-    sa.seed = seed;
-    sa.expect_dir = expect_dir;
-    sa.expect_cap = cap;
-    sa.finish = !xc;
-    return sa;
-  };
-  auto scan = [&](int level, bool seed, char expect_dir, int64_t cap) {
-    be_.scan_units(scan_args(level, seed, expect_dir, cap));
-  };
-  // Frontier double buffer: the seed is frontier_[1]; level L reads
-  // frontier_[(L + 1) & 1] and writes the other one.
-  UpdateArgs ua;
-  ua.g = gv;
-  ua.nchunks = xc ? part_.nranks : 1;
-  ua.cand_stride = W;
-  ua.clear_cand = !xc;
-  ua.visited = vis_own;
-  ua.level = level_.data();
-  ua.level8 = run_narrow_ ? level8_.data() : nullptr;
-  ua.narrow_base = narrow_base_;
-  ua.words = W;
-  ua.unit_cnt = unit_cnt_.data();
-  ua.unit_deg = unit_deg_.data();
-
-  const int64_t td_blocks = div_up(g_.nnz(), kTdEdgesPerBlock);
-  const int64_t td_grid = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_max, 1)));
-  const int64_t td_grid_filter =
-      std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_filter_max, 1)));
-  std::vector<std::pair<int, int>> evs;
-  std::vector<char> enq_dir;     // direction each level was (last) enqueued with
-  std::vector<char> enq_form;    // ... and its chain form ('T', 'S', 'B', 'X')
-  std::vector<int64_t> enq_cap;  // ... sparse form: the global frontier edges it stays live for
-  std::vector<char> enq_gather;  // ... several ranks: its collective also all-gathered its output frontier
-  std::vector<char> enq_fused;   // ... finished in its last kernel (unit prefixes not scanned)
-  // DBFS_HOST_TIMING=1: host-side enqueue / stamp-wait timeline to stderr
-  static const bool host_timing = [] {
-    const char* e = std::getenv("DBFS_HOST_TIMING");
-    return e && *e == '1';
-  }();
-  std::vector<std::pair<std::string, double>> htl;
-  if (host_timing && prev_done.time_since_epoch().count() != 0)
-    htl.emplace_back("since_prev_done", std::chrono::duration<double, std::micro>(t0 - prev_done).count());
-  auto hmark = [&](const std::string& what) {
-    if (host_timing)
-      htl.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
-  };
-  // mf_hint: the level's predicted (or, re-enqueued, actual) frontier edges
-  // (< 0 unknown); gather (several ranks): the chain's collective also
-  // all-gathers its output frontier, for a bottom-up level predicted next
-  auto enqueue_level = [&](int L, char d, int64_t cap, double mf_hint, bool gather) {
-    hmark("enqueue " + std::to_string(L) + d);
-    if (static_cast<size_t>(L) >= enq_dir.size()) {
-      inject_fault(L);
-      enq_dir.resize(static_cast<size_t>(L) + 1);
-      enq_form.resize(static_cast<size_t>(L) + 1);
-      enq_cap.resize(static_cast<size_t>(L) + 1);
-      enq_gather.resize(static_cast<size_t>(L) + 1);
-      enq_fused.resize(static_cast<size_t>(L) + 1);
-      evs.resize(static_cast<size_t>(L) + 1, {-1, -1});
-    }
-    // form: 'T' dense top-down, 'S' sparse top-down, 'B' bottom-up, 'X'
-    // binned top-down (one rank); the previous level's form decides what
-    // hands this one its work list
-    const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    // the input frontier is already global: all-gathered by the previous
-    // level's (or the seed's) collective
-    const bool in_gathered = L == 0 ? seed_gather : enq_gather[static_cast<size_t>(L - 1)] != 0;
-    enq_dir[L] = d == 'B' ? 'B' : 'T';
-    enq_form[L] = d;
-    enq_cap[L] = d == 'S' ? cap : 0;
-    enq_gather[L] = xc && gather;
-    res.chains.push_back({L, d, enq_cap[L], enq_gather[L] != 0});
-    const int64_t chain_cap = enq_cap[L];
-    const int cur = (L + 1) & 1;
-    char trace_name[48];
-    std::snprintf(trace_name, sizeof(trace_name), "bfs.level %d %c (enqueue)", L, d);
-    TraceRange trace_level(trace_name);
-    const int ev0 = opt_.phase_timing ? be_.record_event() : -1;
-    bool fused_scan = false;  // the chain's last kernel finishes the level (no scan launch)
-    bool level_ended = false;  // ... and also ran its level end (several ranks, direct exchange)
-    // several ranks, bottom-up: the input frontier to every rank -- normally
-    // gathered already by the previous level's collective; a chain enqueued
-    // after a top-down prediction gathers it here (not predicated: on a no-op
-    // chain it only refreshes bits every owner already has)
-    if (xc && d == 'B') {
-      if (!in_gathered)
-        comm_.allgather(fr_own(cur), frontier_[cur].data(), static_cast<size_t>(W) * sizeof(word_t));
-      // (bu_merge_visited: the remote slices merged into the replicated
-      // visited bitmap -- by hub_gather with hubs)
-      if (opt_.bu_merge_visited && gv.nhubs == 0) be_.bitmap_or(visited_.data(), frontier_[cur].data(), GW);
-    }
-    // the frontier bitmap -> work list (set L & 1); with sparse levels also
-    // its vertex map, and the bitmap is zeroed as read (a later sparse level
-    // writes into it)
-    auto compact = [&](word_t* clear_all) {
-      if (L > 0 && enq_fused[static_cast<size_t>(L - 1)]) {
-        // the previous level only finished its totals: its unit prefixes
-        // now (no finish; a no-op unless this chain is live)
-        ScanArgs sa = scan_args(L - 1, false, 'T', d == 'S' ? chain_cap : 0);
-        sa.finish = false;
-        be_.scan_units(sa);
-      }
-      CompactArgs ca;
-      ca.g = gv;
-      ca.frontier = fr_own(cur);
-      ca.words = W;
-      ca.unit_cnt_off = unit_cnt_.data();
-      ca.unit_deg_off = unit_deg_.data();
-      ca.part_cnt = part_cnt_.data();
-      ca.part_deg = part_deg_.data();
-      ca.qscan = qscan_set(L);
-      ca.qbase = qbase_set(L);
-      ca.blk_vstart = blk_set(L);
-      if (sparse) {
-        ca.qv = qv_[L & 1].data();
-        ca.clear = fr_own(cur);
-      }
-      ca.clear_all = clear_all;
-      ca.ctrl = ctrl_.data();
-      ca.max_mf = d == 'S' ? chain_cap : 0;
-      be_.compact_frontier(ca);
-    };
-    if (d == 'S') {
-      DBFS_CHECK(sparse, "sparse top-down level without sparse support");
-      // after a bottom-up level the output bitmap is that level's input:
-      // zeroed by the compaction (every other form leaves it clean)
-      const bool compacted = pf == 'T' || pf == 'X' || pf == 'B';
-      // right after a bottom-up level: the kernel reads that level's output
-      // bitmap itself (no unit scan, no compaction); only the stale output
-      // bitmap is cleared first
-      const bool from_bits = pf == 'B' && opt_.td_sparse_bits;
-      if (from_bits) be_.memset_async(fr_own(cur ^ 1), 0, static_cast<size_t>(W) * sizeof(word_t));
-      else if (compacted) compact(pf == 'B' ? fr_own(cur ^ 1) : nullptr);
-      TdSparseArgs sp;
-      sp.g = gv;
-      sp.qscan = qscan_set(L);
-      sp.qbase = qbase_set(L);
-      sp.blk_vstart = blk_set(L);
-      sp.qv = qv_[L & 1].data();
-      sp.dev_stats = sblk(L - 1);
-      sp.frontier_in = fr_own(cur);
-      sp.frontier_out = fr_own(cur ^ 1);
-      sp.visited = visited_.data();
-      sp.level = level_.data();
-      sp.level8 = run_narrow_ ? level8_.data() : nullptr;
-      sp.narrow_base = narrow_base_;
-      sp.new_level = L + 1;
-      sp.oscan = qscan_set(L + 1);
-      sp.obase = qbase_set(L + 1);
-      sp.oblk = blk_set(L + 1);
-      sp.oqv = qv_[(L + 1) & 1].data();
-      sp.counter = sparse_cnt_.data() + ((L + 1) & 1);
-      sp.ticket = sparse_ticket_.data();
-      sp.stats = sblk(L);
-      sp.ctrl = ctrl_.data();
-      sp.rec = rec_at(L);
-      sp.mailbox = mailbox_dev_ + slot(L);
-      sp.level_index = L;
-      sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
-      sp.first = !compacted || from_bits;
-      sp.max_mf = chain_cap;
-      if (from_bits) {
-        sp.from_bits = true;
-        sp.words = W;
-        sp.group_ticket = group_tickets();
-      }
-      if (xc) {
-        // remote claims to their owners' lists, the lists (count-sized) to
-        // their owners, the received ids settled there; the totals go to
-        // the collective below (no decision in the kernels)
-        DBFS_CHECK(list_max > 0 && chain_cap <= list_max, "sparse chain without owner lists");
-        sp.lists = dl_send_lists_.data();
-        sp.list_stride = list_stride_;
-        sp.part = part_.part;
-        sp.mailbox = nullptr;
-        // the exchange itself: by the two kernels through the peers'
-        // windows (direct), or a collective between them
-        const size_t lcap = static_cast<size_t>(chain_cap > 0 ? chain_cap : list_max);
-        const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
-        sp.nranks = P;
-        const int64_t apply_grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
-        // the level's end folded into the apply's last workgroup (no frontier
-        // gather: that one is a bandwidth collective of its own)
-        // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
-        const bool cells_fit = g_.rows() < (int64_t(1) << 32) && g_.nnz() < (int64_t(1) << 40);
-        const bool end_ok = direct && opt_.direct_level_end && cells_fit && !enq_gather[L];
-        // a tiny level (its chain capped at fuse_cap): td_sparse's last
-        // workgroup also runs the owner side and the level end -- one launch
-        // (the direct level end is taken in the same order as unfused)
-        sp.fuse_apply = end_ok && fuse_cap > 0 && chain_cap > 0 && chain_cap <= fuse_cap;
-        if (sp.fuse_apply) {
-          sp.recv_lists = nullptr;
-          if (comm_.direct_level_end(2, &sp.end)) {
-            sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
-            level_ended = true;
-          } else {
-            sp.fuse_apply = false;  // (not taken: the level ends in its collective)
-          }
-          be_.td_sparse(sp);
-          sp.grid = apply_grid;
-          if (!level_ended) be_.td_sparse_apply(sp);
-        } else {
-          be_.td_sparse(sp);
-          if (!direct)
-            comm_.alltoall_lists(dl_send_lists_.data(), dl_recv_lists_.data(), static_cast<size_t>(list_stride_),
-                                 lcap);
-          sp.recv_lists = direct ? nullptr : dl_recv_lists_.data();
-          if (end_ok && comm_.direct_level_end(2, &sp.end)) {
-            sp.fin = finish_args(L, false, enq_dir[L], chain_cap);
-            level_ended = true;
-          }
-          sp.grid = apply_grid;
-          be_.td_sparse_apply(sp);
-        }
-      } else {
-        be_.td_sparse(sp);
-      }
-      fused_scan = true;
-    } else if (d == 'X') {
-      // binned top-down (one rank): a sparse level (or the seed) handed over
-      // the work list, else compact
-      const bool listed = sparse && (pf == 'S' || pf == 'I');
-      if (!listed) compact(nullptr);
-      BinArgs xa;
-      xa.g = gv;
-      xa.qscan = qscan_set(L);
-      xa.qbase = qbase_set(L);
-      xa.blk_vstart = blk_set(L);
-      xa.dev_stats = sblk(L - 1);
-      if (listed) {
-        xa.clear_qv = qv_[L & 1].data();
-        xa.clear_frontier = fr_own(cur);
-      }
-      xa.ctrl = ctrl_.data();
-      xa.shift = bin_shift;
-      xa.nbins = static_cast<int>(nbins);
-      xa.grid = kBinGrid;
-      xa.bin_total = bin_total_.data();
-      xa.cnt = bin_cnt_.data();
-      xa.buf = bin_buf_.data();
-      xa.visited = vis_own;
-      xa.frontier = fr_own(cur ^ 1);
-      xa.words = W;
-      be_.td_binned(xa);
-      // levels and unit statistics of the new frontier (already claimed)
-      UpdateArgs tu = ua;
-      tu.cand = fr_own(cur ^ 1);
-      tu.cand_bytes = nullptr;
-      tu.nchunks = 1;
-      tu.clear_cand = false;
-      tu.force = true;
-      tu.frontier = fr_own(cur ^ 1);
-      tu.new_level = L + 1;
-      tu.ctrl = ctrl_.data();
-      be_.update_frontier(tu);
-    } else if (d == 'T') {
-      // a sparse level (or the seed) already handed over the work list
-      const bool listed = sparse && (pf == 'S' || pf == 'I');
-      if (!listed) compact(nullptr);
-      TdArgs ta;
-      ta.g = gv;
-      ta.qscan = qscan_set(L);
-      ta.qbase = qbase_set(L);
-      ta.blk_vstart = blk_set(L);
-      if (listed) {
-        ta.clear_qv = qv_[L & 1].data();
-        ta.clear_frontier = fr_own(cur);
-      }
-      ta.visited = visited_.data();
-      ta.ctrl = ctrl_.data();
-      ta.dev_stats = sblk(L - 1);
-      ta.grid = td_grid;
-      ta.grid_filter = td_grid_filter;
-      UpdateArgs tu = ua;
-      ta.next = next_.data();
-      ta.next_bytes = next_bytes_.data();
-      // (skipped for levels predicted well below the filter's threshold:
-      // the snapshot kernel would only find its gate closed)
-      if (gv.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
-          (mf_hint < 0 || mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
-        // large levels: the hubs' visited bits, staged in LDS by td_expand
-        if (!td_hub_vis_.data()) td_hub_vis_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(gv.td_nhubs, kWordBits)));
-        HubVisitedArgs hv;
-        hv.g = gv;
-        hv.visited = visited_.data();
-        hv.out = td_hub_vis_.data();
-        hv.ctrl = ctrl_.data();
-        hv.min_edges = opt_.td_hub_edges;
-        hv.vis_frac = opt_.td_hub_vis_frac;
-        be_.hub_visited(hv);
-        ta.td_hub_vis = td_hub_vis_.data();
-        ta.td_hub_min_edges = opt_.td_hub_edges;
-        ta.td_hub_vis_frac = opt_.td_hub_vis_frac;
-      }
-      // (a level past kNarrowMaxLevel would store the unreached byte:
-      // the usual path flags the overflow and the run is repeated wide)
-      if (direct && run_narrow_ && L + 1 <= kNarrowMaxLevel) {
-        // byte-map levels write the level itself (nothing to clear after)
-        ta.level_direct = level8_.data();
-        ta.narrow_base = narrow_base_;
-        ta.new_level = L + 1;
-        tu.level_direct = level8_.data();
-        tu.narrow_base = narrow_base_;
-        if (ta.td_hub_vis && opt_.td_hub_mark) {
-          if (!td_hub_mark_.data()) {
-            td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
-            be_.memset_async(td_hub_mark_.data(), 0, td_hub_mark_.bytes());
-          }
-          ta.td_hub_mark = td_hub_mark_.data();
-        }
-      }
-      be_.td_expand(ta);
-      if (ta.td_hub_mark) {
-        HubApplyArgs ha;
-        ha.g = gv;
-        ha.mark = ta.td_hub_mark;
-        ha.level8 = ta.level_direct;
-        ha.narrow_base = ta.narrow_base;
-        ha.new_level = ta.new_level;
-        ha.ctrl = ctrl_.data();
-        ha.max_mf = ta.max_mf;
-        be_.hub_apply(ha);
-      }
-      tu.cand = next_.data();
-      tu.cand_bytes = next_bytes_.data();
-      if (xc) {
-        // candidates to their owners: the byte map (if this level used it)
-        // packed into `next`, one bitmap slice per peer, `next` re-zeroed
-        if (next_bytes_.data()) {
-          PackArgs pa;
-          pa.bytes = next_bytes_.data();
-          pa.next = next_.data();
-          pa.words = GW;
-          pa.ctrl = ctrl_.data();
-          be_.pack_bytes(pa);
-        }
-        comm_.alltoall(next_.data(), recv_.data(), static_cast<size_t>(W) * sizeof(word_t));
-        be_.memset_async(next_.data(), 0, next_.bytes());
-        tu.cand = recv_.data();
-        tu.cand_bytes = nullptr;
-      }
-      tu.force = false;
-      tu.frontier = fr_own(cur ^ 1);
-      tu.new_level = L + 1;
-      tu.ctrl = ctrl_.data();
-      if (opt_.td_fused_finish) {
-        // totals (and with one rank the decision) in the update's last
-        // workgroup (as bottom-up)
-        if (!td_tot_.data()) td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
-        tu.fuse_scan = true;
-        tu.scan = scan_args(L, false, enq_dir[L], chain_cap);
-        tu.tot = td_tot_.data();
-        if (opt_.td_group_ticket) {
-          tu.group_ticket = group_tickets();
-        }
-        fused_scan = true;
-      }
-      be_.update_frontier(tu);
-    } else {
-      BuArgs ba;
-      ba.g = gv;
-      ba.visited = vis_own;
-      ba.frontier = frontier_[cur].data();
-      ba.new_frontier = fr_own(cur ^ 1);
-      ba.level = level_.data();
-      ba.level8 = run_narrow_ ? level8_.data() : nullptr;
-      ba.narrow_base = narrow_base_;
-      ba.new_level = L + 1;
-      ba.words = W;
-      ba.lane_limit = opt_.bu_lane_limit;
-      ba.whole_units = opt_.bu_whole_units;
-      ba.zdeg = zdeg_.data() + comm_.rank() * W;
-      ba.follow_up = pf == 'B';
-      ba.unit_cnt = unit_cnt_.data();
-      ba.unit_deg = unit_deg_.data();
-      ba.ctrl = ctrl_.data();
-      if (gv.nhubs > 0) {
-        HubGatherArgs hg;
-        hg.g = gv;
-        hg.frontier = frontier_[cur].data();
-        hg.hub_front = hub_front_.data();
-        hg.ctrl = ctrl_.data();
-        // several ranks, bu_merge_visited: the gathered remote slices merged
-        // into the replicated visited bitmap in the same launch
-        if (xc && opt_.bu_merge_visited) {
-          hg.visited = visited_.data();
-          hg.words = GW;
-        }
-        // one rank, a first bottom-up level: the hub cut (decided on the
-        // device from the frontier hubs' degrees hub_gather sums), enqueued
-        // for levels predicted at <= bu_cut_mf_frac of the graph's edges (a first
-        // bottom-up level's non-hub frontier edges grow with its frontier:
-        // the larger ones never cut, and skip its launches)
-        const bool cut = !xc && opt_.bu_cut_edges > 0 && pf != 'B' &&
-                         (mf_hint < 0 || mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(total_directed_)) &&
-                         gv.hub_bits && gv.nz_rec && gv.unit_base &&
-                         gv.nz_pref && gv.nz_row_off && gv.head && ba.zdeg;
-        if (cut) {
-          if (!cut_part_.data()) {
-            cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(gv.nhubs, int64_t(64))));
-            cut_flag_ = DBuf<int>(be_, 1);
-            cut_ticket_ = DBuf<unsigned>(be_, 1);
-            be_.memset_async(cut_ticket_.data(), 0, cut_ticket_.bytes());
-          }
-          hg.cut_part = cut_part_.data();
-          hg.cut_edges = opt_.bu_cut_edges;
-          hg.cut_flag = cut_flag_.data();
-          hg.cut_ticket = cut_ticket_.data();
-        }
-        be_.hub_gather(hg);
-        ba.hub_front = hub_front_.data();
-        if (cut) {
-          ba.cut_edges = opt_.bu_cut_edges;
-          ba.cut_flag = cut_flag_.data();
-          if (!run_narrow_) {
-            // wide levels: claims in a byte array of their own (kept zero)
-            if (!cut_claim_.data()) {
-              cut_claim_ = DBuf<uint8_t>(be_, static_cast<size_t>(W * kWordBits));
-              be_.memset_async(cut_claim_.data(), 0, cut_claim_.bytes());
-            }
-            ba.cut_claim = cut_claim_.data();
-          }
-          be_.bu_cut_prep(ba);
-        }
-      }
-      if (opt_.bu_fused_scan) {
-        // the level's totals (and with one rank its finish) in the
-        // bottom-up kernel's last workgroup; the unit prefixes only if a
-        // top-down chain follows
-        if (!bu_tot_.data()) bu_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid));
-        ba.fuse_scan = true;
-        ba.scan = scan_args(L, false, enq_dir[L], chain_cap);
-        ba.tot = bu_tot_.data();
-        fused_scan = true;
-        // several ranks: the level's end in the kernel's last workgroup too
-        // (no frontier gather; the hub kernels' fused finish)
-        const bool cells_fit = g_.rows() < (int64_t(1) << 32) && g_.nnz() < (int64_t(1) << 40);
-        if (xc && opt_.direct_level_end && cells_fit && gv.nhubs > 0 && !enq_gather[L] &&
-            comm_.direct_level_end(2, &ba.end)) {
-          ba.fin = finish_args(L, false, enq_dir[L], chain_cap);
-          level_ended = true;
-        }
-      }
-      be_.bu_step(ba);
-    }
-    if (!fused_scan) scan(L, false, enq_dir[L], chain_cap);
-    enq_fused[L] = fused_scan && d != 'S';
-    if (xc && !level_ended) finish_ranks(L, false, enq_dir[L], chain_cap, enq_gather[L] != 0);
-    if (opt_.phase_timing) evs[L] = {ev0, be_.record_event()};
-    hmark("enqueued " + std::to_string(L));
-  };
-
-  // Host loop, one level ahead of the device.  The stamp of level L - 1
-  // carries the real direction of level L and its frontier; a mispredicted
-  // level (a no-op chain, its scan skipped too) is enqueued again.
-  //   device_loop_predict: after that stamp, level L + 1 is enqueued with the
-  //     direction the device will choose if the frontier keeps its growth rate
-  //     (n_f and m_f extrapolated geometrically, run through the same
-  //     level_ctrl_finish): the Beamer switches of RMAT traversals are
-  //     predicted exactly, so no chain is wasted.
-  //   otherwise: level L + 1 is enqueued before the stamp, predicted to keep
-  //     level L's direction (two wasted chains per direction change).
-  // Several ranks: a top-down chain is sparse ('S': owner lists, live while
-  // the level's global frontier edges fit them) or dense ('T'); a sparse
-  // chain whose level turns out larger is a no-op and is re-enqueued dense,
-  // like a mispredicted direction.  Each chain's collective also all-gathers
-  // its output frontier when the level after it is predicted bottom-up (two
-  // levels ahead of the stamp: the prediction is extrapolated twice).
-  int nlev = 0;
-  LevelCtrl hc = init;  // host mirror for the prediction
-  int64_t prev_nf = 0, prev_mf = 0;
-  // top-down form of level L whose frontier has (about) mf edges: sparse when
-  // small (right after a bottom-up level too: the compaction then zeroes the
-  // bottom-up input bitmap the sparse level writes into); *cap: the global
-  // frontier edges a sparse chain stays live for
-  // (exact: mf is the level's actual frontier edges -- a re-enqueue, which
-  // must be live)
-  auto td_form = [&](int L, double mf, int64_t* cap, bool exact) {
-    *cap = 0;
-    if (xc) {
-      if (list_max <= 0) return 'T';
-      if (counted) {
-        // count-sized exchange: the largest lists cost nothing extra (cap 0:
-        // lists of a whole part, live for any level)
-        if (!exact && mf > static_cast<double>(xsparse_lim)) return 'T';
-        if (exact && !lists_unlimited && mf > static_cast<double>(list_max)) return 'T';
-        *cap = lists_unlimited ? 0 : list_max;
-        // tiny levels: chains capped at fuse_cap (fused into one launch on a
-        // direct transport; the same chains on every transport, so a shadow
-        // replay follows its recording)
-        if (fuse_cap > 0 && (exact ? mf <= static_cast<double>(fuse_cap) : mf <= static_cast<double>(opt_.xfuse_edges)))
-          *cap = fuse_cap;
-        return 'S';
-      }
-      // fixed-size exchange (cap + 1 ids per peer): lists sized for the
-      // level, list_cap_factor x the prediction (at least the actual edges
-      // of a re-enqueued level), a power of two >= 1024, and no larger than a
-      // bitmap slice's worth of ids (past that the dense form ships less)
-      const int64_t lim = std::min(list_max, std::max<int64_t>(W, 1024));
-      const double want = std::max(1024.0, exact ? mf : mf * opt_.list_cap_factor);
-      if (want > static_cast<double>(lim) || (!exact && mf > static_cast<double>(xsparse_lim))) return 'T';
-      int64_t c = 1024;
-      while (static_cast<double>(c) < want) c <<= 1;
-      *cap = std::min(c, lim);
-      return 'S';
-    }
-    const char pf = L == 0 ? 'I' : enq_form[static_cast<size_t>(L - 1)];
-    // right after a bottom-up level: sparse up to td_sparse_bu_edges, the
-    // chain live up to that many too (the prediction of a shrinking frontier
-    // overshoots, and that level reads the bottom-up output bitmap directly);
-    // elsewhere up to td_sparse_edges, live up to sparse_cap
-    const bool post_bu = pf == 'B' && opt_.td_sparse_bu_edges > opt_.td_sparse_edges;
-    int64_t lim = post_bu ? opt_.td_sparse_bu_edges : opt_.td_sparse_edges;
-    const int64_t live = post_bu && sparse_cap > 0 ? std::max(sparse_cap, opt_.td_sparse_bu_edges) : sparse_cap;
-    if (live > 0) lim = std::min(lim, live);  // (a sparse chain must stay live for mf)
-    if (sparse && mf <= static_cast<double>(lim)) {
-      *cap = live;
-      return 'S';
-    }
-    bool after_bu = false;  // (binned only before the run's first bottom-up level)
-    for (int k = 0; k < L && !after_bu; ++k) after_bu = enq_form[static_cast<size_t>(k)] == 'B';
-    return binned && !after_bu && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
-  };
-  // the chain enqueued for level L is live for a level with direction `dir`
-  // and mf global frontier edges
-  auto chain_valid = [&](int L, char dir, int64_t mf) {
-    if (enq_dir[L] != dir) return false;
-    return enq_form[L] != 'S' || enq_cap[L] <= 0 || mf <= enq_cap[L];
-  };
-  // one prediction step: from a level with frontier (nf, mf), its
-  // predecessor's (pnf, pmf) and `reached` vertices so far, the next level's
-  // frontier extrapolated geometrically (never more than the vertices with
-  // edges not reached yet) and its direction through level_ctrl_finish (c
-  // holds the known level's direction and totals on entry)
-  auto grow = [](double cur, double prev) { return prev <= 0 ? cur * cur : cur * (cur / prev); };
-  auto predict = [&](LevelCtrl& c, double nf, double mf, double pnf, double pmf, double reached, bool first,
-                     double* enf, double* emf) {
-    *enf = std::min({grow(nf, pnf), static_cast<double>(part_.n),
-                     std::max(0.0, static_cast<double>(n_active_) - reached)});
-    // level 1's frontier edges: the source's neighbours have the mean endpoint degree
-    *emf = std::min(first ? mf * std::max(1.0, excess_degree_) : grow(mf, pmf), static_cast<double>(total_directed_));
-    LevelRecDev scratch;
-    level_ctrl_finish(c, std::max<int64_t>(1, static_cast<int64_t>(*enf)), static_cast<int64_t>(*emf), false, &scratch);
-  };
-  {
-    int64_t cap0 = 0;
-    const char f0 = init.dir == 'B' ? 'B' : td_form(0, 0.0, &cap0, false);
-    enqueue_level(0, f0, cap0, -1.0, init.dir == 'B');
-  }
-  for (int L = 0;; ++L) {
-    if (!opt_.device_loop_predict) {
-      // dense top-down or bottom-up, one more level ahead
-      enqueue_level(L + 1, enq_dir[L], 0, -1.0, enq_dir[L] == 'B');
-    }
-    const volatile LevelMailbox* mb = nullptr;
-    try {
-      mb = wait_stamp(L - 1);
-    } catch (const Error& e) {
-      // which level, and the chains enqueued so far (level, form, cap)
-      std::string chains;
-      for (const auto& c : res.chains)
-        chains += " " + std::to_string(c.level) + c.form + ":" + std::to_string(c.cap);
-      throw Error(std::string(e.what()) + " (waiting for level " + std::to_string(L - 1) + "; chains" + chains + ")");
-    }
-    hmark("stamp " + std::to_string(L - 1));
-    if (mb->done) {
-      nlev = L;
-      break;
-    }
-    const char actual = static_cast<char>(mb->next_dir);
-    const int64_t nf = mb->n_f, mf = mb->m_f;
-    const bool valid = chain_valid(L, actual, mf);
-    if (!valid) ++res.mispredicts;
-    if (!opt_.device_loop_predict) {
-      if (!valid) {
-        enqueue_level(L, actual, 0, -1.0, actual == 'B');
-        enqueue_level(L + 1, actual, 0, -1.0, actual == 'B');
-      }
-      continue;
-    }
-    // level L + 1 extrapolated from the frontiers of L - 1 and L, then L + 2
-    hc.dir = actual;
-    hc.n_f = nf;
-    hc.m_f = mf;
-    hc.vis_deg = mb->vis_deg;
-    hc.done = 0;
-    double enf = 0, emf = 0, enf2 = 0, emf2 = 0;
-    predict(hc, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(prev_nf),
-            static_cast<double>(prev_mf), static_cast<double>(mb->reached), L == 0, &enf, &emf);
-    const char d1 = static_cast<char>(hc.dir);
-    LevelCtrl hc2 = hc;
-    predict(hc2, enf, emf, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(mb->reached) + enf,
-            false, &enf2, &emf2);
-    const char d2 = static_cast<char>(hc2.dir);
-    if (!valid) {
-      int64_t cap = 0;
-      const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
-      enqueue_level(L, f, cap, static_cast<double>(mf), d1 == 'B');
-    }
-    prev_nf = nf;
-    prev_mf = mf;
-    int64_t lcap = 0;
-    const char f = d1 == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
-    enqueue_level(L + 1, f, lcap, emf, d2 == 'B');
-  }
-  // The traversal is complete once the last stamp is seen: the stamping
-  // workgroup ran after all of that level's work (and every earlier level's).
-  // The chain enqueued ahead of it is a no-op that drains on its own, ordered
-  // before any later work on the stream -- no synchronisation needed.
-  const auto t1 = std::chrono::steady_clock::now();
-  if (opt_.phase_timing) be_.synchronize();
-  scratch_dirty_ = false;
-  res.ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-  if (xc) res.ms = comm_.max_host(res.ms);
-  if (host_timing) {
-    prev_done = t1;
-    hmark("done");
-    std::string line = "[host timing]";
-    for (auto& [w, us] : htl) line += " " + w + "@" + std::to_string(static_cast<int>(us));
-    std::fprintf(stderr, "%s\n", line.c_str());
-  }
-  const int64_t vis_deg = mailbox_host_[slot(nlev - 1)].vis_deg;
-
-  // per-level records (outside the timed window), from the mapped segments
-  std::vector<LevelRecDev> recs(static_cast<size_t>(nlev));
-  for (int L = 0; L < nlev; ++L) {
-    const volatile LevelRecDev* r = rec_segs_[static_cast<size_t>(L / kRecSeg)].first + L % kRecSeg;
-    recs[L].dir = r->dir;
-    recs[L].n_f = r->n_f;
-    recs[L].m_f = r->m_f;
-    recs[L].discovered = r->discovered;
-    recs[L].t0 = r->t0;
-    recs[L].t1 = r->t1;
-  }
-  res.reached = 1;
-  for (int L = 0; L < nlev; ++L) {
-    LevelRecord r;
-    r.level = L;
-    r.direction = static_cast<char>(recs[L].dir);
-    r.frontier = recs[L].n_f;
-    r.frontier_edges = recs[L].m_f;
-    r.discovered = recs[L].discovered;
-    if (opt_.phase_timing && static_cast<size_t>(L) < evs.size()) r.ms = be_.elapsed_ms(evs[L].first, evs[L].second);
-    // device-clock times (kernels stamp them; no events, no overhead)
-    const double khz = be_.wall_clock_khz();
-    if (khz > 0 && recs[L].t0 != 0 && recs[L].t1 >= recs[L].t0) {
-      if (!opt_.phase_timing) r.ms = static_cast<double>(recs[L].t1 - recs[L].t0) / khz;
-      if (L > 0 && recs[L - 1].t1 != 0)
-        r.gap_ms = (static_cast<double>(recs[L].t0) - static_cast<double>(recs[L - 1].t1)) / khz;
-    }
-    res.reached += r.discovered;
-    res.levels.push_back(r);
-  }
-  res.depth = nlev == 0 ? 1 : nlev;
-  res.edges = vis_deg / 2;
-  return res;
 }
 
 RunResult Engine::run_ref(int64_t source) {

@@ -245,12 +245,15 @@ struct EngineOptions {
   // ... levels predicted at <= xfuse_edges (a chain then live up to 4x that):
   // with a direct exchange and a folded level end, td_sparse's last workgroup
   // runs the owner side too (TdSparseArgs::fuse_apply: one launch per level);
-  // 0 disables.
-  int64_t xfuse_edges = 0;  // (pending GPU validation: 2^12)
+  // 0 disables.  (Validated over the peer transport with 4 processes on one
+  // GPU, tests/test_gpu_engine.py::test_peer_multirank_options; shadow rank 0
+  // of RMAT-26 at P = 8: level 0 11-19 -> 6-10 us.)
+  int64_t xfuse_edges = int64_t(1) << 12;
   // Several ranks, bottom-up levels: merge the gathered frontier into the
   // replicated visited bitmap (the remote slices).  Only top-down levels read
-  // remote visited bits, as a filter: a stale one sends an id its owner drops.
-  bool bu_merge_visited = true;  // (pending GPU validation: false)
+  // remote visited bits, as a filter: a stale one sends an id its owner drops,
+  // so the merge is not needed (off: validated as xfuse_edges).
+  bool bu_merge_visited = false;
   // One rank, device loop, hubs: a first bottom-up level whose frontier has
   // at most bu_cut_edges edges outside the hubs claims those vertices'
   // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
@@ -343,6 +346,8 @@ struct FaultSpec {
   static FaultSpec from_env();
 };
 
+class DeviceLoop;  // the device-driven level loop (csrc/engine/device_loop.cpp)
+
 class Engine {
  public:
   Engine(DeviceGraph& g, Comm& comm, const EngineOptions& opt = {});
@@ -364,6 +369,7 @@ class Engine {
   void set_options(const EngineOptions& o) { opt_ = o; }
 
  private:
+  friend class DeviceLoop;
   RunResult run_bitmap(int64_t source);
   RunResult run_bitmap_device(int64_t source);
   bool use_device_loop() const;
