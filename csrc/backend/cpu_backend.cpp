@@ -256,7 +256,8 @@ class CpuBackend final : public Backend {
       q = a.dev_stats[0];
       bytes = a.ctrl->bytes != 0;
       if (a.clear_qv)
-        for (int64_t i = 0; i < q; ++i) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
+        for (int64_t i = 0; i < q; ++i)
+          if (a.clear_qv[i] != kNoRow) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
     }
     for (int64_t i = 0; i < q; ++i) {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
@@ -294,8 +295,29 @@ class CpuBackend final : public Backend {
     }
   }
 
+  // the next level's hub-split entries (HxAppendArgs)
+  static void hx_append(const HxAppendArgs& h) {
+    int64_t q = h.list_stats[0], m = h.list_stats[1];
+    for (int64_t hub = 0; hub < h.nhubs; ++hub) {
+      if (!((static_cast<word_t>(h.bits[hub >> 6]) >> (hub & 63)) & 1)) continue;
+      const eid_t rs = h.hx_off[hub], d = h.hx_off[hub + 1] - rs;
+      if (d <= 0) continue;
+      const int64_t r = static_cast<int64_t>(h.hub_vertex[hub]) - h.lo;
+      h.qscan[q] = m;
+      h.qbase[q] = rs - m;
+      h.qv[q] = r >= 0 && r < h.rows ? static_cast<vid_t>(r) : kNoRow;
+      for (int64_t blk = div_up(m, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < m + d; ++blk)
+        h.blk_vstart[blk] = static_cast<int32_t>(q);
+      ++q;
+      m += d;
+    }
+    h.qscan[q] = m;
+    h.list_stats[0] = q;
+    h.list_stats[1] = m;
+  }
   void level_finish(const LevelFinishArgs& a) override {
     if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
+    if (a.hx.bits) hx_append(a.hx);
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
     level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
     *a.ctrl = c;
@@ -321,6 +343,18 @@ class CpuBackend final : public Backend {
     const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
     if (d <= 0) return;
     a.frontier_out[r >> 6] |= 1ull << (r & 63);
+    if (a.hx_bits && d >= static_cast<eid_t>(a.g.td_hub_min_deg)) {
+      // hub-split: a top-down hub with a part on this rank leaves the list
+      const vid_t* hv = a.g.td_hub_vertex;
+      const int64_t h = std::lower_bound(hv, hv + a.g.td_nhubs, v) - hv;
+      DBFS_CHECK(h < a.g.td_nhubs && hv[h] == v, "hub-split: a hub-degree vertex is not a top-down hub");
+      if (a.g.hx_off[h + 1] > a.g.hx_off[h]) {
+        a.hx_bits[h >> 6] |= 1ull << (h & 63);
+        a.hx_tot[0] += 1;
+        a.hx_tot[1] += d;
+        return;
+      }
+    }
     const int64_t cnt = sparse_cnt_, deg = sparse_deg_;
     a.oscan[cnt] = deg;
     a.obase[cnt] = rs - deg;
@@ -334,6 +368,17 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = sparse_cnt_;
     a.stats[1] = a.stats[3] = sparse_deg_;
     a.oscan[sparse_cnt_] = sparse_deg_;
+    if (a.hx_bits) {
+      // hub-split: the diverted hubs in the totals, their bits to the stats block
+      a.stats[2] += a.hx_tot[0];
+      a.stats[3] += a.hx_tot[1];
+      a.stats[4] = a.hx_tot[0];
+      a.hx_tot[0] = a.hx_tot[1] = 0;
+      for (int64_t w = 0; w < div_up(a.g.td_nhubs, int64_t(64)); ++w) {
+        a.hx_out[w] = static_cast<int64_t>(a.hx_bits[w]);
+        a.hx_bits[w] = 0;
+      }
+    }
   }
   void td_sparse(const TdSparseArgs& a) override {
     DBFS_CHECK(!a.direct.active, "CpuBackend: no direct list exchange (peer windows are GPU memory)");
@@ -351,7 +396,8 @@ class CpuBackend final : public Backend {
       }
     } else {
       const int64_t q = a.dev_stats[0];
-      for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
+      for (int64_t i = 0; i < q; ++i)
+        if (a.qv[i] != kNoRow) a.frontier_in[a.qv[i] >> 6] = 0;
       for (int64_t i = 0; i < q; ++i) rows.emplace_back(a.qscan[i] + a.qbase[i], a.qscan[i + 1] + a.qbase[i]);
     }
     sparse_cnt_ = sparse_deg_ = 0;
@@ -668,6 +714,16 @@ class CpuBackend final : public Backend {
       }
     }
     (void)pref;
+  }
+  void hx_count(const ShardView& g, eid_t* cnt) override {
+    for (int64_t r = 0; r < g.rows; ++r)
+      for (eid_t e = g.row_off[r]; e < g.row_off[r + 1]; ++e)
+        if (g.td_col[e] & kHubFlag) ++cnt[g.td_col[e] & ~kHubFlag];
+  }
+  void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) override {
+    for (int64_t r = 0; r < g.rows; ++r)
+      for (eid_t e = g.row_off[r]; e < g.row_off[r + 1]; ++e)
+        if (g.td_col[e] & kHubFlag) out[cursor[g.td_col[e] & ~kHubFlag]++] = static_cast<vid_t>(g.lo + r);
   }
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {

@@ -268,6 +268,16 @@ class HipBackend final : public Backend {
     kern::row_heads(ro, col, rows, head, hub_idx, st_);
     chk();
   }
+  void hx_count(const ShardView& g, eid_t* cnt) override {
+    on();
+    kern::hx_rows(g, cnt, nullptr, st_);
+    chk();
+  }
+  void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) override {
+    on();
+    kern::hx_rows(g, cursor, out, st_);
+    chk();
+  }
   void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
     on();
     kern::encode_hub_cols(col, nnz, hub_idx, out, st_);

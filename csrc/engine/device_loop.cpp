@@ -105,7 +105,10 @@ class DeviceLoop {
   bool cells_fit() const { return e_.g_.rows() < (int64_t(1) << 32) && e_.g_.nnz() < (int64_t(1) << 40); }
   const volatile LevelMailbox* wait_stamp(int lv);
   LevelFinishArgs finish_args(int level, bool seed, char expect_dir, int64_t cap);
-  void finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather);
+  void finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather, bool hx = false);
+  // the chain of level L (sparse, several ranks) is hub-split
+  bool hx_chain(int L) const;
+  int64_t hx_words() const { return 1 + div_up(gv_.td_nhubs, kWordBits); }
   ScanArgs scan_args(int level, bool seed, char expect_dir, int64_t cap);
 
   // ---- planner ----
@@ -290,13 +293,40 @@ LevelFinishArgs DeviceLoop::finish_args(int level, bool seed, char expect_dir, i
 // in the same launch the level's output frontier slice all-gathered
 // (Comm::allgather_allreduce) -- then level_finish decides and stamps.
 // (bfs_mpi.cu:615-621 pays a Sendrecv and an Allreduce per level.)
-void DeviceLoop::finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather) {
+// (hx: a hub-split level also all-reduces its hub count and frontier-hub
+// bits -- blk[4 ..] -- and the finish appends the next level's hub-split
+// entries to this level's output list)
+void DeviceLoop::finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather, bool hx) {
   int64_t* blk = sblk(level);
   // level L writes frontier_[L & 1] (the seed: frontier_[1])
   const int out = seed ? 1 : (level & 1);
-  const LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
+  LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
+  if (hx) {
+    HxAppendArgs& h = fa.hx;
+    h.bits = blk + kHxStatsWord;
+    h.hx_off = gv_.hx_off;
+    h.hub_vertex = gv_.td_hub_vertex;
+    h.nhubs = gv_.td_nhubs;
+    h.lo = gv_.lo;
+    h.rows = gv_.rows;
+    h.list_stats = blk;
+    h.qscan = qscan_set(level + 1);
+    h.qbase = qbase_set(level + 1);
+    h.blk_vstart = blk_set(level + 1);
+    h.qv = e_.qv_[(level + 1) & 1].data();
+  }
   comm_.level_end(fr_own(out), e_.frontier_[out].data(), gather ? static_cast<size_t>(W_) * sizeof(word_t) : 0,
-                  blk + 2, 2, fa);
+                  blk + 2, hx ? 2 + static_cast<size_t>(hx_words()) : 2, fa);
+}
+
+// Hub-split sparse chains: several ranks with hub-split rows, the first
+// hx_levels levels, none after a bottom-up level (by then the hubs are
+// visited; a hub settled later is expanded by its owner, as any vertex).
+bool DeviceLoop::hx_chain(int L) const {
+  if (!xc_ || !gv_.hx_off || !e_.hx_bits_.data() || L >= opt_.hx_levels) return false;
+  for (int k = 0; k < L; ++k)
+    if (enq_form_[static_cast<size_t>(k)] == 'B') return false;
+  return true;
 }
 
 ScanArgs DeviceLoop::scan_args(int level, bool seed, char expect_dir, int64_t cap) {
@@ -427,7 +457,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
   enq_form_[L] = d;
   enq_cap_[L] = d == 'S' ? cap : 0;
   enq_gather_[L] = xc_ && gather;
-  res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0});
+  res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
   c.cap = enq_cap_[L];
   c.mf_hint = mf_hint;
   c.cur = (L + 1) & 1;
@@ -455,7 +485,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
   }
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
   enq_fused_[L] = c.fused_scan && d != 'S';
-  if (xc_ && !c.level_ended) finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] != 0);
+  if (xc_ && !c.level_ended) finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] != 0, d == 'S' && hx_chain(L));
   if (opt_.phase_timing) evs_[L] = {ev0, be_.record_event()};
   if (ht_) hmark("enqueued " + std::to_string(L));
 }
@@ -562,10 +592,18 @@ void DeviceLoop::emit_sparse(Chain& c) {
   const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
   sp.nranks = P_;
   const int64_t apply_grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
+  // hub-split: settled hubs leave the owner's list (their bits and totals
+  // ride the level end, a collective: the cells carry two totals only)
+  const bool hx = hx_chain(L);
+  if (hx) {
+    sp.hx_bits = e_.hx_bits_.data();
+    sp.hx_tot = e_.hx_tot_.data();
+    sp.hx_out = sblk(L) + kHxStatsWord;
+  }
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
-  const bool end_ok = direct && opt_.direct_level_end && cells_fit() && !enq_gather_[L];
+  const bool end_ok = direct && opt_.direct_level_end && cells_fit() && !enq_gather_[L] && !hx;
   // a tiny level (its chain capped at fuse_cap): td_sparse's last workgroup
   // also runs the owner side and the level end -- one launch (the direct
   // level end is taken in the same order as unfused)

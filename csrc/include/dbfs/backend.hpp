@@ -79,7 +79,19 @@ struct ShardView {
   // vertex of degree >= the hub threshold, so a hub-first row's hubs are a
   // prefix of it).  Read by the hub-cut bottom-up level (BuArgs::cut_edges).
   const word_t* hub_bits = nullptr;
+  // Several ranks, hub-split top-down levels (EngineOptions::hx_levels):
+  // this rank's part of every top-down hub's row -- the hub's neighbours among
+  // this rank's own vertices, as global ids, in id order -- at
+  // col[hx_off[h] .. hx_off[h + 1]) (and td_col, hub-encoded), past the
+  // rows' nnz entries (td_nhubs + 1 absolute offsets).  A vertex is a
+  // top-down hub iff its degree >= td_hub_min_deg.
+  const eid_t* hx_off = nullptr;
+  uint32_t td_hub_min_deg = 0;
 };
+
+// Work-list entry without a frontier vertex of this rank (a hub-split entry of
+// a hub owned elsewhere): its qv, whose frontier bit the consumer must not clear.
+constexpr vid_t kNoRow = 0xFFFFFFFFu;
 
 // At most kTdMaxHubs top-down hubs (their visited bits, 8 KiB, sit in LDS
 // next to the top-down owner map: five 256-thread workgroups per CU).
@@ -329,6 +341,27 @@ struct UpdateArgs {
 // Device loop, several ranks: after the totals' all-reduce (stats[2..3] =
 // global count / degree sum), one thread runs level_ctrl_finish (seed: from
 // ctrl_init) and stamps rec / the mailbox, as the one-rank scan does.
+// Hub-split top-down levels (several ranks): the level's end also appends,
+// to the level's output work list, an entry per frontier hub -- this rank's
+// part of the hub's row (ShardView::hx_off) -- for every set bit of bits
+// (kTdMaxHubs bits in hub-index order, the all-reduced stats words [5 ..]:
+// each hub's bit comes from its owner alone, so the sum is the OR).  The
+// list's local totals list_stats[0..1] (entries, edges) grow accordingly;
+// entries of hubs owned elsewhere carry qv = kNoRow.  One workgroup, after the
+// reduction (LevelFinishArgs::hx.bits set: active).
+struct HxAppendArgs {
+  const int64_t* bits = nullptr;
+  const eid_t* hx_off = nullptr;
+  const vid_t* hub_vertex = nullptr;  // ShardView::td_hub_vertex (ascending)
+  int64_t nhubs = 0;
+  int64_t lo = 0, rows = 0;
+  int64_t* list_stats = nullptr;
+  int64_t* qscan = nullptr;
+  int64_t* qbase = nullptr;
+  int32_t* blk_vstart = nullptr;
+  vid_t* qv = nullptr;
+};
+
 struct LevelFinishArgs {
   const int64_t* stats = nullptr;
   LevelCtrl* ctrl = nullptr;
@@ -339,7 +372,12 @@ struct LevelFinishArgs {
   bool seed = false;
   int32_t expect_dir = 0;
   int64_t expect_cap = 0;  // see ScanArgs::expect_cap
+  HxAppendArgs hx;         // hub-split entries of the next level (hx.bits: on)
 };
+
+// Words of a hub-split level's end in its stats block: [2] count, [3] degree
+// sum, [4] hubs diverted, then the frontier hubs' bits (kHxStatsWord ...).
+constexpr int64_t kHxStatsWord = 5;
 
 // A device-loop chain's kernels run only when the chain is live: the level is
 // not done, its direction is the one the chain was enqueued for, and (list-form
@@ -495,6 +533,18 @@ struct TdSparseArgs {
   // Comm::level_end without a frontier gather; no collective launch after.
   DirectExchange end;
   LevelFinishArgs fin;
+  // Hub-split top-down (several ranks, ShardView::hx_off): a settled vertex
+  // of degree >= g.td_hub_min_deg (a top-down hub) gets its level and frontier
+  // bit but no entry in the output work list -- every rank expands its own
+  // part of the hub's row at the next level instead (the level end appends
+  // them, HxAppendArgs) -- its bit goes to hx_bits (hub index order, zero on
+  // entry) and its count / degree to hx_tot[0..1] (zero on entry).  The
+  // level's last workgroup adds them to the totals (stats[2..3], stats[4] =
+  // hubs), moves hx_bits to hx_out (the stats block's hub words) and zeroes
+  // hx_bits / hx_tot.
+  word_t* hx_bits = nullptr;
+  int64_t* hx_tot = nullptr;
+  int64_t* hx_out = nullptr;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -963,6 +1013,12 @@ class Backend {
   // (ceil(rows / 4096) + 1 entries).
   virtual void nz_records(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, NzRec* rec,
                           eid_t* unit_base) = 0;
+  // Hub-split rows (ShardView::hx_off): cnt[h] += entries of the rows whose
+  // td_col neighbour is top-down hub h (td_col hub-encoded, cnt zeroed by the
+  // caller); then, after an exclusive scan into cursor, out[cursor[h]++] = lo
+  // + r for every such entry of row r.
+  virtual void hx_count(const ShardView& g, eid_t* cnt) = 0;
+  virtual void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) = 0;
   // out[e] = kHubFlag | hub_idx[col[e]] for hub neighbours, else col[e].
   virtual void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) = 0;
   // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex

@@ -68,7 +68,9 @@ class DeviceGraph {
   // hub-encoded copy and `col` is then put in neighbour-id order for the
   // top-down sweeps (neighbours of one row probe the bitmaps monotonically).
   // ... and with `td_hubs` also the hub-encoded top-down copy td_col (the
-  // kTdMaxHubs highest-degree vertices encoded; one more nnz x 4 B).
+  // kTdMaxHubs highest-degree vertices encoded; one more nnz x 4 B), and with
+  // several ranks the hub-split rows (ShardView::hx_off): this rank's part
+  // of every top-down hub's row, for the hub-split top-down levels.
   void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs, bool id_order = true,
                                 bool td_hubs = true);
   bool hub_sorted() const { return hub_sorted_; }
@@ -81,6 +83,14 @@ class DeviceGraph {
     int64_t byte_begin = -1, byte_end = -1, edges = -1;
   };
   const IngestInfo& ingest() const { return ingest_; }
+  // Hub-split rows copied back (tests): the top-down hubs (ascending), the
+  // offsets of their parts relative to the first, and the parts (global ids)
+  struct HubSplitHost {
+    std::vector<vid_t> hubs;
+    std::vector<eid_t> off;
+    std::vector<vid_t> col;
+  };
+  HubSplitHost hub_split_host() const;
 
  private:
   IngestInfo ingest_;
@@ -93,6 +103,11 @@ class DeviceGraph {
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
+  // several ranks: hub-split rows (ShardView::hx_off), appended to col_ / td_col_
+  DBuf<eid_t> hx_off_;
+  uint32_t td_hub_min_deg_ = 0;
+  void build_hub_split();
+  int64_t hx_total() const;
   DBuf<word_t> hub_bits_;  // global vertex bitmap of the hubs
   int64_t td_nhubs_ = 0;
   DBuf<eid_t> nz_pref_, nz_row_off_;
@@ -254,6 +269,13 @@ struct EngineOptions {
   // remote visited bits, as a filter: a stale one sends an id its owner drops,
   // so the merge is not needed (off: validated as xfuse_edges).
   bool bu_merge_visited = false;
+  // Several ranks, hub-split top-down levels: the sparse chains of the first
+  // hx_levels levels (before any bottom-up level) divert the top-down hubs
+  // they settle from the owner's work list -- every rank then expands its own
+  // part of each frontier hub's row (ShardView::hx_off), claims local, no
+  // exchange -- their bits ride the level end.  Replaces the owner expanding a
+  // hub's whole row and shipping its claims (bfs.cu:577-586, 143).  0: off.
+  int hx_levels = 4;
   // One rank, device loop, hubs: a first bottom-up level whose frontier has
   // at most bu_cut_edges edges outside the hubs claims those vertices'
   // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
@@ -325,6 +347,9 @@ struct ChainRecord {
   char form = 'T';
   int64_t cap = 0;
   bool gather = false;
+  // hub-split chain: its level end all-reduces this many words more than the
+  // totals (the hub count and the frontier-hub bits)
+  int64_t hx_words = 0;
 };
 
 struct RunResult {
@@ -397,6 +422,8 @@ class Engine {
   DBuf<uint8_t> level8_;
   DBuf<uint32_t> td_group_ticket_;  // UpdateArgs::group_ticket
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
+  DBuf<word_t> hx_bits_;  // hub-split levels: TdSparseArgs::hx_bits (zero between levels)
+  DBuf<int64_t> hx_tot_;  // ... TdSparseArgs::hx_tot
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill

@@ -156,9 +156,7 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   }
 }
 
-__global__ void level_finish_kernel(LevelFinishArgs a) {
-  if (threadIdx.x == 0) level_finish_device(a);
-}
+__global__ __launch_bounds__(kBlock) void level_finish_kernel(LevelFinishArgs a) { level_finish_block<kBlock>(a); }
 
 // Level totals -> host-mapped mailbox: values first (system scope), then the
 // sequence number with release semantics, so a host that observes `seq` reads
@@ -791,7 +789,7 @@ void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStr
   widen_levels_kernel<<<grid_for(n, kBlock, 8 * device_cus()), kBlock, 0, st>>>(in, out, n, base);
 }
 
-void level_finish(const LevelFinishArgs& a, hipStream_t st) { level_finish_kernel<<<1, 64, 0, st>>>(a); }
+void level_finish(const LevelFinishArgs& a, hipStream_t st) { level_finish_kernel<<<1, kBlock, 0, st>>>(a); }
 
 void list_scatter(const ListScatterArgs& a, hipStream_t st) {
   if (a.nranks <= 0 || a.list_cap <= 0) return;

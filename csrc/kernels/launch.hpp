@@ -28,6 +28,9 @@ void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
                      unsigned* ticket, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
+// graph_sort.hip: hub-split rows of ShardView::hx_off -- counts per top-down
+// hub (out == nullptr), or the rows' global ids at cnt[h]++ (cursors)
+void hx_rows(const ShardView& g, eid_t* cnt, vid_t* out, hipStream_t st);
 void level_finish(const LevelFinishArgs& a, hipStream_t st);
 void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
@@ -87,12 +90,12 @@ struct PeerUnpackArgs {
   int64_t sum_count = 0;            // > 0: all-reduce -- sum_out[i] = sum_p sum_src[p][i] (uint64, wrapping)
   const void* sum_src[kMaxPeers] = {};
   void* sum_out = nullptr;
-  // then a level's decision on the sums (sum_count <= kPeerFinishMax: the
-  // first workgroup sums everything, its thread 0 finishes the level)
+  // then a level's end on the sums (sum_count <= kPeerFinishMax: the first
+  // workgroup sums everything, then finishes the level: level_finish_block)
   bool has_finish = false;
   LevelFinishArgs finish;
 };
-constexpr int64_t kPeerFinishMax = 256;
+constexpr int64_t kPeerFinishMax = 2048;
 void peer_push(const PeerPushArgs& a, hipStream_t st);
 void peer_wait(const PeerWaitArgs& a, hipStream_t st);
 void peer_unpack(const PeerUnpackArgs& a, hipStream_t st);

@@ -91,9 +91,10 @@ __device__ __forceinline__ void push_pieces(const PeerPushArgs& a, int nthreads)
 // copied to the caller's buffers, segment 1 summed.
 __device__ __forceinline__ void unpack_pieces(const PeerUnpackArgs& a, int64_t gt, int64_t nt) {
   if (a.has_finish) {
-    // a level's end: the first workgroup sums the (few) totals and its
-    // thread 0 makes the level's decision on them (the stamp the host and
-    // the next level's kernels read)
+    // a level's end: the first workgroup sums the totals (and a hub-split
+    // level's hub bits), then finishes the level -- the next level's hub-split
+    // entries, thread 0's decision (the stamp the host and the next level's
+    // kernels read)
     if (blockIdx.x == 0) {
       for (int64_t i = threadIdx.x; i < a.sum_count; i += blockDim.x) {
         uint64_t acc = 0;
@@ -101,7 +102,7 @@ __device__ __forceinline__ void unpack_pieces(const PeerUnpackArgs& a, int64_t g
         static_cast<uint64_t*>(a.sum_out)[i] = acc;
       }
       __syncthreads();
-      if (threadIdx.x == 0) level_finish_device(a.finish);
+      level_finish_block<kBlock>(a.finish);
     }
   } else if (a.sum_count > 0) {
     // all-reduce: out[i] = sum over ranks of slot[p][i] (wrapping, as RCCL)

@@ -200,8 +200,10 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     if (a.clear_qv) stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
     if (a.clear_qv)
       for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < q;
-           i += static_cast<int64_t>(gridDim.x) * kThreads)
-        a.clear_frontier[a.clear_qv[i] >> 6] = 0ull;
+           i += static_cast<int64_t>(gridDim.x) * kThreads) {
+        const vid_t r = a.clear_qv[i];
+        if (r != kNoRow) a.clear_frontier[r >> 6] = 0ull;  // (kNoRow: a hub-split entry)
+      }
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const int t = threadIdx.x;
@@ -319,6 +321,47 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   }
 }
 
+// Hub-split levels (TdSparseArgs::hx_bits): the claimed top-down hubs among a
+// lane's items whose row has a part on this rank (ShardView::hx_off; a hub
+// with none is listed as usual) leave the work list -- re = rs -- and get
+// their frontier bit, their bit in hx_bits and their count / degree in
+// hx_tot (one pair of atomics per wave).  The hub index is found by binary
+// search in td_hub_vertex (ascending): hubs are a handful per level.
+template <int kItems>
+__device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed,
+                                          const eid_t (&rs)[kItems], eid_t (&re)[kItems]) {
+  unsigned hub = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k)
+    if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.td_hub_min_deg)) hub |= 1u << k;
+  if (!__ballot(hub != 0)) return;
+  long long hc = 0, hd = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    if (!((hub >> k) & 1u)) continue;
+    int64_t lo_i = 0, hi_i = a.g.td_nhubs;  // first index with td_hub_vertex >= v
+    while (lo_i < hi_i) {
+      const int64_t mid = (lo_i + hi_i) >> 1;
+      if (a.g.td_hub_vertex[mid] < v[k]) lo_i = mid + 1;
+      else hi_i = mid;
+    }
+    DBFS_DCHECK(lo_i < a.g.td_nhubs && a.g.td_hub_vertex[lo_i] == v[k], 12, v[k]);
+    if (a.g.hx_off[lo_i + 1] == a.g.hx_off[lo_i]) continue;  // (no part here: listed)
+    const int64_t r = static_cast<int64_t>(v[k]) - a.g.lo;
+    atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
+    atomicOr(a.hx_bits + (lo_i >> 6), 1ull << (lo_i & 63));
+    ++hc;
+    hd += static_cast<long long>(re[k] - rs[k]);
+    re[k] = rs[k];
+  }
+  hc = wave_sum(hc);
+  hd = wave_sum(hd);
+  if (lane_id() == 0 && hc) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.hx_tot), static_cast<unsigned long long>(hc));
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.hx_tot + 1), static_cast<unsigned long long>(hd));
+  }
+}
+
 // The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
 // of this shard): level, frontier bit, and the wave's work-list entries of
 // the next level with one packed atomic (count << kSparseEdgeBits | edges)
@@ -342,6 +385,7 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
       re[k] = ro[r + 1];
     }
   }
+  if (a.hx_bits) hx_divert<kItems>(a, v, claimed, rs, re);
   unsigned long long tm[kItems];
   long long incl[kItems], cbase[kItems], ebase[kItems];
   long long ctot = 0, etot = 0;
@@ -385,6 +429,9 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
 
 // The level's local totals from the packed counter (one thread of the last
 // workgroup): stats, the work list's end marker, counter and ticket reset.
+// (hub-split levels: the diverted hubs count in the level's totals -- cnt /
+// deg returned, stats[2..3], stats[4] = hubs -- but not in the list's
+// stats[0..1]; hx_tot zeroed)
 __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -392,9 +439,19 @@ __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& 
   deg = static_cast<long long>(tot & kEdgeMask);
   *a.counter = 0ull;
   *a.ticket = 0u;
-  a.stats[0] = a.stats[2] = cnt;
-  a.stats[1] = a.stats[3] = deg;
+  a.stats[0] = cnt;
+  a.stats[1] = deg;
   a.oscan[cnt] = deg;
+  if (a.hx_bits) {
+    const long long hc = __hip_atomic_load(a.hx_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long hd = __hip_atomic_load(a.hx_tot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.hx_tot[0] = a.hx_tot[1] = 0;
+    a.stats[4] = hc;
+    cnt += hc;
+    deg += hd;
+  }
+  a.stats[2] = cnt;
+  a.stats[3] = deg;
 }
 
 // PeerComm::self_test of the direct exchanges (one workgroup): rank r sends
@@ -570,6 +627,13 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
     s_tot[0] = cnt;
     s_tot[1] = deg;
   }
+  // hub-split: the level's frontier-hub bits to the stats block (the level
+  // end carries them to every rank), the accumulator zeroed for the next
+  if (a.hx_bits)
+    for (int64_t w = t; w < (a.g.td_nhubs + 63) / 64; w += kThreads) {
+      a.hx_out[w] = static_cast<int64_t>(a.hx_bits[w]);
+      a.hx_bits[w] = 0ull;
+    }
   if (!a.end.active) return;
   __syncthreads();
   direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
@@ -616,7 +680,10 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
   const int64_t gstride = static_cast<int64_t>(active) * kThreads;
   // the input vertices' frontier bits (the bitmap is not read here)
-  for (int64_t i = gtid; i < q; i += gstride) a.frontier_in[a.qv[i] >> 6] = 0ull;
+  for (int64_t i = gtid; i < q; i += gstride) {
+    const vid_t r = a.qv[i];
+    if (r != kNoRow) a.frontier_in[r >> 6] = 0ull;  // (kNoRow: a hub-split entry of a hub owned elsewhere)
+  }
 
   const vid_t* __restrict__ col = a.g.col;
   const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);

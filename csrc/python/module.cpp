@@ -579,6 +579,14 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("col_by_id", &DeviceGraph::col_by_id)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
+      // hub-split rows (tests): (hubs, offsets, parts) as numpy arrays
+      .def("hub_split_rows",
+           [](const DeviceGraph& g) {
+             const auto h = g.hub_split_host();
+             return py::make_tuple(py::array_t<vid_t>(h.hubs.size(), h.hubs.data()),
+                                   py::array_t<eid_t>(h.off.size(), h.off.data()),
+                                   py::array_t<vid_t>(h.col.size(), h.col.data()));
+           })
       // from_file: (byte_begin, byte_end, edges) this rank parsed
       .def_property_readonly("ingest",
                              [](const DeviceGraph& g) {
@@ -598,7 +606,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
                              [](const RunResult& r) {
                                py::list out;
                                for (const auto& c : r.chains)
-                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather));
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.hx_words));
                                return out;
                              })
       .def("level_dicts", &level_dicts);

@@ -3,7 +3,7 @@
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
 collectives and bytes of a traversal can be predicted from its chains
-(``BFSResult.chains``: level, form, capacity, gather) and checked against the
+(``BFSResult.chains``: level, form, capacity, gather, hub-split words) and checked against the
 communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
 ``table`` turns a 1-GPU level profile into the per-level bytes / collectives
 table of docs/ARCHITECTURE.md §4.
@@ -74,19 +74,21 @@ class ChainTraffic:
         return sum(v for k, v in self.calls.items() if k not in ("barrier", "fused")) - self.calls["fused"]
 
 
-def level_end(cfg: ModelConfig, gather: bool) -> ChainTraffic:
-    """The one collective that ends a level (or the seed)."""
+def level_end(cfg: ModelConfig, gather: bool, hx_words: int = 0) -> ChainTraffic:
+    """The one collective that ends a level (or the seed); a hub-split level
+    (hx_words > 0) also all-reduces its hub count and frontier-hub bits."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
     if gather:
         t.add("allgather", (P - 1) * W * WORD)
-    t.add("allreduce", (P - 1) * 8 * 2)
+    t.add("allreduce", (P - 1) * 8 * (2 + hx_words))
     if gather and cfg.fused:
         t.add("fused", 0)
     return t
 
 
-def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool) -> ChainTraffic:
+def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool,
+                  hx_words: int = 0) -> ChainTraffic:
     """Collectives of one level chain."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
@@ -96,22 +98,23 @@ def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gather
         t.add("alltoallv", (P - 1) * ((cap or cfg.list_max) + 1) * 4)  # owner lists, count first
     elif form == "T":
         t.add("alltoall", (P - 1) * W * WORD)               # candidate bitmap slices
-    t.merge(level_end(cfg, gather))
+    t.merge(level_end(cfg, gather, hx_words))
     return t
 
 
 def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     """Traffic of one traversal from its enqueued chains (level, form, cap,
-    gather): start barrier, the seed's collective, every chain, the wall-time
-    max at the end."""
+    gather[, hub-split words]): start barrier, the seed's collective, every
+    chain, the wall-time max at the end."""
     P = cfg.nranks
     tot = ChainTraffic()
     tot.add("barrier", 0)
     seed_gather = cfg.mode == "bu"
     tot.merge(level_end(cfg, seed_gather))
     gathered = {-1: seed_gather}
-    for level, form, cap, gather in chains:
-        tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False)))
+    for level, form, cap, gather, *hx in chains:
+        tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False),
+                                int(hx[0]) if hx else 0))
         gathered[level] = bool(gather)
     tot.add("allgather", (P - 1) * 8)  # max over ranks of the wall time
     return tot

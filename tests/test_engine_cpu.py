@@ -644,3 +644,61 @@ def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs, narrow):
         assert res.edges == int(deg[exp != dbfs.UNREACHED].sum()) // 2
         assert "B" in "".join(l["dir"] for l in res.levels)
         assert bfs.validate(src)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("mode", ["do", "td"])
+def test_hub_split_top_down_levels(P, mode):
+    """Hub-split top-down levels (several ranks, hx_levels): the early sparse
+    chains leave the top-down hubs they settle out of the owner's work list and
+    every rank expands its own part of each frontier hub's row (hx_off) at the
+    next level.  Levels exact against the oracle, and the per-level records
+    (direction, frontier vertices / edges, discoveries) equal the run without
+    hub-split levels: the diverted hubs count in the totals."""
+    p = dbfs.rmat_params(13, 16, 23)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [5, 999, 4321]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode=mode)
+        assert b.graph.partition.nranks == P
+        out = []
+        for hx in (4, 0):
+            b.engine.set_option("hx_levels", hx)
+            for s in srcs:
+                r = b.run(s)
+                recs = [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+                out.append((hx, s, b.levels(), recs, [c[4] for c in r.chains]))
+        return out
+
+    for outs in run_virtual_ranks(P, body, device="cpu"):
+        with_hx = {s: (lv, recs, hxw) for hx, s, lv, recs, hxw in outs if hx}
+        without = {s: (lv, recs, hxw) for hx, s, lv, recs, hxw in outs if not hx}
+        for s in srcs:
+            exp = dbfs.cpu_bfs(csr, s)[0]
+            assert np.array_equal(with_hx[s][0], exp) and np.array_equal(without[s][0], exp)
+            assert with_hx[s][1] == without[s][1]
+            assert any(w > 0 for w in with_hx[s][2]) and not any(without[s][2])
+
+
+def test_hub_split_rows_partition_hub_rows():
+    """The hub-split rows of every rank together are exactly the top-down
+    hubs' rows: rank r's part of hub h = h's neighbours owned by r, in id
+    order (duplicates kept, as the rows keep them)."""
+    p = dbfs.rmat_params(11, 16, 3)
+    csr = dbfs.host_csr_from_params(p)
+    ro, col = np.asarray(csr.row_off), np.asarray(csr.col)
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        return b.graph.lo, b.graph.rows, b.graph.hub_split_rows()
+
+    outs = run_virtual_ranks(3, body, device="cpu")
+    hubs = outs[0][2][0]
+    assert len(hubs) > 0 and np.all(np.diff(hubs.astype(np.int64)) > 0)
+    for lo, rows, (h, off, part) in outs:
+        assert np.array_equal(h, hubs)
+        for k in range(0, len(hubs), max(1, len(hubs) // 50)):
+            row = col[ro[hubs[k]]:ro[hubs[k] + 1]].astype(np.int64)
+            mine = np.sort(row[(row >= lo) & (row < lo + rows)])
+            assert np.array_equal(part[off[k]:off[k + 1]].astype(np.int64), mine)

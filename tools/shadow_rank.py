@@ -28,6 +28,7 @@ def main() -> int:
     ap.add_argument("--ranks", type=int, nargs="+", default=[0, 7], help="ranks to replay")
     ap.add_argument("--roots", type=int, default=4)
     ap.add_argument("--root-seed", type=int, default=12345)
+    ap.add_argument("--root-list", type=int, nargs="+", default=None, help="explicit roots (instead of sampling)")
     ap.add_argument("--mode", default="do")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE")
@@ -46,7 +47,7 @@ def main() -> int:
     one = dbfs.BFS(params, rt, mode=args.mode)
     for k, v in opts.items():
         one.engine.set_option(k, v)
-    roots = one.sample_roots(args.roots, seed=args.root_seed)
+    roots = args.root_list or one.sample_roots(args.roots, seed=args.root_seed)
     one.run(roots[0])
     ref = []
     for r in roots:
