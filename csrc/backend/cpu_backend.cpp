@@ -747,7 +747,7 @@ class CpuBackend final : public Backend {
         const vid_t hv = a.g.hub_vertex[w * 64 + b];
         if (test_bit(a.frontier, hv)) {
           m |= 1ull << b;
-          if (a.cut_part) d += a.g.row_off[hv + 1] - a.g.row_off[hv];
+          if (a.cut_part) d += a.g.hub_deg ? a.g.hub_deg[w * 64 + b] : a.g.row_off[hv + 1] - a.g.row_off[hv];
         }
       }
       a.hub_front[w] = m;
@@ -762,18 +762,45 @@ class CpuBackend final : public Backend {
       for (int64_t i = 0; i < a.words; ++i) a.visited[i] |= a.frontier[i];
   }
   void bu_cut_prep(const BuArgs& a) override {
+    DBFS_CHECK(!a.cut_direct.active, "CpuBackend: no direct list exchange");
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     if (!*a.cut_flag) return;
+    const int64_t lo = a.g.lo;
     for (int64_t w = 0; w < a.words; ++w)
-      for (word_t m = a.frontier[w] & ~a.g.hub_bits[w]; m; m &= m - 1) {
+      for (word_t m = a.frontier[a.cut_fr_base + w] & ~a.g.hub_bits[a.cut_fr_base + w]; m; m &= m - 1) {
         const int64_t v = w * 64 + __builtin_ctzll(m);
         for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
           const vid_t t = a.g.col[e];
-          if (test_bit(a.visited, t)) continue;
-          if (a.cut_claim) a.cut_claim[t] = 1;
-          else put_level(nullptr, a.level8, t, a.new_level, a.narrow_base);
+          const int64_t r = static_cast<int64_t>(t) - lo;
+          if (r < 0 || r >= a.g.rows) {
+            // (several ranks) a remote neighbour: once per rank, to its owner
+            if (test_bit(a.cut_visited, t)) continue;
+            a.cut_visited[t >> 6] |= 1ull << (t & 63);
+            vid_t* list = a.cut_lists + (static_cast<int64_t>(t) / a.part) * a.cut_list_stride;
+            DBFS_CHECK(static_cast<int64_t>(list[0]) + 1 < a.cut_list_stride, "hub-cut owner list overflow");
+            list[1 + list[0]++] = t;
+            continue;
+          }
+          if (test_bit(a.visited, static_cast<uint64_t>(r))) continue;
+          if (a.cut_claim) a.cut_claim[r] = 1;
+          else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
         }
       }
+  }
+  void bu_cut_apply(const BuArgs& a) override {
+    for (int p = 0; p < a.nranks; ++p) a.cut_lists[static_cast<int64_t>(p) * a.cut_list_stride] = 0;
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    if (!*a.cut_flag) return;
+    for (int p = 0; p < a.nranks; ++p) {
+      const vid_t* list = a.cut_recv_lists + static_cast<int64_t>(p) * a.cut_list_stride;
+      for (vid_t k = 0; k < list[0]; ++k) {
+        const int64_t r = static_cast<int64_t>(list[1 + k]) - a.g.lo;
+        DBFS_CHECK(r >= 0 && r < a.g.rows, "hub-cut claim outside this shard");
+        if (test_bit(a.visited, static_cast<uint64_t>(r))) continue;
+        if (a.cut_claim) a.cut_claim[r] = 1;
+        else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
+      }
+    }
   }
   void hub_apply(const HubApplyArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

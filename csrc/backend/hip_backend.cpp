@@ -246,6 +246,7 @@ class HipBackend final : public Backend {
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void bu_cut_prep(const BuArgs& a) override { on(); kern::bu_cut_prep(a, st_); chk(); }
+  void bu_cut_apply(const BuArgs& a) override { on(); kern::bu_cut_apply(a, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
   void hub_apply(const HubApplyArgs& a) override { on(); kern::hub_apply(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }

@@ -44,6 +44,7 @@ class DeviceLoop {
     bool in_gathered = false;  // the input frontier is global already
     bool fused_scan = false;   // the chain's last kernel finishes the level
     bool level_ended = false;  // ... and also ran its level end (direct exchange)
+    bool cut = false;          // several ranks: a hub-cut bottom-up level was enqueued
   };
 
   Engine& e_;
@@ -483,6 +484,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     case 'T': emit_dense(c); break;
     default: emit_bottom_up(c); break;
   }
+  res_.chains.back().cut = c.cut;
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
   enq_fused_[L] = c.fused_scan && d != 'S';
   if (xc_ && !c.level_ended) finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] != 0, d == 'S' && hx_chain(L));
@@ -820,15 +822,23 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.visited = e_.visited_.data();
       hg.words = GW_;
     }
-    // one rank, a first bottom-up level: the hub cut (decided on the device
-    // from the frontier hubs' degrees hub_gather sums), enqueued for levels
-    // predicted at <= bu_cut_mf_frac of the graph's edges (a first bottom-up
-    // level's non-hub frontier edges grow with its frontier: the larger ones
-    // never cut, and skip its launches)
-    const bool cut = !xc_ && opt_.bu_cut_edges > 0 && c.pf != 'B' &&
+    // a first bottom-up level: the hub cut (decided on the device from the
+    // frontier hubs' degrees hub_gather sums -- global on every rank),
+    // enqueued for levels predicted at <= bu_cut_mf_frac of the graph's edges
+    // (a first bottom-up level's non-hub frontier edges grow with its
+    // frontier: the larger ones never cut, and skip its launches).  Several
+    // ranks: the non-hub frontier's remote neighbours go to their owners as
+    // lists (the sparse levels' owner lists, so at most list_max of them per
+    // owner: the cut bound is capped there) and bu_cut_apply claims them.
+    // (several ranks: the shard conditions agreed once, cut_ranks_ok_; the rest
+    // are functions of agreed values)
+    const bool shard_ok = xc_ ? e_.cut_ranks_ok_ && list_max_ > 0 && opt_.bu_cut_ranks
+                              : gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref && gv_.nz_row_off &&
+                                    gv_.head && ba.zdeg;
+    const bool cut = opt_.bu_cut_edges > 0 && c.pf != 'B' &&
                      (c.mf_hint < 0 || c.mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(e_.total_directed_)) &&
-                     gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref && gv_.nz_row_off && gv_.head &&
-                     ba.zdeg;
+                     shard_ok;
+    const int64_t cut_edges = xc_ ? std::min(opt_.bu_cut_edges, list_max_) : opt_.bu_cut_edges;
     if (cut) {
       if (!e_.cut_part_.data()) {
         e_.cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(gv_.nhubs, int64_t(64))));
@@ -837,14 +847,14 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         be_.memset_async(e_.cut_ticket_.data(), 0, e_.cut_ticket_.bytes());
       }
       hg.cut_part = e_.cut_part_.data();
-      hg.cut_edges = opt_.bu_cut_edges;
+      hg.cut_edges = cut_edges;
       hg.cut_flag = e_.cut_flag_.data();
       hg.cut_ticket = e_.cut_ticket_.data();
     }
     be_.hub_gather(hg);
     ba.hub_front = e_.hub_front_.data();
     if (cut) {
-      ba.cut_edges = opt_.bu_cut_edges;
+      ba.cut_edges = cut_edges;
       ba.cut_flag = e_.cut_flag_.data();
       if (!e_.run_narrow_) {
         // wide levels: claims in a byte array of their own (kept zero)
@@ -854,7 +864,35 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         }
         ba.cut_claim = e_.cut_claim_.data();
       }
-      be_.bu_cut_prep(ba);
+      if (!xc_) {
+        be_.bu_cut_prep(ba);
+      } else {
+        // several ranks: own claims in place, remote ones as owner lists
+        // (straight into the owners' windows with a direct exchange), then
+        // the owners' side (collectives cannot be predicated: the exchange
+        // runs on every chain, empty when the level does not cut)
+        c.cut = true;
+        ba.nranks = P_;
+        ba.cut_fr_base = static_cast<int64_t>(me_) * W_;
+        ba.cut_lists = e_.dl_send_lists_.data();
+        ba.cut_list_stride = e_.list_stride_;
+        ba.part = part_.part;
+        ba.cut_visited = e_.visited_.data();
+        const size_t lcap = static_cast<size_t>(list_max_);
+        const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &ba.cut_direct);
+        if (direct && !e_.cut_prep_ticket_.data()) {
+          e_.cut_prep_ticket_ = DBuf<unsigned>(be_, 1);
+          be_.memset_async(e_.cut_prep_ticket_.data(), 0, e_.cut_prep_ticket_.bytes());
+        }
+        ba.cut_prep_ticket = e_.cut_prep_ticket_.data();
+        be_.bu_cut_prep(ba);
+        if (!direct)
+          comm_.alltoall_lists(e_.dl_send_lists_.data(), e_.dl_recv_lists_.data(),
+                               static_cast<size_t>(e_.list_stride_), lcap);
+        ba.cut_recv_lists = direct ? nullptr : e_.dl_recv_lists_.data();
+        be_.bu_cut_apply(ba);
+        ba.cut_direct = DirectExchange();  // (the bottom-up kernel does not exchange)
+      }
     }
   }
   if (opt_.bu_fused_scan) {
@@ -868,7 +906,9 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     c.fused_scan = true;
     // several ranks: the level's end in the kernel's last workgroup too (no
     // frontier gather; the hub kernels' fused finish)
-    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && !enq_gather_[L] &&
+    // (not on a hub-cut level: its plain and cut kernels are both launched,
+    // and only the plain ones have the folded end)
+    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && !enq_gather_[L] && !c.cut &&
         comm_.direct_level_end(2, &ba.end)) {
       ba.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;

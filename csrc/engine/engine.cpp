@@ -92,6 +92,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "hx_levels") o.hx_levels = static_cast<int>(v);
   else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
   else if (name == "bu_cut_mf_frac") o.bu_cut_mf_frac = v;
+  else if (name == "bu_cut_ranks") o.bu_cut_ranks = v != 0;
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
@@ -142,6 +143,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"hx_levels", static_cast<double>(o.hx_levels)},
           {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
           {"bu_cut_mf_frac", o.bu_cut_mf_frac},
+          {"bu_cut_ranks", o.bu_cut_ranks ? 1.0 : 0.0},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
@@ -314,6 +316,7 @@ ShardView DeviceGraph::view() const {
   v.nhubs = nhubs_;
   v.hub_col = hub_col_.data();
   v.hub_bits = hub_bits_.data();
+  v.hub_deg = hub_deg_.data();
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -385,6 +388,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   nhubs_ = 0;
   hub_vertex_.reset();
   hub_bits_.reset();
+  hub_deg_.reset();
   hub_col_.reset();
   td_col_.reset();
   td_hub_vertex_.reset();
@@ -410,6 +414,11 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
         for (vid_t v : hv) bits[v >> 6] |= 1ull << (v & 63);
         hub_bits_ = DBuf<word_t>(*be_, bits.size());
         be_->to_device(hub_bits_.data(), bits.data(), bits.size() * sizeof(word_t));
+        // the hubs' degrees (several ranks: the hub-cut decision)
+        std::vector<uint32_t> hd(hv.size());
+        for (size_t i = 0; i < hv.size(); ++i) hd[i] = deg[hv[i]];
+        hub_deg_ = DBuf<uint32_t>(*be_, hd.size());
+        be_->to_device(hub_deg_.data(), hd.data(), hd.size() * sizeof(uint32_t));
       }
       // bottom-up's hub-encoded adjacency copy (one more nnz x 4 B: RMAT-26
       // 8.6 GB of the 288 GB HBM3E)
@@ -694,6 +703,11 @@ void Engine::alloc_bitmap_state() {
   stats_ = DBuf<int64_t>(be_, static_cast<size_t>(exchange() ? kStatsBlocks * stats_stride_ : std::max<int64_t>(stats_stride_, 8)));
   be_.memset_async(stats_.data(), 0, stats_.bytes());
   if (g_.nhubs() > 0) hub_front_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(g_.nhubs(), kWordBits)));
+  if (exchange()) {
+    const ShardView gv = g_.view();
+    const bool ok = gv.hub_bits && gv.hub_deg && gv.nz_rec && gv.unit_base && gv.nz_pref && gv.nz_row_off && gv.head;
+    cut_ranks_ok_ = comm_.sum_host(ok ? 1 : 0) == part_.nranks;
+  }
   // Zero-degree (and padding) vertices can never be discovered: they start out
   // visited, so bottom-up steps skip them without touching row_off.
   ZeroDegArgs za;

@@ -87,6 +87,9 @@ struct ShardView {
   // top-down hub iff its degree >= td_hub_min_deg.
   const eid_t* hx_off = nullptr;
   uint32_t td_hub_min_deg = 0;
+  // Degree of every hub (nhubs entries; several ranks: a hub's row lives on
+  // its owner, so the hub-cut decision sums these instead of row lengths).
+  const uint32_t* hub_deg = nullptr;
 };
 
 // Work-list entry without a frontier vertex of this rank (a hub-split entry of
@@ -736,6 +739,25 @@ struct BuArgs {
   int64_t cut_edges = 0;
   int* cut_flag = nullptr;
   uint8_t* cut_claim = nullptr;
+  // ... several ranks: this rank's non-hub frontier is the owned slice of
+  // `frontier` (words from cut_fr_base, also in g.hub_bits); an unvisited own
+  // neighbour is claimed in place, a remote one -- after a fetch-or of its bit
+  // in the replicated cut_visited, so each goes out at most once -- is
+  // appended to its owner's list (cut_lists: the sparse levels' owner lists,
+  // cut_list_stride words each, owner = v / part; cut_direct.active: stored
+  // straight into the owner's window, the last workgroup of cut_prep_ticket
+  // publishing the counts).  bu_cut_apply then claims the received ids
+  // (cut_recv_lists, or the window) on their owner, before the bottom-up
+  // kernel reads the claims.  nranks > 1 selects this path.
+  int64_t cut_fr_base = 0;
+  vid_t* cut_lists = nullptr;
+  int64_t cut_list_stride = 0;
+  int64_t part = 0;
+  int nranks = 1;
+  word_t* cut_visited = nullptr;
+  DirectExchange cut_direct;
+  unsigned* cut_prep_ticket = nullptr;
+  const vid_t* cut_recv_lists = nullptr;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the
@@ -973,6 +995,8 @@ class Backend {
   // Hub-cut level's top-down part (BuArgs::cut_edges): the unvisited
   // neighbours of the frontier's non-hub vertices claimed into a.pre.
   virtual void bu_cut_prep(const BuArgs& a) = 0;
+  // ... several ranks: the claims received from the other ranks (BuArgs::cut_lists)
+  virtual void bu_cut_apply(const BuArgs& a) = 0;
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their

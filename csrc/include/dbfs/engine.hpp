@@ -106,6 +106,7 @@ class DeviceGraph {
   // several ranks: hub-split rows (ShardView::hx_off), appended to col_ / td_col_
   DBuf<eid_t> hx_off_;
   uint32_t td_hub_min_deg_ = 0;
+  DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
   void build_hub_split();
   int64_t hx_total() const;
   DBuf<word_t> hub_bits_;  // global vertex bitmap of the hubs
@@ -287,6 +288,9 @@ struct EngineOptions {
   // the late-switch first bottom-up levels have 4-15 % of them, the others
   // 37 % and more)
   double bu_cut_mf_frac = 0.25;
+  // ... also with several ranks (the non-hub frontier's remote claims through
+  // the owner lists, bu_cut_apply on the owners)
+  bool bu_cut_ranks = true;
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
@@ -350,6 +354,8 @@ struct ChainRecord {
   // hub-split chain: its level end all-reduces this many words more than the
   // totals (the hub count and the frontier-hub bits)
   int64_t hx_words = 0;
+  // several ranks: a hub-cut bottom-up chain (its owner-list exchange)
+  bool cut = false;
 };
 
 struct RunResult {
@@ -442,7 +448,11 @@ class Engine {
   DBuf<int64_t> cut_part_;
   DBuf<int> cut_flag_;
   DBuf<uint8_t> cut_claim_;  // wide-level runs' claims
-  DBuf<unsigned> cut_ticket_;
+  DBuf<unsigned> cut_ticket_, cut_prep_ticket_;
+  // several ranks: every rank's shard has what a hub-cut level needs (packed
+  // records, hub degrees, lists) -- agreed once, the cut's collectives are
+  // enqueued by every rank or by none
+  bool cut_ranks_ok_ = false;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;

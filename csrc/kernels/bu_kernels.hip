@@ -670,13 +670,20 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
 }
 
-// hub_gather of a hub-cut level (one rank; BuArgs::cut_edges): 4 hubs per
-// thread (loads issued together), the frontier hubs' degrees summed per
-// workgroup; the last-arriving workgroup (of ~128) totals them and stores the
-// decision ctrl->m_f - hub edges <= cut_edges in *cut_flag.
+// hub_front bit h = frontier bit of hub_vertex[h]: 4 hubs per thread, their
+// loads issued together (the frontier bits are random 8-B reads of a bitmap
+// far larger than the L2: one round trip per thread instead of four).
+// Several ranks with bu_merge_visited: the whole grid then merges the gathered
+// frontier into visited.
+// kCut, a hub-cut level (BuArgs::cut_edges): the frontier hubs' degrees
+// (their rows, or with several ranks g.hub_deg) summed per workgroup; the
+// last-arriving workgroup (of ~128) totals them and stores the decision
+// ctrl->m_f - hub edges <= cut_edges in *cut_flag -- the same on every rank
+// (global frontier, global degrees).
 constexpr int kHgThreads = 1024, kHgPer = 4;
-__global__ __launch_bounds__(kHgThreads) void hub_gather_cut_kernel(HubGatherArgs a) {
-  if (a.ctrl->done || a.ctrl->dir != 'B') return;
+template <bool kCut>
+__global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a) {
+  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   stamp_level_start(a.ctrl);
   __shared__ long long s_d[kHgThreads / kWave];
   __shared__ int s_last;
@@ -697,11 +704,22 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_cut_kernel(HubGatherArg
   long long d = 0;
 #pragma unroll
   for (int k = 0; k < kHgPer; ++k) {
+    const int64_t h = base + k * kHgThreads + threadIdx.x;
     const int64_t h0 = base + k * kHgThreads + (threadIdx.x & ~(kWave - 1));
     const word_t m = __ballot(bit[k]);
     if (lane == 0 && h0 < a.g.nhubs) a.hub_front[h0 / kWave] = m;
-    if (bit[k]) d += static_cast<long long>(a.g.row_off[hv[k] + 1] - a.g.row_off[hv[k]]);
+    if (kCut && bit[k])
+      d += a.g.hub_deg ? static_cast<long long>(a.g.hub_deg[h])
+                       : static_cast<long long>(a.g.row_off[hv[k] + 1] - a.g.row_off[hv[k]]);
   }
+  if (a.visited) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kHgThreads;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kHgThreads + threadIdx.x; i < a.words; i += stride) {
+      const word_t f = a.frontier[i];
+      if (f) a.visited[i] |= f;
+    }
+  }
+  if constexpr (!kCut) return;
   d = wave_sum(d);
   if (lane == 0) s_d[threadIdx.x >> 6] = d;
   __syncthreads();
@@ -734,25 +752,6 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_cut_kernel(HubGatherArg
   }
 }
 
-// hub_front bit h = frontier bit of hub_vertex[h]: one wave per hub word;
-// several ranks: then the whole grid merges the frontier into visited.
-__global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-  stamp_level_start(a.ctrl);
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6);
-  const int64_t h = w * kWave + lane_id();
-  const bool bit = h < a.g.nhubs && test_bit(a.frontier, a.g.hub_vertex[h]);
-  const word_t m = __ballot(bit);
-  if (lane_id() == 0 && w * kWave < a.g.nhubs) a.hub_front[w] = m;
-  if (a.visited) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.words; i += stride) {
-      const word_t f = a.frontier[i];
-      if (f) a.visited[i] |= f;
-    }
-  }
-}
-
 // The hub-cut level's top-down part (BuArgs::cut_edges; hub_gather decided):
 // a wave per 64 frontier words finds their non-hub vertices and expands
 // their rows one after another, the lanes striding over the row (four column
@@ -763,39 +762,131 @@ __global__ __launch_bounds__(kBlock) void hub_gather_kernel(HubGatherArgs a) {
 // (kernel trace; grid 256-4096 workgroups flat); a list of the vertices, a
 // wave each, spent 109 us in the list's same-address appends alone; claims
 // in a bitmap by device atomics 160 us.
+// Several ranks: a remote neighbour is claimed in the replicated visited
+// bitmap (fetch-or: each goes out at most once) and appended to its owner's
+// list -- or, with a direct exchange, stored into the owner's window; the
+// workgroups' last one publishes the counts (empty on a level that does not
+// cut: the peers wait for every exchange).
 constexpr int kCutThreads = 1024;
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-  if (!*a.cut_flag) return;
+  const bool lists = a.nranks > 1;
+  const bool dx = lists && a.cut_direct.active;
+  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) {
+    if (dx && blockIdx.x == 0) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, false);
+    return;
+  }
+  __shared__ int s_last;
   const vid_t* __restrict__ col = a.g.col;
   const eid_t* __restrict__ ro = a.g.row_off;
+  const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);
   const int lane = lane_id();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kCutThreads;
   for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCutThreads + (threadIdx.x & ~(kWave - 1)); w0 < a.words;
        w0 += stride) {
     const int64_t w = w0 + lane;
-    word_t m = w < a.words ? a.frontier[w] & ~a.g.hub_bits[w] : 0ull;
+    word_t m = w < a.words ? a.frontier[a.cut_fr_base + w] & ~a.g.hub_bits[a.cut_fr_base + w] : 0ull;
     for (unsigned long long bm = __ballot(m != 0); bm; bm = __ballot(m != 0)) {
       const int l = __ffsll(static_cast<long long>(bm)) - 1;
       const int64_t v = (w0 + l) * 64 + __builtin_ctzll(static_cast<word_t>(__shfl(static_cast<long long>(m), l, kWave)));
       if (lane == l) m &= m - 1;
       const eid_t rs = ro[v], re = ro[v + 1];
       constexpr int kU = 4;
-      for (eid_t e0 = rs + lane; e0 < re; e0 += kU * kWave) {
+      // (wave-uniform loop: the owner lists' appends are wave operations)
+      for (eid_t b0 = rs; b0 < re; b0 += kU * kWave) {
         vid_t t[kU];
         word_t vw[kU];
+        bool own[kU];
 #pragma unroll
-        for (int k = 0; k < kU; ++k) t[k] = e0 + k * kWave < re ? col[e0 + k * kWave] : kNoVertex;
-#pragma unroll
-        for (int k = 0; k < kU; ++k) vw[k] = t[k] != kNoVertex ? a.visited[t[k] >> 6] : ~0ull;
+        for (int k = 0; k < kU; ++k) {
+          const eid_t e = b0 + k * kWave + lane;
+          t[k] = e < re ? col[e] : kNoVertex;
+          own[k] = static_cast<uint64_t>(t[k]) - lo < rows;
+        }
 #pragma unroll
         for (int k = 0; k < kU; ++k)
-          if (!((vw[k] >> (t[k] & 63)) & 1ull)) {
-            if (a.cut_claim) a.cut_claim[t[k]] = 1;  // (wide levels: the bottom-up kernel writes them)
-            else store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
+          vw[k] = t[k] == kNoVertex ? ~0ull
+                                    : own[k] ? a.visited[(t[k] - lo) >> 6] : (lists ? a.cut_visited[t[k] >> 6] : ~0ull);
+        unsigned remote = 0;
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+          const uint32_t tb = own[k] ? static_cast<uint32_t>(t[k] - lo) : t[k];
+          if ((vw[k] >> (tb & 63)) & 1ull) continue;
+          if (own[k]) {
+            if (a.cut_claim) a.cut_claim[tb] = 1;  // (wide levels: the bottom-up kernel writes them)
+            else store_level(nullptr, a.level8, tb, a.new_level, a.narrow_base);
+          } else if (!(atomicOr(a.cut_visited + (t[k] >> 6), 1ull << (t[k] & 63)) & (1ull << (t[k] & 63)))) {
+            remote |= 1u << k;
           }
+        }
+        if (lists && __ballot(remote != 0)) {
+#pragma unroll
+          for (int k = 0; k < kU; ++k)
+            owner_list_append(a.cut_lists, a.cut_list_stride, a.part, t[k], (remote >> k) & 1u,
+                              dx ? a.cut_direct.table : nullptr);
+        }
       }
     }
+  }
+  if (!dx) return;
+  // every wave's write-through stores drained, the workgroups' ticket, the
+  // last one publishes the counts (as td_sparse)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s_last = atomicAdd(a.cut_prep_ticket, 1u) == gridDim.x - 1;
+    if (s_last) {
+      *a.cut_prep_ticket = 0u;
+      last_arriver_acquire();
+    }
+  }
+  __syncthreads();
+  if (s_last) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, true);
+}
+
+// Several ranks, a hub-cut level: the claims the other ranks sent for this
+// rank's vertices -- from this rank's window after the peers' cells (direct),
+// or from cut_recv_lists -- written as level bytes (claim bytes with wide
+// levels) of the still unvisited ones, before the bottom-up kernel reads the
+// claims.  Every workgroup waits for the cells (every exchange is awaited,
+// live or not); the entries form one index space the grid strides over.
+constexpr int kCutApplyThreads = 256;
+__global__ __launch_bounds__(kCutApplyThreads) void bu_cut_apply_kernel(BuArgs a) {
+  __shared__ uint64_t s_cnt[kern::kMaxPeers];
+  __shared__ long long s_end[kern::kMaxPeers];
+  __shared__ const vid_t* s_src[kern::kMaxPeers];
+  const int t = threadIdx.x;
+  const bool dx = a.cut_direct.active;
+  if (dx && direct_wait(a.cut_direct, s_cnt, nullptr) != kWaitOk) return;
+  // (collective exchange: it has read the send lists -- their counts restart
+  // from zero; a direct one's publisher zeroed them)
+  if (!dx && blockIdx.x == 0 && t < a.nranks) a.cut_lists[static_cast<int64_t>(t) * a.cut_list_stride] = 0u;
+  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) return;
+  if (t < kWave) {
+    long long n = 0;
+    if (t < a.nranks) {
+      const vid_t* src = dx ? a.cut_direct.table->src[t] : a.cut_recv_lists + static_cast<int64_t>(t) * a.cut_list_stride;
+      s_src[t] = src;
+      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
+    }
+    DBFS_DCHECK(n < a.cut_list_stride, 13, n);
+    const long long incl = wave_incl_scan(n);
+    if (t < a.nranks) s_end[t] = incl;
+  }
+  __syncthreads();
+  const long long total = s_end[a.nranks - 1];
+  const int64_t lo = a.g.lo;
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kCutApplyThreads + t; j < total;
+       j += static_cast<int64_t>(gridDim.x) * kCutApplyThreads) {
+    int r = 0;
+    while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
+    const long long before = r > 0 ? s_end[r - 1] : 0;
+    const vid_t* src = s_src[r] + 1 + (j - before);
+    const vid_t v = dx ? sys_load_u32(src) : *src;
+    const int64_t row = static_cast<int64_t>(v) - lo;
+    DBFS_DCHECK(row >= 0 && row < a.g.rows, 14, v);
+    if ((a.visited[row >> 6] >> (row & 63)) & 1ull) continue;
+    if (a.cut_claim) a.cut_claim[row] = 1;
+    else store_level(nullptr, a.level8, row, a.new_level, a.narrow_base);
   }
 }
 
@@ -895,21 +986,31 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 void bu_cut_prep(const BuArgs& a, hipStream_t st) {
   DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && (a.level8 || a.cut_claim) && a.g.hub_bits && a.ctrl,
              "bu_cut_prep: hub-cut arguments missing");
+  DBFS_CHECK(a.nranks <= 1 || (a.cut_lists && a.cut_visited && a.part > 0 && a.cut_list_stride > 0 &&
+                               (!a.cut_direct.active || a.cut_prep_ticket)),
+             "bu_cut_prep: several ranks need owner lists, the replicated visited bitmap and a ticket");
   // (grid measured flat from 256 to 4096 workgroups)
   bu_cut_prep_kernel<<<grid_for(a.words, kCutThreads, 2 * device_cus()), kCutThreads, 0, st>>>(a);
+}
+
+void bu_cut_apply(const BuArgs& a, hipStream_t st) {
+  DBFS_CHECK(a.nranks > 1 && a.nranks <= kern::kMaxPeers && a.cut_lists && a.cut_flag &&
+                 (a.cut_direct.active || a.cut_recv_lists) && (a.level8 || a.cut_claim),
+             "bu_cut_apply: several ranks' hub-cut arguments missing");
+  bu_cut_apply_kernel<<<128, kCutApplyThreads, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
   if (a.cut_part) {
-    DBFS_CHECK(!a.visited && a.cut_flag && a.cut_ticket && a.ctrl,
-               "hub_gather: the hub-cut decision needs one rank, a flag, a ticket and the level state");
-    hub_gather_cut_kernel<<<grid_for(a.g.nhubs, kHgThreads * kHgPer), kHgThreads, 0, st>>>(a);
+    DBFS_CHECK(a.cut_flag && a.cut_ticket && a.ctrl, "hub_gather: the hub-cut decision needs a flag, a ticket and the level state");
+    hub_gather_kernel<true><<<grid_for(a.g.nhubs, kHgThreads * kHgPer), kHgThreads, 0, st>>>(a);
     return;
   }
-  unsigned grid = grid_for((a.g.nhubs + kWave - 1) / kWave, kBlock / kWave);
-  if (a.visited) grid = std::max(grid, grid_for(a.words, kBlock, 2048));
-  hub_gather_kernel<<<grid, kBlock, 0, st>>>(a);
+  // (with the visited merge: at least a grid striding over the words well)
+  unsigned grid = grid_for(a.g.nhubs, kHgThreads * kHgPer);
+  if (a.visited) grid = std::max(grid, grid_for(a.words, kHgThreads, 512));
+  hub_gather_kernel<false><<<grid, kHgThreads, 0, st>>>(a);
 }
 
 unsigned long long take_check_bu() { return take_check_local(); }

@@ -38,6 +38,7 @@ void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
 void bu_cut_prep(const BuArgs& a, hipStream_t st);
+void bu_cut_apply(const BuArgs& a, hipStream_t st);
 void hub_visited(const HubVisitedArgs& a, hipStream_t st);
 void hub_apply(const HubApplyArgs& a, hipStream_t st);
 // device-checked build (DBFS_CHECKED): whether checks are compiled in, the

@@ -3,7 +3,8 @@
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
 collectives and bytes of a traversal can be predicted from its chains
-(``BFSResult.chains``: level, form, capacity, gather, hub-split words) and checked against the
+(``BFSResult.chains``: level, form, capacity, gather, hub-split words, hub cut)
+and checked against the
 communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
 ``table`` turns a 1-GPU level profile into the per-level bytes / collectives
 table of docs/ARCHITECTURE.md §4.
@@ -88,12 +89,15 @@ def level_end(cfg: ModelConfig, gather: bool, hx_words: int = 0) -> ChainTraffic
 
 
 def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool,
-                  hx_words: int = 0) -> ChainTraffic:
-    """Collectives of one level chain."""
+                  hx_words: int = 0, cut: bool = False) -> ChainTraffic:
+    """Collectives of one level chain (cut: a hub-cut bottom-up chain, whose
+    non-hub frontier's remote claims travel as owner lists)."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
     if form == "B" and not in_gathered:
         t.add("allgather", (P - 1) * W * WORD)              # input frontier slices (+ visited merge)
+    if cut:
+        t.add("alltoallv", (P - 1) * (cfg.list_max + 1) * 4)  # the cut's owner lists
     if form == "S":
         t.add("alltoallv", (P - 1) * ((cap or cfg.list_max) + 1) * 4)  # owner lists, count first
     elif form == "T":
@@ -112,9 +116,9 @@ def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     seed_gather = cfg.mode == "bu"
     tot.merge(level_end(cfg, seed_gather))
     gathered = {-1: seed_gather}
-    for level, form, cap, gather, *hx in chains:
+    for level, form, cap, gather, *more in chains:
         tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False),
-                                int(hx[0]) if hx else 0))
+                                int(more[0]) if more else 0, bool(more[1]) if len(more) > 1 else False))
         gathered[level] = bool(gather)
     tot.add("allgather", (P - 1) * 8)  # max over ranks of the wall time
     return tot

@@ -702,3 +702,42 @@ def test_hub_split_rows_partition_hub_rows():
             row = col[ro[hubs[k]]:ro[hubs[k] + 1]].astype(np.int64)
             mine = np.sort(row[(row >= lo) & (row < lo + rows)])
             assert np.array_equal(part[off[k]:off[k + 1]].astype(np.int64), mine)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("narrow", [1, 0])
+@pytest.mark.parametrize("alpha,max_hubs", [(24.0, None), (2.0, 300), (1e9, None)])
+def test_hub_cut_several_ranks(P, narrow, alpha, max_hubs):
+    """Hub-cut bottom-up levels with several ranks: the non-hub frontier of
+    each rank claims its own neighbours in place and sends the remote ones to
+    their owners (the owner lists), who claim them (bu_cut_apply) before the
+    bottom-up kernel merges the claims with the rows resolved by frontier hubs
+    (decided on every rank from the global frontier and the hubs' global
+    degrees).  Cut forced on every first bottom-up level: levels exact against
+    the oracle and the level records equal the uncut run's."""
+    p = dbfs.rmat_params(13, 16, 11)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [7, 3001, 8100]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=24.0, max_hubs=max_hubs)
+        b.engine.set_option("narrow_levels", narrow)
+        b.engine.set_option("bu_cut_mf_frac", 1.0)  # (enqueue it on every first bottom-up level)
+        out = []
+        for cut in (1 << 40, 0):
+            b.engine.set_option("bu_cut_edges", cut)
+            for s in srcs:
+                r = b.run(s)
+                recs = [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
+                out.append((cut, s, b.levels(), recs, any(c[5] for c in r.chains)))
+        return out
+
+    for outs in run_virtual_ranks(P, body, device="cpu"):
+        cut = {s: x for c, s, *x in outs if c}
+        plain = {s: x for c, s, *x in outs if not c}
+        for s in srcs:
+            exp = dbfs.cpu_bfs(csr, s)[0]
+            assert np.array_equal(cut[s][0], exp) and np.array_equal(plain[s][0], exp)
+            assert cut[s][1] == plain[s][1]
+            assert not plain[s][2]
+        assert any(cut[s][2] for s in srcs)
