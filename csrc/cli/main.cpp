@@ -232,6 +232,85 @@ std::string json_run(const RunResult& r, const std::string& graph, int64_t n, in
   return s + "]}";
 }
 
+// Backends and communicators of this process's ranks (one for a process of
+// a multi-process job): RCCL + peer windows, TCP, virtual ranks or local.
+// Returns the virtual group when the ranks are virtual.
+std::shared_ptr<VirtualGroup> make_ranks(const Args& a, int P, bool multiproc, int wrank, int world, bool leader,
+                                         std::vector<RankCtx>& ranks) {
+  const int nlocal = static_cast<int>(ranks.size());
+  std::shared_ptr<VirtualGroup> vgroup;
+  if (a.virtual_ranks > 0 && !multiproc) vgroup = std::make_shared<VirtualGroup>(P);
+  const char* dev_pin = std::getenv("DBFS_DEVICE");  // several processes on one GPU (tests)
+  const char* cm_env = std::getenv("DBFS_COMM");
+  const std::string cm = cm_env ? cm_env : "";
+  const bool want_peer = !a.cpu && (cm.empty() || cm == "peer");
+  for (int i = 0; i < nlocal; ++i) {
+    if (a.cpu) ranks[i].be = make_cpu_backend();
+    else if (multiproc) ranks[i].be = make_hip_backend(dev_pin ? std::atoi(dev_pin) : env_int("LOCAL_RANK", 0));
+    else if (a.virtual_ranks > 0) ranks[i].be = make_hip_backend(a.device);
+    else ranks[i].be = make_hip_backend(P > 1 ? i : a.device);
+  }
+  if (multiproc) {
+    const char* addr = std::getenv("MASTER_ADDR");
+    const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
+    auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
+    if (a.cpu || cm == "tcp" || (cm.empty() && dev_pin)) {
+      // host transport (CPU ranks, GPU ranks without RCCL, shared GPU)
+      ranks[0].comm = std::make_shared<TcpComm>(boot, *ranks[0].be);
+    } else {
+      std::shared_ptr<Comm> inner;
+      if (dev_pin) {
+        // RCCL refuses two ranks on one device: TCP carries what does not
+        // fit the peer windows
+        inner = std::make_shared<TcpComm>(boot, *ranks[0].be);
+      } else {
+        std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+        inner = std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
+      }
+      ranks[0].comm = want_peer ? try_peer(boot, *ranks[0].be, inner, cm == "peer", leader) : inner;
+    }
+  } else if (vgroup) {
+    for (int i = 0; i < P; ++i) ranks[i].comm = std::make_shared<VirtualComm>(vgroup, i, *ranks[i].be);
+  } else if (P > 1) {
+    std::vector<Backend*> bes;
+    for (auto& r : ranks) bes.push_back(r.be.get());
+    auto comms = NcclComm::init_all(bes);
+    for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
+    if (want_peer) {
+      auto pgroup = std::make_shared<VirtualGroup>(P);
+      run_ranks(ranks, [&](int i, RankCtx& rc) {
+        rc.comm = try_peer(std::make_shared<GroupBootstrap>(pgroup, i), *rc.be, rc.comm, cm == "peer", i == 0);
+      }, pgroup.get());
+    }
+  } else {
+    ranks[0].comm = std::make_shared<LocalComm>(*ranks[0].be);
+  }
+  return vgroup;
+}
+
+// K random roots of degree >= 1 (the same sequence on every rank; a
+// multi-process job asks each vertex's owner for its degree).
+std::vector<int64_t> sample_roots(const Args& a, const Partition& part, std::vector<RankCtx>& ranks, bool multiproc,
+                                  int wrank) {
+  std::mt19937_64 rng(a.seed * 7919 + 17);
+  std::vector<int64_t> roots;
+  int tries = 0;
+  while (static_cast<int>(roots.size()) < a.roots && tries < 100 * a.roots) {
+    ++tries;
+    const int64_t v = static_cast<int64_t>(rng() % static_cast<uint64_t>(part.n));
+    const int own = part.owner(v);
+    int64_t deg = 0;
+    if (!multiproc) {
+      deg = ranks[own].graph->degrees_of({v - part.lo(own)})[0];
+    } else {
+      const int64_t d = own == wrank ? ranks[0].graph->degrees_of({v - part.lo(own)})[0] : 0;
+      deg = ranks[0].comm->sum_host(d);
+    }
+    if (deg > 0) roots.push_back(v);
+  }
+  return roots;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -340,53 +419,7 @@ int main(int argc, char** argv) {
     // ---- ranks / devices ----
     std::vector<RankCtx> ranks(static_cast<size_t>(nlocal));
     if (!a.cpu && ref_lines && !sharded) std::printf("Enabling peer access between GPU0 and GPU1...\n");
-    std::shared_ptr<VirtualGroup> vgroup;
-    if (a.virtual_ranks > 0 && !multiproc) vgroup = std::make_shared<VirtualGroup>(P);
-    const char* dev_pin = std::getenv("DBFS_DEVICE");  // several processes on one GPU (tests)
-    const char* cm_env = std::getenv("DBFS_COMM");
-    const std::string cm = cm_env ? cm_env : "";
-    const bool want_peer = !a.cpu && (cm.empty() || cm == "peer");
-    for (int i = 0; i < nlocal; ++i) {
-      if (a.cpu) ranks[i].be = make_cpu_backend();
-      else if (multiproc) ranks[i].be = make_hip_backend(dev_pin ? std::atoi(dev_pin) : env_int("LOCAL_RANK", 0));
-      else if (a.virtual_ranks > 0) ranks[i].be = make_hip_backend(a.device);
-      else ranks[i].be = make_hip_backend(P > 1 ? i : a.device);
-    }
-    if (multiproc) {
-      const char* addr = std::getenv("MASTER_ADDR");
-      const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
-      auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
-      if (a.cpu || cm == "tcp" || (cm.empty() && dev_pin)) {
-        // host transport (CPU ranks, GPU ranks without RCCL, shared GPU)
-        ranks[0].comm = std::make_shared<TcpComm>(boot, *ranks[0].be);
-      } else {
-        std::shared_ptr<Comm> inner;
-        if (dev_pin) {
-          // RCCL refuses two ranks on one device: TCP carries what does not
-          // fit the peer windows
-          inner = std::make_shared<TcpComm>(boot, *ranks[0].be);
-        } else {
-          std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
-          inner = std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
-        }
-        ranks[0].comm = want_peer ? try_peer(boot, *ranks[0].be, inner, cm == "peer", leader) : inner;
-      }
-    } else if (vgroup) {
-      for (int i = 0; i < P; ++i) ranks[i].comm = std::make_shared<VirtualComm>(vgroup, i, *ranks[i].be);
-    } else if (P > 1) {
-      std::vector<Backend*> bes;
-      for (auto& r : ranks) bes.push_back(r.be.get());
-      auto comms = NcclComm::init_all(bes);
-      for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
-      if (want_peer) {
-        auto pgroup = std::make_shared<VirtualGroup>(P);
-        run_ranks(ranks, [&](int i, RankCtx& rc) {
-          rc.comm = try_peer(std::make_shared<GroupBootstrap>(pgroup, i), *rc.be, rc.comm, cm == "peer", i == 0);
-        }, pgroup.get());
-      }
-    } else {
-      ranks[0].comm = std::make_shared<LocalComm>(*ranks[0].be);
-    }
+    std::shared_ptr<VirtualGroup> vgroup = make_ranks(a, P, multiproc, wrank, world, leader, ranks);
 
     Partition part;
     if (sharded) {
@@ -506,25 +539,7 @@ int main(int argc, char** argv) {
 
     // ---- optional K random roots (Graph500-style GTEPS) ----
     if (a.roots > 0) {
-      std::mt19937_64 rng(a.seed * 7919 + 17);
-      std::vector<int64_t> roots;
-      // roots are chosen on the leader among vertices with degree >= 1
-      int tries = 0;
-      while (static_cast<int>(roots.size()) < a.roots && tries < 100 * a.roots) {
-        ++tries;
-        const int64_t v = static_cast<int64_t>(rng() % static_cast<uint64_t>(n));
-        // degree check through the owning rank's shard (single-process: any rank ctx)
-        int64_t deg = 0;
-        if (!multiproc) {
-          const int own = part.owner(v);
-          deg = ranks[own].graph->degrees_of({v - part.lo(own)})[0];
-        } else {
-          const int own = part.owner(v);
-          int64_t d = (own == wrank) ? ranks[0].graph->degrees_of({v - part.lo(own)})[0] : 0;
-          deg = ranks[0].comm->sum_host(d);
-        }
-        if (deg > 0) roots.push_back(v);
-      }
+      const std::vector<int64_t> roots = sample_roots(a, part, ranks, multiproc, wrank);
       double inv_sum = 0, ms_sum = 0;
       int64_t e_sum = 0;
       for (int64_t root : roots) {

@@ -728,6 +728,7 @@ void DeviceLoop::emit_dense(Chain& c) {
     ta.level_direct = e_.level8_.data();
     ta.narrow_base = e_.narrow_base_;
     ta.new_level = L + 1;
+    ta.store_mode = opt_.td_store_mode;
     tu.level_direct = e_.level8_.data();
     tu.narrow_base = e_.narrow_base_;
     if (ta.td_hub_vis && opt_.td_hub_mark) {

@@ -81,6 +81,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
+  else if (name == "td_store_mode") o.td_store_mode = static_cast<int>(v);
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
   else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
@@ -132,6 +133,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
+          {"td_store_mode", static_cast<double>(o.td_store_mode)},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
           {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},

@@ -620,6 +620,10 @@ struct TdArgs {
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
   uint8_t narrow_base = 0;  // (level_direct stores narrow_base + new_level)
+  // How those level bytes are stored (EngineOptions::td_store_mode): 0 plain
+  // (write-back L2), 1 write-through (sc1: the line leaves the XCD's L2),
+  // 2 non-temporal.
+  int store_mode = 0;
   // Levels of at least td_hub_min_edges frontier edges read g.td_col and test
   // hub targets in an LDS copy of td_hub_vis (visited bits of the top-down
   // hubs, this level's snapshot: hub_visited); not with owner lists.

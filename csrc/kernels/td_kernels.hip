@@ -272,7 +272,14 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-          if (keep[k]) a.level_direct[vk[k]] = lv;
+          if (keep[k]) {
+            if (a.store_mode == 1)
+              __hip_atomic_store(a.level_direct + vk[k], lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (a.store_mode == 2)
+              __builtin_nontemporal_store(lv, a.level_direct + vk[k]);
+            else
+              a.level_direct[vk[k]] = lv;
+          }
         continue;
       }
       // byte map: with few visited vertices the check costs more than the
