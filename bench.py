@@ -456,6 +456,9 @@ def main(argv=None) -> int:
             # through the windows in slot-sized rounds, so 0 is expected
             "comm_peer_ops": getattr(rt.comm, "peer_ops", None),
             "comm_inner_ops": getattr(rt.comm, "inner_ops", None),
+            # chains of the profiled traversal whose frontier the producing
+            # kernels pushed into the peers' windows (--opt direct_frontier=1)
+            "pushed_chains": sum(1 for c in getattr(prof, "chains", []) if len(c) > 6 and c[6]),
             "heldout": heldout,
             "secondary": secondary,
             "devices": [f"{'hip' if rt.is_gpu else 'cpu'}:{d}" for d in devices],

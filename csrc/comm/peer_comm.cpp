@@ -58,7 +58,10 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   hipIpcMemHandle_t h{};
   try {
     HIP_CHECK(hipSetDevice(be.device_id()));
-    const size_t total = kFlagBytes + 2 * static_cast<size_t>(size_) * slot_;
+    // the pushed frontier slices' region (Comm::direct_frontier)
+    if (const char* fe = std::getenv("DBFS_PEER_FRONTIER_MB")) fslot_ = static_cast<size_t>(std::max(0L, std::atol(fe))) << 20;
+    else fslot_ = size_t(8) << 20;
+    const size_t total = kFlagBytes + 2 * static_cast<size_t>(size_) * (slot_ + fslot_);
     void* w = nullptr;
     HIP_CHECK(hipExtMallocWithFlags(&w, total, hipDeviceMallocUncached));
     win_ = static_cast<char*>(w);
@@ -170,6 +173,31 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
     }
   }
   agree("direct exchange tables");  // (every rank has them, or none goes on)
+  // the pushed frontier slices' tables (one per parity): [parity][sender]
+  // buffers of fslot_ bytes after the slots
+  if (dtab_ && fslot_ > 0) {
+    FrontierTable t[2];
+    auto buf = [&](char* win, int parity, int sender) {
+      return reinterpret_cast<uint64_t*>(win + kFlagBytes + 2 * static_cast<size_t>(size_) * slot_ +
+                                         (static_cast<size_t>(parity) * size_ + sender) * fslot_);
+    };
+    for (int b = 0; b < 2; ++b) {
+      std::memset(&t[b], 0, sizeof(FrontierTable));
+      for (int p = 0; p < size_; ++p) {
+        t[b].dst[p] = p == rank_ ? nullptr : buf(peer_[p], b, rank_);
+        t[b].src[p] = p == rank_ ? nullptr : buf(win_, b, p);
+      }
+    }
+    try {
+      void* d = nullptr;
+      HIP_CHECK(hipMalloc(&d, sizeof(t)));
+      ftab_ = static_cast<FrontierTable*>(d);
+      HIP_CHECK(hipMemcpy(d, t, sizeof(t), hipMemcpyHostToDevice));
+    } catch (const std::exception& e) {
+      local_err = e.what();
+    }
+  }
+  agree("frontier push tables");
   // a wait kernel that timed out leaves its seq in the error word: the host's
   // waits (stream synchronise, mailbox spins) turn it into an error
   prev_watch_ = be.wait_watch();
@@ -216,6 +244,8 @@ void PeerComm::release() {
   ticket_ = nullptr;
   if (dtab_) hipFree(dtab_);
   dtab_ = nullptr;
+  if (ftab_) hipFree(ftab_);
+  ftab_ = nullptr;
   keep_.clear();
   if (win_keep_) win_keep_.reset();  // (in-process: frees with the last holder)
   else if (win_) hipFree(win_);
@@ -494,6 +524,13 @@ bool PeerComm::direct_lists(size_t cap, DirectExchange* x) {
   return true;
 }
 
+const FrontierTable* PeerComm::direct_frontier(size_t words, int parity) {
+  if (!ftab_ || words == 0 || words * sizeof(uint64_t) > fslot_) return nullptr;
+  note(kAllGather, static_cast<int64_t>(size_ - 1) * static_cast<int64_t>(words * sizeof(uint64_t)));
+  ++peer_ops_;
+  return ftab_ + (parity & 1);
+}
+
 bool PeerComm::direct_level_end(size_t count, DirectExchange* x) {
   // (a level's totals: at most 2^32 new vertices and 2^40 of their degrees
   // per rank -- the cells' payload widths)
@@ -670,7 +707,43 @@ bool PeerComm::self_test(std::string* why) {
   if (bad && err.empty()) err = "a peer's self-test failed";
   if (why) *why = err;
   if (bad == 0) direct_self_test();
+  if (bad == 0) frontier_self_test();
   return bad == 0;
+}
+
+// The pushed frontier slices: two rounds (both parities) of known words pushed
+// by every rank, a barrier, every peer's checked; a failure anywhere (agreed)
+// turns them off on every rank (the level ends then all-gather).
+void PeerComm::frontier_self_test() {
+  if (!ftab_) return;
+  std::string err;
+  try {
+    const int64_t words = std::min<int64_t>(static_cast<int64_t>(fslot_ / 8), 4096 + 37);
+    DBuf<unsigned> e(*be_, 1);
+    be_->memset_async(e.data(), 0, sizeof(unsigned));
+    for (int round = 0; round < 2; ++round) {
+      kern::frontier_selftest(ftab_ + round, rank_, size_, words, round, 0, e.data(), S(be_));
+      HIP_CHECK(hipGetLastError());
+      be_->synchronize();
+      HIP_CHECK(hipStreamSynchronize(S(be_)));
+      inner_->sum_host(0);  // (every rank's pushes have landed)
+      kern::frontier_selftest(ftab_ + round, rank_, size_, words, round, 1, e.data(), S(be_));
+      HIP_CHECK(hipGetLastError());
+    }
+    unsigned h = 0;
+    HIP_CHECK(hipStreamSynchronize(S(be_)));
+    be_->to_host(&h, e.data(), sizeof(h));
+    if (h) err = std::to_string(h) + " mismatched words";
+  } catch (const std::exception& ex) {
+    err = ex.what();
+  }
+  const int64_t bad = inner_->sum_host(err.empty() ? 0 : 1);
+  if (bad == 0) return;
+  if (rank_ == 0)
+    std::fprintf(stderr, "[dbfs] peer communicator: frontier push off (self-test: %s)\n",
+                 err.empty() ? "failed on a peer" : err.c_str());
+  hipFree(ftab_);
+  ftab_ = nullptr;
 }
 
 // The direct exchanges (kernels writing into the peers' windows, tagged
@@ -705,6 +778,8 @@ void PeerComm::direct_self_test() {
                  err.empty() ? "failed on a peer" : err.c_str());
   hipFree(dtab_);
   dtab_ = nullptr;
+  if (ftab_) hipFree(ftab_);  // (needs the direct exchanges' self-test passed too)
+  ftab_ = nullptr;
 }
 
 void PeerComm::barrier() {

@@ -45,6 +45,11 @@ class DeviceLoop {
     bool fused_scan = false;   // the chain's last kernel finishes the level
     bool level_ended = false;  // ... and also ran its level end (direct exchange)
     bool cut = false;          // several ranks: a hub-cut bottom-up level was enqueued
+    // several ranks: the output frontier pushed to the peers by the producing
+    // kernel (EngineOptions::direct_frontier), and the input frontier's pushed
+    // slices (the previous chain's table) for hub_gather to copy in
+    const FrontierTable* push = nullptr;
+    const FrontierTable* pull = nullptr;
   };
 
   Engine& e_;
@@ -77,6 +82,7 @@ class DeviceLoop {
 
   // ---- per-level records of what was enqueued ----
   std::vector<char> enq_dir_, enq_form_, enq_gather_, enq_fused_;
+  std::vector<const FrontierTable*> enq_push_;  // level L's output pushed (Chain::push)
   std::vector<int64_t> enq_cap_;
   std::vector<std::pair<int, int>> evs_;
   RunResult res_;
@@ -444,6 +450,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     enq_cap_.resize(static_cast<size_t>(L) + 1);
     enq_gather_.resize(static_cast<size_t>(L) + 1);
     enq_fused_.resize(static_cast<size_t>(L) + 1);
+    enq_push_.resize(static_cast<size_t>(L) + 1);
     evs_.resize(static_cast<size_t>(L) + 1, {-1, -1});
   }
   Chain c;
@@ -458,7 +465,15 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
   enq_form_[L] = d;
   enq_cap_[L] = d == 'S' ? cap : 0;
   enq_gather_[L] = xc_ && gather;
+  // (the pushed slices are copied in by hub_gather: graphs with hubs; the
+  // table's parity is the level's -- see FrontierTable)
+  c.pull = L > 0 ? enq_push_[static_cast<size_t>(L - 1)] : nullptr;
+  c.push = enq_gather_[L] && opt_.direct_frontier && gv_.nhubs > 0 && (d == 'T' || d == 'B')
+               ? comm_.direct_frontier(static_cast<size_t>(W_), L & 1)
+               : nullptr;
+  enq_push_[L] = c.push;
   res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
+  res_.chains.back().push = c.push != nullptr;
   c.cap = enq_cap_[L];
   c.mf_hint = mf_hint;
   c.cur = (L + 1) & 1;
@@ -487,7 +502,8 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
   res_.chains.back().cut = c.cut;
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
   enq_fused_[L] = c.fused_scan && d != 'S';
-  if (xc_ && !c.level_ended) finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] != 0, d == 'S' && hx_chain(L));
+  if (xc_ && !c.level_ended)
+    finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] && !c.push, d == 'S' && hx_chain(L));
   if (opt_.phase_timing) evs_[L] = {ev0, be_.record_event()};
   if (ht_) hmark("enqueued " + std::to_string(L));
 }
@@ -773,6 +789,9 @@ void DeviceLoop::emit_dense(Chain& c) {
   tu.frontier = fr_own(c.cur ^ 1);
   tu.new_level = L + 1;
   tu.ctrl = e_.ctrl_.data();
+  tu.push = c.push;
+  tu.push_rank = me_;
+  tu.push_nranks = P_;
   if (opt_.td_fused_finish) {
     // totals (and with one rank the decision) in the update's last
     // workgroup (as bottom-up)
@@ -811,12 +830,23 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.unit_cnt = e_.unit_cnt_.data();
   ba.unit_deg = e_.unit_deg_.data();
   ba.ctrl = e_.ctrl_.data();
+  ba.push = c.push;
+  ba.push_rank = me_;
+  ba.push_nranks = P_;
   if (gv_.nhubs > 0) {
     HubGatherArgs hg;
     hg.g = gv_;
     hg.frontier = e_.frontier_[c.cur].data();
     hg.hub_front = e_.hub_front_.data();
     hg.ctrl = e_.ctrl_.data();
+    if (c.pull) {
+      // the peers' slices pushed by the previous level's kernels
+      hg.pull = c.pull;
+      hg.pull_out = e_.frontier_[c.cur].data();
+      hg.pull_rank = me_;
+      hg.pull_nranks = P_;
+      hg.pull_words = W_;
+    }
     // several ranks, bu_merge_visited: the gathered remote slices merged into
     // the replicated visited bitmap in the same launch
     if (xc_ && opt_.bu_merge_visited) {
@@ -842,7 +872,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     const int64_t cut_edges = xc_ ? std::min(opt_.bu_cut_edges, list_max_) : opt_.bu_cut_edges;
     if (cut) {
       if (!e_.cut_part_.data()) {
-        e_.cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(div_up(gv_.nhubs, int64_t(64))));
+        e_.cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(div_up(gv_.nhubs, int64_t(64)), kHgCopyGrid)));
         e_.cut_flag_ = DBuf<int>(be_, 1);
         e_.cut_ticket_ = DBuf<unsigned>(be_, 1);
         be_.memset_async(e_.cut_ticket_.data(), 0, e_.cut_ticket_.bytes());
@@ -909,7 +939,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     // frontier gather; the hub kernels' fused finish)
     // (not on a hub-cut level: its plain and cut kernels are both launched,
     // and only the plain ones have the folded end)
-    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && !enq_gather_[L] && !c.cut &&
+    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !c.cut &&
         comm_.direct_level_end(2, &ba.end)) {
       ba.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;

@@ -97,6 +97,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
+  else if (name == "direct_frontier") o.direct_frontier = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -148,7 +149,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_cut_ranks", o.bu_cut_ranks ? 1.0 : 0.0},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
-          {"direct_level_end", o.direct_level_end ? 1.0 : 0.0}};
+          {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
+          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------

@@ -293,6 +293,8 @@ struct ScanArgs {
   bool finish = true;
 };
 
+struct FrontierTable;  // (below, with the direct exchanges)
+
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -338,6 +340,9 @@ struct UpdateArgs {
   // be large without thousands of same-address atomics.  Null: one ticket
   // (grid capped at kMaxFusedGrid / 8).
   unsigned* group_ticket = nullptr;
+  // several ranks: the new frontier words also pushed to the peers (FrontierTable)
+  const FrontierTable* push = nullptr;
+  int push_rank = 0, push_nranks = 1;
 };
 
 
@@ -456,6 +461,20 @@ struct DirectTable {
   const uint32_t* src[kMaxDirectRanks];      // this rank's window slot of sender p
   const uint64_t* cell_in[kMaxDirectRanks];  // this rank's cell of sender p ([rank]: unused)
 };
+// Frontier slices pushed by the kernels that produce them (several ranks,
+// peer transport, Comm::direct_frontier): each output word also goes,
+// write-through, to every peer's window buffer for this rank's slice
+// (dst[p]), and the next level's hub_gather copies the peers' slices from
+// this rank's window (src[p]) into its global frontier -- the all-gather
+// rides the producing kernel instead of a collective after it.  One table per
+// buffer parity (the producing level's parity: a peer writes level L + 2's
+// slice only after level L + 1's end, which this rank reaches after it has
+// copied level L's); [rank] unused.
+struct FrontierTable {
+  uint64_t* dst[kMaxDirectRanks];
+  const uint64_t* src[kMaxDirectRanks];
+};
+
 struct DirectExchange {
   int active = 0;  // 0: the exchange goes through a Comm collective instead
   int nranks = 1, rank = 0;
@@ -762,6 +781,9 @@ struct BuArgs {
   DirectExchange cut_direct;
   unsigned* cut_prep_ticket = nullptr;
   const vid_t* cut_recv_lists = nullptr;
+  // several ranks: the new frontier words also pushed to the peers (FrontierTable)
+  const FrontierTable* push = nullptr;
+  int push_rank = 0, push_nranks = 1;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the
@@ -789,6 +811,10 @@ struct HubApplyArgs {
   int64_t max_mf = 0;  // chain predicate, as TdArgs::max_mf
 };
 
+// hub_gather copies (visited merge, pushed slices) with at most this many
+// workgroups (the hub-cut part sums are sized for it)
+constexpr int kHgCopyGrid = 512;
+
 // hub_front bit h = frontier bit of g.hub_vertex[h] (frontier global); in the
 // device loop only when ctrl->dir == 'B'.
 struct HubGatherArgs {
@@ -807,6 +833,14 @@ struct HubGatherArgs {
   int64_t cut_edges = 0;
   int* cut_flag = nullptr;
   unsigned* cut_ticket = nullptr;
+  // several ranks, the previous level's slices pushed (FrontierTable): the
+  // peers' slices copied from this rank's window into pull_out (the global
+  // frontier; `words` per slice) -- and merged into visited with `visited` --
+  // and the hubs' bits read from their owners' slices directly
+  const FrontierTable* pull = nullptr;
+  word_t* pull_out = nullptr;
+  int pull_rank = 0, pull_nranks = 1;
+  int64_t pull_words = 0;
 };
 
 // Bits of the owned slice for vertices with degree 0 or beyond the shard

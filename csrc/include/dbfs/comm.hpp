@@ -99,6 +99,16 @@ class Comm {
     (void)x;
     return false;
   }
+  // The frontier slices of `words` words each pushed by the producing kernels
+  // themselves into the peers' windows (FrontierTable, buffer `parity`):
+  // the device table, or nullptr when this transport cannot (the caller
+  // all-gathers them with the level end).  The choice depends only on
+  // `words` (the same on every rank).
+  virtual const FrontierTable* direct_frontier(size_t words, int parity) {
+    (void)words;
+    (void)parity;
+    return nullptr;
+  }
   // A level's end on several ranks: its totals all-reduced (buf, count) --
   // with gbytes > 0 also its output frontier slice all-gathered (gsend ->
   // grecv) -- then the device continuation `fin`, the level's decision on the
@@ -406,6 +416,7 @@ class PeerComm final : public Comm {
   bool counted_lists() const override { return true; }
   bool direct_lists(size_t cap, DirectExchange* x) override;
   bool direct_level_end(size_t count, DirectExchange* x) override;
+  const FrontierTable* direct_frontier(size_t words, int parity) override;
   void allgather_allreduce(const void* send, void* recv, size_t bytes, int64_t* buf, size_t count) override;
   void level_end(const void* gsend, void* grecv, size_t gbytes, int64_t* buf, size_t count,
                  const LevelFinishArgs& fin) override;
@@ -465,6 +476,12 @@ class PeerComm final : public Comm {
   // owner lists exchanged by the kernels themselves (DBFS_PEER_DIRECT=0: off):
   // the device tables of DirectExchange, one per parity
   DirectTable* dtab_ = nullptr;
+  // pushed frontier slices: a region of 2 x P buffers of fslot_ bytes after
+  // the slots (DBFS_PEER_FRONTIER_MB, default 8; 0: none) and its device
+  // tables, one per parity
+  size_t fslot_ = 0;
+  FrontierTable* ftab_ = nullptr;
+  void frontier_self_test();
   std::function<void(double)> prev_watch_;
   bool watch_installed_ = false;
   char* slot_ptr(int owner, int parity, int sender) const;

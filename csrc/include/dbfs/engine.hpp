@@ -306,6 +306,12 @@ struct EngineOptions {
   // ... and their level's end folded into td_sparse_apply's last workgroup
   // (Comm::direct_level_end) when it gathers no frontier
   bool direct_level_end = true;
+  // Several ranks, a level whose frontier is all-gathered for a bottom-up
+  // level next (graphs with hubs): the producing kernels push their output
+  // words straight into the peers' windows (Comm::direct_frontier) and the
+  // bottom-up level's hub_gather copies them in -- the level end carries only
+  // its totals (and may fold into the bottom-up kernel).  Off until measured.
+  bool direct_frontier = false;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
@@ -359,6 +365,9 @@ struct ChainRecord {
   int64_t hx_words = 0;
   // several ranks: a hub-cut bottom-up chain (its owner-list exchange)
   bool cut = false;
+  // several ranks: its output frontier pushed by its kernels (no gather in
+  // its level end; EngineOptions::direct_frontier)
+  bool push = false;
 };
 
 struct RunResult {

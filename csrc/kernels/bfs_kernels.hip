@@ -248,6 +248,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
     nb = a.force ? c : (c & ~vis);
     if (nb) a.visited[wl] = vis | nb;
     a.frontier[wl] = nb;
+    if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, wl, nb);
     if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
   // New vertices of the unit, 64 per step (one per lane, whatever word they

@@ -273,6 +273,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   if (total == 0) {
     if (lane < nw) {
       a.new_frontier[w0 + lane] = pw;
+      if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, pw);
       if (pw) a.visited[w0 + lane] = ~um;  // (= visited | pw)
     }
     take_pre();
@@ -467,6 +468,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   if (lane < nw) {
     const word_t res = s_res[lane] | pw;
     a.new_frontier[w0 + lane] = res;
+    if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, res);
     if (res) a.visited[w0 + lane] = ~um | res;  // (~um holds pw)
   }
   take_pre();
@@ -680,7 +682,16 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
 // last-arriving workgroup (of ~128) totals them and stores the decision
 // ctrl->m_f - hub edges <= cut_edges in *cut_flag -- the same on every rank
 // (global frontier, global degrees).
+// Pushed slices (HubGatherArgs::pull): the hubs' bits read from their owners'
+// slices in this rank's window, and the whole grid copies the peers' slices
+// into the global frontier (merging them into visited with the merge).
 constexpr int kHgThreads = 1024, kHgPer = 4;
+__device__ __forceinline__ bool pulled_bit(const HubGatherArgs& a, vid_t v) {
+  const int64_t w = static_cast<int64_t>(v >> 6);
+  const int p = static_cast<int>(w / a.pull_words);
+  const word_t f = p == a.pull_rank ? a.frontier[w] : sys_load_u64(a.pull->src[p] + (w - p * a.pull_words));
+  return (f >> (v & 63)) & 1ull;
+}
 template <bool kCut>
 __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
 #pragma unroll
   for (int k = 0; k < kHgPer; ++k) {
     const int64_t h = base + k * kHgThreads + threadIdx.x;
-    bit[k] = h < a.g.nhubs && test_bit(a.frontier, hv[k]);
+    bit[k] = h < a.g.nhubs && (a.pull ? pulled_bit(a, hv[k]) : test_bit(a.frontier, hv[k]));
   }
   long long d = 0;
 #pragma unroll
@@ -712,7 +723,17 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
       d += a.g.hub_deg ? static_cast<long long>(a.g.hub_deg[h])
                        : static_cast<long long>(a.g.row_off[hv[k] + 1] - a.g.row_off[hv[k]]);
   }
-  if (a.visited) {
+  if (a.pull) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kHgThreads;
+    const int64_t gw = a.pull_words * a.pull_nranks;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kHgThreads + threadIdx.x; i < gw; i += stride) {
+      const int p = static_cast<int>(i / a.pull_words);
+      if (p == a.pull_rank) continue;
+      const word_t f = sys_load_u64(a.pull->src[p] + (i - p * a.pull_words));
+      a.pull_out[i] = f;
+      if (a.visited && f) a.visited[i] |= f;
+    }
+  } else if (a.visited) {
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kHgThreads;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kHgThreads + threadIdx.x; i < a.words; i += stride) {
       const word_t f = a.frontier[i];
@@ -1002,14 +1023,20 @@ void bu_cut_apply(const BuArgs& a, hipStream_t st) {
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {
   if (a.g.nhubs <= 0) return;
+  DBFS_CHECK(!a.pull || (a.pull_out && a.pull_words > 0 && a.pull_nranks > 1 && a.pull_nranks <= kMaxDirectRanks &&
+                         a.pull_rank >= 0 && a.pull_rank < a.pull_nranks),
+             "hub_gather: pushed-slice arguments incomplete");
+  // (with the visited merge or pushed slices: at least a grid striding over
+  // the words well -- <= kHgCopyGrid workgroups, the cut decision's part sums
+  // are sized for that)
+  unsigned grid = grid_for(a.g.nhubs, kHgThreads * kHgPer);
+  if (a.visited || a.pull)
+    grid = std::max(grid, grid_for(a.pull ? a.pull_words * a.pull_nranks : a.words, kHgThreads, kHgCopyGrid));
   if (a.cut_part) {
     DBFS_CHECK(a.cut_flag && a.cut_ticket && a.ctrl, "hub_gather: the hub-cut decision needs a flag, a ticket and the level state");
-    hub_gather_kernel<true><<<grid_for(a.g.nhubs, kHgThreads * kHgPer), kHgThreads, 0, st>>>(a);
+    hub_gather_kernel<true><<<grid, kHgThreads, 0, st>>>(a);
     return;
   }
-  // (with the visited merge: at least a grid striding over the words well)
-  unsigned grid = grid_for(a.g.nhubs, kHgThreads * kHgPer);
-  if (a.visited) grid = std::max(grid, grid_for(a.words, kHgThreads, 512));
   hub_gather_kernel<false><<<grid, kHgThreads, 0, st>>>(a);
 }
 

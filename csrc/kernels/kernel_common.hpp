@@ -151,6 +151,14 @@ __device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Frontier push (backend.hpp FrontierTable): word w of this rank's slice to
+// every peer's window, write-through.
+__device__ __forceinline__ void push_frontier_word(const FrontierTable* t, int rank, int nranks, int64_t w,
+                                                   uint64_t v) {
+  for (int p = 0; p < nranks; ++p)
+    if (p != rank) sys_store_u64(t->dst[p] + w, v);
+}
+
 // Append v (act lanes) to its owner's list: one atomic per wave and owner on
 // the count word (lists + owner * stride), the ids after it -- or, with a
 // direct exchange table, after the count word of the owner's window slot

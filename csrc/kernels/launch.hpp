@@ -27,6 +27,11 @@ void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
 // timeouts counted in *err)
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
                      unsigned* ticket, hipStream_t st);
+// PeerComm::self_test of the pushed frontier slices: phase 0 pushes `words`
+// known words of this rank's slice, phase 1 (after a barrier) checks every
+// peer's (mismatches counted in *err)
+void frontier_selftest(const FrontierTable* t, int rank, int nranks, int64_t words, int round, int phase,
+                       unsigned* err, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
 // graph_sort.hip: hub-split rows of ShardView::hx_off -- counts per top-down
 // hub (out == nullptr), or the rows' global ids at cnt[h]++ (cursors)

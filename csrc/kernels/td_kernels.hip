@@ -1286,6 +1286,32 @@ void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int
   direct_selftest_kernel<<<kSelftestGroups, 256, 0, st>>>(lists, end, round, err, ticket);
 }
 
+namespace {
+__device__ __forceinline__ uint64_t frontier_pat(int r, int64_t i, int round) {
+  return (static_cast<uint64_t>(r + 1) << 48) ^ (static_cast<uint64_t>(i) * 0x9E3779B97F4A7C15ull) ^
+         static_cast<uint64_t>(round);
+}
+__global__ __launch_bounds__(256) void frontier_selftest_kernel(const FrontierTable* t, int rank, int nranks,
+                                                                int64_t words, int round, int phase, unsigned* err) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  unsigned bad = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < words; i += stride) {
+    if (phase == 0) {
+      push_frontier_word(t, rank, nranks, i, frontier_pat(rank, i, round));
+      continue;
+    }
+    for (int p = 0; p < nranks; ++p)
+      if (p != rank && sys_load_u64(t->src[p] + i) != frontier_pat(p, i, round)) ++bad;
+  }
+  if (bad) atomicAdd(err, bad);
+}
+}  // namespace
+
+void frontier_selftest(const FrontierTable* t, int rank, int nranks, int64_t words, int round, int phase,
+                       unsigned* err, hipStream_t st) {
+  frontier_selftest_kernel<<<grid_for(words, 256, 64), 256, 0, st>>>(t, rank, nranks, words, round, phase, err);
+}
+
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {
   // (1024 threads, two ids each: as td_sparse)
   td_sparse_apply_kernel<kTdSparseThreads>

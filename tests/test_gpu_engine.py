@@ -1068,3 +1068,18 @@ def test_peer_multirank_options(opts):
         args += ["--opt", o]
     rec = _bench_peer(args, DBFS_PEER_SLOT_MB="16")
     assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
+
+
+@pytest.mark.parametrize("opts", [["direct_frontier=1"], ["direct_frontier=1", "bu_merge_visited=1"]])
+def test_peer_direct_frontier(opts):
+    """Pushed frontier slices (EngineOptions::direct_frontier): the top-down
+    update and bottom-up kernels store their output words into the peers'
+    windows and the next bottom-up level's hub_gather copies them in (the level
+    end carries only totals).  4 processes on device 0 at RMAT-18, every timed
+    root validated, and the profiled traversal did push."""
+    args = ["--gpus", "4", "--scale", "18", "--steps", "6", "--warmup", "1"]
+    for o in opts:
+        args += ["--opt", o]
+    rec = _bench_peer(args, DBFS_PEER_SLOT_MB="16")
+    assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
+    assert rec["pushed_chains"] > 0
