@@ -802,6 +802,13 @@ void DeviceLoop::emit_dense(Chain& c) {
     tu.tot = e_.td_tot_.data();
     if (opt_.td_group_ticket) tu.group_ticket = group_tickets();
     c.fused_scan = true;
+    // several ranks: the level's end in the same last workgroup (no frontier
+    // gathered, or a pushed one)
+    if (xc_ && opt_.direct_level_end && cells_fit() && (!enq_gather_[L] || c.push) &&
+        comm_.direct_level_end(2, &tu.end)) {
+      tu.fin = finish_args(L, false, enq_dir_[L], c.cap);
+      c.level_ended = true;
+    }
   }
   be_.update_frontier(tu);
 }

@@ -293,59 +293,6 @@ struct ScanArgs {
   bool finish = true;
 };
 
-struct FrontierTable;  // (below, with the direct exchanges)
-
-// new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
-// (force: new = cand, used to seed the source):  visited |= new;
-// frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
-// = count / degree-sum of new vertices with degree > 0.  clear_cand zeroes the
-// consumed cand words (single-chunk top-down: keeps `next` clean).
-struct UpdateArgs {
-  ShardView g;
-  word_t* cand = nullptr;
-  // Byte-map candidates (one byte per vertex, 0/1) instead of `cand`: used
-  // after a byte-map top-down step on one rank; the bytes are cleared.
-  uint8_t* cand_bytes = nullptr;
-  int nchunks = 1;
-  int64_t cand_stride = 0;       // words between chunks
-  bool clear_cand = false;
-  bool force = false;
-  word_t* visited = nullptr;     // owned slice of the global visited bitmap
-  word_t* frontier = nullptr;    // owned slice of the NEXT global frontier bitmap
-  lvl_t* level = nullptr;        // rows
-  uint8_t* level8 = nullptr;     // narrow levels (see InitRunArgs)
-  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
-  lvl_t new_level = 0;
-  int64_t words = 0;             // words of the owned slice
-  int64_t* unit_cnt = nullptr;   // nunits
-  int64_t* unit_deg = nullptr;   // nunits
-  // Device loop: runs only when ctrl->dir == 'T'; reads cand_bytes when
-  // ctrl->bytes, else cand (both given).
-  const LevelCtrl* ctrl = nullptr;
-  int64_t max_mf = 0;  // list-form chain: live only while ctrl->m_f <= max_mf
-  // With the byte-map levels of TdArgs::level_direct: candidates are the
-  // unvisited vertices whose level already reads new_level (level8, padded to
-  // whole words); cand_bytes is not read.
-  const uint8_t* level_direct = nullptr;
-  // One rank, device loop (as BuArgs::fuse_scan): totals and finish in the
-  // last-arriving workgroup, unit statistics left unscanned (a following
-  // compaction scans them first); tot[0..1] zero, reset by the last one.
-  bool fuse_scan = false;
-  ScanArgs scan;
-  int64_t* tot = nullptr;
-  // ... with the ticket two-level: workgroups of kFusedGroup consecutive ids
-  // share a group ticket (kBuQueueStride apart, zero between launches; the
-  // group's last workgroup re-zeroes it, sums the group's slots into
-  // tot[2 kMaxFusedGrid + 2 g] and takes the level ticket), so the grid can
-  // be large without thousands of same-address atomics.  Null: one ticket
-  // (grid capped at kMaxFusedGrid / 8).
-  unsigned* group_ticket = nullptr;
-  // several ranks: the new frontier words also pushed to the peers (FrontierTable)
-  const FrontierTable* push = nullptr;
-  int push_rank = 0, push_nranks = 1;
-};
-
-
 // Device loop, several ranks: after the totals' all-reduce (stats[2..3] =
 // global count / degree sum), one thread runs level_ctrl_finish (seed: from
 // ctrl_init) and stamps rec / the mailbox, as the one-rank scan does.
@@ -485,6 +432,61 @@ struct DirectExchange {
   // a level end: the all-reduced totals as recorded (shadow replay) instead
   // of the peers' cells summed
   const int64_t* result = nullptr;
+};
+
+// new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
+// (force: new = cand, used to seed the source):  visited |= new;
+// frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
+// = count / degree-sum of new vertices with degree > 0.  clear_cand zeroes the
+// consumed cand words (single-chunk top-down: keeps `next` clean).
+struct UpdateArgs {
+  ShardView g;
+  word_t* cand = nullptr;
+  // Byte-map candidates (one byte per vertex, 0/1) instead of `cand`: used
+  // after a byte-map top-down step on one rank; the bytes are cleared.
+  uint8_t* cand_bytes = nullptr;
+  int nchunks = 1;
+  int64_t cand_stride = 0;       // words between chunks
+  bool clear_cand = false;
+  bool force = false;
+  word_t* visited = nullptr;     // owned slice of the global visited bitmap
+  word_t* frontier = nullptr;    // owned slice of the NEXT global frontier bitmap
+  lvl_t* level = nullptr;        // rows
+  uint8_t* level8 = nullptr;     // narrow levels (see InitRunArgs)
+  uint8_t narrow_base = 0;             // narrow level bytes of this run: base + level (kNarrowEpochs)
+  lvl_t new_level = 0;
+  int64_t words = 0;             // words of the owned slice
+  int64_t* unit_cnt = nullptr;   // nunits
+  int64_t* unit_deg = nullptr;   // nunits
+  // Device loop: runs only when ctrl->dir == 'T'; reads cand_bytes when
+  // ctrl->bytes, else cand (both given).
+  const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;  // list-form chain: live only while ctrl->m_f <= max_mf
+  // With the byte-map levels of TdArgs::level_direct: candidates are the
+  // unvisited vertices whose level already reads new_level (level8, padded to
+  // whole words); cand_bytes is not read.
+  const uint8_t* level_direct = nullptr;
+  // One rank, device loop (as BuArgs::fuse_scan): totals and finish in the
+  // last-arriving workgroup, unit statistics left unscanned (a following
+  // compaction scans them first); tot[0..1] zero, reset by the last one.
+  bool fuse_scan = false;
+  ScanArgs scan;
+  int64_t* tot = nullptr;
+  // ... with the ticket two-level: workgroups of kFusedGroup consecutive ids
+  // share a group ticket (kBuQueueStride apart, zero between launches; the
+  // group's last workgroup re-zeroes it, sums the group's slots into
+  // tot[2 kMaxFusedGrid + 2 g] and takes the level ticket), so the grid can
+  // be large without thousands of same-address atomics.  Null: one ticket
+  // (grid capped at kMaxFusedGrid / 8).
+  unsigned* group_ticket = nullptr;
+  // several ranks: the new frontier words also pushed to the peers (FrontierTable)
+  const FrontierTable* push = nullptr;
+  int push_rank = 0, push_nranks = 1;
+  // several ranks, fused finish: the level's end in the last workgroup
+  // (Comm::direct_level_end; no frontier gathered, or a pushed one); it runs
+  // on a no-op chain too (a collective)
+  DirectExchange end;
+  LevelFinishArgs fin;
 };
 
 struct TdSparseArgs {

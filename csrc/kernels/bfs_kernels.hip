@@ -306,9 +306,15 @@ __device__ __forceinline__ void update_unit_split(const UpdateArgs& a, int64_t u
 
 template <bool kSplit>
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
+  __shared__ uint64_t s_x[2 * kern::kMaxPeers];  // (the folded level end's cells)
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
-    if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
+      // a folded level end is a collective: it runs on a no-op chain too
+      if (a.end.active && blockIdx.x == 0)
+        direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin, s_x);
+      return;
+    }
     use_bytes = use_bytes && a.ctrl->bytes != 0;
   }
   const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));  // (wave-uniform)
@@ -353,6 +359,9 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     s_c[wv] = wc;
     s_d[wv] = wd;
   }
+  // (pushed words: every wave's write-through stores drained before the
+  // ticket, so the level end published after it covers them)
+  if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     long long c = 0, d = 0;
@@ -439,6 +448,12 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
       td += s_d[k];
     }
     scan_finish(a.scan, tc, td);
+    s_c[0] = tc;
+    s_d[0] = td;
+  }
+  if (a.end.active) {
+    __syncthreads();
+    direct_level_end(a.end, s_c[0], s_d[0], a.scan.stats, a.fin, s_x);
   }
 }
 
@@ -759,6 +774,7 @@ void publish_stats(const int64_t* stats, StatsMailbox* mb, int64_t seq, hipStrea
 constexpr int64_t kSplitUnits = 4096;
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
+  DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   const bool split = nunits < kSplitUnits;

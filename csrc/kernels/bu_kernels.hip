@@ -613,6 +613,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       }
     }
     if (!a.fuse_scan) return;
+    // (pushed words: every wave's write-through stores drained before the
+    // ticket, so a level end published after it covers them)
+    if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     long long wc = 0, wd = 0;
     if (threadIdx.x == 0)
@@ -662,6 +665,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     __syncthreads();
   }
   if (!a.fuse_scan) return;
+  if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above)
   __syncthreads();  // (an empty loop: the accumulators' zeroing)
   long long wc = 0, wd = 0;
   if (threadIdx.x == 0)
