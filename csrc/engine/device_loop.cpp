@@ -74,6 +74,10 @@ class DeviceLoop {
   int bin_shift_ = 12;
   int64_t nbins_ = 0;
   bool binned_ = false;
+  // one rank: hub marks (EngineOptions::bu_hub_marks; buffer k of the chain
+  // of parity k, backend.hpp)
+  bool marks_ = false;
+  word_t* marks(int L) const { return e_.hub_marks_.data() + (L & 1) * hub_mark_words(gv_.nhubs); }
   static constexpr int kBinGrid = 1024;
   int64_t td_grid_ = 1, td_grid_filter_ = 1;
   bool seed_gather_ = false;
@@ -131,6 +135,7 @@ class DeviceLoop {
   void emit_binned(Chain& c);
   void emit_dense(Chain& c);
   void emit_bottom_up(Chain& c);
+  void fuse_update(Chain& c, UpdateArgs& tu);
 
   RunResult collect(int nlev, std::chrono::steady_clock::time_point t1);
 };
@@ -166,6 +171,11 @@ void DeviceLoop::setup() {
   }
   // one rank with narrow levels: byte-map levels write the levels directly
   direct_ = !xc_ && e_.run_narrow_ && opt_.td_direct;
+  // (the marks' buffers are cleared by the chains' fused finishes)
+  marks_ = !xc_ && opt_.bu_hub_marks && gv_.nhubs > 0 && gv_.hub_min_deg > 0 && gv_.hub_bits && gv_.hub_deg &&
+           opt_.td_fused_finish && opt_.bu_fused_scan;
+  if (marks_ && !e_.hub_marks_.data())
+    e_.hub_marks_ = DBuf<word_t>(be_, static_cast<size_t>(2 * hub_mark_words(gv_.nhubs)));
   byte_edges_ = direct_ ? opt_.td_direct_edges : opt_.td_byte_edges;
   bytes_ok_ = opt_.mode != Mode::BottomUp && byte_edges_ <= e_.total_directed_;
   if (bytes_ok_ && !e_.next_bytes_.data()) {
@@ -586,6 +596,10 @@ void DeviceLoop::emit_sparse(Chain& c) {
   sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
   sp.first = !compacted || from_bits;
   sp.max_mf = c.cap;
+  if (marks_) {
+    sp.hub_mark = marks(L);
+    sp.hub_mark_clear = marks(L + 1);
+  }
   if (from_bits) {
     sp.from_bits = true;
     sp.words = W_;
@@ -690,7 +704,24 @@ void DeviceLoop::emit_binned(Chain& c) {
   tu.frontier = fr_own(c.cur ^ 1);
   tu.new_level = L + 1;
   tu.ctrl = e_.ctrl_.data();
+  if (marks_) {
+    // (hub marks: the fused finish clears the other buffer)
+    fuse_update(c, tu);
+    tu.hub_mark = marks(L);
+    tu.hub_mark_clear = marks(L + 1);
+  }
   be_.update_frontier(tu);
+}
+
+// The update's fused finish: the level's totals (and with one rank its
+// decision) in its last workgroup, as bottom-up.
+void DeviceLoop::fuse_update(Chain& c, UpdateArgs& tu) {
+  if (!e_.td_tot_.data()) e_.td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
+  tu.fuse_scan = true;
+  tu.scan = scan_args(c.L, false, enq_dir_[c.L], c.cap);
+  tu.tot = e_.td_tot_.data();
+  if (opt_.td_group_ticket) tu.group_ticket = group_tickets();
+  c.fused_scan = true;
 }
 
 // 'T': a dense top-down level -- compact (unless a sparse level or the seed
@@ -792,16 +823,14 @@ void DeviceLoop::emit_dense(Chain& c) {
   tu.push = c.push;
   tu.push_rank = me_;
   tu.push_nranks = P_;
+  if (marks_) {
+    tu.hub_mark = marks(L);
+    tu.hub_mark_clear = marks(L + 1);
+  }
   if (opt_.td_fused_finish) {
     // totals (and with one rank the decision) in the update's last
     // workgroup (as bottom-up)
-    if (!e_.td_tot_.data())
-      e_.td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
-    tu.fuse_scan = true;
-    tu.scan = scan_args(L, false, enq_dir_[L], c.cap);
-    tu.tot = e_.td_tot_.data();
-    if (opt_.td_group_ticket) tu.group_ticket = group_tickets();
-    c.fused_scan = true;
+    fuse_update(c, tu);
     // several ranks: the level's end in the same last workgroup (no frontier
     // gathered, or a pushed one)
     if (xc_ && opt_.direct_level_end && cells_fit() && (!enq_gather_[L] || c.push) &&
@@ -840,6 +869,10 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.push = c.push;
   ba.push_rank = me_;
   ba.push_nranks = P_;
+  if (marks_) {
+    ba.hub_mark = marks(L);
+    ba.hub_mark_clear = marks(L + 1);
+  }
   if (gv_.nhubs > 0) {
     HubGatherArgs hg;
     hg.g = gv_;
@@ -889,8 +922,15 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.cut_flag = e_.cut_flag_.data();
       hg.cut_ticket = e_.cut_ticket_.data();
     }
-    be_.hub_gather(hg);
-    ba.hub_front = e_.hub_front_.data();
+    if (marks_) {
+      // the previous chain marked the frontier hubs (its buffer); bu_cut_prep
+      // decides a hub cut from their degree word
+      ba.hub_front = marks(L + 1);
+      ba.cut_from_marks = cut;
+    } else {
+      be_.hub_gather(hg);
+      ba.hub_front = e_.hub_front_.data();
+    }
     if (cut) {
       ba.cut_edges = cut_edges;
       ba.cut_flag = e_.cut_flag_.data();
@@ -999,6 +1039,11 @@ RunResult DeviceLoop::run() {
     ia.blk_vstart = e_.blk_vstart_.data();
     ia.qv = e_.qv_[0].data();
     ia.frontier_clear = fr_own(0);
+  }
+  if (marks_) {
+    // (the seed is the output of "chain -1": parity 1)
+    ia.hub_mark_seed = marks(1);
+    ia.hub_mark_zero = marks(0);
   }
   be_.init_run(ia);
   // the seed's frontier is gathered with its totals when level 0 is bottom-up

@@ -98,6 +98,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
   else if (name == "direct_frontier") o.direct_frontier = v != 0;
+  else if (name == "bu_hub_marks") o.bu_hub_marks = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -150,7 +151,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
-          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
+          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0},
+          {"bu_hub_marks", o.bu_hub_marks ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -321,6 +323,7 @@ ShardView DeviceGraph::view() const {
   v.hub_col = hub_col_.data();
   v.hub_bits = hub_bits_.data();
   v.hub_deg = hub_deg_.data();
+  v.hub_min_deg = hub_min_deg_;
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -390,6 +393,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   comm.allgather(mine.data(), all.data(), static_cast<size_t>(part) * sizeof(uint32_t));
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
   nhubs_ = 0;
+  hub_min_deg_ = 0;
   hub_vertex_.reset();
   hub_bits_.reset();
   hub_deg_.reset();
@@ -411,6 +415,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       nhubs_ = be_->select_hubs(all.data(), nall, min_deg, hub_vertex_.data(), hub_idx.data());
       DBFS_CHECK(nhubs_ >= 0 && nhubs_ <= max_hubs, "hub selection exceeded its capacity");
       if (nhubs_ > 0) {
+        hub_min_deg_ = min_deg;
         // hub membership bitmap over all vertices (hub-cut bottom-up levels)
         std::vector<vid_t> hv(static_cast<size_t>(nhubs_));
         be_->to_host(hv.data(), hub_vertex_.data(), hv.size() * sizeof(vid_t));

@@ -50,6 +50,8 @@ struct ShardView {
   // vertex id.  Bottom-up keeps the hubs' frontier bits in LDS.
   const vid_t* hub_vertex = nullptr;
   int64_t nhubs = 0;
+  // a vertex is a hub iff its degree (row length) >= hub_min_deg (> 0 with hubs)
+  uint32_t hub_min_deg = 0;
   // Hub-encoded copy of col (same layout; hub neighbours as kHubFlag | index),
   // read by bottom-up so that probes of hub neighbours hit LDS too.
   const vid_t* hub_col = nullptr;
@@ -255,6 +257,9 @@ struct InitRunArgs {
   int32_t* blk_vstart = nullptr;
   vid_t* qv = nullptr;
   word_t* frontier_clear = nullptr;
+  // hub marks: the seed's written (hub_mark_seed), the other buffer zeroed
+  word_t* hub_mark_seed = nullptr;
+  word_t* hub_mark_zero = nullptr;
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;
@@ -434,6 +439,17 @@ struct DirectExchange {
   const int64_t* result = nullptr;
 };
 
+// Hub marks (one rank, EngineOptions::bu_hub_marks): the kernels that settle
+// a level's vertices also set the bits a bottom-up level stages for the
+// frontier hubs (hub_gather's hub_front: bit h for hub_vertex[h]) and add the
+// hubs' degrees into the last word (the hub-cut decision) -- no hub_gather
+// launch before a bottom-up level.  Two buffers by the producing chain's
+// parity: the chain of level L marks buffer L & 1 (zero on entry: hub_mark)
+// and its last workgroup zeroes buffer (L + 1) & 1 (hub_mark_clear) -- the
+// one it read, if bottom-up -- so the next chain finds its buffer clean; the
+// run's initialisation writes the seed's marks and zeroes the other buffer.
+constexpr int64_t hub_mark_words(int64_t nhubs) { return (nhubs + 63) / 64 + 1; }
+
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -482,6 +498,10 @@ struct UpdateArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
+  // hub marks (fused finish only): this level's (zero on entry), and the
+  // buffer the last workgroup zeroes
+  word_t* hub_mark = nullptr;
+  word_t* hub_mark_clear = nullptr;
   // several ranks, fused finish: the level's end in the last workgroup
   // (Comm::direct_level_end; no frontier gathered, or a pushed one); it runs
   // on a no-op chain too (a collective)
@@ -569,6 +589,9 @@ struct TdSparseArgs {
   word_t* hx_bits = nullptr;
   int64_t* hx_tot = nullptr;
   int64_t* hx_out = nullptr;
+  // hub marks (one rank; as UpdateArgs)
+  word_t* hub_mark = nullptr;
+  word_t* hub_mark_clear = nullptr;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -786,6 +809,12 @@ struct BuArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
+  // hub marks (one rank; as UpdateArgs): hub_front is then the previous
+  // level's marks, and with cut_from_marks bu_cut_prep decides the hub cut
+  // from their degree word (hub_gather's decision) and stores it in *cut_flag
+  word_t* hub_mark = nullptr;
+  word_t* hub_mark_clear = nullptr;
+  bool cut_from_marks = false;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the

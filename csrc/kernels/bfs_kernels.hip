@@ -121,6 +121,21 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? sbit : 0ull;
   if (a.frontier_clear)
     for (int64_t w = t0; w < a.words; w += stride) a.frontier_clear[w] = 0ull;
+  if (a.hub_mark_seed) {
+    // the seed's hub marks (the source, if a hub: its bit and degree), the
+    // other buffer zeroed
+    const int64_t hw = (a.g.nhubs + 63) / 64;
+    int64_t sh = -1;
+    uint32_t sd = 0;
+    if (src >= 0 && t0 <= hw) {
+      sd = static_cast<uint32_t>(a.g.row_off[src + 1] - a.g.row_off[src]);
+      if (sd >= a.g.hub_min_deg) sh = hub_index(a.g, a.g.lo + src);
+    }
+    for (int64_t i = t0; i <= hw; i += stride) {
+      a.hub_mark_zero[i] = 0ull;
+      a.hub_mark_seed[i] = sh < 0 ? 0ull : i == hw ? static_cast<word_t>(sd) : (sh >> 6) == i ? 1ull << (sh & 63) : 0ull;
+    }
+  }
   // the seed's work-list entry: edge blocks [0, ceil(d / EPB)) all start in it
   if (a.blk_vstart && src >= 0) {
     const eid_t d = a.g.row_off[src + 1] - a.g.row_off[src];
@@ -249,6 +264,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
     if (nb) a.visited[wl] = vis | nb;
     a.frontier[wl] = nb;
     if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, wl, nb);
+    if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + wl, nb);
     if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
   // New vertices of the unit, 64 per step (one per lane, whatever word they
@@ -434,6 +450,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   }
   c = wave_sum(c);
   d = wave_sum(d);
+  clear_hub_marks<kBlock>(a.hub_mark_clear, a.g.nhubs);
   __syncthreads();  // (s_c / s_d reused)
   if (lane_id() == 0) {
     s_c[wv] = c;
@@ -775,6 +792,8 @@ constexpr int64_t kSplitUnits = 4096;
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
+  DBFS_CHECK(!a.hub_mark || (a.fuse_scan && a.g.hub_bits && a.g.hub_deg && a.g.nhubs > 0),
+             "update: hub marks need the fused finish and the hub tables");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   const bool split = nunits < kSplitUnits;

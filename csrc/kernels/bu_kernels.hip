@@ -274,6 +274,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     if (lane < nw) {
       a.new_frontier[w0 + lane] = pw;
       if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, pw);
+      if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + w0 + lane, pw);
       if (pw) a.visited[w0 + lane] = ~um;  // (= visited | pw)
     }
     take_pre();
@@ -469,6 +470,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     const word_t res = s_res[lane] | pw;
     a.new_frontier[w0 + lane] = res;
     if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, res);
+    if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + w0 + lane, res);
     if (res) a.visited[w0 + lane] = ~um | res;  // (~um holds pw)
   }
   take_pre();
@@ -525,6 +527,8 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
   }
   __syncthreads();
   if (!s_last) return;
+  // (every workgroup staged the hub marks it read before its ticket)
+  clear_hub_marks<kThreads>(a.hub_mark_clear, a.g.nhubs);
   long long c = 0, d = 0;
   for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
     c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
@@ -580,7 +584,9 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   // a hub-cut level launches both variants; the decision picks one
   if (a.cut_flag && (*a.cut_flag != 0) != (kCut != 0)) return;
   constexpr bool cut = kCut != 0;
-  if (!a.hub_front) stamp_level_start(a.ctrl);
+  // (the level's first kernel stamps its start: hub_gather, or with hub marks
+  // this one -- bu_cut_prep on a hub-cut level)
+  if (!a.hub_front || (a.hub_mark && !a.cut_from_marks)) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
   __syncthreads();
@@ -796,7 +802,19 @@ constexpr int kCutThreads = 1024;
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
   const bool lists = a.nranks > 1;
   const bool dx = lists && a.cut_direct.active;
-  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) {
+  bool cut_on = !(a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B'));
+  if (cut_on && a.cut_from_marks) {
+    stamp_level_start(a.ctrl);
+    // (hub marks: the decision hub_gather makes otherwise, from the marks'
+    // degree word; every workgroup computes it, the first stores it for the
+    // bottom-up kernels)
+    const long long hub_edges = static_cast<long long>(a.hub_front[(a.g.nhubs + 63) / 64]);
+    cut_on = a.ctrl->m_f - hub_edges <= a.cut_edges;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.cut_flag = cut_on ? 1 : 0;
+  } else if (cut_on) {
+    cut_on = *a.cut_flag != 0;
+  }
+  if (!cut_on) {
     if (dx && blockIdx.x == 0) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, false);
     return;
   }
@@ -940,6 +958,9 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   } report{st};
 #endif
   if (a.words <= 0) return;
+  DBFS_CHECK(!a.hub_mark || (a.fuse_scan && a.hub_front && a.g.nhubs > 0 && a.g.hub_bits && a.g.hub_deg &&
+                             a.g.hub_min_deg > 0 && a.nranks == 1),
+             "bu_step: hub marks need the fused finish, one rank and the hub tables");
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
     // a whole 64-word unit per wave when the shard has enough units to fill
@@ -956,7 +977,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
     if (a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
-      DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the fused finish");
+      DBFS_CHECK(!a.end.active && !a.hub_mark_clear, "bu_step: a folded level end / hub marks need the fused finish");
       // (more workgroups than totals slots: finish in a kernel of its own)
       BuArgs b = a;
       b.fuse_scan = false;

@@ -151,6 +151,41 @@ __device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Hub marks (backend.hpp hub_mark_words): the hubs among a new frontier word
+// `bits` (global word gw) -- their bits, by binary search of g.hub_vertex, and
+// their degrees into the marks' last word.  Per lane.
+__device__ __forceinline__ int64_t hub_index(const ShardView& g, int64_t v) {
+  int64_t lo = 0, hi = g.nhubs;  // first index with hub_vertex >= v
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (static_cast<int64_t>(g.hub_vertex[mid]) < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ void mark_hub(const ShardView& g, word_t* marks, int64_t v, uint32_t deg) {
+  const int64_t h = hub_index(g, v);
+  DBFS_DCHECK(h < g.nhubs && g.hub_vertex[h] == v, 15, v);
+  atomicOr(reinterpret_cast<unsigned long long*>(marks + (h >> 6)), 1ull << (h & 63));
+  atomicAdd(reinterpret_cast<unsigned long long*>(marks + (g.nhubs + 63) / 64), static_cast<unsigned long long>(deg));
+}
+__device__ __forceinline__ void mark_hub_word(const ShardView& g, word_t* marks, int64_t gw, word_t bits) {
+  for (word_t m = bits ? bits & g.hub_bits[gw] : 0ull; m; m &= m - 1) {
+    const int64_t v = gw * 64 + __builtin_ctzll(m);
+    const int64_t h = hub_index(g, v);
+    DBFS_DCHECK(h < g.nhubs && g.hub_vertex[h] == v, 15, v);
+    atomicOr(reinterpret_cast<unsigned long long*>(marks + (h >> 6)), 1ull << (h & 63));
+    atomicAdd(reinterpret_cast<unsigned long long*>(marks + (g.nhubs + 63) / 64),
+              static_cast<unsigned long long>(g.hub_deg[h]));
+  }
+}
+// the other buffer zeroed by the level's last workgroup (every thread calls)
+template <int kThreads>
+__device__ __forceinline__ void clear_hub_marks(word_t* marks, int64_t nhubs) {
+  if (!marks) return;
+  for (int64_t i = threadIdx.x; i < hub_mark_words(nhubs); i += kThreads) marks[i] = 0ull;
+}
+
 // Frontier push (backend.hpp FrontierTable): word w of this rank's slice to
 // every peer's window, write-through.
 __device__ __forceinline__ void push_frontier_word(const FrontierTable* t, int rank, int nranks, int64_t w,

@@ -392,6 +392,12 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
       re[k] = ro[r + 1];
     }
   }
+  if (a.hub_mark) {
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+      if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.hub_min_deg))
+        mark_hub(a.g, a.hub_mark, v[k], static_cast<uint32_t>(re[k] - rs[k]));
+  }
   if (a.hx_bits) hx_divert<kItems>(a, v, claimed, rs, re);
   unsigned long long tm[kItems];
   long long incl[kItems], cbase[kItems], ebase[kItems];
@@ -772,7 +778,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     if (s_last) last_arriver_acquire();
   }
   __syncthreads();
-  if (!s_last || t != 0) return;
+  if (!s_last) return;
+  clear_hub_marks<kThreads>(a.hub_mark_clear, a.g.nhubs);
+  if (t != 0) return;
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
   LevelCtrl c = *a.ctrl;
@@ -921,6 +929,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
     if (dx && a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);
     return;
   }
+  clear_hub_marks<kBlock>(a.hub_mark_clear, a.g.nhubs);
   if (t != 0) return;
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
@@ -1264,6 +1273,8 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
+  DBFS_CHECK(!a.hub_mark || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0),
+             "td_sparse: hub marks are one-rank and need the hub tables");
   if (a.from_bits) {
     // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
     // wave (RMAT-26, one rank: 1024 workgroups, 16 groups on the ticket)
