@@ -114,6 +114,7 @@ class CpuBackend final : public Backend {
         a.visited[w] |= nb;
         a.frontier[w] = nb;
         if (a.hub_mark) mark_hubs(a.g, a.hub_mark, (a.g.lo >> 6) + w, nb);
+        for (int p = 0; p < a.zero_slices; ++p) a.zero_next[p * a.words + w] = 0;
         word_t x = nb;
         while (x) {
           const int b = __builtin_ctzll(x);

@@ -812,7 +812,10 @@ void DeviceLoop::emit_dense(Chain& c) {
       be_.pack_bytes(pa);
     }
     comm_.alltoall(e_.next_.data(), e_.recv_.data(), static_cast<size_t>(W_) * sizeof(word_t));
-    be_.memset_async(e_.next_.data(), 0, e_.next_.bytes());
+    // (`next` re-zeroed by the update, which runs after the exchange: on a
+    // no-op chain nothing wrote it)
+    tu.zero_next = e_.next_.data();
+    tu.zero_slices = P_;
     tu.cand = e_.recv_.data();
     tu.cand_bytes = nullptr;
   }

@@ -502,6 +502,11 @@ struct UpdateArgs {
   // buffer the last workgroup zeroes
   word_t* hub_mark = nullptr;
   word_t* hub_mark_clear = nullptr;
+  // several ranks: the send buffer of the candidates' all-to-all (zero_slices
+  // slices of `words` words) zeroed here -- word w of every slice by the lane
+  // of w -- instead of a memset launch after the exchange
+  word_t* zero_next = nullptr;
+  int zero_slices = 0;
   // several ranks, fused finish: the level's end in the last workgroup
   // (Comm::direct_level_end; no frontier gathered, or a pushed one); it runs
   // on a no-op chain too (a collective)

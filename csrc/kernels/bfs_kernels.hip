@@ -265,6 +265,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
     a.frontier[wl] = nb;
     if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, wl, nb);
     if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + wl, nb);
+    for (int p = 0; p < a.zero_slices; ++p) a.zero_next[p * a.words + wl] = 0ull;
     if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
   // New vertices of the unit, 64 per step (one per lane, whatever word they
