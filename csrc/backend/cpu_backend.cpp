@@ -830,6 +830,8 @@ class CpuBackend final : public Backend {
       }
   }
   void bu_cut_apply(const BuArgs& a) override {
+    DBFS_CHECK(a.nranks > 1 && a.cut_lists && a.cut_flag && a.cut_recv_lists,
+               "bu_cut_apply: several ranks' hub-cut arguments missing");
     for (int p = 0; p < a.nranks; ++p) a.cut_lists[static_cast<int64_t>(p) * a.cut_list_stride] = 0;
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     if (!*a.cut_flag) return;

@@ -509,7 +509,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     case 'T': emit_dense(c); break;
     default: emit_bottom_up(c); break;
   }
-  res_.chains.back().cut = c.cut;
+  res_.chains.back().cut = c.cut && P_ > 1;  // (the owner-list exchange)
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
   enq_fused_[L] = c.fused_scan && d != 'S';
   if (xc_ && !c.level_ended)
@@ -945,8 +945,11 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         }
         ba.cut_claim = e_.cut_claim_.data();
       }
-      if (!xc_) {
+      if (P_ == 1) {
+        // (one rank -- with a forced exchange too: nothing to send; the flag
+        // keeps the level end out of the plain kernel, which may not run)
         be_.bu_cut_prep(ba);
+        c.cut = xc_;
       } else {
         // several ranks: own claims in place, remote ones as owner lists
         // (straight into the owners' windows with a direct exchange), then

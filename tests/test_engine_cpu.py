@@ -160,12 +160,17 @@ def test_parent_tree_virtual_ranks():
         assert parents_are_valid(csr, lv, par, 1)
 
 
+@pytest.mark.parametrize("cut", [0, 1])
 @pytest.mark.parametrize("mode", MODES)
-def test_force_exchange_single_rank(rt, mode):
+def test_force_exchange_single_rank(rt, mode, cut):
     # the multi-rank exchange path (alltoall / allgather / alltoallv) with P = 1
+    # (cut: hub-cut bottom-up levels forced -- the one-rank cut, no owner lists)
     p = dbfs.rmat_params(10, 16, 17)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, rt, mode=mode, force_exchange=True)
+    if cut:
+        bfs.engine.set_option("bu_cut_edges", 1 << 40)
+        bfs.engine.set_option("bu_cut_mf_frac", 1.0)
     for src in bfs.sample_roots(2, seed=3):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), _oracle(csr, src))
