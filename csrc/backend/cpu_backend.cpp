@@ -65,12 +65,20 @@ class CpuBackend final : public Backend {
   // hub marks (backend.hpp hub_mark_words): the hubs among a new frontier word
   static void mark_hubs(const ShardView& g, word_t* marks, int64_t gw, word_t bits) {
     for (word_t m = bits & g.hub_bits[gw]; m; m &= m - 1) {
-      const vid_t v = static_cast<vid_t>(gw * 64 + __builtin_ctzll(m));
+      const int b = __builtin_ctzll(m);
+      const vid_t v = static_cast<vid_t>(gw * 64 + b);
       const int64_t h = std::lower_bound(g.hub_vertex, g.hub_vertex + g.nhubs, v) - g.hub_vertex;
       DBFS_CHECK(h < g.nhubs && g.hub_vertex[h] == v, "hub marks: a hub bit without a hub");
+      DBFS_CHECK(h == g.hub_pref[gw] + __builtin_popcountll(g.hub_bits[gw] & ((1ull << b) - 1ull)),
+                 "hub marks: the hub prefix disagrees with hub_vertex");
       marks[h >> 6] |= 1ull << (h & 63);
-      marks[div_up(g.nhubs, 64)] += g.hub_deg[h];
+      marks[hub_mark_bits_words(g.nhubs) + ((gw >> 6) & (kHubMarkSlots - 1)) * kHubMarkSlotWords] += g.hub_deg[h];
     }
+  }
+  static uint64_t mark_edges(const ShardView& g, const word_t* marks) {
+    uint64_t s = 0;
+    for (int k = 0; k < kHubMarkSlots; ++k) s += marks[hub_mark_bits_words(g.nhubs) + k * kHubMarkSlotWords];
+    return s;
   }
   static void clear_marks(const ShardView& g, word_t* marks) {
     if (marks) std::fill(marks, marks + hub_mark_words(g.nhubs), 0ull);
@@ -90,7 +98,6 @@ class CpuBackend final : public Backend {
       if (!a.ctrl || chain_live(*a.ctrl, 'T', a.max_mf)) clear_marks(a.g, a.hub_mark_clear);
       return;
     }
-    DBFS_CHECK(!a.hub_mark_clear || a.hub_mark, "update: hub marks need the fused finish");
     bool use_bytes = a.cand_bytes != nullptr;
     if (a.ctrl) {
       if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
@@ -512,8 +519,7 @@ class CpuBackend final : public Backend {
       return;
     }
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-    DBFS_CHECK(!a.hub_mark_clear || a.hub_mark, "bottom-up: hub marks need the fused finish");
-    if (a.hub_mark) {
+    if (a.hub_front && a.hub_front_marks) {
       // the previous level's marks (hub_front) must be exactly its frontier
       // hubs, their degree word the hubs' degree sum (what hub_gather computes)
       uint64_t hd = 0;
@@ -522,7 +528,7 @@ class CpuBackend final : public Backend {
         DBFS_CHECK(f == (((a.hub_front[h >> 6] >> (h & 63)) & 1ull) != 0), "hub marks differ from the frontier hubs");
         if (f) hd += a.g.hub_deg[h];
       }
-      DBFS_CHECK(a.hub_front[div_up(a.g.nhubs, 64)] == hd, "hub marks: degree word differs");
+      DBFS_CHECK(mark_edges(a.g, a.hub_front) == hd, "hub marks: degree slots differ");
     }
     // hub-cut level (as the HIP kernel): claimed vertices join the output
     // unscanned, the others find parents among the frontier hubs only
@@ -805,7 +811,7 @@ class CpuBackend final : public Backend {
     DBFS_CHECK(!a.cut_direct.active, "CpuBackend: no direct list exchange");
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     if (a.cut_from_marks)
-      *a.cut_flag = a.ctrl->m_f - static_cast<int64_t>(a.hub_front[div_up(a.g.nhubs, 64)]) <= a.cut_edges ? 1 : 0;
+      *a.cut_flag = a.ctrl->m_f - static_cast<int64_t>(mark_edges(a.g, a.hub_front)) <= a.cut_edges ? 1 : 0;
     if (!*a.cut_flag) return;
     const int64_t lo = a.g.lo;
     for (int64_t w = 0; w < a.words; ++w)

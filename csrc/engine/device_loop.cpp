@@ -50,6 +50,9 @@ class DeviceLoop {
     // slices (the previous chain's table) for hub_gather to copy in
     const FrontierTable* push = nullptr;
     const FrontierTable* pull = nullptr;
+    // one rank, hub marks: this chain marks its output's hubs (a bottom-up
+    // level is predicted next)
+    bool mark = false;
   };
 
   Engine& e_;
@@ -87,6 +90,7 @@ class DeviceLoop {
   // ---- per-level records of what was enqueued ----
   std::vector<char> enq_dir_, enq_form_, enq_gather_, enq_fused_;
   std::vector<const FrontierTable*> enq_push_;  // level L's output pushed (Chain::push)
+  std::vector<char> enq_mark_;                  // level L's output hubs marked (Chain::mark)
   std::vector<int64_t> enq_cap_;
   std::vector<std::pair<int, int>> evs_;
   RunResult res_;
@@ -173,6 +177,7 @@ void DeviceLoop::setup() {
   direct_ = !xc_ && e_.run_narrow_ && opt_.td_direct;
   // (the marks' buffers are cleared by the chains' fused finishes)
   marks_ = !xc_ && opt_.bu_hub_marks && gv_.nhubs > 0 && gv_.hub_min_deg > 0 && gv_.hub_bits && gv_.hub_deg &&
+           gv_.hub_pref &&
            opt_.td_fused_finish && opt_.bu_fused_scan;
   if (marks_ && !e_.hub_marks_.data())
     e_.hub_marks_ = DBuf<word_t>(be_, static_cast<size_t>(2 * hub_mark_words(gv_.nhubs)));
@@ -461,6 +466,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     enq_gather_.resize(static_cast<size_t>(L) + 1);
     enq_fused_.resize(static_cast<size_t>(L) + 1);
     enq_push_.resize(static_cast<size_t>(L) + 1);
+    enq_mark_.resize(static_cast<size_t>(L) + 1);
     evs_.resize(static_cast<size_t>(L) + 1, {-1, -1});
   }
   Chain c;
@@ -482,6 +488,8 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
                ? comm_.direct_frontier(static_cast<size_t>(W_), L & 1)
                : nullptr;
   enq_push_[L] = c.push;
+  c.mark = marks_ && gather;
+  enq_mark_[L] = c.mark;
   res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
   res_.chains.back().push = c.push != nullptr;
   c.cap = enq_cap_[L];
@@ -597,7 +605,7 @@ void DeviceLoop::emit_sparse(Chain& c) {
   sp.first = !compacted || from_bits;
   sp.max_mf = c.cap;
   if (marks_) {
-    sp.hub_mark = marks(L);
+    sp.hub_mark = c.mark ? marks(L) : nullptr;
     sp.hub_mark_clear = marks(L + 1);
   }
   if (from_bits) {
@@ -707,7 +715,7 @@ void DeviceLoop::emit_binned(Chain& c) {
   if (marks_) {
     // (hub marks: the fused finish clears the other buffer)
     fuse_update(c, tu);
-    tu.hub_mark = marks(L);
+    tu.hub_mark = c.mark ? marks(L) : nullptr;
     tu.hub_mark_clear = marks(L + 1);
   }
   be_.update_frontier(tu);
@@ -775,7 +783,6 @@ void DeviceLoop::emit_dense(Chain& c) {
     ta.level_direct = e_.level8_.data();
     ta.narrow_base = e_.narrow_base_;
     ta.new_level = L + 1;
-    ta.store_mode = opt_.td_store_mode;
     tu.level_direct = e_.level8_.data();
     tu.narrow_base = e_.narrow_base_;
     if (ta.td_hub_vis && opt_.td_hub_mark) {
@@ -827,7 +834,7 @@ void DeviceLoop::emit_dense(Chain& c) {
   tu.push_rank = me_;
   tu.push_nranks = P_;
   if (marks_) {
-    tu.hub_mark = marks(L);
+    tu.hub_mark = c.mark ? marks(L) : nullptr;
     tu.hub_mark_clear = marks(L + 1);
   }
   if (opt_.td_fused_finish) {
@@ -873,7 +880,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.push_rank = me_;
   ba.push_nranks = P_;
   if (marks_) {
-    ba.hub_mark = marks(L);
+    ba.hub_mark = c.mark ? marks(L) : nullptr;
     ba.hub_mark_clear = marks(L + 1);
   }
   if (gv_.nhubs > 0) {
@@ -925,10 +932,11 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.cut_flag = e_.cut_flag_.data();
       hg.cut_ticket = e_.cut_ticket_.data();
     }
-    if (marks_) {
-      // the previous chain marked the frontier hubs (its buffer); bu_cut_prep
-      // decides a hub cut from their degree word
+    if (marks_ && (L == 0 || enq_mark_[static_cast<size_t>(L - 1)])) {
+      // the previous chain (or the seed) marked the frontier hubs in its
+      // buffer; bu_cut_prep decides a hub cut from their degree slots
       ba.hub_front = marks(L + 1);
+      ba.hub_front_marks = true;
       ba.cut_from_marks = cut;
     } else {
       be_.hub_gather(hg);

@@ -81,7 +81,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
-  else if (name == "td_store_mode") o.td_store_mode = static_cast<int>(v);
   else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
   else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
@@ -135,7 +134,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
-          {"td_store_mode", static_cast<double>(o.td_store_mode)},
           {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
           {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
@@ -324,6 +322,7 @@ ShardView DeviceGraph::view() const {
   v.hub_bits = hub_bits_.data();
   v.hub_deg = hub_deg_.data();
   v.hub_min_deg = hub_min_deg_;
+  v.hub_pref = hub_pref_.data();
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -396,6 +395,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   hub_min_deg_ = 0;
   hub_vertex_.reset();
   hub_bits_.reset();
+  hub_pref_.reset();
   hub_deg_.reset();
   hub_col_.reset();
   td_col_.reset();
@@ -423,6 +423,15 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
         for (vid_t v : hv) bits[v >> 6] |= 1ull << (v & 63);
         hub_bits_ = DBuf<word_t>(*be_, bits.size());
         be_->to_device(hub_bits_.data(), bits.data(), bits.size() * sizeof(word_t));
+        // hubs before each word (a hub's index without a search: hub marks)
+        std::vector<uint32_t> pref(bits.size());
+        uint32_t run = 0;
+        for (size_t w = 0; w < bits.size(); ++w) {
+          pref[w] = run;
+          run += static_cast<uint32_t>(__builtin_popcountll(bits[w]));
+        }
+        hub_pref_ = DBuf<uint32_t>(*be_, pref.size());
+        be_->to_device(hub_pref_.data(), pref.data(), pref.size() * sizeof(uint32_t));
         // the hubs' degrees (several ranks: the hub-cut decision)
         std::vector<uint32_t> hd(hv.size());
         for (size_t i = 0; i < hv.size(); ++i) hd[i] = deg[hv[i]];

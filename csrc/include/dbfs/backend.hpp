@@ -52,6 +52,9 @@ struct ShardView {
   int64_t nhubs = 0;
   // a vertex is a hub iff its degree (row length) >= hub_min_deg (> 0 with hubs)
   uint32_t hub_min_deg = 0;
+  // hubs in the global words before word w (one rank with hubs: a hub's index
+  // is hub_pref[v >> 6] + its rank among the hub bits of its word)
+  const uint32_t* hub_pref = nullptr;
   // Hub-encoded copy of col (same layout; hub neighbours as kHubFlag | index),
   // read by bottom-up so that probes of hub neighbours hit LDS too.
   const vid_t* hub_col = nullptr;
@@ -440,15 +443,20 @@ struct DirectExchange {
 };
 
 // Hub marks (one rank, EngineOptions::bu_hub_marks): the kernels that settle
-// a level's vertices also set the bits a bottom-up level stages for the
-// frontier hubs (hub_gather's hub_front: bit h for hub_vertex[h]) and add the
-// hubs' degrees into the last word (the hub-cut decision) -- no hub_gather
-// launch before a bottom-up level.  Two buffers by the producing chain's
+// a level predicted to feed a bottom-up one also set the bits that level
+// stages for its frontier hubs (hub_gather's hub_front: bit h for
+// hub_vertex[h]) and add the hubs' degrees into kHubMarkSlots slots after
+// the bits (128 B apart; their sum: the hub-cut decision) -- no hub_gather
+// launch before the bottom-up level.  Two buffers by the producing chain's
 // parity: the chain of level L marks buffer L & 1 (zero on entry: hub_mark)
 // and its last workgroup zeroes buffer (L + 1) & 1 (hub_mark_clear) -- the
 // one it read, if bottom-up -- so the next chain finds its buffer clean; the
 // run's initialisation writes the seed's marks and zeroes the other buffer.
-constexpr int64_t hub_mark_words(int64_t nhubs) { return (nhubs + 63) / 64 + 1; }
+constexpr int kHubMarkSlots = 32, kHubMarkSlotWords = 16;
+constexpr int64_t hub_mark_bits_words(int64_t nhubs) { return (nhubs + 63) / 64; }
+constexpr int64_t hub_mark_words(int64_t nhubs) {
+  return hub_mark_bits_words(nhubs) + int64_t(kHubMarkSlots) * kHubMarkSlotWords;
+}
 
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
@@ -669,10 +677,6 @@ struct TdArgs {
   uint8_t* level_direct = nullptr;
   lvl_t new_level = 0;
   uint8_t narrow_base = 0;  // (level_direct stores narrow_base + new_level)
-  // How those level bytes are stored (EngineOptions::td_store_mode): 0 plain
-  // (write-back L2), 1 write-through (sc1: the line leaves the XCD's L2),
-  // 2 non-temporal.
-  int store_mode = 0;
   // Levels of at least td_hub_min_edges frontier edges read g.td_col and test
   // hub targets in an LDS copy of td_hub_vis (visited bits of the top-down
   // hubs, this level's snapshot: hub_visited); not with owner lists.
@@ -814,11 +818,13 @@ struct BuArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
-  // hub marks (one rank; as UpdateArgs): hub_front is then the previous
-  // level's marks, and with cut_from_marks bu_cut_prep decides the hub cut
-  // from their degree word (hub_gather's decision) and stores it in *cut_flag
+  // hub marks (one rank; as UpdateArgs).  hub_front_marks: hub_front is the
+  // previous chain's marks (no hub_gather ran), and with cut_from_marks
+  // bu_cut_prep decides the hub cut from their degree slots (hub_gather's
+  // decision) and stores it in *cut_flag
   word_t* hub_mark = nullptr;
   word_t* hub_mark_clear = nullptr;
+  bool hub_front_marks = false;
   bool cut_from_marks = false;
 };
 

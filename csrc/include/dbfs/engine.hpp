@@ -107,6 +107,7 @@ class DeviceGraph {
   DBuf<eid_t> hx_off_;
   uint32_t td_hub_min_deg_ = 0;
   uint32_t hub_min_deg_ = 0;  // (ShardView::hub_min_deg)
+  DBuf<uint32_t> hub_pref_;   // (ShardView::hub_pref)
   DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
   void build_hub_split();
   int64_t hx_total() const;
@@ -182,9 +183,6 @@ struct EngineOptions {
   // L2-resident 128 KiB array) and turned into level bytes after the
   // expansion (TdArgs::td_hub_mark, hub_apply).
   bool td_hub_mark = true;
-  // Direct-level top-down: how the level bytes are stored (TdArgs::store_mode;
-  // 0 plain, 1 write-through, 2 non-temporal)
-  int td_store_mode = 0;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.
   double td_check_visited_min = 0.02;

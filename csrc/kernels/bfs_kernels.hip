@@ -124,14 +124,19 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   if (a.hub_mark_seed) {
     // the seed's hub marks (the source, if a hub: its bit and degree), the
     // other buffer zeroed
-    const int64_t hw = (a.g.nhubs + 63) / 64;
+    // (slot 0 holds the seed's degree: only the slots' sum is read)
+    const int64_t hw = hub_mark_bits_words(a.g.nhubs), n = hub_mark_words(a.g.nhubs);
     int64_t sh = -1;
     uint32_t sd = 0;
-    if (src >= 0 && t0 <= hw) {
-      sd = static_cast<uint32_t>(a.g.row_off[src + 1] - a.g.row_off[src]);
-      if (sd >= a.g.hub_min_deg) sh = hub_index(a.g, a.g.lo + src);
+    if (src >= 0 && t0 < n) {
+      const int64_t v = a.g.lo + src;
+      const word_t hb = a.g.hub_bits[v >> 6];
+      if ((hb >> (v & 63)) & 1ull) {
+        sh = a.g.hub_pref[v >> 6] + __popcll(hb & ((1ull << (v & 63)) - 1ull));
+        sd = a.g.hub_deg[sh];
+      }
     }
-    for (int64_t i = t0; i <= hw; i += stride) {
+    for (int64_t i = t0; i < n; i += stride) {
       a.hub_mark_zero[i] = 0ull;
       a.hub_mark_seed[i] = sh < 0 ? 0ull : i == hw ? static_cast<word_t>(sd) : (sh >> 6) == i ? 1ull << (sh & 63) : 0ull;
     }
@@ -778,6 +783,8 @@ void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
 
 void init_run(const InitRunArgs& a, hipStream_t st) {
+  DBFS_CHECK(!a.hub_mark_seed || (a.hub_mark_zero && a.g.hub_pref && a.g.hub_bits && a.g.hub_deg),
+             "init_run: the seed's hub marks need the hub tables");
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
   init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
 }
@@ -793,7 +800,7 @@ constexpr int64_t kSplitUnits = 4096;
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
-  DBFS_CHECK(!a.hub_mark || (a.fuse_scan && a.g.hub_bits && a.g.hub_deg && a.g.nhubs > 0),
+  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear) || (a.fuse_scan && a.g.hub_bits && a.g.hub_deg && a.g.hub_pref && a.g.nhubs > 0),
              "update: hub marks need the fused finish and the hub tables");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;

@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   constexpr bool cut = kCut != 0;
   // (the level's first kernel stamps its start: hub_gather, or with hub marks
   // this one -- bu_cut_prep on a hub-cut level)
-  if (!a.hub_front || (a.hub_mark && !a.cut_from_marks)) stamp_level_start(a.ctrl);
+  if (!a.hub_front || (a.hub_front_marks && !a.cut_from_marks)) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
   __syncthreads();
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
     // (hub marks: the decision hub_gather makes otherwise, from the marks'
     // degree word; every workgroup computes it, the first stores it for the
     // bottom-up kernels)
-    const long long hub_edges = static_cast<long long>(a.hub_front[(a.g.nhubs + 63) / 64]);
+    const long long hub_edges = hub_mark_edges(a.g, a.hub_front);
     cut_on = a.ctrl->m_f - hub_edges <= a.cut_edges;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.cut_flag = cut_on ? 1 : 0;
   } else if (cut_on) {
@@ -958,8 +958,9 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   } report{st};
 #endif
   if (a.words <= 0) return;
-  DBFS_CHECK(!a.hub_mark || (a.fuse_scan && a.hub_front && a.g.nhubs > 0 && a.g.hub_bits && a.g.hub_deg &&
-                             a.g.hub_min_deg > 0 && a.nranks == 1),
+  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear && !a.hub_front_marks) ||
+                 (a.fuse_scan && a.hub_front && a.g.nhubs > 0 && a.g.hub_bits && a.g.hub_deg && a.g.hub_pref &&
+                  a.g.hub_min_deg > 0 && a.nranks == 1),
              "bu_step: hub marks need the fused finish, one rank and the hub tables");
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;

@@ -263,6 +263,9 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         // 55.3 with claims in `next`; the 43 M-edge level stores 29.8 M level
         // bytes for ~2 M new vertices, and removing the repeats with extra
         // reads costs more L2 requests than the writes, tools/gpu_td_stats_roots.sh).
+        // Plain stores: write-through (sc1) or non-temporal ones measured slower,
+        // RMAT-22 88.4 -> 74.8 / 69.3 GTEPS, LJ-sized 56.7 -> 51.4 / 52.0
+        // (profiles/r4_s2_td_store_modes.txt).
         const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
         bool keep[kItems];
 #pragma unroll
@@ -272,14 +275,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
         for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-          if (keep[k]) {
-            if (a.store_mode == 1)
-              __hip_atomic_store(a.level_direct + vk[k], lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else if (a.store_mode == 2)
-              __builtin_nontemporal_store(lv, a.level_direct + vk[k]);
-            else
-              a.level_direct[vk[k]] = lv;
-          }
+          if (keep[k]) a.level_direct[vk[k]] = lv;
         continue;
       }
       // byte map: with few visited vertices the check costs more than the
@@ -396,7 +392,7 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
 #pragma unroll
     for (int k = 0; k < kItems; ++k)
       if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.hub_min_deg))
-        mark_hub(a.g, a.hub_mark, v[k], static_cast<uint32_t>(re[k] - rs[k]));
+        mark_hub_word(a.g, a.hub_mark, v[k] >> 6, 1ull << (v[k] & 63));
   }
   if (a.hx_bits) hx_divert<kItems>(a, v, claimed, rs, re);
   unsigned long long tm[kItems];
@@ -1273,7 +1269,7 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
-  DBFS_CHECK(!a.hub_mark || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0),
+  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear) || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0 && a.g.hub_pref),
              "td_sparse: hub marks are one-rank and need the hub tables");
   if (a.from_bits) {
     // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
