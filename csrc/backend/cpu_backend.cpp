@@ -95,7 +95,6 @@ class CpuBackend final : public Backend {
       scan_units(a.scan);
       std::copy(c.begin(), c.end(), a.scan.unit_cnt);
       std::copy(d.begin(), d.end(), a.scan.unit_deg);
-      if (!a.ctrl || chain_live(*a.ctrl, 'T', a.max_mf)) clear_marks(a.g, a.hub_mark_clear);
       return;
     }
     bool use_bytes = a.cand_bytes != nullptr;
@@ -167,7 +166,6 @@ class CpuBackend final : public Backend {
     if (a.frontier_clear)
       for (int64_t w = 0; w < a.words; ++w) a.frontier_clear[w] = 0;
     if (a.hub_mark_seed) {
-      clear_marks(a.g, a.hub_mark_zero);
       clear_marks(a.g, a.hub_mark_seed);
       if (src >= 0) mark_hubs(a.g, a.hub_mark_seed, (a.g.lo + src) >> 6, 1ull << (src & 63));
     }
@@ -449,7 +447,6 @@ class CpuBackend final : public Backend {
       }
     }
     if (a.lists) return;  // several ranks: td_sparse_apply finishes
-    clear_marks(a.g, a.hub_mark_clear);
     sparse_finish_totals(a);
     level_ctrl_finish(*a.ctrl, sparse_cnt_, sparse_deg_, false, a.rec);
     if (a.mailbox) {
@@ -515,10 +512,10 @@ class CpuBackend final : public Backend {
       scan_units(a.scan);
       std::copy(c.begin(), c.end(), a.scan.unit_cnt);
       std::copy(d.begin(), d.end(), a.scan.unit_deg);
-      if (!a.ctrl || !(a.ctrl->done || a.ctrl->dir != 'B')) clear_marks(a.g, a.hub_mark_clear);
       return;
     }
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    DBFS_CHECK(!a.hub_mark, "bottom-up: bottom-up levels mark no hubs");
     if (a.hub_front && a.hub_front_marks) {
       // the previous level's marks (hub_front) must be exactly its frontier
       // hubs, their degree word the hubs' degree sum (what hub_gather computes)
@@ -576,7 +573,6 @@ class CpuBackend final : public Backend {
         }
         a.visited[w] = vis | out;
         a.new_frontier[w] = out;
-        if (a.hub_mark) mark_hubs(a.g, a.hub_mark, (a.g.lo >> 6) + w, out);
       }
       a.unit_cnt[u] = cnt;
       a.unit_deg[u] = deg;

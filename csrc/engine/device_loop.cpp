@@ -488,8 +488,10 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
                ? comm_.direct_frontier(static_cast<size_t>(W_), L & 1)
                : nullptr;
   enq_push_[L] = c.push;
-  c.mark = marks_ && gather;
+  c.mark = marks_ && gather && d != 'B';
   enq_mark_[L] = c.mark;
+  // (its buffer zeroed first: a small fill, ahead of the chain's kernels)
+  if (c.mark) be_.memset_async(marks(L), 0, static_cast<size_t>(hub_mark_words(gv_.nhubs)) * sizeof(word_t));
   res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
   res_.chains.back().push = c.push != nullptr;
   c.cap = enq_cap_[L];
@@ -606,7 +608,6 @@ void DeviceLoop::emit_sparse(Chain& c) {
   sp.max_mf = c.cap;
   if (marks_) {
     sp.hub_mark = c.mark ? marks(L) : nullptr;
-    sp.hub_mark_clear = marks(L + 1);
   }
   if (from_bits) {
     sp.from_bits = true;
@@ -712,12 +713,7 @@ void DeviceLoop::emit_binned(Chain& c) {
   tu.frontier = fr_own(c.cur ^ 1);
   tu.new_level = L + 1;
   tu.ctrl = e_.ctrl_.data();
-  if (marks_) {
-    // (hub marks: the fused finish clears the other buffer)
-    fuse_update(c, tu);
-    tu.hub_mark = c.mark ? marks(L) : nullptr;
-    tu.hub_mark_clear = marks(L + 1);
-  }
+  if (marks_) tu.hub_mark = c.mark ? marks(L) : nullptr;
   be_.update_frontier(tu);
 }
 
@@ -833,10 +829,7 @@ void DeviceLoop::emit_dense(Chain& c) {
   tu.push = c.push;
   tu.push_rank = me_;
   tu.push_nranks = P_;
-  if (marks_) {
-    tu.hub_mark = c.mark ? marks(L) : nullptr;
-    tu.hub_mark_clear = marks(L + 1);
-  }
+  if (marks_) tu.hub_mark = c.mark ? marks(L) : nullptr;
   if (opt_.td_fused_finish) {
     // totals (and with one rank the decision) in the update's last
     // workgroup (as bottom-up)
@@ -879,10 +872,6 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.push = c.push;
   ba.push_rank = me_;
   ba.push_nranks = P_;
-  if (marks_) {
-    ba.hub_mark = c.mark ? marks(L) : nullptr;
-    ba.hub_mark_clear = marks(L + 1);
-  }
   if (gv_.nhubs > 0) {
     HubGatherArgs hg;
     hg.g = gv_;
@@ -1057,7 +1046,6 @@ RunResult DeviceLoop::run() {
   if (marks_) {
     // (the seed is the output of "chain -1": parity 1)
     ia.hub_mark_seed = marks(1);
-    ia.hub_mark_zero = marks(0);
   }
   be_.init_run(ia);
   // the seed's frontier is gathered with its totals when level 0 is bottom-up

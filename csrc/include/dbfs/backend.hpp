@@ -260,9 +260,8 @@ struct InitRunArgs {
   int32_t* blk_vstart = nullptr;
   vid_t* qv = nullptr;
   word_t* frontier_clear = nullptr;
-  // hub marks: the seed's written (hub_mark_seed), the other buffer zeroed
+  // hub marks: the seed's written (every word of the buffer)
   word_t* hub_mark_seed = nullptr;
-  word_t* hub_mark_zero = nullptr;
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;
@@ -443,15 +442,13 @@ struct DirectExchange {
 };
 
 // Hub marks (one rank, EngineOptions::bu_hub_marks): the kernels that settle
-// a level predicted to feed a bottom-up one also set the bits that level
-// stages for its frontier hubs (hub_gather's hub_front: bit h for
-// hub_vertex[h]) and add the hubs' degrees into kHubMarkSlots slots after
-// the bits (128 B apart; their sum: the hub-cut decision) -- no hub_gather
-// launch before the bottom-up level.  Two buffers by the producing chain's
-// parity: the chain of level L marks buffer L & 1 (zero on entry: hub_mark)
-// and its last workgroup zeroes buffer (L + 1) & 1 (hub_mark_clear) -- the
-// one it read, if bottom-up -- so the next chain finds its buffer clean; the
-// run's initialisation writes the seed's marks and zeroes the other buffer.
+// a (top-down) level predicted to feed a bottom-up one also set the bits that
+// level stages for its frontier hubs (hub_gather's hub_front: bit h for
+// hub_vertex[h]) and add the hubs' degrees into kHubMarkSlots slots after the
+// bits (128 B apart; their sum: the hub-cut decision) -- no hub_gather launch
+// before the bottom-up level.  Two buffers by the producing chain's parity:
+// a marking chain of level L fills buffer L & 1 with zeros ahead of its
+// kernels; the run's initialisation writes the seed's marks into buffer 1.
 constexpr int kHubMarkSlots = 32, kHubMarkSlotWords = 16;
 constexpr int64_t hub_mark_bits_words(int64_t nhubs) { return (nhubs + 63) / 64; }
 constexpr int64_t hub_mark_words(int64_t nhubs) {
@@ -506,10 +503,8 @@ struct UpdateArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
-  // hub marks (fused finish only): this level's (zero on entry), and the
-  // buffer the last workgroup zeroes
+  // hub marks: this level's (zero on entry)
   word_t* hub_mark = nullptr;
-  word_t* hub_mark_clear = nullptr;
   // several ranks: the send buffer of the candidates' all-to-all (zero_slices
   // slices of `words` words) zeroed here -- word w of every slice by the lane
   // of w -- instead of a memset launch after the exchange
@@ -604,7 +599,6 @@ struct TdSparseArgs {
   int64_t* hx_out = nullptr;
   // hub marks (one rank; as UpdateArgs)
   word_t* hub_mark = nullptr;
-  word_t* hub_mark_clear = nullptr;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -818,12 +812,12 @@ struct BuArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
-  // hub marks (one rank; as UpdateArgs).  hub_front_marks: hub_front is the
+  // hub marks (one rank; as UpdateArgs, but a bottom-up level marks nothing:
+  // hub_mark stays null).  hub_front_marks: hub_front is the
   // previous chain's marks (no hub_gather ran), and with cut_from_marks
   // bu_cut_prep decides the hub cut from their degree slots (hub_gather's
   // decision) and stores it in *cut_flag
   word_t* hub_mark = nullptr;
-  word_t* hub_mark_clear = nullptr;
   bool hub_front_marks = false;
   bool cut_from_marks = false;
 };

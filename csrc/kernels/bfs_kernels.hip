@@ -137,7 +137,6 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
       }
     }
     for (int64_t i = t0; i < n; i += stride) {
-      a.hub_mark_zero[i] = 0ull;
       a.hub_mark_seed[i] = sh < 0 ? 0ull : i == hw ? static_cast<word_t>(sd) : (sh >> 6) == i ? 1ull << (sh & 63) : 0ull;
     }
   }
@@ -456,7 +455,6 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   }
   c = wave_sum(c);
   d = wave_sum(d);
-  clear_hub_marks<kBlock>(a.hub_mark_clear, a.g.nhubs);
   __syncthreads();  // (s_c / s_d reused)
   if (lane_id() == 0) {
     s_c[wv] = c;
@@ -783,7 +781,7 @@ void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
 
 void init_run(const InitRunArgs& a, hipStream_t st) {
-  DBFS_CHECK(!a.hub_mark_seed || (a.hub_mark_zero && a.g.hub_pref && a.g.hub_bits && a.g.hub_deg),
+  DBFS_CHECK(!a.hub_mark_seed || (a.g.hub_pref && a.g.hub_bits && a.g.hub_deg),
              "init_run: the seed's hub marks need the hub tables");
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
   init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
@@ -800,8 +798,8 @@ constexpr int64_t kSplitUnits = 4096;
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
-  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear) || (a.fuse_scan && a.g.hub_bits && a.g.hub_deg && a.g.hub_pref && a.g.nhubs > 0),
-             "update: hub marks need the fused finish and the hub tables");
+  DBFS_CHECK(!a.hub_mark || (a.g.hub_bits && a.g.hub_deg && a.g.hub_pref && a.g.nhubs > 0),
+             "update: hub marks need the hub tables");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   const bool split = nunits < kSplitUnits;

@@ -273,8 +273,6 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   if (total == 0) {
     if (lane < nw) {
       a.new_frontier[w0 + lane] = pw;
-      if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, pw);
-      if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + w0 + lane, pw);
       if (pw) a.visited[w0 + lane] = ~um;  // (= visited | pw)
     }
     take_pre();
@@ -469,8 +467,6 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
   if (lane < nw) {
     const word_t res = s_res[lane] | pw;
     a.new_frontier[w0 + lane] = res;
-    if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, res);
-    if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + w0 + lane, res);
     if (res) a.visited[w0 + lane] = ~um | res;  // (~um holds pw)
   }
   take_pre();
@@ -527,8 +523,6 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
   }
   __syncthreads();
   if (!s_last) return;
-  // (every workgroup staged the hub marks it read before its ticket)
-  clear_hub_marks<kThreads>(a.hub_mark_clear, a.g.nhubs);
   long long c = 0, d = 0;
   for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads) {
     c += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.tot + 2 * i),
@@ -560,13 +554,25 @@ __device__ __forceinline__ void bu_fused_finish(const BuArgs& a, long long wc, l
   }
 }
 
+// Pushed frontier words (BuArgs::push) of the words a wave wrote (w0 + lane,
+// lane < nw): a pass of their own after the units, re-reading each lane's own
+// stores, compiled only into the kPost variants -- inline in bu_wave_compact
+// (or in every variant) they cost the hot loop registers (2 VGPRs spilled).
+// Wave-uniform call.
+__device__ __forceinline__ void bu_post_words(const BuArgs& a, int64_t w0, int nw) {
+  const int lane = lane_id();
+  if (lane >= nw || w0 + lane >= a.words) return;
+  push_frontier_word(a.push, a.push_rank, a.push_nranks, w0 + lane, a.new_frontier[w0 + lane]);
+}
+
 // kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
 // code costs the one-rank kernels their spill-free 64 registers).
 // kCut: the hub-cut variant (one rank, first bottom-up level of a run of them),
 // kCutLevels (claims in the narrow level bytes) or kCutClaims (wide levels:
 // claims in BuArgs::cut_claim).
+// kPost: the output words pushed to the peers afterwards (BuArgs::push).
 template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false,
-          int kCut = 0>
+          int kCut = 0, bool kPost = false>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
@@ -618,10 +624,14 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
         s_d[wave] += deg;
       }
     }
+    if constexpr (kPost)
+      for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+           u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock)
+        bu_post_words(a, u * kUnitWords, kUnitWords);
     if (!a.fuse_scan) return;
     // (pushed words: every wave's write-through stores drained before the
     // ticket, so a level end published after it covers them)
-    if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (kPost) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     long long wc = 0, wd = 0;
     if (threadIdx.x == 0)
@@ -670,8 +680,11 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     }
     __syncthreads();
   }
+  if constexpr (kPost)
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride)
+      if (base + group < nunits) bu_post_words(a, (base + group) * kUnitWords + wg * kWaveWords, kWaveWords);
   if (!a.fuse_scan) return;
-  if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above)
+  if constexpr (kPost) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above)
   __syncthreads();  // (an empty loop: the accumulators' zeroing)
   long long wc = 0, wd = 0;
   if (threadIdx.x == 0)
@@ -958,10 +971,12 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   } report{st};
 #endif
   if (a.words <= 0) return;
-  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear && !a.hub_front_marks) ||
+  DBFS_CHECK((!a.hub_mark && !a.hub_front_marks) ||
                  (a.fuse_scan && a.hub_front && a.g.nhubs > 0 && a.g.hub_bits && a.g.hub_deg && a.g.hub_pref &&
                   a.g.hub_min_deg > 0 && a.nranks == 1),
              "bu_step: hub marks need the fused finish, one rank and the hub tables");
+  DBFS_CHECK(((a.g.nhubs > 0 && a.hub_front) || !a.push) && !a.hub_mark,
+             "bu_step: pushed words need the hub kernels (and bottom-up levels mark no hubs)");
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
     // a whole 64-word unit per wave when the shard has enough units to fill
@@ -978,7 +993,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
     if (a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
-      DBFS_CHECK(!a.end.active && !a.hub_mark_clear, "bu_step: a folded level end / hub marks need the fused finish");
+      DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the fused finish");
       // (more workgroups than totals slots: finish in a kernel of its own)
       BuArgs b = a;
       b.fuse_scan = false;
@@ -990,7 +1005,9 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // compiled only into the kEnd variants)
 #define DBFS_BU_LAUNCH(W, T, Q, R)                                                          \
   do {                                                                                    \
-    if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);            \
+    if (a.end.active && a.push) bu_hub_kernel<W, T, Q, R, true, 0, true><<<grid, T, 0, st>>>(a);  \
+    else if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);       \
+    else if (a.push) bu_hub_kernel<W, T, Q, R, false, 0, true><<<grid, T, 0, st>>>(a);  \
     else bu_hub_kernel<W, T, Q, R, false><<<grid, T, 0, st>>>(a);                        \
   } while (0)
     if (a.cut_edges > 0) {
@@ -1003,13 +1020,19 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       // (with the deferred row queue: without it, scans in place, the late-switch
       // levels measured 460-535 -> 505-560 us)
       constexpr int kCutQ = kBuQueue;
+#define DBFS_CUT_LAUNCH(W, C)                                                                        \
+  do {                                                                                             \
+    if (a.push) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C, true><<<grid, kHubBuThreads, 0, st>>>(a); \
+    else bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C><<<grid, kHubBuThreads, 0, st>>>(a);          \
+  } while (0)
       if (a.cut_claim) {
-        if (whole) bu_hub_kernel<true, kHubBuThreads, kCutQ, true, false, kCutClaims><<<grid, kHubBuThreads, 0, st>>>(a);
-        else bu_hub_kernel<false, kHubBuThreads, kCutQ, true, false, kCutClaims><<<grid, kHubBuThreads, 0, st>>>(a);
+        if (whole) DBFS_CUT_LAUNCH(true, kCutClaims);
+        else DBFS_CUT_LAUNCH(false, kCutClaims);
       } else {
-        if (whole) bu_hub_kernel<true, kHubBuThreads, kCutQ, true, false, kCutLevels><<<grid, kHubBuThreads, 0, st>>>(a);
-        else bu_hub_kernel<false, kHubBuThreads, kCutQ, true, false, kCutLevels><<<grid, kHubBuThreads, 0, st>>>(a);
+        if (whole) DBFS_CUT_LAUNCH(true, kCutLevels);
+        else DBFS_CUT_LAUNCH(false, kCutLevels);
       }
+#undef DBFS_CUT_LAUNCH
     }
     if (whole) {
       if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);

@@ -188,12 +188,6 @@ __device__ __forceinline__ long long hub_mark_edges(const ShardView& g, const wo
   for (int k = 0; k < kHubMarkSlots; ++k) s += static_cast<long long>(marks[hub_mark_bits_words(g.nhubs) + k * kHubMarkSlotWords]);
   return s;
 }
-// the other buffer zeroed by the level's last workgroup (every thread calls)
-template <int kThreads>
-__device__ __forceinline__ void clear_hub_marks(word_t* marks, int64_t nhubs) {
-  if (!marks) return;
-  for (int64_t i = threadIdx.x; i < hub_mark_words(nhubs); i += kThreads) marks[i] = 0ull;
-}
 
 // Frontier push (backend.hpp FrontierTable): word w of this rank's slice to
 // every peer's window, write-through.

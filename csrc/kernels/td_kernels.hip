@@ -369,7 +369,9 @@ __device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v
 // of this shard): level, frontier bit, and the wave's work-list entries of
 // the next level with one packed atomic (count << kSparseEdgeBits | edges)
 // for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
-template <int kItems>
+// (kMarks: the settled hubs also marked, TdSparseArgs::hub_mark -- a variant of
+// its own: the code costs the plain kernels 8 VGPRs, an occupancy step)
+template <int kItems, bool kMarks = false>
 __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   if (!__ballot(claimed != 0)) return;
@@ -388,7 +390,7 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
       re[k] = ro[r + 1];
     }
   }
-  if (a.hub_mark) {
+  if constexpr (kMarks) {
 #pragma unroll
     for (int k = 0; k < kItems; ++k)
       if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.hub_min_deg))
@@ -659,7 +661,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
 // their owners' lists and td_sparse_apply finishes the level after the
 // exchange.  kThreads = 1024: 2 edges per thread per block.
 constexpr int kTdSparseThreads = 1024;
-template <int kThreads>
+template <int kThreads, bool kMarks = false>
 __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
@@ -730,7 +732,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       }
     }
     // (B) finish the wave's claimed vertices
-    sparse_settle<kItems>(a, v, claimed);
+    sparse_settle<kItems, kMarks>(a, v, claimed);
   }
   if (a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
@@ -775,7 +777,6 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   }
   __syncthreads();
   if (!s_last) return;
-  clear_hub_marks<kThreads>(a.hub_mark_clear, a.g.nhubs);
   if (t != 0) return;
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
@@ -797,7 +798,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
 // claims, owner lists and settling as td_sparse.  The level ends in the last
 // workgroup of a two-level ticket.
 constexpr int kBitsPre = 4;
-template <int kItems>
+template <int kItems, bool kMarks = false>
 __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) {
   __shared__ long long s_incl[kBlock];  // per wave: the step's inclusive degree prefixes
   __shared__ eid_t s_rs[kBlock];        // ... and row starts
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
           }
         }
         // (B) finish the wave's claimed vertices
-        sparse_settle<kItems>(a, v, claimed);
+        sparse_settle<kItems, kMarks>(a, v, claimed);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // (the next step overwrites w_incl / w_rs)
@@ -925,7 +926,6 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
     if (dx && a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);
     return;
   }
-  clear_hub_marks<kBlock>(a.hub_mark_clear, a.g.nhubs);
   if (t != 0) return;
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
@@ -1269,7 +1269,7 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
-  DBFS_CHECK((!a.hub_mark && !a.hub_mark_clear) || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0 && a.g.hub_pref),
+  DBFS_CHECK(!a.hub_mark || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0 && a.g.hub_pref),
              "td_sparse: hub marks are one-rank and need the hub tables");
   if (a.from_bits) {
     // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
@@ -1278,14 +1278,16 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
     DBFS_CHECK(a.group_ticket, "td_sparse from a bitmap needs the group tickets");
     // (an empty shard still runs one workgroup: the level's finish)
     const unsigned grid = grid_for(nunits, kUnitsPerBlock, std::min<int64_t>(kMaxFusedGrid, 1024));
-    td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
+    if (a.hub_mark) td_sparse_bits_kernel<4, true><<<grid, kBlock, 0, st>>>(a);
+    else td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
     return;
   }
   // 1024-thread workgroups, two edges per thread per block: a sparse level's
   // few blocks get four times the waves (measured against 256 threads / 8
   // edges: RMAT-26 1479 / 1469 -> 1502 / 1481 GTEPS, level 0 9.8 -> 6.7 us;
   // RMAT-22 top-down only 90.5 / 90.8 -> 91.8 / 92.2)
-  td_sparse_kernel<kTdSparseThreads><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
+  if (a.hub_mark) td_sparse_kernel<kTdSparseThreads, true><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
+  else td_sparse_kernel<kTdSparseThreads><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
 }
 
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
