@@ -62,28 +62,6 @@ class CpuBackend final : public Backend {
   void fill_level(lvl_t* level, int64_t n, lvl_t value) override { std::fill(level, level + n, value); }
   void set_bit(word_t* bm, int64_t bit) override { bm[bit >> 6] |= 1ull << (bit & 63); }
 
-  // hub marks (backend.hpp hub_mark_words): the hubs among a new frontier word
-  static void mark_hubs(const ShardView& g, word_t* marks, int64_t gw, word_t bits) {
-    for (word_t m = bits & g.hub_bits[gw]; m; m &= m - 1) {
-      const int b = __builtin_ctzll(m);
-      const vid_t v = static_cast<vid_t>(gw * 64 + b);
-      const int64_t h = std::lower_bound(g.hub_vertex, g.hub_vertex + g.nhubs, v) - g.hub_vertex;
-      DBFS_CHECK(h < g.nhubs && g.hub_vertex[h] == v, "hub marks: a hub bit without a hub");
-      DBFS_CHECK(h == g.hub_pref[gw] + __builtin_popcountll(g.hub_bits[gw] & ((1ull << b) - 1ull)),
-                 "hub marks: the hub prefix disagrees with hub_vertex");
-      marks[h >> 6] |= 1ull << (h & 63);
-      marks[hub_mark_bits_words(g.nhubs) + ((gw >> 6) & (kHubMarkSlots - 1)) * kHubMarkSlotWords] += g.hub_deg[h];
-    }
-  }
-  static uint64_t mark_edges(const ShardView& g, const word_t* marks) {
-    uint64_t s = 0;
-    for (int k = 0; k < kHubMarkSlots; ++k) s += marks[hub_mark_bits_words(g.nhubs) + k * kHubMarkSlotWords];
-    return s;
-  }
-  static void clear_marks(const ShardView& g, word_t* marks) {
-    if (marks) std::fill(marks, marks + hub_mark_words(g.nhubs), 0ull);
-  }
-
   void update_frontier(const UpdateArgs& a) override {
     if (a.fuse_scan) {
       // totals and finish right after the update, unit statistics unscanned
@@ -119,7 +97,6 @@ class CpuBackend final : public Backend {
         const word_t nb = a.force ? c : (c & ~a.visited[w]);
         a.visited[w] |= nb;
         a.frontier[w] = nb;
-        if (a.hub_mark) mark_hubs(a.g, a.hub_mark, (a.g.lo >> 6) + w, nb);
         for (int p = 0; p < a.zero_slices; ++p) a.zero_next[p * a.words + w] = 0;
         word_t x = nb;
         while (x) {
@@ -165,10 +142,6 @@ class CpuBackend final : public Backend {
     a.qscan[cnt] = deg;
     if (a.frontier_clear)
       for (int64_t w = 0; w < a.words; ++w) a.frontier_clear[w] = 0;
-    if (a.hub_mark_seed) {
-      clear_marks(a.g, a.hub_mark_seed);
-      if (src >= 0) mark_hubs(a.g, a.hub_mark_seed, (a.g.lo + src) >> 6, 1ull << (src & 63));
-    }
     if (cnt && a.qbase) {
       a.qscan[0] = 0;
       a.qbase[0] = a.g.row_off[src];
@@ -371,8 +344,6 @@ class CpuBackend final : public Backend {
     const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
     if (d <= 0) return;
     a.frontier_out[r >> 6] |= 1ull << (r & 63);
-    if (a.hub_mark && d >= static_cast<eid_t>(a.g.hub_min_deg))
-      mark_hubs(a.g, a.hub_mark, static_cast<int64_t>(v) >> 6, 1ull << (v & 63));
     if (a.hx_bits && d >= static_cast<eid_t>(a.g.td_hub_min_deg)) {
       // hub-split: a top-down hub with a part on this rank leaves the list
       const vid_t* hv = a.g.td_hub_vertex;
@@ -515,18 +486,6 @@ class CpuBackend final : public Backend {
       return;
     }
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-    DBFS_CHECK(!a.hub_mark, "bottom-up: bottom-up levels mark no hubs");
-    if (a.hub_front && a.hub_front_marks) {
-      // the previous level's marks (hub_front) must be exactly its frontier
-      // hubs, their degree word the hubs' degree sum (what hub_gather computes)
-      uint64_t hd = 0;
-      for (int64_t h = 0; h < a.g.nhubs; ++h) {
-        const bool f = test_bit(a.frontier, a.g.hub_vertex[h]);
-        DBFS_CHECK(f == (((a.hub_front[h >> 6] >> (h & 63)) & 1ull) != 0), "hub marks differ from the frontier hubs");
-        if (f) hd += a.g.hub_deg[h];
-      }
-      DBFS_CHECK(mark_edges(a.g, a.hub_front) == hd, "hub marks: degree slots differ");
-    }
     // hub-cut level (as the HIP kernel): claimed vertices join the output
     // unscanned, the others find parents among the frontier hubs only
     const bool cut = a.cut_edges > 0 && *a.cut_flag;
@@ -806,8 +765,6 @@ class CpuBackend final : public Backend {
   void bu_cut_prep(const BuArgs& a) override {
     DBFS_CHECK(!a.cut_direct.active, "CpuBackend: no direct list exchange");
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-    if (a.cut_from_marks)
-      *a.cut_flag = a.ctrl->m_f - static_cast<int64_t>(mark_edges(a.g, a.hub_front)) <= a.cut_edges ? 1 : 0;
     if (!*a.cut_flag) return;
     const int64_t lo = a.g.lo;
     for (int64_t w = 0; w < a.words; ++w)

@@ -50,9 +50,6 @@ class DeviceLoop {
     // slices (the previous chain's table) for hub_gather to copy in
     const FrontierTable* push = nullptr;
     const FrontierTable* pull = nullptr;
-    // one rank, hub marks: this chain marks its output's hubs (a bottom-up
-    // level is predicted next)
-    bool mark = false;
   };
 
   Engine& e_;
@@ -77,10 +74,6 @@ class DeviceLoop {
   int bin_shift_ = 12;
   int64_t nbins_ = 0;
   bool binned_ = false;
-  // one rank: hub marks (EngineOptions::bu_hub_marks; buffer k of the chain
-  // of parity k, backend.hpp)
-  bool marks_ = false;
-  word_t* marks(int L) const { return e_.hub_marks_.data() + (L & 1) * hub_mark_words(gv_.nhubs); }
   static constexpr int kBinGrid = 1024;
   int64_t td_grid_ = 1, td_grid_filter_ = 1;
   bool seed_gather_ = false;
@@ -90,7 +83,6 @@ class DeviceLoop {
   // ---- per-level records of what was enqueued ----
   std::vector<char> enq_dir_, enq_form_, enq_gather_, enq_fused_;
   std::vector<const FrontierTable*> enq_push_;  // level L's output pushed (Chain::push)
-  std::vector<char> enq_mark_;                  // level L's output hubs marked (Chain::mark)
   std::vector<int64_t> enq_cap_;
   std::vector<std::pair<int, int>> evs_;
   RunResult res_;
@@ -175,12 +167,6 @@ void DeviceLoop::setup() {
   }
   // one rank with narrow levels: byte-map levels write the levels directly
   direct_ = !xc_ && e_.run_narrow_ && opt_.td_direct;
-  // (the marks' buffers are cleared by the chains' fused finishes)
-  marks_ = !xc_ && opt_.bu_hub_marks && gv_.nhubs > 0 && gv_.hub_min_deg > 0 && gv_.hub_bits && gv_.hub_deg &&
-           gv_.hub_pref &&
-           opt_.td_fused_finish && opt_.bu_fused_scan;
-  if (marks_ && !e_.hub_marks_.data())
-    e_.hub_marks_ = DBuf<word_t>(be_, static_cast<size_t>(2 * hub_mark_words(gv_.nhubs)));
   byte_edges_ = direct_ ? opt_.td_direct_edges : opt_.td_byte_edges;
   bytes_ok_ = opt_.mode != Mode::BottomUp && byte_edges_ <= e_.total_directed_;
   if (bytes_ok_ && !e_.next_bytes_.data()) {
@@ -466,7 +452,6 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     enq_gather_.resize(static_cast<size_t>(L) + 1);
     enq_fused_.resize(static_cast<size_t>(L) + 1);
     enq_push_.resize(static_cast<size_t>(L) + 1);
-    enq_mark_.resize(static_cast<size_t>(L) + 1);
     evs_.resize(static_cast<size_t>(L) + 1, {-1, -1});
   }
   Chain c;
@@ -488,10 +473,6 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
                ? comm_.direct_frontier(static_cast<size_t>(W_), L & 1)
                : nullptr;
   enq_push_[L] = c.push;
-  c.mark = marks_ && gather && d != 'B';
-  enq_mark_[L] = c.mark;
-  // (its buffer zeroed first: a small fill, ahead of the chain's kernels)
-  if (c.mark) be_.memset_async(marks(L), 0, static_cast<size_t>(hub_mark_words(gv_.nhubs)) * sizeof(word_t));
   res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
   res_.chains.back().push = c.push != nullptr;
   c.cap = enq_cap_[L];
@@ -606,9 +587,6 @@ void DeviceLoop::emit_sparse(Chain& c) {
   sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
   sp.first = !compacted || from_bits;
   sp.max_mf = c.cap;
-  if (marks_) {
-    sp.hub_mark = c.mark ? marks(L) : nullptr;
-  }
   if (from_bits) {
     sp.from_bits = true;
     sp.words = W_;
@@ -713,7 +691,6 @@ void DeviceLoop::emit_binned(Chain& c) {
   tu.frontier = fr_own(c.cur ^ 1);
   tu.new_level = L + 1;
   tu.ctrl = e_.ctrl_.data();
-  if (marks_) tu.hub_mark = c.mark ? marks(L) : nullptr;
   be_.update_frontier(tu);
 }
 
@@ -829,7 +806,6 @@ void DeviceLoop::emit_dense(Chain& c) {
   tu.push = c.push;
   tu.push_rank = me_;
   tu.push_nranks = P_;
-  if (marks_) tu.hub_mark = c.mark ? marks(L) : nullptr;
   if (opt_.td_fused_finish) {
     // totals (and with one rank the decision) in the update's last
     // workgroup (as bottom-up)
@@ -921,16 +897,8 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.cut_flag = e_.cut_flag_.data();
       hg.cut_ticket = e_.cut_ticket_.data();
     }
-    if (marks_ && (L == 0 || enq_mark_[static_cast<size_t>(L - 1)])) {
-      // the previous chain (or the seed) marked the frontier hubs in its
-      // buffer; bu_cut_prep decides a hub cut from their degree slots
-      ba.hub_front = marks(L + 1);
-      ba.hub_front_marks = true;
-      ba.cut_from_marks = cut;
-    } else {
-      be_.hub_gather(hg);
-      ba.hub_front = e_.hub_front_.data();
-    }
+    be_.hub_gather(hg);
+    ba.hub_front = e_.hub_front_.data();
     if (cut) {
       ba.cut_edges = cut_edges;
       ba.cut_flag = e_.cut_flag_.data();
@@ -1042,10 +1010,6 @@ RunResult DeviceLoop::run() {
     ia.blk_vstart = e_.blk_vstart_.data();
     ia.qv = e_.qv_[0].data();
     ia.frontier_clear = fr_own(0);
-  }
-  if (marks_) {
-    // (the seed is the output of "chain -1": parity 1)
-    ia.hub_mark_seed = marks(1);
   }
   be_.init_run(ia);
   // the seed's frontier is gathered with its totals when level 0 is bottom-up

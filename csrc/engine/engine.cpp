@@ -97,7 +97,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
   else if (name == "direct_frontier") o.direct_frontier = v != 0;
-  else if (name == "bu_hub_marks") o.bu_hub_marks = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -149,8 +148,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
-          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0},
-          {"bu_hub_marks", o.bu_hub_marks ? 1.0 : 0.0}};
+          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------
@@ -321,8 +319,6 @@ ShardView DeviceGraph::view() const {
   v.hub_col = hub_col_.data();
   v.hub_bits = hub_bits_.data();
   v.hub_deg = hub_deg_.data();
-  v.hub_min_deg = hub_min_deg_;
-  v.hub_pref = hub_pref_.data();
   v.nz_pref = nz_pref_.data();
   v.nz_row_off = nz_row_off_.data();
   v.nz_head = nz_head_.data();
@@ -392,10 +388,8 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   comm.allgather(mine.data(), all.data(), static_cast<size_t>(part) * sizeof(uint32_t));
   be_->sort_neighbors(row_off_.data(), col_.data(), rows_, all.data());
   nhubs_ = 0;
-  hub_min_deg_ = 0;
   hub_vertex_.reset();
   hub_bits_.reset();
-  hub_pref_.reset();
   hub_deg_.reset();
   hub_col_.reset();
   td_col_.reset();
@@ -415,7 +409,6 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
       nhubs_ = be_->select_hubs(all.data(), nall, min_deg, hub_vertex_.data(), hub_idx.data());
       DBFS_CHECK(nhubs_ >= 0 && nhubs_ <= max_hubs, "hub selection exceeded its capacity");
       if (nhubs_ > 0) {
-        hub_min_deg_ = min_deg;
         // hub membership bitmap over all vertices (hub-cut bottom-up levels)
         std::vector<vid_t> hv(static_cast<size_t>(nhubs_));
         be_->to_host(hv.data(), hub_vertex_.data(), hv.size() * sizeof(vid_t));
@@ -423,15 +416,6 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
         for (vid_t v : hv) bits[v >> 6] |= 1ull << (v & 63);
         hub_bits_ = DBuf<word_t>(*be_, bits.size());
         be_->to_device(hub_bits_.data(), bits.data(), bits.size() * sizeof(word_t));
-        // hubs before each word (a hub's index without a search: hub marks)
-        std::vector<uint32_t> pref(bits.size());
-        uint32_t run = 0;
-        for (size_t w = 0; w < bits.size(); ++w) {
-          pref[w] = run;
-          run += static_cast<uint32_t>(__builtin_popcountll(bits[w]));
-        }
-        hub_pref_ = DBuf<uint32_t>(*be_, pref.size());
-        be_->to_device(hub_pref_.data(), pref.data(), pref.size() * sizeof(uint32_t));
         // the hubs' degrees (several ranks: the hub-cut decision)
         std::vector<uint32_t> hd(hv.size());
         for (size_t i = 0; i < hv.size(); ++i) hd[i] = deg[hv[i]];

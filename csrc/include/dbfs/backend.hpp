@@ -50,11 +50,6 @@ struct ShardView {
   // vertex id.  Bottom-up keeps the hubs' frontier bits in LDS.
   const vid_t* hub_vertex = nullptr;
   int64_t nhubs = 0;
-  // a vertex is a hub iff its degree (row length) >= hub_min_deg (> 0 with hubs)
-  uint32_t hub_min_deg = 0;
-  // hubs in the global words before word w (one rank with hubs: a hub's index
-  // is hub_pref[v >> 6] + its rank among the hub bits of its word)
-  const uint32_t* hub_pref = nullptr;
   // Hub-encoded copy of col (same layout; hub neighbours as kHubFlag | index),
   // read by bottom-up so that probes of hub neighbours hit LDS too.
   const vid_t* hub_col = nullptr;
@@ -260,8 +255,6 @@ struct InitRunArgs {
   int32_t* blk_vstart = nullptr;
   vid_t* qv = nullptr;
   word_t* frontier_clear = nullptr;
-  // hub marks: the seed's written (every word of the buffer)
-  word_t* hub_mark_seed = nullptr;
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;
@@ -441,20 +434,6 @@ struct DirectExchange {
   const int64_t* result = nullptr;
 };
 
-// Hub marks (one rank, EngineOptions::bu_hub_marks): the kernels that settle
-// a (top-down) level predicted to feed a bottom-up one also set the bits that
-// level stages for its frontier hubs (hub_gather's hub_front: bit h for
-// hub_vertex[h]) and add the hubs' degrees into kHubMarkSlots slots after the
-// bits (128 B apart; their sum: the hub-cut decision) -- no hub_gather launch
-// before the bottom-up level.  Two buffers by the producing chain's parity:
-// a marking chain of level L fills buffer L & 1 with zeros ahead of its
-// kernels; the run's initialisation writes the seed's marks into buffer 1.
-constexpr int kHubMarkSlots = 32, kHubMarkSlotWords = 16;
-constexpr int64_t hub_mark_bits_words(int64_t nhubs) { return (nhubs + 63) / 64; }
-constexpr int64_t hub_mark_words(int64_t nhubs) {
-  return hub_mark_bits_words(nhubs) + int64_t(kHubMarkSlots) * kHubMarkSlotWords;
-}
-
 // new = (OR_r cand[r * cand_stride + w]) & ~visited[w] over the owned slice
 // (force: new = cand, used to seed the source):  visited |= new;
 // frontier = new; level[v] = new_level for v in new; unit_cnt[u] / unit_deg[u]
@@ -503,8 +482,6 @@ struct UpdateArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
-  // hub marks: this level's (zero on entry)
-  word_t* hub_mark = nullptr;
   // several ranks: the send buffer of the candidates' all-to-all (zero_slices
   // slices of `words` words) zeroed here -- word w of every slice by the lane
   // of w -- instead of a memset launch after the exchange
@@ -597,8 +574,6 @@ struct TdSparseArgs {
   word_t* hx_bits = nullptr;
   int64_t* hx_tot = nullptr;
   int64_t* hx_out = nullptr;
-  // hub marks (one rank; as UpdateArgs)
-  word_t* hub_mark = nullptr;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -812,14 +787,6 @@ struct BuArgs {
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
-  // hub marks (one rank; as UpdateArgs, but a bottom-up level marks nothing:
-  // hub_mark stays null).  hub_front_marks: hub_front is the
-  // previous chain's marks (no hub_gather ran), and with cut_from_marks
-  // bu_cut_prep decides the hub cut from their degree slots (hub_gather's
-  // decision) and stores it in *cut_flag
-  word_t* hub_mark = nullptr;
-  bool hub_front_marks = false;
-  bool cut_from_marks = false;
 };
 
 // out bit h = visited bit of g.td_hub_vertex[h] (visited global): the

@@ -106,8 +106,6 @@ class DeviceGraph {
   // several ranks: hub-split rows (ShardView::hx_off), appended to col_ / td_col_
   DBuf<eid_t> hx_off_;
   uint32_t td_hub_min_deg_ = 0;
-  uint32_t hub_min_deg_ = 0;  // (ShardView::hub_min_deg)
-  DBuf<uint32_t> hub_pref_;   // (ShardView::hub_pref)
   DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
   void build_hub_split();
   int64_t hx_total() const;
@@ -311,11 +309,6 @@ struct EngineOptions {
   // bottom-up level's hub_gather copies them in -- the level end carries only
   // its totals (and may fold into the bottom-up kernel).  Off until measured.
   bool direct_frontier = false;
-  // One rank, graphs with hubs: the kernels that settle a level also mark its
-  // frontier hubs (backend.hpp hub marks), so a bottom-up level needs no
-  // hub_gather launch (and the hub cut is decided by bu_cut_prep from the
-  // marks' degree word).  Off until measured.
-  bool bu_hub_marks = false;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
@@ -459,7 +452,6 @@ class Engine {
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_;
-  DBuf<word_t> hub_marks_;  // one rank, EngineOptions::bu_hub_marks: two buffers (backend.hpp)
   // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
   // decision and its ticket (zero between levels)
   DBuf<int64_t> cut_part_;

@@ -121,25 +121,6 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? sbit : 0ull;
   if (a.frontier_clear)
     for (int64_t w = t0; w < a.words; w += stride) a.frontier_clear[w] = 0ull;
-  if (a.hub_mark_seed) {
-    // the seed's hub marks (the source, if a hub: its bit and degree), the
-    // other buffer zeroed
-    // (slot 0 holds the seed's degree: only the slots' sum is read)
-    const int64_t hw = hub_mark_bits_words(a.g.nhubs), n = hub_mark_words(a.g.nhubs);
-    int64_t sh = -1;
-    uint32_t sd = 0;
-    if (src >= 0 && t0 < n) {
-      const int64_t v = a.g.lo + src;
-      const word_t hb = a.g.hub_bits[v >> 6];
-      if ((hb >> (v & 63)) & 1ull) {
-        sh = a.g.hub_pref[v >> 6] + __popcll(hb & ((1ull << (v & 63)) - 1ull));
-        sd = a.g.hub_deg[sh];
-      }
-    }
-    for (int64_t i = t0; i < n; i += stride) {
-      a.hub_mark_seed[i] = sh < 0 ? 0ull : i == hw ? static_cast<word_t>(sd) : (sh >> 6) == i ? 1ull << (sh & 63) : 0ull;
-    }
-  }
   // the seed's work-list entry: edge blocks [0, ceil(d / EPB)) all start in it
   if (a.blk_vstart && src >= 0) {
     const eid_t d = a.g.row_off[src + 1] - a.g.row_off[src];
@@ -246,7 +227,10 @@ __device__ __forceinline__ word_t gather_level_bits(const uint8_t* p, uint8_t lv
 // kSplit waves per unit (small graphs: 4, each over 16 of its words -- a
 // graph of few units would leave most wave slots idle while each wave walks
 // its unit's new vertices 64 per dependent step); `sub` = this wave's part.
-template <int kSplit = 1>
+// (kRanks: the several-rank extras -- pushed words, the send buffer re-zeroed
+// -- compiled into a variant of their own: in every kernel they cost the
+// one-rank update 2 us a level)
+template <int kSplit = 1, bool kRanks = false>
 __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, bool use_bytes, long long& cnt,
                                             long long& deg, int sub = 0) {
   constexpr int kWords = kUnitWords / kSplit;
@@ -267,9 +251,10 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
     nb = a.force ? c : (c & ~vis);
     if (nb) a.visited[wl] = vis | nb;
     a.frontier[wl] = nb;
-    if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, wl, nb);
-    if (a.hub_mark) mark_hub_word(a.g, a.hub_mark, (a.g.lo >> 6) + wl, nb);
-    for (int p = 0; p < a.zero_slices; ++p) a.zero_next[p * a.words + wl] = 0ull;
+    if constexpr (kRanks) {
+      if (a.push) push_frontier_word(a.push, a.push_rank, a.push_nranks, wl, nb);
+      for (int p = 0; p < a.zero_slices; ++p) a.zero_next[p * a.words + wl] = 0ull;
+    }
     if (a.clear_cand && c && !use_bytes) a.cand[wl] = 0;
   }
   // New vertices of the unit, 64 per step (one per lane, whatever word they
@@ -303,10 +288,11 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
 
 // A unit per workgroup, its kSplit (= kUnitsPerBlock) waves each over a part
 // (update_unit<kSplit>); the unit's statistics summed in LDS.
+template <bool kRanks>
 __device__ __forceinline__ void update_unit_split(const UpdateArgs& a, int64_t unit, bool use_bytes, long long& cnt,
                                                   long long& deg, long long* s_pc, long long* s_pd) {
   const int wv = static_cast<int>(threadIdx.x >> 6);
-  update_unit<kUnitsPerBlock>(a, unit, use_bytes, cnt, deg, wv);
+  update_unit<kUnitsPerBlock, kRanks>(a, unit, use_bytes, cnt, deg, wv);
   if (lane_id() == 0) {
     s_pc[wv] = cnt;
     s_pd[wv] = deg;
@@ -325,15 +311,17 @@ __device__ __forceinline__ void update_unit_split(const UpdateArgs& a, int64_t u
   __syncthreads();  // (s_pc / s_pd reused by the next unit)
 }
 
-template <bool kSplit>
+// kRanks: several ranks (UpdateArgs::push / zero_next / end).
+template <bool kSplit, bool kRanks>
 __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
-  __shared__ uint64_t s_x[2 * kern::kMaxPeers];  // (the folded level end's cells)
+  __shared__ uint64_t s_x[kRanks ? 2 * kern::kMaxPeers : 1];  // (the folded level end's cells)
   bool use_bytes = a.cand_bytes != nullptr;
   if (a.ctrl) {
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
       // a folded level end is a collective: it runs on a no-op chain too
-      if (a.end.active && blockIdx.x == 0)
-        direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin, s_x);
+      if constexpr (kRanks)
+        if (a.end.active && blockIdx.x == 0)
+          direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin, s_x);
       return;
     }
     use_bytes = use_bytes && a.ctrl->bytes != 0;
@@ -346,11 +334,11 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     if constexpr (kSplit) {
       const int64_t unit = blockIdx.x;
       if (unit >= nunits) return;
-      update_unit_split(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
+      update_unit_split<kRanks>(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
     } else {
       const int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv;
       if (unit >= nunits) return;
-      update_unit(a, unit, use_bytes, cnt, deg);
+      update_unit<1, kRanks>(a, unit, use_bytes, cnt, deg);
     }
     return;
   }
@@ -363,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   if constexpr (kSplit) {
     for (int64_t unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
       long long cnt, deg;
-      update_unit_split(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
+      update_unit_split<kRanks>(a, unit, use_bytes, cnt, deg, s_pc, s_pd);
       wc += cnt;  // (this wave's part: the workgroup's totals are the waves' sum, as below)
       wd += deg;
     }
@@ -371,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     for (int64_t unit = static_cast<int64_t>(blockIdx.x) * kUnitsPerBlock + wv; unit < nunits;
          unit += static_cast<int64_t>(gridDim.x) * kUnitsPerBlock) {
       long long cnt, deg;
-      update_unit(a, unit, use_bytes, cnt, deg);
+      update_unit<1, kRanks>(a, unit, use_bytes, cnt, deg);
       wc += cnt;
       wd += deg;
     }
@@ -382,7 +370,8 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
   }
   // (pushed words: every wave's write-through stores drained before the
   // ticket, so the level end published after it covers them)
-  if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (kRanks)
+    if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     long long c = 0, d = 0;
@@ -472,9 +461,11 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     s_c[0] = tc;
     s_d[0] = td;
   }
-  if (a.end.active) {
-    __syncthreads();
-    direct_level_end(a.end, s_c[0], s_d[0], a.scan.stats, a.fin, s_x);
+  if constexpr (kRanks) {
+    if (a.end.active) {
+      __syncthreads();
+      direct_level_end(a.end, s_c[0], s_d[0], a.scan.stats, a.fin, s_x);
+    }
   }
 }
 
@@ -781,8 +772,6 @@ void set_bit(word_t* bm, int64_t bit, hipStream_t st) { set_bit_kernel<<<1, 64, 
 void level_ctrl_init(LevelCtrl* c, const LevelCtrl& init, hipStream_t st) { ctrl_init_kernel<<<1, 64, 0, st>>>(c, init); }
 
 void init_run(const InitRunArgs& a, hipStream_t st) {
-  DBFS_CHECK(!a.hub_mark_seed || (a.g.hub_pref && a.g.hub_bits && a.g.hub_deg),
-             "init_run: the seed's hub marks need the hub tables");
   const int64_t work = std::max<int64_t>(std::max<int64_t>(a.g.rows / 4, a.gwords), 1);
   init_run_kernel<<<grid_for(work, kBlock, 8 * device_cus()), kBlock, 0, st>>>(a);
 }
@@ -798,8 +787,6 @@ constexpr int64_t kSplitUnits = 4096;
 
 void update_frontier(const UpdateArgs& a, hipStream_t st) {
   DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
-  DBFS_CHECK(!a.hub_mark || (a.g.hub_bits && a.g.hub_deg && a.g.hub_pref && a.g.nhubs > 0),
-             "update: hub marks need the hub tables");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
   const bool split = nunits < kSplitUnits;
@@ -808,8 +795,11 @@ void update_frontier(const UpdateArgs& a, hipStream_t st) {
   // with one ticket; up to kMaxFusedGrid with the two-level ticket
   const unsigned grid = a.fuse_scan ? grid_for(a.words, per, a.group_ticket ? kMaxFusedGrid : kMaxFusedGrid / 8)
                                     : grid_for(a.words, per);
-  if (split) update_kernel<true><<<grid, kBlock, 0, st>>>(a);
-  else update_kernel<false><<<grid, kBlock, 0, st>>>(a);
+  const bool ranks = a.push || a.zero_next || a.end.active;
+  if (split && ranks) update_kernel<true, true><<<grid, kBlock, 0, st>>>(a);
+  else if (split) update_kernel<true, false><<<grid, kBlock, 0, st>>>(a);
+  else if (ranks) update_kernel<false, true><<<grid, kBlock, 0, st>>>(a);
+  else update_kernel<false, false><<<grid, kBlock, 0, st>>>(a);
 }
 
 void totals_finish(const ScanArgs& a, hipStream_t st) { totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a); }

@@ -590,9 +590,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   // a hub-cut level launches both variants; the decision picks one
   if (a.cut_flag && (*a.cut_flag != 0) != (kCut != 0)) return;
   constexpr bool cut = kCut != 0;
-  // (the level's first kernel stamps its start: hub_gather, or with hub marks
-  // this one -- bu_cut_prep on a hub-cut level)
-  if (!a.hub_front || (a.hub_front_marks && !a.cut_from_marks)) stamp_level_start(a.ctrl);
+  if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
   __syncthreads();
@@ -715,31 +713,34 @@ __device__ __forceinline__ bool pulled_bit(const HubGatherArgs& a, vid_t v) {
   const word_t f = p == a.pull_rank ? a.frontier[w] : sys_load_u64(a.pull->src[p] + (w - p * a.pull_words));
   return (f >> (v & 63)) & 1ull;
 }
-template <bool kCut>
-__global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a) {
+// (kThreads x kPer hubs per workgroup: the plain gather one hub per thread
+// over a grid that fills the chip, the cut decision 4 per thread over ~16
+// workgroups -- fewer ticket arrivals)
+template <bool kCut, int kThreads, int kPer>
+__global__ __launch_bounds__(kThreads) void hub_gather_kernel(HubGatherArgs a) {
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
   stamp_level_start(a.ctrl);
-  __shared__ long long s_d[kHgThreads / kWave];
+  __shared__ long long s_d[kThreads / kWave];
   __shared__ int s_last;
   const int lane = lane_id();
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * (kHgThreads * kHgPer);
-  vid_t hv[kHgPer];
-  bool bit[kHgPer];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * (kThreads * kPer);
+  vid_t hv[kPer];
+  bool bit[kPer];
 #pragma unroll
-  for (int k = 0; k < kHgPer; ++k) {
-    const int64_t h = base + k * kHgThreads + threadIdx.x;
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t h = base + k * kThreads + threadIdx.x;
     hv[k] = h < a.g.nhubs ? a.g.hub_vertex[h] : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < kHgPer; ++k) {
-    const int64_t h = base + k * kHgThreads + threadIdx.x;
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t h = base + k * kThreads + threadIdx.x;
     bit[k] = h < a.g.nhubs && (a.pull ? pulled_bit(a, hv[k]) : test_bit(a.frontier, hv[k]));
   }
   long long d = 0;
 #pragma unroll
-  for (int k = 0; k < kHgPer; ++k) {
-    const int64_t h = base + k * kHgThreads + threadIdx.x;
-    const int64_t h0 = base + k * kHgThreads + (threadIdx.x & ~(kWave - 1));
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t h = base + k * kThreads + threadIdx.x;
+    const int64_t h0 = base + k * kThreads + (threadIdx.x & ~(kWave - 1));
     const word_t m = __ballot(bit[k]);
     if (lane == 0 && h0 < a.g.nhubs) a.hub_front[h0 / kWave] = m;
     if (kCut && bit[k])
@@ -747,9 +748,9 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
                        : static_cast<long long>(a.g.row_off[hv[k] + 1] - a.g.row_off[hv[k]]);
   }
   if (a.pull) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kHgThreads;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
     const int64_t gw = a.pull_words * a.pull_nranks;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kHgThreads + threadIdx.x; i < gw; i += stride) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < gw; i += stride) {
       const int p = static_cast<int>(i / a.pull_words);
       if (p == a.pull_rank) continue;
       const word_t f = sys_load_u64(a.pull->src[p] + (i - p * a.pull_words));
@@ -757,8 +758,8 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
       if (a.visited && f) a.visited[i] |= f;
     }
   } else if (a.visited) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kHgThreads;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kHgThreads + threadIdx.x; i < a.words; i += stride) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < a.words; i += stride) {
       const word_t f = a.frontier[i];
       if (f) a.visited[i] |= f;
     }
@@ -770,7 +771,7 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
   if (threadIdx.x == 0) {
     long long t = 0;
 #pragma unroll
-    for (int k = 0; k < kHgThreads / kWave; ++k) t += s_d[k];
+    for (int k = 0; k < kThreads / kWave; ++k) t += s_d[k];
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.cut_part + blockIdx.x), static_cast<unsigned long long>(t),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
   __syncthreads();
   if (!s_last) return;
   long long t = 0;
-  for (unsigned i = threadIdx.x; i < gridDim.x; i += kHgThreads)
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kThreads)
     t += static_cast<long long>(__hip_atomic_load(reinterpret_cast<unsigned long long*>(a.cut_part + i),
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   t = wave_sum(t);
@@ -790,7 +791,7 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
   if (threadIdx.x == 0) {
     long long hub_edges = 0;
 #pragma unroll
-    for (int k = 0; k < kHgThreads / kWave; ++k) hub_edges += s_d[k];
+    for (int k = 0; k < kThreads / kWave; ++k) hub_edges += s_d[k];
     *a.cut_flag = a.ctrl->m_f - hub_edges <= a.cut_edges ? 1 : 0;
     *a.cut_ticket = 0u;
   }
@@ -812,22 +813,13 @@ __global__ __launch_bounds__(kHgThreads) void hub_gather_kernel(HubGatherArgs a)
 // workgroups' last one publishes the counts (empty on a level that does not
 // cut: the peers wait for every exchange).
 constexpr int kCutThreads = 1024;
+// (kLists: several ranks, remote claims to the owner lists -- a variant of its
+// own: the list code cost the one-rank cut 53.6 -> 56.3 us a level)
+template <bool kLists>
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
-  const bool lists = a.nranks > 1;
+  constexpr bool lists = kLists;
   const bool dx = lists && a.cut_direct.active;
-  bool cut_on = !(a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B'));
-  if (cut_on && a.cut_from_marks) {
-    stamp_level_start(a.ctrl);
-    // (hub marks: the decision hub_gather makes otherwise, from the marks'
-    // degree word; every workgroup computes it, the first stores it for the
-    // bottom-up kernels)
-    const long long hub_edges = hub_mark_edges(a.g, a.hub_front);
-    cut_on = a.ctrl->m_f - hub_edges <= a.cut_edges;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.cut_flag = cut_on ? 1 : 0;
-  } else if (cut_on) {
-    cut_on = *a.cut_flag != 0;
-  }
-  if (!cut_on) {
+  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) {
     if (dx && blockIdx.x == 0) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, false);
     return;
   }
@@ -971,12 +963,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   } report{st};
 #endif
   if (a.words <= 0) return;
-  DBFS_CHECK((!a.hub_mark && !a.hub_front_marks) ||
-                 (a.fuse_scan && a.hub_front && a.g.nhubs > 0 && a.g.hub_bits && a.g.hub_deg && a.g.hub_pref &&
-                  a.g.hub_min_deg > 0 && a.nranks == 1),
-             "bu_step: hub marks need the fused finish, one rank and the hub tables");
-  DBFS_CHECK(((a.g.nhubs > 0 && a.hub_front) || !a.push) && !a.hub_mark,
-             "bu_step: pushed words need the hub kernels (and bottom-up levels mark no hubs)");
+  DBFS_CHECK((a.g.nhubs > 0 && a.hub_front) || !a.push, "bu_step: pushed words need the hub kernels");
   if (a.g.nhubs > 0 && a.hub_front) {
     const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
     // a whole 64-word unit per wave when the shard has enough units to fill
@@ -1060,7 +1047,9 @@ void bu_cut_prep(const BuArgs& a, hipStream_t st) {
                                (!a.cut_direct.active || a.cut_prep_ticket)),
              "bu_cut_prep: several ranks need owner lists, the replicated visited bitmap and a ticket");
   // (grid measured flat from 256 to 4096 workgroups)
-  bu_cut_prep_kernel<<<grid_for(a.words, kCutThreads, 2 * device_cus()), kCutThreads, 0, st>>>(a);
+  const unsigned grid = grid_for(a.words, kCutThreads, 2 * device_cus());
+  if (a.nranks > 1) bu_cut_prep_kernel<true><<<grid, kCutThreads, 0, st>>>(a);
+  else bu_cut_prep_kernel<false><<<grid, kCutThreads, 0, st>>>(a);
 }
 
 void bu_cut_apply(const BuArgs& a, hipStream_t st) {
@@ -1083,10 +1072,16 @@ void hub_gather(const HubGatherArgs& a, hipStream_t st) {
     grid = std::max(grid, grid_for(a.pull ? a.pull_words * a.pull_nranks : a.words, kHgThreads, kHgCopyGrid));
   if (a.cut_part) {
     DBFS_CHECK(a.cut_flag && a.cut_ticket && a.ctrl, "hub_gather: the hub-cut decision needs a flag, a ticket and the level state");
-    hub_gather_kernel<true><<<grid, kHgThreads, 0, st>>>(a);
+    hub_gather_kernel<true, kHgThreads, kHgPer><<<grid, kHgThreads, 0, st>>>(a);
     return;
   }
-  hub_gather_kernel<false><<<grid, kHgThreads, 0, st>>>(a);
+  // (one hub per thread: 256 workgroups for 2^16 hubs, the loads of the
+  // whole chip in flight -- 4 per thread over 16 workgroups measured 5.0 ->
+  // 5.6 us a level)
+  unsigned pgrid = grid_for(a.g.nhubs, kBlock);
+  if (a.visited || a.pull)
+    pgrid = std::max(pgrid, grid_for(a.pull ? a.pull_words * a.pull_nranks : a.words, kBlock, 4 * kHgCopyGrid));
+  hub_gather_kernel<false, kBlock, 1><<<pgrid, kBlock, 0, st>>>(a);
 }
 
 unsigned long long take_check_bu() { return take_check_local(); }

@@ -151,44 +151,6 @@ __device__ __forceinline__ uint64_t sys_load_u64(const uint64_t* p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Hub marks (backend.hpp hub_mark_words): the hubs among a new frontier word
-// `bits` (global word gw) -- their indices from the word's hub prefix (no
-// search), their bits OR-ed per marks word (a word's hubs have consecutive
-// indices: one or two atomics), their degree sum added to the slot of the
-// word's 4096-vertex group.  Per lane.
-__device__ __forceinline__ word_t* hub_mark_slot(const ShardView& g, word_t* marks, int64_t gw) {
-  return marks + hub_mark_bits_words(g.nhubs) + ((gw >> 6) & (kHubMarkSlots - 1)) * kHubMarkSlotWords;
-}
-__device__ __forceinline__ void mark_hub_word(const ShardView& g, word_t* marks, int64_t gw, word_t bits) {
-  if (!bits) return;
-  const word_t hb = g.hub_bits[gw];
-  word_t m = bits & hb;
-  if (!m) return;
-  const int64_t base = g.hub_pref[gw];
-  unsigned long long deg = 0, acc = 0;
-  int64_t accw = -1;
-  for (; m; m &= m - 1) {
-    const int b = __builtin_ctzll(m);
-    const int64_t h = base + __popcll(hb & ((1ull << b) - 1ull));
-    DBFS_DCHECK(h < g.nhubs && g.hub_vertex[h] == gw * 64 + b, 15, h);
-    if ((h >> 6) != accw) {
-      if (accw >= 0) atomicOr(reinterpret_cast<unsigned long long*>(marks + accw), acc);
-      accw = h >> 6;
-      acc = 0;
-    }
-    acc |= 1ull << (h & 63);
-    deg += g.hub_deg[h];
-  }
-  atomicOr(reinterpret_cast<unsigned long long*>(marks + accw), acc);
-  atomicAdd(reinterpret_cast<unsigned long long*>(hub_mark_slot(g, marks, gw)), deg);
-}
-// the hub-cut decision's hub edges: the slots' sum
-__device__ __forceinline__ long long hub_mark_edges(const ShardView& g, const word_t* marks) {
-  long long s = 0;
-  for (int k = 0; k < kHubMarkSlots; ++k) s += static_cast<long long>(marks[hub_mark_bits_words(g.nhubs) + k * kHubMarkSlotWords]);
-  return s;
-}
-
 // Frontier push (backend.hpp FrontierTable): word w of this rank's slice to
 // every peer's window, write-through.
 __device__ __forceinline__ void push_frontier_word(const FrontierTable* t, int rank, int nranks, int64_t w,

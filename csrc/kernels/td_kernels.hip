@@ -369,9 +369,9 @@ __device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v
 // of this shard): level, frontier bit, and the wave's work-list entries of
 // the next level with one packed atomic (count << kSparseEdgeBits | edges)
 // for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
-// (kMarks: the settled hubs also marked, TdSparseArgs::hub_mark -- a variant of
-// its own: the code costs the plain kernels 8 VGPRs, an occupancy step)
-template <int kItems, bool kMarks = false>
+// (kHx: hub-split levels, TdSparseArgs::hx_bits -- a variant of its own: the
+// diversion's code in every kernel cost td_sparse_bits 21 -> 30 us a level)
+template <int kItems, bool kHx = false>
 __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   if (!__ballot(claimed != 0)) return;
@@ -390,13 +390,7 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
       re[k] = ro[r + 1];
     }
   }
-  if constexpr (kMarks) {
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-      if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.hub_min_deg))
-        mark_hub_word(a.g, a.hub_mark, v[k] >> 6, 1ull << (v[k] & 63));
-  }
-  if (a.hx_bits) hx_divert<kItems>(a, v, claimed, rs, re);
+  if constexpr (kHx) hx_divert<kItems>(a, v, claimed, rs, re);
   unsigned long long tm[kItems];
   long long incl[kItems], cbase[kItems], ebase[kItems];
   long long ctot = 0, etot = 0;
@@ -555,7 +549,7 @@ __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, 
 // space the grid strides over.
 // (bx / gx: this workgroup and the workgroups taking part -- the kernel's, or
 // the one last workgroup of a fused tiny level, TdSparseArgs::fuse_apply)
-template <int kThreads>
+template <int kThreads, bool kHx = false>
 __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int s_last;
@@ -615,7 +609,7 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
       const word_t bit = 1ull << (v[k] & 63);
       if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
     }
-    sparse_settle<kItems>(a, v, claimed);
+    sparse_settle<kItems, kHx>(a, v, claimed);
   }
   __syncthreads();
   if (t == 0) {
@@ -650,9 +644,9 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
   direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
 }
 
-template <int kThreads>
+template <int kThreads, bool kHx = false>
 __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
-  sparse_apply<kThreads>(a, blockIdx.x, gridDim.x);
+  sparse_apply<kThreads, kHx>(a, blockIdx.x, gridDim.x);
 }
 
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
@@ -661,7 +655,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
 // their owners' lists and td_sparse_apply finishes the level after the
 // exchange.  kThreads = 1024: 2 edges per thread per block.
 constexpr int kTdSparseThreads = 1024;
-template <int kThreads, bool kMarks = false>
+template <int kThreads, bool kHx = false>
 __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
@@ -675,7 +669,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
       // (the fused owner side waits for the peers all the same: a collective)
-      if (a.fuse_apply) sparse_apply<kThreads>(a, 0, 1);
+      if (a.fuse_apply) sparse_apply<kThreads, kHx>(a, 0, 1);
     }
     return;
   }
@@ -732,7 +726,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       }
     }
     // (B) finish the wave's claimed vertices
-    sparse_settle<kItems, kMarks>(a, v, claimed);
+    sparse_settle<kItems, kHx>(a, v, claimed);
   }
   if (a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
@@ -760,7 +754,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     // a tiny level (fuse_apply): this workgroup is also the owner side --
     // the peers' lists, their claims and the folded level end -- instead of
     // a td_sparse_apply launch
-    if (a.fuse_apply) sparse_apply<kThreads>(a, 0, 1);
+    if (a.fuse_apply) sparse_apply<kThreads, kHx>(a, 0, 1);
     return;
   }
 
@@ -798,7 +792,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
 // claims, owner lists and settling as td_sparse.  The level ends in the last
 // workgroup of a two-level ticket.
 constexpr int kBitsPre = 4;
-template <int kItems, bool kMarks = false>
+template <int kItems>
 __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) {
   __shared__ long long s_incl[kBlock];  // per wave: the step's inclusive degree prefixes
   __shared__ eid_t s_rs[kBlock];        // ... and row starts
@@ -902,7 +896,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
           }
         }
         // (B) finish the wave's claimed vertices
-        sparse_settle<kItems, kMarks>(a, v, claimed);
+        sparse_settle<kItems>(a, v, claimed);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();  // (the next step overwrites w_incl / w_rs)
@@ -1269,8 +1263,8 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
-  DBFS_CHECK(!a.hub_mark || (!a.lists && a.g.hub_min_deg > 0 && a.g.nhubs > 0 && a.g.hub_pref),
-             "td_sparse: hub marks are one-rank and need the hub tables");
+  DBFS_CHECK(!a.hx_bits || (!a.from_bits && a.lists && a.hx_tot && a.hx_out),
+             "td_sparse: hub-split levels are multi-rank list levels (not read from a bitmap)");
   if (a.from_bits) {
     // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
     // wave (RMAT-26, one rank: 1024 workgroups, 16 groups on the ticket)
@@ -1278,15 +1272,14 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
     DBFS_CHECK(a.group_ticket, "td_sparse from a bitmap needs the group tickets");
     // (an empty shard still runs one workgroup: the level's finish)
     const unsigned grid = grid_for(nunits, kUnitsPerBlock, std::min<int64_t>(kMaxFusedGrid, 1024));
-    if (a.hub_mark) td_sparse_bits_kernel<4, true><<<grid, kBlock, 0, st>>>(a);
-    else td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
+    td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
     return;
   }
   // 1024-thread workgroups, two edges per thread per block: a sparse level's
   // few blocks get four times the waves (measured against 256 threads / 8
   // edges: RMAT-26 1479 / 1469 -> 1502 / 1481 GTEPS, level 0 9.8 -> 6.7 us;
   // RMAT-22 top-down only 90.5 / 90.8 -> 91.8 / 92.2)
-  if (a.hub_mark) td_sparse_kernel<kTdSparseThreads, true><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
+  if (a.hx_bits) td_sparse_kernel<kTdSparseThreads, true><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
   else td_sparse_kernel<kTdSparseThreads><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
 }
 
@@ -1323,8 +1316,9 @@ void frontier_selftest(const FrontierTable* t, int rank, int nranks, int64_t wor
 
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {
   // (1024 threads, two ids each: as td_sparse)
-  td_sparse_apply_kernel<kTdSparseThreads>
-      <<<static_cast<unsigned>(std::max<int64_t>(1, a.grid)), kTdSparseThreads, 0, st>>>(a);
+  const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, a.grid));
+  if (a.hx_bits) td_sparse_apply_kernel<kTdSparseThreads, true><<<grid, kTdSparseThreads, 0, st>>>(a);
+  else td_sparse_apply_kernel<kTdSparseThreads><<<grid, kTdSparseThreads, 0, st>>>(a);
 }
 
 void hub_visited(const HubVisitedArgs& a, hipStream_t st) {

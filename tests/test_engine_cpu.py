@@ -651,36 +651,6 @@ def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs, narrow):
         assert bfs.validate(src)
 
 
-@pytest.mark.parametrize("mode,alpha", [("do", 24.0), ("do", 1e9), ("do", 2.0), ("bu", 24.0)])
-@pytest.mark.parametrize("cut_edges", [0, 1 << 40])
-@pytest.mark.parametrize("narrow,max_hubs", [(1, 300), (0, None), (1, None)])
-def test_hub_marks(rt, mode, alpha, cut_edges, narrow, max_hubs):
-    """Hub marks (bu_hub_marks): every chain marks the hubs among the vertices
-    it settles and clears the other buffer, the bottom-up levels stage the
-    previous chain's marks instead of a hub_gather (the CPU bottom-up step
-    checks them against the frontier hubs and their degree sum), and the hub
-    cut is decided from the marks' degree word.  Levels exact, level records
-    equal to the run without marks, over top-down / bottom-up switches early
-    and late, cut forced on and off, narrow and wide levels."""
-    p = dbfs.rmat_params(13, 16, 11)
-    csr = dbfs.host_csr_from_params(p)
-    bfs = dbfs.BFS(p, rt, mode=mode, alpha=alpha, beta=24.0, max_hubs=max_hubs)
-    bfs.engine.set_option("bu_cut_edges", cut_edges)
-    bfs.engine.set_option("bu_cut_mf_frac", 1.0)
-    bfs.engine.set_option("narrow_levels", narrow)
-    assert bfs.graph.nhubs > 0
-    for src in bfs.sample_roots(4, seed=5) + [0]:
-        recs = []
-        for marks in (0, 1):
-            bfs.engine.set_option("bu_hub_marks", marks)
-            res = bfs.run(src)
-            assert np.array_equal(bfs.levels(), _oracle(csr, src))
-            recs.append([(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in res.levels])
-        assert recs[0] == recs[1]
-        if mode == "bu":
-            assert set("".join(r[0] for r in recs[1])) <= {"B"}
-
-
 @pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("mode", ["do", "td"])
 def test_hub_split_top_down_levels(P, mode):

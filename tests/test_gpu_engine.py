@@ -1016,29 +1016,6 @@ def test_hub_cut_bottom_up_gpu(gpu_runtime, max_hubs, whole):
                 _check(bfs, csr, src)
 
 
-@pytest.mark.parametrize("max_hubs", [500, None])
-def test_hub_marks_gpu(gpu_runtime, max_hubs):
-    """Hub marks (bu_hub_marks): the settling kernels (update, td_sparse,
-    bottom-up) mark the frontier hubs, bottom-up levels stage the previous
-    chain's marks instead of a hub_gather launch, and the hub cut is decided in
-    bu_cut_prep from the marks' degree word -- exact against the oracle over
-    early and late switches, bottom-up-only runs, cut on / default / off,
-    narrow and wide levels, and many runs back to back on one engine (the
-    buffers' clearing protocol)."""
-    p = dbfs.rmat_params(18, 16, 61)
-    csr = dbfs.host_csr_from_params(p)
-    for mode, alpha, narrow in [("do", 24.0, 1), ("do", 2.0, 1), ("do", 1e9, 1), ("bu", 24.0, 1), ("do", 2.0, 0)]:
-        bfs = dbfs.BFS(p, gpu_runtime, mode=mode, alpha=alpha, max_hubs=max_hubs)
-        assert bfs.graph.nhubs > 0
-        bfs.engine.set_option("narrow_levels", narrow)
-        bfs.engine.set_option("bu_hub_marks", 1)
-        for cut in [None, 1 << 40, 0]:
-            if cut is not None:
-                bfs.engine.set_option("bu_cut_edges", cut)
-            for src in bfs.sample_roots(3, seed=19):
-                _check(bfs, csr, src)
-
-
 def _bench_peer(args, timeout=200, **env_extra):
     import json
     import subprocess
