@@ -318,7 +318,6 @@ class CpuBackend final : public Backend {
   }
   void level_finish(const LevelFinishArgs& a) override {
     if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
-    if (a.hx.bits) hx_append(a.hx);
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
     level_ctrl_finish(c, a.stats[2], a.stats[3], a.seed, a.seed ? nullptr : a.rec);
     *a.ctrl = c;
@@ -331,6 +330,8 @@ class CpuBackend final : public Backend {
       a.mailbox->reached = c.reached;
       a.mailbox->level = a.seed ? -1 : a.level;
     }
+    // (hub-split entries for a top-down next level only, as the HIP finish)
+    if (a.hx.bits && !c.done && c.dir == 'T') hx_append(a.hx);
   }
 
   // Sparse top-down level (see the HIP kernel): claims in the replicated

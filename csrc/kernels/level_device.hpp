@@ -119,11 +119,19 @@ __device__ __forceinline__ void hx_append(const HxAppendArgs& h) {
 // Several ranks: a level's end after its totals' all-reduce, by every thread
 // of one workgroup of kThreads -- on a live chain (or the seed) the hub-split
 // entries of the next level (fin.hx), then thread 0's decision.
+// (the entries only after the decision, and only for a top-down next level:
+// a bottom-up one reads no work list, and appending the thousands of frontier
+// hubs of its input cost a P = 8 replay 300 us in this one workgroup)
 template <int kThreads>
 __device__ __forceinline__ void level_finish_block(const LevelFinishArgs& a) {
   if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
-  if (a.hx.bits) hx_append<kThreads>(a.hx);
-  if (threadIdx.x == 0) level_finish_device(a);
+  __shared__ int s_append;
+  if (threadIdx.x == 0) {
+    level_finish_device(a);
+    s_append = a.hx.bits && !a.ctrl->done && a.ctrl->dir == 'T';
+  }
+  __syncthreads();
+  if (s_append) hx_append<kThreads>(a.hx);
 }
 
 }  // namespace kern

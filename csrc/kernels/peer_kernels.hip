@@ -92,9 +92,9 @@ __device__ __forceinline__ void push_pieces(const PeerPushArgs& a, int nthreads)
 __device__ __forceinline__ void unpack_pieces(const PeerUnpackArgs& a, int64_t gt, int64_t nt) {
   if (a.has_finish) {
     // a level's end: the first workgroup sums the totals (and a hub-split
-    // level's hub bits), then finishes the level -- the next level's hub-split
-    // entries, thread 0's decision (the stamp the host and the next level's
-    // kernels read)
+    // level's hub bits), then finishes the level -- thread 0's decision (the
+    // stamp the host and the next level's kernels read), then for a top-down
+    // next level its hub-split entries
     if (blockIdx.x == 0) {
       for (int64_t i = threadIdx.x; i < a.sum_count; i += blockDim.x) {
         uint64_t acc = 0;
