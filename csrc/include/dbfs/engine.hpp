@@ -276,7 +276,12 @@ struct EngineOptions {
   // part of each frontier hub's row (ShardView::hx_off), claims local, no
   // exchange -- their bits ride the level end.  Replaces the owner expanding a
   // hub's whole row and shipping its claims (bfs.cu:577-586, 143).  0: off.
-  int hx_levels = 4;
+  // Off by default: shadow ranks of RMAT-26 at P = 8 (8 roots, ranks 0 / 7)
+  // measured it slower -- levels 0-2 of root 13702079 5.6 / 12.4 / 57.3 ->
+  // 11.8 / 19.9 / 85.4 us: the hub-split chains lose the fused tiny-level
+  // launch and the folded level end, and the split td_sparse of the hubs'
+  // parts ran 24 -> 54 us (profiles/r4_s3_shadow_*).
+  int hx_levels = 0;
   // One rank, device loop, hubs: a first bottom-up level whose frontier has
   // at most bu_cut_edges edges outside the hubs claims those vertices'
   // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
@@ -289,8 +294,12 @@ struct EngineOptions {
   // 37 % and more)
   double bu_cut_mf_frac = 0.25;
   // ... also with several ranks (the non-hub frontier's remote claims through
-  // the owner lists, bu_cut_apply on the owners)
-  bool bu_cut_ranks = true;
+  // the owner lists, bu_cut_apply on the owners).  Off by default: at P = 8
+  // (shadow ranks, RMAT-26) the late-switch first bottom-up level took
+  // 119 -> 167 us with it -- bu_cut_prep 67 us + bu_cut_apply 10 us against the
+  // 33 us the cut saves a rank's bottom-up kernel (105 -> 72 us), whose share
+  // of the level already shrank 8x (profiles/r4_s3_shadow_trace_*).
+  bool bu_cut_ranks = false;
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)

@@ -728,6 +728,7 @@ def test_hub_cut_several_ranks(P, narrow, alpha, max_hubs):
         b = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=24.0, max_hubs=max_hubs)
         b.engine.set_option("narrow_levels", narrow)
         b.engine.set_option("bu_cut_mf_frac", 1.0)  # (enqueue it on every first bottom-up level)
+        b.engine.set_option("bu_cut_ranks", 1)  # (opt-in with several ranks)
         out = []
         for cut in (1 << 40, 0):
             b.engine.set_option("bu_cut_edges", cut)

@@ -1056,13 +1056,14 @@ def test_peer_slot_rounds_build_and_ingest(tmp_path):
 
 
 @pytest.mark.parametrize("opts", [["xfuse_edges=4096"], ["bu_merge_visited=0"],
-                                  ["xfuse_edges=4096", "bu_merge_visited=0"]])
+                                  ["xfuse_edges=4096", "bu_merge_visited=0"],
+                                  ["hx_levels=4", "bu_cut_ranks=1", "bu_cut_mf_frac=1"]])
 def test_peer_multirank_options(opts):
-    """The two multi-rank options round 3 left pending -- tiny sparse levels
-    fused into one launch (xfuse_edges) and bottom-up levels without the
-    visited merge of the gathered frontier (bu_merge_visited=0) -- over the
-    peer transport with 4 processes on device 0 at RMAT-18: every timed root
-    validated."""
+    """The multi-rank options -- tiny sparse levels fused into one launch
+    (xfuse_edges), bottom-up levels without the visited merge of the gathered
+    frontier (bu_merge_visited=0), and the opt-in hub-split top-down levels and
+    multi-rank hub cut (hx_levels, bu_cut_ranks) -- over the peer transport with
+    4 processes on device 0 at RMAT-18: every timed root validated."""
     args = ["--gpus", "4", "--scale", "18", "--steps", "6", "--warmup", "1"]
     for o in opts:
         args += ["--opt", o]

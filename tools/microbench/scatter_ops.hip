@@ -10,6 +10,8 @@
 //   byte-store    plain byte store, random vertex of a 64 MiB byte map
 //   xcd-byte      plain byte store into the calling XCD's 8 MiB slice
 //   rand-load     8-B load of a random word of the 8 MiB bitmap (dependent use)
+//   probe-store   visited-bit probe, then the byte store (a direct top-down edge)
+//   xcd-probe-st  the same with targets in the calling XCD's 1/8 of the range
 //
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/scatter_ops tools/microbench/scatter_ops.hip
 #include <hip/hip_runtime.h>
@@ -75,6 +77,15 @@ __global__ __launch_bounds__(kThreads) void scatter_kernel(unsigned long long* w
       const unsigned long long slice = nwords * 8;
       const unsigned long long v = x * slice + (r >> 6) % slice;
       bytes[v] = 1;
+    } else if constexpr (kMode == 6) {
+      // byte store only where a probe of the (static) bitmap says unvisited
+      const unsigned long long v = (r >> 6) % (nwords * 64);
+      if (!(words[v >> 6] & (1ull << (v & 63)))) bytes[v] = 1;
+    } else if constexpr (kMode == 7) {
+      // the same, targets in the calling XCD's slice
+      const unsigned long long slice = nwords * 8;
+      const unsigned long long v = x * slice + (r >> 6) % slice;
+      if (!(words[v >> 6] & (1ull << (v & 63)))) bytes[v] = 1;
     } else {
       const unsigned long long w = (r >> 6) % nwords;
       acc += words[w];
@@ -125,7 +136,9 @@ double run(const char* name, unsigned long long* words, unsigned char* bytes, un
 }
 
 int main(int argc, char** argv) {
-  const unsigned long long nwords = 1ull << 20;  // 8 MiB bitmap = 64 Mi vertices
+  // argv[2]: vertices (default 64 Mi: an 8 MiB bitmap); 4847616 = soc-LiveJournal1's size
+  const unsigned long long nverts = argc > 2 ? std::strtoull(argv[2], nullptr, 10) : (1ull << 26);
+  const unsigned long long nwords = (nverts + 511) / 512 * 8;
   const unsigned blocks = argc > 1 ? static_cast<unsigned>(std::atoi(argv[1])) : 24576;  // 100 M ops
   unsigned long long *words, *scal;
   unsigned char* bytes;
@@ -140,5 +153,7 @@ int main(int argc, char** argv) {
   run<3>("byte-store", words, bytes, nwords, scal, blocks, 3);
   run<4>("xcd-byte", words, bytes, nwords, scal, blocks, 3);
   run<5>("rand-load", words, bytes, nwords, scal, blocks, 3);
+  run<6>("probe-store", words, bytes, nwords, scal, blocks, 3);
+  run<7>("xcd-probe-st", words, bytes, nwords, scal, blocks, 3);
   return 0;
 }
