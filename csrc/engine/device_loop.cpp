@@ -71,6 +71,7 @@ class DeviceLoop {
   int64_t sparse_cap_ = 0;
   int64_t list_max_ = 0, xsparse_lim_ = 0, fuse_cap_ = 0;
   bool lists_unlimited_ = false, counted_ = false;
+  bool range_ok_ = false;  // one rank: range-staged top-down levels available
   int bin_shift_ = 12;
   int64_t nbins_ = 0;
   bool binned_ = false;
@@ -243,6 +244,14 @@ void DeviceLoop::setup() {
     e_.bin_total_ = DBuf<int64_t>(be_, static_cast<size_t>(nbins_));
     e_.bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins_ * kBinGrid));
     e_.bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(e_.g_.nnz()));  // a level's frontier edges <= nnz
+  }
+  // One rank: range-staged top-down levels (the rows' range split points,
+  // built once per graph; the work list's entry -> row map comes from the
+  // sparse levels' machinery)
+  range_ok_ = false;
+  if (!xc_ && sparse_ && opt_.td_range_edges > 0 && opt_.mode != Mode::BottomUp) {
+    if (!e_.range_built_) e_.build_range_split();
+    range_ok_ = e_.range_count_ > 0;
   }
   if (e_.n_active_ < 0) {
     // (outside the timed window, once) the mean degree of an edge's endpoint
@@ -730,9 +739,18 @@ void DeviceLoop::emit_dense(Chain& c) {
   UpdateArgs tu = ua_;
   ta.next = e_.next_.data();
   ta.next_bytes = e_.next_bytes_.data();
+  // range-staged (one rank, large levels): every probe in LDS, no hub filter
+  const bool ranged = range_ok_ && c.pf != 'I' && (c.mf_hint < 0 || c.mf_hint >= static_cast<double>(opt_.td_range_edges));
+  if (ranged) {
+    res_.chains.back().ranged = true;
+    ta.range_split = e_.range_split_.data();
+    ta.range_qv = e_.qv_[L & 1].data();
+    ta.ranges = e_.range_count_;
+    ta.range_span = e_.range_span_;
+  }
   // (skipped for levels predicted well below the filter's threshold: the
   // snapshot kernel would only find its gate closed)
-  if (gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
+  if (!ranged && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
       (c.mf_hint < 0 || c.mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
     // large levels: the hubs' visited bits, staged in LDS by td_expand
     if (!e_.td_hub_vis_.data())

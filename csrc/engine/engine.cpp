@@ -77,6 +77,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
+  else if (name == "td_range_edges") o.td_range_edges = static_cast<int64_t>(v);
+  else if (name == "td_range_words") o.td_range_words = static_cast<int64_t>(v);
   else if (name == "td_bin_log2_bins") o.td_bin_log2_bins = static_cast<int64_t>(v);
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
@@ -129,6 +131,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
+          {"td_range_edges", static_cast<double>(o.td_range_edges)},
+          {"td_range_words", static_cast<double>(o.td_range_words)},
           {"td_bin_log2_bins", static_cast<double>(o.td_bin_log2_bins)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
@@ -721,6 +725,39 @@ void Engine::alloc_bitmap_state() {
   if (exchange()) comm_.allgather(za.out, zdeg_.data(), static_cast<size_t>(W) * sizeof(word_t));
   be_.synchronize();
   bitmap_ready_ = true;
+}
+
+// Range-staged top-down levels: R ranges of at most kRangeWords visited
+// words, each a multiple of 64 vertices and of the id bucket sort_rows_by_id
+// orders long rows by (2^shift ids), and the rows' split positions at the
+// R - 1 inner boundaries ((R - 1) x rows x 4 B: soc-LiveJournal1's size 194 MB).
+// Once per graph, outside any timed window; range_count_ stays 0 when the graph
+// does not qualify (several ranks, rows not in id order, too many vertices).
+void Engine::build_range_split() {
+  range_built_ = true;
+  range_count_ = 0;
+  range_split_.reset();
+  const int64_t n = part_.n;
+  if (part_.nranks != 1 || !g_.col_by_id() || n <= 0 || g_.rows() != n || g_.nnz() <= 0 ||
+      g_.nnz() > (int64_t(1) << 32))
+    return;
+  int bits = 0;
+  while ((int64_t(1) << bits) < n) ++bits;
+  const int shift = bits > 12 ? bits - 12 : 0;
+  const int64_t align = std::max<int64_t>(kWordBits, int64_t(1) << shift);
+  const int64_t cap = std::min<int64_t>(std::max<int64_t>(opt_.td_range_words, 1), kRangeWords) * kWordBits;
+  for (int R = static_cast<int>(div_up(n, cap)); R <= kRangeMax; ++R) {
+    const int64_t span = div_up(div_up(n, R), align) * align;
+    if (span > cap) continue;
+    const int ranges = static_cast<int>(div_up(n, span));
+    if (ranges > 1) {
+      range_split_ = DBuf<uint32_t>(be_, static_cast<size_t>(ranges - 1) * static_cast<size_t>(n));
+      be_.range_split(g_.view().row_off, g_.view().col, n, span, shift, ranges, range_split_.data());
+    }
+    range_count_ = ranges;
+    range_span_ = span;
+    return;
+  }
 }
 
 void Engine::alloc_ref_state() {

@@ -164,6 +164,15 @@ struct EngineOptions {
   // binned level: 256 / 512 / 1024 bins 407 / 417 / 441 us (more bins: the
   // fill pass scatters into more open lines).
   int64_t td_bin_log2_bins = 8;
+  // One rank, graphs of at most kRangeMax x kRangeWords x 64 vertices with
+  // id-ordered rows: dense top-down levels predicted at >= td_range_edges
+  // frontier edges are range-staged (TdArgs::range_split: the vertex ranges
+  // swept one at a time with their visited bits in LDS, claims deduplicated
+  // there) instead of td_expand's scattered visited probes; 0 disables.
+  int64_t td_range_edges = int64_t(1) << 22;
+  // ... ranges of at most this many visited words (<= kRangeWords; smaller
+  // forces more ranges -- tests on small graphs)
+  int64_t td_range_words = kRangeWords;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
@@ -374,6 +383,8 @@ struct ChainRecord {
   // several ranks: its output frontier pushed by its kernels (no gather in
   // its level end; EngineOptions::direct_frontier)
   bool push = false;
+  // one rank: a range-staged dense top-down chain (TdArgs::range_split)
+  bool ranged = false;
 };
 
 struct RunResult {
@@ -415,7 +426,10 @@ class Engine {
   std::vector<int64_t> gather_parents(int64_t source);
   int64_t global_directed_edges() const { return total_directed_; }
   const EngineOptions& options() const { return opt_; }
-  void set_options(const EngineOptions& o) { opt_ = o; }
+  void set_options(const EngineOptions& o) {
+    if (o.td_range_words != opt_.td_range_words) range_built_ = false;  // (the split points depend on it)
+    opt_ = o;
+  }
 
  private:
   friend class DeviceLoop;
@@ -483,6 +497,12 @@ class Engine {
   DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
   // binned top-down levels (one rank): bin counts / positions, bin starts, targets
   DBuf<int64_t> bin_total_;
+  // range-staged top-down levels (TdArgs::range_split): built once per graph
+  DBuf<uint32_t> range_split_;
+  int range_count_ = 0;       // 0: not available on this graph
+  int64_t range_span_ = 0;
+  bool range_built_ = false;
+  void build_range_split();
   DBuf<uint32_t> bin_cnt_;
   DBuf<vid_t> bin_buf_;
   int64_t list_stride_ = 0;

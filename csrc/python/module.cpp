@@ -606,7 +606,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
                              [](const RunResult& r) {
                                py::list out;
                                for (const auto& c : r.chains)
-                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.hx_words, c.cut, c.push));
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.hx_words, c.cut, c.push, c.ranged));
                                return out;
                              })
       .def("level_dicts", &level_dicts);

@@ -676,6 +676,35 @@ def test_td_direct_levels_gpu(gpu_runtime, mode, direct_edges):
 
 
 @pytest.mark.parametrize("mode", ["td", "do"])
+@pytest.mark.parametrize("scale,words", [(17, None), (17, 256), (18, 512), (16, 64)])
+def test_td_range_levels_gpu(gpu_runtime, mode, scale, words):
+    """One rank, range-staged dense top-down levels (td_range_kernel: vertex
+    ranges swept one at a time, their visited bits in LDS, each row's part in
+    the range from the rows' id-ordered split points): forced on every dense
+    level (td_range_edges = 1), with one range (the default on these graphs)
+    or several (td_range_words: 8 to 16 ranges, RMAT hubs' rows of > 4096
+    entries ordered by id bucket only); exact against the oracle on RMAT, a
+    uniform graph and a star whose centre's row spans many edge blocks."""
+    graphs = [dbfs.rmat_params(scale, 16, 53), dbfs.uniform_params(1 << scale, 12 << scale, 59)]
+    n = 1 << scale
+    hub = np.zeros(n - 1, dtype=np.uint32)
+    star = dbfs.build_csr(n, hub, np.arange(1, n, dtype=np.uint32))
+    for g in graphs + [star]:
+        csr = g if g is star else dbfs.host_csr_from_params(g)
+        bfs = dbfs.BFS(g, gpu_runtime, mode=mode)
+        bfs.engine.set_option("td_range_edges", 1)
+        if words is not None:
+            bfs.engine.set_option("td_range_words", words)
+        ranged = False
+        srcs = [0, 5] if g is star else bfs.sample_roots(3, seed=61)
+        for src in srcs:
+            res = _check(bfs, csr, src)
+            ranged = ranged or any(c[7] for c in res.chains)
+        assert ranged or mode == "do"
+        assert bfs.validate(srcs[-1])
+
+
+@pytest.mark.parametrize("mode", ["td", "do"])
 @pytest.mark.parametrize("bin_edges", [1, 1 << 20, 0])
 def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     """One rank, binned top-down levels (targets binned by vertex range, one
