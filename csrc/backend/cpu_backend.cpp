@@ -71,6 +71,7 @@ class CpuBackend final : public Backend {
       const int64_t n = a.scan.nunits;
       std::vector<int64_t> c(a.scan.unit_cnt, a.scan.unit_cnt + n), d(a.scan.unit_deg, a.scan.unit_deg + n);
       scan_units(a.scan);
+      if (a.fold_scan) return;  // (the prefixes stay: the next compaction reads them)
       std::copy(c.begin(), c.end(), a.scan.unit_cnt);
       std::copy(d.begin(), d.end(), a.scan.unit_deg);
       return;

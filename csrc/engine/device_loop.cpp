@@ -44,6 +44,7 @@ class DeviceLoop {
     bool in_gathered = false;  // the input frontier is global already
     bool fused_scan = false;   // the chain's last kernel finishes the level
     bool level_ended = false;  // ... and also ran its level end (direct exchange)
+    bool folded = false;       // ... and also scanned its unit prefixes (UpdateArgs::fold_scan)
     bool cut = false;          // several ranks: a hub-cut bottom-up level was enqueued
     // several ranks: the output frontier pushed to the peers by the producing
     // kernel (EngineOptions::direct_frontier), and the input frontier's pushed
@@ -72,6 +73,7 @@ class DeviceLoop {
   int64_t list_max_ = 0, xsparse_lim_ = 0, fuse_cap_ = 0;
   bool lists_unlimited_ = false, counted_ = false;
   bool range_ok_ = false;  // one rank: range-staged top-down levels available
+  double vis_hint_ = -1.0;  // the next enqueued level's visited degree sum at its start (< 0 unknown)
   int bin_shift_ = 12;
   int64_t nbins_ = 0;
   bool binned_ = false;
@@ -511,7 +513,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
   }
   res_.chains.back().cut = c.cut && P_ > 1;  // (the owner-list exchange)
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
-  enq_fused_[L] = c.fused_scan && d != 'S';
+  enq_fused_[L] = c.fused_scan && d != 'S' && !c.folded;
   if (xc_ && !c.level_ended)
     finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] && !c.push, d == 'S' && hx_chain(L));
   if (opt_.phase_timing) evs_[L] = {ev0, be_.record_event()};
@@ -709,6 +711,9 @@ void DeviceLoop::fuse_update(Chain& c, UpdateArgs& tu) {
   if (!e_.td_tot_.data()) e_.td_tot_ = DBuf<int64_t>(be_, static_cast<size_t>(2 * kMaxFusedGrid + 2 * kFusedGroups));
   tu.fuse_scan = true;
   tu.scan = scan_args(c.L, false, enq_dir_[c.L], c.cap);
+  // small graphs: the next compaction's unit prefixes too (no scan_units launch)
+  tu.fold_scan = opt_.fold_scan && e_.nunits_ <= kFoldScanUnits;
+  c.folded = tu.fold_scan;
   tu.tot = e_.td_tot_.data();
   if (opt_.td_group_ticket) tu.group_ticket = group_tickets();
   c.fused_scan = true;
@@ -740,7 +745,8 @@ void DeviceLoop::emit_dense(Chain& c) {
   ta.next = e_.next_.data();
   ta.next_bytes = e_.next_bytes_.data();
   // range-staged (one rank, large levels): every probe in LDS, no hub filter
-  const bool ranged = range_ok_ && c.pf != 'I' && (c.mf_hint < 0 || c.mf_hint >= static_cast<double>(opt_.td_range_edges));
+  const bool ranged = range_ok_ && c.pf != 'I' && c.mf_hint >= static_cast<double>(opt_.td_range_edges) &&
+                      vis_hint_ >= 0 && vis_hint_ <= opt_.td_range_vis_frac * static_cast<double>(e_.total_directed_);
   if (ranged) {
     res_.chains.back().ranged = true;
     ta.range_split = e_.range_split_.data();
@@ -1123,12 +1129,14 @@ RunResult DeviceLoop::run() {
     if (!valid) {
       int64_t cap = 0;
       const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
+      vis_hint_ = static_cast<double>(mb->vis_deg);  // (exact: level L's start)
       enqueue_level(L, f, cap, static_cast<double>(mf), d1 == 'B');
     }
     prev_nf = nf;
     prev_mf = mf;
     int64_t lcap = 0;
     const char f = d1 == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
+    vis_hint_ = static_cast<double>(mb->vis_deg) + emf;  // (level L + 1's frontier joins visited)
     enqueue_level(L + 1, f, lcap, emf, d2 == 'B');
   }
   // The traversal is complete once the last stamp is seen: the stamping

@@ -77,8 +77,10 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
+  else if (name == "fold_scan") o.fold_scan = v != 0;
   else if (name == "td_range_edges") o.td_range_edges = static_cast<int64_t>(v);
   else if (name == "td_range_words") o.td_range_words = static_cast<int64_t>(v);
+  else if (name == "td_range_vis_frac") o.td_range_vis_frac = v;
   else if (name == "td_bin_log2_bins") o.td_bin_log2_bins = static_cast<int64_t>(v);
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
@@ -131,8 +133,10 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
+          {"fold_scan", o.fold_scan ? 1.0 : 0.0},
           {"td_range_edges", static_cast<double>(o.td_range_edges)},
           {"td_range_words", static_cast<double>(o.td_range_words)},
+          {"td_range_vis_frac", o.td_range_vis_frac},
           {"td_bin_log2_bins", static_cast<double>(o.td_bin_log2_bins)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},

@@ -137,6 +137,9 @@ constexpr int kUnitWaves = 4;
 constexpr int kUnitWords = kWaveWords * kUnitWaves;
 constexpr int kUnitVertices = kUnitWords * kWordBits;
 constexpr int kScanChunk = 1024;
+// At most this many units are prefix-scanned by a fused finish's last
+// workgroup (UpdateArgs::fold_scan): 32 per thread of a 256-thread workgroup.
+constexpr int kFoldScanUnits = 8192;
 // Top-down expansion handles kTdEdgesPerBlock frontier edges per workgroup.
 constexpr int kTdThreads = 256;
 constexpr int kTdItems = 8;
@@ -476,6 +479,11 @@ struct UpdateArgs {
   // last-arriving workgroup, unit statistics left unscanned (a following
   // compaction scans them first); tot[0..1] zero, reset by the last one.
   bool fuse_scan = false;
+  // ... and (graphs of at most kFoldScanUnits units) the unit prefixes the
+  // next compaction reads, scanned by the same last workgroup -- no
+  // scan_units launch between the levels (the unit statistics are stored
+  // write-through and read with agent-scope loads, as the totals)
+  bool fold_scan = false;
   ScanArgs scan;
   int64_t* tot = nullptr;
   // ... with the ticket two-level: workgroups of kFusedGroup consecutive ids

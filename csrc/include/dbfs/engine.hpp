@@ -173,6 +173,15 @@ struct EngineOptions {
   // ... ranges of at most this many visited words (<= kRangeWords; smaller
   // forces more ranges -- tests on small graphs)
   int64_t td_range_words = kRangeWords;
+  // ... and only while the visited vertices hold at most this fraction of the
+  // adjacency entries at the level's start (predicted by the host): a level
+  // whose candidates are mostly unvisited is bound by its scattered stores,
+  // which the ranges keep local in time and deduplicate; once most targets are
+  // visited the direct level's probes (at the L2 request rate) are cheaper
+  // than the ranges' per-row passes.  Measured, soc-LiveJournal1-sized graph:
+  // a 17 M-edge level at 13 % visited 404 -> 273 us ranged, the 100 M-edge
+  // level after it (86 %) 630 -> 1232 us (profiles/r4_s3_td_range_*).
+  double td_range_vis_frac = 0.3;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
@@ -256,6 +265,10 @@ struct EngineOptions {
   // (A first version with one workgroup per 4 units and totals atomics on
   // one address: level 1 of RMAT-26 38 -> 117 us.)
   bool td_fused_finish = true;
+  // ... and on graphs of at most kFoldScanUnits 4096-vertex units (2^25
+  // vertices) its last workgroup also scans the unit prefixes the next
+  // compaction reads (UpdateArgs::fold_scan): one launch less per dense level
+  bool fold_scan = true;
   // ... with a two-level ticket (UpdateArgs::group_ticket): the update runs
   // a full grid (up to kMaxFusedGrid workgroups) instead of kMaxFusedGrid / 8.
   bool td_group_ticket = true;

@@ -222,6 +222,69 @@ __device__ __forceinline__ word_t gather_level_bits(const uint8_t* p, uint8_t lv
   return bits;
 }
 
+// A unit's statistics; write-through when the fused finish's last workgroup
+// scans them (UpdateArgs::fold_scan: read there with agent-scope loads).
+__device__ __forceinline__ void store_unit_stats(const UpdateArgs& a, int64_t unit, long long c, long long d) {
+  if (a.fold_scan) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.unit_cnt + unit), static_cast<unsigned long long>(c),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.unit_deg + unit), static_cast<unsigned long long>(d),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    a.unit_cnt[unit] = c;
+    a.unit_deg[unit] = d;
+  }
+}
+
+// The fused finish's unit prefixes (UpdateArgs::fold_scan; every thread of the
+// last workgroup of kBlock threads): unit_cnt / unit_deg become the exclusive
+// prefixes over all units (at most kFoldScanUnits, a run of kFold per thread)
+// and the chunk prefixes part_cnt / part_deg zero -- what scan_units_kernel
+// leaves for the compaction.  Two passes over the run (sums, then prefixes:
+// the second pass's loads are L2 hits), a few units in flight at a time: the
+// update kernel's register allocation covers this code too.
+__device__ __forceinline__ long long agent_load_i64(const int64_t* p) {
+  return static_cast<long long>(
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void fold_unit_scan(const ScanArgs& a) {
+  constexpr int kFold = kFoldScanUnits / kBlock;
+  __shared__ long long s_fc[kBlock / kWave], s_fd[kBlock / kWave];
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const int64_t u0 = static_cast<int64_t>(t) * kFold;
+  const int64_t u1 = min(u0 + kFold, static_cast<int64_t>(a.nunits));
+  long long sc = 0, sd = 0;
+#pragma unroll 4
+  for (int64_t u = u0; u < u1; ++u) {
+    sc += agent_load_i64(a.unit_cnt + u);
+    sd += agent_load_i64(a.unit_deg + u);
+  }
+  const long long ic = wave_incl_scan(sc), id = wave_incl_scan(sd);
+  __syncthreads();  // (s_fc / s_fd: the caller's earlier LDS use is done)
+  if (lane == kWave - 1) {
+    s_fc[wv] = ic;
+    s_fd[wv] = id;
+  }
+  __syncthreads();
+  long long oc = ic - sc, od = id - sd;
+  for (int k = 0; k < wv; ++k) {
+    oc += s_fc[k];
+    od += s_fd[k];
+  }
+#pragma unroll 4
+  for (int64_t u = u0; u < u1; ++u) {
+    const long long c = agent_load_i64(a.unit_cnt + u), d = agent_load_i64(a.unit_deg + u);
+    a.unit_cnt[u] = oc;
+    a.unit_deg[u] = od;
+    oc += c;
+    od += d;
+  }
+  for (int64_t p = t; p * kScanChunk < a.nunits; p += kBlock) {
+    a.part_cnt[p] = 0;
+    a.part_deg[p] = 0;
+  }
+}
+
 // One wave per 64-word unit, kUnitsPerBlock units per workgroup; with the
 // fused finish a smaller grid strides over the units (fewer ticket arrivals).
 // kSplit waves per unit (small graphs: 4, each over 16 of its words -- a
@@ -280,10 +343,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
   }
   cnt = wave_sum(cnt);
   deg = wave_sum(deg);
-  if (kSplit == 1 && lane == 0) {
-    a.unit_cnt[unit] = cnt;
-    a.unit_deg[unit] = deg;
-  }
+  if (kSplit == 1 && lane == 0) store_unit_stats(a, unit, cnt, deg);
 }
 
 // A unit per workgroup, its kSplit (= kUnitsPerBlock) waves each over a part
@@ -305,8 +365,7 @@ __device__ __forceinline__ void update_unit_split(const UpdateArgs& a, int64_t u
       c += s_pc[k];
       d += s_pd[k];
     }
-    a.unit_cnt[unit] = c;
-    a.unit_deg[unit] = d;
+    store_unit_stats(a, unit, c, d);
   }
   __syncthreads();  // (s_pc / s_pd reused by the next unit)
 }
@@ -461,6 +520,7 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     s_c[0] = tc;
     s_d[0] = td;
   }
+  if (a.fold_scan) fold_unit_scan(a.scan);
   if constexpr (kRanks) {
     if (a.end.active) {
       __syncthreads();
@@ -789,6 +849,8 @@ void update_frontier(const UpdateArgs& a, hipStream_t st) {
   DBFS_CHECK(!a.end.active || (a.fuse_scan && a.ctrl && a.scan.stats), "update: a folded level end needs the fused finish");
   if (a.words <= 0) return;
   const int64_t nunits = (a.words + kUnitWords - 1) / kUnitWords;
+  DBFS_CHECK(!a.fold_scan || (a.fuse_scan && a.scan.nunits == nunits && nunits <= kFoldScanUnits),
+             "update: fold_scan needs the fused finish over at most kFoldScanUnits units");
   const bool split = nunits < kSplitUnits;
   const int64_t per = split ? kUnitWords : kUnitWords * kUnitsPerBlock;
   // fused finish: at most kMaxFusedGrid / 8 workgroups striding over the units

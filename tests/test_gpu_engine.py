@@ -693,6 +693,7 @@ def test_td_range_levels_gpu(gpu_runtime, mode, scale, words):
         csr = g if g is star else dbfs.host_csr_from_params(g)
         bfs = dbfs.BFS(g, gpu_runtime, mode=mode)
         bfs.engine.set_option("td_range_edges", 1)
+        bfs.engine.set_option("td_range_vis_frac", 2.0)  # (every dense level, whatever is visited)
         if words is not None:
             bfs.engine.set_option("td_range_words", words)
         ranged = False

@@ -13,7 +13,8 @@ if [ "${TESTS:-1}" = 1 ]; then
 fi
 for g in "lj:--uniform 4847571:68993773" "r22:--scale 22"; do
   n=${g%%:*}; ga=${g#*:}
-  for v in "on:" "off:--opt td_range_edges=0"; do
+  IFS='|' read -ra VS <<< "${VARIANTS:-on:|off:--opt td_range_edges=0}"
+  for v in "${VS[@]}"; do
     vn=${v%%:*}; va=${v#*:}
     timeout -k 10 300 python bench.py $ga --mode td --steps 16 --warmup 3 --heldout-roots 0 --secondary none --no-int32-pass $va ${TD_ARGS} > gpurun_out/${TAG}_td_${n}_${vn}.json 2> gpurun_out/${TAG}_td_${n}_${vn}.err || { tail -20 gpurun_out/${TAG}_td_${n}_${vn}.err; exit 1; }
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], '%.1f GTEPS %.4f ms validated %s' % (d['value'], d['ms_per_step'], d['validated_roots']), [round(l[1]*1000,1) for l in d['level_clock']['levels']])" gpurun_out/${TAG}_td_${n}_${vn}.json "$n $vn"
