@@ -529,10 +529,18 @@ __device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v
 // for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
 // (kHx: hub-split levels, TdSparseArgs::hx_bits -- a variant of its own: the
 // diversion's code in every kernel cost td_sparse_bits 21 -> 30 us a level)
-template <int kItems, bool kHx = false>
+// kWg: a workgroup-uniform call (every wave of a workgroup of at most
+// kSettleWaves waves): the waves' packed counts summed in LDS and ONE atomic
+// per workgroup on the counter, each wave's base from the waves before it --
+// a level settling thousands of waves' claims queued that many returning
+// atomics on one address (~90 per us).
+constexpr int kSettleWaves = 1024 / kWave;
+template <int kItems, bool kHx = false, bool kWg = false>
 __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
-  if (!__ballot(claimed != 0)) return;
+  if constexpr (!kWg) {
+    if (!__ballot(claimed != 0)) return;
+  }
   const int lane = lane_id();
   const eid_t* __restrict__ ro = a.g.row_off;
   const int64_t lo = a.g.lo;
@@ -567,12 +575,29 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
     ctot += __popcll(tm[k]);
     etot += readlane_i64(incl[k], kWave - 1);
   }
-  if (!ctot) return;
   unsigned long long old = 0;
-  if (lane == 0)
-    old = atomicAdd(a.counter, (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
-                                   static_cast<unsigned long long>(etot));
-  old = __shfl(old, 0, kWave);
+  const unsigned long long packed = (static_cast<unsigned long long>(ctot) << kSparseEdgeBits) +
+                                    static_cast<unsigned long long>(etot);
+  if constexpr (kWg) {
+    __shared__ unsigned long long s_pk[kSettleWaves], s_pbase;
+    const int wv = static_cast<int>(threadIdx.x >> 6);
+    if (lane == 0) s_pk[wv] = packed;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long sum = 0;
+      for (int k = 0; k < static_cast<int>(blockDim.x >> 6); ++k) sum += s_pk[k];
+      s_pbase = sum ? atomicAdd(a.counter, sum) : 0ull;
+    }
+    __syncthreads();
+    old = s_pbase;
+    for (int k = 0; k < wv; ++k) old += s_pk[k];
+    __syncthreads();  // (s_pk / s_pbase reused by the next call)
+    if (!ctot) return;
+  } else {
+    if (!ctot) return;
+    if (lane == 0) old = atomicAdd(a.counter, packed);
+    old = __shfl(old, 0, kWave);
+  }
   const long long p0 = static_cast<long long>(old >> kSparseEdgeBits);
   const long long q0 = static_cast<long long>(old & kEdgeMask);
 #pragma unroll
@@ -707,7 +732,7 @@ __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, 
 // space the grid strides over.
 // (bx / gx: this workgroup and the workgroups taking part -- the kernel's, or
 // the one last workgroup of a fused tiny level, TdSparseArgs::fuse_apply)
-template <int kThreads, bool kHx = false>
+template <int kThreads, bool kHx = false, bool kWg = true>
 __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int s_last;
@@ -767,7 +792,7 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
       const word_t bit = 1ull << (v[k] & 63);
       if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
     }
-    sparse_settle<kItems, kHx>(a, v, claimed);
+    sparse_settle<kItems, kHx, kWg>(a, v, claimed);
   }
   __syncthreads();
   if (t == 0) {
@@ -813,7 +838,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
 // their owners' lists and td_sparse_apply finishes the level after the
 // exchange.  kThreads = 1024: 2 edges per thread per block.
 constexpr int kTdSparseThreads = 1024;
-template <int kThreads, bool kHx = false>
+// kWg: several ranks (owner lists) -- settles aggregated per workgroup
+// (sparse_settle); one rank keeps the per-wave form (its registers).
+template <int kThreads, bool kHx = false, bool kWg = false>
 __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
@@ -827,7 +854,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
       // (the fused owner side waits for the peers all the same: a collective)
-      if (a.fuse_apply) sparse_apply<kThreads, kHx>(a, 0, 1);
+      if (a.fuse_apply) sparse_apply<kThreads, kHx, kWg>(a, 0, 1);
     }
     return;
   }
@@ -883,8 +910,8 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
           owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u, dx ? a.direct.table : nullptr);
       }
     }
-    // (B) finish the wave's claimed vertices
-    sparse_settle<kItems, kHx>(a, v, claimed);
+    // (B) finish the claimed vertices (the whole workgroup: one counter atomic)
+    sparse_settle<kItems, kHx, kWg>(a, v, claimed);
   }
   if (a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
@@ -912,7 +939,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     // a tiny level (fuse_apply): this workgroup is also the owner side --
     // the peers' lists, their claims and the folded level end -- instead of
     // a td_sparse_apply launch
-    if (a.fuse_apply) sparse_apply<kThreads, kHx>(a, 0, 1);
+    if (a.fuse_apply) sparse_apply<kThreads, kHx, kWg>(a, 0, 1);
     return;
   }
 
@@ -959,7 +986,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
-      if (a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);  // (a collective: as td_sparse)
+      if (a.fuse_apply) sparse_apply<kBlock, false, false>(a, 0, 1);  // (a collective: as td_sparse)
     }
     return;
   }
@@ -1075,7 +1102,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
     if (t == 0) *a.ticket = 0u;
     if (dx) direct_publish(a.direct, a.lists, a.list_stride, true);
     // a tiny level (fuse_apply): the owner side and the level end here too
-    if (dx && a.fuse_apply) sparse_apply<kBlock>(a, 0, 1);
+    if (dx && a.fuse_apply) sparse_apply<kBlock, false, false>(a, 0, 1);
     return;
   }
   if (t != 0) return;
@@ -1446,8 +1473,10 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   // few blocks get four times the waves (measured against 256 threads / 8
   // edges: RMAT-26 1479 / 1469 -> 1502 / 1481 GTEPS, level 0 9.8 -> 6.7 us;
   // RMAT-22 top-down only 90.5 / 90.8 -> 91.8 / 92.2)
-  if (a.hx_bits) td_sparse_kernel<kTdSparseThreads, true><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
-  else td_sparse_kernel<kTdSparseThreads><<<static_cast<unsigned>(a.grid), kTdSparseThreads, 0, st>>>(a);
+  const unsigned grid = static_cast<unsigned>(a.grid);
+  if (a.hx_bits) td_sparse_kernel<kTdSparseThreads, true, true><<<grid, kTdSparseThreads, 0, st>>>(a);
+  else if (a.lists) td_sparse_kernel<kTdSparseThreads, false, true><<<grid, kTdSparseThreads, 0, st>>>(a);
+  else td_sparse_kernel<kTdSparseThreads><<<grid, kTdSparseThreads, 0, st>>>(a);
 }
 
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
