@@ -338,6 +338,7 @@ ShardView DeviceGraph::view() const {
     v.td_nhubs = td_nhubs_;
     v.td_hub_min_deg = td_hub_min_deg_;
     v.hx_off = hx_off_.data();
+    v.hx_index = hx_index_.data();
   }
   return v;
 }
@@ -405,6 +406,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   td_nhubs_ = 0;
   td_hub_min_deg_ = 0;
   hx_off_.reset();
+  hx_index_.reset();
   col_by_id_ = false;
   // Hub encoding needs a free flag bit in the vertex ids.
   if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
@@ -453,6 +455,10 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
               td_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
               be_->encode_hub_cols(col_.data(), nnz_, td_idx.data(), td_col_.data());
               if (P > 1) {
+                // each owned row's hub index (a slice of the global map)
+                hx_index_ = DBuf<uint32_t>(*be_, static_cast<size_t>(std::max<int64_t>(rows_, 1)));
+                if (rows_ > 0)
+                  be_->copy_async(hx_index_.data(), td_idx.data() + lo_, static_cast<size_t>(rows_) * sizeof(uint32_t));
                 build_hub_split();
                 // (the appended part hub-encoded too: a filtered dense level reads td_col)
                 be_->encode_hub_cols(col_.data() + nnz_, hx_total(), td_idx.data(), td_col_.data() + nnz_);

@@ -87,6 +87,10 @@ struct ShardView {
   // top-down hub iff its degree >= td_hub_min_deg.
   const eid_t* hx_off = nullptr;
   uint32_t td_hub_min_deg = 0;
+  // ... and each owned row's top-down hub index (UINT32_MAX: not a hub), so a
+  // settled hub finds its part with one load instead of a binary search over
+  // td_hub_vertex (a dependent chain of 16 loads per claiming wave).
+  const uint32_t* hx_index = nullptr;
   // Degree of every hub (nhubs entries; several ranks: a hub's row lives on
   // its owner, so the hub-cut decision sums these instead of row lengths).
   const uint32_t* hub_deg = nullptr;

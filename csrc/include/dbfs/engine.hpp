@@ -105,6 +105,7 @@ class DeviceGraph {
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
   // several ranks: hub-split rows (ShardView::hx_off), appended to col_ / td_col_
   DBuf<eid_t> hx_off_;
+  DBuf<uint32_t> hx_index_;  // ShardView::hx_index (owned rows)
   uint32_t td_hub_min_deg_ = 0;
   DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
   void build_hub_split();

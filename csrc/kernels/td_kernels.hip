@@ -486,8 +486,8 @@ __global__ __launch_bounds__(kRangeThreads, 2 * kRangeThreads / 256) void td_ran
 // lane's items whose row has a part on this rank (ShardView::hx_off; a hub
 // with none is listed as usual) leave the work list -- re = rs -- and get
 // their frontier bit, their bit in hx_bits and their count / degree in
-// hx_tot (one pair of atomics per wave).  The hub index is found by binary
-// search in td_hub_vertex (ascending): hubs are a handful per level.
+// hx_tot (one pair of atomics per wave).  The hub index is the row's entry of
+// ShardView::hx_index.
 template <int kItems>
 __device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed,
                                           const eid_t (&rs)[kItems], eid_t (&re)[kItems]) {
@@ -495,19 +495,16 @@ __device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v
 #pragma unroll
   for (int k = 0; k < kItems; ++k)
     if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.td_hub_min_deg)) hub |= 1u << k;
+  // (a row of degree >= td_hub_min_deg may still be no hub -- ties at the
+  // threshold beyond kTdMaxHubs: hx_index says UINT32_MAX, listed as usual)
   if (!__ballot(hub != 0)) return;
   long long hc = 0, hd = 0;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     if (!((hub >> k) & 1u)) continue;
-    int64_t lo_i = 0, hi_i = a.g.td_nhubs;  // first index with td_hub_vertex >= v
-    while (lo_i < hi_i) {
-      const int64_t mid = (lo_i + hi_i) >> 1;
-      if (a.g.td_hub_vertex[mid] < v[k]) lo_i = mid + 1;
-      else hi_i = mid;
-    }
-    DBFS_DCHECK(lo_i < a.g.td_nhubs && a.g.td_hub_vertex[lo_i] == v[k], 12, v[k]);
-    if (a.g.hx_off[lo_i + 1] == a.g.hx_off[lo_i]) continue;  // (no part here: listed)
+    const int64_t lo_i = a.g.hx_index[static_cast<int64_t>(v[k]) - a.g.lo];  // (owned: a settled vertex)
+    DBFS_DCHECK(lo_i >= a.g.td_nhubs || a.g.td_hub_vertex[lo_i] == v[k], 12, v[k]);
+    if (lo_i >= a.g.td_nhubs || a.g.hx_off[lo_i + 1] == a.g.hx_off[lo_i]) continue;  // (no hub / no part here: listed)
     const int64_t r = static_cast<int64_t>(v[k]) - a.g.lo;
     atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
     atomicOr(a.hx_bits + (lo_i >> 6), 1ull << (lo_i & 63));
