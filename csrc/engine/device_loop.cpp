@@ -756,7 +756,7 @@ void DeviceLoop::emit_dense(Chain& c) {
   }
   // (skipped for levels predicted well below the filter's threshold: the
   // snapshot kernel would only find its gate closed)
-  if (!ranged && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 &&
+  if (!ranged && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 && e_.g_.td_hub_share() >= opt_.td_hub_min_share &&
       (c.mf_hint < 0 || c.mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
     // large levels: the hubs' visited bits, staged in LDS by td_expand
     if (!e_.td_hub_vis_.data())

@@ -78,6 +78,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
   else if (name == "fold_scan") o.fold_scan = v != 0;
+  else if (name == "td_hub_min_share") o.td_hub_min_share = v;
   else if (name == "td_range_edges") o.td_range_edges = static_cast<int64_t>(v);
   else if (name == "td_range_words") o.td_range_words = static_cast<int64_t>(v);
   else if (name == "td_range_vis_frac") o.td_range_vis_frac = v;
@@ -134,6 +135,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
           {"fold_scan", o.fold_scan ? 1.0 : 0.0},
+          {"td_hub_min_share", o.td_hub_min_share},
           {"td_range_edges", static_cast<double>(o.td_range_edges)},
           {"td_range_words", static_cast<double>(o.td_range_words)},
           {"td_range_vis_frac", o.td_range_vis_frac},
@@ -405,6 +407,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   td_hub_vertex_.reset();
   td_nhubs_ = 0;
   td_hub_min_deg_ = 0;
+  td_hub_share_ = 0.0;
   hx_off_.reset();
   hx_index_.reset();
   col_by_id_ = false;
@@ -451,6 +454,14 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
             td_hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(kTdMaxHubs));
             td_nhubs_ = be_->select_hubs(all.data(), nall, td_min, td_hub_vertex_.data(), td_idx.data());
             td_hub_min_deg_ = td_min;
+            {
+              double hub_sum = 0.0, all_sum = 0.0;
+              for (uint32_t d : deg) {
+                all_sum += d;
+                if (d >= td_min) hub_sum += d;
+              }
+              td_hub_share_ = all_sum > 0 ? hub_sum / all_sum : 0.0;
+            }
             if (td_nhubs_ > 0) {
               td_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
               be_->encode_hub_cols(col_.data(), nnz_, td_idx.data(), td_col_.data());

@@ -76,6 +76,10 @@ class DeviceGraph {
   bool hub_sorted() const { return hub_sorted_; }
   // col is in id order (bottom-up must scan hub_col, whose order is hub-first)
   bool col_by_id() const { return col_by_id_; }
+  // share of all adjacency entries held by the top-down hubs' rows (0 without
+  // them): graphs whose hubs are only slightly above the mean degree (uniform
+  // random graphs) gain nothing from the top-down hub filter
+  double td_hub_share() const { return td_hub_share_; }
   int64_t nhubs() const { return nhubs_; }
   // from_file: the byte range [begin, end) of the file this rank parsed and
   // the edges it read (a binary cache: rows, -1 bytes); -1 when not from a file
@@ -107,6 +111,7 @@ class DeviceGraph {
   DBuf<eid_t> hx_off_;
   DBuf<uint32_t> hx_index_;  // ShardView::hx_index (owned rows)
   uint32_t td_hub_min_deg_ = 0;
+  double td_hub_share_ = 0.0;
   DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
   void build_hub_split();
   int64_t hx_total() const;
@@ -196,6 +201,9 @@ struct EngineOptions {
   // slower (58.9 against 63.5 GTEPS: decoding unvisited hubs costs a
   // dependent load); with them 0 is faster (69.0 against 65.9).
   double td_hub_vis_frac = 0.0;
+  // ... only on graphs whose top-down hubs hold at least this share of the
+  // adjacency entries (DeviceGraph::td_hub_share)
+  double td_hub_min_share = 0.0;
   // Direct-level top-down: hub targets claimed as one byte per hub (an
   // L2-resident 128 KiB array) and turned into level bytes after the
   // expansion (TdArgs::td_hub_mark, hub_apply).

@@ -577,6 +577,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
            py::arg("td_hubs") = true,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("col_by_id", &DeviceGraph::col_by_id)
+      .def_property_readonly("td_hub_share", &DeviceGraph::td_hub_share)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
       // hub-split rows (tests): (hubs, offsets, parts) as numpy arrays
