@@ -747,3 +747,24 @@ def test_hub_cut_several_ranks(P, narrow, alpha, max_hubs):
             assert cut[s][1] == plain[s][1]
             assert not plain[s][2]
         assert any(cut[s][2] for s in srcs)
+
+
+@pytest.mark.parametrize("words", [None, 32])
+def test_range_staged_top_down_levels_cpu(rt, words):
+    """Range-staged dense top-down levels (TdArgs::range_split) on the CPU
+    backend: the chains are planned (ranged flag) and the split points built
+    (Backend::range_split); levels exact against the oracle, also with many
+    ranges (td_range_words)."""
+    p = dbfs.rmat_params(14, 16, 53)
+    csr = dbfs.host_csr_from_params(p)
+    b = dbfs.BFS(p, rt, mode="td")
+    b.engine.set_option("td_range_edges", 1)
+    b.engine.set_option("td_range_vis_frac", 2.0)
+    if words is not None:
+        b.engine.set_option("td_range_words", words)
+    ranged = False
+    for s in b.sample_roots(3, seed=5):
+        r = b.run(s)
+        assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0])
+        ranged = ranged or any(c[7] for c in r.chains)
+    assert ranged
