@@ -412,49 +412,11 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     settle(lane < qn && f, ql, qrs, qe);
     qn = 0;
   };
-  // kDeep (packed records over whole units): records fetched two steps ahead
-  // -- a step whose vertices settle on their hub heads in LDS is otherwise
-  // paced by the one record round trip behind it.  A prefetched step is kept
-  // as (offset from the unit base, length, head): 3 registers instead of 5,
-  // the position recomputed from the wave's bit set when it is processed.
-  constexpr bool kDeep = kRec && kWords == kWave;
-  uint32_t d_off[2] = {0u, 0u}, d_len[2] = {0u, 0u};
-  vid_t d_u[2] = {0u, 0u};
-  if constexpr (kDeep) {
-    (void)n_loc;
-    d_off[0] = static_cast<uint32_t>(n_rs - u_base);
-    d_len[0] = n_len;
-    d_u[0] = n_u;
-    int l_;
-    eid_t r_;
-    fetch(1, l_, r_, d_len[1], d_u[1]);
-    d_off[1] = static_cast<uint32_t>(r_ - u_base);
-    if (!head) d_u[1] = d_len[1] ? col[u_base + d_off[1]] : 0u;
-  }
   for (int b = 0; b < nb; ++b) {
-    int loc;
-    eid_t rs, e;
-    vid_t u0;
-    if constexpr (kDeep) {
-      rs = u_base + d_off[0];
-      e = rs + d_len[0];
-      u0 = d_u[0];
-      d_off[0] = d_off[1];
-      d_len[0] = d_len[1];
-      d_u[0] = d_u[1];
-      int l_;
-      eid_t r_;
-      fetch(b + 2, l_, r_, d_len[1], d_u[1]);  // two steps ahead
-      d_off[1] = static_cast<uint32_t>(r_ - u_base);
-      const int idx = b * kWave + lane;
-      loc = idx < total ? wave_set_position(um, incl, idx) : -1;
-    } else {
-      loc = n_loc;
-      rs = n_rs;
-      e = n_rs + n_len;
-      u0 = n_u;
-      fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
-    }
+    const int loc = n_loc;
+    const eid_t rs = n_rs, e = n_rs + n_len;
+    const vid_t u0 = n_u;
+    fetch(b + 1, n_loc, n_rs, n_len, n_u);  // in flight during this batch's probes
     bool found = false;
     bool cut_row = false;  // (kCut) a hub-first row with a non-hub head: nothing to scan
     if constexpr (kCut) {
@@ -466,11 +428,7 @@ __device__ __forceinline__ void bu_wave_compact(const BuArgs& a, int64_t w0, wor
     BU_STAT(0, 1);
     BU_STAT(1, __popcll(__ballot(loc >= 0)));
     BU_STAT(2, __popcll(__ballot(found)));
-    if constexpr (kDeep) {
-      if (!head) d_u[1] = d_len[1] ? col[u_base + d_off[1]] : 0u;
-    } else {
-      if (!head) n_u = n_len ? col[n_rs] : 0u;
-    }
+    if (!head) n_u = n_len ? col[n_rs] : 0u;
     if constexpr (kQueue > 0) {
       // found by the head: settled now; unresolved rows with more neighbours
       // are queued (huge rows / spans scanned in place)
