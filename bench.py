@@ -200,7 +200,13 @@ def validated_pass(bfs, rt, roots):
     ok = 0
     for r, tr in zip(roots, results):
         res = bfs.run(r)
-        ok += int(bfs.validate(r) and (res.reached, res.edges, res.depth) == (tr.reached, tr.edges, tr.depth))
+        valid = bfs.validate(r)
+        same = (res.reached, res.edges, res.depth) == (tr.reached, tr.edges, tr.depth)
+        if not (valid and same):
+            log(f"root {r} FAILED: validator {'ok' if valid else 'REJECTED the levels'}; timed run (reached, edges, "
+                f"depth) {(tr.reached, tr.edges, tr.depth)} rerun {(res.reached, res.edges, res.depth)}; "
+                f"chains timed {[c[:3] for c in tr.chains]} rerun {[c[:3] for c in res.chains]}")
+        ok += int(valid and same)
     return sum(r.edges for r in results) / (wall * 1e6), wall / len(roots), ok, results
 
 
