@@ -119,10 +119,6 @@ class CpuBackend final : public Backend {
     const int64_t src = a.src_local;
     if (a.level8 && a.level8_filled) {
       if (src >= 0) a.level8[src] = a.narrow_base;
-    } else if (!a.level8 && a.level_filled) {
-      // (prefilled: the prefill must really have left every entry unreached)
-      for (int64_t i = 0; i < a.g.rows; ++i) DBFS_CHECK(a.level[i] == kUnreached, "init_run: level not prefilled");
-      if (src >= 0) a.level[src] = 0;
     } else {
       for (int64_t i = 0; i < a.g.rows; ++i) {
         if (a.level8) a.level8[i] = i == src ? a.narrow_base : kNarrowUnreached;

@@ -36,10 +36,7 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipSetDevice(dev_));
     HIP_CHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&fill_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&fill_start_ev_, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&fill_done_ev_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming));
     hipDeviceProp_t prop{};
     HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
@@ -54,13 +51,9 @@ class HipBackend final : public Backend {
     hipSetDevice(dev_);
     hipStreamSynchronize(st_);
     hipStreamSynchronize(side_);
-    hipStreamSynchronize(fill_);
     for (hipEvent_t e : events_) hipEventDestroy(e);
     hipEventDestroy(fork_ev_);
     hipEventDestroy(join_ev_);
-    hipEventDestroy(fill_start_ev_);
-    hipEventDestroy(fill_done_ev_);
-    hipStreamDestroy(fill_);
     hipStreamDestroy(side_);
     if (scan_tmp_) hipFree(scan_tmp_);
     if (pinned_) hipHostFree(pinned_);
@@ -89,21 +82,6 @@ class HipBackend final : public Backend {
     HIP_CHECK(hipStreamWaitEvent(st_, join_ev_, 0));
     forked_ = false;
   }
-  void prefill_level(lvl_t* level, int64_t n, lvl_t value) override {
-    on();
-    HIP_CHECK(hipEventRecord(fill_start_ev_, st_));
-    HIP_CHECK(hipStreamWaitEvent(fill_, fill_start_ev_, 0));
-    kern::fill_level(level, n, value, fill_);
-    chk();
-    HIP_CHECK(hipEventRecord(fill_done_ev_, fill_));
-    fill_pending_ = true;
-  }
-  void wait_prefill() override {
-    on();
-    if (!fill_pending_) return;
-    HIP_CHECK(hipStreamWaitEvent(st_, fill_done_ev_, 0));
-    fill_pending_ = false;
-  }
 
   void* alloc(size_t bytes) override {
     on();
@@ -116,7 +94,6 @@ class HipBackend final : public Backend {
     on();
     hipStreamSynchronize(st_);
     hipStreamSynchronize(side_);
-    hipStreamSynchronize(fill_);
     hipFree(p);
   }
   void memset_async(void* p, int v, size_t bytes) override {
@@ -165,7 +142,6 @@ class HipBackend final : public Backend {
     on();
     join_side();
     wait_stream();
-    if (fill_pending_) HIP_CHECK(hipStreamSynchronize(fill_));  // (its done event stays valid for wait_prefill)
   }
   bool stream_idle() override {
     const hipError_t e = hipStreamQuery(st_);
@@ -452,10 +428,6 @@ class HipBackend final : public Backend {
   hipStream_t side_ = nullptr;
   hipEvent_t fork_ev_ = nullptr, join_ev_ = nullptr;
   bool forked_ = false;
-  // level prefill stream (prefill_level / wait_prefill)
-  hipStream_t fill_ = nullptr;
-  hipEvent_t fill_start_ev_ = nullptr, fill_done_ev_ = nullptr;
-  bool fill_pending_ = false;
   std::string arch_;
   int cus_ = 0;
   double clock_khz_ = 0.0;

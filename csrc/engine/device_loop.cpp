@@ -1036,13 +1036,6 @@ RunResult DeviceLoop::run() {
     ia.frontier_clear = fr_own(0);
   }
   be_.init_run(ia);
-  // 32-bit levels: the other level array refilled for the next run while this
-  // one's kernels execute (its own stream, after everything enqueued so far)
-  if (!e_.run_narrow_ && opt_.prefill_levels) {
-    if (e_.level_alt_.size() != e_.level_.size()) e_.level_alt_ = DBuf<lvl_t>(be_, e_.level_.size());
-    be_.prefill_level(e_.level_alt_.data(), e_.g_.rows(), kUnreached);
-    e_.level_alt_filled_ = true;
-  }
   // the seed's frontier is gathered with its totals when level 0 is bottom-up
   // (bu mode).  (Top-down levels read only their owned slice; the replicated
   // visited bitmap filters candidates with whatever remote bits it has --

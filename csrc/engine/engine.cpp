@@ -67,7 +67,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
-  else if (name == "prefill_levels") o.prefill_levels = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bits") o.td_sparse_bits = v != 0;
@@ -131,7 +130,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
-          {"prefill_levels", o.prefill_levels ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
@@ -829,16 +827,6 @@ RunResult Engine::run(int64_t source) {
     narrow_base_ = static_cast<uint8_t>(epoch * (kNarrowMaxLevel + 2));
     level8_filled_ = epoch != 0;
   }
-  // 32-bit levels, prefilled during the previous run: this run takes that
-  // array (its fill ordered before this run's kernels)
-  level_filled_ = false;
-  if (!ref && !run_narrow_ && use_device_loop() && opt_.prefill_levels && level_alt_filled_ &&
-      level_alt_.size() == level_.size()) {
-    be_.wait_prefill();
-    std::swap(level_, level_alt_);
-    level_filled_ = true;
-    level_alt_filled_ = false;
-  }
   r = ref ? run_ref(source) : (use_device_loop() ? run_bitmap_device(source) : run_bitmap(source));
   check_device();
   levels_narrow_ = run_narrow_;
@@ -847,7 +835,6 @@ RunResult Engine::run(int64_t source) {
     // rerun with 32-bit levels; the reported time includes both traversals
     narrow_failed_ = true;
     run_narrow_ = levels_narrow_ = false;
-    level_filled_ = false;
     const double first_ms = r.ms;
     r = use_device_loop() ? run_bitmap_device(source) : run_bitmap(source);
     check_device();
@@ -905,7 +892,6 @@ InitRunArgs Engine::init_args(int64_t source, word_t* seed_frontier, LevelCtrl* 
   ia.level = level_.data();
   ia.level8 = run_narrow_ ? level8_.data() : nullptr;
   ia.level8_filled = level8_filled_;
-  ia.level_filled = level_filled_ && !run_narrow_;
   ia.narrow_base = narrow_base_;
   ia.zdeg = zdeg_.data();
   ia.visited = visited_.data();

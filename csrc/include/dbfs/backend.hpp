@@ -240,9 +240,6 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
 //   device-loop state is *ctrl = level_ctrl_finish(ctrl_init, seed) and the
 //   mailbox slot of level -1 is stamped.
 struct InitRunArgs {
-  // 32-bit levels already hold kUnreached everywhere (prefilled during the
-  // previous run, Backend::prefill_level): only the source's entry is written
-  bool level_filled = false;
   ShardView g;
   lvl_t* level = nullptr;          // rows
   // Narrow level array (one byte per vertex, kNarrowUnreached = not reached;
@@ -990,12 +987,6 @@ class Backend {
   virtual void* comm_stream_handle() { return stream_handle(); }
   virtual void fork_side() {}
   virtual void join_side() {}
-  // Level prefill (32-bit levels, EngineOptions::prefill_levels): `level` is
-  // filled with `value` on a stream of its own, after everything enqueued on
-  // the compute stream so far, so the fill overlaps the kernels enqueued next;
-  // wait_prefill() makes the compute stream wait for it.  (CPU: in place.)
-  virtual void prefill_level(lvl_t* level, int64_t n, lvl_t value) { fill_level(level, n, value); }
-  virtual void wait_prefill() {}
   // Rate of the device wall clock the kernels stamp level records with (ticks
   // per ms; 0: no device clock, records carry no times).
   virtual double wall_clock_khz() const { return 0.0; }

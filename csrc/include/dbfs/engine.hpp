@@ -358,13 +358,6 @@ struct EngineOptions {
   // kNarrowEpochs values, so only one run in kNarrowEpochs fills the byte
   // array (the others read the earlier epochs' bytes as unreached).
   bool narrow_epochs = true;
-  // 32-bit levels (device loop): two level arrays alternate between runs,
-  // and the one the next run uses is refilled with the unreached value on a
-  // stream of its own while this run's kernels execute
-  // (Backend::prefill_level) -- the next run's initialisation then writes
-  // only the source's entry.  The fill still happens inside the timed
-  // window, overlapped instead of serialized.
-  bool prefill_levels = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -494,9 +487,6 @@ class Engine {
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill
-  DBuf<lvl_t> level_alt_;             // prefill_levels: the other 32-bit level array
-  bool level_alt_filled_ = false;     // ... filled (or being filled) for the next run
-  bool level_filled_ = false;         // level_ was prefilled for the current run
   uint8_t narrow_base_ = 0;           // the current run's level byte base (narrow_epochs)
   int64_t narrow_run_ = 0;            // narrow runs since level8_ was allocated
   bool narrow_failed_ = false;        // a traversal overflowed the narrow levels

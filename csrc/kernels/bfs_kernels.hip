@@ -99,9 +99,6 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
       l16[i] = v;
     }
     for (int64_t i = n16 * 16 + t0; i < rows; i += stride) a.level8[i] = i == src ? a.narrow_base : kNarrowUnreached;
-  } else if (a.level_filled) {
-    // prefilled during the previous run (Backend::prefill_level): the source only
-    if (src >= 0 && t0 == 0) a.level[src] = 0;
   } else {
     // level: rows / 4 int4 stores (+ tail)
     const int64_t n4 = (reinterpret_cast<uintptr_t>(a.level) & 15u) == 0 ? rows / 4 : 0;
