@@ -428,9 +428,13 @@ __global__ __launch_bounds__(kBlock) void update_kernel(UpdateArgs a) {
     s_d[wv] = wd;
   }
   // (pushed words: every wave's write-through stores drained before the
-  // ticket, so the level end published after it covers them)
+  // ticket, so the level end published after it covers them; likewise the
+  // unit statistics the last workgroup scans with fold_scan -- stored by
+  // lane 0 of every wave, and a barrier does not wait for another wave's
+  // stores)
   if constexpr (kRanks)
     if (a.push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.fold_scan) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     long long c = 0, d = 0;
