@@ -864,6 +864,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.words = W_;
   ba.lane_limit = opt_.bu_lane_limit;
   ba.whole_units = opt_.bu_whole_units;
+  ba.small_waves = opt_.bu_small_waves;
   ba.zdeg = e_.zdeg_.data() + me_ * W_;
   ba.follow_up = c.pf == 'B';
   ba.unit_cnt = e_.unit_cnt_.data();

@@ -65,6 +65,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "directed") o.directed = v != 0;
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
+  else if (name == "bu_small_waves") o.bu_small_waves = static_cast<int>(v);
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
   else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
@@ -122,6 +123,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"directed", o.directed ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
+          {"bu_small_waves", static_cast<double>(o.bu_small_waves)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"td_sparse_bits", o.td_sparse_bits ? 1.0 : 0.0},
@@ -1158,6 +1160,7 @@ RunResult Engine::run_bitmap(int64_t source) {
       ba.words = W;
       ba.lane_limit = opt_.bu_lane_limit;
       ba.whole_units = opt_.bu_whole_units;
+      ba.small_waves = opt_.bu_small_waves;
       ba.zdeg = zdeg_.data() + comm_.rank() * W;
       ba.follow_up = !res.levels.empty() && res.levels.back().direction == 'B';
       ba.unit_cnt = unit_cnt_.data();

@@ -765,6 +765,7 @@ struct BuArgs {
   int lane_limit = 32;               // neighbours scanned per lane before wave cooperation
   bool follow_up = false;            // the previous level was bottom-up too (launch shape)
   int whole_units = 0;               // hub kernel, compacted: 64 words per wave (1), 16 (-1), by shard size (0)
+  int small_waves = 0;               // ... split units: 4 words per wave on a first level (1), never (-1), by shard size (0)
   int64_t* unit_cnt = nullptr;
   int64_t* unit_deg = nullptr;
   const LevelCtrl* ctrl = nullptr;   // device loop: runs only when ctrl->dir == 'B'

@@ -139,6 +139,10 @@ struct EngineOptions {
   // Bottom-up waves take a whole 64-word unit (1), 16 words (-1), or by shard
   // size (0: whole units when they fill every resident wave slot).
   int bu_whole_units = 0;
+  // ... units split over waves (small shards): a first bottom-up level at 4
+  // words per wave instead of 16 (1), never (-1), when 16 would leave wave
+  // slots idle (0)
+  int bu_small_waves = 0;
   // Top-down levels with at least this many local frontier edges mark
   // discoveries in a byte map (plain stores) instead of bitmap atomics.
   int64_t td_byte_edges = int64_t(1) << 22;

@@ -571,8 +571,11 @@ __device__ __forceinline__ void bu_post_words(const BuArgs& a, int64_t w0, int n
 // kCutLevels (claims in the narrow level bytes) or kCutClaims (wide levels:
 // claims in BuArgs::cut_claim).
 // kPost: the output words pushed to the peers afterwards (BuArgs::push).
+// kWW: words per wave when units are split over waves (!kWhole): 16, or 4 for
+// shards too small to fill the chip at 16 (a soc-LiveJournal1-sized graph's
+// 1184 units at 16 words per wave are 4736 waves, 18 per CU against 32 slots).
 template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false,
-          int kCut = 0, bool kPost = false>
+          int kCut = 0, bool kPost = false, int kWW = kWaveWords>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
   __shared__ word_t s_hub[kHubWords];
   __shared__ word_t s_res[(kThreads / kWave) * kUnitWords];
@@ -640,11 +643,13 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     bu_fused_finish<kThreads, kEnd>(a, wc, wd, s_c, s_d, reinterpret_cast<uint64_t*>(s_res));
     return;
   }
-  // 16 words per wave: unit groups of 4 waves walk the units; every workgroup
-  // runs the same number of iterations (barriers stay uniform)
-  constexpr int kGroups = kThreads / kUnitThreads;
-  const int group = wave / kUnitWaves;
-  const int wg = wave % kUnitWaves;
+  // kWW words per wave: unit groups of kUW waves walk the units; every
+  // workgroup runs the same number of iterations (barriers stay uniform)
+  constexpr int kUW = kUnitWords / kWW;  // waves per unit
+  static_assert(kUnitWords % kWW == 0 && (kThreads / kWave) % kUW == 0, "whole unit groups per workgroup");
+  constexpr int kGroups = (kThreads / kWave) / kUW;
+  const int group = wave / kUW;
+  const int wg = wave % kUW;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kGroups;
   // the unit groups' totals for the fused finish, in LDS (registers live
   // across the loop would spill)
@@ -654,9 +659,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
     if (u < nunits)
-      bu_wave_compact<true, kWaveWords, kQ, kRec, kCut>(a, u * kUnitWords + wg * kWaveWords,
-                                                        s_res + wave * kWaveWords, s_hub, cnt, deg, s_q + wave * kQ,
-                                                        cut);
+      bu_wave_compact<true, kWW, kQ, kRec, kCut>(a, u * kUnitWords + wg * kWW, s_res + wave * kWW, s_hub, cnt, deg,
+                                                 s_q + wave * kQ, cut);
     cnt = wave_sum(cnt);
     deg = wave_sum(deg);
     if (lane_id() == 0) {
@@ -664,12 +668,12 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       s_d[wave] = deg;
     }
     __syncthreads();
-    if ((threadIdx.x & (kUnitThreads - 1)) == 0 && u < nunits) {
+    if ((threadIdx.x & (kUW * kWave - 1)) == 0 && u < nunits) {
       long long c = 0, d = 0;
 #pragma unroll
-      for (int k = 0; k < kUnitWaves; ++k) {
-        c += s_c[group * kUnitWaves + k];
-        d += s_d[group * kUnitWaves + k];
+      for (int k = 0; k < kUW; ++k) {
+        c += s_c[group * kUW + k];
+        d += s_d[group * kUW + k];
       }
       a.unit_cnt[u] = c;
       a.unit_deg[u] = d;
@@ -680,7 +684,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   }
   if constexpr (kPost)
     for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride)
-      if (base + group < nunits) bu_post_words(a, (base + group) * kUnitWords + wg * kWaveWords, kWaveWords);
+      if (base + group < nunits) bu_post_words(a, (base + group) * kUnitWords + wg * kWW, kWW);
   if (!a.fuse_scan) return;
   if constexpr (kPost) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above)
   __syncthreads();  // (an empty loop: the accumulators' zeroing)
@@ -976,7 +980,15 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // instead of 64); 16-word waves without the row queue (measured)
     constexpr int kFollowThreads = 768;
     const int threads = whole ? (a.follow_up ? kFollowThreads : kHubBuThreads) : kHubBuThreads;
-    const unsigned grid = grid_for(nunits, whole ? threads / kWave : kHubBuThreads / kUnitThreads, 2 * device_cus());
+    // shards too small to fill the wave slots at 16 words per wave: 4 (one
+    // unit per workgroup) for a first bottom-up level -- measured, the
+    // soc-LiveJournal1-sized graph's first level 420 -> 295 us (do mode
+    // 116 -> 146 GTEPS), RMAT-22's 45 -> 36 us; later levels, with few
+    // unvisited vertices left, ran slower that way (21 -> 26 us) and keep 16
+    const bool small = !whole && !a.follow_up &&
+                       (a.small_waves > 0 || (a.small_waves == 0 && nunits * (kUnitWords / kWaveWords) < slots));
+    const unsigned grid = grid_for(nunits, whole ? threads / kWave : (small ? 1 : kHubBuThreads / kUnitThreads),
+                                   2 * device_cus());
     // packed row records (compile-time path: the view's fallback costs registers)
     const bool rec = a.g.nz_rec && a.g.unit_base && a.g.nz_pref && a.g.nz_row_off && a.zdeg && a.g.head;
     if (a.fuse_scan && grid > static_cast<unsigned>(kMaxFusedGrid)) {
@@ -990,12 +1002,17 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     }
     // (every hub kernel runs the fused finish itself; a folded level end is
     // compiled only into the kEnd variants)
-#define DBFS_BU_LAUNCH(W, T, Q, R)                                                          \
-  do {                                                                                    \
-    if (a.end.active && a.push) bu_hub_kernel<W, T, Q, R, true, 0, true><<<grid, T, 0, st>>>(a);  \
-    else if (a.end.active) bu_hub_kernel<W, T, Q, R, true><<<grid, T, 0, st>>>(a);       \
-    else if (a.push) bu_hub_kernel<W, T, Q, R, false, 0, true><<<grid, T, 0, st>>>(a);  \
-    else bu_hub_kernel<W, T, Q, R, false><<<grid, T, 0, st>>>(a);                        \
+#define DBFS_BU_LAUNCH_WW(W, T, Q, R, WW)                                                                \
+  do {                                                                                                   \
+    if (a.end.active && a.push) bu_hub_kernel<W, T, Q, R, true, 0, true, WW><<<grid, T, 0, st>>>(a);     \
+    else if (a.end.active) bu_hub_kernel<W, T, Q, R, true, 0, false, WW><<<grid, T, 0, st>>>(a);         \
+    else if (a.push) bu_hub_kernel<W, T, Q, R, false, 0, true, WW><<<grid, T, 0, st>>>(a);               \
+    else bu_hub_kernel<W, T, Q, R, false, 0, false, WW><<<grid, T, 0, st>>>(a);                          \
+  } while (0)
+#define DBFS_BU_LAUNCH(W, T, Q, R)                  \
+  do {                                              \
+    if (small) DBFS_BU_LAUNCH_WW(W, T, Q, R, 4);     \
+    else DBFS_BU_LAUNCH_WW(W, T, Q, R, kWaveWords);  \
   } while (0)
     if (a.cut_edges > 0) {
       // a hub-cut level (one rank, a first bottom-up level: the engine only
@@ -1022,10 +1039,10 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 #undef DBFS_CUT_LAUNCH
     }
     if (whole) {
-      if (a.follow_up && rec) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, true);
-      else if (a.follow_up) DBFS_BU_LAUNCH(true, kFollowThreads, kBuQueue, false);
-      else if (rec) DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, true);
-      else DBFS_BU_LAUNCH(true, kHubBuThreads, kBuQueue, false);
+      if (a.follow_up && rec) DBFS_BU_LAUNCH_WW(true, kFollowThreads, kBuQueue, true, kWaveWords);
+      else if (a.follow_up) DBFS_BU_LAUNCH_WW(true, kFollowThreads, kBuQueue, false, kWaveWords);
+      else if (rec) DBFS_BU_LAUNCH_WW(true, kHubBuThreads, kBuQueue, true, kWaveWords);
+      else DBFS_BU_LAUNCH_WW(true, kHubBuThreads, kBuQueue, false, kWaveWords);
       return;
     }
     if (a.follow_up && rec) DBFS_BU_LAUNCH(false, kHubBuThreads, 0, true);
@@ -1033,6 +1050,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     else if (rec) DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, true);
     else DBFS_BU_LAUNCH(false, kHubBuThreads, kBuQueue, false);
 #undef DBFS_BU_LAUNCH
+#undef DBFS_BU_LAUNCH_WW
     return;
   }
   DBFS_CHECK(!a.end.active, "bu_step: a folded level end needs the hub kernels' fused finish");
