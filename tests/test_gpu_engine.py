@@ -297,12 +297,14 @@ def test_perf_regression_do_vs_ref_gpu(gpu_runtime):
     assert t_do * 10 < t_ref, (t_do, t_ref)
 
 
-@pytest.mark.parametrize("whole", [1, -1])
+@pytest.mark.parametrize("whole,small", [(1, 0), (-1, -1), (-1, 1)])
 @pytest.mark.parametrize("max_hubs", [None, 64, 3000, 0])
-def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, whole):
+def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, whole, small):
     """Bottom-up with hub-encoded heads probed in the LDS copy of the hub
     frontier bits: every vertex a hub (default cap on a small graph), a few
-    hubs (mixed LDS / global head probes), no hubs (plain kernel)."""
+    hubs (mixed LDS / global head probes), no hubs (plain kernel); whole
+    64-word units per wave, or units split at 16 / 4 words per wave
+    (bu_small_waves)."""
     p = dbfs.rmat_params(16, 16, 53)
     csr = dbfs.host_csr_from_params(p)
     for mode in ["bu", "do"]:
@@ -312,6 +314,7 @@ def test_bottom_up_hub_lds_gpu(gpu_runtime, max_hubs, whole):
         if max_hubs != 0:
             assert bfs.graph.nhubs > 0
         bfs.engine.set_option("bu_whole_units", whole)  # 64 / 16 words per wave (compacted hub kernel)
+        bfs.engine.set_option("bu_small_waves", small)  # (split units: 4 words per wave on first levels)
         for src in bfs.sample_roots(3, seed=11):
             _check(bfs, csr, src)
         bfs.engine.set_option("device_loop", 0)
