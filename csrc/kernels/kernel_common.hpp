@@ -186,6 +186,56 @@ __device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, 
   }
 }
 
+// Workgroup-aggregated owner-list append: every wave of the workgroup calls
+// it (uniform); lane items v[k] with bit k of `act` go to their owners' lists.
+// Per owner the waves take their offsets with LDS atomics and the workgroup
+// takes its slots with ONE atomic on the owner's count word -- with two ranks
+// every wave of a 1 M-edge level appended to the same remote count word
+// (thousands of returning atomics on one address, ~90 per us).
+template <int kItems>
+__device__ __forceinline__ void owner_list_append_wg(vid_t* lists, int64_t stride, int64_t part, int nranks,
+                                                     const vid_t (&v)[kItems], unsigned act,
+                                                     const DirectTable* dt = nullptr) {
+  __shared__ unsigned s_oc[kern::kMaxPeers], s_ob[kern::kMaxPeers];
+  const int t = threadIdx.x;
+  const int lane = lane_id();
+  if (t < nranks) s_oc[t] = 0u;
+  __syncthreads();
+  int own[kItems];
+  unsigned off[kItems];
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    own[k] = ((act >> k) & 1u) ? static_cast<int>(static_cast<int64_t>(v[k]) / part) : -1;
+    off[k] = 0u;
+    unsigned long long pending = __ballot(own[k] >= 0);
+    while (pending) {
+      const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+      const int o = __builtin_amdgcn_readfirstlane(__shfl(own[k], leader, kWave));
+      const unsigned long long msk = __ballot(own[k] == o);
+      unsigned base = 0u;
+      if (lane == leader) base = atomicAdd(&s_oc[o], static_cast<unsigned>(__popcll(msk)));
+      base = __shfl(base, leader, kWave);
+      if (own[k] == o) off[k] = base + mask_rank(msk);
+      pending &= ~msk;
+    }
+  }
+  __syncthreads();
+  if (t < nranks) {
+    const unsigned c = s_oc[t];
+    s_ob[t] = c ? atomicAdd(lists + static_cast<int64_t>(t) * stride, c) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    if (own[k] < 0) continue;
+    const unsigned at = 1u + s_ob[own[k]] + off[k];
+    DBFS_DCHECK(at < static_cast<unsigned long long>(stride), 3, at);
+    if (dt) sys_store_u32(dt->dst[own[k]] + at, v[k]);
+    else lists[static_cast<int64_t>(own[k]) * stride + at] = v[k];
+  }
+  __syncthreads();  // (s_oc / s_ob reused by the next call)
+}
+
 // Direct exchanges' tagged cells (backend.hpp DirectExchange).
 __device__ __forceinline__ uint64_t cell_word0(uint64_t seq, uint64_t v) { return (seq << 32) | (v & 0xffffffffull); }
 __device__ __forceinline__ uint64_t cell_word1(uint64_t seq, uint64_t v) {

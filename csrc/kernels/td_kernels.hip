@@ -901,7 +901,11 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       for (int k = 0; k < kItems; ++k)
         if (((claimed >> k) & 1u) && static_cast<uint64_t>(v[k]) - lo >= rows) remote |= 1u << k;
       claimed &= ~remote;
-      if (__ballot(remote != 0)) {
+      if constexpr (kWg) {
+        // (the whole workgroup: one count atomic per owner and block)
+        owner_list_append_wg<kItems>(a.lists, a.list_stride, a.part, a.nranks, v, remote,
+                                     dx ? a.direct.table : nullptr);
+      } else if (__ballot(remote != 0)) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u, dx ? a.direct.table : nullptr);
