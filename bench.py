@@ -89,7 +89,10 @@ def parse_args(argv=None):
     ap.add_argument("--mode", default="do", choices=["ref", "td", "bu", "do", "simple", "scan"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--root-seed", type=int, default=12345)
-    ap.add_argument("--alpha", type=float, default=24.0)
+    ap.add_argument("--alpha", type=float, default=40.0,
+                    help="Beamer alpha (TD -> BU when m_f > m_u / alpha); 40 measured over 24 / 32 / 48 / 64: same "
+                         "headline, held-out roots 1412 -> 1492 GTEPS, LiveJournal-sized do unchanged (48 loses 10 %% "
+                         "there); profiles/r4_final_alpha_sweep.txt.  The engine and CLI default stays 24")
     ap.add_argument("--beta", type=float, default=96.0)
     ap.add_argument("--bu-lane-limit", type=int, default=16)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
