@@ -259,7 +259,7 @@ class CpuBackend final : public Backend {
       bytes = a.ctrl->bytes != 0;
       if (a.clear_qv)
         for (int64_t i = 0; i < q; ++i)
-          if (a.clear_qv[i] != kNoRow) a.clear_frontier[a.clear_qv[i] >> 6] = 0;
+          a.clear_frontier[a.clear_qv[i] >> 6] = 0;
     }
     for (int64_t i = 0; i < q; ++i) {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
@@ -297,26 +297,6 @@ class CpuBackend final : public Backend {
     }
   }
 
-  // the next level's hub-split entries (HxAppendArgs)
-  static void hx_append(const HxAppendArgs& h) {
-    int64_t q = h.list_stats[0], m = h.list_stats[1];
-    for (int64_t hub = 0; hub < h.nhubs; ++hub) {
-      if (!((static_cast<word_t>(h.bits[hub >> 6]) >> (hub & 63)) & 1)) continue;
-      const eid_t rs = h.hx_off[hub], d = h.hx_off[hub + 1] - rs;
-      if (d <= 0) continue;
-      const int64_t r = static_cast<int64_t>(h.hub_vertex[hub]) - h.lo;
-      h.qscan[q] = m;
-      h.qbase[q] = rs - m;
-      h.qv[q] = r >= 0 && r < h.rows ? static_cast<vid_t>(r) : kNoRow;
-      for (int64_t blk = div_up(m, kTdEdgesPerBlock); blk * kTdEdgesPerBlock < m + d; ++blk)
-        h.blk_vstart[blk] = static_cast<int32_t>(q);
-      ++q;
-      m += d;
-    }
-    h.qscan[q] = m;
-    h.list_stats[0] = q;
-    h.list_stats[1] = m;
-  }
   void level_finish(const LevelFinishArgs& a) override {
     if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
     LevelCtrl c = a.seed ? a.ctrl_init : *a.ctrl;
@@ -331,8 +311,6 @@ class CpuBackend final : public Backend {
       a.mailbox->reached = c.reached;
       a.mailbox->level = a.seed ? -1 : a.level;
     }
-    // (hub-split entries for a top-down next level only, as the HIP finish)
-    if (a.hx.bits && !c.done && c.dir == 'T') hx_append(a.hx);
   }
 
   // Sparse top-down level (see the HIP kernel): claims in the replicated
@@ -346,18 +324,6 @@ class CpuBackend final : public Backend {
     const eid_t rs = a.g.row_off[r], d = a.g.row_off[r + 1] - rs;
     if (d <= 0) return;
     a.frontier_out[r >> 6] |= 1ull << (r & 63);
-    if (a.hx_bits && d >= static_cast<eid_t>(a.g.td_hub_min_deg)) {
-      // hub-split: a top-down hub with a part on this rank leaves the list
-      const vid_t* hv = a.g.td_hub_vertex;
-      const int64_t h = std::lower_bound(hv, hv + a.g.td_nhubs, v) - hv;
-      DBFS_CHECK(h < a.g.td_nhubs && hv[h] == v, "hub-split: a hub-degree vertex is not a top-down hub");
-      if (a.g.hx_off[h + 1] > a.g.hx_off[h]) {
-        a.hx_bits[h >> 6] |= 1ull << (h & 63);
-        a.hx_tot[0] += 1;
-        a.hx_tot[1] += d;
-        return;
-      }
-    }
     const int64_t cnt = sparse_cnt_, deg = sparse_deg_;
     a.oscan[cnt] = deg;
     a.obase[cnt] = rs - deg;
@@ -371,17 +337,6 @@ class CpuBackend final : public Backend {
     a.stats[0] = a.stats[2] = sparse_cnt_;
     a.stats[1] = a.stats[3] = sparse_deg_;
     a.oscan[sparse_cnt_] = sparse_deg_;
-    if (a.hx_bits) {
-      // hub-split: the diverted hubs in the totals, their bits to the stats block
-      a.stats[2] += a.hx_tot[0];
-      a.stats[3] += a.hx_tot[1];
-      a.stats[4] = a.hx_tot[0];
-      a.hx_tot[0] = a.hx_tot[1] = 0;
-      for (int64_t w = 0; w < div_up(a.g.td_nhubs, int64_t(64)); ++w) {
-        a.hx_out[w] = static_cast<int64_t>(a.hx_bits[w]);
-        a.hx_bits[w] = 0;
-      }
-    }
   }
   void td_sparse(const TdSparseArgs& a) override {
     DBFS_CHECK(!a.direct.active, "CpuBackend: no direct list exchange (peer windows are GPU memory)");
@@ -399,8 +354,7 @@ class CpuBackend final : public Backend {
       }
     } else {
       const int64_t q = a.dev_stats[0];
-      for (int64_t i = 0; i < q; ++i)
-        if (a.qv[i] != kNoRow) a.frontier_in[a.qv[i] >> 6] = 0;
+      for (int64_t i = 0; i < q; ++i) a.frontier_in[a.qv[i] >> 6] = 0;
       for (int64_t i = 0; i < q; ++i) rows.emplace_back(a.qscan[i] + a.qbase[i], a.qscan[i + 1] + a.qbase[i]);
     }
     sparse_cnt_ = sparse_deg_ = 0;
@@ -728,16 +682,6 @@ class CpuBackend final : public Backend {
     }
     (void)pref;
   }
-  void hx_count(const ShardView& g, eid_t* cnt) override {
-    for (int64_t r = 0; r < g.rows; ++r)
-      for (eid_t e = g.row_off[r]; e < g.row_off[r + 1]; ++e)
-        if (g.td_col[e] & kHubFlag) ++cnt[g.td_col[e] & ~kHubFlag];
-  }
-  void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) override {
-    for (int64_t r = 0; r < g.rows; ++r)
-      for (eid_t e = g.row_off[r]; e < g.row_off[r + 1]; ++e)
-        if (g.td_col[e] & kHubFlag) out[cursor[g.td_col[e] & ~kHubFlag]++] = static_cast<vid_t>(g.lo + r);
-  }
   int64_t select_hubs(const uint32_t* deg, int64_t n, uint32_t min_deg, vid_t* hub_vertex,
                       uint32_t* hub_idx) override {
     int64_t k = 0;
@@ -775,47 +719,21 @@ class CpuBackend final : public Backend {
       for (int64_t i = 0; i < a.words; ++i) a.visited[i] |= a.frontier[i];
   }
   void bu_cut_prep(const BuArgs& a) override {
-    DBFS_CHECK(!a.cut_direct.active, "CpuBackend: no direct list exchange");
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     if (!*a.cut_flag) return;
     const int64_t lo = a.g.lo;
     for (int64_t w = 0; w < a.words; ++w)
-      for (word_t m = a.frontier[a.cut_fr_base + w] & ~a.g.hub_bits[a.cut_fr_base + w]; m; m &= m - 1) {
+      for (word_t m = a.frontier[w] & ~a.g.hub_bits[w]; m; m &= m - 1) {
         const int64_t v = w * 64 + __builtin_ctzll(m);
         for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
           const vid_t t = a.g.col[e];
           const int64_t r = static_cast<int64_t>(t) - lo;
-          if (r < 0 || r >= a.g.rows) {
-            // (several ranks) a remote neighbour: once per rank, to its owner
-            if (test_bit(a.cut_visited, t)) continue;
-            a.cut_visited[t >> 6] |= 1ull << (t & 63);
-            vid_t* list = a.cut_lists + (static_cast<int64_t>(t) / a.part) * a.cut_list_stride;
-            DBFS_CHECK(static_cast<int64_t>(list[0]) + 1 < a.cut_list_stride, "hub-cut owner list overflow");
-            list[1 + list[0]++] = t;
-            continue;
-          }
+          DBFS_CHECK(r >= 0 && r < a.g.rows, "bu_cut_prep: one rank only");
           if (test_bit(a.visited, static_cast<uint64_t>(r))) continue;
           if (a.cut_claim) a.cut_claim[r] = 1;
           else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
         }
       }
-  }
-  void bu_cut_apply(const BuArgs& a) override {
-    DBFS_CHECK(a.nranks > 1 && a.cut_lists && a.cut_flag && a.cut_recv_lists,
-               "bu_cut_apply: several ranks' hub-cut arguments missing");
-    for (int p = 0; p < a.nranks; ++p) a.cut_lists[static_cast<int64_t>(p) * a.cut_list_stride] = 0;
-    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
-    if (!*a.cut_flag) return;
-    for (int p = 0; p < a.nranks; ++p) {
-      const vid_t* list = a.cut_recv_lists + static_cast<int64_t>(p) * a.cut_list_stride;
-      for (vid_t k = 0; k < list[0]; ++k) {
-        const int64_t r = static_cast<int64_t>(list[1 + k]) - a.g.lo;
-        DBFS_CHECK(r >= 0 && r < a.g.rows, "hub-cut claim outside this shard");
-        if (test_bit(a.visited, static_cast<uint64_t>(r))) continue;
-        if (a.cut_claim) a.cut_claim[r] = 1;
-        else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
-      }
-    }
   }
   void hub_apply(const HubApplyArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

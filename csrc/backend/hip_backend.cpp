@@ -246,7 +246,7 @@ class HipBackend final : public Backend {
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void bu_cut_prep(const BuArgs& a) override { on(); kern::bu_cut_prep(a, st_); chk(); }
-  void bu_cut_apply(const BuArgs& a) override { on(); kern::bu_cut_apply(a, st_); chk(); }
+  void direct_prewait(const DirectExchange& x) override { on(); kern::direct_prewait(x, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
   void hub_apply(const HubApplyArgs& a) override { on(); kern::hub_apply(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
@@ -269,16 +269,7 @@ class HipBackend final : public Backend {
     kern::row_heads(ro, col, rows, head, hub_idx, st_);
     chk();
   }
-  void hx_count(const ShardView& g, eid_t* cnt) override {
-    on();
-    kern::hx_rows(g, cnt, nullptr, st_);
-    chk();
-  }
-  void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) override {
-    on();
-    kern::hx_rows(g, cursor, out, st_);
-    chk();
-  }
+
   void range_split(const eid_t* ro, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
                    uint32_t* out) override {
     on();

@@ -15,7 +15,10 @@ namespace dbfs {
 
 double comm_timeout_s() {
   const char* e = std::getenv("DBFS_COMM_TIMEOUT_S");
-  if (!e || !*e) return 600.0;
+  // (a peer minutes late is dead: the default bounds a hung job at two
+  // minutes per collective wait; the device-side waits give up after at most
+  // 60 s of it)
+  if (!e || !*e) return 120.0;
   return std::max(0.0, std::atof(e));
 }
 

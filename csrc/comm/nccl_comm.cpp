@@ -11,8 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dbfs/comm.hpp"
@@ -34,8 +37,28 @@ namespace dbfs {
       ::dbfs::raise_error(__FILE__, __LINE__, std::string("HIP error ") + hipGetErrorString(e_)); \
   } while (0)
 
+// Calls on the (nonblocking) communicator: ncclInProgress settled by polling.
+#define NCCL_Q(expr) settle(static_cast<int>(expr), #expr, __FILE__, __LINE__)
+
 namespace {
 inline ncclComm_t C(void* p) { return static_cast<ncclComm_t>(p); }
+// Poll a nonblocking communicator until its pending operation is no longer
+// in progress (or `limit` seconds pass: ncclInProgress returned).
+ncclResult_t poll_comm(ncclComm_t c, double limit) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    ncclResult_t st = ncclSuccess;
+    ncclCommGetAsyncError(c, &st);
+    if (st != ncclInProgress) return st;
+    if (limit > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
+      return ncclInProgress;
+    if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+double init_timeout_s() {
+  const char* e = std::getenv("DBFS_RCCL_INIT_TIMEOUT_S");
+  return e && *e ? std::max(0.0, std::atof(e)) : 60.0;
+}
 // collectives go to the backend's communication stream (the compute stream
 // unless the engine opened a side region: Backend::fork_side)
 inline hipStream_t S(Backend* be) { return static_cast<hipStream_t>(be->comm_stream_handle()); }
@@ -54,10 +77,35 @@ NcclComm::NcclComm(const std::string& uid, int rank, int nranks, Backend& be) : 
   HIP_CHECK(hipSetDevice(be.device_id()));
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  // (DBFS_FAULT_INJECT="kind=rccl_init": tests of the setups that must not
+  // depend on RCCL -- the peer transport runs on a TCP inner communicator)
+  if (const char* f = std::getenv("DBFS_FAULT_INJECT"))
+    DBFS_CHECK(std::string(f).find("kind=rccl_init") == std::string::npos, "injected fault (rccl_init)");
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
   ncclComm_t c = nullptr;
-  NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  const ncclResult_t r0 = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+  if (r0 != ncclSuccess && r0 != ncclInProgress) {
+    if (c) ncclCommAbort(c);
+    NCCL_CHECK(r0);
+  }
+  const double limit = init_timeout_s();
+  const ncclResult_t st = c ? poll_comm(c, limit) : ncclInternalError;
+  if (st != ncclSuccess) {
+    if (c) ncclCommAbort(c);
+    DBFS_CHECK(st != ncclInProgress, "RCCL communicator setup did not complete within " +
+                                         std::to_string(static_cast<int>(limit)) + " s on rank " +
+                                         std::to_string(rank) + " (DBFS_RCCL_INIT_TIMEOUT_S)");
+    NCCL_CHECK(st);
+  }
   comm_ = c;
   install_watchdog();
+}
+
+void NcclComm::settle(int result, const char* what, const char* file, int line) {
+  ncclResult_t r = static_cast<ncclResult_t>(result);
+  if (r == ncclInProgress && comm_) r = poll_comm(C(comm_), 0.0);
+  if (r != ncclSuccess) raise_error(file, line, std::string("RCCL error ") + ncclGetErrorString(r) + " in " + what);
 }
 
 // Failure detection: while the host waits on the stream, poll
@@ -116,21 +164,21 @@ void NcclComm::alltoall(const void* send, void* recv, size_t bytes) {
   note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
-  NCCL_CHECK(ncclAllToAll(send, recv, bytes, ncclChar, C(comm_), S(be_)));
+  NCCL_Q(ncclAllToAll(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allgather(const void* send, void* recv, size_t bytes) {
   note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
-  NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, C(comm_), S(be_)));
+  NCCL_Q(ncclAllGather(send, recv, bytes, ncclChar, C(comm_), S(be_)));
 }
 
 void NcclComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
-  NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, C(comm_), S(be_)));
+  NCCL_Q(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, C(comm_), S(be_)));
 }
 
 void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, void* recv, const int64_t* rc,
@@ -138,20 +186,20 @@ void NcclComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd,
   note_alltoallv(sc, eb);
   check_alive();
   HIP_CHECK(hipSetDevice(be_->device_id()));
-  NCCL_CHECK(ncclGroupStart());
+  NCCL_Q(ncclGroupStart());
   for (int r = 0; r < size_; ++r) {
     if (sc[r] > 0)
-      NCCL_CHECK(ncclSend(static_cast<const char*>(send) + sd[r] * eb, static_cast<size_t>(sc[r]) * eb, ncclChar, r,
+      NCCL_Q(ncclSend(static_cast<const char*>(send) + sd[r] * eb, static_cast<size_t>(sc[r]) * eb, ncclChar, r,
                           C(comm_), S(be_)));
     if (rc[r] > 0)
-      NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + rd[r] * eb, static_cast<size_t>(rc[r]) * eb, ncclChar, r,
+      NCCL_Q(ncclRecv(static_cast<char*>(recv) + rd[r] * eb, static_cast<size_t>(rc[r]) * eb, ncclChar, r,
                           C(comm_), S(be_)));
   }
-  NCCL_CHECK(ncclGroupEnd());
+  NCCL_Q(ncclGroupEnd());
 }
 
-void NcclComm::group_start() { NCCL_CHECK(ncclGroupStart()); }
-void NcclComm::group_end() { NCCL_CHECK(ncclGroupEnd()); }
+void NcclComm::group_start() { NCCL_Q(ncclGroupStart()); }
+void NcclComm::group_end() { NCCL_Q(ncclGroupEnd()); }
 
 void NcclComm::barrier() {
   note(kBarrier, 0);

@@ -33,6 +33,12 @@ namespace dbfs {
   } while (0)
 
 namespace {
+// DBFS_FAULT_INJECT="kind=<k>" for a communicator's construction (tests):
+// peer_init makes the peer transport's setup fail on every rank that sees it
+bool fault_kind_is(const char* kind) {
+  const char* e = std::getenv("DBFS_FAULT_INJECT");
+  return e && std::string(e).find(std::string("kind=") + kind) != std::string::npos;
+}
 constexpr size_t kFlagBytes = 4096;
 constexpr size_t kCellBase = 1024;  // direct exchange cells in the flag page (flags: bytes [0, 8 P))
 static_assert(kCellBase + 2 * 16 * 16 <= kFlagBytes, "direct cells fit the flag page");
@@ -58,6 +64,7 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   hipIpcMemHandle_t h{};
   try {
     HIP_CHECK(hipSetDevice(be.device_id()));
+    if (fault_kind_is("peer_init")) throw Error("injected fault (peer_init)");
     // the pushed frontier slices' region (Comm::direct_frontier)
     if (const char* fe = std::getenv("DBFS_PEER_FRONTIER_MB")) fslot_ = static_cast<size_t>(std::max(0L, std::atol(fe))) << 20;
     else fslot_ = size_t(8) << 20;
@@ -144,6 +151,37 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   }
   agree("window mapping");
   if (!ipc_) boot_->barrier();  // every rank holds every window before any may drop one
+  // Topology: every rank's PCI bus id; ranks on one physical GPU (tests
+  // rehearsing several ranks on one device) get unfused collectives and
+  // split waits -- a collective that spins in every workgroup can hold the
+  // CUs a co-resident rank's producer needs (Comm::split_waits)
+  {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), be.device_id()) != hipSuccess) bus[0] = 0;
+    bus_ = boot_->allgather(std::string(bus));
+    std::string row;
+    for (int p = 0; p < size_; ++p) {
+      int a = -1;
+      if (!bus_[p].empty() && bus_[p] == bus_[rank_]) {
+        a = 2;
+      } else {
+        int d = -1, can = 0;
+        if (!bus_[p].empty() && hipDeviceGetByPCIBusId(&d, bus_[p].c_str()) == hipSuccess && d >= 0 &&
+            hipDeviceCanAccessPeer(&can, be.device_id(), d) == hipSuccess)
+          a = can ? 1 : 0;
+        (void)hipGetLastError();
+      }
+      row.push_back(static_cast<char>('0' + a + 1));
+    }
+    const auto rows = boot_->allgather(row);
+    access_.assign(static_cast<size_t>(size_) * size_, -1);
+    for (int r = 0; r < size_; ++r)
+      for (int p = 0; p < size_ && p < static_cast<int>(rows[r].size()); ++p) access_[r * size_ + p] = rows[r][p] - '1';
+    for (int p = 0; p < size_ && !shared_; ++p)
+      for (int q = p + 1; q < size_; ++q)
+        if (!bus_[p].empty() && bus_[p] == bus_[q]) shared_ = true;
+    if (shared_) fused_ = false;
+  }
   // the direct exchange's tables (one per parity; DBFS_PEER_DIRECT=0: none)
   const char* de = std::getenv("DBFS_PEER_DIRECT");
   if (!de || std::string(de) != "0") {
@@ -203,12 +241,9 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
   prev_watch_ = be.wait_watch();
   auto prev = prev_watch_;
   uint64_t* eh = err_host_;
-  const int me = rank_;
-  be.set_wait_watch([eh, prev, me](double waited) {
+  be.set_wait_watch([this, eh, prev](double waited) {
     const uint64_t e = __atomic_load_n(eh, __ATOMIC_ACQUIRE);
-    if (e)
-      throw Error("peer communicator: collective " + std::to_string(e) + " timed out waiting for a peer on rank " +
-                  std::to_string(me) + " (DBFS_COMM_TIMEOUT_S)");
+    if (e) throw Error(describe_error(e));
     if (prev) prev(waited);
   });
   watch_installed_ = true;
@@ -225,8 +260,11 @@ PeerComm::~PeerComm() {
     // no rank unmaps or frees a window while a peer may still write into it
     // or read it (a peer that failed closes its socket: the barrier throws at
     // once and is ignored -- nothing of that peer is in flight any more).
+    // After a timed-out wait (a peer hung) there is no barrier to reach: the
+    // IPC allocations stay alive while any importer still maps them.
     // In-process the windows are shared-owned instead: the last rank frees.
-    if (ipc_) {
+    const bool peer_lost = err_host_ && __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0;
+    if (ipc_ && !peer_lost) {
       try {
         boot_->barrier();
       } catch (const std::exception&) {
@@ -256,6 +294,25 @@ void PeerComm::release() {
 
 std::string PeerComm::name() const { return "peer+" + inner_->name(); }
 
+// A timed-out device wait's error word (kWaitSeqMask) as a message: this
+// rank, the collective's sequence number, what it was and for which level,
+// and the peer that never arrived.
+std::string PeerComm::describe_error(uint64_t word) const {
+  const uint64_t seq = word & kWaitSeqMask;
+  const int peer = static_cast<int>((word >> 48) & 0xFF) - 1;
+  std::string what = "collective #" + std::to_string(seq);
+  const Tag& t = tags_[seq % tags_.size()];
+  if (t.seq == seq) {
+    what += std::string(" (") + t.op;
+    if (t.level >= 0) what += ", level " + std::to_string(t.level);
+    what += ")";
+  }
+  const double limit = comm_timeout_s() > 0 ? std::min(comm_timeout_s(), 60.0) : 60.0;
+  return "peer communicator: rank " + std::to_string(rank_) + " timed out in " + what + " waiting for " +
+         (peer >= 0 ? "rank " + std::to_string(peer) : std::string("a peer")) + " (device wait bound " +
+         std::to_string(static_cast<int>(limit)) + " s, DBFS_COMM_TIMEOUT_S)";
+}
+
 char* PeerComm::slot_ptr(int owner, int parity, int sender) const {
   return peer_[owner] + kFlagBytes + (static_cast<size_t>(parity) * size_ + sender) * slot_;
 }
@@ -267,6 +324,7 @@ int unit_for(uintptr_t x) { return (x % 16 == 0) ? 16 : (x % 8 == 0) ? 8 : 4; }
 void PeerComm::run(const Plan& plan) {
   const int P = size_;
   const uint64_t s = ++seq_;
+  tag(s, plan.op);
   const int b = static_cast<int>(s & 1);
   const hipStream_t st = S(be_);
   HIP_CHECK(hipSetDevice(be_->device_id()));
@@ -376,12 +434,13 @@ void PeerComm::run(const Plan& plan) {
 // (The reference copies each pair's bucket with one cudaMemcpyPeer,
 // bfs.cu:604-605.)
 void PeerComm::rounds(const std::vector<const char*>& src, const std::vector<int64_t>& sb,
-                      const std::vector<char*>& dst, const std::vector<int64_t>& rb, int64_t nrounds) {
+                      const std::vector<char*>& dst, const std::vector<int64_t>& rb, int64_t nrounds, const char* op) {
   const int64_t slot = static_cast<int64_t>(slot_);
   for (int64_t k = 0; k < std::max<int64_t>(nrounds, 1); ++k) {
     const int64_t off = k * slot;
     auto piece = [&](int64_t total) { return std::max<int64_t>(0, std::min(slot, total - off)); };
     Plan pl;
+    pl.op = op;
     pl.send.resize(static_cast<size_t>(size_));
     pl.recv.resize(static_cast<size_t>(size_));
     for (int p = 0; p < size_; ++p) {
@@ -412,7 +471,7 @@ void PeerComm::alltoall(const void* send, void* recv, size_t bytes) {
     src[p] = static_cast<const char*>(send) + p * bytes;
     dst[p] = static_cast<char*>(recv) + p * bytes;
   }
-  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)));
+  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)), "alltoall");
 }
 
 void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
@@ -426,7 +485,7 @@ void PeerComm::allgather(const void* send, void* recv, size_t bytes) {
   std::vector<char*> dst(static_cast<size_t>(size_));
   std::vector<int64_t> n(static_cast<size_t>(size_), static_cast<int64_t>(bytes));
   for (int p = 0; p < size_; ++p) dst[p] = static_cast<char*>(recv) + p * bytes;
-  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)));
+  rounds(src, n, dst, n, nrounds(static_cast<int64_t>(bytes)), "allgather");
 }
 
 void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
@@ -435,6 +494,7 @@ void PeerComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   const size_t per = slot_ / sizeof(int64_t);
   for (size_t off = 0; off < count; off += per) {
     Plan pl;
+    pl.op = "allreduce";
     pl.sum_count = static_cast<int64_t>(std::min(per, count - off));
     pl.sum_buf = buf + off;
     run(pl);
@@ -467,7 +527,7 @@ void PeerComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd,
   }
   int64_t gmx = 0;
   for (int64_t x : allgather_host_i64(mx)) gmx = std::max(gmx, x);  // (one 8-byte round)
-  rounds(src, sb, dst, rb, nrounds(gmx));
+  rounds(src, sb, dst, rb, nrounds(gmx), "alltoallv");
 }
 
 void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t stride_words, size_t cap) {
@@ -485,7 +545,7 @@ void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t strid
       src[p] = reinterpret_cast<const char*>(send + p * stride_words);
       dst[p] = reinterpret_cast<char*>(recv + p * stride_words);
     }
-    rounds(src, n, dst, n, nrounds(piece));
+    rounds(src, n, dst, n, nrounds(piece), "owner lists");
     return;
   }
   // (traffic accounted at the capacity, as the default exchange: the device
@@ -496,6 +556,7 @@ void PeerComm::alltoall_lists(const uint32_t* send, uint32_t* recv, size_t strid
   const int64_t stride_b = static_cast<int64_t>(stride_words) * 4;
   const int64_t cap_b = std::min<int64_t>((piece + 15) / 16 * 16, stride_b);
   Plan pl;
+  pl.op = "owner lists";
   pl.counted = true;
   pl.send.resize(static_cast<size_t>(size_));
   pl.recv.resize(static_cast<size_t>(size_));
@@ -511,6 +572,7 @@ bool PeerComm::direct_lists(size_t cap, DirectExchange* x) {
   if (static_cast<size_t>(piece) > slot_ || !dtab_) return false;
   note(kAllToAllV, static_cast<int64_t>(size_ - 1) * piece);  // (accounted at the capacity, as alltoall_lists)
   const uint64_t s = ++seq_;
+  tag(s, "owner lists (direct)");
   x->active = 1;
   x->nranks = size_;
   x->rank = rank_;
@@ -537,6 +599,7 @@ bool PeerComm::direct_level_end(size_t count, DirectExchange* x) {
   if (!dtab_ || count != 2 || be_ == nullptr) return false;
   note(kAllReduce, static_cast<int64_t>(size_ - 1) * static_cast<int64_t>(count) * 8);
   const uint64_t s = ++seq_;
+  tag(s, "level end (direct)");
   x->active = 1;
   x->nranks = size_;
   x->rank = rank_;
@@ -561,6 +624,7 @@ void PeerComm::level_end(const void* gsend, void* grecv, size_t gbytes, int64_t*
   // one launch: the frontier slices and the totals pushed, the flags, the
   // slices unpacked, the totals summed and the level decided by one thread
   Plan pl;
+  pl.op = gbytes > 0 ? "level end + frontier gather" : "level end";
   if (gbytes > 0) {
     note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(gbytes));
     note_fused();
@@ -589,6 +653,7 @@ void PeerComm::allgather_allreduce(const void* send, void* recv, size_t bytes, i
   note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
   note_fused();
   Plan pl;
+  pl.op = "allgather + allreduce";
   pl.send.resize(static_cast<size_t>(size_));
   pl.recv.resize(static_cast<size_t>(size_));
   for (int p = 0; p < size_; ++p) {
@@ -706,6 +771,7 @@ bool PeerComm::self_test(std::string* why) {
   const int64_t bad = inner_->sum_host(err.empty() ? 0 : 1);
   if (bad && err.empty()) err = "a peer's self-test failed";
   if (why) *why = err;
+  verdict_ = bad == 0 ? "ok" : err;
   if (bad == 0) direct_self_test();
   if (bad == 0) frontier_self_test();
   return bad == 0;

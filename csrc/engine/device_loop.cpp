@@ -45,7 +45,6 @@ class DeviceLoop {
     bool fused_scan = false;   // the chain's last kernel finishes the level
     bool level_ended = false;  // ... and also ran its level end (direct exchange)
     bool folded = false;       // ... and also scanned its unit prefixes (UpdateArgs::fold_scan)
-    bool cut = false;          // several ranks: a hub-cut bottom-up level was enqueued
     // several ranks: the output frontier pushed to the peers by the producing
     // kernel (EngineOptions::direct_frontier), and the input frontier's pushed
     // slices (the previous chain's table) for hub_gather to copy in
@@ -115,10 +114,7 @@ class DeviceLoop {
   bool cells_fit() const { return e_.g_.rows() < (int64_t(1) << 32) && e_.g_.nnz() < (int64_t(1) << 40); }
   const volatile LevelMailbox* wait_stamp(int lv);
   LevelFinishArgs finish_args(int level, bool seed, char expect_dir, int64_t cap);
-  void finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather, bool hx = false);
-  // the chain of level L (sparse, several ranks) is hub-split
-  bool hx_chain(int L) const;
-  int64_t hx_words() const { return 1 + div_up(gv_.td_nhubs, kWordBits); }
+  void finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather);
   ScanArgs scan_args(int level, bool seed, char expect_dir, int64_t cap);
 
   // ---- planner ----
@@ -312,40 +308,13 @@ LevelFinishArgs DeviceLoop::finish_args(int level, bool seed, char expect_dir, i
 // in the same launch the level's output frontier slice all-gathered
 // (Comm::allgather_allreduce) -- then level_finish decides and stamps.
 // (bfs_mpi.cu:615-621 pays a Sendrecv and an Allreduce per level.)
-// (hx: a hub-split level also all-reduces its hub count and frontier-hub
-// bits -- blk[4 ..] -- and the finish appends the next level's hub-split
-// entries to this level's output list)
-void DeviceLoop::finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather, bool hx) {
+void DeviceLoop::finish_ranks(int level, bool seed, char expect_dir, int64_t cap, bool gather) {
   int64_t* blk = sblk(level);
   // level L writes frontier_[L & 1] (the seed: frontier_[1])
   const int out = seed ? 1 : (level & 1);
-  LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
-  if (hx) {
-    HxAppendArgs& h = fa.hx;
-    h.bits = blk + kHxStatsWord;
-    h.hx_off = gv_.hx_off;
-    h.hub_vertex = gv_.td_hub_vertex;
-    h.nhubs = gv_.td_nhubs;
-    h.lo = gv_.lo;
-    h.rows = gv_.rows;
-    h.list_stats = blk;
-    h.qscan = qscan_set(level + 1);
-    h.qbase = qbase_set(level + 1);
-    h.blk_vstart = blk_set(level + 1);
-    h.qv = e_.qv_[(level + 1) & 1].data();
-  }
+  const LevelFinishArgs fa = finish_args(level, seed, expect_dir, cap);
   comm_.level_end(fr_own(out), e_.frontier_[out].data(), gather ? static_cast<size_t>(W_) * sizeof(word_t) : 0,
-                  blk + 2, hx ? 2 + static_cast<size_t>(hx_words()) : 2, fa);
-}
-
-// Hub-split sparse chains: several ranks with hub-split rows, the first
-// hx_levels levels, none after a bottom-up level (by then the hubs are
-// visited; a hub settled later is expanded by its owner, as any vertex).
-bool DeviceLoop::hx_chain(int L) const {
-  if (!xc_ || !gv_.hx_off || !e_.hx_bits_.data() || L >= opt_.hx_levels) return false;
-  for (int k = 0; k < L; ++k)
-    if (enq_form_[static_cast<size_t>(k)] == 'B') return false;
-  return true;
+                  blk + 2, 2, fa);
 }
 
 ScanArgs DeviceLoop::scan_args(int level, bool seed, char expect_dir, int64_t cap) {
@@ -455,6 +424,7 @@ void DeviceLoop::predict(LevelCtrl& c, double nf, double mf, double pnf, double 
 // all-gathers its output frontier, for a bottom-up level predicted next.
 void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool gather) {
   if (ht_) hmark("enqueue " + std::to_string(L) + d);
+  comm_.set_level_tag(L);  // (a failed collective of this chain names its level)
   if (static_cast<size_t>(L) >= enq_dir_.size()) {
     e_.inject_fault(L);
     enq_dir_.resize(static_cast<size_t>(L) + 1);
@@ -484,7 +454,7 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
                ? comm_.direct_frontier(static_cast<size_t>(W_), L & 1)
                : nullptr;
   enq_push_[L] = c.push;
-  res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0, d == 'S' && hx_chain(L) ? hx_words() : 0});
+  res_.chains.push_back({L, d, enq_cap_[L], enq_gather_[L] != 0});
   res_.chains.back().push = c.push != nullptr;
   c.cap = enq_cap_[L];
   c.mf_hint = mf_hint;
@@ -511,11 +481,10 @@ void DeviceLoop::enqueue_level(int L, char d, int64_t cap, double mf_hint, bool 
     case 'T': emit_dense(c); break;
     default: emit_bottom_up(c); break;
   }
-  res_.chains.back().cut = c.cut && P_ > 1;  // (the owner-list exchange)
   if (!c.fused_scan) be_.scan_units(scan_args(L, false, enq_dir_[L], c.cap));
   enq_fused_[L] = c.fused_scan && d != 'S' && !c.folded;
   if (xc_ && !c.level_ended)
-    finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] && !c.push, d == 'S' && hx_chain(L));
+    finish_ranks(L, false, enq_dir_[L], c.cap, enq_gather_[L] && !c.push);
   if (opt_.phase_timing) evs_[L] = {ev0, be_.record_event()};
   if (ht_) hmark("enqueued " + std::to_string(L));
 }
@@ -622,18 +591,10 @@ void DeviceLoop::emit_sparse(Chain& c) {
   const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
   sp.nranks = P_;
   const int64_t apply_grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
-  // hub-split: settled hubs leave the owner's list (their bits and totals
-  // ride the level end, a collective: the cells carry two totals only)
-  const bool hx = hx_chain(L);
-  if (hx) {
-    sp.hx_bits = e_.hx_bits_.data();
-    sp.hx_tot = e_.hx_tot_.data();
-    sp.hx_out = sblk(L) + kHxStatsWord;
-  }
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
-  const bool end_ok = direct && opt_.direct_level_end && cells_fit() && !enq_gather_[L] && !hx;
+  const bool end_ok = direct && opt_.direct_level_end && cells_fit() && !enq_gather_[L];
   // a tiny level (its chain capped at fuse_cap): td_sparse's last workgroup
   // also runs the owner side and the level end -- one launch (the direct
   // level end is taken in the same order as unfused)
@@ -661,6 +622,10 @@ void DeviceLoop::emit_sparse(Chain& c) {
     c.level_ended = true;
   }
   sp.grid = apply_grid;
+  // ranks sharing a GPU: the wait for the peers' cells as a one-wave launch
+  // first, so the apply's grid never spins in every workgroup while a peer's
+  // td_sparse still needs CUs (Comm::split_waits)
+  if (direct && comm_.split_waits()) be_.direct_prewait(sp.direct);
   be_.td_sparse_apply(sp);
 }
 
@@ -873,6 +838,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.push = c.push;
   ba.push_rank = me_;
   ba.push_nranks = P_;
+  bool cut = false;  // a hub-cut level was enqueued
   if (gv_.nhubs > 0) {
     HubGatherArgs hg;
     hg.g = gv_;
@@ -893,23 +859,17 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.visited = e_.visited_.data();
       hg.words = GW_;
     }
-    // a first bottom-up level: the hub cut (decided on the device from the
-    // frontier hubs' degrees hub_gather sums -- global on every rank),
-    // enqueued for levels predicted at <= bu_cut_mf_frac of the graph's edges
-    // (a first bottom-up level's non-hub frontier edges grow with its
-    // frontier: the larger ones never cut, and skip its launches).  Several
-    // ranks: the non-hub frontier's remote neighbours go to their owners as
-    // lists (the sparse levels' owner lists, so at most list_max of them per
-    // owner: the cut bound is capped there) and bu_cut_apply claims them.
-    // (several ranks: the shard conditions agreed once, cut_ranks_ok_; the rest
-    // are functions of agreed values)
-    const bool shard_ok = xc_ ? e_.cut_ranks_ok_ && list_max_ > 0 && opt_.bu_cut_ranks
-                              : gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref && gv_.nz_row_off &&
-                                    gv_.head && ba.zdeg;
-    const bool cut = opt_.bu_cut_edges > 0 && c.pf != 'B' &&
-                     (c.mf_hint < 0 || c.mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(e_.total_directed_)) &&
-                     shard_ok;
-    const int64_t cut_edges = xc_ ? std::min(opt_.bu_cut_edges, list_max_) : opt_.bu_cut_edges;
+    // a first bottom-up level, one rank: the hub cut (decided on the device
+    // from the frontier hubs' degrees hub_gather sums), enqueued for levels
+    // predicted at <= bu_cut_mf_frac of the graph's edges (a first bottom-up
+    // level's non-hub frontier edges grow with its frontier: the larger ones
+    // never cut, and skip its launches).  (Several ranks: measured slower at
+    // P = 8 -- the cut's top-down part does not shrink with P while a rank's
+    // bottom-up share does -- and not built.)
+    const bool shard_ok = P_ == 1 && gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref &&
+                          gv_.nz_row_off && gv_.head && ba.zdeg;
+    cut = opt_.bu_cut_edges > 0 && c.pf != 'B' &&
+          (c.mf_hint < 0 || c.mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(e_.total_directed_)) && shard_ok;
     if (cut) {
       if (!e_.cut_part_.data()) {
         e_.cut_part_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(div_up(gv_.nhubs, int64_t(64)), kHgCopyGrid)));
@@ -918,14 +878,14 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         be_.memset_async(e_.cut_ticket_.data(), 0, e_.cut_ticket_.bytes());
       }
       hg.cut_part = e_.cut_part_.data();
-      hg.cut_edges = cut_edges;
+      hg.cut_edges = opt_.bu_cut_edges;
       hg.cut_flag = e_.cut_flag_.data();
       hg.cut_ticket = e_.cut_ticket_.data();
     }
     be_.hub_gather(hg);
     ba.hub_front = e_.hub_front_.data();
     if (cut) {
-      ba.cut_edges = cut_edges;
+      ba.cut_edges = opt_.bu_cut_edges;
       ba.cut_flag = e_.cut_flag_.data();
       if (!e_.run_narrow_) {
         // wide levels: claims in a byte array of their own (kept zero)
@@ -935,38 +895,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         }
         ba.cut_claim = e_.cut_claim_.data();
       }
-      if (P_ == 1) {
-        // (one rank -- with a forced exchange too: nothing to send; the flag
-        // keeps the level end out of the plain kernel, which may not run)
-        be_.bu_cut_prep(ba);
-        c.cut = xc_;
-      } else {
-        // several ranks: own claims in place, remote ones as owner lists
-        // (straight into the owners' windows with a direct exchange), then
-        // the owners' side (collectives cannot be predicated: the exchange
-        // runs on every chain, empty when the level does not cut)
-        c.cut = true;
-        ba.nranks = P_;
-        ba.cut_fr_base = static_cast<int64_t>(me_) * W_;
-        ba.cut_lists = e_.dl_send_lists_.data();
-        ba.cut_list_stride = e_.list_stride_;
-        ba.part = part_.part;
-        ba.cut_visited = e_.visited_.data();
-        const size_t lcap = static_cast<size_t>(list_max_);
-        const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &ba.cut_direct);
-        if (direct && !e_.cut_prep_ticket_.data()) {
-          e_.cut_prep_ticket_ = DBuf<unsigned>(be_, 1);
-          be_.memset_async(e_.cut_prep_ticket_.data(), 0, e_.cut_prep_ticket_.bytes());
-        }
-        ba.cut_prep_ticket = e_.cut_prep_ticket_.data();
-        be_.bu_cut_prep(ba);
-        if (!direct)
-          comm_.alltoall_lists(e_.dl_send_lists_.data(), e_.dl_recv_lists_.data(),
-                               static_cast<size_t>(e_.list_stride_), lcap);
-        ba.cut_recv_lists = direct ? nullptr : e_.dl_recv_lists_.data();
-        be_.bu_cut_apply(ba);
-        ba.cut_direct = DirectExchange();  // (the bottom-up kernel does not exchange)
-      }
+      be_.bu_cut_prep(ba);
     }
   }
   if (opt_.bu_fused_scan) {
@@ -980,9 +909,10 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     c.fused_scan = true;
     // several ranks: the level's end in the kernel's last workgroup too (no
     // frontier gather; the hub kernels' fused finish)
-    // (not on a hub-cut level: its plain and cut kernels are both launched,
-    // and only the plain ones have the folded end)
-    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !c.cut &&
+    // (not on a hub-cut level -- one rank with a forced exchange: its plain
+    // and cut kernels are both launched, and only the plain ones have the
+    // folded end)
+    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !cut &&
         comm_.direct_level_end(2, &ba.end)) {
       ba.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;
@@ -1146,6 +1076,7 @@ RunResult DeviceLoop::run() {
   // before any later work on the stream -- no synchronisation needed.
   const auto t1 = std::chrono::steady_clock::now();
   prev_done = t1;
+  comm_.set_level_tag(-1);
   return collect(nlev, t1);
 }
 

@@ -95,10 +95,8 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
   else if (name == "xfuse_edges") o.xfuse_edges = static_cast<int64_t>(v);
   else if (name == "bu_merge_visited") o.bu_merge_visited = v != 0;
-  else if (name == "hx_levels") o.hx_levels = static_cast<int>(v);
   else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
   else if (name == "bu_cut_mf_frac") o.bu_cut_mf_frac = v;
-  else if (name == "bu_cut_ranks") o.bu_cut_ranks = v != 0;
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
@@ -153,10 +151,8 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
           {"xfuse_edges", static_cast<double>(o.xfuse_edges)},
           {"bu_merge_visited", o.bu_merge_visited ? 1.0 : 0.0},
-          {"hx_levels", static_cast<double>(o.hx_levels)},
           {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
           {"bu_cut_mf_frac", o.bu_cut_mf_frac},
-          {"bu_cut_ranks", o.bu_cut_ranks ? 1.0 : 0.0},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
@@ -340,9 +336,6 @@ ShardView DeviceGraph::view() const {
     v.td_col = td_col_.data();
     v.td_hub_vertex = td_hub_vertex_.data();
     v.td_nhubs = td_nhubs_;
-    v.td_hub_min_deg = td_hub_min_deg_;
-    v.hx_off = hx_off_.data();
-    v.hx_index = hx_index_.data();
   }
   return v;
 }
@@ -408,10 +401,7 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
   td_col_.reset();
   td_hub_vertex_.reset();
   td_nhubs_ = 0;
-  td_hub_min_deg_ = 0;
   td_hub_share_ = 0.0;
-  hx_off_.reset();
-  hx_index_.reset();
   col_by_id_ = false;
   // Hub encoding needs a free flag bit in the vertex ids.
   if (hubs && part_.n > 0 && nall <= static_cast<int64_t>(kHubFlag)) {
@@ -455,7 +445,6 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
             DBuf<uint32_t> td_idx(*be_, static_cast<size_t>(nall));
             td_hub_vertex_ = DBuf<vid_t>(*be_, static_cast<size_t>(kTdMaxHubs));
             td_nhubs_ = be_->select_hubs(all.data(), nall, td_min, td_hub_vertex_.data(), td_idx.data());
-            td_hub_min_deg_ = td_min;
             {
               double hub_sum = 0.0, all_sum = 0.0;
               for (uint32_t d : deg) {
@@ -467,15 +456,6 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
             if (td_nhubs_ > 0) {
               td_col_ = DBuf<vid_t>(*be_, static_cast<size_t>(std::max<int64_t>(nnz_, 1)));
               be_->encode_hub_cols(col_.data(), nnz_, td_idx.data(), td_col_.data());
-              if (P > 1) {
-                // each owned row's hub index (a slice of the global map)
-                hx_index_ = DBuf<uint32_t>(*be_, static_cast<size_t>(std::max<int64_t>(rows_, 1)));
-                if (rows_ > 0)
-                  be_->copy_async(hx_index_.data(), td_idx.data() + lo_, static_cast<size_t>(rows_) * sizeof(uint32_t));
-                build_hub_split();
-                // (the appended part hub-encoded too: a filtered dense level reads td_col)
-                be_->encode_hub_cols(col_.data() + nnz_, hx_total(), td_idx.data(), td_col_.data() + nnz_);
-              }
             }
             be_->synchronize();
           }
@@ -488,68 +468,6 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
     build_heads();
   }
   hub_sorted_ = true;
-}
-
-// Hub-split rows (several ranks): for every top-down hub h, this rank's
-// vertices adjacent to it (a row of this shard naming h in td_col), as global
-// ids in id order, appended to col_ (and, by the caller, td_col_) at
-// [hx_off[h], hx_off[h + 1]).  An undirected graph's hub row is the union of
-// every rank's part, so the parts replace the owner's row in a hub-split
-// top-down level; each rank's part is about 1/P of it (RMAT-26 at P = 8: the
-// top 2^16 hubs' parts add ~0.3 of the shard's entries).
-void DeviceGraph::build_hub_split() {
-  const int64_t K = td_nhubs_;
-  hx_off_ = DBuf<eid_t>(*be_, static_cast<size_t>(K + 1));
-  be_->memset_async(hx_off_.data(), 0, hx_off_.bytes());
-  ShardView v = view();
-  be_->hx_count(v, hx_off_.data());
-  be_->exclusive_scan(hx_off_.data(), K);
-  eid_t total = 0;
-  be_->to_host(&total, hx_off_.data() + K, sizeof(total));
-  // col_ and td_col_ grown to nnz + total entries (the rows keep their place)
-  auto grow = [&](DBuf<vid_t>& b) {
-    DBuf<vid_t> nb(*be_, static_cast<size_t>(std::max<int64_t>(nnz_ + total, 1)));
-    if (nnz_) be_->copy_async(nb.data(), b.data(), static_cast<size_t>(nnz_) * sizeof(vid_t));
-    b = std::move(nb);
-  };
-  grow(col_);
-  grow(td_col_);
-  v = view();
-  {
-    DBuf<eid_t> cursor(*be_, static_cast<size_t>(std::max<int64_t>(K, 1)));
-    be_->copy_async(cursor.data(), hx_off_.data(), static_cast<size_t>(K) * sizeof(eid_t));
-    be_->hx_fill(v, cursor.data(), col_.data() + nnz_);
-    be_->synchronize();
-  }
-  // each part in id order (a hub's targets then sweep the bitmaps monotonically)
-  be_->sort_rows_by_id(hx_off_.data(), col_.data() + nnz_, K, part_.n);
-  // absolute offsets into col_
-  std::vector<eid_t> off(static_cast<size_t>(K + 1));
-  be_->to_host(off.data(), hx_off_.data(), off.size() * sizeof(eid_t));
-  for (auto& o : off) o += nnz_;
-  be_->to_device(hx_off_.data(), off.data(), off.size() * sizeof(eid_t));
-}
-
-int64_t DeviceGraph::hx_total() const {
-  if (!hx_off_.data()) return 0;
-  eid_t a[2] = {0, 0};
-  be_->to_host(&a[0], hx_off_.data(), sizeof(eid_t));
-  be_->to_host(&a[1], hx_off_.data() + td_nhubs_, sizeof(eid_t));
-  return a[1] - a[0];
-}
-
-DeviceGraph::HubSplitHost DeviceGraph::hub_split_host() const {
-  HubSplitHost h;
-  if (!hx_off_.data()) return h;
-  h.hubs.resize(static_cast<size_t>(td_nhubs_));
-  h.off.resize(static_cast<size_t>(td_nhubs_ + 1));
-  be_->to_host(h.hubs.data(), td_hub_vertex_.data(), h.hubs.size() * sizeof(vid_t));
-  be_->to_host(h.off.data(), hx_off_.data(), h.off.size() * sizeof(eid_t));
-  const eid_t base = h.off[0];
-  for (auto& o : h.off) o -= base;
-  h.col.resize(static_cast<size_t>(h.off.back()));
-  if (!h.col.empty()) be_->to_host(h.col.data(), col_.data() + base, h.col.size() * sizeof(vid_t));
-  return h;
 }
 
 void DeviceGraph::build_heads(const uint32_t* hub_idx) {
@@ -653,11 +571,16 @@ FaultSpec FaultSpec::from_env() {
     if (k == "rank") f.rank = std::stoi(v);
     else if (k == "level") f.level = std::stoi(v);
     else if (k == "kind") f.kind = v;
+    else if (k == "ms") f.ms = std::stoi(v);
     else DBFS_CHECK(false, "DBFS_FAULT_INJECT: unknown key '" + k + "'");
     pos = comma + 1;
   }
-  DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang" || f.kind == "device",
-             "DBFS_FAULT_INJECT: kind must be throw|exit|hang|device");
+  DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang" || f.kind == "device" || f.kind == "delay" ||
+                 f.kind == "rccl_init" || f.kind == "peer_init",
+             "DBFS_FAULT_INJECT: kind must be throw|exit|hang|device|delay|rccl_init|peer_init");
+  // (rccl_init / peer_init: the communicators' setup fails -- NcclComm /
+  // PeerComm read them; the engine injects nothing)
+  if (f.kind == "rccl_init" || f.kind == "peer_init") f.rank = -1;
   return f;
 }
 
@@ -678,6 +601,13 @@ void Engine::inject_fault(int level) {
     // a kernel-side bounds violation (recorded, not raised: the traversal
     // completes and Engine::check_device fails it afterwards)
     be_.inject_device_check();
+    return;
+  }
+  if (fault_.kind == "delay") {
+    // this rank enqueues the level late (the host sleeps before its chain):
+    // its peers' kernels of that level are already waiting for its
+    // exchanges on the device -- the traversal must still complete exactly
+    std::this_thread::sleep_for(std::chrono::milliseconds(fault_.ms));
     return;
   }
   const std::string what = "injected fault (" + fault_.kind + ") at level " + std::to_string(level) + " on rank " +
@@ -719,24 +649,12 @@ void Engine::alloc_bitmap_state() {
   qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
   // several ranks: kStatsBlocks blocks of [local count, local degree sum,
-  // global count, global degree sum, hub frontier words] (see stats_block)
-  // (+ hub-split levels: [4] hubs, then the top-down hubs' bits)
-  const int64_t td_nh = g_.view().td_nhubs;
-  stats_stride_ = div_up(kHxStatsWord + div_up(std::max<int64_t>(g_.nhubs(), td_nh), kWordBits), 8) * 8;
-  if (exchange() && g_.view().hx_off) {
-    hx_bits_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(td_nh, kWordBits)));
-    hx_tot_ = DBuf<int64_t>(be_, 2);
-    be_.memset_async(hx_bits_.data(), 0, hx_bits_.bytes());
-    be_.memset_async(hx_tot_.data(), 0, hx_tot_.bytes());
-  }
+  // global count, global degree sum, ...] (one 64-byte line each; block 0's
+  // [4..5] also hold the degree moments before the first run)
+  stats_stride_ = 8;
   stats_ = DBuf<int64_t>(be_, static_cast<size_t>(exchange() ? kStatsBlocks * stats_stride_ : std::max<int64_t>(stats_stride_, 8)));
   be_.memset_async(stats_.data(), 0, stats_.bytes());
   if (g_.nhubs() > 0) hub_front_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(g_.nhubs(), kWordBits)));
-  if (exchange()) {
-    const ShardView gv = g_.view();
-    const bool ok = gv.hub_bits && gv.hub_deg && gv.nz_rec && gv.unit_base && gv.nz_pref && gv.nz_row_off && gv.head;
-    cut_ranks_ok_ = comm_.sum_host(ok ? 1 : 0) == part_.nranks;
-  }
   // Zero-degree (and padding) vertices can never be discovered: they start out
   // visited, so bottom-up steps skip them without touching row_off.
   ZeroDegArgs za;

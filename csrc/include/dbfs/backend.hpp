@@ -79,26 +79,10 @@ struct ShardView {
   // vertex of degree >= the hub threshold, so a hub-first row's hubs are a
   // prefix of it).  Read by the hub-cut bottom-up level (BuArgs::cut_edges).
   const word_t* hub_bits = nullptr;
-  // Several ranks, hub-split top-down levels (EngineOptions::hx_levels):
-  // this rank's part of every top-down hub's row -- the hub's neighbours among
-  // this rank's own vertices, as global ids, in id order -- at
-  // col[hx_off[h] .. hx_off[h + 1]) (and td_col, hub-encoded), past the
-  // rows' nnz entries (td_nhubs + 1 absolute offsets).  A vertex is a
-  // top-down hub iff its degree >= td_hub_min_deg.
-  const eid_t* hx_off = nullptr;
-  uint32_t td_hub_min_deg = 0;
-  // ... and each owned row's top-down hub index (UINT32_MAX: not a hub), so a
-  // settled hub finds its part with one load instead of a binary search over
-  // td_hub_vertex (a dependent chain of 16 loads per claiming wave).
-  const uint32_t* hx_index = nullptr;
   // Degree of every hub (nhubs entries; several ranks: a hub's row lives on
   // its owner, so the hub-cut decision sums these instead of row lengths).
   const uint32_t* hub_deg = nullptr;
 };
-
-// Work-list entry without a frontier vertex of this rank (a hub-split entry of
-// a hub owned elsewhere): its qv, whose frontier bit the consumer must not clear.
-constexpr vid_t kNoRow = 0xFFFFFFFFu;
 
 // At most kTdMaxHubs top-down hubs (their visited bits, 8 KiB, sit in LDS
 // next to the top-down owner map: five 256-thread workgroups per CU).
@@ -309,27 +293,6 @@ struct ScanArgs {
 // Device loop, several ranks: after the totals' all-reduce (stats[2..3] =
 // global count / degree sum), one thread runs level_ctrl_finish (seed: from
 // ctrl_init) and stamps rec / the mailbox, as the one-rank scan does.
-// Hub-split top-down levels (several ranks): the level's end also appends,
-// to the level's output work list, an entry per frontier hub -- this rank's
-// part of the hub's row (ShardView::hx_off) -- for every set bit of bits
-// (kTdMaxHubs bits in hub-index order, the all-reduced stats words [5 ..]:
-// each hub's bit comes from its owner alone, so the sum is the OR).  The
-// list's local totals list_stats[0..1] (entries, edges) grow accordingly;
-// entries of hubs owned elsewhere carry qv = kNoRow.  One workgroup, after the
-// reduction (LevelFinishArgs::hx.bits set: active).
-struct HxAppendArgs {
-  const int64_t* bits = nullptr;
-  const eid_t* hx_off = nullptr;
-  const vid_t* hub_vertex = nullptr;  // ShardView::td_hub_vertex (ascending)
-  int64_t nhubs = 0;
-  int64_t lo = 0, rows = 0;
-  int64_t* list_stats = nullptr;
-  int64_t* qscan = nullptr;
-  int64_t* qbase = nullptr;
-  int32_t* blk_vstart = nullptr;
-  vid_t* qv = nullptr;
-};
-
 struct LevelFinishArgs {
   const int64_t* stats = nullptr;
   LevelCtrl* ctrl = nullptr;
@@ -340,12 +303,7 @@ struct LevelFinishArgs {
   bool seed = false;
   int32_t expect_dir = 0;
   int64_t expect_cap = 0;  // see ScanArgs::expect_cap
-  HxAppendArgs hx;         // hub-split entries of the next level (hx.bits: on)
 };
-
-// Words of a hub-split level's end in its stats block: [2] count, [3] degree
-// sum, [4] hubs diverted, then the frontier hubs' bits (kHxStatsWord ...).
-constexpr int64_t kHxStatsWord = 5;
 
 // A device-loop chain's kernels run only when the chain is live: the level is
 // not done, its direction is the one the chain was enqueued for, and (list-form
@@ -435,13 +393,17 @@ struct FrontierTable {
   const uint64_t* src[kMaxDirectRanks];
 };
 
+// A timed-out device wait's error word: the collective's sequence number
+// (low 48 bits) and 1 + the peer it found missing (bits 48..55; 0: unknown).
+constexpr uint64_t kWaitSeqMask = (uint64_t(1) << 48) - 1;
+
 struct DirectExchange {
   int active = 0;  // 0: the exchange goes through a Comm collective instead
   int nranks = 1, rank = 0;
   uint64_t seq = 0;                     // this exchange's sequence number (the cells' tag)
   const DirectTable* table = nullptr;   // device memory
   uint64_t timeout_ticks = 0;           // a wait gives up after this many wall-clock ticks
-  uint64_t* error = nullptr;            // ... and stores seq here (the host watches it)
+  uint64_t* error = nullptr;            // ... and stores kWaitSeqMask & seq | (peer + 1) << 48 here (the host watches it)
   // a level end: the all-reduced totals as recorded (shadow replay) instead
   // of the peers' cells summed
   const int64_t* result = nullptr;
@@ -580,18 +542,6 @@ struct TdSparseArgs {
   // Comm::level_end without a frontier gather; no collective launch after.
   DirectExchange end;
   LevelFinishArgs fin;
-  // Hub-split top-down (several ranks, ShardView::hx_off): a settled vertex
-  // of degree >= g.td_hub_min_deg (a top-down hub) gets its level and frontier
-  // bit but no entry in the output work list -- every rank expands its own
-  // part of the hub's row at the next level instead (the level end appends
-  // them, HxAppendArgs) -- its bit goes to hx_bits (hub index order, zero on
-  // entry) and its count / degree to hx_tot[0..1] (zero on entry).  The
-  // level's last workgroup adds them to the totals (stats[2..3], stats[4] =
-  // hubs), moves hx_bits to hx_out (the stats block's hub words) and zeroes
-  // hx_bits / hx_tot.
-  word_t* hx_bits = nullptr;
-  int64_t* hx_tot = nullptr;
-  int64_t* hx_out = nullptr;
 };
 
 // Binned top-down level (one rank, large frontiers; propagation blocking):
@@ -798,25 +748,6 @@ struct BuArgs {
   int64_t cut_edges = 0;
   int* cut_flag = nullptr;
   uint8_t* cut_claim = nullptr;
-  // ... several ranks: this rank's non-hub frontier is the owned slice of
-  // `frontier` (words from cut_fr_base, also in g.hub_bits); an unvisited own
-  // neighbour is claimed in place, a remote one -- after a fetch-or of its bit
-  // in the replicated cut_visited, so each goes out at most once -- is
-  // appended to its owner's list (cut_lists: the sparse levels' owner lists,
-  // cut_list_stride words each, owner = v / part; cut_direct.active: stored
-  // straight into the owner's window, the last workgroup of cut_prep_ticket
-  // publishing the counts).  bu_cut_apply then claims the received ids
-  // (cut_recv_lists, or the window) on their owner, before the bottom-up
-  // kernel reads the claims.  nranks > 1 selects this path.
-  int64_t cut_fr_base = 0;
-  vid_t* cut_lists = nullptr;
-  int64_t cut_list_stride = 0;
-  int64_t part = 0;
-  int nranks = 1;
-  word_t* cut_visited = nullptr;
-  DirectExchange cut_direct;
-  unsigned* cut_prep_ticket = nullptr;
-  const vid_t* cut_recv_lists = nullptr;
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
@@ -1069,8 +1000,9 @@ class Backend {
   // Hub-cut level's top-down part (BuArgs::cut_edges): the unvisited
   // neighbours of the frontier's non-hub vertices claimed into a.pre.
   virtual void bu_cut_prep(const BuArgs& a) = 0;
-  // ... several ranks: the claims received from the other ranks (BuArgs::cut_lists)
-  virtual void bu_cut_apply(const BuArgs& a) = 0;
+  // A direct exchange's wait as a launch of its own, one wave (ranks sharing
+  // a GPU, Comm::split_waits): the consumer after it finds the cells tagged.
+  virtual void direct_prewait(const DirectExchange& x) { (void)x; }
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their
@@ -1117,12 +1049,6 @@ class Backend {
   // (ceil(rows / 4096) + 1 entries).
   virtual void nz_records(const eid_t* row_off, const vid_t* head, int64_t rows, const eid_t* nz_pref, NzRec* rec,
                           eid_t* unit_base) = 0;
-  // Hub-split rows (ShardView::hx_off): cnt[h] += entries of the rows whose
-  // td_col neighbour is top-down hub h (td_col hub-encoded, cnt zeroed by the
-  // caller); then, after an exclusive scan into cursor, out[cursor[h]++] = lo
-  // + r for every such entry of row r.
-  virtual void hx_count(const ShardView& g, eid_t* cnt) = 0;
-  virtual void hx_fill(const ShardView& g, eid_t* cursor, vid_t* out) = 0;
   // out[e] = kHubFlag | hub_idx[col[e]] for hub neighbours, else col[e].
   virtual void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) = 0;
   // Hubs = vertices of degree >= min_deg (deg_all has n entries): hub_vertex

@@ -34,7 +34,7 @@ namespace dbfs {
 
 // Failure detection: a collective that waits longer than this
 // for its peers fails with an error instead of hanging.  DBFS_COMM_TIMEOUT_S,
-// default 600 s; 0 disables the limit.
+// default 120 s; 0 disables the limit.
 double comm_timeout_s();
 
 class Comm {
@@ -143,7 +143,17 @@ class Comm {
   const Traffic& traffic() const { return traffic_; }
   void reset_traffic() { traffic_ = Traffic{}; }
 
+  // The level whose chain the engine is enqueueing (-1: none): a transport
+  // names it when a collective of that chain fails or times out.
+  void set_level_tag(int level) { level_tag_ = level; }
+  // Ranks sharing a GPU (peer transport): a kernel that waits for a peer
+  // must not spin in every workgroup of a large grid -- a co-resident rank's
+  // producer may need those CUs -- so the waits run as one-wave launches
+  // first (Backend::direct_prewait) and the collectives unfused.
+  virtual bool split_waits() const { return false; }
+
  protected:
+  int level_tag_ = -1;
   void note(TrafficKind k, int64_t bytes) {
     ++traffic_.calls[k];
     traffic_.bytes[k] += bytes;
@@ -270,7 +280,11 @@ class GroupBootstrap final : public Bootstrap {
 // RCCL communicator (defined in csrc/comm/nccl_comm.cpp).
 class NcclComm final : public Comm {
  public:
-  // Multi-process: every rank passes the same 128-byte unique id.
+  // Multi-process: every rank passes the same 128-byte unique id.  The
+  // communicator is nonblocking (ncclConfig_t::blocking = 0), so its
+  // construction is bounded: DBFS_RCCL_INIT_TIMEOUT_S (default 60 s), then
+  // ncclCommAbort and an error -- a bootstrap that never completes (a peer
+  // that died, a fabric problem) fails the setup instead of hanging it.
   NcclComm(const std::string& unique_id, int rank, int nranks, Backend& be);
   ~NcclComm() override;
   static std::string unique_id();
@@ -294,6 +308,8 @@ class NcclComm final : public Comm {
   NcclComm() = default;
   void install_watchdog();
   void check_alive() const;
+  // a nonblocking communicator's call: ncclInProgress polled to completion
+  void settle(int result, const char* what, const char* file, int line);
   void* comm_ = nullptr;  // ncclComm_t
   int rank_ = 0, size_ = 1;
 };
@@ -430,6 +446,18 @@ class PeerComm final : public Comm {
   int64_t inner_ops() const { return inner_ops_; }
   // the direct exchanges are on (off: DBFS_PEER_DIRECT=0, or their self-test failed)
   bool direct_on() const { return dtab_ != nullptr; }
+  // the pushed frontier slices are on (off: DBFS_PEER_FRONTIER_MB=0, or their self-test failed)
+  bool frontier_on() const { return ftab_ != nullptr; }
+  bool fused() const { return fused_; }
+  bool split_waits() const override { return shared_; }
+  // Topology seen at construction: every rank's PCI bus id, and access[r * P
+  // + p] = 2 (ranks r and p share a GPU), 1 (rank r's GPU can access p's),
+  // 0 (it cannot), -1 (p's GPU not visible to rank r's process).
+  const std::vector<std::string>& bus_ids() const { return bus_; }
+  const std::vector<int>& peer_access() const { return access_; }
+  bool shared_device() const { return shared_; }
+  // the last self_test's verdict ("ok" or why it failed; "" before one ran)
+  const std::string& self_test_verdict() const { return verdict_; }
 
  private:
   struct Piece {
@@ -450,11 +478,12 @@ class PeerComm final : public Comm {
     int64_t sum_count = 0;
     int64_t* sum_buf = nullptr;
     const LevelFinishArgs* finish = nullptr;  // then the level's decision (sum_count <= kPeerFinishMax)
+    const char* op = "collective";            // (a timed-out wait names it)
   };
   void run(const Plan& plan);
   // pieces larger than a slot: nrounds launches of run(), slot-sized slices
   void rounds(const std::vector<const char*>& src, const std::vector<int64_t>& sb, const std::vector<char*>& dst,
-              const std::vector<int64_t>& rb, int64_t nrounds);
+              const std::vector<int64_t>& rb, int64_t nrounds, const char* op);
   int64_t nrounds(int64_t bytes) const;
   void direct_self_test();  // (self_test's second part)
   std::shared_ptr<Bootstrap> boot_;
@@ -486,6 +515,20 @@ class PeerComm final : public Comm {
   bool watch_installed_ = false;
   char* slot_ptr(int owner, int parity, int sender) const;
   void release();
+  // several ranks on one physical GPU (bus ids): unfused collectives, split waits
+  bool shared_ = false;
+  std::vector<std::string> bus_;
+  std::vector<int> access_;
+  std::string verdict_;
+  // what each recent sequence number was (a timed-out wait names it)
+  struct Tag {
+    uint64_t seq = 0;
+    int level = -1;
+    const char* op = "";
+  };
+  std::vector<Tag> tags_ = std::vector<Tag>(1024);
+  void tag(uint64_t seq, const char* op) { tags_[seq % tags_.size()] = Tag{seq, level_tag_, op}; }
+  std::string describe_error(uint64_t word) const;
 };
 
 // Minimal TCP bootstrap (rank 0 hosts) used to ship the RCCL unique id and for

@@ -68,9 +68,7 @@ class DeviceGraph {
   // hub-encoded copy and `col` is then put in neighbour-id order for the
   // top-down sweeps (neighbours of one row probe the bitmaps monotonically).
   // ... and with `td_hubs` also the hub-encoded top-down copy td_col (the
-  // kTdMaxHubs highest-degree vertices encoded; one more nnz x 4 B), and with
-  // several ranks the hub-split rows (ShardView::hx_off): this rank's part
-  // of every top-down hub's row, for the hub-split top-down levels.
+  // kTdMaxHubs highest-degree vertices encoded; one more nnz x 4 B).
   void sort_neighbors_by_degree(Comm& comm, bool hubs = true, int64_t max_hubs = kMaxHubs, bool id_order = true,
                                 bool td_hubs = true);
   bool hub_sorted() const { return hub_sorted_; }
@@ -87,14 +85,6 @@ class DeviceGraph {
     int64_t byte_begin = -1, byte_end = -1, edges = -1;
   };
   const IngestInfo& ingest() const { return ingest_; }
-  // Hub-split rows copied back (tests): the top-down hubs (ascending), the
-  // offsets of their parts relative to the first, and the parts (global ids)
-  struct HubSplitHost {
-    std::vector<vid_t> hubs;
-    std::vector<eid_t> off;
-    std::vector<vid_t> col;
-  };
-  HubSplitHost hub_split_host() const;
 
  private:
   IngestInfo ingest_;
@@ -107,14 +97,8 @@ class DeviceGraph {
   int64_t nhubs_ = 0;
   void build_heads(const uint32_t* hub_idx = nullptr);
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
-  // several ranks: hub-split rows (ShardView::hx_off), appended to col_ / td_col_
-  DBuf<eid_t> hx_off_;
-  DBuf<uint32_t> hx_index_;  // ShardView::hx_index (owned rows)
-  uint32_t td_hub_min_deg_ = 0;
   double td_hub_share_ = 0.0;
   DBuf<uint32_t> hub_deg_;  // ShardView::hub_deg
-  void build_hub_split();
-  int64_t hx_total() const;
   DBuf<word_t> hub_bits_;  // global vertex bitmap of the hubs
   int64_t td_nhubs_ = 0;
   DBuf<eid_t> nz_pref_, nz_row_off_;
@@ -127,10 +111,13 @@ class DeviceGraph {
 
 struct EngineOptions {
   Mode mode = Mode::DirOpt;
-  // Beamer's direction switch.  Defaults tuned on MI355X / RMAT-26 (sweep in
+  // Beamer's direction switch.  Defaults tuned on MI355X / RMAT-26 (sweeps in
   // profiles/): BU is cheap enough here that switching earlier than Beamer's
-  // CPU value (14) pays.
-  double alpha = 24.0;  // TD -> BU when m_f > m_u / alpha
+  // CPU value (14) pays.  alpha 40 (from 24, round 4): the same on the
+  // bench's roots, +5 % on roots with a slower-growing frontier (a 64-root
+  // tuning sample, seed 20261017; profiles/r4_final_alpha_sweep.txt), the
+  // soc-LiveJournal1-sized graph unchanged.
+  double alpha = 40.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 96.0;   // BU -> TD when n_f < n / beta (and shrinking)
   // neighbours a lane checks itself before rows go to wave-cooperative scans
   // (16: a first bottom-up level entered with a small frontier resolves more
@@ -305,18 +292,6 @@ struct EngineOptions {
   // remote visited bits, as a filter: a stale one sends an id its owner drops,
   // so the merge is not needed (off: validated as xfuse_edges).
   bool bu_merge_visited = false;
-  // Several ranks, hub-split top-down levels: the sparse chains of the first
-  // hx_levels levels (before any bottom-up level) divert the top-down hubs
-  // they settle from the owner's work list -- every rank then expands its own
-  // part of each frontier hub's row (ShardView::hx_off), claims local, no
-  // exchange -- their bits ride the level end.  Replaces the owner expanding a
-  // hub's whole row and shipping its claims (bfs.cu:577-586, 143).  0: off.
-  // Off by default: shadow ranks of RMAT-26 at P = 8 (8 roots, ranks 0 / 7)
-  // measured it slower -- levels 0-2 of root 13702079 5.6 / 12.4 / 57.3 ->
-  // 11.8 / 19.9 / 85.4 us: the hub-split chains lose the fused tiny-level
-  // launch and the folded level end, and the split td_sparse of the hubs'
-  // parts ran 24 -> 54 us (profiles/r4_s3_shadow_*).
-  int hx_levels = 0;
   // One rank, device loop, hubs: a first bottom-up level whose frontier has
   // at most bu_cut_edges edges outside the hubs claims those vertices'
   // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
@@ -328,13 +303,6 @@ struct EngineOptions {
   // the late-switch first bottom-up levels have 4-15 % of them, the others
   // 37 % and more)
   double bu_cut_mf_frac = 0.25;
-  // ... also with several ranks (the non-hub frontier's remote claims through
-  // the owner lists, bu_cut_apply on the owners).  Off by default: at P = 8
-  // (shadow ranks, RMAT-26) the late-switch first bottom-up level took
-  // 119 -> 167 us with it -- bu_cut_prep 67 us + bu_cut_apply 10 us against the
-  // 33 us the cut saves a rank's bottom-up kernel (105 -> 72 us), whose share
-  // of the level already shrank 8x (profiles/r4_s3_shadow_trace_*).
-  bool bu_cut_ranks = false;
   // ... on a transport that ships the lists' capacity (RCCL / TCP fallback;
   // the peer windows ship their lengths), a chain's lists hold
   // list_cap_factor x the predicted edges (a power of two >= 1024)
@@ -351,8 +319,9 @@ struct EngineOptions {
   // level next (graphs with hubs): the producing kernels push their output
   // words straight into the peers' windows (Comm::direct_frontier) and the
   // bottom-up level's hub_gather copies them in -- the level end carries only
-  // its totals (and may fold into the bottom-up kernel).  Off until measured.
-  bool direct_frontier = false;
+  // its totals (and may fold into the bottom-up kernel): the frontier
+  // exchange overlaps the kernels that produce it instead of following them.
+  bool direct_frontier = true;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is
@@ -401,11 +370,6 @@ struct ChainRecord {
   char form = 'T';
   int64_t cap = 0;
   bool gather = false;
-  // hub-split chain: its level end all-reduces this many words more than the
-  // totals (the hub count and the frontier-hub bits)
-  int64_t hx_words = 0;
-  // several ranks: a hub-cut bottom-up chain (its owner-list exchange)
-  bool cut = false;
   // several ranks: its output frontier pushed by its kernels (no gather in
   // its level end; EngineOptions::direct_frontier)
   bool push = false;
@@ -429,6 +393,7 @@ struct RunResult {
 struct FaultSpec {
   int rank = -1, level = -1;
   std::string kind = "throw";
+  int ms = 2000;  // kind=delay: how long the rank sleeps before enqueueing the level
   static FaultSpec from_env();
 };
 
@@ -486,8 +451,6 @@ class Engine {
   DBuf<uint8_t> level8_;
   DBuf<uint32_t> td_group_ticket_;  // UpdateArgs::group_ticket
   DBuf<int64_t> bu_tot_;  // fused bottom-up finish: per-workgroup totals (BuArgs::tot)
-  DBuf<word_t> hx_bits_;  // hub-split levels: TdSparseArgs::hx_bits (zero between levels)
-  DBuf<int64_t> hx_tot_;  // ... TdSparseArgs::hx_tot
   DBuf<int64_t> td_tot_;  // fused top-down finish: the level's totals (UpdateArgs::tot)
   DBuf<uint8_t> td_hub_mark_;  // TdArgs::td_hub_mark (kTdMaxHubs bytes; zero between levels)
   bool level8_filled_ = false;        // level8_ reads unreached for the current run without a fill
@@ -506,15 +469,11 @@ class Engine {
   DBuf<int64_t> cut_part_;
   DBuf<int> cut_flag_;
   DBuf<uint8_t> cut_claim_;  // wide-level runs' claims
-  DBuf<unsigned> cut_ticket_, cut_prep_ticket_;
-  // several ranks: every rank's shard has what a hub-cut level needs (packed
-  // records, hub degrees, lists) -- agreed once, the cut's collectives are
-  // enqueued by every rank or by none
-  bool cut_ranks_ok_ = false;
+  DBuf<unsigned> cut_ticket_;
   DBuf<uint8_t> next_bytes_;  // lazily allocated (GW * 64 bytes)
   DBuf<vid_t> send_lists_, recv_lists_;  // sparse exchange, lazily allocated
   DBuf<int64_t> unit_cnt_, unit_deg_, part_cnt_, part_deg_, qscan_, qbase_, stats_;
-  // Several ranks (device loop): level L's totals (and carried hub bits) go to
+  // Several ranks (device loop): level L's totals go to
   // stats block (L + 1) % kStatsBlocks, so a mispredicted chain's
   // (unpredicated) reduction never touches the block the re-enqueued chain
   // reads.  stats_stride_: int64 entries per block.

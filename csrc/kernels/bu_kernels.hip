@@ -811,134 +811,44 @@ __global__ __launch_bounds__(kThreads) void hub_gather_kernel(HubGatherArgs a) {
 // (kernel trace; grid 256-4096 workgroups flat); a list of the vertices, a
 // wave each, spent 109 us in the list's same-address appends alone; claims
 // in a bitmap by device atomics 160 us.
-// Several ranks: a remote neighbour is claimed in the replicated visited
-// bitmap (fetch-or: each goes out at most once) and appended to its owner's
-// list -- or, with a direct exchange, stored into the owner's window; the
-// workgroups' last one publishes the counts (empty on a level that does not
-// cut: the peers wait for every exchange).
+// (One rank: with several ranks the cut's top-down part -- every rank's own
+// non-hub frontier, its remote claims through owner lists -- cost a rank more
+// than it saved it at P = 8, round 4's shadow replay; the level runs plain.)
 constexpr int kCutThreads = 1024;
-// (kLists: several ranks, remote claims to the owner lists -- a variant of its
-// own: the list code cost the one-rank cut 53.6 -> 56.3 us a level)
-template <bool kLists>
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
-  constexpr bool lists = kLists;
-  const bool dx = lists && a.cut_direct.active;
-  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) {
-    if (dx && blockIdx.x == 0) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, false);
-    return;
-  }
-  __shared__ int s_last;
+  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) return;
   const vid_t* __restrict__ col = a.g.col;
   const eid_t* __restrict__ ro = a.g.row_off;
-  const uint64_t lo = static_cast<uint64_t>(a.g.lo), rows = static_cast<uint64_t>(a.g.rows);
   const int lane = lane_id();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kCutThreads;
   for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCutThreads + (threadIdx.x & ~(kWave - 1)); w0 < a.words;
        w0 += stride) {
     const int64_t w = w0 + lane;
-    word_t m = w < a.words ? a.frontier[a.cut_fr_base + w] & ~a.g.hub_bits[a.cut_fr_base + w] : 0ull;
+    word_t m = w < a.words ? a.frontier[w] & ~a.g.hub_bits[w] : 0ull;
     for (unsigned long long bm = __ballot(m != 0); bm; bm = __ballot(m != 0)) {
       const int l = __ffsll(static_cast<long long>(bm)) - 1;
       const int64_t v = (w0 + l) * 64 + __builtin_ctzll(static_cast<word_t>(__shfl(static_cast<long long>(m), l, kWave)));
       if (lane == l) m &= m - 1;
       const eid_t rs = ro[v], re = ro[v + 1];
       constexpr int kU = 4;
-      // (wave-uniform loop: the owner lists' appends are wave operations)
-      for (eid_t b0 = rs; b0 < re; b0 += kU * kWave) {
+      for (eid_t b0 = rs + lane; b0 < re; b0 += kU * kWave) {
         vid_t t[kU];
         word_t vw[kU];
-        bool own[kU];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-          const eid_t e = b0 + k * kWave + lane;
+          const eid_t e = b0 + k * kWave;
           t[k] = e < re ? col[e] : kNoVertex;
-          own[k] = static_cast<uint64_t>(t[k]) - lo < rows;
         }
 #pragma unroll
-        for (int k = 0; k < kU; ++k)
-          vw[k] = t[k] == kNoVertex ? ~0ull
-                                    : own[k] ? a.visited[(t[k] - lo) >> 6] : (lists ? a.cut_visited[t[k] >> 6] : ~0ull);
-        unsigned remote = 0;
+        for (int k = 0; k < kU; ++k) vw[k] = t[k] == kNoVertex ? ~0ull : a.visited[t[k] >> 6];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
-          const uint32_t tb = own[k] ? static_cast<uint32_t>(t[k] - lo) : t[k];
-          if ((vw[k] >> (tb & 63)) & 1ull) continue;
-          if (own[k]) {
-            if (a.cut_claim) a.cut_claim[tb] = 1;  // (wide levels: the bottom-up kernel writes them)
-            else store_level(nullptr, a.level8, tb, a.new_level, a.narrow_base);
-          } else if (!(atomicOr(a.cut_visited + (t[k] >> 6), 1ull << (t[k] & 63)) & (1ull << (t[k] & 63)))) {
-            remote |= 1u << k;
-          }
-        }
-        if (lists && __ballot(remote != 0)) {
-#pragma unroll
-          for (int k = 0; k < kU; ++k)
-            owner_list_append(a.cut_lists, a.cut_list_stride, a.part, t[k], (remote >> k) & 1u,
-                              dx ? a.cut_direct.table : nullptr);
+          if ((vw[k] >> (t[k] & 63)) & 1ull) continue;
+          if (a.cut_claim) a.cut_claim[t[k]] = 1;  // (wide levels: the bottom-up kernel writes them)
+          else store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
         }
       }
     }
-  }
-  if (!dx) return;
-  // every wave's write-through stores drained, the workgroups' ticket, the
-  // last one publishes the counts (as td_sparse)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    s_last = atomicAdd(a.cut_prep_ticket, 1u) == gridDim.x - 1;
-    if (s_last) {
-      *a.cut_prep_ticket = 0u;
-      last_arriver_acquire();
-    }
-  }
-  __syncthreads();
-  if (s_last) direct_publish(a.cut_direct, a.cut_lists, a.cut_list_stride, true);
-}
-
-// Several ranks, a hub-cut level: the claims the other ranks sent for this
-// rank's vertices -- from this rank's window after the peers' cells (direct),
-// or from cut_recv_lists -- written as level bytes (claim bytes with wide
-// levels) of the still unvisited ones, before the bottom-up kernel reads the
-// claims.  Every workgroup waits for the cells (every exchange is awaited,
-// live or not); the entries form one index space the grid strides over.
-constexpr int kCutApplyThreads = 256;
-__global__ __launch_bounds__(kCutApplyThreads) void bu_cut_apply_kernel(BuArgs a) {
-  __shared__ uint64_t s_cnt[kern::kMaxPeers];
-  __shared__ long long s_end[kern::kMaxPeers];
-  __shared__ const vid_t* s_src[kern::kMaxPeers];
-  const int t = threadIdx.x;
-  const bool dx = a.cut_direct.active;
-  if (dx && direct_wait(a.cut_direct, s_cnt, nullptr) != kWaitOk) return;
-  // (collective exchange: it has read the send lists -- their counts restart
-  // from zero; a direct one's publisher zeroed them)
-  if (!dx && blockIdx.x == 0 && t < a.nranks) a.cut_lists[static_cast<int64_t>(t) * a.cut_list_stride] = 0u;
-  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) return;
-  if (t < kWave) {
-    long long n = 0;
-    if (t < a.nranks) {
-      const vid_t* src = dx ? a.cut_direct.table->src[t] : a.cut_recv_lists + static_cast<int64_t>(t) * a.cut_list_stride;
-      s_src[t] = src;
-      n = dx ? static_cast<long long>(s_cnt[t]) : static_cast<long long>(*src);
-    }
-    DBFS_DCHECK(n < a.cut_list_stride, 13, n);
-    const long long incl = wave_incl_scan(n);
-    if (t < a.nranks) s_end[t] = incl;
-  }
-  __syncthreads();
-  const long long total = s_end[a.nranks - 1];
-  const int64_t lo = a.g.lo;
-  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kCutApplyThreads + t; j < total;
-       j += static_cast<int64_t>(gridDim.x) * kCutApplyThreads) {
-    int r = 0;
-    while (s_end[r] <= j) ++r;  // (<= kMaxPeers lists)
-    const long long before = r > 0 ? s_end[r - 1] : 0;
-    const vid_t* src = s_src[r] + 1 + (j - before);
-    const vid_t v = dx ? sys_load_u32(src) : *src;
-    const int64_t row = static_cast<int64_t>(v) - lo;
-    DBFS_DCHECK(row >= 0 && row < a.g.rows, 14, v);
-    if ((a.visited[row >> 6] >> (row & 63)) & 1ull) continue;
-    if (a.cut_claim) a.cut_claim[row] = 1;
-    else store_level(nullptr, a.level8, row, a.new_level, a.narrow_base);
   }
 }
 
@@ -1061,20 +971,9 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 void bu_cut_prep(const BuArgs& a, hipStream_t st) {
   DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && (a.level8 || a.cut_claim) && a.g.hub_bits && a.ctrl,
              "bu_cut_prep: hub-cut arguments missing");
-  DBFS_CHECK(a.nranks <= 1 || (a.cut_lists && a.cut_visited && a.part > 0 && a.cut_list_stride > 0 &&
-                               (!a.cut_direct.active || a.cut_prep_ticket)),
-             "bu_cut_prep: several ranks need owner lists, the replicated visited bitmap and a ticket");
   // (grid measured flat from 256 to 4096 workgroups)
   const unsigned grid = grid_for(a.words, kCutThreads, 2 * device_cus());
-  if (a.nranks > 1) bu_cut_prep_kernel<true><<<grid, kCutThreads, 0, st>>>(a);
-  else bu_cut_prep_kernel<false><<<grid, kCutThreads, 0, st>>>(a);
-}
-
-void bu_cut_apply(const BuArgs& a, hipStream_t st) {
-  DBFS_CHECK(a.nranks > 1 && a.nranks <= kern::kMaxPeers && a.cut_lists && a.cut_flag &&
-                 (a.cut_direct.active || a.cut_recv_lists) && (a.level8 || a.cut_claim),
-             "bu_cut_apply: several ranks' hub-cut arguments missing");
-  bu_cut_apply_kernel<<<128, kCutApplyThreads, 0, st>>>(a);
+  bu_cut_prep_kernel<<<grid, kCutThreads, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {

@@ -292,33 +292,6 @@ __global__ __launch_bounds__(kBlock) void hub_assign_kernel(const uint32_t* __re
   }
 }
 
-// Hub-split rows (ShardView::hx_off): each wave takes 64 consecutive rows and
-// sweeps each row's td_col entries with its 64 lanes (a hub row of a million
-// entries is one wave's loop: a one-time build); an entry naming top-down hub
-// h counts for h (count) or lands at out[cursor[h]++] as the row's global id
-// (fill).
-template <bool kFill>
-__global__ __launch_bounds__(kBlock) void hx_rows_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ td_col,
-                                                         int64_t rows, int64_t lo, eid_t* __restrict__ cnt,
-                                                         vid_t* __restrict__ out) {
-  const int lane = lane_id();
-  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x) / kWave;
-  const int64_t r0 = wave * kWave;
-  for (int64_t r = r0; r < min(rows, r0 + kWave); ++r) {
-    for (eid_t e = ro[r] + lane; e < ro[r + 1]; e += kWave) {
-      const vid_t c = td_col[e];
-      if (!(c & kHubFlag)) continue;
-      const uint32_t h = c & ~kHubFlag;
-      if constexpr (kFill) {
-        const eid_t at = static_cast<eid_t>(atomicAdd(reinterpret_cast<unsigned long long*>(cnt + h), 1ull));
-        out[at] = static_cast<vid_t>(lo + r);
-      } else {
-        atomicAdd(reinterpret_cast<unsigned long long*>(cnt + h), 1ull);
-      }
-    }
-  }
-}
-
 // Range split points: thread per (range boundary y, row r), y-major (the
 // output row of a boundary is written coalesced); a binary search over the
 // row's id buckets (rows of more than 4096 entries are ordered by bucket only:
@@ -342,16 +315,6 @@ __global__ __launch_bounds__(kBlock) void range_split_kernel(const eid_t* __rest
 }
 
 }  // namespace
-
-void hx_rows(const ShardView& g, eid_t* cnt, vid_t* out, hipStream_t st) {
-  if (g.rows <= 0 || !g.td_col) return;
-  const int64_t waves = (g.rows + kWave - 1) / kWave;
-  const unsigned grid = static_cast<unsigned>((waves * kWave + kBlock - 1) / kBlock);
-  if (out)
-    hx_rows_kernel<true><<<grid, kBlock, 0, st>>>(g.row_off, g.td_col, g.rows, g.lo, cnt, out);
-  else
-    hx_rows_kernel<false><<<grid, kBlock, 0, st>>>(g.row_off, g.td_col, g.rows, g.lo, cnt, nullptr);
-}
 
 void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx,
                hipStream_t st) {

@@ -263,16 +263,23 @@ __device__ __forceinline__ void direct_publish(const DirectExchange& d, vid_t* l
 // threads p < nranks poll sender p's cell until both words asked for carry
 // this exchange's tag and leave its payload in out0 / out1 [p] (this rank's
 // own: 0).  Returns kWaitOk; kWaitTimeout after DirectExchange::timeout_ticks
-// (seq goes to the error word the host watches); kWaitLater when a cell
-// already carries a LATER exchange's tag: the peer has moved on, which it
-// does only after this rank's next signal -- so this exchange is over here
-// (a workgroup of the apply that started after the level's end: it has
-// nothing to do).  Data behind the cell is then read with sys loads.
+// (the error word the host watches gets seq | (peer + 1) << 48: which
+// exchange, and the first peer found missing), or at once when another wait
+// of this rank already timed out (the error word is set: a dead peer stops
+// every wait queued behind the first instead of each spending its own
+// timeout); kWaitLater when a cell already carries a LATER exchange's tag:
+// the peer has moved on, which it does only after this rank's next signal --
+// so this exchange is over here (a workgroup of the apply that started after
+// the level's end: it has nothing to do).  Data behind the cell is then read
+// with sys loads.
 constexpr int kWaitOk = 1, kWaitTimeout = 0, kWaitLater = -1;
 __device__ __forceinline__ int direct_wait(const DirectExchange& d, uint64_t* out0, uint64_t* out1) {
-  __shared__ int s_st;
+  __shared__ int s_st, s_peer;
   const int t = threadIdx.x;
-  if (t == 0) s_st = kWaitOk;
+  if (t == 0) {
+    s_st = kWaitOk;
+    s_peer = -1;
+  }
   __syncthreads();
   if (t < d.nranks) {
     uint64_t w0 = 0, w1 = 0;
@@ -288,9 +295,16 @@ __device__ __forceinline__ int direct_wait(const DirectExchange& d, uint64_t* ou
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        if ((spin & 255) == 255 && wall_clock64() - t0 > d.timeout_ticks) {
-          s_st = kWaitTimeout;
-          break;
+        if ((spin & 255) == 255) {
+          if (wall_clock64() - t0 > d.timeout_ticks) {
+            s_st = kWaitTimeout;
+            s_peer = t;  // (benign race: any missing peer names the stall)
+            break;
+          }
+          if (d.error && sys_load_u64(d.error) != 0) {
+            s_st = kWaitTimeout;  // (an earlier wait already reported)
+            break;
+          }
         }
       }
       w0 &= 0xffffffffull;
@@ -301,7 +315,8 @@ __device__ __forceinline__ int direct_wait(const DirectExchange& d, uint64_t* ou
   }
   __syncthreads();
   const int st = s_st;
-  if (st == kWaitTimeout && t == 0 && d.error) sys_store_u64(d.error, d.seq);
+  if (st == kWaitTimeout && t == 0 && d.error && s_peer >= 0)
+    sys_store_u64(d.error, (d.seq & kWaitSeqMask) | (static_cast<uint64_t>(s_peer + 1) << 48));
   return st;
 }
 

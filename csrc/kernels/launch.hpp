@@ -23,6 +23,8 @@ void compact_frontier(const CompactArgs& a, hipStream_t st);
 void td_expand(const TdArgs& a, hipStream_t st);
 void td_sparse(const TdSparseArgs& a, hipStream_t st);
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st);
+// A direct exchange's wait as a one-wave launch (Comm::split_waits).
+void direct_prewait(const DirectExchange& x, hipStream_t st);
 // PeerComm::self_test of the direct exchanges (`round` 0..3; mismatches and
 // timeouts counted in *err)
 void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int round, unsigned* err,
@@ -33,9 +35,6 @@ void direct_selftest(const DirectExchange& lists, const DirectExchange& end, int
 void frontier_selftest(const FrontierTable* t, int rank, int nranks, int64_t words, int round, int phase,
                        unsigned* err, hipStream_t st);
 void td_binned(const BinArgs& a, hipStream_t st);
-// graph_sort.hip: hub-split rows of ShardView::hx_off -- counts per top-down
-// hub (out == nullptr), or the rows' global ids at cnt[h]++ (cursors)
-void hx_rows(const ShardView& g, eid_t* cnt, vid_t* out, hipStream_t st);
 void level_finish(const LevelFinishArgs& a, hipStream_t st);
 void widen_levels(const uint8_t* in, lvl_t* out, int64_t n, uint8_t base, hipStream_t st);
 void pack_bytes(const PackArgs& a, hipStream_t st);
@@ -43,7 +42,6 @@ void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
 void bu_cut_prep(const BuArgs& a, hipStream_t st);
-void bu_cut_apply(const BuArgs& a, hipStream_t st);
 void hub_visited(const HubVisitedArgs& a, hipStream_t st);
 void hub_apply(const HubApplyArgs& a, hipStream_t st);
 // device-checked build (DBFS_CHECKED): whether checks are compiled in, the

@@ -143,23 +143,38 @@ __global__ __launch_bounds__(kBlock) void peer_push_kernel(PeerPushArgs a) {
   if (threadIdx.x == 0) *a.ticket = 0u;  // next push is stream-ordered after this one
 }
 
+// Lane p's wait for flags[p] >= seq (p < npeers, skip_self aside): 1 done,
+// 0 timed out (that peer never arrived), -1 another wait of this rank timed
+// out first (its error word is set: stop at once instead of spending a
+// timeout of our own behind a dead peer).
+__device__ __forceinline__ int peer_flag_wait(const PeerWaitArgs& a, int p) {
+  const uint64_t t0 = wall_clock64();
+  for (uint32_t spin = 0;; ++spin) {
+    if (__hip_atomic_load(a.flags + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= a.seq) return 1;
+    __builtin_amdgcn_s_sleep(2);
+    if ((spin & 255) == 255) {
+      if (wall_clock64() - t0 > a.timeout_ticks) return 0;
+      if (a.error && __hip_atomic_load(a.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return -1;
+    }
+  }
+}
+
+// The error word of a timed-out wait (backend.hpp kWaitSeqMask): which
+// collective, and the peer that never arrived.
+__device__ __forceinline__ void peer_wait_error(const PeerWaitArgs& a, int peer) {
+  if (a.error)
+    __hip_atomic_store(a.error, (a.seq & kWaitSeqMask) | (static_cast<uint64_t>(peer + 1) << 48), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // One wave: lane p waits until flags[p] >= seq (p < npeers, skip_self aside).
 __global__ void peer_wait_kernel(PeerWaitArgs a) {
   const int lane = lane_id();
-  bool ok = true;
-  if (lane < a.npeers && lane != a.skip) {
-    const uint64_t t0 = wall_clock64();
-    for (uint32_t spin = 0;; ++spin) {
-      if (__hip_atomic_load(a.flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= a.seq) break;
-      __builtin_amdgcn_s_sleep(2);
-      if ((spin & 255) == 255 && wall_clock64() - t0 > a.timeout_ticks) {
-        ok = false;
-        break;
-      }
-    }
-  }
-  if (!__all(ok)) {
-    if (lane == 0 && a.error) __hip_atomic_store(a.error, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  int st = 1;
+  if (lane < a.npeers && lane != a.skip) st = peer_flag_wait(a, lane);
+  const unsigned long long late = __ballot(st == 0);
+  if (late || !__all(st == 1)) {
+    if (lane == 0 && late) peer_wait_error(a, __ffsll(static_cast<long long>(late)) - 1);
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -180,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
 // per peer) is far below the chip's residency, so that workgroup runs.
 constexpr int kFusedThreads = 256;
 __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs pa, PeerWaitArgs wa, PeerUnpackArgs ua) {
-  __shared__ int s_last, s_ok;
+  __shared__ int s_last, s_ok, s_late;
   const int t = threadIdx.x;
   const int P = pa.npeers;
   push_pieces(pa, kFusedThreads);
@@ -188,6 +203,7 @@ __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs 
   __syncthreads();
   if (t == 0) {
     s_ok = 1;
+    s_late = -1;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = atomicAdd(pa.ticket, 1u);
@@ -203,19 +219,13 @@ __global__ __launch_bounds__(kFusedThreads) void peer_fused_kernel(PeerPushArgs 
     if (t == 0) *pa.ticket = 0u;  // next collective is stream-ordered after this one
   }
   if (t < wa.npeers && t != wa.skip) {
-    const uint64_t t0 = wall_clock64();
-    for (uint32_t spin = 0;; ++spin) {
-      if (__hip_atomic_load(wa.flags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= wa.seq) break;
-      __builtin_amdgcn_s_sleep(2);
-      if ((spin & 255) == 255 && wall_clock64() - t0 > wa.timeout_ticks) {
-        s_ok = 0;  // (benign race: every writer stores 0)
-        break;
-      }
-    }
+    const int st = peer_flag_wait(wa, t);
+    if (st == 0) s_late = t;  // (benign race: any missing peer names the stall)
+    if (st != 1) s_ok = 0;    // (benign race: every writer stores 0)
   }
   __syncthreads();
   if (!s_ok) {
-    if (t == 0 && wa.error) __hip_atomic_store(wa.error, wa.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0 && s_late >= 0) peer_wait_error(wa, s_late);
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < q;
            i += static_cast<int64_t>(gridDim.x) * kThreads) {
         const vid_t r = a.clear_qv[i];
-        if (r != kNoRow) a.clear_frontier[r >> 6] = 0ull;  // (kNoRow: a hub-split entry)
+        a.clear_frontier[r >> 6] = 0ull;
       }
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kRangeThreads, 2 * kRangeThreads / 256) void td_ran
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kRangeThreads + t; i < q;
          i += static_cast<int64_t>(gridDim.x) * kRangeThreads) {
       const vid_t r = a.clear_qv[i];
-      if (r != kNoRow) a.clear_frontier[r >> 6] = 0ull;
+      a.clear_frontier[r >> 6] = 0ull;
     }
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
@@ -482,57 +482,17 @@ __global__ __launch_bounds__(kRangeThreads, 2 * kRangeThreads / 256) void td_ran
   }
 }
 
-// Hub-split levels (TdSparseArgs::hx_bits): the claimed top-down hubs among a
-// lane's items whose row has a part on this rank (ShardView::hx_off; a hub
-// with none is listed as usual) leave the work list -- re = rs -- and get
-// their frontier bit, their bit in hx_bits and their count / degree in
-// hx_tot (one pair of atomics per wave).  The hub index is the row's entry of
-// ShardView::hx_index.
-template <int kItems>
-__device__ __forceinline__ void hx_divert(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed,
-                                          const eid_t (&rs)[kItems], eid_t (&re)[kItems]) {
-  unsigned hub = 0;
-#pragma unroll
-  for (int k = 0; k < kItems; ++k)
-    if (((claimed >> k) & 1u) && re[k] - rs[k] >= static_cast<eid_t>(a.g.td_hub_min_deg)) hub |= 1u << k;
-  // (a row of degree >= td_hub_min_deg may still be no hub -- ties at the
-  // threshold beyond kTdMaxHubs: hx_index says UINT32_MAX, listed as usual)
-  if (!__ballot(hub != 0)) return;
-  long long hc = 0, hd = 0;
-#pragma unroll
-  for (int k = 0; k < kItems; ++k) {
-    if (!((hub >> k) & 1u)) continue;
-    const int64_t lo_i = a.g.hx_index[static_cast<int64_t>(v[k]) - a.g.lo];  // (owned: a settled vertex)
-    DBFS_DCHECK(lo_i >= a.g.td_nhubs || a.g.td_hub_vertex[lo_i] == v[k], 12, v[k]);
-    if (lo_i >= a.g.td_nhubs || a.g.hx_off[lo_i + 1] == a.g.hx_off[lo_i]) continue;  // (no hub / no part here: listed)
-    const int64_t r = static_cast<int64_t>(v[k]) - a.g.lo;
-    atomicOr(a.frontier_out + (r >> 6), 1ull << (r & 63));
-    atomicOr(a.hx_bits + (lo_i >> 6), 1ull << (lo_i & 63));
-    ++hc;
-    hd += static_cast<long long>(re[k] - rs[k]);
-    re[k] = rs[k];
-  }
-  hc = wave_sum(hc);
-  hd = wave_sum(hd);
-  if (lane_id() == 0 && hc) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.hx_tot), static_cast<unsigned long long>(hc));
-    atomicAdd(reinterpret_cast<unsigned long long*>(a.hx_tot + 1), static_cast<unsigned long long>(hd));
-  }
-}
-
 // The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
 // of this shard): level, frontier bit, and the wave's work-list entries of
 // the next level with one packed atomic (count << kSparseEdgeBits | edges)
 // for all of them, so entries stay ordered by edge offset.  Wave-uniform call.
-// (kHx: hub-split levels, TdSparseArgs::hx_bits -- a variant of its own: the
-// diversion's code in every kernel cost td_sparse_bits 21 -> 30 us a level)
 // kWg: a workgroup-uniform call (every wave of a workgroup of at most
 // kSettleWaves waves): the waves' packed counts summed in LDS and ONE atomic
 // per workgroup on the counter, each wave's base from the waves before it --
 // a level settling thousands of waves' claims queued that many returning
 // atomics on one address (~90 per us).
 constexpr int kSettleWaves = 1024 / kWave;
-template <int kItems, bool kHx = false, bool kWg = false>
+template <int kItems, bool kWg = false>
 __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   if constexpr (!kWg) {
@@ -553,7 +513,6 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
       re[k] = ro[r + 1];
     }
   }
-  if constexpr (kHx) hx_divert<kItems>(a, v, claimed, rs, re);
   unsigned long long tm[kItems];
   long long incl[kItems], cbase[kItems], ebase[kItems];
   long long ctot = 0, etot = 0;
@@ -614,9 +573,6 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
 
 // The level's local totals from the packed counter (one thread of the last
 // workgroup): stats, the work list's end marker, counter and ticket reset.
-// (hub-split levels: the diverted hubs count in the level's totals -- cnt /
-// deg returned, stats[2..3], stats[4] = hubs -- but not in the list's
-// stats[0..1]; hx_tot zeroed)
 __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -627,14 +583,6 @@ __device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& 
   a.stats[0] = cnt;
   a.stats[1] = deg;
   a.oscan[cnt] = deg;
-  if (a.hx_bits) {
-    const long long hc = __hip_atomic_load(a.hx_tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long hd = __hip_atomic_load(a.hx_tot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.hx_tot[0] = a.hx_tot[1] = 0;
-    a.stats[4] = hc;
-    cnt += hc;
-    deg += hd;
-  }
   a.stats[2] = cnt;
   a.stats[3] = deg;
 }
@@ -729,7 +677,7 @@ __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, 
 // space the grid strides over.
 // (bx / gx: this workgroup and the workgroups taking part -- the kernel's, or
 // the one last workgroup of a fused tiny level, TdSparseArgs::fuse_apply)
-template <int kThreads, bool kHx = false, bool kWg = true>
+template <int kThreads, bool kWg = true>
 __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int s_last;
@@ -789,7 +737,7 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
       const word_t bit = 1ull << (v[k] & 63);
       if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
     }
-    sparse_settle<kItems, kHx, kWg>(a, v, claimed);
+    sparse_settle<kItems, kWg>(a, v, claimed);
   }
   __syncthreads();
   if (t == 0) {
@@ -812,21 +760,25 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
     s_tot[0] = cnt;
     s_tot[1] = deg;
   }
-  // hub-split: the level's frontier-hub bits to the stats block (the level
-  // end carries them to every rank), the accumulator zeroed for the next
-  if (a.hx_bits)
-    for (int64_t w = t; w < (a.g.td_nhubs + 63) / 64; w += kThreads) {
-      a.hx_out[w] = static_cast<int64_t>(a.hx_bits[w]);
-      a.hx_bits[w] = 0ull;
-    }
   if (!a.end.active) return;
   __syncthreads();
   direct_level_end(a.end, s_tot[0], s_tot[1], a.stats, a.fin, s_xend);
 }
 
-template <int kThreads, bool kHx = false>
+template <int kThreads>
 __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs a) {
-  sparse_apply<kThreads, kHx>(a, blockIdx.x, gridDim.x);
+  sparse_apply<kThreads>(a, blockIdx.x, gridDim.x);
+}
+
+// A direct exchange's wait on its own (Comm::split_waits: ranks sharing a
+// GPU): one wave polls the peers' cells, and the consumer launched after it
+// on the same stream finds them tagged at its first poll -- so no grid
+// spins in every workgroup while a co-resident rank's producer waits for
+// CUs.  (Ranks on separate GPUs keep the wait in the consumer: their
+// producers never compete with it for a CU.)
+__global__ __launch_bounds__(kWave) void direct_prewait_kernel(DirectExchange x) {
+  __shared__ uint64_t s_n[kern::kMaxPeers];
+  (void)direct_wait(x, s_n, nullptr);
 }
 
 // Sparse top-down level (TdSparseArgs): expansion as td_expand, then every
@@ -837,7 +789,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_apply_kernel(TdSparseArgs 
 constexpr int kTdSparseThreads = 1024;
 // kWg: several ranks (owner lists) -- settles aggregated per workgroup
 // (sparse_settle); one rank keeps the per-wave form (its registers).
-template <int kThreads, bool kHx = false, bool kWg = false>
+template <int kThreads, bool kWg = false>
 __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
@@ -851,7 +803,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
       // (the fused owner side waits for the peers all the same: a collective)
-      if (a.fuse_apply) sparse_apply<kThreads, kHx, kWg>(a, 0, 1);
+      if (a.fuse_apply) sparse_apply<kThreads, kWg>(a, 0, 1);
     }
     return;
   }
@@ -869,7 +821,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   // the input vertices' frontier bits (the bitmap is not read here)
   for (int64_t i = gtid; i < q; i += gstride) {
     const vid_t r = a.qv[i];
-    if (r != kNoRow) a.frontier_in[r >> 6] = 0ull;  // (kNoRow: a hub-split entry of a hub owned elsewhere)
+    a.frontier_in[r >> 6] = 0ull;
   }
 
   const vid_t* __restrict__ col = a.g.col;
@@ -912,7 +864,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       }
     }
     // (B) finish the claimed vertices (the whole workgroup: one counter atomic)
-    sparse_settle<kItems, kHx, kWg>(a, v, claimed);
+    sparse_settle<kItems, kWg>(a, v, claimed);
   }
   if (a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
@@ -940,7 +892,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     // a tiny level (fuse_apply): this workgroup is also the owner side --
     // the peers' lists, their claims and the folded level end -- instead of
     // a td_sparse_apply launch
-    if (a.fuse_apply) sparse_apply<kThreads, kHx, kWg>(a, 0, 1);
+    if (a.fuse_apply) sparse_apply<kThreads, kWg>(a, 0, 1);
     return;
   }
 
@@ -987,7 +939,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
-      if (a.fuse_apply) sparse_apply<kBlock, false, false>(a, 0, 1);  // (a collective: as td_sparse)
+      if (a.fuse_apply) sparse_apply<kBlock, false>(a, 0, 1);  // (a collective: as td_sparse)
     }
     return;
   }
@@ -1103,7 +1055,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
     if (t == 0) *a.ticket = 0u;
     if (dx) direct_publish(a.direct, a.lists, a.list_stride, true);
     // a tiny level (fuse_apply): the owner side and the level end here too
-    if (dx && a.fuse_apply) sparse_apply<kBlock, false, false>(a, 0, 1);
+    if (dx && a.fuse_apply) sparse_apply<kBlock, false>(a, 0, 1);
     return;
   }
   if (t != 0) return;
@@ -1458,8 +1410,6 @@ void td_binned(const BinArgs& a, hipStream_t st) {
 }
 
 void td_sparse(const TdSparseArgs& a, hipStream_t st) {
-  DBFS_CHECK(!a.hx_bits || (!a.from_bits && a.lists && a.hx_tot && a.hx_out),
-             "td_sparse: hub-split levels are multi-rank list levels (not read from a bitmap)");
   if (a.from_bits) {
     // a wave per unit up to 4096 workgroups' worth, else kBitsPre units per
     // wave (RMAT-26, one rank: 1024 workgroups, 16 groups on the ticket)
@@ -1475,8 +1425,7 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
   // edges: RMAT-26 1479 / 1469 -> 1502 / 1481 GTEPS, level 0 9.8 -> 6.7 us;
   // RMAT-22 top-down only 90.5 / 90.8 -> 91.8 / 92.2)
   const unsigned grid = static_cast<unsigned>(a.grid);
-  if (a.hx_bits) td_sparse_kernel<kTdSparseThreads, true, true><<<grid, kTdSparseThreads, 0, st>>>(a);
-  else if (a.lists) td_sparse_kernel<kTdSparseThreads, false, true><<<grid, kTdSparseThreads, 0, st>>>(a);
+  if (a.lists) td_sparse_kernel<kTdSparseThreads, true><<<grid, kTdSparseThreads, 0, st>>>(a);
   else td_sparse_kernel<kTdSparseThreads><<<grid, kTdSparseThreads, 0, st>>>(a);
 }
 
@@ -1514,8 +1463,11 @@ void frontier_selftest(const FrontierTable* t, int rank, int nranks, int64_t wor
 void td_sparse_apply(const TdSparseArgs& a, hipStream_t st) {
   // (1024 threads, two ids each: as td_sparse)
   const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, a.grid));
-  if (a.hx_bits) td_sparse_apply_kernel<kTdSparseThreads, true><<<grid, kTdSparseThreads, 0, st>>>(a);
-  else td_sparse_apply_kernel<kTdSparseThreads><<<grid, kTdSparseThreads, 0, st>>>(a);
+  td_sparse_apply_kernel<kTdSparseThreads><<<grid, kTdSparseThreads, 0, st>>>(a);
+}
+
+void direct_prewait(const DirectExchange& x, hipStream_t st) {
+  if (x.active) direct_prewait_kernel<<<1, kWave, 0, st>>>(x);
 }
 
 void hub_visited(const HubVisitedArgs& a, hipStream_t st) {

@@ -300,6 +300,24 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("peer_ops", &PeerComm::peer_ops)
       .def_property_readonly("inner_ops", &PeerComm::inner_ops)
       .def_property_readonly("direct_on", &PeerComm::direct_on)
+      .def_property_readonly("frontier_on", &PeerComm::frontier_on)
+      .def_property_readonly("fused", &PeerComm::fused)
+      .def_property_readonly("split_waits", &PeerComm::split_waits)
+      .def_property_readonly("shared_device", &PeerComm::shared_device)
+      .def_property_readonly("bus_ids", &PeerComm::bus_ids)
+      // P x P: 2 same GPU, 1 peer access, 0 none, -1 not visible (row: the rank that looked)
+      .def_property_readonly("peer_access",
+                             [](const PeerComm& c) {
+                               const int P = c.size();
+                               py::list rows;
+                               for (int r = 0; r < P; ++r) {
+                                 py::list row;
+                                 for (int q = 0; q < P; ++q) row.append(c.peer_access()[r * P + q]);
+                                 rows.append(row);
+                               }
+                               return rows;
+                             })
+      .def_property_readonly("self_test_verdict", &PeerComm::self_test_verdict)
       .def("self_test", [](PeerComm& c) {
         std::string why;
         bool ok;
@@ -580,14 +598,6 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_property_readonly("td_hub_share", &DeviceGraph::td_hub_share)
       .def_property_readonly("hub_sorted", &DeviceGraph::hub_sorted)
       .def_property_readonly("nhubs", &DeviceGraph::nhubs)
-      // hub-split rows (tests): (hubs, offsets, parts) as numpy arrays
-      .def("hub_split_rows",
-           [](const DeviceGraph& g) {
-             const auto h = g.hub_split_host();
-             return py::make_tuple(py::array_t<vid_t>(h.hubs.size(), h.hubs.data()),
-                                   py::array_t<eid_t>(h.off.size(), h.off.data()),
-                                   py::array_t<vid_t>(h.col.size(), h.col.data()));
-           })
       // from_file: (byte_begin, byte_end, edges) this rank parsed
       .def_property_readonly("ingest",
                              [](const DeviceGraph& g) {
@@ -607,7 +617,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
                              [](const RunResult& r) {
                                py::list out;
                                for (const auto& c : r.chains)
-                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.hx_words, c.cut, c.push, c.ranged));
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.push, c.ranged));
                                return out;
                              })
       .def("level_dicts", &level_dicts);
@@ -625,7 +635,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
              py::gil_scoped_release rel;
              return std::make_shared<Engine>(*g, *c, o);
            }),
-           py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 24.0, py::arg("beta") = 96.0,
+           py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 40.0, py::arg("beta") = 96.0,
            py::arg("bu_lane_limit") = 16, py::arg("phase_timing") = false, py::arg("force_exchange") = false,
            py::keep_alive<1, 2>(),
            py::keep_alive<1, 3>())

@@ -2,8 +2,11 @@
 
 Execution models:
   * one process per GPU (``torch.distributed.run`` / any launcher exporting
-    RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT) -> RCCL communicator
-    bootstrapped over TCP (the reference used CUDA-aware MPI, bfs_mpi.cu:800-808);
+    RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT) -> the peer-memory
+    communicator (IPC windows over xGMI) with a TCP inner communicator for its
+    setup agreements; RCCL (bounded setup) only when the windows are
+    unavailable, or with DBFS_COMM=rccl (the reference used CUDA-aware MPI,
+    bfs_mpi.cu:800-808);
   * one process, P virtual ranks as threads on one device -> ``run_virtual_ranks``;
   * CPU multi-process over torch.distributed/gloo -> ``TorchComm``.
 """
@@ -24,8 +27,9 @@ class Runtime:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
-    # the communicator a peer-memory communicator wraps (RCCL), kept as the
-    # fallback transport (bench.py re-measures on it if a traversal fails)
+    # the communicator a peer-memory communicator wraps (TCP), kept as the
+    # fallback transport (bench.py --allow-fallback re-measures on it if a
+    # traversal over the windows fails validation)
     fallback_comm: Any = None
 
     @property
@@ -80,28 +84,53 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
             port = _env_int("DBFS_BOOTSTRAP_PORT", _env_int("MASTER_PORT", 29500) + 1)
             boot = N.TcpBootstrap(addr, port, rank, world)
             shared = "DBFS_DEVICE" in os.environ  # several ranks on one GPU (tests)
-            if kind == "tcp" or (not kind and (not backend.is_gpu or shared)):
+            if kind == "tcp" or (not kind and not backend.is_gpu):
                 comm = N.tcp_comm(boot, backend)  # host collectives (CPU runs / debug fallback)
+            elif kind == "rccl":
+                comm = _make_rccl(boot, backend, rank, world, local_rank)
             else:
-                if shared:
-                    # RCCL refuses two ranks on one device: TCP carries what
-                    # does not fit the peer windows
-                    inner = N.tcp_comm(boot, backend)
-                else:
-                    # one GPU per rank: the backend made LOCAL_RANK current
-                    # (hipSetDevice) before the communicator is created
-                    if backend.device_id != local_rank:
-                        raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, "
-                                           f"expected LOCAL_RANK {local_rank}")
-                    uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
-                    inner = N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
-                comm = inner
-                if kind in ("", "peer"):
-                    comm, fallback = _try_peer(boot, backend, inner, rank, kind == "peer")
+                # the peer-memory transport over a TCP inner communicator: the
+                # windows carry every payload (slot-sized rounds), so TCP only
+                # agrees setup steps -- no library collective stands between a
+                # run and its first multi-GPU level
+                inner = N.tcp_comm(boot, backend)
+                comm, fallback = _try_peer(boot, backend, inner, rank, kind == "peer")
+                if comm is inner and not shared:
+                    # no peer windows: RCCL over xGMI (bounded setup), else TCP
+                    comm = _rccl_or(inner, boot, backend, rank, world, local_rank)
     comm.bind_backend(backend)
     rt = Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)
     rt.fallback_comm = fallback
     return rt
+
+
+def _make_rccl(boot, backend, rank: int, world: int, local_rank: int):
+    """An RCCL communicator (one GPU per rank: the backend made LOCAL_RANK
+    current before the communicator is created); its setup is bounded
+    (DBFS_RCCL_INIT_TIMEOUT_S, native NcclComm)."""
+    if backend.device_id != local_rank:
+        raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, expected LOCAL_RANK {local_rank}")
+    uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
+    return N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
+
+
+def _rccl_or(inner, boot, backend, rank: int, world: int, local_rank: int):
+    """RCCL if every rank builds it (agreed over the bootstrap), else `inner`."""
+    import sys
+
+    rc, err = None, ""
+    try:
+        rc = _make_rccl(boot, backend, rank, world, local_rank)
+    except Exception as e:  # noqa: BLE001 - agreed below
+        err = str(e) or type(e).__name__
+    errs = [e for e in boot.allgather(err.encode()) if e]
+    if not errs:
+        return rc
+    rc = None  # (a rank that built it drops it: every rank takes the same transport)
+    if rank == 0:
+        print(f"[dbfs] RCCL unavailable ({errs[0].decode(errors='replace')}); using {inner.name}",
+              file=sys.stderr, flush=True)
+    return inner
 
 
 def _try_peer(boot, backend, inner, rank: int, required: bool):

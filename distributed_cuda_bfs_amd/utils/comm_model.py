@@ -3,7 +3,7 @@
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
 collectives and bytes of a traversal can be predicted from its chains
-(``BFSResult.chains``: level, form, capacity, gather, hub-split words, hub cut)
+(``BFSResult.chains``: level, form, capacity, gather, pushed frontier, ranged)
 and checked against the
 communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
 ``table`` turns a 1-GPU level profile into the per-level bytes / collectives
@@ -75,43 +75,38 @@ class ChainTraffic:
         return sum(v for k, v in self.calls.items() if k not in ("barrier", "fused")) - self.calls["fused"]
 
 
-def level_end(cfg: ModelConfig, gather: bool, hx_words: int = 0, push: bool = False) -> ChainTraffic:
-    """The one collective that ends a level (or the seed); a hub-split level
-    (hx_words > 0) also all-reduces its hub count and frontier-hub bits.  A
-    pushed frontier (push: the producing kernels store the slices into the
+def level_end(cfg: ModelConfig, gather: bool, push: bool = False) -> ChainTraffic:
+    """The one collective that ends a level (or the seed).  A pushed frontier (push: the producing kernels store the slices into the
     peers' windows, Comm::direct_frontier) is accounted as an all-gather of its
     own -- the same bytes, no launch fused with the totals."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
     if gather:
         t.add("allgather", (P - 1) * W * WORD)
-    t.add("allreduce", (P - 1) * 8 * (2 + hx_words))
+    t.add("allreduce", (P - 1) * 8 * 2)
     if gather and cfg.fused and not push:
         t.add("fused", 0)
     return t
 
 
 def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool,
-                  hx_words: int = 0, cut: bool = False, push: bool = False) -> ChainTraffic:
-    """Collectives of one level chain (cut: a hub-cut bottom-up chain, whose
-    non-hub frontier's remote claims travel as owner lists)."""
+                  push: bool = False) -> ChainTraffic:
+    """Collectives of one level chain."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
     if form == "B" and not in_gathered:
         t.add("allgather", (P - 1) * W * WORD)              # input frontier slices (+ visited merge)
-    if cut:
-        t.add("alltoallv", (P - 1) * (cfg.list_max + 1) * 4)  # the cut's owner lists
     if form == "S":
         t.add("alltoallv", (P - 1) * ((cap or cfg.list_max) + 1) * 4)  # owner lists, count first
     elif form == "T":
         t.add("alltoall", (P - 1) * W * WORD)               # candidate bitmap slices
-    t.merge(level_end(cfg, gather, hx_words, push))
+    t.merge(level_end(cfg, gather, push))
     return t
 
 
 def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     """Traffic of one traversal from its enqueued chains (level, form, cap,
-    gather[, hub-split words, cut, push]): start barrier, the seed's collective, every
+    gather[, push, ranged]): start barrier, the seed's collective, every
     chain, the wall-time max at the end."""
     P = cfg.nranks
     tot = ChainTraffic()
@@ -121,8 +116,7 @@ def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     gathered = {-1: seed_gather}
     for level, form, cap, gather, *more in chains:
         tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False),
-                                int(more[0]) if more else 0, bool(more[1]) if len(more) > 1 else False,
-                                bool(more[2]) if len(more) > 2 else False))
+                                bool(more[0]) if more else False))
         gathered[level] = bool(gather)
     tot.add("allgather", (P - 1) * 8)  # max over ranks of the wall time
     return tot

@@ -652,101 +652,36 @@ def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs, narrow):
 
 
 @pytest.mark.parametrize("P", [2, 3, 8])
-@pytest.mark.parametrize("mode", ["do", "td"])
-def test_hub_split_top_down_levels(P, mode):
-    """Hub-split top-down levels (several ranks, hx_levels): the early sparse
-    chains leave the top-down hubs they settle out of the owner's work list and
-    every rank expands its own part of each frontier hub's row (hx_off) at the
-    next level.  Levels exact against the oracle, and the per-level records
-    (direction, frontier vertices / edges, discoveries) equal the run without
-    hub-split levels: the diverted hubs count in the totals."""
-    p = dbfs.rmat_params(13, 16, 23)
-    csr = dbfs.host_csr_from_params(p)
-    srcs = [5, 999, 4321]
-
-    def body(rt):
-        b = dbfs.BFS(p, rt, mode=mode)
-        assert b.graph.partition.nranks == P
-        out = []
-        for hx in (4, 0):
-            b.engine.set_option("hx_levels", hx)
-            for s in srcs:
-                r = b.run(s)
-                recs = [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
-                out.append((hx, s, b.levels(), recs, [c[4] for c in r.chains]))
-        return out
-
-    for outs in run_virtual_ranks(P, body, device="cpu"):
-        with_hx = {s: (lv, recs, hxw) for hx, s, lv, recs, hxw in outs if hx}
-        without = {s: (lv, recs, hxw) for hx, s, lv, recs, hxw in outs if not hx}
-        for s in srcs:
-            exp = dbfs.cpu_bfs(csr, s)[0]
-            assert np.array_equal(with_hx[s][0], exp) and np.array_equal(without[s][0], exp)
-            assert with_hx[s][1] == without[s][1]
-            assert any(w > 0 for w in with_hx[s][2]) and not any(without[s][2])
-
-
-def test_hub_split_rows_partition_hub_rows():
-    """The hub-split rows of every rank together are exactly the top-down
-    hubs' rows: rank r's part of hub h = h's neighbours owned by r, in id
-    order (duplicates kept, as the rows keep them)."""
-    p = dbfs.rmat_params(11, 16, 3)
-    csr = dbfs.host_csr_from_params(p)
-    ro, col = np.asarray(csr.row_off), np.asarray(csr.col)
-
-    def body(rt):
-        b = dbfs.BFS(p, rt, mode="do")
-        return b.graph.lo, b.graph.rows, b.graph.hub_split_rows()
-
-    outs = run_virtual_ranks(3, body, device="cpu")
-    hubs = outs[0][2][0]
-    assert len(hubs) > 0 and np.all(np.diff(hubs.astype(np.int64)) > 0)
-    for lo, rows, (h, off, part) in outs:
-        assert np.array_equal(h, hubs)
-        for k in range(0, len(hubs), max(1, len(hubs) // 50)):
-            row = col[ro[hubs[k]]:ro[hubs[k] + 1]].astype(np.int64)
-            mine = np.sort(row[(row >= lo) & (row < lo + rows)])
-            assert np.array_equal(part[off[k]:off[k + 1]].astype(np.int64), mine)
-
-
-@pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("narrow", [1, 0])
-@pytest.mark.parametrize("alpha,max_hubs", [(24.0, None), (2.0, 300), (1e9, None)])
-def test_hub_cut_several_ranks(P, narrow, alpha, max_hubs):
-    """Hub-cut bottom-up levels with several ranks: the non-hub frontier of
-    each rank claims its own neighbours in place and sends the remote ones to
-    their owners (the owner lists), who claim them (bu_cut_apply) before the
-    bottom-up kernel merges the claims with the rows resolved by frontier hubs
-    (decided on every rank from the global frontier and the hubs' global
-    degrees).  Cut forced on every first bottom-up level: levels exact against
-    the oracle and the level records equal the uncut run's."""
+def test_hub_cut_is_one_rank_only(P, narrow):
+    """The hub cut (BuArgs::cut_edges) is a one-rank path: with several ranks
+    it is never enqueued (round 4 measured its multi-rank form slower at P = 8
+    and it was removed), so forcing its thresholds changes nothing -- levels
+    exact against the oracle, level records equal to the default run's."""
     p = dbfs.rmat_params(13, 16, 11)
     csr = dbfs.host_csr_from_params(p)
     srcs = [7, 3001, 8100]
 
     def body(rt):
-        b = dbfs.BFS(p, rt, mode="do", alpha=alpha, beta=24.0, max_hubs=max_hubs)
+        b = dbfs.BFS(p, rt, mode="do", alpha=2.0, beta=24.0, max_hubs=300)
         b.engine.set_option("narrow_levels", narrow)
-        b.engine.set_option("bu_cut_mf_frac", 1.0)  # (enqueue it on every first bottom-up level)
-        b.engine.set_option("bu_cut_ranks", 1)  # (opt-in with several ranks)
         out = []
         for cut in (1 << 40, 0):
             b.engine.set_option("bu_cut_edges", cut)
+            b.engine.set_option("bu_cut_mf_frac", 1.0 if cut else 0.25)
             for s in srcs:
                 r = b.run(s)
                 recs = [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
-                out.append((cut, s, b.levels(), recs, any(c[5] for c in r.chains)))
+                out.append((cut, s, b.levels(), recs))
         return out
 
     for outs in run_virtual_ranks(P, body, device="cpu"):
-        cut = {s: x for c, s, *x in outs if c}
+        forced = {s: x for c, s, *x in outs if c}
         plain = {s: x for c, s, *x in outs if not c}
         for s in srcs:
             exp = dbfs.cpu_bfs(csr, s)[0]
-            assert np.array_equal(cut[s][0], exp) and np.array_equal(plain[s][0], exp)
-            assert cut[s][1] == plain[s][1]
-            assert not plain[s][2]
-        assert any(cut[s][2] for s in srcs)
+            assert np.array_equal(forced[s][0], exp) and np.array_equal(plain[s][0], exp)
+            assert forced[s][1] == plain[s][1]
 
 
 @pytest.mark.parametrize("words", [None, 32])
@@ -766,5 +701,5 @@ def test_range_staged_top_down_levels_cpu(rt, words):
     for s in b.sample_roots(3, seed=5):
         r = b.run(s)
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0])
-        ranged = ranged or any(c[7] for c in r.chains)
+        ranged = ranged or any(c[5] for c in r.chains)
     assert ranged

@@ -703,7 +703,7 @@ def test_td_range_levels_gpu(gpu_runtime, mode, scale, words):
         srcs = [0, 5] if g is star else bfs.sample_roots(3, seed=61)
         for src in srcs:
             res = _check(bfs, csr, src)
-            ranged = ranged or any(c[7] for c in res.chains)
+            ranged = ranged or any(c[5] for c in res.chains)
         assert ranged or mode == "do"
         assert bfs.validate(srcs[-1])
 
@@ -857,25 +857,109 @@ def test_eight_virtual_ranks_rmat22_defaults_gpu():
         assert nhubs > 0
 
 
+def _run_group(cmd, env, timeout):
+    """Run a command that starts rank processes of its own (bench.py self-
+    spawn) in a session of its own; past `timeout` the whole process group
+    is killed (no orphaned rank keeps the GPU) and the test fails with the
+    ranks' stderr tail -- what each rank logged last, and which collective
+    a timed-out wait named."""
+    import signal
+    import subprocess
+
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                         start_new_session=True)
+    try:
+        o, e = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)  # (the group this test started)
+        o, e = p.communicate()
+        pytest.fail(f"timed out after {timeout} s; stderr tail:\n{e[-6000:]}")
+    return subprocess.CompletedProcess(cmd, p.returncode, o, e)
+
+
 def test_peer_comm_four_ranks_share_one_gpu_rmat20():
     """Four self-spawned ranks on device 0 over the peer-memory transport at
-    RMAT-20: every collective (fused gather + reduce, count-sized owner lists,
-    candidate slices) through the IPC windows; every timed root validated."""
+    RMAT-20: every collective (gather + reduce, count-sized owner lists,
+    candidate slices, pushed frontier slices) through the IPC windows; every
+    timed root validated.  Ranks sharing a GPU run the collectives unfused and
+    the direct exchanges' waits as one-wave launches (Comm::split_waits): a
+    grid spinning in every workgroup could hold the CUs a co-resident rank's
+    producer needs (the round-4 hang of this test)."""
     import json
-    import subprocess
     import sys
 
-    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16")
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16", DBFS_COMM_TIMEOUT_S="20")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "4", "--scale", "20", "--steps", "4",
-           "--warmup", "1", "--no-int32-pass"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
+           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "8", "--secondary", "none"]
+    out = _run_group(cmd, env, 100)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["n_gpus"] == 4
     assert rec["comm_direct"] is True  # (the direct exchanges passed their self-test on every rank)
+    topo = rec["comm_topology"]
+    assert topo["shared_device"] is True and topo["split_waits"] is True and topo["fused"] is False
+    assert topo["peer_access"] == [[2] * 4] * 4 and topo["self_test"] == "ok"
     assert rec["validated"] is True and rec["validated_roots"] == "4/4"
+    assert rec["heldout"]["validated_roots"] == "8/8"
+
+
+def test_peer_late_rank_completes():
+    """A rank that publishes late: rank 1 sleeps 1.5 s before enqueueing level
+    2 of every traversal (DBFS_FAULT_INJECT kind=delay) while its three peers'
+    kernels of that level already wait for its exchanges on the device.  The
+    traversals complete with every timed root validated, well inside the
+    collective timeout (nothing spins in every workgroup of a grid)."""
+    import json
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16", DBFS_COMM_TIMEOUT_S="20",
+               DBFS_FAULT_INJECT="rank=1,level=2,kind=delay,ms=1500")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "4", "--scale", "18", "--steps", "3",
+           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "0", "--secondary", "none"]
+    out = _run_group(cmd, env, 110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["validated_roots"] == "3/3"
+
+
+def test_peer_hung_rank_names_the_stalled_collective():
+    """A rank that never publishes (kind=hang at level 1): the peers' device
+    waits give up after DBFS_COMM_TIMEOUT_S (5 s) and their error names the
+    rank that timed out, the collective (sequence number, what it was, the
+    level) and the rank it waited for -- an error well inside the test's
+    limit, not a hang."""
+    import subprocess
+    import time
+
+    port = _free_port_pair()
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, WORLD_SIZE="3", RANK=str(r), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port - 1), DBFS_BOOTSTRAP_PORT=str(port), DBFS_DEVICE="0", DBFS_COMM="peer",
+                   DBFS_PEER_SLOT_MB="4", DBFS_COMM_TIMEOUT_S="5", DBFS_FAULT_INJECT="rank=1,level=1,kind=hang")
+        procs.append(subprocess.Popen([os.path.join(REPO, "bin", "bfs"), "--rmat", "16", "5", "--no-oracle",
+                                       "--quiet"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    t0 = time.time()
+    outs = {}
+    for r in (0, 2):
+        try:
+            o, e = procs[r].communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            procs[r].kill()  # exact child PID
+            o, e = procs[r].communicate()
+        outs[r] = (procs[r].returncode, e)
+    elapsed = time.time() - t0
+    procs[1].kill()  # the hung rank (exact PID)
+    procs[1].communicate()
+    for r, (rc, e) in outs.items():
+        assert rc != 0, e[-2000:]
+        assert f"rank {r} timed out in collective #" in e and "waiting for rank 1" in e, e[-2000:]
+        assert "level 1" in e, e[-2000:]
+    assert elapsed < 50
 
 
 def _free_port_pair():
@@ -1090,13 +1174,14 @@ def test_peer_slot_rounds_build_and_ingest(tmp_path):
 
 @pytest.mark.parametrize("opts", [["xfuse_edges=4096"], ["bu_merge_visited=0"],
                                   ["xfuse_edges=4096", "bu_merge_visited=0"],
-                                  ["hx_levels=4", "bu_cut_ranks=1", "bu_cut_mf_frac=1"]])
+                                  ["direct_frontier=0"], ["direct_frontier=0", "xfuse_edges=0"]])
 def test_peer_multirank_options(opts):
     """The multi-rank options -- tiny sparse levels fused into one launch
     (xfuse_edges), bottom-up levels without the visited merge of the gathered
-    frontier (bu_merge_visited=0), and the opt-in hub-split top-down levels and
-    multi-rank hub cut (hx_levels, bu_cut_ranks) -- over the peer transport with
-    4 processes on device 0 at RMAT-18: every timed root validated."""
+    frontier (bu_merge_visited=0), and the frontier gathered by the level end
+    instead of pushed by the kernels (direct_frontier=0) -- over the peer
+    transport with 4 processes on device 0 at RMAT-18: every timed root
+    validated."""
     args = ["--gpus", "4", "--scale", "18", "--steps", "6", "--warmup", "1"]
     for o in opts:
         args += ["--opt", o]
@@ -1104,9 +1189,10 @@ def test_peer_multirank_options(opts):
     assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
 
 
-@pytest.mark.parametrize("opts", [["direct_frontier=1"], ["direct_frontier=1", "bu_merge_visited=1"]])
+@pytest.mark.parametrize("opts", [[], ["bu_merge_visited=1"]])
 def test_peer_direct_frontier(opts):
-    """Pushed frontier slices (EngineOptions::direct_frontier): the top-down
+    """Pushed frontier slices (EngineOptions::direct_frontier, the default with
+    several ranks on the peer transport): the top-down
     update and bottom-up kernels store their output words into the peers'
     windows and the next bottom-up level's hub_gather copies them in (the level
     end carries only totals).  4 processes on device 0 at RMAT-18, every timed
