@@ -129,9 +129,10 @@ def parse_args(argv=None):
     ap.add_argument("--heldout-seed", type=int, default=5202611)
     ap.add_argument("--secondary", default="auto", metavar="N:M",
                     help="the metric's second graph, separately timed in the same record: a uniform random graph "
-                         "of N vertices and M input edges in td (the reference's algorithm class) and do modes; "
-                         "'auto' = soc-LiveJournal1's size, 4847571:68993773 (the dataset is not on the pool), on "
-                         "GPUs and none on the CPU backend; 'none' skips")
+                         "and a power-law (Chung-Lu) graph of N vertices and M input edges, each in td (the "
+                         "reference's algorithm class) and do modes; 'auto' = soc-LiveJournal1's size, "
+                         "4847571:68993773 (the dataset is not on the pool), on GPUs and none on the CPU backend; "
+                         "'none' skips")
     ap.add_argument("--secondary-roots", type=int, default=16)
     ap.add_argument("--spawn-timeout", type=float, default=1500.0,
                     help="self-spawned ranks: seconds before the children are killed")
@@ -232,12 +233,10 @@ def comm_topology(rt):
             "inner": c.name.partition("+")[2]}
 
 
-def secondary_block(dbfs, rt, spec: str, nroots: int, seed: int, args):
-    """The metric's second graph (soc-LiveJournal1-sized uniform random graph,
+def secondary_block(dbfs, rt, params, graph: str, nroots: int, seed: int, args):
+    """One of the metric's second-graph stand-ins (soc-LiveJournal1-sized,
     generated on the device) in td and do modes: 2 warm-up roots, then
     `nroots` timed and validated, per mode."""
-    un, _, um = spec.partition(":")
-    params = dbfs.uniform_params(int(un), int(um), seed)
     t0 = time.time()
     g = dbfs.BFS(params, rt, mode="td", alpha=args.alpha, beta=args.beta, bu_lane_limit=args.bu_lane_limit)
     for kv in args.opt:  # (the primary engine's --opt settings apply here too)
@@ -246,8 +245,7 @@ def secondary_block(dbfs, rt, spec: str, nroots: int, seed: int, args):
     rt.barrier()
     gen_s = time.time() - t0
     roots = g.sample_roots(nroots + 2, seed=seed + 1)
-    out = {"graph": f"uniform random {int(un)} V / {int(um)} E " + ("(soc-LiveJournal1's size; synthetic)" if (int(un), int(um)) == (4847571, 68993773) else "(synthetic)"),
-           "generate_s": round(gen_s, 3), "roots": len(roots) - 2, "opts": list(args.opt)}
+    out = {"graph": graph, "generate_s": round(gen_s, 3), "roots": len(roots) - 2, "opts": list(args.opt)}
     for mode in ("td", "do"):
         g.mode = mode
         for r in roots[:2]:
@@ -256,7 +254,7 @@ def secondary_block(dbfs, rt, spec: str, nroots: int, seed: int, args):
         out[mode] = {"value": round(gteps, 4), "ms_per_step": round(ms, 4),
                      "harmonic_mean_gteps": round(len(res) / sum(1.0 / max(x.gteps, 1e-12) for x in res), 4),
                      "validated_roots": f"{ok}/{len(res)}"}
-        log(f"secondary {spec} {mode}: {gteps:.2f} GTEPS ({ms:.4f} ms/root), validated {ok}/{len(res)}")
+        log(f"secondary {graph} {mode}: {gteps:.2f} GTEPS ({ms:.4f} ms/root), validated {ok}/{len(res)}")
     del g
     return out
 
@@ -412,12 +410,28 @@ def main(argv=None) -> int:
     if args.secondary == "auto":
         args.secondary = "4847571:68993773" if rt.is_gpu else "none"
     if args.secondary and args.secondary != "none" and not args.graph and fast_mode:
-        secondary = {"lj_sized": secondary_block(dbfs, rt, args.secondary, args.secondary_roots, args.seed + 100,
-                                                 args)}
-        for m in ("td", "do"):
-            ok, tot = secondary["lj_sized"][m]["validated_roots"].split("/")
-            if ok != tot:
-                validated = False
+        un, _, um = args.secondary.partition(":")
+        n2, m2 = int(un), int(um)
+        lj = (n2, m2) == (4847571, 68993773)
+        secondary = {}
+        # uniform random at that size, and the power-law (Chung-Lu) stand-in
+        # with soc-LiveJournal1's largest degree: its heavy tail is what the
+        # real graph's top-down levels see (parity with the dataset unpinned)
+        secondary["lj_sized"] = secondary_block(
+            dbfs, rt, dbfs.uniform_params(n2, m2, args.seed + 100),
+            f"uniform random {n2} V / {m2} E " + ("(soc-LiveJournal1's size; synthetic)" if lj else "(synthetic)"),
+            args.secondary_roots, args.seed + 100, args)
+        dmax = dbfs.ops.graph.LJ_SIZED_POWER_LAW[2] if lj else max(64, int(20 * 2 * m2 / max(n2, 1)))
+        secondary["lj_power_law"] = secondary_block(
+            dbfs, rt, dbfs.power_law_params(n2, m2, dmax, args.seed + 200),
+            f"power-law (Chung-Lu, degree tail exponent 2.5, max expected degree {dmax}) {n2} V / {m2} E "
+            + ("(soc-LiveJournal1's size and largest degree; synthetic)" if lj else "(synthetic)"),
+            args.secondary_roots, args.seed + 200, args)
+        for blk in secondary.values():
+            for m in ("td", "do"):
+                ok, tot = blk[m]["validated_roots"].split("/")
+                if ok != tot:
+                    validated = False
     # One extra (untimed) traversal of the median timed root with per-level
     # device events: where the time goes (collectives vs kernels) at this N.
     med = sorted(results, key=lambda r: r.ms)[len(results) // 2]

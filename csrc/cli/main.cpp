@@ -9,19 +9,21 @@
 //   default            1 GPU (HIP backend, device --device)
 //   --gpus P           P GPUs in one process, one host thread per GPU: the
 //                      peer-memory communicator (every rank's window shared
-//                      as a device pointer, peer access enabled) over one
-//                      RCCL communicator per GPU (ncclCommInitAll) --
+//                      as a device pointer, peer access enabled) over an
+//                      in-process host communicator; one RCCL communicator
+//                      per GPU (ncclCommInitAll) if the windows fail --
 //                      replaces the reference's intra-node bfs.cu
 //   --virtual-ranks P  P partitions on ONE device (threads + VirtualComm):
 //                      exercises the distributed code path on one GPU
 //   --cpu              CPU backend (no GPU needed)
 //   WORLD_SIZE > 1     one process per GPU (torchrun / any launcher): TCP
 //                      bootstrap on MASTER_ADDR:MASTER_PORT+1, the peer-memory
-//                      communicator over RCCL (IPC windows) -- replaces the
-//                      reference's MPI build bfs_mpi.cu
+//                      communicator (IPC windows) over a TCP inner
+//                      communicator -- replaces the reference's MPI build
+//                      bfs_mpi.cu
 // DBFS_COMM = peer | rccl | tcp selects the transport (default: peer with an
-// agreed fallback to RCCL), DBFS_DEVICE pins every process to one device
-// (several ranks sharing a GPU: TCP carries what the windows do not).
+// agreed fallback to RCCL, then TCP), DBFS_DEVICE pins every process to one
+// device (several ranks sharing a GPU: tests).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -254,33 +256,58 @@ std::shared_ptr<VirtualGroup> make_ranks(const Args& a, int P, bool multiproc, i
     const char* addr = std::getenv("MASTER_ADDR");
     const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
     auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
-    if (a.cpu || cm == "tcp" || (cm.empty() && dev_pin)) {
-      // host transport (CPU ranks, GPU ranks without RCCL, shared GPU)
+    auto make_rccl = [&]() -> std::shared_ptr<Comm> {
+      std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+      return std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
+    };
+    if (a.cpu || cm == "tcp") {
+      // host transport (CPU ranks; debug)
       ranks[0].comm = std::make_shared<TcpComm>(boot, *ranks[0].be);
+    } else if (cm == "rccl") {
+      ranks[0].comm = make_rccl();
     } else {
-      std::shared_ptr<Comm> inner;
-      if (dev_pin) {
-        // RCCL refuses two ranks on one device: TCP carries what does not
-        // fit the peer windows
-        inner = std::make_shared<TcpComm>(boot, *ranks[0].be);
-      } else {
-        std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
-        inner = std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
+      // the peer windows over a TCP inner communicator (setup agreements
+      // only: every payload goes through the windows); RCCL (bounded setup,
+      // agreed) only when the windows are unavailable on separate GPUs
+      auto tcp = std::make_shared<TcpComm>(boot, *ranks[0].be);
+      ranks[0].comm = try_peer(boot, *ranks[0].be, tcp, cm == "peer", leader);
+      if (ranks[0].comm == tcp && !dev_pin) {
+        std::shared_ptr<Comm> rc;
+        std::string err;
+        try {
+          rc = make_rccl();
+        } catch (const std::exception& e) {
+          err = e.what();
+        }
+        std::string first;
+        for (const auto& e : boot->allgather(err))
+          if (first.empty()) first = e;
+        if (first.empty()) ranks[0].comm = rc;
+        else if (leader) std::fprintf(stderr, "[bfs] RCCL unavailable (%s); using tcp\n", first.c_str());
       }
-      ranks[0].comm = want_peer ? try_peer(boot, *ranks[0].be, inner, cm == "peer", leader) : inner;
     }
   } else if (vgroup) {
     for (int i = 0; i < P; ++i) ranks[i].comm = std::make_shared<VirtualComm>(vgroup, i, *ranks[i].be);
   } else if (P > 1) {
-    std::vector<Backend*> bes;
-    for (auto& r : ranks) bes.push_back(r.be.get());
-    auto comms = NcclComm::init_all(bes);
-    for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
+    // one process, P GPUs: the peer windows (device pointers, peer access)
+    // over an in-process host communicator; ncclCommInitAll only when the
+    // windows are unavailable (or DBFS_COMM=rccl)
+    bool peer_ok = false;
     if (want_peer) {
+      auto igroup = std::make_shared<VirtualGroup>(P);
       auto pgroup = std::make_shared<VirtualGroup>(P);
+      std::vector<std::shared_ptr<Comm>> inner(static_cast<size_t>(P));
+      for (int i = 0; i < P; ++i) inner[i] = std::make_shared<VirtualComm>(igroup, i, *ranks[i].be);
       run_ranks(ranks, [&](int i, RankCtx& rc) {
-        rc.comm = try_peer(std::make_shared<GroupBootstrap>(pgroup, i), *rc.be, rc.comm, cm == "peer", i == 0);
+        rc.comm = try_peer(std::make_shared<GroupBootstrap>(pgroup, i), *rc.be, inner[i], cm == "peer", i == 0);
       }, pgroup.get());
+      peer_ok = ranks[0].comm != inner[0];
+    }
+    if (!peer_ok) {
+      std::vector<Backend*> bes;
+      for (auto& r : ranks) bes.push_back(r.be.get());
+      auto comms = NcclComm::init_all(bes);
+      for (int i = 0; i < P; ++i) ranks[i].comm = std::move(comms[i]);
     }
   } else {
     ranks[0].comm = std::make_shared<LocalComm>(*ranks[0].be);

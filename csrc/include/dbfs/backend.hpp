@@ -14,6 +14,7 @@
 // 580-585).
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <functional>
 #include <memory>
@@ -936,6 +937,17 @@ class Backend {
   // memory (alloc/free are synchronous; copies/memsets are stream-ordered)
   virtual void* alloc(size_t bytes) = 0;
   virtual void dealloc(void* p) = 0;
+  // Bytes held in DBufs of this backend now and at most so far: one rank's
+  // device footprint (graph shard + traversal state; the peer transport's
+  // windows are allocated outside DBufs and not counted).
+  int64_t device_bytes() const { return live_bytes_.load(std::memory_order_relaxed); }
+  int64_t peak_device_bytes() const { return peak_bytes_.load(std::memory_order_relaxed); }
+  void note_device_bytes(int64_t delta) {
+    const int64_t now = live_bytes_.fetch_add(delta, std::memory_order_relaxed) + delta;
+    int64_t pk = peak_bytes_.load(std::memory_order_relaxed);
+    while (now > pk && !peak_bytes_.compare_exchange_weak(pk, now, std::memory_order_relaxed)) {
+    }
+  }
   virtual void memset_async(void* p, int value, size_t bytes) = 0;
   virtual void copy_async(void* dst, const void* src, size_t bytes) = 0;
   // Several device-to-device copies as one launch (4-byte multiples; the
@@ -1086,6 +1098,7 @@ class Backend {
  protected:
   std::function<void(double)> wait_watch_;
   double wait_period_ = 0.05;
+  std::atomic<int64_t> live_bytes_{0}, peak_bytes_{0};
 };
 
 std::unique_ptr<Backend> make_cpu_backend();
@@ -1098,7 +1111,10 @@ class DBuf {
  public:
   DBuf() = default;
   DBuf(Backend& be, size_t n) : be_(&be), n_(n) {
-    if (n_) p_ = static_cast<T*>(be_->alloc(n_ * sizeof(T)));
+    if (n_) {
+      p_ = static_cast<T*>(be_->alloc(n_ * sizeof(T)));
+      be_->note_device_bytes(static_cast<int64_t>(n_ * sizeof(T)));
+    }
   }
   ~DBuf() { reset(); }
   DBuf(const DBuf&) = delete;
@@ -1113,7 +1129,10 @@ class DBuf {
     return *this;
   }
   void reset() {
-    if (p_ && be_) be_->dealloc(p_);
+    if (p_ && be_) {
+      be_->dealloc(p_);
+      be_->note_device_bytes(-static_cast<int64_t>(n_ * sizeof(T)));
+    }
     p_ = nullptr; n_ = 0;
   }
   T* data() const { return p_; }

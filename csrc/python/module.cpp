@@ -205,9 +205,13 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_readonly("scale", &GenParams::scale)
       .def_readonly("seed", &GenParams::seed)
       .def_readonly("uniform", &GenParams::uniform)
+      .def_readonly("power_law", &GenParams::power_law)
+      .def_readonly("pl_i0", &GenParams::pl_i0)
+      .def_readonly("pl_dmax", &GenParams::pl_dmax)
       .def_readwrite("scramble", &GenParams::scramble);
   m.def("rmat_params", &rmat_params, py::arg("scale"), py::arg("edge_factor") = 16, py::arg("seed") = 1);
   m.def("uniform_params", &uniform_params, py::arg("n"), py::arg("m"), py::arg("seed") = 1);
+  m.def("power_law_params", &power_law_params, py::arg("n"), py::arg("m"), py::arg("dmax"), py::arg("seed") = 1);
   m.def(
       "generate_edges",
       [](const GenParams& p, int64_t begin, int64_t end) {
@@ -246,6 +250,8 @@ PYBIND11_MODULE(_dbfs_native, m) {
   py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
       .def_property_readonly("name", &Backend::name)
       .def_property_readonly("device_id", &Backend::device_id)
+      .def_property_readonly("device_bytes", &Backend::device_bytes)
+      .def_property_readonly("peak_device_bytes", &Backend::peak_device_bytes)
       .def_property_readonly("is_gpu", [](const Backend& b) { return b.kind() == DeviceKind::HIP; })
       .def("synchronize", &Backend::synchronize, py::call_guard<py::gil_scoped_release>());
   m.def("cpu_backend", []() { return std::shared_ptr<Backend>(make_cpu_backend()); });

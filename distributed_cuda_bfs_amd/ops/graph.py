@@ -43,6 +43,21 @@ def uniform_params(n: int, m: int, seed: int = 1):
     return N.uniform_params(int(n), int(m), int(seed))
 
 
+def power_law_params(n: int, m: int, dmax: int, seed: int = 1):
+    """Chung-Lu power-law graph (degree tail exponent 2.5) of n vertices and m
+    input edges whose largest expected degree is about dmax -- generated on
+    the device like RMAT (rmat.hpp).  The soc-LiveJournal1 / Friendster
+    stand-ins: LJ_SIZED_POWER_LAW, FRIENDSTER_SIZED_POWER_LAW."""
+    return N.power_law_params(int(n), int(m), int(dmax), int(seed))
+
+
+# soc-LiveJournal1 (SNAP: 4,847,571 V, 68,993,773 E; largest undirected degree
+# 20,333) and Friendster (65,608,366 V, 1,806,067,135 E; degrees capped at
+# 5,000 friends, largest 5,214): (n, m, dmax) of their power-law stand-ins.
+LJ_SIZED_POWER_LAW = (4847571, 68993773, 20333)
+FRIENDSTER_SIZED_POWER_LAW = (65608366, 1806067135, 5214)
+
+
 def generate_edges(params, begin: int = 0, end: int = -1):
     """Host copy of the counter-based edge stream (bit-identical to the device generator)."""
     return N.generate_edges(params, int(begin), int(end))

@@ -95,8 +95,10 @@ def init_runtime(device: str = "auto", comm: Optional[Any] = None) -> Runtime:
                 # run and its first multi-GPU level
                 inner = N.tcp_comm(boot, backend)
                 comm, fallback = _try_peer(boot, backend, inner, rank, kind == "peer")
-                if comm is inner and not shared:
+                if comm is inner and (not shared or os.environ.get("DBFS_TRY_RCCL") == "1"):
                     # no peer windows: RCCL over xGMI (bounded setup), else TCP
+                    # (DBFS_TRY_RCCL=1: also on a shared GPU, where RCCL must
+                    # fail -- tests of the agreed fallback)
                     comm = _rccl_or(inner, boot, backend, rank, world, local_rank)
     comm.bind_backend(backend)
     rt = Runtime(backend=backend, comm=comm, rank=comm.rank, world=comm.size, local_rank=local_rank)

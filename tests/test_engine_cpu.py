@@ -703,3 +703,30 @@ def test_range_staged_top_down_levels_cpu(rt, words):
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0])
         ranged = ranged or any(c[5] for c in r.chains)
     assert ranged
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_power_law_generator(P):
+    """Chung-Lu power-law graphs (power_law_params): labels scrambled into
+    [0, n) for an n that is no power of two, a heavy-tailed degree sequence
+    whose top expected degree follows dmax, and levels exact against the oracle
+    on one rank and on virtual ranks (the shard build regenerates the same
+    edges as the host copy)."""
+    p = dbfs.power_law_params(30011, 420000, 1500, 5)
+    assert p.power_law and p.pl_i0 > 0
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off))
+    assert deg.sum() == 2 * 420000
+    assert 0.5 * 1500 < deg.max() < 2.0 * 1500 and deg.max() > 20 * deg.mean()
+    u, v = dbfs.generate_edges(p, 0, 1000)
+    assert np.asarray(u).max() < 30011 and np.asarray(v).max() < 30011
+    srcs = [int(np.argmax(deg)), 4]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        return [(b.run(s), b.levels())[1] for s in srcs]
+
+    outs = [body(dbfs.init_runtime("cpu"))] if P == 1 else run_virtual_ranks(P, body, device="cpu")
+    for rank_out in outs:
+        for lv, s in zip(rank_out, srcs):
+            assert np.array_equal(lv, _oracle(csr, s))

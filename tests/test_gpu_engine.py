@@ -94,6 +94,33 @@ def test_device_generator_matches_host(gpu_runtime):
         assert np.array_equal(np.sort(dc[ro[r]:ro[r + 1]]), np.sort(hc[ro[r]:ro[r + 1]]))
 
 
+def test_power_law_generator_on_device(gpu_runtime):
+    """The Chung-Lu power-law generator (the soc-LiveJournal1 / Friendster
+    stand-in, integer-only inverse CDF): the device-built shard equals the host
+    copy row for row, and every mode's levels equal the oracle from the
+    hubs, a low-degree vertex and 3 virtual ranks."""
+    p = dbfs.power_law_params(200003, 2900000, 6000, 3)
+    csr = dbfs.host_csr_from_params(p)
+    bfs = dbfs.BFS(p, gpu_runtime)
+    dev = bfs.graph.to_host()
+    assert np.array_equal(np.asarray(dev.row_off), np.asarray(csr.row_off))
+    deg = np.diff(np.asarray(csr.row_off))
+    assert deg.max() > 20 * deg.mean()  # (a heavy tail, not a uniform graph)
+    for mode in ("do", "td", "bu"):
+        bfs.mode = mode
+        for s in (int(np.argmax(deg)), int(np.argmin(np.where(deg > 0, deg, 1 << 30)))):
+            _check(bfs, csr, s)
+    srcs = [int(np.argmax(deg)), 17]
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode="do")
+        return [(b.run(s), b.levels())[1] for s in srcs]
+
+    for rank_out in run_virtual_ranks(3, body, device="hip"):
+        for lv, s in zip(rank_out, srcs):
+            assert np.array_equal(lv, dbfs.cpu_bfs(csr, s)[0])
+
+
 @pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("mode", ["do", "td", "ref"])
 def test_virtual_ranks_on_one_gpu(P, mode):
@@ -960,6 +987,31 @@ def test_peer_hung_rank_names_the_stalled_collective():
         assert f"rank {r} timed out in collective #" in e and "waiting for rank 1" in e, e[-2000:]
         assert "level 1" in e, e[-2000:]
     assert elapsed < 50
+
+
+@pytest.mark.parametrize("fault,comm", [("kind=rccl_init", "peer+tcp"), ("kind=peer_init", "tcp")])
+def test_transport_setup_failures_fall_back(fault, comm):
+    """The multi-GPU setup does not depend on RCCL: with RCCL's setup forced
+    to fail (DBFS_FAULT_INJECT kind=rccl_init) two ranks still form the peer
+    transport over its TCP inner communicator and validate every timed root;
+    with the peer windows' setup failing too (kind=peer_init, and RCCL tried
+    anyway: DBFS_TRY_RCCL=1 -- it fails on a shared GPU), every rank agrees on
+    TCP and the run still validates."""
+    import json
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM_TIMEOUT_S="20", DBFS_FAULT_INJECT=fault, DBFS_TRY_RCCL="1",
+               DBFS_RCCL_INIT_TIMEOUT_S="10")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "DBFS_COMM"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "17", "--steps", "3",
+           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "0", "--secondary", "none"]
+    out = _run_group(cmd, env, 110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == comm and rec["validated_roots"] == "3/3"
+    if comm == "peer+tcp":
+        assert rec["comm_topology"]["inner"] == "tcp" and rec["comm_inner_ops"] == 0
 
 
 def _free_port_pair():
