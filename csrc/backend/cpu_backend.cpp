@@ -127,6 +127,14 @@ class CpuBackend final : public Backend {
     }
     for (int64_t w = 0; w < a.gwords; ++w) a.visited[w] = a.zdeg[w];
     for (int64_t w = 0; w < a.words; ++w) a.frontier[w] = 0;
+    if (a.frontier_global)
+      for (int64_t w = 0; w < a.gwords; ++w) a.frontier_global[w] = 0;
+    if (a.src_global >= 0) {
+      // (a seed without collective: the source's bits on every rank)
+      const word_t gbit = 1ull << (a.src_global & 63);
+      a.visited[a.src_global >> 6] |= gbit;
+      if (a.frontier_global) a.frontier_global[a.src_global >> 6] = gbit;
+    }
     int64_t cnt = 0, deg = 0;
     if (src >= 0) {
       const word_t bit = 1ull << (src & 63);
@@ -150,8 +158,15 @@ class CpuBackend final : public Backend {
       for (int64_t b = 0; b * kTdEdgesPerBlock < deg; ++b) a.blk_vstart[b] = 0;
     }
     if (a.ctrl) {
+      int64_t gc = cnt, gd = deg;
+      if (a.deg_all) {
+        gd = a.deg_all[a.src_global];
+        gc = gd > 0 ? 1 : 0;
+        a.stats[2] = gc;
+        a.stats[3] = gd;
+      }
       LevelCtrl c = a.ctrl_init;
-      level_ctrl_finish(c, cnt, deg, true, nullptr);
+      level_ctrl_finish(c, gc, gd, true, nullptr);
       *a.ctrl = c;
       if (a.mailbox) {
         a.mailbox->done = c.done;

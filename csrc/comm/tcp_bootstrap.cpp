@@ -204,9 +204,19 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
       fd = ::socket(AF_INET, SOCK_STREAM, 0);
       if (fd < 0) throw Error("bootstrap socket() failed");
       if (::connect(fd, reinterpret_cast<const sockaddr*>(&a), sizeof(a)) == 0) break;
+      const int err = errno;
       ::close(fd);
-      if (std::chrono::steady_clock::now() > deadline)
-        throw Error("bootstrap connect to " + host + ":" + std::to_string(port) + " timed out");
+      if (std::chrono::steady_clock::now() > deadline) {
+        // (rank 0 listens on the rendezvous address only: a MASTER_ADDR that
+        // is a loopback alias on rank 0's host -- 127.0.1.1 in /etc/hosts --
+        // is unreachable from other hosts unless rank 0 binds every interface)
+        char ip[INET_ADDRSTRLEN] = {0};
+        inet_ntop(AF_INET, &a.sin_addr, ip, sizeof(ip));
+        throw Error("bootstrap connect to " + host + ":" + std::to_string(port) + " (" + ip + ") timed out after " +
+                    std::to_string(static_cast<int>(timeout_s)) + " s: " + std::strerror(err) +
+                    " -- is rank 0 up?  A rank on another host needs rank 0 started with DBFS_BOOTSTRAP_BIND=any "
+                    "when its MASTER_ADDR resolves to a loopback alias there");
+      }
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
     }
     tune_socket(fd);

@@ -957,9 +957,17 @@ RunResult DeviceLoop::run() {
   // frontier_[0] for a sparse level 0 to write).  (Several ranks: the seed
   // totals are all-reduced first, then level_finish seeds the LevelCtrl and
   // stamps level -1.)
-  InitRunArgs ia = e_.init_args(src_, fr_own(1), xc_ ? nullptr : e_.ctrl_.data(), init_,
-                                xc_ ? nullptr : e_.mailbox_dev_ + slot(-1));
+  // (several ranks: each rank seeds the traversal itself from the replicated
+  // degree of the source -- no collective before level 0; a bottom-up level
+  // 0 gets the whole seed frontier written locally)
+  seed_gather_ = xc_ && init_.dir == 'B';
+  InitRunArgs ia = e_.init_args(src_, fr_own(1), e_.ctrl_.data(), init_, e_.mailbox_dev_ + slot(-1));
   ia.stats = sblk(-1);
+  if (xc_) {
+    ia.deg_all = e_.deg_all_.data();
+    ia.src_global = src_;
+    if (seed_gather_) ia.frontier_global = e_.frontier_[1].data();
+  }
   if (sparse_) {
     ia.qbase = e_.qbase_.data();
     ia.blk_vstart = e_.blk_vstart_.data();
@@ -967,13 +975,10 @@ RunResult DeviceLoop::run() {
     ia.frontier_clear = fr_own(0);
   }
   be_.init_run(ia);
-  // the seed's frontier is gathered with its totals when level 0 is bottom-up
-  // (bu mode).  (Top-down levels read only their owned slice; the replicated
-  // visited bitmap filters candidates with whatever remote bits it has --
-  // merged frontiers, and the remote targets this rank claimed and sent -- so
-  // a stale remote bit only costs an id its owner drops.)
-  seed_gather_ = xc_ && init_.dir == 'B';
-  if (xc_) finish_ranks(-1, true, 0, 0, seed_gather_);
+  // (Top-down levels read only their owned slice; the replicated visited
+  // bitmap filters candidates with whatever remote bits it has -- merged
+  // frontiers, and the remote targets this rank claimed and sent -- so a
+  // stale remote bit only costs an id its owner drops.)
 
   // Frontier double buffer: the seed is frontier_[1]; level L reads
   // frontier_[(L + 1) & 1] and writes the other one.

@@ -664,6 +664,16 @@ void Engine::alloc_bitmap_state() {
   za.words = W;
   be_.zero_degree_mask(za);
   if (exchange()) comm_.allgather(za.out, zdeg_.data(), static_cast<size_t>(W) * sizeof(word_t));
+  if (exchange()) {
+    // every vertex's degree on every rank (4 B per vertex): a traversal's
+    // seed totals without a collective (InitRunArgs::deg_all)
+    deg_all_ = DBuf<uint32_t>(be_, static_cast<size_t>(part_.nranks) * static_cast<size_t>(part_.part));
+    DBuf<uint32_t> mine(be_, static_cast<size_t>(part_.part));
+    be_.memset_async(mine.data(), 0, mine.bytes());
+    be_.degrees_u32(g_.view().row_off, g_.rows(), mine.data());
+    comm_.allgather(mine.data(), deg_all_.data(), static_cast<size_t>(part_.part) * sizeof(uint32_t));
+    be_.synchronize();
+  }
   be_.synchronize();
   bitmap_ready_ = true;
 }

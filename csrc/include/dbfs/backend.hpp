@@ -256,6 +256,15 @@ struct InitRunArgs {
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;
+  // Several ranks, seeded without a collective: every rank's replicated
+  // degree array (deg_all, the global source id src_global) gives the seed's
+  // global totals, so with ctrl / mailbox set each rank finishes the seed
+  // itself -- the source's bit set in its replicated visited bitmap, and
+  // (frontier_global, a bottom-up first level) the whole global seed
+  // frontier written locally instead of all-gathered.
+  const uint32_t* deg_all = nullptr;
+  int64_t src_global = -1;
+  word_t* frontier_global = nullptr;
 };
 
 // Multi-block exclusive scan of unit_cnt / unit_deg (in place, per chunk of

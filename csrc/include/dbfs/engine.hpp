@@ -464,6 +464,7 @@ class Engine {
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_;
+  DBuf<uint32_t> deg_all_;  // several ranks: every vertex's degree (InitRunArgs::deg_all)
   // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
   // decision and its ticket (zero between levels)
   DBuf<int64_t> cut_part_;

@@ -115,10 +115,18 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
     }
     for (int64_t i = n4 * 4 + t0; i < rows; i += stride) a.level[i] = i == src ? 0 : kUnreached;
   }
-  const int64_t sw = src >= 0 ? a.vis_word_base + (src >> 6) : -1;
-  const word_t sbit = src >= 0 ? (1ull << (src & 63)) : 0ull;
+  // (the source's visited bit: in every rank's replicated bitmap when the
+  // global id is known -- a seed without collective -- else on its owner)
+  const int64_t sw = a.src_global >= 0 ? (a.src_global >> 6) : src >= 0 ? a.vis_word_base + (src >> 6) : -1;
+  const word_t sbit = a.src_global >= 0 ? (1ull << (a.src_global & 63)) : src >= 0 ? (1ull << (src & 63)) : 0ull;
   for (int64_t w = t0; w < a.gwords; w += stride) a.visited[w] = a.zdeg[w] | (w == sw ? sbit : 0ull);
-  for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? sbit : 0ull;
+  if (a.frontier_global) {
+    // a bottom-up first level reads the whole seed frontier: written here
+    for (int64_t w = t0; w < a.gwords; w += stride) a.frontier_global[w] = w == sw ? sbit : 0ull;
+  } else {
+    const word_t obit = src >= 0 ? (1ull << (src & 63)) : 0ull;
+    for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? obit : 0ull;
+  }
   if (a.frontier_clear)
     for (int64_t w = t0; w < a.words; w += stride) a.frontier_clear[w] = 0ull;
   // the seed's work-list entry: edge blocks [0, ceil(d / EPB)) all start in it
@@ -149,8 +157,17 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
     a.qv[0] = static_cast<vid_t>(src);
   }
   if (a.ctrl) {
+    // the seed's global totals: this rank's own, or (several ranks) from the
+    // replicated degree of the source
+    int64_t gc = cnt, gd = deg;
+    if (a.deg_all) {
+      gd = a.deg_all[a.src_global];
+      gc = gd > 0 ? 1 : 0;
+      a.stats[2] = gc;
+      a.stats[3] = gd;
+    }
     LevelCtrl c = a.ctrl_init;
-    level_ctrl_finish(c, cnt, deg, true, nullptr);
+    level_ctrl_finish(c, gc, gd, true, nullptr);
     *a.ctrl = c;
     if (a.mailbox) stamp_mailbox(a.mailbox, c, -1);
   }

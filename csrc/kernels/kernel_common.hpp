@@ -159,30 +159,55 @@ __device__ __forceinline__ void push_frontier_word(const FrontierTable* t, int r
     if (p != rank) sys_store_u64(t->dst[p] + w, v);
 }
 
-// Append v (act lanes) to its owner's list: one atomic per wave and owner on
-// the count word (lists + owner * stride), the ids after it -- or, with a
-// direct exchange table, after the count word of the owner's window slot
-// (write-through stores over xGMI).  Wave-uniform call.
-__device__ __forceinline__ void owner_list_append(vid_t* lists, int64_t stride, int64_t part, vid_t v, bool act,
-                                                  const DirectTable* dt = nullptr) {
+// Append the kItems items of every lane (bit k of `act`: v[k]) to their
+// owners' lists with ONE atomic per wave and owner for all of them (the
+// per-item form takes one per item index and owner: up to kItems times as
+// many returning atomics on the same count words).  Wave-uniform call.
+template <int kItems>
+__device__ __forceinline__ void owner_list_append_items(vid_t* lists, int64_t stride, int64_t part,
+                                                        const vid_t (&v)[kItems], unsigned act,
+                                                        const DirectTable* dt = nullptr) {
   const int lane = lane_id();
-  const int owner = act ? static_cast<int>(static_cast<int64_t>(v) / part) : -1;
-  unsigned long long pending = __ballot(act);
-  while (pending) {
-    const int leader = __ffsll(static_cast<long long>(pending)) - 1;
-    const int o = __builtin_amdgcn_readfirstlane(__shfl(owner, leader, kWave));
-    const unsigned long long msk = __ballot(owner == o);
-    unsigned base = 0;
-    vid_t* list = lists + static_cast<int64_t>(o) * stride;
-    if (lane == leader) base = atomicAdd(list, static_cast<unsigned>(__popcll(msk)));
-    base = __shfl(base, leader, kWave);
-    DBFS_DCHECK(base + __popcll(msk) < static_cast<unsigned long long>(stride), 3, base);
-    if (owner == o) {
-      const unsigned at = 1 + base + mask_rank(msk);
-      if (dt) sys_store_u32(dt->dst[o] + at, v);
-      else list[at] = v;
+  int own[kItems];
+  unsigned long long left = 0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    own[k] = ((act >> k) & 1u) ? static_cast<int>(static_cast<int64_t>(v[k]) / part) : -1;
+    left |= __ballot(own[k] >= 0);
+  }
+  while (left) {
+    // the next owner: the first active item of the first lane with one
+    const int leader = __ffsll(static_cast<long long>(left)) - 1;
+    int mine = -1;
+#pragma unroll
+    for (int k = kItems - 1; k >= 0; --k)
+      if (own[k] >= 0) mine = own[k];
+    const int o = __builtin_amdgcn_readfirstlane(__shfl(mine, leader, kWave));
+    unsigned long long msk[kItems];
+    unsigned tot = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      msk[k] = __ballot(own[k] == o);
+      tot += static_cast<unsigned>(__popcll(msk[k]));
     }
-    pending &= ~msk;
+    vid_t* list = lists + static_cast<int64_t>(o) * stride;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(list, tot);
+    base = __shfl(base, leader, kWave);
+    DBFS_DCHECK(base + tot < static_cast<unsigned long long>(stride), 3, base);
+    unsigned before = 0;
+    left = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      if (own[k] == o) {
+        const unsigned at = 1u + base + before + mask_rank(msk[k]);
+        if (dt) sys_store_u32(dt->dst[o] + at, v[k]);
+        else list[at] = v[k];
+        own[k] = -1;
+      }
+      before += static_cast<unsigned>(__popcll(msk[k]));
+      left |= __ballot(own[k] >= 0);
+    }
   }
 }
 

@@ -858,9 +858,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
         owner_list_append_wg<kItems>(a.lists, a.list_stride, a.part, a.nranks, v, remote,
                                      dx ? a.direct.table : nullptr);
       } else if (__ballot(remote != 0)) {
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-          owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u, dx ? a.direct.table : nullptr);
+        owner_list_append_items<kItems>(a.lists, a.list_stride, a.part, v, remote, dx ? a.direct.table : nullptr);
       }
     }
     // (B) finish the claimed vertices (the whole workgroup: one counter atomic)
@@ -1026,12 +1024,9 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
           for (int k = 0; k < kItems; ++k)
             if (((claimed >> k) & 1u) && static_cast<uint64_t>(v[k]) - lo >= rows) remote |= 1u << k;
           claimed &= ~remote;
-          if (__ballot(remote != 0)) {
-#pragma unroll
-            for (int k = 0; k < kItems; ++k)
-              owner_list_append(a.lists, a.list_stride, a.part, v[k], (remote >> k) & 1u,
-                                dx ? a.direct.table : nullptr);
-          }
+          // (one count atomic per wave and owner for all its items)
+          if (__ballot(remote != 0))
+            owner_list_append_items<kItems>(a.lists, a.list_stride, a.part, v, remote, dx ? a.direct.table : nullptr);
         }
         // (B) finish the wave's claimed vertices
         sparse_settle<kItems>(a, v, claimed);

@@ -106,13 +106,14 @@ def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gather
 
 def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     """Traffic of one traversal from its enqueued chains (level, form, cap,
-    gather[, push, ranged]): start barrier, the seed's collective, every
-    chain, the wall-time max at the end."""
+    gather[, push, ranged]): start barrier, every chain, the wall-time max at
+    the end.  (The seed needs no collective: every rank seeds the traversal
+    from its replicated degree array, and writes a bottom-up first level's
+    whole seed frontier itself.)"""
     P = cfg.nranks
     tot = ChainTraffic()
     tot.add("barrier", 0)
     seed_gather = cfg.mode == "bu"
-    tot.merge(level_end(cfg, seed_gather))
     gathered = {-1: seed_gather}
     for level, form, cap, gather, *more in chains:
         tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False),

@@ -38,13 +38,14 @@ def test_traffic_matches_model(P, mode, knobs):
                 assert nbytes == want.bytes[kind], (kind, chains, got, dict(want.bytes))
             # one collective per chain (its level's end), plus a top-down
             # chain's payload exchange; a bottom-up chain's input frontier came
-            # with the previous collective unless that one mispredicted
+            # with the previous collective unless that one mispredicted; none
+            # for the seed (every rank seeds itself), one wall-time max
             fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True,
                                             list_form_edges=cfg.list_form_edges), chains)
             n_td = sum(1 for c in chains if c[1] in "ST")
             n_lone_b = sum(1 for i, c in enumerate(chains)
                            if c[1] == "B" and not (chains[i - 1][3] if i else mode == "bu"))
-            assert fused.total_calls == 1 + len(chains) + n_td + n_lone_b + 1
+            assert fused.total_calls == len(chains) + n_td + n_lone_b + 1
 
 
 def test_table_shapes():
