@@ -180,7 +180,12 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
     for (int p = 0; p < size_ && !shared_; ++p)
       for (int q = p + 1; q < size_; ++q)
         if (!bus_[p].empty() && bus_[p] == bus_[q]) shared_ = true;
-    if (shared_) fused_ = false;
+    // (DBFS_PEER_SPLIT=0: the separate-GPU forms on a shared GPU anyway --
+    // tests of the fused collectives and in-kernel waits with two ranks,
+    // which cannot starve each other of CUs)
+    const char* sp = std::getenv("DBFS_PEER_SPLIT");
+    split_ = shared_ && !(sp && std::string(sp) == "0");
+    if (split_) fused_ = false;
   }
   // the direct exchange's tables (one per parity; DBFS_PEER_DIRECT=0: none)
   const char* de = std::getenv("DBFS_PEER_DIRECT");

@@ -449,7 +449,7 @@ class PeerComm final : public Comm {
   // the pushed frontier slices are on (off: DBFS_PEER_FRONTIER_MB=0, or their self-test failed)
   bool frontier_on() const { return ftab_ != nullptr; }
   bool fused() const { return fused_; }
-  bool split_waits() const override { return shared_; }
+  bool split_waits() const override { return split_; }
   // Topology seen at construction: every rank's PCI bus id, and access[r * P
   // + p] = 2 (ranks r and p share a GPU), 1 (rank r's GPU can access p's),
   // 0 (it cannot), -1 (p's GPU not visible to rank r's process).
@@ -515,8 +515,9 @@ class PeerComm final : public Comm {
   bool watch_installed_ = false;
   char* slot_ptr(int owner, int parity, int sender) const;
   void release();
-  // several ranks on one physical GPU (bus ids): unfused collectives, split waits
-  bool shared_ = false;
+  // several ranks on one physical GPU (bus ids): unfused collectives, split
+  // waits (split_; DBFS_PEER_SPLIT=0 keeps the separate-GPU forms)
+  bool shared_ = false, split_ = false;
   std::vector<std::string> bus_;
   std::vector<int> access_;
   std::string verdict_;

@@ -932,6 +932,29 @@ def test_peer_comm_four_ranks_share_one_gpu_rmat20():
     assert rec["heldout"]["validated_roots"] == "8/8"
 
 
+def test_peer_fused_forms_two_ranks_share_one_gpu():
+    """The separate-GPU forms of the peer transport -- every collective one
+    fused launch, the direct exchanges' waits inside their consumer kernels
+    (DBFS_PEER_SPLIT=0 keeps them on a shared GPU) -- with two ranks on device
+    0, which cannot starve each other of CUs: every timed root validated."""
+    import json
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16", DBFS_COMM_TIMEOUT_S="20",
+               DBFS_PEER_SPLIT="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "19", "--steps", "4",
+           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "8", "--secondary", "none"]
+    out = _run_group(cmd, env, 100)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    topo = rec["comm_topology"]
+    assert topo["shared_device"] is True and topo["split_waits"] is False and topo["fused"] is True
+    assert rec["validated_roots"] == "4/4" and rec["heldout"]["validated_roots"] == "8/8"
+    assert rec["pushed_chains"] > 0
+
+
 def test_peer_late_rank_completes():
     """A rank that publishes late: rank 1 sleeps 1.5 s before enqueueing level
     2 of every traversal (DBFS_FAULT_INJECT kind=delay) while its three peers'
