@@ -1012,21 +1012,25 @@ def test_peer_hung_rank_names_the_stalled_collective():
     assert elapsed < 50
 
 
-@pytest.mark.parametrize("fault,comm", [("kind=rccl_init", "peer+tcp"), ("kind=peer_init", "tcp")])
+@pytest.mark.parametrize("fault,comm", [("kind=rccl_init", "peer+tcp"), ("kind=peer_init,kind=rccl_init", "tcp"),
+                                        ("kind=peer_init", "tcp")])
 def test_transport_setup_failures_fall_back(fault, comm):
     """The multi-GPU setup does not depend on RCCL: with RCCL's setup forced
     to fail (DBFS_FAULT_INJECT kind=rccl_init) two ranks still form the peer
     transport over its TCP inner communicator and validate every timed root;
-    with the peer windows' setup failing too (kind=peer_init, and RCCL tried
-    anyway: DBFS_TRY_RCCL=1 -- it fails on a shared GPU), every rank agrees on
-    TCP and the run still validates."""
+    with the peer windows' setup failing too, the RCCL fallback is tried
+    (DBFS_TRY_RCCL=1: on a shared GPU too), fails on every rank, and the ranks
+    agree on TCP; without DBFS_TRY_RCCL ranks sharing a GPU go straight to TCP
+    (RCCL refuses -- or can hang in its setup with -- two ranks on one device)."""
     import json
     import sys
 
-    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM_TIMEOUT_S="20", DBFS_FAULT_INJECT=fault, DBFS_TRY_RCCL="1",
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM_TIMEOUT_S="20", DBFS_FAULT_INJECT=fault,
                DBFS_RCCL_INIT_TIMEOUT_S="10")
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "DBFS_COMM"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "DBFS_COMM", "DBFS_TRY_RCCL"):
         env.pop(k, None)
+    if "rccl_init" in fault:
+        env["DBFS_TRY_RCCL"] = "1"
     cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "17", "--steps", "3",
            "--warmup", "1", "--no-int32-pass", "--heldout-roots", "0", "--secondary", "none"]
     out = _run_group(cmd, env, 110)
