@@ -741,6 +741,10 @@ void DeviceLoop::emit_dense(Chain& c) {
   // (a level past kNarrowMaxLevel would store the unreached byte: the usual
   // path flags the overflow and the run is repeated wide)
   if (direct_ && e_.run_narrow_ && L + 1 <= kNarrowMaxLevel) {
+    // a late level is possible (most of the adjacency visited at its start:
+    // few vertices left for its frontier's edges) -- the variant that can
+    // stop once every vertex with an edge is reached (LevelCtrl::late)
+    ta.late_ok = init_.n_active > 0 && vis_hint_ >= 0.5 * static_cast<double>(e_.total_directed_);
     // byte-map levels write the level itself (nothing to clear after)
     ta.level_direct = e_.level8_.data();
     ta.narrow_base = e_.narrow_base_;
@@ -951,6 +955,9 @@ RunResult DeviceLoop::run() {
   init_.td_byte_edges = bytes_ok_ ? static_cast<double>(byte_edges_) : 1e300;
   init_.check_visited_min = opt_.td_check_visited_min;
   init_.dir = opt_.mode == Mode::BottomUp ? 'B' : 'T';
+  // (directed graphs: a vertex without out-edges can still be reached -- no
+  // all-reached stop)
+  init_.n_active = opt_.directed ? 0 : e_.n_active_;
   // one fused pass: levels, visited, the seed frontier (frontier_[1]), its
   // totals, the seeded LevelCtrl and the mailbox stamp of level -1 (+ with
   // sparse levels: the seed's work-list entry in set 0 and a clean
@@ -1129,6 +1136,9 @@ RunResult DeviceLoop::collect(int nlev, std::chrono::steady_clock::time_point t1
     res_.levels.push_back(r);
   }
   res_.depth = nlev == 0 ? 1 : nlev;
+  // (a traversal that stopped once every vertex with an edge was reached did
+  // not expand its last frontier: its deepest level is the last record's + 1)
+  if (nlev > 0 && recs[nlev - 1].discovered > 0) res_.depth = nlev + 1;
   res_.edges = vis_deg / 2;
   return std::move(res_);
 }

@@ -434,7 +434,9 @@ def test_device_loop_several_ranks(P, mode, predict):
     for rank_out in run_virtual_ranks(P, body, device="cpu"):
         for (ld, lh, ra, rb, ta, tb), s in zip(rank_out, srcs):
             assert np.array_equal(ld, _oracle(csr, s)) and np.array_equal(lh, ld)
-            assert ra == rb and ta == tb
+            # (the device loop stops once every vertex with an edge is reached:
+            # the host loop's extra last level expanded its frontier for nothing)
+            assert ra == rb[:len(ra)] and all(r[3] == 0 for r in rb[len(ra):]) and ta == tb
 
 
 @pytest.mark.parametrize("knobs", [
@@ -477,7 +479,8 @@ def test_device_loop_sparse_lists_several_ranks(P, knobs):
         forms = ""
         for (ld, ra, rb, ta, tb, m, fs), s in zip(rank_out, srcs):
             assert np.array_equal(ld, _oracle(csr, s))
-            assert ra == rb and ta == tb
+            # (the device loop stops once every vertex with an edge is reached)
+            assert ra == rb[:len(ra)] and all(r[3] == 0 for r in rb[len(ra):]) and ta == tb
             mis += m
             forms += "".join(fs)
         if knobs.get("list_form_edges", 1) == 64:

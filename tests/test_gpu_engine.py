@@ -70,6 +70,28 @@ def test_uniform_and_isolated_source(gpu_runtime, mode):
         _check(bfs, csr, s)
 
 
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_all_reached_stop_and_late_levels(gpu_runtime, mode):
+    """A connected graph (every vertex has an edge, one component): the device
+    loop stops once every vertex with an edge is reached instead of expanding
+    the last frontier, and the late top-down levels (most of the graph
+    visited: claims by fetch-or, counted down, the grid stopping at zero)
+    leave exact levels, reached vertices, edges and depth -- uniform graphs
+    of mean degree 28 (the LiveJournal-sized shape, scaled down) and a
+    power-law one, 32-bit levels too."""
+    for p in (dbfs.uniform_params(300000, 4200000, 5), dbfs.power_law_params(300007, 4200000, 4000, 9)):
+        csr = dbfs.host_csr_from_params(p)
+        deg = np.diff(np.asarray(csr.row_off))
+        bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
+        for narrow in (1, 0):
+            bfs.engine.set_option("narrow_levels", narrow)
+            for s in (int(np.argmax(deg)), 12345, 299000):
+                res = _check(bfs, csr, s)
+                exp, _ = dbfs.cpu_bfs(csr, s)
+                assert res.depth == int(exp[exp != dbfs.UNREACHED].max()) + 1
+                assert bfs.validate(s)
+
+
 def test_hub_heavy_star(gpu_runtime):
     # one vertex with degree >> kTdEdgesPerBlock exercises multi-block hubs
     n = 50000
