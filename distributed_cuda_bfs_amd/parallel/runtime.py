@@ -110,9 +110,20 @@ def _make_rccl(boot, backend, rank: int, world: int, local_rank: int):
     """An RCCL communicator (one GPU per rank: the backend made LOCAL_RANK
     current before the communicator is created); its setup is bounded
     (DBFS_RCCL_INIT_TIMEOUT_S, native NcclComm)."""
+    # every rank takes part in the id broadcast before anything can fail (an
+    # empty id tells the others rank 0 could not make one), so the bootstrap's
+    # collective sequence stays aligned for the agreement after a failure
+    uid, why = b"", ""
+    if rank == 0:
+        try:
+            uid = N.nccl_unique_id()
+        except Exception as e:  # noqa: BLE001 - re-raised after the broadcast
+            why = str(e) or type(e).__name__
+    uid = boot.broadcast(uid)
+    if not uid:
+        raise RuntimeError(why or "rank 0 could not create the RCCL id")
     if backend.device_id != local_rank:
         raise RuntimeError(f"rank {rank}: backend on device {backend.device_id}, expected LOCAL_RANK {local_rank}")
-    uid = boot.broadcast(N.nccl_unique_id() if rank == 0 else b"")
     return N.nccl_comm(uid, rank, world, backend)  # RCCL over xGMI
 
 

@@ -158,6 +158,43 @@ def test_bootstrap_ignores_a_silent_stray_connection():
     stray.close()
 
 
+def test_rccl_fallback_keeps_the_bootstrap_aligned():
+    """A failed RCCL setup (here: no GPU, so rank 0 cannot make the id; on a
+    shared GPU: the device check) is agreed over the bootstrap and every rank
+    falls back to the inner communicator with the bootstrap's collective
+    sequence intact -- the id broadcast happens on every rank before anything
+    can fail (a desync here once surfaced as a TcpComm count mismatch)."""
+    import socket
+    import threading
+
+    from distributed_cuda_bfs_amd.parallel.runtime import _rccl_or
+
+    N = dbfs.native
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = [None, None]
+
+    class FakeBackend:
+        device_id = 0
+
+    class Inner:
+        name = "tcp"
+
+    def body(r):
+        boot = N.TcpBootstrap("127.0.0.1", port, r, 2, 60.0)
+        inner = Inner()
+        got = _rccl_or(inner, boot, FakeBackend(), r, 2, r)
+        out[r] = (got is inner, [bytes(x) for x in boot.allgather(b"after%d" % r)])
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert all(o == (True, [b"after0", b"after1"]) for o in out), out
+
+
 def test_group_bootstrap_threads():
     """The in-process bootstrap (GroupBootstrap: the ranks of a VirtualGroup,
     one thread each) gathers every rank's bytes in rank order, broadcasts the
