@@ -741,10 +741,6 @@ void DeviceLoop::emit_dense(Chain& c) {
   // (a level past kNarrowMaxLevel would store the unreached byte: the usual
   // path flags the overflow and the run is repeated wide)
   if (direct_ && e_.run_narrow_ && L + 1 <= kNarrowMaxLevel) {
-    // a late level is possible (most of the adjacency visited at its start:
-    // few vertices left for its frontier's edges) -- the variant that can
-    // stop once every vertex with an edge is reached (LevelCtrl::late)
-    ta.late_ok = opt_.late_levels && init_.n_active > 0 && vis_hint_ >= 0.5 * static_cast<double>(e_.total_directed_);
     // byte-map levels write the level itself (nothing to clear after)
     ta.level_direct = e_.level8_.data();
     ta.narrow_base = e_.narrow_base_;

@@ -101,7 +101,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "direct_lists") o.direct_lists = v != 0;
   else if (name == "direct_level_end") o.direct_level_end = v != 0;
   else if (name == "direct_frontier") o.direct_frontier = v != 0;
-  else if (name == "late_levels") o.late_levels = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
 
@@ -157,8 +156,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"list_cap_factor", o.list_cap_factor},
           {"direct_lists", o.direct_lists ? 1.0 : 0.0},
           {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
-          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0},
-          {"late_levels", o.late_levels ? 1.0 : 0.0}};
+          {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
 }
 
 // ---- DeviceGraph ----------------------------------------------------------------

@@ -168,17 +168,7 @@ struct LevelCtrl {
   // directed graphs).  Once every one of them is reached no edge can discover
   // anything: the traversal is done without expanding its last frontier.
   int64_t n_active = 0;
-  // ... not reached yet at the start of the next level (n_active - reached);
-  // a one-rank late top-down level counts its claims down here and stops
-  // expanding at 0 (TdArgs, `late`)
-  int64_t remaining = 0;
-  // the next level is a late top-down level: few vertices left to reach for
-  // its frontier's edges (remaining x kLateEdgeRatio < m_f) -- claims by
-  // fetch-or on visited, counted in `remaining`
-  int32_t late = 0;
-  int32_t pad1 = 0;
 };
-constexpr int64_t kLateEdgeRatio = 4;
 
 // One record per finished level (device array; read after the run).
 struct LevelRecDev {
@@ -230,8 +220,6 @@ DBFS_HD void level_ctrl_finish(LevelCtrl& c, int64_t count, int64_t degsum, bool
   if (c.n_active > 0 && c.reached >= c.n_active) c.done = 1;
   c.bytes = (c.dir == 'T' && static_cast<double>(c.m_f) >= c.td_byte_edges) ? 1 : 0;
   c.check_visited = static_cast<double>(c.vis_deg) >= c.check_visited_min * c.total_directed ? 1 : 0;
-  c.remaining = c.n_active > 0 ? c.n_active - c.reached : 0;
-  c.late = (!c.done && c.n_active > 0 && c.dir == 'T' && c.remaining * kLateEdgeRatio < c.m_f) ? 1 : 0;
 }
 
 // Per-run initialisation of the bitmap engine in one pass (replaces a level
@@ -615,9 +603,6 @@ constexpr int kBinMaxBins = 2048;
 // For every edge (u, v) with u in the work list and v not visited: next[v] = 1.
 struct TdArgs {
   ShardView g;
-  // device loop, one rank, direct level bytes: launch the late-level variant
-  // (the host expects LevelCtrl::late; the device decides per level)
-  bool late_ok = false;
   const int64_t* qscan = nullptr;
   const int64_t* qbase = nullptr;
   const int32_t* blk_vstart = nullptr;

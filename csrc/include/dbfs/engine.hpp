@@ -322,10 +322,6 @@ struct EngineOptions {
   // its totals (and may fold into the bottom-up kernel): the frontier
   // exchange overlaps the kernels that produce it instead of following them.
   bool direct_frontier = true;
-  // One rank, undirected: top-down levels that start with most of the graph
-  // visited (LevelCtrl::late) claim by fetch-or, count the vertices still
-  // unreached down and stop their grid at zero (td_expand's kLate variant)
-  bool late_levels = true;
   // Bitmap engine (td / bu / do): levels kept in a one-byte-per-vertex array
   // during the traversal (a quarter of the per-run initialisation traffic),
   // widened to 32 bits when read; a traversal deeper than kNarrowMaxLevel is

@@ -328,10 +328,7 @@ __device__ __forceinline__ void update_unit(const UpdateArgs& a, int64_t unit, b
       for (int r = 0; r < a.nchunks; ++r) c |= a.cand[r * a.cand_stride + wl];
     }
     const word_t vis = a.visited[wl];
-    // (a late top-down level claimed its vertices in visited already: the
-    // level bytes are the new ones exactly)
-    const bool claimed = use_bytes && a.level_direct && a.ctrl && a.ctrl->late;
-    nb = a.force || claimed ? c : (c & ~vis);
+    nb = a.force ? c : (c & ~vis);
     if (nb) a.visited[wl] = vis | nb;
     a.frontier[wl] = nb;
     if constexpr (kRanks) {

@@ -140,7 +140,7 @@ template <int kThreads, bool kHubFilter, bool kBase32, typename BaseT, int kItem
 __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __restrict__ col, long long e0, int cnt,
                                               const int32_t* s_owner, const BaseT* s_base, bool filter,
                                               const word_t* s_hubvis, vid_t (&vk)[kItems], bool (&live)[kItems],
-                                              bool (&hubnew)[kItems], bool marks = true) {
+                                              bool (&hubnew)[kItems]) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
@@ -162,7 +162,7 @@ __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __re
           const vid_t h = vk[k] & ~kHubFlag;
           if ((s_hubvis[h >> 6] >> (h & 63)) & 1ull) {
             live[k] = false;
-          } else if (a.td_hub_mark && marks) {
+          } else if (a.td_hub_mark) {
             a.td_hub_mark[h] = 1;  // claimed; hub_apply stores its level byte
             live[k] = false;
           } else {
@@ -180,10 +180,7 @@ __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __re
 // bases in 32 bits (graphs of at most 2^32 adjacency entries): 16 instead of
 // 24 KiB of LDS per workgroup, 8 resident workgroups per CU instead of 6 (5
 // instead of 4 with the filter).
-// kLate: the late-level code (LevelCtrl::late -- claims by fetch-or, counted
-// down, the grid stopping at 0), a variant of its own: in every kernel it
-// cost the hot one-rank top-down variant 7 VGPRs and a wave slot per SIMD.
-template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false, bool kLate = false>
+template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
@@ -192,18 +189,12 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
-  __shared__ int s_stop;
   long long q = a.q, m = a.m;
   bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
-  // a late level (LevelCtrl::late, direct level bytes): claims by fetch-or on
-  // visited, counted down in ctrl->remaining; the grid stops once every
-  // vertex with an edge is reached
-  bool late = false;
   if (a.ctrl) {
     if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
     bytes = a.ctrl->bytes != 0;
     check = a.ctrl->check_visited != 0;
-    late = kLate && kOut != TdOut::Lists && a.level_direct && bytes && a.ctrl->late != 0;
     q = a.dev_stats[0];
     m = a.dev_stats[1];
     if (a.clear_qv) stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
@@ -233,21 +224,13 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
 
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    if (late) {
-      // (workgroup-uniform: thread 0 reads the count, every thread its copy)
-      if (t == 0)
-        s_stop = __hip_atomic_load(&const_cast<LevelCtrl*>(a.ctrl)->remaining, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 0 ? 1 : 0;
-      __syncthreads();
-      if (s_stop) break;
-    }
     const long long e0 = b * kTdEdgesPerBlock;
     const int cnt = td_block_owner_map<kThreads, BaseT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
                                                         s_base, s_wmax);
 
     vid_t vk[kItems];
     bool live[kItems], hubnew[kItems];
-    td_load_items<kThreads, kHubFilter, kBase32>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis, vk, live, hubnew,
-                                                 !late);
+    td_load_items<kThreads, kHubFilter, kBase32>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis, vk, live, hubnew);
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
@@ -288,22 +271,6 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
           keep[k] = live[k] && (hubnew[k] || !(visited[vk[k] >> 6] & (1ull << (vk[k] & 63))));
-        if (late) {
-          // (rare claims: most targets are visited) -- won by fetch-or, so each
-          // new vertex is counted once
-          long long won = 0;
-#pragma unroll
-          for (int k = 0; k < kItems; ++k) {
-            if (!keep[k]) continue;
-            const word_t bit = 1ull << (vk[k] & 63);
-            keep[k] = !(atomicOr(const_cast<word_t*>(a.visited) + (vk[k] >> 6), bit) & bit);
-            won += keep[k] ? 1 : 0;
-          }
-          won = wave_sum(won);
-          if (lane == 0 && won)
-            __hip_atomic_fetch_add(&const_cast<LevelCtrl*>(a.ctrl)->remaining, -static_cast<int64_t>(won),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
 #pragma unroll
         for (int k = 0; k < kItems; ++k) TD_STAT(2, __popcll(__ballot(keep[k])));
 #pragma unroll
@@ -1362,11 +1329,11 @@ static void td_stats_report(hipStream_t st) {
 // workgroups that start when the first ones finish their strided share: with
 // 2048 workgroups and six resident per CU, RMAT-22 top-down 70 against 83
 // GTEPS at 1536.
-template <TdOut kOut, bool kFilter, bool kBase32, bool kLate = false>
+template <TdOut kOut, bool kFilter, bool kBase32>
 unsigned td_resident_grid(int64_t cap) {
   static const int per_cu = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kTdThreads, kFilter, kBase32, kLate>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kTdThreads, kFilter, kBase32>,
                                                      kTdThreads, 0) != hipSuccess || n <= 0)
       n = 1;
     return n;
@@ -1395,21 +1362,18 @@ void td_expand(const TdArgs& a, hipStream_t st) {
     if (a.grid <= 0) return;
     const bool b32 = a.g.nnz <= (int64_t(1) << 32);
     const int64_t fgrid = a.grid_filter > 0 ? a.grid_filter : a.grid;
-#define LAUNCH_TD_DEV(OUT, F, B, L) \
-  td_expand_kernel<OUT, kTdThreads, F, B, L><<<td_resident_grid<OUT, F, B, L>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
-    // (late variants: the host expects a late level -- TdArgs::late_ok; the
-    // device decides, and a late level in a plain variant stays exact)
-    const bool late = a.late_ok && a.level_direct;
+#define LAUNCH_TD_DEV(OUT, F, B) \
+  td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
     if (a.lists)
-      LAUNCH_TD_DEV(TdOut::Lists, false, false, false);
+      LAUNCH_TD_DEV(TdOut::Lists, false, false);
     else if (a.td_hub_vis && b32)
-      late ? LAUNCH_TD_DEV(TdOut::Dyn, true, true, true) : LAUNCH_TD_DEV(TdOut::Dyn, true, true, false);
+      LAUNCH_TD_DEV(TdOut::Dyn, true, true);
     else if (a.td_hub_vis)
-      late ? LAUNCH_TD_DEV(TdOut::Dyn, true, false, true) : LAUNCH_TD_DEV(TdOut::Dyn, true, false, false);
+      LAUNCH_TD_DEV(TdOut::Dyn, true, false);
     else if (b32)
-      late ? LAUNCH_TD_DEV(TdOut::Dyn, false, true, true) : LAUNCH_TD_DEV(TdOut::Dyn, false, true, false);
+      LAUNCH_TD_DEV(TdOut::Dyn, false, true);
     else
-      late ? LAUNCH_TD_DEV(TdOut::Dyn, false, false, true) : LAUNCH_TD_DEV(TdOut::Dyn, false, false, false);
+      LAUNCH_TD_DEV(TdOut::Dyn, false, false);
 #undef LAUNCH_TD_DEV
     return;
   }

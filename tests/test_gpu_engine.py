@@ -71,14 +71,12 @@ def test_uniform_and_isolated_source(gpu_runtime, mode):
 
 
 @pytest.mark.parametrize("mode", ["td", "do"])
-def test_all_reached_stop_and_late_levels(gpu_runtime, mode):
+def test_all_reached_stop(gpu_runtime, mode):
     """A connected graph (every vertex has an edge, one component): the device
     loop stops once every vertex with an edge is reached instead of expanding
-    the last frontier, and the late top-down levels (most of the graph
-    visited: claims by fetch-or, counted down, the grid stopping at zero)
-    leave exact levels, reached vertices, edges and depth -- uniform graphs
-    of mean degree 28 (the LiveJournal-sized shape, scaled down) and a
-    power-law one, 32-bit levels too."""
+    the last frontier; levels, reached vertices, edges and depth stay exact
+    -- a uniform graph of mean degree 28 (the LiveJournal-sized shape, scaled
+    down) and a power-law one, 32-bit levels too."""
     for p in (dbfs.uniform_params(300000, 4200000, 5), dbfs.power_law_params(300007, 4200000, 4000, 9)):
         csr = dbfs.host_csr_from_params(p)
         deg = np.diff(np.asarray(csr.row_off))

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Same-process A/B of top-down-only traversals with and without an engine
-option (default: late_levels), on the LiveJournal-sized uniform and power-law
-graphs and RMAT-22: GTEPS over K roots (alternating A/B passes, 3 each) and,
-for one root, the per-level device time of both.
+"""Same-process A/B of one engine option's two values on the LiveJournal-sized
+uniform and power-law graphs and RMAT-22 (top-down only by default): GTEPS
+over K roots (alternating A/B passes, 3 each), every root validated, and for
+one root the per-level device time (µs) of both.
 
-  python tools/td_late_ab.py --option late_levels --roots 16
+  python tools/td_option_ab.py --option td_hub_edges --a 4096 --b 0 --roots 16
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--option", default="late_levels")
+    ap.add_argument("--option", required=True)
     ap.add_argument("--a", type=float, default=1.0)
     ap.add_argument("--b", type=float, default=0.0)
     ap.add_argument("--roots", type=int, default=16)
