@@ -590,7 +590,7 @@ void DeviceLoop::emit_sparse(Chain& c) {
   const size_t lcap = static_cast<size_t>(c.cap > 0 ? c.cap : list_max_);
   const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
   sp.nranks = P_;
-  const int64_t apply_grid = std::max<int64_t>(1, std::min<int64_t>(opt_.td_sparse_grid, 128));
+  const int64_t apply_grid = std::max<int64_t>(1, opt_.td_apply_grid);
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)

@@ -75,6 +75,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_group_ticket") o.td_group_ticket = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
   else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
+  else if (name == "td_apply_grid") o.td_apply_grid = static_cast<int64_t>(v);
   else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
@@ -131,6 +132,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
           {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
+          {"td_apply_grid", static_cast<double>(o.td_apply_grid)},
           {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},

@@ -231,6 +231,9 @@ struct EngineOptions {
   // 0 disables.  td_sparse_grid: its workgroups.
   int64_t td_sparse_edges = int64_t(1) << 16;
   int64_t td_sparse_grid = 256;
+  // ... several ranks: the owners' side (td_sparse_apply) at most this many
+  // workgroups (only those with received ids take part)
+  int64_t td_apply_grid = 128;
   // A sparse chain stays live up to td_sparse_cap_factor x td_sparse_edges
   // frontier edges (0: any size); a larger level is re-enqueued dense.
   double td_sparse_cap_factor = 8.0;
