@@ -291,10 +291,15 @@ struct EngineOptions {
   // of RMAT-26 at P = 8: level 0 11-19 -> 6-10 us.)
   int64_t xfuse_edges = int64_t(1) << 12;
   // Several ranks, bottom-up levels: merge the gathered frontier into the
-  // replicated visited bitmap (the remote slices).  Only top-down levels read
-  // remote visited bits, as a filter: a stale one sends an id its owner drops,
-  // so the merge is not needed (off: validated as xfuse_edges).
-  bool bu_merge_visited = false;
+  // replicated visited bitmap (the remote slices; folded into hub_gather).
+  // Only top-down levels read remote visited bits, as a filter: a stale one
+  // sends an id its owner drops, so the levels stay exact without it -- but
+  // the top-down level after the bottom-up ones then claims and sends every
+  // remote target the bottom-up levels reached.  Shadow rank 0 of RMAT-26
+  // (profiles/r5_shadow_ab_merge_apply_grid.txt): that level 51-67 -> 21-24
+  // us at P = 2 for 3-5 us per bottom-up level; traversal -6.6 % at P = 2,
+  // -3.6 % at P = 8.
+  bool bu_merge_visited = true;
   // One rank, device loop, hubs: a first bottom-up level whose frontier has
   // at most bu_cut_edges edges outside the hubs claims those vertices'
   // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
