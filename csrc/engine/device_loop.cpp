@@ -590,7 +590,14 @@ void DeviceLoop::emit_sparse(Chain& c) {
   const size_t lcap = static_cast<size_t>(c.cap > 0 ? c.cap : list_max_);
   const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
   sp.nranks = P_;
-  const int64_t apply_grid = std::max<int64_t>(1, opt_.td_apply_grid);
+  // the owners' side sized by its expected ids (a rank receives about
+  // mf (P - 1) / P^2 claims): ~512 per workgroup, up to td_apply_grid -- the
+  // large levels' latency-bound claims spread over every CU, a tiny level's
+  // launch stays small
+  const double est_mf = c.mf_hint >= 0 ? c.mf_hint : static_cast<double>(c.cap > 0 ? c.cap : list_max_);
+  const double est_ids = est_mf * static_cast<double>(P_ - 1) / (static_cast<double>(P_) * P_);
+  const int64_t apply_grid =
+      std::max<int64_t>(1, std::min<int64_t>(opt_.td_apply_grid, static_cast<int64_t>(est_ids / 512.0) + 1));
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)

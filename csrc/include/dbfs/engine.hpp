@@ -232,8 +232,10 @@ struct EngineOptions {
   int64_t td_sparse_edges = int64_t(1) << 16;
   int64_t td_sparse_grid = 256;
   // ... several ranks: the owners' side (td_sparse_apply) at most this many
-  // workgroups (only those with received ids take part)
-  int64_t td_apply_grid = 128;
+  // workgroups (sized by the level's expected received ids, ~512 each; only
+  // those with ids take part).  Shadow rank 0 of RMAT-26 at P = 2, the 1.3
+  // M-edge sparse level: 128 workgroups 91 us, 512 81 us.
+  int64_t td_apply_grid = 512;
   // A sparse chain stays live up to td_sparse_cap_factor x td_sparse_edges
   // frontier edges (0: any size); a larger level is re-enqueued dense.
   double td_sparse_cap_factor = 8.0;
