@@ -280,6 +280,9 @@ class CpuBackend final : public Backend {
       const int64_t b = a.qscan[i], e = a.qscan[i + 1];
       for (int64_t k = b; k < e; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
+        // (the filter's clear bits are visited vertices: skipping on them
+        // changes nothing -- and catches a filter that drops an unvisited one)
+        if (a.unvis && !test_bit(a.unvis, unvis_index(v, a.unvis_mult))) continue;
         if (test_bit(a.visited, v)) continue;
         if (a.lists) {
           vid_t* list = a.lists + static_cast<int64_t>(v / a.part) * (a.list_cap + 1);
@@ -767,6 +770,15 @@ class CpuBackend final : public Backend {
         if (test_bit(a.visited, a.g.td_hub_vertex[w * 64 + b])) m |= 1ull << b;
       a.out[w] = m;
     }
+  }
+  void unvis_filter(const UnvisArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    std::fill(a.out, a.out + kUnvisWords, word_t(0));
+    for (int64_t v = 0; v < a.n; ++v)
+      if (!test_bit(a.visited, static_cast<vid_t>(v))) {
+        const uint32_t i = unvis_index(static_cast<uint64_t>(v), a.mult);
+        a.out[i >> 6] |= 1ull << (i & 63);
+      }
   }
   void row_heads(const eid_t* ro, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx) override {
     for (int64_t r = 0; r < rows; ++r) {

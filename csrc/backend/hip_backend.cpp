@@ -248,6 +248,7 @@ class HipBackend final : public Backend {
   void bu_cut_prep(const BuArgs& a) override { on(); kern::bu_cut_prep(a, st_); chk(); }
   void direct_prewait(const DirectExchange& x) override { on(); kern::direct_prewait(x, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
+  void unvis_filter(const UnvisArgs& a) override { on(); kern::unvis_filter(a, st_); chk(); }
   void hub_apply(const HubApplyArgs& a) override { on(); kern::hub_apply(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }

@@ -645,6 +645,11 @@ struct TdArgs {
   // no decode of the hub id) instead of a level byte store scattered over
   // the whole level array; hub_apply turns the marks into level bytes.
   uint8_t* td_hub_mark = nullptr;
+  // Unvisited filter (UnvisArgs, this level's snapshot): targets whose bit is
+  // clear are visited without a `visited` probe (device loop, Dyn output; a
+  // 1024-thread variant without the hub filter)
+  const word_t* unvis = nullptr;
+  uint64_t unvis_mult = 0;
   // Range-staged level (one rank, device loop, at most 2^32 adjacency
   // entries, rows in id order -- graph_sort's buckets for long rows): each
   // workgroup takes a contiguous run of edge blocks and sweeps the vertex
@@ -780,6 +785,33 @@ struct HubVisitedArgs {
   const LevelCtrl* ctrl = nullptr;
   int64_t min_edges = 0;
   double vis_frac = 0.0;  // as TdArgs::td_hub_vis_frac
+};
+
+// A dense top-down level's unvisited filter (this level's snapshot): bit i
+// is set iff some vertex v with unvis_index(v) == i is unvisited, where
+// unvis_index(v) = (v * mult) >> 32 maps the n vertices onto kUnvisBits bits
+// in contiguous runs (mult = unvis_mult(n): at most 2^32, identity for n <=
+// kUnvisBits).  td_expand (TdArgs::unvis) stages it in LDS and probes
+// `visited` only for targets whose filter bit is set: late levels, where most
+// targets are visited, trade most scattered L2 requests for LDS reads.
+// 8176 words: with td_expand's owner map two 1024-thread workgroups fill a
+// CU's 160 KiB of LDS.
+constexpr int64_t kUnvisWords = 8176;
+constexpr int64_t kUnvisBits = kUnvisWords * 64;
+DBFS_HD uint64_t unvis_mult(int64_t n) {
+  if (n <= kUnvisBits) return uint64_t(1) << 32;
+  return (static_cast<uint64_t>(kUnvisBits) << 32) / static_cast<uint64_t>(n);
+}
+DBFS_HD uint32_t unvis_index(uint64_t v, uint64_t mult) { return static_cast<uint32_t>((v * mult) >> 32); }
+// the first vertex with unvis_index >= i
+DBFS_HD uint64_t unvis_first(uint64_t i, uint64_t mult) { return ((i << 32) + mult - 1) / mult; }
+struct UnvisArgs {
+  const word_t* visited = nullptr;  // global (n bits)
+  int64_t n = 0;
+  uint64_t mult = 0;
+  word_t* out = nullptr;            // kUnvisWords
+  const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;               // chain predicate, as TdArgs::max_mf
 };
 
 // level8[td_hub_vertex[h]] = narrow_base + new_level
@@ -1032,6 +1064,7 @@ class Backend {
   // a GPU, Comm::split_waits): the consumer after it finds the cells tagged.
   virtual void direct_prewait(const DirectExchange& x) { (void)x; }
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
+  virtual void unvis_filter(const UnvisArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their
   // bounds, the first recorded violation (code << 48 | detail; 0: none;

@@ -179,6 +179,13 @@ struct EngineOptions {
   // a 17 M-edge level at 13 % visited 404 -> 273 us ranged, the 100 M-edge
   // level after it (86 %) 630 -> 1232 us (profiles/r4_s3_td_range_*).
   double td_range_vis_frac = 0.3;
+  // Dense top-down levels predicted at >= td_unvis_edges frontier edges that
+  // start with >= td_unvis_vis_frac of the adjacency visited test targets in
+  // an LDS unvisited filter first (UnvisArgs, TdArgs::unvis): a clear bit
+  // means visited, so only the rest cost a scattered `visited` probe.  0
+  // disables.
+  int64_t td_unvis_edges = int64_t(1) << 22;
+  double td_unvis_vis_frac = 0.6;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
@@ -385,6 +392,8 @@ struct ChainRecord {
   bool push = false;
   // one rank: a range-staged dense top-down chain (TdArgs::range_split)
   bool ranged = false;
+  // a dense top-down chain with the unvisited filter (TdArgs::unvis)
+  bool unvis = false;
 };
 
 struct RunResult {
@@ -473,7 +482,7 @@ class Engine {
   void ensure_wide_levels() const;
   // bitmap engine state
   bool bitmap_ready_ = false;
-  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_;
+  DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_, unvis_;
   DBuf<uint32_t> deg_all_;  // several ranks: every vertex's degree (InitRunArgs::deg_all)
   // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
   // decision and its ticket (zero between levels)

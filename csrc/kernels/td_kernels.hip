@@ -180,15 +180,20 @@ __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __re
 // bases in 32 bits (graphs of at most 2^32 adjacency entries): 16 instead of
 // 24 KiB of LDS per workgroup, 8 resident workgroups per CU instead of 6 (5
 // instead of 4 with the filter).
-template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false>
+// kUnvis: the unvisited-filter variant (TdArgs::unvis staged in LDS; 1024
+// threads, no hub filter, Dyn output): a target whose filter bit is clear is
+// visited, so only the others cost a `visited` probe.
+template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false, bool kUnvis = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
+  static_assert(!kUnvis || (!kFilter && kOut == TdOut::Dyn), "the unvisited filter replaces the hub filter");
   using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
   __shared__ int32_t s_owner[kTdEdgesPerBlock];
   __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
+  __shared__ word_t s_unvis[kUnvis ? kUnvisWords : 1];
   long long q = a.q, m = a.m;
   bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
   if (a.ctrl) {
@@ -222,6 +227,10 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     }
   }
   const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
+  // (td_block_owner_map starts with a barrier)
+  if constexpr (kUnvis)
+    if (blockIdx.x < nblocks) stage_words<kThreads, kUnvisWords>(s_unvis, a.unvis, kUnvisWords);
+  const uint64_t umult = a.unvis_mult;
 
   for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
     const long long e0 = b * kTdEdgesPerBlock;
@@ -231,6 +240,14 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
     vid_t vk[kItems];
     bool live[kItems], hubnew[kItems];
     td_load_items<kThreads, kHubFilter, kBase32>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis, vk, live, hubnew);
+    if constexpr (kUnvis) {
+      // filter bit clear: visited at the level's start -- no probe, no store
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) {
+        const uint32_t fi = unvis_index(vk[k], umult);
+        live[k] = live[k] && ((s_unvis[fi >> 6] >> (fi & 63)) & 1ull);
+      }
+    }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       DBFS_DCHECK(!live[k] || vk[k] < a.g.n, 2, vk[k]);
@@ -1287,6 +1304,48 @@ __global__ __launch_bounds__(kBlock) void hub_visited_kernel(HubVisitedArgs a) {
   if (lane_id() == 0 && w * kWave < a.g.td_nhubs) a.out[w] = m;
 }
 
+// UnvisArgs: a workgroup builds kUnvisChunk filter words in LDS from the
+// visited words of their vertex run (coalesced; one LDS atomic per unvisited
+// vertex and filter word its word's run touches), then stores them -- every
+// filter word written, nothing to clear between levels.
+constexpr int kUnvisChunk = 64;
+__global__ __launch_bounds__(kBlock) void unvis_filter_kernel(UnvisArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  __shared__ word_t s_f[kUnvisChunk];
+  const int t = threadIdx.x;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kUnvisChunk;
+  const int64_t w1 = min(w0 + kUnvisChunk, kUnvisWords);
+  if (t < kUnvisChunk) s_f[t] = 0ull;
+  __syncthreads();
+  const uint64_t n = static_cast<uint64_t>(a.n);
+  const uint64_t v0 = unvis_first(static_cast<uint64_t>(w0) * 64, a.mult);
+  const uint64_t v1 = min(n, unvis_first(static_cast<uint64_t>(w1) * 64, a.mult));
+  if (v0 < v1) {
+    const uint64_t j1 = (v1 - 1) >> 6;
+    for (uint64_t j = (v0 >> 6) + t; j <= j1; j += kBlock) {
+      word_t x = ~a.visited[j];
+      if (j == (v0 >> 6)) x &= ~0ull << (v0 & 63);
+      if (j == j1 && (v1 & 63)) x &= (1ull << (v1 & 63)) - 1;
+      int64_t cur = -1;
+      word_t acc = 0;
+      while (x) {
+        const uint64_t v = j * 64 + static_cast<uint64_t>(__builtin_ctzll(x));
+        x &= x - 1;
+        const int64_t i = static_cast<int64_t>(unvis_index(v, a.mult)) - w0 * 64;
+        if ((i >> 6) != cur) {
+          if (cur >= 0) atomicOr(&s_f[cur], acc);
+          cur = i >> 6;
+          acc = 0;
+        }
+        acc |= 1ull << (i & 63);
+      }
+      if (cur >= 0) atomicOr(&s_f[cur], acc);
+    }
+  }
+  __syncthreads();
+  if (t < w1 - w0) a.out[w0 + t] = s_f[t];
+}
+
 // HubApplyArgs: 16 marks per thread (kTdMaxHubs is a multiple of 16; the
 // marks past td_nhubs stay zero).
 __global__ __launch_bounds__(kBlock) void hub_apply_kernel(HubApplyArgs a) {
@@ -1329,12 +1388,12 @@ static void td_stats_report(hipStream_t st) {
 // workgroups that start when the first ones finish their strided share: with
 // 2048 workgroups and six resident per CU, RMAT-22 top-down 70 against 83
 // GTEPS at 1536.
-template <TdOut kOut, bool kFilter, bool kBase32>
+template <TdOut kOut, bool kFilter, bool kBase32, int kThreads = kTdThreads, bool kUnvis = false>
 unsigned td_resident_grid(int64_t cap) {
   static const int per_cu = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kTdThreads, kFilter, kBase32>,
-                                                     kTdThreads, 0) != hipSuccess || n <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, td_expand_kernel<kOut, kThreads, kFilter, kBase32, kUnvis>,
+                                                     kThreads, 0) != hipSuccess || n <= 0)
       n = 1;
     return n;
   }();
@@ -1364,7 +1423,15 @@ void td_expand(const TdArgs& a, hipStream_t st) {
     const int64_t fgrid = a.grid_filter > 0 ? a.grid_filter : a.grid;
 #define LAUNCH_TD_DEV(OUT, F, B) \
   td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
-    if (a.lists)
+    if (a.unvis && !a.lists) {
+      // (the hub filter's launches are not made with it)
+      if (b32)
+        td_expand_kernel<TdOut::Dyn, 1024, false, true, true>
+            <<<td_resident_grid<TdOut::Dyn, false, true, 1024, true>(a.grid), 1024, 0, st>>>(a);
+      else
+        td_expand_kernel<TdOut::Dyn, 1024, false, false, true>
+            <<<td_resident_grid<TdOut::Dyn, false, false, 1024, true>(a.grid), 1024, 0, st>>>(a);
+    } else if (a.lists)
       LAUNCH_TD_DEV(TdOut::Lists, false, false);
     else if (a.td_hub_vis && b32)
       LAUNCH_TD_DEV(TdOut::Dyn, true, true);
@@ -1468,6 +1535,11 @@ void direct_prewait(const DirectExchange& x, hipStream_t st) {
 void hub_visited(const HubVisitedArgs& a, hipStream_t st) {
   if (a.g.td_nhubs <= 0) return;
   hub_visited_kernel<<<grid_for((a.g.td_nhubs + kWave - 1) / kWave, kBlock / kWave), kBlock, 0, st>>>(a);
+}
+
+void unvis_filter(const UnvisArgs& a, hipStream_t st) {
+  DBFS_CHECK(a.mult == unvis_mult(a.n), "unvis_filter: multiplier of another vertex count");
+  unvis_filter_kernel<<<static_cast<unsigned>((kUnvisWords + kUnvisChunk - 1) / kUnvisChunk), kBlock, 0, st>>>(a);
 }
 
 void hub_apply(const HubApplyArgs& a, hipStream_t st) {

@@ -3,7 +3,8 @@
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
 collectives and bytes of a traversal can be predicted from its chains
-(``BFSResult.chains``: level, form, capacity, gather, pushed frontier, ranged)
+(``BFSResult.chains``: level, form, capacity, gather, pushed frontier, ranged,
+unvisited filter)
 and checked against the
 communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
 ``table`` turns a 1-GPU level profile into the per-level bytes / collectives

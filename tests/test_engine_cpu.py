@@ -708,6 +708,38 @@ def test_range_staged_top_down_levels_cpu(rt, words):
     assert ranged
 
 
+@pytest.mark.parametrize("n,m,mode", [(3000, 30000, "td"), (600011, 2400000, "td"), (600011, 2400000, "do")])
+def test_unvisited_filter_levels_cpu(n, m, mode):
+    """The unvisited filter (UnvisArgs, TdArgs::unvis) on the CPU backend:
+    forced on every dense top-down level (td_unvis_edges 1, any visited
+    fraction), the CPU expansion skips a target whose filter bit is clear --
+    so a filter bit lost for an unvisited vertex shows as a wrong level.
+    Identity mapping (n <= kUnvisBits) and the multiply-shift runs (n >
+    kUnvisBits, an n that is no power of two); one rank and 3 virtual ranks."""
+    from distributed_cuda_bfs_amd.parallel.runtime import run_virtual_ranks
+
+    p = dbfs.uniform_params(n, m, 17)
+    csr = dbfs.host_csr_from_params(p)
+    roots = [1, n // 3, n - 5]
+    exp = {s: dbfs.cpu_bfs(csr, s)[0] for s in roots}
+
+    def body(rt):
+        b = dbfs.BFS(p, rt, mode=mode)
+        b.engine.set_option("td_unvis_edges", 1)
+        b.engine.set_option("td_unvis_vis_frac", 0.0)
+        b.engine.set_option("td_range_edges", 0)
+        b.engine.set_option("td_sparse_edges", 0)
+        used = False
+        for s in roots:
+            r = b.run(s)
+            assert np.array_equal(b.levels(), exp[s]), (rt.rank, s)
+            used = used or any(c[6] for c in r.chains)
+        return used
+
+    for P in (1, 3):
+        assert all(run_virtual_ranks(P, body, device="cpu"))
+
+
 @pytest.mark.parametrize("P", [1, 3])
 def test_power_law_generator(P):
     """Chung-Lu power-law graphs (power_law_params): labels scrambled into

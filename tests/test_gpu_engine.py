@@ -90,6 +90,32 @@ def test_all_reached_stop(gpu_runtime, mode):
                 assert bfs.validate(s)
 
 
+@pytest.mark.parametrize("forced", [False, True])
+def test_unvisited_filter_gpu(gpu_runtime, forced):
+    """Dense top-down levels with the LDS unvisited filter (unvis_filter_kernel
+    + td_expand's kUnvis variant): exact levels, reached vertices and edges on
+    a uniform graph larger than the filter (multiply-shift runs), a power-law
+    one and RMAT-18 (32-bit levels too); by default on the late large levels
+    (a uniform graph of mean degree 28 has one), forced: every dense level."""
+    graphs = [dbfs.uniform_params(1500007, 21000000, 5), dbfs.power_law_params(600011, 8400000, 6000, 9),
+              dbfs.rmat_params(18, 16, 3)]
+    used = False
+    for p in graphs:
+        csr = dbfs.host_csr_from_params(p)
+        deg = np.diff(np.asarray(csr.row_off))
+        bfs = dbfs.BFS(p, gpu_runtime, mode="td")
+        if forced:
+            bfs.engine.set_option("td_unvis_edges", 1)
+            bfs.engine.set_option("td_unvis_vis_frac", 0.0)
+        for narrow in (1, 0):
+            bfs.engine.set_option("narrow_levels", narrow)
+            for s in (int(np.argmax(deg)), 12345):
+                res = _check(bfs, csr, s)
+                used = used or any(c[6] for c in res.chains)
+                assert bfs.validate(s)
+    assert used
+
+
 def test_hub_heavy_star(gpu_runtime):
     # one vertex with degree >> kTdEdgesPerBlock exercises multi-block hubs
     n = 50000
