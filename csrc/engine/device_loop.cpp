@@ -726,27 +726,33 @@ void DeviceLoop::emit_dense(Chain& c) {
     ta.ranges = e_.range_count_;
     ta.range_span = e_.range_span_;
   }
-  // late large levels: the unvisited filter (its 1024-thread variant has no
-  // hub filter)
+  // late large levels: the unvisited filter (launched next to the plain
+  // variant; the filter's density picks the one that runs)
   const bool unvis = !ranged && opt_.td_unvis_edges > 0 && c.mf_hint >= static_cast<double>(opt_.td_unvis_edges) &&
                      vis_hint_ >= opt_.td_unvis_vis_frac * static_cast<double>(e_.total_directed_);
   if (unvis) {
     res_.chains.back().unvis = true;
-    if (!e_.unvis_.data()) e_.unvis_ = DBuf<word_t>(be_, static_cast<size_t>(kUnvisWords));
+    if (!e_.unvis_.data()) {
+      e_.unvis_ = DBuf<word_t>(be_, static_cast<size_t>(kUnvisWords));
+      e_.unvis_pop_ = DBuf<uint32_t>(be_, static_cast<size_t>(kUnvisChunks));
+    }
     UnvisArgs uv;
     uv.visited = e_.visited_.data();
     uv.n = gv_.n;
     uv.mult = unvis_mult(gv_.n);
     uv.out = e_.unvis_.data();
+    uv.pop = e_.unvis_pop_.data();
     uv.ctrl = e_.ctrl_.data();
     uv.max_mf = 0;
     be_.unvis_filter(uv);
     ta.unvis = e_.unvis_.data();
     ta.unvis_mult = uv.mult;
+    ta.unvis_pop = uv.pop;
+    ta.unvis_max_density = opt_.td_unvis_max_density;
   }
   // (skipped for levels predicted well below the filter's threshold: the
   // snapshot kernel would only find its gate closed)
-  if (!ranged && !unvis && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 && e_.g_.td_hub_share() >= opt_.td_hub_min_share &&
+  if (!ranged && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 && e_.g_.td_hub_share() >= opt_.td_hub_min_share &&
       (c.mf_hint < 0 || c.mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
     // large levels: the hubs' visited bits, staged in LDS by td_expand
     if (!e_.td_hub_vis_.data())

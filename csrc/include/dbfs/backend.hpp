@@ -650,6 +650,11 @@ struct TdArgs {
   // 1024-thread variant without the hub filter)
   const word_t* unvis = nullptr;
   uint64_t unvis_mult = 0;
+  // ... its chunks' set bits (UnvisArgs::pop): the filter variant and the
+  // plain one are both launched, and the level runs in the filter variant
+  // iff at most unvis_max_density of the filter's bits are set
+  const uint32_t* unvis_pop = nullptr;
+  double unvis_max_density = 0.5;
   // Range-staged level (one rank, device loop, at most 2^32 adjacency
   // entries, rows in id order -- graph_sort's buckets for long rows): each
   // workgroup takes a contiguous run of edge blocks and sweeps the vertex
@@ -794,10 +799,13 @@ struct HubVisitedArgs {
 // kUnvisBits).  td_expand (TdArgs::unvis) stages it in LDS and probes
 // `visited` only for targets whose filter bit is set: late levels, where most
 // targets are visited, trade most scattered L2 requests for LDS reads.
-// 8176 words: with td_expand's owner map two 1024-thread workgroups fill a
-// CU's 160 KiB of LDS.
-constexpr int64_t kUnvisWords = 8176;
+// 6080 words: with td_expand's owner map of two edge blocks (kUnvisSpan) two
+// 1024-thread workgroups fill a CU's 160 KiB of LDS.  Built in chunks of 64
+// words (kUnvisChunks), each chunk's set bits counted (UnvisArgs::pop).
+constexpr int64_t kUnvisWords = 6080;
 constexpr int64_t kUnvisBits = kUnvisWords * 64;
+constexpr int kUnvisChunks = static_cast<int>(kUnvisWords / 64);
+constexpr int kUnvisSpan = 2;
 DBFS_HD uint64_t unvis_mult(int64_t n) {
   if (n <= kUnvisBits) return uint64_t(1) << 32;
   return (static_cast<uint64_t>(kUnvisBits) << 32) / static_cast<uint64_t>(n);
@@ -810,6 +818,7 @@ struct UnvisArgs {
   int64_t n = 0;
   uint64_t mult = 0;
   word_t* out = nullptr;            // kUnvisWords
+  uint32_t* pop = nullptr;          // kUnvisChunks: set bits per 64-word chunk
   const LevelCtrl* ctrl = nullptr;
   int64_t max_mf = 0;               // chain predicate, as TdArgs::max_mf
 };

@@ -186,6 +186,9 @@ struct EngineOptions {
   // disables.
   int64_t td_unvis_edges = int64_t(1) << 22;
   double td_unvis_vis_frac = 0.6;
+  // ... such a level runs with the filter iff at most this fraction of the
+  // filter's bits are set (decided on the device from the built filter)
+  double td_unvis_max_density = 0.5;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
@@ -483,6 +486,7 @@ class Engine {
   // bitmap engine state
   bool bitmap_ready_ = false;
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_, unvis_;
+  DBuf<uint32_t> unvis_pop_;
   DBuf<uint32_t> deg_all_;  // several ranks: every vertex's degree (InitRunArgs::deg_all)
   // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
   // decision and its ticket (zero between levels)

@@ -38,20 +38,24 @@ enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->b
 // edge + qbase).  Returns the block's edge count; ends with a barrier.
 // BaseT uint32_t: qbase kept modulo 2^32 (enough while the column array has
 // at most 2^32 entries: the column index is then (edge + qbase) mod 2^32).
-template <int kThreads, typename BaseT = long long>
+// kSpan > 1: super-block b of kSpan consecutive edge blocks (edges [b * kSpan
+// * EPB, ...), nblocks still counting edge blocks): s_owner / s_base hold
+// kSpan x EPB (+ 1) entries.
+template <int kThreads, typename BaseT = long long, int kSpan = 1>
 __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qscan, const int64_t* __restrict__ qbase,
                                                   const int32_t* __restrict__ blk_vstart, long long b,
                                                   long long nblocks, long long q, long long m, int32_t* s_owner,
                                                   BaseT* s_base, int32_t* s_wmax) {
-  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  constexpr int kEPB = kSpan * kTdEdgesPerBlock;
+  constexpr int kItems = kEPB / kThreads;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const int wv = t >> 6;
-  const long long e0 = b * kTdEdgesPerBlock;
-  const long long e1 = min(m, e0 + kTdEdgesPerBlock);
+  const long long e0 = b * kEPB;
+  const long long e1 = min(m, e0 + kEPB);
   const int cnt = static_cast<int>(e1 - e0);
-  const long long v0 = blk_vstart[b];
-  const long long vlast = (b + 1 < nblocks) ? blk_vstart[b + 1] : q - 1;
+  const long long v0 = blk_vstart[b * kSpan];
+  const long long vlast = (b * kSpan + kSpan < nblocks) ? blk_vstart[b * kSpan + kSpan] : q - 1;
   const int nv = static_cast<int>(vlast - v0 + 1);
 
   // Invariant (zero-degree vertices are never listed): nv <= EPB + 1.  Every
@@ -59,7 +63,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
   // vertices -- a sparse level's tail -- covers up to EPB + 1 entries, which
   // a strided loop fetched one dependent round trip after another), in
   // flight across the barriers of the owner map's zeroing.
-  constexpr int kMapIter = (kTdEdgesPerBlock + kThreads) / kThreads;
+  constexpr int kMapIter = (kEPB + kThreads) / kThreads;
   long long qs[kMapIter];
   BaseT qb[kMapIter];
 #pragma unroll
@@ -67,7 +71,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
     const int i = t + k * kThreads;
     qs[k] = 0;
     qb[k] = 0;
-    if (i < nv && i <= kTdEdgesPerBlock) {
+    if (i < nv && i <= kEPB) {
       qs[k] = qscan[v0 + i];
       qb[k] = static_cast<BaseT>(qbase[v0 + i]);
     }
@@ -79,7 +83,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
 #pragma unroll
   for (int k = 0; k < kMapIter; ++k) {
     const int i = t + k * kThreads;
-    if (i < nv && i <= kTdEdgesPerBlock) {
+    if (i < nv && i <= kEPB) {
       s_base[i] = qb[k];
       const long long p = (qs[k] > e0 ? qs[k] : e0) - e0;
       if (p < cnt) s_owner[p] = i;
@@ -185,15 +189,20 @@ __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __re
 // visited, so only the others cost a `visited` probe.
 template <TdOut kOut, int kThreads, bool kFilter = false, bool kBase32 = false, bool kUnvis = false>
 __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
-  constexpr int kItems = kTdEdgesPerBlock / kThreads;
+  // (the filter variant takes two edge blocks per step: its LDS allows two
+  // workgroups per CU, so each keeps twice the edges in flight)
+  constexpr int kSpan = kUnvis ? kUnvisSpan : 1;
+  constexpr int kEPB = kSpan * kTdEdgesPerBlock;
+  constexpr int kItems = kEPB / kThreads;
   constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
   static_assert(!kUnvis || (!kFilter && kOut == TdOut::Dyn), "the unvisited filter replaces the hub filter");
   using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
-  __shared__ int32_t s_owner[kTdEdgesPerBlock];
-  __shared__ BaseT s_base[kTdEdgesPerBlock + 1];
+  __shared__ int32_t s_owner[kEPB];
+  __shared__ BaseT s_base[kEPB + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
   __shared__ word_t s_unvis[kUnvis ? kUnvisWords : 1];
+  __shared__ int s_unvis_on;
   long long q = a.q, m = a.m;
   bool bytes = kOut == TdOut::Bytes, check = a.check_visited;
   if (a.ctrl) {
@@ -211,9 +220,23 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
       }
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+  const long long nsteps = (nblocks + kSpan - 1) / kSpan;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const word_t* __restrict__ visited = a.visited;
+  // a level with an unvisited filter (TdArgs::unvis_pop) runs in exactly one
+  // of the two variants launched for it: the filter one if the filter's set
+  // bits are at most unvis_max_density of them, else the plain one
+  if (a.unvis_pop) {
+    if (t < kWave) {
+      long long c = 0;
+      for (int i = t; i < kUnvisChunks; i += kWave) c += a.unvis_pop[i];
+      c = wave_sum(c);
+      if (t == 0) s_unvis_on = static_cast<double>(c) <= a.unvis_max_density * static_cast<double>(kUnvisBits) ? 1 : 0;
+    }
+    __syncthreads();
+    if ((s_unvis_on != 0) != kUnvis) return;
+  }
   // large levels: hub targets tested in an LDS copy of the hubs' visited bits
   // (uniform: every workgroup sees the same m)
   bool filter = false;
@@ -229,17 +252,18 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
   // (td_block_owner_map starts with a barrier)
   if constexpr (kUnvis)
-    if (blockIdx.x < nblocks) stage_words<kThreads, kUnvisWords>(s_unvis, a.unvis, kUnvisWords);
+    if (blockIdx.x < nsteps) stage_words<kThreads, kUnvisWords>(s_unvis, a.unvis, kUnvisWords);
   const uint64_t umult = a.unvis_mult;
 
-  for (long long b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    const long long e0 = b * kTdEdgesPerBlock;
-    const int cnt = td_block_owner_map<kThreads, BaseT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m, s_owner,
-                                                        s_base, s_wmax);
+  for (long long b = blockIdx.x; b < nsteps; b += gridDim.x) {
+    const long long e0 = b * kEPB;
+    const int cnt = td_block_owner_map<kThreads, BaseT, kSpan>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m,
+                                                               s_owner, s_base, s_wmax);
 
     vid_t vk[kItems];
     bool live[kItems], hubnew[kItems];
-    td_load_items<kThreads, kHubFilter, kBase32>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis, vk, live, hubnew);
+    td_load_items<kThreads, kHubFilter, kBase32, BaseT, kItems>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis,
+                                                                vk, live, hubnew);
     if constexpr (kUnvis) {
       // filter bit clear: visited at the level's start -- no probe, no store
 #pragma unroll
@@ -1343,7 +1367,15 @@ __global__ __launch_bounds__(kBlock) void unvis_filter_kernel(UnvisArgs a) {
     }
   }
   __syncthreads();
-  if (t < w1 - w0) a.out[w0 + t] = s_f[t];
+  if (t < kWave) {
+    long long c = 0;
+    if (t < w1 - w0) {
+      a.out[w0 + t] = s_f[t];
+      c = __popcll(s_f[t]);
+    }
+    c = wave_sum(c);
+    if (t == 0 && a.pop) a.pop[blockIdx.x] = static_cast<uint32_t>(c);
+  }
 }
 
 // HubApplyArgs: 16 marks per thread (kTdMaxHubs is a multiple of 16; the
@@ -1424,14 +1456,17 @@ void td_expand(const TdArgs& a, hipStream_t st) {
 #define LAUNCH_TD_DEV(OUT, F, B) \
   td_expand_kernel<OUT, kTdThreads, F, B><<<td_resident_grid<OUT, F, B>(F ? fgrid : a.grid), kTdThreads, 0, st>>>(a)
     if (a.unvis && !a.lists) {
-      // (the hub filter's launches are not made with it)
+      // the filter variant, then the plain one: the level runs in one of
+      // them (the filter's density, read by both)
+      DBFS_CHECK(a.unvis_pop, "td_expand: an unvisited filter without its chunk counts");
       if (b32)
         td_expand_kernel<TdOut::Dyn, 1024, false, true, true>
             <<<td_resident_grid<TdOut::Dyn, false, true, 1024, true>(a.grid), 1024, 0, st>>>(a);
       else
         td_expand_kernel<TdOut::Dyn, 1024, false, false, true>
             <<<td_resident_grid<TdOut::Dyn, false, false, 1024, true>(a.grid), 1024, 0, st>>>(a);
-    } else if (a.lists)
+    }
+    if (a.lists)
       LAUNCH_TD_DEV(TdOut::Lists, false, false);
     else if (a.td_hub_vis && b32)
       LAUNCH_TD_DEV(TdOut::Dyn, true, true);
@@ -1539,7 +1574,8 @@ void hub_visited(const HubVisitedArgs& a, hipStream_t st) {
 
 void unvis_filter(const UnvisArgs& a, hipStream_t st) {
   DBFS_CHECK(a.mult == unvis_mult(a.n), "unvis_filter: multiplier of another vertex count");
-  unvis_filter_kernel<<<static_cast<unsigned>((kUnvisWords + kUnvisChunk - 1) / kUnvisChunk), kBlock, 0, st>>>(a);
+  static_assert(kUnvisChunk == kWave, "a chunk's words are one wave's");
+  unvis_filter_kernel<<<static_cast<unsigned>(kUnvisChunks), kBlock, 0, st>>>(a);
 }
 
 void hub_apply(const HubApplyArgs& a, hipStream_t st) {
