@@ -13,6 +13,7 @@
 // The reference's host loop (bfs.cu:569-620, bfs_mpi.cu:581-632) launches,
 // synchronises, copies and reads managed counters once per level.
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -73,6 +74,7 @@ class DeviceLoop {
   bool lists_unlimited_ = false, counted_ = false;
   bool range_ok_ = false;  // one rank: range-staged top-down levels available
   double vis_hint_ = -1.0;  // the next enqueued level's visited degree sum at its start (< 0 unknown)
+  double reach_hint_ = -1.0;  // ... and its reached vertices with an edge (< 0 unknown)
   int bin_shift_ = 12;
   int64_t nbins_ = 0;
   bool binned_ = false;
@@ -728,8 +730,17 @@ void DeviceLoop::emit_dense(Chain& c) {
   }
   // late large levels: the unvisited filter (launched next to the plain
   // variant; the filter's density picks the one that runs)
-  const bool unvis = !ranged && opt_.td_unvis_edges > 0 && c.mf_hint >= static_cast<double>(opt_.td_unvis_edges) &&
-                     vis_hint_ >= opt_.td_unvis_vis_frac * static_cast<double>(e_.total_directed_);
+  // (and, with the count of vertices with an edge known, a filter expected
+  // at most 1.5 x td_unvis_max_density dense: u of the vertices unvisited,
+  // n / kUnvisBits per bit -- so a hub-heavy level whose visited edges are
+  // many but whose unvisited vertices are too launches nothing extra)
+  bool unvis = !ranged && opt_.td_unvis_edges > 0 && c.mf_hint >= static_cast<double>(opt_.td_unvis_edges) &&
+               vis_hint_ >= opt_.td_unvis_vis_frac * static_cast<double>(e_.total_directed_);
+  if (unvis && e_.n_active_ > 0 && reach_hint_ >= 0) {
+    const double u = std::max(0.0, static_cast<double>(e_.n_active_) - reach_hint_) / static_cast<double>(gv_.n);
+    const double per_bit = std::max(1.0, static_cast<double>(gv_.n) / static_cast<double>(kUnvisBits));
+    unvis = 1.0 - std::pow(1.0 - std::min(u, 1.0), per_bit) <= 1.5 * opt_.td_unvis_max_density;
+  }
   if (unvis) {
     res_.chains.back().unvis = true;
     if (!e_.unvis_.data()) {
@@ -1100,6 +1111,7 @@ RunResult DeviceLoop::run() {
       int64_t cap = 0;
       const char f = actual == 'B' ? 'B' : td_form(L, static_cast<double>(mf), &cap, true);
       vis_hint_ = static_cast<double>(mb->vis_deg);  // (exact: level L's start)
+      reach_hint_ = static_cast<double>(mb->reached);
       enqueue_level(L, f, cap, static_cast<double>(mf), d1 == 'B');
     }
     prev_nf = nf;
@@ -1107,6 +1119,7 @@ RunResult DeviceLoop::run() {
     int64_t lcap = 0;
     const char f = d1 == 'B' ? 'B' : td_form(L + 1, emf, &lcap, false);
     vis_hint_ = static_cast<double>(mb->vis_deg) + emf;  // (level L + 1's frontier joins visited)
+    reach_hint_ = static_cast<double>(mb->reached) + enf;
     enqueue_level(L + 1, f, lcap, emf, d2 == 'B');
   }
   // The traversal is complete once the last stamp is seen: the stamping

@@ -727,6 +727,7 @@ def test_unvisited_filter_levels_cpu(n, m, mode):
         b = dbfs.BFS(p, rt, mode=mode)
         b.engine.set_option("td_unvis_edges", 1)
         b.engine.set_option("td_unvis_vis_frac", 0.0)
+        b.engine.set_option("td_unvis_max_density", 1.0)
         b.engine.set_option("td_range_edges", 0)
         b.engine.set_option("td_sparse_edges", 0)
         used = False

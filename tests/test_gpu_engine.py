@@ -107,6 +107,7 @@ def test_unvisited_filter_gpu(gpu_runtime, forced):
         if forced:
             bfs.engine.set_option("td_unvis_edges", 1)
             bfs.engine.set_option("td_unvis_vis_frac", 0.0)
+            bfs.engine.set_option("td_unvis_max_density", 1.0)
         for narrow in (1, 0):
             bfs.engine.set_option("narrow_levels", narrow)
             for s in (int(np.argmax(deg)), 12345):
