@@ -61,12 +61,16 @@ def main() -> int:
             res = bfs.run(roots[len(roots) // 2])
             bfs.engine.phase_timing = False
             levels[side] = [[lv["dir"], round(lv["ms"] * 1e3, 1), int(lv.get("frontier", -1))] for lv in res.levels]
+            # chains: level, form, ranged (R) / unvisited filter (U) flags
+            rec[side + "_chains"] = " ".join(f"{c[0]}{c[1]}{'R' if c[5] else ''}{'U' if c[6] else ''}"
+                                             for c in res.chains)
             rec[side + "_valid"] = ok
         rec["levels_us"] = levels
         out[name] = rec
         print(f"{name} {args.mode} {args.option}={args.a}: {rec['a']} GTEPS  {args.option}={args.b}: {rec['b']} "
               f"valid {rec['a_valid']}/{rec['b_valid']}", flush=True)
         print(f"  levels a: {levels['a']}\n  levels b: {levels['b']}", flush=True)
+        print(f"  chains a: {rec['a_chains']}\n  chains b: {rec['b_chains']}", flush=True)
         del bfs
     if args.json:
         with open(args.json, "w") as f:
