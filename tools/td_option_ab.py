@@ -34,7 +34,7 @@ def main() -> int:
     rt = init_runtime(args.device)
     n, m, dmax = dbfs.ops.graph.LJ_SIZED_POWER_LAW
     graphs = {"lj": dbfs.uniform_params(n, m, 101), "lj_pl": dbfs.power_law_params(n, m, dmax, 201),
-              "r22": dbfs.rmat_params(22, 16, 1)}
+              "r22": dbfs.rmat_params(22, 16, 1), "r26": dbfs.rmat_params(26, 16, 1)}
     out = {}
     for name in args.graphs.split(","):
         bfs = dbfs.BFS(graphs[name], rt, mode=args.mode)
