@@ -1063,53 +1063,21 @@ RunResult DeviceLoop::run() {
     const char f0 = init_.dir == 'B' ? 'B' : td_form(0, 0.0, &cap0, false);
     enqueue_level(0, f0, cap0, -1.0, init_.dir == 'B');
   }
-  // The seed's stamp computed on the host (EngineOptions::host_seed): the
-  // same level_ctrl_finish the init kernel runs, from the source's degree --
-  // level 1's chain then follows level 0's at once; the real stamp is checked
-  // against it when level 0's arrives.
-  LevelMailbox pre{};
-  bool pre_ok = false;
-  if (opt_.device_loop_predict && opt_.host_seed && !e_.host_deg_.empty()) {
-    const int64_t d = e_.host_deg_[static_cast<size_t>(src_)];
-    LevelCtrl c = init_;
-    level_ctrl_finish(c, d > 0 ? 1 : 0, d, true, nullptr);
-    if (!c.done) {
-      pre.level = -1;
-      pre.done = c.done;
-      pre.vis_deg = c.vis_deg;
-      pre.next_dir = c.dir;
-      pre.n_f = c.n_f;
-      pre.m_f = c.m_f;
-      pre.reached = c.reached;
-      pre_ok = true;
-    }
-  }
   for (int L = 0;; ++L) {
     if (!opt_.device_loop_predict) {
       // dense top-down or bottom-up, one more level ahead
       enqueue_level(L + 1, enq_dir_[L], 0, -1.0, enq_dir_[L] == 'B');
     }
     const volatile LevelMailbox* mb = nullptr;
-    if (L == 0 && pre_ok) {
-      mb = &pre;
-    } else {
-      try {
-        mb = wait_stamp(L - 1);
-      } catch (const Error& err) {
-        // which level, and the chains enqueued so far (level, form, cap)
-        std::string chains;
-        for (const auto& ch : res_.chains) chains += " " + std::to_string(ch.level) + ch.form + ":" + std::to_string(ch.cap);
-        throw Error(std::string(err.what()) + " (waiting for level " + std::to_string(L - 1) + "; chains" + chains + ")");
-      }
-      if (ht_) hmark("stamp " + std::to_string(L - 1));
+    try {
+      mb = wait_stamp(L - 1);
+    } catch (const Error& err) {
+      // which level, and the chains enqueued so far (level, form, cap)
+      std::string chains;
+      for (const auto& ch : res_.chains) chains += " " + std::to_string(ch.level) + ch.form + ":" + std::to_string(ch.cap);
+      throw Error(std::string(err.what()) + " (waiting for level " + std::to_string(L - 1) + "; chains" + chains + ")");
     }
-    if (L == 1 && pre_ok) {
-      // (the seed's stamp precedes level 0's: its slot holds it by now)
-      const volatile LevelMailbox* s = e_.mailbox_host_ + slot(-1);
-      DBFS_CHECK(s->level == -1 && s->done == pre.done && s->next_dir == pre.next_dir && s->n_f == pre.n_f &&
-                     s->m_f == pre.m_f && s->vis_deg == pre.vis_deg && s->reached == pre.reached,
-                 "device loop: the seed's stamp differs from the host's (host_seed)");
-    }
+    if (ht_) hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {
       nlev = L;
       break;

@@ -61,7 +61,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
   else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
-  else if (name == "host_seed") o.host_seed = v != 0;
   else if (name == "device_loop_ranks") o.device_loop_ranks = v != 0;
   else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "directed") o.directed = v != 0;
@@ -122,7 +121,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
           {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
-          {"host_seed", o.host_seed ? 1.0 : 0.0},
           {"device_loop_ranks", o.device_loop_ranks ? 1.0 : 0.0},
           {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"directed", o.directed ? 1.0 : 0.0},
@@ -683,21 +681,6 @@ void Engine::alloc_bitmap_state() {
     be_.degrees_u32(g_.view().row_off, g_.rows(), mine.data());
     comm_.allgather(mine.data(), deg_all_.data(), static_cast<size_t>(part_.part) * sizeof(uint32_t));
     be_.synchronize();
-  }
-  // the host's copy of every vertex's degree (EngineOptions::host_seed): a
-  // run's seed totals known before its first kernel
-  host_deg_.clear();
-  const int64_t nall = static_cast<int64_t>(part_.nranks) * part_.part;
-  if (nall <= (int64_t(1) << 30)) {
-    host_deg_.resize(static_cast<size_t>(nall));
-    if (exchange()) {
-      be_.to_host(host_deg_.data(), deg_all_.data(), host_deg_.size() * sizeof(uint32_t));
-    } else {
-      DBuf<uint32_t> d(be_, static_cast<size_t>(part_.part));
-      be_.memset_async(d.data(), 0, d.bytes());
-      be_.degrees_u32(g_.view().row_off, g_.rows(), d.data());
-      be_.to_host(host_deg_.data(), d.data(), d.bytes());
-    }
   }
   be_.synchronize();
   bitmap_ready_ = true;

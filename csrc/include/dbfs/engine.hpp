@@ -231,12 +231,6 @@ struct EngineOptions {
   // ... enqueueing each level with an extrapolated direction prediction (else:
   // the previous level's direction, one more level ahead).
   bool device_loop_predict = true;
-  // ... and the seed's totals computed on the host from a host copy of every
-  // vertex's degree (4 B per vertex, graphs of at most 2^30 vertices), so
-  // level 1's chain is enqueued right behind level 0's instead of after the
-  // seed's stamp (a run's first levels are tiny: the GPU otherwise waits for
-  // the host's enqueue)
-  bool host_seed = true;
   // Host loop (several ranks, or device_loop off): read each level's totals
   // through a device-mapped mailbox the host spins on, instead of a D2H copy
   // plus a stream synchronisation.
@@ -494,7 +488,6 @@ class Engine {
   DBuf<word_t> visited_, zdeg_, frontier_[2], next_, recv_, cand_, hub_front_, td_hub_vis_, unvis_;
   DBuf<uint32_t> unvis_pop_;
   DBuf<uint32_t> deg_all_;  // several ranks: every vertex's degree (InitRunArgs::deg_all)
-  std::vector<uint32_t> host_deg_;  // every vertex's degree, host copy (EngineOptions::host_seed)
   // hub-cut bottom-up levels: per-workgroup frontier hub degrees, the
   // decision and its ticket (zero between levels)
   DBuf<int64_t> cut_part_;
