@@ -24,6 +24,8 @@ def main() -> int:
     ap.add_argument("--roots", type=int, default=16)
     ap.add_argument("--mode", default="td")
     ap.add_argument("--graphs", default="lj,lj_pl,r22")
+    ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
+                    help="an engine option set on both sides")
     ap.add_argument("--device", default="hip")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
@@ -38,6 +40,9 @@ def main() -> int:
     out = {}
     for name in args.graphs.split(","):
         bfs = dbfs.BFS(graphs[name], rt, mode=args.mode)
+        for kv in args.set:
+            k, v = kv.split("=", 1)
+            bfs.engine.set_option(k, float(v))
         roots = bfs.sample_roots(args.roots, seed=7)
         rec = {"a": [], "b": []}
         for _ in range(3):
