@@ -979,6 +979,30 @@ def test_peer_comm_four_ranks_share_one_gpu_rmat20():
     assert rec["heldout"]["validated_roots"] == "8/8"
 
 
+def test_peer_comm_eight_ranks_share_one_gpu():
+    """The driver's 8-rank shape over the peer-memory transport, rehearsed
+    with eight self-spawned processes on device 0 (RMAT-19): the 16-peer
+    tables, 8-way owner lists, pushed frontier slices and folded level ends
+    at P = 8, every timed and held-out root validated."""
+    import json
+    import sys
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="8", DBFS_PEER_FRONTIER_MB="2",
+               DBFS_COMM_TIMEOUT_S="30")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "8", "--scale", "19", "--steps", "4",
+           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "8", "--secondary", "none"]
+    out = _run_group(cmd, env, 140)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["comm"] == "peer+tcp" and rec["n_gpus"] == 8 and rec["comm_direct"] is True
+    topo = rec["comm_topology"]
+    assert topo["shared_device"] is True and topo["self_test"] == "ok" and len(topo["peer_access"]) == 8
+    assert rec["validated"] is True and rec["validated_roots"] == "4/4"
+    assert rec["heldout"]["validated_roots"] == "8/8"
+
+
 def test_peer_fused_forms_two_ranks_share_one_gpu():
     """The separate-GPU forms of the peer transport -- every collective one
     fused launch, the direct exchanges' waits inside their consumer kernels

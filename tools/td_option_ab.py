@@ -22,6 +22,7 @@ def main() -> int:
     ap.add_argument("--a", type=float, default=1.0)
     ap.add_argument("--b", type=float, default=0.0)
     ap.add_argument("--roots", type=int, default=16)
+    ap.add_argument("--root-seed", type=int, default=7)
     ap.add_argument("--mode", default="td")
     ap.add_argument("--graphs", default="lj,lj_pl,r22")
     ap.add_argument("--set", action="append", default=[], metavar="NAME=VALUE",
@@ -43,7 +44,7 @@ def main() -> int:
         for kv in args.set:
             k, v = kv.split("=", 1)
             bfs.engine.set_option(k, float(v))
-        roots = bfs.sample_roots(args.roots, seed=7)
+        roots = bfs.sample_roots(args.roots, seed=args.root_seed)
         rec = {"a": [], "b": []}
         for _ in range(3):
             for side, v in (("a", args.a), ("b", args.b)):
