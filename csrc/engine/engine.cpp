@@ -72,26 +72,18 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bits") o.td_sparse_bits = v != 0;
   else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
-  else if (name == "td_group_ticket") o.td_group_ticket = v != 0;
   else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
-  else if (name == "td_sparse_grid") o.td_sparse_grid = static_cast<int64_t>(v);
-  else if (name == "td_apply_grid") o.td_apply_grid = static_cast<int64_t>(v);
-  else if (name == "td_direct") o.td_direct = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
-  else if (name == "fold_scan") o.fold_scan = v != 0;
-  else if (name == "td_hub_min_share") o.td_hub_min_share = v;
   else if (name == "td_range_edges") o.td_range_edges = static_cast<int64_t>(v);
   else if (name == "td_range_words") o.td_range_words = static_cast<int64_t>(v);
   else if (name == "td_range_vis_frac") o.td_range_vis_frac = v;
-  else if (name == "td_bin_log2_bins") o.td_bin_log2_bins = static_cast<int64_t>(v);
   else if (name == "td_unvis_edges") o.td_unvis_edges = static_cast<int64_t>(v);
   else if (name == "td_unvis_vis_frac") o.td_unvis_vis_frac = v;
   else if (name == "td_unvis_max_density") o.td_unvis_max_density = v;
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
-  else if (name == "td_sparse_cap_factor") o.td_sparse_cap_factor = v;
   else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
   else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
@@ -130,28 +122,20 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"td_sparse_bits", o.td_sparse_bits ? 1.0 : 0.0},
           {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
-          {"td_group_ticket", o.td_group_ticket ? 1.0 : 0.0},
           {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
           {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
-          {"td_sparse_grid", static_cast<double>(o.td_sparse_grid)},
-          {"td_apply_grid", static_cast<double>(o.td_apply_grid)},
-          {"td_direct", o.td_direct ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
-          {"fold_scan", o.fold_scan ? 1.0 : 0.0},
-          {"td_hub_min_share", o.td_hub_min_share},
           {"td_range_edges", static_cast<double>(o.td_range_edges)},
           {"td_range_words", static_cast<double>(o.td_range_words)},
           {"td_range_vis_frac", o.td_range_vis_frac},
-          {"td_bin_log2_bins", static_cast<double>(o.td_bin_log2_bins)},
           {"td_unvis_edges", static_cast<double>(o.td_unvis_edges)},
           {"td_unvis_vis_frac", o.td_unvis_vis_frac},
           {"td_unvis_max_density", o.td_unvis_max_density},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
-          {"td_sparse_cap_factor", o.td_sparse_cap_factor},
           {"td_grid_max", static_cast<double>(o.td_grid_max)},
           {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},

@@ -139,7 +139,7 @@ struct EngineOptions {
   // to clear; the update reads the level bytes back) -- cheaper than the
   // candidate bitmap's memory-side atomics from ~64 K edges (RMAT-26: a
   // 1.7 M-edge level 115 -> 68 us).  Replaces td_byte_edges there.
-  bool td_direct = true;
+  static constexpr bool td_direct = true;
   int64_t td_direct_edges = int64_t(1) << 16;
   // Device loop, one rank: top-down levels predicted to have at least this
   // many frontier edges run binned (BinArgs: targets binned by vertex range,
@@ -160,7 +160,7 @@ struct EngineOptions {
   // kBinMaxBins; each bin's visited slice must fit LDS).  RMAT-26, the 28 M-edge
   // binned level: 256 / 512 / 1024 bins 407 / 417 / 441 us (more bins: the
   // fill pass scatters into more open lines).
-  int64_t td_bin_log2_bins = 8;
+  static constexpr int64_t td_bin_log2_bins = 8;
   // One rank, graphs of at most kRangeMax x kRangeWords x 64 vertices with
   // id-ordered rows: dense top-down levels predicted at >= td_range_edges
   // frontier edges are range-staged (TdArgs::range_split: the vertex ranges
@@ -204,7 +204,7 @@ struct EngineOptions {
   double td_hub_vis_frac = 0.0;
   // ... only on graphs whose top-down hubs hold at least this share of the
   // adjacency entries (DeviceGraph::td_hub_share)
-  double td_hub_min_share = 0.0;
+  static constexpr double td_hub_min_share = 0.0;
   // Direct-level top-down: hub targets claimed as one byte per hub (an
   // L2-resident 128 KiB array) and turned into level bytes after the
   // expansion (TdArgs::td_hub_mark, hub_apply).
@@ -240,15 +240,15 @@ struct EngineOptions {
   // handed to the next level) instead of compact + td_expand + update + scan;
   // 0 disables.  td_sparse_grid: its workgroups.
   int64_t td_sparse_edges = int64_t(1) << 16;
-  int64_t td_sparse_grid = 256;
+  static constexpr int64_t td_sparse_grid = 256;
   // ... several ranks: the owners' side (td_sparse_apply) at most this many
   // workgroups (sized by the level's expected received ids, ~512 each; only
   // those with ids take part).  Shadow rank 0 of RMAT-26 at P = 2, the 1.3
   // M-edge sparse level: 128 workgroups 91 us, 512 81 us.
-  int64_t td_apply_grid = 512;
+  static constexpr int64_t td_apply_grid = 512;
   // A sparse chain stays live up to td_sparse_cap_factor x td_sparse_edges
   // frontier edges (0: any size); a larger level is re-enqueued dense.
-  double td_sparse_cap_factor = 8.0;
+  static constexpr double td_sparse_cap_factor = 8.0;
   // Device loop: workgroups of the dense top-down expansion grid (at most;
   // they stride over the level's edge blocks; the launcher also caps the grid
   // at the kernel's residency), without and with the hub filter.  Measured:
@@ -283,10 +283,10 @@ struct EngineOptions {
   // ... and on graphs of at most kFoldScanUnits 4096-vertex units (2^25
   // vertices) its last workgroup also scans the unit prefixes the next
   // compaction reads (UpdateArgs::fold_scan): one launch less per dense level
-  bool fold_scan = true;
+  static constexpr bool fold_scan = true;
   // ... with a two-level ticket (UpdateArgs::group_ticket): the update runs
   // a full grid (up to kMaxFusedGrid workgroups) instead of kMaxFusedGrid / 8.
-  bool td_group_ticket = true;
+  static constexpr bool td_group_ticket = true;
   // Device loop, several ranks: sparse top-down levels (td_sparse with owner
   // lists, the lists exchanged count-sized, td_sparse_apply on the owners)
   // for levels predicted at <= xsparse_edges global frontier edges; such a

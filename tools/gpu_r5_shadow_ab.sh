@@ -2,7 +2,7 @@
 # OPTSETS: ";"-separated sets of space-separated NAME=VALUE (empty set: defaults).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 T=${TAG:-r5a}
-IFS=';' read -ra sets <<< "${OPTSETS:-;td_apply_grid=512;bu_merge_visited=1}"
+IFS=";" read -ra sets <<< "${OPTSETS:-;bu_merge_visited=0}"
 for P in ${PS:-2 8}; do
   i=0
   for set in "${sets[@]}"; do
