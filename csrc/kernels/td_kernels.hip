@@ -154,7 +154,7 @@ __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __re
       ci = static_cast<uint32_t>(static_cast<uint32_t>(e0 + idx) + s_base[s_owner[idx]]);
     else
       ci = e0 + idx + s_base[s_owner[idx]];
-    vk[k] = idx < cnt ? col[ci] : 0u;
+    vk[k] = idx < cnt ? __builtin_nontemporal_load(col + ci) : 0u;
     live[k] = idx < cnt;
     hubnew[k] = false;
   }
