@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kRangeThreads, 2 * kRangeThreads / 256) void td_ran
 #pragma unroll
         for (int k = 0; k < kRangeItems; ++k) {
           const int idx = k * kRangeThreads + t;
-          v[k] = idx < cnt ? col[static_cast<uint32_t>(w0 + idx) + s_cs[s_owner[idx]]] : 0u;
+          v[k] = idx < cnt ? __builtin_nontemporal_load(col + (static_cast<uint32_t>(w0 + idx) + s_cs[s_owner[idx]])) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < kRangeItems; ++k) {
