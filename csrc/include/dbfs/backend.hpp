@@ -799,10 +799,11 @@ struct HubVisitedArgs {
 // kUnvisBits).  td_expand (TdArgs::unvis) stages it in LDS and probes
 // `visited` only for targets whose filter bit is set: late levels, where most
 // targets are visited, trade most scattered L2 requests for LDS reads.
-// 6080 words: with td_expand's owner map of two edge blocks (kUnvisSpan) two
-// 1024-thread workgroups fill a CU's 160 KiB of LDS.  Built in chunks of 64
-// words (kUnvisChunks), each chunk's set bits counted (UnvisArgs::pop).
-constexpr int64_t kUnvisWords = 6080;
+// 7104 words: with td_expand's owner map of two edge blocks (kUnvisSpan,
+// 16-bit entries) two 1024-thread workgroups fill a CU's 160 KiB of LDS.
+// Built in chunks of 64 words (kUnvisChunks), each chunk's set bits counted
+// (UnvisArgs::pop).
+constexpr int64_t kUnvisWords = 7104;
 constexpr int64_t kUnvisBits = kUnvisWords * 64;
 constexpr int kUnvisChunks = static_cast<int>(kUnvisWords / 64);
 constexpr int kUnvisSpan = 2;

@@ -41,11 +41,14 @@ enum class TdOut { Bits, Bytes, Lists, Dyn };  // Dyn: bits or bytes per ctrl->b
 // kSpan > 1: super-block b of kSpan consecutive edge blocks (edges [b * kSpan
 // * EPB, ...), nblocks still counting edge blocks): s_owner / s_base hold
 // kSpan x EPB (+ 1) entries.
-template <int kThreads, typename BaseT = long long, int kSpan = 1>
+// OwnerT: int32_t, or uint16_t where LDS is tight (entries <= kSpan x EPB + 1
+// < 2^16).
+template <int kThreads, typename BaseT = long long, int kSpan = 1, typename OwnerT = int32_t>
 __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qscan, const int64_t* __restrict__ qbase,
                                                   const int32_t* __restrict__ blk_vstart, long long b,
-                                                  long long nblocks, long long q, long long m, int32_t* s_owner,
+                                                  long long nblocks, long long q, long long m, OwnerT* s_owner,
                                                   BaseT* s_base, int32_t* s_wmax) {
+  static_assert(sizeof(OwnerT) >= 4 || kSpan * kTdEdgesPerBlock < 65535, "owner map entries fit OwnerT");
   constexpr int kEPB = kSpan * kTdEdgesPerBlock;
   constexpr int kItems = kEPB / kThreads;
   const int t = threadIdx.x;
@@ -86,7 +89,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
     if (i < nv && i <= kEPB) {
       s_base[i] = qb[k];
       const long long p = (qs[k] > e0 ? qs[k] : e0) - e0;
-      if (p < cnt) s_owner[p] = i;
+      if (p < cnt) s_owner[p] = static_cast<OwnerT>(i);
     }
   }
   __syncthreads();
@@ -95,7 +98,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
   int run = 0;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    run = max(run, s_owner[t * kItems + k]);
+    run = max(run, static_cast<int>(s_owner[t * kItems + k]));
     vals[k] = run;
   }
   const int incl = wave_incl_max(run);
@@ -106,7 +109,7 @@ __device__ __forceinline__ int td_block_owner_map(const int64_t* __restrict__ qs
   const int prev = __shfl_up(incl, 1, kWave);
   const int excl = lane > 0 ? max(carry, prev) : carry;
 #pragma unroll
-  for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = max(vals[k], excl);
+  for (int k = 0; k < kItems; ++k) s_owner[t * kItems + k] = static_cast<OwnerT>(max(vals[k], excl));
   __syncthreads();
   return cnt;
 }
@@ -140,9 +143,10 @@ __device__ unsigned long long g_td_stats[4];
 // level's start, no global visited probe needed).  (Measured: claiming hubs
 // in LDS as well, to store each once per workgroup, is slower -- few repeats
 // per workgroup, LDS atomics on popular hubs serialise.)
-template <int kThreads, bool kHubFilter, bool kBase32, typename BaseT, int kItems = kTdEdgesPerBlock / kThreads>
+template <int kThreads, bool kHubFilter, bool kBase32, typename BaseT, int kItems = kTdEdgesPerBlock / kThreads,
+          typename OwnerT = int32_t>
 __device__ __forceinline__ void td_load_items(const TdArgs& a, const vid_t* __restrict__ col, long long e0, int cnt,
-                                              const int32_t* s_owner, const BaseT* s_base, bool filter,
+                                              const OwnerT* s_owner, const BaseT* s_base, bool filter,
                                               const word_t* s_hubvis, vid_t (&vk)[kItems], bool (&live)[kItems],
                                               bool (&hubnew)[kItems]) {
   const int t = threadIdx.x;
@@ -197,7 +201,9 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   constexpr bool kHubFilter = kFilter && kOut != TdOut::Lists && kThreads == kTdThreads;
   static_assert(!kUnvis || (!kFilter && kOut == TdOut::Dyn), "the unvisited filter replaces the hub filter");
   using BaseT = std::conditional_t<kBase32, uint32_t, long long>;
-  __shared__ int32_t s_owner[kEPB];
+  // (the filter variant's owner map in 16 bits: 8 KiB more for the filter)
+  using OwnerT = std::conditional_t<kUnvis, uint16_t, int32_t>;
+  __shared__ OwnerT s_owner[kEPB];
   __shared__ BaseT s_base[kEPB + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ word_t s_hubvis[kHubFilter ? kTdMaxHubs / kWordBits : 1];
@@ -257,13 +263,13 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 
   for (long long b = blockIdx.x; b < nsteps; b += gridDim.x) {
     const long long e0 = b * kEPB;
-    const int cnt = td_block_owner_map<kThreads, BaseT, kSpan>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q, m,
-                                                               s_owner, s_base, s_wmax);
+    const int cnt = td_block_owner_map<kThreads, BaseT, kSpan, OwnerT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q,
+                                                                       m, s_owner, s_base, s_wmax);
 
     vid_t vk[kItems];
     bool live[kItems], hubnew[kItems];
-    td_load_items<kThreads, kHubFilter, kBase32, BaseT, kItems>(a, col, e0, cnt, s_owner, s_base, filter, s_hubvis,
-                                                                vk, live, hubnew);
+    td_load_items<kThreads, kHubFilter, kBase32, BaseT, kItems, OwnerT>(a, col, e0, cnt, s_owner, s_base, filter,
+                                                                        s_hubvis, vk, live, hubnew);
     if constexpr (kUnvis) {
       // filter bit clear: visited at the level's start -- no probe, no store
 #pragma unroll
