@@ -39,6 +39,13 @@ class CpuBackend final : public Backend {
   void* alloc(size_t bytes) override {
     void* p = std::aligned_alloc(64, round_up(std::max<size_t>(bytes, 64), 64));
     if (!p) raise_error(__FILE__, __LINE__, "host allocation failed");
+    // DBFS_POISON_ALLOC=<byte>: as the HIP backend's (memory never written
+    // reads as that byte instead of whatever the allocator hands back)
+    static const int poison = [] {
+      const char* e = std::getenv("DBFS_POISON_ALLOC");
+      return e && *e ? static_cast<int>(std::strtol(e, nullptr, 0)) & 0xff : -1;
+    }();
+    if (poison >= 0) std::memset(p, poison, round_up(std::max<size_t>(bytes, 64), 64));
     return p;
   }
   void dealloc(void* p) override { std::free(p); }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -88,6 +89,17 @@ class HipBackend final : public Backend {
     void* p = nullptr;
     if (bytes == 0) bytes = 64;
     HIP_CHECK(hipMalloc(&p, bytes));
+    // DBFS_POISON_ALLOC=<byte>: every allocation filled with that byte (a
+    // debugging aid -- a read of memory never written shows up as a wrong
+    // result in a fresh process too, not only after freed memory is reused)
+    static const int poison = [] {
+      const char* e = std::getenv("DBFS_POISON_ALLOC");
+      return e && *e ? static_cast<int>(std::strtol(e, nullptr, 0)) & 0xff : -1;
+    }();
+    if (poison >= 0) {
+      HIP_CHECK(hipMemsetAsync(p, poison, bytes, st_));
+      HIP_CHECK(hipStreamSynchronize(st_));
+    }
     return p;
   }
   void dealloc(void* p) override {

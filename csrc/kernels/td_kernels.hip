@@ -886,12 +886,8 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       const int idx = k * kThreads + t;
       v[k] = idx < cnt ? col[e0 + idx + s_base[s_owner[idx]]] : 0u;
     }
-    // (few vertices visited yet -- LevelCtrl::check_visited off: an early
-    // level's targets are mostly new, and the pre-read only delays the claim)
-    const bool check = a.ctrl->check_visited != 0;
 #pragma unroll
-    for (int k = 0; k < kItems; ++k)
-      seen[k] = k * kThreads + t < cnt ? (check ? a.visited[v[k] >> 6] : 0ull) : ~0ull;
+    for (int k = 0; k < kItems; ++k) seen[k] = k * kThreads + t < cnt ? a.visited[v[k] >> 6] : ~0ull;
     unsigned claimed = 0;  // bit k: item k claimed by this lane
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
