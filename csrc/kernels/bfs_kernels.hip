@@ -255,26 +255,43 @@ __device__ __forceinline__ void store_unit_stats(const UpdateArgs& a, int64_t un
 
 // The fused finish's unit prefixes (UpdateArgs::fold_scan; every thread of the
 // last workgroup of kBlock threads): unit_cnt / unit_deg become the exclusive
-// prefixes over all units (at most kFoldScanUnits, a run of kFold per thread)
-// and the chunk prefixes part_cnt / part_deg zero -- what scan_units_kernel
-// leaves for the compaction.  Two passes over the run (sums, then prefixes:
-// the second pass's loads are L2 hits), a few units in flight at a time: the
-// update kernel's register allocation covers this code too.
+// prefixes over all units (at most kFoldScanUnits) and the chunk prefixes
+// part_cnt / part_deg zero -- what scan_units_kernel leaves for the
+// compaction.  The units are spread over all kBlock threads (a run of
+// ceil(nunits / kBlock) each) and a run's agent-scope loads go out kFoldRun at
+// a time: each batch is one round trip to memory (the stats were stored
+// write-through by other XCDs' waves), so a run of up to kFoldRun units -- 2048
+// units, a 2^23-vertex shard -- costs one round trip, its values kept in
+// registers for the second pass.  (The first version gave each thread a run of
+// kFoldScanUnits / kBlock units, four loads in flight: on a 2048-unit shard one
+// wave made 16 dependent round trips -- the P = 8 post-bottom-up update 39.4 ->
+// 33.8 us, RMAT-22 top-down only +2 %, profiles/r5_fold_scan_ab.txt.)
 __device__ __forceinline__ long long agent_load_i64(const int64_t* p) {
   return static_cast<long long>(
       __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+constexpr int kFoldRun = 8;
 __device__ __forceinline__ void fold_unit_scan(const ScanArgs& a) {
-  constexpr int kFold = kFoldScanUnits / kBlock;
   __shared__ long long s_fc[kBlock / kWave], s_fd[kBlock / kWave];
   const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
-  const int64_t u0 = static_cast<int64_t>(t) * kFold;
-  const int64_t u1 = min(u0 + kFold, static_cast<int64_t>(a.nunits));
+  const int64_t n = a.nunits;
+  const int64_t per = (n + kBlock - 1) / kBlock;
+  const int64_t u0 = min(static_cast<int64_t>(t) * per, n);
+  const int64_t u1 = min(u0 + per, n);
+  long long c[kFoldRun], d[kFoldRun];
   long long sc = 0, sd = 0;
-#pragma unroll 4
-  for (int64_t u = u0; u < u1; ++u) {
-    sc += agent_load_i64(a.unit_cnt + u);
-    sd += agent_load_i64(a.unit_deg + u);
+  for (int64_t b = u0; b < u1; b += kFoldRun) {
+#pragma unroll
+    for (int k = 0; k < kFoldRun; ++k) {
+      const bool in = b + k < u1;
+      c[k] = in ? agent_load_i64(a.unit_cnt + b + k) : 0ll;
+      d[k] = in ? agent_load_i64(a.unit_deg + b + k) : 0ll;
+    }
+#pragma unroll
+    for (int k = 0; k < kFoldRun; ++k) {
+      sc += c[k];
+      sd += d[k];
+    }
   }
   const long long ic = wave_incl_scan(sc), id = wave_incl_scan(sd);
   __syncthreads();  // (s_fc / s_fd: the caller's earlier LDS use is done)
@@ -288,13 +305,25 @@ __device__ __forceinline__ void fold_unit_scan(const ScanArgs& a) {
     oc += s_fc[k];
     od += s_fd[k];
   }
-#pragma unroll 4
-  for (int64_t u = u0; u < u1; ++u) {
-    const long long c = agent_load_i64(a.unit_cnt + u), d = agent_load_i64(a.unit_deg + u);
-    a.unit_cnt[u] = oc;
-    a.unit_deg[u] = od;
-    oc += c;
-    od += d;
+  for (int64_t b = u0; b < u1; b += kFoldRun) {
+    if (per > kFoldRun) {
+      // (a longer run: the batch again -- the registers hold the last one)
+#pragma unroll
+      for (int k = 0; k < kFoldRun; ++k) {
+        const bool in = b + k < u1;
+        c[k] = in ? agent_load_i64(a.unit_cnt + b + k) : 0ll;
+        d[k] = in ? agent_load_i64(a.unit_deg + b + k) : 0ll;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kFoldRun; ++k) {
+      if (b + k < u1) {
+        a.unit_cnt[b + k] = oc;
+        a.unit_deg[b + k] = od;
+      }
+      oc += c[k];
+      od += d[k];
+    }
   }
   for (int64_t p = t; p * kScanChunk < a.nunits; p += kBlock) {
     a.part_cnt[p] = 0;

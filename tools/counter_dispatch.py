@@ -28,7 +28,8 @@ def load(run_dir, kernel):
     for r in csv.DictReader(open(kt[0])):
         d = int(r["Dispatch_Id"])
         dur[d] = (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    rows = [(dur[d][0], d, dur[d][1], counters[d]) for d in counters if kernel in names[d] and d in dur]
+    rows = [(dur[d][0], d, dur[d][1], counters[d], names[d]) for d in counters
+            if kernel in names[d] and d in dur]
     rows.sort()
     return rows
 
@@ -37,16 +38,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--top", type=int, default=6)
+    ap.add_argument("--timeline", type=int, default=0,
+                    help="instead: the last N dispatches in time order (GRBM_GUI_ACTIVE / duration = clock)")
     ap.add_argument("dirs", nargs="+")
     a = ap.parse_args()
     passes = [load(d, a.kernel) for d in a.dirs]
+    if a.timeline:
+        rows = passes[0][-a.timeline:]
+        t0 = rows[0][0]
+        for start, d, us, c, name in rows:
+            mhz = c.get("GRBM_GUI_ACTIVE", 0) / us if us else 0
+            extra = " ".join(f"{k}={v:.4g}" for k, v in sorted(c.items()) if k != "GRBM_GUI_ACTIVE")
+            print(f"{(start - t0) / 1e3:9.1f} {us:7.1f} us {mhz:7.0f} MHz  {name.split('(')[0][-36:]:36s} {extra}")
+        return
     n = min(len(p) for p in passes)
     merged = []
     for i in range(n):
         c = {}
         for p in passes:
             c.update(p[i][3])
-        merged.append((passes[0][i][2], c))
+        merged.append((passes[0][i][2], c))  # (start, id, us, counters, name)
     merged.sort(key=lambda x: -x[0])
     keys = sorted({k for _, c in merged for k in c})
     print("us".rjust(8), *[k[:16].rjust(16) for k in keys])
