@@ -283,8 +283,12 @@ class CpuBackend final : public Backend {
         for (int64_t i = 0; i < q; ++i)
           a.clear_frontier[a.clear_qv[i] >> 6] = 0;
     }
+    // a split level's part (TdArgs::split_k): its run of the level's edges
+    const int64_t m = a.ctrl ? a.dev_stats[1] : a.m;
+    const int64_t e_lo = a.split_k > 1 ? m * a.split_i / a.split_k : 0;
+    const int64_t e_hi = a.split_k > 1 ? m * (a.split_i + 1) / a.split_k : m;
     for (int64_t i = 0; i < q; ++i) {
-      const int64_t b = a.qscan[i], e = a.qscan[i + 1];
+      const int64_t b = std::max(a.qscan[i], e_lo), e = std::min(a.qscan[i + 1], e_hi);
       for (int64_t k = b; k < e; ++k) {
         const vid_t v = a.g.col[k + a.qbase[i]];
         // (the filter's clear bits are visited vertices: skipping on them
@@ -767,6 +771,16 @@ class CpuBackend final : public Backend {
       const vid_t v = a.g.td_hub_vertex[h];
       a.level8[v] = static_cast<uint8_t>(a.narrow_base + a.new_level);
       a.mark[h] = 0;
+    }
+  }
+  void refresh_visited(const RefreshArgs& a) override {
+    if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+    const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
+    for (int64_t w = 0; w < a.words; ++w) {
+      word_t m = 0;
+      for (int b = 0; b < 64; ++b)
+        if (a.level8[w * 64 + b] == lv) m |= 1ull << b;
+      a.visited[w] |= m;
     }
   }
   void hub_visited(const HubVisitedArgs& a) override {

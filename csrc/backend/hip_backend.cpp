@@ -262,6 +262,7 @@ class HipBackend final : public Backend {
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
   void unvis_filter(const UnvisArgs& a) override { on(); kern::unvis_filter(a, st_); chk(); }
   void hub_apply(const HubApplyArgs& a) override { on(); kern::hub_apply(a, st_); chk(); }
+  void refresh_visited(const RefreshArgs& a) override { on(); kern::refresh_visited(a, st_); chk(); }
   void status_expand(const StatusArgs& a) override { on(); kern::status_expand(a, st_); chk(); }
   void bitmap_or(word_t* d, const word_t* s, int64_t w) override { on(); kern::bitmap_or(d, s, w, st_); chk(); }
   void ref_expand(const RefExpandArgs& a) override { on(); kern::ref_expand(a, st_); chk(); }

@@ -797,7 +797,37 @@ void DeviceLoop::emit_dense(Chain& c) {
       ta.td_hub_mark = e_.td_hub_mark_.data();
     }
   }
-  be_.td_expand(ta);
+  // large level-byte levels (one rank): the level in parts, the claims so far
+  // ORed into visited between them (Options::td_split_edges)
+  // (not with the unvisited filter: a late level claims few vertices, and
+  // every part would stage the filter and launch both variants again --
+  // RMAT-22's level 4 87 -> 134 us in 4 parts)
+  const int parts = (ta.level_direct && !ranged && !unvis && !xc_ && opt_.td_split_edges > 0 && opt_.td_split_parts > 1 &&
+                     c.mf_hint >= static_cast<double>(opt_.td_split_edges))
+                        ? opt_.td_split_parts
+                        : 1;
+  if (parts > 1) {
+    res_.chains.back().split = parts;
+    RefreshArgs ra;
+    ra.level8 = ta.level_direct;
+    ra.narrow_base = ta.narrow_base;
+    ra.new_level = ta.new_level;
+    ra.visited = e_.visited_.data();
+    ra.words = GW_;
+    ra.ctrl = e_.ctrl_.data();
+    ra.max_mf = ta.max_mf;
+    ta.split_k = parts;
+    for (int i = 0; i < parts; ++i) {
+      ta.split_i = i;
+      be_.td_expand(ta);
+      // (the input list's frontier words cleared, the level stamped: once)
+      ta.clear_qv = nullptr;
+      ta.clear_frontier = nullptr;
+      if (i + 1 < parts) be_.refresh_visited(ra);
+    }
+  } else {
+    be_.td_expand(ta);
+  }
   if (ta.td_hub_mark) {
     HubApplyArgs ha;
     ha.g = gv_;
@@ -830,7 +860,9 @@ void DeviceLoop::emit_dense(Chain& c) {
     tu.cand = e_.recv_.data();
     tu.cand_bytes = nullptr;
   }
-  tu.force = false;
+  // (a split level: visited already holds the earlier parts' claims -- every
+  // level byte of this level is a new vertex, as every `next` bit is)
+  tu.force = parts > 1;
   tu.frontier = fr_own(c.cur ^ 1);
   tu.new_level = L + 1;
   tu.ctrl = e_.ctrl_.data();

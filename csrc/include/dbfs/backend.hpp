@@ -685,6 +685,24 @@ struct TdArgs {
   // global frontier edges ctrl->m_f <= max_mf (= list_cap: no list can
   // overflow, every rank decides alike); else a no-op the host re-enqueues.
   int64_t max_mf = 0;
+  // Split level (one rank, level_direct): this launch runs part split_i of
+  // split_k equal runs of the level's edge blocks; between parts
+  // refresh_visited ORs the vertices claimed so far into `visited`, so a
+  // later part's probes skip them instead of storing their level byte again.
+  int split_k = 1, split_i = 0;
+};
+
+// A split top-down level (TdArgs::split_k): visited |= the vertices whose level
+// byte is narrow_base + new_level (claimed by the parts so far).  words:
+// visited words (level8 holds 64 x words bytes).
+struct RefreshArgs {
+  const uint8_t* level8 = nullptr;
+  uint8_t narrow_base = 0;
+  lvl_t new_level = 0;
+  word_t* visited = nullptr;
+  int64_t words = 0;
+  const LevelCtrl* ctrl = nullptr;
+  int64_t max_mf = 0;  // chain predicate, as TdArgs::max_mf
 };
 
 // Received candidate lists (nranks lists of list_cap + 1 words, count first)
@@ -1076,6 +1094,7 @@ class Backend {
   virtual void hub_visited(const HubVisitedArgs& a) = 0;
   virtual void unvis_filter(const UnvisArgs& a) = 0;
   virtual void hub_apply(const HubApplyArgs& a) = 0;
+  virtual void refresh_visited(const RefreshArgs& a) = 0;
   // Device-checked build (make checked): whether the kernels verify their
   // bounds, the first recorded violation (code << 48 | detail; 0: none;
   // synchronises, clears), and a hook recording violation 99 (fault tests).

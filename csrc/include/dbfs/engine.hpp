@@ -189,6 +189,13 @@ struct EngineOptions {
   // ... such a level runs with the filter iff at most this fraction of the
   // filter's bits are set (decided on the device from the built filter)
   double td_unvis_max_density = 0.5;
+  // One rank, level-byte (level_direct) top-down levels predicted at >=
+  // td_split_edges frontier edges run in td_split_parts parts, the claims of
+  // the parts so far ORed into `visited` between them (refresh_visited): a
+  // target reached by many frontier edges stores its level byte about once
+  // per part instead of once per edge.  0 disables.
+  int64_t td_split_edges = int64_t(1) << 23;
+  int td_split_parts = 4;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.
@@ -397,6 +404,8 @@ struct ChainRecord {
   bool ranged = false;
   // a dense top-down chain with the unvisited filter (TdArgs::unvis)
   bool unvis = false;
+  // ... run in this many parts (TdArgs::split_k; 1: whole)
+  int split = 1;
 };
 
 struct RunResult {

@@ -862,6 +862,18 @@ __global__ __launch_bounds__(kBlock) void copy_pieces_kernel(Backend::CopyPieces
     d[k] = s[k];
 }
 
+// RefreshArgs (a split top-down level): the claims of the parts so far into
+// visited -- a word per thread, its 64 level bytes in four 16-byte loads.
+__global__ __launch_bounds__(kBlock) void refresh_visited_kernel(RefreshArgs a) {
+  if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;
+  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; w < a.words; w += stride) {
+    const word_t m = gather_level_bits(a.level8 + w * 64, lv);
+    if (m) a.visited[w] |= m;
+  }
+}
+
 }  // namespace
 
 void fill_level(lvl_t* level, int64_t n, lvl_t value, hipStream_t st) {
@@ -912,6 +924,11 @@ void update_frontier(const UpdateArgs& a, hipStream_t st) {
   else if (split) update_kernel<true, false><<<grid, kBlock, 0, st>>>(a);
   else if (ranks) update_kernel<false, true><<<grid, kBlock, 0, st>>>(a);
   else update_kernel<false, false><<<grid, kBlock, 0, st>>>(a);
+}
+
+void refresh_visited(const RefreshArgs& a, hipStream_t st) {
+  if (a.words <= 0) return;
+  refresh_visited_kernel<<<grid_for(a.words, kBlock, 4 * device_cus()), kBlock, 0, st>>>(a);
 }
 
 void totals_finish(const ScanArgs& a, hipStream_t st) { totals_finish_kernel<<<1, kScanChunk, 0, st>>>(a); }

@@ -45,6 +45,7 @@ void bu_cut_prep(const BuArgs& a, hipStream_t st);
 void hub_visited(const HubVisitedArgs& a, hipStream_t st);
 void unvis_filter(const UnvisArgs& a, hipStream_t st);
 void hub_apply(const HubApplyArgs& a, hipStream_t st);
+void refresh_visited(const RefreshArgs& a, hipStream_t st);
 // device-checked build (DBFS_CHECKED): whether checks are compiled in, the
 // first recorded violation (code << 48 | detail, 0: none; cleared), and a
 // test hook recording code 99

@@ -227,6 +227,9 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   }
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   const long long nsteps = (nblocks + kSpan - 1) / kSpan;
+  // a split level's part (TdArgs::split_k): its run [s_lo, s_hi) of the steps
+  const long long s_lo = a.split_k > 1 ? nsteps * a.split_i / a.split_k : 0;
+  const long long s_hi = a.split_k > 1 ? nsteps * (a.split_i + 1) / a.split_k : nsteps;
   const int t = threadIdx.x;
   const int lane = lane_id();
   const word_t* __restrict__ visited = a.visited;
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   // (uniform: every workgroup sees the same m)
   bool filter = false;
   if constexpr (kHubFilter) {
-    filter = a.td_hub_vis && a.g.td_col && m >= a.td_hub_min_edges && blockIdx.x < nblocks &&
+    filter = a.td_hub_vis && a.g.td_col && m >= a.td_hub_min_edges && blockIdx.x < s_hi - s_lo &&
              (!a.ctrl || static_cast<double>(a.ctrl->vis_deg) >= a.td_hub_vis_frac * a.ctrl->total_directed);
     if (filter) {
       const int64_t hw = (a.g.td_nhubs + kWordBits - 1) / kWordBits;
@@ -258,10 +261,10 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   const vid_t* __restrict__ col = filter ? a.g.td_col : a.g.col;
   // (td_block_owner_map starts with a barrier)
   if constexpr (kUnvis)
-    if (blockIdx.x < nsteps) stage_words<kThreads, kUnvisWords>(s_unvis, a.unvis, kUnvisWords);
+    if (blockIdx.x < s_hi - s_lo) stage_words<kThreads, kUnvisWords>(s_unvis, a.unvis, kUnvisWords);
   const uint64_t umult = a.unvis_mult;
 
-  for (long long b = blockIdx.x; b < nsteps; b += gridDim.x) {
+  for (long long b = s_lo + blockIdx.x; b < s_hi; b += gridDim.x) {
     const long long e0 = b * kEPB;
     const int cnt = td_block_owner_map<kThreads, BaseT, kSpan, OwnerT>(a.qscan, a.qbase, a.blk_vstart, b, nblocks, q,
                                                                        m, s_owner, s_base, s_wmax);

@@ -766,3 +766,28 @@ def test_power_law_generator(P):
     for rank_out in outs:
         for lv, s in zip(rank_out, srcs):
             assert np.array_equal(lv, _oracle(csr, s))
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_split_levels_cpu(parts, mode):
+    """Split top-down levels (TdArgs::split_k, refresh_visited) on the CPU
+    backend: every level-byte top-down level of at least one frontier edge
+    forced into `parts` parts, the claims so far ORed into visited between
+    them and the update taking every level byte as new -- levels exact against
+    the oracle, and the chain records show the split."""
+    p = dbfs.rmat_params(14, 16, 23)
+    csr = dbfs.host_csr_from_params(p)
+    roots = [0, 77, 9000]
+    b = dbfs.BFS(p, init_runtime("cpu"), mode=mode)
+    b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+    b.engine.set_option("td_split_edges", 1)
+    b.engine.set_option("td_split_parts", parts)
+    b.engine.set_option("td_range_edges", 0)
+    b.engine.set_option("td_sparse_edges", 0)
+    used = False
+    for s in roots:
+        r = b.run(s)
+        assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
+        used = used or any(c[7] == parts for c in r.chains)
+    assert used

@@ -1353,3 +1353,26 @@ def test_peer_direct_frontier(opts):
     rec = _bench_peer(args, DBFS_PEER_SLOT_MB="16")
     assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
     assert rec["pushed_chains"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 4])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_split_levels_gpu(gpu_runtime, parts, mode):
+    """Split top-down levels on the GPU (TdArgs::split_k: each part a run of
+    the edge steps, refresh_visited between parts, the update forced): every
+    level-byte top-down level split, levels exact against the oracle."""
+    p = dbfs.rmat_params(18, 16, 23)
+    csr = dbfs.host_csr_from_params(p)
+    b = dbfs.BFS(p, gpu_runtime, mode=mode)
+    b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+    b.engine.set_option("td_split_edges", 1)
+    b.engine.set_option("td_split_parts", parts)
+    b.engine.set_option("td_range_edges", 0)
+    b.engine.set_option("td_sparse_edges", 0)
+    used = False
+    for s in b.sample_roots(4, seed=3):
+        r = b.run(s)
+        assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
+        used = used or any(c[7] == parts for c in r.chains)
+    assert used

@@ -68,7 +68,7 @@ def main() -> int:
             bfs.engine.phase_timing = False
             levels[side] = [[lv["dir"], round(lv["ms"] * 1e3, 1), int(lv.get("frontier", -1))] for lv in res.levels]
             # chains: level, form, ranged (R) / unvisited filter (U) flags
-            rec[side + "_chains"] = " ".join(f"{c[0]}{c[1]}{'R' if c[5] else ''}{'U' if c[6] else ''}"
+            rec[side + "_chains"] = " ".join(f"{c[0]}{c[1]}{'R' if c[5] else ''}{'U' if c[6] else ''}{'/%d' % c[7] if c[7] > 1 else ''}"
                                              for c in res.chains)
             rec[side + "_valid"] = ok
         rec["levels_us"] = levels
