@@ -855,14 +855,8 @@ void DeviceLoop::emit_dense(Chain& c) {
     comm_.alltoall(e_.next_.data(), e_.recv_.data(), static_cast<size_t>(W_) * sizeof(word_t));
     // (`next` re-zeroed by the update, which runs after the exchange: on a
     // no-op chain nothing wrote it)
-    if (opt_.x_zero_fill) {
-      // (one 16-byte-store fill after the exchange instead of 8-byte stores
-      // of every slice in the update)
-      be_.memset_async(e_.next_.data(), 0, e_.next_.bytes());
-    } else {
-      tu.zero_next = e_.next_.data();
-      tu.zero_slices = P_;
-    }
+    tu.zero_next = e_.next_.data();
+    tu.zero_slices = P_;
     tu.cand = e_.recv_.data();
     tu.cand_bytes = nullptr;
   }

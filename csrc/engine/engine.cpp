@@ -83,7 +83,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_unvis_max_density") o.td_unvis_max_density = v;
   else if (name == "td_split_edges") o.td_split_edges = static_cast<int64_t>(v);
   else if (name == "td_split_parts") o.td_split_parts = std::max(1, static_cast<int>(v));
-  else if (name == "x_zero_fill") o.x_zero_fill = v != 0;
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
   else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
@@ -138,7 +137,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_unvis_max_density", o.td_unvis_max_density},
           {"td_split_edges", static_cast<double>(o.td_split_edges)},
           {"td_split_parts", static_cast<double>(o.td_split_parts)},
-          {"x_zero_fill", o.x_zero_fill ? 1.0 : 0.0},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
           {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},

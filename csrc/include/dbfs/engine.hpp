@@ -196,9 +196,6 @@ struct EngineOptions {
   // per part instead of once per edge.  0 disables.
   int64_t td_split_edges = int64_t(1) << 23;
   int td_split_parts = 4;
-  // Several ranks: the candidates' send buffer re-zeroed by a fill kernel
-  // after the exchange instead of by the update's lanes.
-  bool x_zero_fill = false;
   // Dense top-down levels with at least this many frontier edges test hub
   // targets in an LDS copy of the hubs' visited bits (ShardView::td_col);
   // 0 disables.

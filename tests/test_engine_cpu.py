@@ -791,25 +791,3 @@ def test_split_levels_cpu(parts, mode):
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
         used = used or any(c[7] == parts for c in r.chains)
     assert used
-
-
-@pytest.mark.parametrize("mode", ["td", "do"])
-def test_zero_fill_send_buffer_cpu(mode):
-    """Several ranks, x_zero_fill: the candidates' send buffer re-zeroed by a
-    fill after the exchange instead of in the update -- levels exact on 3
-    virtual ranks (byte-map and bitmap levels alike)."""
-    p = dbfs.rmat_params(14, 16, 29)
-    csr = dbfs.host_csr_from_params(p)
-    roots = [0, 123, 15000]
-    exp = {s: dbfs.cpu_bfs(csr, s)[0] for s in roots}
-
-    def body(rt):
-        b = dbfs.BFS(p, rt, mode=mode)
-        b.engine.set_option("x_zero_fill", 1)
-        b.engine.set_option("td_sparse_edges", 0)
-        for s in roots:
-            b.run(s)
-            assert np.array_equal(b.levels(), exp[s]), (rt.rank, s)
-        return True
-
-    assert all(run_virtual_ranks(3, body, device="cpu"))
