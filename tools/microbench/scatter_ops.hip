@@ -12,6 +12,8 @@
 //   rand-load     8-B load of a random word of the 8 MiB bitmap (dependent use)
 //   probe-store   visited-bit probe, then the byte store (a direct top-down edge)
 //   xcd-probe-st  the same with targets in the calling XCD's 1/8 of the range
+//   agent-or32    32-bit atomicOr (returning), agent scope, random 32-bit word of the same bitmap
+//   agent-or32-nr same, result unused
 //
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/scatter_ops tools/microbench/scatter_ops.hip
 #include <hip/hip_runtime.h>
@@ -86,12 +88,22 @@ __global__ __launch_bounds__(kThreads) void scatter_kernel(unsigned long long* w
       const unsigned long long slice = nwords * 8;
       const unsigned long long v = x * slice + (r >> 6) % slice;
       if (!(words[v >> 6] & (1ull << (v & 63)))) bytes[v] = 1;
+    } else if constexpr (kMode == 8 || kMode == 9) {
+      unsigned* w32 = reinterpret_cast<unsigned*>(words);
+      const unsigned long long w = (r >> 5) % (nwords * 2);
+      const unsigned b32 = 1u << (r & 31);
+      if constexpr (kMode == 8) {
+        const unsigned old = __hip_atomic_fetch_or(w32 + w, b32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        local += !(old & b32);
+      } else {
+        __hip_atomic_fetch_or(w32 + w, b32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
       const unsigned long long w = (r >> 6) % nwords;
       acc += words[w];
     }
   }
-  if (kMode == 0 || kMode == 2) atomicAdd(claims, local);
+  if (kMode == 0 || kMode == 2 || kMode == 8) atomicAdd(claims, local);
   if (kMode == 5 && acc == 0x123456789ull) sink[0] = acc;
 }
 
@@ -122,7 +134,7 @@ double run(const char* name, unsigned long long* words, unsigned char* bytes, un
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
     if (ms < best) best = ms;
-    if (kMode == 0 || kMode == 2) {
+    if (kMode == 0 || kMode == 2 || kMode == 8) {
       popcount_kernel<<<1024, 256>>>(words, nwords, dev_scalars + 1);
       unsigned long long h[2];
       CK(hipMemcpy(h, dev_scalars, 16, hipMemcpyDeviceToHost));
@@ -155,5 +167,7 @@ int main(int argc, char** argv) {
   run<5>("rand-load", words, bytes, nwords, scal, blocks, 3);
   run<6>("probe-store", words, bytes, nwords, scal, blocks, 3);
   run<7>("xcd-probe-st", words, bytes, nwords, scal, blocks, 3);
+  run<8>("agent-or32", words, bytes, nwords, scal, blocks, 3);
+  run<9>("agent-or32-nr", words, bytes, nwords, scal, blocks, 3);
   return 0;
 }
