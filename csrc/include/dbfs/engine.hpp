@@ -152,7 +152,11 @@ struct EngineOptions {
   // Measured, RMAT-26 per root: a 28 M-edge second-level expansion 556 ->
   // 402 us; 1354 -> 1368 GTEPS with the bottom-up gate missing (post-bottom-up
   // levels of 200 K edges predicted at 2 M: 58 -> 80 us).
-  int64_t td_bin_edges = int64_t(1) << 21;
+  // Off by default since split top-down levels (td_split_edges): RMAT-26 top-down
+  // only 39.1 GTEPS binned against 67.7 direct and split (its 0.5 B-edge level
+  // 5.6 -> 5.0 ms, the next one, then with the unvisited filter, 21.3 -> 10.8 ms);
+  // RMAT-26 / 27 direction-optimising flat (profiles/r5_td_binned_off_ab.txt).
+  int64_t td_bin_edges = 0;
   // (2^26: RMAT-24, 2^24 vertices, measured 2 % slower binned -- 785 / 793
   // against 815 / 800 GTEPS; RMAT-26 +2-4 %; RMAT-27 flat)
   int64_t td_bin_min_rows = int64_t(1) << 26;
@@ -190,10 +194,13 @@ struct EngineOptions {
   // filter's bits are set (decided on the device from the built filter)
   double td_unvis_max_density = 0.5;
   // One rank, level-byte (level_direct) top-down levels predicted at >=
-  // td_split_edges frontier edges run in td_split_parts parts, the claims of
-  // the parts so far ORed into `visited` between them (refresh_visited): a
-  // target reached by many frontier edges stores its level byte about once
-  // per part instead of once per edge.  0 disables.
+  // td_split_edges frontier edges run in td_split_parts parts (twice as many
+  // from 16 x td_split_edges), the claims of the parts so far ORed into
+  // `visited` between them (refresh_visited): a target reached by many
+  // frontier edges stores its level byte about once per part instead of once
+  // per edge.  0 disables.  RMAT-22 top-down only 98.5 -> 105.7 GTEPS (8 parts:
+  // 103); RMAT-26 top-down only 55.8 -> 67.7 (its 0.5 B-edge level 9.4 -> 5.0
+  // ms; 8 parts 69.5): profiles/r5_td_split_levels_ab.txt.
   int64_t td_split_edges = int64_t(1) << 23;
   int td_split_parts = 4;
   // Dense top-down levels with at least this many frontier edges test hub
