@@ -392,7 +392,13 @@ char DeviceLoop::td_form(int L, double mf, int64_t* cap, bool exact) const {
   }
   bool after_bu = false;  // (binned only before the run's first bottom-up level)
   for (int k = 0; k < L && !after_bu; ++k) after_bu = enq_form_[static_cast<size_t>(k)] == 'B';
-  return binned_ && !after_bu && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
+  // ... and not for a level the direct form does better: one of 16 x
+  // td_split_edges or more (split in parts), or one late enough for the
+  // unvisited filter (top-down only on RMAT-26: 0.5 B-edge level 5.6 -> 4.3
+  // ms, the filter levels 21.3 -> 10.8 and 0.72 -> 0.42 ms)
+  const bool huge = opt_.td_split_edges > 0 && mf >= 16.0 * static_cast<double>(opt_.td_split_edges);
+  const bool late = opt_.td_unvis_edges > 0 && vis_hint_ >= opt_.td_unvis_vis_frac * static_cast<double>(e_.total_directed_);
+  return binned_ && !after_bu && !huge && !late && mf >= static_cast<double>(opt_.td_bin_edges) ? 'X' : 'T';
 }
 
 // the chain enqueued for level L is live for a level with direction `dir`

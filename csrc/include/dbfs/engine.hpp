@@ -152,11 +152,11 @@ struct EngineOptions {
   // Measured, RMAT-26 per root: a 28 M-edge second-level expansion 556 ->
   // 402 us; 1354 -> 1368 GTEPS with the bottom-up gate missing (post-bottom-up
   // levels of 200 K edges predicted at 2 M: 58 -> 80 us).
-  // Off by default since split top-down levels (td_split_edges): RMAT-26 top-down
-  // only 39.1 GTEPS binned against 67.7 direct and split (its 0.5 B-edge level
-  // 5.6 -> 5.0 ms, the next one, then with the unvisited filter, 21.3 -> 10.8 ms);
-  // RMAT-26 / 27 direction-optimising flat (profiles/r5_td_binned_off_ab.txt).
-  int64_t td_bin_edges = 0;
+  // Not for levels the direct form does better since split top-down levels
+  // (DeviceLoop::td_form): RMAT-26 top-down only 39.1 GTEPS binned against
+  // 67.7 direct and split (its 0.5 B-edge level 5.6 -> 5.0 ms, the next one,
+  // with the unvisited filter, 21.3 -> 10.8 ms; profiles/r5_td_binned_off_ab.txt).
+  int64_t td_bin_edges = int64_t(1) << 21;
   // (2^26: RMAT-24, 2^24 vertices, measured 2 % slower binned -- 785 / 793
   // against 815 / 800 GTEPS; RMAT-26 +2-4 %; RMAT-27 flat)
   int64_t td_bin_min_rows = int64_t(1) << 26;
