@@ -810,7 +810,10 @@ void DeviceLoop::emit_dense(Chain& c) {
   // RMAT-22's level 4 87 -> 134 us in 4 parts)
   const int parts = (ta.level_direct && !ranged && !unvis && !xc_ && opt_.td_split_edges > 0 && opt_.td_split_parts > 1 &&
                      c.mf_hint >= static_cast<double>(opt_.td_split_edges))
-                        ? opt_.td_split_parts * (c.mf_hint >= 16.0 * static_cast<double>(opt_.td_split_edges) ? 2 : 1)
+                        ? opt_.td_split_parts * (c.mf_hint >= 16.0 * static_cast<double>(opt_.td_split_edges) &&
+                                                         gv_.n >= (int64_t(1) << 25)
+                                                     ? 2
+                                                     : 1)
                         : 1;
   if (parts > 1) {
     res_.chains.back().split = parts;

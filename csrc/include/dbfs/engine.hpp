@@ -170,7 +170,10 @@ struct EngineOptions {
   // frontier edges are range-staged (TdArgs::range_split: the vertex ranges
   // swept one at a time with their visited bits in LDS, claims deduplicated
   // there) instead of td_expand's scattered visited probes; 0 disables.
-  int64_t td_range_edges = int64_t(1) << 22;
+  // Off by default since split top-down levels: the LJ-sized graph's level it
+  // served (the store-bound one) runs split instead, top-down only 81.5 ->
+  // 92.0 GTEPS; power-law +0.5 %, RMAT-22 flat (profiles/r5_td_range_vs_split.txt).
+  int64_t td_range_edges = 0;
   // ... ranges of at most this many visited words (<= kRangeWords; smaller
   // forces more ranges -- tests on small graphs)
   int64_t td_range_words = kRangeWords;
@@ -195,7 +198,8 @@ struct EngineOptions {
   double td_unvis_max_density = 0.5;
   // One rank, level-byte (level_direct) top-down levels predicted at >=
   // td_split_edges frontier edges run in td_split_parts parts (twice as many
-  // from 16 x td_split_edges), the claims of the parts so far ORed into
+  // from 16 x td_split_edges on graphs of >= 2^25 vertices: a smaller graph's
+  // predicted level overshoots, and RMAT-22 runs 3 % slower in 8), the claims of the parts so far ORed into
   // `visited` between them (refresh_visited): a target reached by many
   // frontier edges stores its level byte about once per part instead of once
   // per edge.  0 disables.  RMAT-22 top-down only 98.5 -> 105.7 GTEPS (8 parts:
