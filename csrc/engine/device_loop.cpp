@@ -81,6 +81,7 @@ class DeviceLoop {
   static constexpr int kBinGrid = 1024;
   int64_t td_grid_ = 1, td_grid_filter_ = 1;
   bool seed_gather_ = false;
+  uint64_t late_ticks_ = 0;  // DBFS_FAULT_INJECT=kind=late_wg (TdSparseArgs::late_ticks)
   LevelCtrl init_;
   UpdateArgs ua_;  // the update's fields common to every chain
 
@@ -99,13 +100,24 @@ class DeviceLoop {
   std::chrono::steady_clock::time_point t0_;
   std::vector<std::pair<std::string, double>> htl_;
   void hmark(const std::string& what);
+  std::string describe(int waiting) const;
 
   void setup();
   word_t* fr_own(int k) const { return e_.frontier_[k].data() + me_ * W_; }
-  // stats block of level L's output (L = -1: the seed); one block with one rank
+  // stats block of level L's output (L = -1: the seed): kStatsBlocks blocks
+  // in turn with several ranks, two with one rank.  (One rank needs two: a
+  // kernel that finishes its level in its last workgroup -- td_sparse -- has
+  // workgroups that return before its ticket, past the level's active count,
+  // and one dispatched after that finish re-reads its input totals.  With one
+  // block it read the NEXT level's totals, ran them against this level's work
+  // list and took a ticket the next sparse level then missed: round 5's wrong
+  // levels and missing stamp, root 0 of RMAT-16.  With the input block apart
+  // from the output block it finds the same active count and returns.
+  // tests/test_gpu_engine.py::test_sparse_level_late_workgroups_gpu makes
+  // every such workgroup late.)
   int64_t* sblk(int L) const {
-    return xc_ ? e_.stats_.data() + static_cast<int64_t>((L + 1) % Engine::kStatsBlocks) * e_.stats_stride_
-               : e_.stats_.data();
+    const int blocks = xc_ ? Engine::kStatsBlocks : Engine::kStatsBlocks1;
+    return e_.stats_.data() + static_cast<int64_t>((L + 1) % blocks) * e_.stats_stride_;
   }
   static int slot(int level) { return (level + 1) % kMailboxSlots; }
   // work-list set k (level L reads set L & 1; one set without sparse levels)
@@ -136,6 +148,28 @@ class DeviceLoop {
 
   RunResult collect(int nlev, std::chrono::steady_clock::time_point t1);
 };
+
+// A failed wait, self-described: the source, the level waited for, every
+// chain enqueued (level, form, cap), the mailbox slots (level, direction, n_f,
+// m_f, done) and the device records of the levels that finished.
+std::string DeviceLoop::describe(int waiting) const {
+  std::string s = "source " + std::to_string(src_) + ", waiting for level " + std::to_string(waiting) + "; chains";
+  for (const auto& ch : res_.chains) s += " " + std::to_string(ch.level) + ch.form + ":" + std::to_string(ch.cap);
+  s += "; mailbox";
+  for (int i = 0; i < kMailboxSlots; ++i) {
+    const volatile LevelMailbox* mb = e_.mailbox_host_ + i;
+    if (mb->level < -1) continue;
+    s += " [" + std::to_string(mb->level) + " " + static_cast<char>(mb->next_dir) + " nf=" + std::to_string(mb->n_f) +
+         " mf=" + std::to_string(mb->m_f) + (mb->done ? " done" : "") + "]";
+  }
+  s += "; records";
+  for (int L = 0; L < waiting && static_cast<size_t>(L / Engine::kRecSeg) < e_.rec_segs_.size(); ++L) {
+    const volatile LevelRecDev* r = e_.rec_segs_[static_cast<size_t>(L / Engine::kRecSeg)].first + L % Engine::kRecSeg;
+    s += " [" + std::to_string(L) + " " + static_cast<char>(r->dir) + " nf=" + std::to_string(r->n_f) +
+         " mf=" + std::to_string(r->m_f) + " new=" + std::to_string(r->discovered) + "]";
+  }
+  return s;
+}
 
 void DeviceLoop::hmark(const std::string& what) {
   htl_.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0_).count());
@@ -269,6 +303,8 @@ void DeviceLoop::setup() {
   const int64_t td_blocks = div_up(e_.g_.nnz(), kTdEdgesPerBlock);
   td_grid_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_max, 1)));
   td_grid_filter_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_filter_max, 1)));
+  if (e_.fault_.kind == "late_wg")
+    late_ticks_ = static_cast<uint64_t>(static_cast<double>(e_.fault_.us) * be_.wall_clock_khz() / 1000.0);
   // Mailbox stamps can be reset although the previous run did not end with a
   // synchronize: its trailing (speculative) chain may still be executing, but
   // every kernel that stamps a mailbox slot (scan_units, level_finish,
@@ -573,6 +609,7 @@ void DeviceLoop::emit_sparse(Chain& c) {
   sp.mailbox = e_.mailbox_dev_ + slot(L);
   sp.level_index = L;
   sp.grid = std::max<int64_t>(1, opt_.td_sparse_grid);
+  sp.late_ticks = late_ticks_;
   sp.first = !compacted || from_bits;
   sp.max_mf = c.cap;
   if (from_bits) {
@@ -1113,10 +1150,7 @@ RunResult DeviceLoop::run() {
     try {
       mb = wait_stamp(L - 1);
     } catch (const Error& err) {
-      // which level, and the chains enqueued so far (level, form, cap)
-      std::string chains;
-      for (const auto& ch : res_.chains) chains += " " + std::to_string(ch.level) + ch.form + ":" + std::to_string(ch.cap);
-      throw Error(std::string(err.what()) + " (waiting for level " + std::to_string(L - 1) + "; chains" + chains + ")");
+      throw Error(std::string(err.what()) + " (" + describe(L - 1) + ")");
     }
     if (ht_) hmark("stamp " + std::to_string(L - 1));
     if (mb->done) {

@@ -549,8 +549,11 @@ void Engine::read_level_stats(int64_t* host_stats) {
 // at the start of level L of every run: `throw` raises an Error (in-process
 // ranks abort their group), `exit` ends the process with status 17 (a crashed
 // rank), `hang` stops participating (peers must time out), `device` records
-// a device-check violation (the run fails when it ends).  Used by the
-// failure-detection tests; unset in normal runs.
+// a device-check violation (the run fails when it ends), `delay` enqueues the
+// level ms late; kind=late_wg[,us=U] (every rank, every level) makes the
+// workgroups of a sparse top-down level that take no ticket start U us late
+// on the device (TdSparseArgs::late_ticks).  Used by the failure-detection
+// and level-loop tests; unset in normal runs.
 FaultSpec FaultSpec::from_env() {
   FaultSpec f;
   const char* e = std::getenv("DBFS_FAULT_INJECT");
@@ -568,15 +571,18 @@ FaultSpec FaultSpec::from_env() {
     else if (k == "level") f.level = std::stoi(v);
     else if (k == "kind") f.kind = v;
     else if (k == "ms") f.ms = std::stoi(v);
+    else if (k == "us") f.us = std::stoi(v);
     else DBFS_CHECK(false, "DBFS_FAULT_INJECT: unknown key '" + k + "'");
     pos = comma + 1;
   }
   DBFS_CHECK(f.kind == "throw" || f.kind == "exit" || f.kind == "hang" || f.kind == "device" || f.kind == "delay" ||
-                 f.kind == "rccl_init" || f.kind == "peer_init",
-             "DBFS_FAULT_INJECT: kind must be throw|exit|hang|device|delay|rccl_init|peer_init");
+                 f.kind == "rccl_init" || f.kind == "peer_init" || f.kind == "late_wg",
+             "DBFS_FAULT_INJECT: kind must be throw|exit|hang|device|delay|rccl_init|peer_init|late_wg");
   // (rccl_init / peer_init: the communicators' setup fails -- NcclComm /
-  // PeerComm read them; the engine injects nothing)
-  if (f.kind == "rccl_init" || f.kind == "peer_init") f.rank = -1;
+  // PeerComm read them; late_wg: every sparse top-down level's ticket-less
+  // workgroups start late, on every rank (DeviceLoop::emit_sparse) -- the
+  // engine injects nothing at a level)
+  if (f.kind == "rccl_init" || f.kind == "peer_init" || f.kind == "late_wg") f.rank = -1;
   return f;
 }
 
@@ -644,11 +650,12 @@ void Engine::alloc_bitmap_state() {
   qscan_ = DBuf<int64_t>(be_, static_cast<size_t>(g_.rows() + 1));
   qbase_ = DBuf<int64_t>(be_, static_cast<size_t>(std::max<int64_t>(g_.rows(), 1)));
   blk_vstart_ = DBuf<int32_t>(be_, static_cast<size_t>(div_up(g_.nnz(), kTdEdgesPerBlock) + 2));
-  // several ranks: kStatsBlocks blocks of [local count, local degree sum,
-  // global count, global degree sum, ...] (one 64-byte line each; block 0's
-  // [4..5] also hold the degree moments before the first run)
+  // kStatsBlocks (several ranks) or kStatsBlocks1 (one rank) blocks of
+  // [local count, local degree sum, global count, global degree sum, ...]
+  // (one 64-byte line each; block 0's [4..5] also hold the degree moments
+  // before the first run)
   stats_stride_ = 8;
-  stats_ = DBuf<int64_t>(be_, static_cast<size_t>(exchange() ? kStatsBlocks * stats_stride_ : std::max<int64_t>(stats_stride_, 8)));
+  stats_ = DBuf<int64_t>(be_, static_cast<size_t>((exchange() ? kStatsBlocks : kStatsBlocks1) * stats_stride_));
   be_.memset_async(stats_.data(), 0, stats_.bytes());
   if (g_.nhubs() > 0) hub_front_ = DBuf<word_t>(be_, static_cast<size_t>(div_up(g_.nhubs(), kWordBits)));
   // Zero-degree (and padding) vertices can never be discovered: they start out

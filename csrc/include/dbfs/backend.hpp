@@ -529,6 +529,11 @@ struct TdSparseArgs {
   // kBuQueueStride apart, zero between launches).
   bool from_bits = false;
   int64_t words = 0;
+  // Fault injection (DBFS_FAULT_INJECT=kind=late_wg): the workgroups that
+  // take no ticket (blockIdx >= the level's active count) first wait this
+  // many wall-clock ticks, so they start after the level's last workgroup has
+  // finished it -- the dispatch order a busy or cold GPU can produce.  0: off.
+  uint64_t late_ticks = 0;
   // Several ranks, direct exchange with a folded level end, a tiny level:
   // td_sparse's last workgroup publishes the lists and then runs the owner
   // side itself (td_sparse_apply's work on one workgroup: nranks, end, fin

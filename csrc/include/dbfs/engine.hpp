@@ -436,6 +436,7 @@ struct FaultSpec {
   int rank = -1, level = -1;
   std::string kind = "throw";
   int ms = 2000;  // kind=delay: how long the rank sleeps before enqueueing the level
+  int us = 500;   // kind=late_wg: how long td_sparse's ticket-less workgroups wait (TdSparseArgs::late_ticks)
   static FaultSpec from_env();
 };
 
@@ -520,8 +521,11 @@ class Engine {
   // Several ranks (device loop): level L's totals go to
   // stats block (L + 1) % kStatsBlocks, so a mispredicted chain's
   // (unpredicated) reduction never touches the block the re-enqueued chain
-  // reads.  stats_stride_: int64 entries per block.
+  // reads.  One rank: level L's totals in block (L + 1) % kStatsBlocks1, so a
+  // level's input totals stay put while its own kernels finish it (see
+  // DeviceLoop::sblk).  stats_stride_: int64 entries per block.
   static constexpr int kStatsBlocks = 3;
+  static constexpr int kStatsBlocks1 = 2;
   int64_t stats_stride_ = 8;
   DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
   // binned top-down levels (one rank): bin counts / positions, bin starts, targets

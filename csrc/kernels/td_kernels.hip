@@ -848,6 +848,15 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ int s_last;
   const bool dx = a.lists && a.direct.active;
+  if (a.late_ticks) {
+    // fault injection: a workgroup that will take no ticket starts late
+    const long long m0 = a.dev_stats[1];
+    const long long nb0 = (m0 + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
+    if (static_cast<long long>(blockIdx.x) >= (nb0 < 1 ? 1 : nb0)) {
+      const uint64_t t0 = wall_clock64();
+      while (wall_clock64() - t0 < a.late_ticks) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   // uniform: the whole grid returns, no workgroup takes a ticket (a direct
   // exchange still publishes, empty)
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {

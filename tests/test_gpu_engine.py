@@ -19,12 +19,26 @@ pytestmark = pytest.mark.gpu
 MODES = ["do", "td", "bu", "ref", "simple", "scan"]
 
 
+def _describe(src, res, got, exp):
+    """A levels mismatch, self-described: the root, the first mismatching
+    vertices, the chains the device loop enqueued and its level records."""
+    bad = np.nonzero(got != exp)[0]
+    first = ", ".join(f"{int(v)}: {int(got[v])} vs {int(exp[v])}" for v in bad[:8])
+    recs = []
+    if res is not None:
+        for r in res.levels:
+            recs.append(f"[{r.get('level')} {r.get('dir')} nf={r.get('frontier')} mf={r.get('frontier_edges')} "
+                        f"new={r.get('discovered')}]")
+    chains = [f"{c[0]}{c[1]}:{c[2]}" for c in res.chains] if res is not None else []
+    return (f"root {src}: {bad.size} vertices differ (got vs expected: {first}); "
+            f"chains {' '.join(chains)}; records {' '.join(recs)}")
+
+
 def _check(bfs, csr, src):
     res = bfs.run(src)
     exp, _ = dbfs.cpu_bfs(csr, src)
     got = bfs.levels()
-    bad = np.nonzero(got != exp)[0]
-    assert bad.size == 0, f"first mismatch at {bad[0]}: got {got[bad[0]]} expected {exp[bad[0]]}"
+    assert np.array_equal(got, exp), _describe(src, res, got, exp)
     reached = int(np.count_nonzero(exp != dbfs.UNREACHED))
     assert res.reached == reached
     ro = np.asarray(csr.row_off)
@@ -263,13 +277,50 @@ def test_td_byte_map_mode_gpu(P, mode, knobs):
             bfs.engine.set_option(k, v)
         out = []
         for s in srcs:
-            bfs.run(s)
-            out.append(bfs.levels())
+            res = bfs.run(s)
+            out.append((s, res, bfs.levels()))
         return out
 
     for rank_out in run_virtual_ranks(P, body, device="hip"):
-        for lv, e in zip(rank_out, exp):
-            assert np.array_equal(lv, e)
+        for (s, res, lv), e in zip(rank_out, exp):
+            assert np.array_equal(lv, e), _describe(s, res, lv, e)
+
+
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_sparse_level_late_workgroups_gpu(mode, monkeypatch):
+    """Regression for round 5's intermittent wrong levels / missing stamp
+    (test_td_byte_map_mode_gpu[*-td-1], root 0 of RMAT-16).  A one-rank
+    td_sparse launch finishes its level in its last workgroup; workgroups past
+    the level's active count return before the ticket, so one dispatched after
+    that finish must not see the next level's totals.  DBFS_FAULT_INJECT
+    kind=late_wg makes every such workgroup start 300 us late, which turns the
+    rare dispatch order into the only one: with the level's input and output
+    totals in one stats block, root 0 (the RMAT hub: a level-0 list of a few
+    blocks, a level-1 list of ~250) ran level-1 totals against level 0's
+    lists -- vertices one level early and late, and a shifted ticket that left
+    a later one-block sparse level without its stamp."""
+    monkeypatch.setenv("DBFS_FAULT_INJECT", "kind=late_wg,us=300")
+    p = dbfs.rmat_params(16, 16, 29)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [0, 5, 40000, 0]
+    exp = {s: dbfs.cpu_bfs(csr, s)[0] for s in set(srcs)}
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        bfs.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+        bfs.engine.set_option("td_check_visited_min", 0.0)
+        out = []
+        for s in srcs:
+            res = bfs.run(s)
+            out.append((s, res, bfs.levels()))
+        return out
+
+    (rank_out,) = run_virtual_ranks(1, body, device="hip")
+    sparse = 0
+    for s, res, lv in rank_out:
+        assert np.array_equal(lv, exp[s]), _describe(s, res, lv, exp[s])
+        sparse += sum(1 for c in res.chains if c[1] == "S")
+    assert sparse > 0  # (the injected kernel ran)
 
 
 @pytest.mark.parametrize("P", [1, 3])
