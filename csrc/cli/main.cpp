@@ -257,7 +257,19 @@ std::shared_ptr<VirtualGroup> make_ranks(const Args& a, int P, bool multiproc, i
     const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);
     auto boot = std::make_shared<TcpBootstrap>(addr ? addr : "127.0.0.1", port, wrank, world);
     auto make_rccl = [&]() -> std::shared_ptr<Comm> {
-      std::string uid = boot->broadcast(wrank == 0 ? NcclComm::unique_id() : std::string());
+      // every rank takes part in the id broadcast before anything can fail
+      // (an empty id: rank 0 could not make one), so the bootstrap's message
+      // sequence stays aligned for the agreement after a failure
+      std::string uid, why;
+      if (wrank == 0) {
+        try {
+          uid = NcclComm::unique_id();
+        } catch (const std::exception& e) {
+          why = e.what();
+        }
+      }
+      uid = boot->broadcast(uid);
+      if (uid.empty()) throw Error(why.empty() ? "rank 0 could not create the RCCL id" : why);
       return std::make_shared<NcclComm>(uid, wrank, world, *ranks[0].be);
     };
     if (a.cpu || cm == "tcp") {

@@ -22,6 +22,12 @@ double comm_timeout_s() {
   return std::max(0.0, std::atof(e));
 }
 
+double bootstrap_timeout_s() {
+  const char* e = std::getenv("DBFS_BOOTSTRAP_TIMEOUT_S");
+  if (!e || !*e) return 600.0;
+  return std::max(0.0, std::atof(e));
+}
+
 int64_t* Comm::scratch(size_t n) {
   DBFS_CHECK(be_ != nullptr, "comm has no backend bound");
   if (scratch_.size() < n) scratch_ = DBuf<int64_t>(*be_, std::max<size_t>(n, 64));

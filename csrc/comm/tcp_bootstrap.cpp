@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <thread>
 
@@ -36,31 +37,36 @@ void write_all(int fd, const void* p, size_t n) {
   }
 }
 
-void read_all(int fd, void* p, size_t n) {
+// Receive exactly n bytes, each wait bounded by timeout_s (0: unbounded;
+// `knob` names the variable that sets it in the error).
+void read_all(int fd, void* p, size_t n, double timeout_s, const char* knob) {
   char* c = static_cast<char*>(p);
   while (n) {
+    if (timeout_s > 0) {
+      pollfd pfd{fd, POLLIN, 0};
+      const int pr = ::poll(&pfd, 1, static_cast<int>(std::min(timeout_s * 1000.0, 2.0e9)));
+      if (pr < 0 && errno == EINTR) continue;
+      if (pr == 0)
+        throw Error("bootstrap peer timed out after " + std::to_string(timeout_s) + " s (" + knob +
+                    "); a rank stopped participating");
+    }
     ssize_t k = ::recv(fd, c, n, 0);
     if (k < 0 && errno == EINTR) continue;
-    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
-      throw Error("bootstrap peer timed out after " + std::to_string(comm_timeout_s()) +
-                  " s (DBFS_COMM_TIMEOUT_S); a rank stopped participating");
     if (k <= 0) throw Error("bootstrap peer closed the connection (a rank failed)");
     c += k;
     n -= static_cast<size_t>(k);
   }
 }
 
-// Connected sockets: no Nagle, and a receive timeout so a hung peer turns into
-// an error (failure detection).
+// Connected sockets: no Nagle.  (Receive waits are bounded per message by
+// read_all: the bootstrap's own exchanges by DBFS_BOOTSTRAP_TIMEOUT_S --
+// they also wait for the peers' setup: per-rank ingest of a large file, the
+// CSR build, hub selection, which can take minutes -- and TcpComm's
+// collectives by DBFS_COMM_TIMEOUT_S.  A peer that dies closes its socket
+// and fails the wait at once.)
 void tune_socket(int fd) {
   int one = 1;
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-  // (0: no limit -- also replaces the short hello timeout of an accepted socket)
-  const double t = comm_timeout_s() > 0 ? comm_timeout_s() : 0.0;
-  timeval tv{};
-  tv.tv_sec = static_cast<time_t>(t);
-  tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 
 void send_msg(int fd, const std::string& s) {
@@ -84,24 +90,15 @@ uint64_t max_msg_bytes() {
 // connections that are not from this program.
 constexpr uint64_t kHelloMagic = 0x31544f4f42534642ull;  // "BFSBOOT1"
 
-std::string recv_msg(int fd) {
+std::string recv_msg(int fd, double timeout_s, const char* knob) {
   uint64_t n = 0;
-  read_all(fd, &n, sizeof(n));
+  read_all(fd, &n, sizeof(n), timeout_s, knob);
   if (n > max_msg_bytes())
     throw Error("bootstrap peer announced a " + std::to_string(n) + "-byte message (limit " +
                 std::to_string(max_msg_bytes()) + ", DBFS_BOOTSTRAP_MAX_MSG)");
   std::string s(n, '\0');
-  if (n) read_all(fd, &s[0], n);
+  if (n) read_all(fd, &s[0], n, timeout_s, knob);
   return s;
-}
-
-// Receive timeout of a freshly accepted connection's hello (a stray
-// connection that sends nothing must not stall the accept loop).
-void set_recv_timeout(int fd, double t) {
-  timeval tv{};
-  tv.tv_sec = static_cast<time_t>(t);
-  tv.tv_usec = static_cast<suseconds_t>((t - static_cast<double>(tv.tv_sec)) * 1e6);
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 
 bool is_literal_ipv4(const std::string& host) {
@@ -179,12 +176,11 @@ TcpBootstrap::TcpBootstrap(const std::string& host, int port, int rank, int nran
       // a rank sends its hello right after connecting: a connection silent
       // for 10 s (or closed, or speaking another protocol) is not one of ours
       // -- dropped, and the loop keeps waiting for the real peers
-      set_recv_timeout(fd, 10.0);
       bool ours = false;
       try {
-        read_all(fd, &hello, sizeof(hello));
+        read_all(fd, &hello, sizeof(hello), 10.0, "hello");
         ours = hello == kHelloMagic;
-        if (ours) read_all(fd, &r, sizeof(r));
+        if (ours) read_all(fd, &r, sizeof(r), 10.0, "hello");
       } catch (const Error&) {
         ours = false;
       }
@@ -241,10 +237,14 @@ std::string TcpBootstrap::broadcast(const std::string& data, int root) {
     for (int r = 1; r < size_; ++r) send_msg(peers_[r], data);
     return data;
   }
-  return recv_msg(peers_[0]);
+  return recv_msg(peers_[0], bootstrap_timeout_s(), "DBFS_BOOTSTRAP_TIMEOUT_S");
 }
 
 std::vector<std::string> TcpBootstrap::allgather(const std::string& data) {
+  return allgather_within(data, bootstrap_timeout_s(), "DBFS_BOOTSTRAP_TIMEOUT_S");
+}
+
+std::vector<std::string> TcpBootstrap::allgather_within(const std::string& data, double timeout_s, const char* knob) {
   std::vector<std::string> out(static_cast<size_t>(size_));
   if (size_ == 1) {
     out[0] = data;
@@ -252,12 +252,12 @@ std::vector<std::string> TcpBootstrap::allgather(const std::string& data) {
   }
   if (rank_ == 0) {
     out[0] = data;
-    for (int r = 1; r < size_; ++r) out[r] = recv_msg(peers_[r]);
+    for (int r = 1; r < size_; ++r) out[r] = recv_msg(peers_[r], timeout_s, knob);
     for (int r = 1; r < size_; ++r)
       for (int k = 0; k < size_; ++k) send_msg(peers_[r], out[k]);
   } else {
     send_msg(peers_[0], data);
-    for (int k = 0; k < size_; ++k) out[k] = recv_msg(peers_[0]);
+    for (int k = 0; k < size_; ++k) out[k] = recv_msg(peers_[0], timeout_s, knob);
   }
   return out;
 }
@@ -269,6 +269,9 @@ void TcpBootstrap::barrier() { allgather(std::string()); }
 // ---- TcpComm --------------------------------------------------------------------
 
 namespace dbfs {
+
+// (TcpComm's collectives are traversal collectives: the shorter bound)
+static const char* const kCommKnob = "DBFS_COMM_TIMEOUT_S";
 
 TcpComm::TcpComm(std::shared_ptr<TcpBootstrap> boot, Backend& be) : boot_(std::move(boot)) { bind_backend(&be); }
 int TcpComm::rank() const { return boot_->rank(); }
@@ -287,19 +290,19 @@ void TcpComm::store(void* p, const std::string& s, size_t off, size_t bytes) {
 void TcpComm::alltoall(const void* send, void* recv, size_t bytes) {
   note(kAllToAll, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
   const int P = size(), me = rank();
-  auto all = boot_->allgather(fetch(send, bytes * P));
+  auto all = boot_->allgather_within(fetch(send, bytes * P), comm_timeout_s(), kCommKnob);
   for (int r = 0; r < P; ++r) store(static_cast<char*>(recv) + r * bytes, all[r], me * bytes, bytes);
 }
 
 void TcpComm::allgather(const void* send, void* recv, size_t bytes) {
   note(kAllGather, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(bytes));
-  auto all = boot_->allgather(fetch(send, bytes));
+  auto all = boot_->allgather_within(fetch(send, bytes), comm_timeout_s(), kCommKnob);
   for (int r = 0; r < size(); ++r) store(static_cast<char*>(recv) + r * bytes, all[r], 0, bytes);
 }
 
 void TcpComm::allreduce_sum_i64(int64_t* buf, size_t count) {
   note(kAllReduce, static_cast<int64_t>(size() - 1) * static_cast<int64_t>(count) * 8);
-  auto all = boot_->allgather(fetch(buf, count * sizeof(int64_t)));
+  auto all = boot_->allgather_within(fetch(buf, count * sizeof(int64_t)), comm_timeout_s(), kCommKnob);
   // two's-complement (wrapping) sums, as RCCL's: the engine also reduces
   // disjoint bit sets (hub frontier words) and, on no-op chains, stale blocks
   std::vector<uint64_t> acc(count, 0);
@@ -326,7 +329,7 @@ void TcpComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, 
     data += fetch(static_cast<const char*>(send) + sd[r] * eb, static_cast<size_t>(sc[r]) * eb);
     off += sc[r];
   }
-  auto all = boot_->allgather(msg + data);
+  auto all = boot_->allgather_within(msg + data, comm_timeout_s(), kCommKnob);
   for (int r = 0; r < P; ++r) {
     int64_t hdr[2];
     std::memcpy(hdr, all[r].data() + static_cast<size_t>(me) * 2 * sizeof(int64_t), sizeof(hdr));
@@ -339,7 +342,7 @@ void TcpComm::alltoallv(const void* send, const int64_t* sc, const int64_t* sd, 
 void TcpComm::barrier() {
   note(kBarrier, 0);
   be_->synchronize();
-  boot_->barrier();
+  boot_->allgather_within(std::string(), comm_timeout_s(), kCommKnob);
 }
 
 }  // namespace dbfs

@@ -36,6 +36,10 @@ namespace dbfs {
 // for its peers fails with an error instead of hanging.  DBFS_COMM_TIMEOUT_S,
 // default 120 s; 0 disables the limit.
 double comm_timeout_s();
+// The host bootstrap's socket timeout (TcpBootstrap, and TcpComm over it):
+// DBFS_BOOTSTRAP_TIMEOUT_S, default 600 s (setup exchanges wait for every
+// rank's ingest and CSR build); 0 disables it.
+double bootstrap_timeout_s();
 
 class Comm {
  public:
@@ -567,6 +571,9 @@ class TcpBootstrap final : public Bootstrap {
   std::string broadcast(const std::string& data, int root = 0) override;
   std::vector<std::string> allgather(const std::string& data) override;
   void barrier() override;
+  // allgather with every receive bounded by timeout_s (0: unbounded), `knob`
+  // naming the setting in a timeout's error (TcpComm: DBFS_COMM_TIMEOUT_S)
+  std::vector<std::string> allgather_within(const std::string& data, double timeout_s, const char* knob);
 
  private:
   int rank_, size_;

@@ -152,3 +152,36 @@ def test_multiprocess_hung_rank_times_out():
     rc0, _, e0 = rc0_out
     assert rc0 != 0 and "timed out" in e0, e0
     assert elapsed < 60
+
+
+@pytest.mark.timeout(60)
+def test_bootstrap_and_collective_timeouts_are_separate(monkeypatch):
+    """The TCP bootstrap's own exchanges wait DBFS_BOOTSTRAP_TIMEOUT_S (setup:
+    a peer may still be ingesting its shard), TcpComm's collectives
+    DBFS_COMM_TIMEOUT_S; each timeout names its setting.  Rank 1 connects and
+    then never joins an exchange."""
+    from distributed_cuda_bfs_amd._native import N
+
+    monkeypatch.setenv("DBFS_BOOTSTRAP_TIMEOUT_S", "1.0")
+    monkeypatch.setenv("DBFS_COMM_TIMEOUT_S", "0.3")
+    port = _free_port()
+    boots = [None, None]
+
+    def make(r):
+        boots[r] = N.TcpBootstrap("127.0.0.1", port, r, 2, 20.0)
+
+    th = [threading.Thread(target=make, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    b0 = boots[0]
+    t0 = time.time()
+    with pytest.raises(Exception, match="DBFS_BOOTSTRAP_TIMEOUT_S"):
+        b0.allgather(b"x")
+    assert 0.8 < time.time() - t0 < 10
+    comm = N.tcp_comm(b0, dbfs.init_runtime("cpu").backend)
+    t0 = time.time()
+    with pytest.raises(Exception, match="DBFS_COMM_TIMEOUT_S"):
+        comm.barrier()
+    assert time.time() - t0 < 0.9
