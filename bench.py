@@ -516,6 +516,10 @@ def main(argv=None) -> int:
             "traversed_edges_mean": edges // len(results),
             "depth_mean": sum(r.depth for r in results) / len(results),
             "mispredicted_levels": sum(r.mispredicts for r in results),
+            # timed traversals that ended at the all-reached stop (every vertex
+            # with an edge reached: the last frontier was not expanded, so its
+            # last level record discovered vertices)
+            "all_reached_stops": sum(1 for r in results if r.levels and r.levels[-1]["discovered"] > 0),
             "validated": validated,
             "validated_roots": (f"{n_valid}/{len(timed)}" if validated is not None else None),
             "generate_s": round(gen_s, 3),

@@ -57,6 +57,8 @@ class HipBackend final : public Backend {
     hipEventDestroy(join_ev_);
     hipStreamDestroy(side_);
     if (scan_tmp_) hipFree(scan_tmp_);
+    for (void* p : deferred_) hipFree(p);
+    for (void* h : deferred_host_) hipHostFree(h);
     if (pinned_) hipHostFree(pinned_);
     hipStreamDestroy(st_);
   }
@@ -106,7 +108,18 @@ class HipBackend final : public Backend {
     on();
     hipStreamSynchronize(st_);
     hipStreamSynchronize(side_);
-    hipFree(p);
+    release_(p);
+  }
+  // Frees deferred to the backend's destruction (Backend::set_deferred_frees):
+  // hipFree waits for every stream of the device, and with several ranks of
+  // one process on one device that includes a peer's kernel spinning on this
+  // rank's next collective -- which this rank enqueues only after the free.
+  void set_deferred_frees(bool on) override { defer_ = on; }
+  bool deferred_frees() const override { return defer_; }
+  void release_(void* p) {
+    if (!p) return;
+    if (defer_) deferred_.push_back(p);
+    else hipFree(p);
   }
   void memset_async(void* p, int v, size_t bytes) override {
     if (!bytes) return;
@@ -229,7 +242,8 @@ class HipBackend final : public Backend {
     if (!h) return;
     on();
     hipStreamSynchronize(st_);
-    hipHostFree(h);
+    if (defer_) deferred_host_.push_back(h);
+    else hipHostFree(h);
   }
   void zero_degree_mask(const ZeroDegArgs& a) override { on(); kern::zero_degree_mask(a, st_); chk(); }
   void compact_frontier(const CompactArgs& a) override { on(); kern::compact_frontier(a, st_); chk(); }
@@ -329,7 +343,7 @@ class HipBackend final : public Backend {
     eid_t h = 0;
     HIP_CHECK(hipMemcpyAsync(&h, cnt + words, sizeof(h), hipMemcpyDeviceToHost, st_));
     HIP_CHECK(hipStreamSynchronize(st_));
-    HIP_CHECK(hipFree(cnt));
+    release_(cnt);
     return static_cast<int64_t>(h);
   }
   void sort_neighbors(const eid_t* ro, vid_t* col, int64_t rows, const uint32_t* key_deg) override {
@@ -341,8 +355,8 @@ class HipBackend final : public Backend {
     kern::sort_neighbors(ro, col, rows, key_deg, list, count, st_);
     chk();
     HIP_CHECK(hipStreamSynchronize(st_));
-    HIP_CHECK(hipFree(list));
-    HIP_CHECK(hipFree(count));
+    release_(list);
+    release_(count);
   }
 
   void sort_rows_by_id(const eid_t* ro, vid_t* col, int64_t rows, int64_t n) override {
@@ -359,9 +373,9 @@ class HipBackend final : public Backend {
     kern::sort_rows_by_id(ro, col, rows, n, list, count, tmp, st_);
     chk();
     HIP_CHECK(hipStreamSynchronize(st_));
-    HIP_CHECK(hipFree(list));
-    HIP_CHECK(hipFree(count));
-    HIP_CHECK(hipFree(tmp));
+    release_(list);
+    release_(count);
+    release_(tmp);
   }
 
   void gen_count_degrees(const GenParams& p, int64_t lo, int64_t rows, eid_t* deg) override {
@@ -374,7 +388,7 @@ class HipBackend final : public Backend {
     const size_t need = static_cast<size_t>(kern::scan_tmp_elems(n));
     if (need > scan_tmp_n_) {
       HIP_CHECK(hipStreamSynchronize(st_));
-      if (scan_tmp_) HIP_CHECK(hipFree(scan_tmp_));
+      if (scan_tmp_) release_(scan_tmp_);
       HIP_CHECK(hipMalloc(&scan_tmp_, need * sizeof(eid_t)));
       scan_tmp_n_ = need;
     }
@@ -440,6 +454,8 @@ class HipBackend final : public Backend {
   size_t ev_used_ = 0;
   eid_t* scan_tmp_ = nullptr;
   size_t scan_tmp_n_ = 0;
+  bool defer_ = false;
+  std::vector<void*> deferred_, deferred_host_;
 };
 
 }  // namespace

@@ -250,8 +250,13 @@ std::shared_ptr<VirtualGroup> make_ranks(const Args& a, int P, bool multiproc, i
     if (a.cpu) ranks[i].be = make_cpu_backend();
     else if (multiproc) ranks[i].be = make_hip_backend(dev_pin ? std::atoi(dev_pin) : env_int("LOCAL_RANK", 0));
     else if (a.virtual_ranks > 0) ranks[i].be = make_hip_backend(a.device);
-    else ranks[i].be = make_hip_backend(P > 1 ? i : a.device);
+    else ranks[i].be = make_hip_backend(P > 1 ? (dev_pin ? std::atoi(dev_pin) : i) : a.device);
   }
+  // one process, P ranks pinned to one device (DBFS_DEVICE: the --gpus P
+  // path rehearsed on one GPU): every free deferred to the end, so no rank's
+  // hipFree waits for a peer's kernel spinning on that rank's next collective
+  if (!multiproc && !a.cpu && a.virtual_ranks == 0 && P > 1 && dev_pin)
+    for (auto& r : ranks) r.be->set_deferred_frees(true);
   if (multiproc) {
     const char* addr = std::getenv("MASTER_ADDR");
     const int port = env_int("DBFS_BOOTSTRAP_PORT", env_int("MASTER_PORT", 29500) + 1);

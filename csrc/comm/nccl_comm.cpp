@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -129,19 +130,56 @@ void NcclComm::install_watchdog() {
   });
 }
 
+// One process, one communicator per backend (the reference's one process
+// driving every GPU, bfs.cu:328-332): ncclCommInitAll's work as a group of
+// nonblocking per-rank inits, so its setup is bounded like the multi-process
+// one (DBFS_RCCL_INIT_TIMEOUT_S): a setup that cannot complete -- RCCL
+// refusing two ranks on one device, a fabric problem -- aborts every
+// communicator and fails instead of hanging the process.
 std::vector<std::unique_ptr<NcclComm>> NcclComm::init_all(const std::vector<Backend*>& bes) {
   const int n = static_cast<int>(bes.size());
-  std::vector<int> devs(static_cast<size_t>(n));
-  for (int i = 0; i < n; ++i) {
-    DBFS_CHECK(bes[i]->kind() == DeviceKind::HIP, "NcclComm requires HIP backends");
-    devs[i] = bes[i]->device_id();
+  for (int i = 0; i < n; ++i) DBFS_CHECK(bes[i]->kind() == DeviceKind::HIP, "NcclComm requires HIP backends");
+  if (const char* f = std::getenv("DBFS_FAULT_INJECT"))
+    DBFS_CHECK(std::string(f).find("kind=rccl_init") == std::string::npos, "injected fault (rccl_init)");
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  std::vector<ncclComm_t> comms(static_cast<size_t>(n), nullptr);
+  auto abort_all = [&] {
+    for (auto& c : comms)
+      if (c) ncclCommAbort(c);
+  };
+  ncclResult_t r0 = ncclGroupStart();
+  for (int i = 0; i < n && (r0 == ncclSuccess || r0 == ncclInProgress); ++i) {
+    HIP_CHECK(hipSetDevice(bes[i]->device_id()));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    r0 = ncclCommInitRankConfig(&comms[static_cast<size_t>(i)], n, id, i, &cfg);
   }
-  std::vector<ncclComm_t> comms(static_cast<size_t>(n));
-  NCCL_CHECK(ncclCommInitAll(comms.data(), n, devs.data()));
+  const ncclResult_t r1 = ncclGroupEnd();
+  if ((r0 != ncclSuccess && r0 != ncclInProgress) || (r1 != ncclSuccess && r1 != ncclInProgress)) {
+    abort_all();
+    NCCL_CHECK(r0 != ncclSuccess && r0 != ncclInProgress ? r0 : r1);
+  }
+  const double limit = init_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i) {
+    const double left =
+        limit > 0 ? std::max(0.001, limit - std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count())
+                  : 0.0;
+    const ncclResult_t st = comms[static_cast<size_t>(i)] ? poll_comm(comms[static_cast<size_t>(i)], left)
+                                                          : ncclInternalError;
+    if (st != ncclSuccess) {
+      abort_all();
+      DBFS_CHECK(st != ncclInProgress, "RCCL in-process setup (" + std::to_string(n) +
+                                           " communicators) did not complete within " +
+                                           std::to_string(static_cast<int>(limit)) + " s (DBFS_RCCL_INIT_TIMEOUT_S)");
+      NCCL_CHECK(st);
+    }
+  }
   std::vector<std::unique_ptr<NcclComm>> out;
   for (int i = 0; i < n; ++i) {
     std::unique_ptr<NcclComm> c(new NcclComm());
-    c->comm_ = comms[i];
+    c->comm_ = comms[static_cast<size_t>(i)];
     c->rank_ = i;
     c->size_ = n;
     c->bind_backend(bes[i]);

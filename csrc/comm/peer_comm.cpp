@@ -121,12 +121,15 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
         Local pl;
         std::memcpy(&pl, all[p].data(), sizeof(pl));
         // threads of one process sharing a device cannot wait for each other in
-        // kernels: any device-wide synchronisation one of them makes (hipFree
-        // does) waits for the other's spinning collective
-        DBFS_CHECK(pl.device != be.device_id(), "PeerComm: in-process ranks " + std::to_string(rank_) + " and " +
-                                                    std::to_string(p) + " share device " + std::to_string(pl.device) +
-                                                    " (one device per rank, or one process per rank)");
-        {
+        // kernels while any of them makes a device-wide synchronisation
+        // (hipFree does: it waits for the other's spinning collective): only
+        // with the backend's frees deferred (Backend::set_deferred_frees -- the
+        // single-process CLI rehearsing --gpus P on one device, DBFS_DEVICE)
+        DBFS_CHECK(pl.device != be.device_id() || be.deferred_frees(),
+                   "PeerComm: in-process ranks " + std::to_string(rank_) + " and " + std::to_string(p) +
+                       " share device " + std::to_string(pl.device) +
+                       " (one device per rank, or one process per rank)");
+        if (pl.device != be.device_id()) {
           int can = 0;
           HIP_CHECK(hipDeviceCanAccessPeer(&can, be.device_id(), pl.device));
           DBFS_CHECK(can, "PeerComm: device " + std::to_string(be.device_id()) + " cannot access device " +
@@ -180,6 +183,9 @@ PeerComm::PeerComm(std::shared_ptr<Bootstrap> boot, Backend& be, std::shared_ptr
     for (int p = 0; p < size_ && !shared_; ++p)
       for (int q = p + 1; q < size_; ++q)
         if (!bus_[p].empty() && bus_[p] == bus_[q]) shared_ = true;
+    coresident_ = 0;
+    for (int p = 0; p < size_; ++p) coresident_ += !bus_[rank_].empty() && bus_[p] == bus_[rank_] ? 1 : 0;
+    coresident_ = std::max(coresident_, 1);
     // (DBFS_PEER_SPLIT=0: the separate-GPU forms on a shared GPU anyway --
     // tests of the fused collectives and in-kernel waits with two ranks,
     // which cannot starve each other of CUs)
@@ -283,11 +289,12 @@ void PeerComm::release() {
   for (int p = 0; p < static_cast<int>(peer_.size()); ++p)
     if (ipc_ && p != rank_ && peer_[p]) hipIpcCloseMemHandle(peer_[p]);
   peer_.clear();
-  if (ticket_) hipFree(ticket_);
+  // (through the backend: deferred when it defers frees)
+  if (ticket_) be_ ? be_->dealloc(ticket_) : (void)hipFree(ticket_);
   ticket_ = nullptr;
-  if (dtab_) hipFree(dtab_);
+  if (dtab_) be_ ? be_->dealloc(dtab_) : (void)hipFree(dtab_);
   dtab_ = nullptr;
-  if (ftab_) hipFree(ftab_);
+  if (ftab_) be_ ? be_->dealloc(ftab_) : (void)hipFree(ftab_);
   ftab_ = nullptr;
   keep_.clear();
   if (win_keep_) win_keep_.reset();  // (in-process: frees with the last holder)
@@ -417,6 +424,11 @@ void PeerComm::run(const Plan& plan) {
   wa.timeout_ticks = static_cast<uint64_t>(limit * khz * 1000.0);
   wa.error = err_dev_;
   if (fused) {
+    // ranks sharing a GPU (DBFS_PEER_SPLIT=0): every workgroup of a fused
+    // launch spins on the peers' flags, so the co-resident ranks' launches
+    // together stay a small part of the chip (<= kPeerFusedGroups x 256
+    // threads per peer over all of them) -- a peer's producer always finds CUs
+    pa.max_groups = coresident_ > 1 ? std::max<int>(1, static_cast<int>(kern::kPeerFusedGroups) / coresident_) : 0;
     kern::peer_fused(pa, wa, ua, st);
     HIP_CHECK(hipGetLastError());
     ++peer_ops_;
@@ -813,7 +825,7 @@ void PeerComm::frontier_self_test() {
   if (rank_ == 0)
     std::fprintf(stderr, "[dbfs] peer communicator: frontier push off (self-test: %s)\n",
                  err.empty() ? "failed on a peer" : err.c_str());
-  hipFree(ftab_);
+  be_->dealloc(ftab_);
   ftab_ = nullptr;
 }
 
@@ -847,9 +859,9 @@ void PeerComm::direct_self_test() {
   if (rank_ == 0)
     std::fprintf(stderr, "[dbfs] peer communicator: direct exchanges off (self-test: %s)\n",
                  err.empty() ? "failed on a peer" : err.c_str());
-  hipFree(dtab_);
+  be_->dealloc(dtab_);
   dtab_ = nullptr;
-  if (ftab_) hipFree(ftab_);  // (needs the direct exchanges' self-test passed too)
+  if (ftab_) be_->dealloc(ftab_);  // (needs the direct exchanges' self-test passed too)
   ftab_ = nullptr;
 }
 

@@ -641,8 +641,14 @@ void DeviceLoop::emit_sparse(Chain& c) {
   // launch stays small
   const double est_mf = c.mf_hint >= 0 ? c.mf_hint : static_cast<double>(c.cap > 0 ? c.cap : list_max_);
   const double est_ids = est_mf * static_cast<double>(P_ - 1) / (static_cast<double>(P_) * P_);
-  const int64_t apply_grid =
+  int64_t apply_grid =
       std::max<int64_t>(1, std::min<int64_t>(opt_.td_apply_grid, static_cast<int64_t>(est_ids / 512.0) + 1));
+  // (ranks sharing a GPU with the waits inside the apply -- every workgroup
+  // spins on the peers' cells: at most 64 1024-thread workgroups over all of
+  // them, an eighth of the chip's residency, so a peer's td_sparse always
+  // finds CUs)
+  if (comm_.coresident() > 1 && !comm_.split_waits())
+    apply_grid = std::min<int64_t>(apply_grid, std::max(1, 64 / comm_.coresident()));
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)

@@ -1018,6 +1018,11 @@ class Backend {
   // memory (alloc/free are synchronous; copies/memsets are stream-ordered)
   virtual void* alloc(size_t bytes) = 0;
   virtual void dealloc(void* p) = 0;
+  // Device and mapped frees held until the backend is destroyed (HIP: several
+  // ranks of one process sharing a device -- a free waits for every stream of
+  // the device, a peer's spinning collective included); a no-op elsewhere.
+  virtual void set_deferred_frees(bool on) { (void)on; }
+  virtual bool deferred_frees() const { return false; }
   // Bytes held in DBufs of this backend now and at most so far: one rank's
   // device footprint (graph shard + traversal state; the peer transport's
   // windows are allocated outside DBufs and not counted).

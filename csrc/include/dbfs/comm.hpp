@@ -155,6 +155,12 @@ class Comm {
   // producer may need those CUs -- so the waits run as one-wave launches
   // first (Backend::direct_prewait) and the collectives unfused.
   virtual bool split_waits() const { return false; }
+  // Ranks of this communicator on this rank's GPU, itself included (peer
+  // transport; 1 elsewhere): with the in-kernel waits (no split_waits) the
+  // engine and the transport size every grid whose workgroups all spin on a
+  // peer so the co-resident ranks' grids together leave the chip room for
+  // the producers they wait for.
+  virtual int coresident() const { return 1; }
 
  protected:
   int level_tag_ = -1;
@@ -454,6 +460,7 @@ class PeerComm final : public Comm {
   bool frontier_on() const { return ftab_ != nullptr; }
   bool fused() const { return fused_; }
   bool split_waits() const override { return split_; }
+  int coresident() const override { return coresident_; }
   // Topology seen at construction: every rank's PCI bus id, and access[r * P
   // + p] = 2 (ranks r and p share a GPU), 1 (rank r's GPU can access p's),
   // 0 (it cannot), -1 (p's GPU not visible to rank r's process).
@@ -522,6 +529,7 @@ class PeerComm final : public Comm {
   // several ranks on one physical GPU (bus ids): unfused collectives, split
   // waits (split_; DBFS_PEER_SPLIT=0 keeps the separate-GPU forms)
   bool shared_ = false, split_ = false;
+  int coresident_ = 1;
   std::vector<std::string> bus_;
   std::vector<int> access_;
   std::string verdict_;

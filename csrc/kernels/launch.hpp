@@ -77,6 +77,9 @@ struct PeerPushArgs {
   int unit = 4;                     // copy granule (4, 8, 16 B; every size and address a multiple)
   uint64_t seq = 0;
   unsigned* ticket = nullptr;       // zero on entry; reset by the last workgroup
+  // the fused launch's workgroups per peer at most (0: kPeerFusedGroups) --
+  // ranks sharing a GPU with the in-kernel waits (PeerComm::coresident)
+  int max_groups = 0;
 };
 struct PeerWaitArgs {
   const uint64_t* flags = nullptr;  // this rank's window: one word per sender

@@ -260,7 +260,8 @@ void peer_fused(const PeerPushArgs& push, const PeerWaitArgs& wait, const PeerUn
   // one group of workgroups per peer, sized for the largest piece (at most
   // kPeerFusedGroups per peer: the push of 1 MiB per peer keeps every link busy)
   const int64_t per = (mx / push.unit + kFusedThreads - 1) / kFusedThreads;
-  const int64_t groups = per < 1 ? 1 : (per > kPeerFusedGroups ? kPeerFusedGroups : per);
+  const int64_t cap = push.max_groups > 0 && push.max_groups < kPeerFusedGroups ? push.max_groups : kPeerFusedGroups;
+  const int64_t groups = per < 1 ? 1 : (per > cap ? cap : per);
   peer_fused_kernel<<<static_cast<unsigned>(groups * push.npeers), kFusedThreads, 0, st>>>(push, wait, unpack);
 }
 

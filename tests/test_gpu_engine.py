@@ -1054,21 +1054,26 @@ def test_peer_comm_eight_ranks_share_one_gpu():
     assert rec["heldout"]["validated_roots"] == "8/8"
 
 
-def test_peer_fused_forms_two_ranks_share_one_gpu():
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_peer_fused_forms_share_one_gpu(ranks):
     """The separate-GPU forms of the peer transport -- every collective one
     fused launch, the direct exchanges' waits inside their consumer kernels
-    (DBFS_PEER_SPLIT=0 keeps them on a shared GPU) -- with two ranks on device
-    0, which cannot starve each other of CUs: every timed root validated."""
+    (DBFS_PEER_SPLIT=0 keeps them on a shared GPU) -- the forms the first
+    8-GPU run takes, with 2, 4 and 8 ranks on device 0.  Every grid whose
+    workgroups all spin on a peer is sized for the co-resident ranks
+    (Comm::coresident: the fused collectives' groups per peer, the owner
+    side's grid), so no rank starves a peer's producer of CUs: every timed
+    and held-out root validated."""
     import json
     import sys
 
-    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="16", DBFS_COMM_TIMEOUT_S="20",
-               DBFS_PEER_SPLIT="0")
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="8", DBFS_PEER_FRONTIER_MB="2",
+               DBFS_COMM_TIMEOUT_S="30", DBFS_PEER_SPLIT="0")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", "2", "--scale", "19", "--steps", "4",
-           "--warmup", "1", "--no-int32-pass", "--heldout-roots", "8", "--secondary", "none"]
-    out = _run_group(cmd, env, 100)
+    cmd = [sys.executable, "-u", os.path.join(REPO, "bench.py"), "--gpus", str(ranks), "--scale", "19", "--steps",
+           "4", "--warmup", "1", "--no-int32-pass", "--heldout-roots", "8", "--secondary", "none"]
+    out = _run_group(cmd, env, 140)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     topo = rec["comm_topology"]
@@ -1204,6 +1209,53 @@ def test_cli_peer_two_processes_share_one_gpu():
     assert "Output OK!" in o and "Validation OK" in o
     rec = json.loads([l for l in o.splitlines() if l.startswith("{")][-1])
     assert rec["comm"] == "peer+tcp" and rec["ranks"] == 2
+
+
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_cli_single_process_gpus_share_one_gpu(gpus):
+    """The reference's own execution model -- one process driving P GPUs
+    (bfs.cu:328-332, 577-609) -- as `bin/bfs --gpus P`, rehearsed on one GPU:
+    DBFS_DEVICE pins every rank's backend to device 0 and defers its frees
+    (Backend::set_deferred_frees), so the in-process peer transport runs with
+    split waits between rank threads that share the device.  Levels equal the
+    oracle ("Output OK!") and pass the Graph500 validator, several roots."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_COMM="peer", DBFS_PEER_SLOT_MB="4", DBFS_COMM_TIMEOUT_S="30")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    for src in ("5", "0"):
+        out = subprocess.run([os.path.join(REPO, "bin", "bfs"), "--gpus", str(gpus), "--rmat", "17", src, "--validate",
+                              "--json"], capture_output=True, text=True, timeout=110, env=env)
+        assert out.returncode == 0, out.stderr[-3000:]
+        assert "Output OK!" in out.stdout and "Validation OK" in out.stdout, out.stdout[-2000:]
+        rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+        assert rec["ranks"] == gpus and rec["comm"].startswith("peer+"), rec
+
+
+def test_cli_single_process_rccl_fallback_is_bounded():
+    """The --gpus P path's RCCL fallback (ncclCommInitAll's work as a group of
+    nonblocking inits, bounded by DBFS_RCCL_INIT_TIMEOUT_S): with the peer
+    transport's setup failing (DBFS_FAULT_INJECT kind=peer_init) two ranks on
+    device 0 either run over RCCL with exact levels or fail cleanly with an
+    RCCL error -- within the bound, never a hang."""
+    import subprocess
+    import time
+
+    env = dict(os.environ, DBFS_DEVICE="0", DBFS_FAULT_INJECT="kind=peer_init", DBFS_RCCL_INIT_TIMEOUT_S="20",
+               DBFS_COMM_TIMEOUT_S="20")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    t0 = time.time()
+    out = subprocess.run([os.path.join(REPO, "bin", "bfs"), "--gpus", "2", "--rmat", "14", "3"], capture_output=True,
+                         text=True, timeout=100, env=env)
+    elapsed = time.time() - t0
+    assert elapsed < 80
+    if out.returncode == 0:
+        assert "Output OK!" in out.stdout
+    else:
+        assert "RCCL" in out.stderr, out.stderr[-2000:]
 
 
 def test_in_process_peer_refuses_a_shared_device():
@@ -1349,6 +1401,20 @@ def _bench_peer(args, timeout=200, **env_extra):
     return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
 
 
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_all_reached_stop_peer_ranks(ranks):
+    """The all-reached stop with several ranks over the peer transport (direct
+    owner lists and level ends, pushed frontiers): self-spawned ranks on device
+    0 traverse a connected uniform graph of mean degree 28 in do mode, roots
+    back to back.  The stop leaves the last frontier (and any pushed slice of
+    it) unconsumed; every timed root is validated against the oracle, and the
+    stop must have fired."""
+    rec = _bench_peer(["--gpus", str(ranks), "--uniform", "262144:3670016", "--mode", "do", "--steps", "6",
+                       "--warmup", "1"])
+    assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
+    assert rec["all_reached_stops"] > 0
+
+
 def test_peer_slot_rounds_build_and_ingest(tmp_path):
     """Collectives larger than a window slot go through the windows in
     slot-sized rounds (PeerComm::rounds), never to the wrapped transport: two
@@ -1409,14 +1475,21 @@ def test_peer_direct_frontier(opts):
 @pytest.mark.gpu
 @pytest.mark.parametrize("parts", [2, 4])
 @pytest.mark.parametrize("mode", ["td", "do"])
-def test_split_levels_gpu(gpu_runtime, parts, mode):
+@pytest.mark.parametrize("bits", [False, True])
+def test_split_levels_gpu(gpu_runtime, parts, mode, bits):
     """Split top-down levels on the GPU (TdArgs::split_k: each part a run of
     the edge steps, refresh_visited between parts, the update forced): every
-    level-byte top-down level split, levels exact against the oracle."""
+    direct top-down level split, levels exact against the oracle.  bits: the
+    device picks the bitmap form for every level (td_direct_edges above the
+    graph's edges, ctrl->bytes 0) -- the parts claim into `next` and the
+    refreshes between them find no level bytes."""
     p = dbfs.rmat_params(18, 16, 23)
     csr = dbfs.host_csr_from_params(p)
     b = dbfs.BFS(p, gpu_runtime, mode=mode)
-    b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
+    if bits:
+        b.engine.set_option("td_direct_edges", float(1 << 40))
+    else:
+        b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
     b.engine.set_option("td_split_edges", 1)
     b.engine.set_option("td_split_parts", parts)
     b.engine.set_option("td_range_edges", 0)
