@@ -234,9 +234,11 @@ def comm_topology(rt):
 
 
 def secondary_block(dbfs, rt, params, graph: str, nroots: int, seed: int, args):
-    """One of the metric's second-graph stand-ins (soc-LiveJournal1-sized,
-    generated on the device) in td and do modes: 2 warm-up roots, then
-    `nroots` timed and validated, per mode."""
+    """One of the metric's second-graph stand-ins (soc-LiveJournal1-sized, or
+    the high-diameter road-like grid; generated on the device) in td and do
+    modes: 2 warm-up roots, then `nroots` timed and validated, per mode --
+    with the mean depth and the time per level (the per-level latency a
+    high-diameter traversal is made of)."""
     t0 = time.time()
     g = dbfs.BFS(params, rt, mode="td", alpha=args.alpha, beta=args.beta, bu_lane_limit=args.bu_lane_limit)
     for kv in args.opt:  # (the primary engine's --opt settings apply here too)
@@ -251,10 +253,13 @@ def secondary_block(dbfs, rt, params, graph: str, nroots: int, seed: int, args):
         for r in roots[:2]:
             g.run(r)
         gteps, ms, ok, res = validated_pass(g, rt, roots[2:])
+        depth = sum(x.depth for x in res) / len(res)
         out[mode] = {"value": round(gteps, 4), "ms_per_step": round(ms, 4),
                      "harmonic_mean_gteps": round(len(res) / sum(1.0 / max(x.gteps, 1e-12) for x in res), 4),
+                     "depth_mean": round(depth, 1), "us_per_level": round(1e3 * ms / max(depth, 1.0), 3),
                      "validated_roots": f"{ok}/{len(res)}"}
-        log(f"secondary {graph} {mode}: {gteps:.2f} GTEPS ({ms:.4f} ms/root), validated {ok}/{len(res)}")
+        log(f"secondary {graph} {mode}: {gteps:.2f} GTEPS ({ms:.4f} ms/root, depth {depth:.0f}, "
+            f"{1e3 * ms / max(depth, 1.0):.2f} us/level), validated {ok}/{len(res)}")
     del g
     return out
 
@@ -427,6 +432,13 @@ def main(argv=None) -> int:
             f"power-law (Chung-Lu, degree tail exponent 2.5, max expected degree {dmax}) {n2} V / {m2} E "
             + ("(soc-LiveJournal1's size and largest degree; synthetic)" if lj else "(synthetic)"),
             args.secondary_roots, args.seed + 200, args)
+        if lj:
+            # the high-diameter case: a 1024 x 1024 road-like
+            # grid, ~1000-2000 levels of a few hundred vertices each
+            secondary["road_grid"] = secondary_block(
+                dbfs, rt, dbfs.grid_params(1024, 1024),
+                "2-D grid 1024 x 1024 (road-like: degree <= 4, diameter 2046; synthetic)",
+                max(4, args.secondary_roots // 4), args.seed + 300, args)
         for blk in secondary.values():
             for m in ("td", "do"):
                 ok, tot = blk[m]["validated_roots"].split("/")

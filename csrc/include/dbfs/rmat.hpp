@@ -38,6 +38,10 @@ struct GenParams {
   bool uniform = false;       // uniform random instead of RMAT
   bool power_law = false;     // Chung-Lu power law instead of RMAT (below)
   bool scramble = true;       // permute RMAT / power-law vertex labels
+  // > 0: a 2-D grid of grid_w columns and n / grid_w rows, each vertex joined
+  // to its right and lower neighbour -- road-like (degree <= 4, diameter
+  // grid_w + n / grid_w - 2), the high-diameter case; labels row-major
+  int64_t grid_w = 0;
   // Power law, inverse-CDF sampling in 32.32 fixed point (integer arithmetic
   // only, so host and device agree bit for bit): an endpoint is
   // floor(t^3) - pl_i0 with t = pl_a + r * pl_span (r uniform in [0, 1)),
@@ -104,6 +108,20 @@ DBFS_HD uint64_t power_law_vertex(const GenParams& p, uint64_t r) {
 
 // Edge i of the stream described by p.
 DBFS_HD void gen_edge(const GenParams& p, uint64_t i, uint64_t& u, uint64_t& v) {
+  if (p.grid_w > 0) {
+    // edges [0, (w - 1) h) horizontal, row-major; the rest vertical
+    const uint64_t w = static_cast<uint64_t>(p.grid_w), h = static_cast<uint64_t>(p.n) / w;
+    const uint64_t he = (w - 1) * h;
+    if (i < he) {
+      const uint64_t r = i / (w - 1);
+      u = r * w + (i - r * (w - 1));
+      v = u + 1;
+    } else {
+      u = i - he;
+      v = u + w;
+    }
+    return;
+  }
   const uint64_t base = mix64(p.seed * 0xD1B54A32D192ED03ull ^ mix64(i));
   if (p.power_law) {
     u = power_law_vertex(p, mix64(base + 1));
@@ -161,6 +179,17 @@ inline GenParams uniform_params(int64_t n, int64_t m, uint64_t seed) {
   p.n = n;
   p.m = m;
   p.seed = seed;
+  return p;
+}
+
+// The w x h grid (GenParams::grid_w): n = w h vertices, (w - 1) h + w (h - 1)
+// edges.
+inline GenParams grid_params(int64_t w, int64_t h) {
+  GenParams p;
+  p.grid_w = w;
+  p.scramble = false;
+  p.n = w * h;
+  p.m = (w - 1) * h + w * (h - 1);
   return p;
 }
 

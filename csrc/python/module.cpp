@@ -208,10 +208,12 @@ PYBIND11_MODULE(_dbfs_native, m) {
       .def_readonly("power_law", &GenParams::power_law)
       .def_readonly("pl_i0", &GenParams::pl_i0)
       .def_readonly("pl_dmax", &GenParams::pl_dmax)
+      .def_readonly("grid_w", &GenParams::grid_w)
       .def_readwrite("scramble", &GenParams::scramble);
   m.def("rmat_params", &rmat_params, py::arg("scale"), py::arg("edge_factor") = 16, py::arg("seed") = 1);
   m.def("uniform_params", &uniform_params, py::arg("n"), py::arg("m"), py::arg("seed") = 1);
   m.def("power_law_params", &power_law_params, py::arg("n"), py::arg("m"), py::arg("dmax"), py::arg("seed") = 1);
+  m.def("grid_params", &grid_params, py::arg("w"), py::arg("h"));
   m.def(
       "generate_edges",
       [](const GenParams& p, int64_t begin, int64_t end) {

@@ -15,7 +15,7 @@ Layout
 from ._native import N as native  # noqa: F401  (fails loudly if the core is not built)
 from .models.bfs import BFS, BFSResult, MODES  # noqa: F401
 from .ops.graph import (  # noqa: F401
-    read_graph, read_edge_list, detect_format, build_csr, rmat_params, uniform_params, power_law_params, generate_edges,
+    read_graph, read_edge_list, detect_format, build_csr, rmat_params, uniform_params, power_law_params, grid_params, generate_edges,
     host_csr_from_params, cpu_bfs, write_binary_csr, write_levels)
 from .parallel.partition import Partition  # noqa: F401
 from .parallel.runtime import Runtime, init_runtime  # noqa: F401

@@ -51,6 +51,14 @@ def power_law_params(n: int, m: int, dmax: int, seed: int = 1):
     return N.power_law_params(int(n), int(m), int(dmax), int(seed))
 
 
+def grid_params(w: int, h: int):
+    """The w x h grid graph (each vertex joined to its right and lower
+    neighbour; row-major labels): road-like, degree <= 4, diameter w + h - 2
+    -- the high-diameter case, where a traversal is thousands of tiny levels
+    and the per-level latency is everything.  Generated on the device."""
+    return N.grid_params(int(w), int(h))
+
+
 # soc-LiveJournal1 (SNAP: 4,847,571 V, 68,993,773 E; largest undirected degree
 # 20,333) and Friendster (65,608,366 V, 1,806,067,135 E; degrees capped at
 # 5,000 friends, largest 5,214): (n, m, dmax) of their power-law stand-ins.

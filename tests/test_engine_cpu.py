@@ -791,3 +791,40 @@ def test_split_levels_cpu(parts, mode):
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
         used = used or any(c[7] in (parts, 2 * parts) for c in r.chains)
     assert used
+
+
+def test_grid_generator_shape():
+    # 2-D grid (road-like): row-major labels, right and lower neighbours
+    p = dbfs.grid_params(7, 5)
+    assert p.n == 35 and p.m == 6 * 5 + 7 * 4
+    csr = dbfs.host_csr_from_params(p)
+    deg = np.diff(np.asarray(csr.row_off)).reshape(5, 7)
+    assert deg[0, 0] == 2 and deg[2, 3] == 4 and deg[0, 3] == 3
+    lv = _oracle(csr, 0).reshape(5, 7)
+    assert np.array_equal(lv, np.add.outer(np.arange(5), np.arange(7)))
+
+
+@pytest.mark.parametrize("mode", ["td", "do", "bu"])
+@pytest.mark.parametrize("P", [1, 3])
+def test_high_diameter_grid(mode, P):
+    """A 48 x 40 grid: 86 levels from a corner (past the one-byte levels'
+    62: the traversal reruns with 32-bit levels), tiny frontiers throughout
+    -- the per-level path every level takes; exact against the oracle, on one
+    and on three virtual ranks."""
+    p = dbfs.grid_params(48, 40)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [0, 48 * 20 + 24, 48 * 40 - 1]
+    exp = [_oracle(csr, s) for s in srcs]
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        out = []
+        for s in srcs:
+            r = bfs.run(s)
+            out.append((bfs.levels(), r.depth))
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="cpu"):
+        for (lv, depth), e in zip(rank_out, exp):
+            assert np.array_equal(lv, e)
+            assert depth == int(e.max()) + 1

@@ -1500,3 +1500,29 @@ def test_split_levels_gpu(gpu_runtime, parts, mode, bits):
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
         used = used or any(c[7] in (parts, 2 * parts) for c in r.chains)
     assert used
+
+
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("mode", ["td", "do"])
+def test_high_diameter_grid_gpu(P, mode):
+    """The road-like 2-D grid (256 x 200: 454 levels from a corner, a few
+    hundred vertices each): past the one-byte levels, hundreds of tiny
+    sparse levels in a row through the device loop -- every one stamped and
+    exact against the oracle, one rank and three virtual ranks."""
+    p = dbfs.grid_params(256, 200)
+    csr = dbfs.host_csr_from_params(p)
+    srcs = [0, 256 * 100 + 128, 256 * 200 - 1, 0]
+    exp = {s: dbfs.cpu_bfs(csr, s)[0] for s in set(srcs)}
+
+    def body(rt):
+        bfs = dbfs.BFS(p, rt, mode=mode)
+        out = []
+        for s in srcs:
+            res = bfs.run(s)
+            out.append((s, res, bfs.levels()))
+        return out
+
+    for rank_out in run_virtual_ranks(P, body, device="hip"):
+        for s, res, lv in rank_out:
+            assert np.array_equal(lv, exp[s]), _describe(s, res, lv, exp[s])
+            assert res.depth == int(exp[s].max()) + 1
