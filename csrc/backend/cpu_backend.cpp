@@ -664,16 +664,6 @@ class CpuBackend final : public Backend {
     for (int64_t r = 0; r < rows; ++r) std::sort(col + ro[r], col + ro[r + 1]);
   }
 
-  void range_split(const eid_t* ro, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
-                   uint32_t* out) override {
-    for (int y = 1; y < ranges; ++y)
-      for (int64_t r = 0; r < rows; ++r) {
-        const uint64_t key = static_cast<uint64_t>(y * span) >> shift;
-        const vid_t* p = std::partition_point(col + ro[r], col + ro[r + 1],
-                                              [&](vid_t v) { return (static_cast<uint64_t>(v) >> shift) < key; });
-        out[static_cast<int64_t>(y - 1) * rows + r] = static_cast<uint32_t>(p - (col + ro[r]));
-      }
-  }
   void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
     for (int64_t e = 0; e < nnz; ++e) out[e] = hub_idx[col[e]] != 0xFFFFFFFFu ? (kHubFlag | hub_idx[col[e]]) : col[e];
   }

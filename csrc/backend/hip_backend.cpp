@@ -298,12 +298,6 @@ class HipBackend final : public Backend {
     chk();
   }
 
-  void range_split(const eid_t* ro, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
-                   uint32_t* out) override {
-    on();
-    kern::range_split(ro, col, rows, span, shift, ranges, out, st_);
-    chk();
-  }
   void encode_hub_cols(const vid_t* col, int64_t nnz, const uint32_t* hub_idx, vid_t* out) override {
     on();
     kern::encode_hub_cols(col, nnz, hub_idx, out, st_);

@@ -72,7 +72,6 @@ class DeviceLoop {
   int64_t sparse_cap_ = 0;
   int64_t list_max_ = 0, xsparse_lim_ = 0, fuse_cap_ = 0;
   bool lists_unlimited_ = false, counted_ = false;
-  bool range_ok_ = false;  // one rank: range-staged top-down levels available
   double vis_hint_ = -1.0;  // the next enqueued level's visited degree sum at its start (< 0 unknown)
   double reach_hint_ = -1.0;  // ... and its reached vertices with an edge (< 0 unknown)
   int bin_shift_ = 12;
@@ -279,14 +278,6 @@ void DeviceLoop::setup() {
     e_.bin_cnt_ = DBuf<uint32_t>(be_, static_cast<size_t>(nbins_ * kBinGrid));
     e_.bin_buf_ = DBuf<vid_t>(be_, static_cast<size_t>(e_.g_.nnz()));  // a level's frontier edges <= nnz
   }
-  // One rank: range-staged top-down levels (the rows' range split points,
-  // built once per graph; the work list's entry -> row map comes from the
-  // sparse levels' machinery)
-  range_ok_ = false;
-  if (!xc_ && sparse_ && opt_.td_range_edges > 0 && opt_.mode != Mode::BottomUp) {
-    if (!e_.range_built_) e_.build_range_split();
-    range_ok_ = e_.range_count_ > 0;
-  }
   if (e_.n_active_ < 0) {
     // (outside the timed window, once) the mean degree of an edge's endpoint
     // (sum deg^2 / sum deg) predicts the edges of level 1's frontier (the
@@ -301,8 +292,8 @@ void DeviceLoop::setup() {
     e_.n_active_ = mom[1];
   }
   const int64_t td_blocks = div_up(e_.g_.nnz(), kTdEdgesPerBlock);
-  td_grid_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_max, 1)));
-  td_grid_filter_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, std::max<int64_t>(opt_.td_grid_filter_max, 1)));
+  td_grid_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, opt_.td_grid_max));
+  td_grid_filter_ = std::max<int64_t>(1, std::min<int64_t>(td_blocks, opt_.td_grid_filter_max));
   if (e_.fault_.kind == "late_wg")
     late_ticks_ = static_cast<uint64_t>(static_cast<double>(e_.fault_.us) * be_.wall_clock_khz() / 1000.0);
   // Mailbox stamps can be reset although the previous run did not end with a
@@ -633,7 +624,7 @@ void DeviceLoop::emit_sparse(Chain& c) {
   // the exchange itself: by the two kernels through the peers' windows
   // (direct), or a collective between them
   const size_t lcap = static_cast<size_t>(c.cap > 0 ? c.cap : list_max_);
-  const bool direct = opt_.direct_lists && comm_.direct_lists(lcap, &sp.direct);
+  const bool direct = comm_.direct_lists(lcap, &sp.direct);
   sp.nranks = P_;
   // the owners' side sized by its expected ids (a rank receives about
   // mf (P - 1) / P^2 claims): ~512 per workgroup, up to td_apply_grid -- the
@@ -652,7 +643,7 @@ void DeviceLoop::emit_sparse(Chain& c) {
   // the level's end folded into the apply's last workgroup (no frontier
   // gather: that one is a bandwidth collective of its own)
   // (the cells carry < 2^32 new vertices and < 2^40 degrees per rank)
-  const bool end_ok = direct && opt_.direct_level_end && cells_fit() && !enq_gather_[L];
+  const bool end_ok = direct && cells_fit() && !enq_gather_[L];
   // a tiny level (its chain capped at fuse_cap): td_sparse's last workgroup
   // also runs the owner side and the level end -- one launch (the direct
   // level end is taken in the same order as unfused)
@@ -767,23 +758,13 @@ void DeviceLoop::emit_dense(Chain& c) {
   UpdateArgs tu = ua_;
   ta.next = e_.next_.data();
   ta.next_bytes = e_.next_bytes_.data();
-  // range-staged (one rank, large levels): every probe in LDS, no hub filter
-  const bool ranged = range_ok_ && c.pf != 'I' && c.mf_hint >= static_cast<double>(opt_.td_range_edges) &&
-                      vis_hint_ >= 0 && vis_hint_ <= opt_.td_range_vis_frac * static_cast<double>(e_.total_directed_);
-  if (ranged) {
-    res_.chains.back().ranged = true;
-    ta.range_split = e_.range_split_.data();
-    ta.range_qv = e_.qv_[L & 1].data();
-    ta.ranges = e_.range_count_;
-    ta.range_span = e_.range_span_;
-  }
   // late large levels: the unvisited filter (launched next to the plain
   // variant; the filter's density picks the one that runs)
   // (and, with the count of vertices with an edge known, a filter expected
   // at most 1.5 x td_unvis_max_density dense: u of the vertices unvisited,
   // n / kUnvisBits per bit -- so a hub-heavy level whose visited edges are
   // many but whose unvisited vertices are too launches nothing extra)
-  bool unvis = !ranged && opt_.td_unvis_edges > 0 && c.mf_hint >= static_cast<double>(opt_.td_unvis_edges) &&
+  bool unvis = opt_.td_unvis_edges > 0 && c.mf_hint >= static_cast<double>(opt_.td_unvis_edges) &&
                vis_hint_ >= opt_.td_unvis_vis_frac * static_cast<double>(e_.total_directed_);
   if (unvis && e_.n_active_ > 0 && reach_hint_ >= 0) {
     const double u = std::max(0.0, static_cast<double>(e_.n_active_) - reach_hint_) / static_cast<double>(gv_.n);
@@ -812,7 +793,7 @@ void DeviceLoop::emit_dense(Chain& c) {
   }
   // (skipped for levels predicted well below the filter's threshold: the
   // snapshot kernel would only find its gate closed)
-  if (!ranged && gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 && e_.g_.td_hub_share() >= opt_.td_hub_min_share &&
+  if (gv_.td_nhubs > 0 && opt_.td_hub_edges > 0 && e_.g_.td_hub_share() >= opt_.td_hub_min_share &&
       (c.mf_hint < 0 || c.mf_hint * 4.0 >= static_cast<double>(opt_.td_hub_edges))) {
     // large levels: the hubs' visited bits, staged in LDS by td_expand
     if (!e_.td_hub_vis_.data())
@@ -838,7 +819,7 @@ void DeviceLoop::emit_dense(Chain& c) {
     ta.new_level = L + 1;
     tu.level_direct = e_.level8_.data();
     tu.narrow_base = e_.narrow_base_;
-    if (ta.td_hub_vis && opt_.td_hub_mark) {
+    if (ta.td_hub_vis) {
       if (!e_.td_hub_mark_.data()) {
         e_.td_hub_mark_ = DBuf<uint8_t>(be_, static_cast<size_t>(kTdMaxHubs));
         be_.memset_async(e_.td_hub_mark_.data(), 0, e_.td_hub_mark_.bytes());
@@ -851,7 +832,7 @@ void DeviceLoop::emit_dense(Chain& c) {
   // (not with the unvisited filter: a late level claims few vertices, and
   // every part would stage the filter and launch both variants again --
   // RMAT-22's level 4 87 -> 134 us in 4 parts)
-  const int parts = (ta.level_direct && !ranged && !unvis && !xc_ && opt_.td_split_edges > 0 && opt_.td_split_parts > 1 &&
+  const int parts = (ta.level_direct && !unvis && !xc_ && opt_.td_split_edges > 0 && opt_.td_split_parts > 1 &&
                      c.mf_hint >= static_cast<double>(opt_.td_split_edges))
                         ? opt_.td_split_parts * (c.mf_hint >= 16.0 * static_cast<double>(opt_.td_split_edges) &&
                                                          gv_.n >= (int64_t(1) << 25)
@@ -927,7 +908,7 @@ void DeviceLoop::emit_dense(Chain& c) {
     fuse_update(c, tu);
     // several ranks: the level's end in the same last workgroup (no frontier
     // gathered, or a pushed one)
-    if (xc_ && opt_.direct_level_end && cells_fit() && (!enq_gather_[L] || c.push) &&
+    if (xc_ && cells_fit() && (!enq_gather_[L] || c.push) &&
         comm_.direct_level_end(2, &tu.end)) {
       tu.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;
@@ -1038,7 +1019,7 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     // (not on a hub-cut level -- one rank with a forced exchange: its plain
     // and cut kernels are both launched, and only the plain ones have the
     // folded end)
-    if (xc_ && opt_.direct_level_end && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !cut &&
+    if (xc_ && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !cut &&
         comm_.direct_level_end(2, &ba.end)) {
       ba.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;

@@ -61,23 +61,14 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "phase_timing") o.phase_timing = v != 0;
   else if (name == "device_loop") o.device_loop = v != 0;
   else if (name == "device_loop_predict") o.device_loop_predict = v != 0;
-  else if (name == "device_loop_ranks") o.device_loop_ranks = v != 0;
-  else if (name == "stats_mailbox") o.stats_mailbox = v != 0;
   else if (name == "directed") o.directed = v != 0;
   else if (name == "bu_whole_units") o.bu_whole_units = static_cast<int>(v);
   else if (name == "bu_small_waves") o.bu_small_waves = static_cast<int>(v);
   else if (name == "narrow_levels") o.narrow_levels = v != 0;
-  else if (name == "narrow_epochs") o.narrow_epochs = v != 0;
   else if (name == "td_sparse_edges") o.td_sparse_edges = static_cast<int64_t>(v);
-  else if (name == "td_sparse_bu_edges") o.td_sparse_bu_edges = static_cast<int64_t>(v);
   else if (name == "td_sparse_bits") o.td_sparse_bits = v != 0;
-  else if (name == "bu_fused_scan") o.bu_fused_scan = v != 0;
-  else if (name == "td_fused_finish") o.td_fused_finish = v != 0;
   else if (name == "td_bin_edges") o.td_bin_edges = static_cast<int64_t>(v);
   else if (name == "td_bin_min_rows") o.td_bin_min_rows = static_cast<int64_t>(v);
-  else if (name == "td_range_edges") o.td_range_edges = static_cast<int64_t>(v);
-  else if (name == "td_range_words") o.td_range_words = static_cast<int64_t>(v);
-  else if (name == "td_range_vis_frac") o.td_range_vis_frac = v;
   else if (name == "td_unvis_edges") o.td_unvis_edges = static_cast<int64_t>(v);
   else if (name == "td_unvis_vis_frac") o.td_unvis_vis_frac = v;
   else if (name == "td_unvis_max_density") o.td_unvis_max_density = v;
@@ -85,9 +76,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "td_split_parts") o.td_split_parts = std::max(1, static_cast<int>(v));
   else if (name == "td_hub_edges") o.td_hub_edges = static_cast<int64_t>(v);
   else if (name == "td_hub_vis_frac") o.td_hub_vis_frac = v;
-  else if (name == "td_hub_mark") o.td_hub_mark = v != 0;
-  else if (name == "td_grid_max") o.td_grid_max = static_cast<int64_t>(v);
-  else if (name == "td_grid_filter_max") o.td_grid_filter_max = static_cast<int64_t>(v);
   else if (name == "td_direct_edges") o.td_direct_edges = static_cast<int64_t>(v);
   else if (name == "list_form_edges") o.list_form_edges = static_cast<int64_t>(v);
   else if (name == "xsparse_edges") o.xsparse_edges = static_cast<int64_t>(v);
@@ -96,8 +84,6 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
   else if (name == "bu_cut_mf_frac") o.bu_cut_mf_frac = v;
   else if (name == "list_cap_factor") o.list_cap_factor = v;
-  else if (name == "direct_lists") o.direct_lists = v != 0;
-  else if (name == "direct_level_end") o.direct_level_end = v != 0;
   else if (name == "direct_frontier") o.direct_frontier = v != 0;
   else throw Error("unknown engine option '" + name + "'");
 }
@@ -115,23 +101,14 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"phase_timing", o.phase_timing ? 1.0 : 0.0},
           {"device_loop", o.device_loop ? 1.0 : 0.0},
           {"device_loop_predict", o.device_loop_predict ? 1.0 : 0.0},
-          {"device_loop_ranks", o.device_loop_ranks ? 1.0 : 0.0},
-          {"stats_mailbox", o.stats_mailbox ? 1.0 : 0.0},
           {"directed", o.directed ? 1.0 : 0.0},
           {"bu_whole_units", static_cast<double>(o.bu_whole_units)},
           {"bu_small_waves", static_cast<double>(o.bu_small_waves)},
           {"td_sparse_edges", static_cast<double>(o.td_sparse_edges)},
-          {"td_sparse_bu_edges", static_cast<double>(o.td_sparse_bu_edges)},
           {"td_sparse_bits", o.td_sparse_bits ? 1.0 : 0.0},
-          {"bu_fused_scan", o.bu_fused_scan ? 1.0 : 0.0},
-          {"td_fused_finish", o.td_fused_finish ? 1.0 : 0.0},
           {"narrow_levels", o.narrow_levels ? 1.0 : 0.0},
-          {"narrow_epochs", o.narrow_epochs ? 1.0 : 0.0},
           {"td_bin_edges", static_cast<double>(o.td_bin_edges)},
           {"td_bin_min_rows", static_cast<double>(o.td_bin_min_rows)},
-          {"td_range_edges", static_cast<double>(o.td_range_edges)},
-          {"td_range_words", static_cast<double>(o.td_range_words)},
-          {"td_range_vis_frac", o.td_range_vis_frac},
           {"td_unvis_edges", static_cast<double>(o.td_unvis_edges)},
           {"td_unvis_vis_frac", o.td_unvis_vis_frac},
           {"td_unvis_max_density", o.td_unvis_max_density},
@@ -139,9 +116,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"td_split_parts", static_cast<double>(o.td_split_parts)},
           {"td_hub_edges", static_cast<double>(o.td_hub_edges)},
           {"td_hub_vis_frac", o.td_hub_vis_frac},
-          {"td_hub_mark", o.td_hub_mark ? 1.0 : 0.0},
-          {"td_grid_max", static_cast<double>(o.td_grid_max)},
-          {"td_grid_filter_max", static_cast<double>(o.td_grid_filter_max)},
           {"td_direct_edges", static_cast<double>(o.td_direct_edges)},
           {"list_form_edges", static_cast<double>(o.list_form_edges)},
           {"xsparse_edges", static_cast<double>(o.xsparse_edges)},
@@ -150,8 +124,6 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
           {"bu_cut_mf_frac", o.bu_cut_mf_frac},
           {"list_cap_factor", o.list_cap_factor},
-          {"direct_lists", o.direct_lists ? 1.0 : 0.0},
-          {"direct_level_end", o.direct_level_end ? 1.0 : 0.0},
           {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
 }
 
@@ -527,10 +499,6 @@ Engine::~Engine() {
 // Totals of the level just scanned (stats[0..3]: local count, local degree
 // sum, global count, global degree sum) to the host.
 void Engine::read_level_stats(int64_t* host_stats) {
-  if (!opt_.stats_mailbox) {
-    be_.to_host(host_stats, stats_.data(), 4 * sizeof(int64_t));
-    return;
-  }
   if (!stats_mb_host_) {
     void* dptr = nullptr;
     stats_mb_host_ = static_cast<StatsMailbox*>(be_.alloc_mapped(sizeof(StatsMailbox), &dptr));
@@ -681,39 +649,6 @@ void Engine::alloc_bitmap_state() {
   bitmap_ready_ = true;
 }
 
-// Range-staged top-down levels: R ranges of at most kRangeWords visited
-// words, each a multiple of 64 vertices and of the id bucket sort_rows_by_id
-// orders long rows by (2^shift ids), and the rows' split positions at the
-// R - 1 inner boundaries ((R - 1) x rows x 4 B: soc-LiveJournal1's size 194 MB).
-// Once per graph, outside any timed window; range_count_ stays 0 when the graph
-// does not qualify (several ranks, rows not in id order, too many vertices).
-void Engine::build_range_split() {
-  range_built_ = true;
-  range_count_ = 0;
-  range_split_.reset();
-  const int64_t n = part_.n;
-  if (part_.nranks != 1 || !g_.col_by_id() || n <= 0 || g_.rows() != n || g_.nnz() <= 0 ||
-      g_.nnz() > (int64_t(1) << 32))
-    return;
-  int bits = 0;
-  while ((int64_t(1) << bits) < n) ++bits;
-  const int shift = bits > 12 ? bits - 12 : 0;
-  const int64_t align = std::max<int64_t>(kWordBits, int64_t(1) << shift);
-  const int64_t cap = std::min<int64_t>(std::max<int64_t>(opt_.td_range_words, 1), kRangeWords) * kWordBits;
-  for (int R = static_cast<int>(div_up(n, cap)); R <= kRangeMax; ++R) {
-    const int64_t span = div_up(div_up(n, R), align) * align;
-    if (span > cap) continue;
-    const int ranges = static_cast<int>(div_up(n, span));
-    if (ranges > 1) {
-      range_split_ = DBuf<uint32_t>(be_, static_cast<size_t>(ranges - 1) * static_cast<size_t>(n));
-      be_.range_split(g_.view().row_off, g_.view().col, n, span, shift, ranges, range_split_.data());
-    }
-    range_count_ = ranges;
-    range_span_ = span;
-    return;
-  }
-}
-
 void Engine::alloc_ref_state() {
   const int P = part_.nranks;
   const int64_t cap = part_.part;
@@ -750,7 +685,7 @@ RunResult Engine::run(int64_t source) {
   }
   level8_filled_ = false;
   narrow_base_ = 0;
-  if (run_narrow_ && opt_.narrow_epochs) {
+  if (run_narrow_) {
     // Level bytes are stored as base + level with base cycling through
     // kNarrowEpochs values: the previous epochs' bytes (and the 0xFF fill)
     // lie outside this run's [base, base + kNarrowMaxLevel], so they already
@@ -1161,7 +1096,7 @@ LevelRecDev* Engine::rec_at(int level) {
 }
 
 bool Engine::use_device_loop() const {
-  return opt_.device_loop && (!exchange() || opt_.device_loop_ranks) &&
+  return opt_.device_loop &&
          (opt_.mode == Mode::TopDown || opt_.mode == Mode::BottomUp || opt_.mode == Mode::DirOpt);
 }
 

@@ -133,12 +133,6 @@ constexpr int kFoldScanUnits = 8192;
 constexpr int kTdThreads = 256;
 constexpr int kTdItems = 8;
 constexpr int kTdEdgesPerBlock = kTdThreads * kTdItems;
-// Range-staged top-down levels (TdArgs::range_split): the vertices are cut
-// into at most kRangeMax ranges of at most kRangeWords visited words (56 KiB
-// of LDS: two 1024-thread workgroups per CU with their owner maps), so graphs
-// of up to kRangeMax x kRangeWords x 64 (7.3 M) vertices.
-constexpr int kRangeWords = 7168;
-constexpr int kRangeMax = 16;
 
 // ---- device-driven level loop (one rank) -------------------------------------
 // The host enqueues level L+1 before level L has finished; every kernel of a
@@ -660,20 +654,6 @@ struct TdArgs {
   // iff at most unvis_max_density of the filter's bits are set
   const uint32_t* unvis_pop = nullptr;
   double unvis_max_density = 0.5;
-  // Range-staged level (one rank, device loop, at most 2^32 adjacency
-  // entries, rows in id order -- graph_sort's buckets for long rows): each
-  // workgroup takes a contiguous run of edge blocks and sweeps the vertex
-  // ranges one at a time: the range's visited bits staged in LDS, then the
-  // part of every row of the run that lands in the range (range_split:
-  // (ranges - 1) x rows row positions, the first entry of range y >= 1 in row
-  // r at [(y - 1) * rows + r]), claims deduplicated in the LDS copy.  The
-  // visited probe of an edge is an LDS read instead of a scattered L2 request,
-  // and a target is stored once per workgroup.  Output as the byte-map /
-  // bitmap modes above.  range_qv: entry -> row.
-  const uint32_t* range_split = nullptr;
-  const vid_t* range_qv = nullptr;
-  int ranges = 0;
-  int64_t range_span = 0;  // vertices per range (a multiple of 64 and of the long rows' id bucket)
   // Launch 1024-thread workgroups when the grid has fewer blocks than this.
   int64_t wide_below_blocks = 0;
   // Device loop: q / m come from dev_stats[0..1], bits vs bytes and the
@@ -1129,12 +1109,6 @@ class Backend {
   // Every row in neighbour-id order (n: vertex count; the device orders rows
   // of more than 4096 entries by 4096 id buckets only).
   virtual void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n) = 0;
-  // Range-staged top-down levels (TdArgs::range_split): out[(y - 1) * rows + r]
-  // = the first position of row r (rows in id order, or in id buckets of
-  // 2^shift ids) whose neighbour is >= y * span, for y = 1 .. ranges - 1
-  // (span a multiple of 2^shift).
-  virtual void range_split(const eid_t* row_off, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
-                           uint32_t* out) = 0;
   // head[r] = col[row_off[r]] (0 for empty rows); with hub_idx (one entry per
   // vertex, UINT32_MAX for non-hubs) a hub head is stored as kHubFlag | index.
   virtual void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head,

@@ -165,27 +165,6 @@ struct EngineOptions {
   // binned level: 256 / 512 / 1024 bins 407 / 417 / 441 us (more bins: the
   // fill pass scatters into more open lines).
   static constexpr int64_t td_bin_log2_bins = 8;
-  // One rank, graphs of at most kRangeMax x kRangeWords x 64 vertices with
-  // id-ordered rows: dense top-down levels predicted at >= td_range_edges
-  // frontier edges are range-staged (TdArgs::range_split: the vertex ranges
-  // swept one at a time with their visited bits in LDS, claims deduplicated
-  // there) instead of td_expand's scattered visited probes; 0 disables.
-  // Off by default since split top-down levels: the LJ-sized graph's level it
-  // served (the store-bound one) runs split instead, top-down only 81.5 ->
-  // 92.0 GTEPS; power-law +0.5 %, RMAT-22 flat (profiles/r5_td_range_vs_split.txt).
-  int64_t td_range_edges = 0;
-  // ... ranges of at most this many visited words (<= kRangeWords; smaller
-  // forces more ranges -- tests on small graphs)
-  int64_t td_range_words = kRangeWords;
-  // ... and only while the visited vertices hold at most this fraction of the
-  // adjacency entries at the level's start (predicted by the host): a level
-  // whose candidates are mostly unvisited is bound by its scattered stores,
-  // which the ranges keep local in time and deduplicate; once most targets are
-  // visited the direct level's probes (at the L2 request rate) are cheaper
-  // than the ranges' per-row passes.  Measured, soc-LiveJournal1-sized graph:
-  // a 17 M-edge level at 13 % visited 404 -> 273 us ranged, the 100 M-edge
-  // level after it (86 %) 630 -> 1232 us (profiles/r4_s3_td_range_*).
-  double td_range_vis_frac = 0.3;
   // Dense top-down levels predicted at >= td_unvis_edges frontier edges that
   // start with >= td_unvis_vis_frac of the adjacency visited test targets in
   // an LDS unvisited filter first (UnvisArgs, TdArgs::unvis): a clear bit
@@ -226,7 +205,7 @@ struct EngineOptions {
   // Direct-level top-down: hub targets claimed as one byte per hub (an
   // L2-resident 128 KiB array) and turned into level bytes after the
   // expansion (TdArgs::td_hub_mark, hub_apply).
-  bool td_hub_mark = true;
+  static constexpr bool td_hub_mark = true;
   // Byte-map levels skip the visited pre-check while the visited vertices
   // hold less than this fraction of all adjacency entries.
   double td_check_visited_min = 0.02;
@@ -245,14 +224,14 @@ struct EngineOptions {
   // ... also with several ranks: each level's chain carries its collectives
   // (frontier all-gather, candidate all-to-all, totals all-reduce), enqueued
   // ahead like the kernels; level_finish decides on the reduced totals.
-  bool device_loop_ranks = true;
+  static constexpr bool device_loop_ranks = true;
   // ... enqueueing each level with an extrapolated direction prediction (else:
   // the previous level's direction, one more level ahead).
   bool device_loop_predict = true;
   // Host loop (several ranks, or device_loop off): read each level's totals
   // through a device-mapped mailbox the host spins on, instead of a D2H copy
   // plus a stream synchronisation.
-  bool stats_mailbox = true;
+  static constexpr bool stats_mailbox = true;
   // Device loop: top-down levels whose frontier is predicted to have at most
   // this many edges run as one sparse kernel (TdSparseArgs: direct claims, work list
   // handed to the next level) instead of compact + td_expand + update + scan;
@@ -273,15 +252,15 @@ struct EngineOptions {
   // RMAT-26 (no filter levels) 1024 workgroups 1354 / 1334 against 1323 /
   // 1318 GTEPS at 2048; RMAT-22 top-down only (filter levels) 1024 / 1280 /
   // 1536 (= residency) 77 / 81 / 83 GTEPS.
-  int64_t td_grid_max = 1024;
-  int64_t td_grid_filter_max = 2048;
+  static constexpr int64_t td_grid_max = 1024;
+  static constexpr int64_t td_grid_filter_max = 2048;
   // The sparse threshold for the first top-down level after a bottom-up one
   // (the extrapolated prediction of a shrinking frontier overshoots), and
   // how far such a chain stays live.  RMAT-26: the late-switch roots' level
   // after three bottom-up levels (0.2-0.6 M edges, predicted 2-6 M) 52-58 ->
   // 19-28 us sparse; a shared cap (td_sparse_cap_factor) would also keep
   // mispredicted early chains sparse (measured: 112 -> 331 us).
-  int64_t td_sparse_bu_edges = int64_t(1) << 23;
+  static constexpr int64_t td_sparse_bu_edges = int64_t(1) << 23;
   // ... and that level reads the bottom-up level's output bitmap itself
   // (TdSparseArgs::from_bits: one kernel after a clear of its output bitmap,
   // instead of scan_units + compact + td_sparse).
@@ -289,7 +268,7 @@ struct EngineOptions {
   // Device loop: a bottom-up level's unit scan (totals; one rank: direction
   // decision, mailbox stamp) runs in the bottom-up kernel's last-arriving
   // workgroup instead of a kernel of its own.
-  bool bu_fused_scan = true;
+  static constexpr bool bu_fused_scan = true;
   // Device loop: a dense top-down level's update finishes the
   // level itself (as bu_fused_scan; per-workgroup totals slots, 512
   // workgroups striding over the units with one ticket, the full grid with
@@ -297,7 +276,7 @@ struct EngineOptions {
   // RMAT-26 1344 / 1341 -> 1363 / 1353 GTEPS; top-down only equal within noise.
   // (A first version with one workgroup per 4 units and totals atomics on
   // one address: level 1 of RMAT-26 38 -> 117 us.)
-  bool td_fused_finish = true;
+  static constexpr bool td_fused_finish = true;
   // ... and on graphs of at most kFoldScanUnits 4096-vertex units (2^25
   // vertices) its last workgroup also scans the unit prefixes the next
   // compaction reads (UpdateArgs::fold_scan): one launch less per dense level
@@ -349,10 +328,10 @@ struct EngineOptions {
   // Comm::direct_lists): td_sparse stores remote claims straight into their
   // owners' windows and td_sparse_apply waits for the flags -- no exchange
   // launch in between
-  bool direct_lists = true;
+  static constexpr bool direct_lists = true;
   // ... and their level's end folded into td_sparse_apply's last workgroup
   // (Comm::direct_level_end) when it gathers no frontier
-  bool direct_level_end = true;
+  static constexpr bool direct_level_end = true;
   // Several ranks, a level whose frontier is all-gathered for a bottom-up
   // level next (graphs with hubs): the producing kernels push their output
   // words straight into the peers' windows (Comm::direct_frontier) and the
@@ -368,7 +347,7 @@ struct EngineOptions {
   // Narrow level bytes stored as base + level with the base cycling through
   // kNarrowEpochs values, so only one run in kNarrowEpochs fills the byte
   // array (the others read the earlier epochs' bytes as unreached).
-  bool narrow_epochs = true;
+  static constexpr bool narrow_epochs = true;
   // Take the multi-rank exchange path (alltoall / allgather / alltoallv) even
   // with one rank: lets a 1-rank RCCL communicator exercise every collective
   // call on a single GPU (tests).
@@ -411,8 +390,6 @@ struct ChainRecord {
   // several ranks: its output frontier pushed by its kernels (no gather in
   // its level end; EngineOptions::direct_frontier)
   bool push = false;
-  // one rank: a range-staged dense top-down chain (TdArgs::range_split)
-  bool ranged = false;
   // a dense top-down chain with the unvisited filter (TdArgs::unvis)
   bool unvis = false;
   // ... run in this many parts (TdArgs::split_k; 1: whole)
@@ -461,7 +438,6 @@ class Engine {
   int64_t global_directed_edges() const { return total_directed_; }
   const EngineOptions& options() const { return opt_; }
   void set_options(const EngineOptions& o) {
-    if (o.td_range_words != opt_.td_range_words) range_built_ = false;  // (the split points depend on it)
     opt_ = o;
   }
 
@@ -530,12 +506,6 @@ class Engine {
   DBuf<vid_t> dl_send_lists_, dl_recv_lists_;  // device loop list form, stride list_stride_ + 1
   // binned top-down levels (one rank): bin counts / positions, bin starts, targets
   DBuf<int64_t> bin_total_;
-  // range-staged top-down levels (TdArgs::range_split): built once per graph
-  DBuf<uint32_t> range_split_;
-  int range_count_ = 0;       // 0: not available on this graph
-  int64_t range_span_ = 0;
-  bool range_built_ = false;
-  void build_range_split();
   DBuf<uint32_t> bin_cnt_;
   DBuf<vid_t> bin_buf_;
   int64_t list_stride_ = 0;

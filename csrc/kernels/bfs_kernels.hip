@@ -167,9 +167,7 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
       a.stats[3] = gd;
     }
     LevelCtrl c = a.ctrl_init;
-    level_ctrl_finish(c, gc, gd, true, nullptr);
-    *a.ctrl = c;
-    if (a.mailbox) stamp_mailbox(a.mailbox, c, -1);
+    finish_level(a.ctrl, c, gc, gd, true, nullptr, a.mailbox, -1);
   }
 }
 

@@ -292,28 +292,6 @@ __global__ __launch_bounds__(kBlock) void hub_assign_kernel(const uint32_t* __re
   }
 }
 
-// Range split points: thread per (range boundary y, row r), y-major (the
-// output row of a boundary is written coalesced); a binary search over the
-// row's id buckets (rows of more than 4096 entries are ordered by bucket only:
-// the key is a bucket boundary, so the predicate is monotone either way).
-__global__ __launch_bounds__(kBlock) void range_split_kernel(const eid_t* __restrict__ ro, const vid_t* __restrict__ col,
-                                                            int64_t rows, int64_t span, int shift, int64_t total,
-                                                            uint32_t* __restrict__ out) {
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * kBlock) {
-    const int64_t y = i / rows + 1, r = i - (y - 1) * rows;
-    const eid_t b = ro[r];
-    eid_t lo = b, hi = ro[r + 1];
-    const uint64_t key = static_cast<uint64_t>(y * span) >> shift;
-    while (lo < hi) {
-      const eid_t mid = lo + (hi - lo) / 2;
-      if ((static_cast<uint64_t>(col[mid]) >> shift) < key) lo = mid + 1;
-      else hi = mid;
-    }
-    out[i] = static_cast<uint32_t>(lo - b);
-  }
-}
-
 }  // namespace
 
 void row_heads(const eid_t* row_off, const vid_t* col, int64_t rows, vid_t* head, const uint32_t* hub_idx,
@@ -375,13 +353,6 @@ void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32
   list_medium_rows_kernel<<<static_cast<unsigned>((rows + kBlock - 1) / kBlock), kBlock, 0, st>>>(row_off, rows,
                                                                                                   list, count);
   sort_medium_rows_kernel<<<4096, kBlock, 0, st>>>(row_off, col, list, count, key_deg);
-}
-
-void range_split(const eid_t* row_off, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
-                 uint32_t* out, hipStream_t st) {
-  const int64_t total = rows * (ranges - 1);
-  if (total <= 0) return;
-  range_split_kernel<<<static_cast<unsigned>(std::min<int64_t>((total + kBlock - 1) / kBlock, 65536)), kBlock, 0, st>>>(row_off, col, rows, span, shift, total, out);
 }
 
 void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n, int64_t* list,

@@ -98,13 +98,7 @@ __device__ __forceinline__ void scan_finish(const ScanArgs& a, long long carry_c
   *a.ticket = 0u;  // next launch is stream-ordered after this one
   if (a.ctrl && a.finish) {
     LevelCtrl c = *a.ctrl;
-    level_ctrl_finish(c, carry_c, carry_d, a.seed, a.seed ? nullptr : a.rec);
-    if (!a.seed) {
-      a.rec->t0 = c.t_start;
-      a.rec->t1 = wall_clock64();
-    }
-    *a.ctrl = c;
-    if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level);
+    finish_level(a.ctrl, c, carry_c, carry_d, a.seed, a.rec, a.mailbox, a.level);
   }
 }
 

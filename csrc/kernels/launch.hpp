@@ -162,9 +162,6 @@ void sort_neighbors(const eid_t* row_off, vid_t* col, int64_t rows, const uint32
 // tmp holds nnz entries
 void sort_rows_by_id(const eid_t* row_off, vid_t* col, int64_t rows, int64_t n, int64_t* list,
                      unsigned long long* count, vid_t* tmp, hipStream_t st);
-// range-staged top-down levels' row split points (Backend::range_split)
-void range_split(const eid_t* row_off, const vid_t* col, int64_t rows, int64_t span, int shift, int ranges,
-                 uint32_t* out, hipStream_t st);
 void reached_degree_sum(const ShardView& g, const lvl_t* level, int64_t* out2, hipStream_t st);
 void degree_moments(const ShardView& g, int64_t* out2, hipStream_t st);
 

@@ -374,164 +374,6 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Range-staged top-down level (TdArgs::range_split; one rank, large levels of
-// graphs of at most kRangeMax x kRangeWords x 64 vertices).  A direct level
-// costs every frontier edge a visited probe -- one scattered L2 request: on
-// the soc-LiveJournal1-sized graph's 100 M-edge level the probes alone run at
-// the L2 request rate (~260 G/s, tools/microbench/scatter_ops.hip) -- and a
-// scattered level-byte store per unvisited candidate.  Here a workgroup takes
-// a contiguous run of edge blocks (entries i0 .. ilast, edges [E0, E1)) and
-// sweeps the vertex ranges: for range y its visited words are staged in LDS,
-// then the part of every entry's row that lands in y (rows are in id order:
-// range_split gives the split positions) is expanded -- the entries, 2 per
-// thread, their parts prefix-summed, then windows of kRangeWin edges mapped to
-// their entry through an owner map (as td_block_owner_map) -- and each target
-// is probed and claimed in the LDS copy (atomicOr): only the first claim of a
-// target in the workgroup stores it.  The visited snapshot is the level's
-// start, as the direct path's.
-constexpr int kRangeThreads = 1024;
-constexpr int kRangeItems = 4;
-constexpr int kRangeWin = kRangeThreads * kRangeItems;
-constexpr int kRangeEnt = 2;  // entries per thread per group
-constexpr int kRangeGroup = kRangeThreads * kRangeEnt;
-static_assert(kRangeGroup <= 32767, "owner map entries in int16");
-
-__global__ __launch_bounds__(kRangeThreads, 2 * kRangeThreads / 256) void td_range_kernel(TdArgs a) {
-  __shared__ word_t s_vis[kRangeWords];
-  __shared__ int16_t s_owner[kRangeWin];
-  __shared__ uint32_t s_cs[kRangeGroup];
-  __shared__ int32_t s_wsum[kRangeThreads / kWave];
-  __shared__ int32_t s_wmax[kRangeThreads / kWave];
-  if (!chain_live(*a.ctrl, 'T', a.max_mf)) return;
-  const bool bytes = a.ctrl->bytes != 0;
-  const long long q = a.dev_stats[0], m = a.dev_stats[1];
-  const int t = threadIdx.x;
-  const int lane = lane_id();
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-  if (a.clear_qv) {
-    stamp_level_start(a.ctrl);  // first kernel of the level (no compaction)
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kRangeThreads + t; i < q;
-         i += static_cast<int64_t>(gridDim.x) * kRangeThreads) {
-      const vid_t r = a.clear_qv[i];
-      a.clear_frontier[r >> 6] = 0ull;
-    }
-  }
-  const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
-  const long long per = (nblocks + gridDim.x - 1) / gridDim.x;
-  const long long b0 = static_cast<long long>(blockIdx.x) * per;
-  if (b0 >= nblocks) return;
-  const long long b1 = min(nblocks, b0 + per);
-  const long long E0 = b0 * kTdEdgesPerBlock, E1 = min(m, b1 * kTdEdgesPerBlock);
-  const long long i0 = a.blk_vstart[b0];
-  const long long ilast = b1 < nblocks ? a.blk_vstart[b1] : q - 1;
-  const int64_t rows = a.g.rows;
-  const uint8_t lv = static_cast<uint8_t>(a.narrow_base + a.new_level);
-  const vid_t* __restrict__ col = a.g.col;
-  for (int y = 0; y < a.ranges; ++y) {
-    const int64_t lo = static_cast<int64_t>(y) * a.range_span;
-    const int64_t hi = min(lo + a.range_span, static_cast<int64_t>(a.g.n));
-    __syncthreads();  // (the previous range's last window is done with s_vis)
-    stage_words<kRangeThreads, kRangeWords>(s_vis, a.visited + lo / kWordBits, (hi - lo + kWordBits - 1) / kWordBits);
-    for (long long g0 = i0; g0 <= ilast; g0 += kRangeGroup) {
-      // this thread's entries g0 + kRangeEnt t + k: their parts in range y
-      int len[kRangeEnt];
-      uint32_t cs[kRangeEnt];
-      int tl = 0;
-#pragma unroll
-      for (int k = 0; k < kRangeEnt; ++k) {
-        const long long i = g0 + kRangeEnt * t + k;
-        len[k] = 0;
-        cs[k] = 0;
-        if (i <= ilast) {
-          const long long qs = a.qscan[i], qe = a.qscan[i + 1];
-          const vid_t r = a.range_qv[i];
-          const long long s0 = y == 0 ? 0ll : static_cast<long long>(a.range_split[(y - 1) * rows + r]);
-          const long long s1 = y == a.ranges - 1 ? qe - qs : static_cast<long long>(a.range_split[y * rows + r]);
-          const long long p0 = max(s0, max(qs, E0) - qs), p1 = min(s1, min(qe, E1) - qs);
-          if (p1 > p0) {
-            len[k] = static_cast<int>(p1 - p0);
-            cs[k] = static_cast<uint32_t>(a.qbase[i] + qs + p0);  // (column index mod 2^32: nnz <= 2^32)
-          }
-        }
-        tl += len[k];
-      }
-      // exclusive prefix of the parts over the group (thread-major)
-      const int incl = static_cast<int>(wave_incl_scan(tl));
-      if (lane == kWave - 1) s_wsum[wv] = incl;
-      __syncthreads();  // (also: s_vis staged)
-      int carry = 0, total = 0;
-#pragma unroll
-      for (int k = 0; k < kRangeThreads / kWave; ++k) {
-        const int x = s_wsum[k];
-        carry += k < wv ? x : 0;
-        total += x;
-      }
-      int pre[kRangeEnt];
-      {
-        int run = carry + incl - tl;
-#pragma unroll
-        for (int k = 0; k < kRangeEnt; ++k) {
-          pre[k] = run;
-          // column of part edge j of this entry = j + s_cs[entry] (mod 2^32)
-          s_cs[kRangeEnt * t + k] = cs[k] - static_cast<uint32_t>(run);
-          run += len[k];
-        }
-      }
-      for (int w0 = 0; w0 < total; w0 += kRangeWin) {
-#pragma unroll
-        for (int k = 0; k < kRangeItems; ++k) s_owner[k * kRangeThreads + t] = 0;
-        __syncthreads();
-        // every part that starts in the window (or covers its first edge)
-#pragma unroll
-        for (int k = 0; k < kRangeEnt; ++k)
-          if (len[k] > 0 && pre[k] < w0 + kRangeWin && pre[k] + len[k] > w0)
-            s_owner[pre[k] > w0 ? pre[k] - w0 : 0] = static_cast<int16_t>(kRangeEnt * t + k);
-        __syncthreads();
-        // inclusive max-scan: thread t owns positions [t * Items, (t + 1) * Items)
-        int vals[kRangeItems];
-        int run = 0;
-#pragma unroll
-        for (int k = 0; k < kRangeItems; ++k) {
-          run = max(run, static_cast<int>(s_owner[t * kRangeItems + k]));
-          vals[k] = run;
-        }
-        const int wi = wave_incl_max(run);
-        if (lane == kWave - 1) s_wmax[wv] = wi;
-        __syncthreads();
-        int c2 = 0;
-        for (int k = 0; k < wv; ++k) c2 = max(c2, s_wmax[k]);
-        const int prev = __shfl_up(wi, 1, kWave);
-        const int ex = lane > 0 ? max(c2, prev) : c2;
-#pragma unroll
-        for (int k = 0; k < kRangeItems; ++k) s_owner[t * kRangeItems + k] = static_cast<int16_t>(max(vals[k], ex));
-        __syncthreads();
-        const int cnt = min(kRangeWin, total - w0);
-        vid_t v[kRangeItems];
-#pragma unroll
-        for (int k = 0; k < kRangeItems; ++k) {
-          const int idx = k * kRangeThreads + t;
-          v[k] = idx < cnt ? __builtin_nontemporal_load(col + (static_cast<uint32_t>(w0 + idx) + s_cs[s_owner[idx]])) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kRangeItems; ++k) {
-          if (k * kRangeThreads + t >= cnt) continue;
-          const uint32_t rel = static_cast<uint32_t>(static_cast<int64_t>(v[k]) - lo);
-          DBFS_DCHECK(static_cast<int64_t>(rel) < hi - lo, 12, v[k]);
-          const word_t bit = 1ull << (rel & 63);
-          if (s_vis[rel >> 6] & bit) continue;
-          if (atomicOr(&s_vis[rel >> 6], bit) & bit) continue;
-          if (!bytes) atomicOr(a.next + (v[k] >> 6), 1ull << (v[k] & 63));
-          else if (a.level_direct) a.level_direct[v[k]] = lv;
-          else a.next_bytes[v[k]] = 1;
-        }
-        __syncthreads();  // (s_owner rewritten by the next window)
-      }
-      __syncthreads();  // (s_wsum / s_cs rewritten by the next group)
-    }
-  }
-}
-
 // The claimed, owned items of a lane (bit k of `claimed`: v[k], a global id
 // of this shard): level, frontier bit, and the wave's work-list entries of
 // the next level with one packed atomic (count << kSparseEdgeBits | edges)
@@ -971,11 +813,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
   LevelCtrl c = *a.ctrl;
-  level_ctrl_finish(c, cnt, deg, false, a.rec);
-  a.rec->t0 = c.t_start;
-  a.rec->t1 = wall_clock64();
-  *a.ctrl = c;
-  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+  finish_level(a.ctrl, c, cnt, deg, false, a.rec, a.mailbox, a.level_index);
 }
 
 // Sparse top-down level read straight from the bitmap a bottom-up level left
@@ -1117,11 +955,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   long long cnt = 0, deg = 0;
   sparse_totals(a, cnt, deg);
   LevelCtrl c = *a.ctrl;
-  level_ctrl_finish(c, cnt, deg, false, a.rec);
-  a.rec->t0 = c.t_start;
-  a.rec->t1 = wall_clock64();
-  *a.ctrl = c;
-  if (a.mailbox) stamp_mailbox(a.mailbox, c, a.level_index);
+  finish_level(a.ctrl, c, cnt, deg, false, a.rec, a.mailbox, a.level_index);
 }
 
 
@@ -1458,15 +1292,6 @@ void td_expand(const TdArgs& a, hipStream_t st) {
     ~Report() { td_stats_report(st); }
   } report{st};
 #endif
-  if (a.ctrl && a.range_split) {
-    // range-staged level: two workgroups per CU, each a contiguous run of blocks
-    DBFS_CHECK(a.ranges >= 1 && a.ranges <= kRangeMax && a.range_span > 0 && a.range_span % kWordBits == 0 &&
-                   a.range_span / kWordBits <= kRangeWords && a.range_span * a.ranges >= a.g.n &&
-                   a.g.nnz <= (int64_t(1) << 32) && a.range_qv && a.g.lo == 0 && a.g.rows == a.g.n,
-               "td_range: bad range geometry");
-    td_range_kernel<<<static_cast<unsigned>(2 * device_cus()), kRangeThreads, 0, st>>>(a);
-    return;
-  }
   if (a.ctrl) {
     // device loop: fixed grid, size and output mode read on the device
     if (a.grid <= 0) return;

@@ -33,7 +33,7 @@ class BFSResult:
     @property
     def chains(self) -> List[Any]:
         """Device loop: every level chain enqueued, in order, as (level, form,
-        list capacity, gathered, pushed, range-staged, unvisited filter, parts)
+        list capacity, gathered, pushed, unvisited filter, parts)
         -- form T / S / L / B / X (mispredicted chains included); parts > 1: a
         split top-down level (Options td_split_edges / td_split_parts)."""
         return list(self._native.chains) if self._native is not None else []

@@ -295,10 +295,9 @@ def test_device_loop_matches_host_loop(rt, mode, predict):
         assert (a.reached, a.edges, a.depth) == (b.reached, b.edges, b.depth)
 
 
-@pytest.mark.parametrize("mailbox", [0, 1])
-def test_host_loop_stats_mailbox(mailbox):
+def test_host_loop_stats_mailbox():
     # host loop on 3 virtual ranks: level totals read through the mapped
-    # mailbox (or a plain copy) give the oracle's levels; with phase timing
+    # mailbox give the oracle's levels; with phase timing
     # every level reports its collective time (comm_ms <= ms)
     p = dbfs.rmat_params(11, 16, 19)
     csr = dbfs.host_csr_from_params(p)
@@ -308,7 +307,6 @@ def test_host_loop_stats_mailbox(mailbox):
     def body(rt):
         bfs = dbfs.BFS(p, rt, mode="do")
         bfs.engine.set_option("device_loop", 0)  # the host loop (several ranks default to the device loop)
-        bfs.engine.set_option("stats_mailbox", mailbox)
         bfs.engine.phase_timing = True
         out = []
         for s in srcs:
@@ -355,9 +353,8 @@ def test_sparse_top_down_levels(rt, mode, predict, sparse_edges):
     assert dev.validate(12345)
 
 
-@pytest.mark.parametrize("epochs", [1, 0])
 @pytest.mark.parametrize("mode", ["td", "bu", "do"])
-def test_narrow_epochs_stale_bytes(rt, mode, epochs):
+def test_narrow_epochs_stale_bytes(rt, mode):
     # level bytes are base + level with a base per run (narrow_epochs): runs
     # alternate between two components (a 62-level path: the deepest narrow
     # traversal, and a 40-level one) so every run meets the other
@@ -368,7 +365,6 @@ def test_narrow_epochs_stale_bytes(rt, mode, epochs):
     dst_e = src_e + 1
     csr = dbfs.build_csr(n1 + n2, src_e, dst_e)
     b = dbfs.BFS(csr, rt, mode=mode)
-    b.engine.set_option("narrow_epochs", epochs)
     for i in range(11):
         src = (0, n1, n1 - 1, n1 + 20)[i % 4]
         r = b.run(src)
@@ -445,7 +441,6 @@ def test_device_loop_several_ranks(P, mode, predict):
     {"list_form_edges": 64},                        # lists too small: sparse chains re-enqueued dense
     {"xsparse_edges": 0},                           # only level 0 predicted sparse
     {"device_loop_predict": 0},                     # no prediction: two wasted chains per switch
-    {"bu_fused_scan": 0, "td_fused_finish": 0},     # separate scans
 ])
 @pytest.mark.parametrize("P", [2, 3, 8])
 def test_device_loop_sparse_lists_several_ranks(P, knobs):
@@ -557,7 +552,6 @@ def test_td_fused_finish_cpu(rt, mode):
     p = dbfs.rmat_params(12, 16, 67)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, rt, mode=mode)
-    bfs.engine.set_option("td_fused_finish", 1)
     for src in bfs.sample_roots(3, seed=9):
         bfs.run(src)
         assert np.array_equal(bfs.levels(), dbfs.cpu_bfs(csr, src)[0])
@@ -687,27 +681,6 @@ def test_hub_cut_is_one_rank_only(P, narrow):
             assert forced[s][1] == plain[s][1]
 
 
-@pytest.mark.parametrize("words", [None, 32])
-def test_range_staged_top_down_levels_cpu(rt, words):
-    """Range-staged dense top-down levels (TdArgs::range_split) on the CPU
-    backend: the chains are planned (ranged flag) and the split points built
-    (Backend::range_split); levels exact against the oracle, also with many
-    ranges (td_range_words)."""
-    p = dbfs.rmat_params(14, 16, 53)
-    csr = dbfs.host_csr_from_params(p)
-    b = dbfs.BFS(p, rt, mode="td")
-    b.engine.set_option("td_range_edges", 1)
-    b.engine.set_option("td_range_vis_frac", 2.0)
-    if words is not None:
-        b.engine.set_option("td_range_words", words)
-    ranged = False
-    for s in b.sample_roots(3, seed=5):
-        r = b.run(s)
-        assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0])
-        ranged = ranged or any(c[5] for c in r.chains)
-    assert ranged
-
-
 @pytest.mark.parametrize("n,m,mode", [(3000, 30000, "td"), (600011, 2400000, "td"), (600011, 2400000, "do")])
 def test_unvisited_filter_levels_cpu(n, m, mode):
     """The unvisited filter (UnvisArgs, TdArgs::unvis) on the CPU backend:
@@ -728,13 +701,12 @@ def test_unvisited_filter_levels_cpu(n, m, mode):
         b.engine.set_option("td_unvis_edges", 1)
         b.engine.set_option("td_unvis_vis_frac", 0.0)
         b.engine.set_option("td_unvis_max_density", 1.0)
-        b.engine.set_option("td_range_edges", 0)
         b.engine.set_option("td_sparse_edges", 0)
         used = False
         for s in roots:
             r = b.run(s)
             assert np.array_equal(b.levels(), exp[s]), (rt.rank, s)
-            used = used or any(c[6] for c in r.chains)
+            used = used or any(c[5] for c in r.chains)
         return used
 
     for P in (1, 3):
@@ -783,13 +755,12 @@ def test_split_levels_cpu(parts, mode):
     b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
     b.engine.set_option("td_split_edges", 1)
     b.engine.set_option("td_split_parts", parts)
-    b.engine.set_option("td_range_edges", 0)
     b.engine.set_option("td_sparse_edges", 0)
     used = False
     for s in roots:
         r = b.run(s)
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
-        used = used or any(c[7] in (parts, 2 * parts) for c in r.chains)
+        used = used or any(c[6] in (parts, 2 * parts) for c in r.chains)
     assert used
 
 

@@ -126,7 +126,7 @@ def test_unvisited_filter_gpu(gpu_runtime, forced):
             bfs.engine.set_option("narrow_levels", narrow)
             for s in (int(np.argmax(deg)), 12345):
                 res = _check(bfs, csr, s)
-                used = used or any(c[6] for c in res.chains)
+                used = used or any(c[5] for c in res.chains)
                 assert bfs.validate(s)
     assert used
 
@@ -605,19 +605,17 @@ def test_validator_counts_gpu(gpu_runtime):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mark", [1, 0])
 @pytest.mark.parametrize("vis_frac", [0.0, 0.75])
 @pytest.mark.parametrize("mode", ["td", "do"])
-def test_td_hub_filter_gpu(gpu_runtime, mode, vis_frac, mark):
+def test_td_hub_filter_gpu(gpu_runtime, mode, vis_frac):
     """Top-down hub filter (hubs' visited bits in LDS, hub-encoded td_col) on
-    every dense level (td_hub_edges=1), with hub targets claimed through the
-    hub marks + hub_apply or decoded and stored directly: exact levels."""
+    every dense level (td_hub_edges=1), hub targets claimed through the hub
+    marks + hub_apply: exact levels."""
     p = dbfs.rmat_params(17, 16, 21)
     csr = dbfs.host_csr_from_params(p)
     b = dbfs.BFS(p, gpu_runtime, mode=mode)
     b.engine.set_option("td_hub_edges", 1)
     b.engine.set_option("td_hub_vis_frac", vis_frac)
-    b.engine.set_option("td_hub_mark", mark)
     b.engine.set_option("td_direct_edges", 1)
     for src in b.sample_roots(5, seed=3):
         r = b.run(src)
@@ -804,36 +802,6 @@ def test_td_direct_levels_gpu(gpu_runtime, mode, direct_edges):
 
 
 @pytest.mark.parametrize("mode", ["td", "do"])
-@pytest.mark.parametrize("scale,words", [(17, None), (17, 256), (18, 512), (16, 64)])
-def test_td_range_levels_gpu(gpu_runtime, mode, scale, words):
-    """One rank, range-staged dense top-down levels (td_range_kernel: vertex
-    ranges swept one at a time, their visited bits in LDS, each row's part in
-    the range from the rows' id-ordered split points): forced on every dense
-    level (td_range_edges = 1), with one range (the default on these graphs)
-    or several (td_range_words: 8 to 16 ranges, RMAT hubs' rows of > 4096
-    entries ordered by id bucket only); exact against the oracle on RMAT, a
-    uniform graph and a star whose centre's row spans many edge blocks."""
-    graphs = [dbfs.rmat_params(scale, 16, 53), dbfs.uniform_params(1 << scale, 12 << scale, 59)]
-    n = 1 << scale
-    hub = np.zeros(n - 1, dtype=np.uint32)
-    star = dbfs.build_csr(n, hub, np.arange(1, n, dtype=np.uint32))
-    for g in graphs + [star]:
-        csr = g if g is star else dbfs.host_csr_from_params(g)
-        bfs = dbfs.BFS(g, gpu_runtime, mode=mode)
-        bfs.engine.set_option("td_range_edges", 1)
-        bfs.engine.set_option("td_range_vis_frac", 2.0)  # (every dense level, whatever is visited)
-        if words is not None:
-            bfs.engine.set_option("td_range_words", words)
-        ranged = False
-        srcs = [0, 5] if g is star else bfs.sample_roots(3, seed=61)
-        for src in srcs:
-            res = _check(bfs, csr, src)
-            ranged = ranged or any(c[5] for c in res.chains)
-        assert ranged or mode == "do"
-        assert bfs.validate(srcs[-1])
-
-
-@pytest.mark.parametrize("mode", ["td", "do"])
 @pytest.mark.parametrize("bin_edges", [1, 1 << 20, 0])
 def test_binned_top_down_gpu(gpu_runtime, mode, bin_edges):
     """One rank, binned top-down levels (targets binned by vertex range, one
@@ -926,7 +894,6 @@ def test_td_fused_finish_gpu(gpu_runtime, mode):
     p = dbfs.rmat_params(17, 16, 67)
     csr = dbfs.host_csr_from_params(p)
     bfs = dbfs.BFS(p, gpu_runtime, mode=mode)
-    bfs.engine.set_option("td_fused_finish", 1)
     for src in bfs.sample_roots(3, seed=9):
         _check(bfs, csr, src)
 
@@ -1492,13 +1459,12 @@ def test_split_levels_gpu(gpu_runtime, parts, mode, bits):
         b.engine.set_heuristics(24.0, 24.0, 8, td_byte_edges=0)
     b.engine.set_option("td_split_edges", 1)
     b.engine.set_option("td_split_parts", parts)
-    b.engine.set_option("td_range_edges", 0)
     b.engine.set_option("td_sparse_edges", 0)
     used = False
     for s in b.sample_roots(4, seed=3):
         r = b.run(s)
         assert np.array_equal(b.levels(), dbfs.cpu_bfs(csr, s)[0]), s
-        used = used or any(c[7] in (parts, 2 * parts) for c in r.chains)
+        used = used or any(c[6] in (parts, 2 * parts) for c in r.chains)
     assert used
 
 

@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--grid", default=None, metavar="W:H", help="the road-like W x H grid instead of RMAT")
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--ranks-of", type=int, default=8, help="P: ranks of the recorded job")
@@ -40,7 +41,11 @@ def main() -> int:
     from distributed_cuda_bfs_amd.parallel.shadow import shadow_ranks
 
     opts = {k: float(v) for k, v in (kv.split("=", 1) for kv in args.opt)}
-    params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
+    if args.grid:
+        gw, _, gh = args.grid.partition(":")
+        params = dbfs.grid_params(int(gw), int(gh))
+    else:
+        params = dbfs.rmat_params(args.scale, args.edge_factor, args.seed)
     t0 = time.time()
     # one rank, same roots: the 1-GPU level times (and the root sample)
     rt = init_runtime(args.device)
@@ -60,7 +65,8 @@ def main() -> int:
     print(f"[shadow] record + replay: {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
 
     P = args.ranks_of
-    print(f"RMAT-{args.scale} ef{args.edge_factor}, mode {args.mode}: rank r of P = {P} replayed alone "
+    gname = f"grid {args.grid}" if args.grid else f"RMAT-{args.scale} ef{args.edge_factor}"
+    print(f"{gname}, mode {args.mode}: rank r of P = {P} replayed alone "
           f"(device-clock level times, us; the P = {P} rank also pays one device copy per collective)")
     for i, root in enumerate(roots):
         print(f"\nroot {root}")
@@ -80,6 +86,10 @@ def main() -> int:
         for s in runs:
             tot += f" {sum(x[1] for x in s.levels[i]) * 1e3:>8.1f}"
         print(tot)
+        per = f"{'per':>3} {'lvl':>3} {'(us per level)':>15} {sum(x[1] for x in ref[i]) * 1e3 / max(len(ref[i]), 1):>8.2f}"
+        for s in runs:
+            per += f" {sum(x[1] for x in s.levels[i]) * 1e3 / max(len(s.levels[i]), 1):>8.2f}"
+        print(per)
     for s in runs:
         kinds = {}
         for kind, a, b, nb in s.collectives:
