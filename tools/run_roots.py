@@ -28,4 +28,6 @@ for r in args.roots:
     res = bfs.run(r)
     print(r, f"{res.ms:.3f} ms", "".join(lv["dir"] for lv in res.levels),
           [lv["frontier_edges"] for lv in res.levels], [round(lv["ms"] * 1e3, 1) for lv in res.levels],
-          f"mispredicts {res.mispredicts}", "chains " + " ".join(f"{L}{f}" for L, f, *_ in res.chains), flush=True)
+          f"mispredicts {res.mispredicts}", "chains " + " ".join(f"{L}{f}" for L, f, *_ in res.chains),
+          "gap-us", [round(lv.get("gap_ms", -1.0) * 1e3, 1) for lv in res.levels],
+          f"unaccounted {res.ms * 1e3 - sum(lv['ms'] for lv in res.levels) * 1e3:.1f} us", flush=True)
