@@ -405,8 +405,9 @@ def main(argv=None) -> int:
     if args.heldout_roots > 0 and fast_mode:
         hroots = bfs.sample_roots(args.heldout_roots, seed=args.heldout_seed)
         if hroots:
-            hv, hms, hok, _ = validated_pass(bfs, rt, hroots)
+            hv, hms, hok, hres = validated_pass(bfs, rt, hroots)
             heldout = {"value": round(hv, 4), "ms_per_step": round(hms, 4), "roots": len(hroots),
+                       "mispredicted_levels": sum(r.mispredicts for r in hres),
                        "seed": args.heldout_seed, "validated_roots": f"{hok}/{len(hroots)}"}
             log(f"held-out roots (seed {args.heldout_seed}): {hv:.2f} GTEPS, validated {hok}/{len(hroots)}")
             if hok != len(hroots):

@@ -133,8 +133,8 @@ class DeviceLoop {
   // ---- planner ----
   char td_form(int L, double mf, int64_t* cap, bool exact) const;
   bool chain_valid(int L, char dir, int64_t mf) const;
-  void predict(LevelCtrl& c, double nf, double mf, double pnf, double pmf, double reached, bool first, double* enf,
-               double* emf) const;
+  void predict(LevelCtrl& c, double nf, double mf, double pnf, double pmf, double reached, bool first, bool rising,
+               double* enf, double* emf) const;
 
   // ---- emitters ----
   void enqueue_level(int L, char d, int64_t cap, double mf_hint, bool gather);
@@ -441,15 +441,38 @@ bool DeviceLoop::chain_valid(int L, char dir, int64_t mf) const {
 // edges not reached yet) and its direction through level_ctrl_finish (c
 // holds the known level's direction and totals on entry).
 void DeviceLoop::predict(LevelCtrl& c, double nf, double mf, double pnf, double pmf, double reached, bool first,
-                         double* enf, double* emf) const {
+                         bool rising, double* enf, double* emf) const {
   auto grow = [](double cur, double prev) { return prev <= 0 ? cur * cur : cur * (cur / prev); };
-  *enf = std::min({grow(nf, pnf), static_cast<double>(part_.n),
-                   std::max(0.0, static_cast<double>(e_.n_active_) - reached)});
+  const double unreached = std::max(0.0, static_cast<double>(e_.n_active_) - reached);
+  *enf = std::min({grow(nf, pnf), static_cast<double>(part_.n), unreached});
   // level 1's frontier edges: the source's neighbours have the mean endpoint degree
   *emf = std::min(first ? mf * std::max(1.0, e_.excess_degree_) : grow(mf, pmf),
                   static_cast<double>(e_.total_directed_));
+  const LevelCtrl c0 = c;
   LevelRecDev scratch;
   level_ctrl_finish(c, std::max<int64_t>(1, static_cast<int64_t>(*enf)), static_cast<int64_t>(*emf), false, &scratch);
+  // Rising phase (no bottom-up level yet): each frontier edge finds about one
+  // new vertex, of the mean endpoint degree.  Taken only when that estimate
+  // turns the decision bottom-up -- a root whose few neighbours are hubs (1
+  // -> 1 vertex but 1 -> 17 K edges: the vertex count's growth says
+  // top-down; RMAT-26's late-switch roots, 91-153 M edges bottom-up, cost a
+  // wasted chain and a host round trip each); the edge estimate would
+  // otherwise oversize the forms of levels that stay top-down.
+  // (A/B, same box, 128 held-out RMAT-26 roots twice each: mispredicted
+  // levels 34 -> 19, 1489 / 1498 -> 1504 / 1506 GTEPS; profiles/r6_predictor_ab.txt)
+  if (rising && !first && e_.n_active_ > 0 && c.dir != 'B') {
+    const double e = std::min(mf, unreached);
+    const double em = std::min(e * std::max(1.0, e_.excess_degree_), static_cast<double>(e_.total_directed_));
+    if (e > *enf && em > *emf) {
+      LevelCtrl c2 = c0;
+      level_ctrl_finish(c2, std::max<int64_t>(1, static_cast<int64_t>(e)), static_cast<int64_t>(em), false, &scratch);
+      if (c2.dir == 'B') {
+        c = c2;
+        *enf = e;
+        *emf = em;
+      }
+    }
+  }
 }
 
 // ---- emitters -------------------------------------------------------------------
@@ -1052,7 +1075,7 @@ RunResult DeviceLoop::run() {
   e_.begin_run_scratch();
   init_.mode = opt_.mode == Mode::TopDown ? 0 : opt_.mode == Mode::BottomUp ? 1 : 2;
   init_.alpha = opt_.alpha;
-  init_.beta = opt_.beta;
+  init_.beta = e_.effective_beta();
   init_.n = static_cast<double>(part_.n);
   init_.total_directed = static_cast<double>(e_.total_directed_);
   init_.td_byte_edges = bytes_ok_ ? static_cast<double>(byte_edges_) : 1e300;
@@ -1123,6 +1146,7 @@ RunResult DeviceLoop::run() {
   int nlev = 0;
   LevelCtrl hc = init_;  // host mirror for the prediction
   int64_t prev_nf = 0, prev_mf = 0;
+  bool any_bu = init_.dir == 'B';  // a bottom-up level was decided (the rising phase is over)
   {
     int64_t cap0 = 0;
     const char f0 = init_.dir == 'B' ? 'B' : td_form(0, 0.0, &cap0, false);
@@ -1162,12 +1186,13 @@ RunResult DeviceLoop::run() {
     hc.vis_deg = mb->vis_deg;
     hc.done = 0;
     double enf = 0, emf = 0, enf2 = 0, emf2 = 0;
+    if (actual == 'B') any_bu = true;
     predict(hc, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(prev_nf),
-            static_cast<double>(prev_mf), static_cast<double>(mb->reached), L == 0, &enf, &emf);
+            static_cast<double>(prev_mf), static_cast<double>(mb->reached), L == 0, !any_bu, &enf, &emf);
     const char d1 = static_cast<char>(hc.dir);
     LevelCtrl hc2 = hc;
     predict(hc2, enf, emf, static_cast<double>(nf), static_cast<double>(mf), static_cast<double>(mb->reached) + enf,
-            false, &enf2, &emf2);
+            false, !any_bu && d1 != 'B', &enf2, &emf2);
     const char d2 = static_cast<char>(hc2.dir);
     if (!valid) {
       int64_t cap = 0;

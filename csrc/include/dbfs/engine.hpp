@@ -119,6 +119,15 @@ struct EngineOptions {
   // soc-LiveJournal1-sized graph unchanged.
   double alpha = 40.0;  // TD -> BU when m_f > m_u / alpha
   double beta = 96.0;   // BU -> TD when n_f < n / beta (and shrinking)
+  // ... with several ranks the bottom-up levels shrink with P and the sparse
+  // top-down ones do not (a sparse level's claims and owner lists cost a rank
+  // the same at any P), so a shrinking frontier stays bottom-up longer: beta
+  // x kBetaRanksScale.  Shadow replays of RMAT-26 (ranks 0 and P-1, the
+  // post-bottom-up level of the late-switch roots 103 -> 24 us at P = 8):
+  // late-switch traversals -12 % at P = 2, -11 % at P = 4, -19 % at P = 8,
+  // early-switch ones unchanged (profiles/r6_policy_shadow_p*.txt); 16x was
+  // no better, and alpha x 4 changed nothing.
+  static constexpr double kBetaRanksScale = 4.0;
   // neighbours a lane checks itself before rows go to wave-cooperative scans
   // (16: a first bottom-up level entered with a small frontier resolves more
   // rows per lane; RMAT-26 1240 -> 1259 GTEPS, 8 and 32 worse)
@@ -479,6 +488,9 @@ class Engine {
   bool run_narrow_ = false;           // the current run writes level8_
   mutable bool levels_narrow_ = false;  // level_ is stale: level8_ holds the last run's levels
   bool use_narrow() const;
+  // Beamer's beta at this rank count: EngineOptions::beta on one rank,
+  // kBetaRanksScale x that with several (EngineOptions::beta's note)
+  double effective_beta() const { return part_.nranks > 1 ? opt_.beta * EngineOptions::kBetaRanksScale : opt_.beta; }
   void ensure_wide_levels() const;
   // bitmap engine state
   bool bitmap_ready_ = false;

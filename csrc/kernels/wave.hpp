@@ -29,24 +29,46 @@ __device__ __forceinline__ long long readlane_i64(long long x, int l) {
   return static_cast<long long>(readlane64(static_cast<unsigned long long>(x), l));
 }
 
-__device__ __forceinline__ long long wave_incl_scan(long long x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const long long y = __shfl_up(x, off, kWave);
-    if (l >= off) x += y;
-  }
-  return x;
+// Inclusive wave64 scans on DPP lane moves (VALU, no LDS crossbar): a
+// Hillis-Steele scan inside each 16-lane row (row_shr 1 / 2 / 4 / 8, lanes
+// shifted in from outside the row read 0: bound_ctrl), then the row totals
+// carried across rows with the gfx9 row broadcasts (row_bcast:15 into rows 1
+// and 3, row_bcast:31 into rows 2 and 3).  A lane a DPP move does not write
+// (row / bank mask) reads `old` = 0, so every step is x += move(x).
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ unsigned dpp_u32(unsigned x) {
+  return static_cast<unsigned>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, kRowMask, 0xf, true));
+}
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long x) {
+  const unsigned lo = dpp_u32<kCtrl, kRowMask>(static_cast<unsigned>(x));
+  const unsigned hi = dpp_u32<kCtrl, kRowMask>(static_cast<unsigned>(x >> 32));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
 }
 
 __device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned x) {
-  const int l = lane_id();
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const unsigned y = __shfl_up(x, off, kWave);
-    if (l >= off) x += y;
-  }
+  x += dpp_u32<kDppRowShr1>(x);
+  x += dpp_u32<kDppRowShr2>(x);
+  x += dpp_u32<kDppRowShr4>(x);
+  x += dpp_u32<kDppRowShr8>(x);
+  x += dpp_u32<kDppRowBcast15, 0xa>(x);
+  x += dpp_u32<kDppRowBcast31, 0xc>(x);
   return x;
+}
+
+__device__ __forceinline__ long long wave_incl_scan(long long x) {
+  unsigned long long v = static_cast<unsigned long long>(x);
+  v += dpp_u64<kDppRowShr1>(v);
+  v += dpp_u64<kDppRowShr2>(v);
+  v += dpp_u64<kDppRowShr4>(v);
+  v += dpp_u64<kDppRowShr8>(v);
+  v += dpp_u64<kDppRowBcast15, 0xa>(v);
+  v += dpp_u64<kDppRowBcast31, 0xc>(v);
+  return static_cast<long long>(v);
 }
 
 __device__ __forceinline__ int wave_incl_max(int x) {

@@ -43,8 +43,15 @@ def test_traffic_matches_model(P, mode, knobs):
             fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True,
                                             list_form_edges=cfg.list_form_edges), chains)
             n_td = sum(1 for c in chains if c[1] in "ST")
-            n_lone_b = sum(1 for i, c in enumerate(chains)
-                           if c[1] == "B" and not (chains[i - 1][3] if i else mode == "bu"))
+
+            def gathered_before(i):
+                # the previous level's collective (its last chain: a
+                # mispredicted chain of this level in between does not count)
+                lv = chains[i][0]
+                prev = [c for c in chains[:i] if c[0] == lv - 1]
+                return prev[-1][3] if prev else mode == "bu"
+
+            n_lone_b = sum(1 for i, c in enumerate(chains) if c[1] == "B" and not gathered_before(i))
             assert fused.total_calls == len(chains) + n_td + n_lone_b + 1
 
 
