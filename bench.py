@@ -98,7 +98,7 @@ def parse_args(argv=None):
                     help="Beamer alpha (TD -> BU when m_f > m_u / alpha); the engine / CLI default, 40: chosen over "
                          "24 / 32 / 48 / 64 on the 64-root tuning sample of seed 20261017 (profiles/"
                          "r4_final_alpha_sweep.txt) -- that seed is a tuning seed now, not a held-out one")
-    ap.add_argument("--beta", type=float, default=96.0)
+    ap.add_argument("--beta", type=float, default=384.0)
     ap.add_argument("--bu-lane-limit", type=int, default=16)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning option (see Engine.get_options()), repeatable")

@@ -51,7 +51,7 @@ struct Args {
   int device = 0;
   bool cpu = false;
   std::string mode = "do";
-  double alpha = 40.0, beta = 96.0;
+  double alpha = 40.0, beta = 384.0;
   int bu_lane_limit = 16;
   int rmat_scale = 0, rmat_ef = 16;
   int64_t uni_n = 0, uni_m = 0;

@@ -1075,7 +1075,7 @@ RunResult DeviceLoop::run() {
   e_.begin_run_scratch();
   init_.mode = opt_.mode == Mode::TopDown ? 0 : opt_.mode == Mode::BottomUp ? 1 : 2;
   init_.alpha = opt_.alpha;
-  init_.beta = e_.effective_beta();
+  init_.beta = opt_.beta;
   init_.n = static_cast<double>(part_.n);
   init_.total_directed = static_cast<double>(e_.total_directed_);
   init_.td_byte_edges = bytes_ok_ ? static_cast<double>(byte_edges_) : 1e300;

@@ -893,7 +893,7 @@ RunResult Engine::run_bitmap(int64_t source) {
     // full bottom-up sweep.
     if (dir == 'T' && static_cast<double>(m_f) > m_u / opt_.alpha && n_f > prev_nf) {
       dir = 'B';
-    } else if (dir == 'B' && static_cast<double>(n_f) < n_d / effective_beta() && n_f < prev_nf) {
+    } else if (dir == 'B' && static_cast<double>(n_f) < n_d / opt_.beta && n_f < prev_nf) {
       dir = 'T';
     }
   };

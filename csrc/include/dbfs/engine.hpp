@@ -118,16 +118,17 @@ struct EngineOptions {
   // tuning sample, seed 20261017; profiles/r4_final_alpha_sweep.txt), the
   // soc-LiveJournal1-sized graph unchanged.
   double alpha = 40.0;  // TD -> BU when m_f > m_u / alpha
-  double beta = 96.0;   // BU -> TD when n_f < n / beta (and shrinking)
-  // ... with several ranks the bottom-up levels shrink with P and the sparse
-  // top-down ones do not (a sparse level's claims and owner lists cost a rank
-  // the same at any P), so a shrinking frontier stays bottom-up longer: beta
-  // x kBetaRanksScale.  Shadow replays of RMAT-26 (ranks 0 and P-1, the
-  // post-bottom-up level of the late-switch roots 103 -> 24 us at P = 8):
-  // late-switch traversals -12 % at P = 2, -11 % at P = 4, -19 % at P = 8,
-  // early-switch ones unchanged (profiles/r6_policy_shadow_p*.txt); 16x was
-  // no better, and alpha x 4 changed nothing.
-  static constexpr double kBetaRanksScale = 4.0;
+  double beta = 384.0;  // BU -> TD when n_f < n / beta (and shrinking)
+  // (384 since round 6, from 96: a shrinking frontier stays bottom-up
+  // longer.  Asked to be a function of P -- a bottom-up level's cost per rank
+  // shrinks with P, a sparse top-down level's does not -- the shadow replays
+  // of RMAT-26 (ranks 0 and P - 1, four roots) found one value best at every
+  // P: the late-switch roots' post-bottom-up level stays bottom-up (P = 8:
+  // 103 -> 24 us), their traversals -12 % / -11 % / -19 % at P = 2 / 4 / 8,
+  // early-switch ones unchanged, 768 and 1536 no better (profiles/
+  // r6_policy_shadow_p*.txt); one GPU, 128 held-out roots, same box: 1498 /
+  // 1494 -> 1506 / 1513 GTEPS (profiles/r6_beta_one_gpu_ab.txt).  alpha x 4
+  // changed nothing at P = 8.)
   // neighbours a lane checks itself before rows go to wave-cooperative scans
   // (16: a first bottom-up level entered with a small frontier resolves more
   // rows per lane; RMAT-26 1240 -> 1259 GTEPS, 8 and 32 worse)
@@ -244,7 +245,8 @@ struct EngineOptions {
   // Device loop: top-down levels whose frontier is predicted to have at most
   // this many edges run as one sparse kernel (TdSparseArgs: direct claims, work list
   // handed to the next level) instead of compact + td_expand + update + scan;
-  // 0 disables.  td_sparse_grid: its workgroups.
+  // 0 disables.  td_sparse_grid: its workgroups (RMAT-26, 256 / 512 / 1024:
+  // 1504-1509 / 1506-1509 / 1492-1503 GTEPS held-out, profiles/r6_sparse_grid_ab.txt).
   int64_t td_sparse_edges = int64_t(1) << 16;
   static constexpr int64_t td_sparse_grid = 256;
   // ... several ranks: the owners' side (td_sparse_apply) at most this many
@@ -488,9 +490,6 @@ class Engine {
   bool run_narrow_ = false;           // the current run writes level8_
   mutable bool levels_narrow_ = false;  // level_ is stale: level8_ holds the last run's levels
   bool use_narrow() const;
-  // Beamer's beta at this rank count: EngineOptions::beta on one rank,
-  // kBetaRanksScale x that with several (EngineOptions::beta's note)
-  double effective_beta() const { return part_.nranks > 1 ? opt_.beta * EngineOptions::kBetaRanksScale : opt_.beta; }
   void ensure_wide_levels() const;
   // bitmap engine state
   bool bitmap_ready_ = false;

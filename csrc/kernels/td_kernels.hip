@@ -699,6 +699,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       while (wall_clock64() - t0 < a.late_ticks) __builtin_amdgcn_s_sleep(8);
     }
   }
+  // (the input totals loaded with the chain check: one round trip for both;
+  // dev_stats is valid memory on a no-op chain too)
+  const long long q = a.dev_stats[0], m = a.dev_stats[1];
   // uniform: the whole grid returns, no workgroup takes a ticket (a direct
   // exchange still publishes, empty)
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
@@ -710,7 +713,6 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     return;
   }
   if (a.first) stamp_level_start(a.ctrl);
-  const long long q = a.dev_stats[0], m = a.dev_stats[1];
   const long long nblocks = (m + kTdEdgesPerBlock - 1) / kTdEdgesPerBlock;
   // Only the workgroups that have an edge block take part (at least one, for
   // the finish): the others return before the ticket -- on a level of a few
@@ -803,9 +805,11 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     // workgroup reads only the counter, a device-scope atomic; the level's
     // stores are read by later launches.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = atomicAdd(a.ticket, 1u);
+    // (one active workgroup -- a tail level: trivially the last, no ticket
+    // round trip; its own atomics are ordered by the s_waitcnt)
+    const unsigned prev = active == 1 ? 0u : atomicAdd(a.ticket, 1u);
     s_last = (prev == active - 1) ? 1 : 0;
-    if (s_last) last_arriver_acquire();
+    if (s_last && active > 1) last_arriver_acquire();
   }
   __syncthreads();
   if (!s_last) return;

@@ -643,7 +643,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
              py::gil_scoped_release rel;
              return std::make_shared<Engine>(*g, *c, o);
            }),
-           py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 40.0, py::arg("beta") = 96.0,
+           py::arg("graph"), py::arg("comm"), py::arg("mode") = "do", py::arg("alpha") = 40.0, py::arg("beta") = 384.0,
            py::arg("bu_lane_limit") = 16, py::arg("phase_timing") = false, py::arg("force_exchange") = false,
            py::keep_alive<1, 2>(),
            py::keep_alive<1, 3>())

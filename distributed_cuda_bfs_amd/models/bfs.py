@@ -60,7 +60,7 @@ class BFS:
     """Distributed BFS over a graph given as a HostCSR, generator params, or a file path."""
 
     def __init__(self, graph: Union[str, Any], runtime: Optional[Runtime] = None, mode: str = "do",
-                 alpha: float = 40.0, beta: float = 96.0, bu_lane_limit: int = 16, phase_timing: bool = False,
+                 alpha: float = 40.0, beta: float = 384.0, bu_lane_limit: int = 16, phase_timing: bool = False,
                  hub_sort: bool = True, force_exchange: bool = False, hubs: bool = True,
                  max_hubs: Optional[int] = None, directed: bool = False, sharded: bool = True,
                  read_threads: int = 0, id_order: bool = True):
