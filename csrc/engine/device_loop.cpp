@@ -462,8 +462,8 @@ void DeviceLoop::predict(LevelCtrl& c, double nf, double mf, double pnf, double 
   // levels 34 -> 19, 1489 / 1498 -> 1504 / 1506 GTEPS; profiles/r6_predictor_ab.txt)
   if (rising && !first && e_.n_active_ > 0 && c.dir != 'B') {
     const double e = std::min(mf, unreached);
-    const double em = std::min(e * std::max(1.0, e_.excess_degree_), static_cast<double>(e_.total_directed_));
-    if (e > *enf && em > *emf) {
+    const double em = std::max(*emf, std::min(e * std::max(1.0, e_.excess_degree_), static_cast<double>(e_.total_directed_)));
+    if (e > *enf) {
       LevelCtrl c2 = c0;
       level_ctrl_finish(c2, std::max<int64_t>(1, static_cast<int64_t>(e)), static_cast<int64_t>(em), false, &scratch);
       if (c2.dir == 'B') {
