@@ -436,6 +436,9 @@ void PeerComm::run(const Plan& plan) {
   }
   kern::peer_wait(wa, st);
   HIP_CHECK(hipGetLastError());
+  // (a timed-out wait leaves its error word set: the unpack then copies
+  // nothing and finishes no level -- the host's wait watch reports the stall)
+  ua.error = err_dev_;
   kern::peer_unpack(ua, st);
   HIP_CHECK(hipGetLastError());
   ++peer_ops_;

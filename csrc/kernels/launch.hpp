@@ -103,6 +103,11 @@ struct PeerUnpackArgs {
   // workgroup sums everything, then finishes the level: level_finish_block)
   bool has_finish = false;
   LevelFinishArgs finish;
+  // the wait's error word (split collectives: the unpack is a launch of its
+  // own, stream-ordered after the wait whatever its outcome): non-zero -- a
+  // wait of this rank timed out -- and the unpack copies nothing and the
+  // level is not finished on payloads that never arrived
+  const uint64_t* error = nullptr;
 };
 constexpr int64_t kPeerFinishMax = 2048;
 void peer_push(const PeerPushArgs& a, hipStream_t st);

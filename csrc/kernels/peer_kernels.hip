@@ -181,6 +181,7 @@ __global__ void peer_wait_kernel(PeerWaitArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void peer_unpack_kernel(PeerUnpackArgs a) {
+  if (a.error && __hip_atomic_load(a.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
   unpack_pieces(a, static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x, static_cast<int64_t>(gridDim.x) * kBlock);
 }
 

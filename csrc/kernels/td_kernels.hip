@@ -635,10 +635,11 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
   __syncthreads();
   if (t == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // (one workgroup -- a fused tiny level's: trivially the last, no ticket)
-    const unsigned prev = gx == 1 ? 0u : atomicAdd(a.ticket, 1u);
+    // (one workgroup taking part -- a fused tiny level's, or a small level's:
+    // trivially the last, no ticket)
+    const unsigned prev = (gx == 1 || active == 1) ? 0u : atomicAdd(a.ticket, 1u);
     s_last = (prev == active - 1) ? 1 : 0;
-    if (s_last) last_arriver_acquire();
+    if (s_last && active > 1) last_arriver_acquire();
   }
   __syncthreads();
   if (!s_last) return;
@@ -776,9 +777,11 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-      const unsigned prev = atomicAdd(a.ticket, 1u);
+      // (one active workgroup -- a tiny level: trivially the last, no
+      // ticket round trip; every wave drained its stores before the barrier)
+      const unsigned prev = active == 1 ? 0u : atomicAdd(a.ticket, 1u);
       s_last = (prev == active - 1) ? 1 : 0;
-      if (s_last) {
+      if (s_last && active > 1) {
         *a.ticket = 0u;  // (the apply's ticket next, stream-ordered)
         // the counts the publish reads were added by every workgroup's
         // waves; the ids are write-through stores every wave drained before
