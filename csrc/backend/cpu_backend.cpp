@@ -452,7 +452,8 @@ class CpuBackend final : public Backend {
   }
 
   void pack_bytes(const PackArgs& a) override {
-    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T' || !a.ctrl->bytes)) return;
+    if (a.ctrl && (a.ctrl->done || (a.flag ? a.ctrl->dir != 'B' || !*a.flag : a.ctrl->dir != 'T' || !a.ctrl->bytes)))
+      return;
     for (int64_t w = 0; w < a.words; ++w) a.next[w] |= gather_bytes(a.bytes + w * 64);
   }
 
@@ -740,19 +741,45 @@ class CpuBackend final : public Backend {
   void bu_cut_prep(const BuArgs& a) override {
     if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
     if (!*a.cut_flag) return;
-    const int64_t lo = a.g.lo;
+    const bool x = a.cut_bytes != nullptr;
+    DBFS_CHECK(x || a.g.lo == 0, "bu_cut_prep: a shard past vertex 0 needs the several-rank arguments");
+    const int64_t lo = a.g.lo, off = x ? a.cut_word_off : 0;
+    const word_t* vis = x ? a.cut_vis : a.visited;
     for (int64_t w = 0; w < a.words; ++w)
-      for (word_t m = a.frontier[w] & ~a.g.hub_bits[w]; m; m &= m - 1) {
+      for (word_t m = a.frontier[off + w] & ~a.g.hub_bits[off + w]; m; m &= m - 1) {
         const int64_t v = w * 64 + __builtin_ctzll(m);
         for (eid_t e = a.g.row_off[v]; e < a.g.row_off[v + 1]; ++e) {
           const vid_t t = a.g.col[e];
+          if (test_bit(vis, t)) continue;
           const int64_t r = static_cast<int64_t>(t) - lo;
-          DBFS_CHECK(r >= 0 && r < a.g.rows, "bu_cut_prep: one rank only");
-          if (test_bit(a.visited, static_cast<uint64_t>(r))) continue;
+          if (r < 0 || r >= a.g.rows) {
+            DBFS_CHECK(x, "bu_cut_prep: a remote neighbour without the several-rank arguments");
+            a.cut_bytes[t] = 1;
+            continue;
+          }
           if (a.cut_claim) a.cut_claim[r] = 1;
           else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
         }
       }
+  }
+  void bu_cut_merge(const BuArgs& a) override {
+    DBFS_CHECK(a.cut_flag && a.cut_recv && a.cut_next && (a.level8 || a.cut_claim) && a.cut_nranks > 1,
+               "bu_cut_merge: several ranks' hub-cut arguments missing");
+    if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) return;
+    if (!*a.cut_flag) return;
+    for (int64_t w = 0; w < a.words; ++w) {
+      word_t c = 0;
+      for (int p = 0; p < a.cut_nranks; ++p) {
+        if (p == a.cut_rank) continue;
+        c |= a.cut_recv[p * a.words + w];
+        a.cut_next[p * a.words + w] = 0;
+      }
+      for (c &= ~a.visited[w]; c; c &= c - 1) {
+        const int64_t r = w * 64 + __builtin_ctzll(c);
+        if (a.cut_claim) a.cut_claim[r] = 1;
+        else put_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
+      }
+    }
   }
   void hub_apply(const HubApplyArgs& a) override {
     if (a.ctrl && !chain_live(*a.ctrl, 'T', a.max_mf)) return;

@@ -272,6 +272,7 @@ class HipBackend final : public Backend {
   void bu_step(const BuArgs& a) override { on(); kern::bu_step(a, st_); chk(); }
   void hub_gather(const HubGatherArgs& a) override { on(); kern::hub_gather(a, st_); chk(); }
   void bu_cut_prep(const BuArgs& a) override { on(); kern::bu_cut_prep(a, st_); chk(); }
+  void bu_cut_merge(const BuArgs& a) override { on(); kern::bu_cut_merge(a, st_); chk(); }
   void direct_prewait(const DirectExchange& x) override { on(); kern::direct_prewait(x, st_); chk(); }
   void hub_visited(const HubVisitedArgs& a) override { on(); kern::hub_visited(a, st_); chk(); }
   void unvis_filter(const UnvisArgs& a) override { on(); kern::unvis_filter(a, st_); chk(); }

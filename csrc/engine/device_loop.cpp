@@ -989,15 +989,19 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
       hg.visited = e_.visited_.data();
       hg.words = GW_;
     }
-    // a first bottom-up level, one rank: the hub cut (decided on the device
-    // from the frontier hubs' degrees hub_gather sums), enqueued for levels
-    // predicted at <= bu_cut_mf_frac of the graph's edges (a first bottom-up
-    // level's non-hub frontier edges grow with its frontier: the larger ones
-    // never cut, and skip its launches).  (Several ranks: measured slower at
-    // P = 8 -- the cut's top-down part does not shrink with P while a rank's
-    // bottom-up share does -- and not built.)
-    const bool shard_ok = P_ == 1 && gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref &&
-                          gv_.nz_row_off && gv_.head && ba.zdeg;
+    // a first bottom-up level: the hub cut (decided on the device from the
+    // frontier hubs' degrees hub_gather sums -- global, so the same on every
+    // rank), enqueued for levels predicted at <= bu_cut_mf_frac of the
+    // graph's edges (a first bottom-up level's non-hub frontier edges grow
+    // with its frontier: the larger ones never cut, and skip its launches).
+    // Several ranks (up to bu_cut_ranks): the remote claims as one bitmap
+    // all-to-all (xcut).
+    const bool xcut = P_ > 1;
+    // (several ranks: every condition the same on every rank -- the chain
+    // then carries the claims' collective)
+    const bool shard_ok = P_ == 1 ? gv_.hub_bits && gv_.nz_rec && gv_.unit_base && gv_.nz_pref && gv_.nz_row_off &&
+                                        gv_.head && ba.zdeg
+                                  : xc_ && P_ <= opt_.bu_cut_ranks && e_.g_.rec_all();
     cut = opt_.bu_cut_edges > 0 && c.pf != 'B' &&
           (c.mf_hint < 0 || c.mf_hint <= opt_.bu_cut_mf_frac * static_cast<double>(e_.total_directed_)) && shard_ok;
     if (cut) {
@@ -1025,7 +1029,37 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         }
         ba.cut_claim = e_.cut_claim_.data();
       }
+      res_.chains.back().cut = true;
+      if (xcut) {
+        // the remote claims: bytes of the global byte map (zero between its
+        // users: every pack clears what it read)
+        if (!e_.next_bytes_.data()) {
+          e_.next_bytes_ = DBuf<uint8_t>(be_, static_cast<size_t>(GW_) * kWordBits);
+          be_.memset_async(e_.next_bytes_.data(), 0, e_.next_bytes_.bytes());
+        }
+        ba.cut_bytes = e_.next_bytes_.data();
+        ba.cut_vis = e_.visited_.data();
+        ba.cut_word_off = me_ * W_;
+      }
       be_.bu_cut_prep(ba);
+      if (xcut) {
+        // ... packed per owner into `next`, one bitmap all-to-all (a
+        // collective: on a plain or no-op chain too, then empty), merged on
+        // the owners; `next` re-zeroed by the merge
+        PackArgs pa;
+        pa.bytes = e_.next_bytes_.data();
+        pa.next = e_.next_.data();
+        pa.words = GW_;
+        pa.ctrl = e_.ctrl_.data();
+        pa.flag = e_.cut_flag_.data();
+        be_.pack_bytes(pa);
+        comm_.alltoall(e_.next_.data(), e_.recv_.data(), static_cast<size_t>(W_) * sizeof(word_t));
+        ba.cut_recv = e_.recv_.data();
+        ba.cut_next = e_.next_.data();
+        ba.cut_rank = me_;
+        ba.cut_nranks = P_;
+        be_.bu_cut_merge(ba);
+      }
     }
   }
   if (opt_.bu_fused_scan) {

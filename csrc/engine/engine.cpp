@@ -83,6 +83,7 @@ void set_engine_option(EngineOptions& o, const std::string& name, double v) {
   else if (name == "bu_merge_visited") o.bu_merge_visited = v != 0;
   else if (name == "bu_cut_edges") o.bu_cut_edges = static_cast<int64_t>(v);
   else if (name == "bu_cut_mf_frac") o.bu_cut_mf_frac = v;
+  else if (name == "bu_cut_ranks") o.bu_cut_ranks = static_cast<int64_t>(v);
   else if (name == "list_cap_factor") o.list_cap_factor = v;
   else if (name == "direct_frontier") o.direct_frontier = v != 0;
   else throw Error("unknown engine option '" + name + "'");
@@ -123,6 +124,7 @@ std::vector<std::pair<std::string, double>> engine_option_map(const EngineOption
           {"bu_merge_visited", o.bu_merge_visited ? 1.0 : 0.0},
           {"bu_cut_edges", static_cast<double>(o.bu_cut_edges)},
           {"bu_cut_mf_frac", o.bu_cut_mf_frac},
+          {"bu_cut_ranks", static_cast<double>(o.bu_cut_ranks)},
           {"list_cap_factor", o.list_cap_factor},
           {"direct_frontier", o.direct_frontier ? 1.0 : 0.0}};
 }
@@ -434,6 +436,18 @@ void DeviceGraph::sort_neighbors_by_degree(Comm& comm, bool hubs, int64_t max_hu
     }
   } else {
     build_heads();
+  }
+  // whether every rank has the packed row records (a shard of no rows, or
+  // with a unit of 2^32+ edges, has none): the several-rank hub cut needs
+  // them on all (its chains carry a collective, so the choice must agree)
+  {
+    DBuf<int64_t> miss(*be_, 1);
+    const int64_t m = nz_rec_.data() && unit_base_.data() ? 0 : 1;
+    be_->to_device(miss.data(), &m, sizeof(m));
+    if (P > 1) comm.allreduce_sum_i64(miss.data(), 1);
+    int64_t h = 0;
+    be_->to_host(&h, miss.data(), sizeof(h));
+    rec_all_ = h == 0;
   }
   hub_sorted_ = true;
 }

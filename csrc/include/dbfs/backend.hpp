@@ -712,8 +712,11 @@ struct PackArgs {
   uint8_t* bytes = nullptr;
   word_t* next = nullptr;
   int64_t words = 0;
-  // device loop: runs only on a byte-map top-down level (ctrl->bytes)
+  // device loop: runs only on a byte-map top-down level (ctrl->bytes) --
+  // or, with `flag`, on a live bottom-up level whose *flag is set (the
+  // several-rank hub cut's remote claims, BuArgs::cut_bytes)
   const LevelCtrl* ctrl = nullptr;
+  const int* flag = nullptr;
 };
 
 // Bottom-up step fused with the frontier update: for every owned unvisited v,
@@ -778,6 +781,20 @@ struct BuArgs {
   int64_t cut_edges = 0;
   int* cut_flag = nullptr;
   uint8_t* cut_claim = nullptr;
+  // ... several ranks (bu_cut_prep): this rank's non-hub frontier is the
+  // global frontier's words [cut_word_off, + words); a neighbour is skipped
+  // when its bit in cut_vis (the replicated global visited bitmap) is set;
+  // an owned one is claimed as above, a remote one gets its byte of
+  // cut_bytes (the global byte map, packed per owner and all-to-all'ed).
+  // bu_cut_merge then claims the received words (cut_recv: P slices of
+  // `words`, this rank's own empty) and zeroes cut_next (the packed bitmap,
+  // P slices) for the next user.
+  uint8_t* cut_bytes = nullptr;
+  const word_t* cut_vis = nullptr;
+  int64_t cut_word_off = 0;
+  const word_t* cut_recv = nullptr;
+  word_t* cut_next = nullptr;
+  int cut_rank = 0, cut_nranks = 1;
   // several ranks: the new frontier words also pushed to the peers (FrontierTable)
   const FrontierTable* push = nullptr;
   int push_rank = 0, push_nranks = 1;
@@ -1078,6 +1095,9 @@ class Backend {
   // Hub-cut level's top-down part (BuArgs::cut_edges): the unvisited
   // neighbours of the frontier's non-hub vertices claimed into a.pre.
   virtual void bu_cut_prep(const BuArgs& a) = 0;
+  // ... several ranks: the claims the peers sent (BuArgs::cut_recv) into the
+  // owned claim bytes, the packed bitmap zeroed -- on a live cut level only
+  virtual void bu_cut_merge(const BuArgs& a) = 0;
   // A direct exchange's wait as a launch of its own, one wave (ranks sharing
   // a GPU, Comm::split_waits): the consumer after it finds the cells tagged.
   virtual void direct_prewait(const DirectExchange& x) { (void)x; }

@@ -78,6 +78,8 @@ class DeviceGraph {
   // them): graphs whose hubs are only slightly above the mean degree (uniform
   // random graphs) gain nothing from the top-down hub filter
   double td_hub_share() const { return td_hub_share_; }
+  // every rank's shard has the packed row records (agreed at the degree sort)
+  bool rec_all() const { return rec_all_; }
   int64_t nhubs() const { return nhubs_; }
   // from_file: the byte range [begin, end) of the file this rank parsed and
   // the edges it read (a binary cache: rows, -1 bytes); -1 when not from a file
@@ -95,6 +97,7 @@ class DeviceGraph {
   bool hub_sorted_ = false;
   bool col_by_id_ = false;
   int64_t nhubs_ = 0;
+  bool rec_all_ = false;  // every rank has the packed row records (rec_all())
   void build_heads(const uint32_t* hub_idx = nullptr);
   DBuf<vid_t> head_, hub_vertex_, nz_head_, hub_col_, td_col_, td_hub_vertex_;
   double td_hub_share_ = 0.0;
@@ -320,12 +323,19 @@ struct EngineOptions {
   // us at P = 2 for 3-5 us per bottom-up level; traversal -6.6 % at P = 2,
   // -3.6 % at P = 8.
   bool bu_merge_visited = true;
-  // One rank, device loop, hubs: a first bottom-up level whose frontier has
-  // at most bu_cut_edges edges outside the hubs claims those vertices'
-  // neighbours top-down (bu_cut_prep) and scans only the rows' hub prefixes
+  // Device loop, hubs: a first bottom-up level whose frontier has at most
+  // bu_cut_edges edges outside the hubs claims those vertices' neighbours
+  // top-down (bu_cut_prep) and scans only the rows' hub prefixes
   // (BuArgs::cut_edges) -- the late-switch level, whose frontier is a few
   // thousand vertices, mostly hubs.  0 disables.
   int64_t bu_cut_edges = int64_t(1) << 22;
+  // ... with several ranks too, up to this many: every rank claims its own
+  // non-hub frontier's neighbours, the remote ones in the byte map, packed
+  // and sent to their owners as one bitmap all-to-all (bu_cut_merge applies
+  // them) -- the top-down part shrinks with P as the bottom-up share does.
+  // (Round 4's form sent the remote claims as owner lists and measured
+  // slower at P = 8.)
+  int64_t bu_cut_ranks = 8;
   // ... enqueued (its decision and top-down launches) only for levels
   // predicted at <= bu_cut_mf_frac of the graph's directed edges (RMAT-26:
   // the late-switch first bottom-up levels have 4-15 % of them, the others
@@ -405,6 +415,8 @@ struct ChainRecord {
   bool unvis = false;
   // ... run in this many parts (TdArgs::split_k; 1: whole)
   int split = 1;
+  // a bottom-up chain with the hub cut's launches (decided on the device)
+  bool cut = false;
 };
 
 struct RunResult {

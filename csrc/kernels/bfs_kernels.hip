@@ -810,7 +810,8 @@ __global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a)
 
 // Byte map -> bitmap for the multi-rank exchange (words of 64 vertices).
 __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
-  if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'T' || !a.ctrl->bytes)) return;
+  if (a.ctrl && (a.ctrl->done || (a.flag ? a.ctrl->dir != 'B' || !*a.flag : a.ctrl->dir != 'T' || !a.ctrl->bytes)))
+    return;
   const int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (w >= a.words) return;
   const word_t bits = gather_byte_bits(a.bytes + w * 64);

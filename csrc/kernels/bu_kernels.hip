@@ -811,20 +811,29 @@ __global__ __launch_bounds__(kThreads) void hub_gather_kernel(HubGatherArgs a) {
 // (kernel trace; grid 256-4096 workgroups flat); a list of the vertices, a
 // wave each, spent 109 us in the list's same-address appends alone; claims
 // in a bitmap by device atomics 160 us.
-// (One rank: with several ranks the cut's top-down part -- every rank's own
-// non-hub frontier, its remote claims through owner lists -- cost a rank more
-// than it saved it at P = 8, round 4's shadow replay; the level runs plain.)
+// Several ranks (kX): a rank expands its own non-hub frontier vertices (its
+// slice of the global frontier, BuArgs::cut_word_off), filters the targets by
+// the replicated visited bitmap, claims the owned ones as above and marks the
+// remote ones in the global byte map (BuArgs::cut_bytes), which pack_bytes
+// turns into one bitmap slice per owner for the all-to-all; bu_cut_merge
+// claims what arrives.  (Round 4 sent them as owner lists -- one returning
+// atomic per claim -- and measured slower at P = 8.)
 constexpr int kCutThreads = 1024;
+template <bool kX>
 __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
   if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) return;
   const vid_t* __restrict__ col = a.g.col;
   const eid_t* __restrict__ ro = a.g.row_off;
+  const word_t* __restrict__ fr = a.frontier + (kX ? a.cut_word_off : 0);
+  const word_t* __restrict__ hub = a.g.hub_bits + (kX ? a.cut_word_off : 0);
+  const word_t* __restrict__ vis = kX ? a.cut_vis : a.visited;
+  const uint64_t lo = kX ? static_cast<uint64_t>(a.g.lo) : 0ull, rows = static_cast<uint64_t>(a.g.rows);
   const int lane = lane_id();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kCutThreads;
   for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kCutThreads + (threadIdx.x & ~(kWave - 1)); w0 < a.words;
        w0 += stride) {
     const int64_t w = w0 + lane;
-    word_t m = w < a.words ? a.frontier[w] & ~a.g.hub_bits[w] : 0ull;
+    word_t m = w < a.words ? fr[w] & ~hub[w] : 0ull;
     for (unsigned long long bm = __ballot(m != 0); bm; bm = __ballot(m != 0)) {
       const int l = __ffsll(static_cast<long long>(bm)) - 1;
       const int64_t v = (w0 + l) * 64 + __builtin_ctzll(static_cast<word_t>(__shfl(static_cast<long long>(m), l, kWave)));
@@ -840,15 +849,43 @@ __global__ __launch_bounds__(kCutThreads) void bu_cut_prep_kernel(BuArgs a) {
           t[k] = e < re ? col[e] : kNoVertex;
         }
 #pragma unroll
-        for (int k = 0; k < kU; ++k) vw[k] = t[k] == kNoVertex ? ~0ull : a.visited[t[k] >> 6];
+        for (int k = 0; k < kU; ++k) vw[k] = t[k] == kNoVertex ? ~0ull : vis[t[k] >> 6];
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
           if ((vw[k] >> (t[k] & 63)) & 1ull) continue;
-          if (a.cut_claim) a.cut_claim[t[k]] = 1;  // (wide levels: the bottom-up kernel writes them)
-          else store_level(nullptr, a.level8, t[k], a.new_level, a.narrow_base);
+          const uint64_t r = static_cast<uint64_t>(t[k]) - lo;
+          if (kX && r >= rows) {
+            a.cut_bytes[t[k]] = 1;  // (a remote claim: packed for its owner)
+            continue;
+          }
+          if (a.cut_claim) a.cut_claim[r] = 1;  // (wide levels: the bottom-up kernel writes them)
+          else store_level(nullptr, a.level8, static_cast<int64_t>(r), a.new_level, a.narrow_base);
         }
       }
     }
+  }
+}
+
+// Several ranks, a live hub-cut level: owned word w's claims from the peers
+// (OR of their slices in cut_recv, filtered by visited) into the claim bytes
+// (narrow level bytes or cut_claim), and every slice of the packed bitmap
+// zeroed (cut_next: the dense top-down levels' candidate bitmap, kept zero
+// between users).
+__global__ __launch_bounds__(kBlock) void bu_cut_merge_kernel(BuArgs a) {
+  if ((a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) || !*a.cut_flag) return;
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (w >= a.words) return;
+  word_t c = 0;
+  for (int p = 0; p < a.cut_nranks; ++p) {
+    if (p == a.cut_rank) continue;
+    c |= a.cut_recv[p * a.words + w];
+    a.cut_next[p * a.words + w] = 0ull;
+  }
+  c &= ~a.visited[w];
+  for (; c; c &= c - 1) {
+    const int64_t r = w * 64 + __builtin_ctzll(c);
+    if (a.cut_claim) a.cut_claim[r] = 1;
+    else store_level(nullptr, a.level8, r, a.new_level, a.narrow_base);
   }
 }
 
@@ -971,9 +1008,20 @@ void bu_step(const BuArgs& a, hipStream_t st) {
 void bu_cut_prep(const BuArgs& a, hipStream_t st) {
   DBFS_CHECK(a.cut_edges > 0 && a.cut_flag && (a.level8 || a.cut_claim) && a.g.hub_bits && a.ctrl,
              "bu_cut_prep: hub-cut arguments missing");
+  const bool x = a.cut_bytes != nullptr;
+  DBFS_CHECK(!x || (a.cut_vis && a.cut_word_off >= 0), "bu_cut_prep: several ranks' claim arguments missing");
+  DBFS_CHECK(x || a.g.lo == 0, "bu_cut_prep: a shard past vertex 0 needs the several-rank arguments");
   // (grid measured flat from 256 to 4096 workgroups)
   const unsigned grid = grid_for(a.words, kCutThreads, 2 * device_cus());
-  bu_cut_prep_kernel<<<grid, kCutThreads, 0, st>>>(a);
+  if (x) bu_cut_prep_kernel<true><<<grid, kCutThreads, 0, st>>>(a);
+  else bu_cut_prep_kernel<false><<<grid, kCutThreads, 0, st>>>(a);
+}
+
+void bu_cut_merge(const BuArgs& a, hipStream_t st) {
+  DBFS_CHECK(a.cut_flag && a.cut_recv && a.cut_next && (a.level8 || a.cut_claim) && a.cut_nranks > 1 &&
+                 a.cut_rank >= 0 && a.cut_rank < a.cut_nranks && a.words > 0,
+             "bu_cut_merge: several ranks' hub-cut arguments missing");
+  bu_cut_merge_kernel<<<grid_for(a.words, kBlock), kBlock, 0, st>>>(a);
 }
 
 void hub_gather(const HubGatherArgs& a, hipStream_t st) {

@@ -42,6 +42,7 @@ void list_scatter(const ListScatterArgs& a, hipStream_t st);
 void bu_step(const BuArgs& a, hipStream_t st);
 void hub_gather(const HubGatherArgs& a, hipStream_t st);
 void bu_cut_prep(const BuArgs& a, hipStream_t st);
+void bu_cut_merge(const BuArgs& a, hipStream_t st);
 void hub_visited(const HubVisitedArgs& a, hipStream_t st);
 void unvis_filter(const UnvisArgs& a, hipStream_t st);
 void hub_apply(const HubApplyArgs& a, hipStream_t st);

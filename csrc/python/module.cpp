@@ -625,7 +625,7 @@ PYBIND11_MODULE(_dbfs_native, m) {
                              [](const RunResult& r) {
                                py::list out;
                                for (const auto& c : r.chains)
-                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.push, c.unvis, c.split));
+                                 out.append(py::make_tuple(c.level, std::string(1, c.form), c.cap, c.gather, c.push, c.unvis, c.split, c.cut));
                                return out;
                              })
       .def("level_dicts", &level_dicts);

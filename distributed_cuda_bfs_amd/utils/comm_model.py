@@ -3,8 +3,8 @@
 Mirrors what ``Engine::run_bitmap_device`` (csrc/engine/engine.cpp,
 ``enqueue_level`` / ``finish_ranks``) issues for each level chain, so the
 collectives and bytes of a traversal can be predicted from its chains
-(``BFSResult.chains``: level, form, capacity, gather, pushed frontier, ranged,
-unvisited filter)
+(``BFSResult.chains``: level, form, capacity, gather, pushed frontier,
+unvisited filter, split parts, hub cut)
 and checked against the
 communicators' traffic counters (``Comm.traffic()``, tests/test_comm_model.py).
 ``table`` turns a 1-GPU level profile into the per-level bytes / collectives
@@ -19,7 +19,8 @@ One collective per level, plus the payload a top-down level must move:
   peer transport (accounted here, as by the counters, at the lists' capacity);
 * a dense top-down chain (``T``) exchanges candidate bitmap slices;
 * a bottom-up chain (``B``) whose input frontier was not gathered by the
-  previous collective (a mispredicted switch) gathers it itself.
+  previous collective (a mispredicted switch) gathers it itself; one with the
+  hub cut's launches exchanges its remote claims as bitmap slices.
 
 Bytes are what one rank sends to the other ranks under a direct exchange:
 alltoall / allgather (P - 1) x the per-peer bytes, all-reduce (P - 1) x the
@@ -91,12 +92,14 @@ def level_end(cfg: ModelConfig, gather: bool, push: bool = False) -> ChainTraffi
 
 
 def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gathered: bool,
-                  push: bool = False) -> ChainTraffic:
+                  push: bool = False, cut: bool = False) -> ChainTraffic:
     """Collectives of one level chain."""
     P, W = cfg.nranks, cfg.slice_words
     t = ChainTraffic()
     if form == "B" and not in_gathered:
         t.add("allgather", (P - 1) * W * WORD)              # input frontier slices (+ visited merge)
+    if form == "B" and cut and P > 1:
+        t.add("alltoall", (P - 1) * W * WORD)               # the hub cut's remote claims
     if form == "S":
         t.add("alltoallv", (P - 1) * ((cap or cfg.list_max) + 1) * 4)  # owner lists, count first
     elif form == "T":
@@ -107,7 +110,7 @@ def chain_traffic(cfg: ModelConfig, form: str, cap: int, gather: bool, in_gather
 
 def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     """Traffic of one traversal from its enqueued chains (level, form, cap,
-    gather[, push, ranged]): start barrier, every chain, the wall-time max at
+    gather[, push, unvis, split, cut]): start barrier, every chain, the wall-time max at
     the end.  (The seed needs no collective: every rank seeds the traversal
     from its replicated degree array, and writes a bottom-up first level's
     whole seed frontier itself.)"""
@@ -118,7 +121,7 @@ def run_traffic(cfg: ModelConfig, chains: Iterable[Tuple]) -> ChainTraffic:
     gathered = {-1: seed_gather}
     for level, form, cap, gather, *more in chains:
         tot.merge(chain_traffic(cfg, form, int(cap), bool(gather), gathered.get(level - 1, False),
-                                bool(more[0]) if more else False))
+                                bool(more[0]) if more else False, bool(more[3]) if len(more) > 3 else False))
         gathered[level] = bool(gather)
     tot.add("allgather", (P - 1) * 8)  # max over ranks of the wall time
     return tot

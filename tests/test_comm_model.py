@@ -37,7 +37,7 @@ def test_traffic_matches_model(P, mode, knobs):
                 assert calls == want.calls[kind], (kind, chains, got, dict(want.calls))
                 assert nbytes == want.bytes[kind], (kind, chains, got, dict(want.bytes))
             # one collective per chain (its level's end), plus a top-down
-            # chain's payload exchange; a bottom-up chain's input frontier came
+            # (or hub-cut) chain's payload exchange; a bottom-up chain's input frontier came
             # with the previous collective unless that one mispredicted; none
             # for the seed (every rank seeds itself), one wall-time max
             fused = run_traffic(ModelConfig(nranks=P, slice_words=W, mode=mode, fused=True,
@@ -52,7 +52,9 @@ def test_traffic_matches_model(P, mode, knobs):
                 return prev[-1][3] if prev else mode == "bu"
 
             n_lone_b = sum(1 for i, c in enumerate(chains) if c[1] == "B" and not gathered_before(i))
-            assert fused.total_calls == len(chains) + n_td + n_lone_b + 1
+            # (a hub-cut bottom-up chain: its remote claims' all-to-all)
+            n_cut = sum(1 for c in chains if c[1] == "B" and c[7])
+            assert fused.total_calls == len(chains) + n_td + n_lone_b + n_cut + 1
 
 
 def test_table_shapes():

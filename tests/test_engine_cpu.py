@@ -650,11 +650,15 @@ def test_hub_cut_bottom_up_levels(rt, cut_edges, alpha, max_hubs, narrow):
 
 @pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("narrow", [1, 0])
-def test_hub_cut_is_one_rank_only(P, narrow):
-    """The hub cut (BuArgs::cut_edges) is a one-rank path: with several ranks
-    it is never enqueued (round 4 measured its multi-rank form slower at P = 8
-    and it was removed), so forcing its thresholds changes nothing -- levels
-    exact against the oracle, level records equal to the default run's."""
+def test_hub_cut_several_ranks(P, narrow):
+    """The hub cut with several ranks (EngineOptions::bu_cut_ranks): every
+    rank claims its own non-hub frontier's neighbours, the remote ones packed
+    per owner and all-to-all'ed, merged on the owners (bu_cut_merge) -- forced
+    on every first bottom-up level (bu_cut_edges 2^40, any prediction), then
+    off (bu_cut_ranks 1): levels exact against the oracle both ways, the level
+    records equal, and the cut chains enqueued only when allowed.  300 hubs
+    leave most frontier vertices to the top-down part; narrow levels keep the
+    claims in the level bytes, wide ones in the claim bytes."""
     p = dbfs.rmat_params(13, 16, 11)
     csr = dbfs.host_csr_from_params(p)
     srcs = [7, 3001, 8100]
@@ -662,23 +666,26 @@ def test_hub_cut_is_one_rank_only(P, narrow):
     def body(rt):
         b = dbfs.BFS(p, rt, mode="do", alpha=2.0, beta=24.0, max_hubs=300)
         b.engine.set_option("narrow_levels", narrow)
+        b.engine.set_option("bu_cut_edges", 1 << 40)
+        b.engine.set_option("bu_cut_mf_frac", 1.0)
         out = []
-        for cut in (1 << 40, 0):
-            b.engine.set_option("bu_cut_edges", cut)
-            b.engine.set_option("bu_cut_mf_frac", 1.0 if cut else 0.25)
+        for ranks in (8, 1):
+            b.engine.set_option("bu_cut_ranks", ranks)
             for s in srcs:
                 r = b.run(s)
                 recs = [(l["dir"], l["frontier"], l["frontier_edges"], l["discovered"]) for l in r.levels]
-                out.append((cut, s, b.levels(), recs))
+                out.append((ranks, s, b.levels(), recs, sum(1 for c in r.chains if c[7])))
         return out
 
     for outs in run_virtual_ranks(P, body, device="cpu"):
-        forced = {s: x for c, s, *x in outs if c}
-        plain = {s: x for c, s, *x in outs if not c}
+        cut = {s: x for c, s, *x in outs if c == 8}
+        plain = {s: x for c, s, *x in outs if c == 1}
         for s in srcs:
             exp = dbfs.cpu_bfs(csr, s)[0]
-            assert np.array_equal(forced[s][0], exp) and np.array_equal(plain[s][0], exp)
-            assert forced[s][1] == plain[s][1]
+            assert np.array_equal(cut[s][0], exp) and np.array_equal(plain[s][0], exp)
+            assert cut[s][1] == plain[s][1]
+            assert plain[s][2] == 0
+        assert sum(cut[s][2] for s in srcs) > 0
 
 
 @pytest.mark.parametrize("n,m,mode", [(3000, 30000, "td"), (600011, 2400000, "td"), (600011, 2400000, "do")])
