@@ -521,6 +521,8 @@ def main(argv=None) -> int:
             # chains of the profiled traversal whose frontier the producing
             # kernels pushed into the peers' windows (direct_frontier)
             "pushed_chains": sum(1 for c in getattr(prof, "chains", []) if len(c) > 4 and c[4]),
+            # ... and its bottom-up chains with the hub cut's launches
+            "cut_chains": sum(1 for c in getattr(prof, "chains", []) if len(c) > 7 and c[7]),
             "heldout": heldout,
             "secondary": secondary,
             "devices": [f"{'hip' if rt.is_gpu else 'cpu'}:{d}" for d in devices],

@@ -454,7 +454,8 @@ class CpuBackend final : public Backend {
   void pack_bytes(const PackArgs& a) override {
     if (a.ctrl && (a.ctrl->done || (a.flag ? a.ctrl->dir != 'B' || !*a.flag : a.ctrl->dir != 'T' || !a.ctrl->bytes)))
       return;
-    for (int64_t w = 0; w < a.words; ++w) a.next[w] |= gather_bytes(a.bytes + w * 64);
+    for (int64_t w = 0; w < a.words; ++w)
+      if (w < a.skip_begin || w >= a.skip_end) a.next[w] |= gather_bytes(a.bytes + w * 64);
   }
 
   void bu_step(const BuArgs& a) override {

@@ -1052,6 +1052,8 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
         pa.words = GW_;
         pa.ctrl = e_.ctrl_.data();
         pa.flag = e_.cut_flag_.data();
+        pa.skip_begin = me_ * W_;
+        pa.skip_end = (me_ + 1) * W_;
         be_.pack_bytes(pa);
         comm_.alltoall(e_.next_.data(), e_.recv_.data(), static_cast<size_t>(W_) * sizeof(word_t));
         ba.cut_recv = e_.recv_.data();
@@ -1072,11 +1074,10 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
     ba.tot = e_.bu_tot_.data();
     c.fused_scan = true;
     // several ranks: the level's end in the kernel's last workgroup too (no
-    // frontier gather; the hub kernels' fused finish)
-    // (not on a hub-cut level -- one rank with a forced exchange: its plain
-    // and cut kernels are both launched, and only the plain ones have the
-    // folded end)
-    if (xc_ && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) && !cut &&
+    // frontier gather; the hub kernels' fused finish) -- on a hub-cut level
+    // in whichever of its two kernels the decision runs (the plain one on a
+    // no-op chain)
+    if (xc_ && cells_fit() && gv_.nhubs > 0 && (!enq_gather_[L] || c.push) &&
         comm_.direct_level_end(2, &ba.end)) {
       ba.fin = finish_args(L, false, enq_dir_[L], c.cap);
       c.level_ended = true;

@@ -717,6 +717,9 @@ struct PackArgs {
   // several-rank hub cut's remote claims, BuArgs::cut_bytes)
   const LevelCtrl* ctrl = nullptr;
   const int* flag = nullptr;
+  // words [skip_begin, skip_end) are left alone (the hub cut: this rank's own
+  // slice, whose claims never go through the byte map)
+  int64_t skip_begin = 0, skip_end = 0;
 };
 
 // Bottom-up step fused with the frontier update: for every owned unvisited v,

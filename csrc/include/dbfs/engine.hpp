@@ -334,8 +334,13 @@ struct EngineOptions {
   // and sent to their owners as one bitmap all-to-all (bu_cut_merge applies
   // them) -- the top-down part shrinks with P as the bottom-up share does.
   // (Round 4's form sent the remote claims as owner lists and measured
-  // slower at P = 8.)
-  int64_t bu_cut_ranks = 8;
+  // slower at P = 8.)  Shadow replays of RMAT-26's late-switch roots
+  // (profiles/r6_xcut_shadow_ab.txt, traversal us per rank): P = 2
+  // 602-766 -> 530-620, P = 4 393-508 -> 397-453, P = 8 270-334 ->
+  // 298-345 -- the cut's fixed launches (decision, top-down part, 64 MB byte
+  // map pack, all-to-all, merge) outweigh what it saves a rank's 1/8 share
+  // of the bottom-up scan at P = 8, so it stops at 4.
+  int64_t bu_cut_ranks = 4;
   // ... enqueued (its decision and top-down launches) only for levels
   // predicted at <= bu_cut_mf_frac of the graph's directed edges (RMAT-26:
   // the late-switch first bottom-up levels have 4-15 % of them, the others

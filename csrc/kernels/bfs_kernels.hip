@@ -812,7 +812,8 @@ __global__ __launch_bounds__(kBlock) void list_scatter_kernel(ListScatterArgs a)
 __global__ __launch_bounds__(kBlock) void pack_bytes_kernel(PackArgs a) {
   if (a.ctrl && (a.ctrl->done || (a.flag ? a.ctrl->dir != 'B' || !*a.flag : a.ctrl->dir != 'T' || !a.ctrl->bytes)))
     return;
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  int64_t w = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (w >= a.skip_begin) w += a.skip_end - a.skip_begin;  // (the grid covers the other words only)
   if (w >= a.words) return;
   const word_t bits = gather_byte_bits(a.bytes + w * 64);
   if (bits) a.next[w] |= bits;
@@ -958,8 +959,9 @@ void list_scatter(const ListScatterArgs& a, hipStream_t st) {
 }
 
 void pack_bytes(const PackArgs& a, hipStream_t st) {
-  if (a.words <= 0) return;
-  pack_bytes_kernel<<<grid_for(a.words, kBlock), kBlock, 0, st>>>(a);
+  if (a.words - (a.skip_end - a.skip_begin) <= 0) return;
+  DBFS_CHECK(a.skip_begin >= 0 && a.skip_begin <= a.skip_end && a.skip_end <= a.words, "pack_bytes: skipped range out of bounds");
+  pack_bytes_kernel<<<grid_for(a.words - (a.skip_end - a.skip_begin), kBlock), kBlock, 0, st>>>(a);
 }
 
 // Compute units of the current device (cached per device id).

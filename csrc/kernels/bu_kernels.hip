@@ -567,7 +567,7 @@ __device__ __forceinline__ void bu_post_words(const BuArgs& a, int64_t w0, int n
 
 // kEnd: the level's end folded in (BuArgs::end; several ranks only -- its
 // code costs the one-rank kernels their spill-free 64 registers).
-// kCut: the hub-cut variant (one rank, first bottom-up level of a run of them),
+// kCut: the hub-cut variant (first bottom-up level of a run of them),
 // kCutLevels (claims in the narrow level bytes) or kCutClaims (wide levels:
 // claims in BuArgs::cut_claim).
 // kPost: the output words pushed to the peers afterwards (BuArgs::push).
@@ -582,15 +582,17 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
   __shared__ unsigned long long s_q[kQ > 0 ? (kThreads / kWave) * kQ : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) {
-    // a folded level end is a collective: it runs on a no-op chain too
-    if constexpr (kEnd) {
+    // a folded level end is a collective: it runs on a no-op chain too (a
+    // hub-cut level launches a cut and a plain variant: the plain one's)
+    if constexpr (kEnd && kCut == 0) {
       if (blockIdx.x == 0)
         direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin,
                          reinterpret_cast<uint64_t*>(s_res));
     }
     return;
   }
-  // a hub-cut level launches both variants; the decision picks one
+  // a hub-cut level launches both variants; the decision picks one (which
+  // also runs the folded level end, if any)
   if (a.cut_flag && (*a.cut_flag != 0) != (kCut != 0)) return;
   constexpr bool cut = kCut != 0;
   if (!a.hub_front) stamp_level_start(a.ctrl);
@@ -962,18 +964,20 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     else DBFS_BU_LAUNCH_WW(W, T, Q, R, kWaveWords);  \
   } while (0)
     if (a.cut_edges > 0) {
-      // a hub-cut level (one rank, a first bottom-up level: the engine only
-      // asks for it there): the cut variant, then the plain one -- whichever
-      // the device decision does not pick returns at once
-      DBFS_CHECK(rec && !a.follow_up && !a.end.active && a.cut_flag && (a.level8 || (a.cut_claim && a.level)) &&
-                     a.g.hub_bits,
+      // a hub-cut level (a first bottom-up level: the engine only asks for
+      // it there): the cut variant, then the plain one -- whichever the
+      // device decision does not pick returns at once (a folded level end:
+      // the running one's, the plain one's on a no-op chain)
+      DBFS_CHECK(rec && !a.follow_up && a.cut_flag && (a.level8 || (a.cut_claim && a.level)) && a.g.hub_bits,
                  "bu_step: hub-cut level without packed records / flag / claim bytes");
       // (with the deferred row queue: without it, scans in place, the late-switch
       // levels measured 460-535 -> 505-560 us)
       constexpr int kCutQ = kBuQueue;
-#define DBFS_CUT_LAUNCH(W, C)                                                                        \
-  do {                                                                                             \
-    if (a.push) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C, true><<<grid, kHubBuThreads, 0, st>>>(a); \
+#define DBFS_CUT_LAUNCH(W, C)                                                                                   \
+  do {                                                                                                        \
+    if (a.end.active && a.push) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, true, C, true><<<grid, kHubBuThreads, 0, st>>>(a); \
+    else if (a.end.active) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, true, C><<<grid, kHubBuThreads, 0, st>>>(a); \
+    else if (a.push) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C, true><<<grid, kHubBuThreads, 0, st>>>(a); \
     else bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C><<<grid, kHubBuThreads, 0, st>>>(a);          \
   } while (0)
       if (a.cut_claim) {

@@ -669,7 +669,7 @@ def test_hub_cut_several_ranks(P, narrow):
         b.engine.set_option("bu_cut_edges", 1 << 40)
         b.engine.set_option("bu_cut_mf_frac", 1.0)
         out = []
-        for ranks in (8, 1):
+        for ranks in (8, 1):  # (8: at least P)
             b.engine.set_option("bu_cut_ranks", ranks)
             for s in srcs:
                 r = b.run(s)

@@ -1406,21 +1406,29 @@ def test_peer_slot_rounds_build_and_ingest(tmp_path):
     assert rec["comm_inner_ops"] == 0
 
 
+_CUT = ["bu_cut_mf_frac=1", "bu_cut_edges=1099511627776"]
+
+
 @pytest.mark.parametrize("opts", [["xfuse_edges=4096"], ["bu_merge_visited=0"],
                                   ["xfuse_edges=4096", "bu_merge_visited=0"],
-                                  ["direct_frontier=0"], ["direct_frontier=0", "xfuse_edges=0"]])
+                                  ["direct_frontier=0"], ["direct_frontier=0", "xfuse_edges=0"],
+                                  _CUT, _CUT + ["narrow_levels=0"], _CUT + ["direct_frontier=0"]])
 def test_peer_multirank_options(opts):
     """The multi-rank options -- tiny sparse levels fused into one launch
     (xfuse_edges), bottom-up levels without the visited merge of the gathered
-    frontier (bu_merge_visited=0), and the frontier gathered by the level end
-    instead of pushed by the kernels (direct_frontier=0) -- over the peer
-    transport with 4 processes on device 0 at RMAT-18: every timed root
-    validated."""
+    frontier (bu_merge_visited=0), the frontier gathered by the level end
+    instead of pushed by the kernels (direct_frontier=0), and the hub cut
+    forced on every first bottom-up level (its remote claims' all-to-all over
+    the windows; 32-bit levels keep the claims in their own bytes) -- over the
+    peer transport with 4 processes on device 0 at RMAT-18: every timed root
+    validated (the forced cut: taken in the profiled traversal)."""
     args = ["--gpus", "4", "--scale", "18", "--steps", "6", "--warmup", "1"]
     for o in opts:
         args += ["--opt", o]
     rec = _bench_peer(args, DBFS_PEER_SLOT_MB="16")
     assert rec["comm_direct"] is True and rec["validated_roots"] == "6/6"
+    if "bu_cut_mf_frac=1" in opts:
+        assert rec["cut_chains"] > 0
 
 
 @pytest.mark.parametrize("opts", [[], ["bu_merge_visited=1"]])
