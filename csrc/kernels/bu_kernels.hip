@@ -582,19 +582,20 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   __shared__ long long s_c[kThreads / kWave], s_d[kThreads / kWave];
   __shared__ unsigned long long s_q[kQ > 0 ? (kThreads / kWave) * kQ : 1];
   if (a.ctrl && (a.ctrl->done || a.ctrl->dir != 'B')) {
-    // a folded level end is a collective: it runs on a no-op chain too (a
-    // hub-cut level launches a cut and a plain variant: the plain one's)
-    if constexpr (kEnd && kCut == 0) {
+    // a folded level end is a collective: it runs on a no-op chain too
+    if constexpr (kEnd) {
       if (blockIdx.x == 0)
         direct_level_end(a.end, a.scan.stats[2], a.scan.stats[3], a.scan.stats, a.fin,
                          reinterpret_cast<uint64_t*>(s_res));
     }
     return;
   }
-  // a hub-cut level launches both variants; the decision picks one (which
-  // also runs the folded level end, if any)
-  if (a.cut_flag && (*a.cut_flag != 0) != (kCut != 0)) return;
-  constexpr bool cut = kCut != 0;
+  // a hub-cut level launches the cut variant alone: the device decision
+  // (hub_gather's) picks the scan at run time -- the plain one when it says
+  // no (rare: the level is enqueued only when predicted small), instead of a
+  // second, plain launch that returned at once on every cut level (~4.5 us
+  // of idle GPU per late-switch traversal)
+  const bool cut = kCut != 0 && *a.cut_flag != 0;
   if (!a.hub_front) stamp_level_start(a.ctrl);
   const int64_t hw = (a.g.nhubs + kWordBits - 1) / kWordBits;
   stage_words<kThreads, kHubWords>(s_hub, a.hub_front, hw);
@@ -965,9 +966,8 @@ void bu_step(const BuArgs& a, hipStream_t st) {
   } while (0)
     if (a.cut_edges > 0) {
       // a hub-cut level (a first bottom-up level: the engine only asks for
-      // it there): the cut variant, then the plain one -- whichever the
-      // device decision does not pick returns at once (a folded level end:
-      // the running one's, the plain one's on a no-op chain)
+      // it there): the cut variant alone, which scans plain when the device
+      // decision says no
       DBFS_CHECK(rec && !a.follow_up && a.cut_flag && (a.level8 || (a.cut_claim && a.level)) && a.g.hub_bits,
                  "bu_step: hub-cut level without packed records / flag / claim bytes");
       // (with the deferred row queue: without it, scans in place, the late-switch
@@ -988,6 +988,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
         else DBFS_CUT_LAUNCH(false, kCutLevels);
       }
 #undef DBFS_CUT_LAUNCH
+      return;
     }
     if (whole) {
       if (a.follow_up && rec) DBFS_BU_LAUNCH_WW(true, kFollowThreads, kBuQueue, true, kWaveWords);
