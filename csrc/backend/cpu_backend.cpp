@@ -133,6 +133,12 @@ class CpuBackend final : public Backend {
       }
     }
     for (int64_t w = 0; w < a.gwords; ++w) a.visited[w] = a.zdeg[w];
+    if (a.frontier_clean && !a.frontier_global) {
+      // (the claim the device kernel relies on, checked: no stale bit left)
+      for (int64_t w = 0; w < a.words; ++w)
+        DBFS_CHECK(a.frontier[w] == 0 && (!a.frontier_clear || a.frontier_clear[w] == 0),
+                   "init_run: a frontier claimed clean holds a stale bit");
+    }
     for (int64_t w = 0; w < a.words; ++w) a.frontier[w] = 0;
     if (a.frontier_global)
       for (int64_t w = 0; w < a.gwords; ++w) a.frontier_global[w] = 0;

@@ -1142,6 +1142,10 @@ RunResult DeviceLoop::run() {
     ia.qv = e_.qv_[0].data();
     ia.frontier_clear = fr_own(0);
   }
+  // (the previous traversal left both owned slices zero: 16 B per vertex of
+  // stores saved; cleared until this run completes)
+  ia.frontier_clean = e_.frontier_clean_ && !seed_gather_;
+  e_.frontier_clean_ = false;
   be_.init_run(ia);
   // (Top-down levels read only their owned slice; the replicated visited
   // bitmap filters candidates with whatever remote bits it has -- merged
@@ -1297,6 +1301,12 @@ RunResult DeviceLoop::collect(int nlev, std::chrono::steady_clock::time_point t1
     res_.reached += r.discovered;
     res_.levels.push_back(r);
   }
+  // the owned frontier slices are zero again when the last level was top-down
+  // and found nothing (top-down levels clear their input as they read it and
+  // set only new bits; a bottom-up level leaves its input, an all-reached
+  // stop its last frontier)
+  // (with sparse levels on: only then does the compaction clear as it reads)
+  e_.frontier_clean_ = sparse_ && nlev > 0 && recs[nlev - 1].dir == 'T' && recs[nlev - 1].discovered == 0;
   res_.depth = nlev == 0 ? 1 : nlev;
   // (a traversal that stopped once every vertex with an edge was reached did
   // not expand its last frontier: its deepest level is the last record's + 1)

@@ -254,6 +254,11 @@ struct InitRunArgs {
   int32_t* blk_vstart = nullptr;
   vid_t* qv = nullptr;
   word_t* frontier_clear = nullptr;
+  // both owned frontier slices are known zero (the previous traversal ended
+  // on a top-down level that found nothing: top-down levels clear their input
+  // as they read it and set only new bits): only the seed's word is written
+  // (the CPU backend checks the claim)
+  bool frontier_clean = false;
   LevelCtrl* ctrl = nullptr;
   LevelCtrl ctrl_init;
   LevelMailbox* mailbox = nullptr;

@@ -480,6 +480,7 @@ class Engine {
   InitRunArgs init_args(int64_t source, word_t* seed_frontier, LevelCtrl* ctrl, const LevelCtrl& ctrl_init,
                         LevelMailbox* mailbox);
   bool scratch_dirty_ = true;  // cand / next / byte map may hold stale bits
+  bool frontier_clean_ = false;  // the owned frontier slices are zero (InitRunArgs::frontier_clean)
   void alloc_ref_state();
   void gather_levels_device(DBuf<lvl_t>& full);
   bool exchange() const { return part_.nranks > 1 || opt_.force_exchange; }

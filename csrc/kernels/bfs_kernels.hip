@@ -123,11 +123,13 @@ __global__ __launch_bounds__(kBlock) void init_run_kernel(InitRunArgs a) {
   if (a.frontier_global) {
     // a bottom-up first level reads the whole seed frontier: written here
     for (int64_t w = t0; w < a.gwords; w += stride) a.frontier_global[w] = w == sw ? sbit : 0ull;
+  } else if (a.frontier_clean) {
+    if (src >= 0 && t0 == 0) a.frontier[src >> 6] = 1ull << (src & 63);
   } else {
     const word_t obit = src >= 0 ? (1ull << (src & 63)) : 0ull;
     for (int64_t w = t0; w < a.words; w += stride) a.frontier[w] = (src >= 0 && w == (src >> 6)) ? obit : 0ull;
   }
-  if (a.frontier_clear)
+  if (a.frontier_clear && !a.frontier_clean)
     for (int64_t w = t0; w < a.words; w += stride) a.frontier_clear[w] = 0ull;
   // the seed's work-list entry: edge blocks [0, ceil(d / EPB)) all start in it
   if (a.blk_vstart && src >= 0) {
