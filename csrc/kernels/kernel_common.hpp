@@ -211,14 +211,10 @@ __device__ __forceinline__ void owner_list_append_items(vid_t* lists, int64_t st
 // takes its slots with ONE atomic on the owner's count word -- with two ranks
 // every wave of a 1 M-edge level appended to the same remote count word
 // (thousands of returning atomics on one address, ~90 per us).
-// solo (optional, LDS, one entry per owner, zero at the level's start): the
-// workgroup is the level's only appender -- the counts are kept there and
-// the count words are not touched (no returning atomic; the publish reads
-// them from there).
 template <int kItems>
 __device__ __forceinline__ void owner_list_append_wg(vid_t* lists, int64_t stride, int64_t part, int nranks,
                                                      const vid_t (&v)[kItems], unsigned act,
-                                                     const DirectTable* dt = nullptr, unsigned* solo = nullptr) {
+                                                     const DirectTable* dt = nullptr) {
   __shared__ unsigned s_oc[kern::kMaxPeers], s_ob[kern::kMaxPeers];
   const int t = threadIdx.x;
   const int lane = lane_id();
@@ -245,12 +241,7 @@ __device__ __forceinline__ void owner_list_append_wg(vid_t* lists, int64_t strid
   __syncthreads();
   if (t < nranks) {
     const unsigned c = s_oc[t];
-    if (solo) {
-      s_ob[t] = solo[t];
-      solo[t] += c;
-    } else {
-      s_ob[t] = c ? atomicAdd(lists + static_cast<int64_t>(t) * stride, c) : 0u;
-    }
+    s_ob[t] = c ? atomicAdd(lists + static_cast<int64_t>(t) * stride, c) : 0u;
   }
   __syncthreads();
 #pragma unroll
@@ -277,14 +268,11 @@ __device__ __forceinline__ bool cell_ok1(uint64_t w, uint64_t seq) { return (w >
 // count for owner p in p's cell -- one store -- and zeroes the local count for
 // the next list level.  A chain that is not live publishes empty lists: the
 // peers wait all the same.
-// (solo: the counts kept by owner_list_append_wg for the level's only
-// appending workgroup -- no load)
-__device__ __forceinline__ void direct_publish(const DirectExchange& d, vid_t* lists, int64_t stride, bool live,
-                                               const unsigned* solo = nullptr) {
+__device__ __forceinline__ void direct_publish(const DirectExchange& d, vid_t* lists, int64_t stride, bool live) {
   const int t = threadIdx.x;
   if (t < d.nranks && t != d.rank) {
     vid_t* cnt = lists + static_cast<int64_t>(t) * stride;
-    const vid_t n = !live ? 0u : solo ? solo[t] : __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const vid_t n = live ? __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
     *cnt = 0u;
     sys_store_u64(d.table->cell_out[t], cell_word0(d.seq, n));
   }

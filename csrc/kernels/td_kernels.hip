@@ -384,12 +384,8 @@ __global__ __launch_bounds__(kThreads) void td_expand_kernel(TdArgs a) {
 // a level settling thousands of waves' claims queued that many returning
 // atomics on one address (~90 per us).
 constexpr int kSettleWaves = 1024 / kWave;
-// (kWg, solo: the workgroup is the level's only settler -- the counter is kept
-// there instead, zero at the level's start: no returning atomic; sparse_totals
-// reads it from there)
 template <int kItems, bool kWg = false>
-__device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed,
-                                              unsigned long long* solo = nullptr) {
+__device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t (&v)[kItems], unsigned claimed) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
   if constexpr (!kWg) {
     if (!__ballot(claimed != 0)) return;
@@ -438,12 +434,7 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
     if (threadIdx.x == 0) {
       unsigned long long sum = 0;
       for (int k = 0; k < static_cast<int>(blockDim.x >> 6); ++k) sum += s_pk[k];
-      if (solo) {
-        s_pbase = *solo;
-        *solo += sum;
-      } else {
-        s_pbase = sum ? atomicAdd(a.counter, sum) : 0ull;
-      }
+      s_pbase = sum ? atomicAdd(a.counter, sum) : 0ull;
     }
     __syncthreads();
     old = s_pbase;
@@ -474,11 +465,9 @@ __device__ __forceinline__ void sparse_settle(const TdSparseArgs& a, const vid_t
 
 // The level's local totals from the packed counter (one thread of the last
 // workgroup): stats, the work list's end marker, counter and ticket reset.
-// (solo: the counter's value kept by the level's only settling workgroup)
-__device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg,
-                                              const unsigned long long* solo = nullptr) {
+__device__ __forceinline__ void sparse_totals(const TdSparseArgs& a, long long& cnt, long long& deg) {
   constexpr unsigned long long kEdgeMask = (1ull << kSparseEdgeBits) - 1;
-  const unsigned long long tot = solo ? *solo : __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long tot = __hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   cnt = static_cast<long long>(tot >> kSparseEdgeBits);
   deg = static_cast<long long>(tot & kEdgeMask);
   *a.counter = 0ull;
@@ -582,11 +571,8 @@ __global__ __launch_bounds__(256) void direct_selftest_kernel(DirectExchange l, 
 // the one last workgroup of a fused tiny level, TdSparseArgs::fuse_apply)
 // (live: called from a live td_sparse -- the chain check is not repeated: the
 // level's own finish, the only writer of *ctrl, comes after it)
-// (solo: the fused tiny level's one workgroup was the level's only settler:
-// the counter's running value in LDS, sparse_settle / sparse_totals)
 template <int kThreads, bool kWg = true>
-__device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx, bool live = false,
-                                             unsigned long long* solo = nullptr) {
+__device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx, unsigned gx, bool live = false) {
   constexpr int kItems = kTdEdgesPerBlock / kThreads;
   __shared__ int s_last;
   __shared__ long long s_end[kern::kMaxPeers];  // inclusive prefix of the counts
@@ -646,7 +632,7 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
       if (i0 + static_cast<int64_t>(k) * kThreads + t < total && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit))
         claimed |= 1u << k;
     }
-    sparse_settle<kItems, kWg>(a, v, claimed, solo);
+    sparse_settle<kItems, kWg>(a, v, claimed);
   }
   __syncthreads();
   if (t == 0) {
@@ -666,7 +652,7 @@ __device__ __forceinline__ void sparse_apply(const TdSparseArgs& a, unsigned bx,
   __shared__ long long s_tot[2];
   if (t == 0) {
     long long cnt = 0, deg = 0;
-    sparse_totals(a, cnt, deg, solo);
+    sparse_totals(a, cnt, deg);
     s_tot[0] = cnt;
     s_tot[1] = deg;
   }
@@ -706,7 +692,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   __shared__ long long s_base[kTdEdgesPerBlock + 1];
   __shared__ int32_t s_wmax[kThreads / kWave];
   __shared__ int s_last;
-  const bool dx = a.lists && a.direct.active;
+  // (kWg: several ranks -- the launcher's choice whenever there are owner
+  // lists, so the one-rank variant compiles none of their code)
+  const bool dx = kWg && a.lists && a.direct.active;
   if (a.late_ticks) {
     // fault injection: a workgroup that will take no ticket starts late
     const long long m0 = a.dev_stats[1];
@@ -737,26 +725,10 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   const unsigned active = static_cast<unsigned>(nblocks < 1 ? 1 : (nblocks < gridDim.x ? nblocks : gridDim.x));
   if (blockIdx.x >= active) return;
   const int t = threadIdx.x;
-  // a fused tiny level expanded by one workgroup: it is the level's only
-  // appender and settler, so the list counts and the counter's value are kept
-  // in LDS -- the publish and the totals need no load of them (two of the
-  // level's dependent round trips)
-  __shared__ unsigned s_solo_cnt[kern::kMaxPeers];
-  __shared__ unsigned long long s_solo_ctr;
-  const bool solo = kWg && dx && a.fuse_apply && active == 1;
-  if (solo) {
-    if (t < kern::kMaxPeers) s_solo_cnt[t] = 0u;
-    if (t == 0) s_solo_ctr = 0ull;
-    __syncthreads();
-  }
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
   const int64_t gstride = static_cast<int64_t>(active) * kThreads;
-  // the input vertices' frontier bits (the bitmap is not read here) -- the
-  // first entry's load issued now and its store made after the claims' loads,
-  // so its round trip overlaps theirs instead of preceding them
-  constexpr vid_t kNoEntry = 0xFFFFFFFFu;
-  vid_t r_first = gtid < q ? a.qv[gtid] : kNoEntry;
-  for (int64_t i = gtid + gstride; i < q; i += gstride) {
+  // the input vertices' frontier bits (the bitmap is not read here)
+  for (int64_t i = gtid; i < q; i += gstride) {
     const vid_t r = a.qv[i];
     a.frontier_in[r >> 6] = 0ull;
   }
@@ -783,11 +755,7 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       const word_t bit = 1ull << (v[k] & 63);
       if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
     }
-    if (r_first != kNoEntry) {
-      a.frontier_in[r_first >> 6] = 0ull;
-      r_first = kNoEntry;
-    }
-    if (a.lists) {
+    if (kWg && a.lists) {
       // several ranks: claimed remote targets to their owners' lists
       unsigned remote = 0;
 #pragma unroll
@@ -797,16 +765,15 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       if constexpr (kWg) {
         // (the whole workgroup: one count atomic per owner and block)
         owner_list_append_wg<kItems>(a.lists, a.list_stride, a.part, a.nranks, v, remote,
-                                     dx ? a.direct.table : nullptr, solo ? s_solo_cnt : nullptr);
+                                     dx ? a.direct.table : nullptr);
       } else if (__ballot(remote != 0)) {
         owner_list_append_items<kItems>(a.lists, a.list_stride, a.part, v, remote, dx ? a.direct.table : nullptr);
       }
     }
     // (B) finish the claimed vertices (the whole workgroup: one counter atomic)
-    sparse_settle<kItems, kWg>(a, v, claimed, solo ? &s_solo_ctr : nullptr);
+    sparse_settle<kItems, kWg>(a, v, claimed);
   }
-  if (r_first != kNoEntry) a.frontier_in[r_first >> 6] = 0ull;  // (no edge block ran here)
-  if (a.lists) {
+  if (kWg && a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
     // every wave's write-through stores drained, the workgroups' ticket, and
     // the last one publishes the counts and flags.
@@ -830,11 +797,11 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
     }
     __syncthreads();
     if (!s_last) return;
-    direct_publish(a.direct, a.lists, a.list_stride, true, solo ? s_solo_cnt : nullptr);
+    direct_publish(a.direct, a.lists, a.list_stride, true);
     // a tiny level (fuse_apply): this workgroup is also the owner side --
     // the peers' lists, their claims and the folded level end -- instead of
     // a td_sparse_apply launch
-    if (a.fuse_apply) sparse_apply<kThreads, kWg>(a, 0, 1, true, solo ? &s_solo_ctr : nullptr);
+    if (a.fuse_apply) sparse_apply<kThreads, kWg>(a, 0, 1, true);
     return;
   }
 
