@@ -1,6 +1,6 @@
 # Same-box A/B of a compile-time variant on shadow replays: the tree as is (A) against a copy
 # built with EXTRA_HIPFLAGS="$FLAGS" (B), P ranks, ranks 0 and P-1, four RMAT-26 roots, twice each.
-#   FLAGS="-DDBFS_NO_SOLO" P=8 bash tools/gpu_replay_ab.sh
+#   FLAGS="-DSOME_VARIANT" P=8 bash tools/gpu_replay_ab.sh   (round 6: the LDS-kept tiny-level counts, since reverted)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 ROOT=$PWD; T=${TAG:-rab}; P=${P:-8}; d=/tmp/rab_tree
 ROOTS=${ROOTS:-8766153 17872028 13702079 43129764}
