@@ -71,13 +71,30 @@ __device__ __forceinline__ void level_finish_device(const LevelFinishArgs& a) {
   finish_level(a.ctrl, c, a.stats[2], a.stats[3], a.seed, a.rec, a.mailbox, a.level);
 }
 
+// ... for a kernel whose argument block holds `a` (level_finish_block: the
+// peer collectives, level_finish_kernel): two plain copies instead of the
+// select above, which takes the kernel argument's address and made those
+// kernels copy their whole argument struct to scratch (752 B a lane in the
+// peer unpack).  (The select stays where `a` is a kernel's own copy: the
+// split form costs td_sparse a spill.)
+__device__ __forceinline__ void level_finish_device_arg(const LevelFinishArgs& a) {
+  if (!a.seed && !chain_live(*a.ctrl, a.expect_dir, a.expect_cap)) return;
+  if (a.seed) {
+    LevelCtrl c = a.ctrl_init;
+    finish_level(a.ctrl, c, a.stats[2], a.stats[3], true, a.rec, a.mailbox, a.level);
+  } else {
+    LevelCtrl c = *a.ctrl;
+    finish_level(a.ctrl, c, a.stats[2], a.stats[3], false, a.rec, a.mailbox, a.level);
+  }
+}
+
 // Several ranks: a level's end after its totals' all-reduce, in one
 // workgroup (the peer transport's fused collective): thread 0's decision.
 // (The chain check is thread 0's alone -- it reads the control block the
 // decision then writes.)
 template <int kThreads>
 __device__ __forceinline__ void level_finish_block(const LevelFinishArgs& a) {
-  if (threadIdx.x == 0) level_finish_device(a);
+  if (threadIdx.x == 0) level_finish_device_arg(a);
 }
 
 }  // namespace kern
