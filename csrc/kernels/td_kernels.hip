@@ -683,6 +683,7 @@ __global__ __launch_bounds__(kWave) void direct_prewait_kernel(DirectExchange x)
 // their owners' lists and td_sparse_apply finishes the level after the
 // exchange.  kThreads = 1024: 2 edges per thread per block.
 constexpr int kTdSparseThreads = 1024;
+constexpr long long kTdWgSettleBlocks = 32;  // (one rank: td_sparse's per-workgroup settle from here)
 // kWg: several ranks (owner lists) -- settles aggregated per workgroup
 // (sparse_settle); one rank keeps the per-wave form (its registers).
 template <int kThreads, bool kWg = false>
@@ -724,6 +725,16 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
   // blocks, 256 workgroups queueing on one ticket address cost several us.
   const unsigned active = static_cast<unsigned>(nblocks < 1 ? 1 : (nblocks < gridDim.x ? nblocks : gridDim.x));
   if (blockIdx.x >= active) return;
+  // one rank, a level of many edge blocks: claims settled per workgroup too
+  // (one counter atomic each, as with several ranks) -- hundreds of
+  // workgroups' per-wave atomics on the one counter queue (~90 per us); a
+  // small level keeps the per-wave form (the workgroup form's barriers cost
+  // it ~2 us).  (Workgroup-uniform: nblocks is.)
+#ifdef DBFS_NO_WG_SETTLE
+  constexpr bool wg_settle = false;  // (diagnostic build: same-box A/B)
+#else
+  const bool wg_settle = nblocks >= kTdWgSettleBlocks;
+#endif
   const int t = threadIdx.x;
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * kThreads + t;
   const int64_t gstride = static_cast<int64_t>(active) * kThreads;
@@ -771,7 +782,9 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
       }
     }
     // (B) finish the claimed vertices (the whole workgroup: one counter atomic)
-    sparse_settle<kItems, kWg>(a, v, claimed);
+    if constexpr (kWg) sparse_settle<kItems, true>(a, v, claimed);
+    else if (wg_settle) sparse_settle<kItems, true>(a, v, claimed);
+    else sparse_settle<kItems, false>(a, v, claimed);
   }
   if (kWg && a.lists) {
     // several ranks: td_sparse_apply finishes the level.  A direct exchange:
