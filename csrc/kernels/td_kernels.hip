@@ -850,12 +850,14 @@ __global__ __launch_bounds__(kThreads) void td_sparse_kernel(TdSparseArgs a) {
 // claims, owner lists and settling as td_sparse.  The level ends in the last
 // workgroup of a two-level ticket.
 constexpr int kBitsPre = 4;
-template <int kItems>
+// kLists: several ranks (owner lists) -- the one-rank variant compiles none of
+// their code (its registers).
+template <int kItems, bool kLists>
 __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) {
   __shared__ long long s_incl[kBlock];  // per wave: the step's inclusive degree prefixes
   __shared__ eid_t s_rs[kBlock];        // ... and row starts
   __shared__ int s_last;
-  const bool dx = a.lists && a.direct.active;
+  const bool dx = kLists && a.lists && a.direct.active;
   if (!chain_live(*a.ctrl, 'T', a.max_mf)) {
     if (dx && blockIdx.x == 0) {
       direct_publish(a.direct, a.lists, a.list_stride, false);
@@ -940,7 +942,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
           const word_t bit = 1ull << (v[k] & 63);
           if (!(seen[k] & bit) && !(atomicOr(a.visited + (v[k] >> 6), bit) & bit)) claimed |= 1u << k;
         }
-        if (a.lists) {
+        if (kLists && a.lists) {
           unsigned remote = 0;
 #pragma unroll
           for (int k = 0; k < kItems; ++k)
@@ -966,7 +968,7 @@ __global__ __launch_bounds__(kBlock) void td_sparse_bits_kernel(TdSparseArgs a) 
   }
   __syncthreads();
   if (!s_last) return;
-  if (a.lists) {
+  if (kLists && a.lists) {
     // several ranks: td_sparse_apply finishes the level (a direct exchange:
     // the counts and flags published here)
     if (t == 0) *a.ticket = 0u;
@@ -1382,7 +1384,8 @@ void td_sparse(const TdSparseArgs& a, hipStream_t st) {
     DBFS_CHECK(a.group_ticket, "td_sparse from a bitmap needs the group tickets");
     // (an empty shard still runs one workgroup: the level's finish)
     const unsigned grid = grid_for(nunits, kUnitsPerBlock, std::min<int64_t>(kMaxFusedGrid, 1024));
-    td_sparse_bits_kernel<4><<<grid, kBlock, 0, st>>>(a);
+    if (a.lists) td_sparse_bits_kernel<4, true><<<grid, kBlock, 0, st>>>(a);
+    else td_sparse_bits_kernel<4, false><<<grid, kBlock, 0, st>>>(a);
     return;
   }
   // 1024-thread workgroups, two edges per thread per block: a sparse level's
