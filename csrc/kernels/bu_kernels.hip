@@ -980,13 +980,22 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     else if (a.push) bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C, true><<<grid, kHubBuThreads, 0, st>>>(a); \
     else bu_hub_kernel<W, kHubBuThreads, kCutQ, true, false, C><<<grid, kHubBuThreads, 0, st>>>(a);          \
   } while (0)
+      // (a small shard's first level -- 4 words per wave, one unit per
+      // workgroup, as the plain launch below: the cut variant scans plain when
+      // the decision says no, and the soc-LiveJournal1-sized graph's first
+      // level then ran at 16 words per wave, do mode 154 -> 120 GTEPS)
+      const bool small4 = small && !a.end.active && !a.push;
+#define DBFS_CUT_LAUNCH4(C) bu_hub_kernel<false, kHubBuThreads, kCutQ, true, false, C, 0, 4><<<grid, kHubBuThreads, 0, st>>>(a)
       if (a.cut_claim) {
         if (whole) DBFS_CUT_LAUNCH(true, kCutClaims);
+        else if (small4) DBFS_CUT_LAUNCH4(kCutClaims);
         else DBFS_CUT_LAUNCH(false, kCutClaims);
       } else {
         if (whole) DBFS_CUT_LAUNCH(true, kCutLevels);
+        else if (small4) DBFS_CUT_LAUNCH4(kCutLevels);
         else DBFS_CUT_LAUNCH(false, kCutLevels);
       }
+#undef DBFS_CUT_LAUNCH4
 #undef DBFS_CUT_LAUNCH
       return;
     }
