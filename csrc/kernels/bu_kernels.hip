@@ -574,6 +574,28 @@ __device__ __forceinline__ void bu_post_words(const BuArgs& a, int64_t w0, int n
 // kWW: words per wave when units are split over waves (!kWhole): 16, or 4 for
 // shards too small to fill the chip at 16 (a soc-LiveJournal1-sized graph's
 // 1184 units at 16 words per wave are 4736 waves, 18 per CU against 32 slots).
+// XCD-aware unit walk: workgroup b takes the slot (b % 8) * (G / 8) + b / 8 of
+// the grid-stride walk, so each XCD (workgroups dispatch round-robin over the
+// 8) scans one contiguous eighth of every round's units -- its row records,
+// level bytes and edge runs in its own L2 and translation caches -- instead
+// of every eighth group of them.  Only when every round is full (units a
+// multiple of G x per, as on the power-of-two RMAT shards): a partial last
+// round remapped would sit on the first few XCDs only (a small shard's one
+// partial round measured -10 % on the soc-LiveJournal1-sized graph).  Decided
+// once, before the walk: a per-round choice cost the fused-finish variants
+// 2-4 VGPRs and the cut variant a 12-B spill.
+// Same-box A/B on RMAT-26 (profiles/r6_xcd_remap_ab.txt): flat to +0.5 %
+// (the scan's traffic is streaming rows plus random frontier probes, which
+// no mapping localises); DBFS_NO_XCD_REMAP restores the plain order.
+__device__ __forceinline__ int64_t bu_block(int64_t nunits, int per) {
+  const uint32_t g = gridDim.x, b = blockIdx.x;
+#ifndef DBFS_NO_XCD_REMAP
+  if (g % 8 == 0 && nunits % (static_cast<int64_t>(g) * per) == 0)
+    return static_cast<int64_t>(b % 8) * (g / 8) + b / 8;
+#endif
+  return b;
+}
+
 template <bool kWhole, int kThreads = kHubBuThreads, int kQ = kBuQueue, bool kRec = false, bool kEnd = false,
           int kCut = 0, bool kPost = false, int kWW = kWaveWords>
 __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(BuArgs a) {
@@ -614,8 +636,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     // Static stride over the units.  (A dynamic unit queue measured slower:
     // RMAT-26 per level 387 / 182 / 104 against 346 / 137 / 30 us -- the
     // returning device-scope atomics cost more than the stride's imbalance.)
-    for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
-         u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
+    const int64_t blk = bu_block(nunits, kWavesPerBlock);
+    for (int64_t u = blk * kWavesPerBlock + wave; u < nunits; u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
       long long cnt = 0, deg = 0;
       bu_wave_compact<true, kUnitWords, kQ, kRec, kCut>(a, u * kUnitWords, s_res + wave * kUnitWords, s_hub, cnt,
                                                         deg, s_q + wave * kQ, cut);
@@ -629,7 +651,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
       }
     }
     if constexpr (kPost)
-      for (int64_t u = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave; u < nunits;
+      for (int64_t u = blk * kWavesPerBlock + wave; u < nunits;
            u += static_cast<int64_t>(gridDim.x) * kWavesPerBlock)
         bu_post_words(a, u * kUnitWords, kUnitWords);
     if (!a.fuse_scan) return;
@@ -658,7 +680,8 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
   // across the loop would spill)
   __shared__ long long s_acc[2 * kGroups];
   if (threadIdx.x < 2 * kGroups) s_acc[threadIdx.x] = 0;
-  for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride) {
+  const int64_t blk = bu_block(nunits, kGroups);
+  for (int64_t base = blk * kGroups; base < nunits; base += stride) {
     const int64_t u = base + group;
     long long cnt = 0, deg = 0;
     if (u < nunits)
@@ -686,7 +709,7 @@ __global__ __launch_bounds__(kThreads, 2 * kThreads / 256) void bu_hub_kernel(Bu
     __syncthreads();
   }
   if constexpr (kPost)
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kGroups; base < nunits; base += stride)
+    for (int64_t base = blk * kGroups; base < nunits; base += stride)
       if (base + group < nunits) bu_post_words(a, (base + group) * kUnitWords + wg * kWW, kWW);
   if (!a.fuse_scan) return;
   if constexpr (kPost) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (as above)
