@@ -948,11 +948,13 @@ void bu_step(const BuArgs& a, hipStream_t st) {
     // words per wave for parallelism
     const int64_t slots = 2 * static_cast<int64_t>(device_cus()) * (kHubBuThreads / kWave);
     const bool whole = a.whole_units > 0 || (a.whole_units == 0 && nunits >= slots);
-    // a bottom-up level after another one (few unvisited vertices left, most
-    // of them scanning rows): whole units in 768-thread workgroups (80 VGPRs
-    // instead of 64); 16-word waves without the row queue (measured)
-    constexpr int kFollowThreads = 768;
-    const int threads = whole ? (a.follow_up ? kFollowThreads : kHubBuThreads) : kHubBuThreads;
+    // whole units in 1024-thread workgroups for every bottom-up level: a
+    // level after another one (few unvisited vertices left, most of them
+    // scanning rows) ran in 768-thread ones while that variant needed 80
+    // VGPRs; at 60-65 now, 1024 threads measured the late-switch second
+    // level 188-191 -> 160 us, RMAT-26 +2.4 % (held-out +1.7 %) on two boxes
+    // (profiles/r6_follow_1024_ab.txt)
+    const int threads = kHubBuThreads;
     // shards too small to fill the wave slots at 16 words per wave: 4 (one
     // unit per workgroup) for a first bottom-up level -- measured, the
     // soc-LiveJournal1-sized graph's first level 420 -> 295 us (do mode
@@ -1023,9 +1025,7 @@ void bu_step(const BuArgs& a, hipStream_t st) {
       return;
     }
     if (whole) {
-      if (a.follow_up && rec) DBFS_BU_LAUNCH_WW(true, kFollowThreads, kBuQueue, true, kWaveWords);
-      else if (a.follow_up) DBFS_BU_LAUNCH_WW(true, kFollowThreads, kBuQueue, false, kWaveWords);
-      else if (rec) DBFS_BU_LAUNCH_WW(true, kHubBuThreads, kBuQueue, true, kWaveWords);
+      if (rec) DBFS_BU_LAUNCH_WW(true, kHubBuThreads, kBuQueue, true, kWaveWords);
       else DBFS_BU_LAUNCH_WW(true, kHubBuThreads, kBuQueue, false, kWaveWords);
       return;
     }
