@@ -959,6 +959,13 @@ void DeviceLoop::emit_bottom_up(Chain& c) {
   ba.words = W_;
   ba.lane_limit = opt_.bu_lane_limit;
   ba.whole_units = opt_.bu_whole_units;
+  // the third and later bottom-up levels of a run (few unvisited vertices
+  // left) scan whole units even on shards too small to fill the chip that
+  // way: shadow ranks of P = 4 on RMAT-26, those levels 28-31 -> 22-24 us,
+  // where the first two lost 4-10 % (profiles/r6_bu_whole_late_levels.txt)
+  if (ba.whole_units == 0 && L >= 2 && enq_form_[static_cast<size_t>(L - 1)] == 'B' &&
+      enq_form_[static_cast<size_t>(L - 2)] == 'B')
+    ba.whole_units = 1;
   ba.small_waves = opt_.bu_small_waves;
   ba.zdeg = e_.zdeg_.data() + me_ * W_;
   ba.follow_up = c.pf == 'B';
